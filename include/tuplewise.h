@@ -1,0 +1,158 @@
+/*
+ * tuplewise.h — C ABI of libtuplewise.so, the MI355X (gfx950) implementation of the
+ * tuplewise hot path of "Trade-offs in Large Scale Distributed Tuplewise Estimation and
+ * Learning" (reference: RobinVogel/Trade-offs-in-Distributed-Tuplewise-Estimation-and-Learning).
+ *
+ * The reference is pure Python/NumPy; its boundary is the `f_block(X_block, Z_block)`
+ * protocol consumed by UN / UN_split (learning-experiment/compute_stats.py:44-92) and the
+ * estimator functions that produce block values.  Each entry point below replaces the
+ * per-shard NumPy body of one of those functions for ALL shards in one launch; the Python
+ * package (tuplewise.compute_stats / tuplewise.estimation) keeps the reference names and
+ * calls these through ctypes.
+ *
+ * Conventions
+ *   - every pointer argument named d_* is DEVICE memory (hipMalloc / torch.cuda); everything
+ *     else is a host scalar.  No entry point allocates, copies to/from the host, or
+ *     synchronises: all work is enqueued on `stream` (a hipStream_t, NULL = default stream),
+ *     so calls are graph-capturable.
+ *   - shards are described by offset arrays: shard s owns elements [off[s], off[s+1]) of the
+ *     concatenated input; n_shards+1 int64 entries, device memory.
+ *   - dtype codes: TW_F64 (double), TW_I64 (int64).  Both sides of a call share one dtype
+ *     (the Python layer applies NumPy's promotion rules first).
+ *   - return value: TW_OK (0) or an error code; tw_last_error() gives a thread-local message.
+ *     TW_ERR_ARG maps to the reference's AssertionError/ValueError, TW_ERR_HIP to RuntimeError.
+ */
+#ifndef TUPLEWISE_H
+#define TUPLEWISE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TW_OK 0
+#define TW_ERR_ARG 1
+#define TW_ERR_HIP 2
+
+#define TW_F64 0
+#define TW_I64 1
+
+/* Pair predicates.  TW_PRED_GT is the reference AUC kernel 1{x > z}
+ * (estimation-experiment/main.py:31; compute_stats.py:19 `X - Z > 0`, identical for IEEE
+ * doubles).  TW_PRED_HALF is the opt-in "+0.5 on ties" mode asked for by BASELINE.json: the
+ * counter then holds half-units 2*#{x>z} + #{x==z} = #{x>z} + #{x>=z}.
+ * TW_PRED_SUBGT is `(x - z) > 0` with int64 wrap-around, the literal cs.Un AUC body for int64
+ * inputs (compute_stats.py:19, :30); for doubles it equals TW_PRED_GT. */
+#define TW_PRED_GT 0
+#define TW_PRED_HALF 1
+#define TW_PRED_SUBGT 2
+
+/* Float pair kernels of cs.Un / cs.UB_indices (compute_stats.py:15-18, :27-29) and the
+ * hinge surrogate conv_AUC (compute_stats.py:129-135). */
+#define TW_KERN_PROD 0  /* x * z                 */
+#define TW_KERN_GINI 1  /* |x - z|               */
+#define TW_KERN_HINGE 2 /* max(z - x + margin, 0) */
+
+const char* tw_last_error(void);
+int tw_version(void);
+/* number of visible HIP devices (0 when no GPU); does not create a context on failure */
+int tw_device_count(int* out_count);
+
+/* ---- Row A1/A2/A6/A7: complete two-sample count, all shards in one launch -------------
+ * Replaces est.Un (estimation-experiment/main.py:29-31) and cs.Un(kernel="AUC")
+ * (compute_stats.py:10-19) as the f_block of UN (main.py:33-69, compute_stats.py:56-92).
+ * d_out[s] (uint64) = #{(i,j): pred(x_i, z_j)} over shard s (half-units for TW_PRED_HALF).
+ * max_nx / max_nz: the largest shard sizes (host-known; they size the grid). */
+int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                   const int64_t* d_z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
+                   int32_t dtype, int32_t pred, uint64_t* d_out, void* stream);
+
+/* ---- Row A3/A4/A5/A8: incomplete count on given index pairs (replay mode) -------------
+ * Replaces cs.UB_indices / UB_pairs / UB (compute_stats.py:22-42): pair p of shard s
+ * compares x[d_ix[p]] with z[d_iz[p]] for p in [d_pair_off[s], d_pair_off[s+1]); indices are
+ * absolute positions in d_x / d_z (int64, as NumPy randint returns them). */
+int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
+                       const int64_t* d_iz, const int64_t* d_pair_off, int32_t n_shards,
+                       int64_t max_pairs, int32_t dtype, int32_t pred, uint64_t* d_out,
+                       void* stream);
+
+/* ---- Row A5/A8, device-RNG mode: B pairs per shard drawn on the device ----------------
+ * Pair p of local shard s: Philox4x32-10(key = seed, counter = (p lo, p hi, shard_base + s, 0))
+ * gives 4 words; (w1:w0) and (w3:w2) are mapped to [0, nx_s) and [0, nz_s) by 64-bit
+ * multiply-high; with-replacement sampling like UB's randint (compute_stats.py:40-41).
+ * shard_base = the global index of local shard 0, so draws do not depend on how shards are
+ * spread over ranks.  Not bit-comparable with NumPy's stream; statistically equivalent
+ * (tests/test_statistics.py). */
+int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                       const int64_t* d_z_off, int32_t n_shards, int64_t B, uint64_t seed,
+                       uint64_t shard_base, int32_t dtype, int32_t pred, uint64_t* d_out,
+                       void* stream);
+
+/* ---- Row A2 (prod/gini) and f1 (conv_AUC): float pair sums, complete -------------------
+ * d_out[s] (double) = sum over all pairs of shard s of kern(x_i, z_j).  Deterministic: fixed
+ * per-block partial order, then an ordered per-shard reduction.  d_work: n_shards *
+ * tw_pair_sum_work_per_shard(max_nx, max_nz) doubles. */
+int64_t tw_pair_sum_work_per_shard(int64_t max_nx, int64_t max_nz);
+int tw_pair_sum_f64(const double* d_x, const int64_t* d_x_off, const double* d_z,
+                    const int64_t* d_z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
+                    int32_t kern, double margin, double* d_work, double* d_out, void* stream);
+
+/* ---- f1: float pair sums on given index pairs (conv_AUC_deter_pairs, UB_indices prod/gini)
+ * d_out[s] = sum_p kern(x[ix_p], z[iz_p]); d_work: n_shards * tw_pair_sum_idx_work_per_shard(max_pairs). */
+int64_t tw_pair_sum_idx_work_per_shard(int64_t max_pairs);
+int tw_pair_sum_idx_f64(const double* d_x, const double* d_z, const int64_t* d_ix,
+                        const int64_t* d_iz, const int64_t* d_pair_off, int32_t n_shards,
+                        int64_t max_pairs, int32_t kern, double margin, double* d_work,
+                        double* d_out, void* stream);
+
+/* ---- Row L1: pairwise hinge gradient, all shards in one launch ------------------------
+ * Replaces grad_inc_block(w, B, margin)(X_s, Z_s) (compute_stats.py:146-162) for every shard
+ * of UN_split (compute_stats.py:44-46).  X: (n_X, d) row-major doubles, Z: (n_Z, d).
+ * Shard s, pair b: rx = d_rows_x[s*kx + d_ix[s*B+b]], rz = d_rows_z[s*kz + d_iz[s*B+b]]
+ * (SWR_divide row draws composed with the per-block randint draws, compute_stats.py:48-54,
+ * :155-156); d_rows_x / d_rows_z may be NULL meaning identity (shard = whole array).
+ * diff = Z[rz] - X[rx]; S = diff . w + margin; d_out[s*d + j] = (sum_{b: S_b > 0} diff_bj) / B,
+ * summed over b in order (as NumPy's axis-0 reduce does). */
+int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                  int64_t kx, const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix,
+                  const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
+                  double margin, double* d_out, void* stream);
+
+/* ---- Row L2: update of learning_process (make_exps.py:130-141) ------------------------
+ * g = mean_s(d_grads[s]) + reg * w  (shards summed in order, then / n_shards — np.mean axis 0)
+ * momentum: dw = momentum * dw + lr * g;  SGD (momentum < 0): dw = lr * g;   w = w - dw. */
+int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, int32_t n_shards, int64_t d,
+                  double reg, double lr, double momentum, void* stream);
+
+/* ---- f1: scores = A @ w for a row-major (n, d) matrix (evaluation_step, make_exps.py:163,
+ * :170-171).  Row dot products in index order. */
+int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w, double* d_out,
+                void* stream);
+
+/* ---- Row A6/A9/(e): repartition on the device ----------------------------------------
+ * Keyed pseudo-random permutation of [0, n): a 4-round Feistel network over the smallest
+ * even-bit power-of-two domain >= n, with cycle walking (a bijection on [0, n)).
+ * tw_permute_scatter: d_out[perm(i)] = d_in[i] for i in [0, n) (8-byte elements).
+ * tw_perm_index: d_perm[i] = perm(i). */
+int tw_permute_scatter(const void* d_in, void* d_out, int64_t n, uint64_t key, void* stream);
+int tw_perm_index(int64_t* d_perm, int64_t n, int64_t base, int64_t n_total, uint64_t key,
+                  void* stream);
+
+/* ---- (e) multi-rank repartition: counting sort of this rank's elements by destination rank
+ * (dest = perm / n_loc, G <= 64 ranks), packed as 16-byte records {value bits, dest-local
+ * position} for an all-to-all(v); the receiver scatters the records into its local array.
+ * tw_rank_histogram: d_counts[g] = #elements bound for rank g.  tw_bucket_scatter: record of
+ * element i goes to d_send[2*(d_start[dst] + k)], k a per-destination cursor (d_cursor, G
+ * uint64 scratch).  tw_scatter_records: d_out[rec.pos] = rec.value for m records. */
+int tw_rank_histogram(const int64_t* d_perm, int64_t n, int64_t n_loc, int32_t G,
+                      uint64_t* d_counts, void* stream);
+int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int64_t n, int64_t n_loc,
+                      int32_t G, const int64_t* d_start, uint64_t* d_cursor, void* d_send,
+                      void* stream);
+int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TUPLEWISE_H */

@@ -1,0 +1,323 @@
+"""ORACLE — test infrastructure only.  CPU restatement of the reference's hot path.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker (or, for cpu_baseline, as the timed CPU port).  The product package
+never imports it; the product path fails loudly without the HIP library.
+
+Every function restates one reference function (RobinVogel/Trade-offs-in-Distributed-
+Tuplewise-Estimation-and-Learning) with NumPy, citing file:line.  Parity is PINNED: the
+restatement is checked against golden vectors produced by the reference itself
+(tests/golden/make_golden.py imports the reference read-only; tests/test_oracle_golden.py).
+
+Beyond the reference (the device-only paths, whose results NumPy never produced):
+  feistel_perm / philox4x32_10 restate csrc/permute.hip and csrc/count.hip bit for bit so the
+  device-RNG repartition and incomplete paths can be checked exactly on small inputs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# ----------------------------------------------------------------- estimators (reference)
+
+
+def un_count(X, Z) -> int:
+    """#{(i,j): X_i > Z_j}: the integer behind est.Un (estimation-experiment/main.py:29-31)."""
+    return int((np.asarray(X).reshape((-1, 1)) > np.asarray(Z).reshape((1, -1))).sum())
+
+
+def est_Un(X, Z):
+    """estimation-experiment/main.py:29-31"""
+    return (X.reshape((-1, 1)) > Z.reshape((1, -1))).mean()
+
+
+def cs_Un(X, Z, kernel="prod"):
+    """learning-experiment/compute_stats.py:10-19"""
+    X_col = X.reshape((-1, 1))
+    Z_row = Z.reshape((1, -1))
+    assert kernel in ["prod", "gini", "AUC"]
+    if kernel == "prod":
+        return (X_col.dot(Z_row)).mean()
+    if kernel == "gini":
+        return np.mean(np.abs(X_col - Z_row))
+    return np.mean((X_col - Z_row > 0).astype(int))
+
+
+def UB_indices(X, Z, ind_X, ind_Z, kernel):
+    """compute_stats.py:22-30"""
+    X_select = X[ind_X]
+    Z_select = Z[ind_Z]
+    assert kernel in ["prod", "gini", "AUC"]
+    if kernel == "prod":
+        return np.mean(X_select * Z_select)
+    if kernel == "gini":
+        return np.mean(np.abs(X_select - Z_select))
+    return np.mean((X_select - Z_select > 0).astype(int))
+
+
+def UB_pairs(X, Z, indices, kernel):
+    """compute_stats.py:32-35"""
+    idx = np.asarray(indices).reshape(-1, 2)
+    return UB_indices(X, Z, idx[:, 0], idx[:, 1], kernel)
+
+
+def UB(X, Z, B, kernel="prod"):
+    """compute_stats.py:37-42 (draw order: X indices, then Z indices)"""
+    return UB_indices(X, Z, np.random.randint(0, X.shape[0], B),
+                      np.random.randint(0, Z.shape[0], B), kernel)
+
+
+def UN(X, Z, N, f_block, sampling_type="SWOR", variant="cs"):
+    """compute_stats.py:56-92 (variant "cs") / estimation-experiment/main.py:33-69 ("est").
+    The two differ only for degenerate blocks (k in (0, tau)): cs asserts SWOR and appends 0;
+    est appends 0 for SWOR and skips the block otherwise."""
+    vals = []
+    X_rem, Z_rem = X, Z
+    np.random.shuffle(X_rem)
+    np.random.shuffle(Z_rem)
+    n_X, n_Z = X_rem.shape[0], Z_rem.shape[0]
+    tau = int((n_X + n_Z) / N)
+    for _ in range(N):
+        if sampling_type != "prop-SWR":
+            if sampling_type.startswith("prop"):
+                k = int(n_X / N)
+            else:
+                n_X, n_Z = X_rem.shape[0], Z_rem.shape[0]
+                k = np.random.binomial(tau, n_X / (n_X + n_Z))
+            if k in (0, tau):
+                if variant == "cs":
+                    assert sampling_type == "SWOR"
+                    vals.append(0)
+                elif sampling_type == "SWOR":
+                    vals.append(0)
+            else:
+                vals.append(f_block(X_rem[:k], Z_rem[:(tau - k)]))
+            X_rem = X_rem[k:]
+            Z_rem = Z_rem[(tau - k):]
+        elif sampling_type == "prop-SWR":
+            vals.append(f_block(X_rem[np.random.randint(0, n_X, int(n_X / N))],
+                                Z_rem[np.random.randint(0, n_Z, int(n_Z / N))]))
+    return np.mean(vals)
+
+
+def est_UnN(X, Z, N, sampling_type):
+    """estimation-experiment/main.py:72-74"""
+    return UN(X, Z, N, est_Un, sampling_type, variant="est")
+
+
+def est_UnNT(X, Z, N, T, sampling_type):
+    """estimation-experiment/main.py:76-79"""
+    return np.mean([est_UnN(X, Z, N, sampling_type) for _ in range(T)])
+
+
+def cs_UnN(X, Z, N, sampling_type, kernel="prod"):
+    """compute_stats.py:95-101"""
+    return UN(X, Z, N, lambda x, z: cs_Un(x, z, kernel=kernel), sampling_type, "cs")
+
+
+def cs_UnNB(X, Z, N, B, sampling_type, kernel="prod"):
+    """compute_stats.py:104-110"""
+    return UN(X, Z, N, lambda x, z: UB(x, z, B, kernel=kernel), sampling_type, "cs")
+
+
+def cs_UnNT(X, Z, N, T, sampling_type, kernel="prod"):
+    """compute_stats.py:113-116"""
+    return np.mean([cs_UnN(X, Z, N, sampling_type, kernel) for _ in range(T)])
+
+
+def cs_UnNBT(X, Z, N, B, T, sampling_type, kernel="prod"):
+    """compute_stats.py:119-123"""
+    return np.mean([cs_UnNB(X, Z, N, B, sampling_type, kernel) for _ in range(T)])
+
+
+def SWR_divide(X, Z, N):
+    """compute_stats.py:48-54 (all N X-draws first, then all N Z-draws)"""
+    n_X, n_Z = X.shape[0], Z.shape[0]
+    X_s = [X[np.random.randint(0, n_X, int(n_X / N))] for _ in range(N)]
+    Z_s = [Z[np.random.randint(0, n_Z, int(n_Z / N))] for _ in range(N)]
+    return X_s, Z_s
+
+
+def UN_split(X_s, Z_s, f_block):
+    """compute_stats.py:44-46"""
+    return np.mean([f_block(X, Z) for X, Z in zip(X_s, Z_s)], axis=0)
+
+
+def conv_AUC(margin):
+    """compute_stats.py:129-135"""
+    def res_function(X, Z):
+        return np.maximum(Z.reshape((1, -1)) - X.reshape((-1, 1)) + margin, 0).mean()
+    return res_function
+
+
+def conv_AUC_deter_pairs(margin):
+    """compute_stats.py:137-144"""
+    def res(X, Z, indices):
+        idx = np.asarray(indices).reshape(-1, 2)
+        return np.maximum(Z[idx[:, 1]] - X[idx[:, 0]] + margin, 0).mean()
+    return res
+
+
+def grad_inc_block(w, B, margin):
+    """compute_stats.py:146-162"""
+    def res(X, Z):
+        X_sel = X[np.random.randint(0, X.shape[0], B)]
+        Z_sel = Z[np.random.randint(0, Z.shape[0], B)]
+        diff = Z_sel - X_sel
+        S_diff = diff.dot(w) + margin
+        filt = (S_diff > 0).ravel()
+        return (diff[filt].sum(axis=0) / B).reshape([-1, 1])
+    return res
+
+
+def sgd_step(w, delta_w, gradient_mean, reg, learning_rate, optim_type="momentum"):
+    """learning-experiment/make_exps.py:130-141"""
+    gradient = gradient_mean + reg * w
+    if optim_type == "SGD":
+        delta_w = learning_rate * gradient
+    if optim_type == "momentum":
+        delta_w = 0.9 * delta_w + learning_rate * gradient
+    return w - delta_w, delta_w
+
+
+def learning_trajectory(X, Z, p_learn, capture_every=1):
+    """learning_process (make_exps.py:96-141) without evaluation: returns the w before every
+    gradient step (the values the reference passes to grad_inc_block at :130)."""
+    N, B = p_learn["N"], p_learn["B"]
+    w = p_learn["w_init"]
+    ws = []
+    X_s, Z_s = SWR_divide(X, Z, N)
+    delta_w = 0
+    for i in range(p_learn["n_it"]):
+        if i % p_learn["reshuffle_mod"] == 0:
+            X_s, Z_s = SWR_divide(X, Z, N)
+        if i % capture_every == 0:
+            ws.append(np.array(w, copy=True))
+        g = UN_split(X_s, Z_s, grad_inc_block(w, B, p_learn["margin"]))
+        w, delta_w = sgd_step(w, delta_w, g, p_learn["reg"], p_learn["learning_rate"])
+    return ws, w
+
+
+# ----------------------------------------------------------------- theory (reference)
+def Mean_Un(e):
+    """estimation-experiment/main.py:26-27 with p(e)=e, q(e)=1-e (:10-14)"""
+    return (1 - e) + e * (1 - e)
+
+
+def Var_Un(e, n, m):
+    """estimation-experiment/main.py:16-23, :103-104"""
+    p, q = e, 1 - e
+    s1 = (p ** 2) * q * (1 - q)
+    s2 = ((1 - q) ** 2) * p * (1 - p)
+    s0 = p * q * (1 - p) * (1 - q)
+    return s1 / n + s2 / m + s0 / (n * m)
+
+
+# ----------------------------------------------------------------- exact large-n count
+def count_gt_sorted(X, Z) -> int:
+    """#{(i,j): X_i > Z_j} in O((n+m) log m) (NaN-free inputs): for each x, the number of z
+    strictly below it.  Same integer as un_count; feasible at n = 1e6 where the reference's
+    n*m boolean temporary is not."""
+    zs = np.sort(np.asarray(Z).reshape(-1))
+    return int(np.searchsorted(zs, np.asarray(X).reshape(-1), side="left").sum())
+
+
+def count_half_sorted(X, Z) -> int:
+    """2*#{x>z} + #{x==z} (tie_mode="half" half-units)."""
+    zs = np.sort(np.asarray(Z).reshape(-1))
+    x = np.asarray(X).reshape(-1)
+    lo = np.searchsorted(zs, x, side="left")
+    hi = np.searchsorted(zs, x, side="right")
+    return int((lo + hi).sum())
+
+
+# ----------------------------------------------------------------- device-RNG restatements
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _mix32(v):
+    v = v & _M32
+    v ^= v >> np.uint64(16)
+    v = (v * np.uint64(0x85EBCA6B)) & _M32
+    v ^= v >> np.uint64(13)
+    v = (v * np.uint64(0xC2B2AE35)) & _M32
+    v ^= v >> np.uint64(16)
+    return v
+
+
+def _feistel_keys(n: int, key: int):
+    bits = 2
+    while bits < 62 and (1 << bits) < n:
+        bits += 1
+    if bits & 1:
+        bits += 1
+    half = bits // 2
+    st = (key ^ 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+    ks = []
+    for _ in range(6):
+        st = (st + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+        z = st
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2 ** 64 - 1)
+        z ^= z >> 31
+        ks.append(z & 0xFFFFFFFF)
+    return half, ks
+
+
+def feistel_perm(idx, n: int, key: int) -> np.ndarray:
+    """Restates csrc/permute.hip feistel_perm: keyed bijection of [0, n)."""
+    half, ks = _feistel_keys(n, key)
+    mask = np.uint64((1 << half) - 1)
+    hb = np.uint64(half)
+
+    def once(v):
+        L = (v >> hb) & mask
+        R = v & mask
+        for k in ks:
+            nL = R
+            R = (L ^ _mix32((R * np.uint64(0x9E3779B1) + np.uint64(k)) & _M32)) & mask
+            L = nL
+        return (L << hb) | R
+
+    v = once(np.asarray(idx, dtype=np.uint64))
+    while True:
+        bad = v >= np.uint64(n)
+        if not bad.any():
+            return v.astype(np.int64)
+        v[bad] = once(v[bad])
+
+
+def permute_scatter(vals: np.ndarray, key: int) -> np.ndarray:
+    """out[perm(i)] = vals[i] (tw_permute_scatter)."""
+    out = np.empty_like(vals)
+    out[feistel_perm(np.arange(len(vals)), len(vals), key)] = vals
+    return out
+
+
+def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
+    """Philox4x32-10 (Salmon et al. 2011), vectorised; restates csrc/count.hip."""
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    W0, W1 = 0x9E3779B9, 0xBB67AE85
+    a, b, c, d = (np.asarray(v, dtype=np.uint64) & _M32 for v in (c0, c1, c2, c3))
+    for _ in range(10):
+        p0 = a * M0
+        p1 = c * M1
+        hi0, lo0 = p0 >> np.uint64(32), p0 & _M32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & _M32
+        a, b, c, d = (hi1 ^ b ^ np.uint64(k0)) & _M32, lo1, (hi0 ^ d ^ np.uint64(k1)) & _M32, lo0
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return a, b, c, d
+
+
+def _mulhi64(a: np.ndarray, n: int) -> np.ndarray:
+    return np.array([(int(v) * n) >> 64 for v in a], dtype=np.int64)
+
+
+def rng_pairs(nx: int, nz: int, B: int, seed: int, shard: int):
+    """The (i, j) pairs tw_count_pairs_rng draws for one shard (global shard index)."""
+    p = np.arange(B, dtype=np.uint64)
+    a, b, c, d = philox4x32_10(p & _M32, p >> np.uint64(32), np.full(B, shard, np.uint64),
+                               np.zeros(B, np.uint64), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    u = (b << np.uint64(32)) | a
+    v = (d << np.uint64(32)) | c
+    return _mulhi64(u, nx), _mulhi64(v, nz)

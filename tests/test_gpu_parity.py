@@ -1,0 +1,215 @@
+"""HIP path vs the reference's golden vectors and vs the pinned oracle (MI355X).
+
+Bar: bit-exact for every count-derived value (U-statistics are count / #pairs); float-valued
+kernels (prod, gini, hinge) within rtol 1e-12 of NumPy (different summation order); the
+hinge gradient within 1e-12 relative (only BLAS's dot-product order can differ).
+"""
+import warnings
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["gauss", "bern_int64", "ties_int", "edge_float", "n1", "m1", "ragged", "int64_wrap",
+         "float32", "col_scores"]
+FLOAT_RTOL = 1e-12
+
+
+def same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_un_golden(gpu, golden, case):
+    import tuplewise.estimation as est
+    import tuplewise.compute_stats as cs
+    X, Z = golden[f"un/{case}/X"], golden[f"un/{case}/Z"]
+    assert same(est.Un(X, Z), golden[f"un/{case}/est_Un"])
+    assert same(cs.Un(X, Z, kernel="AUC"), golden[f"un/{case}/cs_AUC"])
+    if f"un/{case}/cs_prod" in golden:
+        # float32 inputs: NumPy accumulates in float32 (~1e-7 relative per add), we in float64
+        rtol = FLOAT_RTOL if X.dtype == np.float64 else 1e-5
+        for k in ("prod", "gini"):
+            got = cs.Un(X, Z, kernel=k)
+            assert np.asarray(got).dtype == golden[f"un/{case}/cs_{k}"].dtype
+            np.testing.assert_allclose(got, golden[f"un/{case}/cs_{k}"], rtol=rtol, atol=1e-15)
+        np.testing.assert_allclose(cs.conv_AUC(1)(X, Z), golden[f"un/{case}/conv_AUC"],
+                                   rtol=rtol)
+
+
+def _calls():
+    import tuplewise.estimation as est
+    import tuplewise.compute_stats as cs
+    return {
+        "est_UnN_propSWOR": lambda X, Z: est.UnN(X, Z, 10, "prop-SWOR"),
+        "est_UnN_SWOR": lambda X, Z: est.UnN(X, Z, 10, "SWOR"),
+        "est_UnN_propSWR": lambda X, Z: est.UnN(X, Z, 10, "prop-SWR"),
+        "est_UnNT_propSWOR": lambda X, Z: est.UnNT(X, Z, 10, 4, "prop-SWOR"),
+        "est_UnNT_bern": lambda X, Z: est.UnNT(X, Z, 10, 4, "prop-SWOR"),
+        "est_UnN_SWOR_degenerate": lambda X, Z: est.UnN(X, Z, 40, "SWOR"),
+        "est_UnN_prop_degenerate": lambda X, Z: est.UnN(X, Z, 40, "prop-SWOR"),
+        "cs_UnN_AUC": lambda X, Z: cs.UnN(X, Z, 10, "prop-SWOR", kernel="AUC"),
+        "cs_UnN_AUC_SWOR": lambda X, Z: cs.UnN(X, Z, 10, "SWOR", kernel="AUC"),
+        "cs_UnN_prod": lambda X, Z: cs.UnN(X, Z, 10, "prop-SWOR"),
+        "cs_UnN_gini_SWR": lambda X, Z: cs.UnN(X, Z, 10, "prop-SWR", kernel="gini"),
+        "cs_UnNB_AUC": lambda X, Z: cs.UnNB(X, Z, 10, 500, "prop-SWOR", kernel="AUC"),
+        "cs_UnNB_AUC_SWR": lambda X, Z: cs.UnNB(X, Z, 10, 300, "prop-SWR", kernel="AUC"),
+        "cs_UnNBT_AUC": lambda X, Z: cs.UnNBT(X, Z, 10, 200, 3, "SWOR", kernel="AUC"),
+        "cs_UnNT_AUC": lambda X, Z: cs.UnNT(X, Z, 10, 3, "prop-SWOR", kernel="AUC"),
+        "cs_UnNB_prod": lambda X, Z: cs.UnNB(X, Z, 10, 400, "prop-SWOR"),
+    }
+
+
+FLOAT_SHARDED = {"cs_UnN_prod", "cs_UnN_gini_SWR", "cs_UnNB_prod"}
+
+
+@pytest.mark.parametrize("name", [
+    "est_UnN_propSWOR", "est_UnN_SWOR", "est_UnN_propSWR", "est_UnNT_propSWOR", "est_UnNT_bern",
+    "est_UnN_SWOR_degenerate", "est_UnN_prop_degenerate", "cs_UnN_AUC", "cs_UnN_AUC_SWOR",
+    "cs_UnN_prod", "cs_UnN_gini_SWR", "cs_UnNB_AUC", "cs_UnNB_AUC_SWR", "cs_UnNBT_AUC",
+    "cs_UnNT_AUC", "cs_UnNB_prod"])
+def test_sharded_golden(gpu, golden, name):
+    fn = _calls()[name]
+    X, Z = golden[f"sh/{name}/X"].copy(), golden[f"sh/{name}/Z"].copy()
+    np.random.seed(int(golden[f"sh/{name}/seed"]))
+    with warnings.catch_warnings(), np.errstate(all="ignore"):
+        warnings.simplefilter("ignore")
+        val = fn(X, Z)
+    if name in FLOAT_SHARDED:
+        np.testing.assert_allclose(val, golden[f"sh/{name}/value"], rtol=FLOAT_RTOL)
+    else:
+        assert same(val, golden[f"sh/{name}/value"]), (val, golden[f"sh/{name}/value"])
+    # in-place shuffle side effect and RNG consumption identical to the reference
+    assert same(X, golden[f"sh/{name}/X_after"]) and same(Z, golden[f"sh/{name}/Z_after"])
+    assert np.random.randint(0, 2 ** 31 - 1) == golden[f"sh/{name}/probe"]
+
+
+def test_indexed_golden(gpu, golden):
+    import tuplewise.compute_stats as cs
+    X, Z, ix, iz = golden["idx/X"], golden["idx/Z"], golden["idx/ix"], golden["idx/iz"]
+    assert same(cs.UB_indices(X, Z, ix, iz, "AUC"), golden["idx/UB_indices_AUC"])
+    for k in ("prod", "gini"):
+        np.testing.assert_allclose(cs.UB_indices(X, Z, ix, iz, k), golden[f"idx/UB_indices_{k}"],
+                                   rtol=FLOAT_RTOL)
+    pairs = list(zip(list(ix), list(iz)))
+    assert same(cs.UB_pairs(X, Z, pairs, "AUC"), golden["idx/UB_pairs_AUC"])
+    np.testing.assert_allclose(cs.conv_AUC_deter_pairs(1)(X, Z, pairs), golden["idx/conv_deter"],
+                               rtol=FLOAT_RTOL)
+    np.random.seed(77)
+    assert same(cs.UB(X, Z, 1000, kernel="AUC"), golden["idx/UB_AUC_seed77"])
+
+
+def test_grad_golden(gpu, golden):
+    import tuplewise.compute_stats as cs
+    X, Z, w = golden["grad/X"], golden["grad/Z"], golden["grad/w"]
+    np.random.seed(5)
+    g = cs.grad_inc_block(w, 100, 1)(X, Z)
+    np.testing.assert_allclose(g, golden["grad/single_seed5"], rtol=1e-12, atol=1e-15)
+    np.random.seed(6)
+    Xs, Zs = cs.SWR_divide(X, Z, 10)
+    gs = cs.UN_split(Xs, Zs, cs.grad_inc_block(w, 50, 1))
+    np.testing.assert_allclose(gs, golden["grad/split_seed6"], rtol=1e-12, atol=1e-15)
+    assert gs.shape == golden["grad/split_seed6"].shape
+
+
+# ------------------------------------------------------------------ kernels vs oracle
+@pytest.mark.parametrize("dtype", ["f64", "i64"])
+@pytest.mark.parametrize("mode", ["gt", "half"])
+def test_count_kernel_ragged_shards(gpu, dtype, mode):
+    from tuplewise import _engine as E, _lib as L
+    rng = np.random.RandomState(7)
+    nx = [0, 1, 5, 257, 3000, 1, 4096 + 3, 700]
+    nz = [3, 0, 9, 1000, 2049, 1, 513, 700]
+    if dtype == "f64":
+        xs = [rng.normal(size=k).round(1) for k in nx]  # rounding forces ties
+        zs = [rng.normal(size=k).round(1) for k in nz]
+        code = L.TW_F64
+    else:
+        xs = [rng.randint(-20, 20, k) for k in nx]
+        zs = [rng.randint(-20, 20, k) for k in nz]
+        code = L.TW_I64
+    sh = E.Shards.from_blocks(xs, zs, code)
+    got = E.count_complete(sh, mode)
+    for s, (x, z) in enumerate(zip(xs, zs)):
+        want = O.un_count(x, z) if mode == "gt" else O.count_half_sorted(x, z)
+        assert int(got[s]) == want, (s, int(got[s]), want)
+
+
+def test_count_c2_single_shard_1e5(gpu):
+    """BASELINE config C2: n = m = 1e5 in one shard (1e10 pairs), exact vs O(n log n) count."""
+    import tuplewise.estimation as est
+    rng = np.random.RandomState(2)
+    X, Z = rng.normal(0.5, 1, 100_000), rng.normal(0, 1, 100_000)
+    v = est.Un(X, Z)
+    c = O.count_gt_sorted(X, Z)
+    assert v == np.float64(c) / np.float64(10 ** 10)
+
+
+def test_device_sharded_sample_matches_oracle(gpu):
+    """Device repartition (Feistel) + one-launch count == oracle restatement, per shard."""
+    import torch
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(4)
+    n, m, N = 20_000, 15_000, 16
+    X, Z = rng.normal(0.3, 1, n), rng.normal(0, 1, m)
+    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
+    key = 99
+    v = S.UnN(key)
+    Xp = O.permute_scatter(X, 2 * key)
+    Zp = O.permute_scatter(Z, 2 * key + 1)
+    assert np.array_equal(S.X.cpu().numpy(), Xp) and np.array_equal(S.Z.cpu().numpy(), Zp)
+    k, tau = int(n / N), int((n + m) / N)
+    vals = [O.un_count(Xp[s * k:(s + 1) * k], Zp[s * (tau - k):(s + 1) * (tau - k)])
+            / (k * (tau - k)) for s in range(N)]
+    assert v == np.mean(vals)
+
+
+def test_device_rng_incomplete_matches_oracle(gpu):
+    import torch
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(8)
+    n, m, N, B = 4000, 3000, 4, 777
+    X, Z = rng.normal(0.2, 1, n), rng.normal(0, 1, m)
+    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
+    seed = 0x1234_5678_9ABC
+    v = S.UnNB(B, seed)
+    k, tau = int(n / N), int((n + m) / N)
+    vals = []
+    for s in range(N):
+        xs, zs = X[s * k:(s + 1) * k], Z[s * (tau - k):(s + 1) * (tau - k)]
+        i, j = O.rng_pairs(len(xs), len(zs), B, seed, s)
+        vals.append(np.float64(int((xs[i] > zs[j]).sum())) / np.float64(B))
+    assert v == np.mean(vals)
+
+
+def test_north_star_config_exact(gpu):
+    """BASELINE config C3 shape: n = 1e6 per class, N = 64 shards (1.5625e10 pairs), one
+    repartition on the device; every shard's count equals the oracle's exact count."""
+    import torch
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(5)
+    n, N = 1_000_000, 64
+    X, Z = rng.normal(0.5, 1, n), rng.normal(0, 1, n)
+    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
+    S.repartition(7)
+    counts = S.local_counts().cpu().numpy()
+    Xp, Zp = S.X.cpu().numpy(), S.Z.cpu().numpy()
+    assert np.array_equal(np.sort(Xp), np.sort(X))  # a permutation
+    k = n // N
+    for s in range(N):
+        assert counts[s] == O.count_gt_sorted(Xp[s * k:(s + 1) * k], Zp[s * k:(s + 1) * k])
+
+
+def test_errors_match_reference(gpu):
+    import tuplewise.compute_stats as cs
+    X, Z = np.random.normal(size=10), np.random.normal(size=5)
+    with pytest.raises(AssertionError):
+        cs.Un(X, Z, kernel="bogus")
+    with pytest.raises(AssertionError):
+        cs.UN(X.copy(), Z.copy(), 20, cs.Un, sampling_type="prop-SWOR")  # k == 0 block
+    with pytest.raises(TypeError):
+        cs.Un(np.array([True, False]), np.array([False]), kernel="AUC")

@@ -1,0 +1,248 @@
+"""The block protocol of the reference and its one-launch dispatch.
+
+The reference's distributed estimator is a serial loop over N simulated workers (UN,
+learning-experiment/compute_stats.py:56-92 and estimation-experiment/main.py:33-69): shuffle
+the caller's arrays in place, cut consecutive blocks (or resample them), call
+``f_block(X_block, Z_block)`` per block, and average.  Here the loop still runs on the host —
+it owns the NumPy global RNG, whose draws must happen in exactly the reference's order — but
+it only *plans*: block boundaries, index draws and degenerate-block handling.  The block
+functions this package returns carry a ``_tw_block`` spec; ``run_un`` hands all planned
+blocks of such a spec to one device launch and then averages with the reference's own
+``np.mean``.  A user-supplied f_block without a spec is called block by block, exactly as the
+reference does (that is the reference protocol, not a fallback of our kernels).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _engine as E
+from . import _lib as L
+
+
+class Block:
+    """One planned block: x/z are either (start, stop) slices of the shuffled arrays or index
+    arrays (prop-SWR resampling); aux holds RNG draws the block function made."""
+    __slots__ = ("x", "z", "aux")
+
+    def __init__(self, x, z, aux=None):
+        self.x, self.z, self.aux = x, z, aux
+
+    def nx(self) -> int:
+        return (self.x[1] - self.x[0]) if isinstance(self.x, tuple) else len(self.x)
+
+    def nz(self) -> int:
+        return (self.z[1] - self.z[0]) if isinstance(self.z, tuple) else len(self.z)
+
+
+def _flat(a: np.ndarray) -> np.ndarray:
+    return np.asarray(a).reshape(-1)
+
+
+def _layout(arr_dev, blocks, side: str):
+    """Device array + int64 offsets (len(blocks)+1) for the blocks' x or z parts."""
+    parts = [getattr(b, side) for b in blocks]
+    if all(isinstance(p, tuple) for p in parts):
+        # consecutive slices (possibly of length 0) of one array: offsets straight into it
+        starts = np.array([p[0] for p in parts], dtype=np.int64)
+        stops = np.array([p[1] for p in parts], dtype=np.int64)
+        if len(parts) == 0 or np.all(starts[1:] == stops[:-1]):
+            off = np.concatenate([starts[:1], stops]).astype(np.int64)
+            return arr_dev, off
+    # resampled blocks: gather on the device into one concatenated array
+    t = L.torch()
+    idx = [np.arange(p[0], p[1], dtype=np.int64) if isinstance(p, tuple)
+           else np.asarray(p, dtype=np.int64) for p in parts]
+    off = np.concatenate([[0], np.cumsum([len(i) for i in idx])]).astype(np.int64)
+    cat = np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
+    gathered = arr_dev.index_select(0, t.from_numpy(cat).to(arr_dev.device))
+    return gathered, off
+
+
+class BlockSpec:
+    """Descriptor of a package block function (see module docstring)."""
+
+    def draw(self, nx: int, nz: int):
+        """RNG draws the reference block function makes on a block of this shape."""
+        return None
+
+    def evaluate(self, X: np.ndarray, Z: np.ndarray, blocks: list) -> list:
+        raise NotImplementedError
+
+
+class CompleteCount(BlockSpec):
+    """Un-type block: exact count of a comparison predicate over all pairs, divided by nx*nz.
+
+    literal_sub=False: est.Un ``X > Z`` (estimation-experiment/main.py:31)
+    literal_sub=True : cs.Un AUC ``(X - Z) > 0`` (compute_stats.py:19)
+    tie_mode="half" : opt-in +0.5 on ties (BASELINE.json); value = half-units / (2 nx nz)."""
+
+    def __init__(self, literal_sub: bool, tie_mode: str = "strict"):
+        self.literal_sub = literal_sub
+        self.tie_mode = tie_mode
+
+    def operands(self, X, Z):
+        if self.literal_sub:
+            x, z, code, mode = E.subtract_gt_operands(X, Z)
+        else:
+            (x, z, code), mode = E.compare_operands(X, Z), "gt"
+        if self.tie_mode == "half":
+            if mode != "gt" and mode != "subgt":
+                raise NotImplementedError("tie_mode='half' needs an ordered comparison")
+            mode = "half"
+        return x, z, code, mode
+
+    def evaluate(self, X, Z, blocks):
+        x, z, code, mode = self.operands(_flat(X), _flat(Z))
+        xd, zd = L.to_device(x), L.to_device(z)
+        xa, xo = _layout(xd, blocks, "x")
+        za, zo = _layout(zd, blocks, "z")
+        counts = E.count_complete(E.Shards(xa, xo, za, zo, code), mode)
+        out = []
+        for b, c in zip(blocks, counts):
+            pairs = b.nx() * b.nz()
+            out.append(E.ratio(c, 2 * pairs) if mode == "half" else E.ratio(c, pairs))
+        return out
+
+
+class CompleteSum(BlockSpec):
+    """cs.Un prod/gini (compute_stats.py:15-18) and conv_AUC (compute_stats.py:129-135):
+    mean over all pairs of a float kernel."""
+
+    def __init__(self, kern: int, margin: float = 0.0):
+        self.kern = kern
+        self.margin = margin
+
+    def evaluate(self, X, Z, blocks):
+        x = _flat(X).astype(np.float64, copy=False)
+        z = _flat(Z).astype(np.float64, copy=False)
+        xd, zd = L.to_device(x), L.to_device(z)
+        xa, xo = _layout(xd, blocks, "x")
+        za, zo = _layout(zd, blocks, "z")
+        sums = E.pair_sum_complete(E.Shards(xa, xo, za, zo, L.TW_F64), self.kern, self.margin)
+        # NumPy returns the mean in the operands' float type (float32 stays float32); the
+        # device accumulates in float64, so float32 results are the better-rounded value.
+        rt = np.result_type(np.asarray(X).dtype, np.asarray(Z).dtype)
+        cast = rt.type if rt.kind == "f" else np.float64
+        return [cast(s / np.float64(b.nx() * b.nz())) for b, s in zip(blocks, sums)]
+
+
+class Incomplete(BlockSpec):
+    """cs.UB (compute_stats.py:37-42): B pairs drawn with replacement by two randint calls
+    (X indices first, then Z indices), then UB_indices on them."""
+
+    def __init__(self, B: int, kernel: str):
+        self.B = int(B)
+        self.kernel = kernel
+
+    def draw(self, nx, nz):
+        ix = np.random.randint(0, nx, self.B)
+        iz = np.random.randint(0, nz, self.B)
+        return ix, iz
+
+    def evaluate(self, X, Z, blocks):
+        ix_abs, iz_abs, offs = [], [], [0]
+        xs = _flat(X)
+        zs = _flat(Z)
+        # absolute positions: slices are offsets into X/Z, resampled blocks map through idx
+        for b in blocks:
+            ix, iz = b.aux
+            ix_abs.append(ix + b.x[0] if isinstance(b.x, tuple) else np.asarray(b.x)[ix])
+            iz_abs.append(iz + b.z[0] if isinstance(b.z, tuple) else np.asarray(b.z)[iz])
+            offs.append(offs[-1] + len(ix))
+        return indexed_values(xs, zs, np.concatenate(ix_abs), np.concatenate(iz_abs),
+                              np.array(offs, dtype=np.int64), self.kernel)
+
+
+def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,
+                   pair_off: np.ndarray, kernel: str, margin: float = 0.0) -> list:
+    """Per-shard means of `kernel` over index pairs (UB_indices semantics, compute_stats.py:22-30)."""
+    npairs = np.diff(pair_off)
+    if kernel == "AUC":
+        xx, zz, code, mode = E.subtract_gt_operands(x, z)
+        counts = E.count_indexed(L.to_device(xx), L.to_device(zz), code, ix, iz, pair_off, mode)
+        return [E.ratio(c, p) for c, p in zip(counts, npairs)]
+    kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI, "hinge": L.TW_KERN_HINGE}[kernel]
+    xd = L.to_device(x.astype(np.float64, copy=False))
+    zd = L.to_device(z.astype(np.float64, copy=False))
+    sums = E.pair_sum_indexed(xd, zd, ix, iz, pair_off, kern, margin)
+    return [np.float64(s / np.float64(p)) for s, p in zip(sums, npairs)]
+
+
+def run_un(X, Z, N, f_block, sampling_type, variant: str):
+    """Shared body of UN (compute_stats.py:56-92, variant "cs"; estimation-experiment/main.py
+    :33-69, variant "est").  Keeps the in-place shuffle and every RNG draw in order."""
+    vals = list()
+    X_rem = X
+    Z_rem = Z
+    np.random.shuffle(X_rem)
+    np.random.shuffle(Z_rem)
+    n_X = X_rem.shape[0]
+    n_Z = Z_rem.shape[0]
+    tau = int((n_X + n_Z) / N)
+    spec = getattr(f_block, "_tw_block", None)
+
+    if spec is None:  # user block function: the reference protocol, block by block
+        return _run_un_python(X_rem, Z_rem, N, f_block, sampling_type, variant, n_X, n_Z, tau)
+
+    plan = []  # ("val", block) | ("zero",) in the order the reference appends
+    x_pos = z_pos = 0
+    for _ in range(N):
+        if sampling_type != "prop-SWR":
+            if sampling_type.startswith("prop"):
+                k = int(n_X / N)
+            else:
+                n_X = X_rem.shape[0] - x_pos
+                n_Z = Z_rem.shape[0] - z_pos
+                k = np.random.binomial(tau, n_X / (n_X + n_Z))
+            if k in (0, tau):
+                if variant == "cs":
+                    assert sampling_type == "SWOR"
+                    plan.append(("zero",))
+                elif sampling_type == "SWOR":
+                    plan.append(("zero",))
+            else:
+                xs = (x_pos, min(x_pos + k, X_rem.shape[0]))
+                zs = (z_pos, min(z_pos + tau - k, Z_rem.shape[0]))
+                blk = Block(xs, zs)
+                blk.aux = spec.draw(blk.nx(), blk.nz())
+                plan.append(("val", blk))
+            x_pos = min(x_pos + k, X_rem.shape[0])
+            z_pos = min(z_pos + (tau - k), Z_rem.shape[0])
+        elif sampling_type == "prop-SWR":
+            ix = np.random.randint(0, n_X, int(n_X / N))
+            iz = np.random.randint(0, n_Z, int(n_Z / N))
+            blk = Block(ix, iz)
+            blk.aux = spec.draw(blk.nx(), blk.nz())
+            plan.append(("val", blk))
+
+    blocks = [p[1] for p in plan if p[0] == "val"]
+    values = iter(spec.evaluate(X_rem, Z_rem, blocks) if blocks else [])
+    for p in plan:
+        vals.append(0 if p[0] == "zero" else next(values))
+    return np.mean(vals)
+
+
+def _run_un_python(X_rem, Z_rem, N, f_block, sampling_type, variant, n_X, n_Z, tau):
+    vals = list()
+    for _ in range(N):
+        if sampling_type != "prop-SWR":
+            if sampling_type.startswith("prop"):
+                k = int(n_X / N)
+            else:
+                n_X = X_rem.shape[0]
+                n_Z = Z_rem.shape[0]
+                k = np.random.binomial(tau, n_X / (n_X + n_Z))
+            if k in (0, tau):
+                if variant == "cs":
+                    assert sampling_type == "SWOR"
+                    vals.append(0)
+                elif sampling_type == "SWOR":
+                    vals.append(0)
+            else:
+                vals.append(f_block(X_rem[:k], Z_rem[:(tau - k)]))
+            X_rem = X_rem[k:]
+            Z_rem = Z_rem[(tau - k):]
+        elif sampling_type == "prop-SWR":
+            vals.append(f_block(X_rem[np.random.randint(0, n_X, int(n_X / N))],
+                                Z_rem[np.random.randint(0, n_Z, int(n_Z / N))]))
+    return np.mean(vals)

@@ -1,0 +1,214 @@
+"""Device dispatch for the tuplewise hot path.
+
+Host side of the drop-in API: it turns NumPy inputs into device tensors (PyTorch-ROCm is used
+only for allocation, copies and the stream), describes shards by offset arrays, and calls the
+C ABI of libtuplewise.so (include/tuplewise.h).  All pair arithmetic happens in the HIP
+kernels; this file only does bookkeeping, NumPy dtype promotion and the final exact division.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib as L
+
+# ----------------------------------------------------------------------------- dtype rules
+_INT64_MIN = np.int64(-(2 ** 63))
+
+
+def compare_operands(X: np.ndarray, Z: np.ndarray):
+    """Operands of NumPy's `X > Z` as (x, z, dtype code) with identical ordering.
+
+    NumPy compares in np.result_type(X, Z): float kinds compare as float64 (exact for every
+    float input), signed/bool integers as int64, uint64 vs uint64 as unsigned (mapped to int64
+    keys by flipping the sign bit, an order isomorphism), uint64 vs signed as float64.
+    """
+    X = np.asarray(X)
+    Z = np.asarray(Z)
+    rt = np.result_type(X.dtype, Z.dtype)
+    if rt.kind == "f":
+        return X.astype(np.float64, copy=False), Z.astype(np.float64, copy=False), L.TW_F64
+    if rt.kind in "bi":
+        return X.astype(np.int64, copy=False), Z.astype(np.int64, copy=False), L.TW_I64
+    if rt.kind == "u":  # both unsigned
+        xk = X.astype(np.uint64, copy=False).view(np.int64) ^ _INT64_MIN
+        zk = Z.astype(np.uint64, copy=False).view(np.int64) ^ _INT64_MIN
+        return xk, zk, L.TW_I64
+    raise TypeError(f"unsupported dtypes for a pair comparison: {X.dtype}, {Z.dtype}")
+
+
+def subtract_gt_operands(X: np.ndarray, Z: np.ndarray):
+    """Operands + predicate for cs.Un's literal `(X - Z) > 0` (compute_stats.py:19, :30).
+
+    Returns (x, z, dtype code, mode) with mode in {"gt", "subgt", "ne"}:
+      float result  -> `x > z` (identical for IEEE doubles)
+      int64 result  -> wrapping int64 subtraction then `> 0`             ("subgt")
+      narrower signed ints that cannot wrap -> `x > z`
+      unsigned result -> (x - z) wraps to >= 0, so `> 0` means `x != z`  ("ne")
+      bool          -> NumPy raises TypeError for boolean subtract; so do we.
+    """
+    X = np.asarray(X)
+    Z = np.asarray(Z)
+    if X.dtype == np.bool_ and Z.dtype == np.bool_:
+        raise TypeError("numpy boolean subtract, the `-` operator, is not supported")
+    rt = np.result_type(X.dtype, Z.dtype)
+    if rt.kind == "f":
+        return X.astype(np.float64, copy=False), Z.astype(np.float64, copy=False), L.TW_F64, "gt"
+    if rt.kind == "u":
+        x, z, code = compare_operands(X, Z)
+        return x, z, code, "ne"
+    if rt.kind == "i":
+        x = X.astype(np.int64, copy=False)
+        z = Z.astype(np.int64, copy=False)
+        if rt.itemsize == 8:
+            return x, z, L.TW_I64, "subgt"
+        info = np.iinfo(rt)
+        lo = int(x.min()) - int(z.max()) if x.size and z.size else 0
+        hi = int(x.max()) - int(z.min()) if x.size and z.size else 0
+        if info.min <= lo and hi <= info.max:
+            return x, z, L.TW_I64, "gt"
+        raise NotImplementedError(
+            f"(X - Z) > 0 wraps in {rt}; only int64 wrap-around is reproduced on the device")
+    raise TypeError(f"unsupported dtypes for X - Z: {X.dtype}, {Z.dtype}")
+
+
+# ----------------------------------------------------------------------------- shard layout
+class Shards:
+    """Concatenated shard data on the device + host-side offsets.
+
+    x_off/z_off are int64 host arrays of length n_shards+1; shard s owns x[x_off[s]:x_off[s+1]].
+    """
+
+    def __init__(self, x_dev, x_off: np.ndarray, z_dev, z_off: np.ndarray, dtype_code: int):
+        self.x = x_dev
+        self.z = z_dev
+        self.x_off = np.asarray(x_off, dtype=np.int64)
+        self.z_off = np.asarray(z_off, dtype=np.int64)
+        self.dtype = dtype_code
+        self.n_shards = len(self.x_off) - 1
+        self._x_off_dev = None
+        self._z_off_dev = None
+
+    @property
+    def nx(self) -> np.ndarray:
+        return np.diff(self.x_off)
+
+    @property
+    def nz(self) -> np.ndarray:
+        return np.diff(self.z_off)
+
+    def offsets_dev(self):
+        if self._x_off_dev is None:
+            self._x_off_dev = L.to_device(self.x_off)
+            self._z_off_dev = L.to_device(self.z_off)
+        return self._x_off_dev, self._z_off_dev
+
+    @classmethod
+    def from_host(cls, x: np.ndarray, x_off, z: np.ndarray, z_off, dtype_code: int):
+        return cls(L.to_device(x), x_off, L.to_device(z), z_off, dtype_code)
+
+    @classmethod
+    def from_blocks(cls, xs, zs, dtype_code: int):
+        xs = [np.asarray(a).reshape(-1) for a in xs]
+        zs = [np.asarray(a).reshape(-1) for a in zs]
+        x_off = np.concatenate([[0], np.cumsum([len(a) for a in xs])]).astype(np.int64)
+        z_off = np.concatenate([[0], np.cumsum([len(a) for a in zs])]).astype(np.int64)
+        x = np.concatenate(xs) if xs else np.zeros(0)
+        z = np.concatenate(zs) if zs else np.zeros(0)
+        return cls.from_host(x, x_off, z, z_off, dtype_code)
+
+
+def _counts_to_host(out) -> np.ndarray:
+    return out.cpu().numpy().view(np.uint64)
+
+
+def count_complete(sh: Shards, mode: str = "gt") -> np.ndarray:
+    """Per-shard exact counts (uint64) of the predicate over all pairs of each shard.
+
+    mode: "gt" (#x>z), "half" (2#x>z + #x==z), "subgt" (#(x-z)>0 with int64 wrap),
+    "ne" (#x!=z, derived on the device from the half and gt counts)."""
+    n = sh.n_shards
+    if n == 0:
+        return np.zeros(0, dtype=np.uint64)
+    xo, zo = sh.offsets_dev()
+    max_nx = int(sh.nx.max())
+    max_nz = int(sh.nz.max())
+    t = L.torch()
+
+    def run(pred):
+        out = L.empty((n,), t.int64)
+        L.call("tw_count_pairs", L.ptr(sh.x), L.ptr(xo), L.ptr(sh.z), L.ptr(zo), n, max_nx,
+               max_nz, sh.dtype, pred, L.ptr(out), L.stream_handle())
+        return out
+
+    if mode == "ne":
+        half = _counts_to_host(run(L.TW_PRED_HALF)).astype(object)
+        gt = _counts_to_host(run(L.TW_PRED_GT)).astype(object)
+        pairs = (sh.nx.astype(object) * sh.nz.astype(object))
+        return np.array(pairs - (half - 2 * gt), dtype=np.uint64)
+    pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}[mode]
+    return _counts_to_host(run(pred))
+
+
+def count_indexed(x_dev, z_dev, dtype_code: int, ix: np.ndarray, iz: np.ndarray,
+                  pair_off: np.ndarray, mode: str = "gt") -> np.ndarray:
+    """Per-shard counts over explicit (absolute) index pairs."""
+    n = len(pair_off) - 1
+    if n == 0:
+        return np.zeros(0, dtype=np.uint64)
+    t = L.torch()
+    ixd = L.to_device(np.asarray(ix, dtype=np.int64))
+    izd = L.to_device(np.asarray(iz, dtype=np.int64))
+    pod = L.to_device(np.asarray(pair_off, dtype=np.int64))
+    max_pairs = int(np.diff(pair_off).max())
+
+    def run(pred):
+        out = L.empty((n,), t.int64)
+        L.call("tw_count_pairs_idx", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd),
+               L.ptr(pod), n, max_pairs, dtype_code, pred, L.ptr(out), L.stream_handle())
+        return _counts_to_host(out)
+
+    if mode == "ne":
+        half = run(L.TW_PRED_HALF).astype(object)
+        gt = run(L.TW_PRED_GT).astype(object)
+        pairs = np.diff(pair_off).astype(object)
+        return np.array(pairs - (half - 2 * gt), dtype=np.uint64)
+    pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}[mode]
+    return run(pred)
+
+
+def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
+    """Per-shard float64 sums of kern(x_i, z_j) over all pairs."""
+    n = sh.n_shards
+    if n == 0:
+        return np.zeros(0)
+    t = L.torch()
+    xo, zo = sh.offsets_dev()
+    max_nx, max_nz = int(sh.nx.max()), int(sh.nz.max())
+    per = int(L.lib().tw_pair_sum_work_per_shard(max_nx, max_nz))
+    work = L.empty((per * n,), t.float64)
+    out = L.empty((n,), t.float64)
+    L.call("tw_pair_sum_f64", L.ptr(sh.x), L.ptr(xo), L.ptr(sh.z), L.ptr(zo), n, max_nx, max_nz,
+           kern, float(margin), L.ptr(work), L.ptr(out), L.stream_handle())
+    return out.cpu().numpy()
+
+
+def pair_sum_indexed(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 0.0):
+    n = len(pair_off) - 1
+    if n == 0:
+        return np.zeros(0)
+    t = L.torch()
+    ixd = L.to_device(np.asarray(ix, dtype=np.int64))
+    izd = L.to_device(np.asarray(iz, dtype=np.int64))
+    pod = L.to_device(np.asarray(pair_off, dtype=np.int64))
+    max_pairs = int(np.diff(pair_off).max())
+    per = int(L.lib().tw_pair_sum_idx_work_per_shard(max_pairs))
+    work = L.empty((per * n,), t.float64)
+    out = L.empty((n,), t.float64)
+    L.call("tw_pair_sum_idx_f64", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd), L.ptr(pod),
+           n, max_pairs, kern, float(margin), L.ptr(work), L.ptr(out), L.stream_handle())
+    return out.cpu().numpy()
+
+
+def ratio(count, pairs) -> np.float64:
+    """NumPy's mean of a 0/1 array: float64(sum) / float64(count), bit for bit."""
+    return np.float64(np.float64(int(count)) / np.float64(int(pairs)))

@@ -1,0 +1,96 @@
+"""Pairwise hinge gradient on shards — host side.
+
+grad_inc_block(w, B, margin) (learning-experiment/compute_stats.py:146-162) returns a closure;
+UN_split (compute_stats.py:44-46) calls it once per shard and averages with np.mean(axis=0).
+The closure returned here draws the same randint pairs in the same order and evaluates the
+gradient with tw_hinge_grad; UN_split recognises it and evaluates all shards in one launch.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _blocks as Bk
+from . import _lib as L
+
+
+class ShardList(list):
+    """list of shard row-copies (what the reference's SWR_divide returns) that also remembers
+    the source matrix and the drawn row indices, so device code can gather rows on the GPU."""
+
+    def __init__(self, items, source=None, rows=None):
+        super().__init__(items)
+        self.source = source
+        self.rows = rows
+
+
+def _as_matrix(A) -> np.ndarray:
+    A = np.asarray(A, dtype=np.float64)
+    return A.reshape(-1, 1) if A.ndim == 1 else A
+
+
+def hinge_grads_device(Xd, Zd, d, rows_x, kx, rows_z, kz, ixd, izd, n_shards, B, wd, margin):
+    """Per-shard gradients (n_shards, d) on the device via tw_hinge_grad."""
+    t = L.torch()
+    out = L.empty((n_shards, d), t.float64)
+    L.call("tw_hinge_grad", L.ptr(Xd), L.ptr(Zd), int(d), L.ptr(rows_x), int(kx), L.ptr(rows_z),
+           int(kz), L.ptr(ixd), L.ptr(izd), int(n_shards), int(B), L.ptr(wd), float(margin),
+           L.ptr(out), L.stream_handle())
+    return out
+
+
+class GradSpec(Bk.BlockSpec):
+    def __init__(self, w, B, margin):
+        self.w = np.asarray(w, dtype=np.float64)
+        self.B = int(B)
+        self.margin = margin
+
+    def draw(self, nx, nz):
+        ix = np.random.randint(0, nx, self.B)
+        iz = np.random.randint(0, nz, self.B)
+        return ix, iz
+
+    def _grads(self, X_s, Z_s):
+        draws = [self.draw(np.asarray(x).shape[0], np.asarray(z).shape[0])
+                 for x, z in zip(X_s, Z_s)]
+        N = len(draws)
+        if N == 0:
+            return []
+        t = L.torch()
+        ix = np.stack([dr[0] for dr in draws]).astype(np.int64)
+        iz = np.stack([dr[1] for dr in draws]).astype(np.int64)
+        d = _as_matrix(X_s[0]).shape[1]
+
+        def side(S, draws_idx):
+            rows = getattr(S, "rows", None)
+            src = getattr(S, "source", None)
+            if rows is not None and src is not None and len({len(r) for r in rows}) == 1:
+                return (L.to_device(_as_matrix(src)), L.to_device(np.stack(rows).astype(np.int64)),
+                        len(rows[0]), draws_idx)
+            mats = [_as_matrix(a) for a in S]
+            off = np.concatenate([[0], np.cumsum([m.shape[0] for m in mats])])[:-1]
+            absolute = draws_idx + off[:, None]  # rows of the concatenated shards
+            return L.to_device(np.concatenate(mats)), None, 0, absolute
+
+        Xd, rx, kx, ixa = side(X_s, ix)
+        Zd, rz, kz, iza = side(Z_s, iz)
+        wd = L.to_device(self.w.reshape(-1))
+        out = hinge_grads_device(Xd, Zd, d, rx, kx, rz, kz, L.to_device(ixa), L.to_device(iza),
+                                 N, self.B, wd, self.margin)
+        return [g.reshape(-1, 1) for g in out.cpu().numpy()]
+
+    def evaluate_split(self, X_s, Z_s):
+        return np.mean(self._grads(X_s, Z_s), axis=0)
+
+
+def grad_block(w, B, margin):
+    spec = GradSpec(w, B, margin)
+
+    def res(X, Z):
+        """
+            Returns:
+            1/B sum_{i,j in D_B} I{w^T(Z_j - X_i + margin > 0)}(Z_j - X_i)
+        """
+        return spec._grads([X], [Z])[0]
+
+    res._tw_block = spec
+    return res

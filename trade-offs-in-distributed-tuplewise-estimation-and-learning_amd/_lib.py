@@ -1,0 +1,126 @@
+"""ctypes binding of libtuplewise.so (the C ABI declared in include/tuplewise.h).
+
+This module is the only place the package touches the native library.  It fails loudly:
+there is no CPU fallback for any hot-path computation — a missing library or a machine
+without a HIP device raises instead of silently computing elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+
+import numpy as np
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libtuplewise.so"
+
+TW_OK, TW_ERR_ARG, TW_ERR_HIP = 0, 1, 2
+TW_F64, TW_I64 = 0, 1
+TW_PRED_GT, TW_PRED_HALF, TW_PRED_SUBGT = 0, 1, 2
+TW_KERN_PROD, TW_KERN_GINI, TW_KERN_HINGE = 0, 1, 2
+
+_vp, _i64, _i32, _u64, _f64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                               ctypes.c_uint64, ctypes.c_double)
+
+# name -> argtypes (all return int status unless listed in _RESTYPES)
+_SIGNATURES = {
+    "tw_last_error": [],
+    "tw_version": [],
+    "tw_device_count": [_vp],
+    "tw_count_pairs": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp],
+    "tw_count_pairs_idx": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _vp],
+    "tw_count_pairs_rng": [_vp, _vp, _vp, _vp, _i32, _i64, _u64, _u64, _i32, _i32, _vp, _vp],
+    "tw_pair_sum_work_per_shard": [_i64, _i64],
+    "tw_pair_sum_f64": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _f64, _vp, _vp, _vp],
+    "tw_pair_sum_idx_work_per_shard": [_i64],
+    "tw_pair_sum_idx_f64": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _f64, _vp, _vp, _vp],
+    "tw_hinge_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64,
+                      _vp, _vp],
+    "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp],
+    "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
+    "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],
+    "tw_perm_index": [_vp, _i64, _i64, _i64, _u64, _vp],
+    "tw_rank_histogram": [_vp, _i64, _i64, _i32, _vp, _vp],
+    "tw_bucket_scatter": [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
+    "tw_scatter_records": [_vp, _i64, _vp, _vp],
+}
+_RESTYPES = {
+    "tw_last_error": ctypes.c_char_p,
+    "tw_pair_sum_work_per_shard": ctypes.c_int64,
+    "tw_pair_sum_idx_work_per_shard": ctypes.c_int64,
+}
+
+_lib = None
+
+
+class TuplewiseError(RuntimeError):
+    """A HIP runtime failure inside libtuplewise.so."""
+
+
+def lib() -> ctypes.CDLL:
+    """Load libtuplewise.so once (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g;"
+                " g.build()'` (hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+        handle = ctypes.CDLL(str(LIB_PATH))
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = handle
+    return _lib
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGNATURES)
+
+
+def check(rc: int) -> None:
+    """Map a C-ABI status to the exception family the reference would raise."""
+    if rc == TW_OK:
+        return
+    msg = lib().tw_last_error().decode(errors="replace")
+    if rc == TW_ERR_ARG:
+        raise ValueError(msg)
+    raise TuplewiseError(msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args))
+
+
+# ----------------------------------------------------------------------------- device memory
+def torch():
+    import torch as _torch  # imported lazily: the C ABI itself has no torch dependency
+    return _torch
+
+
+def device():
+    """The HIP device all package work runs on (current torch device)."""
+    t = torch()
+    if not t.cuda.is_available():
+        raise TuplewiseError(
+            "tuplewise: no HIP device is visible; the MI355X path has no CPU fallback")
+    return t.device("cuda", t.cuda.current_device())
+
+
+def stream_handle():
+    return ctypes.c_void_p(torch().cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def to_device(arr: np.ndarray, dtype=None):
+    """Host ndarray -> contiguous device tensor (copy)."""
+    t = torch()
+    a = np.ascontiguousarray(arr if dtype is None else arr.astype(dtype, copy=False))
+    return t.from_numpy(a).to(device())
+
+
+def empty(shape, dtype):
+    return torch().empty(shape, dtype=dtype, device=device())

@@ -1,0 +1,341 @@
+// count.hip — exact two-sample pair counting on gfx950.
+//
+// Reference semantics
+//   est.Un      estimation-experiment/main.py:29-31   mean(X[:,None] > Z[None,:])
+//   cs.Un AUC   learning-experiment/compute_stats.py:19   mean((X_col - Z_row > 0).astype(int))
+//   cs.UB_indices / UB_pairs / UB   compute_stats.py:22-42 (AUC branch at :30)
+// Every block value of those functions is count / #pairs, count an exact integer; the kernels
+// below produce that integer (uint64 per shard) and the host divides exactly as NumPy does.
+//
+// Complete kernel (k_count_complete) — VALU-bound, one launch for all shards:
+//   * a 256-thread block owns a tile of 256*R x-values of one shard (R per lane, in VGPRs)
+//     and a chunk of that shard's z-values;
+//   * z is wave-uniform: it streams through the SCALAR cache (s_load_dwordx16 = 8 doubles)
+//     straight into SGPR operands of v_cmp_*_f64 — no LDS staging and no VGPR traffic for z;
+//   * per pair: one v_cmp (VCC) + one carry-add into a per-(lane, r) u32 counter
+//     (the compiler folds two compares into v_cndmask + v_addc); u32 cannot overflow because a
+//     counter sees at most 2 * z_chunk increments;
+//   * epilogue: valid counters -> u64 -> wave butterfly (DPP) -> LDS -> one u64 atomic per block.
+//   Measured on MI355X (tools/mb_issue*.hip): v_cmp_*_f64 and v_addc issue at ~0.94
+//   wave-instructions/cycle/CU, so 2 such instructions per pair cap this kernel at ~1.9e13
+//   pairs/s; see DESIGN.md "count kernel roofline".
+#include "tw_common.h"
+#include <algorithm>
+#include <type_traits>
+
+namespace tw {
+
+template <typename T, int PRED>
+__device__ __forceinline__ unsigned pair_pred(T x, T z) {
+  if constexpr (PRED == TW_PRED_GT) {
+    return x > z;
+  } else if constexpr (PRED == TW_PRED_HALF) {
+    return (unsigned)(x > z) + (unsigned)(x >= z);
+  } else {  // TW_PRED_SUBGT: literal (x - z) > 0 of cs.Un; int64 wraps like NumPy
+    if constexpr (std::is_integral<T>::value) {
+      return (long long)((unsigned long long)x - (unsigned long long)z) > 0;
+    } else {
+      return x > z;  // identical to (x - z) > 0 for IEEE doubles (no FTZ on f64)
+    }
+  }
+}
+
+template <typename T, int R, int PRED>
+__global__ __launch_bounds__(kBlock) void k_count_complete(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, int tiles_x, int zchunks, int64_t z_chunk,
+    unsigned long long* __restrict__ out) {
+  const int per_shard = tiles_x * zchunks;
+  const int s = blockIdx.x / per_shard;
+  const int rem = blockIdx.x - s * per_shard;
+  const int cz = rem / tiles_x;
+  const int tx = rem - cz * tiles_x;
+
+  const int64_t xb = x_off[s], xe = x_off[s + 1];
+  const int64_t zb = z_off[s], ze = z_off[s + 1];
+  const int64_t x0 = xb + (int64_t)tx * (kBlock * R);
+  const int64_t z0 = zb + (int64_t)cz * z_chunk;
+  if (x0 >= xe || z0 >= ze) return;  // block-uniform: ragged shard smaller than the grid
+  const int64_t z1 = (z0 + z_chunk < ze) ? z0 + z_chunk : ze;
+
+  T xv[R];
+  unsigned acc[R];
+  bool valid[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = x0 + r * kBlock + threadIdx.x;
+    valid[r] = i < xe;
+    xv[r] = valid[r] ? x[i] : (T)0;
+    acc[r] = 0;
+  }
+
+  const T* __restrict__ zp = z + z0;
+  const int nz = (int)(z1 - z0);
+#pragma unroll 8
+  for (int j = 0; j < nz; ++j) {
+    const T zv = zp[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += pair_pred<T, PRED>(xv[r], zv);
+  }
+
+  unsigned long long tot = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) tot += valid[r] ? (unsigned long long)acc[r] : 0ull;
+  tot = wave_sum_u64(tot);
+  __shared__ unsigned long long part[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / kWave; ++w) b += part[w];
+    if (b) atomicAdd(out + s, b);
+  }
+}
+
+// Incomplete count on explicit index pairs (replay of NumPy's randint draws).
+template <typename T, int PRED, int PPT>
+__global__ __launch_bounds__(kBlock) void k_count_idx(const T* __restrict__ x,
+                                                      const T* __restrict__ z,
+                                                      const int64_t* __restrict__ ix,
+                                                      const int64_t* __restrict__ iz,
+                                                      const int64_t* __restrict__ pair_off,
+                                                      int blocks_per_shard,
+                                                      unsigned long long* __restrict__ out) {
+  const int s = blockIdx.x / blocks_per_shard;
+  const int bi = blockIdx.x - s * blocks_per_shard;
+  const int64_t pb = pair_off[s], pe = pair_off[s + 1];
+  const int64_t p0 = pb + (int64_t)bi * (kBlock * PPT);
+  if (p0 >= pe) return;
+  unsigned acc = 0;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int64_t p = p0 + k * kBlock + threadIdx.x;
+    if (p < pe) acc += pair_pred<T, PRED>(x[ix[p]], z[iz[p]]);
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = part[0] + part[1] + part[2] + part[3];
+    if (b) atomicAdd(out + s, b);
+  }
+}
+
+// ---------------------------------------------------------------- Philox4x32-10 (Salmon et al.)
+struct u32x4 {
+  uint32_t a, b, c, d;
+};
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(M0, ctr.a), lo0 = M0 * ctr.a;
+    const uint32_t hi1 = __umulhi(M1, ctr.c), lo1 = M1 * ctr.c;
+    ctr = u32x4{hi1 ^ ctr.b ^ k0, lo1, hi0 ^ ctr.d ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return ctr;
+}
+__device__ __forceinline__ uint64_t mulhi_u64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
+
+// Incomplete count with pairs drawn on the device (with replacement, like UB's randint).
+template <typename T, int PRED, int PPT>
+__global__ __launch_bounds__(kBlock) void k_count_rng(const T* __restrict__ x,
+                                                      const int64_t* __restrict__ x_off,
+                                                      const T* __restrict__ z,
+                                                      const int64_t* __restrict__ z_off,
+                                                      int64_t B, int blocks_per_shard,
+                                                      uint32_t k0, uint32_t k1, uint32_t sid,
+                                                      unsigned long long* __restrict__ out) {
+  const int s = blockIdx.x / blocks_per_shard;
+  const int bi = blockIdx.x - s * blocks_per_shard;
+  const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
+  const int64_t zb = z_off[s], nz = z_off[s + 1] - zb;
+  const int64_t p0 = (int64_t)bi * (kBlock * PPT);
+  if (p0 >= B || nx <= 0 || nz <= 0) return;
+  unsigned acc = 0;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int64_t p = p0 + k * kBlock + threadIdx.x;
+    if (p < B) {
+      const u32x4 r = philox4x32_10(u32x4{(uint32_t)p, (uint32_t)(p >> 32), (uint32_t)s + sid, 0u}, k0, k1);
+      const uint64_t i = mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)nx);
+      const uint64_t j = mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)nz);
+      acc += pair_pred<T, PRED>(x[xb + i], z[zb + j]);
+    }
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = part[0] + part[1] + part[2] + part[3];
+    if (b) atomicAdd(out + s, b);
+  }
+}
+
+// ---------------------------------------------------------------- launch plans
+struct CompletePlan {
+  int R, tiles_x, zchunks;
+  int64_t z_chunk;
+  int64_t blocks;
+};
+
+// R in {1,2,4,8}: least padded x-slots per shard, larger R on ties (fewer z loads per
+// compare); then split z into chunks until the grid has >= 16 blocks per CU.
+inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shards) {
+  CompletePlan p{8, 1, 1, max_nz, 0};
+  int64_t best = -1;
+  for (int R : {8, 4, 2, 1}) {
+    const int64_t slots = ceil_div(max_nx, (int64_t)kBlock * R) * kBlock * R;
+    if (best < 0 || slots < best) {
+      best = slots;
+      p.R = R;
+    }
+  }
+  p.tiles_x = (int)ceil_div(max_nx, (int64_t)kBlock * p.R);
+  const int64_t target = 256 * 16;
+  const int64_t base = (int64_t)p.tiles_x * n_shards;
+  int64_t zc = base >= target ? 1 : ceil_div(target, base);
+  const int64_t min_chunk = 1024;
+  zc = std::min<int64_t>(zc, std::max<int64_t>(1, max_nz / min_chunk));
+  p.z_chunk = ceil_div(max_nz, zc);
+  p.z_chunk = ceil_div(p.z_chunk, 8) * 8;
+  p.zchunks = (int)ceil_div(max_nz, p.z_chunk);
+  p.blocks = (int64_t)p.tiles_x * p.zchunks * n_shards;
+  return p;
+}
+
+template <typename T, int PRED>
+int launch_complete(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                    int32_t n_shards, int64_t max_nx, int64_t max_nz, uint64_t* out,
+                    hipStream_t st) {
+  const CompletePlan p = plan_complete(max_nx, max_nz, n_shards);
+  TW_ARG_CHECK(p.blocks < (1ll << 31), "tw_count_pairs: grid too large (%lld blocks)",
+               (long long)p.blocks);
+  TW_ARG_CHECK(p.z_chunk < (1ll << 30), "tw_count_pairs: z chunk too large");
+  const T* xs = (const T*)x;
+  const T* zs = (const T*)z;
+  auto* o = (unsigned long long*)out;
+  dim3 g((unsigned)p.blocks), b(kBlock);
+  switch (p.R) {
+    case 8: hipLaunchKernelGGL((k_count_complete<T, 8, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
+    case 4: hipLaunchKernelGGL((k_count_complete<T, 4, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
+    case 2: hipLaunchKernelGGL((k_count_complete<T, 2, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
+    default: hipLaunchKernelGGL((k_count_complete<T, 1, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
+  }
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+template <typename T>
+int dispatch_complete(int32_t pred, const void* x, const int64_t* x_off, const void* z,
+                      const int64_t* z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
+                      uint64_t* out, hipStream_t st) {
+  switch (pred) {
+    case TW_PRED_GT: return launch_complete<T, TW_PRED_GT>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, st);
+    case TW_PRED_HALF: return launch_complete<T, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, st);
+    case TW_PRED_SUBGT: return launch_complete<T, TW_PRED_SUBGT>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, st);
+  }
+  set_error("tw_count_pairs: unknown predicate %d", pred);
+  return TW_ERR_ARG;
+}
+
+constexpr int kPPT = 8;  // pairs per thread in the incomplete kernels
+
+template <typename T, int PRED>
+int launch_idx(const void* x, const void* z, const int64_t* ix, const int64_t* iz,
+               const int64_t* pair_off, int32_t n_shards, int64_t max_pairs, uint64_t* out,
+               hipStream_t st) {
+  const int64_t bps = std::max<int64_t>(1, ceil_div(max_pairs, (int64_t)kBlock * kPPT));
+  TW_ARG_CHECK(bps * n_shards < (1ll << 31), "tw_count_pairs_idx: grid too large");
+  hipLaunchKernelGGL((k_count_idx<T, PRED, kPPT>), dim3((unsigned)(bps * n_shards)), dim3(kBlock), 0, st,
+                     (const T*)x, (const T*)z, ix, iz, pair_off, (int)bps, (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+template <typename T, int PRED>
+int launch_rng(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+               int32_t n_shards, int64_t B, uint64_t seed, uint64_t sid, uint64_t* out,
+               hipStream_t st) {
+  const int64_t bps = std::max<int64_t>(1, ceil_div(B, (int64_t)kBlock * kPPT));
+  TW_ARG_CHECK(bps * n_shards < (1ll << 31), "tw_count_pairs_rng: grid too large");
+  hipLaunchKernelGGL((k_count_rng<T, PRED, kPPT>), dim3((unsigned)(bps * n_shards)), dim3(kBlock), 0, st,
+                     (const T*)x, x_off, (const T*)z, z_off, B, (int)bps, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), (uint32_t)sid, (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+}  // namespace tw
+
+using namespace tw;
+
+extern "C" int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                              const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                              int64_t max_nz, int32_t dtype, int32_t pred, uint64_t* d_out,
+                              void* stream) {
+  TW_ARG_CHECK(n_shards >= 0, "tw_count_pairs: n_shards < 0");
+  TW_ARG_CHECK(max_nx >= 0 && max_nz >= 0, "tw_count_pairs: negative shard size");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_shards == 0) return TW_OK;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  if (max_nx == 0 || max_nz == 0) return TW_OK;
+  if (dtype == TW_F64) return dispatch_complete<double>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, st);
+  if (dtype == TW_I64) return dispatch_complete<long long>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, st);
+  set_error("tw_count_pairs: unknown dtype %d", dtype);
+  return TW_ERR_ARG;
+}
+
+extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
+                                  const int64_t* d_iz, const int64_t* d_pair_off,
+                                  int32_t n_shards, int64_t max_pairs, int32_t dtype,
+                                  int32_t pred, uint64_t* d_out, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && max_pairs >= 0, "tw_count_pairs_idx: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_shards == 0) return TW_OK;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  if (max_pairs == 0) return TW_OK;
+#define TW_IDX(T, P) return launch_idx<T, P>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, d_out, st)
+  if (dtype == TW_F64) {
+    if (pred == TW_PRED_GT || pred == TW_PRED_SUBGT) TW_IDX(double, TW_PRED_GT);
+    if (pred == TW_PRED_HALF) TW_IDX(double, TW_PRED_HALF);
+  } else if (dtype == TW_I64) {
+    if (pred == TW_PRED_GT) TW_IDX(long long, TW_PRED_GT);
+    if (pred == TW_PRED_HALF) TW_IDX(long long, TW_PRED_HALF);
+    if (pred == TW_PRED_SUBGT) TW_IDX(long long, TW_PRED_SUBGT);
+  }
+#undef TW_IDX
+  set_error("tw_count_pairs_idx: unknown dtype %d / predicate %d", dtype, pred);
+  return TW_ERR_ARG;
+}
+
+extern "C" int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                  const int64_t* d_z_off, int32_t n_shards, int64_t B,
+                                  uint64_t seed, uint64_t stream_id, int32_t dtype, int32_t pred,
+                                  uint64_t* d_out, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && B >= 0, "tw_count_pairs_rng: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_shards == 0) return TW_OK;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  if (B == 0) return TW_OK;
+#define TW_RNG(T, P) return launch_rng<T, P>(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, d_out, st)
+  if (dtype == TW_F64) {
+    if (pred == TW_PRED_GT || pred == TW_PRED_SUBGT) TW_RNG(double, TW_PRED_GT);
+    if (pred == TW_PRED_HALF) TW_RNG(double, TW_PRED_HALF);
+  } else if (dtype == TW_I64) {
+    if (pred == TW_PRED_GT) TW_RNG(long long, TW_PRED_GT);
+    if (pred == TW_PRED_HALF) TW_RNG(long long, TW_PRED_HALF);
+    if (pred == TW_PRED_SUBGT) TW_RNG(long long, TW_PRED_SUBGT);
+  }
+#undef TW_RNG
+  set_error("tw_count_pairs_rng: unknown dtype %d / predicate %d", dtype, pred);
+  return TW_ERR_ARG;
+}

@@ -1,0 +1,164 @@
+// hinge.hip — pairwise hinge SGD on shards (f1 GEMV).
+//
+//   grad_inc_block(w, B, margin)   learning-experiment/compute_stats.py:146-162
+//       X_sel = X[randint(0,n_X,B)]; Z_sel = Z[randint(0,n_Z,B)]; diff = Z_sel - X_sel
+//       S = diff.dot(w) + margin; filt = S > 0; return diff[filt].sum(axis=0) / B
+//   UN_split(X_s, Z_s, f)          compute_stats.py:44-46  np.mean([...], axis=0)
+//   learning_process update        learning-experiment/make_exps.py:130-141
+//
+// Numerics (compiled with -ffp-contract=off, like NumPy which never fuses multiply-add):
+//   * diff and the column sums are bit-identical to NumPy: the filtered rows are added in
+//     row order starting from +0.0, as NumPy's axis-0 add.reduce does (so an empty filter
+//     gives +0.0 and a column of -0.0 sums to +0.0, exactly like the reference).
+//   * S uses lane-strided partial dots + a fixed butterfly; NumPy uses BLAS dgemv, whose
+//     summation order is library-specific.  Only the SIGN of S matters, so the gradient
+//     differs from NumPy's only when |S| is within a few ulps of 0 (tolerance 1e-5 rel).
+//
+// Layout: one block per shard; the block streams its B pairs in chunks of CH pairs whose diff
+// rows are staged in LDS (CH*d doubles <= 64 KiB), so every X/Z row is read from HBM once.
+#include "tw_common.h"
+#include <algorithm>
+
+namespace tw {
+
+constexpr int kLdsDoubles = 8192;  // 64 KiB of diff rows per block
+constexpr int kMaxColsPerThread = 16;  // d <= 4096
+
+__global__ __launch_bounds__(kBlock) void k_hinge_grad(
+    const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
+    const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
+    int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
+    int CH, const double* __restrict__ w, double margin, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* diff = (double*)smem;                             // CH * d
+  int64_t* rx = (int64_t*)(smem + sizeof(double) * CH * d);  // CH
+  int64_t* rz = rx + CH;                                     // CH
+  int* flag = (int*)(rz + CH);                               // CH
+
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  double acc[kMaxColsPerThread];
+#pragma unroll
+  for (int q = 0; q < kMaxColsPerThread; ++q) acc[q] = 0.0;
+
+  for (int64_t b0 = 0; b0 < B; b0 += CH) {
+    const int nb = (int)std::min<int64_t>(CH, B - b0);
+    // rows of this chunk: compose the SWR shard draw with the per-step pair draw
+    for (int t = threadIdx.x; t < nb; t += kBlock) {
+      const int64_t p = (int64_t)s * B + b0 + t;
+      const int64_t ax = ix[p], az = iz[p];
+      rx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+      rz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+    }
+    __syncthreads();
+    // stage diff = Z[rz] - X[rx] (row-contiguous, coalesced)
+    const int64_t tot = (int64_t)nb * d;
+    for (int64_t e = threadIdx.x; e < tot; e += kBlock) {
+      const int t = (int)(e / d);
+      const int64_t j = e - (int64_t)t * d;
+      diff[e] = Z[rz[t] * d + j] - X[rx[t] * d + j];
+    }
+    __syncthreads();
+    // S_t = diff_t . w + margin ; one wave per pair, lanes over features
+    for (int t = wid; t < nb; t += kBlock / kWave) {
+      double part = 0.0;
+      for (int64_t j = lane; j < d; j += kWave) part += diff[(int64_t)t * d + j] * w[j];
+      part = wave_sum_f64(part);
+      if (lane == 0) {
+        flag[t] = (part + margin) > 0.0;
+      }
+    }
+    __syncthreads();
+    // column sums over the filtered rows, in row order
+#pragma unroll
+    for (int q = 0; q < kMaxColsPerThread; ++q) {
+      const int64_t j = threadIdx.x + (int64_t)q * kBlock;
+      if (j < d) {
+        double a = acc[q];
+        for (int t = 0; t < nb; ++t)
+          if (flag[t]) a += diff[(int64_t)t * d + j];
+        acc[q] = a;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < kMaxColsPerThread; ++q) {
+    const int64_t j = threadIdx.x + (int64_t)q * kBlock;
+    if (j < d) out[(int64_t)s * d + j] = acc[q] / (double)B;
+  }
+}
+
+// g = (sum_s grads[s]) / N + reg*w ; dw = momentum*dw + lr*g (SGD: dw = lr*g) ; w = w - dw
+__global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
+                                                       double* __restrict__ dw,
+                                                       const double* __restrict__ grads,
+                                                       int n_shards, int64_t d, double reg,
+                                                       double lr, double momentum) {
+  for (int64_t j = blockIdx.x * (int64_t)kBlock + threadIdx.x; j < d;
+       j += (int64_t)gridDim.x * kBlock) {
+    double sum = 0.0;  // np.mean(axis=0): 0.0 + g_0 + g_1 + ... in shard order, then / N
+    for (int s = 0; s < n_shards; ++s) sum += grads[(int64_t)s * d + j];
+    const double wj = w[j];
+    const double g = sum / (double)n_shards + reg * wj;
+    const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
+    dw[j] = step;
+    w[j] = wj - step;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gemv(const double* __restrict__ A, int64_t n,
+                                                 int64_t d, const double* __restrict__ w,
+                                                 double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const double* row = A + i * d;
+    double a = 0.0;
+    for (int64_t j = 0; j < d; ++j) a += row[j] * w[j];
+    out[i] = a;
+  }
+}
+
+}  // namespace tw
+
+using namespace tw;
+
+extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
+                             const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                             int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                             int32_t n_shards, int64_t B, const double* d_w, double margin,
+                             double* d_out, void* stream) {
+  TW_ARG_CHECK(d >= 1 && d <= (int64_t)kBlock * kMaxColsPerThread,
+               "tw_hinge_grad: d=%lld outside [1, %d]", (long long)d, kBlock * kMaxColsPerThread);
+  TW_ARG_CHECK(n_shards >= 0 && B >= 1, "tw_hinge_grad: bad n_shards/B");
+  if (n_shards == 0) return TW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
+  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
+  hipLaunchKernelGGL(k_hinge_grad, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x,
+                     kx, d_rows_z, kz, d_ix, d_iz, B, CH, d_w, margin, d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, int32_t n_shards,
+                             int64_t d, double reg, double lr, double momentum, void* stream) {
+  TW_ARG_CHECK(n_shards >= 1 && d >= 1, "tw_sgd_update: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (int)std::min<int64_t>(1024, ceil_div(d, kBlock));
+  hipLaunchKernelGGL(k_sgd_update, dim3(blocks), dim3(kBlock), 0, st, d_w, d_dw, d_grads,
+                     n_shards, d, reg, lr, momentum);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w,
+                           double* d_out, void* stream) {
+  TW_ARG_CHECK(n >= 0 && d >= 1, "tw_gemv_f64: bad sizes");
+  if (n == 0) return TW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (int)std::min<int64_t>(4096, ceil_div(n, kBlock));
+  hipLaunchKernelGGL(k_gemv, dim3(blocks), dim3(kBlock), 0, st, d_A, n, d, d_w, d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}

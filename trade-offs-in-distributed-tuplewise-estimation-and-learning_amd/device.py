@@ -1,0 +1,207 @@
+"""Device-resident sharded estimation.
+
+The drop-in functions (tuplewise.estimation / tuplewise.compute_stats) keep the reference's
+host-side NumPy shuffle so their results are bit-identical to it.  This module is the
+production path behind them for data that lives on the GPU(s): the samples stay in HBM, each
+repartition is a keyed pseudo-random bijection evaluated on the device (Feistel, csrc/
+permute.hip), and all shards are counted in one launch.
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): rank r holds n_loc X-scores
+and m_loc Z-scores and owns shards [r*N, (r+1)*N) of the global prop-SWOR layout.  A
+repartition draws ONE global permutation of the G*n_loc X-scores (and of the Z-scores);
+every element is sent to the rank owning its new position with a single all-to-all(v) of
+{value, position} records, and the receiver scatters them into place.  The resulting global
+array — hence every shard's integer count and the final np.mean — is identical for any G.
+Per-shard counts are combined with one all-reduce (sum of a zero-padded int64 vector; exact).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _engine as E
+from . import _lib as L
+
+
+def prop_swor_layout(n_X: int, n_Z: int, N: int):
+    """Block bounds of UN(..., sampling_type="prop-SWOR") on already-shuffled arrays
+    (compute_stats.py:70-87 / estimation-experiment/main.py:45-64): k = int(n_X/N) X-scores
+    and tau-k Z-scores per block, consumed from the front, clamped at the array ends.
+    Returns (x_off, z_off, keep) where keep[s] is False for degenerate blocks (k in (0, tau)),
+    which the est variant skips."""
+    tau = int((n_X + n_Z) / N)
+    k = int(n_X / N)
+    x_off = [0]
+    z_off = [0]
+    keep = []
+    for _ in range(N):
+        x_off.append(min(x_off[-1] + k, n_X))
+        z_off.append(min(z_off[-1] + (tau - k), n_Z))
+        keep.append(k not in (0, tau))
+    return np.array(x_off, np.int64), np.array(z_off, np.int64), np.array(keep, bool)
+
+
+class HipOps:
+    """The device operations of a repartition step, bound to libtuplewise.so."""
+
+    def __init__(self):
+        self.t = L.torch()
+
+    def perm_index(self, n, base, n_total, key):
+        out = L.empty((n,), self.t.int64)
+        L.call("tw_perm_index", L.ptr(out), int(n), int(base), int(n_total), int(key),
+               L.stream_handle())
+        return out
+
+    def permute(self, vals, key):
+        out = self.t.empty_like(vals)
+        L.call("tw_permute_scatter", L.ptr(vals), L.ptr(out), int(vals.numel()), int(key),
+               L.stream_handle())
+        return out
+
+    def rank_histogram(self, perm, n_loc, G):
+        out = L.empty((G,), self.t.int64)
+        L.call("tw_rank_histogram", L.ptr(perm), int(perm.numel()), int(n_loc), int(G),
+               L.ptr(out), L.stream_handle())
+        return out
+
+    def bucket_scatter(self, perm, vals, n_loc, G, start):
+        send = L.empty((perm.numel(), 2), self.t.int64)
+        cursor = L.empty((G,), self.t.int64)
+        L.call("tw_bucket_scatter", L.ptr(perm), L.ptr(vals), int(perm.numel()), int(n_loc),
+               int(G), L.ptr(start), L.ptr(cursor), L.ptr(send), L.stream_handle())
+        return send
+
+    def scatter_records(self, rec, out):
+        L.call("tw_scatter_records", L.ptr(rec), int(rec.shape[0]), L.ptr(out),
+               L.stream_handle())
+        return out
+
+    def count(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred):
+        out = L.empty((n_shards,), self.t.int64)
+        L.call("tw_count_pairs", L.ptr(x), L.ptr(x_off_dev), L.ptr(z), L.ptr(z_off_dev),
+               int(n_shards), int(max_nx), int(max_nz), int(dtype), int(pred), L.ptr(out),
+               L.stream_handle())
+        return out
+
+    def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred):
+        out = L.empty((n_shards,), self.t.int64)
+        L.call("tw_count_pairs_rng", L.ptr(x), L.ptr(x_off_dev), L.ptr(z), L.ptr(z_off_dev),
+               int(n_shards), int(B), int(seed), int(shard_base), int(dtype), int(pred), L.ptr(out),
+               L.stream_handle())
+        return out
+
+    def to_dev(self, arr):
+        return L.to_device(arr)
+
+
+class ShardedSample:
+    """Two-sample scores resident on this rank's GPU, cut into N local prop-SWOR shards.
+
+    X, Z: this rank's 1-D tensors (float64 or int64; all ranks the same sizes and dtype).
+    group: a torch.distributed process group (None = single process).
+    tie_mode: "strict" (reference) or "half" (ties score 1/2)."""
+
+    def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None):
+        self.ops = ops if ops is not None else HipOps()
+        t = L.torch()
+        self.t = t
+        self.group = group
+        if group is not None:
+            import torch.distributed as dist
+            self.dist = dist
+            self.G = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+        else:
+            self.dist = None
+            self.G, self.rank = 1, 0
+        if X.dtype == t.float64:
+            self.dtype = L.TW_F64
+        elif X.dtype == t.int64:
+            self.dtype = L.TW_I64
+        else:
+            raise TypeError("ShardedSample holds float64 or int64 scores")
+        if Z.dtype != X.dtype:
+            raise TypeError("X and Z must share a dtype")
+        self.X, self.Z = X.contiguous(), Z.contiguous()
+        self.N = int(N)
+        self.n_loc, self.m_loc = self.X.numel(), self.Z.numel()
+        self.pred = {"strict": L.TW_PRED_GT, "half": L.TW_PRED_HALF}[tie_mode]
+        self.tie_mode = tie_mode
+        x_off, z_off, keep = prop_swor_layout(self.n_loc, self.m_loc, self.N)
+        self.x_off, self.z_off, self.keep = x_off, z_off, keep
+        self.x_off_dev = self.ops.to_dev(x_off)
+        self.z_off_dev = self.ops.to_dev(z_off)
+        self.max_nx = int(np.diff(x_off).max()) if N else 0
+        self.max_nz = int(np.diff(z_off).max()) if N else 0
+        self.pairs = np.diff(x_off).astype(object) * np.diff(z_off).astype(object)
+
+    # ------------------------------------------------------------------ repartition
+    def _permute_global(self, A, n_loc, key):
+        """Apply the global permutation (over G*n_loc elements) to the distributed array A."""
+        if self.G == 1:
+            return self.ops.permute(A, key)
+        t, dist, G = self.t, self.dist, self.G
+        perm = self.ops.perm_index(n_loc, self.rank * n_loc, G * n_loc, key)
+        send_counts = self.ops.rank_histogram(perm, n_loc, G)
+        start = t.cumsum(send_counts, 0) - send_counts
+        send = self.ops.bucket_scatter(perm, A, n_loc, G, start)
+        recv_counts = t.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        sc = send_counts.cpu().tolist()
+        rc = recv_counts.cpu().tolist()
+        recv = t.empty((int(sum(rc)), 2), dtype=t.int64, device=A.device)
+        dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
+                               group=self.group)
+        out = t.empty_like(A)
+        return self.ops.scatter_records(recv, out)
+
+    def repartition(self, key: int):
+        """One repartition: new random shards for both samples (key = any 64-bit integer)."""
+        self.X = self._permute_global(self.X, self.n_loc, (key * 2) & (2 ** 64 - 1))
+        self.Z = self._permute_global(self.Z, self.m_loc, (key * 2 + 1) & (2 ** 64 - 1))
+
+    # ------------------------------------------------------------------ estimation
+    def local_counts(self):
+        """Per-local-shard exact counts (int64 device tensor; uint64 semantics)."""
+        return self.ops.count(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                              self.max_nx, self.max_nz, self.dtype, self.pred)
+
+    def global_counts(self, local):
+        """All G*N shard counts, in global shard order, on every rank (one all-reduce)."""
+        if self.G == 1:
+            return local
+        t = self.t
+        full = t.zeros((self.G * self.N,), dtype=t.int64, device=local.device)
+        full[self.rank * self.N:(self.rank + 1) * self.N] = local
+        self.dist.all_reduce(full, group=self.group)
+        return full
+
+    def values(self, counts) -> list:
+        c = counts.cpu().numpy().view(np.uint64)
+        keep = np.tile(self.keep, self.G)
+        pairs = np.tile(self.pairs, self.G)
+        scale = 2 if self.tie_mode == "half" else 1
+        return [E.ratio(ci, scale * pi) for ci, pi, k in zip(c, pairs, keep) if k]
+
+    def UnN(self, key=None) -> np.float64:
+        """Block-wise complete U-statistic over all G*N shards (est.UnN with prop-SWOR,
+        estimation-experiment/main.py:72-74); repartitions first when key is given."""
+        if key is not None:
+            self.repartition(key)
+        return np.mean(self.values(self.global_counts(self.local_counts())))
+
+    def UnNT(self, T: int, key0: int = 0) -> np.float64:
+        """T repartitions, averaged (est.UnNT, estimation-experiment/main.py:76-79)."""
+        return np.mean([self.UnN(key0 + t) for t in range(T)])
+
+    def UnNB(self, B: int, seed: int, key=None) -> np.float64:
+        """Block-wise incomplete U-statistic with B device-drawn pairs per shard
+        (cs.UnNB(kernel="AUC"), compute_stats.py:104-110, device-RNG mode)."""
+        if key is not None:
+            self.repartition(key)
+        local = self.ops.count_rng(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N, B,
+                                   seed, self.rank * self.N, self.dtype, self.pred)
+        c = self.global_counts(local).cpu().numpy().view(np.uint64)
+        keep = np.tile(self.keep, self.G)
+        scale = 2 if self.tie_mode == "half" else 1
+        return np.mean([E.ratio(ci, scale * B) for ci, k in zip(c, keep) if k])
