@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: pair comparisons/s of the sharded AUC U-statistic (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2] shape, one GPU's share): every rank holds n = 1e6 X-scores
+and 1e6 Z-scores (float64, synthetic N(0.5,1) / N(0,1)) resident in HBM, cut into N = 64
+prop-SWOR shards of 15625 x 15625 pairs.  One step = one block-wise complete U-statistic
+UnN (estimation-experiment/main.py:72-74): a fresh device repartition of BOTH samples (one
+global keyed permutation; at G > 1 an RCCL all-to-all moves every score to its new owner),
+the exact pair count of all shards in one launch, an RCCL all-reduce of the per-shard counts
+and the final np.mean on the host.  Weak scaling: per-GPU work is fixed (1.5625e10 pairs).
+
+value = pairs compared by all ranks / max-over-ranks wall time of the K timed steps.
+roofline: the count kernel (k_count_complete), VALU-bound: 1 compare lane-op per pair
+against the f64 vector-op peak 3.93e13 lane-op/s (256 CU x 64 lanes x 2.4 GHz; SURVEY.md
+§8(d)); its duration is measured live with HIP events on the stream it runs on.
+cpu_baseline: the CPU port of the reference (oracle/oracle.py, identical NumPy operations to
+est.UnN) timed on rank 0 at N=1 on one full UnN of the same configuration.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+N_PER_CLASS = 1_000_000
+N_SHARDS = 64
+PEAK_LANE_OPS = 256 * 64 * 2.4e9  # 3.93e13 f64 vector lane-ops/s (MI355X_MICROARCH chip table)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=N_PER_CLASS)
+    ap.add_argument("--shards", type=int, default=N_SHARDS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-shards", type=int, default=N_SHARDS,
+                    help="shards of the CPU-baseline sample (64 = one full UnN)")
+    return ap.parse_args()
+
+
+def cpu_baseline(n, N, shards):
+    """The reference's UnN restated with its own NumPy operations (oracle.est_Un per block),
+    single-threaded, on `shards` of the N prop-SWOR blocks of one shuffled sample."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import oracle as O
+    rng = np.random.RandomState(0)
+    X, Z = rng.normal(0.5, 1, n), rng.normal(0, 1, n)
+    k = n // N
+    t0 = time.perf_counter()
+    np.random.shuffle(X)
+    np.random.shuffle(Z)
+    vals = [O.est_Un(X[s * k:(s + 1) * k], Z[s * k:(s + 1) * k]) for s in range(shards)]
+    float(np.mean(vals))
+    dt = time.perf_counter() - t0
+    pairs = shards * k * k
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"est.UnN body (in-place shuffle + {shards} of {N} prop-SWOR blocks of "
+                      f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
+
+
+def pmc_traffic():
+    """HBM bytes per count-kernel launch from the committed rocprofv3 --pmc summary of this
+    exact workload (profiles/*count_pmc*.json), or None."""
+    cands = sorted(ROOT.glob("profiles/*count_pmc*.json"))
+    if not cands:
+        return None
+    try:
+        return json.loads(cands[-1].read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+    import tuplewise  # noqa: F401
+    from tuplewise.device import ShardedSample
+
+    gen = torch.Generator(device="cuda").manual_seed(1000 + rank)
+    n = args.n
+    X = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) + 0.5
+    Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+    S = ShardedSample(X, Z, args.shards, group=group)
+    k = n // args.shards
+    pairs_per_step_rank = args.shards * k * k
+
+    # live kernel timing: events on the stream the C ABI launches on (torch's current stream)
+    ops = S.ops
+    kernel_ms = []
+    orig_count = ops.count
+
+    def timed_count(*a, **kw):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = orig_count(*a, **kw)
+        e1.record()
+        kernel_ms.append((e0, e1))
+        return out
+
+    ops.count = timed_count
+
+    def barrier():
+        if group is not None:
+            dist.barrier(device_ids=[local])
+
+    for w in range(args.warmup):
+        S.UnN(key=w)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    kernel_ms.clear()
+    t0 = time.perf_counter()
+    est = None
+    for s in range(args.steps):
+        est = S.UnN(key=args.warmup + s)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if group is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+
+    total_pairs = pairs_per_step_rank * world * args.steps
+    value = total_pairs / dt
+    achieved = pairs_per_step_rank / (kms * 1e-3)  # lane-ops/s, 1 compare per pair (strict)
+    out = {
+        "metric": "pair comparisons/sec (node) for sharded AUC U-stat at n=1e6/class (UnN, "
+                  "N=64 prop-SWOR shards per GPU, device repartition each step)",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: X~N(0.5,1), Z~N(0,1) float64 scores generated on the device",
+        "config": {"workload": "UnN sharded complete AUC U-statistic (estimation-experiment/"
+                               "main.py:72-74) + device repartition per step",
+                   "n_per_class_per_gpu": n, "shards_per_gpu": args.shards,
+                   "pairs_per_step_per_gpu": pairs_per_step_rank,
+                   "parallelism": f"dp{world}: shards over ranks, RCCL all-to-all repartition "
+                                  f"+ all-reduce of counts"},
+        "roofline": {"bound": "valu", "kernel": "k_count_complete",
+                     "achieved": achieved / 1e12, "peak": PEAK_LANE_OPS / 1e12,
+                     "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
+                     "count_kernel_ms": kms, "traffic": pmc_traffic(),
+                     "note": "1 v_cmp_f64 lane-op per pair; traffic = HBM bytes/launch from "
+                             "the committed rocprofv3 --pmc summary"},
+        "estimate_last_step": float(est),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if group is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -68,6 +68,10 @@ int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const void* d_z,
                    const int64_t* d_z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
                    int32_t dtype, int32_t pred, uint64_t* d_out, void* stream);
 
+/* Tuning hook for tw_count_pairs' launch plan: R x-values per lane (1, 2, 4, 8; 0 = automatic)
+ * and z-chunk length per block (0 = automatic).  Process-global; results do not depend on it. */
+int tw_count_set_plan(int32_t R, int64_t z_chunk);
+
 /* ---- Row A3/A4/A5/A8: incomplete count on given index pairs (replay mode) -------------
  * Replaces cs.UB_indices / UB_pairs / UB (compute_stats.py:22-42): pair p of shard s
  * compares x[d_ix[p]] with z[d_iz[p]] for p in [d_pair_off[s], d_pair_off[s+1]); indices are

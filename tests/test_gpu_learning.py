@@ -1,0 +1,68 @@
+"""learning_process / evaluation_step (make_exps.py:96-190) on the device vs the reference's
+golden run: the w trajectory (captured by hooking grad_inc_block in the reference) and the
+evaluation lists that learning_process appends to p_learn.
+
+Tolerance: north_star asks for SGD trajectories within 1e-5 relative; the device
+reproduces NumPy's operation order except BLAS's dot-product order inside the filter test,
+so we hold it to 1e-10 here.  AUC values are count-derived but sit on device-computed scores
+(GEMV order differs from BLAS by an ulp): exact unless a score pair ties within an ulp."""
+import logging
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _p_learn(golden, n_it=300):
+    return {"n_it": n_it, "margin": 1, "N": 10, "B": 20, "reshuffle_mod": 5, "reg": 0.05,
+            "learning_rate": 0.01, "eval_mod": 25, "w_init": golden["learn/w0"],
+            "test_X": golden["learn/test_X"], "test_Z": golden["learn/test_Z"],
+            "train_mon_pairs": [tuple(p) for p in golden["learn/mon"]],
+            "train_X": golden["learn/X"], "train_Z": golden["learn/Z"]}
+
+
+def test_trajectory_matches_reference(gpu, golden):
+    import tuplewise.learning as lr
+    p = _p_learn(golden)
+    traj = []
+    logging.disable(logging.CRITICAL)
+    np.random.seed(2024)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=traj)
+    ref = golden["learn/ws"]
+    got = np.stack(traj)
+    assert got.shape == ref.shape
+    rel = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel < 1e-10, rel
+    for k in ("iter", "norm_w"):
+        np.testing.assert_allclose(p[k], golden[f"learn/{k}"], rtol=1e-10)
+    for k in ("bc_AUC", "tc_AUC"):
+        np.testing.assert_allclose(p[k], golden[f"learn/{k}"], rtol=1e-9)
+    for k in ("br_AUC", "tr_AUC"):
+        np.testing.assert_allclose(p[k], golden[f"learn/{k}"], rtol=0, atol=1e-12)
+
+
+def test_sgd_optimizer_and_assert(gpu, golden):
+    import tuplewise.learning as lr
+    from oracle import oracle as O
+    p = _p_learn(golden, n_it=30)
+    traj = []
+    np.random.seed(7)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, optim_type="SGD",
+                        trajectory=traj)
+    # oracle with plain SGD updates
+    np.random.seed(7)
+    w = golden["learn/w0"]
+    X, Z = golden["learn/X"], golden["learn/Z"]
+    X_s, Z_s = O.SWR_divide(X, Z, 10)
+    dw = 0
+    ws = []
+    for i in range(30):
+        if i % 5 == 0:
+            X_s, Z_s = O.SWR_divide(X, Z, 10)
+        ws.append(w.copy())
+        g = O.UN_split(X_s, Z_s, O.grad_inc_block(w, 20, 1))
+        w, dw = O.sgd_step(w, dw, g, 0.05, 0.01, optim_type="SGD")
+    np.testing.assert_allclose(np.stack(traj), np.stack(ws), rtol=1e-10, atol=1e-14)
+    with pytest.raises(AssertionError):
+        lr.learning_process(X, Z, _p_learn(golden, n_it=2), optim_type="adam")

@@ -189,10 +189,14 @@ struct CompletePlan {
 
 // R in {1,2,4,8}: least padded x-slots per shard, larger R on ties (fewer z loads per
 // compare); then split z into chunks until the grid has >= 16 blocks per CU.
+static int g_force_R = 0;            // tuning hook (tw_count_set_plan); 0 = automatic
+static int64_t g_force_zchunk = 0;
+
 inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shards) {
   CompletePlan p{8, 1, 1, max_nz, 0};
   int64_t best = -1;
   for (int R : {8, 4, 2, 1}) {
+    if (g_force_R && R != g_force_R) continue;
     const int64_t slots = ceil_div(max_nx, (int64_t)kBlock * R) * kBlock * R;
     if (best < 0 || slots < best) {
       best = slots;
@@ -200,13 +204,17 @@ inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shar
     }
   }
   p.tiles_x = (int)ceil_div(max_nx, (int64_t)kBlock * p.R);
-  const int64_t target = 256 * 16;
+  // Many short z-chunks balance the tail across 256 CUs (measured: 1024-long chunks beat
+  // 5k-15k chunks by 10-30% on 64 shards of 15625); below ~512 the per-block x loads and
+  // epilogue start to show.
+  const int64_t target = 256 * 128;
   const int64_t base = (int64_t)p.tiles_x * n_shards;
   int64_t zc = base >= target ? 1 : ceil_div(target, base);
-  const int64_t min_chunk = 1024;
+  const int64_t min_chunk = 512;
   zc = std::min<int64_t>(zc, std::max<int64_t>(1, max_nz / min_chunk));
   p.z_chunk = ceil_div(max_nz, zc);
   p.z_chunk = ceil_div(p.z_chunk, 8) * 8;
+  if (g_force_zchunk > 0) p.z_chunk = g_force_zchunk;
   p.zchunks = (int)ceil_div(max_nz, p.z_chunk);
   p.blocks = (int64_t)p.tiles_x * p.zchunks * n_shards;
   return p;
@@ -277,6 +285,14 @@ int launch_rng(const void* x, const int64_t* x_off, const void* z, const int64_t
 }  // namespace tw
 
 using namespace tw;
+
+extern "C" int tw_count_set_plan(int32_t R, int64_t z_chunk) {
+  TW_ARG_CHECK(R == 0 || R == 1 || R == 2 || R == 4 || R == 8, "tw_count_set_plan: R in {0,1,2,4,8}");
+  TW_ARG_CHECK(z_chunk >= 0 && z_chunk < (1ll << 30), "tw_count_set_plan: bad z_chunk");
+  g_force_R = R;
+  g_force_zchunk = z_chunk;
+  return TW_OK;
+}
 
 extern "C" int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const void* d_z,
                               const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,

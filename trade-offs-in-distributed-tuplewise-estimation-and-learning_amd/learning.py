@@ -1,0 +1,222 @@
+"""Drop-in replacement for the learning loop of learning-experiment/make_exps.py.
+
+learning_process(X, Z, p_learn, optim_type="momentum")  make_exps.py:96-141
+evaluation_step(i, X_s, Z_s, w, p_learn)                 make_exps.py:143-190
+
+Same logging lines, same p_learn side effects (iter, norm_w, bc_AUC, br_AUC, tr_AUC, tc_AUC
+lists), same NumPy global-RNG draws in the same order (the initial redundant SWR_divide, the
+per-reshuffle SWR_divide draws, and per shard the two randint calls of grad_inc_block).  The
+state lives on the GPU: X, Z, the shard row indices, w and the momentum buffer; each step is
+one tw_hinge_grad launch (all shards) + one tw_sgd_update launch.  w is copied to the host
+only when evaluation_step needs it.  Evaluation runs on the device too: score GEMVs, the
+fixed-pair hinge and AUC, the complete test hinge and AUC.
+
+Keyword-only extra: ``trajectory`` (a list) receives a copy of w before every gradient step,
+the value the reference passes to grad_inc_block at make_exps.py:130.
+"""
+from __future__ import annotations
+
+import logging
+
+import numpy as np
+
+from . import _engine as E
+from . import _lib as L
+from . import _learn
+from . import compute_stats as cs
+
+SEED_SHUFFLE = 42
+TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
+SEED_TRAIN_MONITOR = 54
+SIZE_TRAIN_MONITOR = 450000
+PROP_TEST = 0.2
+DEFAULT_ITE_NUMBER = 5000
+
+
+class SGDEngine:
+    """Device-resident pairwise-hinge SGD state for one learning_process run."""
+
+    def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type):
+        t = L.torch()
+        self.t = t
+        self.X = L.to_device(np.asarray(X, dtype=np.float64))
+        self.Z = L.to_device(np.asarray(Z, dtype=np.float64))
+        self.n_X, self.d = self.X.shape
+        self.n_Z = self.Z.shape[0]
+        self.N, self.B = int(N), int(B)
+        self.kx, self.kz = int(self.n_X / N), int(self.n_Z / N)
+        self.margin, self.reg, self.lr = float(margin), float(reg), float(learning_rate)
+        self.momentum = 0.9 if optim_type == "momentum" else -1.0
+        self.w_shape = np.asarray(w_init).shape
+        self.w = L.to_device(np.asarray(w_init, dtype=np.float64).reshape(-1))
+        self.dw = t.zeros_like(self.w)
+        self.grads = L.empty((self.N, self.d), t.float64)
+        self.rows_x = self.rows_z = None
+
+    def set_shards(self, rows_x, rows_z):
+        self.rows_x = L.to_device(np.stack(rows_x).astype(np.int64))
+        self.rows_z = L.to_device(np.stack(rows_z).astype(np.int64))
+
+    def step(self, ix: np.ndarray, iz: np.ndarray):
+        ixd, izd = L.to_device(ix), L.to_device(iz)
+        s = L.stream_handle()
+        L.call("tw_hinge_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x), self.kx,
+               L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N, self.B,
+               L.ptr(self.w), self.margin, L.ptr(self.grads), s)
+        L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
+               self.d, self.reg, self.lr, self.momentum, s)
+
+    def w_host(self) -> np.ndarray:
+        return self.w.cpu().numpy().reshape(self.w_shape)
+
+
+def _swr_rows(n_X, n_Z, N):
+    """The index draws of SWR_divide (compute_stats.py:48-54), same order."""
+    rows_x = [np.random.randint(0, n_X, int(n_X / N)) for _ in range(N)]
+    rows_z = [np.random.randint(0, n_Z, int(n_Z / N)) for _ in range(N)]
+    return rows_x, rows_z
+
+
+def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None):
+    """Learning process for our experiments.  (make_exps.py:96-141)"""
+    n_X, n_Z = X.shape[0], Z.shape[0]
+    N = p_learn["N"]
+    B = p_learn["B"]
+    learning_rate = p_learn["learning_rate"]
+    margin = p_learn["margin"]
+    w = p_learn["w_init"]
+
+    to_log = ["{} : {}".format(k, v) for k, v in p_learn.items()
+              if not k.startswith(("train_", "test_", "w"))]
+    i = 0
+    while i < len(to_log) / 4:
+        logging.info("%s", " / ".join(to_log[(i * 4):(i * 4 + 4)]))
+        i += 1
+    logging.info("#X: %d / #Z: %d ", n_X, n_Z)
+    logging.info("#X/N: %d / #Z/N: %d ", n_X / N, n_Z / N)
+    logging.info("pairs_per_clust: %d ", (n_X / N) * (n_Z / N))
+    logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
+
+    eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type)
+    rows_x, rows_z = _swr_rows(n_X, n_Z, N)  # the reference's redundant initial draw (:119)
+    eng.set_shards(rows_x, rows_z)
+    kx, kz = eng.kx, eng.kz
+
+    for i in range(0, p_learn["n_it"]):
+        if i % p_learn["reshuffle_mod"] == 0:
+            rows_x, rows_z = _swr_rows(n_X, n_Z, N)
+            eng.set_shards(rows_x, rows_z)
+        if i % p_learn["eval_mod"] == 0:
+            w = eng.w_host()
+            if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
+                X_s = [X[r] for r in rows_x]
+                Z_s = [Z[r] for r in rows_z]
+            else:
+                X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
+            evaluation_step(i, X_s, Z_s, w, p_learn)
+        if trajectory is not None:
+            trajectory.append(eng.w_host())
+        ix = np.empty((N, B), dtype=np.int64)
+        iz = np.empty((N, B), dtype=np.int64)
+        for s in range(N):  # grad_inc_block's draws, shard by shard (compute_stats.py:155-156)
+            ix[s] = np.random.randint(0, kx, B)
+            iz[s] = np.random.randint(0, kz, B)
+        assert optim_type in ["SGD", "momentum"]
+        eng.step(ix, iz)
+    return None
+
+
+class _EvalCache:
+    """Device copies of p_learn's evaluation matrices and monitor pairs, reused across calls
+    while p_learn holds the same objects."""
+
+    def __init__(self):
+        self.src = {}
+        self.dev = {}
+
+    def get(self, key, obj, make):
+        if self.src.get(key) is not obj:
+            self.src[key] = obj
+            self.dev[key] = make(obj)
+        return self.dev[key]
+
+
+_CACHE = _EvalCache()
+
+
+def _scores(A_dev, w):
+    """A @ w on the device (tw_gemv_f64)."""
+    t = L.torch()
+    wd = L.to_device(np.asarray(w, dtype=np.float64).reshape(-1))
+    out = L.empty((A_dev.shape[0],), t.float64)
+    L.call("tw_gemv_f64", L.ptr(A_dev), A_dev.shape[0], A_dev.shape[1], L.ptr(wd), L.ptr(out),
+           L.stream_handle())
+    return out
+
+
+def _complete(sx, sz, which, margin=0.0):
+    n, m = sx.shape[0], sz.shape[0]
+    sh = E.Shards(sx, np.array([0, n], np.int64), sz, np.array([0, m], np.int64), L.TW_F64)
+    if which == "AUC":
+        return E.ratio(E.count_complete(sh, "gt")[0], n * m)
+    return np.float64(E.pair_sum_complete(sh, L.TW_KERN_HINGE, margin)[0] / np.float64(n * m))
+
+
+def evaluation_step(i, X_s, Z_s, w, p_learn):
+    """
+        Modify the value of p_learn to add to the evaluation.  (make_exps.py:143-190)
+        Monitored values, added in p_learn:
+        * br_AUC: block real AUC, on the training data,
+        * bc_AUC: block convexified AUC, on the training data,
+        * tr_AUC: real AUC, on the testing data,
+        * tc_AUC: convexified AUC, on the testing data,
+    """
+    margin = p_learn["margin"]
+    logging.debug("Step %d: Begin evaluation", i)
+    reg_term = p_learn["reg"] * (np.linalg.norm(w) ** 2) / 2
+    if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
+        sc_X = [x.dot(w) for x in X_s]
+        sc_Z = [z.dot(w) for z in Z_s]
+        bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin)) + reg_term
+        br_AUC = cs.UN_split(sc_X, sc_Z, lambda x, z: cs.Un(x, z, kernel="AUC"))
+    elif TYPE_TRAIN_MONITOR == "FIXED_PAIRS":
+        tX = _CACHE.get("train_X", p_learn["train_X"],
+                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+        tZ = _CACHE.get("train_Z", p_learn["train_Z"],
+                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+        pairs = _CACHE.get("pairs", p_learn["train_mon_pairs"],
+                           lambda p: np.asarray(p, dtype=np.int64).reshape(-1, 2))
+        sx, sz = _scores(tX, w), _scores(tZ, w)
+        off = np.array([0, pairs.shape[0]], dtype=np.int64)
+        hinge = E.pair_sum_indexed(sx, sz, pairs[:, 0], pairs[:, 1], off, L.TW_KERN_HINGE,
+                                   float(margin))[0]
+        bc_AUC = np.float64(hinge / np.float64(pairs.shape[0])) + reg_term
+        cnt = E.count_indexed(sx, sz, L.TW_F64, pairs[:, 0], pairs[:, 1], off, "gt")[0]
+        br_AUC = E.ratio(cnt, pairs.shape[0])
+
+    eX = _CACHE.get("test_X", p_learn["test_X"],
+                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+    eZ = _CACHE.get("test_Z", p_learn["test_Z"],
+                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+    sxt, szt = _scores(eX, w), _scores(eZ, w)
+    tc_AUC = _complete(sxt, szt, "hinge", float(margin)) + reg_term
+    tr_AUC = _complete(sxt, szt, "AUC")
+
+    s_log = ("it %5d: bc_AUC = %.4f | br_AUC = %.4f "
+             + "| tc_AUC = %5.4f | tr_AUC = %5.4f")
+    logging.info(s_log, i, bc_AUC, br_AUC, tc_AUC, tr_AUC)
+
+    elems = [("iter", i), ("norm_w", np.linalg.norm(w)),
+             ("bc_AUC", bc_AUC), ("br_AUC", br_AUC),
+             ("tr_AUC", tr_AUC), ("tc_AUC", tc_AUC)]
+    for k, v in elems:
+        if k in p_learn:
+            p_learn[k].append(v)
+        else:
+            p_learn[k] = [v]
+    logging.debug("Step %d: End evaluation", i)
+
+
+# convenience re-export for drivers that import SWR_divide / UN_split from here
+SWR_divide = cs.SWR_divide
+ShardList = _learn.ShardList
