@@ -1,0 +1,56 @@
+"""The C ABI (include/tuplewise.h) without a GPU: the library loads, every declared symbol is
+exported and bound in _lib, and argument errors are reported before any device work."""
+import ctypes
+import pathlib
+import re
+
+import numpy as np
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def header_functions():
+    text = (ROOT / "include" / "tuplewise.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(tw_\w+)\s*\(", text, re.M)))
+
+
+def test_header_symbols_exported(tw):
+    lib = tw._lib.lib()
+    names = header_functions()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+    assert sorted(tw._lib.exported_symbols()) == names
+
+
+def test_version_and_device_count(tw):
+    lib = tw._lib.lib()
+    assert lib.tw_version() == 1
+    n = ctypes.c_int(-1)
+    assert lib.tw_device_count(ctypes.byref(n)) == 0
+    assert n.value >= 0
+
+
+def test_argument_errors_without_gpu(tw):
+    L = tw._lib
+    lib = L.lib()
+    rc = lib.tw_count_pairs(None, None, None, None, -1, 0, 0, 0, 0, None, None)
+    assert rc == L.TW_ERR_ARG
+    assert b"n_shards" in lib.tw_last_error()
+    with pytest.raises(ValueError):
+        L.call("tw_hinge_grad", None, None, 0, None, 0, None, 0, None, None, 1, 1, None, 1.0,
+               None, None)
+    with pytest.raises(ValueError):
+        L.call("tw_count_set_plan", 3, 0)
+    assert lib.tw_pair_sum_idx_work_per_shard(10_000) == 5
+
+
+def test_no_device_raises(tw):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is present")
+    import tuplewise.estimation as est
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        est.Un(np.ones(3), np.zeros(2))

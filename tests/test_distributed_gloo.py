@@ -1,0 +1,133 @@
+"""Multi-rank repartition + reduction of tuplewise.device.ShardedSample on CPU (gloo).
+
+The product runs one process per GPU over RCCL; here the same orchestration (global keyed
+permutation, destination histogram, all-to-all of {value, position} records, scatter,
+zero-padded all-reduce of per-shard counts, host np.mean) runs at world size 2 and 4 with
+gloo, with the device operations replaced by their oracle restatements (test-only).  Checks:
+the permuted global arrays equal the single-process permutation, and the estimate is
+bit-identical to the G = 1 result — the G-invariance the design promises.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+
+class OracleOps:
+    """CPU stand-ins for tuplewise.device.HipOps (test infrastructure)."""
+
+    def perm_index(self, n, base, n_total, key):
+        return torch.from_numpy(O.feistel_perm(np.arange(base, base + n), n_total, key))
+
+    def permute(self, vals, key):
+        return torch.from_numpy(O.permute_scatter(vals.numpy(), key))
+
+    def rank_histogram(self, perm, n_loc, G):
+        return torch.from_numpy(np.bincount(perm.numpy() // n_loc, minlength=G).astype(np.int64))
+
+    def bucket_scatter(self, perm, vals, n_loc, G, start):
+        p = perm.numpy()
+        dst = p // n_loc
+        order = np.argsort(dst, kind="stable")
+        rec = np.empty((len(p), 2), dtype=np.int64)
+        rec[:, 0] = vals.numpy().view(np.int64)[order]
+        rec[:, 1] = (p - dst * n_loc)[order]
+        assert np.array_equal(np.cumsum(np.bincount(dst, minlength=G)) -
+                              np.bincount(dst, minlength=G), start.numpy())
+        return torch.from_numpy(rec)
+
+    def scatter_records(self, rec, out):
+        o = out.numpy().view(np.int64)
+        r = rec.numpy()
+        o[r[:, 1]] = r[:, 0]
+        return out
+
+    def count(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred):
+        xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
+        xs, zs = x.numpy(), z.numpy()
+        f = O.un_count if pred == 0 else O.count_half_sorted
+        return torch.tensor([f(xs[xo[s]:xo[s + 1]], zs[zo[s]:zo[s + 1]])
+                             for s in range(n_shards)], dtype=torch.int64)
+
+    def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred):
+        xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
+        out = []
+        for s in range(n_shards):
+            xs, zs = x.numpy()[xo[s]:xo[s + 1]], z.numpy()[zo[s]:zo[s + 1]]
+            i, j = O.rng_pairs(len(xs), len(zs), B, seed, shard_base + s)
+            out.append(int((xs[i] > zs[j]).sum()))
+        return torch.tensor(out, dtype=torch.int64)
+
+    def to_dev(self, arr):
+        return torch.from_numpy(np.ascontiguousarray(arr))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _global_data(G, n_loc, m_loc):
+    rng = np.random.RandomState(42)
+    return rng.normal(0.4, 1, G * n_loc), rng.normal(0, 1, G * m_loc)
+
+
+def _worker(rank, G, port, n_loc, m_loc, N, keys, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(G, n_loc, m_loc)
+    S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
+                      torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
+                      group=dist.group.WORLD, ops=OracleOps())
+    vals = [float(S.UnN(k)) for k in keys]
+    inc = float(S.UnNB(B, seed=77))
+    Xg = [torch.empty_like(S.X) for _ in range(G)]
+    Zg = [torch.empty_like(S.Z) for _ in range(G)]
+    dist.all_gather(Xg, S.X)
+    dist.all_gather(Zg, S.Z)
+    if rank == 0:
+        q.put((vals, inc, torch.cat(Xg).numpy(), torch.cat(Zg).numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_multirank_repartition_is_G_invariant(G):
+    import tuplewise  # noqa: F401  (package import only; no device work in this test)
+    from tuplewise.device import ShardedSample
+    n_loc, m_loc, N, keys, B = 600, 450, 3, [5, 6], 200
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, G, port, n_loc, m_loc, N, keys, B, q))
+             for r in range(G)]
+    for p in procs:
+        p.start()
+    vals, inc, Xg, Zg = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    # single-process reference of the same global problem (G*N shards of the same layout)
+    X, Z = _global_data(G, n_loc, m_loc)
+    S1 = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
+                       ops=OracleOps())
+    # the global permutation after both repartitions equals the G=1 permutation
+    Xp, Zp = X.copy(), Z.copy()
+    for k in keys:
+        Xp = O.permute_scatter(Xp, 2 * k)
+        Zp = O.permute_scatter(Zp, 2 * k + 1)
+    assert np.array_equal(Xg, Xp) and np.array_equal(Zg, Zp)
+    # per-rank shards are the rank-local prop-SWOR blocks; with n_loc divisible by N they
+    # coincide with the global layout, so the estimates are bit-identical to G = 1
+    want = [float(S1.UnN(k)) for k in keys]
+    assert vals == want
+    assert inc == float(S1.UnNB(B, seed=77))
