@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--n", type=int, default=N_PER_CLASS)
     ap.add_argument("--shards", type=int, default=N_SHARDS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sgd", action="store_true", help="skip the SGD steps/s secondary")
     ap.add_argument("--cpu-shards", type=int, default=N_SHARDS,
                     help="shards of the CPU-baseline sample (64 = one full UnN)")
     return ap.parse_args()
@@ -71,6 +72,41 @@ def cpu_baseline(n, N, shards):
     return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
             "sample": f"est.UnN body (in-place shuffle + {shards} of {N} prop-SWOR blocks of "
                       f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
+
+
+def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup):
+    """Pairwise-hinge SGD steps/s (BASELINE metric, second half): learning_process's loop
+    (make_exps.py:122-141) without evaluation, device-RNG mode, hipGraph-replayed segments.
+    Synthetic data of the given shape generated on the device."""
+    import torch
+    from tuplewise.learning import SGDEngine
+    g = torch.Generator(device="cuda").manual_seed(7)
+    X = torch.randn((n_X, d), dtype=torch.float64, device="cuda", generator=g)
+    Z = torch.randn((n_Z, d), dtype=torch.float64, device="cuda", generator=g) + 0.3
+    w0 = torch.randn((d, 1), dtype=torch.float64, device="cuda", generator=g)
+    eng = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
+                    optim_type="momentum")
+    eng.enable_device_rng(12345)
+
+    def run(k):
+        i = 0
+        while i < k:
+            nxt = min(k, (i // reshuffle_mod + 1) * reshuffle_mod)
+            eng.run_segment(nxt - i, i % reshuffle_mod == 0, graphs=True)
+            i = nxt
+
+    run(max(warmup * reshuffle_mod, reshuffle_mod))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
+            "gather_GBps": N * B * 16 * d * steps / dt / 1e9,
+            "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B,
+                       "reshuffle_mod": reshuffle_mod, "optim": "momentum",
+                       "rng": "device (Philox)", "graphs": True, "steps": steps}}
 
 
 def pmc_traffic():
@@ -180,6 +216,15 @@ def main():
                              "the committed rocprofv3 --pmc summary"},
         "estimate_last_step": float(est),
     }
+    if world == 1 and not args.no_sgd:
+        # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'
+        out["secondary"] = {
+            "metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)",
+            "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2),
+            "C5_scaled_d512": sgd_steps_per_s(1_000_000, 1_000_000, 512, 256, 100, 25, 500, 2),
+            "C5_scaled_d512_B4096": sgd_steps_per_s(1_000_000, 1_000_000, 512, 256, 4096, 25,
+                                                    100, 1),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
     if rank == 0:

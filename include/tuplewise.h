@@ -123,11 +123,27 @@ int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t
                   const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
                   double margin, double* d_out, void* stream);
 
+/* ---- Row L1/A9, device-RNG mode (no host RNG in the loop; graph-capturable) -----------
+ * Draws are Philox4x32-10(key = seed, counter = (index, shard, step lo, tag | step hi)) with
+ * step = *d_step (device memory, advanced by tw_sgd_update), mapped by 64-bit multiply-high:
+ * tw_hinge_grad_rng: pair b of shard s -> (ix, iz) in [0,kx) x [0,kz) (tag 0x80000000);
+ * tw_swr_rows_rng:   d_rows[s*k + t] in [0, n), side 0 = X rows (tag 0x40000000), 1 = Z rows
+ *                    (tag 0x20000000) — SWR_divide (compute_stats.py:48-54) on the device.
+ * Statistically equivalent to the reference's NumPy draws, not bit-comparable; exactly
+ * reproducible from (seed, step) and checked against oracle/oracle.py's restatement. */
+int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                      int64_t kx, const int64_t* d_rows_z, int64_t kz, int32_t n_shards,
+                      int64_t B, const double* d_w, double margin, uint64_t seed,
+                      const uint64_t* d_step, double* d_out, void* stream);
+int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n, uint64_t seed,
+                    const uint64_t* d_step, int32_t side, void* stream);
+
 /* ---- Row L2: update of learning_process (make_exps.py:130-141) ------------------------
  * g = mean_s(d_grads[s]) + reg * w  (shards summed in order, then / n_shards — np.mean axis 0)
- * momentum: dw = momentum * dw + lr * g;  SGD (momentum < 0): dw = lr * g;   w = w - dw. */
+ * momentum: dw = momentum * dw + lr * g;  SGD (momentum < 0): dw = lr * g;   w = w - dw.
+ * d_step (nullable): device-RNG step counter, incremented once. */
 int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, int32_t n_shards, int64_t d,
-                  double reg, double lr, double momentum, void* stream);
+                  double reg, double lr, double momentum, uint64_t* d_step, void* stream);
 
 /* ---- f1: scores = A @ w for a row-major (n, d) matrix (evaluation_step, make_exps.py:163,
  * :170-171).  Row dot products in index order. */
@@ -155,6 +171,17 @@ int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int64_t n, int6
                       int32_t G, const int64_t* d_start, uint64_t* d_cursor, void* d_send,
                       void* stream);
 int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream);
+
+/* ---- f2: bulk draws of NumPy's legacy global RNG (host code, no GPU) ------------------
+ * key (624 words) / pos: the MT19937 state of np.random.get_state(), advanced in place.
+ * tw_np_randint_batch: n_calls consecutive RandomState.randint(low[c], high[c], cnt[c]) calls
+ * (int64 output, NumPy's masked-rejection algorithm), values concatenated into out; returns
+ * 0, or 1 when a range is empty (high <= low).  Replaces the per-shard randint calls of
+ * grad_inc_block (compute_stats.py:155-156) and SWR_divide (:52-53) in replay mode.
+ * tw_np_mt_next32: the raw genrand_int32 stream. */
+int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
+                        const int64_t* high, const int64_t* cnt, int64_t* out);
+int tw_np_mt_next32(uint32_t* key, int32_t* pos, int64_t cnt, uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -321,3 +321,45 @@ def rng_pairs(nx: int, nz: int, B: int, seed: int, shard: int):
     u = (b << np.uint64(32)) | a
     v = (d << np.uint64(32)) | c
     return _mulhi64(u, nx), _mulhi64(v, nz)
+
+
+def _sgd_draw(seed, step, idx, shard, tag):
+    """Restates csrc/hinge.hip sgd_draw: Philox counter (idx, shard, step lo, tag|step hi)."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    n = idx.size
+    a, b, c, d = philox4x32_10(idx, np.full(n, shard, np.uint64),
+                               np.full(n, step & 0xFFFFFFFF, np.uint64),
+                               np.full(n, tag | (step >> 32), np.uint64),
+                               seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return (b << np.uint64(32)) | a, (d << np.uint64(32)) | c
+
+
+def device_rng_learning_trajectory(X, Z, p_learn, seed, optim_type="momentum"):
+    """learning_process (make_exps.py:96-141) with the device-RNG draws of
+    tw_swr_rows_rng / tw_hinge_grad_rng (tags 0x40000000 / 0x20000000 / 0x80000000) and the
+    reference's gradient/update arithmetic; returns w before every step."""
+    N, B = p_learn["N"], p_learn["B"]
+    n_X, n_Z = X.shape[0], Z.shape[0]
+    kx, kz = int(n_X / N), int(n_Z / N)
+    w = p_learn["w_init"]
+    delta_w = 0
+    ws = []
+    rows_x = rows_z = None
+    for i in range(p_learn["n_it"]):
+        if i % p_learn["reshuffle_mod"] == 0:
+            rows_x = [_mulhi64(_sgd_draw(seed, i, np.arange(kx), s, 0x40000000)[0], n_X)
+                      for s in range(N)]
+            rows_z = [_mulhi64(_sgd_draw(seed, i, np.arange(kz), s, 0x20000000)[0], n_Z)
+                      for s in range(N)]
+        ws.append(np.array(w, copy=True))
+        grads = []
+        for s in range(N):
+            u, v = _sgd_draw(seed, i, np.arange(B), s, 0x80000000)
+            ix, iz = _mulhi64(u, kx), _mulhi64(v, kz)
+            diff = Z[rows_z[s]][iz] - X[rows_x[s]][ix]
+            filt = ((diff.dot(w) + p_learn["margin"]) > 0).ravel()
+            grads.append((diff[filt].sum(axis=0) / B).reshape([-1, 1]))
+        g = np.mean(grads, axis=0)
+        w, delta_w = sgd_step(w, delta_w, g, p_learn["reg"], p_learn["learning_rate"],
+                              optim_type)
+    return ws, w

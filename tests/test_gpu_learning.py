@@ -66,3 +66,33 @@ def test_sgd_optimizer_and_assert(gpu, golden):
     np.testing.assert_allclose(np.stack(traj), np.stack(ws), rtol=1e-10, atol=1e-14)
     with pytest.raises(AssertionError):
         lr.learning_process(X, Z, _p_learn(golden, n_it=2), optim_type="adam")
+
+
+def test_device_rng_mode_matches_restatement(gpu, golden):
+    """rng_mode="device": draws on the GPU (Philox), exact vs oracle's restatement."""
+    import tuplewise.learning as lr
+    from oracle import oracle as O
+    p = _p_learn(golden, n_it=60)
+    traj = []
+    np.random.seed(31)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, rng_mode="device",
+                        trajectory=traj)
+    np.random.seed(31)
+    seed = int(np.random.randint(0, 2 ** 63 - 1, dtype=np.int64))
+    ws, _ = O.device_rng_learning_trajectory(golden["learn/X"], golden["learn/Z"], p, seed)
+    np.testing.assert_allclose(np.stack(traj), np.stack(ws), rtol=1e-10, atol=1e-14)
+
+
+def test_device_rng_graphs_equal_eager(gpu, golden):
+    """hipGraph-replayed segments give the same w as eager launches."""
+    import tuplewise.learning as lr
+    out = []
+    for graphs in (False, True):
+        p = _p_learn(golden, n_it=137)
+        p["eval_mod"] = 50
+        np.random.seed(8)
+        eng_w = []
+        lr.learning_process(golden["learn/X"], golden["learn/Z"], p, rng_mode="device",
+                            graphs=graphs)
+        out.append((p["norm_w"], p["bc_AUC"]))
+    assert out[0] == out[1]

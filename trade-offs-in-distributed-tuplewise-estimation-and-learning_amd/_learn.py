@@ -11,6 +11,7 @@ import numpy as np
 
 from . import _blocks as Bk
 from . import _lib as L
+from .numpy_rng import randint_batch
 
 
 class ShardList(list):
@@ -50,14 +51,16 @@ class GradSpec(Bk.BlockSpec):
         return ix, iz
 
     def _grads(self, X_s, Z_s):
-        draws = [self.draw(np.asarray(x).shape[0], np.asarray(z).shape[0])
-                 for x, z in zip(X_s, Z_s)]
-        N = len(draws)
+        N = min(len(X_s), len(Z_s))
         if N == 0:
             return []
-        t = L.torch()
-        ix = np.stack([dr[0] for dr in draws]).astype(np.int64)
-        iz = np.stack([dr[1] for dr in draws]).astype(np.int64)
+        # every shard's two randint calls (X then Z, shard by shard) in one native batch
+        calls = []
+        for x, z in zip(X_s, Z_s):
+            calls += [(0, np.asarray(x).shape[0], self.B), (0, np.asarray(z).shape[0], self.B)]
+        out = randint_batch(calls)
+        ix = np.stack(out[0::2])
+        iz = np.stack(out[1::2])
         d = _as_matrix(X_s[0]).shape[1]
 
         def side(S, draws_idx):

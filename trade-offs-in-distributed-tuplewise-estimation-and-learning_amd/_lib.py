@@ -37,13 +37,18 @@ _SIGNATURES = {
     "tw_pair_sum_idx_f64": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _f64, _vp, _vp, _vp],
     "tw_hinge_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64,
                       _vp, _vp],
-    "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp],
+    "tw_hinge_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _u64,
+                          _vp, _vp, _vp],
+    "tw_swr_rows_rng": [_vp, _i32, _i64, _i64, _u64, _vp, _i32, _vp],
+    "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
     "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],
     "tw_perm_index": [_vp, _i64, _i64, _i64, _u64, _vp],
     "tw_rank_histogram": [_vp, _i64, _i64, _i32, _vp, _vp],
     "tw_bucket_scatter": [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     "tw_scatter_records": [_vp, _i64, _vp, _vp],
+    "tw_np_randint_batch": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
+    "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
 }
 _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,

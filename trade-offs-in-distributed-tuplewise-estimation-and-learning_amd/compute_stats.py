@@ -13,6 +13,7 @@ import numpy as np
 from . import _blocks as Bk
 from . import _lib as L
 from . import _learn
+from .numpy_rng import randint_batch
 
 _KERNELS = ["prod", "gini", "AUC"]
 
@@ -75,8 +76,8 @@ def SWR_divide(X, Z, N):
     indices so device consumers (UN_split with grad_inc_block) can gather on the GPU."""
     n_X = X.shape[0]
     n_Z = Z.shape[0]
-    rows_x = [np.random.randint(0, n_X, int(n_X / N)) for _ in range(N)]
-    rows_z = [np.random.randint(0, n_Z, int(n_Z / N)) for _ in range(N)]
+    rows = randint_batch([(0, n_X, int(n_X / N))] * N + [(0, n_Z, int(n_Z / N))] * N)
+    rows_x, rows_z = rows[:N], rows[N:]
     return (_learn.ShardList([X[r] for r in rows_x], X, rows_x),
             _learn.ShardList([Z[r] for r in rows_z], Z, rows_z))
 

@@ -24,11 +24,22 @@ namespace tw {
 constexpr int kLdsDoubles = 8192;  // 64 KiB of diff rows per block
 constexpr int kMaxColsPerThread = 16;  // d <= 4096
 
+// Device-RNG mode counters: Philox4x32-10 keyed by the run's seed; counter words
+// (index, shard, step lo, tag | step hi).  Tags separate the three draw streams.
+constexpr uint32_t kTagPairs = 0x80000000u, kTagRowsX = 0x40000000u, kTagRowsZ = 0x20000000u;
+
+__device__ __forceinline__ u32x4 sgd_draw(uint64_t seed, uint64_t step, uint32_t idx,
+                                          uint32_t shard, uint32_t tag) {
+  return philox4x32_10(u32x4{idx, shard, (uint32_t)step, tag | (uint32_t)(step >> 32)},
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
 __global__ __launch_bounds__(kBlock) void k_hinge_grad(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
-    int CH, const double* __restrict__ w, double margin, double* __restrict__ out) {
+    int CH, const double* __restrict__ w, double margin, double* __restrict__ out,
+    uint64_t seed, const uint64_t* __restrict__ d_step) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* diff = (double*)smem;                             // CH * d
   int64_t* rx = (int64_t*)(smem + sizeof(double) * CH * d);  // CH
@@ -41,12 +52,21 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
 #pragma unroll
   for (int q = 0; q < kMaxColsPerThread; ++q) acc[q] = 0.0;
 
+  const uint64_t step = d_step ? *d_step : 0;
   for (int64_t b0 = 0; b0 < B; b0 += CH) {
     const int nb = (int)std::min<int64_t>(CH, B - b0);
     // rows of this chunk: compose the SWR shard draw with the per-step pair draw
     for (int t = threadIdx.x; t < nb; t += kBlock) {
       const int64_t p = (int64_t)s * B + b0 + t;
-      const int64_t ax = ix[p], az = iz[p];
+      int64_t ax, az;
+      if (ix) {  // replay: NumPy's randint draws
+        ax = ix[p];
+        az = iz[p];
+      } else {  // device RNG
+        const u32x4 r = sgd_draw(seed, step, (uint32_t)(b0 + t), (uint32_t)s, kTagPairs);
+        ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
+        az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
+      }
       rx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
       rz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
     }
@@ -89,12 +109,30 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
   }
 }
 
+// SWR_divide row draws on the device: rows[s*k + t] uniform in [0, n) (with replacement).
+__global__ __launch_bounds__(kBlock) void k_swr_rows(int64_t* __restrict__ rows, int n_shards,
+                                                     int64_t k, int64_t n, uint64_t seed,
+                                                     const uint64_t* __restrict__ d_step,
+                                                     uint32_t tag) {
+  const uint64_t step = *d_step;
+  const int64_t total = (int64_t)n_shards * k;
+  for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * kBlock) {
+    const int64_t s = e / k, t = e - s * k;
+    const u32x4 r = sgd_draw(seed, step, (uint32_t)t, (uint32_t)s, tag);
+    rows[e] = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)n);
+  }
+}
+
 // g = (sum_s grads[s]) / N + reg*w ; dw = momentum*dw + lr*g (SGD: dw = lr*g) ; w = w - dw
+// d_step (optional): the device-RNG step counter, advanced once per update.
 __global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
                                                        double* __restrict__ dw,
                                                        const double* __restrict__ grads,
                                                        int n_shards, int64_t d, double reg,
-                                                       double lr, double momentum) {
+                                                       double lr, double momentum,
+                                                       uint64_t* __restrict__ d_step) {
+  if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += 1;
   for (int64_t j = blockIdx.x * (int64_t)kBlock + threadIdx.x; j < d;
        j += (int64_t)gridDim.x * kBlock) {
     double sum = 0.0;  // np.mean(axis=0): 0.0 + g_0 + g_1 + ... in shard order, then / N
@@ -135,19 +173,58 @@ extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
   hipStream_t st = (hipStream_t)stream;
   const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
   const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
+  TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_hinge_grad: pair indices required");
   hipLaunchKernelGGL(k_hinge_grad, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x,
-                     kx, d_rows_z, kz, d_ix, d_iz, B, CH, d_w, margin, d_out);
+                     kx, d_rows_z, kz, d_ix, d_iz, B, CH, d_w, margin, d_out, (uint64_t)0,
+                     (const uint64_t*)nullptr);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,
+                                 const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                                 int64_t kz, int32_t n_shards, int64_t B, const double* d_w,
+                                 double margin, uint64_t seed, const uint64_t* d_step,
+                                 double* d_out, void* stream) {
+  TW_ARG_CHECK(d >= 1 && d <= (int64_t)kBlock * kMaxColsPerThread,
+               "tw_hinge_grad_rng: d=%lld outside [1, %d]", (long long)d, kBlock * kMaxColsPerThread);
+  TW_ARG_CHECK(n_shards >= 0 && B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1,
+               "tw_hinge_grad_rng: bad n_shards/B/kx/kz");
+  TW_ARG_CHECK(d_step != nullptr, "tw_hinge_grad_rng: step counter required");
+  if (n_shards == 0) return TW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
+  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
+  hipLaunchKernelGGL(k_hinge_grad, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x,
+                     kx, d_rows_z, kz, (const int64_t*)nullptr, (const int64_t*)nullptr, B, CH,
+                     d_w, margin, d_out, seed, d_step);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n,
+                               uint64_t seed, const uint64_t* d_step, int32_t side,
+                               void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && k >= 0 && n >= 1 && k < (1ll << 32) && d_step != nullptr,
+               "tw_swr_rows_rng: bad sizes");
+  TW_ARG_CHECK(side == 0 || side == 1, "tw_swr_rows_rng: side must be 0 (X) or 1 (Z)");
+  const int64_t total = (int64_t)n_shards * k;
+  if (total == 0) return TW_OK;
+  const int blocks = (int)std::min<int64_t>(256 * 8, ceil_div(total, kBlock));
+  hipLaunchKernelGGL(k_swr_rows, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, d_rows,
+                     (int)n_shards, k, n, seed, d_step, side == 0 ? kTagRowsX : kTagRowsZ);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
 
 extern "C" int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, int32_t n_shards,
-                             int64_t d, double reg, double lr, double momentum, void* stream) {
+                             int64_t d, double reg, double lr, double momentum, uint64_t* d_step,
+                             void* stream) {
   TW_ARG_CHECK(n_shards >= 1 && d >= 1, "tw_sgd_update: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (int)std::min<int64_t>(1024, ceil_div(d, kBlock));
   hipLaunchKernelGGL(k_sgd_update, dim3(blocks), dim3(kBlock), 0, st, d_w, d_dw, d_grads,
-                     n_shards, d, reg, lr, momentum);
+                     n_shards, d, reg, lr, momentum, d_step);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

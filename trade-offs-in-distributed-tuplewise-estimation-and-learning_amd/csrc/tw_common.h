@@ -51,4 +51,22 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// Philox4x32-10 (Salmon et al., SC'11): counter-based RNG for the device-RNG modes.
+struct u32x4 {
+  uint32_t a, b, c, d;
+};
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(M0, ctr.a), lo0 = M0 * ctr.a;
+    const uint32_t hi1 = __umulhi(M1, ctr.c), lo1 = M1 * ctr.c;
+    ctr = u32x4{hi1 ^ ctr.b ^ k0, lo1, hi0 ^ ctr.d ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return ctr;
+}
+__device__ __forceinline__ uint64_t mulhi_u64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
+
 }  // namespace tw

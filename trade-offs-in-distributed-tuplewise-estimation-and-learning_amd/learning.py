@@ -24,6 +24,7 @@ from . import _engine as E
 from . import _lib as L
 from . import _learn
 from . import compute_stats as cs
+from .numpy_rng import randint_batch
 
 SEED_SHUFFLE = 42
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
@@ -37,18 +38,19 @@ class SGDEngine:
     """Device-resident pairwise-hinge SGD state for one learning_process run."""
 
     def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type):
+        """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is)."""
         t = L.torch()
         self.t = t
-        self.X = L.to_device(np.asarray(X, dtype=np.float64))
-        self.Z = L.to_device(np.asarray(Z, dtype=np.float64))
+        self.X = _dev_f64(X)
+        self.Z = _dev_f64(Z)
         self.n_X, self.d = self.X.shape
         self.n_Z = self.Z.shape[0]
         self.N, self.B = int(N), int(B)
         self.kx, self.kz = int(self.n_X / N), int(self.n_Z / N)
         self.margin, self.reg, self.lr = float(margin), float(reg), float(learning_rate)
         self.momentum = 0.9 if optim_type == "momentum" else -1.0
-        self.w_shape = np.asarray(w_init).shape
-        self.w = L.to_device(np.asarray(w_init, dtype=np.float64).reshape(-1))
+        self.w_shape = tuple(w_init.shape)
+        self.w = _dev_f64(w_init).reshape(-1).clone()
         self.dw = t.zeros_like(self.w)
         self.grads = L.empty((self.N, self.d), t.float64)
         self.rows_x = self.rows_z = None
@@ -64,21 +66,100 @@ class SGDEngine:
                L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N, self.B,
                L.ptr(self.w), self.margin, L.ptr(self.grads), s)
         L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
-               self.d, self.reg, self.lr, self.momentum, s)
+               self.d, self.reg, self.lr, self.momentum, None, s)
 
     def w_host(self) -> np.ndarray:
         return self.w.cpu().numpy().reshape(self.w_shape)
 
+    # ------------------------------------------------------------ device-RNG mode
+    def enable_device_rng(self, seed: int):
+        """Draw SWR rows and pair indices on the device (Philox keyed by `seed`, counter =
+        the step number kept in device memory).  Steps then need no host work at all and can
+        be captured in hipGraphs."""
+        t = self.t
+        self.seed = int(seed) & (2 ** 64 - 1)
+        self.step_ctr = t.zeros((1,), dtype=t.int64, device=self.w.device)
+        self.rows_x = t.empty((self.N, self.kx), dtype=t.int64, device=self.w.device)
+        self.rows_z = t.empty((self.N, self.kz), dtype=t.int64, device=self.w.device)
+        self._graphs = {}
+
+    def reshuffle_device(self):
+        s = L.stream_handle()
+        L.call("tw_swr_rows_rng", L.ptr(self.rows_x), self.N, self.kx, self.n_X, self.seed,
+               L.ptr(self.step_ctr), 0, s)
+        L.call("tw_swr_rows_rng", L.ptr(self.rows_z), self.N, self.kz, self.n_Z, self.seed,
+               L.ptr(self.step_ctr), 1, s)
+
+    def step_device(self):
+        s = L.stream_handle()
+        L.call("tw_hinge_grad_rng", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
+               self.kx, L.ptr(self.rows_z), self.kz, self.N, self.B, L.ptr(self.w), self.margin,
+               self.seed, L.ptr(self.step_ctr), L.ptr(self.grads), s)
+        L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
+               self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr), s)
+
+    def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True):
+        """nsteps device-RNG steps (reshuffling first if asked), replayed from a captured
+        hipGraph per distinct segment shape."""
+        if not graphs:
+            if reshuffle_first:
+                self.reshuffle_device()
+            for _ in range(nsteps):
+                self.step_device()
+            return
+        t = self.t
+        while nsteps > 0:
+            n = min(nsteps, 256)
+            key = (n, reshuffle_first)
+            g = self._graphs.get(key)
+            if g is None:
+                g = t.cuda.CUDAGraph()
+                side = t.cuda.Stream()
+                side.wait_stream(t.cuda.current_stream())
+                with t.cuda.stream(side):  # warm the launch path outside capture
+                    pass
+                t.cuda.current_stream().wait_stream(side)
+                with t.cuda.graph(g):
+                    if reshuffle_first:
+                        self.reshuffle_device()
+                    for _ in range(n):
+                        self.step_device()
+                self._graphs[key] = g
+            g.replay()
+            nsteps -= n
+            reshuffle_first = False
+
+
+def _dev_f64(a):
+    t = L.torch()
+    if isinstance(a, t.Tensor):
+        return a.to(device=L.device(), dtype=t.float64).contiguous()
+    return L.to_device(np.asarray(a, dtype=np.float64))
+
 
 def _swr_rows(n_X, n_Z, N):
-    """The index draws of SWR_divide (compute_stats.py:48-54), same order."""
-    rows_x = [np.random.randint(0, n_X, int(n_X / N)) for _ in range(N)]
-    rows_z = [np.random.randint(0, n_Z, int(n_Z / N)) for _ in range(N)]
-    return rows_x, rows_z
+    """The index draws of SWR_divide (compute_stats.py:48-54), same order, in one native
+    call (tuplewise.numpy_rng: NumPy's own MT19937 stream and randint algorithm)."""
+    kx, kz = int(n_X / N), int(n_Z / N)
+    out = randint_batch([(0, n_X, kx)] * N + [(0, n_Z, kz)] * N)
+    return out[:N], out[N:]
 
 
-def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None):
-    """Learning process for our experiments.  (make_exps.py:96-141)"""
+def _pair_draws(N, kx, kz, B):
+    """grad_inc_block's draws for every shard of one UN_split call (compute_stats.py:155-156:
+    X indices then Z indices, shard by shard) as two (N, B) arrays."""
+    out = randint_batch([(0, kx, B), (0, kz, B)] * N)
+    return np.stack(out[0::2]), np.stack(out[1::2])
+
+
+def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
+                     rng_mode="replay", graphs=True):
+    """Learning process for our experiments.  (make_exps.py:96-141)
+
+    rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference.
+    rng_mode="device": SWR rows and pairs drawn on the device from a seed taken from the
+    global RNG (one randint); statistically equivalent, and with graphs=True each run of
+    steps between evaluations/reshuffles is one hipGraph replay."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -98,6 +179,11 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None):
     logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
 
     eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type)
+    if rng_mode == "device":
+        assert optim_type in ["SGD", "momentum"]
+        return _learning_device(eng, X, Z, p_learn, trajectory, graphs)
+    if rng_mode != "replay":
+        raise ValueError(f"rng_mode must be 'replay' or 'device', not {rng_mode!r}")
     rows_x, rows_z = _swr_rows(n_X, n_Z, N)  # the reference's redundant initial draw (:119)
     eng.set_shards(rows_x, rows_z)
     kx, kz = eng.kx, eng.kz
@@ -116,13 +202,31 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None):
             evaluation_step(i, X_s, Z_s, w, p_learn)
         if trajectory is not None:
             trajectory.append(eng.w_host())
-        ix = np.empty((N, B), dtype=np.int64)
-        iz = np.empty((N, B), dtype=np.int64)
-        for s in range(N):  # grad_inc_block's draws, shard by shard (compute_stats.py:155-156)
-            ix[s] = np.random.randint(0, kx, B)
-            iz[s] = np.random.randint(0, kz, B)
+        ix, iz = _pair_draws(N, kx, kz, B)
         assert optim_type in ["SGD", "momentum"]
         eng.step(ix, iz)
+    return None
+
+
+def _learning_device(eng, X, Z, p_learn, trajectory, graphs):
+    eng.enable_device_rng(int(np.random.randint(0, 2 ** 63 - 1, dtype=np.int64)))
+    n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
+    if trajectory is not None:
+        graphs = False
+    i = 0
+    while i < n_it:
+        if i % eval_mod == 0:
+            evaluation_step(i, None, None, eng.w_host(), p_learn)
+        if trajectory is not None:  # one step at a time, recording w
+            if i % mod == 0:
+                eng.reshuffle_device()
+            trajectory.append(eng.w_host())
+            eng.step_device()
+            i += 1
+            continue
+        nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod)
+        eng.run_segment(nxt - i, i % mod == 0, graphs)
+        i = nxt
     return None
 
 
