@@ -141,7 +141,7 @@ def main():
     n = args.n
     X = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) + 0.5
     Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
-    S = ShardedSample(X, Z, args.shards, group=group)
+    S = ShardedSample(X, Z, args.shards, group=group, algo="pairs")
     k = n // args.shards
     pairs_per_step_rank = args.shards * k * k
 
@@ -185,6 +185,28 @@ def main():
         dt = float(tt.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
 
+    # same workload, exact sort + binary-search count (csrc/rankcount.hip): logical pairs/s
+    same_counts = bool(torch.equal(S.local_counts(), (setattr(S, "algo", "sorted"),
+                                                      S.local_counts())[1]))
+    S.algo = "sorted"
+    for w in range(args.warmup):
+        S.UnN(key=10_000 + w)
+    torch.cuda.synchronize()
+    barrier()
+    kernel_ms.clear()
+    t1 = time.perf_counter()
+    for s_ in range(args.steps):
+        est_sorted = S.UnN(key=args.warmup + s_)  # same keys as the timed all-pairs steps
+    torch.cuda.synchronize()
+    barrier()
+    dt_sorted = time.perf_counter() - t1
+    if group is not None:
+        tt = torch.tensor([dt_sorted], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt_sorted = float(tt.item())
+    kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    S.algo = "pairs"
+
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
     achieved = pairs_per_step_rank / (kms * 1e-3)  # lane-ops/s, 1 compare per pair (strict)
@@ -215,6 +237,13 @@ def main():
                      "note": "1 v_cmp_f64 lane-op per pair; traffic = HBM bytes/launch from "
                              "the committed rocprofv3 --pmc summary"},
         "estimate_last_step": float(est),
+        "sorted_count": {
+            "note": "same UnN steps with the exact sort+binary-search count (algo='sorted', "
+                    "bit-identical estimates); pairs are logical, not compared one by one",
+            "value": total_pairs / dt_sorted, "unit": "logical pairs/s",
+            "ms_per_step": dt_sorted / args.steps * 1e3, "count_kernels_ms": kms_sorted,
+            "estimate_last_step": float(est_sorted),
+            "counts_identical_to_all_pairs": same_counts},
     }
     if world == 1 and not args.no_sgd:
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'

@@ -72,6 +72,16 @@ int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const void* d_z,
  * and z-chunk length per block (0 = automatic).  Process-global; results do not depend on it. */
 int tw_count_set_plan(int32_t R, int64_t z_chunk);
 
+/* ---- f4: the same counts in O((n+m) log m): sort each z-chunk (<= 16384 keys) in LDS as
+ * order-preserving u64 keys, then binary-search every x (csrc/rankcount.hip).  Bit-identical
+ * to tw_count_pairs for TW_PRED_GT and TW_PRED_HALF (not SUBGT).  d_work: device scratch of
+ * tw_count_pairs_sorted_work_bytes(n_shards, max_nz) bytes. */
+int64_t tw_count_pairs_sorted_work_bytes(int32_t n_shards, int64_t max_nz);
+int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                          const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                          int64_t max_nz, int32_t dtype, int32_t pred, void* d_work,
+                          uint64_t* d_out, void* stream);
+
 /* ---- Row A3/A4/A5/A8: incomplete count on given index pairs (replay mode) -------------
  * Replaces cs.UB_indices / UB_pairs / UB (compute_stats.py:22-42): pair p of shard s
  * compares x[d_ix[p]] with z[d_iz[p]] for p in [d_pair_off[s], d_pair_off[s+1]); indices are

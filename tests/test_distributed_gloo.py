@@ -48,7 +48,8 @@ class OracleOps:
         o[r[:, 1]] = r[:, 0]
         return out
 
-    def count(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred):
+    def count(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred,
+              algo="pairs"):
         xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
         xs, zs = x.numpy(), z.numpy()
         f = O.un_count if pred == 0 else O.count_half_sorted

@@ -30,7 +30,10 @@ def test_compare_operands_preserve_numpy_order(tw, dx, dz):
 def test_subtract_gt_modes(tw):
     from tuplewise import _engine as E
     x, z, code, mode = E.subtract_gt_operands(np.array([1, 2], np.int64), np.array([3], np.int64))
-    assert mode == "subgt"
+    assert mode == "gt"  # int64 that cannot wrap: the plain ordered comparison
+    _, _, _, mode = E.subtract_gt_operands(np.array([2 ** 62, -2 ** 63], np.int64),
+                                           np.array([-2 ** 62 - 1], np.int64))
+    assert mode == "subgt"  # 2^62 - (-2^62 - 1) wraps in int64
     _, _, _, mode = E.subtract_gt_operands(np.array([1, 2], np.uint8), np.array([3], np.uint8))
     assert mode == "ne"  # uint8: x - z wraps to >= 0, so "> 0" means "!="
     _, _, _, mode = E.subtract_gt_operands(np.array([1.0]), np.array([3], np.int64))

@@ -60,6 +60,11 @@ def subtract_gt_operands(X: np.ndarray, Z: np.ndarray):
         x = X.astype(np.int64, copy=False)
         z = Z.astype(np.int64, copy=False)
         if rt.itemsize == 8:
+            if x.size and z.size:  # no wrap possible -> plain ordered comparison
+                lo = int(x.min()) - int(z.max())
+                hi = int(x.max()) - int(z.min())
+                if -(2 ** 63) <= lo and hi <= 2 ** 63 - 1:
+                    return x, z, L.TW_I64, "gt"
             return x, z, L.TW_I64, "subgt"
         info = np.iinfo(rt)
         lo = int(x.min()) - int(z.max()) if x.size and z.size else 0
@@ -121,24 +126,51 @@ def _counts_to_host(out) -> np.ndarray:
     return out.cpu().numpy().view(np.uint64)
 
 
-def count_complete(sh: Shards, mode: str = "gt") -> np.ndarray:
+SORTED_MIN_PAIRS = 1 << 22  # "auto": per-shard pair count above which sort+search wins
+
+
+def pick_algo(algo: str, max_nx: int, max_nz: int, mode: str) -> str:
+    if algo == "auto":
+        return "sorted" if (mode in ("gt", "half", "ne")
+                            and max_nx * max_nz >= SORTED_MIN_PAIRS) else "pairs"
+    if algo not in ("pairs", "sorted"):
+        raise ValueError(f"algo must be 'auto', 'pairs' or 'sorted', not {algo!r}")
+    if algo == "sorted" and mode == "subgt":
+        raise ValueError("algo='sorted' needs an ordered predicate (no int64 wrap-around)")
+    return algo
+
+
+def count_launch(x_dev, x_off_dev, z_dev, z_off_dev, n, max_nx, max_nz, dtype, pred, algo):
+    """Enqueue one count of all shards (no host sync); returns the int64 device tensor."""
+    t = L.torch()
+    out = L.empty((n,), t.int64)
+    if algo == "sorted":
+        work = L.empty((int(L.lib().tw_count_pairs_sorted_work_bytes(n, max_nz)),), t.uint8)
+        L.call("tw_count_pairs_sorted", L.ptr(x_dev), L.ptr(x_off_dev), L.ptr(z_dev),
+               L.ptr(z_off_dev), n, max_nx, max_nz, dtype, pred, L.ptr(work), L.ptr(out),
+               L.stream_handle())
+    else:
+        L.call("tw_count_pairs", L.ptr(x_dev), L.ptr(x_off_dev), L.ptr(z_dev), L.ptr(z_off_dev),
+               n, max_nx, max_nz, dtype, pred, L.ptr(out), L.stream_handle())
+    return out
+
+
+def count_complete(sh: Shards, mode: str = "gt", algo: str = "auto") -> np.ndarray:
     """Per-shard exact counts (uint64) of the predicate over all pairs of each shard.
 
     mode: "gt" (#x>z), "half" (2#x>z + #x==z), "subgt" (#(x-z)>0 with int64 wrap),
-    "ne" (#x!=z, derived on the device from the half and gt counts)."""
+    "ne" (#x!=z, derived on the device from the half and gt counts).
+    algo: "pairs" (all-pairs VALU kernel), "sorted" (sort + binary search), "auto"."""
     n = sh.n_shards
     if n == 0:
         return np.zeros(0, dtype=np.uint64)
     xo, zo = sh.offsets_dev()
     max_nx = int(sh.nx.max())
     max_nz = int(sh.nz.max())
-    t = L.torch()
+    algo = pick_algo(algo, max_nx, max_nz, mode)
 
     def run(pred):
-        out = L.empty((n,), t.int64)
-        L.call("tw_count_pairs", L.ptr(sh.x), L.ptr(xo), L.ptr(sh.z), L.ptr(zo), n, max_nx,
-               max_nz, sh.dtype, pred, L.ptr(out), L.stream_handle())
-        return out
+        return count_launch(sh.x, xo, sh.z, zo, n, max_nx, max_nz, sh.dtype, pred, algo)
 
     if mode == "ne":
         half = _counts_to_host(run(L.TW_PRED_HALF)).astype(object)

@@ -71,22 +71,34 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
       rz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
     }
     __syncthreads();
-    // stage diff = Z[rz] - X[rx] (row-contiguous, coalesced)
-    const int64_t tot = (int64_t)nb * d;
-    for (int64_t e = threadIdx.x; e < tot; e += kBlock) {
-      const int t = (int)(e / d);
-      const int64_t j = e - (int64_t)t * d;
-      diff[e] = Z[rz[t] * d + j] - X[rx[t] * d + j];
-    }
-    __syncthreads();
-    // S_t = diff_t . w + margin ; one wave per pair, lanes over features
-    for (int t = wid; t < nb; t += kBlock / kWave) {
-      double part = 0.0;
-      for (int64_t j = lane; j < d; j += kWave) part += diff[(int64_t)t * d + j] * w[j];
-      part = wave_sum_f64(part);
-      if (lane == 0) {
+    // stage diff rows Z[rz] - X[rx] in LDS and reduce S = diff . w + margin on the way.
+    // Narrow rows (d <= 32): one thread per pair, sequential j (all row loads independent).
+    // Wide rows: one wave per pair, coalesced lane-strided loads + fixed butterfly.
+    if (d <= 32) {
+      for (int t = threadIdx.x; t < nb; t += kBlock) {
+        const double* zr = Z + rz[t] * d;
+        const double* xr = X + rx[t] * d;
+        double* dr = diff + (int64_t)t * d;
+        double part = 0.0;
+        for (int j = 0; j < (int)d; ++j) {
+          const double v = zr[j] - xr[j];
+          dr[j] = v;
+          part += v * w[j];
+        }
         flag[t] = (part + margin) > 0.0;
       }
+    } else for (int t = wid; t < nb; t += kBlock / kWave) {
+      const double* zr = Z + rz[t] * d;
+      const double* xr = X + rx[t] * d;
+      double* dr = diff + (int64_t)t * d;
+      double part = 0.0;
+      for (int64_t j = lane; j < d; j += kWave) {
+        const double v = zr[j] - xr[j];
+        dr[j] = v;
+        part += v * w[j];
+      }
+      part = wave_sum_f64(part);
+      if (lane == 0) flag[t] = (part + margin) > 0.0;
     }
     __syncthreads();
     // column sums over the filtered rows, in row order
@@ -136,7 +148,15 @@ __global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
   for (int64_t j = blockIdx.x * (int64_t)kBlock + threadIdx.x; j < d;
        j += (int64_t)gridDim.x * kBlock) {
     double sum = 0.0;  // np.mean(axis=0): 0.0 + g_0 + g_1 + ... in shard order, then / N
-    for (int s = 0; s < n_shards; ++s) sum += grads[(int64_t)s * d + j];
+    int s = 0;
+    for (; s + 8 <= n_shards; s += 8) {  // 8 independent loads in flight, adds stay in order
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = grads[(int64_t)(s + k) * d + j];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += v[k];
+    }
+    for (; s < n_shards; ++s) sum += grads[(int64_t)s * d + j];
     const double wj = w[j];
     const double g = sum / (double)n_shards + reg * wj;
     const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;

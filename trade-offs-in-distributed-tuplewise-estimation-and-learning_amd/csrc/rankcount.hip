@@ -1,0 +1,222 @@
+// rankcount.hip — exact pair counts by sorting + binary search.
+//
+// Same integers as k_count_complete (the reference's #{x > z}, estimation-experiment/
+// main.py:31; half-units for ties), in O((n+m) log m) per shard instead of O(n m):
+//   #{j : z_j < x} summed over x.
+// Scores become order-preserving u64 keys, which makes NumPy's comparison semantics exact:
+//   float64: -0.0 -> +0.0 (they compare equal), NaN -> 0xFFFF..FF (never below anything);
+//            key = sign ? ~bits : bits | 2^63
+//   int64:   key = v ^ 2^63
+// x-values that are NaN contribute nothing (x > z is false for every z).
+//
+// Kernel 1 (k_sort_chunks): one 1024-thread block per (shard, z-chunk of C <= 16384 keys):
+//   load + key transform into LDS (C*8 <= 128 KiB), pad with the max key, bitonic sort in
+//   LDS, write the sorted chunk to the workspace.
+// Kernel 2 (k_rank_count): one 1024-thread block per (shard, x-tile): for every sorted chunk
+//   of its shard, stage the chunk in LDS and let each thread binary-search its x keys
+//   (log2(C) + 1 dependent ds_read_b64 per x, branchless); u32 -> u64 -> block sum -> one
+//   atomic per block.  Padding keys (max) are never < a non-NaN x key.
+#include "tw_common.h"
+#include <algorithm>
+#include <type_traits>
+
+namespace tw {
+
+constexpr int kSortThreads = 1024;
+constexpr int64_t kMaxChunk = 16384;  // 128 KiB of u64 keys in LDS
+constexpr int kXPerThread = 4;
+
+template <typename T>
+__device__ __forceinline__ uint64_t order_key(T v);
+
+template <>
+__device__ __forceinline__ uint64_t order_key<double>(double v) {
+  if (v != v) return ~0ull;                     // NaN: above everything
+  uint64_t b = (uint64_t)__double_as_longlong(v);
+  if (b == 0x8000000000000000ull) b = 0;        // -0.0 == +0.0
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+template <>
+__device__ __forceinline__ uint64_t order_key<long long>(long long v) {
+  return (uint64_t)v ^ 0x8000000000000000ull;
+}
+
+template <typename T>
+__device__ __forceinline__ bool is_nan_score(T v) {
+  if constexpr (std::is_floating_point<T>::value) return v != v;
+  return false;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restrict__ z,
+                                                              const int64_t* __restrict__ z_off,
+                                                              int chunks, int C,
+                                                              uint64_t* __restrict__ sorted) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+  const int s = blockIdx.x / chunks;
+  const int c = blockIdx.x - s * chunks;
+  const int64_t zb = z_off[s], ze = z_off[s + 1];
+  const int64_t c0 = zb + (int64_t)c * C;
+  for (int i = threadIdx.x; i < C; i += kSortThreads) {
+    const int64_t g = c0 + i;
+    keys[i] = (g < ze) ? order_key<T>(z[g]) : ~0ull;
+  }
+  __syncthreads();
+  if (c0 < ze) {  // block-uniform: an empty chunk stays all-padding
+    for (int k = 2; k <= C; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int p = threadIdx.x; p < (C >> 1); p += kSortThreads) {
+          const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+          const int hi = lo + j;
+          const uint64_t a = keys[lo], b = keys[hi];
+          const bool up = (lo & k) == 0;
+          if ((a > b) == up) {
+            keys[lo] = b;
+            keys[hi] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  uint64_t* dst = sorted + (int64_t)blockIdx.x * C;
+  for (int i = threadIdx.x; i < C; i += kSortThreads) dst[i] = keys[i];
+}
+
+// #{keys < k} in a sorted power-of-two array (branchless).
+__device__ __forceinline__ uint32_t lower_bound_lds(const uint64_t* a, int C, uint64_t k) {
+  uint32_t i = 0;
+  for (int st = C >> 1; st > 0; st >>= 1) i += (a[i + st - 1] < k) ? st : 0;
+  return i + (a[i] < k ? 1 : 0);
+}
+__device__ __forceinline__ uint32_t upper_bound_lds(const uint64_t* a, int C, uint64_t k) {
+  uint32_t i = 0;
+  for (int st = C >> 1; st > 0; st >>= 1) i += (a[i + st - 1] <= k) ? st : 0;
+  return i + (a[i] <= k ? 1 : 0);
+}
+
+template <typename T, int PRED>
+__global__ __launch_bounds__(kSortThreads) void k_rank_count(const T* __restrict__ x,
+                                                             const int64_t* __restrict__ x_off,
+                                                             const uint64_t* __restrict__ sorted,
+                                                             int chunks, int C, int tiles_x,
+                                                             unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+  const int s = blockIdx.x / tiles_x;
+  const int t = blockIdx.x - s * tiles_x;
+  const int64_t xb = x_off[s], xe = x_off[s + 1];
+  const int64_t x0 = xb + (int64_t)t * (kSortThreads * kXPerThread);
+  if (x0 >= xe) return;
+  uint64_t xk[kXPerThread];
+  bool valid[kXPerThread];
+#pragma unroll
+  for (int r = 0; r < kXPerThread; ++r) {
+    const int64_t i = x0 + r * kSortThreads + threadIdx.x;
+    valid[r] = i < xe;
+    const T v = valid[r] ? x[i] : (T)0;
+    valid[r] = valid[r] && !is_nan_score<T>(v);
+    xk[r] = order_key<T>(v);
+  }
+  unsigned long long acc = 0;
+  for (int c = 0; c < chunks; ++c) {
+    const uint64_t* src = sorted + ((int64_t)s * chunks + c) * C;
+    __syncthreads();
+    for (int i = threadIdx.x; i < C; i += kSortThreads) keys[i] = src[i];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kXPerThread; ++r) {
+      if (valid[r]) {
+        uint32_t v = lower_bound_lds(keys, C, xk[r]);
+        if (PRED == TW_PRED_HALF) v += upper_bound_lds(keys, C, xk[r]);
+        acc += v;
+      }
+    }
+  }
+  acc = wave_sum_u64(acc);
+  __shared__ unsigned long long part[kSortThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < kSortThreads / kWave; ++w) b += part[w];
+    if (b) atomicAdd(out + s, b);
+  }
+}
+
+struct RankPlan {
+  int C, chunks, tiles_x;
+};
+inline RankPlan plan_rank(int64_t max_nx, int64_t max_nz) {
+  RankPlan p;
+  int64_t C = 64;
+  while (C < max_nz && C < kMaxChunk) C <<= 1;
+  p.C = (int)C;
+  p.chunks = (int)std::max<int64_t>(1, ceil_div(max_nz, C));
+  p.tiles_x = (int)std::max<int64_t>(1, ceil_div(max_nx, (int64_t)kSortThreads * kXPerThread));
+  return p;
+}
+
+template <typename T>
+int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                int32_t n_shards, int64_t max_nx, int64_t max_nz, int32_t pred, void* work,
+                uint64_t* out, hipStream_t st) {
+  const RankPlan p = plan_rank(max_nx, max_nz);
+  TW_ARG_CHECK((int64_t)n_shards * p.chunks < (1ll << 31) &&
+                   (int64_t)n_shards * p.tiles_x < (1ll << 31),
+               "tw_count_pairs_sorted: grid too large");
+  const size_t lds = sizeof(uint64_t) * p.C;
+  static bool attrs_set = false;  // > 64 KiB of dynamic LDS must be opted into once
+  if (!attrs_set) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_count<T, TW_PRED_GT>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_count<T, TW_PRED_HALF>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    attrs_set = true;
+  }
+  hipLaunchKernelGGL(k_sort_chunks<T>, dim3(n_shards * p.chunks), dim3(kSortThreads), lds, st,
+                     (const T*)z, z_off, p.chunks, p.C, (uint64_t*)work);
+  TW_LAUNCH_CHECK();
+  if (pred == TW_PRED_HALF)
+    hipLaunchKernelGGL((k_rank_count<T, TW_PRED_HALF>), dim3(n_shards * p.tiles_x),
+                       dim3(kSortThreads), lds, st, (const T*)x, x_off, (const uint64_t*)work,
+                       p.chunks, p.C, p.tiles_x, (unsigned long long*)out);
+  else
+    hipLaunchKernelGGL((k_rank_count<T, TW_PRED_GT>), dim3(n_shards * p.tiles_x),
+                       dim3(kSortThreads), lds, st, (const T*)x, x_off, (const uint64_t*)work,
+                       p.chunks, p.C, p.tiles_x, (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+}  // namespace tw
+
+using namespace tw;
+
+extern "C" int64_t tw_count_pairs_sorted_work_bytes(int32_t n_shards, int64_t max_nz) {
+  const RankPlan p = plan_rank(1, std::max<int64_t>(1, max_nz));
+  return (int64_t)n_shards * p.chunks * p.C * (int64_t)sizeof(uint64_t);
+}
+
+extern "C" int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                     const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                     int64_t max_nz, int32_t dtype, int32_t pred, void* d_work,
+                                     uint64_t* d_out, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && max_nx >= 0 && max_nz >= 0, "tw_count_pairs_sorted: bad sizes");
+  TW_ARG_CHECK(pred == TW_PRED_GT || pred == TW_PRED_HALF,
+               "tw_count_pairs_sorted: predicate must be TW_PRED_GT or TW_PRED_HALF");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_shards == 0) return TW_OK;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  if (max_nx == 0 || max_nz == 0) return TW_OK;
+  if (dtype == TW_F64) return launch_rank<double>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, pred, d_work, d_out, st);
+  if (dtype == TW_I64) return launch_rank<long long>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, pred, d_work, d_out, st);
+  set_error("tw_count_pairs_sorted: unknown dtype %d", dtype);
+  return TW_ERR_ARG;
+}

@@ -76,12 +76,10 @@ class HipOps:
                L.stream_handle())
         return out
 
-    def count(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred):
-        out = L.empty((n_shards,), self.t.int64)
-        L.call("tw_count_pairs", L.ptr(x), L.ptr(x_off_dev), L.ptr(z), L.ptr(z_off_dev),
-               int(n_shards), int(max_nx), int(max_nz), int(dtype), int(pred), L.ptr(out),
-               L.stream_handle())
-        return out
+    def count(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred,
+              algo="pairs"):
+        return E.count_launch(x, x_off_dev, z, z_off_dev, int(n_shards), int(max_nx),
+                              int(max_nz), int(dtype), int(pred), algo)
 
     def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred):
         out = L.empty((n_shards,), self.t.int64)
@@ -99,9 +97,12 @@ class ShardedSample:
 
     X, Z: this rank's 1-D tensors (float64 or int64; all ranks the same sizes and dtype).
     group: a torch.distributed process group (None = single process).
-    tie_mode: "strict" (reference) or "half" (ties score 1/2)."""
+    tie_mode: "strict" (reference) or "half" (ties score 1/2).
+    algo: "pairs" (all-pairs compare kernel), "sorted" (sort + binary search, same integers),
+    "auto" (sorted for large shards)."""
 
-    def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None):
+    def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None,
+                 algo: str = "auto"):
         self.ops = ops if ops is not None else HipOps()
         t = L.torch()
         self.t = t
@@ -134,6 +135,7 @@ class ShardedSample:
         self.max_nx = int(np.diff(x_off).max()) if N else 0
         self.max_nz = int(np.diff(z_off).max()) if N else 0
         self.pairs = np.diff(x_off).astype(object) * np.diff(z_off).astype(object)
+        self.algo = E.pick_algo(algo, self.max_nx, self.max_nz, "gt")
 
     # ------------------------------------------------------------------ repartition
     def _permute_global(self, A, n_loc, key):
@@ -164,7 +166,7 @@ class ShardedSample:
     def local_counts(self):
         """Per-local-shard exact counts (int64 device tensor; uint64 semantics)."""
         return self.ops.count(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
-                              self.max_nx, self.max_nz, self.dtype, self.pred)
+                              self.max_nx, self.max_nz, self.dtype, self.pred, algo=self.algo)
 
     def global_counts(self, local):
         """All G*N shard counts, in global shard order, on every rank (one all-reduce)."""
