@@ -182,6 +182,28 @@ def main():
                      if isinstance(v, (int, float)) and not isinstance(v, bool)}
     meta["learn"]["seed"] = 2024
 
+    # ---------------------------------------------------------------- 7. data preprocessing
+    # load_preprocess_data (make_exps.py:51-93) on a synthetic shuttle-like pickle written to
+    # a temp dir (the real dataset is a download, absent offline).  Written by us, read by the
+    # reference: no reference-shipped file is unpickled.
+    import pickle
+    import tempfile
+    pre_X = np.round(rng.normal(size=(1530, 9)) * 10, 1)
+    pre_y = np.where(rng.rand(1530) < 0.08, 1, -1)
+    with tempfile.TemporaryDirectory() as td:
+        cwd = os.getcwd()
+        os.chdir(td)
+        try:
+            with open("shuttle.pickle", "wb") as fh:
+                pickle.dump({"X": pre_X, "y": pre_y}, fh)
+            Zt, Xt, Zs, Xs = me.load_preprocess_data()
+        finally:
+            os.chdir(cwd)
+    put("pre/X", pre_X)
+    put("pre/y", pre_y)
+    for k, v in (("Z_train", Zt), ("X_train", Xt), ("Z_test", Zs), ("X_test", Xs)):
+        put(f"pre/{k}", v)
+
     # ---------------------------------------------------------------- 6. RNG stream KAT
     np.random.seed(9)
     put("rng/randint_seed9", np.random.randint(0, 1000, 64))

@@ -96,3 +96,27 @@ def test_device_rng_graphs_equal_eager(gpu, golden):
                             graphs=graphs)
         out.append((p["norm_w"], p["bc_AUC"]))
     assert out[0] == out[1]
+
+
+def test_make_exps_writes_reference_schema(gpu, golden, tmp_path):
+    """make_exps (make_exps.py:192-243): dynamics.json keys/lengths and the log file."""
+    import json
+    import tuplewise.learning as lr
+    p = {"n_it": 60, "margin": 1, "N": 10, "B": 20, "reshuffle_mod": 5, "reg": 0.05,
+         "learning_rate": 0.01, "eval_mod": 25, "w_init": np.random.normal(0, 1, (10, 1)),
+         "test_X": golden["learn/test_X"], "test_Z": golden["learn/test_Z"]}
+    out = tmp_path / "run_00"
+    logging.disable(logging.NOTSET)
+    for h in logging.root.handlers[:]:
+        logging.root.removeHandler(h)
+    lr.make_exps(5, str(out), p, data={"X": golden["pre/X"], "y": golden["pre/y"]})
+    dyn = json.loads((out / "dynamics.json").read_text())
+    for k in ("n_it", "margin", "N", "B", "reshuffle_mod", "reg", "learning_rate", "eval_mod",
+              "iter", "norm_w", "bc_AUC", "br_AUC", "tr_AUC", "tc_AUC"):
+        assert k in dyn, k
+    assert dyn["iter"] == [0, 25, 50]
+    assert not any(k.startswith(("train_", "test_", "w_")) for k in dyn)
+    log = (out / "learning_process.log").read_text()
+    assert "it     0: bc_AUC = " in log and "#X: " in log
+    for h in logging.root.handlers[:]:
+        logging.root.removeHandler(h)

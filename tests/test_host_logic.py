@@ -102,3 +102,20 @@ def test_block_planner_rng_order(tw, st, variant):
     probe_got = np.random.randint(0, 2 ** 31 - 1)
     assert got == want and probe_got == probe_want
     assert np.array_equal(X1, X2) and np.array_equal(Z1, Z2)
+
+
+def test_load_preprocess_data_matches_reference(tw, golden):
+    """make_exps.py:51-93 incl. the `~ind` train-split quirk, vs the reference's own output."""
+    import tuplewise.learning as lr
+    out = lr.load_preprocess_data({"X": golden["pre/X"], "y": golden["pre/y"]})
+    for got, k in zip(out, ("Z_train", "X_train", "Z_test", "X_test")):
+        assert np.array_equal(got, golden[f"pre/{k}"]), k
+
+
+def test_load_preprocess_constant_column_raises(tw):
+    import tuplewise.learning as lr
+    X = np.ones((100, 3))
+    X[:, 1] = np.arange(100)
+    y = np.where(np.arange(100) % 10 == 0, 1, -1)
+    with pytest.raises(ValueError, match="constant var"):
+        lr.load_preprocess_data({"X": X, "y": y})

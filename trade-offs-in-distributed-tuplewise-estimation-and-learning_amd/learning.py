@@ -324,3 +324,95 @@ def evaluation_step(i, X_s, Z_s, w, p_learn):
 # convenience re-export for drivers that import SWR_divide / UN_split from here
 SWR_divide = cs.SWR_divide
 ShardList = _learn.ShardList
+
+
+# ------------------------------------------------------------------ driver I/O (make_exps.py)
+def load_preprocess_data(data=None):
+    """Loads and preprocesses the data.  (make_exps.py:51-93)
+
+    data: a dict with "X" (n, d) and "y" (n,) in {-1, +1} (the shuttle pickle's content);
+    None reads "shuttle.pickle" from the working directory like the reference (the user's own
+    file, produced by convert_data_to_pickle).  Reproduces the reference exactly, including
+    its train split `X_tot[~ind_X_test]`: `~` on an int index array is -(i+1), so "train" is
+    a same-size sample taken from the other end, not the complement of the test indices."""
+    if data is None:
+        import pickle
+        with open("shuttle.pickle", "rb") as fh:
+            data = pickle.load(fh)
+    X = data["X"]
+    y = data["y"]
+    Z_tot = X[y == +1]  # Minority class is the anomaly class, i.e. y = +1
+    X_tot = X[y == -1]
+
+    np.random.seed(SEED_SHUFFLE)
+    ind_X_test = np.random.choice(X_tot.shape[0], size=int(PROP_TEST * X_tot.shape[0]),
+                                  replace=False)
+    ind_Z_test = np.random.choice(Z_tot.shape[0], size=int(PROP_TEST * Z_tot.shape[0]),
+                                  replace=False)
+    np.random.seed()
+    Z_train, X_train = Z_tot[~ind_Z_test], X_tot[~ind_X_test]
+    Z_test, X_test = Z_tot[ind_Z_test], X_tot[ind_X_test]
+    train_tot = np.vstack([X_train, Z_train])
+
+    train_mean = train_tot.mean(axis=0)
+    train_std = train_tot.std(axis=0)
+    if np.min(train_std) == 0:
+        raise ValueError("One of the columns in the data has constant var.")
+
+    X_train = (X_train - train_mean) / train_std
+    Z_train = (Z_train - train_mean) / train_std
+    X_test = (X_test - train_mean) / train_std
+    Z_test = (Z_test - train_mean) / train_std
+
+    def add_constant(a):
+        return np.hstack([a, np.ones((a.shape[0], 1))])
+
+    return (add_constant(Z_train), add_constant(X_train), add_constant(Z_test),
+            add_constant(X_test))
+
+
+def make_exps(reshuffle_mod, out_folder="exps/test", p_learn=None, data=None,
+              rng_mode="replay"):
+    """Make the experiments for the desired parameters.  (make_exps.py:192-243, without the
+    plots): writes <out_folder>/learning_process.log and <out_folder>/dynamics.json with the
+    reference's schema (scalar parameters + the iter/norm_w/bc_AUC/br_AUC/tr_AUC/tc_AUC
+    lists).  Returns p_learn."""
+    import json
+    import os
+    import shutil
+    if not os.path.exists(out_folder):
+        os.makedirs(out_folder)
+        shutil.copy(__file__, "{}/executed_script.py".format(out_folder))
+
+    Z_train, X_train, Z_test, X_test = load_preprocess_data(data)
+    n_feats = Z_train.shape[1]
+
+    logging.basicConfig(filename='{}/learning_process.log'.format(out_folder),
+                        format='%(asctime)s - %(message)s',
+                        level=logging.INFO, datefmt='%m/%d/%y %I:%M:%S %p', filemode="w")
+
+    if p_learn is None:
+        p_learn = {"n_it": DEFAULT_ITE_NUMBER, "margin": 1, "N": 100,
+                   "B": 100, "reshuffle_mod": reshuffle_mod, "reg": 0.05,
+                   "learning_rate": 0.01, "eval_mod": 25,
+                   "w_init": np.random.normal(0, 1, (n_feats, 1)),
+                   "test_X": X_test, "test_Z": Z_test}
+
+    if TYPE_TRAIN_MONITOR == "FIXED_PAIRS":
+        np.random.seed(SEED_TRAIN_MONITOR)
+        p_learn["train_mon_pairs"] = list(zip(
+            list(np.random.randint(0, X_train.shape[0], SIZE_TRAIN_MONITOR)),
+            list(np.random.randint(0, Z_train.shape[0], SIZE_TRAIN_MONITOR))))
+        p_learn["train_X"] = X_train
+        p_learn["train_Z"] = Z_train
+        np.random.seed()
+
+    print("Started optimization")
+    learning_process(X_train, Z_train, p_learn, rng_mode=rng_mode)
+    print("Finished optimization")
+
+    for x in [k for k in p_learn if k.startswith(("train_", "test_", "w_"))]:
+        p_learn.pop(x)
+    with open("{}/dynamics.json".format(out_folder), "wt") as fh:
+        json.dump(p_learn, fh)
+    return p_learn
