@@ -135,7 +135,9 @@ int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t
 
 /* ---- Row L1/A9, device-RNG mode (no host RNG in the loop; graph-capturable) -----------
  * Draws are Philox4x32-10(key = seed, counter = (index, shard, step lo, tag | step hi)) with
- * step = *d_step (device memory, advanced by tw_sgd_update), mapped by 64-bit multiply-high:
+ * step = *d_step (device memory, advanced by tw_sgd_update), mapped by 64-bit multiply-high;
+ * the shard word is shard_base + local shard, so draws follow GLOBAL shard indices and a
+ * run spread over ranks draws exactly what a single GPU draws:
  * tw_hinge_grad_rng: pair b of shard s -> (ix, iz) in [0,kx) x [0,kz) (tag 0x80000000);
  * tw_swr_rows_rng:   d_rows[s*k + t] in [0, n), side 0 = X rows (tag 0x40000000), 1 = Z rows
  *                    (tag 0x20000000) — SWR_divide (compute_stats.py:48-54) on the device.
@@ -144,9 +146,9 @@ int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t
 int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
                       int64_t kx, const int64_t* d_rows_z, int64_t kz, int32_t n_shards,
                       int64_t B, const double* d_w, double margin, uint64_t seed,
-                      const uint64_t* d_step, double* d_out, void* stream);
+                      const uint64_t* d_step, int32_t shard_base, double* d_out, void* stream);
 int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n, uint64_t seed,
-                    const uint64_t* d_step, int32_t side, void* stream);
+                    const uint64_t* d_step, int32_t side, int32_t shard_base, void* stream);
 
 /* ---- Row L2: update of learning_process (make_exps.py:130-141) ------------------------
  * g = mean_s(d_grads[s]) + reg * w  (shards summed in order, then / n_shards — np.mean axis 0)

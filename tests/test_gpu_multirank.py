@@ -1,0 +1,112 @@
+"""Multi-rank paths with the real HIP kernels: 2 processes on the box's one GPU, gloo
+(RCCL needs distinct devices; the 8-GPU RCCL run is the driver's scaling bench).  Checks that
+sharding over ranks changes nothing: trajectories and estimates equal the 1-process ones."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _learn_worker(rank, port, G, mode, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    torch.cuda.set_device(0)
+    import tuplewise.learning as lr
+    X, Z, w0, p = _problem()
+    traj = []
+    np.random.seed(99)
+    lr.learning_process(X, Z, p, rng_mode=mode, trajectory=traj, group=dist.group.WORLD)
+    if rank == 0:
+        q.put(np.stack(traj))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _problem():
+    rng = np.random.RandomState(0)
+    X = np.hstack([rng.normal(size=(400, 7)), np.ones((400, 1))])
+    Z = np.hstack([rng.normal(0.5, 1, size=(90, 7)), np.ones((90, 1))])
+    w0 = rng.normal(size=(8, 1))
+    tX = np.hstack([rng.normal(size=(50, 7)), np.ones((50, 1))])
+    tZ = np.hstack([rng.normal(0.5, 1, size=(20, 7)), np.ones((20, 1))])
+    mon = [(int(a), int(b)) for a, b in zip(rng.randint(0, 400, 300), rng.randint(0, 90, 300))]
+    p = {"n_it": 40, "margin": 1, "N": 8, "B": 16, "reshuffle_mod": 5, "reg": 0.05,
+         "learning_rate": 0.01, "eval_mod": 1000, "w_init": w0, "test_X": tX, "test_Z": tZ,
+         "train_mon_pairs": mon, "train_X": X, "train_Z": Z}
+    return X, Z, w0, p
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_learning_two_ranks_equals_one(gpu, mode):
+    import torch.multiprocessing as mp
+    import tuplewise.learning as lr
+    X, Z, w0, p = _problem()
+    ref = []
+    np.random.seed(99)
+    lr.learning_process(X, Z, p, rng_mode=mode, trajectory=ref)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_learn_worker, args=(r, port, 2, mode, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert np.array_equal(got, np.stack(ref))
+
+
+def _est_worker(rank, port, G, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    torch.cuda.set_device(0)
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(3)
+    n_loc, N = 40_000, 8
+    X = rng.normal(0.3, 1, G * n_loc)
+    Z = rng.normal(0, 1, G * n_loc)
+    S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(),
+                      torch.from_numpy(Z[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(), N,
+                      group=dist.group.WORLD)
+    vals = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
+    if rank == 0:
+        q.put(vals)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_sample_two_ranks_equals_one(gpu):
+    import torch
+    import torch.multiprocessing as mp
+    from tuplewise.device import ShardedSample
+    G, n_loc, N = 2, 40_000, 8
+    rng = np.random.RandomState(3)
+    X = rng.normal(0.3, 1, G * n_loc)
+    Z = rng.normal(0, 1, G * n_loc)
+    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), G * N)
+    want = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q)) for r in range(G)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert got == want

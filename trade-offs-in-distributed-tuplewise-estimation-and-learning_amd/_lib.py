@@ -40,8 +40,8 @@ _SIGNATURES = {
     "tw_hinge_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64,
                       _vp, _vp],
     "tw_hinge_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _u64,
-                          _vp, _vp, _vp],
-    "tw_swr_rows_rng": [_vp, _i32, _i64, _i64, _u64, _vp, _i32, _vp],
+                          _vp, _i32, _vp, _vp],
+    "tw_swr_rows_rng": [_vp, _i32, _i64, _i64, _u64, _vp, _i32, _i32, _vp],
     "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
     "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],

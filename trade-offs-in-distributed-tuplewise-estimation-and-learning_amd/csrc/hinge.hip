@@ -22,7 +22,9 @@
 namespace tw {
 
 constexpr int kLdsDoubles = 8192;  // 64 KiB of diff rows per block
-constexpr int kMaxColsPerThread = 16;  // d <= 4096
+constexpr int kMaxColsPerThread = 16;  // d <= 16 * block size
+constexpr int kWideBlock = 1024;      // d > 32: 16 waves = 16 diff rows in flight per CU
+constexpr int kMaxD = 4096;
 
 // Device-RNG mode counters: Philox4x32-10 keyed by the run's seed; counter words
 // (index, shard, step lo, tag | step hi).  Tags separate the three draw streams.
@@ -34,12 +36,13 @@ __device__ __forceinline__ u32x4 sgd_draw(uint64_t seed, uint64_t step, uint32_t
                        (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-__global__ __launch_bounds__(kBlock) void k_hinge_grad(
+template <int BS>
+__global__ __launch_bounds__(BS) void k_hinge_grad(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     int CH, const double* __restrict__ w, double margin, double* __restrict__ out,
-    uint64_t seed, const uint64_t* __restrict__ d_step) {
+    uint64_t seed, const uint64_t* __restrict__ d_step, uint32_t shard_base) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* diff = (double*)smem;                             // CH * d
   int64_t* rx = (int64_t*)(smem + sizeof(double) * CH * d);  // CH
@@ -56,14 +59,15 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
   for (int64_t b0 = 0; b0 < B; b0 += CH) {
     const int nb = (int)std::min<int64_t>(CH, B - b0);
     // rows of this chunk: compose the SWR shard draw with the per-step pair draw
-    for (int t = threadIdx.x; t < nb; t += kBlock) {
+    for (int t = threadIdx.x; t < nb; t += BS) {
       const int64_t p = (int64_t)s * B + b0 + t;
       int64_t ax, az;
       if (ix) {  // replay: NumPy's randint draws
         ax = ix[p];
         az = iz[p];
       } else {  // device RNG
-        const u32x4 r = sgd_draw(seed, step, (uint32_t)(b0 + t), (uint32_t)s, kTagPairs);
+        const u32x4 r = sgd_draw(seed, step, (uint32_t)(b0 + t), shard_base + (uint32_t)s,
+                                  kTagPairs);
         ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
         az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
       }
@@ -75,11 +79,12 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
     // Narrow rows (d <= 32): one thread per pair, sequential j (all row loads independent).
     // Wide rows: one wave per pair, coalesced lane-strided loads + fixed butterfly.
     if (d <= 32) {
-      for (int t = threadIdx.x; t < nb; t += kBlock) {
+      for (int t = threadIdx.x; t < nb; t += BS) {
         const double* zr = Z + rz[t] * d;
         const double* xr = X + rx[t] * d;
         double* dr = diff + (int64_t)t * d;
         double part = 0.0;
+#pragma unroll 4
         for (int j = 0; j < (int)d; ++j) {
           const double v = zr[j] - xr[j];
           dr[j] = v;
@@ -87,15 +92,29 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
         }
         flag[t] = (part + margin) > 0.0;
       }
-    } else for (int t = wid; t < nb; t += kBlock / kWave) {
+    } else for (int t = wid; t < nb; t += BS / kWave) {
       const double* zr = Z + rz[t] * d;
       const double* xr = X + rx[t] * d;
       double* dr = diff + (int64_t)t * d;
       double part = 0.0;
-      for (int64_t j = lane; j < d; j += kWave) {
-        const double v = zr[j] - xr[j];
-        dr[j] = v;
-        part += v * w[j];
+      // batches of 8 lane-strided columns: all 16 row loads in flight before the first use
+      for (int64_t j0 = lane; j0 < d; j0 += 8 * kWave) {
+        double zv[8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t j = j0 + u * kWave;
+          zv[u] = j < d ? zr[j] : 0.0;
+          xv[u] = j < d ? xr[j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t j = j0 + u * kWave;
+          if (j < d) {
+            const double v = zv[u] - xv[u];
+            dr[j] = v;
+            part += v * w[j];
+          }
+        }
       }
       part = wave_sum_f64(part);
       if (lane == 0) flag[t] = (part + margin) > 0.0;
@@ -104,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
     // column sums over the filtered rows, in row order
 #pragma unroll
     for (int q = 0; q < kMaxColsPerThread; ++q) {
-      const int64_t j = threadIdx.x + (int64_t)q * kBlock;
+      const int64_t j = threadIdx.x + (int64_t)q * BS;
       if (j < d) {
         double a = acc[q];
         for (int t = 0; t < nb; ++t)
@@ -116,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
   }
 #pragma unroll
   for (int q = 0; q < kMaxColsPerThread; ++q) {
-    const int64_t j = threadIdx.x + (int64_t)q * kBlock;
+    const int64_t j = threadIdx.x + (int64_t)q * BS;
     if (j < d) out[(int64_t)s * d + j] = acc[q] / (double)B;
   }
 }
@@ -125,38 +144,47 @@ __global__ __launch_bounds__(kBlock) void k_hinge_grad(
 __global__ __launch_bounds__(kBlock) void k_swr_rows(int64_t* __restrict__ rows, int n_shards,
                                                      int64_t k, int64_t n, uint64_t seed,
                                                      const uint64_t* __restrict__ d_step,
-                                                     uint32_t tag) {
+                                                     uint32_t tag, uint32_t shard_base) {
   const uint64_t step = *d_step;
   const int64_t total = (int64_t)n_shards * k;
   for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * kBlock) {
     const int64_t s = e / k, t = e - s * k;
-    const u32x4 r = sgd_draw(seed, step, (uint32_t)t, (uint32_t)s, tag);
+    const u32x4 r = sgd_draw(seed, step, (uint32_t)t, shard_base + (uint32_t)s, tag);
     rows[e] = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)n);
   }
 }
 
 // g = (sum_s grads[s]) / N + reg*w ; dw = momentum*dw + lr*g (SGD: dw = lr*g) ; w = w - dw
 // d_step (optional): the device-RNG step counter, advanced once per update.
+// One block per kUpdCols columns: shard rows are staged in LDS (coalesced), then one thread
+// per column adds them in shard order — the sequential order of np.mean(axis=0).
+constexpr int kUpdCols = 16;
+constexpr int kUpdRows = 512;  // shard rows staged per pass: 512 x 16 doubles = 64 KiB
 __global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
                                                        double* __restrict__ dw,
                                                        const double* __restrict__ grads,
                                                        int n_shards, int64_t d, double reg,
                                                        double lr, double momentum,
                                                        uint64_t* __restrict__ d_step) {
+  __shared__ double tile[kUpdRows * kUpdCols];
   if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += 1;
-  for (int64_t j = blockIdx.x * (int64_t)kBlock + threadIdx.x; j < d;
-       j += (int64_t)gridDim.x * kBlock) {
-    double sum = 0.0;  // np.mean(axis=0): 0.0 + g_0 + g_1 + ... in shard order, then / N
-    int s = 0;
-    for (; s + 8 <= n_shards; s += 8) {  // 8 independent loads in flight, adds stay in order
-      double v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = grads[(int64_t)(s + k) * d + j];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sum += v[k];
+  const int64_t j0 = (int64_t)blockIdx.x * kUpdCols;
+  const int nc = (int)std::min<int64_t>(kUpdCols, d - j0);
+  double sum = 0.0;  // thread c < nc: 0.0 + g_0 + g_1 + ... in shard order
+  for (int s0 = 0; s0 < n_shards; s0 += kUpdRows) {
+    const int ns = std::min(kUpdRows, n_shards - s0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * kUpdCols; e += kBlock) {
+      const int r = e / kUpdCols, c = e - r * kUpdCols;
+      tile[e] = c < nc ? grads[(int64_t)(s0 + r) * d + j0 + c] : 0.0;
     }
-    for (; s < n_shards; ++s) sum += grads[(int64_t)s * d + j];
+    __syncthreads();
+    if (threadIdx.x < nc)
+      for (int r = 0; r < ns; ++r) sum += tile[r * kUpdCols + threadIdx.x];
+  }
+  if (threadIdx.x < nc) {
+    const int64_t j = j0 + threadIdx.x;
     const double wj = w[j];
     const double g = sum / (double)n_shards + reg * wj;
     const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
@@ -177,6 +205,24 @@ __global__ __launch_bounds__(kBlock) void k_gemv(const double* __restrict__ A, i
   }
 }
 
+int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* rows_x, int64_t kx,
+                 const int64_t* rows_z, int64_t kz, const int64_t* ix, const int64_t* iz,
+                 int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
+                 const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st) {
+  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
+  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
+  if (d <= 32)
+    hipLaunchKernelGGL(k_hinge_grad<kBlock>, dim3(n_shards), dim3(kBlock), lds, st, X, Z, d,
+                       rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
+                       shard_base);
+  else
+    hipLaunchKernelGGL(k_hinge_grad<kWideBlock>, dim3(n_shards), dim3(kWideBlock), lds, st, X, Z,
+                       d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
+                       shard_base);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 }  // namespace tw
 
 using namespace tw;
@@ -186,45 +232,35 @@ extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
                              int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
                              int32_t n_shards, int64_t B, const double* d_w, double margin,
                              double* d_out, void* stream) {
-  TW_ARG_CHECK(d >= 1 && d <= (int64_t)kBlock * kMaxColsPerThread,
-               "tw_hinge_grad: d=%lld outside [1, %d]", (long long)d, kBlock * kMaxColsPerThread);
+  TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_hinge_grad: d=%lld outside [1, %d]", (long long)d, kMaxD);
   TW_ARG_CHECK(n_shards >= 0 && B >= 1, "tw_hinge_grad: bad n_shards/B");
   if (n_shards == 0) return TW_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
-  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
   TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_hinge_grad: pair indices required");
-  hipLaunchKernelGGL(k_hinge_grad, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x,
-                     kx, d_rows_z, kz, d_ix, d_iz, B, CH, d_w, margin, d_out, (uint64_t)0,
-                     (const uint64_t*)nullptr);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+  return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
+                      margin, 0, nullptr, 0, d_out, st);
 }
 
 extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,
                                  const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
                                  int64_t kz, int32_t n_shards, int64_t B, const double* d_w,
                                  double margin, uint64_t seed, const uint64_t* d_step,
-                                 double* d_out, void* stream) {
-  TW_ARG_CHECK(d >= 1 && d <= (int64_t)kBlock * kMaxColsPerThread,
-               "tw_hinge_grad_rng: d=%lld outside [1, %d]", (long long)d, kBlock * kMaxColsPerThread);
+                                 int32_t shard_base, double* d_out, void* stream) {
+  TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_hinge_grad_rng: d=%lld outside [1, %d]", (long long)d,
+               kMaxD);
   TW_ARG_CHECK(n_shards >= 0 && B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1,
                "tw_hinge_grad_rng: bad n_shards/B/kx/kz");
   TW_ARG_CHECK(d_step != nullptr, "tw_hinge_grad_rng: step counter required");
   if (n_shards == 0) return TW_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
-  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
-  hipLaunchKernelGGL(k_hinge_grad, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x,
-                     kx, d_rows_z, kz, (const int64_t*)nullptr, (const int64_t*)nullptr, B, CH,
-                     d_w, margin, d_out, seed, d_step);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+  TW_ARG_CHECK(shard_base >= 0, "tw_hinge_grad_rng: shard_base < 0");
+  return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, nullptr, nullptr, n_shards, B,
+                      d_w, margin, seed, d_step, (uint32_t)shard_base, d_out, st);
 }
 
 extern "C" int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n,
                                uint64_t seed, const uint64_t* d_step, int32_t side,
-                               void* stream) {
+                               int32_t shard_base, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && k >= 0 && n >= 1 && k < (1ll << 32) && d_step != nullptr,
                "tw_swr_rows_rng: bad sizes");
   TW_ARG_CHECK(side == 0 || side == 1, "tw_swr_rows_rng: side must be 0 (X) or 1 (Z)");
@@ -232,7 +268,8 @@ extern "C" int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int
   if (total == 0) return TW_OK;
   const int blocks = (int)std::min<int64_t>(256 * 8, ceil_div(total, kBlock));
   hipLaunchKernelGGL(k_swr_rows, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, d_rows,
-                     (int)n_shards, k, n, seed, d_step, side == 0 ? kTagRowsX : kTagRowsZ);
+                     (int)n_shards, k, n, seed, d_step, side == 0 ? kTagRowsX : kTagRowsZ,
+                     (uint32_t)shard_base);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -242,7 +279,7 @@ extern "C" int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, i
                              void* stream) {
   TW_ARG_CHECK(n_shards >= 1 && d >= 1, "tw_sgd_update: bad sizes");
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (int)std::min<int64_t>(1024, ceil_div(d, kBlock));
+  const int blocks = (int)ceil_div(d, kUpdCols);
   hipLaunchKernelGGL(k_sgd_update, dim3(blocks), dim3(kBlock), 0, st, d_w, d_dw, d_grads,
                      n_shards, d, reg, lr, momentum, d_step);
   TW_LAUNCH_CHECK();

@@ -35,12 +35,29 @@ DEFAULT_ITE_NUMBER = 5000
 
 
 class SGDEngine:
-    """Device-resident pairwise-hinge SGD state for one learning_process run."""
+    """Device-resident pairwise-hinge SGD state for one learning_process run.
 
-    def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type):
+    Multi-GPU (group = a torch.distributed process group, one process per GPU): X and Z are
+    replicated (n x d fp64 fits every MI355X's 288 GB up to n*d ~ 3e10), rank r owns shards
+    [r*N/G, (r+1)*N/G); each step computes its shards' gradients, all-gathers the (N/G, d)
+    partials in shard order (one RCCL all-gather) and applies the same shard-ordered update
+    on every rank — so w, and the whole trajectory, is identical for any G."""
+
+    def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None):
         """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is)."""
         t = L.torch()
         self.t = t
+        self.group = group
+        if group is not None:
+            import torch.distributed as dist
+            self.dist = dist
+            self.G, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        else:
+            self.dist, self.G, self.rank = None, 1, 0
+        if int(N) % self.G:
+            raise ValueError(f"N={N} shards do not split evenly over {self.G} ranks")
+        self.N_loc = int(N) // self.G
+        self.shard_base = self.rank * self.N_loc
         self.X = _dev_f64(X)
         self.Z = _dev_f64(Z)
         self.n_X, self.d = self.X.shape
@@ -52,21 +69,33 @@ class SGDEngine:
         self.w_shape = tuple(w_init.shape)
         self.w = _dev_f64(w_init).reshape(-1).clone()
         self.dw = t.zeros_like(self.w)
-        self.grads = L.empty((self.N, self.d), t.float64)
+        self.grads = L.empty((self.N, self.d), t.float64)  # all shards, global order
+        self.grads_loc = self.grads if self.G == 1 else L.empty((self.N_loc, self.d), t.float64)
         self.rows_x = self.rows_z = None
+        self.step_ctr = None
+
+    def _local(self, a):
+        return a[self.shard_base:self.shard_base + self.N_loc]
 
     def set_shards(self, rows_x, rows_z):
-        self.rows_x = L.to_device(np.stack(rows_x).astype(np.int64))
-        self.rows_z = L.to_device(np.stack(rows_z).astype(np.int64))
+        """Replay mode: the full SWR draw (all N shards; identical on every rank)."""
+        self.rows_x = L.to_device(np.stack(self._local(rows_x)).astype(np.int64))
+        self.rows_z = L.to_device(np.stack(self._local(rows_z)).astype(np.int64))
+
+    def _update(self):
+        s = L.stream_handle()
+        if self.G > 1:
+            self.dist.all_gather_into_tensor(self.grads, self.grads_loc, group=self.group)
+        L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
+               self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr), s)
 
     def step(self, ix: np.ndarray, iz: np.ndarray):
-        ixd, izd = L.to_device(ix), L.to_device(iz)
-        s = L.stream_handle()
+        """Replay mode: ix, iz are the (N, B) NumPy draws of every shard."""
+        ixd, izd = L.to_device(self._local(ix)), L.to_device(self._local(iz))
         L.call("tw_hinge_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x), self.kx,
-               L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N, self.B,
-               L.ptr(self.w), self.margin, L.ptr(self.grads), s)
-        L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
-               self.d, self.reg, self.lr, self.momentum, None, s)
+               L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N_loc, self.B,
+               L.ptr(self.w), self.margin, L.ptr(self.grads_loc), L.stream_handle())
+        self._update()
 
     def w_host(self) -> np.ndarray:
         return self.w.cpu().numpy().reshape(self.w_shape)
@@ -79,29 +108,28 @@ class SGDEngine:
         t = self.t
         self.seed = int(seed) & (2 ** 64 - 1)
         self.step_ctr = t.zeros((1,), dtype=t.int64, device=self.w.device)
-        self.rows_x = t.empty((self.N, self.kx), dtype=t.int64, device=self.w.device)
-        self.rows_z = t.empty((self.N, self.kz), dtype=t.int64, device=self.w.device)
+        self.rows_x = t.empty((self.N_loc, self.kx), dtype=t.int64, device=self.w.device)
+        self.rows_z = t.empty((self.N_loc, self.kz), dtype=t.int64, device=self.w.device)
         self._graphs = {}
 
     def reshuffle_device(self):
         s = L.stream_handle()
-        L.call("tw_swr_rows_rng", L.ptr(self.rows_x), self.N, self.kx, self.n_X, self.seed,
-               L.ptr(self.step_ctr), 0, s)
-        L.call("tw_swr_rows_rng", L.ptr(self.rows_z), self.N, self.kz, self.n_Z, self.seed,
-               L.ptr(self.step_ctr), 1, s)
+        L.call("tw_swr_rows_rng", L.ptr(self.rows_x), self.N_loc, self.kx, self.n_X, self.seed,
+               L.ptr(self.step_ctr), 0, self.shard_base, s)
+        L.call("tw_swr_rows_rng", L.ptr(self.rows_z), self.N_loc, self.kz, self.n_Z, self.seed,
+               L.ptr(self.step_ctr), 1, self.shard_base, s)
 
     def step_device(self):
-        s = L.stream_handle()
         L.call("tw_hinge_grad_rng", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
-               self.kx, L.ptr(self.rows_z), self.kz, self.N, self.B, L.ptr(self.w), self.margin,
-               self.seed, L.ptr(self.step_ctr), L.ptr(self.grads), s)
-        L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
-               self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr), s)
+               self.kx, L.ptr(self.rows_z), self.kz, self.N_loc, self.B, L.ptr(self.w),
+               self.margin, self.seed, L.ptr(self.step_ctr), self.shard_base,
+               L.ptr(self.grads_loc), L.stream_handle())
+        self._update()
 
     def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True):
         """nsteps device-RNG steps (reshuffling first if asked), replayed from a captured
-        hipGraph per distinct segment shape."""
-        if not graphs:
+        hipGraph per distinct segment shape (eager when the step holds a collective)."""
+        if not graphs or self.G > 1:
             if reshuffle_first:
                 self.reshuffle_device()
             for _ in range(nsteps):
@@ -153,13 +181,16 @@ def _pair_draws(N, kx, kz, B):
 
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
-                     rng_mode="replay", graphs=True):
+                     rng_mode="replay", graphs=True, group=None):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference.
     rng_mode="device": SWR rows and pairs drawn on the device from a seed taken from the
     global RNG (one randint); statistically equivalent, and with graphs=True each run of
-    steps between evaluations/reshuffles is one hipGraph replay."""
+    steps between evaluations/reshuffles is one hipGraph replay.
+    group: a torch.distributed group (one process per GPU); shards are spread over its ranks
+    and the trajectory is identical to the single-GPU one.  Every rank must call with the
+    same inputs and the same NumPy global RNG state."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -178,7 +209,8 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     logging.info("pairs_per_clust: %d ", (n_X / N) * (n_Z / N))
     logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
 
-    eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type)
+    eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
+                    group=group)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs)
