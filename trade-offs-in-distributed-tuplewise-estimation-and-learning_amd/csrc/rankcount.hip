@@ -48,6 +48,32 @@ __device__ __forceinline__ bool is_nan_score(T v) {
   return false;
 }
 
+// Register-blocked bitonic sort of one chunk: thread t owns keys [16t, 16t+16).  For every
+// merge size k the passes with partner distance j >= 16 run through LDS (one compare-exchange
+// per pair), the last four (j = 8, 4, 2, 1) on the thread's own 16 registers.  C >= 1024.
+constexpr int kE = 16;
+
+__device__ __forceinline__ void cex(uint64_t& a, uint64_t& b, bool up) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = up ? lo : hi;
+  b = up ? hi : lo;
+}
+
+// bitonic levels j = 8..1 of merge size k on v[0..15] = keys[base .. base+15]
+__device__ __forceinline__ void reg_levels(uint64_t (&v)[kE], int base, int k, int jmax) {
+#pragma unroll
+  for (int j = 8; j > 0; j >>= 1) {
+    if (j > jmax) continue;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      if ((e & j) == 0) {
+        const bool up = ((base + e) & k) == 0;
+        cex(v[e], v[e | j], up);
+      }
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restrict__ z,
                                                               const int64_t* __restrict__ z_off,
@@ -58,30 +84,48 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restric
   const int c = blockIdx.x - s * chunks;
   const int64_t zb = z_off[s], ze = z_off[s + 1];
   const int64_t c0 = zb + (int64_t)c * C;
-  for (int i = threadIdx.x; i < C; i += kSortThreads) {
+  const int nthr = C / kE;  // active threads (C >= 1024 -> >= 64)
+  const int tid = threadIdx.x;
+  for (int i = tid; i < C; i += kSortThreads) {  // coalesced load + key transform
     const int64_t g = c0 + i;
     keys[i] = (g < ze) ? order_key<T>(z[g]) : ~0ull;
   }
   __syncthreads();
   if (c0 < ze) {  // block-uniform: an empty chunk stays all-padding
-    for (int k = 2; k <= C; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int p = threadIdx.x; p < (C >> 1); p += kSortThreads) {
+    const int base = tid * kE;
+    uint64_t v[kE];
+    if (tid < nthr) {
+#pragma unroll
+      for (int e = 0; e < kE; ++e) v[e] = keys[base + e];
+      for (int k = 2; k <= kE; k <<= 1) reg_levels(v, base, k, k >> 1);  // sort runs of 16
+#pragma unroll
+      for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
+    }
+    __syncthreads();
+    for (int k = 2 * kE; k <= C; k <<= 1) {
+      for (int j = k >> 1; j >= kE; j >>= 1) {  // long-distance levels through LDS
+        for (int p = tid; p < (C >> 1); p += kSortThreads) {
           const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
           const int hi = lo + j;
-          const uint64_t a = keys[lo], b = keys[hi];
-          const bool up = (lo & k) == 0;
-          if ((a > b) == up) {
-            keys[lo] = b;
-            keys[hi] = a;
-          }
+          uint64_t a = keys[lo], b = keys[hi];
+          cex(a, b, (lo & k) == 0);
+          keys[lo] = a;
+          keys[hi] = b;
         }
         __syncthreads();
       }
+      if (tid < nthr) {  // j = 8..1 in registers
+#pragma unroll
+        for (int e = 0; e < kE; ++e) v[e] = keys[base + e];
+        reg_levels(v, base, k, kE >> 1);
+#pragma unroll
+        for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
+      }
+      __syncthreads();
     }
   }
   uint64_t* dst = sorted + (int64_t)blockIdx.x * C;
-  for (int i = threadIdx.x; i < C; i += kSortThreads) dst[i] = keys[i];
+  for (int i = tid; i < C; i += kSortThreads) dst[i] = keys[i];
 }
 
 // #{keys < k} in a sorted power-of-two array (branchless).
@@ -150,7 +194,7 @@ struct RankPlan {
 };
 inline RankPlan plan_rank(int64_t max_nx, int64_t max_nz) {
   RankPlan p;
-  int64_t C = 64;
+  int64_t C = 1024;  // register-blocked sort needs C / 16 >= 64 threads
   while (C < max_nz && C < kMaxChunk) C <<= 1;
   p.C = (int)C;
   p.chunks = (int)std::max<int64_t>(1, ceil_div(max_nz, C));
