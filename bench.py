@@ -132,7 +132,12 @@ def main():
     torch.cuda.set_device(local)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL over xGMI; TW_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
+        backend = os.environ.get("TW_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
     import tuplewise  # noqa: F401
     from tuplewise.device import ShardedSample
@@ -163,7 +168,10 @@ def main():
 
     def barrier():
         if group is not None:
-            dist.barrier(device_ids=[local])
+            if dist.get_backend(group) == "nccl":
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
 
     for w in range(args.warmup):
         S.UnN(key=w)

@@ -77,6 +77,9 @@ int tw_count_set_plan(int32_t R, int64_t z_chunk);
  * to tw_count_pairs for TW_PRED_GT and TW_PRED_HALF (not SUBGT).  d_work: device scratch of
  * tw_count_pairs_sorted_work_bytes(n_shards, max_nz) bytes. */
 int64_t tw_count_pairs_sorted_work_bytes(int32_t n_shards, int64_t max_nz);
+/* Tuning hook: largest sorted chunk (power of two in [1024, 16384]; default 4096).
+ * Process-global; results do not depend on it (the workspace size does). */
+int tw_count_sorted_set_chunk(int64_t cap);
 int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, int32_t dtype, int32_t pred, void* d_work,

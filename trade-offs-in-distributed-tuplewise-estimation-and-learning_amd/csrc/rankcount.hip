@@ -192,10 +192,12 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_count(const T* __restrict
 struct RankPlan {
   int C, chunks, tiles_x;
 };
+static int64_t g_chunk_cap = 4096;  // tuning hook (tw_count_sorted_set_chunk)
+
 inline RankPlan plan_rank(int64_t max_nx, int64_t max_nz) {
   RankPlan p;
   int64_t C = 1024;  // register-blocked sort needs C / 16 >= 64 threads
-  while (C < max_nz && C < kMaxChunk) C <<= 1;
+  while (C < max_nz && C < g_chunk_cap) C <<= 1;
   p.C = (int)C;
   p.chunks = (int)std::max<int64_t>(1, ceil_div(max_nz, C));
   p.tiles_x = (int)std::max<int64_t>(1, ceil_div(max_nx, (int64_t)kSortThreads * kXPerThread));
@@ -242,6 +244,13 @@ int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_
 }  // namespace tw
 
 using namespace tw;
+
+extern "C" int tw_count_sorted_set_chunk(int64_t cap) {
+  TW_ARG_CHECK(cap >= 1024 && cap <= kMaxChunk && (cap & (cap - 1)) == 0,
+               "tw_count_sorted_set_chunk: cap must be a power of two in [1024, 16384]");
+  g_chunk_cap = cap;
+  return TW_OK;
+}
 
 extern "C" int64_t tw_count_pairs_sorted_work_bytes(int32_t n_shards, int64_t max_nz) {
   const RankPlan p = plan_rank(1, std::max<int64_t>(1, max_nz));
