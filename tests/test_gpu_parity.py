@@ -223,3 +223,35 @@ def test_errors_match_reference(gpu):
         cs.UN(X.copy(), Z.copy(), 20, cs.Un, sampling_type="prop-SWOR")  # k == 0 block
     with pytest.raises(TypeError):
         cs.Un(np.array([True, False]), np.array([False]), kernel="AUC")
+
+
+def test_multicolumn_scores_match_oracle(gpu):
+    """2-D score arrays: Un flattens (reshape(-1)), UN slices rows, UB subtracts rows."""
+    import tuplewise.estimation as est
+    import tuplewise.compute_stats as cs
+    rng = np.random.RandomState(12)
+    X, Z = rng.normal(size=(300, 3)).round(1), rng.normal(size=(200, 3)).round(1)
+    assert est.Un(X, Z) == O.est_Un(X, Z)
+    for st in ("prop-SWOR", "SWOR", "prop-SWR"):
+        a, b = X.copy(), Z.copy()
+        np.random.seed(4)
+        got = est.UnN(a, b, 7, st)
+        c, d = X.copy(), Z.copy()
+        np.random.seed(4)
+        want = O.est_UnN(c, d, 7, st)
+        assert got == want and np.array_equal(a, c)
+    np.random.seed(5)
+    got = cs.UnNB(X.copy(), Z.copy(), 5, 64, "prop-SWOR", kernel="AUC")
+    np.random.seed(5)
+    want = O.cs_UnNB(X.copy(), Z.copy(), 5, 64, "prop-SWOR", "AUC")
+    assert got == want
+    ix, iz = rng.randint(0, 300, 50), rng.randint(0, 200, 50)
+    assert cs.UB_indices(X, Z, ix, iz, "AUC") == O.UB_indices(X, Z, ix, iz, "AUC")
+
+
+def test_empty_inputs_like_numpy(gpu):
+    import tuplewise.estimation as est
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        assert np.isnan(est.Un(np.zeros(0), np.ones(3)))
+        assert np.isnan(O.est_Un(np.zeros(0), np.ones(3)))

@@ -38,6 +38,28 @@ def _flat(a: np.ndarray) -> np.ndarray:
     return np.asarray(a).reshape(-1)
 
 
+def _row_size(a) -> int:
+    a = np.asarray(a)
+    return int(np.prod(a.shape[1:], dtype=np.int64)) if a.ndim > 1 else 1
+
+
+def _elements(blocks, side: str, rs: int) -> list:
+    """Blocks' row selections (slices or row-index arrays) of a (n, ...) array whose rows
+    hold rs elements, as selections of the flattened array (what Un's reshape(-1) sees)."""
+    if rs == 1:
+        return blocks
+    out = []
+    for b in blocks:
+        sel = getattr(b, side)
+        if isinstance(sel, tuple):
+            e = (sel[0] * rs, sel[1] * rs)
+        else:
+            e = (np.asarray(sel, dtype=np.int64)[:, None] * rs + np.arange(rs)).reshape(-1)
+        nb = Block(e, b.z, b.aux) if side == "x" else Block(b.x, e, b.aux)
+        out.append(nb)
+    return out
+
+
 def _layout(arr_dev, blocks, side: str):
     """Device array + int64 offsets (len(blocks)+1) for the blocks' x or z parts."""
     parts = [getattr(b, side) for b in blocks]
@@ -93,6 +115,7 @@ class CompleteCount(BlockSpec):
 
     def evaluate(self, X, Z, blocks):
         x, z, code, mode = self.operands(_flat(X), _flat(Z))
+        blocks = _elements(_elements(blocks, "x", _row_size(X)), "z", _row_size(Z))
         xd, zd = L.to_device(x), L.to_device(z)
         xa, xo = _layout(xd, blocks, "x")
         za, zo = _layout(zd, blocks, "z")
@@ -115,6 +138,7 @@ class CompleteSum(BlockSpec):
     def evaluate(self, X, Z, blocks):
         x = _flat(X).astype(np.float64, copy=False)
         z = _flat(Z).astype(np.float64, copy=False)
+        blocks = _elements(_elements(blocks, "x", _row_size(X)), "z", _row_size(Z))
         xd, zd = L.to_device(x), L.to_device(z)
         xa, xo = _layout(xd, blocks, "x")
         za, zo = _layout(zd, blocks, "z")
@@ -143,14 +167,20 @@ class Incomplete(BlockSpec):
         ix_abs, iz_abs, offs = [], [], [0]
         xs = _flat(X)
         zs = _flat(Z)
-        # absolute positions: slices are offsets into X/Z, resampled blocks map through idx
+        rs = _row_size(X)
+        if _row_size(Z) != rs:
+            raise ValueError("UB on rows of different widths cannot broadcast")
+        # absolute row positions: slices are offsets into X/Z, resampled blocks map through idx
         for b in blocks:
             ix, iz = b.aux
             ix_abs.append(ix + b.x[0] if isinstance(b.x, tuple) else np.asarray(b.x)[ix])
             iz_abs.append(iz + b.z[0] if isinstance(b.z, tuple) else np.asarray(b.z)[iz])
-            offs.append(offs[-1] + len(ix))
-        return indexed_values(xs, zs, np.concatenate(ix_abs), np.concatenate(iz_abs),
-                              np.array(offs, dtype=np.int64), self.kernel)
+            offs.append(offs[-1] + len(ix) * rs)
+        ixa, iza = np.concatenate(ix_abs), np.concatenate(iz_abs)
+        if rs > 1:  # X[ind] - Z[ind] on rows: element pairs (r*rs + c, r'*rs + c)
+            ixa = (ixa[:, None] * rs + np.arange(rs)).reshape(-1)
+            iza = (iza[:, None] * rs + np.arange(rs)).reshape(-1)
+        return indexed_values(xs, zs, ixa, iza, np.array(offs, dtype=np.int64), self.kernel)
 
 
 def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,

@@ -42,9 +42,16 @@ def UB_indices(X, Z, ind_X, ind_Z, kernel):
     if ind_X.shape != ind_Z.shape:
         raise ValueError(f"operands could not be broadcast together with shapes "
                          f"{ind_X.shape} {ind_Z.shape}")
-    x, z = _columns(X), _columns(Z)
-    off = np.array([0, ind_X.size], dtype=np.int64)
-    return Bk.indexed_values(x, z, ind_X.reshape(-1), ind_Z.reshape(-1), off, kernel)[0]
+    rs = Bk._row_size(X)
+    if Bk._row_size(Z) != rs:
+        raise ValueError(f"operands could not be broadcast together with shapes "
+                         f"{X[ind_X].shape} {Z[ind_Z].shape}")
+    ix, iz = ind_X.reshape(-1), ind_Z.reshape(-1)
+    if rs > 1:  # X[ind_X] - Z[ind_Z] on whole rows: element pairs column by column
+        ix = (ix[:, None] * rs + np.arange(rs)).reshape(-1)
+        iz = (iz[:, None] * rs + np.arange(rs)).reshape(-1)
+    off = np.array([0, ix.size], dtype=np.int64)
+    return Bk.indexed_values(X.reshape(-1), Z.reshape(-1), ix, iz, off, kernel)[0]
 
 
 def UB_pairs(X, Z, indices, kernel):

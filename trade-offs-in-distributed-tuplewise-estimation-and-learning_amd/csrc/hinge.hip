@@ -125,9 +125,18 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
     for (int q = 0; q < kMaxColsPerThread; ++q) {
       const int64_t j = threadIdx.x + (int64_t)q * BS;
       if (j < d) {
+        // branch-free: an unfiltered row adds -0.0, which leaves every value (incl. +-0.0)
+        // bit-identical, so the order and result are NumPy's; 8 LDS reads in flight
         double a = acc[q];
-        for (int t = 0; t < nb; ++t)
-          if (flag[t]) a += diff[(int64_t)t * d + j];
+        int t = 0;
+        for (; t + 8 <= nb; t += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = flag[t + u] ? diff[(int64_t)(t + u) * d + j] : -0.0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; t < nb; ++t) a += flag[t] ? diff[(int64_t)t * d + j] : -0.0;
         acc[q] = a;
       }
     }
