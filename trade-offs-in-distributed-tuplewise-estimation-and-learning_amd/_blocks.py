@@ -43,6 +43,13 @@ def _row_size(a) -> int:
     return int(np.prod(a.shape[1:], dtype=np.int64)) if a.ndim > 1 else 1
 
 
+def whole(X, Z) -> "Block":
+    """One block spanning every row of X and Z (blocks are in rows; see _elements)."""
+    nx = X.shape[0] if X.ndim else 1
+    nz = Z.shape[0] if Z.ndim else 1
+    return Block((0, nx), (0, nz))
+
+
 def _elements(blocks, side: str, rs: int) -> list:
     """Blocks' row selections (slices or row-index arrays) of a (n, ...) array whose rows
     hold rs elements, as selections of the flattened array (what Un's reshape(-1) sees)."""

@@ -25,7 +25,7 @@ def Un(X, Z, kernel="prod"):
     assert kernel in _KERNELS
     X = np.asarray(X)
     Z = np.asarray(Z)
-    blk = Bk.Block((0, X.size), (0, Z.size))
+    blk = Bk.whole(X, Z)
     if kernel == "AUC":
         return Bk.CompleteCount(literal_sub=True).evaluate(X, Z, [blk])[0]
     kern = L.TW_KERN_PROD if kernel == "prod" else L.TW_KERN_GINI
@@ -148,7 +148,7 @@ def conv_AUC(margin):
         """Computes the convexification of the 1-AUC that we minimize."""
         X = np.asarray(X)
         Z = np.asarray(Z)
-        blk = Bk.Block((0, X.size), (0, Z.size))
+        blk = Bk.whole(X, Z)
         return Bk.CompleteSum(L.TW_KERN_HINGE, float(margin)).evaluate(X, Z, [blk])[0]
     return _block_fn(Bk.CompleteSum(L.TW_KERN_HINGE, float(margin)), res_function)
 

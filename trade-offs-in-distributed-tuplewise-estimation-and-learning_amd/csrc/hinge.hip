@@ -189,8 +189,17 @@ __global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
       tile[e] = c < nc ? grads[(int64_t)(s0 + r) * d + j0 + c] : 0.0;
     }
     __syncthreads();
-    if (threadIdx.x < nc)
-      for (int r = 0; r < ns; ++r) sum += tile[r * kUpdCols + threadIdx.x];
+    if (threadIdx.x < nc) {  // shard order kept; 8 LDS reads in flight per batch
+      int r = 0;
+      for (; r + 8 <= ns; r += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * kUpdCols + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum += v[u];
+      }
+      for (; r < ns; ++r) sum += tile[r * kUpdCols + threadIdx.x];
+    }
   }
   if (threadIdx.x < nc) {
     const int64_t j = j0 + threadIdx.x;

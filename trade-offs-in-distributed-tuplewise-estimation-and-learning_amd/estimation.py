@@ -50,7 +50,7 @@ def _un_block(tie_mode):
     def Un_block(X, Z):
         X = np.asarray(X)
         Z = np.asarray(Z)
-        return spec.evaluate(X, Z, [Bk.Block((0, X.size), (0, Z.size))])[0]
+        return spec.evaluate(X, Z, [Bk.whole(X, Z)])[0]
 
     Un_block._tw_block = spec
     return Un_block
