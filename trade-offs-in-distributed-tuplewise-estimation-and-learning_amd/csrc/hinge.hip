@@ -71,17 +71,11 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
         ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
         az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
       }
-      rx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-      rz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
-    }
-    __syncthreads();
-    // stage diff rows Z[rz] - X[rx] in LDS and reduce S = diff . w + margin on the way.
-    // Narrow rows (d <= 32): one thread per pair, sequential j (all row loads independent).
-    // Wide rows: one wave per pair, coalesced lane-strided loads + fixed butterfly.
-    if (d <= 32) {
-      for (int t = threadIdx.x; t < nb; t += BS) {
-        const double* zr = Z + rz[t] * d;
-        const double* xr = X + rx[t] * d;
+      const int64_t rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+      const int64_t rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      if (d <= 32) {  // narrow rows: this thread stages its own pair right away (no barrier)
+        const double* zr = Z + rzt * d;
+        const double* xr = X + rxt * d;
         double* dr = diff + (int64_t)t * d;
         double part = 0.0;
 #pragma unroll 4
@@ -91,8 +85,16 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
           part += v * w[j];
         }
         flag[t] = (part + margin) > 0.0;
+      } else {
+        rx[t] = rxt;
+        rz[t] = rzt;
       }
-    } else for (int t = wid; t < nb; t += BS / kWave) {
+    }
+    __syncthreads();
+    // stage diff rows Z[rz] - X[rx] in LDS and reduce S = diff . w + margin on the way.
+    // Narrow rows (d <= 32): one thread per pair, sequential j (all row loads independent).
+    // Wide rows: one wave per pair, coalesced lane-strided loads + fixed butterfly.
+    if (d > 32) for (int t = wid; t < nb; t += BS / kWave) {
       const double* zr = Z + rz[t] * d;
       const double* xr = X + rx[t] * d;
       double* dr = diff + (int64_t)t * d;
