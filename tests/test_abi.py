@@ -54,3 +54,16 @@ def test_no_device_raises(tw):
     import tuplewise.estimation as est
     with pytest.raises(RuntimeError, match="no HIP device"):
         est.Un(np.ones(3), np.zeros(2))
+
+
+def test_single_hip_runtime_whatever_the_import_order():
+    """Loading libtuplewise.so before torch must not bring a second HIP/HSA runtime."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import tuplewise; tuplewise._lib.lib(); "
+            "import torch; m = open('/proc/self/maps').read(); "
+            "print(len({l.split()[-1] for l in m.splitlines() if 'libamdhip64' in l}))") % str(ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "1"

@@ -71,6 +71,11 @@ def lib() -> ctypes.CDLL:
     """Load libtuplewise.so once (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64/libhsa-runtime64, and
+        # libtuplewise.so's NEEDED libamdhip64.so.7 must bind to that copy.  Loading our
+        # library first would pull /opt/rocm's runtime in beside torch's (two HSA runtimes,
+        # one of which then sees no device), so torch is imported before the dlopen.
+        import torch as _torch  # noqa: F401
         if not LIB_PATH.exists():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g;"
