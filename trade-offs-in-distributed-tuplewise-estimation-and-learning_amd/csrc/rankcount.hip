@@ -51,21 +51,20 @@ __device__ __forceinline__ bool is_nan_score(T v) {
 // Register-blocked bitonic sort of one chunk: thread t owns keys [16t, 16t+16).  For every
 // merge size k the passes with partner distance j >= 16 run through LDS (one compare-exchange
 // per pair), the last four (j = 8, 4, 2, 1) on the thread's own 16 registers.  C >= 1024.
-constexpr int kE = 16;
-
 __device__ __forceinline__ void cex(uint64_t& a, uint64_t& b, bool up) {
   const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
   a = up ? lo : hi;
   b = up ? hi : lo;
 }
 
-// bitonic levels j = 8..1 of merge size k on v[0..15] = keys[base .. base+15]
-__device__ __forceinline__ void reg_levels(uint64_t (&v)[kE], int base, int k, int jmax) {
+// bitonic levels j = E/2..1 of merge size k on v[0..E) = keys[base .. base+E)
+template <int E>
+__device__ __forceinline__ void reg_levels(uint64_t (&v)[E], int base, int k, int jmax) {
 #pragma unroll
-  for (int j = 8; j > 0; j >>= 1) {
+  for (int j = E / 2; j > 0; j >>= 1) {
     if (j > jmax) continue;
 #pragma unroll
-    for (int e = 0; e < kE; ++e) {
+    for (int e = 0; e < E; ++e) {
       if ((e & j) == 0) {
         const bool up = ((base + e) & k) == 0;
         cex(v[e], v[e | j], up);
@@ -74,7 +73,15 @@ __device__ __forceinline__ void reg_levels(uint64_t (&v)[kE], int base, int k, i
   }
 }
 
-template <typename T>
+// Keys stay in registers for the whole network: thread t owns keys [E t, E t + E) of the
+// chunk (C / E threads; E = max(4, C / 1024) so a block always has >= 256 threads and
+// chunks >= 4096 get 16 waves to hide shuffle/LDS latency).  Level (k, j) pairs key i with
+// key i ^ j:
+//   j <  E          same thread          -> compare-exchange in registers
+//   E <= j < 64 E   same wave (lane ^ j/E) -> __shfl_xor, no barrier
+//   j >= 64 E       other wave           -> exchange through LDS (one barrier pair)
+// Direction: ascending iff (i & k) == 0.  C is a power of two >= 1024.
+template <typename T, int kE>
 __global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restrict__ z,
                                                               const int64_t* __restrict__ z_off,
                                                               int chunks, int C,
@@ -84,48 +91,54 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restric
   const int c = blockIdx.x - s * chunks;
   const int64_t zb = z_off[s], ze = z_off[s + 1];
   const int64_t c0 = zb + (int64_t)c * C;
-  const int nthr = C / kE;  // active threads (C >= 1024 -> >= 64)
+  const int nthr = blockDim.x;  // == C / kE
   const int tid = threadIdx.x;
-  for (int i = tid; i < C; i += kSortThreads) {  // coalesced load + key transform
+  for (int i = tid; i < C; i += nthr) {  // coalesced load + key transform
     const int64_t g = c0 + i;
     keys[i] = (g < ze) ? order_key<T>(z[g]) : ~0ull;
   }
   __syncthreads();
-  if (c0 < ze) {  // block-uniform: an empty chunk stays all-padding
-    const int base = tid * kE;
-    uint64_t v[kE];
-    if (tid < nthr) {
+  uint64_t* dst = sorted + (int64_t)blockIdx.x * C;
+  if (c0 >= ze) {  // block-uniform: an empty chunk stays all-padding
+    for (int i = tid; i < C; i += nthr) dst[i] = ~0ull;
+    return;
+  }
+  const int base = tid * kE;
+  uint64_t v[kE];
 #pragma unroll
-      for (int e = 0; e < kE; ++e) v[e] = keys[base + e];
-      for (int k = 2; k <= kE; k <<= 1) reg_levels(v, base, k, k >> 1);  // sort runs of 16
-#pragma unroll
-      for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
-    }
-    __syncthreads();
-    for (int k = 2 * kE; k <= C; k <<= 1) {
-      for (int j = k >> 1; j >= kE; j >>= 1) {  // long-distance levels through LDS
-        for (int p = tid; p < (C >> 1); p += kSortThreads) {
-          const int lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
-          const int hi = lo + j;
-          uint64_t a = keys[lo], b = keys[hi];
-          cex(a, b, (lo & k) == 0);
-          keys[lo] = a;
-          keys[hi] = b;
-        }
+  for (int e = 0; e < kE; ++e) v[e] = keys[base + e];
+  for (int k = 2; k <= kE; k <<= 1) reg_levels<kE>(v, base, k, k >> 1);  // runs of E sorted
+  for (int k = 2 * kE; k <= C; k <<= 1) {
+    const bool up = ((base & k) == 0);  // (i & k) for every e, since k >= 2E > e
+    for (int j = k >> 1; j >= kE; j >>= 1) {
+      const int m = j / kE;  // partner thread distance
+      const bool keep_min = (((tid & m) == 0) == up);
+      if (m >= kWave) {  // across waves: through LDS
         __syncthreads();
-      }
-      if (tid < nthr) {  // j = 8..1 in registers
-#pragma unroll
-        for (int e = 0; e < kE; ++e) v[e] = keys[base + e];
-        reg_levels(v, base, k, kE >> 1);
 #pragma unroll
         for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
+        __syncthreads();
+        const int pb = (tid ^ m) * kE;
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const uint64_t o = keys[pb + e];
+          v[e] = keep_min ? (o < v[e] ? o : v[e]) : (o > v[e] ? o : v[e]);
+        }
+      } else {  // inside the wave: lane shuffles
+#pragma unroll
+        for (int e = 0; e < kE; ++e) {
+          const uint64_t o = __shfl_xor(v[e], m, kWave);
+          v[e] = keep_min ? (o < v[e] ? o : v[e]) : (o > v[e] ? o : v[e]);
+        }
       }
-      __syncthreads();
     }
+    reg_levels<kE>(v, base, k, kE >> 1);
   }
-  uint64_t* dst = sorted + (int64_t)blockIdx.x * C;
-  for (int i = tid; i < C; i += kSortThreads) dst[i] = keys[i];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
+  __syncthreads();
+  for (int i = tid; i < C; i += nthr) dst[i] = keys[i];
 }
 
 // #{keys < k} in a sorted power-of-two array (branchless).
@@ -163,17 +176,24 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_count(const T* __restrict
     xk[r] = order_key<T>(v);
   }
   unsigned long long acc = 0;
-  for (int c = 0; c < chunks; ++c) {
-    const uint64_t* src = sorted + ((int64_t)s * chunks + c) * C;
+  // stage as many sorted chunks as fit (<= 16384 keys = 128 KiB) at once, then run every
+  // search of this thread back to back (independent LDS chains in flight)
+  const int group = (int)std::max<int64_t>(1, kMaxChunk / C);
+  for (int c0 = 0; c0 < chunks; c0 += group) {
+    const int ng = std::min(group, chunks - c0);
+    const uint64_t* src = sorted + ((int64_t)s * chunks + c0) * C;
     __syncthreads();
-    for (int i = threadIdx.x; i < C; i += kSortThreads) keys[i] = src[i];
+    for (int i = threadIdx.x; i < ng * C; i += kSortThreads) keys[i] = src[i];
     __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+      const uint64_t* kc = keys + g * C;
 #pragma unroll
-    for (int r = 0; r < kXPerThread; ++r) {
-      if (valid[r]) {
-        uint32_t v = lower_bound_lds(keys, C, xk[r]);
-        if (PRED == TW_PRED_HALF) v += upper_bound_lds(keys, C, xk[r]);
-        acc += v;
+      for (int r = 0; r < kXPerThread; ++r) {
+        if (valid[r]) {
+          uint32_t v = lower_bound_lds(kc, C, xk[r]);
+          if (PRED == TW_PRED_HALF) v += upper_bound_lds(kc, C, xk[r]);
+          acc += v;
+        }
       }
     }
   }
@@ -213,9 +233,16 @@ int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_
                    (int64_t)n_shards * p.tiles_x < (1ll << 31),
                "tw_count_pairs_sorted: grid too large");
   const size_t lds = sizeof(uint64_t) * p.C;
+  const size_t lds_rank = sizeof(uint64_t) * std::min<int64_t>((int64_t)p.chunks * p.C, kMaxChunk);
   static bool attrs_set = false;  // > 64 KiB of dynamic LDS must be opted into once
   if (!attrs_set) {
-    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T>,
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 4>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 8>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 16>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)(sizeof(uint64_t) * kMaxChunk)));
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_count<T, TW_PRED_GT>,
@@ -226,16 +253,24 @@ int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_
                                      (int)(sizeof(uint64_t) * kMaxChunk)));
     attrs_set = true;
   }
-  hipLaunchKernelGGL(k_sort_chunks<T>, dim3(n_shards * p.chunks), dim3(kSortThreads), lds, st,
-                     (const T*)z, z_off, p.chunks, p.C, (uint64_t*)work);
+  const int E = std::max(4, p.C / kSortThreads);
+  if (E == 4)
+    hipLaunchKernelGGL((k_sort_chunks<T, 4>), dim3(n_shards * p.chunks), dim3(p.C / 4), lds, st,
+                       (const T*)z, z_off, p.chunks, p.C, (uint64_t*)work);
+  else if (E == 8)
+    hipLaunchKernelGGL((k_sort_chunks<T, 8>), dim3(n_shards * p.chunks), dim3(p.C / 8), lds, st,
+                       (const T*)z, z_off, p.chunks, p.C, (uint64_t*)work);
+  else
+    hipLaunchKernelGGL((k_sort_chunks<T, 16>), dim3(n_shards * p.chunks), dim3(p.C / 16), lds,
+                       st, (const T*)z, z_off, p.chunks, p.C, (uint64_t*)work);
   TW_LAUNCH_CHECK();
   if (pred == TW_PRED_HALF)
     hipLaunchKernelGGL((k_rank_count<T, TW_PRED_HALF>), dim3(n_shards * p.tiles_x),
-                       dim3(kSortThreads), lds, st, (const T*)x, x_off, (const uint64_t*)work,
+                       dim3(kSortThreads), lds_rank, st, (const T*)x, x_off, (const uint64_t*)work,
                        p.chunks, p.C, p.tiles_x, (unsigned long long*)out);
   else
     hipLaunchKernelGGL((k_rank_count<T, TW_PRED_GT>), dim3(n_shards * p.tiles_x),
-                       dim3(kSortThreads), lds, st, (const T*)x, x_off, (const uint64_t*)work,
+                       dim3(kSortThreads), lds_rank, st, (const T*)x, x_off, (const uint64_t*)work,
                        p.chunks, p.C, p.tiles_x, (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
