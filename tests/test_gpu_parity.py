@@ -255,3 +255,21 @@ def test_empty_inputs_like_numpy(gpu):
         warnings.simplefilter("ignore")
         assert np.isnan(est.Un(np.zeros(0), np.ones(3)))
         assert np.isnan(O.est_Un(np.zeros(0), np.ones(3)))
+
+
+@pytest.mark.parametrize("which", ["Un", "UnN", "UnNT"])
+def test_replicate_equals_reference_loop(gpu, which):
+    """estimation.replicate == the Monte-Carlo list comprehension of main.py:106-112."""
+    import tuplewise.estimation as est
+    n, m, e = 500, 50, 0.1
+    gen_X = lambda: 2 * np.random.binomial(1, 1 - e, n)
+    gen_Z = lambda: 2 * np.random.binomial(1, e, m) - 1
+    args = {"Un": (), "UnN": (10, "prop-SWOR"), "UnNT": (10, 4, "prop-SWOR")}[which]
+    fo = {"Un": O.est_Un, "UnN": O.est_UnN, "UnNT": O.est_UnNT}[which]
+    np.random.seed(21)
+    want = [fo(gen_X(), gen_Z(), *args) for _ in range(60)]
+    probe_want = np.random.randint(2 ** 30)
+    np.random.seed(21)
+    got = est.replicate(getattr(est, which), gen_X, gen_Z, 60, *args, flush_elems=20_000)
+    probe_got = np.random.randint(2 ** 30)
+    assert got == want and probe_got == probe_want

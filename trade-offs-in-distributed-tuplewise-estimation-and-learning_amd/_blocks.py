@@ -205,10 +205,10 @@ def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,
     return [np.float64(s / np.float64(p)) for s, p in zip(sums, npairs)]
 
 
-def run_un(X, Z, N, f_block, sampling_type, variant: str):
-    """Shared body of UN (compute_stats.py:56-92, variant "cs"; estimation-experiment/main.py
-    :33-69, variant "est").  Keeps the in-place shuffle and every RNG draw in order."""
-    vals = list()
+def plan_un(X, Z, N, spec, sampling_type, variant: str) -> list:
+    """The host half of UN (compute_stats.py:56-92 "cs", estimation-experiment/main.py:33-69
+    "est"): shuffle X and Z in place, then walk the N blocks making every RNG draw of the
+    reference in order.  Returns the plan [("val", Block) | ("zero",)] in append order."""
     X_rem = X
     Z_rem = Z
     np.random.shuffle(X_rem)
@@ -216,12 +216,7 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
     n_X = X_rem.shape[0]
     n_Z = Z_rem.shape[0]
     tau = int((n_X + n_Z) / N)
-    spec = getattr(f_block, "_tw_block", None)
-
-    if spec is None:  # user block function: the reference protocol, block by block
-        return _run_un_python(X_rem, Z_rem, N, f_block, sampling_type, variant, n_X, n_Z, tau)
-
-    plan = []  # ("val", block) | ("zero",) in the order the reference appends
+    plan = []
     x_pos = z_pos = 0
     for _ in range(N):
         if sampling_type != "prop-SWR":
@@ -251,12 +246,55 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
             blk = Block(ix, iz)
             blk.aux = spec.draw(blk.nx(), blk.nz())
             plan.append(("val", blk))
+    return plan
 
+
+def finish_un(plan, values) -> np.float64:
+    """UN's `np.mean(vals)` with the block values in plan order."""
+    values = iter(values)
+    return np.mean([0 if p[0] == "zero" else next(values) for p in plan])
+
+
+def run_un(X, Z, N, f_block, sampling_type, variant: str):
+    """Shared body of UN (compute_stats.py:56-92, variant "cs"; estimation-experiment/main.py
+    :33-69, variant "est").  Keeps the in-place shuffle and every RNG draw in order."""
+    spec = getattr(f_block, "_tw_block", None)
+    if spec is None:  # user block function: the reference protocol, block by block
+        np.random.shuffle(X)
+        np.random.shuffle(Z)
+        n_X, n_Z = X.shape[0], Z.shape[0]
+        return _run_un_python(X, Z, N, f_block, sampling_type, variant, n_X, n_Z,
+                              int((n_X + n_Z) / N))
+    plan = plan_un(X, Z, N, spec, sampling_type, variant)
     blocks = [p[1] for p in plan if p[0] == "val"]
-    values = iter(spec.evaluate(X_rem, Z_rem, blocks) if blocks else [])
-    for p in plan:
-        vals.append(0 if p[0] == "zero" else next(values))
-    return np.mean(vals)
+    return finish_un(plan, spec.evaluate(X, Z, blocks) if blocks else [])
+
+
+def evaluate_many(spec, jobs) -> list:
+    """Block values of several independent (X, Z, blocks) jobs of one spec in ONE launch:
+    the jobs' score vectors are concatenated and their blocks shifted.  Scores must be 1-D
+    (or (n, 1)); returns one list of values per job."""
+    xs, zs, blocks, counts = [], [], [], []
+    xo = zo = 0
+    for X, Z, blks in jobs:
+        x, z = _flat(X), _flat(Z)
+        for b in blks:
+            bx = (b.x[0] + xo, b.x[1] + xo) if isinstance(b.x, tuple) else np.asarray(b.x) + xo
+            bz = (b.z[0] + zo, b.z[1] + zo) if isinstance(b.z, tuple) else np.asarray(b.z) + zo
+            blocks.append(Block(bx, bz, b.aux))
+        xs.append(x)
+        zs.append(z)
+        counts.append(len(blks))
+        xo += x.shape[0]
+        zo += z.shape[0]
+    if not blocks:
+        return [[] for _ in jobs]
+    vals = spec.evaluate(np.concatenate(xs), np.concatenate(zs), blocks)
+    out, i = [], 0
+    for c in counts:
+        out.append(vals[i:i + c])
+        i += c
+    return out
 
 
 def _run_un_python(X_rem, Z_rem, N, f_block, sampling_type, variant, n_X, n_Z, tau):

@@ -85,3 +85,69 @@ def UnNT(X, Z, N, T, sampling_type, tie_mode="strict"):
     """Computes reshuffled block-wise complete U-statistic.  (main.py:76-79)"""
     return np.mean([UnN(X, Z, N, sampling_type=sampling_type, tie_mode=tie_mode)
                     for _ in range(T)])
+
+
+def replicate(estimator, gen_X, gen_Z, n_tries, *args, flush_elems=1 << 24, **kwargs):
+    """``[estimator(gen_X(), gen_Z(), *args, **kwargs) for _ in range(n_tries)]`` — the
+    Monte-Carlo loops of main.py:106-112 — with identical results and identical NumPy RNG
+    consumption, but the pair counts of many tries evaluated in one device launch.
+
+    estimator: Un, UnN or UnNT of this module.  The host side (gen_X/gen_Z, the in-place
+    shuffles, every RNG draw) runs in exactly the reference's order; the shuffled samples of
+    pending tries are snapshotted and counted in batches of about `flush_elems` scores.
+    """
+    tie_mode = kwargs.pop("tie_mode", "strict")
+    if kwargs:
+        raise TypeError(f"unexpected keyword arguments {sorted(kwargs)}")
+    spec = (_UN_HALF if tie_mode == "half" else _UN_STRICT)._tw_block
+    if estimator is Un:
+        reps, mk = 1, None
+    elif estimator is UnN:
+        N, sampling_type = args
+        reps = 1
+    elif estimator is UnNT:
+        N, T, sampling_type = args
+        reps = T
+    else:
+        raise ValueError("replicate supports estimation.Un, UnN and UnNT")
+
+    results = []
+    pending = []  # (try index, [(plan, job) per repetition])
+    jobs = []
+    size = 0
+
+    def flush():
+        nonlocal jobs, pending, size
+        vals = Bk.evaluate_many(spec, jobs)
+        j = 0
+        for _, plans in pending:
+            per_rep = []
+            for plan in plans:
+                if plan is None:  # Un: one whole block, value as is
+                    per_rep.append(vals[j][0])
+                else:
+                    per_rep.append(Bk.finish_un(plan, vals[j]))
+                j += 1
+            results.append(per_rep[0] if estimator is not UnNT else np.mean(per_rep))
+        jobs, pending, size = [], [], 0
+
+    for t in range(n_tries):
+        X = np.asarray(gen_X())
+        Z = np.asarray(gen_Z())
+        plans = []
+        for _ in range(reps):
+            if estimator is Un:
+                jobs.append((X, Z, [Bk.whole(X, Z)]))
+                plans.append(None)
+            else:
+                plan = Bk.plan_un(X, Z, N, spec, sampling_type, "est")
+                blocks = [p[1] for p in plan if p[0] == "val"]
+                jobs.append((X.copy(), Z.copy(), blocks))  # later repetitions reshuffle X, Z
+                plans.append(plan)
+            size += X.size + Z.size
+        pending.append((t, plans))
+        if size >= flush_elems:
+            flush()
+    if jobs:
+        flush()
+    return results
