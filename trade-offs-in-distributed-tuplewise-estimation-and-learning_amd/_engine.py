@@ -181,16 +181,23 @@ def count_complete(sh: Shards, mode: str = "gt", algo: str = "auto") -> np.ndarr
     return _counts_to_host(run(pred))
 
 
-def count_indexed(x_dev, z_dev, dtype_code: int, ix: np.ndarray, iz: np.ndarray,
-                  pair_off: np.ndarray, mode: str = "gt") -> np.ndarray:
-    """Per-shard counts over explicit (absolute) index pairs."""
+def _idx_dev(a):
+    """int64 index array on the device: device tensors pass through (callers cache them)."""
+    t = L.torch()
+    if isinstance(a, t.Tensor):
+        return a
+    return L.to_device(np.asarray(a, dtype=np.int64))
+
+
+def count_indexed(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray,
+                  mode: str = "gt", pair_off_dev=None) -> np.ndarray:
+    """Per-shard counts over explicit (absolute) index pairs (host or device index arrays)."""
     n = len(pair_off) - 1
     if n == 0:
         return np.zeros(0, dtype=np.uint64)
     t = L.torch()
-    ixd = L.to_device(np.asarray(ix, dtype=np.int64))
-    izd = L.to_device(np.asarray(iz, dtype=np.int64))
-    pod = L.to_device(np.asarray(pair_off, dtype=np.int64))
+    ixd, izd = _idx_dev(ix), _idx_dev(iz)
+    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
     max_pairs = int(np.diff(pair_off).max())
 
     def run(pred):
@@ -224,14 +231,14 @@ def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
     return out.cpu().numpy()
 
 
-def pair_sum_indexed(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 0.0):
+def pair_sum_indexed(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 0.0,
+                     pair_off_dev=None):
     n = len(pair_off) - 1
     if n == 0:
         return np.zeros(0)
     t = L.torch()
-    ixd = L.to_device(np.asarray(ix, dtype=np.int64))
-    izd = L.to_device(np.asarray(iz, dtype=np.int64))
-    pod = L.to_device(np.asarray(pair_off, dtype=np.int64))
+    ixd, izd = _idx_dev(ix), _idx_dev(iz)
+    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
     max_pairs = int(np.diff(pair_off).max())
     per = int(L.lib().tw_pair_sum_idx_work_per_shard(max_pairs))
     work = L.empty((per * n,), t.float64)

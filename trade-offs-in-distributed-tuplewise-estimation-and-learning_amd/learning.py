@@ -280,6 +280,13 @@ class _EvalCache:
 _CACHE = _EvalCache()
 
 
+def _pairs_dev(pairs):
+    a = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    off = np.array([0, a.shape[0]], dtype=np.int64)
+    return (L.to_device(np.ascontiguousarray(a[:, 0])), L.to_device(np.ascontiguousarray(a[:, 1])),
+            off, L.to_device(off))
+
+
 def _scores(A_dev, w):
     """A @ w on the device (tw_gemv_f64)."""
     t = L.torch()
@@ -320,15 +327,15 @@ def evaluation_step(i, X_s, Z_s, w, p_learn):
                         lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
         tZ = _CACHE.get("train_Z", p_learn["train_Z"],
                         lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-        pairs = _CACHE.get("pairs", p_learn["train_mon_pairs"],
-                           lambda p: np.asarray(p, dtype=np.int64).reshape(-1, 2))
+        # the monitor pairs live on the device for as long as p_learn holds the same list
+        ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
+        n_pairs = int(off[1])
         sx, sz = _scores(tX, w), _scores(tZ, w)
-        off = np.array([0, pairs.shape[0]], dtype=np.int64)
-        hinge = E.pair_sum_indexed(sx, sz, pairs[:, 0], pairs[:, 1], off, L.TW_KERN_HINGE,
-                                   float(margin))[0]
-        bc_AUC = np.float64(hinge / np.float64(pairs.shape[0])) + reg_term
-        cnt = E.count_indexed(sx, sz, L.TW_F64, pairs[:, 0], pairs[:, 1], off, "gt")[0]
-        br_AUC = E.ratio(cnt, pairs.shape[0])
+        hinge = E.pair_sum_indexed(sx, sz, ixd, izd, off, L.TW_KERN_HINGE, float(margin),
+                                   pair_off_dev=offd)[0]
+        bc_AUC = np.float64(hinge / np.float64(n_pairs)) + reg_term
+        cnt = E.count_indexed(sx, sz, L.TW_F64, ixd, izd, off, "gt", pair_off_dev=offd)[0]
+        br_AUC = E.ratio(cnt, n_pairs)
 
     eX = _CACHE.get("test_X", p_learn["test_X"],
                     lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
