@@ -109,6 +109,34 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup):
                        "rng": "device (Philox)", "graphs": True, "steps": steps}}
 
 
+def sgd_replay_steps_per_s(steps):
+    """learning_process in replay mode (NumPy's own draws, bit-identical to the reference)
+    at the C4 shape, no evaluation: host RNG (one native MT19937 batch per step) + index
+    upload + two kernels per step."""
+    import logging
+    import torch
+    import tuplewise.learning as lr
+    rng = np.random.RandomState(3)
+    X = np.hstack([rng.normal(size=(9117, 9)), np.ones((9117, 1))])
+    Z = np.hstack([rng.normal(0.5, 1, size=(702, 9)), np.ones((702, 1))])
+    p = {"n_it": steps, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": 25, "reg": 0.05,
+         "learning_rate": 0.01, "eval_mod": 10 ** 9, "w_init": rng.normal(size=(10, 1)),
+         "test_X": X[:10], "test_Z": Z[:10], "train_mon_pairs": [(0, 0)], "train_X": X,
+         "train_Z": Z}
+    logging.disable(logging.CRITICAL)
+    np.random.seed(0)
+    lr.learning_process(X, Z, dict(p, n_it=50))  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lr.learning_process(X, Z, p)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "config": {"n_X": 9117, "n_Z": 702, "d": 10, "N": 100, "B": 100,
+                       "reshuffle_mod": 25, "rng": "replay (NumPy legacy MT19937, bit-exact)",
+                       "steps": steps}}
+
+
 def pmc_traffic():
     """HBM bytes per count-kernel launch from the committed rocprofv3 --pmc summary of this
     exact workload (profiles/*count_pmc*.json), or None."""
@@ -258,6 +286,7 @@ def main():
         out["secondary"] = {
             "metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)",
             "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2),
+            "C4_shuttle_shape_replay": sgd_replay_steps_per_s(2000),
             "C5_scaled_d512": sgd_steps_per_s(1_000_000, 1_000_000, 512, 256, 100, 25, 500, 2),
             "C5_scaled_d512_B4096": sgd_steps_per_s(1_000_000, 1_000_000, 512, 256, 4096, 25,
                                                     100, 1),

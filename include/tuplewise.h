@@ -197,6 +197,10 @@ int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream);
 int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
                         const int64_t* high, const int64_t* cnt, int64_t* out);
 int tw_np_mt_next32(uint32_t* key, int32_t* pos, int64_t cnt, uint32_t* out);
+/* grad_inc_block's draws for every shard of one UN_split call: for s < N, randint(0,kx,B)
+ * into ix[s*B..] then randint(0,kz,B) into iz[s*B..].  Returns 1 if kx or kz <= 0. */
+int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
+                        int64_t B, int64_t* ix, int64_t* iz);
 
 #ifdef __cplusplus
 }

@@ -34,3 +34,44 @@ def test_randint_batch_empty_range_raises_like_numpy(tw):
     with pytest.raises(ValueError):
         np.random.randint(4, 4, 1)
     assert np.random.random() == after
+
+
+@pytest.mark.parametrize("N,kx,kz,B", [(100, 91, 7, 100), (3, 1, 5, 17), (2, 2 ** 33, 3, 4)])
+def test_session_pairs_match_grad_inc_block_draws(tw, N, kx, kz, B):
+    """Session.pairs == the per-shard randint(0,kx,B), randint(0,kz,B) calls of
+    grad_inc_block (compute_stats.py:155-156), and the state written back matches."""
+    from tuplewise.numpy_rng import Session
+    np.random.seed(99)
+    np.random.random(5)  # start mid-block
+    want_x, want_z = [], []
+    for _ in range(N):
+        want_x.append(np.random.randint(0, kx, B))
+        want_z.append(np.random.randint(0, kz, B))
+    probe_want = np.random.random()
+    np.random.seed(99)
+    np.random.random(5)
+    ix = np.empty((N, B), np.int64)
+    iz = np.empty((N, B), np.int64)
+    with Session() as s:
+        s.pairs(N, kx, kz, B, ix, iz)
+    assert np.array_equal(ix, np.stack(want_x)) and np.array_equal(iz, np.stack(want_z))
+    assert np.random.random() == probe_want
+
+
+def test_session_flat_draws_commit_and_reacquire(tw):
+    from tuplewise.numpy_rng import Session
+    np.random.seed(7)
+    a = np.random.randint(0, 9117, 91 * 3)
+    mid = np.random.normal()  # foreign draw between session phases (touches has_gauss)
+    b = np.random.randint(-3, 702, 50)
+    end = np.random.random()
+    np.random.seed(7)
+    s = Session()
+    ga = s.randint_flat([0, 0, 0], [9117] * 3, [91] * 3)
+    s.commit()
+    gmid = np.random.normal()
+    s.acquire()
+    gb = s.randint_flat([-3], [702], [50])
+    s.commit()
+    assert np.array_equal(ga, a) and gmid == mid and np.array_equal(gb, b)
+    assert np.random.random() == end

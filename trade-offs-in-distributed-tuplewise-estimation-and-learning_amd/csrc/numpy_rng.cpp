@@ -26,8 +26,10 @@ constexpr int kN = 624, kM = 397;
 constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
 
 struct MT {
-  uint32_t* key;  // caller-owned 624 words
+  uint32_t* key;  // caller-owned 624 words (NumPy's untempered state)
   int pos;
+  uint32_t tmp[kN];  // tempered outputs of the current state block
+  int tempered_upto = 0;  // tmp[0, tempered_upto) valid for the current block
 
   void generate() {
     int i = 0;
@@ -43,16 +45,29 @@ struct MT {
     y = (key[kN - 1] & kUpper) | (key[0] & kLower);
     key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
     pos = 0;
+    tempered_upto = 0;
   }
 
-  uint32_t next32() {
-    if (pos >= kN) generate();
-    uint32_t y = key[pos++];
+  static inline uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
+  }
+
+  // make tmp[pos, kN) valid (vectorisable loop over the rest of the block)
+  inline void temper_rest() {
+    if (tempered_upto < kN) {
+      const int from = pos > tempered_upto ? pos : tempered_upto;
+      for (int i = from; i < kN; ++i) tmp[i] = temper(key[i]);
+      tempered_upto = kN;
+    }
+  }
+
+  uint32_t next32() {
+    if (pos >= kN) generate();
+    return temper(key[pos++]);
   }
 
   uint64_t next64() {
@@ -83,12 +98,21 @@ void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) 
       for (int64_t i = 0; i < cnt; ++i) out[i] = (int64_t)((uint64_t)low + mt.next32());
       return;
     }
+    // masked rejection, branch-free: every raw draw is written, the slot advances only when
+    // the draw is accepted; raw draws come from a pre-tempered 624-word block
     const uint32_t mask = (uint32_t)gen_mask(rng);
-    for (int64_t i = 0; i < cnt; ++i) {
-      uint32_t v;
-      while ((v = (mt.next32() & mask)) > (uint32_t)rng) {
+    const uint32_t r32 = (uint32_t)rng;
+    int64_t o = 0;
+    while (o < cnt) {
+      if (mt.pos >= kN) mt.generate();
+      mt.temper_rest();
+      int p = mt.pos;
+      while (p < kN && o < cnt) {
+        const uint32_t v = mt.tmp[p++] & mask;
+        out[o] = (int64_t)((uint64_t)low + v);
+        o += (v <= r32);
       }
-      out[i] = (int64_t)((uint64_t)low + v);
+      mt.pos = p;
     }
     return;
   }
@@ -111,7 +135,9 @@ extern "C" {
 // ValueError "high <= low"), leaving the state where the failing call would have started.
 int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
                         const int64_t* high, const int64_t* cnt, int64_t* out) {
-  MT mt{key, *pos};
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
   int64_t o = 0;
   for (int32_t c = 0; c < n_calls; ++c) {
     if (high[c] <= low[c]) {
@@ -125,9 +151,27 @@ int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int6
   return 0;
 }
 
+// grad_inc_block's draws for all N shards of one UN_split call (compute_stats.py:155-156):
+// for s in 0..N-1: ix[s*B .. s*B+B) = randint(0, kx, B), then iz[s*B ..) = randint(0, kz, B).
+int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
+                        int64_t B, int64_t* ix, int64_t* iz) {
+  if (kx <= 0 || kz <= 0) return 1;
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  for (int32_t s = 0; s < N; ++s) {
+    randint_fill(mt, 0, kx, B, ix + (int64_t)s * B);
+    randint_fill(mt, 0, kz, B, iz + (int64_t)s * B);
+  }
+  *pos = mt.pos;
+  return 0;
+}
+
 // Raw genrand_int32 stream (for tests).
 int tw_np_mt_next32(uint32_t* key, int32_t* pos, int64_t cnt, uint32_t* out) {
-  MT mt{key, *pos};
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
   for (int64_t i = 0; i < cnt; ++i) out[i] = mt.next32();
   *pos = mt.pos;
   return 0;

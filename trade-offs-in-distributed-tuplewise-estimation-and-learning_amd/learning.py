@@ -24,7 +24,7 @@ from . import _engine as E
 from . import _lib as L
 from . import _learn
 from . import compute_stats as cs
-from .numpy_rng import randint_batch
+from .numpy_rng import Session
 
 SEED_SHUFFLE = 42
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
@@ -89,9 +89,12 @@ class SGDEngine:
         L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
                self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr), s)
 
-    def step(self, ix: np.ndarray, iz: np.ndarray):
-        """Replay mode: ix, iz are the (N, B) NumPy draws of every shard."""
-        ixd, izd = L.to_device(self._local(ix)), L.to_device(self._local(iz))
+    def step(self, ix, iz):
+        """Replay mode: ix, iz are the (N, B) NumPy draws of every shard (host arrays or
+        device tensors)."""
+        t = self.t
+        ixd = self._local(ix) if isinstance(ix, t.Tensor) else L.to_device(self._local(ix))
+        izd = self._local(iz) if isinstance(iz, t.Tensor) else L.to_device(self._local(iz))
         L.call("tw_hinge_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x), self.kx,
                L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N_loc, self.B,
                L.ptr(self.w), self.margin, L.ptr(self.grads_loc), L.stream_handle())
@@ -165,19 +168,41 @@ def _dev_f64(a):
     return L.to_device(np.asarray(a, dtype=np.float64))
 
 
-def _swr_rows(n_X, n_Z, N):
-    """The index draws of SWR_divide (compute_stats.py:48-54), same order, in one native
-    call (tuplewise.numpy_rng: NumPy's own MT19937 stream and randint algorithm)."""
-    kx, kz = int(n_X / N), int(n_Z / N)
-    out = randint_batch([(0, n_X, kx)] * N + [(0, n_Z, kz)] * N)
-    return out[:N], out[N:]
+class _ReplayDraws:
+    """NumPy's own draws for the replay loop, made natively (tuplewise.numpy_rng.Session):
+    SWR_divide's rows (compute_stats.py:52-53) and grad_inc_block's pairs (:155-156).  Pair
+    draws go into one of two pinned host buffers and ship with one asynchronous H2D copy, so
+    the host draws step i+1 while the device runs step i."""
 
+    def __init__(self, N, kx, kz, B):
+        t = L.torch()
+        self.N, self.kx, self.kz, self.B = N, kx, kz, B
+        self.host = [t.empty((2, N, B), dtype=t.int64, pin_memory=True) for _ in range(2)]
+        self.hnp = [h.numpy() for h in self.host]
+        self.dev = [L.empty((2, N, B), t.int64) for _ in range(2)]
+        self.done = [None, None]  # event: the copy out of host[k] has finished
+        self.k = 0
+        self.rng = Session()
 
-def _pair_draws(N, kx, kz, B):
-    """grad_inc_block's draws for every shard of one UN_split call (compute_stats.py:155-156:
-    X indices then Z indices, shard by shard) as two (N, B) arrays."""
-    out = randint_batch([(0, kx, B), (0, kz, B)] * N)
-    return np.stack(out[0::2]), np.stack(out[1::2])
+    def swr_rows(self, n_X, n_Z):
+        N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
+        flat = self.rng.randint_flat([0] * (2 * N), [n_X] * N + [n_Z] * N, [kx] * N + [kz] * N)
+        return list(flat[:N * kx].reshape(N, kx)), list(flat[N * kx:].reshape(N, kz))
+
+    def pairs(self):
+        t = L.torch()
+        k = self.k
+        self.k ^= 1
+        if self.done[k] is not None:
+            self.done[k].synchronize()
+        h = self.hnp[k]
+        self.rng.pairs(self.N, self.kx, self.kz, self.B, h[0], h[1])
+        # stream-ordered: dev[k]'s previous reader (two steps back) precedes this copy
+        self.dev[k].copy_(self.host[k], non_blocking=True)
+        if self.done[k] is None:
+            self.done[k] = t.cuda.Event()
+        self.done[k].record()
+        return self.dev[k][0], self.dev[k][1]
 
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
@@ -216,27 +241,29 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs)
     if rng_mode != "replay":
         raise ValueError(f"rng_mode must be 'replay' or 'device', not {rng_mode!r}")
-    rows_x, rows_z = _swr_rows(n_X, n_Z, N)  # the reference's redundant initial draw (:119)
-    eng.set_shards(rows_x, rows_z)
-    kx, kz = eng.kx, eng.kz
-
-    for i in range(0, p_learn["n_it"]):
-        if i % p_learn["reshuffle_mod"] == 0:
-            rows_x, rows_z = _swr_rows(n_X, n_Z, N)
-            eng.set_shards(rows_x, rows_z)
-        if i % p_learn["eval_mod"] == 0:
-            w = eng.w_host()
-            if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
-                X_s = [X[r] for r in rows_x]
-                Z_s = [Z[r] for r in rows_z]
-            else:
-                X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
-            evaluation_step(i, X_s, Z_s, w, p_learn)
-        if trajectory is not None:
-            trajectory.append(eng.w_host())
-        ix, iz = _pair_draws(N, kx, kz, B)
-        assert optim_type in ["SGD", "momentum"]
-        eng.step(ix, iz)
+    draws = _ReplayDraws(N, eng.kx, eng.kz, B)
+    with draws.rng:  # the global RNG state lives natively until the loop ends
+        rows_x, rows_z = draws.swr_rows(n_X, n_Z)  # the reference's redundant draw (:119)
+        eng.set_shards(rows_x, rows_z)
+        for i in range(0, p_learn["n_it"]):
+            if i % p_learn["reshuffle_mod"] == 0:
+                rows_x, rows_z = draws.swr_rows(n_X, n_Z)
+                eng.set_shards(rows_x, rows_z)
+            if i % p_learn["eval_mod"] == 0:
+                w = eng.w_host()
+                if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
+                    X_s = [X[r] for r in rows_x]
+                    Z_s = [Z[r] for r in rows_z]
+                else:
+                    X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
+                draws.rng.commit()  # np.random is consistent while foreign code runs
+                evaluation_step(i, X_s, Z_s, w, p_learn)
+                draws.rng.acquire()
+            if trajectory is not None:
+                trajectory.append(eng.w_host())
+            ix, iz = draws.pairs()
+            assert optim_type in ["SGD", "momentum"]
+            eng.step(ix, iz)
     return None
 
 

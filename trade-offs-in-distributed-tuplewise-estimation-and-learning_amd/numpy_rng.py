@@ -15,6 +15,7 @@ from . import _lib as L
 
 
 def randint_batch(calls) -> list:
+    """[np.random.randint(lo, hi, n) for lo, hi, n in calls], one native call."""
     calls = list(calls)
     if not calls:
         return []
@@ -35,4 +36,57 @@ def randint_batch(calls) -> list:
     np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
     if bad:
         raise ValueError("high <= low")
-    return np.split(out, np.cumsum(cnt)[:-1])
+    offs = np.concatenate([[0], np.cumsum(cnt)])
+    return [out[offs[i]:offs[i + 1]] for i in range(len(cnt))]
+
+
+class Session:
+    """NumPy's legacy global MT19937 state held in native code for a run of draws.
+
+    While a session is open nothing else may draw from np.random; commit() writes the
+    advanced state back (and is called on exit).  acquire() re-reads it after foreign draws.
+    Every draw equals the corresponding np.random.randint call bit for bit."""
+
+    def __init__(self):
+        self.acquire()
+
+    def acquire(self):
+        name, key, pos, self._has_gauss, self._gauss = np.random.get_state(legacy=True)
+        if name != "MT19937":
+            raise NotImplementedError("only the MT19937 legacy RandomState is supported")
+        self._key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+        self._pos = ctypes.c_int32(int(pos))
+
+    def commit(self):
+        np.random.set_state(("MT19937", self._key, self._pos.value, self._has_gauss,
+                             self._gauss))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.commit()
+        return False
+
+    def randint_flat(self, low, high, cnt, out=None) -> np.ndarray:
+        """Consecutive randint(low[c], high[c], cnt[c]) calls, concatenated."""
+        low = np.ascontiguousarray(low, dtype=np.int64)
+        high = np.ascontiguousarray(high, dtype=np.int64)
+        cnt = np.ascontiguousarray(cnt, dtype=np.int64)
+        if out is None:
+            out = np.empty(int(cnt.sum()), dtype=np.int64)
+        rc = L.lib().tw_np_randint_batch(self._key.ctypes.data, ctypes.byref(self._pos),
+                                         len(cnt), low.ctypes.data, high.ctypes.data,
+                                         cnt.ctypes.data, out.ctypes.data)
+        if rc:
+            raise ValueError("high <= low")
+        return out
+
+    def pairs(self, N, kx, kz, B, ix, iz):
+        """grad_inc_block's draws of all N shards into int64 arrays ix, iz of shape (N, B)."""
+        assert ix.flags.c_contiguous and iz.flags.c_contiguous
+        rc = L.lib().tw_np_randint_pairs(self._key.ctypes.data, ctypes.byref(self._pos),
+                                         int(N), int(kx), int(kz), int(B), ix.ctypes.data,
+                                         iz.ctypes.data)
+        if rc:
+            raise ValueError("high <= low")
