@@ -187,6 +187,24 @@ int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int64_t n, int6
                       void* stream);
 int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream);
 
+/* ---- (e): row exchange for the row-partitioned learning layout ------------------------
+ * Replaces the row copies of SWR_divide (compute_stats.py:48-54) when X is split by rows over
+ * G ranks.  d_rows: the M = N*k global row indices of all N shards (shard-major; identical on
+ * every rank).  Requester q owns positions [q*M_q, (q+1)*M_q).  This rank owns matrix rows
+ * [lo, hi), stored row-major as d_part ((hi-lo) x d).
+ * tw_row_route_counts: d_counts[q] = #positions of q whose row lies in [lo, hi).
+ * tw_row_pack: one record of d+1 doubles per such position into d_send — the row, then the
+ *   requester-local position bit-cast to a double — requester q's records occupying
+ *   [d_start[q], d_start[q] + d_counts[q]) (order inside a bucket unspecified); d_cursor: G
+ *   int64 of scratch.  G <= 1024.
+ * tw_row_unpack: d_out[pos*d + c] = record[c] for m received records. */
+int tw_row_route_counts(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo, int64_t hi,
+                        int32_t G, int64_t* d_counts, void* stream);
+int tw_row_pack(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo, int64_t hi, int32_t G,
+                const double* d_part, int64_t d, const int64_t* d_start, int64_t* d_cursor,
+                double* d_send, void* stream);
+int tw_row_unpack(const double* d_rec, int64_t m, int64_t d, double* d_out, void* stream);
+
 /* ---- f2: bulk draws of NumPy's legacy global RNG (host code, no GPU) ------------------
  * key (624 words) / pos: the MT19937 state of np.random.get_state(), advanced in place.
  * tw_np_randint_batch: n_calls consecutive RandomState.randint(low[c], high[c], cnt[c]) calls

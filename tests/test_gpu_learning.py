@@ -120,3 +120,59 @@ def test_make_exps_writes_reference_schema(gpu, golden, tmp_path):
     assert "it     0: bc_AUC = " in log and "#X: " in log
     for h in logging.root.handlers[:]:
         logging.root.removeHandler(h)
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_partitioned_layout_equals_replicated(gpu, golden, mode):
+    """x_layout="partitioned" (rows exchanged at each reshuffle) changes no arithmetic."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for layout in ("replicated", "partitioned"):
+        p = _p_learn(golden, n_it=60)
+        traj = []
+        np.random.seed(31)
+        lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=traj,
+                            rng_mode=mode, x_layout=layout)
+        out[layout] = (np.stack(traj), p["bc_AUC"], p["tc_AUC"])
+    assert np.array_equal(out["replicated"][0], out["partitioned"][0])
+    assert out["replicated"][1:] == out["partitioned"][1:]
+
+
+def test_row_exchange_kernels_simulated_ranks(gpu):
+    """tw_row_route_counts / tw_row_pack / tw_row_unpack for G=3 owners simulated in one
+    process (the all_to_all is a host-side regrouping): every requester's matrix == X[rows]."""
+    import torch
+    from tuplewise import _lib as L
+    rng = np.random.RandomState(5)
+    n, d, N, k, G = 1001, 13, 6, 37, 3
+    X = rng.normal(size=(n, d))
+    rows = rng.randint(0, n, size=N * k).astype(np.int64)
+    rows[:5] = [0, n - 1, n // 3, n // 3 - 1, 2 * n // 3]  # owner boundaries
+    M, M_q = N * k, (N // G) * k
+    rows_d = L.to_device(rows)
+    buckets = [[] for _ in range(G)]
+    for r in range(G):
+        lo, hi = r * n // G, (r + 1) * n // G
+        part = L.to_device(X[lo:hi])
+        counts = L.empty((G,), torch.int64)
+        L.call("tw_row_route_counts", L.ptr(rows_d), M, M_q, lo, hi, G, L.ptr(counts),
+               L.stream_handle())
+        c = counts.cpu().numpy()
+        owned = (rows >= lo) & (rows < hi)
+        assert np.array_equal(c, owned.reshape(G, M_q).sum(1))
+        start = torch.cumsum(counts, 0) - counts
+        send = L.empty((max(int(c.sum()), 1), d + 1), torch.float64)
+        cursor = L.empty((G,), torch.int64)
+        L.call("tw_row_pack", L.ptr(rows_d), M, M_q, lo, hi, G, L.ptr(part), d, L.ptr(start),
+               L.ptr(cursor), L.ptr(send), L.stream_handle())
+        s = send.cpu().numpy()
+        off = np.concatenate([[0], np.cumsum(c)])
+        for q in range(G):
+            buckets[q].append(s[off[q]:off[q + 1]])
+    for q in range(G):
+        recv = L.to_device(np.concatenate(buckets[q]))
+        assert recv.shape[0] == M_q
+        out = L.empty((M_q, d), torch.float64)
+        L.call("tw_row_unpack", L.ptr(recv), M_q, d, L.ptr(out), L.stream_handle())
+        assert np.array_equal(out.cpu().numpy(), X[rows[q * M_q:(q + 1) * M_q]])

@@ -16,7 +16,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _learn_worker(rank, port, G, mode, q):
+def _learn_worker(rank, port, G, mode, q, layout="replicated"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -26,7 +26,8 @@ def _learn_worker(rank, port, G, mode, q):
     X, Z, w0, p = _problem()
     traj = []
     np.random.seed(99)
-    lr.learning_process(X, Z, p, rng_mode=mode, trajectory=traj, group=dist.group.WORLD)
+    lr.learning_process(X, Z, p, rng_mode=mode, trajectory=traj, group=dist.group.WORLD,
+                        x_layout=layout)
     if rank == 0:
         q.put(np.stack(traj))
     dist.barrier()
@@ -47,8 +48,9 @@ def _problem():
     return X, Z, w0, p
 
 
+@pytest.mark.parametrize("layout", ["replicated", "partitioned"])
 @pytest.mark.parametrize("mode", ["replay", "device"])
-def test_learning_two_ranks_equals_one(gpu, mode):
+def test_learning_two_ranks_equals_one(gpu, mode, layout):
     import torch.multiprocessing as mp
     import tuplewise.learning as lr
     X, Z, w0, p = _problem()
@@ -58,7 +60,8 @@ def test_learning_two_ranks_equals_one(gpu, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_learn_worker, args=(r, port, 2, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_learn_worker, args=(r, port, 2, mode, q, layout))
+             for r in range(2)]
     for pr in procs:
         pr.start()
     got = q.get(timeout=300)

@@ -75,3 +75,23 @@ def test_session_flat_draws_commit_and_reacquire(tw):
     s.commit()
     assert np.array_equal(ga, a) and gmid == mid and np.array_equal(gb, b)
     assert np.random.random() == end
+
+
+def test_scalar_path_matches_numpy(tw):
+    """The portable (non-AVX2) compaction, forced in a fresh process, against np.random."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, tuplewise\n"
+        "from tuplewise.numpy_rng import Session, randint_batch\n"
+        "np.random.seed(3); w=[np.random.randint(0,k,100) for _ in range(40) for k in (91,7)]\n"
+        "np.random.seed(3); ix=np.empty((40,100),np.int64); iz=np.empty((40,100),np.int64)\n"
+        "s=Session(); s.pairs(40,91,7,100,ix,iz); s.commit()\n"
+        "assert np.array_equal(ix, np.stack(w[0::2])) and np.array_equal(iz, np.stack(w[1::2]))\n"
+        "print('ok')\n")
+    env = dict(os.environ, TW_NP_RNG_SCALAR="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr

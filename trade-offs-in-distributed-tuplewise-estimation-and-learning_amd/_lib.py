@@ -50,6 +50,9 @@ _SIGNATURES = {
     "tw_rank_histogram": [_vp, _i64, _i64, _i32, _vp, _vp],
     "tw_bucket_scatter": [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
     "tw_scatter_records": [_vp, _i64, _vp, _vp],
+    "tw_row_route_counts": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
+    "tw_row_pack": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp],
+    "tw_row_unpack": [_vp, _i64, _i64, _vp, _vp],
     "tw_np_randint_batch": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],

@@ -17,8 +17,16 @@
 //     rng == 2^32-1     -> low + next32;
 //     rng >= 2^32       -> masked rejection on 64-bit draws (hi32 << 32 | lo32).
 // Parity is pinned by tests/test_numpy_rng.py against np.random itself.
+//
+// Speed: the 624-word block is generated and tempered with vector loops, and the masked
+// rejection is a left-pack of accepted draws (8 lanes at a time with AVX2, chosen at run time
+// by __builtin_cpu_supports; scalar branch-free compaction otherwise).
+#include <immintrin.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+#define TW_INLINE inline __attribute__((always_inline))
 
 namespace {
 
@@ -31,7 +39,7 @@ struct MT {
   uint32_t tmp[kN];  // tempered outputs of the current state block
   int tempered_upto = 0;  // tmp[0, tempered_upto) valid for the current block
 
-  void generate() {
+  TW_INLINE void generate() {
     int i = 0;
     uint32_t y;
     for (; i < kN - kM; ++i) {
@@ -57,7 +65,7 @@ struct MT {
   }
 
   // make tmp[pos, kN) valid (vectorisable loop over the rest of the block)
-  inline void temper_rest() {
+  TW_INLINE void temper_rest() {
     if (tempered_upto < kN) {
       const int from = pos > tempered_upto ? pos : tempered_upto;
       for (int i = from; i < kN; ++i) tmp[i] = temper(key[i]);
@@ -87,7 +95,48 @@ inline uint64_t gen_mask(uint64_t max) {
   return m;
 }
 
-void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) {
+// lane indices of the accepted lanes of an 8-bit accept mask, packed to the front
+struct PackLut {
+  uint32_t idx[256][8];
+  PackLut() {
+    for (int m = 0; m < 256; ++m) {
+      int k = 0;
+      for (int l = 0; l < 8; ++l)
+        if (m >> l & 1) idx[m][k++] = (uint32_t)l;
+      for (; k < 8; ++k) idx[m][k] = 0;
+    }
+  }
+};
+const PackLut g_pack;
+
+// 8 raw draws at a time: accept v = tmp & mask iff v <= r32, left-pack, widen, add low.
+// Needs cnt - o >= 8 for the unconditional 8-wide store.  Returns the new p (o updated).
+__attribute__((target("avx2,popcnt"))) inline int pack8_avx2(const uint32_t* tmp, int p,
+                                                             uint32_t mask, uint32_t r32,
+                                                             int64_t low, int64_t cnt,
+                                                             int64_t* out, int64_t& o) {
+  const __m256i vm = _mm256_set1_epi32((int)mask);
+  const __m256i sign = _mm256_set1_epi32((int)0x80000000u);
+  const __m256i vr = _mm256_set1_epi32((int)(r32 ^ 0x80000000u));
+  const __m256i vlow = _mm256_set1_epi64x(low);
+  while (p + 8 <= kN && cnt - o >= 8) {
+    const __m256i v = _mm256_and_si256(_mm256_loadu_si256((const __m256i*)(tmp + p)), vm);
+    const __m256i rej = _mm256_cmpgt_epi32(_mm256_xor_si256(v, sign), vr);  // unsigned v > r
+    const int acc = ~_mm256_movemask_ps(_mm256_castsi256_ps(rej)) & 0xFF;
+    const __m256i packed = _mm256_permutevar8x32_epi32(
+        v, _mm256_loadu_si256((const __m256i*)g_pack.idx[acc]));
+    const __m256i lo4 = _mm256_cvtepu32_epi64(_mm256_castsi256_si128(packed));
+    const __m256i hi4 = _mm256_cvtepu32_epi64(_mm256_extracti128_si256(packed, 1));
+    _mm256_storeu_si256((__m256i*)(out + o), _mm256_add_epi64(lo4, vlow));
+    _mm256_storeu_si256((__m256i*)(out + o + 4), _mm256_add_epi64(hi4, vlow));
+    o += __builtin_popcount((unsigned)acc);
+    p += 8;
+  }
+  return p;
+}
+
+template <bool kAvx2>
+TW_INLINE void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) {
   const uint64_t rng = (uint64_t)(high - 1) - (uint64_t)low;
   if (rng == 0) {
     for (int64_t i = 0; i < cnt; ++i) out[i] = low;
@@ -98,8 +147,8 @@ void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) 
       for (int64_t i = 0; i < cnt; ++i) out[i] = (int64_t)((uint64_t)low + mt.next32());
       return;
     }
-    // masked rejection, branch-free: every raw draw is written, the slot advances only when
-    // the draw is accepted; raw draws come from a pre-tempered 624-word block
+    // masked rejection: every raw draw is written, the slot advances only when the draw is
+    // accepted; raw draws come from a pre-tempered 624-word block
     const uint32_t mask = (uint32_t)gen_mask(rng);
     const uint32_t r32 = (uint32_t)rng;
     int64_t o = 0;
@@ -107,6 +156,7 @@ void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) 
       if (mt.pos >= kN) mt.generate();
       mt.temper_rest();
       int p = mt.pos;
+      if (kAvx2) p = pack8_avx2(mt.tmp, p, mask, r32, low, cnt, out, o);
       while (p < kN && o < cnt) {
         const uint32_t v = mt.tmp[p++] & mask;
         out[o] = (int64_t)((uint64_t)low + v);
@@ -125,6 +175,68 @@ void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) 
   }
 }
 
+template <bool kAvx2>
+TW_INLINE int batch_body(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
+                         const int64_t* high, const int64_t* cnt, int64_t* out) {
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  int64_t o = 0;
+  for (int32_t c = 0; c < n_calls; ++c) {
+    if (high[c] <= low[c]) {
+      *pos = mt.pos;
+      return 1;
+    }
+    randint_fill<kAvx2>(mt, low[c], high[c], cnt[c], out + o);
+    o += cnt[c];
+  }
+  *pos = mt.pos;
+  return 0;
+}
+
+template <bool kAvx2>
+TW_INLINE void pairs_body(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
+                          int64_t B, int64_t* ix, int64_t* iz) {
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  for (int32_t s = 0; s < N; ++s) {
+    randint_fill<kAvx2>(mt, 0, kx, B, ix + (int64_t)s * B);
+    randint_fill<kAvx2>(mt, 0, kz, B, iz + (int64_t)s * B);
+  }
+  *pos = mt.pos;
+}
+
+int batch_generic(uint32_t* key, int32_t* pos, int32_t n, const int64_t* lo, const int64_t* hi,
+                  const int64_t* cnt, int64_t* out) {
+  return batch_body<false>(key, pos, n, lo, hi, cnt, out);
+}
+__attribute__((target("avx2,popcnt"))) int batch_avx2(uint32_t* key, int32_t* pos, int32_t n,
+                                                      const int64_t* lo, const int64_t* hi,
+                                                      const int64_t* cnt, int64_t* out) {
+  return batch_body<true>(key, pos, n, lo, hi, cnt, out);
+}
+void pairs_generic(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B,
+                   int64_t* ix, int64_t* iz) {
+  pairs_body<false>(key, pos, N, kx, kz, B, ix, iz);
+}
+__attribute__((target("avx2,popcnt"))) void pairs_avx2(uint32_t* key, int32_t* pos, int32_t N,
+                                                       int64_t kx, int64_t kz, int64_t B,
+                                                       int64_t* ix, int64_t* iz) {
+  pairs_body<true>(key, pos, N, kx, kz, B, ix, iz);
+}
+
+// TW_NP_RNG_SCALAR=1 forces the portable path (tests compare both)
+bool use_avx2() {
+  static const int v = [] {
+    const char* e = getenv("TW_NP_RNG_SCALAR");
+    if (e && e[0] == '1') return 0;
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("popcnt") ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -135,20 +247,8 @@ extern "C" {
 // ValueError "high <= low"), leaving the state where the failing call would have started.
 int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
                         const int64_t* high, const int64_t* cnt, int64_t* out) {
-  MT mt;
-  mt.key = key;
-  mt.pos = *pos;
-  int64_t o = 0;
-  for (int32_t c = 0; c < n_calls; ++c) {
-    if (high[c] <= low[c]) {
-      *pos = mt.pos;
-      return 1;
-    }
-    randint_fill(mt, low[c], high[c], cnt[c], out + o);
-    o += cnt[c];
-  }
-  *pos = mt.pos;
-  return 0;
+  return use_avx2() ? batch_avx2(key, pos, n_calls, low, high, cnt, out)
+                    : batch_generic(key, pos, n_calls, low, high, cnt, out);
 }
 
 // grad_inc_block's draws for all N shards of one UN_split call (compute_stats.py:155-156):
@@ -156,14 +256,10 @@ int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int6
 int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
                         int64_t B, int64_t* ix, int64_t* iz) {
   if (kx <= 0 || kz <= 0) return 1;
-  MT mt;
-  mt.key = key;
-  mt.pos = *pos;
-  for (int32_t s = 0; s < N; ++s) {
-    randint_fill(mt, 0, kx, B, ix + (int64_t)s * B);
-    randint_fill(mt, 0, kz, B, iz + (int64_t)s * B);
-  }
-  *pos = mt.pos;
+  if (use_avx2())
+    pairs_avx2(key, pos, N, kx, kz, B, ix, iz);
+  else
+    pairs_generic(key, pos, N, kx, kz, B, ix, iz);
   return 0;
 }
 

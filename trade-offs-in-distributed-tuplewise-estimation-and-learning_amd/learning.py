@@ -41,9 +41,16 @@ class SGDEngine:
     replicated (n x d fp64 fits every MI355X's 288 GB up to n*d ~ 3e10), rank r owns shards
     [r*N/G, (r+1)*N/G); each step computes its shards' gradients, all-gathers the (N/G, d)
     partials in shard order (one RCCL all-gather) and applies the same shard-ordered update
-    on every rank — so w, and the whole trajectory, is identical for any G."""
+    on every rank — so w, and the whole trajectory, is identical for any G.
 
-    def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None):
+    x_layout="partitioned" is the other side of the memory/communication trade-off (SURVEY.md
+    §8(e)): rank r keeps only rows [r*n/G, (r+1)*n/G) of X and of Z, and every reshuffle moves
+    the drawn rows to the ranks whose shards drew them (tw_row_pack -> one all_to_all ->
+    tw_row_unpack into a shard-local matrix).  The gradient kernels then read the local matrix
+    through an identity row table, so the arithmetic — and the trajectory — is unchanged."""
+
+    def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None,
+                 x_layout="replicated"):
         """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is)."""
         t = L.torch()
         self.t = t
@@ -58,12 +65,28 @@ class SGDEngine:
             raise ValueError(f"N={N} shards do not split evenly over {self.G} ranks")
         self.N_loc = int(N) // self.G
         self.shard_base = self.rank * self.N_loc
-        self.X = _dev_f64(X)
-        self.Z = _dev_f64(Z)
-        self.n_X, self.d = self.X.shape
-        self.n_Z = self.Z.shape[0]
+        if x_layout not in ("replicated", "partitioned"):
+            raise ValueError(f"x_layout must be 'replicated' or 'partitioned', not {x_layout!r}")
+        self.layout = x_layout
+        self.n_X, self.d = int(X.shape[0]), int(X.shape[1])
+        self.n_Z = int(Z.shape[0])
         self.N, self.B = int(N), int(B)
         self.kx, self.kz = int(self.n_X / N), int(self.n_Z / N)
+        if x_layout == "replicated":
+            self.X = _dev_f64(X)
+            self.Z = _dev_f64(Z)
+        else:
+            G, r = self.G, self.rank
+            self.x_own = (r * self.n_X // G, (r + 1) * self.n_X // G)
+            self.z_own = (r * self.n_Z // G, (r + 1) * self.n_Z // G)
+            self.X_part = _dev_f64(X[self.x_own[0]:self.x_own[1]]).reshape(-1, self.d)
+            self.Z_part = _dev_f64(Z[self.z_own[0]:self.z_own[1]]).reshape(-1, self.d)
+            # the kernels read the shard-local matrices through identity row tables
+            self.X = L.empty((self.N_loc * self.kx, self.d), t.float64)
+            self.Z = L.empty((self.N_loc * self.kz, self.d), t.float64)
+            dev = self.X.device
+            self.ident_x = t.arange(self.N_loc * self.kx, device=dev).view(self.N_loc, self.kx)
+            self.ident_z = t.arange(self.N_loc * self.kz, device=dev).view(self.N_loc, self.kz)
         self.margin, self.reg, self.lr = float(margin), float(reg), float(learning_rate)
         self.momentum = 0.9 if optim_type == "momentum" else -1.0
         self.w_shape = tuple(w_init.shape)
@@ -79,8 +102,44 @@ class SGDEngine:
 
     def set_shards(self, rows_x, rows_z):
         """Replay mode: the full SWR draw (all N shards; identical on every rank)."""
+        if self.layout == "partitioned":
+            self._exchange(L.to_device(np.stack(rows_x).astype(np.int64).reshape(-1)), self.kx,
+                           self.X_part, self.x_own, self.X)
+            self._exchange(L.to_device(np.stack(rows_z).astype(np.int64).reshape(-1)), self.kz,
+                           self.Z_part, self.z_own, self.Z)
+            self.rows_x, self.rows_z = self.ident_x, self.ident_z
+            return
         self.rows_x = L.to_device(np.stack(self._local(rows_x)).astype(np.int64))
         self.rows_z = L.to_device(np.stack(self._local(rows_z)).astype(np.int64))
+
+    def _exchange(self, rows, k, part, own, out):
+        """Partitioned layout: move the rows drawn for this rank's shards (rows: all N*k global
+        row indices, shard-major) from their owners into `out` (N_loc*k, d), in draw order."""
+        t, G, d = self.t, self.G, self.d
+        s = L.stream_handle()
+        M, M_q = self.N * k, self.N_loc * k
+        counts = L.empty((G,), t.int64)
+        L.call("tw_row_route_counts", L.ptr(rows), M, M_q, own[0], own[1], G, L.ptr(counts), s)
+        start = t.cumsum(counts, 0) - counts
+        sc = counts.cpu().tolist()
+        total = int(sum(sc))
+        send = L.empty((max(total, 1), d + 1), t.float64)
+        cursor = L.empty((G,), t.int64)
+        L.call("tw_row_pack", L.ptr(rows), M, M_q, own[0], own[1], G, L.ptr(part), d,
+               L.ptr(start), L.ptr(cursor), L.ptr(send), s)
+        if G > 1:
+            rcounts = t.empty_like(counts)
+            self.dist.all_to_all_single(rcounts, counts, group=self.group)
+            rc = rcounts.cpu().tolist()
+            recv = L.empty((max(int(sum(rc)), 1), d + 1), t.float64)
+            self.dist.all_to_all_single(recv[:int(sum(rc))], send[:total], output_split_sizes=rc,
+                                        input_split_sizes=sc, group=self.group)
+            m = int(sum(rc))
+        else:
+            recv, m = send, total
+        if m != M_q:
+            raise RuntimeError(f"row exchange delivered {m} rows for {M_q} positions")
+        L.call("tw_row_unpack", L.ptr(recv), m, d, L.ptr(out), s)
 
     def _update(self):
         s = L.stream_handle()
@@ -111,12 +170,25 @@ class SGDEngine:
         t = self.t
         self.seed = int(seed) & (2 ** 64 - 1)
         self.step_ctr = t.zeros((1,), dtype=t.int64, device=self.w.device)
-        self.rows_x = t.empty((self.N_loc, self.kx), dtype=t.int64, device=self.w.device)
-        self.rows_z = t.empty((self.N_loc, self.kz), dtype=t.int64, device=self.w.device)
+        if self.layout == "partitioned":  # owners need every shard's draws
+            self.rows_all_x = t.empty((self.N, self.kx), dtype=t.int64, device=self.w.device)
+            self.rows_all_z = t.empty((self.N, self.kz), dtype=t.int64, device=self.w.device)
+            self.rows_x, self.rows_z = self.ident_x, self.ident_z
+        else:
+            self.rows_x = t.empty((self.N_loc, self.kx), dtype=t.int64, device=self.w.device)
+            self.rows_z = t.empty((self.N_loc, self.kz), dtype=t.int64, device=self.w.device)
         self._graphs = {}
 
     def reshuffle_device(self):
         s = L.stream_handle()
+        if self.layout == "partitioned":
+            L.call("tw_swr_rows_rng", L.ptr(self.rows_all_x), self.N, self.kx, self.n_X,
+                   self.seed, L.ptr(self.step_ctr), 0, 0, s)
+            L.call("tw_swr_rows_rng", L.ptr(self.rows_all_z), self.N, self.kz, self.n_Z,
+                   self.seed, L.ptr(self.step_ctr), 1, 0, s)
+            self._exchange(self.rows_all_x.view(-1), self.kx, self.X_part, self.x_own, self.X)
+            self._exchange(self.rows_all_z.view(-1), self.kz, self.Z_part, self.z_own, self.Z)
+            return
         L.call("tw_swr_rows_rng", L.ptr(self.rows_x), self.N_loc, self.kx, self.n_X, self.seed,
                L.ptr(self.step_ctr), 0, self.shard_base, s)
         L.call("tw_swr_rows_rng", L.ptr(self.rows_z), self.N_loc, self.kz, self.n_Z, self.seed,
@@ -132,6 +204,9 @@ class SGDEngine:
     def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True):
         """nsteps device-RNG steps (reshuffling first if asked), replayed from a captured
         hipGraph per distinct segment shape (eager when the step holds a collective)."""
+        if reshuffle_first and self.layout == "partitioned":
+            self.reshuffle_device()  # the exchange sizes its buffers on the host: not captured
+            reshuffle_first = False
         if not graphs or self.G > 1:
             if reshuffle_first:
                 self.reshuffle_device()
@@ -206,7 +281,7 @@ class _ReplayDraws:
 
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
-                     rng_mode="replay", graphs=True, group=None):
+                     rng_mode="replay", graphs=True, group=None, x_layout="replicated"):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference.
@@ -215,7 +290,9 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     steps between evaluations/reshuffles is one hipGraph replay.
     group: a torch.distributed group (one process per GPU); shards are spread over its ranks
     and the trajectory is identical to the single-GPU one.  Every rank must call with the
-    same inputs and the same NumPy global RNG state."""
+    same inputs and the same NumPy global RNG state.
+    x_layout: "replicated" (X, Z whole on every GPU; a reshuffle moves no data) or
+    "partitioned" (1/G of the rows per GPU; a reshuffle exchanges the drawn rows)."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -235,7 +312,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
 
     eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
-                    group=group)
+                    group=group, x_layout=x_layout)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs)
