@@ -35,6 +35,7 @@ ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 N_PER_CLASS = 1_000_000
+C5_N = 5_000_000  # n=1e7 rows (5e6/5e6), d=512 fp64 = 41 GB
 N_SHARDS = 64
 PEAK_LANE_OPS = 256 * 64 * 2.4e9  # 3.93e13 f64 vector lane-ops/s (MI355X_MICROARCH chip table)
 HBM_PEAK_GBS = 8000.0
@@ -74,10 +75,12 @@ def cpu_baseline(n, N, shards):
                       f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
 
 
-def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup):
+def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="replicated"):
     """Pairwise-hinge SGD steps/s (BASELINE metric, second half): learning_process's loop
     (make_exps.py:122-141) without evaluation, device-RNG mode, hipGraph-replayed segments.
-    Synthetic data of the given shape generated on the device."""
+    Synthetic data of the given shape generated on the device.  layout="partitioned" also
+    times one reshuffle's row exchange (route + pack + unpack; at N=1 GPU the all_to_all is
+    the identity, so this is the HBM side of the exchange)."""
     import torch
     from tuplewise.learning import SGDEngine
     g = torch.Generator(device="cuda").manual_seed(7)
@@ -85,7 +88,7 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup):
     Z = torch.randn((n_Z, d), dtype=torch.float64, device="cuda", generator=g) + 0.3
     w0 = torch.randn((d, 1), dtype=torch.float64, device="cuda", generator=g)
     eng = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
-                    optim_type="momentum")
+                    optim_type="momentum", x_layout=layout)
     eng.enable_device_rng(12345)
 
     def run(k):
@@ -101,12 +104,26 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup):
     run(steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
-            "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
-            "gather_GBps": N * B * 16 * d * steps / dt / 1e9,
-            "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B,
-                       "reshuffle_mod": reshuffle_mod, "optim": "momentum",
-                       "rng": "device (Philox)", "graphs": True, "steps": steps}}
+    out = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+           "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
+           "gather_GBps": N * B * 16 * d * steps / dt / 1e9,
+           "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B,
+                      "reshuffle_mod": reshuffle_mod, "optim": "momentum",
+                      "rng": "device (Philox)", "graphs": True, "steps": steps,
+                      "x_layout": layout}}
+    if layout == "partitioned":
+        reps = 3
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            eng.reshuffle_device()
+        torch.cuda.synchronize()
+        rs = (time.perf_counter() - t0) / reps
+        rows = N * (eng.kx + eng.kz)
+        moved = rows * 8 * (2 * d + 2 * (d + 1))  # pack: read row, write record; unpack: back
+        out["reshuffle_exchange"] = {"ms": rs * 1e3, "rows": rows, "bytes": moved,
+                                     "GBps": moved / rs / 1e9}
+    return out
 
 
 def sgd_replay_steps_per_s(steps):
@@ -287,9 +304,10 @@ def main():
             "metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)",
             "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2),
             "C4_shuttle_shape_replay": sgd_replay_steps_per_s(2000),
-            "C5_scaled_d512": sgd_steps_per_s(1_000_000, 1_000_000, 512, 256, 100, 25, 500, 2),
-            "C5_scaled_d512_B4096": sgd_steps_per_s(1_000_000, 1_000_000, 512, 256, 4096, 25,
-                                                    100, 1),
+            "C5_scaled_d512": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2),
+            "C5_scaled_d512_B4096": sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1),
+            "C5_scaled_d512_partitioned": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,
+                                                          1, layout="partitioned"),
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
