@@ -68,6 +68,24 @@ int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const void* d_z,
                    const int64_t* d_z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
                    int32_t dtype, int32_t pred, uint64_t* d_out, void* stream);
 
+/* One step of est.UnNT's loop (estimation-experiment/main.py:76-79) in ONE launch: the counts
+ * of the current partition exactly as tw_count_pairs — except that d_out must already be zero
+ * (the kernel accumulates into it) — and, on spare leading blocks of the same grid, the NEXT
+ * repartition: d_x_next = the n_x scores of d_x permuted with key_x, d_z_next likewise (as
+ * tw_permute_pair), and d_out_next[0 .. n_next_shards) zeroed for the next step.
+ * d_x_next == NULL: count only (d_out_next, if given, is zeroed by a memset). */
+int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                        const int64_t* d_z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
+                        int32_t dtype, int32_t pred, uint64_t* d_out, int64_t n_x, void* d_x_next,
+                        uint64_t key_x, int64_t n_z, void* d_z_next, uint64_t key_z,
+                        uint64_t* d_out_next, int32_t n_next_shards, void* stream);
+
+/* Tuning hook for tw_count_pairs_step: number of spare blocks (0 = automatic), their
+ * placement (tail = 1, the default: the last blocks of the grid; tail = 0: one group of 8
+ * every `every` blocks, 0 = automatic spacing, 8 = the leading blocks).  Process-global;
+ * results do not depend on it. */
+int tw_count_step_set_plan(int32_t blocks, int32_t every, int32_t tail);
+
 /* Tuning hook for tw_count_pairs' launch plan: R x-values per lane (1, 2, 4, 8; 0 = automatic)
  * and z-chunk length per block (0 = automatic).  Process-global; results do not depend on it. */
 int tw_count_set_plan(int32_t R, int64_t z_chunk);
@@ -150,6 +168,9 @@ int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int
                       int64_t kx, const int64_t* d_rows_z, int64_t kz, int32_t n_shards,
                       int64_t B, const double* d_w, double margin, uint64_t seed,
                       const uint64_t* d_step, int32_t shard_base, double* d_out, void* stream);
+/* Tuning hook: 1 selects the unpipelined kernel for 32 < d <= 512 rows too (the pipelined
+ * one is the default, 0).  Process-global; both give identical bits. */
+int tw_hinge_set_variant(int32_t legacy_wide);
 int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n, uint64_t seed,
                     const uint64_t* d_step, int32_t side, int32_t shard_base, void* stream);
 
@@ -166,25 +187,35 @@ int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w, doub
                 void* stream);
 
 /* ---- Row A6/A9/(e): repartition on the device ----------------------------------------
- * Keyed pseudo-random permutation of [0, n): a 4-round Feistel network over the smallest
+ * Keyed pseudo-random permutation of [0, n): a 6-round Feistel network over the smallest
  * even-bit power-of-two domain >= n, with cycle walking (a bijection on [0, n)).
  * tw_permute_scatter: d_out[perm(i)] = d_in[i] for i in [0, n) (8-byte elements).
  * tw_perm_index: d_perm[i] = perm(i). */
 int tw_permute_scatter(const void* d_in, void* d_out, int64_t n, uint64_t key, void* stream);
+/* Both samples of one repartition in one launch: X (n elements, key_x) and Z (m, key_z),
+ * each exactly as tw_permute_scatter. */
+int tw_permute_pair(const void* d_x_in, void* d_x_out, int64_t n, uint64_t key_x,
+                    const void* d_z_in, void* d_z_out, int64_t m, uint64_t key_z, void* stream);
 int tw_perm_index(int64_t* d_perm, int64_t n, int64_t base, int64_t n_total, uint64_t key,
                   void* stream);
 
 /* ---- (e) multi-rank repartition: counting sort of this rank's elements by destination rank
  * (dest = perm / n_loc, G <= 64 ranks), packed as 16-byte records {value bits, dest-local
- * position} for an all-to-all(v); the receiver scatters the records into its local array.
- * tw_rank_histogram: d_counts[g] = #elements bound for rank g.  tw_bucket_scatter: record of
- * element i goes to d_send[2*(d_start[dst] + k)], k a per-destination cursor (d_cursor, G
- * uint64 scratch).  tw_scatter_records: d_out[rec.pos] = rec.value for m records. */
+ * position + pos_base} for an all-to-all(v); the receiver scatters the records into its local
+ * array.  tw_rank_histogram: d_counts[g] = #elements bound for rank g.  tw_source_histogram:
+ * d_counts[q] = #positions in [base, base+n) whose source perm^-1(p) (the permutation of
+ * [0, n_total) keyed by `key`, as tw_perm_index) lies on rank q = source / n_loc — what this
+ * rank receives from q, known without a message.  tw_bucket_scatter: record of element i goes
+ * to d_send[2*(d_start[dst] + k)], k a per-destination slot reserved per block (d_cursor: G
+ * uint64 of scratch); pos_base lets two arrays share one record buffer (e.g. Z positions
+ * offset by n_loc of X).  tw_scatter_records: d_out[rec.pos] = rec.value for m records. */
 int tw_rank_histogram(const int64_t* d_perm, int64_t n, int64_t n_loc, int32_t G,
                       uint64_t* d_counts, void* stream);
+int tw_source_histogram(int64_t n, int64_t base, int64_t n_total, uint64_t key, int64_t n_loc,
+                        int32_t G, uint64_t* d_counts, void* stream);
 int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int64_t n, int64_t n_loc,
-                      int32_t G, const int64_t* d_start, uint64_t* d_cursor, void* d_send,
-                      void* stream);
+                      int32_t G, const int64_t* d_start, uint64_t* d_cursor, int64_t pos_base,
+                      void* d_send, void* stream);
 int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream);
 
 /* ---- (e): row exchange for the row-partitioned learning layout ------------------------

@@ -286,6 +286,30 @@ def feistel_perm(idx, n: int, key: int) -> np.ndarray:
         v[bad] = once(v[bad])
 
 
+def feistel_perm_inv(pos, n: int, key: int) -> np.ndarray:
+    """Restates csrc/permute.hip feistel_perm_inv: the inverse bijection (rounds reversed,
+    cycle walking backwards)."""
+    half, ks = _feistel_keys(n, key)
+    mask = np.uint64((1 << half) - 1)
+    hb = np.uint64(half)
+
+    def once_inv(v):
+        L = (v >> hb) & mask
+        R = v & mask
+        for k in reversed(ks):
+            pR = L
+            L = (R ^ _mix32((pR * np.uint64(0x9E3779B1) + np.uint64(k)) & _M32)) & mask
+            R = pR
+        return (L << hb) | R
+
+    v = once_inv(np.asarray(pos, dtype=np.uint64))
+    while True:
+        bad = v >= np.uint64(n)
+        if not bad.any():
+            return v.astype(np.int64)
+        v[bad] = once_inv(v[bad])
+
+
 def permute_scatter(vals: np.ndarray, key: int) -> np.ndarray:
     """out[perm(i)] = vals[i] (tw_permute_scatter)."""
     out = np.empty_like(vals)

@@ -1,8 +1,9 @@
 """Multi-rank repartition + reduction of tuplewise.device.ShardedSample on CPU (gloo).
 
 The product runs one process per GPU over RCCL; here the same orchestration (global keyed
-permutation, destination histogram, all-to-all of {value, position} records, scatter,
-zero-padded all-reduce of per-shard counts, host np.mean) runs at world size 2 and 4 with
+permutation, send counts from the forward and receive counts from the inverse permutation,
+one all-to-all of {value, position} records for X and Z together, scatter, zero-padded
+all-reduce of per-shard counts, host np.mean) runs at world size 2 and 4 with
 gloo, with the device operations replaced by their oracle restatements (test-only).  Checks:
 the permuted global arrays equal the single-process permutation, and the estimate is
 bit-identical to the G = 1 result — the G-invariance the design promises.
@@ -28,19 +29,26 @@ class OracleOps:
     def permute(self, vals, key):
         return torch.from_numpy(O.permute_scatter(vals.numpy(), key))
 
+    def permute_pair(self, X, kx, Z, kz):
+        return self.permute(X, kx), self.permute(Z, kz)
+
     def rank_histogram(self, perm, n_loc, G):
         return torch.from_numpy(np.bincount(perm.numpy() // n_loc, minlength=G).astype(np.int64))
 
-    def bucket_scatter(self, perm, vals, n_loc, G, start):
+    def source_histogram(self, n, base, n_total, key, n_loc, G):
+        src = O.feistel_perm_inv(np.arange(base, base + n), n_total, key)
+        return torch.from_numpy(np.bincount(src // n_loc, minlength=G).astype(np.int64))
+
+    def bucket_scatter(self, perm, vals, n_loc, G, start, send, pos_base):
         p = perm.numpy()
         dst = p // n_loc
         order = np.argsort(dst, kind="stable")
-        rec = np.empty((len(p), 2), dtype=np.int64)
-        rec[:, 0] = vals.numpy().view(np.int64)[order]
-        rec[:, 1] = (p - dst * n_loc)[order]
-        assert np.array_equal(np.cumsum(np.bincount(dst, minlength=G)) -
-                              np.bincount(dst, minlength=G), start.numpy())
-        return torch.from_numpy(rec)
+        k = np.arange(len(p)) - np.searchsorted(dst[order], dst[order])  # slot in its bucket
+        rows = start.numpy()[dst[order]] + k
+        rec = send.numpy()
+        rec[rows, 0] = vals.numpy().view(np.int64)[order]
+        rec[rows, 1] = (p - dst * n_loc)[order] + pos_base
+        return send
 
     def scatter_records(self, rec, out):
         o = out.numpy().view(np.int64)

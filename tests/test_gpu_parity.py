@@ -273,3 +273,130 @@ def test_replicate_equals_reference_loop(gpu, which):
     got = est.replicate(getattr(est, which), gen_X, gen_Z, 60, *args, flush_elems=20_000)
     probe_got = np.random.randint(2 ** 30)
     assert got == want and probe_got == probe_want
+
+
+def test_pipelined_unn_many_equals_sequential(gpu):
+    """ShardedSample.UnN_many (repartition i+1 on a side stream during the counts of step i,
+    counts combined at the end) == one UnN call per key, value for value, and leaves the
+    same permuted arrays."""
+    import torch
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(12)
+    n, m, N = 300_000, 250_000, 16
+    X, Z = rng.normal(0.3, 1, n), rng.normal(0, 1, m)
+    keys = [3, 4, 5, 6, 7]
+    for algo in ("pairs", "sorted"):
+        S1 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N, algo=algo)
+        S2 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N, algo=algo)
+        seq = [S1.UnN(k) for k in keys]
+        pipe = S2.UnN_many(keys)
+        assert seq == pipe
+        assert torch.equal(S1.X, S2.X) and torch.equal(S1.Z, S2.Z)
+        assert S2.UnNT(3, key0=40) == np.mean([S1.UnN(k) for k in (40, 41, 42)])
+
+
+def test_exchange_kernels_simulated_ranks(gpu):
+    """Multi-rank repartition kernels for G=5 ranks simulated in one process (the all-to-all
+    is a host-side regrouping): send counts, receive counts from the inverse permutation,
+    block-reserved bucket scatter with a position base, scatter into place == the global
+    permutation of the oracle."""
+    import torch
+    from tuplewise.device import HipOps
+    ops = HipOps()
+    G, n_loc, key = 5, 30_011, 0xDEADBEEF
+    n_tot = G * n_loc
+    rng = np.random.RandomState(1)
+    vals = rng.normal(size=n_tot)
+    want = O.permute_scatter(vals, key)
+    inbox = [[] for _ in range(G)]
+    for r in range(G):
+        perm = ops.perm_index(n_loc, r * n_loc, n_tot, key)
+        p = O.feistel_perm(np.arange(r * n_loc, (r + 1) * n_loc), n_tot, key)
+        assert np.array_equal(perm.cpu().numpy(), p)
+        sc = ops.rank_histogram(perm, n_loc, G)
+        assert np.array_equal(sc.cpu().numpy(), np.bincount(p // n_loc, minlength=G))
+        rc = ops.source_histogram(n_loc, r * n_loc, n_tot, key, n_loc, G).cpu().numpy()
+        src = O.feistel_perm_inv(np.arange(r * n_loc, (r + 1) * n_loc), n_tot, key)
+        assert np.array_equal(rc, np.bincount(src // n_loc, minlength=G))
+        start = torch.cumsum(sc, 0) - sc
+        send = torch.full((n_loc, 2), -1, dtype=torch.int64, device="cuda")
+        ops.bucket_scatter(perm, torch.from_numpy(vals[r * n_loc:(r + 1) * n_loc]).cuda(),
+                           n_loc, G, start, send, 7)
+        s = send.cpu().numpy()
+        off = np.concatenate([[0], np.cumsum(sc.cpu().numpy())])
+        for q in range(G):
+            inbox[q].append(s[off[q]:off[q + 1]])
+    for q in range(G):
+        rec = np.concatenate(inbox[q])
+        assert rec.shape[0] == n_loc
+        assert np.array_equal(np.sort(rec[:, 1]), np.arange(n_loc) + 7)  # every slot once
+        rec[:, 1] -= 7
+        out = torch.empty(n_loc, dtype=torch.float64, device="cuda")
+        ops.scatter_records(torch.from_numpy(rec).cuda(), out)
+        assert np.array_equal(out.cpu().numpy(), want[q * n_loc:(q + 1) * n_loc])
+
+
+@pytest.mark.parametrize("d,B", [(33, 100), (100, 1500), (512, 100), (512, 2100), (700, 64)])
+def test_hinge_grad_wide_rows(gpu, d, B):
+    """tw_hinge_grad for wide rows (the pipelined kernel for 32 < d <= 512, the unpipelined one
+    above): per-shard gradients vs the restated reference body (compute_stats.py:153-162), and
+    both wide kernels bit-identical to each other."""
+    import torch
+    from tuplewise import _lib as L, _learn
+    rng = np.random.RandomState(d + B)
+    nX, nZ, N, kx, kz = 3000, 2000, 6, 400, 300
+    X, Z = rng.normal(size=(nX, d)), rng.normal(0.2, 1, size=(nZ, d))
+    w = rng.normal(size=d) / np.sqrt(d)
+    rows_x = rng.randint(0, nX, size=(N, kx))
+    rows_z = rng.randint(0, nZ, size=(N, kz))
+    ix = rng.randint(0, kx, size=(N, B))
+    iz = rng.randint(0, kz, size=(N, B))
+    dev = [L.to_device(a) for a in (X, Z, rows_x, rows_z, ix, iz, w)]
+    outs = []
+    for legacy in (0, 1):
+        L.call("tw_hinge_set_variant", legacy)
+        try:
+            g = _learn.hinge_grads_device(dev[0], dev[1], d, dev[2], kx, dev[3], kz, dev[4],
+                                          dev[5], N, B, dev[6], 1.0)
+        finally:
+            L.call("tw_hinge_set_variant", 0)
+        outs.append(g.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    for s in range(N):
+        diff = Z[rows_z[s][iz[s]]] - X[rows_x[s][ix[s]]]
+        filt = (diff.dot(w) + 1.0) > 0
+        want = diff[filt].sum(axis=0) / B
+        np.testing.assert_allclose(outs[0][s], want, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("dtype,mode", [("f64", "gt"), ("f64", "half"), ("i64", "subgt")])
+def test_count_pairs_step_fused_repartition(gpu, dtype, mode):
+    """tw_count_pairs_step: counts == tw_count_pairs on ragged shards, and the same launch
+    writes the next repartition (== oracle permutation) and zeroes the next counters."""
+    import torch
+    from tuplewise import _engine as E, _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(21)
+    nx = [0, 1, 5, 257, 3000, 1, 4096 + 3, 700]
+    nz = [3, 0, 9, 1000, 2049, 1, 513, 700]
+    if dtype == "f64":
+        xs = [rng.normal(size=k).round(1) for k in nx]
+        zs = [rng.normal(size=k).round(1) for k in nz]
+        code = L.TW_F64
+    else:
+        xs = [rng.randint(-2 ** 62, 2 ** 62, k) * 2 for k in nx]  # wraps in x - z
+        zs = [rng.randint(-2 ** 62, 2 ** 62, k) * 2 for k in nz]
+        code = L.TW_I64
+    sh = E.Shards.from_blocks(xs, zs, code)
+    want = E.count_complete(sh, mode, algo="pairs")
+    xo, zo = sh.offsets_dev()
+    pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}[mode]
+    out = torch.zeros(len(nx), dtype=torch.int64, device="cuda")
+    out_next = torch.full((5,), 77, dtype=torch.int64, device="cuda")
+    xn, zn = torch.empty_like(sh.x), torch.empty_like(sh.z)
+    HipOps().count_step(sh.x, xo, sh.z, zo, len(nx), max(nx), max(nz), code, pred, out, xn, 11,
+                        zn, 12, out_next)
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want)
+    assert not out_next.cpu().numpy().any()
+    assert np.array_equal(xn.cpu().numpy(), O.permute_scatter(sh.x.cpu().numpy(), 11))
+    assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 12))

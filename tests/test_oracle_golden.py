@@ -135,3 +135,10 @@ def test_feistel_is_bijection():
     for n in (1, 2, 3, 17, 1000, 4097):
         p = O.feistel_perm(np.arange(n), n, key=12345)
         assert np.array_equal(np.sort(p), np.arange(n))
+
+
+def test_feistel_inverse_undoes_forward():
+    for n in (1, 2, 3, 17, 1000, 4097, 100_003):
+        i = np.arange(n)
+        p = O.feistel_perm(i, n, key=777)
+        assert np.array_equal(O.feistel_perm_inv(p, n, key=777), i)

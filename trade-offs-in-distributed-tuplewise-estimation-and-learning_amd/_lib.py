@@ -28,6 +28,9 @@ _SIGNATURES = {
     "tw_version": [],
     "tw_device_count": [_vp],
     "tw_count_pairs": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp],
+    "tw_count_pairs_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _i64, _vp,
+                            _u64, _i64, _vp, _u64, _vp, _i32, _vp],
+    "tw_count_step_set_plan": [_i32, _i32, _i32],
     "tw_count_set_plan": [_i32, _i64],
     "tw_count_pairs_sorted_work_bytes": [_i32, _i64],
     "tw_count_sorted_set_chunk": [_i64],
@@ -42,13 +45,16 @@ _SIGNATURES = {
                       _vp, _vp],
     "tw_hinge_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _u64,
                           _vp, _i32, _vp, _vp],
+    "tw_hinge_set_variant": [_i32],
     "tw_swr_rows_rng": [_vp, _i32, _i64, _i64, _u64, _vp, _i32, _i32, _vp],
     "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
     "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],
+    "tw_permute_pair": [_vp, _vp, _i64, _u64, _vp, _vp, _i64, _u64, _vp],
     "tw_perm_index": [_vp, _i64, _i64, _i64, _u64, _vp],
     "tw_rank_histogram": [_vp, _i64, _i64, _i32, _vp, _vp],
-    "tw_bucket_scatter": [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp],
+    "tw_source_histogram": [_i64, _i64, _i64, _u64, _i64, _i32, _vp, _vp],
+    "tw_bucket_scatter": [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64, _vp, _vp],
     "tw_scatter_records": [_vp, _i64, _vp, _vp],
     "tw_row_route_counts": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
     "tw_row_pack": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp],

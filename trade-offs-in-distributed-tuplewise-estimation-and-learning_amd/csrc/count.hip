@@ -19,7 +19,7 @@
 //   Measured on MI355X (tools/mb_issue*.hip): v_cmp_*_f64 and v_addc issue at ~0.94
 //   wave-instructions/cycle/CU, so 2 such instructions per pair cap this kernel at ~1.9e13
 //   pairs/s; see DESIGN.md "count kernel roofline".
-#include "tw_common.h"
+#include "feistel.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -40,14 +40,81 @@ __device__ __forceinline__ unsigned pair_pred(T x, T z) {
   }
 }
 
+// The next repartition of est.UnNT's loop, carried by the leading `blocks` blocks of a count
+// launch (tw_count_pairs_step): the permutation of both samples as a gather (tw_permute_pair)
+// and the zeroing of the next step's counters.  These blocks are memory-latency bound and
+// share the CUs with the VALU-bound count blocks, so the repartition costs no separate
+// kernel, no launch gap and almost no time.
+struct NextStep {
+  const uint64_t* x_in;
+  uint64_t* x_out;
+  int64_t nx;
+  const uint64_t* z_in;
+  uint64_t* z_out;
+  int64_t nz;
+  unsigned long long* zero;
+  int64_t nzero;
+  Feistel fx, fz;
+  int blocks;  // a multiple of kXcds
+  int every;   // placement of the spare blocks (see k_count_complete)
+  int tail;
+};
+
+__device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
+  constexpr int kU = 8;  // independent gathers in flight per thread
+  const int64_t stride = (int64_t)nx.blocks * kBlock;
+  for (int64_t i = (int64_t)b * kBlock + threadIdx.x; i < nx.nzero; i += stride) nx.zero[i] = 0;
+  const int64_t tot = nx.nx + nx.nz;
+  for (int64_t p0 = (int64_t)b * kBlock + threadIdx.x; p0 < tot; p0 += stride * kU) {
+    uint64_t v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t p = p0 + u * stride;
+      if (p < nx.nx)
+        v[u] = nx.x_in[feistel_perm_inv(nx.fx, (uint64_t)p, (uint64_t)nx.nx)];
+      else if (p < tot)
+        v[u] = nx.z_in[feistel_perm_inv(nx.fz, (uint64_t)(p - nx.nx), (uint64_t)nx.nz)];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t p = p0 + u * stride;
+      if (p < nx.nx)
+        nx.x_out[p] = v[u];
+      else if (p < tot)
+        nx.z_out[p - nx.nx] = v[u];
+    }
+  }
+}
+
 template <typename T, int R, int PRED>
 __global__ __launch_bounds__(kBlock) void k_count_complete(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, int tiles_x, int zchunks, int64_t z_chunk,
-    unsigned long long* __restrict__ out) {
+    unsigned long long* __restrict__ out, NextStep nxt) {
+  // Spare blocks (block-uniform branch), in groups of kXcds so count blocks keep their XCD:
+  // group g occupies blocks [g*every, g*every + kXcds) — every == kXcds: the leading blocks,
+  // every > kXcds: spread through the grid — or, with tail != 0, the last nxt.blocks blocks.
+  int cb = blockIdx.x;  // index among the count blocks
+  if (nxt.blocks) {
+    const int b = blockIdx.x, ng = nxt.blocks / kXcds;
+    if (nxt.tail) {
+      if (b >= (int)gridDim.x - nxt.blocks) {
+        next_step_part(nxt, b - ((int)gridDim.x - nxt.blocks));
+        return;
+      }
+    } else {
+      const int g = b / nxt.every, r = b - g * nxt.every;
+      if (r < kXcds && g < ng) {
+        next_step_part(nxt, g * kXcds + r);
+        return;
+      }
+      cb = b - kXcds * ((g < ng ? g : ng) + ((r >= kXcds && g < ng) ? 1 : 0));
+    }
+  }
   const int per_shard = tiles_x * zchunks;
-  const int s = blockIdx.x / per_shard;
-  const int rem = blockIdx.x - s * per_shard;
+  const int lb = xcd_block(cb, gridDim.x - nxt.blocks);  // whole shards per XCD
+  const int s = lb / per_shard;
+  const int rem = lb - s * per_shard;
   const int cz = rem / tiles_x;
   const int tx = rem - cz * tiles_x;
 
@@ -103,8 +170,9 @@ __global__ __launch_bounds__(kBlock) void k_count_idx(const T* __restrict__ x,
                                                       const int64_t* __restrict__ pair_off,
                                                       int blocks_per_shard,
                                                       unsigned long long* __restrict__ out) {
-  const int s = blockIdx.x / blocks_per_shard;
-  const int bi = blockIdx.x - s * blocks_per_shard;
+  const int lb = xcd_block(blockIdx.x, gridDim.x);  // whole shards per XCD
+  const int s = lb / blocks_per_shard;
+  const int bi = lb - s * blocks_per_shard;
   const int64_t pb = pair_off[s], pe = pair_off[s + 1];
   const int64_t p0 = pb + (int64_t)bi * (kBlock * PPT);
   if (p0 >= pe) return;
@@ -134,8 +202,9 @@ __global__ __launch_bounds__(kBlock) void k_count_rng(const T* __restrict__ x,
                                                       int64_t B, int blocks_per_shard,
                                                       uint32_t k0, uint32_t k1, uint32_t sid,
                                                       unsigned long long* __restrict__ out) {
-  const int s = blockIdx.x / blocks_per_shard;
-  const int bi = blockIdx.x - s * blocks_per_shard;
+  const int lb = xcd_block(blockIdx.x, gridDim.x);  // whole shards per XCD
+  const int s = lb / blocks_per_shard;
+  const int bi = lb - s * blocks_per_shard;
   const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
   const int64_t zb = z_off[s], nz = z_off[s + 1] - zb;
   const int64_t p0 = (int64_t)bi * (kBlock * PPT);
@@ -205,20 +274,20 @@ inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shar
 template <typename T, int PRED>
 int launch_complete(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                     int32_t n_shards, int64_t max_nx, int64_t max_nz, uint64_t* out,
-                    hipStream_t st) {
+                    const NextStep& nxt, hipStream_t st) {
   const CompletePlan p = plan_complete(max_nx, max_nz, n_shards);
-  TW_ARG_CHECK(p.blocks < (1ll << 31), "tw_count_pairs: grid too large (%lld blocks)",
+  TW_ARG_CHECK(p.blocks + nxt.blocks < (1ll << 31), "tw_count_pairs: grid too large (%lld blocks)",
                (long long)p.blocks);
   TW_ARG_CHECK(p.z_chunk < (1ll << 30), "tw_count_pairs: z chunk too large");
   const T* xs = (const T*)x;
   const T* zs = (const T*)z;
   auto* o = (unsigned long long*)out;
-  dim3 g((unsigned)p.blocks), b(kBlock);
+  dim3 g((unsigned)(p.blocks + nxt.blocks)), b(kBlock);
   switch (p.R) {
-    case 8: hipLaunchKernelGGL((k_count_complete<T, 8, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
-    case 4: hipLaunchKernelGGL((k_count_complete<T, 4, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
-    case 2: hipLaunchKernelGGL((k_count_complete<T, 2, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
-    default: hipLaunchKernelGGL((k_count_complete<T, 1, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o); break;
+    case 8: hipLaunchKernelGGL((k_count_complete<T, 8, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
+    case 4: hipLaunchKernelGGL((k_count_complete<T, 4, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
+    case 2: hipLaunchKernelGGL((k_count_complete<T, 2, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
+    default: hipLaunchKernelGGL((k_count_complete<T, 1, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
   }
   TW_LAUNCH_CHECK();
   return TW_OK;
@@ -227,11 +296,11 @@ int launch_complete(const void* x, const int64_t* x_off, const void* z, const in
 template <typename T>
 int dispatch_complete(int32_t pred, const void* x, const int64_t* x_off, const void* z,
                       const int64_t* z_off, int32_t n_shards, int64_t max_nx, int64_t max_nz,
-                      uint64_t* out, hipStream_t st) {
+                      uint64_t* out, const NextStep& nxt, hipStream_t st) {
   switch (pred) {
-    case TW_PRED_GT: return launch_complete<T, TW_PRED_GT>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, st);
-    case TW_PRED_HALF: return launch_complete<T, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, st);
-    case TW_PRED_SUBGT: return launch_complete<T, TW_PRED_SUBGT>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, st);
+    case TW_PRED_GT: return launch_complete<T, TW_PRED_GT>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, nxt, st);
+    case TW_PRED_HALF: return launch_complete<T, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, nxt, st);
+    case TW_PRED_SUBGT: return launch_complete<T, TW_PRED_SUBGT>(x, x_off, z, z_off, n_shards, max_nx, max_nz, out, nxt, st);
   }
   set_error("tw_count_pairs: unknown predicate %d", pred);
   return TW_ERR_ARG;
@@ -286,10 +355,80 @@ extern "C" int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const voi
   if (n_shards == 0) return TW_OK;
   TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (max_nx == 0 || max_nz == 0) return TW_OK;
-  if (dtype == TW_F64) return dispatch_complete<double>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, st);
-  if (dtype == TW_I64) return dispatch_complete<long long>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, st);
+  const NextStep none{};
+  if (dtype == TW_F64) return dispatch_complete<double>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, none, st);
+  if (dtype == TW_I64) return dispatch_complete<long long>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, none, st);
   set_error("tw_count_pairs: unknown dtype %d", dtype);
   return TW_ERR_ARG;
+}
+
+// Spare blocks given to the next repartition: enough threads for ~8 gathers each, at most
+// 2 per CU, a multiple of the XCD count.  Tuning hook tw_count_step_set_plan overrides the
+// number and placement.
+// Measured (tools/tune_step.py, bench workload): the last 512-768 blocks cost ~8 us over the
+// bare count (they fill the count's tail); leading / spread placements cost 18-23 us.
+static int g_step_blocks = 0, g_step_every = 0, g_step_tail = 1;
+static int next_step_blocks(int64_t elems) {
+  int64_t b = ceil_div(elems, (int64_t)kBlock * 8);
+  b = std::min<int64_t>(std::max<int64_t>(b, 8), 512);
+  if (g_step_blocks > 0) b = g_step_blocks;
+  return (int)(ceil_div(b, kXcds) * kXcds);
+}
+
+extern "C" int tw_count_step_set_plan(int32_t blocks, int32_t every, int32_t tail) {
+  TW_ARG_CHECK(blocks >= 0 && every >= 0 && every % kXcds == 0 && (tail == 0 || tail == 1),
+               "tw_count_step_set_plan: blocks >= 0, every a multiple of 8, tail 0/1");
+  g_step_blocks = blocks;
+  g_step_every = every;
+  g_step_tail = tail;
+  return TW_OK;
+}
+
+extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                   const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                   int64_t max_nz, int32_t dtype, int32_t pred, uint64_t* d_out,
+                                   int64_t n_x, void* d_x_next, uint64_t key_x, int64_t n_z,
+                                   void* d_z_next, uint64_t key_z, uint64_t* d_out_next,
+                                   int32_t n_next_shards, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && max_nx >= 0 && max_nz >= 0 && n_x >= 0 && n_z >= 0 &&
+                   n_x < (1ll << 60) && n_z < (1ll << 60) && n_next_shards >= 0,
+               "tw_count_pairs_step: bad sizes");
+  TW_ARG_CHECK(dtype == TW_F64 || dtype == TW_I64, "tw_count_pairs_step: unknown dtype %d", dtype);
+  TW_ARG_CHECK(pred == TW_PRED_GT || pred == TW_PRED_HALF || pred == TW_PRED_SUBGT,
+               "tw_count_pairs_step: unknown predicate %d", pred);
+  TW_ARG_CHECK(d_x_next == nullptr || ((n_x == 0 || d_x_next != d_x) &&
+                                       (n_z == 0 || (d_z_next != nullptr && d_z_next != d_z))),
+               "tw_count_pairs_step: next arrays must be distinct buffers");
+  hipStream_t st = (hipStream_t)stream;
+  NextStep nxt{};
+  if (d_x_next != nullptr) {
+    nxt = NextStep{(const uint64_t*)d_x, (uint64_t*)d_x_next, n_x, (const uint64_t*)d_z,
+                   (uint64_t*)d_z_next, n_z, (unsigned long long*)d_out_next,
+                   d_out_next ? (int64_t)n_next_shards : 0,
+                   make_feistel(std::max<int64_t>(n_x, 1), key_x),
+                   make_feistel(std::max<int64_t>(n_z, 1), key_z),
+                   next_step_blocks(n_x + n_z), 0, g_step_tail};
+    // spread over the grid by default: one group of 8 every `every` blocks
+    const CompletePlan p = plan_complete(std::max<int64_t>(max_nx, 1),
+                                         std::max<int64_t>(max_nz, 1), std::max(n_shards, 1));
+    const int ng = nxt.blocks / kXcds;
+    nxt.every = g_step_every ? g_step_every
+                             : (int)std::max<int64_t>(kXcds, (p.blocks / ng) / kXcds * kXcds);
+    if (n_shards == 0 || max_nx == 0 || max_nz == 0 ||
+        (int64_t)(ng - 1) * nxt.every + kXcds > p.blocks + nxt.blocks)
+      nxt.every = kXcds;  // leading blocks
+  } else if (d_out_next != nullptr && n_next_shards > 0) {
+    TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+  }
+  if (n_shards == 0 || max_nx == 0 || max_nz == 0) {  // nothing to count: only the next step
+    if (nxt.blocks == 0) return TW_OK;
+    hipLaunchKernelGGL((k_count_complete<double, 1, TW_PRED_GT>), dim3(nxt.blocks), dim3(kBlock),
+                       0, st, nullptr, nullptr, nullptr, nullptr, 1, 1, 1, nullptr, nxt);
+    TW_LAUNCH_CHECK();
+    return TW_OK;
+  }
+  if (dtype == TW_F64) return dispatch_complete<double>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, nxt, st);
+  return dispatch_complete<long long>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, nxt, st);
 }
 
 extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,

@@ -1,0 +1,83 @@
+// feistel.h — the keyed bijection of [0, n) behind every device repartition
+// (csrc/permute.hip; restated in oracle/oracle.py feistel_perm / feistel_perm_inv): a 6-round
+// balanced Feistel network on the smallest even-bit power-of-two domain >= n, cycle-walked
+// into [0, n).
+#pragma once
+#include "tw_common.h"
+
+namespace tw {
+
+struct Feistel {
+  uint32_t half_bits;
+  uint32_t mask;
+  uint32_t k[6];
+};
+
+__host__ __device__ inline uint32_t mix32(uint32_t v) {  // murmur3 finaliser
+  v ^= v >> 16;
+  v *= 0x85EBCA6Bu;
+  v ^= v >> 13;
+  v *= 0xC2B2AE35u;
+  v ^= v >> 16;
+  return v;
+}
+
+inline Feistel make_feistel(int64_t n, uint64_t key) {
+  Feistel f;
+  int bits = 2;
+  while (bits < 62 && (1ll << bits) < n) ++bits;
+  if (bits & 1) ++bits;
+  f.half_bits = bits / 2;
+  f.mask = (uint32_t)((1ull << f.half_bits) - 1);
+  uint64_t st = key ^ 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < 6; ++i) {  // splitmix64 key schedule
+    st += 0x9E3779B97F4A7C15ull;
+    uint64_t zz = st;
+    zz = (zz ^ (zz >> 30)) * 0xBF58476D1CE4E5B9ull;
+    zz = (zz ^ (zz >> 27)) * 0x94D049BB133111EBull;
+    zz ^= zz >> 31;
+    f.k[i] = (uint32_t)zz;
+  }
+  return f;
+}
+
+__host__ __device__ inline uint64_t feistel_once(const Feistel& f, uint64_t v) {
+  uint32_t L = (uint32_t)(v >> f.half_bits) & f.mask;
+  uint32_t R = (uint32_t)v & f.mask;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const uint32_t nL = R;
+    R = (L ^ mix32(R * 0x9E3779B1u + f.k[i])) & f.mask;
+    L = nL;
+  }
+  return ((uint64_t)L << f.half_bits) | R;
+}
+
+__host__ __device__ inline uint64_t feistel_perm(const Feistel& f, uint64_t i, uint64_t n) {
+  uint64_t v = feistel_once(f, i);
+  while (v >= n) v = feistel_once(f, v);  // cycle walking: terminates (bijection on domain)
+  return v;
+}
+
+// Inverse network: rounds in reverse order.  Round i maps (L, R) -> (R, L ^ F_i(R)), so its
+// inverse maps (L', R') -> (R' ^ F_i(L'), L').  Cycle walking backwards from a position in
+// [0, n) retraces the forward walk, so feistel_perm_inv(feistel_perm(i)) == i.
+__host__ __device__ inline uint64_t feistel_once_inv(const Feistel& f, uint64_t v) {
+  uint32_t L = (uint32_t)(v >> f.half_bits) & f.mask;
+  uint32_t R = (uint32_t)v & f.mask;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    const uint32_t pR = L;
+    L = (R ^ mix32(pR * 0x9E3779B1u + f.k[i])) & f.mask;
+    R = pR;
+  }
+  return ((uint64_t)L << f.half_bits) | R;
+}
+
+__host__ __device__ inline uint64_t feistel_perm_inv(const Feistel& f, uint64_t p, uint64_t n) {
+  uint64_t v = feistel_once_inv(f, p);
+  while (v >= n) v = feistel_once_inv(f, v);
+  return v;
+}
+
+}  // namespace tw

@@ -151,6 +151,122 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
   }
 }
 
+// Wide rows, 32 < d <= 512 (C5: d = 512) — the HBM-bound case, pipelined:
+//  * per phase of up to kIdxPhase pairs the block resolves every pair's absolute X/Z row
+//    (SWR row table composed with the pair draw) into LDS: one dependent round trip per phase
+//    instead of one per chunk;
+//  * chunks of kWideCH = 16 waves x kWidePW pairs: a wave holds its pairs' two rows in
+//    registers (8 columns per lane), writes diff = Z[rz] - X[rx] to LDS and the filter flag;
+//  * the rows of chunk c+1 are loaded right after the barrier, so their HBM latency overlaps
+//    chunk c's column sums (thread j adds column j over the filtered rows, in row order).
+// Arithmetic and order are those of k_hinge_grad (same lane-strided dot + butterfly, same
+// row-order sums from +0.0), so both kernels give identical bits.
+constexpr int kWidePW = 2;
+constexpr int kWideCH = (kWideBlock / kWave) * kWidePW;  // 32 pairs per chunk
+constexpr int kWideCols = 8;                             // columns per lane
+constexpr int kWideMaxD = kWideCols * kWave;             // 512
+constexpr int kIdxPhase = 1024;
+
+__global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
+    const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
+    const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
+    int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
+    const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
+    const uint64_t* __restrict__ d_step, uint32_t shard_base) {
+  __shared__ double diff[kWideCH * kWideMaxD];  // 128 KiB
+  __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
+  __shared__ int flag[kWideCH];
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int dd = (int)d;
+  const uint64_t step = d_step ? *d_step : 0;
+  double wv[kWideCols];
+#pragma unroll
+  for (int c = 0; c < kWideCols; ++c) {
+    const int j = lane + c * kWave;
+    wv[c] = j < dd ? w[j] : 0.0;
+  }
+  double acc = 0.0;  // thread j < d: column j
+  double zv[kWidePW][kWideCols], xv[kWidePW][kWideCols];
+
+  for (int64_t P0 = 0; P0 < B; P0 += kIdxPhase) {
+    const int np = (int)std::min<int64_t>(kIdxPhase, B - P0);
+    __syncthreads();  // the previous phase's readers of prx/prz are done
+    for (int t = threadIdx.x; t < np; t += kWideBlock) {
+      const int64_t b = P0 + t;
+      int64_t ax, az;
+      if (ix) {  // replay: NumPy's randint draws
+        ax = ix[(int64_t)s * B + b];
+        az = iz[(int64_t)s * B + b];
+      } else {  // device RNG
+        const u32x4 r = sgd_draw(seed, step, (uint32_t)b, shard_base + (uint32_t)s, kTagPairs);
+        ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
+        az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
+      }
+      prx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+      prz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+    }
+    __syncthreads();
+
+    auto load = [&](int c0) {
+#pragma unroll
+      for (int u = 0; u < kWidePW; ++u) {
+        const int t = c0 + wid * kWidePW + u;
+        if (t < np) {
+          const double* zr = Z + prz[t] * d;
+          const double* xr = X + prx[t] * d;
+#pragma unroll
+          for (int c = 0; c < kWideCols; ++c) {
+            const int j = lane + c * kWave;
+            zv[u][c] = j < dd ? zr[j] : 0.0;
+            xv[u][c] = j < dd ? xr[j] : 0.0;
+          }
+        }
+      }
+    };
+    load(0);
+    for (int c0 = 0; c0 < np; c0 += kWideCH) {
+      const int nb = std::min(kWideCH, np - c0);
+#pragma unroll
+      for (int u = 0; u < kWidePW; ++u) {
+        const int t = wid * kWidePW + u;
+        if (t < nb) {
+          double part = 0.0;
+#pragma unroll
+          for (int c = 0; c < kWideCols; ++c) {
+            const int j = lane + c * kWave;
+            if (j < dd) {
+              const double v = zv[u][c] - xv[u][c];
+              diff[t * dd + j] = v;
+              part += v * wv[c];
+            }
+          }
+          part = wave_sum_f64(part);
+          if (lane == 0) flag[t] = (part + margin) > 0.0;
+        }
+      }
+      __syncthreads();
+      if (c0 + kWideCH < np) load(c0 + kWideCH);  // in flight during the sums below
+      if (threadIdx.x < dd) {
+        const int j = threadIdx.x;
+        double a = acc;
+        int t = 0;
+        for (; t + 8 <= nb; t += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = flag[t + u] ? diff[(t + u) * dd + j] : -0.0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; t < nb; ++t) a += flag[t] ? diff[t * dd + j] : -0.0;
+        acc = a;
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
+}
+
 // SWR_divide row draws on the device: rows[s*k + t] uniform in [0, n) (with replacement).
 __global__ __launch_bounds__(kBlock) void k_swr_rows(int64_t* __restrict__ rows, int n_shards,
                                                      int64_t k, int64_t n, uint64_t seed,
@@ -225,6 +341,8 @@ __global__ __launch_bounds__(kBlock) void k_gemv(const double* __restrict__ A, i
   }
 }
 
+static int g_hinge_legacy_wide = 0;  // tw_hinge_set_variant: 1 = unpipelined wide kernel
+
 int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* rows_x, int64_t kx,
                  const int64_t* rows_z, int64_t kz, const int64_t* ix, const int64_t* iz,
                  int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
@@ -234,6 +352,10 @@ int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* row
   if (d <= 32)
     hipLaunchKernelGGL(k_hinge_grad<kBlock>, dim3(n_shards), dim3(kBlock), lds, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
+                       shard_base);
+  else if (d <= kWideMaxD && !g_hinge_legacy_wide)
+    hipLaunchKernelGGL(k_hinge_grad_wide, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
+                       rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
                        shard_base);
   else
     hipLaunchKernelGGL(k_hinge_grad<kWideBlock>, dim3(n_shards), dim3(kWideBlock), lds, st, X, Z,
@@ -259,6 +381,12 @@ extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
   TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_hinge_grad: pair indices required");
   return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
                       margin, 0, nullptr, 0, d_out, st);
+}
+
+extern "C" int tw_hinge_set_variant(int32_t legacy_wide) {
+  TW_ARG_CHECK(legacy_wide == 0 || legacy_wide == 1, "tw_hinge_set_variant: 0 or 1");
+  g_hinge_legacy_wide = legacy_wide;
+  return TW_OK;
 }
 
 extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,

@@ -8,69 +8,25 @@
 // >= n, with cycle walking to stay inside [0, n).  Every rank of a multi-GPU job evaluates the
 // same bijection for its own global indices, so the permuted global array — and therefore
 // every shard's count — is identical at 1, 2, 4 and 8 GPUs.
-#include "tw_common.h"
+#include "feistel.h"
 #include <algorithm>
 
 namespace tw {
 
-struct Feistel {
-  uint32_t half_bits;
-  uint32_t mask;
-  uint32_t k[6];
-};
-
-__host__ __device__ inline uint32_t mix32(uint32_t v) {  // murmur3 finaliser
-  v ^= v >> 16;
-  v *= 0x85EBCA6Bu;
-  v ^= v >> 13;
-  v *= 0xC2B2AE35u;
-  v ^= v >> 16;
-  return v;
-}
-
-inline Feistel make_feistel(int64_t n, uint64_t key) {
-  Feistel f;
-  int bits = 2;
-  while (bits < 62 && (1ll << bits) < n) ++bits;
-  if (bits & 1) ++bits;
-  f.half_bits = bits / 2;
-  f.mask = (uint32_t)((1ull << f.half_bits) - 1);
-  uint64_t st = key ^ 0x9E3779B97F4A7C15ull;
-  for (int i = 0; i < 6; ++i) {  // splitmix64 key schedule
-    st += 0x9E3779B97F4A7C15ull;
-    uint64_t zz = st;
-    zz = (zz ^ (zz >> 30)) * 0xBF58476D1CE4E5B9ull;
-    zz = (zz ^ (zz >> 27)) * 0x94D049BB133111EBull;
-    zz ^= zz >> 31;
-    f.k[i] = (uint32_t)zz;
+// out[perm(i)] = in[i], evaluated as a GATHER out[p] = in[perm^-1(p)]: the writes are
+// coalesced and the random 8-byte reads hit the L2 / Infinity Cache (the input was just read
+// by the previous count), where a scatter would pay a partial-line write per element.
+// Two arrays (the X and Z samples of one repartition) share one launch.
+__global__ __launch_bounds__(kBlock) void k_permute_gather2(
+    const uint64_t* __restrict__ a_in, uint64_t* __restrict__ a_out, int64_t na, Feistel fa,
+    const uint64_t* __restrict__ b_in, uint64_t* __restrict__ b_out, int64_t nb, Feistel fb) {
+  for (int64_t p = blockIdx.x * (int64_t)kBlock + threadIdx.x; p < na + nb;
+       p += (int64_t)gridDim.x * kBlock) {
+    if (p < na)
+      a_out[p] = a_in[feistel_perm_inv(fa, (uint64_t)p, (uint64_t)na)];
+    else
+      b_out[p - na] = b_in[feistel_perm_inv(fb, (uint64_t)(p - na), (uint64_t)nb)];
   }
-  return f;
-}
-
-__host__ __device__ inline uint64_t feistel_once(const Feistel& f, uint64_t v) {
-  uint32_t L = (uint32_t)(v >> f.half_bits) & f.mask;
-  uint32_t R = (uint32_t)v & f.mask;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const uint32_t nL = R;
-    R = (L ^ mix32(R * 0x9E3779B1u + f.k[i])) & f.mask;
-    L = nL;
-  }
-  return ((uint64_t)L << f.half_bits) | R;
-}
-
-__host__ __device__ inline uint64_t feistel_perm(const Feistel& f, uint64_t i, uint64_t n) {
-  uint64_t v = feistel_once(f, i);
-  while (v >= n) v = feistel_once(f, v);  // cycle walking: terminates (bijection on domain)
-  return v;
-}
-
-__global__ __launch_bounds__(kBlock) void k_permute_scatter(const uint64_t* __restrict__ in,
-                                                            uint64_t* __restrict__ out,
-                                                            int64_t n, Feistel f) {
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock)
-    out[feistel_perm(f, (uint64_t)i, (uint64_t)n)] = in[i];
 }
 
 __global__ __launch_bounds__(kBlock) void k_perm_index(int64_t* __restrict__ perm, int64_t n,
@@ -86,10 +42,13 @@ __global__ __launch_bounds__(kBlock) void k_perm_index(int64_t* __restrict__ per
 // a histogram pass, an exclusive scan on the host side of the collective, then a scatter that
 // packs {value bits, destination-local position} records per destination (order inside a
 // destination bucket is irrelevant: the position travels with the value).
+// The receive side needs no message to size its buffers: position p of rank r is filled from
+// global source perm^-1(p), so k_source_histogram counts, per source rank, what r will receive.
+constexpr int kMaxG = 64;
 __global__ __launch_bounds__(kBlock) void k_rank_histogram(const int64_t* __restrict__ perm,
                                                            int64_t n, int64_t n_loc, int G,
                                                            unsigned long long* __restrict__ counts) {
-  __shared__ unsigned int h[64];
+  __shared__ unsigned int h[kMaxG];
   for (int i = threadIdx.x; i < G; i += kBlock) h[i] = 0;
   __syncthreads();
   for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
@@ -100,20 +59,67 @@ __global__ __launch_bounds__(kBlock) void k_rank_histogram(const int64_t* __rest
     if (h[i]) atomicAdd(counts + i, (unsigned long long)h[i]);
 }
 
+__global__ __launch_bounds__(kBlock) void k_source_histogram(int64_t n, int64_t base,
+                                                             uint64_t n_total, int64_t n_loc,
+                                                             int G, Feistel f,
+                                                             unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int h[kMaxG];
+  for (int i = threadIdx.x; i < G; i += kBlock) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock)
+    atomicAdd(&h[(int)((int64_t)feistel_perm_inv(f, (uint64_t)(base + i), n_total) / n_loc)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < G; i += kBlock)
+    if (h[i]) atomicAdd(counts + i, (unsigned long long)h[i]);
+}
+
+// Records of a chunk of kScatChunk consecutive elements are placed with ONE global
+// reservation per (block, destination): LDS counters give each element its rank inside the
+// block's share of a bucket.  (A global atomic per element would serialise ~n/G returning
+// atomics on each of G cursor words.)
+constexpr int kScatPer = 8;
+constexpr int kScatChunk = kBlock * kScatPer;
 __global__ __launch_bounds__(kBlock) void k_bucket_scatter(const int64_t* __restrict__ perm,
                                                            const uint64_t* __restrict__ vals,
-                                                           int64_t n, int64_t n_loc,
+                                                           int64_t n, int64_t n_loc, int G,
                                                            const int64_t* __restrict__ start,
                                                            unsigned long long* __restrict__ cursor,
+                                                           int64_t pos_base,
                                                            uint64_t* __restrict__ send) {
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int64_t pg = perm[i];
-    const int dst = (int)(pg / n_loc);
-    const unsigned long long slot = atomicAdd(cursor + dst, 1ull);
-    const int64_t o = start[dst] + (int64_t)slot;
-    send[2 * o] = vals[i];
-    send[2 * o + 1] = (uint64_t)(pg - (int64_t)dst * n_loc);
+  __shared__ unsigned int lcnt[kMaxG];
+  __shared__ int64_t lbase[kMaxG];
+  for (int64_t c0 = (int64_t)blockIdx.x * kScatChunk; c0 < n;
+       c0 += (int64_t)gridDim.x * kScatChunk) {
+    for (int i = threadIdx.x; i < G; i += kBlock) lcnt[i] = 0;
+    __syncthreads();
+    int dst[kScatPer];
+    unsigned slot[kScatPer];
+    int64_t pos[kScatPer];
+#pragma unroll
+    for (int k = 0; k < kScatPer; ++k) {
+      const int64_t i = c0 + k * kBlock + threadIdx.x;
+      dst[k] = -1;
+      if (i < n) {
+        const int64_t pg = perm[i];
+        dst[k] = (int)(pg / n_loc);
+        pos[k] = pg - (int64_t)dst[k] * n_loc;
+        slot[k] = atomicAdd(&lcnt[dst[k]], 1u);
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G; i += kBlock)
+      if (lcnt[i]) lbase[i] = start[i] + (int64_t)atomicAdd(cursor + i, (unsigned long long)lcnt[i]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScatPer; ++k) {
+      if (dst[k] >= 0) {
+        const int64_t o = lbase[dst[k]] + slot[k];
+        send[2 * o] = vals[c0 + k * kBlock + threadIdx.x];
+        send[2 * o + 1] = (uint64_t)(pos[k] + pos_base);
+      }
+    }
+    __syncthreads();  // lcnt / lbase are reset by the next chunk
   }
 }
 
@@ -128,17 +134,37 @@ __global__ __launch_bounds__(kBlock) void k_scatter_records(const uint64_t* __re
 
 using namespace tw;
 
+static int launch_permute2(const void* a_in, void* a_out, int64_t na, uint64_t ka,
+                           const void* b_in, void* b_out, int64_t nb, uint64_t kb,
+                           hipStream_t st) {
+  const Feistel fa = make_feistel(std::max<int64_t>(na, 1), ka);
+  const Feistel fb = make_feistel(std::max<int64_t>(nb, 1), kb);
+  const int blocks = (int)std::min<int64_t>(256 * 16, ceil_div(na + nb, kBlock));
+  hipLaunchKernelGGL(k_permute_gather2, dim3(blocks), dim3(kBlock), 0, st,
+                     (const uint64_t*)a_in, (uint64_t*)a_out, na, fa, (const uint64_t*)b_in,
+                     (uint64_t*)b_out, nb, fb);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 extern "C" int tw_permute_scatter(const void* d_in, void* d_out, int64_t n, uint64_t key,
                                   void* stream) {
   TW_ARG_CHECK(n >= 0 && n < (1ll << 60), "tw_permute_scatter: bad n");
   TW_ARG_CHECK(n == 0 || d_in != d_out, "tw_permute_scatter: in-place not supported");
   if (n == 0) return TW_OK;
-  const Feistel f = make_feistel(n, key);
-  const int blocks = (int)std::min<int64_t>(256 * 8, ceil_div(n, kBlock));
-  hipLaunchKernelGGL(k_permute_scatter, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream,
-                     (const uint64_t*)d_in, (uint64_t*)d_out, n, f);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+  return launch_permute2(d_in, d_out, n, key, nullptr, nullptr, 0, 0, (hipStream_t)stream);
+}
+
+extern "C" int tw_permute_pair(const void* d_x_in, void* d_x_out, int64_t n, uint64_t key_x,
+                               const void* d_z_in, void* d_z_out, int64_t m, uint64_t key_z,
+                               void* stream) {
+  TW_ARG_CHECK(n >= 0 && m >= 0 && n < (1ll << 60) && m < (1ll << 60),
+               "tw_permute_pair: bad sizes");
+  TW_ARG_CHECK((n == 0 || d_x_in != d_x_out) && (m == 0 || d_z_in != d_z_out),
+               "tw_permute_pair: in-place not supported");
+  if (n + m == 0) return TW_OK;
+  return launch_permute2(d_x_in, d_x_out, n, key_x, d_z_in, d_z_out, m, key_z,
+                         (hipStream_t)stream);
 }
 
 extern "C" int tw_perm_index(int64_t* d_perm, int64_t n, int64_t base, int64_t n_total,
@@ -156,7 +182,7 @@ extern "C" int tw_perm_index(int64_t* d_perm, int64_t n, int64_t base, int64_t n
 
 extern "C" int tw_rank_histogram(const int64_t* d_perm, int64_t n, int64_t n_loc, int32_t G,
                                  uint64_t* d_counts, void* stream) {
-  TW_ARG_CHECK(G >= 1 && G <= 64 && n >= 0 && n_loc >= 1, "tw_rank_histogram: bad sizes");
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && n >= 0 && n_loc >= 1, "tw_rank_histogram: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * G, st));
   if (n == 0) return TW_OK;
@@ -167,17 +193,35 @@ extern "C" int tw_rank_histogram(const int64_t* d_perm, int64_t n, int64_t n_loc
   return TW_OK;
 }
 
+extern "C" int tw_source_histogram(int64_t n, int64_t base, int64_t n_total, uint64_t key,
+                                   int64_t n_loc, int32_t G, uint64_t* d_counts, void* stream) {
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && n >= 0 && n_loc >= 1 && base >= 0 &&
+                   base + n <= n_total && n_total <= n_loc * (int64_t)G && n_total < (1ll << 60),
+               "tw_source_histogram: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * G, st));
+  if (n == 0) return TW_OK;
+  const Feistel f = make_feistel(n_total, key);
+  const int blocks = (int)std::min<int64_t>(256 * 4, ceil_div(n, kBlock));
+  hipLaunchKernelGGL(k_source_histogram, dim3(blocks), dim3(kBlock), 0, st, n, base,
+                     (uint64_t)n_total, n_loc, (int)G, f, (unsigned long long*)d_counts);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 extern "C" int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int64_t n,
                                  int64_t n_loc, int32_t G, const int64_t* d_start,
-                                 uint64_t* d_cursor, void* d_send, void* stream) {
-  TW_ARG_CHECK(G >= 1 && n >= 0 && n_loc >= 1, "tw_bucket_scatter: bad sizes");
+                                 uint64_t* d_cursor, int64_t pos_base, void* d_send,
+                                 void* stream) {
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && n >= 0 && n_loc >= 1 && pos_base >= 0,
+               "tw_bucket_scatter: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   TW_HIP_CHECK(hipMemsetAsync(d_cursor, 0, sizeof(uint64_t) * G, st));
   if (n == 0) return TW_OK;
-  const int blocks = (int)std::min<int64_t>(256 * 8, ceil_div(n, kBlock));
+  const int blocks = (int)std::min<int64_t>(256 * 4, ceil_div(n, kScatChunk));
   hipLaunchKernelGGL(k_bucket_scatter, dim3(blocks), dim3(kBlock), 0, st, d_perm,
-                     (const uint64_t*)d_vals, n, n_loc, d_start, (unsigned long long*)d_cursor,
-                     (uint64_t*)d_send);
+                     (const uint64_t*)d_vals, n, n_loc, (int)G, d_start,
+                     (unsigned long long*)d_cursor, pos_base, (uint64_t*)d_send);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

@@ -160,8 +160,9 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_count(const T* __restrict
                                                              int chunks, int C, int tiles_x,
                                                              unsigned long long* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
-  const int s = blockIdx.x / tiles_x;
-  const int t = blockIdx.x - s * tiles_x;
+  const int lb = xcd_block(blockIdx.x, gridDim.x);  // a shard's x-tiles share one L2
+  const int s = lb / tiles_x;
+  const int t = lb - s * tiles_x;
   const int64_t xb = x_off[s], xe = x_off[s + 1];
   const int64_t x0 = xb + (int64_t)t * (kSortThreads * kXPerThread);
   if (x0 >= xe) return;

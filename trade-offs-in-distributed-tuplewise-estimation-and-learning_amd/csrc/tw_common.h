@@ -37,6 +37,19 @@ constexpr int kWave = 64;
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// XCD-aware block order.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (blocks b and b+8 share one XCD and its 4 MiB L2; MI355X_MICROARCH.md "Workgroup dispatch").
+// xcd_block() maps the hardware block id to a logical id so that each XCD receives one
+// CONTIGUOUS range of logical ids: with shard-major logical order an XCD works on whole
+// shards, and a shard's scores are fetched into one L2 instead of all eight.  Bijective for
+// any grid size; placement affects speed only, never results.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_block(int b, int nblocks) {
+  const int q = nblocks / kXcds, r = nblocks - q * kXcds;
+  const int x = b % kXcds, i = b / kXcds;
+  return x * q + (x < r ? x : r) + i;
+}
+
 // Wave-level sum of a 64-bit value (DPP/ds_swizzle lowering of __shfl_xor on gfx950).
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll

@@ -58,17 +58,29 @@ class HipOps:
                L.stream_handle())
         return out
 
+    def permute_pair(self, X, kx, Z, kz):
+        Xo, Zo = self.t.empty_like(X), self.t.empty_like(Z)
+        L.call("tw_permute_pair", L.ptr(X), L.ptr(Xo), int(X.numel()), int(kx), L.ptr(Z),
+               L.ptr(Zo), int(Z.numel()), int(kz), L.stream_handle())
+        return Xo, Zo
+
     def rank_histogram(self, perm, n_loc, G):
         out = L.empty((G,), self.t.int64)
         L.call("tw_rank_histogram", L.ptr(perm), int(perm.numel()), int(n_loc), int(G),
                L.ptr(out), L.stream_handle())
         return out
 
-    def bucket_scatter(self, perm, vals, n_loc, G, start):
-        send = L.empty((perm.numel(), 2), self.t.int64)
+    def source_histogram(self, n, base, n_total, key, n_loc, G):
+        out = L.empty((G,), self.t.int64)
+        L.call("tw_source_histogram", int(n), int(base), int(n_total), int(key), int(n_loc),
+               int(G), L.ptr(out), L.stream_handle())
+        return out
+
+    def bucket_scatter(self, perm, vals, n_loc, G, start, send, pos_base):
         cursor = L.empty((G,), self.t.int64)
         L.call("tw_bucket_scatter", L.ptr(perm), L.ptr(vals), int(perm.numel()), int(n_loc),
-               int(G), L.ptr(start), L.ptr(cursor), L.ptr(send), L.stream_handle())
+               int(G), L.ptr(start), L.ptr(cursor), int(pos_base), L.ptr(send),
+               L.stream_handle())
         return send
 
     def scatter_records(self, rec, out):
@@ -80,6 +92,17 @@ class HipOps:
               algo="pairs"):
         return E.count_launch(x, x_off_dev, z, z_off_dev, int(n_shards), int(max_nx),
                               int(max_nz), int(dtype), int(pred), algo)
+
+    def count_step(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype, pred,
+                   out, x_next, key_x, z_next, key_z, out_next):
+        """Counts of the current partition into `out` (already zero) and, in the same launch,
+        the next repartition into x_next / z_next and zeroing of out_next (tw_count_pairs_step)."""
+        L.call("tw_count_pairs_step", L.ptr(x), L.ptr(x_off_dev), L.ptr(z), L.ptr(z_off_dev),
+               int(n_shards), int(max_nx), int(max_nz), int(dtype), int(pred), L.ptr(out),
+               int(x.numel()), L.ptr(x_next), int(key_x), int(z.numel()), L.ptr(z_next),
+               int(key_z), L.ptr(out_next), int(out_next.numel()) if out_next is not None else 0,
+               L.stream_handle())
+        return out
 
     def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred):
         out = L.empty((n_shards,), self.t.int64)
@@ -138,29 +161,44 @@ class ShardedSample:
         self.algo = E.pick_algo(algo, self.max_nx, self.max_nz, "gt")
 
     # ------------------------------------------------------------------ repartition
-    def _permute_global(self, A, n_loc, key):
-        """Apply the global permutation (over G*n_loc elements) to the distributed array A."""
-        if self.G == 1:
-            return self.ops.permute(A, key)
-        t, dist, G = self.t, self.dist, self.G
-        perm = self.ops.perm_index(n_loc, self.rank * n_loc, G * n_loc, key)
-        send_counts = self.ops.rank_histogram(perm, n_loc, G)
-        start = t.cumsum(send_counts, 0) - send_counts
-        send = self.ops.bucket_scatter(perm, A, n_loc, G, start)
-        recv_counts = t.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-        sc = send_counts.cpu().tolist()
-        rc = recv_counts.cpu().tolist()
-        recv = t.empty((int(sum(rc)), 2), dtype=t.int64, device=A.device)
+    def _repartition_multi(self, key_x, key_z):
+        """Apply the global permutations (over G*n_loc X- and G*m_loc Z-scores) with ONE
+        all-to-all of 16-byte records.  Send counts come from the forward permutation, receive
+        counts from the inverse one (tw_source_histogram), so the only host round trip of a
+        repartition is the copy of the split sizes that all_to_all_single needs."""
+        t, dist, G, r, ops = self.t, self.dist, self.G, self.rank, self.ops
+        n, m = self.n_loc, self.m_loc
+        px = ops.perm_index(n, r * n, G * n, key_x)
+        pz = ops.perm_index(m, r * m, G * m, key_z)
+        cnt = t.stack([ops.rank_histogram(px, n, G),
+                       ops.source_histogram(n, r * n, G * n, key_x, n, G),
+                       ops.rank_histogram(pz, m, G),
+                       ops.source_histogram(m, r * m, G * m, key_z, m, G)])
+        send_tot = cnt[0] + cnt[2]
+        start_x = t.cumsum(send_tot, 0) - send_tot  # bucket g = [X records, Z records]
+        start_z = start_x + cnt[0]
+        send = t.empty((n + m, 2), dtype=t.int64, device=self.X.device)
+        ops.bucket_scatter(px, self.X, n, G, start_x, send, 0)
+        ops.bucket_scatter(pz, self.Z, m, G, start_z, send, n)  # Z positions follow X's
+        c = cnt.cpu().numpy()
+        sc = (c[0] + c[2]).tolist()
+        rc = (c[1] + c[3]).tolist()
+        if sum(rc) != n + m:
+            raise RuntimeError(f"repartition: {sum(rc)} records expected for {n + m} positions")
+        recv = t.empty_like(send)
         dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
                                group=self.group)
-        out = t.empty_like(A)
-        return self.ops.scatter_records(recv, out)
+        XZ = t.empty((n + m,), dtype=self.X.dtype, device=self.X.device)
+        ops.scatter_records(recv, XZ)
+        self.X, self.Z = XZ[:n], XZ[n:]
 
     def repartition(self, key: int):
         """One repartition: new random shards for both samples (key = any 64-bit integer)."""
-        self.X = self._permute_global(self.X, self.n_loc, (key * 2) & (2 ** 64 - 1))
-        self.Z = self._permute_global(self.Z, self.m_loc, (key * 2 + 1) & (2 ** 64 - 1))
+        kx, kz = (key * 2) & (2 ** 64 - 1), (key * 2 + 1) & (2 ** 64 - 1)
+        if self.G == 1:
+            self.X, self.Z = self.ops.permute_pair(self.X, kx, self.Z, kz)
+        else:
+            self._repartition_multi(kx, kz)
 
     # ------------------------------------------------------------------ estimation
     def local_counts(self):
@@ -178,12 +216,16 @@ class ShardedSample:
         self.dist.all_reduce(full, group=self.group)
         return full
 
-    def values(self, counts) -> list:
-        c = counts.cpu().numpy().view(np.uint64)
+    def values(self, counts) -> np.ndarray:
+        """Block values count / #pairs of the kept shards, in global shard order: each one
+        float64(count) / float64(pairs), as the reference's np.mean of a 0/1 array gives.
+        counts: (G*N,) or (T, G*N); returns an array of the same rank."""
+        c = np.asarray(counts.cpu().numpy()).view(np.uint64)
         keep = np.tile(self.keep, self.G)
-        pairs = np.tile(self.pairs, self.G)
         scale = 2 if self.tie_mode == "half" else 1
-        return [E.ratio(ci, scale * pi) for ci, pi, k in zip(c, pairs, keep) if k]
+        # uint64 -> float64 and Python int -> float are both correctly rounded, like E.ratio
+        den = np.array([float(scale * int(p)) for p in np.tile(self.pairs, self.G)])
+        return (c.astype(np.float64) / den)[..., keep]
 
     def UnN(self, key=None) -> np.float64:
         """Block-wise complete U-statistic over all G*N shards (est.UnN with prop-SWOR,
@@ -192,9 +234,76 @@ class ShardedSample:
             self.repartition(key)
         return np.mean(self.values(self.global_counts(self.local_counts())))
 
+    def UnN_many(self, keys) -> list:
+        """[UnN(k) for k in keys], in order, with identical values, without a host round trip
+        per step: the per-shard counts stay on the device until the end (one all-reduce, one
+        copy).  One GPU: one launch per step counts step i and, on spare blocks of the same
+        grid, repartitions both samples for step i+1 (tw_count_pairs_step).  Several GPUs: repartition i+1 (pack kernels, the split-size copy, the RCCL
+        all-to-all) is issued on a side stream while the counts of step i run."""
+        keys = list(keys)
+        t = self.t
+        if not keys:
+            return []
+        if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
+            return [self.UnN(k) for k in keys]
+        local = []
+        if self.G == 1 and self.algo == "pairs" and hasattr(self.ops, "count_step"):
+            # each launch counts step i and, on spare blocks, repartitions for step i+1
+            self.repartition(keys[0])
+            out = t.zeros((self.N,), dtype=t.int64, device=self.X.device)
+            for i in range(len(keys)):
+                last = i + 1 == len(keys)
+                if last:
+                    Xn = Zn = out_n = None
+                    kx = kz = 0
+                else:
+                    Xn, Zn = t.empty_like(self.X), t.empty_like(self.Z)
+                    out_n = t.empty((self.N,), dtype=t.int64, device=self.X.device)
+                    kx = (keys[i + 1] * 2) & (2 ** 64 - 1)
+                    kz = (keys[i + 1] * 2 + 1) & (2 ** 64 - 1)
+                self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                    self.max_nx, self.max_nz, self.dtype, self.pred, out, Xn, kx,
+                                    Zn, kz, out_n)
+                local.append(out)
+                if not last:
+                    self.X, self.Z, out = Xn, Zn, out_n
+        elif self.G == 1:
+            for k in keys:
+                self.repartition(k)
+                local.append(self.local_counts())
+        else:
+            main = t.cuda.current_stream()
+            if getattr(self, "_side", None) is None:
+                self._side = t.cuda.Stream()
+            side = self._side
+
+            def repartition_on_side(k):
+                self.X.record_stream(side)  # old arrays are read on side before being dropped
+                self.Z.record_stream(side)
+                with t.cuda.stream(side):
+                    self.repartition(k)
+
+            side.wait_stream(main)
+            repartition_on_side(keys[0])
+            for i in range(len(keys)):
+                main.wait_stream(side)  # repartition i (only it is queued on side so far)
+                local.append(self.local_counts())
+                self.X.record_stream(main)  # allocated on side, read by this count on main
+                self.Z.record_stream(main)
+                if i + 1 < len(keys):
+                    repartition_on_side(keys[i + 1])
+            main.wait_stream(side)
+        counts = t.stack(local)  # (T, N)
+        if self.G > 1:
+            full = t.zeros((len(keys), self.G * self.N), dtype=t.int64, device=counts.device)
+            full[:, self.rank * self.N:(self.rank + 1) * self.N] = counts
+            self.dist.all_reduce(full, group=self.group)
+            counts = full
+        return [np.mean(v) for v in self.values(counts)]
+
     def UnNT(self, T: int, key0: int = 0) -> np.float64:
         """T repartitions, averaged (est.UnNT, estimation-experiment/main.py:76-79)."""
-        return np.mean([self.UnN(key0 + t) for t in range(T)])
+        return np.mean(self.UnN_many(range(key0, key0 + T)))
 
     def UnNB(self, B: int, seed: int, key=None) -> np.float64:
         """Block-wise incomplete U-statistic with B device-drawn pairs per shard
