@@ -16,9 +16,10 @@ and the per-shard counts of all K steps are combined by one RCCL all-reduce and 
 np.mean at the end.  Weak scaling: per-GPU work is fixed (1.5625e10 pairs).
 
 value = pairs compared by all ranks / max-over-ranks wall time of the K timed steps.
-roofline: the count kernel (k_count_complete), VALU-bound: 1 compare lane-op per pair
-against the f64 vector-op peak 3.93e13 lane-op/s (256 CU x 64 lanes x 2.4 GHz; SURVEY.md
-§8(d)); its duration is measured live with HIP events on the stream it runs on.
+roofline: the count kernel (k_count_complete, launched as the one-launch step that also
+carries the next repartition), VALU-bound: 1 compare lane-op per pair against the f64
+vector-op peak 3.93e13 lane-op/s (256 CU x 64 lanes x 2.4 GHz); its duration
+is measured live with HIP events on the stream it runs on.
 cpu_baseline: the CPU port of the reference (oracle/oracle.py, identical NumPy operations to
 est.UnN) timed on rank 0 at N=1 on one full UnN of the same configuration.
 """
@@ -159,15 +160,19 @@ def sgd_replay_steps_per_s(steps):
 
 
 def pmc_traffic():
-    """HBM bytes per count-kernel launch from the committed rocprofv3 --pmc summary of this
-    exact workload (profiles/*count_pmc*.json), or None."""
+    """HBM bytes per launch of the count kernel from the committed rocprofv3 --pmc summary of
+    this workload (profiles/*count_pmc*.json, FETCH_SIZE + WRITE_SIZE): the timed one-launch
+    step (count + next repartition) and, when present, a plain count launch."""
     cands = sorted(ROOT.glob("profiles/*count_pmc*.json"))
     if not cands:
-        return None
+        return None, None
     try:
-        return json.loads(cands[-1].read_text()).get("hbm_bytes_per_launch")
+        d = json.loads(cands[-1].read_text())
     except Exception:
-        return None
+        return None, None
+    plain = [e.get("hbm_bytes_per_launch") for g, e in d.get("by_grid", {}).items()
+             if g != d.get("timed_grid")]
+    return d.get("hbm_bytes_per_launch"), (plain[0] if plain else None)
 
 
 def main():
@@ -286,6 +291,7 @@ def main():
     kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
     S.algo = "pairs"
 
+    traffic, traffic_plain = pmc_traffic()
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
     achieved = pairs_per_step_rank / (kms * 1e-3)  # lane-ops/s, 1 compare per pair (strict)
@@ -313,9 +319,13 @@ def main():
         "roofline": {"bound": "valu", "kernel": "k_count_complete",
                      "achieved": achieved / 1e12, "peak": PEAK_LANE_OPS / 1e12,
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
-                     "count_kernel_ms": kms, "traffic": pmc_traffic(),
-                     "note": "1 v_cmp_f64 lane-op per pair; traffic = HBM bytes/launch from "
-                             "the committed rocprofv3 --pmc summary"},
+                     "count_kernel_ms": kms, "traffic": traffic,
+                     "traffic_count_only": traffic_plain,
+                     "note": "1 v_cmp_f64 lane-op per pair; the timed launch also carries the "
+                             "next repartition on its tail blocks (tw_count_pairs_step); "
+                             "traffic = HBM bytes/launch (FETCH_SIZE+WRITE_SIZE) from the "
+                             "committed rocprofv3 --pmc summary: the timed launch, and a plain "
+                             "count launch (algorithmic: 16 MB of scores)"},
         "estimate_last_step": float(est),
         "sorted_count": {
             "note": "same UnN steps with the exact sort+binary-search count (algo='sorted', "
