@@ -53,6 +53,14 @@ extern "C" {
 #define TW_KERN_PROD 0  /* x * z                 */
 #define TW_KERN_GINI 1  /* |x - z|               */
 #define TW_KERN_HINGE 2 /* max(z - x + margin, 0) */
+#define TW_KERN_LOGISTIC 3 /* log(1 + exp(z - x + margin)): extension, SURVEY.md §8 row L3 */
+
+/* Pairwise losses of the gradient kernels.  TW_LOSS_HINGE is grad_inc_block's
+ * (compute_stats.py:146-162).  TW_LOSS_LOGISTIC is the pairwise-logistic loss BASELINE.json
+ * names, absent from the reference (parity pinned against
+ * oracle/oracle.py only): softplus(S), S = diff . w + margin, pair weight sigma(S). */
+#define TW_LOSS_HINGE 0
+#define TW_LOSS_LOGISTIC 1
 
 const char* tw_last_error(void);
 int tw_version(void);
@@ -154,6 +162,13 @@ int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t
                   const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
                   double margin, double* d_out, void* stream);
 
+/* Same for either loss: d_out[s*d + j] = (sum_b weight_b * diff_bj) / B in row order, with
+ * weight 1{S_b > 0} (hinge: filtered rows only, exactly as above) or sigma(S_b) (logistic). */
+int tw_pair_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                 int64_t kx, const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix,
+                 const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
+                 double margin, int32_t loss, double* d_out, void* stream);
+
 /* ---- Row L1/A9, device-RNG mode (no host RNG in the loop; graph-capturable) -----------
  * Draws are Philox4x32-10(key = seed, counter = (index, shard, step lo, tag | step hi)) with
  * step = *d_step (device memory, advanced by tw_sgd_update), mapped by 64-bit multiply-high;
@@ -171,6 +186,10 @@ int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int
 /* Tuning hook: 1 selects the unpipelined kernel for 32 < d <= 512 rows too (the pipelined
  * one is the default, 0).  Process-global; both give identical bits. */
 int tw_hinge_set_variant(int32_t legacy_wide);
+int tw_pair_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                     int64_t kx, const int64_t* d_rows_z, int64_t kz, int32_t n_shards, int64_t B,
+                     const double* d_w, double margin, int32_t loss, uint64_t seed,
+                     const uint64_t* d_step, int32_t shard_base, double* d_out, void* stream);
 int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n, uint64_t seed,
                     const uint64_t* d_step, int32_t side, int32_t shard_base, void* stream);
 

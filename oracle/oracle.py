@@ -12,6 +12,10 @@ restatement is checked against golden vectors produced by the reference itself
 Beyond the reference (the device-only paths, whose results NumPy never produced):
   feistel_perm / philox4x32_10 restate csrc/permute.hip and csrc/count.hip bit for bit so the
   device-RNG repartition and incomplete paths can be checked exactly on small inputs.
+  loss="logistic" (the pairwise-logistic loss BASELINE.json names) has
+  no reference implementation: PARITY UNPINNED against the reference.  Its restatement is
+  pinned only by its own definition — tests/test_oracle_golden.py checks the gradient against
+  finite differences of the loss.
 """
 from __future__ import annotations
 
@@ -142,30 +146,52 @@ def UN_split(X_s, Z_s, f_block):
     return np.mean([f_block(X, Z) for X, Z in zip(X_s, Z_s)], axis=0)
 
 
-def conv_AUC(margin):
+def _surrogate(t, loss):
+    """Pair loss of the convexified 1-AUC: hinge max(t, 0) (compute_stats.py:135) or, for the
+    row-L3 extension (NOT in the reference; parity unpinned against it), the logistic
+    softplus(t) = log(1 + e^t), evaluated as NumPy's stable logaddexp(0, t)."""
+    if loss == "hinge":
+        return np.maximum(t, 0)
+    if loss == "logistic":
+        return np.logaddexp(0, t)
+    raise ValueError(loss)
+
+
+def conv_AUC(margin, loss="hinge"):
     """compute_stats.py:129-135"""
     def res_function(X, Z):
-        return np.maximum(Z.reshape((1, -1)) - X.reshape((-1, 1)) + margin, 0).mean()
+        return _surrogate(Z.reshape((1, -1)) - X.reshape((-1, 1)) + margin, loss).mean()
     return res_function
 
 
-def conv_AUC_deter_pairs(margin):
+def conv_AUC_deter_pairs(margin, loss="hinge"):
     """compute_stats.py:137-144"""
     def res(X, Z, indices):
         idx = np.asarray(indices).reshape(-1, 2)
-        return np.maximum(Z[idx[:, 1]] - X[idx[:, 0]] + margin, 0).mean()
+        return _surrogate(Z[idx[:, 1]] - X[idx[:, 0]] + margin, loss).mean()
     return res
 
 
-def grad_inc_block(w, B, margin):
+def pair_grad(diff, w, margin, B, loss="hinge"):
+    """The body of grad_inc_block after the draws (compute_stats.py:157-162): hinge sums the
+    filtered rows in row order; logistic (row L3 extension) weights every row by
+    sigma(S) = 1 / (1 + e^-S), the derivative of softplus(S), and sums in row order."""
+    S_diff = diff.dot(w) + margin
+    if loss == "hinge":
+        filt = (S_diff > 0).ravel()
+        return (diff[filt].sum(axis=0) / B).reshape([-1, 1])
+    if loss == "logistic":
+        wgt = 1.0 / (1.0 + np.exp(-S_diff.ravel()))
+        return ((wgt[:, None] * diff).sum(axis=0) / B).reshape([-1, 1])
+    raise ValueError(loss)
+
+
+def grad_inc_block(w, B, margin, loss="hinge"):
     """compute_stats.py:146-162"""
     def res(X, Z):
         X_sel = X[np.random.randint(0, X.shape[0], B)]
         Z_sel = Z[np.random.randint(0, Z.shape[0], B)]
-        diff = Z_sel - X_sel
-        S_diff = diff.dot(w) + margin
-        filt = (S_diff > 0).ravel()
-        return (diff[filt].sum(axis=0) / B).reshape([-1, 1])
+        return pair_grad(Z_sel - X_sel, w, margin, B, loss)
     return res
 
 
@@ -179,7 +205,7 @@ def sgd_step(w, delta_w, gradient_mean, reg, learning_rate, optim_type="momentum
     return w - delta_w, delta_w
 
 
-def learning_trajectory(X, Z, p_learn, capture_every=1):
+def learning_trajectory(X, Z, p_learn, capture_every=1, loss="hinge", optim_type="momentum"):
     """learning_process (make_exps.py:96-141) without evaluation: returns the w before every
     gradient step (the values the reference passes to grad_inc_block at :130)."""
     N, B = p_learn["N"], p_learn["B"]
@@ -192,8 +218,9 @@ def learning_trajectory(X, Z, p_learn, capture_every=1):
             X_s, Z_s = SWR_divide(X, Z, N)
         if i % capture_every == 0:
             ws.append(np.array(w, copy=True))
-        g = UN_split(X_s, Z_s, grad_inc_block(w, B, p_learn["margin"]))
-        w, delta_w = sgd_step(w, delta_w, g, p_learn["reg"], p_learn["learning_rate"])
+        g = UN_split(X_s, Z_s, grad_inc_block(w, B, p_learn["margin"], loss))
+        w, delta_w = sgd_step(w, delta_w, g, p_learn["reg"], p_learn["learning_rate"],
+                              optim_type)
     return ws, w
 
 
@@ -358,7 +385,7 @@ def _sgd_draw(seed, step, idx, shard, tag):
     return (b << np.uint64(32)) | a, (d << np.uint64(32)) | c
 
 
-def device_rng_learning_trajectory(X, Z, p_learn, seed, optim_type="momentum"):
+def device_rng_learning_trajectory(X, Z, p_learn, seed, optim_type="momentum", loss="hinge"):
     """learning_process (make_exps.py:96-141) with the device-RNG draws of
     tw_swr_rows_rng / tw_hinge_grad_rng (tags 0x40000000 / 0x20000000 / 0x80000000) and the
     reference's gradient/update arithmetic; returns w before every step."""
@@ -381,8 +408,7 @@ def device_rng_learning_trajectory(X, Z, p_learn, seed, optim_type="momentum"):
             u, v = _sgd_draw(seed, i, np.arange(B), s, 0x80000000)
             ix, iz = _mulhi64(u, kx), _mulhi64(v, kz)
             diff = Z[rows_z[s]][iz] - X[rows_x[s]][ix]
-            filt = ((diff.dot(w) + p_learn["margin"]) > 0).ravel()
-            grads.append((diff[filt].sum(axis=0) / B).reshape([-1, 1]))
+            grads.append(pair_grad(diff, w, p_learn["margin"], B, loss))
         g = np.mean(grads, axis=0)
         w, delta_w = sgd_step(w, delta_w, g, p_learn["reg"], p_learn["learning_rate"],
                               optim_type)

@@ -176,3 +176,27 @@ def test_row_exchange_kernels_simulated_ranks(gpu):
         out = L.empty((M_q, d), torch.float64)
         L.call("tw_row_unpack", L.ptr(recv), M_q, d, L.ptr(out), L.stream_handle())
         assert np.array_equal(out.cpu().numpy(), X[rows[q * M_q:(q + 1) * M_q]])
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_logistic_learning_matches_restatement(gpu, golden, mode):
+    """learning_process(..., loss="logistic") — the pairwise-logistic SGD BASELINE.json names
+    (no reference implementation, parity pinned against the oracle's
+    restatement) — follows the oracle's trajectory within 1e-10."""
+    import tuplewise.learning as lr
+    from oracle import oracle as O
+    logging.disable(logging.CRITICAL)
+    p = _p_learn(golden, n_it=80)
+    traj = []
+    np.random.seed(41)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=traj,
+                        rng_mode=mode, loss="logistic")
+    np.random.seed(41)
+    if mode == "replay":
+        ws, _ = O.learning_trajectory(golden["learn/X"], golden["learn/Z"], p, loss="logistic")
+    else:
+        seed = int(np.random.randint(0, 2 ** 63 - 1, dtype=np.int64))
+        ws, _ = O.device_rng_learning_trajectory(golden["learn/X"], golden["learn/Z"], p, seed,
+                                                 loss="logistic")
+    np.testing.assert_allclose(np.stack(traj), np.stack(ws), rtol=1e-10, atol=1e-14)
+    assert len(p["tc_AUC"]) == len(p["iter"]) and np.all(np.isfinite(p["tc_AUC"]))

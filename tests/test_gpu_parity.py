@@ -336,8 +336,10 @@ def test_exchange_kernels_simulated_ranks(gpu):
         assert np.array_equal(out.cpu().numpy(), want[q * n_loc:(q + 1) * n_loc])
 
 
-@pytest.mark.parametrize("d,B", [(33, 100), (100, 1500), (512, 100), (512, 2100), (700, 64)])
-def test_hinge_grad_wide_rows(gpu, d, B):
+@pytest.mark.parametrize("loss", ["hinge", "logistic"])
+@pytest.mark.parametrize("d,B", [(10, 300), (33, 100), (100, 1500), (512, 100), (512, 2100),
+                                 (700, 64)])
+def test_hinge_grad_wide_rows(gpu, d, B, loss):
     """tw_hinge_grad for wide rows (the pipelined kernel for 32 < d <= 512, the unpipelined one
     above): per-shard gradients vs the restated reference body (compute_stats.py:153-162), and
     both wide kernels bit-identical to each other."""
@@ -349,6 +351,7 @@ def test_hinge_grad_wide_rows(gpu, d, B):
     w = rng.normal(size=d) / np.sqrt(d)
     rows_x = rng.randint(0, nX, size=(N, kx))
     rows_z = rng.randint(0, nZ, size=(N, kz))
+    code = L.TW_LOSS_HINGE if loss == "hinge" else L.TW_LOSS_LOGISTIC
     ix = rng.randint(0, kx, size=(N, B))
     iz = rng.randint(0, kz, size=(N, B))
     dev = [L.to_device(a) for a in (X, Z, rows_x, rows_z, ix, iz, w)]
@@ -357,16 +360,17 @@ def test_hinge_grad_wide_rows(gpu, d, B):
         L.call("tw_hinge_set_variant", legacy)
         try:
             g = _learn.hinge_grads_device(dev[0], dev[1], d, dev[2], kx, dev[3], kz, dev[4],
-                                          dev[5], N, B, dev[6], 1.0)
+                                          dev[5], N, B, dev[6], 1.0, code)
         finally:
             L.call("tw_hinge_set_variant", 0)
         outs.append(g.cpu().numpy())
     assert np.array_equal(outs[0], outs[1])
     for s in range(N):
         diff = Z[rows_z[s][iz[s]]] - X[rows_x[s][ix[s]]]
-        filt = (diff.dot(w) + 1.0) > 0
-        want = diff[filt].sum(axis=0) / B
-        np.testing.assert_allclose(outs[0][s], want, rtol=1e-12, atol=1e-15)
+        want = O.pair_grad(diff, w.reshape(-1, 1), 1.0, B, loss).ravel()
+        # hinge: same row-order sums, only BLAS's dot order differs (sign flips at |S| ~ ulp);
+        # logistic: sigma(S) also carries the device exp's last-ulp differences
+        np.testing.assert_allclose(outs[0][s], want, rtol=1e-12, atol=1e-14)
 
 
 @pytest.mark.parametrize("dtype,mode", [("f64", "gt"), ("f64", "half"), ("i64", "subgt")])
@@ -400,3 +404,30 @@ def test_count_pairs_step_fused_repartition(gpu, dtype, mode):
     assert not out_next.cpu().numpy().any()
     assert np.array_equal(xn.cpu().numpy(), O.permute_scatter(sh.x.cpu().numpy(), 11))
     assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 12))
+
+
+def test_logistic_surrogates_and_block_gradient(gpu):
+    """Row L3 extension (parity pinned against the oracle only): conv_AUC / conv_AUC_deter_pairs
+    with loss="logistic" and grad_inc_block(..., loss="logistic") inside UN_split."""
+    import tuplewise.compute_stats as cs
+    rng = np.random.RandomState(17)
+    sx, sz = rng.normal(0.3, 1, 700), rng.normal(0, 1, 300)
+    for margin in (1.0, 0.0, -0.5):
+        got = cs.conv_AUC(margin, loss="logistic")(sx, sz)
+        want = O.conv_AUC(margin, loss="logistic")(sx, sz)
+        np.testing.assert_allclose(got, want, rtol=1e-12)
+    pairs = list(zip(rng.randint(0, 700, 5000), rng.randint(0, 300, 5000)))
+    np.testing.assert_allclose(cs.conv_AUC_deter_pairs(1, loss="logistic")(sx, sz, pairs),
+                               O.conv_AUC_deter_pairs(1, loss="logistic")(sx, sz, pairs),
+                               rtol=1e-12)
+    X, Z = rng.normal(size=(400, 12)), rng.normal(0.4, 1, size=(150, 12))
+    w = rng.normal(size=(12, 1))
+    np.random.seed(9)
+    Xs, Zs = cs.SWR_divide(X, Z, 5)
+    g = cs.UN_split(Xs, Zs, cs.grad_inc_block(w, 64, 1, loss="logistic"))
+    np.random.seed(9)
+    Xo, Zo = O.SWR_divide(X, Z, 5)
+    want = O.UN_split(Xo, Zo, O.grad_inc_block(w, 64, 1, loss="logistic"))
+    np.testing.assert_allclose(g, want, rtol=1e-12, atol=1e-15)
+    with pytest.raises(ValueError):
+        cs.grad_inc_block(w, 64, 1, loss="exp")

@@ -142,3 +142,28 @@ def test_feistel_inverse_undoes_forward():
         i = np.arange(n)
         p = O.feistel_perm(i, n, key=777)
         assert np.array_equal(O.feistel_perm_inv(p, n, key=777), i)
+
+
+def test_logistic_gradient_is_the_derivative_of_its_loss():
+    """Row L3 (pairwise logistic, not in the reference: parity unpinned against it): the
+    oracle's gradient equals the finite-difference gradient of its own surrogate loss,
+    (1/B) sum_b softplus(diff_b . w + margin)."""
+    rng = np.random.RandomState(3)
+    B, d, margin = 50, 6, 0.7
+    diff = rng.normal(size=(B, d))
+    w = rng.normal(size=(d, 1))
+
+    def loss(wv):
+        return O._surrogate(diff.dot(wv).ravel() + margin, "logistic").sum() / B
+
+    g = O.pair_grad(diff, w, margin, B, "logistic").ravel()
+    h = 1e-6
+    fd = np.array([(loss(w + h * e[:, None]) - loss(w - h * e[:, None])) / (2 * h)
+                   for e in np.eye(d)])
+    np.testing.assert_allclose(g, fd, rtol=1e-7, atol=1e-9)
+    # and the hinge restatement is the subgradient of its loss away from the kinks
+    gh = O.pair_grad(diff, w, margin, B, "hinge").ravel()
+    fdh = np.array([(O._surrogate(diff.dot(w + h * e[:, None]).ravel() + margin, "hinge").sum()
+                     - O._surrogate(diff.dot(w - h * e[:, None]).ravel() + margin,
+                                    "hinge").sum()) / (2 * h * B) for e in np.eye(d)])
+    np.testing.assert_allclose(gh, fdh, rtol=1e-6, atol=1e-9)

@@ -198,7 +198,8 @@ def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,
         xx, zz, code, mode = E.subtract_gt_operands(x, z)
         counts = E.count_indexed(L.to_device(xx), L.to_device(zz), code, ix, iz, pair_off, mode)
         return [E.ratio(c, p) for c, p in zip(counts, npairs)]
-    kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI, "hinge": L.TW_KERN_HINGE}[kernel]
+    kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI, "hinge": L.TW_KERN_HINGE,
+            "logistic": L.TW_KERN_LOGISTIC}[kernel]
     xd = L.to_device(x.astype(np.float64, copy=False))
     zd = L.to_device(z.astype(np.float64, copy=False))
     sums = E.pair_sum_indexed(xd, zd, ix, iz, pair_off, kern, margin)

@@ -29,21 +29,23 @@ def _as_matrix(A) -> np.ndarray:
     return A.reshape(-1, 1) if A.ndim == 1 else A
 
 
-def hinge_grads_device(Xd, Zd, d, rows_x, kx, rows_z, kz, ixd, izd, n_shards, B, wd, margin):
-    """Per-shard gradients (n_shards, d) on the device via tw_hinge_grad."""
+def hinge_grads_device(Xd, Zd, d, rows_x, kx, rows_z, kz, ixd, izd, n_shards, B, wd, margin,
+                       loss=L.TW_LOSS_HINGE):
+    """Per-shard gradients (n_shards, d) on the device via tw_pair_grad."""
     t = L.torch()
     out = L.empty((n_shards, d), t.float64)
-    L.call("tw_hinge_grad", L.ptr(Xd), L.ptr(Zd), int(d), L.ptr(rows_x), int(kx), L.ptr(rows_z),
+    L.call("tw_pair_grad", L.ptr(Xd), L.ptr(Zd), int(d), L.ptr(rows_x), int(kx), L.ptr(rows_z),
            int(kz), L.ptr(ixd), L.ptr(izd), int(n_shards), int(B), L.ptr(wd), float(margin),
-           L.ptr(out), L.stream_handle())
+           int(loss), L.ptr(out), L.stream_handle())
     return out
 
 
 class GradSpec(Bk.BlockSpec):
-    def __init__(self, w, B, margin):
+    def __init__(self, w, B, margin, loss=L.TW_LOSS_HINGE):
         self.w = np.asarray(w, dtype=np.float64)
         self.B = int(B)
         self.margin = margin
+        self.loss = loss
 
     def draw(self, nx, nz):
         ix = np.random.randint(0, nx, self.B)
@@ -78,15 +80,15 @@ class GradSpec(Bk.BlockSpec):
         Zd, rz, kz, iza = side(Z_s, iz)
         wd = L.to_device(self.w.reshape(-1))
         out = hinge_grads_device(Xd, Zd, d, rx, kx, rz, kz, L.to_device(ixa), L.to_device(iza),
-                                 N, self.B, wd, self.margin)
+                                 N, self.B, wd, self.margin, self.loss)
         return [g.reshape(-1, 1) for g in out.cpu().numpy()]
 
     def evaluate_split(self, X_s, Z_s):
         return np.mean(self._grads(X_s, Z_s), axis=0)
 
 
-def grad_block(w, B, margin):
-    spec = GradSpec(w, B, margin)
+def grad_block(w, B, margin, loss=L.TW_LOSS_HINGE):
+    spec = GradSpec(w, B, margin, loss)
 
     def res(X, Z):
         """

@@ -17,7 +17,8 @@ LIB_PATH = _HERE / "libtuplewise.so"
 TW_OK, TW_ERR_ARG, TW_ERR_HIP = 0, 1, 2
 TW_F64, TW_I64 = 0, 1
 TW_PRED_GT, TW_PRED_HALF, TW_PRED_SUBGT = 0, 1, 2
-TW_KERN_PROD, TW_KERN_GINI, TW_KERN_HINGE = 0, 1, 2
+TW_KERN_PROD, TW_KERN_GINI, TW_KERN_HINGE, TW_KERN_LOGISTIC = 0, 1, 2, 3
+TW_LOSS_HINGE, TW_LOSS_LOGISTIC = 0, 1
 
 _vp, _i64, _i32, _u64, _f64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                ctypes.c_uint64, ctypes.c_double)
@@ -43,6 +44,10 @@ _SIGNATURES = {
     "tw_pair_sum_idx_f64": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _f64, _vp, _vp, _vp],
     "tw_hinge_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64,
                       _vp, _vp],
+    "tw_pair_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64, _i32,
+                     _vp, _vp],
+    "tw_pair_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _i32, _u64,
+                         _vp, _i32, _vp, _vp],
     "tw_hinge_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _u64,
                           _vp, _i32, _vp, _vp],
     "tw_hinge_set_variant": [_i32],

@@ -142,20 +142,37 @@ def UnNBT(X, Z, N, B, T, sampling_type, kernel="prod"):
 # ---------- Gradient descent functions ----------
 
 
-def conv_AUC(margin):
-    """Complete hinge surrogate of 1-AUC.  (compute_stats.py:129-135)"""
+_LOSSES = {"hinge": (L.TW_KERN_HINGE, L.TW_LOSS_HINGE),
+           "logistic": (L.TW_KERN_LOGISTIC, L.TW_LOSS_LOGISTIC)}
+
+
+def _loss_codes(loss):
+    if loss not in _LOSSES:
+        raise ValueError(f"loss must be 'hinge' or 'logistic', not {loss!r}")
+    return _LOSSES[loss]
+
+
+def conv_AUC(margin, *, loss="hinge"):
+    """Complete hinge surrogate of 1-AUC.  (compute_stats.py:129-135)
+
+    loss="logistic" (keyword-only extension; not in the reference):
+    softplus(z - x + margin) instead of max(z - x + margin, 0)."""
+    kern = _loss_codes(loss)[0]
+
     def res_function(X, Z):
         """Computes the convexification of the 1-AUC that we minimize."""
         X = np.asarray(X)
         Z = np.asarray(Z)
         blk = Bk.whole(X, Z)
-        return Bk.CompleteSum(L.TW_KERN_HINGE, float(margin)).evaluate(X, Z, [blk])[0]
-    return _block_fn(Bk.CompleteSum(L.TW_KERN_HINGE, float(margin)), res_function)
+        return Bk.CompleteSum(kern, float(margin)).evaluate(X, Z, [blk])[0]
+    return _block_fn(Bk.CompleteSum(kern, float(margin)), res_function)
 
 
-def conv_AUC_deter_pairs(margin):
+def conv_AUC_deter_pairs(margin, *, loss="hinge"):
     """Returns function that computes the convex loss on incomplete U-stat.
-    (compute_stats.py:137-144)"""
+    (compute_stats.py:137-144); loss as in conv_AUC."""
+    _loss_codes(loss)
+
     def res(X, Z, indices):
         """Computes the convexification of the 1-AUC that we minimize."""
         idx = np.asarray(indices, dtype=np.int64).reshape(-1, 2)
@@ -164,15 +181,18 @@ def conv_AUC_deter_pairs(margin):
         ix = _check_index(idx[:, 0], X.shape[0])
         iz = _check_index(idx[:, 1], Z.shape[0])
         off = np.array([0, len(ix)], dtype=np.int64)
-        return Bk.indexed_values(_columns(X), _columns(Z), ix, iz, off, "hinge",
+        return Bk.indexed_values(_columns(X), _columns(Z), ix, iz, off, loss,
                                  float(margin))[0]
     return res
 
 
-def grad_inc_block(w, B, margin):
+def grad_inc_block(w, B, margin, *, loss="hinge"):
     """Returns a function that computes the gradient on incomplete U-stat.
-    (compute_stats.py:146-162)"""
-    return _learn.grad_block(w, B, margin)
+    (compute_stats.py:146-162)
+
+    loss="logistic" (keyword-only extension, row L3): every drawn pair's diff is weighted by
+    sigma(diff . w + margin), the gradient of softplus, instead of the hinge filter."""
+    return _learn.grad_block(w, B, margin, _loss_codes(loss)[1])
 
 # ---------- End gradient descent functions ----------
 

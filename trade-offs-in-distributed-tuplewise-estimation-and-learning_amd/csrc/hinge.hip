@@ -30,13 +30,28 @@ constexpr int kMaxD = 4096;
 // (index, shard, step lo, tag | step hi).  Tags separate the three draw streams.
 constexpr uint32_t kTagPairs = 0x80000000u, kTagRowsX = 0x40000000u, kTagRowsZ = 0x20000000u;
 
+// Pair weights of the gradient sum.  TW_LOSS_HINGE: grad_inc_block's filter 1{S > 0}
+// (compute_stats.py:158-161), applied as a branch so unfiltered rows are skipped exactly as
+// diff[filt] skips them.  TW_LOSS_LOGISTIC (extension, SURVEY.md §8 row L3 — not in the
+// reference): the gradient of softplus(S) = log(1 + e^S), weight sigma(S) = 1 / (1 + e^-S).
+template <int LOSS>
+__device__ __forceinline__ double pair_weight(double S) {
+  if constexpr (LOSS == TW_LOSS_HINGE) return S > 0.0 ? 1.0 : 0.0;
+  else return 1.0 / (1.0 + exp(-S));
+}
+template <int LOSS>
+__device__ __forceinline__ double weighted(double wgt, double v) {
+  if constexpr (LOSS == TW_LOSS_HINGE) return wgt != 0.0 ? v : -0.0;  // -0.0 leaves sums as is
+  else return wgt * v;
+}
+
 __device__ __forceinline__ u32x4 sgd_draw(uint64_t seed, uint64_t step, uint32_t idx,
                                           uint32_t shard, uint32_t tag) {
   return philox4x32_10(u32x4{idx, shard, (uint32_t)step, tag | (uint32_t)(step >> 32)},
                        (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-template <int BS>
+template <int BS, int LOSS>
 __global__ __launch_bounds__(BS) void k_hinge_grad(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
@@ -47,7 +62,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
   double* diff = (double*)smem;                             // CH * d
   int64_t* rx = (int64_t*)(smem + sizeof(double) * CH * d);  // CH
   int64_t* rz = rx + CH;                                     // CH
-  int* flag = (int*)(rz + CH);                               // CH
+  double* flag = (double*)(rz + CH);                         // CH pair weights
 
   const int s = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -84,7 +99,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
           dr[j] = v;
           part += v * w[j];
         }
-        flag[t] = (part + margin) > 0.0;
+        flag[t] = pair_weight<LOSS>(part + margin);
       } else {
         rx[t] = rxt;
         rz[t] = rzt;
@@ -119,7 +134,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
         }
       }
       part = wave_sum_f64(part);
-      if (lane == 0) flag[t] = (part + margin) > 0.0;
+      if (lane == 0) flag[t] = pair_weight<LOSS>(part + margin);
     }
     __syncthreads();
     // column sums over the filtered rows, in row order
@@ -134,11 +149,11 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
         for (; t + 8 <= nb; t += 8) {
           double v[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = flag[t + u] ? diff[(int64_t)(t + u) * d + j] : -0.0;
+          for (int u = 0; u < 8; ++u) v[u] = weighted<LOSS>(flag[t + u], diff[(int64_t)(t + u) * d + j]);
 #pragma unroll
           for (int u = 0; u < 8; ++u) a += v[u];
         }
-        for (; t < nb; ++t) a += flag[t] ? diff[(int64_t)t * d + j] : -0.0;
+        for (; t < nb; ++t) a += weighted<LOSS>(flag[t], diff[(int64_t)t * d + j]);
         acc[q] = a;
       }
     }
@@ -167,6 +182,7 @@ constexpr int kWideCols = 8;                             // columns per lane
 constexpr int kWideMaxD = kWideCols * kWave;             // 512
 constexpr int kIdxPhase = 1024;
 
+template <int LOSS>
 __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
@@ -175,7 +191,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
     const uint64_t* __restrict__ d_step, uint32_t shard_base) {
   __shared__ double diff[kWideCH * kWideMaxD];  // 128 KiB
   __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
-  __shared__ int flag[kWideCH];
+  __shared__ double flag[kWideCH];  // pair weights
   const int s = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int dd = (int)d;
@@ -242,7 +258,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
             }
           }
           part = wave_sum_f64(part);
-          if (lane == 0) flag[t] = (part + margin) > 0.0;
+          if (lane == 0) flag[t] = pair_weight<LOSS>(part + margin);
         }
       }
       __syncthreads();
@@ -254,11 +270,11 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
         for (; t + 8 <= nb; t += 8) {
           double v[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = flag[t + u] ? diff[(t + u) * dd + j] : -0.0;
+          for (int u = 0; u < 8; ++u) v[u] = weighted<LOSS>(flag[t + u], diff[(t + u) * dd + j]);
 #pragma unroll
           for (int u = 0; u < 8; ++u) a += v[u];
         }
-        for (; t < nb; ++t) a += flag[t] ? diff[t * dd + j] : -0.0;
+        for (; t < nb; ++t) a += weighted<LOSS>(flag[t], diff[t * dd + j]);
         acc = a;
       }
       __syncthreads();
@@ -343,24 +359,40 @@ __global__ __launch_bounds__(kBlock) void k_gemv(const double* __restrict__ A, i
 
 static int g_hinge_legacy_wide = 0;  // tw_hinge_set_variant: 1 = unpipelined wide kernel
 
-int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* rows_x, int64_t kx,
-                 const int64_t* rows_z, int64_t kz, const int64_t* ix, const int64_t* iz,
-                 int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
-                 const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st) {
-  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / d));
-  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(int) * CH;
+template <int LOSS>
+void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64_t* rows_x,
+                        int64_t kx, const int64_t* rows_z, int64_t kz, const int64_t* ix,
+                        const int64_t* iz, int32_t n_shards, int64_t B, const double* w,
+                        double margin, uint64_t seed, const uint64_t* d_step,
+                        uint32_t shard_base, double* out, hipStream_t st) {
+  // per staged pair: d diff doubles + two row indices + one weight, <= 64 KiB in all
+  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / (d + 3)));
+  const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(double) * CH;
   if (d <= 32)
-    hipLaunchKernelGGL(k_hinge_grad<kBlock>, dim3(n_shards), dim3(kBlock), lds, st, X, Z, d,
-                       rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
+    hipLaunchKernelGGL((k_hinge_grad<kBlock, LOSS>), dim3(n_shards), dim3(kBlock), lds, st, X, Z,
+                       d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
                        shard_base);
   else if (d <= kWideMaxD && !g_hinge_legacy_wide)
-    hipLaunchKernelGGL(k_hinge_grad_wide, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
+    hipLaunchKernelGGL(k_hinge_grad_wide<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
                        shard_base);
   else
-    hipLaunchKernelGGL(k_hinge_grad<kWideBlock>, dim3(n_shards), dim3(kWideBlock), lds, st, X, Z,
-                       d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
-                       shard_base);
+    hipLaunchKernelGGL((k_hinge_grad<kWideBlock, LOSS>), dim3(n_shards), dim3(kWideBlock), lds, st,
+                       X, Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed,
+                       d_step, shard_base);
+}
+
+int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* rows_x, int64_t kx,
+                 const int64_t* rows_z, int64_t kz, const int64_t* ix, const int64_t* iz,
+                 int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
+                 const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st,
+                 int32_t loss = TW_LOSS_HINGE) {
+  if (loss == TW_LOSS_LOGISTIC)
+    launch_grad_kernel<TW_LOSS_LOGISTIC>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
+                                         margin, seed, d_step, shard_base, out, st);
+  else
+    launch_grad_kernel<TW_LOSS_HINGE>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
+                                      margin, seed, d_step, shard_base, out, st);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -369,18 +401,33 @@ int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* row
 
 using namespace tw;
 
+static int check_loss(int32_t loss) {
+  TW_ARG_CHECK(loss == TW_LOSS_HINGE || loss == TW_LOSS_LOGISTIC, "unknown loss %d", loss);
+  return TW_OK;
+}
+
+extern "C" int tw_pair_grad(const double* d_X, const double* d_Z, int64_t d,
+                            const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                            int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                            int32_t n_shards, int64_t B, const double* d_w, double margin,
+                            int32_t loss, double* d_out, void* stream) {
+  TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_hinge_grad: d=%lld outside [1, %d]", (long long)d, kMaxD);
+  TW_ARG_CHECK(n_shards >= 0 && B >= 1, "tw_hinge_grad: bad n_shards/B");
+  if (int rc = check_loss(loss)) return rc;
+  if (n_shards == 0) return TW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_hinge_grad: pair indices required");
+  return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
+                      margin, 0, nullptr, 0, d_out, st, loss);
+}
+
 extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
                              const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
                              int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
                              int32_t n_shards, int64_t B, const double* d_w, double margin,
                              double* d_out, void* stream) {
-  TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_hinge_grad: d=%lld outside [1, %d]", (long long)d, kMaxD);
-  TW_ARG_CHECK(n_shards >= 0 && B >= 1, "tw_hinge_grad: bad n_shards/B");
-  if (n_shards == 0) return TW_OK;
-  hipStream_t st = (hipStream_t)stream;
-  TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_hinge_grad: pair indices required");
-  return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
-                      margin, 0, nullptr, 0, d_out, st);
+  return tw_pair_grad(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
+                      margin, TW_LOSS_HINGE, d_out, stream);
 }
 
 extern "C" int tw_hinge_set_variant(int32_t legacy_wide) {
@@ -389,21 +436,32 @@ extern "C" int tw_hinge_set_variant(int32_t legacy_wide) {
   return TW_OK;
 }
 
-extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,
-                                 const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
-                                 int64_t kz, int32_t n_shards, int64_t B, const double* d_w,
-                                 double margin, uint64_t seed, const uint64_t* d_step,
-                                 int32_t shard_base, double* d_out, void* stream) {
+extern "C" int tw_pair_grad_rng(const double* d_X, const double* d_Z, int64_t d,
+                                const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                                int64_t kz, int32_t n_shards, int64_t B, const double* d_w,
+                                double margin, int32_t loss, uint64_t seed,
+                                const uint64_t* d_step, int32_t shard_base, double* d_out,
+                                void* stream) {
   TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_hinge_grad_rng: d=%lld outside [1, %d]", (long long)d,
                kMaxD);
   TW_ARG_CHECK(n_shards >= 0 && B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1,
                "tw_hinge_grad_rng: bad n_shards/B/kx/kz");
   TW_ARG_CHECK(d_step != nullptr, "tw_hinge_grad_rng: step counter required");
+  if (int rc = check_loss(loss)) return rc;
   if (n_shards == 0) return TW_OK;
   hipStream_t st = (hipStream_t)stream;
   TW_ARG_CHECK(shard_base >= 0, "tw_hinge_grad_rng: shard_base < 0");
   return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, nullptr, nullptr, n_shards, B,
-                      d_w, margin, seed, d_step, (uint32_t)shard_base, d_out, st);
+                      d_w, margin, seed, d_step, (uint32_t)shard_base, d_out, st, loss);
+}
+
+extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,
+                                 const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                                 int64_t kz, int32_t n_shards, int64_t B, const double* d_w,
+                                 double margin, uint64_t seed, const uint64_t* d_step,
+                                 int32_t shard_base, double* d_out, void* stream) {
+  return tw_pair_grad_rng(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, n_shards, B, d_w, margin,
+                          TW_LOSS_HINGE, seed, d_step, shard_base, d_out, stream);
 }
 
 extern "C" int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n,

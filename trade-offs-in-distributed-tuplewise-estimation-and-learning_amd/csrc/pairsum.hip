@@ -1,4 +1,5 @@
-// pairsum.hip — float-valued pair kernels (SURVEY.md §8 row A2 prod/gini, row f1 conv_AUC).
+// pairsum.hip — float-valued pair kernels (SURVEY.md §8 row A2 prod/gini, row f1 conv_AUC;
+// the logistic surrogate is the row-L3 extension).
 //
 //   cs.Un(kernel="prod")   compute_stats.py:15-16   mean(X_col.dot(Z_row))
 //   cs.Un(kernel="gini")   compute_stats.py:17-18   mean(|X_col - Z_row|)
@@ -16,7 +17,11 @@ template <int K>
 __device__ __forceinline__ double fkern(double x, double z, double margin) {
   if constexpr (K == TW_KERN_PROD) return x * z;
   else if constexpr (K == TW_KERN_GINI) return fabs(x - z);
-  else return fmax(z - x + margin, 0.0);
+  else if constexpr (K == TW_KERN_HINGE) return fmax(z - x + margin, 0.0);
+  else {  // TW_KERN_LOGISTIC: softplus as NumPy's logaddexp(0, t) evaluates it
+    const double t = z - x + margin;
+    return t == 0.0 ? 0.6931471805599453 : fmax(t, 0.0) + log1p(exp(-fabs(t)));
+  }
 }
 
 constexpr int kSumR = 4;           // x-values per lane
@@ -143,7 +148,7 @@ extern "C" int tw_pair_sum_f64(const double* d_x, const int64_t* d_x_off, const 
                                int64_t max_nz, int32_t kern, double margin, double* d_work,
                                double* d_out, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && max_nx >= 0 && max_nz >= 0, "tw_pair_sum_f64: bad sizes");
-  TW_ARG_CHECK(kern >= TW_KERN_PROD && kern <= TW_KERN_HINGE, "tw_pair_sum_f64: unknown kernel %d", kern);
+  TW_ARG_CHECK(kern >= TW_KERN_PROD && kern <= TW_KERN_LOGISTIC, "tw_pair_sum_f64: unknown kernel %d", kern);
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
   const SumPlan p = plan_sum(max_nx, max_nz);
@@ -152,7 +157,8 @@ extern "C" int tw_pair_sum_f64(const double* d_x, const int64_t* d_x_off, const 
   dim3 g((unsigned)(per * n_shards)), b(kBlock);
   if (kern == TW_KERN_PROD) hipLaunchKernelGGL(k_pair_sum<TW_KERN_PROD>, g, b, 0, st, d_x, d_x_off, d_z, d_z_off, p.tiles_x, p.zchunks, margin, d_work);
   else if (kern == TW_KERN_GINI) hipLaunchKernelGGL(k_pair_sum<TW_KERN_GINI>, g, b, 0, st, d_x, d_x_off, d_z, d_z_off, p.tiles_x, p.zchunks, margin, d_work);
-  else hipLaunchKernelGGL(k_pair_sum<TW_KERN_HINGE>, g, b, 0, st, d_x, d_x_off, d_z, d_z_off, p.tiles_x, p.zchunks, margin, d_work);
+  else if (kern == TW_KERN_HINGE) hipLaunchKernelGGL(k_pair_sum<TW_KERN_HINGE>, g, b, 0, st, d_x, d_x_off, d_z, d_z_off, p.tiles_x, p.zchunks, margin, d_work);
+  else hipLaunchKernelGGL(k_pair_sum<TW_KERN_LOGISTIC>, g, b, 0, st, d_x, d_x_off, d_z, d_z_off, p.tiles_x, p.zchunks, margin, d_work);
   TW_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_shards), dim3(kWave), 0, st, d_work, (int)per, d_out);
   TW_LAUNCH_CHECK();
@@ -164,7 +170,7 @@ extern "C" int tw_pair_sum_idx_f64(const double* d_x, const double* d_z, const i
                                    int32_t n_shards, int64_t max_pairs, int32_t kern,
                                    double margin, double* d_work, double* d_out, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && max_pairs >= 0, "tw_pair_sum_idx_f64: bad sizes");
-  TW_ARG_CHECK(kern >= TW_KERN_PROD && kern <= TW_KERN_HINGE, "tw_pair_sum_idx_f64: unknown kernel %d", kern);
+  TW_ARG_CHECK(kern >= TW_KERN_PROD && kern <= TW_KERN_LOGISTIC, "tw_pair_sum_idx_f64: unknown kernel %d", kern);
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
   const int64_t per = tw_pair_sum_idx_work_per_shard(max_pairs);
@@ -172,7 +178,8 @@ extern "C" int tw_pair_sum_idx_f64(const double* d_x, const double* d_z, const i
   dim3 g((unsigned)(per * n_shards)), b(kBlock);
   if (kern == TW_KERN_PROD) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_PROD, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
   else if (kern == TW_KERN_GINI) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_GINI, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
-  else hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_HINGE, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
+  else if (kern == TW_KERN_HINGE) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_HINGE, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
+  else hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_LOGISTIC, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
   TW_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_shards), dim3(kWave), 0, st, d_work, (int)per, d_out);
   TW_LAUNCH_CHECK();

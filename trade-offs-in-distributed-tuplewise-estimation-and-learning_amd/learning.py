@@ -50,7 +50,7 @@ class SGDEngine:
     through an identity row table, so the arithmetic — and the trajectory — is unchanged."""
 
     def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None,
-                 x_layout="replicated"):
+                 x_layout="replicated", loss="hinge"):
         """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is)."""
         t = L.torch()
         self.t = t
@@ -88,6 +88,7 @@ class SGDEngine:
             self.ident_x = t.arange(self.N_loc * self.kx, device=dev).view(self.N_loc, self.kx)
             self.ident_z = t.arange(self.N_loc * self.kz, device=dev).view(self.N_loc, self.kz)
         self.margin, self.reg, self.lr = float(margin), float(reg), float(learning_rate)
+        self.loss = cs._loss_codes(loss)[1]
         self.momentum = 0.9 if optim_type == "momentum" else -1.0
         self.w_shape = tuple(w_init.shape)
         self.w = _dev_f64(w_init).reshape(-1).clone()
@@ -154,9 +155,9 @@ class SGDEngine:
         t = self.t
         ixd = self._local(ix) if isinstance(ix, t.Tensor) else L.to_device(self._local(ix))
         izd = self._local(iz) if isinstance(iz, t.Tensor) else L.to_device(self._local(iz))
-        L.call("tw_hinge_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x), self.kx,
+        L.call("tw_pair_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x), self.kx,
                L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N_loc, self.B,
-               L.ptr(self.w), self.margin, L.ptr(self.grads_loc), L.stream_handle())
+               L.ptr(self.w), self.margin, self.loss, L.ptr(self.grads_loc), L.stream_handle())
         self._update()
 
     def w_host(self) -> np.ndarray:
@@ -195,9 +196,9 @@ class SGDEngine:
                L.ptr(self.step_ctr), 1, self.shard_base, s)
 
     def step_device(self):
-        L.call("tw_hinge_grad_rng", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
+        L.call("tw_pair_grad_rng", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
                self.kx, L.ptr(self.rows_z), self.kz, self.N_loc, self.B, L.ptr(self.w),
-               self.margin, self.seed, L.ptr(self.step_ctr), self.shard_base,
+               self.margin, self.loss, self.seed, L.ptr(self.step_ctr), self.shard_base,
                L.ptr(self.grads_loc), L.stream_handle())
         self._update()
 
@@ -281,7 +282,8 @@ class _ReplayDraws:
 
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
-                     rng_mode="replay", graphs=True, group=None, x_layout="replicated"):
+                     rng_mode="replay", graphs=True, group=None, x_layout="replicated",
+                     loss="hinge"):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference.
@@ -292,7 +294,9 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     and the trajectory is identical to the single-GPU one.  Every rank must call with the
     same inputs and the same NumPy global RNG state.
     x_layout: "replicated" (X, Z whole on every GPU; a reshuffle moves no data) or
-    "partitioned" (1/G of the rows per GPU; a reshuffle exchanges the drawn rows)."""
+    "partitioned" (1/G of the rows per GPU; a reshuffle exchanges the drawn rows).
+    loss: "hinge" (the reference) or "logistic" (SURVEY.md §8 row L3 extension: pairwise
+    logistic loss softplus(diff . w + margin); evaluation reports its surrogate too)."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -312,10 +316,10 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
 
     eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
-                    group=group, x_layout=x_layout)
+                    group=group, x_layout=x_layout, loss=loss)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
-        return _learning_device(eng, X, Z, p_learn, trajectory, graphs)
+        return _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss)
     if rng_mode != "replay":
         raise ValueError(f"rng_mode must be 'replay' or 'device', not {rng_mode!r}")
     draws = _ReplayDraws(N, eng.kx, eng.kz, B)
@@ -334,7 +338,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                 else:
                     X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
                 draws.rng.commit()  # np.random is consistent while foreign code runs
-                evaluation_step(i, X_s, Z_s, w, p_learn)
+                evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss)
                 draws.rng.acquire()
             if trajectory is not None:
                 trajectory.append(eng.w_host())
@@ -344,7 +348,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     return None
 
 
-def _learning_device(eng, X, Z, p_learn, trajectory, graphs):
+def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
     eng.enable_device_rng(int(np.random.randint(0, 2 ** 63 - 1, dtype=np.int64)))
     n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
     if trajectory is not None:
@@ -352,7 +356,7 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs):
     i = 0
     while i < n_it:
         if i % eval_mod == 0:
-            evaluation_step(i, None, None, eng.w_host(), p_learn)
+            evaluation_step(i, None, None, eng.w_host(), p_learn, loss=loss)
         if trajectory is not None:  # one step at a time, recording w
             if i % mod == 0:
                 eng.reshuffle_device()
@@ -406,10 +410,11 @@ def _complete(sx, sz, which, margin=0.0):
     sh = E.Shards(sx, np.array([0, n], np.int64), sz, np.array([0, m], np.int64), L.TW_F64)
     if which == "AUC":
         return E.ratio(E.count_complete(sh, "gt")[0], n * m)
-    return np.float64(E.pair_sum_complete(sh, L.TW_KERN_HINGE, margin)[0] / np.float64(n * m))
+    kern = cs._loss_codes(which)[0]
+    return np.float64(E.pair_sum_complete(sh, kern, margin)[0] / np.float64(n * m))
 
 
-def evaluation_step(i, X_s, Z_s, w, p_learn):
+def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge"):
     """
         Modify the value of p_learn to add to the evaluation.  (make_exps.py:143-190)
         Monitored values, added in p_learn:
@@ -424,7 +429,7 @@ def evaluation_step(i, X_s, Z_s, w, p_learn):
     if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
         sc_X = [x.dot(w) for x in X_s]
         sc_Z = [z.dot(w) for z in Z_s]
-        bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin)) + reg_term
+        bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin, loss=loss)) + reg_term
         br_AUC = cs.UN_split(sc_X, sc_Z, lambda x, z: cs.Un(x, z, kernel="AUC"))
     elif TYPE_TRAIN_MONITOR == "FIXED_PAIRS":
         tX = _CACHE.get("train_X", p_learn["train_X"],
@@ -435,8 +440,8 @@ def evaluation_step(i, X_s, Z_s, w, p_learn):
         ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
         n_pairs = int(off[1])
         sx, sz = _scores(tX, w), _scores(tZ, w)
-        hinge = E.pair_sum_indexed(sx, sz, ixd, izd, off, L.TW_KERN_HINGE, float(margin),
-                                   pair_off_dev=offd)[0]
+        hinge = E.pair_sum_indexed(sx, sz, ixd, izd, off, cs._loss_codes(loss)[0],
+                                   float(margin), pair_off_dev=offd)[0]
         bc_AUC = np.float64(hinge / np.float64(n_pairs)) + reg_term
         cnt = E.count_indexed(sx, sz, L.TW_F64, ixd, izd, off, "gt", pair_off_dev=offd)[0]
         br_AUC = E.ratio(cnt, n_pairs)
@@ -446,7 +451,7 @@ def evaluation_step(i, X_s, Z_s, w, p_learn):
     eZ = _CACHE.get("test_Z", p_learn["test_Z"],
                     lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
     sxt, szt = _scores(eX, w), _scores(eZ, w)
-    tc_AUC = _complete(sxt, szt, "hinge", float(margin)) + reg_term
+    tc_AUC = _complete(sxt, szt, loss, float(margin)) + reg_term
     tr_AUC = _complete(sxt, szt, "AUC")
 
     s_log = ("it %5d: bc_AUC = %.4f | br_AUC = %.4f "
