@@ -189,7 +189,12 @@ def main():
         # RCCL over xGMI; TW_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
         backend = os.environ.get("TW_BENCH_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # RCCL kernels on a high-priority stream: the repartition's all-to-all runs beside
+            # the VALU-bound count kernel of the previous step (ShardedSample.UnN_many)
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    pg_options=opts)
         else:
             dist.init_process_group(backend)
         group = dist.group.WORLD

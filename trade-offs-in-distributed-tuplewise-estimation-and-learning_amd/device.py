@@ -192,10 +192,15 @@ class ShardedSample:
         ops.scatter_records(recv, XZ)
         self.X, self.Z = XZ[:n], XZ[n:]
 
+    def _multi(self) -> bool:
+        """The exchange path (always with G > 1; at G = 1 only when _force_multi is set, a
+        probe hook for timing the multi-rank orchestration on one GPU)."""
+        return self.G > 1 or getattr(self, "_force_multi", False)
+
     def repartition(self, key: int):
         """One repartition: new random shards for both samples (key = any 64-bit integer)."""
         kx, kz = (key * 2) & (2 ** 64 - 1), (key * 2 + 1) & (2 ** 64 - 1)
-        if self.G == 1:
+        if not self._multi():
             self.X, self.Z = self.ops.permute_pair(self.X, kx, self.Z, kz)
         else:
             self._repartition_multi(kx, kz)
@@ -247,7 +252,7 @@ class ShardedSample:
         if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
             return [self.UnN(k) for k in keys]
         local = []
-        if self.G == 1 and self.algo == "pairs" and hasattr(self.ops, "count_step"):
+        if not self._multi() and self.algo == "pairs" and hasattr(self.ops, "count_step"):
             # each launch counts step i and, on spare blocks, repartitions for step i+1
             self.repartition(keys[0])
             out = t.zeros((self.N,), dtype=t.int64, device=self.X.device)
@@ -267,14 +272,17 @@ class ShardedSample:
                 local.append(out)
                 if not last:
                     self.X, self.Z, out = Xn, Zn, out_n
-        elif self.G == 1:
+        elif not self._multi():
             for k in keys:
                 self.repartition(k)
                 local.append(self.local_counts())
         else:
             main = t.cuda.current_stream()
             if getattr(self, "_side", None) is None:
-                self._side = t.cuda.Stream()
+                # high priority: the exchange's small kernels get CU slots as soon as count
+                # blocks retire (normal priority: 1.13 ms/step, high: 1.00, one-GPU path 0.88
+                # on the world-size-1 probe, tools/multi_path_probe.py)
+                self._side = t.cuda.Stream(priority=-1)
             side = self._side
 
             def repartition_on_side(k):
