@@ -42,6 +42,7 @@ C5_N = 5_000_000  # n=1e7 rows (5e6/5e6), d=512 fp64 = 41 G
 N_SHARDS = 64
 PEAK_LANE_OPS = 256 * 64 * 2.4e9  # 3.93e13 f64 vector lane-ops/s (MI355X_MICROARCH chip table)
 HBM_PEAK_GBS = 8000.0
+INC_LANE_OPS = 53  # algorithmic lane-ops per device-RNG incomplete pair
 
 
 def parse():
@@ -53,8 +54,12 @@ def parse():
     ap.add_argument("--shards", type=int, default=N_SHARDS)
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed steps before the warmup, until the GPU clock is steady")
+    ap.add_argument("--incomplete-B", type=int, default=1_000_000,
+                    help="pairs per shard of the incomplete-statistic line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sgd", action="store_true", help="skip the SGD steps/s secondary")
+    ap.add_argument("--cpu-inc-shards", type=int, default=16,
+                    help="shards of the incomplete CPU-baseline sample")
     ap.add_argument("--cpu-shards", type=int, default=N_SHARDS,
                     help="shards of the CPU-baseline sample (64 = one full UnN)")
     return ap.parse_args()
@@ -78,6 +83,26 @@ def cpu_baseline(n, N, shards):
     return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
             "sample": f"est.UnN body (in-place shuffle + {shards} of {N} prop-SWOR blocks of "
                       f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
+
+
+def cpu_baseline_incomplete(n, N, B, shards):
+    """The reference's UnNB(kernel="AUC") restated (oracle.UB per block: two randint draws and
+    a fancy-indexed compare, compute_stats.py:37-42), single-threaded, on `shards` of the N
+    prop-SWOR blocks of one shuffled sample."""
+    from oracle import oracle as O
+    rng = np.random.RandomState(1)
+    X, Z = rng.normal(0.5, 1, n), rng.normal(0, 1, n)
+    k = n // N
+    t0 = time.perf_counter()
+    np.random.shuffle(X)
+    np.random.shuffle(Z)
+    vals = [O.UB(X[s * k:(s + 1) * k], Z[s * k:(s + 1) * k], B, kernel="AUC")
+            for s in range(shards)]
+    float(np.mean(vals))
+    dt = time.perf_counter() - t0
+    return {"value": shards * B / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"cs.UnNB body (in-place shuffle + {shards} of {N} prop-SWOR blocks, "
+                      f"B={B} randint pairs each), n={n}/class, {dt:.2f} s"}
 
 
 def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="replicated"):
@@ -296,6 +321,38 @@ def main():
     kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
     S.algo = "pairs"
 
+    # incomplete U-statistic (BASELINE config C3: B pairs per shard + a repartition per step;
+    # cs.UnNBT's loop, device-RNG draws): pairs/s and the k_count_rng roofline
+    orig_rng = ops.count_rng
+
+    def timed_rng(*a, **kw):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = orig_rng(*a, **kw)
+        e1.record()
+        kernel_ms.append((e0, e1))
+        return out
+
+    ops.count_rng = timed_rng
+    B_inc = args.incomplete_B
+    S.UnNB_many(B_inc, 5, range(30_000, 30_000 + args.warmup))
+    torch.cuda.synchronize()
+    barrier()
+    kernel_ms.clear()
+    t2 = time.perf_counter()
+    est_inc = S.UnNB_many(B_inc, 1234, range(args.warmup, args.warmup + args.steps))[-1]
+    torch.cuda.synchronize()
+    barrier()
+    dt_inc = time.perf_counter() - t2
+    if group is not None:
+        tt = torch.tensor([dt_inc], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt_inc = float(tt.item())
+    kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    ops.count_rng = orig_rng
+    inc_pairs_rank = args.shards * B_inc
+
     traffic, traffic_plain = pmc_traffic()
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
@@ -339,6 +396,20 @@ def main():
             "ms_per_step": dt_sorted / args.steps * 1e3, "count_kernels_ms": kms_sorted,
             "estimate_last_step": float(est_sorted),
             "counts_identical_to_all_pairs": same_counts},
+        "incomplete": {
+            "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
+                    "drawn pairs per shard (Philox4x32-10) counted per step",
+            "B_per_shard": B_inc, "value": inc_pairs_rank * world * args.steps / dt_inc,
+            "unit": "pairs/s", "ms_per_step": dt_inc / args.steps * 1e3,
+            "estimate_last_step": float(est_inc),
+            "roofline": {"bound": "valu", "kernel": "k_count_rng",
+                         "achieved": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3) / 1e12,
+                         "peak": PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
+                         "frac": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3)
+                         / PEAK_LANE_OPS,
+                         "kernel_ms": kms_inc,
+                         "note": f"{INC_LANE_OPS} lane-ops per pair (SURVEY.md §8(d) contract "
+                                 "constant: Philox4x32-10 + 2 range maps + 1 compare)"}},
     }
     if world == 1 and not args.no_sgd:
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'
@@ -353,6 +424,8 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
+        out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, args.shards, B_inc,
+                                                                    args.cpu_inc_shards)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:

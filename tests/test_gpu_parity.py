@@ -293,6 +293,11 @@ def test_pipelined_unn_many_equals_sequential(gpu):
         assert seq == pipe
         assert torch.equal(S1.X, S2.X) and torch.equal(S1.Z, S2.Z)
         assert S2.UnNT(3, key0=40) == np.mean([S1.UnN(k) for k in (40, 41, 42)])
+    # incomplete statistic with fresh device draws per repartition (cs.UnNBT's loop)
+    S1 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
+    S2 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
+    seq = [S1.UnNB(5000, 77 + i, key=k) for i, k in enumerate(keys)]
+    assert S2.UnNB_many(5000, 77, keys) == seq
 
 
 def test_exchange_kernels_simulated_ranks(gpu):

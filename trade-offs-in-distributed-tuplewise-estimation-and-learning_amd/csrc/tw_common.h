@@ -72,8 +72,10 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t 
   constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t hi0 = __umulhi(M0, ctr.a), lo0 = M0 * ctr.a;
-    const uint32_t hi1 = __umulhi(M1, ctr.c), lo1 = M1 * ctr.c;
+    // one 32x32->64 multiply per product (v_mad_u64_u32) gives both halves
+    const uint64_t p0 = (uint64_t)M0 * ctr.a, p1 = (uint64_t)M1 * ctr.c;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     ctr = u32x4{hi1 ^ ctr.b ^ k0, lo1, hi0 ^ ctr.d ^ k1, lo0};
     k0 += W0;
     k1 += W1;

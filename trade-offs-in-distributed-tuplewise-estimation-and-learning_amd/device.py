@@ -221,15 +221,17 @@ class ShardedSample:
         self.dist.all_reduce(full, group=self.group)
         return full
 
-    def values(self, counts) -> np.ndarray:
+    def values(self, counts, pairs=None) -> np.ndarray:
         """Block values count / #pairs of the kept shards, in global shard order: each one
         float64(count) / float64(pairs), as the reference's np.mean of a 0/1 array gives.
-        counts: (G*N,) or (T, G*N); returns an array of the same rank."""
+        counts: (G*N,) or (T, G*N); returns an array of the same rank.  pairs: the pairs per
+        shard (default: all pairs of each shard; B for the incomplete statistic)."""
         c = np.asarray(counts.cpu().numpy()).view(np.uint64)
         keep = np.tile(self.keep, self.G)
         scale = 2 if self.tie_mode == "half" else 1
+        per = np.tile(self.pairs, self.G) if pairs is None else [pairs] * (self.G * self.N)
         # uint64 -> float64 and Python int -> float are both correctly rounded, like E.ratio
-        den = np.array([float(scale * int(p)) for p in np.tile(self.pairs, self.G)])
+        den = np.array([float(scale * int(p)) for p in per])
         return (c.astype(np.float64) / den)[..., keep]
 
     def UnN(self, key=None) -> np.float64:
@@ -239,20 +241,17 @@ class ShardedSample:
             self.repartition(key)
         return np.mean(self.values(self.global_counts(self.local_counts())))
 
-    def UnN_many(self, keys) -> list:
-        """[UnN(k) for k in keys], in order, with identical values, without a host round trip
-        per step: the per-shard counts stay on the device until the end (one all-reduce, one
-        copy).  One GPU: one launch per step counts step i and, on spare blocks of the same
-        grid, repartitions both samples for step i+1 (tw_count_pairs_step).  Several GPUs: repartition i+1 (pack kernels, the split-size copy, the RCCL
-        all-to-all) is issued on a side stream while the counts of step i run."""
-        keys = list(keys)
+    def _run_steps(self, keys, count_local, fusable):
+        """One repartition + one count of all local shards per key, with no host round trip
+        per step; returns the (T, G*N) device counts in global shard order (one all-reduce).
+        One GPU and a fusable (all-pairs) count: one launch per step counts step i and, on
+        spare blocks of the same grid, repartitions both samples for step i+1
+        (tw_count_pairs_step).  Several GPUs: repartition i+1 (pack kernels, the split-size
+        copy, the RCCL all-to-all) is issued on a side stream while the counts of step i run.
+        count_local(i) enqueues step i's count on the current stream."""
         t = self.t
-        if not keys:
-            return []
-        if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
-            return [self.UnN(k) for k in keys]
         local = []
-        if not self._multi() and self.algo == "pairs" and hasattr(self.ops, "count_step"):
+        if not self._multi() and fusable and hasattr(self.ops, "count_step"):
             # each launch counts step i and, on spare blocks, repartitions for step i+1
             self.repartition(keys[0])
             out = t.zeros((self.N,), dtype=t.int64, device=self.X.device)
@@ -273,9 +272,9 @@ class ShardedSample:
                 if not last:
                     self.X, self.Z, out = Xn, Zn, out_n
         elif not self._multi():
-            for k in keys:
+            for i, k in enumerate(keys):
                 self.repartition(k)
-                local.append(self.local_counts())
+                local.append(count_local(i))
         else:
             main = t.cuda.current_stream()
             if getattr(self, "_side", None) is None:
@@ -295,7 +294,7 @@ class ShardedSample:
             repartition_on_side(keys[0])
             for i in range(len(keys)):
                 main.wait_stream(side)  # repartition i (only it is queued on side so far)
-                local.append(self.local_counts())
+                local.append(count_local(i))
                 self.X.record_stream(main)  # allocated on side, read by this count on main
                 self.Z.record_stream(main)
                 if i + 1 < len(keys):
@@ -307,20 +306,44 @@ class ShardedSample:
             full[:, self.rank * self.N:(self.rank + 1) * self.N] = counts
             self.dist.all_reduce(full, group=self.group)
             counts = full
+        return counts
+
+    def UnN_many(self, keys) -> list:
+        """[UnN(k) for k in keys], in order, with identical values (est.UnNT's loop,
+        estimation-experiment/main.py:76-79), pipelined as _run_steps describes."""
+        keys = list(keys)
+        if not keys:
+            return []
+        if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
+            return [self.UnN(k) for k in keys]
+        counts = self._run_steps(keys, lambda i: self.local_counts(), self.algo == "pairs")
         return [np.mean(v) for v in self.values(counts)]
 
     def UnNT(self, T: int, key0: int = 0) -> np.float64:
         """T repartitions, averaged (est.UnNT, estimation-experiment/main.py:76-79)."""
         return np.mean(self.UnN_many(range(key0, key0 + T)))
 
+    def _count_rng(self, B, seed):
+        return self.ops.count_rng(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N, B,
+                                  seed, self.rank * self.N, self.dtype, self.pred)
+
     def UnNB(self, B: int, seed: int, key=None) -> np.float64:
         """Block-wise incomplete U-statistic with B device-drawn pairs per shard
         (cs.UnNB(kernel="AUC"), compute_stats.py:104-110, device-RNG mode)."""
         if key is not None:
             self.repartition(key)
-        local = self.ops.count_rng(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N, B,
-                                   seed, self.rank * self.N, self.dtype, self.pred)
-        c = self.global_counts(local).cpu().numpy().view(np.uint64)
-        keep = np.tile(self.keep, self.G)
-        scale = 2 if self.tie_mode == "half" else 1
-        return np.mean([E.ratio(ci, scale * B) for ci, k in zip(c, keep) if k])
+        counts = self.global_counts(self._count_rng(B, seed))
+        return np.mean(self.values(counts, pairs=B))
+
+    def UnNB_many(self, B: int, seed: int, keys) -> list:
+        """[UnNB(B, seed + t, key_t) for t, key_t in enumerate(keys)]: T repartitions, each
+        with fresh device draws (cs.UnNBT's loop, compute_stats.py:119-123), pipelined like
+        UnN_many."""
+        keys = list(keys)
+        seeds = [(seed + i) & (2 ** 64 - 1) for i in range(len(keys))]
+        if not keys:
+            return []
+        if not self.X.is_cuda:
+            return [self.UnNB(B, sd, k) for sd, k in zip(seeds, keys)]
+        counts = self._run_steps(keys, lambda i: self._count_rng(B, seeds[i]), False)
+        return [np.mean(v) for v in self.values(counts, pairs=B)]
