@@ -236,6 +236,24 @@ int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int64_t n, int6
                       int32_t G, const int64_t* d_start, uint64_t* d_cursor, int64_t pos_base,
                       void* d_send, void* stream);
 int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream);
+/* The same exchange for BOTH samples of one repartition in two launches and without a
+ * permutation array (what ShardedSample runs).  Rank `rank` owns global X positions
+ * [rank*n_loc, (rank+1)*n_loc) of G*n_loc (key_x) and Z positions likewise (m_loc, key_z).
+ * tw_exchange_counts: d_counts (4G uint64) = [send X | receive X | send Z | receive Z] per
+ *   rank; zeroes d_cursor (2G uint64 of scratch).
+ * tw_exchange_pack: d_send ((n_loc+m_loc) records of 16 bytes) grouped by destination rank g,
+ *   each group [X records | Z records] in the order of the send counts; a record is {value
+ *   bits, destination-local position}, Z positions offset by n_loc, so the receiver scatters
+ *   everything into one [X | Z] array with tw_scatter_records. */
+/* Tuning hook: grid cap (blocks) of tw_exchange_counts / tw_exchange_pack /
+ * tw_scatter_records, which run beside a count kernel (0 = default).  Results do not
+ * depend on it. */
+int tw_exchange_set_grid(int32_t blocks);
+int tw_exchange_counts(int64_t n_loc, int64_t m_loc, int32_t rank, int32_t G, uint64_t key_x,
+                       uint64_t key_z, uint64_t* d_counts, uint64_t* d_cursor, void* stream);
+int tw_exchange_pack(const void* d_x, int64_t n_loc, const void* d_z, int64_t m_loc, int32_t rank,
+                     int32_t G, uint64_t key_x, uint64_t key_z, const uint64_t* d_counts,
+                     uint64_t* d_cursor, void* d_send, void* stream);
 
 /* ---- (e): row exchange for the row-partitioned learning layout ------------------------
  * Replaces the row copies of SWR_divide (compute_stats.py:48-54) when X is split by rows over

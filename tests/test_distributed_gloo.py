@@ -77,6 +77,29 @@ class OracleOps:
         return torch.from_numpy(np.ascontiguousarray(arr))
 
 
+class OracleOpsFused(OracleOps):
+    """Adds the fused exchange (tw_exchange_counts / tw_exchange_pack) restated."""
+
+    def exchange_counts(self, n_loc, m_loc, rank, G, key_x, key_z):
+        out = []
+        for n, key in ((n_loc, key_x), (m_loc, key_z)):
+            g = np.arange(rank * n, (rank + 1) * n)
+            out.append(np.bincount(O.feistel_perm(g, G * n, key) // n, minlength=G))
+            out.append(np.bincount(O.feistel_perm_inv(g, G * n, key) // n, minlength=G))
+        return torch.from_numpy(np.concatenate(out).astype(np.int64)), None
+
+    def exchange_pack(self, X, Z, rank, G, key_x, key_z, counts, cursor):
+        n_loc, m_loc = X.numel(), Z.numel()
+        recs = []
+        for side, (A, n, key, base) in enumerate(((X, n_loc, key_x, 0), (Z, m_loc, key_z, n_loc))):
+            p = O.feistel_perm(np.arange(rank * n, (rank + 1) * n), G * n, key)
+            dst = p // n
+            recs.append((dst, np.full(n, side), A.numpy().view(np.int64), p - dst * n + base))
+        dst, side, val, pos = (np.concatenate(c) for c in zip(*recs))
+        order = np.lexsort((side, dst))  # bucket g = [X records | Z records]
+        return torch.from_numpy(np.stack([val[order], pos[order]], axis=1))
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -88,14 +111,14 @@ def _global_data(G, n_loc, m_loc):
     return rng.normal(0.4, 1, G * n_loc), rng.normal(0, 1, G * m_loc)
 
 
-def _worker(rank, G, port, n_loc, m_loc, N, keys, B, q):
+def _worker(rank, G, port, n_loc, m_loc, N, keys, B, q, fused):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     from tuplewise.device import ShardedSample
     X, Z = _global_data(G, n_loc, m_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
                       torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
-                      group=dist.group.WORLD, ops=OracleOps())
+                      group=dist.group.WORLD, ops=OracleOpsFused() if fused else OracleOps())
     vals = [float(S.UnN(k)) for k in keys]
     inc = float(S.UnNB(B, seed=77))
     Xg = [torch.empty_like(S.X) for _ in range(G)]
@@ -108,15 +131,16 @@ def _worker(rank, G, port, n_loc, m_loc, N, keys, B, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("G", [2, 4])
-def test_multirank_repartition_is_G_invariant(G):
+def test_multirank_repartition_is_G_invariant(G, fused):
     import tuplewise  # noqa: F401  (package import only; no device work in this test)
     from tuplewise.device import ShardedSample
     n_loc, m_loc, N, keys, B = 600, 450, 3, [5, 6], 200
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, G, port, n_loc, m_loc, N, keys, B, q))
+    procs = [ctx.Process(target=_worker, args=(r, G, port, n_loc, m_loc, N, keys, B, q, fused))
              for r in range(G)]
     for p in procs:
         p.start()

@@ -436,3 +436,42 @@ def test_logistic_surrogates_and_block_gradient(gpu):
     np.testing.assert_allclose(g, want, rtol=1e-12, atol=1e-15)
     with pytest.raises(ValueError):
         cs.grad_inc_block(w, 64, 1, loss="exp")
+
+
+def test_fused_exchange_kernels_simulated_ranks(gpu):
+    """tw_exchange_counts / tw_exchange_pack for G=3 ranks simulated in one process: counts vs
+    the oracle's forward/inverse permutation histograms, every bucket [X records | Z records],
+    and after the (host-side) all-to-all and the scatter both samples equal the oracle's
+    global permutations."""
+    import torch
+    from tuplewise.device import HipOps
+    ops = HipOps()
+    G, n_loc, m_loc, kx, kz = 3, 20_011, 7_003, 101, 202
+    rng = np.random.RandomState(4)
+    X, Z = rng.normal(size=G * n_loc), rng.normal(size=G * m_loc)
+    want_x, want_z = O.permute_scatter(X, kx), O.permute_scatter(Z, kz)
+    inbox = [[] for _ in range(G)]
+    for r in range(G):
+        cnt, cur = ops.exchange_counts(n_loc, m_loc, r, G, kx, kz)
+        c = cnt.cpu().numpy().reshape(4, G)
+        for row, (n, key, inv) in enumerate([(n_loc, kx, False), (n_loc, kx, True),
+                                             (m_loc, kz, False), (m_loc, kz, True)]):
+            g = np.arange(r * n, (r + 1) * n)
+            p = O.feistel_perm_inv(g, G * n, key) if inv else O.feistel_perm(g, G * n, key)
+            assert np.array_equal(c[row], np.bincount(p // n, minlength=G))
+        send = ops.exchange_pack(torch.from_numpy(X[r * n_loc:(r + 1) * n_loc]).cuda(),
+                                 torch.from_numpy(Z[r * m_loc:(r + 1) * m_loc]).cuda(), r, G, kx,
+                                 kz, cnt, cur).cpu().numpy()
+        off = np.concatenate([[0], np.cumsum(c[0] + c[2])])
+        for q in range(G):
+            b = send[off[q]:off[q + 1]]
+            assert (b[:c[0][q], 1] < n_loc).all() and (b[c[0][q]:, 1] >= n_loc).all()
+            inbox[q].append(b)
+    for q in range(G):
+        rec = np.concatenate(inbox[q])
+        assert np.array_equal(np.sort(rec[:, 1]), np.arange(n_loc + m_loc))
+        out = torch.empty(n_loc + m_loc, dtype=torch.float64, device="cuda")
+        ops.scatter_records(torch.from_numpy(rec).cuda(), out)
+        o = out.cpu().numpy()
+        assert np.array_equal(o[:n_loc], want_x[q * n_loc:(q + 1) * n_loc])
+        assert np.array_equal(o[n_loc:], want_z[q * m_loc:(q + 1) * m_loc])

@@ -27,7 +27,9 @@ X = torch.randn(n, dtype=torch.float64, device="cuda", generator=g) + 0.5
 Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
 S = ShardedSample(X, Z, N, group=dist.group.WORLD, algo="pairs")
 S._force_multi = True  # take the multi-rank code path at world size 1
-for prio in (0, -1):
+from tuplewise import _lib as L
+for prio, grid in ((0, 2048), (-1, 2048), (-1, 256), (-1, 0), (-1, 64), (-1, 32)):
+    L.call("tw_exchange_set_grid", grid)
     S._side = torch.cuda.Stream(priority=prio)
     S.UnN_many(range(30))
     torch.cuda.synchronize()
@@ -35,7 +37,9 @@ for prio in (0, -1):
     K = 30
     S.UnN_many(range(100, 100 + K))
     torch.cuda.synchronize()
-    print(f"side priority {prio}: {(time.perf_counter() - t0) / K * 1e3:.4f} ms/step", flush=True)
+    print(f"side priority {prio}, exchange grid {grid}: "
+          f"{(time.perf_counter() - t0) / K * 1e3:.4f} ms/step", flush=True)
+L.call("tw_exchange_set_grid", 0)
 S._force_multi = False
 S.UnN_many(range(30))
 torch.cuda.synchronize()

@@ -61,6 +61,9 @@ _SIGNATURES = {
     "tw_source_histogram": [_i64, _i64, _i64, _u64, _i64, _i32, _vp, _vp],
     "tw_bucket_scatter": [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64, _vp, _vp],
     "tw_scatter_records": [_vp, _i64, _vp, _vp],
+    "tw_exchange_set_grid": [_i32],
+    "tw_exchange_counts": [_i64, _i64, _i32, _i32, _u64, _u64, _vp, _vp, _vp],
+    "tw_exchange_pack": [_vp, _i64, _vp, _i64, _i32, _i32, _u64, _u64, _vp, _vp, _vp, _vp],
     "tw_row_route_counts": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
     "tw_row_pack": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "tw_row_unpack": [_vp, _i64, _i64, _vp, _vp],

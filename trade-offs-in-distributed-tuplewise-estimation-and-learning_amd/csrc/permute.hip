@@ -123,6 +123,102 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(const int64_t* __rest
   }
 }
 
+// ---- the fused exchange of ONE repartition of both samples (what ShardedSample runs): two
+// launches instead of perm_index/histogram/scan/scatter per array, and no permutation array.
+//   k_exchange_counts: per element of the X and Z slices owned here, the destination rank
+//     (forward permutation) and, per local position, the source rank (inverse permutation);
+//     counts[0..G) send X, [G..2G) receive X, [2G..3G) send Z, [3G..4G) receive Z.  Also
+//     zeroes the 2G pack cursors.
+//   k_exchange_pack: records {value, position} bucketed by destination rank, each bucket
+//     [X records | Z records], Z positions offset by n_loc; bucket starts are prefix sums of
+//     the send counts, computed by every block (G <= 64).
+__global__ __launch_bounds__(kBlock) void k_exchange_counts(int64_t n_loc, int64_t m_loc,
+                                                            int64_t xbase, int64_t zbase, int G,
+                                                            Feistel fx, Feistel fz,
+                                                            unsigned long long* __restrict__ counts,
+                                                            unsigned long long* __restrict__ cursor) {
+  __shared__ unsigned int h[4 * kMaxG];
+  for (int i = threadIdx.x; i < 4 * G; i += kBlock) h[i] = 0;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < 2 * G; i += kBlock) cursor[i] = 0;
+  __syncthreads();
+  const uint64_t NX = (uint64_t)n_loc * G, NZ = (uint64_t)m_loc * G;
+  for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < n_loc + m_loc;
+       e += (int64_t)gridDim.x * kBlock) {
+    if (e < n_loc) {
+      const uint64_t g = (uint64_t)(xbase + e);
+      atomicAdd(&h[(int)(feistel_perm(fx, g, NX) / (uint64_t)n_loc)], 1u);
+      atomicAdd(&h[G + (int)(feistel_perm_inv(fx, g, NX) / (uint64_t)n_loc)], 1u);
+    } else {
+      const uint64_t g = (uint64_t)(zbase + e - n_loc);
+      atomicAdd(&h[2 * G + (int)(feistel_perm(fz, g, NZ) / (uint64_t)m_loc)], 1u);
+      atomicAdd(&h[3 * G + (int)(feistel_perm_inv(fz, g, NZ) / (uint64_t)m_loc)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * G; i += kBlock)
+    if (h[i]) atomicAdd(counts + i, (unsigned long long)h[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_exchange_pack(
+    const uint64_t* __restrict__ xv, int64_t n_loc, const uint64_t* __restrict__ zv,
+    int64_t m_loc, int64_t xbase, int64_t zbase, int G, Feistel fx, Feistel fz,
+    const unsigned long long* __restrict__ counts, unsigned long long* __restrict__ cursor,
+    uint64_t* __restrict__ send) {
+  __shared__ int64_t start[2 * kMaxG];  // bucket start of X (g) and Z (G + g) records
+  __shared__ unsigned int lcnt[2 * kMaxG];
+  __shared__ int64_t lbase[2 * kMaxG];
+  if (threadIdx.x == 0) {
+    int64_t o = 0;
+    for (int g = 0; g < G; ++g) {
+      start[g] = o;
+      start[G + g] = o + (int64_t)counts[g];
+      o += (int64_t)counts[g] + (int64_t)counts[2 * G + g];
+    }
+  }
+  const uint64_t NX = (uint64_t)n_loc * G, NZ = (uint64_t)m_loc * G;
+  const int64_t tot = n_loc + m_loc;
+  for (int64_t c0 = (int64_t)blockIdx.x * kScatChunk; c0 < tot;
+       c0 += (int64_t)gridDim.x * kScatChunk) {
+    for (int i = threadIdx.x; i < 2 * G; i += kBlock) lcnt[i] = 0;
+    __syncthreads();
+    int bucket[kScatPer];
+    unsigned slot[kScatPer];
+    int64_t pos[kScatPer];
+#pragma unroll
+    for (int k = 0; k < kScatPer; ++k) {
+      const int64_t e = c0 + k * kBlock + threadIdx.x;
+      bucket[k] = -1;
+      if (e < n_loc) {
+        const int64_t p = (int64_t)feistel_perm(fx, (uint64_t)(xbase + e), NX);
+        const int dst = (int)(p / n_loc);
+        bucket[k] = dst;
+        pos[k] = p - (int64_t)dst * n_loc;
+      } else if (e < tot) {
+        const int64_t p = (int64_t)feistel_perm(fz, (uint64_t)(zbase + e - n_loc), NZ);
+        const int dst = (int)(p / m_loc);
+        bucket[k] = G + dst;
+        pos[k] = p - (int64_t)dst * m_loc + n_loc;  // Z follows X in the receive buffer
+      }
+      if (bucket[k] >= 0) slot[k] = atomicAdd(&lcnt[bucket[k]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * G; i += kBlock)
+      if (lcnt[i]) lbase[i] = start[i] + (int64_t)atomicAdd(cursor + i, (unsigned long long)lcnt[i]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScatPer; ++k) {
+      if (bucket[k] >= 0) {
+        const int64_t e = c0 + k * kBlock + threadIdx.x;
+        const int64_t o = lbase[bucket[k]] + slot[k];
+        send[2 * o] = e < n_loc ? xv[e] : zv[e - n_loc];
+        send[2 * o + 1] = (uint64_t)pos[k];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_scatter_records(const uint64_t* __restrict__ rec,
                                                             int64_t m, uint64_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < m;
@@ -226,10 +322,64 @@ extern "C" int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int6
   return TW_OK;
 }
 
+// Grid cap for the exchange kernels, which run beside the previous step's count kernel:
+// fewer blocks take fewer of its CU slots.  World-size-1 probe (tools/multi_path_probe.py,
+// profiles/r01_multi_path_probe.log): 1024-2048 blocks 1.00 ms/step, 128-256 blocks 0.925,
+// 32-64 blocks 1.00-1.04 (the exchange then outlasts the count); one-GPU path 0.87.
+// Tuning hook tw_exchange_set_grid (0 = this default).
+constexpr int kExchangeGrid = 128;
+static int g_exchange_grid = 0;
+static int exchange_grid(int) { return g_exchange_grid > 0 ? g_exchange_grid : kExchangeGrid; }
+
+extern "C" int tw_exchange_set_grid(int32_t blocks) {
+  TW_ARG_CHECK(blocks >= 0, "tw_exchange_set_grid: blocks >= 0");
+  g_exchange_grid = blocks;
+  return TW_OK;
+}
+
+extern "C" int tw_exchange_counts(int64_t n_loc, int64_t m_loc, int32_t rank, int32_t G,
+                                  uint64_t key_x, uint64_t key_z, uint64_t* d_counts,
+                                  uint64_t* d_cursor, void* stream) {
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && rank >= 0 && rank < G && n_loc >= 1 && m_loc >= 1 &&
+                   n_loc * (int64_t)G < (1ll << 60) && m_loc * (int64_t)G < (1ll << 60),
+               "tw_exchange_counts: bad sizes");
+  TW_ARG_CHECK(d_counts && d_cursor, "tw_exchange_counts: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * 4 * G, st));
+  const Feistel fx = make_feistel(n_loc * (int64_t)G, key_x);
+  const Feistel fz = make_feistel(m_loc * (int64_t)G, key_z);
+  const int blocks = (int)std::min<int64_t>(exchange_grid(256 * 4), ceil_div(n_loc + m_loc, kBlock));
+  hipLaunchKernelGGL(k_exchange_counts, dim3(blocks), dim3(kBlock), 0, st, n_loc, m_loc,
+                     (int64_t)rank * n_loc, (int64_t)rank * m_loc, (int)G, fx, fz,
+                     (unsigned long long*)d_counts, (unsigned long long*)d_cursor);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_exchange_pack(const void* d_x, int64_t n_loc, const void* d_z, int64_t m_loc,
+                                int32_t rank, int32_t G, uint64_t key_x, uint64_t key_z,
+                                const uint64_t* d_counts, uint64_t* d_cursor, void* d_send,
+                                void* stream) {
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && rank >= 0 && rank < G && n_loc >= 1 && m_loc >= 1 &&
+                   n_loc * (int64_t)G < (1ll << 60) && m_loc * (int64_t)G < (1ll << 60),
+               "tw_exchange_pack: bad sizes");
+  TW_ARG_CHECK(d_x && d_z && d_counts && d_cursor && d_send, "tw_exchange_pack: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const Feistel fx = make_feistel(n_loc * (int64_t)G, key_x);
+  const Feistel fz = make_feistel(m_loc * (int64_t)G, key_z);
+  const int blocks = (int)std::min<int64_t>(exchange_grid(256 * 4), ceil_div(n_loc + m_loc, kScatChunk));
+  hipLaunchKernelGGL(k_exchange_pack, dim3(blocks), dim3(kBlock), 0, st, (const uint64_t*)d_x,
+                     n_loc, (const uint64_t*)d_z, m_loc, (int64_t)rank * n_loc,
+                     (int64_t)rank * m_loc, (int)G, fx, fz, (const unsigned long long*)d_counts,
+                     (unsigned long long*)d_cursor, (uint64_t*)d_send);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 extern "C" int tw_scatter_records(const void* d_rec, int64_t m, void* d_out, void* stream) {
   TW_ARG_CHECK(m >= 0, "tw_scatter_records: bad size");
   if (m == 0) return TW_OK;
-  const int blocks = (int)std::min<int64_t>(256 * 8, ceil_div(m, kBlock));
+  const int blocks = (int)std::min<int64_t>(exchange_grid(256 * 8), ceil_div(m, kBlock));
   hipLaunchKernelGGL(k_scatter_records, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream,
                      (const uint64_t*)d_rec, m, (uint64_t*)d_out);
   TW_LAUNCH_CHECK();

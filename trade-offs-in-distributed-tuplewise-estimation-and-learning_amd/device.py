@@ -83,6 +83,21 @@ class HipOps:
                L.stream_handle())
         return send
 
+    def exchange_counts(self, n_loc, m_loc, rank, G, key_x, key_z):
+        """(4G,) counts [send X | receive X | send Z | receive Z] and the pack cursors."""
+        counts = L.empty((4 * G,), self.t.int64)
+        cursor = L.empty((2 * G,), self.t.int64)
+        L.call("tw_exchange_counts", int(n_loc), int(m_loc), int(rank), int(G), int(key_x),
+               int(key_z), L.ptr(counts), L.ptr(cursor), L.stream_handle())
+        return counts, cursor
+
+    def exchange_pack(self, X, Z, rank, G, key_x, key_z, counts, cursor):
+        send = self.t.empty((X.numel() + Z.numel(), 2), dtype=self.t.int64, device=X.device)
+        L.call("tw_exchange_pack", L.ptr(X), int(X.numel()), L.ptr(Z), int(Z.numel()),
+               int(rank), int(G), int(key_x), int(key_z), L.ptr(counts), L.ptr(cursor),
+               L.ptr(send), L.stream_handle())
+        return send
+
     def scatter_records(self, rec, out):
         L.call("tw_scatter_records", L.ptr(rec), int(rec.shape[0]), L.ptr(out),
                L.stream_handle())
@@ -164,10 +179,17 @@ class ShardedSample:
     def _repartition_multi(self, key_x, key_z):
         """Apply the global permutations (over G*n_loc X- and G*m_loc Z-scores) with ONE
         all-to-all of 16-byte records.  Send counts come from the forward permutation, receive
-        counts from the inverse one (tw_source_histogram), so the only host round trip of a
-        repartition is the copy of the split sizes that all_to_all_single needs."""
+        counts from the inverse one, so the only host round trip of a repartition is the copy
+        of the split sizes that all_to_all_single needs.  With the fused device ops
+        (tw_exchange_counts / tw_exchange_pack) that is two launches; the primitive path
+        (perm_index, rank/source histograms, bucket scatter) does the same in steps."""
         t, dist, G, r, ops = self.t, self.dist, self.G, self.rank, self.ops
         n, m = self.n_loc, self.m_loc
+        if hasattr(ops, "exchange_counts"):  # fused: two launches, no permutation array
+            cnt, cursor = ops.exchange_counts(n, m, r, G, key_x, key_z)
+            send = ops.exchange_pack(self.X, self.Z, r, G, key_x, key_z, cnt, cursor)
+            c = cnt.cpu().numpy().reshape(4, G)
+            return self._exchange_records(send, c)
         px = ops.perm_index(n, r * n, G * n, key_x)
         pz = ops.perm_index(m, r * m, G * m, key_z)
         cnt = t.stack([ops.rank_histogram(px, n, G),
@@ -181,6 +203,13 @@ class ShardedSample:
         ops.bucket_scatter(px, self.X, n, G, start_x, send, 0)
         ops.bucket_scatter(pz, self.Z, m, G, start_z, send, n)  # Z positions follow X's
         c = cnt.cpu().numpy()
+        return self._exchange_records(send, c)
+
+    def _exchange_records(self, send, c):
+        """All-to-all of the packed records (split sizes from the (4, G) host counts) and the
+        scatter into one [X | Z] array."""
+        t, dist = self.t, self.dist
+        n, m = self.n_loc, self.m_loc
         sc = (c[0] + c[2]).tolist()
         rc = (c[1] + c[3]).tolist()
         if sum(rc) != n + m:
@@ -189,7 +218,7 @@ class ShardedSample:
         dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
                                group=self.group)
         XZ = t.empty((n + m,), dtype=self.X.dtype, device=self.X.device)
-        ops.scatter_records(recv, XZ)
+        self.ops.scatter_records(recv, XZ)
         self.X, self.Z = XZ[:n], XZ[n:]
 
     def _multi(self) -> bool:
