@@ -81,6 +81,8 @@ def cpu_baseline(n, N, shards):
     dt = time.perf_counter() - t0
     pairs = shards * k * k
     return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "host_cores": {"os_cpu_count": os.cpu_count(),
+                           "affinity": len(os.sched_getaffinity(0))},
             "sample": f"est.UnN body (in-place shuffle + {shards} of {N} prop-SWOR blocks of "
                       f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
 
