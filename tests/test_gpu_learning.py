@@ -200,3 +200,31 @@ def test_logistic_learning_matches_restatement(gpu, golden, mode):
                                                  loss="logistic")
     np.testing.assert_allclose(np.stack(traj), np.stack(ws), rtol=1e-10, atol=1e-14)
     assert len(p["tc_AUC"]) == len(p["iter"]) and np.all(np.isfinite(p["tc_AUC"]))
+
+
+def test_replay_segments_graphs_match_reference(gpu, golden):
+    """Replay mode without trajectory capture: the steps between reshuffles/evaluations are
+    drawn in one native call and replayed as hipGraphs.  The evaluation lists (w at every
+    evaluation) match the reference's golden run as in the per-step path, graphs and eager
+    launches agree bit for bit, and the NumPy RNG ends in the reference's state."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for graphs in (True, False):
+        p = _p_learn(golden)
+        np.random.seed(2024)
+        lr.learning_process(golden["learn/X"], golden["learn/Z"], p, graphs=graphs)
+        out[graphs] = (p, np.random.get_state()[1].copy(), np.random.get_state()[2])
+        for k in ("iter", "norm_w"):
+            np.testing.assert_allclose(p[k], golden[f"learn/{k}"], rtol=1e-10)
+        for k in ("bc_AUC", "tc_AUC"):
+            np.testing.assert_allclose(p[k], golden[f"learn/{k}"], rtol=1e-9)
+    for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        assert out[True][0][k] == out[False][0][k], k
+    assert np.array_equal(out[True][1], out[False][1]) and out[True][2] == out[False][2]
+    # the per-step (trajectory) path leaves the same RNG state
+    p = _p_learn(golden)
+    np.random.seed(2024)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=[])
+    assert np.array_equal(np.random.get_state()[1], out[True][1])
+    assert p["norm_w"] == out[True][0]["norm_w"]

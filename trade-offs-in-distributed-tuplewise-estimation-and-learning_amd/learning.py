@@ -110,8 +110,25 @@ class SGDEngine:
                            self.Z_part, self.z_own, self.Z)
             self.rows_x, self.rows_z = self.ident_x, self.ident_z
             return
-        self.rows_x = L.to_device(np.stack(self._local(rows_x)).astype(np.int64))
-        self.rows_z = L.to_device(np.stack(self._local(rows_z)).astype(np.int64))
+        # copied into persistent tables (captured replay graphs keep valid pointers) through a
+        # pinned staging buffer, asynchronously: the host does not wait for queued steps
+        t = self.t
+        rx, rz = np.stack(self._local(rows_x)), np.stack(self._local(rows_z))
+        if self.rows_x is None or tuple(self.rows_x.shape) != rx.shape:
+            self.rows_x = L.empty(rx.shape, t.int64)
+            self.rows_z = L.empty(rz.shape, t.int64)
+            self._rows_pinned = (t.empty(rx.shape, dtype=t.int64, pin_memory=True),
+                                 t.empty(rz.shape, dtype=t.int64, pin_memory=True))
+            self._rows_done = None
+        if self._rows_done is not None:
+            self._rows_done.synchronize()  # the previous upload has left the staging buffer
+        hx, hz = self._rows_pinned
+        hx.numpy()[...] = rx
+        hz.numpy()[...] = rz
+        self.rows_x.copy_(hx, non_blocking=True)
+        self.rows_z.copy_(hz, non_blocking=True)
+        self._rows_done = t.cuda.Event()
+        self._rows_done.record()
 
     def _exchange(self, rows, k, part, own, out):
         """Partitioned layout: move the rows drawn for this rank's shards (rows: all N*k global
@@ -159,6 +176,28 @@ class SGDEngine:
                L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N_loc, self.B,
                L.ptr(self.w), self.margin, self.loss, L.ptr(self.grads_loc), L.stream_handle())
         self._update()
+
+    def run_replay_segment(self, draws_dev, nsteps: int, graphs: bool = True, tag=0):
+        """nsteps replay steps whose NumPy draws sit in draws_dev[s] ((2, N, B) int64 on the
+        device): one gradient + one update launch per step, replayed from a hipGraph captured
+        per (tag, nsteps) — tag names the draw buffer, whose address the graph holds — or
+        launched eagerly (graphs=False, or a collective in the step)."""
+        if not graphs or self.G > 1:
+            for st in range(nsteps):
+                self.step(draws_dev[st, 0], draws_dev[st, 1])
+            return
+        t = self.t
+        if not hasattr(self, "_replay_graphs"):
+            self._replay_graphs = {}
+        key = (tag, nsteps, draws_dev.data_ptr())
+        g = self._replay_graphs.get(key)
+        if g is None:
+            g = t.cuda.CUDAGraph()
+            with t.cuda.graph(g):
+                for st in range(nsteps):
+                    self.step(draws_dev[st, 0], draws_dev[st, 1])
+            self._replay_graphs[key] = g
+        g.replay()
 
     def w_host(self) -> np.ndarray:
         return self.w.cpu().numpy().reshape(self.w_shape)
@@ -265,6 +304,35 @@ class _ReplayDraws:
         flat = self.rng.randint_flat([0] * (2 * N), [n_X] * N + [n_Z] * N, [kx] * N + [kz] * N)
         return list(flat[:N * kx].reshape(N, kx)), list(flat[N * kx:].reshape(N, kz))
 
+    def segment_capacity(self) -> int:
+        """Steps per drawn segment: <= 256, and <= 64 MiB of int64 draws per buffer."""
+        per = 2 * self.N * self.B * 8
+        return int(max(1, min(256, (64 << 20) // per)))
+
+    def pairs_segment(self, S):
+        """Draws of the next S steps (NumPy's order) into one of two pinned buffers, shipped
+        with one asynchronous H2D copy; returns (device buffer (S_cap, 2, N, B), tag)."""
+        t = L.torch()
+        if not hasattr(self, "seg_host"):
+            cap = self.segment_capacity()
+            shape = (cap, 2, self.N, self.B)
+            self.seg_host = [t.empty(shape, dtype=t.int64, pin_memory=True) for _ in range(2)]
+            self.seg_np = [h.numpy() for h in self.seg_host]
+            self.seg_dev = [L.empty(shape, t.int64) for _ in range(2)]
+            self.seg_done = [None, None]
+            self.seg_k = 0
+        k = self.seg_k
+        self.seg_k ^= 1
+        if self.seg_done[k] is not None:
+            self.seg_done[k].synchronize()  # the copy out of seg_host[k] two segments back
+        self.rng.pairs_steps(S, self.N, self.kx, self.kz, self.B, self.seg_np[k])
+        # stream-ordered: the graph that read seg_dev[k] two segments back precedes this copy
+        self.seg_dev[k][:S].copy_(self.seg_host[k][:S], non_blocking=True)
+        if self.seg_done[k] is None:
+            self.seg_done[k] = t.cuda.Event()
+        self.seg_done[k].record()
+        return self.seg_dev[k], k
+
     def pairs(self):
         t = L.torch()
         k = self.k
@@ -286,7 +354,9 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                      loss="hinge"):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
-    rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference.
+    rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference; the
+    steps between two reshuffles/evaluations are drawn in one native call and, with
+    graphs=True, replayed as one hipGraph.
     rng_mode="device": SWR rows and pairs drawn on the device from a seed taken from the
     global RNG (one randint); statistically equivalent, and with graphs=True each run of
     steps between evaluations/reshuffles is one hipGraph replay.
@@ -326,11 +396,13 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     with draws.rng:  # the global RNG state lives natively until the loop ends
         rows_x, rows_z = draws.swr_rows(n_X, n_Z)  # the reference's redundant draw (:119)
         eng.set_shards(rows_x, rows_z)
-        for i in range(0, p_learn["n_it"]):
-            if i % p_learn["reshuffle_mod"] == 0:
+        n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
+        i = 0
+        while i < n_it:
+            if i % mod == 0:
                 rows_x, rows_z = draws.swr_rows(n_X, n_Z)
                 eng.set_shards(rows_x, rows_z)
-            if i % p_learn["eval_mod"] == 0:
+            if i % eval_mod == 0:
                 w = eng.w_host()
                 if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
                     X_s = [X[r] for r in rows_x]
@@ -340,11 +412,20 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                 draws.rng.commit()  # np.random is consistent while foreign code runs
                 evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss)
                 draws.rng.acquire()
-            if trajectory is not None:
-                trajectory.append(eng.w_host())
-            ix, iz = draws.pairs()
             assert optim_type in ["SGD", "momentum"]
-            eng.step(ix, iz)
+            if trajectory is not None:  # one step at a time, recording w
+                trajectory.append(eng.w_host())
+                ix, iz = draws.pairs()
+                eng.step(ix, iz)
+                i += 1
+                continue
+            # the steps up to the next reshuffle / evaluation draw nothing else from the RNG:
+            # draw them all at once (same order) and replay them as one graph
+            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
+                      i + draws.segment_capacity())
+            buf, tag = draws.pairs_segment(nxt - i)
+            eng.run_replay_segment(buf, nxt - i, graphs, tag)
+            i = nxt
     return None
 
 
