@@ -186,6 +186,38 @@ def sgd_replay_steps_per_s(steps):
                        "steps": steps}}
 
 
+def learning_end_to_end(steps, rng_mode):
+    """learning_process at the C4 shape WITH its evaluation every 25 steps (make_exps.py:
+    122-141, 143-190): shuttle-shaped synthetic train/test sets, 450k fixed monitor pairs
+    (make_exps.py:216-224).  The reference spends ~2.6 ms per step and 158 ms per evaluation
+    here, i.e. ~110 steps/s."""
+    import logging
+    import torch
+    import tuplewise.learning as lr
+    rng = np.random.RandomState(4)
+    X = np.hstack([rng.normal(size=(9117, 9)), np.ones((9117, 1))])
+    Z = np.hstack([rng.normal(0.5, 1, size=(702, 9)), np.ones((702, 1))])
+    Xe = np.hstack([rng.normal(size=(2279, 9)), np.ones((2279, 1))])
+    Ze = np.hstack([rng.normal(0.5, 1, size=(175, 9)), np.ones((175, 1))])
+    mon = list(zip(rng.randint(0, 9117, 450000), rng.randint(0, 702, 450000)))
+    p = {"n_it": steps, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": 25, "reg": 0.05,
+         "learning_rate": 0.01, "eval_mod": 25, "w_init": rng.normal(size=(10, 1)),
+         "test_X": Xe, "test_Z": Ze, "train_mon_pairs": mon, "train_X": X, "train_Z": Z}
+    logging.disable(logging.CRITICAL)
+    np.random.seed(0)
+    lr.learning_process(X, Z, dict(p, n_it=50), rng_mode=rng_mode)  # warm (captures graphs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lr.learning_process(X, Z, p, rng_mode=rng_mode)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "evaluations": len(p["iter"]),
+            "config": {"n_X": 9117, "n_Z": 702, "d": 10, "N": 100, "B": 100,
+                       "reshuffle_mod": 25, "eval_mod": 25, "monitor_pairs": 450000,
+                       "test": "2279 x 175", "rng": rng_mode, "steps": steps}}
+
+
 def pmc_traffic():
     """HBM bytes per launch of the count kernel from the committed rocprofv3 --pmc summary of
     this workload (profiles/*count_pmc*.json, FETCH_SIZE + WRITE_SIZE): the timed one-launch
@@ -419,6 +451,8 @@ def main():
             "metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)",
             "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2),
             "C4_shuttle_shape_replay": sgd_replay_steps_per_s(2000),
+            "C4_end_to_end_with_evaluation_replay": learning_end_to_end(2000, "replay"),
+            "C4_end_to_end_with_evaluation_device": learning_end_to_end(2000, "device"),
             "C5_scaled_d512": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2),
             "C5_scaled_d512_B4096": sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1),
             "C5_scaled_d512_partitioned": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,

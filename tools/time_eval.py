@@ -21,3 +21,12 @@ for i in range(20):
 torch.cuda.synchronize()
 print(f"evaluation_step: {(time.perf_counter() - t0) / 20 * 1e3:.3f} ms per call "
       f"(reference: 158 ms, SURVEY.md §3)")
+wd = torch.from_numpy(w.reshape(-1)).cuda()
+lr.evaluation_step(0, None, None, w, p, _w_dev=wd)  # warm: captures the evaluation graph
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i in range(20):
+    lr.evaluation_step(i, None, None, w, p, _w_dev=wd)
+torch.cuda.synchronize()
+print(f"evaluation_step with w resident (the learning loop's call): "
+      f"{(time.perf_counter() - t0) / 20 * 1e3:.3f} ms per call")

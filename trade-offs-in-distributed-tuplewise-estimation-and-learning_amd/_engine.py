@@ -189,22 +189,33 @@ def _idx_dev(a):
     return L.to_device(np.asarray(a, dtype=np.int64))
 
 
+def count_indexed_dev(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray, pred: int,
+                      pair_off_dev=None):
+    """Per-shard counts over index pairs, enqueued only: the (n_shards,) int64 device tensor
+    (uint64 semantics)."""
+    t = L.torch()
+    n = len(pair_off) - 1
+    ixd, izd = _idx_dev(ix), _idx_dev(iz)
+    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
+    max_pairs = int(np.diff(pair_off).max())
+    out = L.empty((n,), t.int64)
+    L.call("tw_count_pairs_idx", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd),
+           L.ptr(pod), n, max_pairs, dtype_code, pred, L.ptr(out), L.stream_handle())
+    return out
+
+
 def count_indexed(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray,
                   mode: str = "gt", pair_off_dev=None) -> np.ndarray:
     """Per-shard counts over explicit (absolute) index pairs (host or device index arrays)."""
     n = len(pair_off) - 1
     if n == 0:
         return np.zeros(0, dtype=np.uint64)
-    t = L.torch()
     ixd, izd = _idx_dev(ix), _idx_dev(iz)
     pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
-    max_pairs = int(np.diff(pair_off).max())
 
     def run(pred):
-        out = L.empty((n,), t.int64)
-        L.call("tw_count_pairs_idx", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd),
-               L.ptr(pod), n, max_pairs, dtype_code, pred, L.ptr(out), L.stream_handle())
-        return _counts_to_host(out)
+        return _counts_to_host(count_indexed_dev(x_dev, z_dev, dtype_code, ixd, izd, pair_off,
+                                                 pred, pod))
 
     if mode == "ne":
         half = run(L.TW_PRED_HALF).astype(object)
@@ -217,9 +228,14 @@ def count_indexed(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray,
 
 def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
     """Per-shard float64 sums of kern(x_i, z_j) over all pairs."""
-    n = sh.n_shards
-    if n == 0:
+    if sh.n_shards == 0:
         return np.zeros(0)
+    return pair_sum_complete_dev(sh, kern, margin).cpu().numpy()
+
+
+def pair_sum_complete_dev(sh: Shards, kern: int, margin: float = 0.0):
+    """pair_sum_complete, enqueued only: the (n_shards,) float64 device tensor."""
+    n = sh.n_shards
     t = L.torch()
     xo, zo = sh.offsets_dev()
     max_nx, max_nz = int(sh.nx.max()), int(sh.nz.max())
@@ -228,14 +244,21 @@ def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
     out = L.empty((n,), t.float64)
     L.call("tw_pair_sum_f64", L.ptr(sh.x), L.ptr(xo), L.ptr(sh.z), L.ptr(zo), n, max_nx, max_nz,
            kern, float(margin), L.ptr(work), L.ptr(out), L.stream_handle())
-    return out.cpu().numpy()
+    return out
 
 
 def pair_sum_indexed(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 0.0,
                      pair_off_dev=None):
-    n = len(pair_off) - 1
-    if n == 0:
+    if len(pair_off) - 1 == 0:
         return np.zeros(0)
+    return pair_sum_indexed_dev(x_dev, z_dev, ix, iz, pair_off, kern, margin,
+                                pair_off_dev).cpu().numpy()
+
+
+def pair_sum_indexed_dev(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 0.0,
+                         pair_off_dev=None):
+    """pair_sum_indexed, enqueued only: the (n_shards,) float64 device tensor."""
+    n = len(pair_off) - 1
     t = L.torch()
     ixd, izd = _idx_dev(ix), _idx_dev(iz)
     pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
@@ -245,7 +268,7 @@ def pair_sum_indexed(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 
     out = L.empty((n,), t.float64)
     L.call("tw_pair_sum_idx_f64", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd), L.ptr(pod),
            n, max_pairs, kern, float(margin), L.ptr(work), L.ptr(out), L.stream_handle())
-    return out.cpu().numpy()
+    return out
 
 
 def ratio(count, pairs) -> np.float64:

@@ -202,6 +202,21 @@ class SGDEngine:
     def w_host(self) -> np.ndarray:
         return self.w.cpu().numpy().reshape(self.w_shape)
 
+    def w_host_async(self):
+        """Start copying w to pinned host memory; returns a callable that waits and gives
+        the array (the host can draw the next segment meanwhile)."""
+        t = self.t
+        if getattr(self, "_w_pinned", None) is None:
+            self._w_pinned = t.empty(self.w.shape, dtype=t.float64, pin_memory=True)
+            self._w_event = t.cuda.Event()
+        self._w_pinned.copy_(self.w, non_blocking=True)
+        self._w_event.record()
+
+        def wait():
+            self._w_event.synchronize()
+            return self._w_pinned.numpy().reshape(self.w_shape).copy()
+        return wait
+
     # ------------------------------------------------------------ device-RNG mode
     def enable_device_rng(self, seed: int):
         """Draw SWR rows and pair indices on the device (Philox keyed by `seed`, counter =
@@ -402,31 +417,38 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
             if i % mod == 0:
                 rows_x, rows_z = draws.swr_rows(n_X, n_Z)
                 eng.set_shards(rows_x, rows_z)
-            if i % eval_mod == 0:
-                w = eng.w_host()
-                if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
-                    X_s = [X[r] for r in rows_x]
-                    Z_s = [Z[r] for r in rows_z]
-                else:
-                    X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
-                draws.rng.commit()  # np.random is consistent while foreign code runs
-                evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss)
-                draws.rng.acquire()
             assert optim_type in ["SGD", "momentum"]
             if trajectory is not None:  # one step at a time, recording w
+                if i % eval_mod == 0:
+                    _evaluate(i, eng, eng.w_host(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
                 trajectory.append(eng.w_host())
                 ix, iz = draws.pairs()
                 eng.step(ix, iz)
                 i += 1
                 continue
-            # the steps up to the next reshuffle / evaluation draw nothing else from the RNG:
-            # draw them all at once (same order) and replay them as one graph
+            # The steps up to the next reshuffle / evaluation draw nothing else from the RNG
+            # (evaluation_step draws nothing either): draw them all at once, in the same
+            # order, while the device still runs the previous segment, and replay them as one
+            # graph.  At an evaluation, w leaves the device asynchronously before the draws.
             nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
                       i + draws.segment_capacity())
+            w_pending = eng.w_host_async() if i % eval_mod == 0 else None
             buf, tag = draws.pairs_segment(nxt - i)
+            if w_pending is not None:
+                _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
             eng.run_replay_segment(buf, nxt - i, graphs, tag)
             i = nxt
     return None
+
+
+def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs):
+    """evaluation_step at step i of the replay loop (make_exps.py:127-128)."""
+    if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
+        X_s = [X[r] for r in rows_x]
+        Z_s = [Z[r] for r in rows_z]
+    else:
+        X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
+    evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss, _w_dev=eng.w, _graph=graphs)
 
 
 def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
@@ -437,7 +459,8 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
     i = 0
     while i < n_it:
         if i % eval_mod == 0:
-            evaluation_step(i, None, None, eng.w_host(), p_learn, loss=loss)
+            evaluation_step(i, None, None, eng.w_host(), p_learn, loss=loss, _w_dev=eng.w,
+                            _graph=graphs)
         if trajectory is not None:  # one step at a time, recording w
             if i % mod == 0:
                 eng.reshuffle_device()
@@ -476,26 +499,72 @@ def _pairs_dev(pairs):
             off, L.to_device(off))
 
 
-def _scores(A_dev, w):
-    """A @ w on the device (tw_gemv_f64)."""
+def _scores(A_dev, wd):
+    """A @ w on the device (tw_gemv_f64); wd: w as a (d,) float64 device tensor."""
     t = L.torch()
-    wd = L.to_device(np.asarray(w, dtype=np.float64).reshape(-1))
     out = L.empty((A_dev.shape[0],), t.float64)
     L.call("tw_gemv_f64", L.ptr(A_dev), A_dev.shape[0], A_dev.shape[1], L.ptr(wd), L.ptr(out),
            L.stream_handle())
     return out
 
 
-def _complete(sx, sz, which, margin=0.0):
-    n, m = sx.shape[0], sz.shape[0]
-    sh = E.Shards(sx, np.array([0, n], np.int64), sz, np.array([0, m], np.int64), L.TW_F64)
-    if which == "AUC":
-        return E.ratio(E.count_complete(sh, "gt")[0], n * m)
-    kern = cs._loss_codes(which)[0]
-    return np.float64(E.pair_sum_complete(sh, kern, margin)[0] / np.float64(n * m))
+def _eval_sources(p_learn, fixed):
+    """The p_learn objects the device evaluation reads (a cached graph is valid while
+    p_learn still holds these very objects)."""
+    keys = ("test_X", "test_Z") + (("train_X", "train_Z", "train_mon_pairs") if fixed else ())
+    return tuple(p_learn[k] for k in keys)
 
 
-def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge"):
+_OFFSETS = {}
+
+
+def _offsets(n, m):
+    """Host and device offsets of one (n, m) shard, uploaded once."""
+    if (n, m) not in _OFFSETS:
+        xo, zo = np.array([0, n], np.int64), np.array([0, m], np.int64)
+        _OFFSETS[(n, m)] = (xo, zo, L.to_device(xo), L.to_device(zo))
+    return _OFFSETS[(n, m)]
+
+
+def _eval_device(wd, p_learn, loss, margin, fixed):
+    """Every device statistic of evaluation_step, enqueued only (graph-capturable: no host
+    copies, no syncs).  Returns (float64 device tensor [monitor surrogate sum, monitor count
+    bits, test surrogate sum, test count bits], #monitor pairs, #test pairs)."""
+    t = L.torch()
+    kern = cs._loss_codes(loss)[0]
+    parts = []
+    n_pairs = 0
+    if fixed:
+        tX = _CACHE.get("train_X", p_learn["train_X"],
+                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+        tZ = _CACHE.get("train_Z", p_learn["train_Z"],
+                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+        # the monitor pairs live on the device for as long as p_learn holds the same list
+        ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
+        n_pairs = int(off[1])
+        sx, sz = _scores(tX, wd), _scores(tZ, wd)
+        parts += [E.pair_sum_indexed_dev(sx, sz, ixd, izd, off, kern, float(margin),
+                                         pair_off_dev=offd),
+                  E.count_indexed_dev(sx, sz, L.TW_F64, ixd, izd, off, L.TW_PRED_GT,
+                                      pair_off_dev=offd).view(t.float64)]
+    else:
+        parts.append(t.zeros((2,), dtype=t.float64, device=wd.device))
+    eX = _CACHE.get("test_X", p_learn["test_X"],
+                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+    eZ = _CACHE.get("test_Z", p_learn["test_Z"],
+                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+    sxt, szt = _scores(eX, wd), _scores(eZ, wd)
+    n, m = sxt.shape[0], szt.shape[0]
+    xo, zo, xod, zod = _offsets(n, m)
+    sh = E.Shards(sxt, xo, szt, zo, L.TW_F64)
+    sh._x_off_dev, sh._z_off_dev = xod, zod
+    parts += [E.pair_sum_complete_dev(sh, kern, margin),
+              E.count_launch(sxt, xod, szt, zod, 1, n, m, L.TW_F64, L.TW_PRED_GT,
+                             E.pick_algo("auto", n, m, "gt")).view(t.float64)]
+    return t.cat([v.reshape(-1) for v in parts]), n_pairs, n * m
+
+
+def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _graph=True):
     """
         Modify the value of p_learn to add to the evaluation.  (make_exps.py:143-190)
         Monitored values, added in p_learn:
@@ -507,33 +576,47 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge"):
     margin = p_learn["margin"]
     logging.debug("Step %d: Begin evaluation", i)
     reg_term = p_learn["reg"] * (np.linalg.norm(w) ** 2) / 2
+    t = L.torch()
     if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
         sc_X = [x.dot(w) for x in X_s]
         sc_Z = [z.dot(w) for z in Z_s]
         bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin, loss=loss)) + reg_term
         br_AUC = cs.UN_split(sc_X, sc_Z, lambda x, z: cs.Un(x, z, kernel="AUC"))
-    elif TYPE_TRAIN_MONITOR == "FIXED_PAIRS":
-        tX = _CACHE.get("train_X", p_learn["train_X"],
-                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-        tZ = _CACHE.get("train_Z", p_learn["train_Z"],
-                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-        # the monitor pairs live on the device for as long as p_learn holds the same list
-        ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
-        n_pairs = int(off[1])
-        sx, sz = _scores(tX, w), _scores(tZ, w)
-        hinge = E.pair_sum_indexed(sx, sz, ixd, izd, off, cs._loss_codes(loss)[0],
-                                   float(margin), pair_off_dev=offd)[0]
-        bc_AUC = np.float64(hinge / np.float64(n_pairs)) + reg_term
-        cnt = E.count_indexed(sx, sz, L.TW_F64, ixd, izd, off, "gt", pair_off_dev=offd)[0]
-        br_AUC = E.ratio(cnt, n_pairs)
-
-    eX = _CACHE.get("test_X", p_learn["test_X"],
-                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-    eZ = _CACHE.get("test_Z", p_learn["test_Z"],
-                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-    sxt, szt = _scores(eX, w), _scores(eZ, w)
-    tc_AUC = _complete(sxt, szt, loss, float(margin)) + reg_term
-    tr_AUC = _complete(sxt, szt, "AUC")
+    fixed = TYPE_TRAIN_MONITOR == "FIXED_PAIRS"
+    if _w_dev is not None and _graph:  # the learning loop: w resident, device work one graph
+        # one cached graph: valid while p_learn holds the same objects; w reaches it through
+        # a persistent buffer, so later runs (new engines, new w) replay it too
+        key = (fixed, loss, float(margin), int(_w_dev.numel()))
+        srcs = _eval_sources(p_learn, fixed)
+        ent = _CACHE.dev.get("eval_graph")
+        if (ent is None or ent[0] != key or len(ent[1]) != len(srcs)
+                or any(a is not b for a, b in zip(ent[1], srcs))):
+            _CACHE.dev["eval_graph"] = None  # release the previous graph's pool first
+            g = t.cuda.CUDAGraph()
+            wbuf = t.empty_like(_w_dev)
+            wbuf.copy_(_w_dev)
+            _eval_device(wbuf, p_learn, loss, margin, fixed)  # warm: caches, allocations
+            t.cuda.synchronize()
+            with t.cuda.graph(g):
+                out = _eval_device(wbuf, p_learn, loss, margin, fixed)
+            # the entry keeps the device copies the graph reads alive, even if a later call
+            # with other p_learn objects replaces them in _CACHE
+            held = tuple(_CACHE.dev[k] for k in ("test_X", "test_Z") +
+                         (("train_X", "train_Z", "pairs") if fixed else ()))
+            ent = (key, srcs, g, out, held, wbuf)
+            _CACHE.dev["eval_graph"] = ent
+        ent[5].copy_(_w_dev)
+        ent[2].replay()
+        res_dev, n_pairs, n_test = ent[3]
+    else:
+        wd = _w_dev if _w_dev is not None else L.to_device(np.asarray(w, np.float64).reshape(-1))
+        res_dev, n_pairs, n_test = _eval_device(wd, p_learn, loss, margin, fixed)
+    res = res_dev.cpu().numpy()  # the ONE copy back: [hinge sum, count] x (pairs, test)
+    if fixed:
+        bc_AUC = np.float64(res[0] / np.float64(n_pairs)) + reg_term
+        br_AUC = E.ratio(int(res[1:2].view(np.uint64)[0]), n_pairs)
+    tc_AUC = np.float64(res[2] / np.float64(n_test)) + reg_term
+    tr_AUC = E.ratio(int(res[3:4].view(np.uint64)[0]), n_test)
 
     s_log = ("it %5d: bc_AUC = %.4f | br_AUC = %.4f "
              + "| tc_AUC = %5.4f | tr_AUC = %5.4f")
