@@ -169,6 +169,21 @@ int tw_pair_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t*
                  const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
                  double margin, int32_t loss, double* d_out, void* stream);
 
+/* ---- Complete-block gradient (extension; BASELINE.json north_star item (2)) -------------
+ * The same surrogate's gradient over ALL kx*kz pairs of each shard, computed as per-point
+ * pair-coefficient reductions followed by X^T c (csrc/complete_grad.hip):
+ *   sx_i = X[rx_i].w, sz_j = Z[rz_j].w, S_ij = sz_j - sx_i + margin,
+ *   a_j = sum_i phi'(S_ij), b_i = sum_j phi'(S_ij)  (phi' = 1{S>0} hinge, sigma(S) logistic),
+ *   d_out[s*d + c] = (sum_j a_j Z[rz_j][c] - sum_i b_i X[rx_i][c]) / (kx*kz).
+ * Rows as tw_hinge_grad (d_rows_* NULL = shard s owns rows [s*k, (s+1)*k)).  d_work: device
+ * scratch of tw_pair_grad_complete_work_bytes(n_shards, kx, kz, d) bytes.  Deterministic
+ * (fixed summation orders); not in the reference (its learner samples B pairs). */
+int64_t tw_pair_grad_complete_work_bytes(int32_t n_shards, int64_t kx, int64_t kz, int64_t d);
+int tw_pair_grad_complete(const double* d_X, const double* d_Z, int64_t d,
+                          const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                          int64_t kz, int32_t n_shards, const double* d_w, double margin,
+                          int32_t loss, void* d_work, double* d_out, void* stream);
+
 /* ---- Row L1/A9, device-RNG mode (no host RNG in the loop; graph-capturable) -----------
  * Draws are Philox4x32-10(key = seed, counter = (index, shard, step lo, tag | step hi)) with
  * step = *d_step (device memory, advanced by tw_sgd_update), mapped by 64-bit multiply-high;

@@ -186,6 +186,27 @@ def pair_grad(diff, w, margin, B, loss="hinge"):
     raise ValueError(loss)
 
 
+def grad_complete_block(w, margin, loss="hinge"):
+    """Extension, NOT in the reference (BASELINE.json north_star item (2)): the surrogate's
+    gradient over ALL pairs of a block, (1/(kx kz)) sum_ij phi'(S_ij) (z_j - x_i) with
+    S_ij = z_j.w - x_i.w + margin, factorised into per-point coefficients
+    a_j = sum_i phi'(S_ij), b_i = sum_j phi'(S_ij) and (a.Z - b.X) / (kx kz).  Pinned in
+    tests/test_oracle_golden.py against the unfactorised double sum and, for the logistic loss,
+    finite differences of the complete surrogate."""
+    def res(X, Z):
+        sx, sz = X.dot(w).ravel(), Z.dot(w).ravel()
+        S = sz[None, :] - sx[:, None] + margin
+        if loss == "hinge":
+            P = (S > 0).astype(np.float64)
+        elif loss == "logistic":
+            P = 1.0 / (1.0 + np.exp(-S))
+        else:
+            raise ValueError(loss)
+        a, b = P.sum(axis=0), P.sum(axis=1)
+        return ((a.dot(Z) - b.dot(X)) / (len(sx) * len(sz))).reshape([-1, 1])
+    return res
+
+
 def grad_inc_block(w, B, margin, loss="hinge"):
     """compute_stats.py:146-162"""
     def res(X, Z):

@@ -475,3 +475,49 @@ def test_fused_exchange_kernels_simulated_ranks(gpu):
         o = out.cpu().numpy()
         assert np.array_equal(o[:n_loc], want_x[q * n_loc:(q + 1) * n_loc])
         assert np.array_equal(o[n_loc:], want_z[q * m_loc:(q + 1) * m_loc])
+
+
+@pytest.mark.parametrize("loss", ["hinge", "logistic"])
+@pytest.mark.parametrize("d,kx,kz", [(1, 300, 77), (10, 500, 64), (100, 1300, 5000),
+                                     (512, 257, 300)])
+def test_complete_block_gradient(gpu, loss, d, kx, kz):
+    """tw_pair_grad_complete (extension, north_star item (2): per-point pair coefficients then
+    X^T c) vs the oracle's restatement, per shard, through SWR-style row tables."""
+    from tuplewise import _lib as L, _learn
+    rng = np.random.RandomState(d + kx)
+    N, nX, nZ = 5, 4000, 6000
+    X, Z = rng.normal(size=(nX, d)), rng.normal(0.2, 1, size=(nZ, d))
+    w = rng.normal(size=d) / np.sqrt(d)
+    rows_x, rows_z = rng.randint(0, nX, size=(N, kx)), rng.randint(0, nZ, size=(N, kz))
+    code = L.TW_LOSS_HINGE if loss == "hinge" else L.TW_LOSS_LOGISTIC
+    g = _learn.complete_grads_device(L.to_device(X), L.to_device(Z), d, L.to_device(rows_x), kx,
+                                     L.to_device(rows_z), kz, N, L.to_device(w), 0.5,
+                                     code).cpu().numpy()
+    for s in range(N):
+        want = O.grad_complete_block(w.reshape(-1, 1), 0.5, loss)(X[rows_x[s]], Z[rows_z[s]])
+        np.testing.assert_allclose(g[s], want.ravel(), rtol=1e-10, atol=1e-13)
+
+
+def test_grad_complete_block_drop_in(gpu):
+    """compute_stats.grad_complete_block composes with SWR_divide / UN_split like
+    grad_inc_block (one launch for all shards), and with ragged user-made shard lists."""
+    import tuplewise.compute_stats as cs
+    rng = np.random.RandomState(2)
+    X, Z = rng.normal(size=(600, 7)), rng.normal(0.5, 1, size=(250, 7))
+    w = rng.normal(size=(7, 1))
+    for loss in ("hinge", "logistic"):
+        np.random.seed(12)
+        Xs, Zs = cs.SWR_divide(X, Z, 6)
+        g = cs.UN_split(Xs, Zs, cs.grad_complete_block(w, 1, loss=loss))
+        np.random.seed(12)
+        Xo, Zo = O.SWR_divide(X, Z, 6)
+        want = O.UN_split(Xo, Zo, O.grad_complete_block(w, 1, loss))
+        np.testing.assert_allclose(g, want, rtol=1e-10, atol=1e-13)
+        assert g.shape == (7, 1)
+    ragged_x, ragged_z = [X[:100], X[100:350]], [Z[:40], Z[40:41]]
+    g = cs.UN_split(ragged_x, ragged_z, cs.grad_complete_block(w, 1))
+    want = O.UN_split(ragged_x, ragged_z, O.grad_complete_block(w, 1))
+    np.testing.assert_allclose(g, want, rtol=1e-10, atol=1e-13)
+    one = cs.grad_complete_block(w, 1, loss="logistic")(X[:50], Z[:30])
+    np.testing.assert_allclose(one, O.grad_complete_block(w, 1, "logistic")(X[:50], Z[:30]),
+                               rtol=1e-10, atol=1e-13)

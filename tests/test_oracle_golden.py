@@ -167,3 +167,32 @@ def test_logistic_gradient_is_the_derivative_of_its_loss():
                      - O._surrogate(diff.dot(w - h * e[:, None]).ravel() + margin,
                                     "hinge").sum()) / (2 * h * B) for e in np.eye(d)])
     np.testing.assert_allclose(gh, fdh, rtol=1e-6, atol=1e-9)
+
+
+def test_complete_gradient_factorisation():
+    """The complete-block gradient's per-point factorisation (north_star item (2), an extension
+    with no reference counterpart) equals the plain double sum over pairs, and for the
+    logistic loss the finite-difference gradient of mean_ij softplus(S_ij)."""
+    rng = np.random.RandomState(8)
+    X, Z = rng.normal(size=(37, 5)), rng.normal(0.3, 1, size=(23, 5))
+    w = rng.normal(size=(5, 1))
+    for loss, margin in (("hinge", 1.0), ("logistic", 0.4)):
+        g = O.grad_complete_block(w, margin, loss)(X, Z).ravel()
+        brute = np.zeros(5)
+        for i in range(len(X)):
+            for j in range(len(Z)):
+                dlt = Z[j] - X[i]
+                S = dlt.dot(w.ravel()) + margin
+                wt = (S > 0) if loss == "hinge" else 1 / (1 + np.exp(-S))
+                brute += wt * dlt
+        np.testing.assert_allclose(g, brute / (len(X) * len(Z)), rtol=1e-12, atol=1e-15)
+
+    def loss_fn(wv):
+        S = Z.dot(wv).ravel()[None, :] - X.dot(wv).ravel()[:, None] + 0.4
+        return np.logaddexp(0, S).mean()
+
+    h = 1e-6
+    fd = np.array([(loss_fn(w + h * e[:, None]) - loss_fn(w - h * e[:, None])) / (2 * h)
+                   for e in np.eye(5)])
+    np.testing.assert_allclose(O.grad_complete_block(w, 0.4, "logistic")(X, Z).ravel(), fd,
+                               rtol=1e-7, atol=1e-9)

@@ -99,3 +99,78 @@ def grad_block(w, B, margin, loss=L.TW_LOSS_HINGE):
 
     res._tw_block = spec
     return res
+
+
+def complete_grads_device(Xd, Zd, d, rows_x, kx, rows_z, kz, n_shards, wd, margin,
+                          loss=L.TW_LOSS_HINGE):
+    """Per-shard complete-block gradients (n_shards, d) via tw_pair_grad_complete."""
+    t = L.torch()
+    out = L.empty((n_shards, d), t.float64)
+    work = L.empty((max(1, int(L.lib().tw_pair_grad_complete_work_bytes(n_shards, kx, kz,
+                                                                          d))),), t.uint8)
+    L.call("tw_pair_grad_complete", L.ptr(Xd), L.ptr(Zd), int(d), L.ptr(rows_x), int(kx),
+           L.ptr(rows_z), int(kz), int(n_shards), L.ptr(wd), float(margin), int(loss),
+           L.ptr(work), L.ptr(out), L.stream_handle())
+    return out
+
+
+class CompleteGradSpec(Bk.BlockSpec):
+    """The complete-block gradient (extension): all pairs of each block, per-point pair
+    coefficients then X^T c on the device."""
+
+    def __init__(self, w, margin, loss=L.TW_LOSS_HINGE):
+        self.w = np.asarray(w, dtype=np.float64)
+        self.margin = margin
+        self.loss = loss
+
+    def _grads(self, X_s, Z_s):
+        N = min(len(X_s), len(Z_s))
+        if N == 0:
+            return []
+        X_s, Z_s = list(X_s)[:N], list(Z_s)[:N]
+        d = _as_matrix(X_s[0]).shape[1]
+        wd = L.to_device(self.w.reshape(-1))
+        sizes_x = {_as_matrix(a).shape[0] for a in X_s}
+        sizes_z = {_as_matrix(a).shape[0] for a in Z_s}
+        if len(sizes_x) == 1 and len(sizes_z) == 1:  # one launch for all shards
+            def side(S, full):
+                rows = getattr(full, "rows", None)
+                src = getattr(full, "source", None)
+                if rows is not None and src is not None and len(rows) >= N:
+                    return (L.to_device(_as_matrix(src)),
+                            L.to_device(np.stack(rows[:N]).astype(np.int64)))
+                return L.to_device(np.concatenate([_as_matrix(a) for a in S])), None
+            Xd, rx = side(X_s, getattr(self, "_full_x", None))
+            Zd, rz = side(Z_s, getattr(self, "_full_z", None))
+            out = complete_grads_device(Xd, Zd, d, rx, sizes_x.pop(), rz, sizes_z.pop(), N,
+                                        wd, self.margin, self.loss)
+            return [g.reshape(-1, 1) for g in out.cpu().numpy()]
+        res = []  # ragged shards: one launch each
+        for x, z in zip(X_s, Z_s):
+            xm, zm = _as_matrix(x), _as_matrix(z)
+            out = complete_grads_device(L.to_device(xm), L.to_device(zm), d, None,
+                                        xm.shape[0], None, zm.shape[0], 1, wd, self.margin,
+                                        self.loss)
+            res.append(out.cpu().numpy()[0].reshape(-1, 1))
+        return res
+
+    def evaluate_split(self, X_s, Z_s):
+        self._full_x, self._full_z = X_s, Z_s  # SWR_divide's row tables, when present
+        try:
+            return np.mean(self._grads(X_s, Z_s), axis=0)
+        finally:
+            self._full_x = self._full_z = None
+
+
+def complete_grad_block(w, margin, loss=L.TW_LOSS_HINGE):
+    spec = CompleteGradSpec(w, margin, loss)
+
+    def res(X, Z):
+        """
+            Returns:
+            1/(n_X n_Z) sum_{i,j} phi'(w^T(Z_j - X_i) + margin)(Z_j - X_i)
+        """
+        return spec._grads([X], [Z])[0]
+
+    res._tw_block = spec
+    return res

@@ -46,6 +46,9 @@ _SIGNATURES = {
                       _vp, _vp],
     "tw_pair_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64, _i32,
                      _vp, _vp],
+    "tw_pair_grad_complete_work_bytes": [_i32, _i64, _i64, _i64],
+    "tw_pair_grad_complete": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _f64, _i32, _vp,
+                              _vp, _vp],
     "tw_pair_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _i32, _u64,
                          _vp, _i32, _vp, _vp],
     "tw_hinge_grad_rng": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _vp, _f64, _u64,
@@ -76,6 +79,7 @@ _RESTYPES = {
     "tw_count_pairs_sorted_work_bytes": ctypes.c_int64,
     "tw_pair_sum_work_per_shard": ctypes.c_int64,
     "tw_pair_sum_idx_work_per_shard": ctypes.c_int64,
+    "tw_pair_grad_complete_work_bytes": ctypes.c_int64,
 }
 
 _lib = None

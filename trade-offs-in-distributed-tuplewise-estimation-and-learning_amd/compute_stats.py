@@ -194,6 +194,14 @@ def grad_inc_block(w, B, margin, *, loss="hinge"):
     sigma(diff . w + margin), the gradient of softplus, instead of the hinge filter."""
     return _learn.grad_block(w, B, margin, _loss_codes(loss)[1])
 
+def grad_complete_block(w, margin, *, loss="hinge"):
+    """Extension (not in the reference; BASELINE.json north_star item (2)): a block function
+    returning the surrogate's gradient over ALL pairs of the block,
+    1/(n_X n_Z) sum_ij phi'(S_ij) (Z_j - X_i), S_ij = w.(Z_j - X_i) + margin, computed on the
+    device as per-point pair-coefficient reductions followed by X^T c.  Composes with UN_split
+    like grad_inc_block (one launch for all shards)."""
+    return _learn.complete_grad_block(w, margin, _loss_codes(loss)[1])
+
 # ---------- End gradient descent functions ----------
 
 

@@ -30,21 +30,6 @@ constexpr int kMaxD = 4096;
 // (index, shard, step lo, tag | step hi).  Tags separate the three draw streams.
 constexpr uint32_t kTagPairs = 0x80000000u, kTagRowsX = 0x40000000u, kTagRowsZ = 0x20000000u;
 
-// Pair weights of the gradient sum.  TW_LOSS_HINGE: grad_inc_block's filter 1{S > 0}
-// (compute_stats.py:158-161), applied as a branch so unfiltered rows are skipped exactly as
-// diff[filt] skips them.  TW_LOSS_LOGISTIC (extension, SURVEY.md §8 row L3 — not in the
-// reference): the gradient of softplus(S) = log(1 + e^S), weight sigma(S) = 1 / (1 + e^-S).
-template <int LOSS>
-__device__ __forceinline__ double pair_weight(double S) {
-  if constexpr (LOSS == TW_LOSS_HINGE) return S > 0.0 ? 1.0 : 0.0;
-  else return 1.0 / (1.0 + exp(-S));
-}
-template <int LOSS>
-__device__ __forceinline__ double weighted(double wgt, double v) {
-  if constexpr (LOSS == TW_LOSS_HINGE) return wgt != 0.0 ? v : -0.0;  // -0.0 leaves sums as is
-  else return wgt * v;
-}
-
 __device__ __forceinline__ u32x4 sgd_draw(uint64_t seed, uint64_t step, uint32_t idx,
                                           uint32_t shard, uint32_t tag) {
   return philox4x32_10(u32x4{idx, shard, (uint32_t)step, tag | (uint32_t)(step >> 32)},

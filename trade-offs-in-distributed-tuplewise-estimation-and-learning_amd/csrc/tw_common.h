@@ -64,6 +64,21 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// Pair weights of the gradient sum.  TW_LOSS_HINGE: grad_inc_block's filter 1{S > 0}
+// (compute_stats.py:158-161), applied as a branch so unfiltered rows are skipped exactly as
+// diff[filt] skips them.  TW_LOSS_LOGISTIC (extension, SURVEY.md §8 row L3 — not in the
+// reference): the gradient of softplus(S) = log(1 + e^S), weight sigma(S) = 1 / (1 + e^-S).
+template <int LOSS>
+__device__ __forceinline__ double pair_weight(double S) {
+  if constexpr (LOSS == TW_LOSS_HINGE) return S > 0.0 ? 1.0 : 0.0;
+  else return 1.0 / (1.0 + exp(-S));
+}
+template <int LOSS>
+__device__ __forceinline__ double weighted(double wgt, double v) {
+  if constexpr (LOSS == TW_LOSS_HINGE) return wgt != 0.0 ? v : -0.0;  // -0.0 leaves sums as is
+  else return wgt * v;
+}
+
 // Philox4x32-10 (Salmon et al., SC'11): counter-based RNG for the device-RNG modes.
 struct u32x4 {
   uint32_t a, b, c, d;
