@@ -87,6 +87,35 @@ def cpu_baseline(n, N, shards):
                       f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
 
 
+def sgd_complete_steps_per_s(n_X, n_Z, d, N, steps, loss="hinge"):
+    """SGD steps with the complete-block gradient (extension; north_star item (2)): every step
+    takes ALL pairs of every shard through per-point pair coefficients + X^T c
+    (tw_pair_grad_complete), device-RNG shards, one reshuffle before the timed steps."""
+    import torch
+    from tuplewise.learning import SGDEngine
+    g = torch.Generator(device="cuda").manual_seed(9)
+    X = torch.randn((n_X, d), dtype=torch.float64, device="cuda", generator=g)
+    Z = torch.randn((n_Z, d), dtype=torch.float64, device="cuda", generator=g) + 0.3
+    w0 = torch.randn((d, 1), dtype=torch.float64, device="cuda", generator=g) / d ** 0.5
+    eng = SGDEngine(X, Z, w0, N, 1, margin=1, reg=0.05, learning_rate=0.01,
+                    optim_type="momentum", loss=loss, gradient="complete")
+    eng.enable_device_rng(99)
+    eng.run_segment(1, True, graphs=False)  # reshuffle + one warm step
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run_segment(steps, False, graphs=False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    pairs = N * eng.kx * eng.kz
+    rows_bytes = 2 * N * (eng.kx + eng.kz) * d * 8  # scores pass + weighted column sums
+    return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "pairs_per_step": pairs, "pairs_per_s": pairs * steps / dt,
+            "row_GBps": rows_bytes * steps / dt / 1e9,
+            "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "loss": loss,
+                       "gradient": "complete (per-point pair coefficients + X^T c)",
+                       "steps": steps}}
+
+
 def cpu_baseline_incomplete(n, N, B, shards):
     """The reference's UnNB(kernel="AUC") restated (oracle.UB per block: two randint draws and
     a fancy-indexed compare, compute_stats.py:37-42), single-threaded, on `shards` of the N
@@ -455,6 +484,8 @@ def main():
             "C4_end_to_end_with_evaluation_device": learning_end_to_end(2000, "device"),
             "C5_scaled_d512": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2),
             "C5_scaled_d512_B4096": sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1),
+            "C5_scaled_d512_complete_gradient": sgd_complete_steps_per_s(C5_N, C5_N, 512,
+                                                                          256, 3),
             "C5_scaled_d512_partitioned": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,
                                                           1, layout="partitioned"),
         }

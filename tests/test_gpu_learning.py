@@ -228,3 +228,46 @@ def test_replay_segments_graphs_match_reference(gpu, golden):
     lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=[])
     assert np.array_equal(np.random.get_state()[1], out[True][1])
     assert p["norm_w"] == out[True][0]["norm_w"]
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_complete_gradient_learning(gpu, golden, mode):
+    """learning_process(..., gradient="complete") (extension): every step uses all pairs of
+    every shard; the trajectory follows the oracle's complete-block restatement, graphs and
+    eager launches agree."""
+    import tuplewise.learning as lr
+    from oracle import oracle as O
+    logging.disable(logging.CRITICAL)
+    p = _p_learn(golden, n_it=40)
+    traj = []
+    np.random.seed(5)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=traj,
+                        rng_mode=mode, gradient="complete", loss="logistic")
+    X, Z = golden["learn/X"], golden["learn/Z"]
+    np.random.seed(5)
+    if mode == "replay":
+        O.SWR_divide(X, Z, p["N"])  # the reference's redundant first draw
+    else:
+        seed = int(np.random.randint(0, 2 ** 63 - 1, dtype=np.int64))
+    w, dw, ws = p["w_init"], 0, []
+    kx, kz = int(X.shape[0] / p["N"]), int(Z.shape[0] / p["N"])
+    for i in range(p["n_it"]):
+        if i % p["reshuffle_mod"] == 0:
+            if mode == "replay":
+                X_s, Z_s = O.SWR_divide(X, Z, p["N"])
+            else:
+                X_s = [X[O._mulhi64(O._sgd_draw(seed, i, np.arange(kx), s, 0x40000000)[0],
+                                    X.shape[0])] for s in range(p["N"])]
+                Z_s = [Z[O._mulhi64(O._sgd_draw(seed, i, np.arange(kz), s, 0x20000000)[0],
+                                    Z.shape[0])] for s in range(p["N"])]
+        ws.append(np.array(w, copy=True))
+        g = O.UN_split(X_s, Z_s, O.grad_complete_block(w, p["margin"], "logistic"))
+        w, dw = O.sgd_step(w, dw, g, p["reg"], p["learning_rate"])
+    np.testing.assert_allclose(np.stack(traj), np.stack(ws), rtol=1e-10, atol=1e-14)
+    out = []
+    for graphs in (True, False):
+        q = _p_learn(golden, n_it=40)
+        np.random.seed(5)
+        lr.learning_process(X, Z, q, rng_mode=mode, gradient="complete", graphs=graphs)
+        out.append(q["norm_w"])
+    assert out[0] == out[1]

@@ -50,7 +50,7 @@ class SGDEngine:
     through an identity row table, so the arithmetic — and the trajectory — is unchanged."""
 
     def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None,
-                 x_layout="replicated", loss="hinge"):
+                 x_layout="replicated", loss="hinge", gradient="incomplete"):
         """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is)."""
         t = L.torch()
         self.t = t
@@ -89,6 +89,10 @@ class SGDEngine:
             self.ident_z = t.arange(self.N_loc * self.kz, device=dev).view(self.N_loc, self.kz)
         self.margin, self.reg, self.lr = float(margin), float(reg), float(learning_rate)
         self.loss = cs._loss_codes(loss)[1]
+        if gradient not in ("incomplete", "complete"):
+            raise ValueError(f"gradient must be 'incomplete' or 'complete', not {gradient!r}")
+        self.complete = gradient == "complete"
+        self._cwork = None
         self.momentum = 0.9 if optim_type == "momentum" else -1.0
         self.w_shape = tuple(w_init.shape)
         self.w = _dev_f64(w_init).reshape(-1).clone()
@@ -166,6 +170,20 @@ class SGDEngine:
         L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
                self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr), s)
 
+    def step_complete(self):
+        """One step with the complete-block gradient (all kx*kz pairs of every local shard,
+        tw_pair_grad_complete) — no pair draws."""
+        t = self.t
+        if self._cwork is None:
+            nb = int(L.lib().tw_pair_grad_complete_work_bytes(self.N_loc, self.kx, self.kz,
+                                                              self.d))
+            self._cwork = L.empty((max(nb, 1),), t.uint8)
+        L.call("tw_pair_grad_complete", L.ptr(self.X), L.ptr(self.Z), self.d,
+               L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, self.N_loc,
+               L.ptr(self.w), self.margin, self.loss, L.ptr(self._cwork),
+               L.ptr(self.grads_loc), L.stream_handle())
+        self._update()
+
     def step(self, ix, iz):
         """Replay mode: ix, iz are the (N, B) NumPy draws of every shard (host arrays or
         device tensors)."""
@@ -182,20 +200,30 @@ class SGDEngine:
         device): one gradient + one update launch per step, replayed from a hipGraph captured
         per (tag, nsteps) — tag names the draw buffer, whose address the graph holds — or
         launched eagerly (graphs=False, or a collective in the step)."""
+        def one(st):
+            if self.complete:
+                self.step_complete()
+            else:
+                self.step(draws_dev[st, 0], draws_dev[st, 1])
+
         if not graphs or self.G > 1:
             for st in range(nsteps):
-                self.step(draws_dev[st, 0], draws_dev[st, 1])
+                one(st)
             return
         t = self.t
         if not hasattr(self, "_replay_graphs"):
             self._replay_graphs = {}
-        key = (tag, nsteps, draws_dev.data_ptr())
+        key = (tag, nsteps, draws_dev.data_ptr() if draws_dev is not None else 0)
         g = self._replay_graphs.get(key)
         if g is None:
+            if self.complete and self._cwork is None:  # allocated outside the capture
+                nb = int(L.lib().tw_pair_grad_complete_work_bytes(self.N_loc, self.kx,
+                                                                  self.kz, self.d))
+                self._cwork = L.empty((max(nb, 1),), t.uint8)
             g = t.cuda.CUDAGraph()
             with t.cuda.graph(g):
                 for st in range(nsteps):
-                    self.step(draws_dev[st, 0], draws_dev[st, 1])
+                    one(st)
             self._replay_graphs[key] = g
         g.replay()
 
@@ -250,6 +278,8 @@ class SGDEngine:
                L.ptr(self.step_ctr), 1, self.shard_base, s)
 
     def step_device(self):
+        if self.complete:
+            return self.step_complete()
         L.call("tw_pair_grad_rng", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
                self.kx, L.ptr(self.rows_z), self.kz, self.N_loc, self.B, L.ptr(self.w),
                self.margin, self.loss, self.seed, L.ptr(self.step_ctr), self.shard_base,
@@ -366,7 +396,7 @@ class _ReplayDraws:
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                      rng_mode="replay", graphs=True, group=None, x_layout="replicated",
-                     loss="hinge"):
+                     loss="hinge", gradient="incomplete"):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference; the
@@ -381,7 +411,9 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     x_layout: "replicated" (X, Z whole on every GPU; a reshuffle moves no data) or
     "partitioned" (1/G of the rows per GPU; a reshuffle exchanges the drawn rows).
     loss: "hinge" (the reference) or "logistic" (SURVEY.md §8 row L3 extension: pairwise
-    logistic loss softplus(diff . w + margin); evaluation reports its surrogate too)."""
+    logistic loss softplus(diff . w + margin); evaluation reports its surrogate too).
+    gradient: "incomplete" (the reference: B sampled pairs per shard) or "complete" (extension:
+    all pairs of every shard via per-point pair coefficients + X^T c; draws no pairs)."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -401,7 +433,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
 
     eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
-                    group=group, x_layout=x_layout, loss=loss)
+                    group=group, x_layout=x_layout, loss=loss, gradient=gradient)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss)
@@ -422,8 +454,11 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                 if i % eval_mod == 0:
                     _evaluate(i, eng, eng.w_host(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
                 trajectory.append(eng.w_host())
-                ix, iz = draws.pairs()
-                eng.step(ix, iz)
+                if eng.complete:
+                    eng.step_complete()
+                else:
+                    ix, iz = draws.pairs()
+                    eng.step(ix, iz)
                 i += 1
                 continue
             # The steps up to the next reshuffle / evaluation draw nothing else from the RNG
@@ -433,7 +468,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
             nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
                       i + draws.segment_capacity())
             w_pending = eng.w_host_async() if i % eval_mod == 0 else None
-            buf, tag = draws.pairs_segment(nxt - i)
+            buf, tag = (None, 0) if eng.complete else draws.pairs_segment(nxt - i)
             if w_pending is not None:
                 _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
             eng.run_replay_segment(buf, nxt - i, graphs, tag)
