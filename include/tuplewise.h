@@ -94,6 +94,11 @@ int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, const void* d_z
  * results do not depend on it. */
 int tw_count_step_set_plan(int32_t blocks, int32_t every, int32_t tail);
 
+/* Tuning hook: 1 (default) counts part of each lane's x-values on the scalar unit (double
+ * inputs, one-bit predicates; csrc/count.hip), 0 = VALU-only accumulation.  Process-global;
+ * results do not depend on it. */
+int tw_count_set_scalar_mix(int32_t on);
+
 /* Tuning hook for tw_count_pairs' launch plan: R x-values per lane (1, 2, 4, 8; 0 = automatic)
  * and z-chunk length per block (0 = automatic).  Process-global; results do not depend on it. */
 int tw_count_set_plan(int32_t R, int64_t z_chunk);

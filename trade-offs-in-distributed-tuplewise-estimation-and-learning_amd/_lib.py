@@ -32,6 +32,7 @@ _SIGNATURES = {
     "tw_count_pairs_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _i64, _vp,
                             _u64, _i64, _vp, _u64, _vp, _i32, _vp],
     "tw_count_step_set_plan": [_i32, _i32, _i32],
+    "tw_count_set_scalar_mix": [_i32],
     "tw_count_set_plan": [_i32, _i64],
     "tw_count_pairs_sorted_work_bytes": [_i32, _i64],
     "tw_count_sorted_set_chunk": [_i64],

@@ -86,7 +86,15 @@ __device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
   }
 }
 
-template <typename T, int R, int PRED>
+// Mixed VALU/SALU accumulation (double, strict predicate).  Per pair the compare is one
+// v_cmp_*_f64; accumulating its 64 result bits costs one more VALU op (carry-add into a per-lane
+// counter) — the VALU issue ceiling of §4.1 — or, if the compare writes an SGPR pair, two
+// SCALAR ops (s_bcnt1_i32_b64 + s_add) on the scalar unit, which issues beside the VALU.
+// Counting NS of the R x-values per lane on the scalar unit moves that share of the work off
+// the VALU (tools/mb_mix.hip, profiles/r01_microbench_salu_mix.log: R=4 with NS=2 reaches
+// 0.63 of the lane-op peak against 0.49 for VALU-only accumulation).  Padded lanes hold NaN,
+// for which every predicate is false, so the scalar counts need no lane mask.
+template <typename T, int R, int NS, int PRED>
 __global__ __launch_bounds__(kBlock) void k_count_complete(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, int tiles_x, int zchunks, int64_t z_chunk,
@@ -125,6 +133,8 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
   if (x0 >= xe || z0 >= ze) return;  // block-uniform: ragged shard smaller than the grid
   const int64_t z1 = (z0 + z_chunk < ze) ? z0 + z_chunk : ze;
 
+  static_assert(NS == 0 || (std::is_floating_point<T>::value && PRED != TW_PRED_HALF),
+                "scalar-unit counting needs NaN padding and a one-bit predicate");
   T xv[R];
   unsigned acc[R];
   bool valid[R];
@@ -132,26 +142,59 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
   for (int r = 0; r < R; ++r) {
     const int64_t i = x0 + r * kBlock + threadIdx.x;
     valid[r] = i < xe;
-    xv[r] = valid[r] ? x[i] : (T)0;
+    if constexpr (NS > 0)
+      xv[r] = valid[r] ? x[i] : (T)__builtin_nan("");
+    else
+      xv[r] = valid[r] ? x[i] : (T)0;
     acc[r] = 0;
   }
 
   const T* __restrict__ zp = z + z0;
   const int nz = (int)(z1 - z0);
+  unsigned sacc = 0;  // wave-uniform: the scalar unit's count (NS > 0)
+  if constexpr (NS == 0) {
 #pragma unroll 8
-  for (int j = 0; j < nz; ++j) {
-    const T zv = zp[j];
+    for (int j = 0; j < nz; ++j) {
+      const T zv = zp[j];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] += pair_pred<T, PRED>(xv[r], zv);
+      for (int r = 0; r < R; ++r) acc[r] += pair_pred<T, PRED>(xv[r], zv);
+    }
+  } else {
+    int j = 0;
+    for (; j + 8 <= nz; j += 8) {  // 8 z per s_load_dwordx16
+      T zv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zv[u] = zp[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r < NS)
+            sacc += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv[u])));
+          else
+            acc[r] += pair_pred<T, PRED>(xv[r], zv[u]);
+        }
+      }
+    }
+    for (; j < nz; ++j) {
+      const T zv = zp[j];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r < NS)
+          sacc += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv)));
+        else
+          acc[r] += pair_pred<T, PRED>(xv[r], zv);
+      }
+    }
   }
 
   unsigned long long tot = 0;
 #pragma unroll
-  for (int r = 0; r < R; ++r) tot += valid[r] ? (unsigned long long)acc[r] : 0ull;
+  for (int r = NS; r < R; ++r) tot += valid[r] ? (unsigned long long)acc[r] : 0ull;
   tot = wave_sum_u64(tot);
   __shared__ unsigned long long part[kBlock / kWave];
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  if (lane == 0) part[wid] = tot;
+  if (lane == 0) part[wid] = tot + sacc;
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long b = 0;
@@ -243,14 +286,31 @@ struct CompletePlan {
 static int g_force_R = 0;            // tuning hook (tw_count_set_plan); 0 = automatic
 static int64_t g_force_zchunk = 0;
 
-inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shards) {
+static int g_scalar_mix = 1;  // tw_count_set_scalar_mix: 0 = VALU-only accumulation
+
+// Measured pair rates (fraction of the lane-op peak, tools/tune_count.py on the bench shape,
+// profiles/r01_count_mix_sweep.log) used to pick R: VALU-only accumulation is flat in R; the
+// mixed VALU/SALU one is best at R = 4 and 8.
+inline double pair_rate(int R, bool mix) {
+  if (!mix) return 0.465;
+  switch (R) {
+    case 8: return 0.533;
+    case 4: return 0.532;
+    case 2: return 0.504;
+    default: return 0.465;
+  }
+}
+
+inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shards,
+                                  bool mix = false) {
   CompletePlan p{8, 1, 1, max_nz, 0};
-  int64_t best = -1;
-  for (int R : {8, 4, 2, 1}) {
+  double best = -1.0;
+  for (int R : {8, 4, 2, 1}) {  // least modelled time per shard (padded slots / rate)
     if (g_force_R && R != g_force_R) continue;
     const int64_t slots = ceil_div(max_nx, (int64_t)kBlock * R) * kBlock * R;
-    if (best < 0 || slots < best) {
-      best = slots;
+    const double cost = (double)slots / pair_rate(R, mix);
+    if (best < 0 || cost < best * (1.0 - 1e-9)) {
+      best = cost;
       p.R = R;
     }
   }
@@ -263,6 +323,7 @@ inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shar
   int64_t zc = base >= target ? 1 : ceil_div(target, base);
   const int64_t min_chunk = 512;
   zc = std::min<int64_t>(zc, std::max<int64_t>(1, max_nz / min_chunk));
+  zc = std::max<int64_t>(zc, ceil_div(max_nz, (int64_t)1 << 24));  // u32 counters never wrap
   p.z_chunk = ceil_div(max_nz, zc);
   p.z_chunk = ceil_div(p.z_chunk, 8) * 8;
   if (g_force_zchunk > 0) p.z_chunk = g_force_zchunk;
@@ -275,7 +336,10 @@ template <typename T, int PRED>
 int launch_complete(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                     int32_t n_shards, int64_t max_nx, int64_t max_nz, uint64_t* out,
                     const NextStep& nxt, hipStream_t st) {
-  const CompletePlan p = plan_complete(max_nx, max_nz, n_shards);
+  // scalar-unit counting for the one-bit predicate on doubles (NaN padding)
+  constexpr bool kMixable = std::is_floating_point<T>::value && PRED != TW_PRED_HALF;
+  const bool mix = kMixable && g_scalar_mix;
+  const CompletePlan p = plan_complete(max_nx, max_nz, n_shards, mix);
   TW_ARG_CHECK(p.blocks + nxt.blocks < (1ll << 31), "tw_count_pairs: grid too large (%lld blocks)",
                (long long)p.blocks);
   TW_ARG_CHECK(p.z_chunk < (1ll << 30), "tw_count_pairs: z chunk too large");
@@ -283,12 +347,26 @@ int launch_complete(const void* x, const int64_t* x_off, const void* z, const in
   const T* zs = (const T*)z;
   auto* o = (unsigned long long*)out;
   dim3 g((unsigned)(p.blocks + nxt.blocks)), b(kBlock);
-  switch (p.R) {
-    case 8: hipLaunchKernelGGL((k_count_complete<T, 8, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
-    case 4: hipLaunchKernelGGL((k_count_complete<T, 4, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
-    case 2: hipLaunchKernelGGL((k_count_complete<T, 2, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
-    default: hipLaunchKernelGGL((k_count_complete<T, 1, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt); break;
+#define TW_CC(R_, NS_) hipLaunchKernelGGL((k_count_complete<T, R_, NS_, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt)
+  if constexpr (kMixable) {
+    if (mix) {
+      switch (p.R) {
+        case 8: TW_CC(8, 4); break;
+        case 4: TW_CC(4, 2); break;
+        case 2: TW_CC(2, 1); break;
+        default: TW_CC(1, 0); break;
+      }
+      TW_LAUNCH_CHECK();
+      return TW_OK;
+    }
   }
+  switch (p.R) {
+    case 8: TW_CC(8, 0); break;
+    case 4: TW_CC(4, 0); break;
+    case 2: TW_CC(2, 0); break;
+    default: TW_CC(1, 0); break;
+  }
+#undef TW_CC
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -336,6 +414,12 @@ int launch_rng(const void* x, const int64_t* x_off, const void* z, const int64_t
 }  // namespace tw
 
 using namespace tw;
+
+extern "C" int tw_count_set_scalar_mix(int32_t on) {
+  TW_ARG_CHECK(on == 0 || on == 1, "tw_count_set_scalar_mix: 0 or 1");
+  g_scalar_mix = on;
+  return TW_OK;
+}
 
 extern "C" int tw_count_set_plan(int32_t R, int64_t z_chunk) {
   TW_ARG_CHECK(R == 0 || R == 1 || R == 2 || R == 4 || R == 8, "tw_count_set_plan: R in {0,1,2,4,8}");
@@ -410,7 +494,9 @@ extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, cons
                    next_step_blocks(n_x + n_z), 0, g_step_tail};
     // spread over the grid by default: one group of 8 every `every` blocks
     const CompletePlan p = plan_complete(std::max<int64_t>(max_nx, 1),
-                                         std::max<int64_t>(max_nz, 1), std::max(n_shards, 1));
+                                         std::max<int64_t>(max_nz, 1), std::max(n_shards, 1),
+                                         dtype == TW_F64 && pred != TW_PRED_HALF &&
+                                             g_scalar_mix);
     const int ng = nxt.blocks / kXcds;
     nxt.every = g_step_every ? g_step_every
                              : (int)std::max<int64_t>(kXcds, (p.blocks / ng) / kXcds * kXcds);
@@ -422,7 +508,7 @@ extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, cons
   }
   if (n_shards == 0 || max_nx == 0 || max_nz == 0) {  // nothing to count: only the next step
     if (nxt.blocks == 0) return TW_OK;
-    hipLaunchKernelGGL((k_count_complete<double, 1, TW_PRED_GT>), dim3(nxt.blocks), dim3(kBlock),
+    hipLaunchKernelGGL((k_count_complete<double, 1, 0, TW_PRED_GT>), dim3(nxt.blocks), dim3(kBlock),
                        0, st, nullptr, nullptr, nullptr, nullptr, 1, 1, 1, nullptr, nxt);
     TW_LAUNCH_CHECK();
     return TW_OK;
