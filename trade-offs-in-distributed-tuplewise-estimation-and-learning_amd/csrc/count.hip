@@ -8,14 +8,14 @@
 // below produce that integer (uint64 per shard) and the host divides exactly as NumPy does.
 //
 // Complete kernel (k_count_complete) — VALU-bound, one launch for all shards:
-//   * a 256-thread block owns a tile of 256*R x-values of one shard (R per lane, in VGPRs)
-//     and a chunk of that shard's z-values;
+//   * each wave owns a tile of 64*R x-values of one shard (R per lane, in VGPRs) and a chunk
+//     of that shard's z-values (a block = 4 consecutive wave items, normally one z chunk);
 //   * z is wave-uniform: it streams through the SCALAR cache (s_load_dwordx16 = 8 doubles)
 //     straight into SGPR operands of v_cmp_*_f64 — no LDS staging and no VGPR traffic for z;
 //   * per pair: one v_cmp (VCC) + one carry-add into a per-(lane, r) u32 counter
 //     (the compiler folds two compares into v_cndmask + v_addc); u32 cannot overflow because a
 //     counter sees at most 2 * z_chunk increments;
-//   * epilogue: valid counters -> u64 -> wave butterfly (DPP) -> LDS -> one u64 atomic per block.
+//   * epilogue: valid counters -> u64 -> wave butterfly (DPP) -> one u64 atomic per wave.
 //   Measured on MI355X (tools/mb_issue*.hip): v_cmp_*_f64 and v_addc issue at ~0.94
 //   wave-instructions/cycle/CU, so 2 such instructions per pair cap this kernel at ~1.9e13
 //   pairs/s; see DESIGN.md "count kernel roofline".
@@ -97,7 +97,7 @@ __device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
 template <typename T, int R, int NS, int PRED>
 __global__ __launch_bounds__(kBlock) void k_count_complete(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
-    const int64_t* __restrict__ z_off, int tiles_x, int zchunks, int64_t z_chunk,
+    const int64_t* __restrict__ z_off, int n_shards, int tiles_x, int zchunks, int64_t z_chunk,
     unsigned long long* __restrict__ out, NextStep nxt) {
   // Spare blocks (block-uniform branch), in groups of kXcds so count blocks keep their XCD:
   // group g occupies blocks [g*every, g*every + kXcds) — every == kXcds: the leading blocks,
@@ -119,18 +119,25 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
       cb = b - kXcds * ((g < ng ? g : ng) + ((r >= kXcds && g < ng) ? 1 : 0));
     }
   }
+  // Work items are per WAVE: (shard, x wave-tile of 64*R values, z chunk), x tile fastest, so
+  // a shard pads its x-values to a multiple of 64*R (not 256*R) and a block's 4 waves share
+  // one z chunk (scalar-cache hits) on consecutive x tiles.
   const int per_shard = tiles_x * zchunks;
   const int lb = xcd_block(cb, gridDim.x - nxt.blocks);  // whole shards per XCD
-  const int s = lb / per_shard;
-  const int rem = lb - s * per_shard;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int item = lb * (kBlock / kWave) + wid;
+  const int s = item / per_shard;
+  if (s >= n_shards) return;  // wave-uniform; the kernel has no block barrier after this
+  const int rem = item - s * per_shard;
   const int cz = rem / tiles_x;
   const int tx = rem - cz * tiles_x;
 
   const int64_t xb = x_off[s], xe = x_off[s + 1];
   const int64_t zb = z_off[s], ze = z_off[s + 1];
-  const int64_t x0 = xb + (int64_t)tx * (kBlock * R);
+  const int64_t x0 = xb + (int64_t)tx * (kWave * R);
   const int64_t z0 = zb + (int64_t)cz * z_chunk;
-  if (x0 >= xe || z0 >= ze) return;  // block-uniform: ragged shard smaller than the grid
+  if (x0 >= xe || z0 >= ze) return;  // wave-uniform: ragged shard smaller than the grid
   const int64_t z1 = (z0 + z_chunk < ze) ? z0 + z_chunk : ze;
 
   static_assert(NS == 0 || (std::is_floating_point<T>::value && PRED != TW_PRED_HALF),
@@ -140,7 +147,7 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
   bool valid[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int64_t i = x0 + r * kBlock + threadIdx.x;
+    const int64_t i = x0 + r * kWave + lane;
     valid[r] = i < xe;
     if constexpr (NS > 0)
       xv[r] = valid[r] ? x[i] : (T)__builtin_nan("");
@@ -151,7 +158,12 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
 
   const T* __restrict__ zp = z + z0;
   const int nz = (int)(z1 - z0);
-  unsigned sacc = 0;  // wave-uniform: the scalar unit's count (NS > 0)
+  // wave-uniform scalar-unit counts, one per scalar-counted x-value: independent s_add chains
+  // let the scheduler spread the SALU work between the compares (one shared accumulator made
+  // a 16-long dependent chain at the loop end and cost ~10%)
+  unsigned sacc[NS > 0 ? NS : 1];
+#pragma unroll
+  for (int r = 0; r < (NS > 0 ? NS : 1); ++r) sacc[r] = 0;
   if constexpr (NS == 0) {
 #pragma unroll 8
     for (int j = 0; j < nz; ++j) {
@@ -170,10 +182,24 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           if (r < NS)
-            sacc += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv[u])));
+            sacc[r] += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv[u])));
           else
             acc[r] += pair_pred<T, PRED>(xv[r], zv[u]);
         }
+#ifndef TW_COUNT_NO_SCHED
+        // interleave per z: groups of (VALU, SALU) so each wave's instruction stream alternates
+        // compare and scalar-count work instead of clustering the SALU at the loop end
+#ifndef TW_SCHED_G
+#define TW_SCHED_G NS
+#endif
+        constexpr int kG = TW_SCHED_G;  // groups per z
+        constexpr int kV = (2 * R - NS + kG - 1) / kG, kS = (2 * NS + kG - 1) / kG;
+#pragma unroll
+        for (int k = 0; k < kG; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
+          __builtin_amdgcn_sched_group_barrier(0x004, kS, 0);
+        }
+#endif
       }
     }
     for (; j < nz; ++j) {
@@ -181,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (r < NS)
-          sacc += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv)));
+          sacc[r] += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv)));
         else
           acc[r] += pair_pred<T, PRED>(xv[r], zv);
       }
@@ -192,16 +218,11 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
 #pragma unroll
   for (int r = NS; r < R; ++r) tot += valid[r] ? (unsigned long long)acc[r] : 0ull;
   tot = wave_sum_u64(tot);
-  __shared__ unsigned long long part[kBlock / kWave];
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  if (lane == 0) part[wid] = tot + sacc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long b = 0;
+  unsigned long long stot = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / kWave; ++w) b += part[w];
-    if (b) atomicAdd(out + s, b);
-  }
+  for (int r = 0; r < NS; ++r) stot += sacc[r];
+  tot += stot;
+  if (lane == 0 && tot) atomicAdd(out + s, tot);  // one u64 atomic per wave
 }
 
 // Incomplete count on explicit index pairs (replay of NumPy's randint draws).
@@ -288,14 +309,14 @@ static int64_t g_force_zchunk = 0;
 
 static int g_scalar_mix = 1;  // tw_count_set_scalar_mix: 0 = VALU-only accumulation
 
-// Measured pair rates (fraction of the lane-op peak, tools/tune_count.py on the bench shape,
-// profiles/r01_count_mix_sweep.log) used to pick R: VALU-only accumulation is flat in R; the
-// mixed VALU/SALU one is best at R = 4 and 8.
+// Measured pair rates (fraction of the lane-op peak on the bench shape: tools/tune_count.py,
+// tools/count_variants.py; profiles/r01_count_mix_sweep.log, r01_count_variants.log) used to
+// pick R: VALU-only accumulation is flat in R; the mixed VALU/SALU one is best at R = 8.
 inline double pair_rate(int R, bool mix) {
   if (!mix) return 0.465;
   switch (R) {
-    case 8: return 0.533;
-    case 4: return 0.532;
+    case 8: return 0.586;
+    case 4: return 0.568;
     case 2: return 0.504;
     default: return 0.465;
   }
@@ -307,18 +328,18 @@ inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shar
   double best = -1.0;
   for (int R : {8, 4, 2, 1}) {  // least modelled time per shard (padded slots / rate)
     if (g_force_R && R != g_force_R) continue;
-    const int64_t slots = ceil_div(max_nx, (int64_t)kBlock * R) * kBlock * R;
+    const int64_t slots = ceil_div(max_nx, (int64_t)kWave * R) * kWave * R;
     const double cost = (double)slots / pair_rate(R, mix);
     if (best < 0 || cost < best * (1.0 - 1e-9)) {
       best = cost;
       p.R = R;
     }
   }
-  p.tiles_x = (int)ceil_div(max_nx, (int64_t)kBlock * p.R);
+  p.tiles_x = (int)ceil_div(max_nx, (int64_t)kWave * p.R);  // wave tiles
   // Many short z-chunks balance the tail across 256 CUs (measured: 1024-long chunks beat
   // 5k-15k chunks by 10-30% on 64 shards of 15625); below ~512 the per-block x loads and
   // epilogue start to show.
-  const int64_t target = 256 * 128;
+  const int64_t target = 256 * 128 * (kBlock / kWave);  // wave items
   const int64_t base = (int64_t)p.tiles_x * n_shards;
   int64_t zc = base >= target ? 1 : ceil_div(target, base);
   const int64_t min_chunk = 512;
@@ -328,7 +349,7 @@ inline CompletePlan plan_complete(int64_t max_nx, int64_t max_nz, int32_t n_shar
   p.z_chunk = ceil_div(p.z_chunk, 8) * 8;
   if (g_force_zchunk > 0) p.z_chunk = g_force_zchunk;
   p.zchunks = (int)ceil_div(max_nz, p.z_chunk);
-  p.blocks = (int64_t)p.tiles_x * p.zchunks * n_shards;
+  p.blocks = ceil_div((int64_t)p.tiles_x * p.zchunks * n_shards, kBlock / kWave);
   return p;
 }
 
@@ -340,19 +361,26 @@ int launch_complete(const void* x, const int64_t* x_off, const void* z, const in
   constexpr bool kMixable = std::is_floating_point<T>::value && PRED != TW_PRED_HALF;
   const bool mix = kMixable && g_scalar_mix;
   const CompletePlan p = plan_complete(max_nx, max_nz, n_shards, mix);
-  TW_ARG_CHECK(p.blocks + nxt.blocks < (1ll << 31), "tw_count_pairs: grid too large (%lld blocks)",
+  TW_ARG_CHECK((p.blocks + nxt.blocks) * (kBlock / kWave) < (1ll << 31),
+               "tw_count_pairs: grid too large (%lld blocks)",
                (long long)p.blocks);
   TW_ARG_CHECK(p.z_chunk < (1ll << 30), "tw_count_pairs: z chunk too large");
   const T* xs = (const T*)x;
   const T* zs = (const T*)z;
   auto* o = (unsigned long long*)out;
   dim3 g((unsigned)(p.blocks + nxt.blocks)), b(kBlock);
-#define TW_CC(R_, NS_) hipLaunchKernelGGL((k_count_complete<T, R_, NS_, PRED>), g, b, 0, st, xs, x_off, zs, z_off, p.tiles_x, p.zchunks, p.z_chunk, o, nxt)
+#define TW_CC(R_, NS_) hipLaunchKernelGGL((k_count_complete<T, R_, NS_, PRED>), g, b, 0, st, xs, x_off, zs, z_off, n_shards, p.tiles_x, p.zchunks, p.z_chunk, o, nxt)
   if constexpr (kMixable) {
     if (mix) {
       switch (p.R) {
-        case 8: TW_CC(8, 4); break;
-        case 4: TW_CC(4, 2); break;
+#ifndef TW_NS8
+#define TW_NS8 4
+#endif
+#ifndef TW_NS4
+#define TW_NS4 2
+#endif
+        case 8: TW_CC(8, TW_NS8); break;
+        case 4: TW_CC(4, TW_NS4); break;
         case 2: TW_CC(2, 1); break;
         default: TW_CC(1, 0); break;
       }
@@ -509,7 +537,7 @@ extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, cons
   if (n_shards == 0 || max_nx == 0 || max_nz == 0) {  // nothing to count: only the next step
     if (nxt.blocks == 0) return TW_OK;
     hipLaunchKernelGGL((k_count_complete<double, 1, 0, TW_PRED_GT>), dim3(nxt.blocks), dim3(kBlock),
-                       0, st, nullptr, nullptr, nullptr, nullptr, 1, 1, 1, nullptr, nxt);
+                       0, st, nullptr, nullptr, nullptr, nullptr, 0, 1, 1, 1, nullptr, nxt);
     TW_LAUNCH_CHECK();
     return TW_OK;
   }
