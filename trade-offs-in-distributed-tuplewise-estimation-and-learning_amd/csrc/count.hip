@@ -181,14 +181,19 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
       for (int u = 0; u < 8; ++u) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if (r < NS)
+          if (r < NS) {
             sacc[r] += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv[u])));
-          else
+          } else {
             acc[r] += pair_pred<T, PRED>(xv[r], zv[u]);
+          }
         }
 #ifndef TW_COUNT_NO_SCHED
         // interleave per z: groups of (VALU, SALU) so each wave's instruction stream alternates
         // compare and scalar-count work instead of clustering the SALU at the loop end
+        // (+9%, profiles/r01_count_variants.log "nosched"; carrying the masks one z forward or
+        // putting the SALU group first measured within noise, 5 of 8 x-values on the scalar
+        // unit likewise).  TW_SCHED_G / TW_NS8 / TW_NS4 are build-time tuning hooks
+        // (tools/build_count_variants.sh).
 #ifndef TW_SCHED_G
 #define TW_SCHED_G NS
 #endif
