@@ -416,6 +416,47 @@ def main():
     ops.count_rng = orig_rng
     inc_pairs_rank = args.shards * B_inc
 
+    # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
+    # estimation-experiment/main.py:29-31), 1e10 pairs per launch; no repartition
+    n1 = 100_000
+    g1 = torch.Generator(device="cuda").manual_seed(7 + rank)
+    X1 = torch.randn(n1, dtype=torch.float64, device="cuda", generator=g1) + 0.5
+    Z1 = torch.randn(n1, dtype=torch.float64, device="cuda", generator=g1)
+    S1 = ShardedSample(X1, Z1, 1, algo="pairs")
+    orig_count1 = S1.ops.count
+
+    def timed_count1(*a, **kw):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = orig_count1(*a, **kw)
+        e1.record()
+        kernel_ms.append((e0, e1))
+        return out
+
+    S1.ops.count = timed_count1
+    for _ in range(3):
+        S1.local_counts()
+    torch.cuda.synchronize()
+    kernel_ms.clear()
+    reps1 = 20
+    t3 = time.perf_counter()
+    for _ in range(reps1):
+        c1 = S1.local_counts()
+    torch.cuda.synchronize()
+    dt1 = time.perf_counter() - t3
+    kms1 = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    c1 = int(c1.sum())
+    single = {"note": "BASELINE configs[1]: est.Un complete AUC, n=1e5/class, one shard "
+                      "(1e10 pairs per launch), inputs resident, per-rank",
+              "value": n1 * n1 * reps1 / dt1, "unit": "pairs/s", "ms_per_call": dt1 / reps1 * 1e3,
+              "count": c1, "estimate": c1 / (n1 * n1),
+              "roofline": {"bound": "valu", "kernel": "k_count_complete",
+                           "achieved": n1 * n1 / (kms1 * 1e-3) / 1e12,
+                           "peak": PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
+                           "frac": n1 * n1 / (kms1 * 1e-3) / PEAK_LANE_OPS, "kernel_ms": kms1}}
+    del S1, X1, Z1
+
     traffic, traffic_plain = pmc_traffic()
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
@@ -452,6 +493,7 @@ def main():
                              "committed rocprofv3 --pmc summary: the timed launch, and a plain "
                              "count launch (algorithmic: 16 MB of scores)"},
         "estimate_last_step": float(est),
+        "single_shard_C2": single,
         "sorted_count": {
             "note": "same UnN steps with the exact sort+binary-search count (algo='sorted', "
                     "bit-identical estimates); pairs are logical, not compared one by one",

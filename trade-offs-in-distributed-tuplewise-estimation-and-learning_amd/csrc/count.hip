@@ -86,60 +86,12 @@ __device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
   }
 }
 
-// Mixed VALU/SALU accumulation (double, strict predicate).  Per pair the compare is one
-// v_cmp_*_f64; accumulating its 64 result bits costs one more VALU op (carry-add into a per-lane
-// counter) — the VALU issue ceiling of §4.1 — or, if the compare writes an SGPR pair, two
-// SCALAR ops (s_bcnt1_i32_b64 + s_add) on the scalar unit, which issues beside the VALU.
-// Counting NS of the R x-values per lane on the scalar unit moves that share of the work off
-// the VALU (tools/mb_mix.hip, profiles/r01_microbench_salu_mix.log: R=4 with NS=2 reaches
-// 0.63 of the lane-op peak against 0.49 for VALU-only accumulation).  Padded lanes hold NaN,
-// for which every predicate is false, so the scalar counts need no lane mask.
+// One wave item: its 64*R x-values (from x0, valid below xe) against z[z0, z1).  Returns the
+// wave's count (wave-uniform).
 template <typename T, int R, int NS, int PRED>
-__global__ __launch_bounds__(kBlock) void k_count_complete(
-    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
-    const int64_t* __restrict__ z_off, int n_shards, int tiles_x, int zchunks, int64_t z_chunk,
-    unsigned long long* __restrict__ out, NextStep nxt) {
-  // Spare blocks (block-uniform branch), in groups of kXcds so count blocks keep their XCD:
-  // group g occupies blocks [g*every, g*every + kXcds) — every == kXcds: the leading blocks,
-  // every > kXcds: spread through the grid — or, with tail != 0, the last nxt.blocks blocks.
-  int cb = blockIdx.x;  // index among the count blocks
-  if (nxt.blocks) {
-    const int b = blockIdx.x, ng = nxt.blocks / kXcds;
-    if (nxt.tail) {
-      if (b >= (int)gridDim.x - nxt.blocks) {
-        next_step_part(nxt, b - ((int)gridDim.x - nxt.blocks));
-        return;
-      }
-    } else {
-      const int g = b / nxt.every, r = b - g * nxt.every;
-      if (r < kXcds && g < ng) {
-        next_step_part(nxt, g * kXcds + r);
-        return;
-      }
-      cb = b - kXcds * ((g < ng ? g : ng) + ((r >= kXcds && g < ng) ? 1 : 0));
-    }
-  }
-  // Work items are per WAVE: (shard, x wave-tile of 64*R values, z chunk), x tile fastest, so
-  // a shard pads its x-values to a multiple of 64*R (not 256*R) and a block's 4 waves share
-  // one z chunk (scalar-cache hits) on consecutive x tiles.
-  const int per_shard = tiles_x * zchunks;
-  const int lb = xcd_block(cb, gridDim.x - nxt.blocks);  // whole shards per XCD
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int item = lb * (kBlock / kWave) + wid;
-  const int s = item / per_shard;
-  if (s >= n_shards) return;  // wave-uniform; the kernel has no block barrier after this
-  const int rem = item - s * per_shard;
-  const int cz = rem / tiles_x;
-  const int tx = rem - cz * tiles_x;
-
-  const int64_t xb = x_off[s], xe = x_off[s + 1];
-  const int64_t zb = z_off[s], ze = z_off[s + 1];
-  const int64_t x0 = xb + (int64_t)tx * (kWave * R);
-  const int64_t z0 = zb + (int64_t)cz * z_chunk;
-  if (x0 >= xe || z0 >= ze) return;  // wave-uniform: ragged shard smaller than the grid
-  const int64_t z1 = (z0 + z_chunk < ze) ? z0 + z_chunk : ze;
-
+__device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x, int64_t x0,
+                                                         int64_t xe, const T* __restrict__ z,
+                                                         int64_t z0, int64_t z1, int lane) {
   static_assert(NS == 0 || (std::is_floating_point<T>::value && PRED != TW_PRED_HALF),
                 "scalar-unit counting needs NaN padding and a one-bit predicate");
   T xv[R];
@@ -226,8 +178,91 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
   unsigned long long stot = 0;
 #pragma unroll
   for (int r = 0; r < NS; ++r) stot += sacc[r];
-  tot += stot;
-  if (lane == 0 && tot) atomicAdd(out + s, tot);  // one u64 atomic per wave
+  return tot + stot;
+}
+
+// Mixed VALU/SALU accumulation (double, strict predicate).  Per pair the compare is one
+// v_cmp_*_f64; accumulating its 64 result bits costs one more VALU op (carry-add into a per-lane
+// counter) — the VALU issue ceiling of §4.1 — or, if the compare writes an SGPR pair, two
+// SCALAR ops (s_bcnt1_i32_b64 + s_add) on the scalar unit, which issues beside the VALU.
+// Counting NS of the R x-values per lane on the scalar unit moves that share of the work off
+// the VALU (tools/mb_mix.hip, profiles/r01_microbench_salu_mix.log: R=4 with NS=2 reaches
+// 0.63 of the lane-op peak against 0.49 for VALU-only accumulation).  Padded lanes hold NaN,
+// for which every predicate is false, so the scalar counts need no lane mask.
+template <typename T, int R, int NS, int PRED>
+__global__ __launch_bounds__(kBlock) void k_count_complete(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, int n_shards, int tiles_x, int zchunks, int64_t z_chunk,
+    unsigned long long* __restrict__ out, NextStep nxt) {
+  // Spare blocks (block-uniform branch), in groups of kXcds so count blocks keep their XCD:
+  // group g occupies blocks [g*every, g*every + kXcds) — every == kXcds: the leading blocks,
+  // every > kXcds: spread through the grid — or, with tail != 0, the last nxt.blocks blocks.
+  int cb = blockIdx.x;  // index among the count blocks
+  if (nxt.blocks) {
+    const int b = blockIdx.x, ng = nxt.blocks / kXcds;
+    if (nxt.tail) {
+      if (b >= (int)gridDim.x - nxt.blocks) {
+        next_step_part(nxt, b - ((int)gridDim.x - nxt.blocks));
+        return;
+      }
+    } else {
+      const int g = b / nxt.every, r = b - g * nxt.every;
+      if (r < kXcds && g < ng) {
+        next_step_part(nxt, g * kXcds + r);
+        return;
+      }
+      cb = b - kXcds * ((g < ng ? g : ng) + ((r >= kXcds && g < ng) ? 1 : 0));
+    }
+  }
+  // Work items are per WAVE: (shard, x wave-tile of 64*R values, z chunk), x tile fastest, so
+  // a shard pads its x-values to a multiple of 64*R (not 256*R) and a block's 4 waves share
+  // one z chunk (scalar-cache hits) on consecutive x tiles.
+  const int per_shard = tiles_x * zchunks;
+  const int lb = xcd_block(cb, gridDim.x - nxt.blocks);  // whole shards per XCD
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int item = lb * (kBlock / kWave) + wid;
+  const int s = item / per_shard;
+  bool active = s < n_shards;  // wave-uniform (no early return: the block reduces below)
+  int64_t x0 = 0, xe = 0, z0 = 0, z1 = 0;
+  if (active) {
+    const int rem = item - s * per_shard;
+    const int cz = rem / tiles_x;
+    const int tx = rem - cz * tiles_x;
+    const int64_t xb = x_off[s], zb = z_off[s], ze = z_off[s + 1];
+    xe = x_off[s + 1];
+    x0 = xb + (int64_t)tx * (kWave * R);
+    z0 = zb + (int64_t)cz * z_chunk;
+    z1 = (z0 + z_chunk < ze) ? z0 + z_chunk : ze;
+    active = x0 < xe && z0 < ze;  // ragged shard smaller than the grid
+  }
+
+  unsigned long long tot = 0;
+  if (active) tot = count_item<T, R, NS, PRED>(x, x0, xe, z, z0, z1, lane);
+  // Block reduction: the 4 waves of a block normally count the same shard, and one atomic per
+  // block and shard keeps same-address atomics rare (a single-shard launch with one atomic
+  // per wave serialised on them: tools/tune_c2.py).
+  __shared__ unsigned long long part[kBlock / kWave];
+  __shared__ int part_s[kBlock / kWave];
+  if (lane == 0) {
+    part[wid] = tot;
+    part_s[wid] = active ? s : -1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int cur = part_s[0];
+    unsigned long long sum = part[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / kWave; ++w) {
+      if (part_s[w] != cur) {
+        if (cur >= 0 && sum) atomicAdd(out + cur, sum);
+        cur = part_s[w];
+        sum = 0;
+      }
+      sum += part[w];
+    }
+    if (cur >= 0 && sum) atomicAdd(out + cur, sum);
+  }
 }
 
 // Incomplete count on explicit index pairs (replay of NumPy's randint draws).
