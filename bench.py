@@ -503,18 +503,22 @@ def main():
             "counts_identical_to_all_pairs": same_counts},
         "incomplete": {
             "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
-                    "drawn pairs per shard (Philox4x32-10) counted per step",
+                    "drawn pairs per shard (Philox4x32-10, two pairs per block, Lemire maps) "
+                    "counted per step on 16-bit rank codes in LDS",
             "B_per_shard": B_inc, "value": inc_pairs_rank * world * args.steps / dt_inc,
             "unit": "pairs/s", "ms_per_step": dt_inc / args.steps * 1e3,
             "estimate_last_step": float(est_inc),
-            "roofline": {"bound": "valu", "kernel": "k_count_rng",
+            "roofline": {"bound": "valu",
+                         "kernel": "k_sort_chunks + k_rank_codes + k_count_rng_ranked",
                          "achieved": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3) / 1e12,
                          "peak": PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
                          "frac": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3)
                          / PEAK_LANE_OPS,
                          "kernel_ms": kms_inc,
                          "note": f"{INC_LANE_OPS} lane-ops per pair (SURVEY.md §8(d) contract "
-                                 "constant: Philox4x32-10 + 2 range maps + 1 compare)"}},
+                                 "constant: 2 Philox4x32-10 words + 2 range maps + 1 compare); "
+                                 "kernel_ms = the whole tw_count_pairs_rng_ws call (z sort, "
+                                 "rank codes, draw-and-count)"}},
     }
     if world == 1 and not args.no_sgd:
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'

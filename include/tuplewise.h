@@ -126,9 +126,13 @@ int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
                        void* stream);
 
 /* ---- Row A5/A8, device-RNG mode: B pairs per shard drawn on the device ----------------
- * Pair p of local shard s: Philox4x32-10(key = seed, counter = (p lo, p hi, shard_base + s, 0))
- * gives 4 words; (w1:w0) and (w3:w2) are mapped to [0, nx_s) and [0, nz_s) by 64-bit
- * multiply-high; with-replacement sampling like UB's randint (compute_stats.py:40-41).
+ * Philox4x32-10(key = seed, counter = (q lo, q hi, shard_base + s, 0)) gives the 4 words
+ * (w0, w1, w2, w3) of pairs 2q (i from w0, j from w1) and 2q+1 (w2, w3) of local shard s; a word
+ * w maps to [0, n) by Lemire's multiply-shift (w * n) >> 32 with rejection of (w * n) mod 2^32
+ * < 2^32 mod n, a rejected word being replaced by the same word of counter word 3 = 1, 2, ...
+ * (exactly uniform; with-replacement sampling like UB's randint, compute_stats.py:40-41).
+ * Shards of >= 2^32 values: pair p uses counter (p lo, p hi, shard_base + s, 0) and maps
+ * (w1:w0), (w3:w2) by 64-bit multiply-high.
  * shard_base = the global index of local shard 0, so draws do not depend on how shards are
  * spread over ranks.  Not bit-comparable with NumPy's stream; statistically equivalent
  * (tests/test_statistics.py). */
@@ -136,6 +140,20 @@ int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,
                        const int64_t* d_z_off, int32_t n_shards, int64_t B, uint64_t seed,
                        uint64_t shard_base, int32_t dtype, int32_t pred, uint64_t* d_out,
                        void* stream);
+
+/* The same draws and counts as tw_count_pairs_rng, with the compares on 16-bit rank codes held
+ * in LDS (sorted z per shard; c_i = #{z < x_i}, c'_i = #{z <= x_i}, p_j = #{z < z_j}; x > z iff
+ * c_i > p_j, x >= z iff c'_i > p_j) instead of random 8-B gathers of the scores.  Applies when
+ * every shard has nx, nz < 65536, the codes fit in LDS and pred is GT or HALF: then
+ * tw_count_pairs_rng_work_bytes() > 0 and d_work must hold that many bytes; otherwise (or with
+ * d_work == NULL) this call runs tw_count_pairs_rng. */
+int64_t tw_count_pairs_rng_work_bytes(int32_t n_shards, int64_t max_nx, int64_t max_nz,
+                                      int32_t dtype, int32_t pred);
+int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                          const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                          int64_t max_nz, int64_t B, uint64_t seed, uint64_t shard_base,
+                          int32_t dtype, int32_t pred, void* d_work, int64_t work_bytes,
+                          uint64_t* d_out, void* stream);
 
 /* ---- Row A2 (prod/gini) and f1 (conv_AUC): float pair sums, complete -------------------
  * d_out[s] (double) = sum over all pairs of shard s of kern(x_i, z_j).  Deterministic: fixed

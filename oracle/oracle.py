@@ -385,14 +385,44 @@ def _mulhi64(a: np.ndarray, n: int) -> np.ndarray:
     return np.array([(int(v) * n) >> 64 for v in a], dtype=np.int64)
 
 
+def _lemire(words: np.ndarray, n: int, q: np.ndarray, shard: int, w: int, seed: int):
+    """Lemire's multiply-shift with rejection (csrc/count.hip lemire_index): (r * n) >> 32,
+    a rejected word replaced by word w of the Philox block at counter word 3 = 1, 2, ..."""
+    m = words.astype(np.uint64) * np.uint64(n)
+    t = np.uint64(((1 << 32) - n) % n)
+    bad = (m & _M32) < t
+    att = 1
+    while bad.any():
+        qb = q[bad]
+        r = philox4x32_10(qb & _M32, qb >> np.uint64(32), np.full(qb.size, shard, np.uint64),
+                          np.full(qb.size, att, np.uint64), seed & 0xFFFFFFFF,
+                          (seed >> 32) & 0xFFFFFFFF)[w]
+        m[bad] = r * np.uint64(n)
+        bad = (m & _M32) < t
+        att += 1
+    return (m >> np.uint64(32)).astype(np.int64)
+
+
 def rng_pairs(nx: int, nz: int, B: int, seed: int, shard: int):
-    """The (i, j) pairs tw_count_pairs_rng draws for one shard (global shard index)."""
-    p = np.arange(B, dtype=np.uint64)
-    a, b, c, d = philox4x32_10(p & _M32, p >> np.uint64(32), np.full(B, shard, np.uint64),
-                               np.zeros(B, np.uint64), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    u = (b << np.uint64(32)) | a
-    v = (d << np.uint64(32)) | c
-    return _mulhi64(u, nx), _mulhi64(v, nz)
+    """The (i, j) pairs tw_count_pairs_rng draws for one shard (global shard index):
+    Philox block q gives pairs 2q (words 0, 1) and 2q+1 (words 2, 3) (csrc/count.hip
+    k_count_rng); shards of >= 2^32 values use one block per pair and 64-bit multiply-high."""
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    if nx >= 1 << 32 or nz >= 1 << 32:
+        p = np.arange(B, dtype=np.uint64)
+        a, b, c, d = philox4x32_10(p & _M32, p >> np.uint64(32), np.full(B, shard, np.uint64),
+                                   np.zeros(B, np.uint64), k0, k1)
+        return (_mulhi64((b << np.uint64(32)) | a, nx), _mulhi64((d << np.uint64(32)) | c, nz))
+    q = np.arange((B + 1) // 2, dtype=np.uint64)
+    a, b, c, d = philox4x32_10(q & _M32, q >> np.uint64(32), np.full(q.size, shard, np.uint64),
+                               np.zeros(q.size, np.uint64), k0, k1)
+    i = np.empty(2 * q.size, np.int64)
+    j = np.empty(2 * q.size, np.int64)
+    i[0::2] = _lemire(a, nx, q, shard, 0, seed)
+    j[0::2] = _lemire(b, nz, q, shard, 1, seed)
+    i[1::2] = _lemire(c, nx, q, shard, 2, seed)
+    j[1::2] = _lemire(d, nz, q, shard, 3, seed)
+    return i[:B], j[:B]
 
 
 def _sgd_draw(seed, step, idx, shard, tag):

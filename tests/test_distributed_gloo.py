@@ -64,7 +64,8 @@ class OracleOps:
         return torch.tensor([f(xs[xo[s]:xo[s + 1]], zs[zo[s]:zo[s + 1]])
                              for s in range(n_shards)], dtype=torch.int64)
 
-    def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred):
+    def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred,
+                  max_nx=None, max_nz=None):
         xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
         out = []
         for s in range(n_shards):

@@ -521,3 +521,47 @@ def test_grad_complete_block_drop_in(gpu):
     one = cs.grad_complete_block(w, 1, loss="logistic")(X[:50], Z[:30])
     np.testing.assert_allclose(one, O.grad_complete_block(w, 1, "logistic")(X[:50], Z[:30]),
                                rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.parametrize("dtype_name", ["f64", "i64"])
+@pytest.mark.parametrize("pred_name", ["gt", "half"])
+def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name):
+    """tw_count_pairs_rng_ws (rank codes in LDS) == tw_count_pairs_rng (score gathers) ==
+    oracle, on tie-heavy shards with NaN, -0.0/+0.0 and ragged sizes (incl. an empty one)."""
+    import torch
+    from tuplewise import _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(21)
+    nxs, nzs = [1000, 1, 0, 4097, 3000], [700, 5, 9, 20000, 1]  # 20000: 2 LDS groups
+    if dtype_name == "f64":
+        xs = [rng.randint(-20, 20, n).astype(np.float64) for n in nxs]
+        zs = [rng.randint(-20, 20, n).astype(np.float64) for n in nzs]
+        xs[0][:50] = np.nan
+        zs[0][:30] = np.nan
+        xs[3][:100] = -0.0
+        zs[3][:100] = 0.0
+        dt = L.TW_F64
+    else:
+        xs = [rng.randint(-30, 30, n).astype(np.int64) for n in nxs]
+        zs = [rng.randint(-30, 30, n).astype(np.int64) for n in nzs]
+        dt = L.TW_I64
+    pred = L.TW_PRED_GT if pred_name == "gt" else L.TW_PRED_HALF
+    X, Z = np.concatenate(xs), np.concatenate(zs)
+    xo = np.concatenate([[0], np.cumsum(nxs)]).astype(np.int64)
+    zo = np.concatenate([[0], np.cumsum(nzs)]).astype(np.int64)
+    dev = lambda a: torch.from_numpy(a).cuda()
+    ops = HipOps()
+    B, seed, base = 12_345, 0xC0FFEE, 17
+    args = (dev(X), dev(xo), dev(Z), dev(zo), len(nxs), B, seed, base, dt, pred)
+    assert L.lib().tw_count_pairs_rng_work_bytes(len(nxs), max(nxs), max(nzs), dt, pred) > 0
+    ranked = ops.count_rng(*args, max_nx=max(nxs), max_nz=max(nzs)).cpu().numpy()
+    plain = ops.count_rng(*args).cpu().numpy()
+    assert np.array_equal(ranked, plain)
+    for s in range(len(nxs)):
+        if nxs[s] == 0 or nzs[s] == 0:
+            assert ranked[s] == 0
+            continue
+        i, j = O.rng_pairs(nxs[s], nzs[s], B, seed, base + s)
+        a, b = xs[s][i], zs[s][j]
+        want = int(np.sum(a > b)) + (int(np.sum(a >= b)) if pred_name == "half" else 0)
+        assert ranked[s] == want, s

@@ -39,6 +39,9 @@ _SIGNATURES = {
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],
     "tw_count_pairs_idx": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _vp],
     "tw_count_pairs_rng": [_vp, _vp, _vp, _vp, _i32, _i64, _u64, _u64, _i32, _i32, _vp, _vp],
+    "tw_count_pairs_rng_work_bytes": [_i32, _i64, _i64, _i32, _i32],
+    "tw_count_pairs_rng_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _u64, _u64, _i32, _i32,
+                              _vp, _i64, _vp, _vp],
     "tw_pair_sum_work_per_shard": [_i64, _i64],
     "tw_pair_sum_f64": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _f64, _vp, _vp, _vp],
     "tw_pair_sum_idx_work_per_shard": [_i64],
@@ -78,6 +81,7 @@ _SIGNATURES = {
 _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,
     "tw_count_pairs_sorted_work_bytes": ctypes.c_int64,
+    "tw_count_pairs_rng_work_bytes": ctypes.c_int64,
     "tw_pair_sum_work_per_shard": ctypes.c_int64,
     "tw_pair_sum_idx_work_per_shard": ctypes.c_int64,
     "tw_pair_grad_complete_work_bytes": ctypes.c_int64,

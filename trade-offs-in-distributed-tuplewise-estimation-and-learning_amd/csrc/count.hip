@@ -298,6 +298,12 @@ __global__ __launch_bounds__(kBlock) void k_count_idx(const T* __restrict__ x,
 }
 
 // Incomplete count with pairs drawn on the device (with replacement, like UB's randint).
+// One Philox4x32-10 block (counter (q lo, q hi, shard, 0)) gives the 4 words of TWO pairs,
+// 2q (words a, b) and 2q+1 (words c, d): word -> index by Lemire's multiply-shift with
+// rejection, exactly uniform on [0, n).  A rejected word (probability < n / 2^32) is replaced by
+// the same word of the block at counter word 3 = 1, 2, ...  The Philox multiplies
+// (v_mad_u64_u32) dominate the kernel, so two pairs per block halves its cost.  Shards of 2^32
+// or more values use the 64-bit multiply-high of two words instead (one pair per block).
 template <typename T, int PRED, int PPT>
 __global__ __launch_bounds__(kBlock) void k_count_rng(const T* __restrict__ x,
                                                       const int64_t* __restrict__ x_off,
@@ -311,17 +317,38 @@ __global__ __launch_bounds__(kBlock) void k_count_rng(const T* __restrict__ x,
   const int bi = lb - s * blocks_per_shard;
   const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
   const int64_t zb = z_off[s], nz = z_off[s + 1] - zb;
-  const int64_t p0 = (int64_t)bi * (kBlock * PPT);
-  if (p0 >= B || nx <= 0 || nz <= 0) return;
+  const uint32_t ss = (uint32_t)s + sid;
   unsigned acc = 0;
+  if (nx > 0 && nz > 0) {
+    if (((nx | nz) >> 32) == 0) {
+      const int64_t nq = (B + 1) / 2;  // Philox blocks of this shard
+      const int64_t q0 = (int64_t)bi * (kBlock * (PPT / 2));
+      if (q0 < nq) {
 #pragma unroll
-  for (int k = 0; k < PPT; ++k) {
-    const int64_t p = p0 + k * kBlock + threadIdx.x;
-    if (p < B) {
-      const u32x4 r = philox4x32_10(u32x4{(uint32_t)p, (uint32_t)(p >> 32), (uint32_t)s + sid, 0u}, k0, k1);
-      const uint64_t i = mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)nx);
-      const uint64_t j = mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)nz);
-      acc += pair_pred<T, PRED>(x[xb + i], z[zb + j]);
+        for (int k = 0; k < PPT / 2; ++k) {
+          const int64_t q = q0 + k * kBlock + threadIdx.x;
+          if (q < nq) {
+            const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
+            const uint32_t i0 = lemire_index(r.a, (uint32_t)nx, q, ss, 0, k0, k1);
+            const uint32_t j0 = lemire_index(r.b, (uint32_t)nz, q, ss, 1, k0, k1);
+            acc += pair_pred<T, PRED>(x[xb + i0], z[zb + j0]);
+            if (2 * q + 1 < B) {
+              const uint32_t i1 = lemire_index(r.c, (uint32_t)nx, q, ss, 2, k0, k1);
+              const uint32_t j1 = lemire_index(r.d, (uint32_t)nz, q, ss, 3, k0, k1);
+              acc += pair_pred<T, PRED>(x[xb + i1], z[zb + j1]);
+            }
+          }
+        }
+      }
+    } else {  // huge shards: one pair per block, 64-bit multiply-high
+      for (int64_t p = (int64_t)bi * (kBlock * PPT) + threadIdx.x,
+                   pe = std::min<int64_t>(B, (int64_t)(bi + 1) * (kBlock * PPT));
+           p < pe; p += kBlock) {
+        const u32x4 r = philox4x32_10(u32x4{(uint32_t)p, (uint32_t)(p >> 32), ss, 0u}, k0, k1);
+        const uint64_t i = mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)nx);
+        const uint64_t j = mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)nz);
+        acc += pair_pred<T, PRED>(x[xb + i], z[zb + j]);
+      }
     }
   }
   unsigned long long tot = wave_sum_u64((unsigned long long)acc);

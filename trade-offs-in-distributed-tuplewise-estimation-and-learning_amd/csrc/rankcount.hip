@@ -277,6 +277,227 @@ int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_
   return TW_OK;
 }
 
+// ------------------------------------------------ ranked device-RNG incomplete count
+// tw_count_pairs_rng_ws: the draws of tw_count_pairs_rng (Philox blocks of two pairs, Lemire
+// index maps), but the compares read 16-bit RANK CODES from LDS instead of gathering doubles
+// from L2.  With zs the shard's sorted z keys:
+//   p_j  = #{zs < z_j}          (first position of z_j's value)
+//   c_i  = #{zs < x_i}          x_i >  z_j  <=>  c_i  > p_j
+//   c'_i = #{zs <= x_i}         x_i >= z_j  <=>  c'_i > p_j      (half-ties: add both)
+// exact for any keys (order_key makes -0 == +0; NaN x gets c = c' = 0, NaN z the largest p,
+// so every compare with a NaN is false, as in NumPy).  The random 8-B gathers of the plain
+// kernel fetch a whole L2 line each and bound it by L2 bandwidth; the codes of a 15625-value
+// shard pair are 62 KiB (94 KiB with ties) and sit in LDS.  z is sorted in the sorted-count
+// path's chunks (k_sort_chunks); a code is the sum of its per-chunk binary searches.  Applies
+// when every shard has nx, nz < 65536 and the codes fit in LDS; otherwise the plain kernel runs.
+constexpr int kRngThreads = 1024;
+#ifndef TW_CODE_ELEMS
+#define TW_CODE_ELEMS 4
+#endif
+constexpr int kCodeElems = TW_CODE_ELEMS;  // elements per thread in k_rank_codes
+
+template <typename T, int PRED>
+__global__ __launch_bounds__(kSortThreads) void k_rank_codes(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, const uint64_t* __restrict__ sorted, int chunks, int C,
+    int tiles, int64_t max_nx, int64_t max_nz, uint16_t* __restrict__ cx,
+    uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int s = lb / tiles;
+  const int t = lb - s * tiles;
+  const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
+  const int64_t zb = z_off[s], nz = z_off[s + 1] - zb;
+  // this thread's elements: x-values first, then z-values, of the shard's (nx + nz)
+  const int64_t e0 = (int64_t)t * (kSortThreads * kCodeElems);
+  uint64_t k[kCodeElems];
+  uint32_t lo[kCodeElems], hi[kCodeElems];
+  bool isx[kCodeElems], live[kCodeElems];
+#pragma unroll
+  for (int r = 0; r < kCodeElems; ++r) {
+    const int64_t e = e0 + r * kSortThreads + threadIdx.x;
+    isx[r] = e < nx;
+    live[r] = e < nx + nz;
+    T v = (T)0;
+    if (isx[r]) v = x[xb + e];
+    else if (live[r]) v = z[zb + (e - nx)];
+    k[r] = order_key<T>(v);
+    if (isx[r] && is_nan_score<T>(v)) live[r] = false;  // NaN x: codes 0, below every p_j
+    lo[r] = hi[r] = 0;
+  }
+  // #{keys < k} (and <= k) summed over the shard's sorted chunks, staged as in k_rank_count
+  const int group = (int)std::max<int64_t>(1, kMaxChunk / C);
+  for (int c0 = 0; c0 < chunks; c0 += group) {
+    const int ng = std::min(group, chunks - c0);
+    const uint64_t* src = sorted + ((int64_t)s * chunks + c0) * C;
+    __syncthreads();
+    for (int i = threadIdx.x; i < ng * C; i += kSortThreads) keys[i] = src[i];
+    __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+      const uint64_t* kc = keys + g * C;
+#pragma unroll
+      for (int r = 0; r < kCodeElems; ++r) {
+        if (live[r]) {
+          lo[r] += lower_bound_lds(kc, C, k[r]);
+          if (PRED == TW_PRED_HALF && isx[r]) hi[r] += upper_bound_lds(kc, C, k[r]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kCodeElems; ++r) {
+    const int64_t e = e0 + r * kSortThreads + threadIdx.x;
+    if (isx[r]) {
+      cx[(int64_t)s * max_nx + e] = (uint16_t)lo[r];
+      if (PRED == TW_PRED_HALF) cx2[(int64_t)s * max_nx + e] = (uint16_t)hi[r];
+    } else if (e < nx + nz) {
+      pz[(int64_t)s * max_nz + (e - nx)] = (uint16_t)lo[r];
+    }
+  }
+}
+
+template <int PRED>
+__global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
+    const int64_t* __restrict__ x_off, const int64_t* __restrict__ z_off,
+    const uint16_t* __restrict__ cx, const uint16_t* __restrict__ cx2,
+    const uint16_t* __restrict__ pz, int64_t max_nx, int64_t max_nz, int64_t B, int parts,
+    uint32_t k0, uint32_t k1, uint32_t sid, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t codes[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);  // a shard's parts share one L2
+  const int s = lb / parts;
+  const int part = lb - s * parts;
+  const int64_t nx = x_off[s + 1] - x_off[s], nz = z_off[s + 1] - z_off[s];
+  unsigned acc = 0;
+  if (nx > 0 && nz > 0) {
+    uint16_t* lx = codes;
+    uint16_t* lx2 = codes + nx;
+    uint16_t* lz = codes + (PRED == TW_PRED_HALF ? 2 : 1) * nx;
+    for (int64_t i = threadIdx.x; i < nx; i += kRngThreads) {
+      lx[i] = cx[(int64_t)s * max_nx + i];
+      if (PRED == TW_PRED_HALF) lx2[i] = cx2[(int64_t)s * max_nx + i];
+    }
+    for (int64_t j = threadIdx.x; j < nz; j += kRngThreads) lz[j] = pz[(int64_t)s * max_nz + j];
+    __syncthreads();
+    const uint32_t ss = (uint32_t)s + sid;
+    const int64_t nq = (B + 1) / 2;
+    const int64_t per = (nq + parts - 1) / parts;
+    const int64_t q0 = (int64_t)part * per, q1 = std::min<int64_t>(nq, q0 + per);
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += kRngThreads) {
+      const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
+      const uint32_t i0 = lemire_index(r.a, (uint32_t)nx, q, ss, 0, k0, k1);
+      const uint32_t j0 = lemire_index(r.b, (uint32_t)nz, q, ss, 1, k0, k1);
+      const uint32_t pj0 = lz[j0];
+      acc += lx[i0] > pj0;
+      if (PRED == TW_PRED_HALF) acc += lx2[i0] > pj0;
+      if (2 * q + 1 < B) {
+        const uint32_t i1 = lemire_index(r.c, (uint32_t)nx, q, ss, 2, k0, k1);
+        const uint32_t j1 = lemire_index(r.d, (uint32_t)nz, q, ss, 3, k0, k1);
+        const uint32_t pj1 = lz[j1];
+        acc += lx[i1] > pj1;
+        if (PRED == TW_PRED_HALF) acc += lx2[i1] > pj1;
+      }
+    }
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part_sum[kRngThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part_sum[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < kRngThreads / kWave; ++w) b += part_sum[w];
+    if (b) atomicAdd(out + s, b);
+  }
+}
+
+struct RngRankPlan {
+  bool ok;
+  int C, chunks, tiles, parts;
+  int64_t keys_bytes, cx_off, cx2_off, pz_off, total;
+  size_t lds;
+};
+
+static RngRankPlan plan_rng_ranked(int32_t n_shards, int64_t max_nx, int64_t max_nz, int32_t pred,
+                                   int64_t B) {
+  RngRankPlan p{};
+  p.ok = n_shards > 0 && max_nx > 0 && max_nz > 0 && max_nz < 65536 && max_nx < 65536 &&
+         (pred == TW_PRED_GT || pred == TW_PRED_HALF);
+  if (!p.ok) return p;
+  const RankPlan rp = plan_rank(max_nx, max_nz);  // the sorted-count path's z chunks
+  p.C = rp.C;
+  p.chunks = rp.chunks;
+  p.tiles = (int)ceil_div(max_nx + max_nz, (int64_t)kSortThreads * kCodeElems);
+  const int nc = pred == TW_PRED_HALF ? 2 : 1;
+  p.lds = (size_t)(nc * max_nx + max_nz) * sizeof(uint16_t);
+  p.ok = p.lds <= 160 * 1024 - 1024;
+  // ~2 blocks of 1024 threads per CU over the whole grid, >= 8192 draws per block
+  const int64_t nq = std::max<int64_t>(1, (B + 1) / 2);
+  p.parts = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(512, n_shards),
+                                                        ceil_div(nq, 8192)));
+  auto al = [](int64_t b) { return ceil_div(b, 256) * 256; };
+  p.keys_bytes = al((int64_t)n_shards * p.chunks * p.C * 8);
+  p.cx_off = p.keys_bytes;
+  p.cx2_off = p.cx_off + al((int64_t)n_shards * max_nx * 2);
+  p.pz_off = p.cx2_off + (pred == TW_PRED_HALF ? al((int64_t)n_shards * max_nx * 2) : 0);
+  p.total = p.pz_off + al((int64_t)n_shards * max_nz * 2);
+  return p;
+}
+
+template <typename T, int PRED>
+int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                      int32_t n_shards, int64_t max_nx, int64_t max_nz, int64_t B, uint64_t seed,
+                      uint64_t sid, const RngRankPlan& p, void* work, uint64_t* out,
+                      hipStream_t st) {
+  static bool attrs_set = false;
+  if (!attrs_set) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 4>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 8>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 16>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_codes<T, PRED>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_ranked<PRED>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 1024));
+    attrs_set = true;
+  }
+  char* w = (char*)work;
+  uint64_t* keys = (uint64_t*)w;
+  uint16_t* cx = (uint16_t*)(w + p.cx_off);
+  uint16_t* cx2 = (uint16_t*)(w + p.cx2_off);
+  uint16_t* pz = (uint16_t*)(w + p.pz_off);
+  const size_t lds_sort = sizeof(uint64_t) * p.C;
+  const size_t lds_codes = sizeof(uint64_t) * std::min<int64_t>((int64_t)p.chunks * p.C, kMaxChunk);
+  const int E = std::max(4, p.C / kSortThreads);
+  const dim3 gs((unsigned)(n_shards * p.chunks));
+  if (E == 4)
+    hipLaunchKernelGGL((k_sort_chunks<T, 4>), gs, dim3(p.C / 4), lds_sort, st, (const T*)z,
+                       z_off, p.chunks, p.C, keys);
+  else if (E == 8)
+    hipLaunchKernelGGL((k_sort_chunks<T, 8>), gs, dim3(p.C / 8), lds_sort, st, (const T*)z,
+                       z_off, p.chunks, p.C, keys);
+  else
+    hipLaunchKernelGGL((k_sort_chunks<T, 16>), gs, dim3(p.C / 16), lds_sort, st, (const T*)z,
+                       z_off, p.chunks, p.C, keys);
+  TW_LAUNCH_CHECK();
+  hipLaunchKernelGGL((k_rank_codes<T, PRED>), dim3(n_shards * p.tiles), dim3(kSortThreads),
+                     lds_codes, st, (const T*)x, x_off, (const T*)z, z_off, keys, p.chunks, p.C,
+                     p.tiles, max_nx, max_nz, cx, cx2, pz);
+  TW_LAUNCH_CHECK();
+  hipLaunchKernelGGL((k_count_rng_ranked<PRED>), dim3(n_shards * p.parts), dim3(kRngThreads),
+                     p.lds, st, x_off, z_off, cx, cx2, pz, max_nx, max_nz, B, p.parts,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
+                     (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 }  // namespace tw
 
 using namespace tw;
@@ -308,4 +529,44 @@ extern "C" int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, co
   if (dtype == TW_I64) return launch_rank<long long>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, pred, d_work, d_out, st);
   set_error("tw_count_pairs_sorted: unknown dtype %d", dtype);
   return TW_ERR_ARG;
+}
+
+extern "C" int64_t tw_count_pairs_rng_work_bytes(int32_t n_shards, int64_t max_nx,
+                                                 int64_t max_nz, int32_t dtype, int32_t pred) {
+  if (dtype != TW_F64 && dtype != TW_I64) return 0;
+  const RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pred, 1);
+  return p.ok ? p.total : 0;
+}
+
+extern "C" int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                  const int64_t* d_z_off, int32_t n_shards, int64_t B,
+                                  uint64_t seed, uint64_t stream_id, int32_t dtype, int32_t pred,
+                                  uint64_t* d_out, void* stream);
+
+extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                     const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                     int64_t max_nz, int64_t B, uint64_t seed,
+                                     uint64_t stream_id, int32_t dtype, int32_t pred,
+                                     void* d_work, int64_t work_bytes, uint64_t* d_out,
+                                     void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && B >= 0 && max_nx >= 0 && max_nz >= 0,
+               "tw_count_pairs_rng_ws: bad sizes");
+  const RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pred, B);
+  if (!p.ok || (dtype != TW_F64 && dtype != TW_I64) || B == 0 || d_work == nullptr ||
+      work_bytes < p.total)  // not applicable: the plain kernel draws the same pairs
+    return tw_count_pairs_rng(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, dtype,
+                              pred, d_out, stream);
+  TW_ARG_CHECK((int64_t)n_shards * p.parts < (1ll << 31) && (int64_t)n_shards * p.tiles < (1ll << 31) &&
+                   (int64_t)n_shards * p.chunks < (1ll << 31),
+               "tw_count_pairs_rng_ws: grid too large");
+  hipStream_t st = (hipStream_t)stream;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  if (dtype == TW_F64) {
+    if (pred == TW_PRED_HALF)
+      return launch_rng_ranked<double, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
+    return launch_rng_ranked<double, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
+  }
+  if (pred == TW_PRED_HALF)
+    return launch_rng_ranked<long long, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
+  return launch_rng_ranked<long long, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
 }

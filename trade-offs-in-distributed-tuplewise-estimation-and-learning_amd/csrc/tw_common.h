@@ -99,4 +99,23 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t 
 }
 __device__ __forceinline__ uint64_t mulhi_u64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
 
+// Device-RNG pair draws (tw_count_pairs_rng, include/tuplewise.h): word w of the Philox block
+// (q lo, q hi, shard, att), and Lemire's exactly uniform map of a word to [0, n).
+__device__ __forceinline__ uint32_t philox_word(uint64_t q, uint32_t sid, uint32_t att, int w,
+                                                uint32_t k0, uint32_t k1) {
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), sid, att}, k0, k1);
+  return w == 0 ? r.a : w == 1 ? r.b : w == 2 ? r.c : r.d;
+}
+
+__device__ __forceinline__ uint32_t lemire_index(uint32_t r, uint32_t n, uint64_t q, uint32_t sid,
+                                                 int w, uint32_t k0, uint32_t k1) {
+  uint64_t m = (uint64_t)r * n;
+  if ((uint32_t)m < n) {  // rare: only then can the draw fall in the biased zone
+    const uint32_t t = (0u - n) % n;
+    for (uint32_t att = 1; (uint32_t)m < t; ++att)
+      m = (uint64_t)philox_word(q, sid, att, w, k0, k1) * n;
+  }
+  return (uint32_t)(m >> 32);
+}
+
 }  // namespace tw

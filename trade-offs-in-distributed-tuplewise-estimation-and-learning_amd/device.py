@@ -119,11 +119,25 @@ class HipOps:
                L.stream_handle())
         return out
 
-    def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred):
+    def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred,
+                  max_nx=None, max_nz=None):
+        """Device-RNG incomplete counts.  With the shard bounds known, the ranked kernels
+        (16-bit rank codes in LDS, csrc/rankcount.hip) run; same draws, same integers."""
         out = L.empty((n_shards,), self.t.int64)
-        L.call("tw_count_pairs_rng", L.ptr(x), L.ptr(x_off_dev), L.ptr(z), L.ptr(z_off_dev),
-               int(n_shards), int(B), int(seed), int(shard_base), int(dtype), int(pred), L.ptr(out),
-               L.stream_handle())
+        wb = 0
+        if max_nx is not None and max_nz is not None:
+            wb = int(L.lib().tw_count_pairs_rng_work_bytes(int(n_shards), int(max_nx),
+                                                           int(max_nz), int(dtype), int(pred)))
+        if wb > 0:
+            work = L.empty((wb,), self.t.uint8)
+            L.call("tw_count_pairs_rng_ws", L.ptr(x), L.ptr(x_off_dev), L.ptr(z),
+                   L.ptr(z_off_dev), int(n_shards), int(max_nx), int(max_nz), int(B), int(seed),
+                   int(shard_base), int(dtype), int(pred), L.ptr(work), wb, L.ptr(out),
+                   L.stream_handle())
+        else:
+            L.call("tw_count_pairs_rng", L.ptr(x), L.ptr(x_off_dev), L.ptr(z), L.ptr(z_off_dev),
+                   int(n_shards), int(B), int(seed), int(shard_base), int(dtype), int(pred),
+                   L.ptr(out), L.stream_handle())
         return out
 
     def to_dev(self, arr):
@@ -354,7 +368,8 @@ class ShardedSample:
 
     def _count_rng(self, B, seed):
         return self.ops.count_rng(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N, B,
-                                  seed, self.rank * self.N, self.dtype, self.pred)
+                                  seed, self.rank * self.N, self.dtype, self.pred,
+                                  max_nx=self.max_nx, max_nz=self.max_nz)
 
     def UnNB(self, B: int, seed: int, key=None) -> np.float64:
         """Block-wise incomplete U-statistic with B device-drawn pairs per shard
