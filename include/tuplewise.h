@@ -206,6 +206,11 @@ int tw_pair_grad_complete(const double* d_X, const double* d_Z, int64_t d,
                           const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
                           int64_t kz, int32_t n_shards, const double* d_w, double margin,
                           int32_t loss, void* d_work, double* d_out, void* stream);
+/* Hinge coefficients are counts; by default they come from binary searches with the exact
+ * floating-point predicate over each shard's sorted scores (S is monotone in each score), the
+ * same integers as the pair-by-pair sums in O(k log k).  on = 0 selects the pair-by-pair
+ * kernel (kept for A/B checks). */
+int tw_pair_grad_complete_set_search(int32_t on);
 
 /* ---- Row L1/A9, device-RNG mode (no host RNG in the loop; graph-capturable) -----------
  * Draws are Philox4x32-10(key = seed, counter = (index, shard, step lo, tag | step hi)) with

@@ -498,6 +498,33 @@ def test_complete_block_gradient(gpu, loss, d, kx, kz):
         np.testing.assert_allclose(g[s], want.ravel(), rtol=1e-10, atol=1e-13)
 
 
+@pytest.mark.parametrize("kx,kz", [(300, 77), (5000, 20000), (4096, 1)])
+def test_complete_hinge_search_equals_pair_sums(gpu, kx, kz):
+    """Hinge coefficients by threshold search == pair-by-pair sums, bit for bit, on
+    integer-valued data where S = 0 exactly for many pairs (the boundary of 1{S > 0}), with
+    NaN and +-inf scores and several sorted chunks / LDS groups."""
+    from tuplewise import _lib as L, _learn
+    rng = np.random.RandomState(kx + kz)
+    N, d = 3, 4
+    X = rng.randint(-5, 6, size=(kx * N, d)).astype(np.float64)
+    Z = rng.randint(-5, 6, size=(kz * N, d)).astype(np.float64)
+    X[1, 0], Z[0, 1], X[2, 2] = np.nan, np.inf, -np.inf  # shard 0 only
+    w = np.array([1.0, -2.0, 0.5, 3.0])
+    args = (L.to_device(X), L.to_device(Z), d, None, kx, None, kz, N, L.to_device(w), 2.0,
+            L.TW_LOSS_HINGE)
+    g_search = _learn.complete_grads_device(*args).cpu().numpy()
+    L.call("tw_pair_grad_complete_set_search", 0)
+    try:
+        g_pairs = _learn.complete_grads_device(*args).cpu().numpy()
+    finally:
+        L.call("tw_pair_grad_complete_set_search", 1)
+    assert np.array_equal(g_search, g_pairs, equal_nan=True)
+    for s in range(1, N):  # finite shards: the oracle's pair-by-pair restatement
+        want = O.grad_complete_block(w.reshape(-1, 1), 2.0, "hinge")(
+            X[s * kx:(s + 1) * kx], Z[s * kz:(s + 1) * kz])
+        np.testing.assert_array_equal(g_search[s], want.ravel())
+
+
 def test_grad_complete_block_drop_in(gpu):
     """compute_stats.grad_complete_block composes with SWR_divide / UN_split like
     grad_inc_block (one launch for all shards), and with ragged user-made shard lists."""

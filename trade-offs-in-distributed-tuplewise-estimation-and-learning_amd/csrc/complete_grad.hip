@@ -13,11 +13,16 @@
 //
 // Kernels (all deterministic: every sum has a fixed order):
 //   k_row_scores     one wave per row: lane-strided partial dot + fixed butterfly
-//   k_pair_coef      thread per point, the other side's scores staged in LDS chunks; the
-//                    point's coefficient is summed in the other side's index order
+//   k_pair_coef      (logistic) thread per point, the other side's scores staged in LDS
+//                    chunks; the point's coefficient is summed in the other side's index order
+//   k_sort_chunks +  (hinge) the coefficients are COUNTS: b_i = #{j : S_ij > 0}, a_j =
+//   k_hinge_coef     #{i : S_ij > 0}.  S = fl(fl(sz - sx) + m) is monotone in each score, so
+//                    over the other side's sorted chunks each count is a binary search with
+//                    the exact floating-point predicate: O(k log k) instead of O(k^2), and the
+//                    same integers as summing 1{S > 0} pair by pair
 //   k_wcolsum_part   thread per column, 256-row chunks of [Z rows (+a) | X rows (-b)] in order
 //   k_wcolsum_final  chunk partials added in chunk order, / (kx kz)
-#include "tw_common.h"
+#include "sortkeys.h"
 #include <algorithm>
 
 namespace tw {
@@ -71,6 +76,75 @@ __global__ __launch_bounds__(kBlock) void k_pair_coef(const double* __restrict__
   if (valid) coef[(int64_t)s * k_own + p] = acc;
 }
 
+// Number of leading entries of the sorted chunk a[0, C) (C a power of two) with pred true, for
+// pred monotone true...true false...false along the chunk.
+template <typename P>
+__device__ __forceinline__ uint32_t prefix_count(const uint64_t* a, int C, P pred) {
+  uint32_t i = 0;
+  for (int st = C >> 1; st > 0; st >>= 1) i += pred(a[i + st - 1]) ? st : 0;
+  return i + (pred(a[i]) ? 1 : 0);
+}
+
+// Hinge coefficients by threshold search.  SIDE 0: own = x-scores, b_i = #{j : (sz_j - v) + m
+// > 0}; SIDE 1: own = z-scores, a_j = #{i : (v - sx_i) + m > 0}; the other side's scores are
+// sorted chunks of order keys (padding / NaN = ~0, never counted).  A NaN own score counts 0.
+constexpr int kHcPer = 4;  // own points per thread
+template <int SIDE>
+__global__ __launch_bounds__(kSortThreads) void k_hinge_coef(const double* __restrict__ s_own,
+                                                             int64_t k_own,
+                                                             const uint64_t* __restrict__ keys_other,
+                                                             int chunks, int C, double margin,
+                                                             int tiles, double* __restrict__ coef) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int s = lb / tiles;
+  const int tile = lb - s * tiles;
+  const double* own = s_own + (int64_t)s * k_own;
+  double v[kHcPer];
+  uint32_t cnt[kHcPer];
+  bool live[kHcPer];
+#pragma unroll
+  for (int r = 0; r < kHcPer; ++r) {
+    const int64_t p = (int64_t)tile * (kSortThreads * kHcPer) + r * kSortThreads + threadIdx.x;
+    live[r] = p < k_own;
+    v[r] = live[r] ? own[p] : 0.0;
+    live[r] = live[r] && v[r] == v[r];
+    cnt[r] = 0;
+  }
+  const int group = (int)std::max<int64_t>(1, kMaxChunk / C);
+  for (int c0 = 0; c0 < chunks; c0 += group) {
+    const int ng = std::min(group, chunks - c0);
+    const uint64_t* src = keys_other + ((int64_t)s * chunks + c0) * C;
+    __syncthreads();
+    for (int i = threadIdx.x; i < ng * C; i += kSortThreads) keys[i] = src[i];
+    __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+      const uint64_t* kc = keys + g * C;
+#pragma unroll
+      for (int r = 0; r < kHcPer; ++r) {
+        if (!live[r]) continue;
+        const double vv = v[r];
+        if (SIDE == 1) {  // true for small sx: (v - sx) + m > 0
+          cnt[r] += prefix_count(kc, C, [=](uint64_t k) {
+            return k != ~0ull && (vv - key_to_double(k)) + margin > 0.0;
+          });
+        } else {  // true for large sz: count = valid - #{leading sz with S <= 0}
+          const uint32_t valid = lower_bound_lds(kc, C, ~0ull);
+          const uint32_t below = prefix_count(kc, C, [=](uint64_t k) {
+            return k != ~0ull && !((key_to_double(k) - vv) + margin > 0.0);
+          });
+          cnt[r] += valid - below;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kHcPer; ++r) {
+    const int64_t p = (int64_t)tile * (kSortThreads * kHcPer) + r * kSortThreads + threadIdx.x;
+    if (p < k_own) coef[(int64_t)s * k_own + p] = (double)cnt[r];
+  }
+}
+
 // partial[s][c][col] = sum over rows r of chunk c (in order) of w_r * row_r[col], rows of shard
 // s being [Z rows j (w = +a_j) | X rows i (w = -b_i)].
 __global__ __launch_bounds__(kBlock) void k_wcolsum_part(
@@ -118,22 +192,67 @@ __global__ __launch_bounds__(kBlock) void k_wcolsum_final(const double* __restri
 }
 
 struct CgLayout {
-  int64_t sx, sz, bx, az, part;  // offsets (doubles) into the workspace
+  int64_t sx, sz, bx, az, part, keys_x, keys_z;  // offsets (8-B words) into the workspace
   int64_t total;
   int chunks;
+  int Cx, chx, Cz, chz;  // sorted-chunk length and count of the x / z scores (hinge)
 };
+
+// sorted chunks of C <= 4096 keys (the sorted-count path's best chunk, rankcount.hip)
+static void score_chunks(int64_t k, int& C, int& ch) {
+  int64_t c = 1024;
+  while (c < k && c < 4096) c <<= 1;
+  C = (int)c;
+  ch = (int)std::max<int64_t>(1, ceil_div(k, c));
+}
 
 static CgLayout cg_layout(int32_t n_shards, int64_t kx, int64_t kz, int64_t d) {
   CgLayout l;
   const int64_t nx = (int64_t)n_shards * kx, nz = (int64_t)n_shards * kz;
   l.chunks = (int)std::max<int64_t>(1, ceil_div(kx + kz, kColRows));
+  score_chunks(kx, l.Cx, l.chx);
+  score_chunks(kz, l.Cz, l.chz);
   l.sx = 0;
   l.sz = l.sx + nx;
   l.bx = l.sz + nz;
   l.az = l.bx + nx;
   l.part = l.az + nz;
-  l.total = l.part + (int64_t)n_shards * l.chunks * d;
+  l.keys_x = l.part + (int64_t)n_shards * l.chunks * d;
+  l.keys_z = l.keys_x + (int64_t)n_shards * l.chx * l.Cx;
+  l.total = l.keys_z + (int64_t)n_shards * l.chz * l.Cz;
   return l;
+}
+
+static int launch_hinge_coef(const double* sx, int64_t kx, const double* sz, int64_t kz,
+                             int32_t n_shards, double margin, const CgLayout& l, double* work,
+                             double* bx, double* az, hipStream_t st) {
+  static bool attrs_set = false;
+  if (!attrs_set) {
+    for (const void* f : {(const void*)k_sort_chunks<double, 4>, (const void*)k_hinge_coef<0>,
+                          (const void*)k_hinge_coef<1>})
+      TW_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(sizeof(uint64_t) * kMaxChunk)));
+    attrs_set = true;
+  }
+  uint64_t* keys_x = (uint64_t*)(work + l.keys_x);
+  uint64_t* keys_z = (uint64_t*)(work + l.keys_z);
+  TW_ARG_CHECK((int64_t)n_shards * std::max(l.chx, l.chz) < (1ll << 31),
+               "tw_pair_grad_complete: grid too large");
+  // C <= 4096 -> E = 4, C / 4 threads per block
+  hipLaunchKernelGGL((k_sort_chunks<double, 4>), dim3(n_shards * l.chx), dim3(l.Cx / 4),
+                     sizeof(uint64_t) * l.Cx, st, sx, nullptr, l.chx, l.Cx, keys_x, kx);
+  hipLaunchKernelGGL((k_sort_chunks<double, 4>), dim3(n_shards * l.chz), dim3(l.Cz / 4),
+                     sizeof(uint64_t) * l.Cz, st, sz, nullptr, l.chz, l.Cz, keys_z, kz);
+  const int tx = (int)ceil_div(kx, (int64_t)kSortThreads * kHcPer);
+  const int tz = (int)ceil_div(kz, (int64_t)kSortThreads * kHcPer);
+  const size_t lds_x = sizeof(uint64_t) * std::min<int64_t>((int64_t)l.chz * l.Cz, kMaxChunk);
+  const size_t lds_z = sizeof(uint64_t) * std::min<int64_t>((int64_t)l.chx * l.Cx, kMaxChunk);
+  hipLaunchKernelGGL((k_hinge_coef<0>), dim3(n_shards * tx), dim3(kSortThreads), lds_x, st, sx,
+                     kx, keys_z, l.chz, l.Cz, margin, tx, bx);
+  hipLaunchKernelGGL((k_hinge_coef<1>), dim3(n_shards * tz), dim3(kSortThreads), lds_z, st, sz,
+                     kz, keys_x, l.chx, l.Cx, margin, tz, az);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
 }
 
 template <int LOSS>
@@ -147,9 +266,17 @@ static void launch_coef(const double* sx, int64_t kx, const double* sz, int64_t 
                      sx, kx, margin, tz, az);
 }
 
+static int g_hinge_by_search = 1;  // tw_pair_grad_complete_set_search: 0 = all-pairs sums
+
 }  // namespace tw
 
 using namespace tw;
+
+extern "C" int tw_pair_grad_complete_set_search(int32_t on) {
+  TW_ARG_CHECK(on == 0 || on == 1, "tw_pair_grad_complete_set_search: 0 or 1");
+  g_hinge_by_search = on;
+  return TW_OK;
+}
 
 extern "C" int64_t tw_pair_grad_complete_work_bytes(int32_t n_shards, int64_t kx, int64_t kz,
                                                     int64_t d) {
@@ -184,7 +311,11 @@ extern "C" int tw_pair_grad_complete(const double* d_X, const double* d_Z, int64
   if (loss == TW_LOSS_LOGISTIC)
     launch_coef<TW_LOSS_LOGISTIC>(work + l.sx, kx, work + l.sz, kz, n_shards, margin,
                                   work + l.bx, work + l.az, st);
-  else
+  else if (g_hinge_by_search) {
+    const int rc = launch_hinge_coef(work + l.sx, kx, work + l.sz, kz, n_shards, margin, l, work,
+                                     work + l.bx, work + l.az, st);
+    if (rc != TW_OK) return rc;
+  } else
     launch_coef<TW_LOSS_HINGE>(work + l.sx, kx, work + l.sz, kz, n_shards, margin, work + l.bx,
                                work + l.az, st);
   const int ctiles = (int)ceil_div(d, kBlock);
