@@ -38,6 +38,24 @@ __global__ __launch_bounds__(kBlock) void k_row_scores(const double* __restrict_
                                                        double* __restrict__ out) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
+  if ((d & 1) == 0) {  // 16-B loads: lane takes column pairs 2j, 2j+1 (rows are 16-B aligned)
+    const int64_t d2 = d >> 1;
+    const double2* __restrict__ w2 = (const double2*)w;
+    for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave; r < total;
+         r += waves) {
+      const double2* __restrict__ a2 = (const double2*)(A + (rows ? rows[r] : r) * d);
+      double p0 = 0.0, p1 = 0.0;
+#pragma unroll 4
+      for (int64_t j = lane; j < d2; j += kWave) {
+        const double2 v = a2[j], ww = w2[j];
+        p0 += v.x * ww.x;
+        p1 += v.y * ww.y;
+      }
+      const double p = wave_sum_f64(p0 + p1);
+      if (lane == 0) out[r] = p;
+    }
+    return;
+  }
   for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave; r < total; r += waves) {
     const double* a = A + (rows ? rows[r] : r) * d;
     double p = 0.0;
@@ -156,9 +174,34 @@ __global__ __launch_bounds__(kBlock) void k_wcolsum_part(
   const int s = blockIdx.x / per;
   const int rem = blockIdx.x - s * per;
   const int c = rem / ctiles;
+  const int64_t r0 = (int64_t)c * kColRows, r1 = std::min<int64_t>(r0 + kColRows, kx + kz);
+  if ((d & 1) == 0) {  // two columns per thread, 16-B loads; each column still in row order
+    const int64_t col2 = (int64_t)(rem - c * ctiles) * kBlock + threadIdx.x;
+    if (2 * col2 >= d) return;
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll 4
+    for (int64_t r = r0; r < r1; ++r) {
+      double wr;
+      const double* rowp;
+      if (r < kz) {
+        wr = a[(int64_t)s * kz + r];
+        rowp = Z + (rows_z ? rows_z[(int64_t)s * kz + r] : (int64_t)s * kz + r) * d;
+      } else {
+        const int64_t i = r - kz;
+        wr = -b[(int64_t)s * kx + i];
+        rowp = X + (rows_x ? rows_x[(int64_t)s * kx + i] : (int64_t)s * kx + i) * d;
+      }
+      const double2 v = ((const double2*)rowp)[col2];
+      acc0 += wr * v.x;
+      acc1 += wr * v.y;
+    }
+    double* dst = partial + ((int64_t)s * chunks + c) * d + 2 * col2;
+    dst[0] = acc0;
+    dst[1] = acc1;
+    return;
+  }
   const int64_t col = (int64_t)(rem - c * ctiles) * kBlock + threadIdx.x;
   if (col >= d) return;
-  const int64_t r0 = (int64_t)c * kColRows, r1 = std::min<int64_t>(r0 + kColRows, kx + kz);
   double acc = 0.0;
   for (int64_t r = r0; r < r1; ++r) {
     double wr, v;
@@ -318,7 +361,7 @@ extern "C" int tw_pair_grad_complete(const double* d_X, const double* d_Z, int64
   } else
     launch_coef<TW_LOSS_HINGE>(work + l.sx, kx, work + l.sz, kz, n_shards, margin, work + l.bx,
                                work + l.az, st);
-  const int ctiles = (int)ceil_div(d, kBlock);
+  const int ctiles = (int)ceil_div((d & 1) == 0 ? d / 2 : d, kBlock);  // column (pair) tiles
   TW_ARG_CHECK((int64_t)n_shards * l.chunks * ctiles < (1ll << 31),
                "tw_pair_grad_complete: grid too large");
   hipLaunchKernelGGL(k_wcolsum_part, dim3(n_shards * l.chunks * ctiles), dim3(kBlock), 0, st,
