@@ -208,8 +208,9 @@ int tw_pair_grad_complete(const double* d_X, const double* d_Z, int64_t d,
                           int32_t loss, void* d_work, double* d_out, void* stream);
 /* Hinge coefficients are counts; by default they come from binary searches with the exact
  * floating-point predicate over each shard's sorted scores (S is monotone in each score), the
- * same integers as the pair-by-pair sums in O(k log k).  on = 0 selects the pair-by-pair
- * kernel (kept for A/B checks). */
+ * same integers as the pair-by-pair sums in O(k log k); logistic coefficients come from one
+ * pass over the pairs (each sigma(S_ij) feeds a_j and b_i).  on = 0 selects the two-pass
+ * pair-by-pair kernels (kept for A/B checks). */
 int tw_pair_grad_complete_set_search(int32_t on);
 
 /* ---- Row L1/A9, device-RNG mode (no host RNG in the loop; graph-capturable) -----------

@@ -411,6 +411,38 @@ def test_count_pairs_step_fused_repartition(gpu, dtype, mode):
     assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 12))
 
 
+def test_device_sigmoid_accuracy(gpu):
+    """The device sigma (tw_common.h pair_weight: 1 / (1 + exp(-S)) with the device exp) within 4 ulp of
+    NumPy's 1 / (1 + exp(-S)) over the whole range, incl. saturation, +-inf and NaN: one
+    shard per S value, d = 1, x = 0, z = c, w = 1, margin 0, B = 1 -> gradient = sigma(c) c."""
+    from tuplewise import _lib as L, _learn
+    c = np.concatenate([np.linspace(-50, 50, 2001), [-745.5, -709.9, -40.0, -1e-300, 1e-300,
+                        36.0, 40.0, 800.0, 1e10, -1e10], np.random.RandomState(3).normal(0, 5, 2000)])
+    c = c[c != 0]
+    N = len(c)
+    X, Z = np.zeros((N, 1)), c.reshape(-1, 1)
+    rows = L.to_device(np.arange(N, dtype=np.int64).reshape(N, 1))
+    idx = L.to_device(np.zeros(N, dtype=np.int64))
+    g = _learn.hinge_grads_device(L.to_device(X), L.to_device(Z), 1, rows, 1, rows, 1, idx, idx,
+                                  N, 1, L.to_device(np.ones(1)), 0.0,
+                                  L.TW_LOSS_LOGISTIC).cpu().numpy().ravel()
+    with np.errstate(over="ignore"):
+        want = (1.0 / (1.0 + np.exp(-c))) * c
+    ulp = np.spacing(np.abs(want))
+    assert np.all(np.abs(g - want) <= 4 * ulp), np.max(np.abs(g - want) / ulp)
+    # inf / NaN scores
+    Xs = np.array([[0.0], [0.0], [0.0]])
+    Zs = np.array([[np.inf], [-np.inf], [np.nan]])
+    r3 = L.to_device(np.arange(3, dtype=np.int64).reshape(3, 1))
+    i3 = L.to_device(np.zeros(3, dtype=np.int64))
+    g3 = _learn.hinge_grads_device(L.to_device(Xs), L.to_device(Zs), 1, r3, 1, r3, 1, i3, i3, 3,
+                                   1, L.to_device(np.ones(1)), 0.0,
+                                   L.TW_LOSS_LOGISTIC).cpu().numpy().ravel()
+    with np.errstate(over="ignore", invalid="ignore"):
+        w3 = (1.0 / (1.0 + np.exp(-Zs.ravel()))) * Zs.ravel()
+    assert np.array_equal(g3, w3, equal_nan=True), (g3, w3)
+
+
 def test_logistic_surrogates_and_block_gradient(gpu):
     """Row L3 extension (parity pinned against the oracle only): conv_AUC / conv_AUC_deter_pairs
     with loss="logistic" and grad_inc_block(..., loss="logistic") inside UN_split."""
@@ -523,6 +555,26 @@ def test_complete_hinge_search_equals_pair_sums(gpu, kx, kz):
         want = O.grad_complete_block(w.reshape(-1, 1), 2.0, "hinge")(
             X[s * kx:(s + 1) * kx], Z[s * kz:(s + 1) * kz])
         np.testing.assert_array_equal(g_search[s], want.ravel())
+
+
+@pytest.mark.parametrize("kx,kz", [(300, 77), (5000, 1300), (1, 9000)])
+def test_complete_logistic_one_pass_equals_two_pass(gpu, kx, kz):
+    """One-pass logistic coefficients (k_logistic_coef + k_apart_final) agree with the two-pass
+    pair-by-pair kernel to summation-order rounding."""
+    from tuplewise import _lib as L, _learn
+    rng = np.random.RandomState(kx * 7 + kz)
+    N, d = 3, 6
+    X, Z = rng.normal(size=(kx * N, d)), rng.normal(0.3, 1, size=(kz * N, d))
+    w = rng.normal(size=d)
+    args = (L.to_device(X), L.to_device(Z), d, None, kx, None, kz, N, L.to_device(w), 0.7,
+            L.TW_LOSS_LOGISTIC)
+    g1 = _learn.complete_grads_device(*args).cpu().numpy()
+    L.call("tw_pair_grad_complete_set_search", 0)
+    try:
+        g2 = _learn.complete_grads_device(*args).cpu().numpy()
+    finally:
+        L.call("tw_pair_grad_complete_set_search", 1)
+    np.testing.assert_allclose(g1, g2, rtol=1e-12, atol=1e-15)
 
 
 def test_grad_complete_block_drop_in(gpu):

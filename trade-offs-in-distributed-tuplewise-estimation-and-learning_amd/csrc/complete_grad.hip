@@ -163,6 +163,87 @@ __global__ __launch_bounds__(kSortThreads) void k_hinge_coef(const double* __res
   }
 }
 
+// Logistic coefficients in ONE pass over the pairs (each sigma(S_ij) is evaluated once and
+// feeds both sums).  A 1024-thread block holds kLgR x-scores per lane (a tile of 1024 kLgR
+// x-points of one shard) and streams the shard's z-scores through LDS in chunks of kLgChunk:
+//   b_i += sigma(S_ij)              per lane, in j order (registers)
+//   a_j  = sum over the tile's x    lane butterfly, then the 16 waves in wave order (LDS),
+// writing one partial of a_j per (tile, j); k_apart_final adds the tiles in tile order.
+// Deterministic; the f64 exp is the cost, so one pass halves the two-pass k_pair_coef.
+constexpr int kLgR = 4;
+constexpr int kLgThreads = 1024;
+constexpr int kLgChunk = 512;
+__global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __restrict__ sx,
+                                                              int64_t kx,
+                                                              const double* __restrict__ sz,
+                                                              int64_t kz, double margin,
+                                                              int tiles,
+                                                              double* __restrict__ bx,
+                                                              double* __restrict__ apart) {
+  __shared__ double zc[kLgChunk];
+  __shared__ double wpart[kLgThreads / kWave][kLgChunk];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int s = lb / tiles;
+  const int tile = lb - s * tiles;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  double v[kLgR], b[kLgR];
+  bool valid[kLgR];
+#pragma unroll
+  for (int r = 0; r < kLgR; ++r) {
+    const int64_t i = (int64_t)tile * (kLgThreads * kLgR) + r * kLgThreads + threadIdx.x;
+    valid[r] = i < kx;
+    v[r] = valid[r] ? sx[(int64_t)s * kx + i] : 0.0;
+    b[r] = 0.0;
+  }
+  const double* zs = sz + (int64_t)s * kz;
+  double* ap = apart + ((int64_t)s * tiles + tile) * kz;
+  for (int64_t c0 = 0; c0 < kz; c0 += kLgChunk) {
+    const int n = (int)std::min<int64_t>(kLgChunk, kz - c0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += kLgThreads) zc[j] = zs[c0 + j];
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+      const double zj = zc[j];
+      double t = 0.0;
+#pragma unroll
+      for (int r = 0; r < kLgR; ++r) {
+        const double S = (zj - v[r]) + margin;
+        const double p = pair_weight<TW_LOSS_LOGISTIC>(S);
+        b[r] += p;
+        t += valid[r] ? p : 0.0;
+      }
+      t = wave_sum_f64(t);
+      if (lane == 0) wpart[wid][j] = t;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += kLgThreads) {
+      double a = 0.0;
+#pragma unroll
+      for (int w = 0; w < kLgThreads / kWave; ++w) a += wpart[w][j];
+      ap[c0 + j] = a;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kLgR; ++r) {
+    const int64_t i = (int64_t)tile * (kLgThreads * kLgR) + r * kLgThreads + threadIdx.x;
+    if (valid[r]) bx[(int64_t)s * kx + i] = b[r];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_apart_final(const double* __restrict__ apart,
+                                                        int n_shards, int tiles, int64_t kz,
+                                                        double* __restrict__ az) {
+  const int64_t total = (int64_t)n_shards * kz;
+  for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * kBlock) {
+    const int64_t s = e / kz, j = e - s * kz;
+    const double* p = apart + (int64_t)s * tiles * kz + j;
+    double a = 0.0;
+    for (int t = 0; t < tiles; ++t) a += p[(int64_t)t * kz];
+    az[e] = a;
+  }
+}
+
 // partial[s][c][col] = sum over rows r of chunk c (in order) of w_r * row_r[col], rows of shard
 // s being [Z rows j (w = +a_j) | X rows i (w = -b_i)].
 __global__ __launch_bounds__(kBlock) void k_wcolsum_part(
@@ -239,6 +320,8 @@ struct CgLayout {
   int64_t total;
   int chunks;
   int Cx, chx, Cz, chz;  // sorted-chunk length and count of the x / z scores (hinge)
+  int64_t apart;         // per-(x tile, z point) partials of a_j (logistic)
+  int lg_tiles;
 };
 
 // sorted chunks of C <= 4096 keys (the sorted-count path's best chunk, rankcount.hip)
@@ -262,7 +345,9 @@ static CgLayout cg_layout(int32_t n_shards, int64_t kx, int64_t kz, int64_t d) {
   l.part = l.az + nz;
   l.keys_x = l.part + (int64_t)n_shards * l.chunks * d;
   l.keys_z = l.keys_x + (int64_t)n_shards * l.chx * l.Cx;
-  l.total = l.keys_z + (int64_t)n_shards * l.chz * l.Cz;
+  l.lg_tiles = (int)ceil_div(kx, (int64_t)kLgThreads * kLgR);
+  l.apart = l.keys_z + (int64_t)n_shards * l.chz * l.Cz;
+  l.total = l.apart + (int64_t)n_shards * l.lg_tiles * kz;
   return l;
 }
 
@@ -310,6 +395,7 @@ static void launch_coef(const double* sx, int64_t kx, const double* sz, int64_t 
 }
 
 static int g_hinge_by_search = 1;  // tw_pair_grad_complete_set_search: 0 = all-pairs sums
+static int g_logistic_one_pass = 1;  // likewise: 0 = the two-pass k_pair_coef
 
 }  // namespace tw
 
@@ -318,6 +404,7 @@ using namespace tw;
 extern "C" int tw_pair_grad_complete_set_search(int32_t on) {
   TW_ARG_CHECK(on == 0 || on == 1, "tw_pair_grad_complete_set_search: 0 or 1");
   g_hinge_by_search = on;
+  g_logistic_one_pass = on;
   return TW_OK;
 }
 
@@ -351,7 +438,16 @@ extern "C" int tw_pair_grad_complete(const double* d_X, const double* d_Z, int64
                      nx, d_w, work + l.sx);
   hipLaunchKernelGGL(k_row_scores, dim3(rs_blocks_z), dim3(kBlock), 0, st, d_Z, d, d_rows_z,
                      nz, d_w, work + l.sz);
-  if (loss == TW_LOSS_LOGISTIC)
+  if (loss == TW_LOSS_LOGISTIC && g_logistic_one_pass) {
+    TW_ARG_CHECK((int64_t)n_shards * l.lg_tiles < (1ll << 31),
+                 "tw_pair_grad_complete: grid too large");
+    hipLaunchKernelGGL(k_logistic_coef, dim3(n_shards * l.lg_tiles), dim3(kLgThreads), 0, st,
+                       work + l.sx, kx, work + l.sz, kz, margin, l.lg_tiles, work + l.bx,
+                       work + l.apart);
+    const int fb = (int)std::min<int64_t>(256 * 8, ceil_div((int64_t)n_shards * kz, kBlock));
+    hipLaunchKernelGGL(k_apart_final, dim3(fb), dim3(kBlock), 0, st, work + l.apart,
+                       (int)n_shards, l.lg_tiles, kz, work + l.az);
+  } else if (loss == TW_LOSS_LOGISTIC)
     launch_coef<TW_LOSS_LOGISTIC>(work + l.sx, kx, work + l.sz, kz, n_shards, margin,
                                   work + l.bx, work + l.az, st);
   else if (g_hinge_by_search) {
