@@ -532,6 +532,8 @@ def main():
             "C5_scaled_d512_B4096": sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1),
             "C5_scaled_d512_complete_gradient": sgd_complete_steps_per_s(C5_N, C5_N, 512,
                                                                           256, 3),
+            "C5_scaled_d512_complete_gradient_logistic": sgd_complete_steps_per_s(
+                C5_N, C5_N, 512, 256, 2, loss="logistic"),
             "C5_scaled_d512_partitioned": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,
                                                           1, layout="partitioned"),
         }
