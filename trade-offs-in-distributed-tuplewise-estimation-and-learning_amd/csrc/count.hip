@@ -86,14 +86,25 @@ __device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
   }
 }
 
+// Wave count of one compare on the scalar unit: v_cmp to an SGPR pair, s_bcnt1; half-ties
+// count the two one-bit masks x > z and x >= z.
+template <typename T, int PRED>
+__device__ __forceinline__ unsigned scalar_count(T x, T z) {
+  if constexpr (PRED == TW_PRED_HALF)
+    return (unsigned)__builtin_popcountll(__ballot(x > z)) +
+           (unsigned)__builtin_popcountll(__ballot(x >= z));
+  else
+    return (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(x, z)));
+}
+
 // One wave item: its 64*R x-values (from x0, valid below xe) against z[z0, z1).  Returns the
 // wave's count (wave-uniform).
 template <typename T, int R, int NS, int PRED>
 __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x, int64_t x0,
                                                          int64_t xe, const T* __restrict__ z,
                                                          int64_t z0, int64_t z1, int lane) {
-  static_assert(NS == 0 || (std::is_floating_point<T>::value && PRED != TW_PRED_HALF),
-                "scalar-unit counting needs NaN padding and a one-bit predicate");
+  static_assert(NS == 0 || std::is_floating_point<T>::value,
+                "scalar-unit counting needs NaN padding");
   T xv[R];
   unsigned acc[R];
   bool valid[R];
@@ -134,7 +145,7 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           if (r < NS) {
-            sacc[r] += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv[u])));
+            sacc[r] += scalar_count<T, PRED>(xv[r], zv[u]);
           } else {
             acc[r] += pair_pred<T, PRED>(xv[r], zv[u]);
           }
@@ -150,7 +161,8 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
 #define TW_SCHED_G NS
 #endif
         constexpr int kG = TW_SCHED_G;  // groups per z
-        constexpr int kV = (2 * R - NS + kG - 1) / kG, kS = (2 * NS + kG - 1) / kG;
+        constexpr int kM = PRED == TW_PRED_HALF ? 2 : 1;  // compares per pair
+        constexpr int kV = (kM * (2 * R - NS) + kG - 1) / kG, kS = (2 * kM * NS + kG - 1) / kG;
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
@@ -164,7 +176,7 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (r < NS)
-          sacc[r] += (unsigned)__builtin_popcountll(__ballot(pair_pred<T, PRED>(xv[r], zv)));
+          sacc[r] += scalar_count<T, PRED>(xv[r], zv);
         else
           acc[r] += pair_pred<T, PRED>(xv[r], zv);
       }
@@ -425,7 +437,7 @@ int launch_complete(const void* x, const int64_t* x_off, const void* z, const in
                     int32_t n_shards, int64_t max_nx, int64_t max_nz, uint64_t* out,
                     const NextStep& nxt, hipStream_t st) {
   // scalar-unit counting for the one-bit predicate on doubles (NaN padding)
-  constexpr bool kMixable = std::is_floating_point<T>::value && PRED != TW_PRED_HALF;
+  constexpr bool kMixable = std::is_floating_point<T>::value;
   const bool mix = kMixable && g_scalar_mix;
   const CompletePlan p = plan_complete(max_nx, max_nz, n_shards, mix);
   TW_ARG_CHECK((p.blocks + nxt.blocks) * (kBlock / kWave) < (1ll << 31),
@@ -590,7 +602,7 @@ extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, cons
     // spread over the grid by default: one group of 8 every `every` blocks
     const CompletePlan p = plan_complete(std::max<int64_t>(max_nx, 1),
                                          std::max<int64_t>(max_nz, 1), std::max(n_shards, 1),
-                                         dtype == TW_F64 && pred != TW_PRED_HALF &&
+                                         dtype == TW_F64 &&
                                              g_scalar_mix);
     const int ng = nxt.blocks / kXcds;
     nxt.every = g_step_every ? g_step_every
