@@ -15,7 +15,8 @@
 //   * per pair: one v_cmp (VCC) + one carry-add into a per-(lane, r) u32 counter
 //     (the compiler folds two compares into v_cndmask + v_addc); u32 cannot overflow because a
 //     counter sees at most 2 * z_chunk increments;
-//   * epilogue: valid counters -> u64 -> wave butterfly (DPP) -> one u64 atomic per wave.
+//   * epilogue: valid counters -> u64 -> wave butterfly (DPP) -> block sum per shard (LDS) ->
+//     one u64 atomic per block and shard.
 //   Measured on MI355X (tools/mb_issue*.hip): v_cmp_*_f64 and v_addc issue at ~0.94
 //   wave-instructions/cycle/CU, so 2 such instructions per pair cap this kernel at ~1.9e13
 //   pairs/s; see DESIGN.md "count kernel roofline".
