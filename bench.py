@@ -116,6 +116,34 @@ def sgd_complete_steps_per_s(n_X, n_Z, d, N, steps, loss="hinge"):
                        "steps": steps}}
 
 
+def plumbing_C1(with_cpu, reps=200):
+    """est.UnNT(X, Z, N=10, T=4, "prop-SWOR") at n = 1000/class (BASELINE configs[0]) through
+    the drop-in API on host arrays: latency per call, and the CPU restatement beside it."""
+    import tuplewise.estimation as est
+    rng = np.random.RandomState(0)
+    X, Z = rng.normal(0.5, 1, 1000), rng.normal(0, 1, 1000)
+    np.random.seed(1)
+    for _ in range(5):
+        est.UnNT(X, Z, 10, 4, "prop-SWOR")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        v = est.UnNT(X, Z, 10, 4, "prop-SWOR")
+    dt = (time.perf_counter() - t0) / reps
+    out = {"note": "BASELINE configs[0]: est.UnNT on host arrays (drop-in), n=1000/class, "
+                   "N=10, T=4, prop-SWOR; host shuffles (reference RNG order) + one device launch "
+                   "for the T repetitions",
+           "ms_per_call": dt * 1e3, "pairs_per_call": 4 * 10 * 100 * 100, "last_value": v}
+    if with_cpu:
+        sys.path.insert(0, str(ROOT))
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.est_UnNT(X, Z, 10, 4, "prop-SWOR")
+        out["cpu_ms_per_call"] = (time.perf_counter() - t0) / reps * 1e3
+        out["cpu_kind"] = "port (oracle est_UnNT, NumPy, 1 core)"
+    return out
+
+
 def cpu_baseline_incomplete(n, N, B, shards):
     """The reference's UnNB(kernel="AUC") restated (oracle.UB per block: two randint draws and
     a fancy-indexed compare, compute_stats.py:37-42), single-threaded, on `shards` of the N
@@ -457,6 +485,11 @@ def main():
                            "frac": n1 * n1 / (kms1 * 1e-3) / PEAK_LANE_OPS, "kernel_ms": kms1}}
     del S1, X1, Z1
 
+    # BASELINE.json configs[0] (C1, plumbing): estimation-experiment/main.py's UnNT on host
+    # arrays through the drop-in API (host shuffles as the reference, one device launch per
+    # UN), n = 1000/class, N = 10, T = 4; the reference restated on the CPU beside it
+    c1 = plumbing_C1(rank == 0 and world == 1 and not args.no_cpu_baseline)
+
     traffic, traffic_plain = pmc_traffic()
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
@@ -493,6 +526,7 @@ def main():
                              "committed rocprofv3 --pmc summary: the timed launch, and a plain "
                              "count launch (algorithmic: 16 MB of scores)"},
         "estimate_last_step": float(est),
+        "plumbing_C1": c1,
         "single_shard_C2": single,
         "sorted_count": {
             "note": "same UnN steps with the exact sort+binary-search count (algo='sorted', "
