@@ -486,8 +486,8 @@ def main():
     del S1, X1, Z1
 
     # BASELINE.json configs[0] (C1, plumbing): estimation-experiment/main.py's UnNT on host
-    # arrays through the drop-in API (host shuffles as the reference, one device launch per
-    # UN), n = 1000/class, N = 10, T = 4; the reference restated on the CPU beside it
+    # arrays through the drop-in API (host shuffles as the reference, one device launch for
+    # the T repetitions), n = 1000/class, N = 10, T = 4; the reference restated on the CPU
     c1 = plumbing_C1(rank == 0 and world == 1 and not args.no_cpu_baseline)
 
     traffic, traffic_plain = pmc_traffic()
