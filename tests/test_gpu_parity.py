@@ -644,3 +644,40 @@ def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name):
         a, b = xs[s][i], zs[s][j]
         want = int(np.sum(a > b)) + (int(np.sum(a >= b)) if pred_name == "half" else 0)
         assert ranked[s] == want, s
+
+
+@pytest.mark.parametrize("kind", ["est_UnNT", "cs_UnNT_prod", "cs_UnNT_gini_SWR", "cs_UnNBT_AUC",
+                                  "cs_UnNBT_prod_propSWR"])
+def test_repeated_un_one_launch_equals_loop(gpu, kind):
+    """UnNT / UnNBT count their T repetitions in one launch (_blocks.run_un_repeated): same
+    value, same in-place shuffles and same RNG stream as T separate UN calls."""
+    import tuplewise.compute_stats as cs
+    import tuplewise.estimation as est
+    rng = np.random.RandomState(4)
+    X0, Z0 = rng.normal(0.3, 1, 700), rng.normal(0, 1, 500)
+    f, loop = {
+        "est_UnNT": (lambda X, Z: est.UnNT(X, Z, 7, 3, "SWOR"),
+                     lambda X, Z: np.mean([est.UnN(X, Z, 7, "SWOR") for _ in range(3)])),
+        "cs_UnNT_prod": (lambda X, Z: cs.UnNT(X, Z, 7, 3, "prop-SWOR", kernel="prod"),
+                         lambda X, Z: np.mean([cs.UnN(X, Z, 7, "prop-SWOR", kernel="prod")
+                                               for _ in range(3)])),
+        "cs_UnNT_gini_SWR": (lambda X, Z: cs.UnNT(X, Z, 5, 2, "prop-SWR", kernel="gini"),
+                             lambda X, Z: np.mean([cs.UnN(X, Z, 5, "prop-SWR", kernel="gini")
+                                                   for _ in range(2)])),
+        "cs_UnNBT_AUC": (lambda X, Z: cs.UnNBT(X, Z, 6, 150, 4, "SWOR", kernel="AUC"),
+                         lambda X, Z: np.mean([cs.UnNB(X, Z, 6, 150, "SWOR", kernel="AUC")
+                                               for _ in range(4)])),
+        "cs_UnNBT_prod_propSWR": (
+            lambda X, Z: cs.UnNBT(X, Z, 6, 90, 3, "prop-SWR", kernel="prod"),
+            lambda X, Z: np.mean([cs.UnNB(X, Z, 6, 90, "prop-SWR", kernel="prod")
+                                  for _ in range(3)])),
+    }[kind]
+    X1, Z1, X2, Z2 = X0.copy(), Z0.copy(), X0.copy(), Z0.copy()
+    np.random.seed(9)
+    a = f(X1, Z1)
+    s1 = np.random.randint(0, 2**31)
+    np.random.seed(9)
+    b = loop(X2, Z2)
+    s2 = np.random.randint(0, 2**31)
+    assert a == b and s1 == s2
+    assert np.array_equal(X1, X2) and np.array_equal(Z1, Z2)

@@ -271,6 +271,26 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
     return finish_un(plan, spec.evaluate(X, Z, blocks) if blocks else [])
 
 
+def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
+    """np.mean([UN(X, Z, N, f_block, sampling_type) for _ in range(T)]) (UnNT, UnNBT) with
+    the T host halves (in-place shuffles, every RNG draw) in the reference's order and all
+    T x N blocks counted in ONE launch on snapshots of the shuffled samples.  Scores must be
+    1-D or (n, 1) (evaluate_many); returns None otherwise (the caller loops)."""
+    if not (isinstance(X, np.ndarray) and isinstance(Z, np.ndarray)):
+        return None  # the in-place shuffles must act on the caller's own objects
+    if any(a.ndim > 2 or (a.ndim == 2 and a.shape[1] != 1) for a in (X, Z)):
+        return None
+    plans, jobs = [], []
+    for t in range(T):
+        plan = plan_un(X, Z, N, spec, sampling_type, variant)
+        last = t + 1 == T
+        jobs.append((X if last else X.copy(), Z if last else Z.copy(),
+                     [p[1] for p in plan if p[0] == "val"]))
+        plans.append(plan)
+    vals = evaluate_many(spec, jobs) if jobs else []
+    return np.mean([finish_un(p, v) for p, v in zip(plans, vals)])
+
+
 def evaluate_many(spec, jobs) -> list:
     """Block values of several independent (X, Z, blocks) jobs of one spec in ONE launch:
     the jobs' score vectors are concatenated and their blocks shifted.  Scores must be 1-D

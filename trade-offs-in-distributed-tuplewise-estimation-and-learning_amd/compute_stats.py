@@ -127,13 +127,27 @@ def UnNB(X, Z, N, B, sampling_type, kernel="prod"):
 
 
 def UnNT(X, Z, N, T, sampling_type, kernel="prod"):
-    """Computes reshuffled block-wise complete U-statistic.  (compute_stats.py:113-116)"""
+    """Computes reshuffled block-wise complete U-statistic.  (compute_stats.py:113-116)
+    The T repetitions' blocks are counted in one launch (_blocks.run_un_repeated)."""
+    assert kernel in _KERNELS
+    if kernel == "AUC":
+        spec = Bk.CompleteCount(literal_sub=True)
+    else:
+        spec = Bk.CompleteSum(L.TW_KERN_PROD if kernel == "prod" else L.TW_KERN_GINI)
+    v = Bk.run_un_repeated(X, Z, N, spec, sampling_type, "cs", T)
+    if v is not None:
+        return v
     return np.mean([UnN(X, Z, N, sampling_type=sampling_type, kernel=kernel)
                     for _ in range(T)])
 
 
 def UnNBT(X, Z, N, B, T, sampling_type, kernel="prod"):
-    """Computes reshuffled block-wise incomplete U-statistic.  (compute_stats.py:119-123)"""
+    """Computes reshuffled block-wise incomplete U-statistic.  (compute_stats.py:119-123)
+    The T repetitions' blocks are counted in one launch (_blocks.run_un_repeated)."""
+    assert kernel in _KERNELS
+    v = Bk.run_un_repeated(X, Z, N, Bk.Incomplete(B, kernel), sampling_type, "cs", T)
+    if v is not None:
+        return v
     return np.mean([UnNB(X, Z, N, B, sampling_type=sampling_type, kernel=kernel)
                     for _ in range(T)])
 

@@ -87,18 +87,12 @@ def UnNT(X, Z, N, T, sampling_type, tie_mode="strict"):
     The T repetitions' host halves (in-place shuffles, every RNG draw) run in the reference's
     order; their blocks are counted in ONE device launch (snapshots of the shuffled samples),
     so a small UnNT costs one round trip instead of T."""
-    X = np.asarray(X)
-    Z = np.asarray(Z)
     spec = (_UN_HALF if tie_mode == "half" else _UN_STRICT)._tw_block
-    plans, jobs = [], []
-    for t in range(T):
-        plan = Bk.plan_un(X, Z, N, spec, sampling_type, "est")
-        blocks = [p[1] for p in plan if p[0] == "val"]
-        last = t + 1 == T
-        jobs.append((X if last else X.copy(), Z if last else Z.copy(), blocks))
-        plans.append(plan)
-    vals = Bk.evaluate_many(spec, jobs) if jobs else []
-    return np.mean([Bk.finish_un(plan, v) for plan, v in zip(plans, vals)])
+    v = Bk.run_un_repeated(X, Z, N, spec, sampling_type, "est", T)
+    if v is not None:
+        return v
+    return np.mean([UnN(X, Z, N, sampling_type=sampling_type, tie_mode=tie_mode)
+                    for _ in range(T)])
 
 
 def replicate(estimator, gen_X, gen_Z, n_tries, *args, flush_elems=1 << 24, **kwargs):
