@@ -1,0 +1,16 @@
+"""C4 SGD steps/s (bench.sgd_steps_per_s, sgd_replay_steps_per_s) on their own (GPU box)."""
+import json
+import pathlib
+import sys
+
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+torch.cuda.set_device(0)
+for _ in range(2):
+    a = bench.sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2)
+    b = bench.sgd_replay_steps_per_s(2000)
+    print(json.dumps({"device_steps_per_s": a["steps_per_s"],
+                      "replay_steps_per_s": b["steps_per_s"]}), flush=True)
