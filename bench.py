@@ -45,10 +45,47 @@ HBM_PEAK_GBS = 8000.0
 INC_LANE_OPS = 53  # algorithmic lane-ops per device-RNG incomplete pair
 
 
+class EventPool:
+    """Pre-created timing events; wrap(fn) records a pair around every `stride`-th call (until
+    the pool runs out); used() lists the pairs recorded since the last clear(stride).  Timing
+    every launch is not needed for the mean, so a timed region samples about 20 launches
+    spread over it (the events are made before any timed region)."""
+
+    def __init__(self, torch, n):
+        self._ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in range(n)]
+        self._i = 0
+        self._calls = 0
+        self._stride = 1
+
+    def clear(self, stride=1):
+        self._i = 0
+        self._calls = 0
+        self._stride = max(1, int(stride))
+
+    def used(self):
+        return self._ev[:self._i]
+
+    def wrap(self, fn):
+        def timed(*a, **kw):
+            c = self._calls
+            self._calls += 1
+            if self._i >= len(self._ev) or c % self._stride:
+                return fn(*a, **kw)
+            e0, e1 = self._ev[self._i]
+            self._i += 1
+            e0.record()
+            out = fn(*a, **kw)
+            e1.record()
+            return out
+        timed.__wrapped__ = fn
+        return timed
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=N_PER_CLASS)
     ap.add_argument("--shards", type=int, default=N_SHARDS)
@@ -325,33 +362,14 @@ def main():
     k = n // args.shards
     pairs_per_step_rank = args.shards * k * k
 
-    # live kernel timing: events on the stream the C ABI launches on (torch's current stream)
+    # live kernel timing: HIP events on the stream the C ABI launches on (torch's current
+    # stream), created before the timed regions (creating them inside the loop stalled the
+    # launch queue: 0.75 ms/step at K = 100 against 0.67 with a pre-made pool)
+    kernel_ms = EventPool(torch, 64)
+    sample = max(1, args.steps // 20)  # launches per timed event pair
     ops = S.ops
-    kernel_ms = []
-    orig_count = ops.count
-
-    def timed_count(*a, **kw):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        out = orig_count(*a, **kw)
-        e1.record()
-        kernel_ms.append((e0, e1))
-        return out
-
-    ops.count = timed_count
-    orig_step = ops.count_step
-
-    def timed_step(*a, **kw):  # the one-launch step: count + next repartition on spare blocks
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        out = orig_step(*a, **kw)
-        e1.record()
-        kernel_ms.append((e0, e1))
-        return out
-
-    ops.count_step = timed_step
+    ops.count = kernel_ms.wrap(ops.count)
+    ops.count_step = kernel_ms.wrap(ops.count_step)  # count + next repartition on spare blocks
 
     def barrier():
         if group is not None:
@@ -362,6 +380,9 @@ def main():
 
     # settle: untimed steps for >= settle_ms so the timed steps run at the steady-state clock
     # (the chip raises its clock over the first ~10 ms of load; measured 3 % on this step)
+    # one untimed run at the timed run's length first: the first K-step UnN_many of a process
+    # ran ~7 % slower than the later ones at K = 100 (tools/bench_bisect.py)
+    S.UnN_many(range(40_000, 40_000 + args.steps))
     t_s = time.perf_counter()
     while True:
         S.UnN_many(range(20_000, 20_005))
@@ -376,7 +397,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    kernel_ms.clear()
+    kernel_ms.clear(sample)
     t0 = time.perf_counter()
     # K UnN steps (est.UnNT's loop): repartition i+1 overlaps the counts of step i
     ests = S.UnN_many(range(args.warmup, args.warmup + args.steps))
@@ -389,7 +410,7 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()] or [float("nan")]))
 
     # same workload, exact sort + binary-search count (csrc/rankcount.hip): logical pairs/s
     same_counts = bool(torch.equal(S.local_counts(), (setattr(S, "algo", "sorted"),
@@ -398,7 +419,7 @@ def main():
     S.UnN_many(range(10_000, 10_000 + args.warmup))
     torch.cuda.synchronize()
     barrier()
-    kernel_ms.clear()
+    kernel_ms.clear(sample)
     t1 = time.perf_counter()
     # same keys as the timed all-pairs steps
     est_sorted = S.UnN_many(range(args.warmup, args.warmup + args.steps))[-1]
@@ -409,28 +430,17 @@ def main():
         tt = torch.tensor([dt_sorted], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt_sorted = float(tt.item())
-    kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
     S.algo = "pairs"
 
     # incomplete U-statistic (BASELINE config C3: B pairs per shard + a repartition per step;
     # cs.UnNBT's loop, device-RNG draws): pairs/s and the k_count_rng roofline
-    orig_rng = ops.count_rng
-
-    def timed_rng(*a, **kw):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        out = orig_rng(*a, **kw)
-        e1.record()
-        kernel_ms.append((e0, e1))
-        return out
-
-    ops.count_rng = timed_rng
+    ops.count_rng = kernel_ms.wrap(ops.count_rng)
     B_inc = args.incomplete_B
     S.UnNB_many(B_inc, 5, range(30_000, 30_000 + args.warmup))
     torch.cuda.synchronize()
     barrier()
-    kernel_ms.clear()
+    kernel_ms.clear(sample)
     t2 = time.perf_counter()
     est_inc = S.UnNB_many(B_inc, 1234, range(args.warmup, args.warmup + args.steps))[-1]
     torch.cuda.synchronize()
@@ -440,8 +450,8 @@ def main():
         tt = torch.tensor([dt_inc], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt_inc = float(tt.item())
-    kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
-    ops.count_rng = orig_rng
+    kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
+    ops.count_rng = ops.count_rng.__wrapped__
     inc_pairs_rank = args.shards * B_inc
 
     # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
@@ -451,18 +461,7 @@ def main():
     X1 = torch.randn(n1, dtype=torch.float64, device="cuda", generator=g1) + 0.5
     Z1 = torch.randn(n1, dtype=torch.float64, device="cuda", generator=g1)
     S1 = ShardedSample(X1, Z1, 1, algo="pairs")
-    orig_count1 = S1.ops.count
-
-    def timed_count1(*a, **kw):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        out = orig_count1(*a, **kw)
-        e1.record()
-        kernel_ms.append((e0, e1))
-        return out
-
-    S1.ops.count = timed_count1
+    S1.ops.count = kernel_ms.wrap(S1.ops.count)
     for _ in range(3):
         S1.local_counts()
     torch.cuda.synchronize()
@@ -473,7 +472,7 @@ def main():
         c1 = S1.local_counts()
     torch.cuda.synchronize()
     dt1 = time.perf_counter() - t3
-    kms1 = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    kms1 = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
     c1 = int(c1.sum())
     single = {"note": "BASELINE configs[1]: est.Un complete AUC, n=1e5/class, one shard "
                       "(1e10 pairs per launch), inputs resident, per-rank",
