@@ -124,6 +124,19 @@ def cpu_baseline(n, N, shards):
                       f"{k}x{k}, NumPy broadcast compare), n={n}/class, {dt:.2f} s"}
 
 
+def cpu_baseline_all_cores(n, N, workers):
+    """The same est.UnN with its blocks spread over `workers` CPU processes (SURVEY.md §8(d)
+    all-cores figure), run by a fresh Python process that never touches the GPU."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "oracle.parallel_baseline", str(n), str(N),
+                        str(workers)], cwd=str(ROOT), env=env, capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def sgd_complete_steps_per_s(n_X, n_Z, d, N, steps, loss="hinge"):
     """SGD steps with the complete-block gradient (extension; north_star item (2)): every step
     takes ALL pairs of every shard through per-point pair coefficients + X^T c
@@ -316,16 +329,18 @@ def pmc_traffic():
     """HBM bytes per launch of the count kernel from the committed rocprofv3 --pmc summary of
     this workload (profiles/*count_pmc*.json, FETCH_SIZE + WRITE_SIZE): the timed one-launch
     step (count + next repartition) and, when present, a plain count launch."""
-    cands = sorted(ROOT.glob("profiles/*count_pmc*.json"))
+    import re
+    # newest round/session first: natural order of the numbers in the name (r01s27 > r01s5)
+    cands = sorted(ROOT.glob("profiles/*count_pmc*.json"),
+                   key=lambda p: [int(v) for v in re.findall(r"\d+", p.name)])
     if not cands:
         return None, None
     try:
         d = json.loads(cands[-1].read_text())
     except Exception:
         return None, None
-    plain = [e.get("hbm_bytes_per_launch") for g, e in d.get("by_grid", {}).items()
-             if g != d.get("timed_grid")]
-    return d.get("hbm_bytes_per_launch"), (plain[0] if plain else None)
+    plain = d.get("by_grid", {}).get(d.get("plain_grid") or "", {}).get("hbm_bytes_per_launch")
+    return d.get("hbm_bytes_per_launch"), plain
 
 
 def main():
@@ -572,6 +587,9 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
+        # the box's CPU share is 16 cores per GPU (os.cpu_count() shows the whole machine)
+        out["cpu_baseline"]["all_cores"] = cpu_baseline_all_cores(
+            n, args.shards, min(16, len(os.sched_getaffinity(0))))
         out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, args.shards, B_inc,
                                                                     args.cpu_inc_shards)
     if rank == 0:

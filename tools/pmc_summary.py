@@ -34,9 +34,13 @@ for c, grids in per.items():
 for g, e in res["by_grid"].items():
     if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
         e["hbm_bytes_per_launch"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
-# the grid with the most dispatches is the one the timed bench steps launch
-main = max(res["by_grid"], key=lambda g: res["by_grid"][g].get("FETCH_SIZE_dispatches", 0))
+# the largest grid is the timed one-launch step (count blocks + the next repartition's spare
+# blocks); the next largest is a plain count launch of the same shards (other, smaller grids
+# come from the bench's other lines, e.g. the C1/C2 launches)
+grids = sorted((g for g in res["by_grid"] if g.isdigit()), key=int, reverse=True)
+main = grids[0] if grids else next(iter(res["by_grid"]))
 res["timed_grid"] = main
+res["plain_grid"] = grids[1] if len(grids) > 1 else None
 res["hbm_bytes_per_launch"] = res["by_grid"][main].get("hbm_bytes_per_launch")
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
