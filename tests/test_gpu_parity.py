@@ -157,6 +157,24 @@ def test_count_c2_single_shard_1e5(gpu, algo):
     assert got == O.count_gt_sorted(X, Z)
 
 
+@pytest.mark.parametrize("algo", ["pairs", "sorted"])
+def test_count_c2_half_ties_1e5(gpu, algo):
+    """C2 size with heavy ties (1000 distinct values): half-unit counts 2#{x>z} + #{x==z}
+    (the mixed VALU/SALU kernel counts both masks) vs an O(n log n) restatement."""
+    from tuplewise import _engine as E, _lib as L
+    rng = np.random.RandomState(3)
+    X = rng.randint(0, 1000, 100_000).astype(np.float64)
+    Z = rng.randint(0, 1000, 100_000).astype(np.float64)
+    X[:7] = -0.0
+    Z[:5] = 0.0
+    sh = E.Shards.from_blocks([X], [Z], L.TW_F64)
+    got = int(E.count_complete(sh, "half", algo=algo)[0])
+    zs = np.sort(Z)
+    gt = int(np.searchsorted(zs, X, side="left").sum())
+    ge = int(np.searchsorted(zs, X, side="right").sum())
+    assert got == gt + ge
+
+
 def test_device_sharded_sample_matches_oracle(gpu):
     """Device repartition (Feistel) + one-launch count == oracle restatement, per shard."""
     import torch
