@@ -149,6 +149,9 @@ int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,
  * d_work == NULL) this call runs tw_count_pairs_rng. */
 int64_t tw_count_pairs_rng_work_bytes(int32_t n_shards, int64_t max_nx, int64_t max_nz,
                                       int32_t dtype, int32_t pred);
+/* Rank codes of tw_count_pairs_rng_ws: 1 (default) = value buckets in LDS when every shard has
+ * nz <= 16384, 0 = always sort + binary search (A/B and tests; same codes). */
+int tw_count_rng_set_codes(int32_t by_bucket);
 int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, int64_t B, uint64_t seed, uint64_t shard_base,

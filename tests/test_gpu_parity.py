@@ -622,14 +622,17 @@ def test_grad_complete_block_drop_in(gpu):
 
 @pytest.mark.parametrize("dtype_name", ["f64", "i64"])
 @pytest.mark.parametrize("pred_name", ["gt", "half"])
-def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name):
+@pytest.mark.parametrize("zmax,codes", [(20000, "sort"), (16384, "bucket"), (16384, "sort")])
+def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name, zmax, codes):
     """tw_count_pairs_rng_ws (rank codes in LDS) == tw_count_pairs_rng (score gathers) ==
-    oracle, on tie-heavy shards with NaN, -0.0/+0.0 and ragged sizes (incl. an empty one)."""
+    oracle, on tie-heavy shards with NaN, -0.0/+0.0, +-inf and ragged sizes (incl. an empty
+    one); rank codes by bucketing (nz <= 16384) and by sort + search (20000: 2 LDS groups)."""
     import torch
     from tuplewise import _lib as L
     from tuplewise.device import HipOps
     rng = np.random.RandomState(21)
-    nxs, nzs = [1000, 1, 0, 4097, 3000], [700, 5, 9, 20000, 1]  # 20000: 2 LDS groups
+    nxs, nzs = [1000, 1, 0, 4097, 3000, 500], [700, 5, 9, zmax, 1, 600]
+    L.call("tw_count_rng_set_codes", 1 if codes == "bucket" else 0)
     if dtype_name == "f64":
         xs = [rng.randint(-20, 20, n).astype(np.float64) for n in nxs]
         zs = [rng.randint(-20, 20, n).astype(np.float64) for n in nzs]
@@ -637,6 +640,8 @@ def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name):
         zs[0][:30] = np.nan
         xs[3][:100] = -0.0
         zs[3][:100] = 0.0
+        xs[4][:3], zs[0][30:33] = [np.inf, -np.inf, 1e300], [np.inf, -np.inf, -1e300]
+        xs[5][:], zs[5][:] = 7.0, 7.0  # a degenerate shard: every score equal
         dt = L.TW_F64
     else:
         xs = [rng.randint(-30, 30, n).astype(np.int64) for n in nxs]
@@ -651,7 +656,10 @@ def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name):
     B, seed, base = 12_345, 0xC0FFEE, 17
     args = (dev(X), dev(xo), dev(Z), dev(zo), len(nxs), B, seed, base, dt, pred)
     assert L.lib().tw_count_pairs_rng_work_bytes(len(nxs), max(nxs), max(nzs), dt, pred) > 0
-    ranked = ops.count_rng(*args, max_nx=max(nxs), max_nz=max(nzs)).cpu().numpy()
+    try:
+        ranked = ops.count_rng(*args, max_nx=max(nxs), max_nz=max(nzs)).cpu().numpy()
+    finally:
+        L.call("tw_count_rng_set_codes", 1)
     plain = ops.count_rng(*args).cpu().numpy()
     assert np.array_equal(ranked, plain)
     for s in range(len(nxs)):

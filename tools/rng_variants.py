@@ -27,8 +27,11 @@ S.repartition(1)
 import os  # noqa: E402
 
 caps = [int(c) for c in os.environ.get("CAPS", "4096").split(",")]
-for ranked, cap in [(True, c) for c in caps] + [(False, 4096)]:
+# (ranked, chunk cap, codes by bucket)
+for ranked, cap, bucket in ([(True, c, 0) for c in caps] + [(True, 4096, 1)] +
+                            [(False, 4096, 1)]):
     L.call("tw_count_sorted_set_chunk", cap)
+    L.call("tw_count_rng_set_codes", bucket)
     kw = dict(max_nx=S.max_nx, max_nz=S.max_nz) if ranked else {}
     f = lambda i: S.ops.count_rng(S.X, S.x_off_dev, S.Z, S.z_off_dev, N, B, i, 0, S.dtype,
                                   S.pred, **kw)
@@ -42,6 +45,7 @@ for ranked, cap in [(True, c) for c in caps] + [(False, 4096)]:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
-    print(f"{tag:10s} {'ranked' if ranked else 'plain ':6s} cap={cap:5d} {ms:.4f} ms  "
+    print(f"{tag:10s} {'ranked' if ranked else 'plain ':6s} cap={cap:5d} bucket={bucket} "
+          f"{ms:.4f} ms  "
           f"{N * B / ms / 1e-3:.3e} pairs/s  sum={int(c.sum())}", flush=True)
 L.call("tw_count_sorted_set_chunk", 4096)

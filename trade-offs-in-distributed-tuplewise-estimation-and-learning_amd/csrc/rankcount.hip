@@ -227,6 +227,140 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes(
   }
 }
 
+// Rank codes without a sort (shards with nz <= kBucketMaxZ): the block loads the shard's z
+// into LDS, buckets it by VALUE — b(v) = clamp(int((v - zmin) * NB / (zmax - zmin)), 0, NB-1)
+// over the finite z, a monotone map (every IEEE step in it is monotone), so bucket order is
+// value order — with an LDS histogram, prefix sum and scatter, and then a code is
+//   (#z in lower buckets) + (#z in its own bucket below / at most v)
+// by a scan of one bucket (~nz / NB values for smooth data).  Exact for any data: ties share
+// a bucket; NaN z sit in no bucket (their p is the count of non-NaN z, above every x code),
+// NaN x get code 0, +-inf clamp to the end buckets; degenerate or very skewed data only make
+// the scans longer.  Every block of a shard rebuilds the buckets (O(nz) LDS work) and codes
+// its share of the shard's x and z.  Replaces k_sort_chunks + k_rank_codes (41 + 78 us at
+// the bench shape).
+constexpr int kBucketNB = 2048;
+constexpr int64_t kBucketMaxZ = 16384;  // 128 KiB of z in LDS
+constexpr int kBucketParts = 4;
+
+template <typename T>
+__device__ __forceinline__ double bucket_value(T v) { return (double)v; }
+
+template <typename T, int PRED>
+__global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, int parts, int64_t max_nx, int64_t max_nz,
+    uint16_t* __restrict__ cx, uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* zb = (T*)smem;                                       // z by bucket (kBucketMaxZ)
+  unsigned* start = (unsigned*)(smem + sizeof(T) * kBucketMaxZ);  // NB + 1 bucket starts
+  unsigned* cur = start + kBucketNB + 1;                  // NB fill cursors / counts
+  __shared__ double red_min[kSortThreads / kWave], red_max[kSortThreads / kWave];
+  __shared__ unsigned nan_z;
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int s = lb / parts;
+  const int part = lb - s * parts;
+  const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
+  const int64_t zo = z_off[s], nz = z_off[s + 1] - zo;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  // 1. range of the finite z
+  double mn = __builtin_inf(), mx = -__builtin_inf();
+  for (int64_t j = tid; j < nz; j += kSortThreads) {
+    const double v = bucket_value<T>(z[zo + j]);
+    if (v - v == 0.0) {  // finite (not NaN, not inf)
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double a = __shfl_xor(mn, o, kWave), b = __shfl_xor(mx, o, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = 0;
+  if (tid == 0) nan_z = 0;
+  if (lane == 0) {
+    red_min[wid] = mn;
+    red_max[wid] = mx;
+  }
+  __syncthreads();
+  mn = red_min[0];
+  mx = red_max[0];
+  for (int w = 1; w < kSortThreads / kWave; ++w) {
+    mn = red_min[w] < mn ? red_min[w] : mn;
+    mx = red_max[w] > mx ? red_max[w] : mx;
+  }
+  const double scale = mx > mn ? (double)kBucketNB / (mx - mn) : 0.0;
+  auto bucket = [&](double v) -> int {
+    const double t = (v - mn) * scale;  // NaN when v == mn and scale == inf: bucket 0
+    return (int)__builtin_fmin(__builtin_fmax(t, 0.0), (double)(kBucketNB - 1));
+  };
+  // 2. histogram (NaN z counted apart)
+  for (int64_t j = tid; j < nz; j += kSortThreads) {
+    const T v = z[zo + j];
+    if (is_nan_score<T>(v)) atomicAdd(&nan_z, 1u);
+    else atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u);
+  }
+  __syncthreads();
+  // 3. exclusive prefix over NB buckets (two per thread, then a block scan of the pairs)
+  {
+    const int i0 = 2 * tid;  // kBucketNB == 2 * kSortThreads
+    const unsigned a = cur[i0], b = cur[i0 + 1];
+    unsigned v = a + b;
+    for (int o = 1; o < kWave; o <<= 1) {  // inclusive wave scan
+      const unsigned t = __shfl_up(v, o, kWave);
+      if (lane >= o) v += t;
+    }
+    __shared__ unsigned wave_tot[kSortThreads / kWave];
+    if (lane == kWave - 1) wave_tot[wid] = v;
+    __syncthreads();
+    unsigned base = 0;
+    for (int w = 0; w < wid; ++w) base += wave_tot[w];
+    const unsigned excl = base + v - (a + b);
+    start[i0] = excl;
+    start[i0 + 1] = excl + a;
+    if (tid == kSortThreads - 1) start[kBucketNB] = excl + a + b;
+    __syncthreads();
+    cur[i0] = excl;
+    cur[i0 + 1] = excl + a;
+  }
+  __syncthreads();
+  // 4. scatter z into bucket order
+  for (int64_t j = tid; j < nz; j += kSortThreads) {
+    const T v = z[zo + j];
+    if (!is_nan_score<T>(v)) zb[atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u)] = v;
+  }
+  __syncthreads();
+  const unsigned n_valid = start[kBucketNB];
+  // 5. codes of this block's share of the shard's x and z
+  const int64_t tot = nx + nz, per = (tot + parts - 1) / parts;
+  const int64_t e0 = (int64_t)part * per, e1 = e0 + per < tot ? e0 + per : tot;
+  for (int64_t e = e0 + tid; e < e1; e += kSortThreads) {
+    const bool isx = e < nx;
+    const T v = isx ? x[xb + e] : z[zo + (e - nx)];
+    unsigned lo = 0, hi = 0;
+    if (is_nan_score<T>(v)) {
+      lo = isx ? 0u : n_valid;  // NaN x: below every p; NaN z: above every c
+      hi = lo;
+    } else {
+      const int b = bucket(bucket_value<T>(v));
+      const unsigned b0 = start[b], b1 = start[b + 1];
+      lo = b0;
+      hi = b0;
+      for (unsigned q = b0; q < b1; ++q) {
+        const T w = zb[q];
+        lo += w < v;
+        hi += w <= v;
+      }
+    }
+    if (isx) {
+      cx[(int64_t)s * max_nx + e] = (uint16_t)lo;
+      if (PRED == TW_PRED_HALF) cx2[(int64_t)s * max_nx + e] = (uint16_t)hi;
+    } else {
+      pz[(int64_t)s * max_nz + (e - nx)] = (uint16_t)lo;
+    }
+  }
+}
+
 template <int PRED>
 __global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
     const int64_t* __restrict__ x_off, const int64_t* __restrict__ z_off,
@@ -281,6 +415,8 @@ __global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
   }
 }
 
+static int g_rng_codes_by_bucket = 1;  // tw_count_rng_set_codes: 0 = sort + binary search
+
 struct RngRankPlan {
   bool ok;
   int C, chunks, tiles, parts;
@@ -333,6 +469,10 @@ int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const 
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_codes<T, PRED>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)(sizeof(uint64_t) * kMaxChunk)));
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_codes_bucket<T, PRED>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(sizeof(T) * kBucketMaxZ +
+                                           sizeof(unsigned) * (2 * kBucketNB + 1))));
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_ranked<PRED>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024 - 1024));
@@ -343,6 +483,12 @@ int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const 
   uint16_t* cx = (uint16_t*)(w + p.cx_off);
   uint16_t* cx2 = (uint16_t*)(w + p.cx2_off);
   uint16_t* pz = (uint16_t*)(w + p.pz_off);
+  if (max_nz <= kBucketMaxZ && g_rng_codes_by_bucket) {
+    const size_t lds_b = sizeof(T) * kBucketMaxZ + sizeof(unsigned) * (2 * kBucketNB + 1);
+    hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED>), dim3(n_shards * kBucketParts),
+                       dim3(kSortThreads), lds_b, st, (const T*)x, x_off, (const T*)z, z_off,
+                       kBucketParts, max_nx, max_nz, cx, cx2, pz);
+  } else {
   const size_t lds_sort = sizeof(uint64_t) * p.C;
   const size_t lds_codes = sizeof(uint64_t) * std::min<int64_t>((int64_t)p.chunks * p.C, kMaxChunk);
   const int E = std::max(4, p.C / kSortThreads);
@@ -360,6 +506,7 @@ int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const 
   hipLaunchKernelGGL((k_rank_codes<T, PRED>), dim3(n_shards * p.tiles), dim3(kSortThreads),
                      lds_codes, st, (const T*)x, x_off, (const T*)z, z_off, keys, p.chunks, p.C,
                      p.tiles, max_nx, max_nz, cx, cx2, pz);
+  }
   TW_LAUNCH_CHECK();
   hipLaunchKernelGGL((k_count_rng_ranked<PRED>), dim3(n_shards * p.parts), dim3(kRngThreads),
                      p.lds, st, x_off, z_off, cx, cx2, pz, max_nx, max_nz, B, p.parts,
@@ -440,4 +587,10 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
   if (pred == TW_PRED_HALF)
     return launch_rng_ranked<long long, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
   return launch_rng_ranked<long long, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
+}
+
+extern "C" int tw_count_rng_set_codes(int32_t by_bucket) {
+  TW_ARG_CHECK(by_bucket == 0 || by_bucket == 1, "tw_count_rng_set_codes: 0 or 1");
+  g_rng_codes_by_bucket = by_bucket;
+  return TW_OK;
 }
