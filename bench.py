@@ -543,8 +543,10 @@ def main():
         "plumbing_C1": c1,
         "single_shard_C2": single,
         "sorted_count": {
-            "note": "same UnN steps with the exact sort+binary-search count (algo='sorted', "
-                    "bit-identical estimates); pairs are logical, not compared one by one",
+            "note": "same UnN steps with the exact O((n+m) log m)-class count (algo='sorted':"
+                    " value buckets of z in LDS for shards of <= 16384, else sort + binary "
+                    "search; bit-identical estimates); pairs are logical, not compared one by "
+                    "one",
             "value": total_pairs / dt_sorted, "unit": "logical pairs/s",
             "ms_per_step": dt_sorted / args.steps * 1e3, "count_kernels_ms": kms_sorted,
             "estimate_last_step": float(est_sorted),

@@ -115,6 +115,10 @@ int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, const void* d
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, int32_t dtype, int32_t pred, void* d_work,
                           uint64_t* d_out, void* stream);
+/* Shards with nz <= 16384 (default 1): the count comes from value buckets of z in LDS (an
+ * LDS histogram, prefix and scatter, then one bucket scanned per x) instead of sorted chunks +
+ * binary searches; the same integers.  0 = always sort + search (A/B, tests). */
+int tw_count_sorted_set_bucket(int32_t by_bucket);
 
 /* ---- Row A3/A4/A5/A8: incomplete count on given index pairs (replay mode) -------------
  * Replaces cs.UB_indices / UB_pairs / UB (compute_stats.py:22-42): pair p of shard s

@@ -707,3 +707,39 @@ def test_repeated_un_one_launch_equals_loop(gpu, kind):
     s2 = np.random.randint(0, 2**31)
     assert a == b and s1 == s2
     assert np.array_equal(X1, X2) and np.array_equal(Z1, Z2)
+
+
+@pytest.mark.parametrize("dtype_name", ["f64", "i64"])
+@pytest.mark.parametrize("mode", ["gt", "half"])
+def test_sorted_count_bucket_equals_sort(gpu, dtype_name, mode):
+    """algo="sorted": value buckets (nz <= 16384) == sorted chunks + binary search == oracle,
+    on ties, NaN, +-0, +-inf, a degenerate all-equal shard and ragged / empty shards."""
+    from tuplewise import _engine as E, _lib as L
+    rng = np.random.RandomState(17)
+    nxs, nzs = [3000, 1, 0, 16384, 7000, 400], [2500, 3, 11, 16384, 1, 300]
+    if dtype_name == "f64":
+        xs = [rng.normal(0, 3, n).round(1) for n in nxs]
+        zs = [rng.normal(0, 3, n).round(1) for n in nzs]
+        xs[0][:40], zs[0][:25] = np.nan, np.nan
+        xs[3][:50], zs[3][:50] = -0.0, 0.0
+        xs[4][:2], zs[3][60:62] = [np.inf, -np.inf], [np.inf, -np.inf]
+        xs[5][:], zs[5][:] = 2.5, 2.5
+        dt = L.TW_F64
+    else:
+        xs = [rng.randint(-50, 50, n).astype(np.int64) for n in nxs]
+        zs = [rng.randint(-50, 50, n).astype(np.int64) for n in nzs]
+        dt = L.TW_I64
+    sh = E.Shards.from_blocks(xs, zs, dt)
+    got = []
+    for bucket in (1, 0):
+        L.call("tw_count_sorted_set_bucket", bucket)
+        try:
+            got.append(np.asarray(E.count_complete(sh, mode, algo="sorted")))
+        finally:
+            L.call("tw_count_sorted_set_bucket", 1)
+    assert np.array_equal(got[0], got[1])
+    for s, (x, z) in enumerate(zip(xs, zs)):
+        want = int((x.reshape(-1, 1) > z.reshape(1, -1)).sum())
+        if mode == "half":
+            want = 2 * want + int((x.reshape(-1, 1) == z.reshape(1, -1)).sum())
+        assert int(got[0][s]) == want, s

@@ -96,10 +96,191 @@ inline RankPlan plan_rank(int64_t max_nx, int64_t max_nz) {
   return p;
 }
 
+// Rank codes without a sort (shards with nz <= kBucketMaxZ): the block loads the shard's z
+// into LDS, buckets it by VALUE — b(v) = clamp(int((v - zmin) * NB / (zmax - zmin)), 0, NB-1)
+// over the finite z, a monotone map (every IEEE step in it is monotone), so bucket order is
+// value order — with an LDS histogram, prefix sum and scatter, and then a code is
+//   (#z in lower buckets) + (#z in its own bucket below / at most v)
+// by a scan of one bucket (~nz / NB values for smooth data).  Exact for any data: ties share
+// a bucket; NaN z sit in no bucket (their p is the count of non-NaN z, above every x code),
+// NaN x get code 0, +-inf clamp to the end buckets; degenerate or very skewed data only make
+// the scans longer.  Every block of a shard rebuilds the buckets (O(nz) LDS work) and codes
+// its share of the shard's x and z.  Replaces k_sort_chunks + k_rank_codes (41 + 78 us at
+// the bench shape).
+constexpr int kBucketNB = 2048;
+constexpr int64_t kBucketMaxZ = 16384;  // 128 KiB of z in LDS
+constexpr int kBucketParts = 4;
+
+template <typename T>
+__device__ __forceinline__ double bucket_value(T v) { return (double)v; }
+
+// COUNT = true: the complete count instead of codes (tw_count_pairs_sorted): the same
+// buckets, only the x-values, and the block's sum of their codes (#z < x, plus #z <= x for
+// half-ties) added to out[s] — the integer of k_count_complete / k_rank_count.
+template <typename T, int PRED, bool COUNT = false>
+__global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, int parts, int64_t max_nx, int64_t max_nz,
+    uint16_t* __restrict__ cx, uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz,
+    unsigned long long* __restrict__ out = nullptr) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* zb = (T*)smem;                                       // z by bucket (kBucketMaxZ)
+  unsigned* start = (unsigned*)(smem + sizeof(T) * kBucketMaxZ);  // NB + 1 bucket starts
+  unsigned* cur = start + kBucketNB + 1;                  // NB fill cursors / counts
+  __shared__ double red_min[kSortThreads / kWave], red_max[kSortThreads / kWave];
+  __shared__ unsigned nan_z;
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int s = lb / parts;
+  const int part = lb - s * parts;
+  const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
+  const int64_t zo = z_off[s], nz = z_off[s + 1] - zo;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  // 1. range of the finite z
+  double mn = __builtin_inf(), mx = -__builtin_inf();
+  for (int64_t j = tid; j < nz; j += kSortThreads) {
+    const double v = bucket_value<T>(z[zo + j]);
+    if (v - v == 0.0) {  // finite (not NaN, not inf)
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double a = __shfl_xor(mn, o, kWave), b = __shfl_xor(mx, o, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = 0;
+  if (tid == 0) nan_z = 0;
+  if (lane == 0) {
+    red_min[wid] = mn;
+    red_max[wid] = mx;
+  }
+  __syncthreads();
+  mn = red_min[0];
+  mx = red_max[0];
+  for (int w = 1; w < kSortThreads / kWave; ++w) {
+    mn = red_min[w] < mn ? red_min[w] : mn;
+    mx = red_max[w] > mx ? red_max[w] : mx;
+  }
+  const double scale = mx > mn ? (double)kBucketNB / (mx - mn) : 0.0;
+  auto bucket = [&](double v) -> int {
+    const double t = (v - mn) * scale;  // NaN when v == mn and scale == inf: bucket 0
+    return (int)__builtin_fmin(__builtin_fmax(t, 0.0), (double)(kBucketNB - 1));
+  };
+  // 2. histogram (NaN z counted apart)
+  for (int64_t j = tid; j < nz; j += kSortThreads) {
+    const T v = z[zo + j];
+    if (is_nan_score<T>(v)) atomicAdd(&nan_z, 1u);
+    else atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u);
+  }
+  __syncthreads();
+  // 3. exclusive prefix over NB buckets (two per thread, then a block scan of the pairs)
+  {
+    const int i0 = 2 * tid;  // kBucketNB == 2 * kSortThreads
+    const unsigned a = cur[i0], b = cur[i0 + 1];
+    unsigned v = a + b;
+    for (int o = 1; o < kWave; o <<= 1) {  // inclusive wave scan
+      const unsigned t = __shfl_up(v, o, kWave);
+      if (lane >= o) v += t;
+    }
+    __shared__ unsigned wave_tot[kSortThreads / kWave];
+    if (lane == kWave - 1) wave_tot[wid] = v;
+    __syncthreads();
+    unsigned base = 0;
+    for (int w = 0; w < wid; ++w) base += wave_tot[w];
+    const unsigned excl = base + v - (a + b);
+    start[i0] = excl;
+    start[i0 + 1] = excl + a;
+    if (tid == kSortThreads - 1) start[kBucketNB] = excl + a + b;
+    __syncthreads();
+    cur[i0] = excl;
+    cur[i0 + 1] = excl + a;
+  }
+  __syncthreads();
+  // 4. scatter z into bucket order
+  for (int64_t j = tid; j < nz; j += kSortThreads) {
+    const T v = z[zo + j];
+    if (!is_nan_score<T>(v)) zb[atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u)] = v;
+  }
+  __syncthreads();
+  const unsigned n_valid = start[kBucketNB];
+  // 5. codes of this block's share of the shard's x and z (COUNT: of its x only)
+  const int64_t tot = COUNT ? nx : nx + nz, per = (tot + parts - 1) / parts;
+  const int64_t e0 = (int64_t)part * per, e1 = e0 + per < tot ? e0 + per : tot;
+  unsigned long long acc = 0;
+  for (int64_t e = e0 + tid; e < e1; e += kSortThreads) {
+    const bool isx = e < nx;
+    const T v = isx ? x[xb + e] : z[zo + (e - nx)];
+    unsigned lo = 0, hi = 0;
+    if (is_nan_score<T>(v)) {
+      lo = isx ? 0u : n_valid;  // NaN x: below every p; NaN z: above every c
+      hi = lo;
+    } else {
+      const int b = bucket(bucket_value<T>(v));
+      const unsigned b0 = start[b], b1 = start[b + 1];
+      lo = b0;
+      hi = b0;
+      for (unsigned q = b0; q < b1; ++q) {
+        const T w = zb[q];
+        lo += w < v;
+        hi += w <= v;
+      }
+    }
+    if constexpr (COUNT) {
+      acc += lo + (PRED == TW_PRED_HALF ? hi : 0u);
+    } else if (isx) {
+      cx[(int64_t)s * max_nx + e] = (uint16_t)lo;
+      if (PRED == TW_PRED_HALF) cx2[(int64_t)s * max_nx + e] = (uint16_t)hi;
+    } else {
+      pz[(int64_t)s * max_nz + (e - nx)] = (uint16_t)lo;
+    }
+  }
+  if constexpr (COUNT) {
+    acc = wave_sum_u64(acc);
+    __shared__ unsigned long long part_acc[kSortThreads / kWave];
+    if (lane == 0) part_acc[wid] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long b = 0;
+      for (int w = 0; w < kSortThreads / kWave; ++w) b += part_acc[w];
+      if (b) atomicAdd(out + s, b);
+    }
+  }
+}
+
+static int g_sorted_by_bucket = 1;  // tw_count_sorted_set_bucket: 0 = sort + binary search
+
+template <typename T, int PRED>
+int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                        int32_t n_shards, int64_t max_nx, uint64_t* out, hipStream_t st) {
+  const size_t lds_b = sizeof(T) * kBucketMaxZ + sizeof(unsigned) * (2 * kBucketNB + 1);
+  static bool attr = false;
+  if (!attr) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_codes_bucket<T, PRED, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b));
+    attr = true;
+  }
+  // enough blocks per shard for the chip: each rebuilds the shard's buckets, then sums the
+  // codes of its share of x
+  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(512, n_shards),
+                                                                ceil_div(max_nx, 4096)));
+  TW_ARG_CHECK((int64_t)n_shards * parts < (1ll << 31), "tw_count_pairs_sorted: grid too large");
+  hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED, true>), dim3(n_shards * parts),
+                     dim3(kSortThreads), lds_b, st, (const T*)x, x_off, (const T*)z, z_off, parts,
+                     max_nx, (int64_t)0, nullptr, nullptr, nullptr, (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 template <typename T>
 int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                 int32_t n_shards, int64_t max_nx, int64_t max_nz, int32_t pred, void* work,
                 uint64_t* out, hipStream_t st) {
+  if (max_nz <= kBucketMaxZ && g_sorted_by_bucket) {
+    if (pred == TW_PRED_HALF)
+      return launch_bucket_count<T, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, max_nx, out, st);
+    return launch_bucket_count<T, TW_PRED_GT>(x, x_off, z, z_off, n_shards, max_nx, out, st);
+  }
   const RankPlan p = plan_rank(max_nx, max_nz);
   TW_ARG_CHECK((int64_t)n_shards * p.chunks < (1ll << 31) &&
                    (int64_t)n_shards * p.tiles_x < (1ll << 31),
@@ -223,140 +404,6 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes(
       if (PRED == TW_PRED_HALF) cx2[(int64_t)s * max_nx + e] = (uint16_t)hi[r];
     } else if (e < nx + nz) {
       pz[(int64_t)s * max_nz + (e - nx)] = (uint16_t)lo[r];
-    }
-  }
-}
-
-// Rank codes without a sort (shards with nz <= kBucketMaxZ): the block loads the shard's z
-// into LDS, buckets it by VALUE — b(v) = clamp(int((v - zmin) * NB / (zmax - zmin)), 0, NB-1)
-// over the finite z, a monotone map (every IEEE step in it is monotone), so bucket order is
-// value order — with an LDS histogram, prefix sum and scatter, and then a code is
-//   (#z in lower buckets) + (#z in its own bucket below / at most v)
-// by a scan of one bucket (~nz / NB values for smooth data).  Exact for any data: ties share
-// a bucket; NaN z sit in no bucket (their p is the count of non-NaN z, above every x code),
-// NaN x get code 0, +-inf clamp to the end buckets; degenerate or very skewed data only make
-// the scans longer.  Every block of a shard rebuilds the buckets (O(nz) LDS work) and codes
-// its share of the shard's x and z.  Replaces k_sort_chunks + k_rank_codes (41 + 78 us at
-// the bench shape).
-constexpr int kBucketNB = 2048;
-constexpr int64_t kBucketMaxZ = 16384;  // 128 KiB of z in LDS
-constexpr int kBucketParts = 4;
-
-template <typename T>
-__device__ __forceinline__ double bucket_value(T v) { return (double)v; }
-
-template <typename T, int PRED>
-__global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
-    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
-    const int64_t* __restrict__ z_off, int parts, int64_t max_nx, int64_t max_nz,
-    uint16_t* __restrict__ cx, uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* zb = (T*)smem;                                       // z by bucket (kBucketMaxZ)
-  unsigned* start = (unsigned*)(smem + sizeof(T) * kBucketMaxZ);  // NB + 1 bucket starts
-  unsigned* cur = start + kBucketNB + 1;                  // NB fill cursors / counts
-  __shared__ double red_min[kSortThreads / kWave], red_max[kSortThreads / kWave];
-  __shared__ unsigned nan_z;
-  const int lb = xcd_block(blockIdx.x, gridDim.x);
-  const int s = lb / parts;
-  const int part = lb - s * parts;
-  const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
-  const int64_t zo = z_off[s], nz = z_off[s + 1] - zo;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  // 1. range of the finite z
-  double mn = __builtin_inf(), mx = -__builtin_inf();
-  for (int64_t j = tid; j < nz; j += kSortThreads) {
-    const double v = bucket_value<T>(z[zo + j]);
-    if (v - v == 0.0) {  // finite (not NaN, not inf)
-      mn = v < mn ? v : mn;
-      mx = v > mx ? v : mx;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    const double a = __shfl_xor(mn, o, kWave), b = __shfl_xor(mx, o, kWave);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
-  for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = 0;
-  if (tid == 0) nan_z = 0;
-  if (lane == 0) {
-    red_min[wid] = mn;
-    red_max[wid] = mx;
-  }
-  __syncthreads();
-  mn = red_min[0];
-  mx = red_max[0];
-  for (int w = 1; w < kSortThreads / kWave; ++w) {
-    mn = red_min[w] < mn ? red_min[w] : mn;
-    mx = red_max[w] > mx ? red_max[w] : mx;
-  }
-  const double scale = mx > mn ? (double)kBucketNB / (mx - mn) : 0.0;
-  auto bucket = [&](double v) -> int {
-    const double t = (v - mn) * scale;  // NaN when v == mn and scale == inf: bucket 0
-    return (int)__builtin_fmin(__builtin_fmax(t, 0.0), (double)(kBucketNB - 1));
-  };
-  // 2. histogram (NaN z counted apart)
-  for (int64_t j = tid; j < nz; j += kSortThreads) {
-    const T v = z[zo + j];
-    if (is_nan_score<T>(v)) atomicAdd(&nan_z, 1u);
-    else atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u);
-  }
-  __syncthreads();
-  // 3. exclusive prefix over NB buckets (two per thread, then a block scan of the pairs)
-  {
-    const int i0 = 2 * tid;  // kBucketNB == 2 * kSortThreads
-    const unsigned a = cur[i0], b = cur[i0 + 1];
-    unsigned v = a + b;
-    for (int o = 1; o < kWave; o <<= 1) {  // inclusive wave scan
-      const unsigned t = __shfl_up(v, o, kWave);
-      if (lane >= o) v += t;
-    }
-    __shared__ unsigned wave_tot[kSortThreads / kWave];
-    if (lane == kWave - 1) wave_tot[wid] = v;
-    __syncthreads();
-    unsigned base = 0;
-    for (int w = 0; w < wid; ++w) base += wave_tot[w];
-    const unsigned excl = base + v - (a + b);
-    start[i0] = excl;
-    start[i0 + 1] = excl + a;
-    if (tid == kSortThreads - 1) start[kBucketNB] = excl + a + b;
-    __syncthreads();
-    cur[i0] = excl;
-    cur[i0 + 1] = excl + a;
-  }
-  __syncthreads();
-  // 4. scatter z into bucket order
-  for (int64_t j = tid; j < nz; j += kSortThreads) {
-    const T v = z[zo + j];
-    if (!is_nan_score<T>(v)) zb[atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u)] = v;
-  }
-  __syncthreads();
-  const unsigned n_valid = start[kBucketNB];
-  // 5. codes of this block's share of the shard's x and z
-  const int64_t tot = nx + nz, per = (tot + parts - 1) / parts;
-  const int64_t e0 = (int64_t)part * per, e1 = e0 + per < tot ? e0 + per : tot;
-  for (int64_t e = e0 + tid; e < e1; e += kSortThreads) {
-    const bool isx = e < nx;
-    const T v = isx ? x[xb + e] : z[zo + (e - nx)];
-    unsigned lo = 0, hi = 0;
-    if (is_nan_score<T>(v)) {
-      lo = isx ? 0u : n_valid;  // NaN x: below every p; NaN z: above every c
-      hi = lo;
-    } else {
-      const int b = bucket(bucket_value<T>(v));
-      const unsigned b0 = start[b], b1 = start[b + 1];
-      lo = b0;
-      hi = b0;
-      for (unsigned q = b0; q < b1; ++q) {
-        const T w = zb[q];
-        lo += w < v;
-        hi += w <= v;
-      }
-    }
-    if (isx) {
-      cx[(int64_t)s * max_nx + e] = (uint16_t)lo;
-      if (PRED == TW_PRED_HALF) cx2[(int64_t)s * max_nx + e] = (uint16_t)hi;
-    } else {
-      pz[(int64_t)s * max_nz + (e - nx)] = (uint16_t)lo;
     }
   }
 }
@@ -592,5 +639,11 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
 extern "C" int tw_count_rng_set_codes(int32_t by_bucket) {
   TW_ARG_CHECK(by_bucket == 0 || by_bucket == 1, "tw_count_rng_set_codes: 0 or 1");
   g_rng_codes_by_bucket = by_bucket;
+  return TW_OK;
+}
+
+extern "C" int tw_count_sorted_set_bucket(int32_t by_bucket) {
+  TW_ARG_CHECK(by_bucket == 0 || by_bucket == 1, "tw_count_sorted_set_bucket: 0 or 1");
+  g_sorted_by_bucket = by_bucket;
   return TW_OK;
 }
