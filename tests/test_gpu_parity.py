@@ -575,6 +575,26 @@ def test_complete_hinge_search_equals_pair_sums(gpu, kx, kz):
         np.testing.assert_array_equal(g_search[s], want.ravel())
 
 
+def test_complete_logistic_large_scores(gpu):
+    """Scores beyond +-350 send their (tile, chunk) to the direct-formula path of
+    k_logistic_coef (the separated factors could leave the normal range); the gradient still
+    matches the oracle, incl. saturated sigmas (S of several hundred)."""
+    from tuplewise import _lib as L, _learn
+    rng = np.random.RandomState(12)
+    N, d, kx, kz = 3, 4, 5000, 1300
+    X, Z = rng.normal(size=(kx * N, d)), rng.normal(0.3, 1, size=(kz * N, d))
+    X[: kx, :] *= 300.0  # shard 0: |scores| up to ~1000 on the x side
+    Z[kz:2 * kz, :] *= 250.0  # shard 1: on the z side
+    w = np.array([1.0, -0.5, 0.25, 0.8])
+    g = _learn.complete_grads_device(L.to_device(X), L.to_device(Z), d, None, kx, None, kz, N,
+                                     L.to_device(w), 0.7, L.TW_LOSS_LOGISTIC).cpu().numpy()
+    for s in range(N):
+        with np.errstate(over="ignore"):  # the oracle's exp saturates, as NumPy's does
+            want = O.grad_complete_block(w.reshape(-1, 1), 0.7, "logistic")(
+                X[s * kx:(s + 1) * kx], Z[s * kz:(s + 1) * kz])
+        np.testing.assert_allclose(g[s], want.ravel(), rtol=1e-10, atol=1e-12)
+
+
 @pytest.mark.parametrize("kx,kz", [(300, 77), (5000, 1300), (1, 9000)])
 def test_complete_logistic_one_pass_equals_two_pass(gpu, kx, kz):
     """One-pass logistic coefficients (k_logistic_coef + k_apart_final) agree with the two-pass

@@ -164,14 +164,14 @@ __global__ __launch_bounds__(kSortThreads) void k_hinge_coef(const double* __res
 }
 
 // Logistic coefficients in ONE pass over the pairs (each sigma(S_ij) is evaluated once and
-// feeds both sums).  A 1024-thread block holds kLgR x-scores per lane (a tile of 1024 kLgR
+// feeds both sums).  A 512-thread block holds kLgR = 8 x-scores per lane (a tile of 4096
 // x-points of one shard) and streams the shard's z-scores through LDS in chunks of kLgChunk:
 //   b_i += sigma(S_ij)              per lane, in j order (registers)
-//   a_j  = sum over the tile's x    lane butterfly, then the 16 waves in wave order (LDS),
+//   a_j  = sum over the tile's x    lane butterfly, then the 8 waves in wave order (LDS),
 // writing one partial of a_j per (tile, j); k_apart_final adds the tiles in tile order.
-// Deterministic; the f64 exp is the cost, so one pass halves the two-pass k_pair_coef.
-constexpr int kLgR = 4;
-constexpr int kLgThreads = 1024;
+// Deterministic.  With the separated exponent (below) a sigma is an FMA and a division.
+constexpr int kLgR = 16;
+constexpr int kLgThreads = 256;
 constexpr int kLgChunk = 512;
 __global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __restrict__ sx,
                                                               int64_t kx,
@@ -181,39 +181,77 @@ __global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __re
                                                               double* __restrict__ bx,
                                                               double* __restrict__ apart) {
   __shared__ double zc[kLgChunk];
+  __shared__ double eb[kLgChunk];  // exp(-sz_j), or NaN where that is out of range
   __shared__ double wpart[kLgThreads / kWave][kLgChunk];
   const int lb = xcd_block(blockIdx.x, gridDim.x);
   const int s = lb / tiles;
   const int tile = lb - s * tiles;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  double v[kLgR], b[kLgR];
-  bool valid[kLgR];
+  // e^-S_ij = e^(sx_i - m) * e^(-sz_j): the exponent SEPARATES, so a sigma is one FMA and a
+  // Newton reciprocal instead of an exp and an IEEE division.  Used for a (tile, chunk) when
+  // every factor's exponent is within +-350 (the product then stays a normal double); any
+  // other chunk takes the direct formula, so the result never depends on the data's range.
+  // registers: the factors e^(sx - m) and the b sums (the scores themselves are re-read
+  // only by the rare direct-formula chunks), so 16 x-values per lane fit
+  double b[kLgR], ea[kLgR];
+  unsigned valid = 0;  // bit r: x-value r of this lane exists
+  int tile_sep = 1;
+  const double* xs = sx + (int64_t)s * kx + (int64_t)tile * (kLgThreads * kLgR) + threadIdx.x;
 #pragma unroll
   for (int r = 0; r < kLgR; ++r) {
     const int64_t i = (int64_t)tile * (kLgThreads * kLgR) + r * kLgThreads + threadIdx.x;
-    valid[r] = i < kx;
-    v[r] = valid[r] ? sx[(int64_t)s * kx + i] : 0.0;
+    const bool ok = i < kx;
+    valid |= (unsigned)ok << r;
+    const double u = (ok ? xs[r * kLgThreads] : 0.0) - margin;
     b[r] = 0.0;
+    tile_sep &= __builtin_fabs(u) <= 350.0;
+    ea[r] = exp(u);
   }
+  tile_sep = __syncthreads_and(tile_sep);
   const double* zs = sz + (int64_t)s * kz;
   double* ap = apart + ((int64_t)s * tiles + tile) * kz;
   for (int64_t c0 = 0; c0 < kz; c0 += kLgChunk) {
     const int n = (int)std::min<int64_t>(kLgChunk, kz - c0);
     __syncthreads();
-    for (int j = threadIdx.x; j < n; j += kLgThreads) zc[j] = zs[c0 + j];
-    __syncthreads();
-    for (int j = 0; j < n; ++j) {
-      const double zj = zc[j];
-      double t = 0.0;
+    int chunk_sep = tile_sep;
+    for (int j = threadIdx.x; j < n; j += kLgThreads) {
+      const double zj = zs[c0 + j];
+      zc[j] = zj;
+      eb[j] = exp(-zj);
+      chunk_sep &= __builtin_fabs(zj) <= 350.0;
+    }
+    chunk_sep = __syncthreads_and(chunk_sep);  // block-uniform
+    if (chunk_sep) {
+      for (int j = 0; j < n; ++j) {
+        const double ej = eb[j];
+        double t = 0.0;
 #pragma unroll
-      for (int r = 0; r < kLgR; ++r) {
-        const double S = (zj - v[r]) + margin;
-        const double p = pair_weight<TW_LOSS_LOGISTIC>(S);
-        b[r] += p;
-        t += valid[r] ? p : 0.0;
+        for (int r = 0; r < kLgR; ++r) {
+          const double q = __builtin_fma(ea[r], ej, 1.0);  // 1 + e^-S in [1, e^700]
+          double y = __builtin_amdgcn_rcp(q);
+          y = __builtin_fma(__builtin_fma(-q, y, 1.0), y, y);
+          y = __builtin_fma(__builtin_fma(-q, y, 1.0), y, y);
+          b[r] += y;
+          t += (valid >> r) & 1u ? y : 0.0;
+        }
+        t = wave_sum_f64(t);
+        if (lane == 0) wpart[wid][j] = t;
       }
-      t = wave_sum_f64(t);
-      if (lane == 0) wpart[wid][j] = t;
+    } else {
+      for (int j = 0; j < n; ++j) {
+        const double zj = zc[j];
+        double t = 0.0;
+#pragma unroll 1
+        for (int r = 0; r < kLgR; ++r) {
+          const bool ok = (valid >> r) & 1u;
+          const double vr = ok ? xs[r * kLgThreads] : 0.0;
+          const double p = pair_weight<TW_LOSS_LOGISTIC>((zj - vr) + margin);
+          b[r] += p;
+          t += ok ? p : 0.0;
+        }
+        t = wave_sum_f64(t);
+        if (lane == 0) wpart[wid][j] = t;
+      }
     }
     __syncthreads();
     for (int j = threadIdx.x; j < n; j += kLgThreads) {
@@ -226,7 +264,7 @@ __global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __re
 #pragma unroll
   for (int r = 0; r < kLgR; ++r) {
     const int64_t i = (int64_t)tile * (kLgThreads * kLgR) + r * kLgThreads + threadIdx.x;
-    if (valid[r]) bx[(int64_t)s * kx + i] = b[r];
+    if ((valid >> r) & 1u) bx[(int64_t)s * kx + i] = b[r];
   }
 }
 
