@@ -250,6 +250,32 @@ int tw_swr_rows_rng(int64_t* d_rows, int32_t n_shards, int64_t k, int64_t n, uin
  * d_step (nullable): device-RNG step counter, incremented once. */
 int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, int32_t n_shards, int64_t d,
                   double reg, double lr, double momentum, uint64_t* d_step, void* stream);
+/* Same update from (d_w_in, d_dw_in) into (d_w, d_dw) (may be the same buffers); the step
+ * counter (nullable) advances by step_inc.  Ends a segment of tw_sgd_step launches. */
+int tw_sgd_update_to(const double* d_w_in, const double* d_dw_in, double* d_w, double* d_dw,
+                     const double* d_grads, int32_t n_shards, int64_t d, double reg, double lr,
+                     double momentum, uint64_t* d_step, int32_t step_inc, void* stream);
+
+/* ---- Rows L1 + L2 fused: one launch per SGD step (narrow rows, d <= 32, n_shards*d <= 4096;
+ * tw_sgd_step_fusable says whether a shape qualifies).  The launch first applies the update of
+ * the PREVIOUS step (d_grads_in, d_w_in, d_dw_in -> w, written by block 0 to d_w_out/d_dw_out;
+ * every block computes it, so no grid synchronisation), then computes this step's per-shard
+ * gradients with it into d_grads_out.  d_grads_in == NULL: no pending update (w = d_w_in).
+ * Draws: replay (d_ix, d_iz) or device RNG at step *d_step + step_off (the counter itself is
+ * advanced by the tw_sgd_update_to that ends the segment).  A segment of k steps is
+ *   step 0: in (w0, -, -) -> grads G0;   step j>0: in (W[j-1&1], DW[j-1&1], G[j-1&1]) ->
+ *   out (W[j&1], DW[j&1], G[j&1]);  then tw_sgd_update_to(W[k-1&1], DW[k-1&1] -> w0, dw0,
+ *   G[k-1&1], step_inc = k)
+ * (ping-pong slots, slot 0 = w0/dw0): the same bits as k tw_pair_grad(_rng) + tw_sgd_update
+ * pairs, with k + 1 launches instead of 2k. */
+int tw_sgd_step_fusable(int64_t d, int32_t n_shards);
+int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                int64_t kx, const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix,
+                const int64_t* d_iz, int32_t n_shards, int64_t B, double margin, int32_t loss,
+                uint64_t seed, const uint64_t* d_step, int32_t step_off, int32_t shard_base,
+                const double* d_w_in, const double* d_dw_in, const double* d_grads_in, double reg,
+                double lr, double momentum, double* d_w_out, double* d_dw_out,
+                double* d_grads_out, void* stream);
 
 /* ---- f1: scores = A @ w for a row-major (n, d) matrix (evaluation_step, make_exps.py:163,
  * :170-171).  Row dot products in index order. */

@@ -271,3 +271,47 @@ def test_complete_gradient_learning(gpu, golden, mode):
         lr.learning_process(X, Z, q, rng_mode=mode, gradient="complete", graphs=graphs)
         out.append(q["norm_w"])
     assert out[0] == out[1]
+
+
+@pytest.mark.parametrize("loss", ["hinge", "logistic"])
+@pytest.mark.parametrize("optim", ["momentum", "SGD"])
+def test_fused_sgd_step_equals_grad_plus_update(gpu, golden, loss, optim):
+    """tw_sgd_step (the previous step's update fused into the gradient launch, ping-pong
+    w/dw/grads slots) gives the bits of one gradient + one update launch per step: device
+    and replay draws, segments of 1, 2 and 7 steps, eager and hipGraph."""
+    import torch
+    import tuplewise.learning as lr
+    X, Z, w0 = golden["learn/X"], golden["learn/Z"], golden["learn/w0"]
+    N, B = 10, 20
+    rs = np.random.RandomState(3)
+    kx, kz = X.shape[0] // N, Z.shape[0] // N
+
+    def run(fused, mode, graphs):
+        eng = lr.SGDEngine(X, Z, w0, N, B, 1, 0.05, 0.01, optim, loss=loss)
+        assert eng.fused  # d = 10, N*d = 100: the fusable shape
+        eng.fused = fused
+        ws = []
+        if mode == "device":
+            eng.enable_device_rng(12345)
+            for n, resh in ((1, True), (2, False), (7, True), (7, False)):
+                eng.run_segment(n, resh, graphs)
+                ws.append(eng.w_host())
+        else:
+            rr = np.random.RandomState(9)
+            eng.set_shards([rr.randint(0, X.shape[0], kx) for _ in range(N)],
+                           [rr.randint(0, Z.shape[0], kz) for _ in range(N)])
+            for tag, n in enumerate((1, 2, 7)):
+                d = np.stack([np.stack([rr.randint(0, kx, (N, B)), rr.randint(0, kz, (N, B))])
+                              for _ in range(n)]).astype(np.int64)
+                eng.run_replay_segment(torch.from_numpy(d).cuda(), n, graphs, tag)
+                ws.append(eng.w_host())
+        torch.cuda.synchronize()
+        return np.stack(ws), eng.dw.cpu().numpy()
+
+    for mode in ("device", "replay"):
+        ref = run(False, mode, False)
+        assert np.all(np.isfinite(ref[0])) and np.abs(ref[0][-1] - w0).max() > 0
+        for graphs in (False, True):
+            got = run(True, mode, graphs)
+            assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), \
+                (mode, graphs)

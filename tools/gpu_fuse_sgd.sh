@@ -1,0 +1,5 @@
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_learning.py -x -v --timeout 120 --timeout-method thread > gpurun_out/fuse_tests.log 2>&1 && \
+timeout -k 10 300 python -u tools/time_sgd.py > gpurun_out/fuse_sgd.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fuse_prof -o run -- python3 tools/time_sgd.py > gpurun_out/fuse_prof.log 2>&1

@@ -63,6 +63,10 @@ _SIGNATURES = {
     "tw_hinge_set_variant": [_i32],
     "tw_swr_rows_rng": [_vp, _i32, _i64, _i64, _u64, _vp, _i32, _i32, _vp],
     "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _vp],
+    "tw_sgd_update_to": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _i32, _vp],
+    "tw_sgd_step_fusable": [_i64, _i32],
+    "tw_sgd_step": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _f64, _i32, _u64,
+                    _vp, _i32, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
     "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],
     "tw_permute_pair": [_vp, _vp, _i64, _u64, _vp, _vp, _i64, _u64, _vp],

@@ -268,6 +268,133 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
   if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
 }
 
+// One whole SGD step for narrow rows (d <= 32, C4) in ONE launch: the update of the PREVIOUS
+// step (make_exps.py:130-141) runs as this kernel's prologue, redundantly in every block, and
+// then the gradient of this step (compute_stats.py:146-162) with the updated w.
+//   * The prologue's loads (the previous step's N x d shard gradients, w, dw) are issued first
+//     and the pair chain (draws -> row tables -> rows -> diff rows in LDS) runs while they are in
+//     flight; the two dependent chains overlap instead of running in two launches.
+//   * Ping-pong buffers: step k reads w/dw/grads of slot (k-1)&1 and writes slot k&1 (block 0
+//     writes w/dw), so no block overwrites what another block of the same launch still reads.
+//   * Arithmetic is that of k_sgd_update (shard-order sum from +0.0, /N, + reg*w, momentum)
+//     followed by k_hinge_grad's narrow path (same diff, same sequential dot, same row-order
+//     column sums), so a fused segment gives the bits of grad+update launches.
+// grads_in == nullptr: no pending update (the first step of a segment reads w_in as is).
+constexpr int kFuseMaxGrads = 4096;                  // N*d staged per block (32 KiB)
+constexpr int kFusePerThread = kFuseMaxGrads / kBlock;
+constexpr int kFuseMaxD = 32;
+
+template <int LOSS>
+__global__ __launch_bounds__(kBlock) void k_sgd_step_narrow(
+    const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
+    const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
+    int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
+    int CH, double margin, uint64_t seed, const uint64_t* __restrict__ d_step,
+    uint32_t step_off, uint32_t shard_base, int n_shards, const double* __restrict__ w_in,
+    const double* __restrict__ dw_in, const double* __restrict__ grads_in, double reg,
+    double lr, double momentum, double* __restrict__ w_out, double* __restrict__ dw_out,
+    double* __restrict__ grads_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* diff = (double*)smem;    // CH * d
+  double* flag = diff + CH * d;    // CH pair weights
+  double* wsh = flag + CH;         // kFuseMaxD: this step's w
+  double* gt = wsh + kFuseMaxD;    // n_shards * d: the previous step's shard gradients
+  const int s = blockIdx.x, tid = threadIdx.x, dd = (int)d;
+  const int ng = grads_in ? n_shards * dd : 0;
+
+  double gv[kFusePerThread];  // prologue loads first: in flight during the pair chain
+#pragma unroll
+  for (int u = 0; u < kFusePerThread; ++u) {
+    const int e = tid + u * kBlock;
+    gv[u] = e < ng ? grads_in[e] : 0.0;
+  }
+  double wj = 0.0, dwj = 0.0;
+  if (tid < dd) {
+    wj = w_in[tid];
+    if (grads_in) dwj = dw_in[tid];
+  }
+  const uint64_t step = (d_step ? *d_step : 0) + step_off;
+  double acc = 0.0;  // thread tid < d: column tid
+
+  for (int64_t b0 = 0; b0 < B; b0 += CH) {
+    const int nb = (int)std::min<int64_t>(CH, B - b0);
+    for (int t = tid; t < nb; t += kBlock) {  // this thread's pair -> its diff row in LDS
+      const int64_t p = (int64_t)s * B + b0 + t;
+      int64_t ax, az;
+      if (ix) {
+        ax = ix[p];
+        az = iz[p];
+      } else {
+        const u32x4 r = sgd_draw(seed, step, (uint32_t)(b0 + t), shard_base + (uint32_t)s,
+                                 kTagPairs);
+        ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
+        az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
+      }
+      const int64_t rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+      const int64_t rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      const double* zr = Z + rzt * d;
+      const double* xr = X + rxt * d;
+      double* dr = diff + (int64_t)t * d;
+#pragma unroll 4
+      for (int j = 0; j < dd; ++j) dr[j] = zr[j] - xr[j];
+    }
+    if (b0 == 0) {  // prologue: w of this step = update(w, dw, grads of the previous step)
+#pragma unroll
+      for (int u = 0; u < kFusePerThread; ++u) {
+        const int e = tid + u * kBlock;
+        if (e < ng) gt[e] = gv[u];
+      }
+      __syncthreads();
+      if (tid < dd) {
+        double wt = wj;
+        if (grads_in) {
+          double sum = 0.0;  // shard order, as np.mean(axis=0) / k_sgd_update
+          int r = 0;
+          for (; r + 8 <= n_shards; r += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = gt[(r + u) * dd + tid];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sum += v[u];
+          }
+          for (; r < n_shards; ++r) sum += gt[r * dd + tid];
+          const double g = sum / (double)n_shards + reg * wj;
+          const double st = momentum >= 0.0 ? momentum * dwj + lr * g : lr * g;
+          wt = wj - st;
+          if (s == 0) {
+            w_out[tid] = wt;
+            dw_out[tid] = st;
+          }
+        }
+        wsh[tid] = wt;
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < nb; t += kBlock) {  // S = diff . w + margin, sequential j
+      const double* dr = diff + (int64_t)t * d;
+      double part = 0.0;
+      for (int j = 0; j < dd; ++j) part += dr[j] * wsh[j];
+      flag[t] = pair_weight<LOSS>(part + margin);
+    }
+    __syncthreads();
+    if (tid < dd) {  // column sums over the filtered rows, in row order (as k_hinge_grad)
+      double a = acc;
+      int t = 0;
+      for (; t + 8 <= nb; t += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = weighted<LOSS>(flag[t + u], diff[(t + u) * dd + tid]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+      }
+      for (; t < nb; ++t) a += weighted<LOSS>(flag[t], diff[t * dd + tid]);
+      acc = a;
+    }
+    __syncthreads();
+  }
+  if (tid < dd) grads_out[(int64_t)s * d + tid] = acc / (double)B;
+}
+
 // SWR_divide row draws on the device: rows[s*k + t] uniform in [0, n) (with replacement).
 __global__ __launch_bounds__(kBlock) void k_swr_rows(int64_t* __restrict__ rows, int n_shards,
                                                      int64_t k, int64_t n, uint64_t seed,
@@ -289,14 +416,16 @@ __global__ __launch_bounds__(kBlock) void k_swr_rows(int64_t* __restrict__ rows,
 // per column adds them in shard order — the sequential order of np.mean(axis=0).
 constexpr int kUpdCols = 16;
 constexpr int kUpdRows = 512;  // shard rows staged per pass: 512 x 16 doubles = 64 KiB
-__global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
-                                                       double* __restrict__ dw,
+// w_in/dw_in may equal w/dw (in place); step_inc: how far the step counter advances.
+__global__ __launch_bounds__(kBlock) void k_sgd_update(const double* w_in, const double* dw_in,
+                                                       double* w, double* dw,
                                                        const double* __restrict__ grads,
                                                        int n_shards, int64_t d, double reg,
                                                        double lr, double momentum,
-                                                       uint64_t* __restrict__ d_step) {
+                                                       uint64_t* __restrict__ d_step,
+                                                       uint32_t step_inc) {
   __shared__ double tile[kUpdRows * kUpdCols];
-  if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += 1;
+  if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += step_inc;
   const int64_t j0 = (int64_t)blockIdx.x * kUpdCols;
   const int nc = (int)std::min<int64_t>(kUpdCols, d - j0);
   double sum = 0.0;  // thread c < nc: 0.0 + g_0 + g_1 + ... in shard order
@@ -322,9 +451,9 @@ __global__ __launch_bounds__(kBlock) void k_sgd_update(double* __restrict__ w,
   }
   if (threadIdx.x < nc) {
     const int64_t j = j0 + threadIdx.x;
-    const double wj = w[j];
+    const double wj = w_in[j];
     const double g = sum / (double)n_shards + reg * wj;
-    const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
+    const double step = momentum >= 0.0 ? momentum * dw_in[j] + lr * g : lr * g;
     dw[j] = step;
     w[j] = wj - step;
   }
@@ -471,8 +600,63 @@ extern "C" int tw_sgd_update(double* d_w, double* d_dw, const double* d_grads, i
   TW_ARG_CHECK(n_shards >= 1 && d >= 1, "tw_sgd_update: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (int)ceil_div(d, kUpdCols);
-  hipLaunchKernelGGL(k_sgd_update, dim3(blocks), dim3(kBlock), 0, st, d_w, d_dw, d_grads,
-                     n_shards, d, reg, lr, momentum, d_step);
+  hipLaunchKernelGGL(k_sgd_update, dim3(blocks), dim3(kBlock), 0, st, d_w, d_dw, d_w, d_dw,
+                     d_grads, n_shards, d, reg, lr, momentum, d_step, 1u);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_sgd_update_to(const double* d_w_in, const double* d_dw_in, double* d_w,
+                                double* d_dw, const double* d_grads, int32_t n_shards, int64_t d,
+                                double reg, double lr, double momentum, uint64_t* d_step,
+                                int32_t step_inc, void* stream) {
+  TW_ARG_CHECK(n_shards >= 1 && d >= 1 && step_inc >= 0, "tw_sgd_update_to: bad sizes");
+  const int blocks = (int)ceil_div(d, kUpdCols);
+  hipLaunchKernelGGL(k_sgd_update, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, d_w_in,
+                     d_dw_in, d_w, d_dw, d_grads, n_shards, d, reg, lr, momentum, d_step,
+                     (uint32_t)step_inc);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_sgd_step_fusable(int64_t d, int32_t n_shards) {
+  return d >= 1 && d <= kFuseMaxD && n_shards >= 1 && (int64_t)n_shards * d <= kFuseMaxGrads;
+}
+
+extern "C" int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d,
+                           const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                           int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                           int32_t n_shards, int64_t B, double margin, int32_t loss,
+                           uint64_t seed, const uint64_t* d_step, int32_t step_off,
+                           int32_t shard_base, const double* d_w_in, const double* d_dw_in,
+                           const double* d_grads_in, double reg, double lr, double momentum,
+                           double* d_w_out, double* d_dw_out, double* d_grads_out,
+                           void* stream) {
+  TW_ARG_CHECK(tw_sgd_step_fusable(d, n_shards), "tw_sgd_step: d=%lld, n_shards=%d not fusable",
+               (long long)d, n_shards);
+  TW_ARG_CHECK(B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1 && step_off >= 0 &&
+                   shard_base >= 0, "tw_sgd_step: bad B/kx/kz/step_off/shard_base");
+  TW_ARG_CHECK((d_ix == nullptr) == (d_iz == nullptr), "tw_sgd_step: ix and iz go together");
+  TW_ARG_CHECK(d_ix != nullptr || d_step != nullptr, "tw_sgd_step: device draws need d_step");
+  TW_ARG_CHECK(d_grads_in == nullptr || (d_dw_in != nullptr && d_w_out != nullptr &&
+                                         d_dw_out != nullptr),
+               "tw_sgd_step: a pending update needs dw_in, w_out, dw_out");
+  if (int rc = check_loss(loss)) return rc;
+  // diff rows + weights + w + the staged shard gradients within 64 KiB
+  const int64_t room = kLdsDoubles - kFuseMaxD - (int64_t)n_shards * d;  // >= 4064
+  const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, room / (d + 1)));
+  const size_t lds = sizeof(double) * ((size_t)CH * d + CH + kFuseMaxD + (size_t)n_shards * d);
+  hipStream_t st = (hipStream_t)stream;
+  if (loss == TW_LOSS_LOGISTIC)
+    hipLaunchKernelGGL(k_sgd_step_narrow<TW_LOSS_LOGISTIC>, dim3(n_shards), dim3(kBlock), lds, st,
+                       d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, B, CH, margin, seed,
+                       d_step, (uint32_t)step_off, (uint32_t)shard_base, (int)n_shards, d_w_in,
+                       d_dw_in, d_grads_in, reg, lr, momentum, d_w_out, d_dw_out, d_grads_out);
+  else
+    hipLaunchKernelGGL(k_sgd_step_narrow<TW_LOSS_HINGE>, dim3(n_shards), dim3(kBlock), lds, st,
+                       d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, B, CH, margin, seed,
+                       d_step, (uint32_t)step_off, (uint32_t)shard_base, (int)n_shards, d_w_in,
+                       d_dw_in, d_grads_in, reg, lr, momentum, d_w_out, d_dw_out, d_grads_out);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

@@ -101,6 +101,39 @@ class SGDEngine:
         self.grads_loc = self.grads if self.G == 1 else L.empty((self.N_loc, self.d), t.float64)
         self.rows_x = self.rows_z = None
         self.step_ctr = None
+        # one launch per step (tw_sgd_step: the previous step's update fused into the gradient
+        # launch) for narrow rows on one GPU; fused=False keeps grad + update launches
+        self.fused = (self.G == 1 and not self.complete
+                      and bool(L.lib().tw_sgd_step_fusable(self.d, self.N_loc)))
+        self._slot1 = None
+
+    def _fused_steps(self, nsteps: int, draws_dev=None):
+        """nsteps steps as nsteps tw_sgd_step launches + one tw_sgd_update_to (ping-pong
+        slots for w/dw/grads; slot 0 = self.w/self.dw/self.grads holds the state before and
+        after).  Same bits as step()/step_device() + _update() per step."""
+        t = self.t
+        if self._slot1 is None:
+            self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw), t.empty_like(self.grads))
+        W, DW, Gs = zip((self.w, self.dw, self.grads), self._slot1)
+        s = L.stream_handle()
+        seed = getattr(self, "seed", 0) if draws_dev is None else 0
+        for k in range(nsteps):
+            a, b = (k - 1) & 1, k & 1
+            ix = iz = None
+            if draws_dev is not None:
+                ix, iz = draws_dev[k, 0], draws_dev[k, 1]
+            pend = k > 0
+            L.call("tw_sgd_step", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
+                   self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix), L.ptr(iz), self.N_loc,
+                   self.B, self.margin, self.loss, seed, L.ptr(self.step_ctr), k,
+                   self.shard_base, L.ptr(W[a] if pend else W[0]),
+                   L.ptr(DW[a] if pend else None), L.ptr(Gs[a] if pend else None), self.reg,
+                   self.lr, self.momentum, L.ptr(W[b] if pend else None),
+                   L.ptr(DW[b] if pend else None), L.ptr(Gs[b]), s)
+        last = (nsteps - 1) & 1
+        L.call("tw_sgd_update_to", L.ptr(W[last]), L.ptr(DW[last]), L.ptr(W[0]), L.ptr(DW[0]),
+               L.ptr(Gs[last]), self.N, self.d, self.reg, self.lr, self.momentum,
+               L.ptr(self.step_ctr), nsteps, s)
 
     def _local(self, a):
         return a[self.shard_base:self.shard_base + self.N_loc]
@@ -206,9 +239,15 @@ class SGDEngine:
             else:
                 self.step(draws_dev[st, 0], draws_dev[st, 1])
 
+        def steps():
+            if self.fused:
+                self._fused_steps(nsteps, draws_dev)
+            else:
+                for st in range(nsteps):
+                    one(st)
+
         if not graphs or self.G > 1:
-            for st in range(nsteps):
-                one(st)
+            steps()
             return
         t = self.t
         if not hasattr(self, "_replay_graphs"):
@@ -220,10 +259,12 @@ class SGDEngine:
                 nb = int(L.lib().tw_pair_grad_complete_work_bytes(self.N_loc, self.kx,
                                                                   self.kz, self.d))
                 self._cwork = L.empty((max(nb, 1),), t.uint8)
+            if self.fused and self._slot1 is None:  # allocated outside the capture
+                self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw),
+                               t.empty_like(self.grads))
             g = t.cuda.CUDAGraph()
             with t.cuda.graph(g):
-                for st in range(nsteps):
-                    one(st)
+                steps()
             self._replay_graphs[key] = g
         g.replay()
 
@@ -292,13 +333,22 @@ class SGDEngine:
         if reshuffle_first and self.layout == "partitioned":
             self.reshuffle_device()  # the exchange sizes its buffers on the host: not captured
             reshuffle_first = False
+
+        def steps(n):
+            if self.fused:
+                self._fused_steps(n)
+            else:
+                for _ in range(n):
+                    self.step_device()
+
         if not graphs or self.G > 1:
             if reshuffle_first:
                 self.reshuffle_device()
-            for _ in range(nsteps):
-                self.step_device()
+            steps(nsteps)
             return
         t = self.t
+        if self.fused and self._slot1 is None:  # allocated outside any capture
+            self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw), t.empty_like(self.grads))
         while nsteps > 0:
             n = min(nsteps, 256)
             key = (n, reshuffle_first)
@@ -313,8 +363,7 @@ class SGDEngine:
                 with t.cuda.graph(g):
                     if reshuffle_first:
                         self.reshuffle_device()
-                    for _ in range(n):
-                        self.step_device()
+                    steps(n)
                 self._graphs[key] = g
             g.replay()
             nsteps -= n
