@@ -136,11 +136,8 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
       for (int r = 0; r < R; ++r) acc[r] += pair_pred<T, PRED>(xv[r], zv);
     }
   } else {
-    int j = 0;
-    for (; j + 8 <= nz; j += 8) {  // 8 z per s_load_dwordx16
-      T zv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) zv[u] = zp[j + u];
+    // 8 z (one s_load_dwordx16) against the R x-values of every lane
+    auto group8 = [&](const T (&zv)[8]) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
 #pragma unroll
@@ -171,6 +168,34 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
         }
 #endif
       }
+    };
+    int j = 0;
+#ifndef TW_COUNT_NO_ZPIPE
+    // z loads one group ahead, two register buffers (no per-group copies on the SALU): the
+    // scalar loads of group g+1 are in flight while group g is compared.  Loads past the
+    // chunk are clamped to its last full group (in bounds, unused).
+    if (nz >= 16) {
+      T za[8], zb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) za[u] = zp[u];
+      const int last = nz - 8;
+      for (; j + 16 <= nz; j += 16) {
+        const T* qb = zp + j + 8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) zb[u] = qb[u];
+        group8(za);
+        const T* qa = zp + (j + 16 <= last ? j + 16 : last);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) za[u] = qa[u];
+        group8(zb);
+      }
+    }
+#endif
+    for (; j + 8 <= nz; j += 8) {
+      T zv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zv[u] = zp[j + u];
+      group8(zv);
     }
     for (; j < nz; ++j) {
       const T zv = zp[j];
@@ -390,13 +415,14 @@ static int64_t g_force_zchunk = 0;
 static int g_scalar_mix = 1;  // tw_count_set_scalar_mix: 0 = VALU-only accumulation
 
 // Measured pair rates (fraction of the lane-op peak on the bench shape: tools/tune_count.py,
+// profiles/r01s41_tune_zpipe.log;
 // tools/count_variants.py; profiles/r01_count_mix_sweep.log, r01_count_variants.log) used to
 // pick R: VALU-only accumulation is flat in R; the mixed VALU/SALU one is best at R = 8.
 inline double pair_rate(int R, bool mix) {
   if (!mix) return 0.465;
   switch (R) {
-    case 8: return 0.586;
-    case 4: return 0.568;
+    case 8: return 0.605;
+    case 4: return 0.582;
     case 2: return 0.504;
     default: return 0.465;
   }
