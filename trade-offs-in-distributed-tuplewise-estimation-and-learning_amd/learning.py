@@ -167,6 +167,18 @@ class SGDEngine:
         self._rows_done = t.cuda.Event()
         self._rows_done.record()
 
+    def _records(self, name, rows, expect):
+        """Persistent (rows, d+1) record buffer for the row exchange, kept across reshuffles
+        and grown with headroom only when a draw needs more: a fresh ~n*d*8-byte allocation
+        per reshuffle made the caching allocator flush and re-map (a 1 s stall at C5)."""
+        bufs = self.__dict__.setdefault("_xbufs", {})
+        b = bufs.get(name)
+        if b is None or b.shape[0] < rows:
+            bufs[name] = None  # release the old block first
+            cap = max(rows, expect + (expect // 16 if self.G > 1 else 0), 1)
+            b = bufs[name] = L.empty((cap, self.d + 1), self.t.float64)
+        return b[:max(rows, 1)]
+
     def _exchange(self, rows, k, part, own, out):
         """Partitioned layout: move the rows drawn for this rank's shards (rows: all N*k global
         row indices, shard-major) from their owners into `out` (N_loc*k, d), in draw order."""
@@ -178,7 +190,7 @@ class SGDEngine:
         start = t.cumsum(counts, 0) - counts
         sc = counts.cpu().tolist()
         total = int(sum(sc))
-        send = L.empty((max(total, 1), d + 1), t.float64)
+        send = self._records("send", total, M_q)
         cursor = L.empty((G,), t.int64)
         L.call("tw_row_pack", L.ptr(rows), M, M_q, own[0], own[1], G, L.ptr(part), d,
                L.ptr(start), L.ptr(cursor), L.ptr(send), s)
@@ -186,7 +198,7 @@ class SGDEngine:
             rcounts = t.empty_like(counts)
             self.dist.all_to_all_single(rcounts, counts, group=self.group)
             rc = rcounts.cpu().tolist()
-            recv = L.empty((max(int(sum(rc)), 1), d + 1), t.float64)
+            recv = self._records("recv", int(sum(rc)), M_q)
             self.dist.all_to_all_single(recv[:int(sum(rc))], send[:total], output_split_sizes=rc,
                                         input_split_sizes=sc, group=self.group)
             m = int(sum(rc))
