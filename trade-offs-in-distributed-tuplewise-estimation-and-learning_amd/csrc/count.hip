@@ -125,9 +125,15 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
   // wave-uniform scalar-unit counts, one per scalar-counted x-value: independent s_add chains
   // let the scheduler spread the SALU work between the compares (one shared accumulator made
   // a 16-long dependent chain at the loop end and cost ~10%)
-  unsigned sacc[NS > 0 ? NS : 1];
+#ifndef TW_NS_EXTRA
+#define TW_NS_EXTRA 0
+#endif
+  // NSE: x-values counted on the scalar unit for odd z of a group (NS for even z), so the
+  // scalar share can sit between NS/R and (NS+1)/R
+  constexpr int NSE = (NS > 0 && NS + TW_NS_EXTRA <= R) ? NS + TW_NS_EXTRA : NS;
+  unsigned sacc[NSE > 0 ? NSE : 1];
 #pragma unroll
-  for (int r = 0; r < (NS > 0 ? NS : 1); ++r) sacc[r] = 0;
+  for (int r = 0; r < (NSE > 0 ? NSE : 1); ++r) sacc[r] = 0;
   if constexpr (NS == 0) {
 #pragma unroll 8
     for (int j = 0; j < nz; ++j) {
@@ -136,18 +142,17 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
       for (int r = 0; r < R; ++r) acc[r] += pair_pred<T, PRED>(xv[r], zv);
     }
   } else {
-    // 8 z (one s_load_dwordx16) against the R x-values of every lane
-    auto group8 = [&](const T (&zv)[8]) {
+    // one z against the R x-values of every lane, NSZ of them counted on the scalar unit
+    auto one_z = [&](const T zu, auto nsz) {
+      constexpr int NSZ = decltype(nsz)::value;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (r < NS) {
-            sacc[r] += scalar_count<T, PRED>(xv[r], zv[u]);
-          } else {
-            acc[r] += pair_pred<T, PRED>(xv[r], zv[u]);
-          }
+      for (int r = 0; r < R; ++r) {
+        if (r < NSZ) {
+          sacc[r] += scalar_count<T, PRED>(xv[r], zu);
+        } else {
+          acc[r] += pair_pred<T, PRED>(xv[r], zu);
         }
+      }
 #ifndef TW_COUNT_NO_SCHED
         // interleave per z: groups of (VALU, SALU) so each wave's instruction stream alternates
         // compare and scalar-count work instead of clustering the SALU at the loop end
@@ -160,13 +165,20 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
 #endif
         constexpr int kG = TW_SCHED_G;  // groups per z
         constexpr int kM = PRED == TW_PRED_HALF ? 2 : 1;  // compares per pair
-        constexpr int kV = (kM * (2 * R - NS) + kG - 1) / kG, kS = (2 * kM * NS + kG - 1) / kG;
+        constexpr int kV = (kM * (2 * R - NSZ) + kG - 1) / kG, kS = (2 * kM * NSZ + kG - 1) / kG;
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x002, kV, 0);
           __builtin_amdgcn_sched_group_barrier(0x004, kS, 0);
         }
 #endif
+    };
+    // 8 z (one s_load_dwordx16)
+    auto group8 = [&](const T (&zv)[8]) {
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        one_z(zv[u], std::integral_constant<int, NS>{});
+        one_z(zv[u + 1], std::integral_constant<int, NSE>{});
       }
     };
     int j = 0;
@@ -215,7 +227,7 @@ __device__ __forceinline__ unsigned long long count_item(const T* __restrict__ x
   tot = wave_sum_u64(tot);
   unsigned long long stot = 0;
 #pragma unroll
-  for (int r = 0; r < NS; ++r) stot += sacc[r];
+  for (int r = 0; r < NSE; ++r) stot += sacc[r];
   return tot + stot;
 }
 
