@@ -7,6 +7,24 @@
 
 namespace tw {
 
+// v / d for the exchange's rank arithmetic (v < G*n_loc < 2^53, d = n_loc >= 1): one f64
+// multiply by the reciprocal and an exact integer correction, instead of the ~50-instruction
+// 64-bit division sequence — the exchange kernels run beside the VALU-bound count kernel and
+// every instruction they issue is taken from it.
+struct FastDiv {
+  uint64_t d;
+  double inv;
+};
+
+__host__ __device__ inline FastDiv make_fastdiv(uint64_t d) { return FastDiv{d, 1.0 / (double)d}; }
+
+__host__ __device__ inline uint64_t fast_div(uint64_t v, const FastDiv& f) {
+  uint64_t q = (uint64_t)((double)v * f.inv);
+  while (q * f.d > v) --q;            // the product is within one of v / d for v < 2^53
+  while ((q + 1) * f.d <= v) ++q;
+  return q;
+}
+
 struct Feistel {
   uint32_t half_bits;
   uint32_t mask;

@@ -143,16 +143,17 @@ __global__ __launch_bounds__(kBlock) void k_exchange_counts(int64_t n_loc, int64
     for (int i = threadIdx.x; i < 2 * G; i += kBlock) cursor[i] = 0;
   __syncthreads();
   const uint64_t NX = (uint64_t)n_loc * G, NZ = (uint64_t)m_loc * G;
+  const FastDiv dx = make_fastdiv((uint64_t)n_loc), dz = make_fastdiv((uint64_t)m_loc);
   for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < n_loc + m_loc;
        e += (int64_t)gridDim.x * kBlock) {
     if (e < n_loc) {
       const uint64_t g = (uint64_t)(xbase + e);
-      atomicAdd(&h[(int)(feistel_perm(fx, g, NX) / (uint64_t)n_loc)], 1u);
-      atomicAdd(&h[G + (int)(feistel_perm_inv(fx, g, NX) / (uint64_t)n_loc)], 1u);
+      atomicAdd(&h[(int)fast_div(feistel_perm(fx, g, NX), dx)], 1u);
+      atomicAdd(&h[G + (int)fast_div(feistel_perm_inv(fx, g, NX), dx)], 1u);
     } else {
       const uint64_t g = (uint64_t)(zbase + e - n_loc);
-      atomicAdd(&h[2 * G + (int)(feistel_perm(fz, g, NZ) / (uint64_t)m_loc)], 1u);
-      atomicAdd(&h[3 * G + (int)(feistel_perm_inv(fz, g, NZ) / (uint64_t)m_loc)], 1u);
+      atomicAdd(&h[2 * G + (int)fast_div(feistel_perm(fz, g, NZ), dz)], 1u);
+      atomicAdd(&h[3 * G + (int)fast_div(feistel_perm_inv(fz, g, NZ), dz)], 1u);
     }
   }
   __syncthreads();
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(kBlock) void k_exchange_pack(
     }
   }
   const uint64_t NX = (uint64_t)n_loc * G, NZ = (uint64_t)m_loc * G;
+  const FastDiv dx = make_fastdiv((uint64_t)n_loc), dz = make_fastdiv((uint64_t)m_loc);
   const int64_t tot = n_loc + m_loc;
   for (int64_t c0 = (int64_t)blockIdx.x * kScatChunk; c0 < tot;
        c0 += (int64_t)gridDim.x * kScatChunk) {
@@ -191,12 +193,12 @@ __global__ __launch_bounds__(kBlock) void k_exchange_pack(
       bucket[k] = -1;
       if (e < n_loc) {
         const int64_t p = (int64_t)feistel_perm(fx, (uint64_t)(xbase + e), NX);
-        const int dst = (int)(p / n_loc);
+        const int dst = (int)fast_div((uint64_t)p, dx);
         bucket[k] = dst;
         pos[k] = p - (int64_t)dst * n_loc;
       } else if (e < tot) {
         const int64_t p = (int64_t)feistel_perm(fz, (uint64_t)(zbase + e - n_loc), NZ);
-        const int dst = (int)(p / m_loc);
+        const int dst = (int)fast_div((uint64_t)p, dz);
         bucket[k] = G + dst;
         pos[k] = p - (int64_t)dst * m_loc + n_loc;  // Z follows X in the receive buffer
       }
