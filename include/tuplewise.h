@@ -331,6 +331,20 @@ int tw_exchange_counts(int64_t n_loc, int64_t m_loc, int32_t rank, int32_t G, ui
 int tw_exchange_pack(const void* d_x, int64_t n_loc, const void* d_z, int64_t m_loc, int32_t rank,
                      int32_t G, uint64_t key_x, uint64_t key_z, const uint64_t* d_counts,
                      uint64_t* d_cursor, void* d_send, void* stream);
+/* Fixed-capacity variant (the default exchange of ShardedSample): ONE forward-permutation pass,
+ * no count pass and no host round trip.  d_send holds G buckets of (1 + cap) records: bucket g =
+ * [header {count, 0} | records {value bits, position at rank g (Z offset by n_loc)}], so the
+ * all-to-all is an equal-split one (G*(1+cap) records each way).  d_cursor (G uint64) must be
+ * zero on the first call; it is left zero for the next.  A bucket over cap sets *d_flag (the
+ * records past cap are dropped): the caller must check the flag before using the result.
+ * tw_scatter_buckets: for every received bucket, d_out[pos] = value for its first
+ * min(header, cap) records; a header over cap or a position outside [0, n_out) sets *d_flag.
+ * Replaces the same reference loop as tw_exchange_pack (compute_stats.py:64-67 per rank). */
+int tw_exchange_pack_fixed(const void* d_x, int64_t n_loc, const void* d_z, int64_t m_loc,
+                           int32_t rank, int32_t G, uint64_t key_x, uint64_t key_z, int64_t cap,
+                           uint64_t* d_cursor, void* d_send, int32_t* d_flag, void* stream);
+int tw_scatter_buckets(const void* d_recv, int32_t G, int64_t cap, void* d_out, int64_t n_out,
+                       int32_t* d_flag, void* stream);
 
 /* ---- (e): row exchange for the row-partitioned learning layout ------------------------
  * Replaces the row copies of SWR_divide (compute_stats.py:48-54) when X is split by rows over

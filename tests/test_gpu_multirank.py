@@ -71,7 +71,7 @@ def test_learning_two_ranks_equals_one(gpu, mode, layout):
     assert np.array_equal(got, np.stack(ref))
 
 
-def _est_worker(rank, port, G, q):
+def _est_worker(rank, port, G, q, exchange="fixed"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -84,15 +84,17 @@ def _est_worker(rank, port, G, q):
     Z = rng.normal(0, 1, G * n_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(),
                       torch.from_numpy(Z[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(), N,
-                      group=dist.group.WORLD)
+                      group=dist.group.WORLD, exchange=exchange)
     vals = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
+    vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # the side-stream pipeline
     if rank == 0:
         q.put(vals)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_sharded_sample_two_ranks_equals_one(gpu):
+@pytest.mark.parametrize("exchange", ["fixed", "exact"])
+def test_sharded_sample_two_ranks_equals_one(gpu, exchange):
     import torch
     import torch.multiprocessing as mp
     from tuplewise.device import ShardedSample
@@ -102,10 +104,11 @@ def test_sharded_sample_two_ranks_equals_one(gpu):
     Z = rng.normal(0, 1, G * n_loc)
     S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), G * N)
     want = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
+    want += [float(v) for v in S.UnN_many([5, 6, 7])]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q)) for r in range(G)]
+    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q, exchange)) for r in range(G)]
     for pr in procs:
         pr.start()
     got = q.get(timeout=300)

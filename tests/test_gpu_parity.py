@@ -527,6 +527,58 @@ def test_fused_exchange_kernels_simulated_ranks(gpu):
         assert np.array_equal(o[n_loc:], want_z[q * m_loc:(q + 1) * m_loc])
 
 
+@pytest.mark.parametrize("G,n_loc,m_loc", [(3, 20_011, 7_003), (5, 1_000, 3), (2, 1, 1)])
+def test_fixed_exchange_kernels_simulated_ranks(gpu, G, n_loc, m_loc):
+    """tw_exchange_pack_fixed / tw_scatter_buckets (the default multi-rank exchange) for G
+    ranks simulated in one process: bucket headers equal the oracle's forward-permutation
+    histograms, the equal-split all-to-all is done on the host, and after the scatter both
+    samples equal the oracle's global permutations; a capacity below a bucket's size raises
+    the flag on both sides (never a silent drop)."""
+    import torch
+    from tuplewise.device import HipOps
+    ops = HipOps()
+    kx, kz = 101, 202
+    rng = np.random.RandomState(5)
+    X, Z = rng.normal(size=G * n_loc), rng.normal(size=G * m_loc)
+    want_x, want_z = O.permute_scatter(X, kx), O.permute_scatter(Z, kz)
+    tot = n_loc + m_loc
+    for cap in (max(1, min(tot, tot // G + tot // (8 * G) + 1024)), None):
+        hist = np.zeros((G, G), dtype=np.int64)  # [source, destination]
+        for r in range(G):
+            gx, gz = np.arange(r * n_loc, (r + 1) * n_loc), np.arange(r * m_loc, (r + 1) * m_loc)
+            hist[r] = (np.bincount(O.feistel_perm(gx, G * n_loc, kx) // n_loc, minlength=G) +
+                       np.bincount(O.feistel_perm(gz, G * m_loc, kz) // m_loc, minlength=G))
+        over = cap is None
+        if over:
+            cap = int(hist.max()) - 1  # one bucket too small
+            if cap < 1:
+                continue
+        sends = []
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        cursor = torch.zeros(G, dtype=torch.int64, device="cuda")
+        for r in range(G):
+            send = torch.empty((G * (cap + 1), 2), dtype=torch.int64, device="cuda")
+            ops.exchange_pack_fixed(torch.from_numpy(X[r * n_loc:(r + 1) * n_loc]).cuda(),
+                                    torch.from_numpy(Z[r * m_loc:(r + 1) * m_loc]).cuda(), r, G,
+                                    kx, kz, cap, cursor, send, flag)
+            s = send.cpu().numpy().reshape(G, cap + 1, 2)
+            assert np.array_equal(s[:, 0, 0], hist[r])
+            assert not cursor.cpu().numpy().any()  # left zero for the next repartition
+            sends.append(s)
+        assert bool(flag.item()) == over
+        for q in range(G):
+            recv = np.concatenate([sends[r][q] for r in range(G)])  # equal-split all-to-all
+            out = torch.zeros(tot, dtype=torch.float64, device="cuda")
+            rflag = torch.zeros(1, dtype=torch.int32, device="cuda")
+            ops.scatter_buckets(torch.from_numpy(np.ascontiguousarray(recv)).cuda(), G, cap,
+                                out, rflag)
+            assert bool(rflag.item()) == (over and bool((hist[:, q] > cap).any()))
+            if not over:
+                o = out.cpu().numpy()
+                assert np.array_equal(o[:n_loc], want_x[q * n_loc:(q + 1) * n_loc])
+                assert np.array_equal(o[n_loc:], want_z[q * m_loc:(q + 1) * m_loc])
+
+
 @pytest.mark.parametrize("loss", ["hinge", "logistic"])
 @pytest.mark.parametrize("d,kx,kz", [(1, 300, 77), (10, 500, 64), (100, 1300, 5000),
                                      (512, 257, 300)])

@@ -78,6 +78,9 @@ _SIGNATURES = {
     "tw_exchange_set_grid": [_i32],
     "tw_exchange_counts": [_i64, _i64, _i32, _i32, _u64, _u64, _vp, _vp, _vp],
     "tw_exchange_pack": [_vp, _i64, _vp, _i64, _i32, _i32, _u64, _u64, _vp, _vp, _vp, _vp],
+    "tw_exchange_pack_fixed": [_vp, _i64, _vp, _i64, _i32, _i32, _u64, _u64, _i64, _vp, _vp, _vp,
+                               _vp],
+    "tw_scatter_buckets": [_vp, _i32, _i64, _vp, _i64, _vp, _vp],
     "tw_row_route_counts": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
     "tw_row_pack": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "tw_row_unpack": [_vp, _i64, _i64, _vp, _vp],

@@ -221,6 +221,103 @@ __global__ __launch_bounds__(kBlock) void k_exchange_pack(
   }
 }
 
+// ---- fixed-capacity exchange: no split sizes on the host, ONE Feistel pass per element.
+// The send buffer is G buckets of (1 + cap) 16-byte records; bucket g = [header {count, 0} |
+// up to cap records {value bits, position at g}], X and Z records mixed (Z positions offset by
+// n_loc).  Equal-size buckets make the all-to-all a plain equal-split one whose sizes every rank
+// knows, so a repartition needs no count pass, no inverse permutation and no host round trip.
+// cap is the expected bucket size (n_loc + m_loc) / G plus a margin of dozens of standard
+// deviations; a bucket that would overflow sets *flag (records past cap are dropped) and the
+// host refuses the result.
+__global__ __launch_bounds__(kBlock) void k_exchange_pack_fixed(
+    const uint64_t* __restrict__ xv, int64_t n_loc, const uint64_t* __restrict__ zv,
+    int64_t m_loc, int64_t xbase, int64_t zbase, int G, Feistel fx, Feistel fz, int64_t cap,
+    unsigned long long* __restrict__ cursor, uint64_t* __restrict__ send, int* __restrict__ flag) {
+  __shared__ unsigned int lcnt[kMaxG];
+  __shared__ int64_t lbase[kMaxG];
+  const uint64_t NX = (uint64_t)n_loc * G, NZ = (uint64_t)m_loc * G;
+  const FastDiv dx = make_fastdiv((uint64_t)n_loc), dz = make_fastdiv((uint64_t)m_loc);
+  const int64_t tot = n_loc + m_loc, bsz = cap + 1;
+  for (int64_t c0 = (int64_t)blockIdx.x * kScatChunk; c0 < tot;
+       c0 += (int64_t)gridDim.x * kScatChunk) {
+    for (int i = threadIdx.x; i < G; i += kBlock) lcnt[i] = 0;
+    __syncthreads();
+    int dst[kScatPer];
+    unsigned slot[kScatPer];
+    int64_t pos[kScatPer];
+#pragma unroll
+    for (int k = 0; k < kScatPer; ++k) {
+      const int64_t e = c0 + k * kBlock + threadIdx.x;
+      dst[k] = -1;
+      if (e < n_loc) {
+        const uint64_t p = feistel_perm(fx, (uint64_t)(xbase + e), NX);
+        dst[k] = (int)fast_div(p, dx);
+        pos[k] = (int64_t)p - (int64_t)dst[k] * n_loc;
+      } else if (e < tot) {
+        const uint64_t p = feistel_perm(fz, (uint64_t)(zbase + e - n_loc), NZ);
+        dst[k] = (int)fast_div(p, dz);
+        pos[k] = (int64_t)p - (int64_t)dst[k] * m_loc + n_loc;
+      }
+      if (dst[k] >= 0) slot[k] = atomicAdd(&lcnt[dst[k]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G; i += kBlock)
+      if (lcnt[i]) lbase[i] = (int64_t)atomicAdd(cursor + i, (unsigned long long)lcnt[i]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScatPer; ++k) {
+      if (dst[k] >= 0) {
+        const int64_t o = lbase[dst[k]] + slot[k];
+        if (o < cap) {
+          const int64_t e = c0 + k * kBlock + threadIdx.x;
+          uint64_t* r = send + 2 * (dst[k] * bsz + 1 + o);
+          r[0] = e < n_loc ? xv[e] : zv[e - n_loc];
+          r[1] = (uint64_t)pos[k];
+        } else {
+          *flag = 1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Bucket headers from the cursors (then zeroed for the next repartition).
+__global__ void k_exchange_seal(int G, int64_t cap, unsigned long long* __restrict__ cursor,
+                                uint64_t* __restrict__ send, int* __restrict__ flag) {
+  const int g = threadIdx.x;
+  if (g < G) {
+    const unsigned long long c = cursor[g];
+    send[2 * (g * (cap + 1))] = c;
+    send[2 * (g * (cap + 1)) + 1] = 0;
+    cursor[g] = 0;
+    if (c > (unsigned long long)cap) *flag = 1;
+  }
+}
+
+// Receive side: bucket g's first min(header, cap) records, out[pos] = value.  A header past cap
+// or a position outside [0, n_out) flags the exchange instead of writing.
+__global__ __launch_bounds__(kBlock) void k_scatter_buckets(const uint64_t* __restrict__ recv,
+                                                            int G, int64_t cap,
+                                                            uint64_t* __restrict__ out,
+                                                            int64_t n_out, int* __restrict__ flag) {
+  const int64_t bsz = cap + 1, tot = (int64_t)G * cap;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t g = i / cap, r = i - g * cap;
+    const uint64_t c = recv[2 * (g * bsz)];
+    if (c > (uint64_t)cap) *flag = 1;
+    if ((uint64_t)r < c && r < cap) {
+      const uint64_t* q = recv + 2 * (g * bsz + 1 + r);
+      const uint64_t p = q[1];
+      if (p < (uint64_t)n_out)
+        out[p] = q[0];
+      else
+        *flag = 1;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_scatter_records(const uint64_t* __restrict__ rec,
                                                             int64_t m, uint64_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < m;
@@ -374,6 +471,41 @@ extern "C" int tw_exchange_pack(const void* d_x, int64_t n_loc, const void* d_z,
                      n_loc, (const uint64_t*)d_z, m_loc, (int64_t)rank * n_loc,
                      (int64_t)rank * m_loc, (int)G, fx, fz, (const unsigned long long*)d_counts,
                      (unsigned long long*)d_cursor, (uint64_t*)d_send);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_exchange_pack_fixed(const void* d_x, int64_t n_loc, const void* d_z,
+                                      int64_t m_loc, int32_t rank, int32_t G, uint64_t key_x,
+                                      uint64_t key_z, int64_t cap, uint64_t* d_cursor,
+                                      void* d_send, int32_t* d_flag, void* stream) {
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && rank >= 0 && rank < G && n_loc >= 1 && m_loc >= 1 &&
+                   n_loc * (int64_t)G < (1ll << 52) && m_loc * (int64_t)G < (1ll << 52) &&
+                   cap >= 1 && cap <= n_loc + m_loc,
+               "tw_exchange_pack_fixed: bad sizes");
+  TW_ARG_CHECK(d_x && d_z && d_cursor && d_send && d_flag, "tw_exchange_pack_fixed: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const Feistel fx = make_feistel(n_loc * (int64_t)G, key_x);
+  const Feistel fz = make_feistel(m_loc * (int64_t)G, key_z);
+  const int blocks = (int)std::min<int64_t>(exchange_grid(256 * 4), ceil_div(n_loc + m_loc, kScatChunk));
+  hipLaunchKernelGGL(k_exchange_pack_fixed, dim3(blocks), dim3(kBlock), 0, st,
+                     (const uint64_t*)d_x, n_loc, (const uint64_t*)d_z, m_loc,
+                     (int64_t)rank * n_loc, (int64_t)rank * m_loc, (int)G, fx, fz, cap,
+                     (unsigned long long*)d_cursor, (uint64_t*)d_send, (int*)d_flag);
+  TW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_exchange_seal, dim3(1), dim3(kMaxG), 0, st, (int)G, cap,
+                     (unsigned long long*)d_cursor, (uint64_t*)d_send, (int*)d_flag);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_scatter_buckets(const void* d_recv, int32_t G, int64_t cap, void* d_out,
+                                  int64_t n_out, int32_t* d_flag, void* stream) {
+  TW_ARG_CHECK(G >= 1 && G <= kMaxG && cap >= 1 && n_out >= 0 && d_recv && d_out && d_flag,
+               "tw_scatter_buckets: bad arguments");
+  const int blocks = (int)std::min<int64_t>(exchange_grid(256 * 8), ceil_div((int64_t)G * cap, kBlock));
+  hipLaunchKernelGGL(k_scatter_buckets, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const uint64_t*)d_recv, (int)G, cap, (uint64_t*)d_out, n_out, (int*)d_flag);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

@@ -98,6 +98,17 @@ class HipOps:
                L.ptr(send), L.stream_handle())
         return send
 
+    def exchange_pack_fixed(self, X, Z, rank, G, key_x, key_z, cap, cursor, send, flag):
+        L.call("tw_exchange_pack_fixed", L.ptr(X), int(X.numel()), L.ptr(Z), int(Z.numel()),
+               int(rank), int(G), int(key_x), int(key_z), int(cap), L.ptr(cursor), L.ptr(send),
+               L.ptr(flag), L.stream_handle())
+        return send
+
+    def scatter_buckets(self, recv, G, cap, out, flag):
+        L.call("tw_scatter_buckets", L.ptr(recv), int(G), int(cap), L.ptr(out), int(out.numel()),
+               L.ptr(flag), L.stream_handle())
+        return out
+
     def scatter_records(self, rec, out):
         L.call("tw_scatter_records", L.ptr(rec), int(rec.shape[0]), L.ptr(out),
                L.stream_handle())
@@ -151,10 +162,17 @@ class ShardedSample:
     group: a torch.distributed process group (None = single process).
     tie_mode: "strict" (reference) or "half" (ties score 1/2).
     algo: "pairs" (all-pairs compare kernel), "sorted" (sort + binary search, same integers),
-    "auto" (sorted for large shards)."""
+    "auto" (sorted for large shards).
+    exchange (several ranks): "fixed" (equal-size buckets, one permutation pass, no host round
+    trip per repartition) or "exact" (counted buckets: a count pass, the inverse permutation and
+    a host copy of the split sizes).  Both give the same arrays."""
 
     def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None,
-                 algo: str = "auto"):
+                 algo: str = "auto", exchange: str = "fixed"):
+        if exchange not in ("fixed", "exact"):
+            raise ValueError(f"exchange must be 'fixed' or 'exact', not {exchange!r}")
+        self.exchange = exchange
+        self._xf = None
         self.ops = ops if ops is not None else HipOps()
         t = L.torch()
         self.t = t
@@ -199,6 +217,15 @@ class ShardedSample:
         (perm_index, rank/source histograms, bucket scatter) does the same in steps."""
         t, dist, G, r, ops = self.t, self.dist, self.G, self.rank, self.ops
         n, m = self.n_loc, self.m_loc
+        if self.exchange == "fixed" and hasattr(ops, "exchange_pack_fixed"):
+            xf = self._fixed_buffers()
+            ops.exchange_pack_fixed(self.X, self.Z, r, G, key_x, key_z, xf["cap"], xf["cursor"],
+                                    xf["send"], xf["flag"])
+            dist.all_to_all_single(xf["recv"], xf["send"], group=self.group)
+            XZ = t.empty((n + m,), dtype=self.X.dtype, device=self.X.device)
+            ops.scatter_buckets(xf["recv"], G, xf["cap"], XZ, xf["flag"])
+            self.X, self.Z = XZ[:n], XZ[n:]
+            return
         if hasattr(ops, "exchange_counts"):  # fused: two launches, no permutation array
             cnt, cursor = ops.exchange_counts(n, m, r, G, key_x, key_z)
             send = ops.exchange_pack(self.X, self.Z, r, G, key_x, key_z, cnt, cursor)
@@ -218,6 +245,29 @@ class ShardedSample:
         ops.bucket_scatter(pz, self.Z, m, G, start_z, send, n)  # Z positions follow X's
         c = cnt.cpu().numpy()
         return self._exchange_records(send, c)
+
+    def _fixed_buffers(self):
+        """Persistent buffers of the fixed-capacity exchange.  A bucket (records of one source
+        rank for one destination) holds (n_loc + m_loc) / G records on average, with a
+        hypergeometric spread of about sqrt of that; cap adds 1/8 + 1024 (dozens of standard
+        deviations at any size), and an overflow is detected, never silently dropped."""
+        if self._xf is None:
+            t, G = self.t, self.G
+            tot = self.n_loc + self.m_loc
+            cap = max(1, min(tot, tot // G + tot // (8 * G) + 1024))
+            dev = self.X.device
+            self._xf = {"cap": cap,
+                        "cursor": t.zeros((G,), dtype=t.int64, device=dev),
+                        "flag": t.zeros((1,), dtype=t.int32, device=dev),
+                        "send": t.empty((G * (cap + 1), 2), dtype=t.int64, device=dev),
+                        "recv": t.empty((G * (cap + 1), 2), dtype=t.int64, device=dev)}
+        return self._xf
+
+    def check_exchange(self):
+        """Raise if a fixed-capacity repartition overflowed a bucket (host sync)."""
+        if self._xf is not None and int(self._xf["flag"].item()):
+            raise RuntimeError("repartition: an exchange bucket overflowed its capacity; the "
+                               "arrays are invalid (use ShardedSample(..., exchange='exact'))")
 
     def _exchange_records(self, send, c):
         """All-to-all of the packed records (split sizes from the (4, G) host counts) and the
@@ -270,6 +320,7 @@ class ShardedSample:
         counts: (G*N,) or (T, G*N); returns an array of the same rank.  pairs: the pairs per
         shard (default: all pairs of each shard; B for the incomplete statistic)."""
         c = np.asarray(counts.cpu().numpy()).view(np.uint64)
+        self.check_exchange()
         keep = np.tile(self.keep, self.G)
         scale = 2 if self.tie_mode == "half" else 1
         per = np.tile(self.pairs, self.G) if pairs is None else [pairs] * (self.G * self.N)
@@ -333,11 +384,22 @@ class ShardedSample:
                 with t.cuda.stream(side):
                     self.repartition(k)
 
+            # all-pairs counts go into one buffer zeroed up front: one count launch per step
+            # on main, no per-step fill kernel between the counts
+            pre = None
+            if fusable and hasattr(self.ops, "count_step"):
+                pre = t.zeros((len(keys), self.N), dtype=t.int64, device=self.X.device)
             side.wait_stream(main)
             repartition_on_side(keys[0])
             for i in range(len(keys)):
                 main.wait_stream(side)  # repartition i (only it is queued on side so far)
-                local.append(count_local(i))
+                if pre is not None:
+                    self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                        self.max_nx, self.max_nz, self.dtype, self.pred, pre[i],
+                                        None, 0, None, 0, None)
+                    local.append(pre[i])
+                else:
+                    local.append(count_local(i))
                 self.X.record_stream(main)  # allocated on side, read by this count on main
                 self.Z.record_stream(main)
                 if i + 1 < len(keys):
