@@ -6,7 +6,9 @@ one all-to-all of {value, position} records for X and Z together, scatter, zero-
 all-reduce of per-shard counts, host np.mean) runs at world size 2 and 4 with
 gloo, with the device operations replaced by their oracle restatements (test-only).  Checks:
 the permuted global arrays equal the single-process permutation, and the estimate is
-bit-identical to the G = 1 result — the G-invariance the design promises.
+bit-identical to the G = 1 result — the G-invariance the design promises.  Three exchange
+protocols: step-by-step primitives, the counted fused exchange, and the fixed-capacity one
+(equal-split all-to-all, the default).
 """
 import os
 import socket
@@ -101,6 +103,46 @@ class OracleOpsFused(OracleOps):
         return torch.from_numpy(np.stack([val[order], pos[order]], axis=1))
 
 
+class OracleOpsFixed(OracleOps):
+    """Adds the fixed-capacity exchange (tw_exchange_pack_fixed / tw_scatter_buckets, the
+    default of ShardedSample) restated: equal buckets of 1 + cap records, a count header each,
+    an equal-split all-to-all, overflow flagged."""
+
+    def exchange_pack_fixed(self, X, Z, rank, G, key_x, key_z, cap, cursor, send, flag):
+        n_loc, m_loc = X.numel(), Z.numel()
+        dst, val, pos = [], [], []
+        for A, n, key, base in ((X, n_loc, key_x, 0), (Z, m_loc, key_z, n_loc)):
+            p = O.feistel_perm(np.arange(rank * n, (rank + 1) * n), G * n, key)
+            dst.append(p // n)
+            val.append(A.numpy().view(np.int64))
+            pos.append(p - (p // n) * n + base)
+        dst, val, pos = np.concatenate(dst), np.concatenate(val), np.concatenate(pos)
+        b = send.numpy().reshape(G, cap + 1, 2)
+        for g in range(G):
+            sel = np.flatnonzero(dst == g)
+            b[g, 0] = (len(sel), 0)
+            if len(sel) > cap:
+                flag.numpy()[0] = 1
+                sel = sel[:cap]
+            b[g, 1:1 + len(sel), 0] = val[sel]
+            b[g, 1:1 + len(sel), 1] = pos[sel]
+        return send
+
+    def scatter_buckets(self, recv, G, cap, out, flag):
+        o = out.numpy().view(np.int64)
+        b = recv.numpy().reshape(G, cap + 1, 2)
+        for g in range(G):
+            c = int(b[g, 0, 0])
+            if c > cap:
+                flag.numpy()[0] = 1
+            r = b[g, 1:1 + min(c, cap)]
+            o[r[:, 1]] = r[:, 0]
+        return out
+
+
+_OPS = {"plain": OracleOps, "fused": OracleOpsFused, "fixed": OracleOpsFixed}
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -119,7 +161,7 @@ def _worker(rank, G, port, n_loc, m_loc, N, keys, B, q, fused):
     X, Z = _global_data(G, n_loc, m_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
                       torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
-                      group=dist.group.WORLD, ops=OracleOpsFused() if fused else OracleOps())
+                      group=dist.group.WORLD, ops=_OPS[fused]())
     vals = [float(S.UnN(k)) for k in keys]
     inc = float(S.UnNB(B, seed=77))
     Xg = [torch.empty_like(S.X) for _ in range(G)]
@@ -132,8 +174,8 @@ def _worker(rank, G, port, n_loc, m_loc, N, keys, B, q, fused):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fused", [False, True])
-@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("G,fused", [(G, f) for G in (2, 4) for f in ("plain", "fused", "fixed")]
+                         + [(8, "fixed")])  # 8 = the driver's scaling run, default protocol
 def test_multirank_repartition_is_G_invariant(G, fused):
     import tuplewise  # noqa: F401  (package import only; no device work in this test)
     from tuplewise.device import ShardedSample
