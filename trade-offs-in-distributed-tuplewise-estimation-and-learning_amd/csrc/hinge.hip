@@ -414,8 +414,9 @@ __global__ __launch_bounds__(kBlock) void k_swr_rows(int64_t* __restrict__ rows,
 // d_step (optional): the device-RNG step counter, advanced once per update.
 // One block per kUpdCols columns: shard rows are staged in LDS (coalesced), then one thread
 // per column adds them in shard order — the sequential order of np.mean(axis=0).
-constexpr int kUpdCols = 16;
-constexpr int kUpdRows = 512;  // shard rows staged per pass: 512 x 16 doubles = 64 KiB
+constexpr int kUpdCols = 8;     // d = 512: 64 blocks
+constexpr int kUpdRows = 1024;  // shard rows staged per pass: 1024 x 8 doubles = 64 KiB
+constexpr int kUpdBatch = 16;   // staging loads in flight per thread
 // w_in/dw_in may equal w/dw (in place); step_inc: how far the step counter advances.
 __global__ __launch_bounds__(kBlock) void k_sgd_update(const double* w_in, const double* dw_in,
                                                        double* w, double* dw,
@@ -432,9 +433,21 @@ __global__ __launch_bounds__(kBlock) void k_sgd_update(const double* w_in, const
   for (int s0 = 0; s0 < n_shards; s0 += kUpdRows) {
     const int ns = std::min(kUpdRows, n_shards - s0);
     __syncthreads();
-    for (int e = threadIdx.x; e < ns * kUpdCols; e += kBlock) {
-      const int r = e / kUpdCols, c = e - r * kUpdCols;
-      tile[e] = c < nc ? grads[(int64_t)(s0 + r) * d + j0 + c] : 0.0;
+    // batches of kUpdBatch independent loads per thread, then the LDS stores (a load-store
+    // loop waited for every load in turn: 10 us for the C5 update, 256 shards x 512 columns)
+    for (int e0 = 0; e0 < ns * kUpdCols; e0 += kBlock * kUpdBatch) {
+      double v[kUpdBatch];
+#pragma unroll
+      for (int u = 0; u < kUpdBatch; ++u) {
+        const int e = e0 + u * kBlock + threadIdx.x;
+        const int r = e / kUpdCols, c = e - r * kUpdCols;
+        v[u] = (e < ns * kUpdCols && c < nc) ? grads[(int64_t)(s0 + r) * d + j0 + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kUpdBatch; ++u) {
+        const int e = e0 + u * kBlock + threadIdx.x;
+        if (e < ns * kUpdCols) tile[e] = v[u];
+      }
     }
     __syncthreads();
     if (threadIdx.x < nc) {  // shard order kept; 8 LDS reads in flight per batch
