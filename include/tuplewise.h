@@ -234,8 +234,9 @@ int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int
                       int64_t kx, const int64_t* d_rows_z, int64_t kz, int32_t n_shards,
                       int64_t B, const double* d_w, double margin, uint64_t seed,
                       const uint64_t* d_step, int32_t shard_base, double* d_out, void* stream);
-/* Tuning hook: 1 selects the unpipelined kernel for 32 < d <= 512 rows too (the pipelined
- * one is the default, 0).  Process-global; both give identical bits. */
+/* Tuning hook for 32 < d <= 512 rows: 0 = the streaming kernel (default: two register stages,
+ * 16-pair chunks), 1 = the unpipelined kernel, 2 = the burst-pipelined kernel (32-pair chunks).
+ * Process-global; all give identical bits. */
 int tw_hinge_set_variant(int32_t legacy_wide);
 int tw_pair_grad_rng(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
                      int64_t kx, const int64_t* d_rows_z, int64_t kz, int32_t n_shards, int64_t B,

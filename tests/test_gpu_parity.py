@@ -361,11 +361,12 @@ def test_exchange_kernels_simulated_ranks(gpu):
 
 @pytest.mark.parametrize("loss", ["hinge", "logistic"])
 @pytest.mark.parametrize("d,B", [(10, 300), (33, 100), (100, 1500), (512, 100), (512, 2100),
-                                 (700, 64)])
+                                 (512, 16), (512, 17), (512, 48), (700, 64)])
 def test_hinge_grad_wide_rows(gpu, d, B, loss):
-    """tw_hinge_grad for wide rows (the pipelined kernel for 32 < d <= 512, the unpipelined one
-    above): per-shard gradients vs the restated reference body (compute_stats.py:153-162), and
-    both wide kernels bit-identical to each other."""
+    """tw_hinge_grad for wide rows (the streaming kernel for 32 < d <= 512 — chunk counts
+    odd/even/partial via B = 16, 17, 48, 100 —, the burst-pipelined and unpipelined ones):
+    per-shard gradients vs the restated reference body (compute_stats.py:153-162), and all wide
+    kernels bit-identical to each other."""
     import torch
     from tuplewise import _lib as L, _learn
     rng = np.random.RandomState(d + B)
@@ -379,7 +380,7 @@ def test_hinge_grad_wide_rows(gpu, d, B, loss):
     iz = rng.randint(0, kz, size=(N, B))
     dev = [L.to_device(a) for a in (X, Z, rows_x, rows_z, ix, iz, w)]
     outs = []
-    for legacy in (0, 1):
+    for legacy in (0, 1, 2):
         L.call("tw_hinge_set_variant", legacy)
         try:
             g = _learn.hinge_grads_device(dev[0], dev[1], d, dev[2], kx, dev[3], kz, dev[4],
@@ -387,7 +388,7 @@ def test_hinge_grad_wide_rows(gpu, d, B, loss):
         finally:
             L.call("tw_hinge_set_variant", 0)
         outs.append(g.cpu().numpy())
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
     for s in range(N):
         diff = Z[rows_z[s][iz[s]]] - X[rows_x[s][ix[s]]]
         want = O.pair_grad(diff, w.reshape(-1, 1), 1.0, B, loss).ravel()

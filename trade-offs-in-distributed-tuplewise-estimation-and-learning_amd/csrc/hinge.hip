@@ -268,6 +268,117 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
   if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
 }
 
+// Streaming variant of k_hinge_grad_wide (the default for 32 < d <= 512): one pair per wave
+// per chunk (16-pair chunks) and TWO register stages, so the rows of chunks k+1 and k+2 are
+// in flight while chunk k is reduced — the loads form a continuous stream instead of one
+// 32-pair burst per chunk that drains HBM before the next is issued.  Diff rows and weights are
+// double-buffered in LDS (2 x 16 rows): chunk k+1 writes the buffer chunk k-1's sums read,
+// which every thread finished before chunk k's barrier.  Same arithmetic and order as
+// k_hinge_grad_wide (per pair: lane partial dots over the same 8 columns + the same butterfly;
+// column sums in row order), so identical bits.
+constexpr int kStreamCH = kWideBlock / kWave;  // 16 pairs per chunk
+
+template <int LOSS>
+__global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
+    const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
+    const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
+    int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
+    const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
+    const uint64_t* __restrict__ d_step, uint32_t shard_base) {
+  __shared__ double diff[2][kStreamCH * kWideMaxD];  // 128 KiB
+  __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
+  __shared__ double flag[2][kStreamCH];
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int dd = (int)d;
+  const uint64_t step = d_step ? *d_step : 0;
+  double wv[kWideCols];
+#pragma unroll
+  for (int c = 0; c < kWideCols; ++c) {
+    const int j = lane + c * kWave;
+    wv[c] = j < dd ? w[j] : 0.0;
+  }
+  double acc = 0.0;  // thread j < d: column j
+  double zv[2][kWideCols], xv[2][kWideCols];
+
+  for (int64_t P0 = 0; P0 < B; P0 += kIdxPhase) {
+    const int np = (int)std::min<int64_t>(kIdxPhase, B - P0);
+    __syncthreads();  // the previous phase's readers of prx/prz and diff/flag are done
+    for (int t = threadIdx.x; t < np; t += kWideBlock) {
+      const int64_t b = P0 + t;
+      int64_t ax, az;
+      if (ix) {
+        ax = ix[(int64_t)s * B + b];
+        az = iz[(int64_t)s * B + b];
+      } else {
+        const u32x4 r = sgd_draw(seed, step, (uint32_t)b, shard_base + (uint32_t)s, kTagPairs);
+        ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
+        az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
+      }
+      prx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+      prz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+    }
+    __syncthreads();
+
+    auto load = [&](int st, int c0) {  // this wave's pair of the chunk at c0 into stage st
+      const int t = c0 + wid;
+      if (t < np) {
+        const double* zr = Z + prz[t] * d;
+        const double* xr = X + prx[t] * d;
+#pragma unroll
+        for (int c = 0; c < kWideCols; ++c) {
+          const int j = lane + c * kWave;
+          zv[st][c] = j < dd ? zr[j] : 0.0;
+          xv[st][c] = j < dd ? xr[j] : 0.0;
+        }
+      }
+    };
+    auto chunk = [&](int st, int c0) {
+      const int nb = std::min(kStreamCH, np - c0);
+      const int t = wid;
+      if (t < nb) {
+        double part = 0.0;
+#pragma unroll
+        for (int c = 0; c < kWideCols; ++c) {
+          const int j = lane + c * kWave;
+          if (j < dd) {
+            const double v = zv[st][c] - xv[st][c];
+            diff[st][t * dd + j] = v;
+            part += v * wv[c];
+          }
+        }
+        part = wave_sum_f64(part);
+        if (lane == 0) flag[st][t] = pair_weight<LOSS>(part + margin);
+      }
+      if (c0 + 2 * kStreamCH < np) load(st, c0 + 2 * kStreamCH);  // refill: chunk k+2
+      __syncthreads();
+      if (threadIdx.x < dd) {
+        const int j = threadIdx.x;
+        double a = acc;
+        int u0 = 0;
+        for (; u0 + 8 <= nb; u0 += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = weighted<LOSS>(flag[st][u0 + u], diff[st][(u0 + u) * dd + j]);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; u0 < nb; ++u0) a += weighted<LOSS>(flag[st][u0], diff[st][u0 * dd + j]);
+        acc = a;
+      }
+    };
+    load(0, 0);
+    if (kStreamCH < np) load(1, kStreamCH);
+    int c0 = 0;
+    for (; c0 + kStreamCH < np; c0 += 2 * kStreamCH) {  // stages alternate; constant indices
+      chunk(0, c0);
+      chunk(1, c0 + kStreamCH);
+    }
+    if (c0 < np) chunk(0, c0);
+  }
+  if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
+}
+
 // One whole SGD step for narrow rows (d <= 32, C4) in ONE launch: the update of the PREVIOUS
 // step (make_exps.py:130-141) runs as this kernel's prologue, redundantly in every block, and
 // then the gradient of this step (compute_stats.py:146-162) with the updated w.
@@ -499,7 +610,11 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
     hipLaunchKernelGGL((k_hinge_grad<kBlock, LOSS>), dim3(n_shards), dim3(kBlock), lds, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
                        shard_base);
-  else if (d <= kWideMaxD && !g_hinge_legacy_wide)
+  else if (d <= kWideMaxD && g_hinge_legacy_wide == 0)
+    hipLaunchKernelGGL(k_hinge_grad_stream<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z,
+                       d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
+                       shard_base);
+  else if (d <= kWideMaxD && g_hinge_legacy_wide == 2)
     hipLaunchKernelGGL(k_hinge_grad_wide<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
                        shard_base);
@@ -558,7 +673,7 @@ extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
 }
 
 extern "C" int tw_hinge_set_variant(int32_t legacy_wide) {
-  TW_ARG_CHECK(legacy_wide == 0 || legacy_wide == 1, "tw_hinge_set_variant: 0 or 1");
+  TW_ARG_CHECK(legacy_wide >= 0 && legacy_wide <= 2, "tw_hinge_set_variant: 0, 1 or 2");
   g_hinge_legacy_wide = legacy_wide;
   return TW_OK;
 }
