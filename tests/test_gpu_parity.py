@@ -312,10 +312,21 @@ def test_pipelined_unn_many_equals_sequential(gpu):
         assert torch.equal(S1.X, S2.X) and torch.equal(S1.Z, S2.Z)
         assert S2.UnNT(3, key0=40) == np.mean([S1.UnN(k) for k in (40, 41, 42)])
     # incomplete statistic with fresh device draws per repartition (cs.UnNBT's loop)
-    S1 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
-    S2 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N)
-    seq = [S1.UnNB(5000, 77 + i, key=k) for i, k in enumerate(keys)]
-    assert S2.UnNB_many(5000, 77, keys) == seq
+    # (one GPU: each ranked draw-and-count launch also repartitions for the next key on spare
+    # blocks, tw_count_pairs_rng_step) — ranked via sort (18750-value shards) and via buckets
+    # (<= 16384), strict and half ties, float64 and int64, ragged shards, one key
+    ri = np.random.RandomState(13)
+    cases = [(X, Z, N, "strict", keys), (X[:200_000], Z[:150_001], 16, "half", keys),
+             (ri.randint(0, 50, 160_003), ri.randint(0, 50, 120_000), 12, "half", keys),
+             (X[:50_000], Z[:40_000], 4, "strict", [9])]
+    for xa, za, nn, tie, ks in cases:
+        S1 = ShardedSample(torch.from_numpy(xa).cuda(), torch.from_numpy(za).cuda(), nn,
+                           tie_mode=tie)
+        S2 = ShardedSample(torch.from_numpy(xa).cuda(), torch.from_numpy(za).cuda(), nn,
+                           tie_mode=tie)
+        seq = [S1.UnNB(5000, 77 + i, key=k) for i, k in enumerate(ks)]
+        assert S2.UnNB_many(5000, 77, ks) == seq, (len(xa), tie)
+        assert torch.equal(S1.X, S2.X) and torch.equal(S1.Z, S2.Z)
 
 
 def test_exchange_kernels_simulated_ranks(gpu):

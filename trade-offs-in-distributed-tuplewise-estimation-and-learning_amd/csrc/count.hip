@@ -21,6 +21,7 @@
 //   wave-instructions/cycle/CU, so 2 such instructions per pair cap this kernel at ~1.9e13
 //   pairs/s; see DESIGN.md "count kernel roofline".
 #include "feistel.h"
+#include "nextstep.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -37,52 +38,6 @@ __device__ __forceinline__ unsigned pair_pred(T x, T z) {
       return (long long)((unsigned long long)x - (unsigned long long)z) > 0;
     } else {
       return x > z;  // identical to (x - z) > 0 for IEEE doubles (no FTZ on f64)
-    }
-  }
-}
-
-// The next repartition of est.UnNT's loop, carried by the leading `blocks` blocks of a count
-// launch (tw_count_pairs_step): the permutation of both samples as a gather (tw_permute_pair)
-// and the zeroing of the next step's counters.  These blocks are memory-latency bound and
-// share the CUs with the VALU-bound count blocks, so the repartition costs no separate
-// kernel, no launch gap and almost no time.
-struct NextStep {
-  const uint64_t* x_in;
-  uint64_t* x_out;
-  int64_t nx;
-  const uint64_t* z_in;
-  uint64_t* z_out;
-  int64_t nz;
-  unsigned long long* zero;
-  int64_t nzero;
-  Feistel fx, fz;
-  int blocks;  // a multiple of kXcds
-  int every;   // placement of the spare blocks (see k_count_complete)
-  int tail;
-};
-
-__device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
-  constexpr int kU = 8;  // independent gathers in flight per thread
-  const int64_t stride = (int64_t)nx.blocks * kBlock;
-  for (int64_t i = (int64_t)b * kBlock + threadIdx.x; i < nx.nzero; i += stride) nx.zero[i] = 0;
-  const int64_t tot = nx.nx + nx.nz;
-  for (int64_t p0 = (int64_t)b * kBlock + threadIdx.x; p0 < tot; p0 += stride * kU) {
-    uint64_t v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t p = p0 + u * stride;
-      if (p < nx.nx)
-        v[u] = nx.x_in[feistel_perm_inv(nx.fx, (uint64_t)p, (uint64_t)nx.nx)];
-      else if (p < tot)
-        v[u] = nx.z_in[feistel_perm_inv(nx.fz, (uint64_t)(p - nx.nx), (uint64_t)nx.nz)];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t p = p0 + u * stride;
-      if (p < nx.nx)
-        nx.x_out[p] = v[u];
-      else if (p < tot)
-        nx.z_out[p - nx.nx] = v[u];
     }
   }
 }
@@ -252,13 +207,13 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
     const int b = blockIdx.x, ng = nxt.blocks / kXcds;
     if (nxt.tail) {
       if (b >= (int)gridDim.x - nxt.blocks) {
-        next_step_part(nxt, b - ((int)gridDim.x - nxt.blocks));
+        next_step_part<kBlock>(nxt, b - ((int)gridDim.x - nxt.blocks));
         return;
       }
     } else {
       const int g = b / nxt.every, r = b - g * nxt.every;
       if (r < kXcds && g < ng) {
-        next_step_part(nxt, g * kXcds + r);
+        next_step_part<kBlock>(nxt, g * kXcds + r);
         return;
       }
       cb = b - kXcds * ((g < ng ? g : ng) + ((r >= kXcds && g < ng) ? 1 : 0));
