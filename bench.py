@@ -343,6 +343,74 @@ def pmc_traffic():
     return d.get("hbm_bytes_per_launch"), plain
 
 
+def incomplete_replay(X, Z, shards, B, reps=20):
+    """UnNB in replay mode (compute_stats.py:37-42 via UB): B explicit index pairs per shard,
+    as NumPy's randint would hand them over, already resident as int64 (16 B per pair), counted
+    by k_count_idx (tw_count_pairs_idx).  HBM-bound: the 16 B of indices per pair stream from
+    HBM, the gathered scores (16 MB) stay in L2 / Infinity Cache.  Indices are drawn on the
+    device here (uniform within each shard's contiguous range); the kernel sees the same
+    layout as the drop-in UB/UnNB path."""
+    import torch
+    from tuplewise import _engine, _lib as L
+    n = X.numel()
+    k = n // shards
+    g = torch.Generator(device="cuda").manual_seed(4321)
+    base = (torch.arange(shards, device="cuda", dtype=torch.int64) * k).repeat_interleave(B)
+    ix = base + torch.randint(0, k, (shards * B,), device="cuda", generator=g)
+    iz = base + torch.randint(0, k, (shards * B,), device="cuda", generator=g)
+    pair_off = np.arange(shards + 1, dtype=np.int64) * B
+    pod = L.to_device(pair_off)
+
+    off = L.to_device(np.arange(shards + 1, dtype=np.int64) * k)
+    work = L.empty((int(L.lib().tw_count_pairs_rng_work_bytes(shards, k, k, L.TW_F64,
+                                                              L.TW_PRED_GT)),), torch.uint8)
+
+    def plain():
+        return _engine.count_indexed_dev(X, Z, L.TW_F64, ix, iz, pair_off, L.TW_PRED_GT, pod)
+
+    def ranked():
+        return _engine.count_indexed_ranked_dev(X, off, Z, off, k, k, L.TW_F64, ix, iz,
+                                                pair_off, L.TW_PRED_GT, pod, work)
+
+    def timed(launch):
+        for _ in range(3):
+            launch()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for e0, e1 in ev:
+            e0.record()
+            out = launch()
+            e1.record()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return out, dt, float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    out_p, dt_p, kms_p = timed(plain)
+    out, dt, kms = timed(ranked)
+    # spot check against a torch gather-compare of shard 0's pairs (exact integer)
+    s0 = int((X[ix[:B]] > Z[iz[:B]]).sum())
+    pairs = shards * B
+    return {"note": "UnNB replay mode: B explicit int64 index pairs per shard resident in HBM "
+                    "(NumPy-drawn in the drop-in path; device-drawn here); tw_count_pairs_idx_ws:"
+                    " rank codes of both samples, then k_count_idx_ranked compares codes held in"
+                    " LDS; the plain gather kernel k_count_idx timed beside it",
+            "B_per_shard": B, "value": pairs * reps / dt, "unit": "pairs/s",
+            "ms_per_call": dt / reps * 1e3,
+            "counts_identical_to_plain": bool(torch.equal(out, out_p)),
+            "shard0_count_matches_torch": int(out[0].item()) == s0,
+            "plain_k_count_idx": {"value": pairs * reps / dt_p, "ms_per_call": dt_p / reps * 1e3,
+                                  "kernel_ms": kms_p,
+                                  "GBps_indices": 16 * pairs / (kms_p * 1e-3) / 1e9},
+            "roofline": {"bound": "hbm", "kernel": "k_rank_codes_bucket + k_count_idx_ranked",
+                         "achieved": 16 * pairs / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": 16 * pairs / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "kernel_ms": kms,
+                         "note": "16 algorithmic bytes per pair (two int64 indices); kernel_ms ="
+                                 " the whole call (codes + draw-and-count)"}}
+
+
 def main():
     args = parse()
     import torch
@@ -468,6 +536,7 @@ def main():
     kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
     ops.count_rng = ops.count_rng.__wrapped__
     inc_pairs_rank = args.shards * B_inc
+    inc_replay = incomplete_replay(X, Z, args.shards, B_inc)
 
     # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
     # estimation-experiment/main.py:29-31), 1e10 pairs per launch; no repartition
@@ -569,6 +638,7 @@ def main():
                                  "constant: 2 Philox4x32-10 words + 2 range maps + 1 compare); "
                                  "kernel_ms = the whole tw_count_pairs_rng_ws call (z sort, "
                                  "rank codes, draw-and-count)"}},
+        "incomplete_replay": inc_replay,
     }
     if world == 1 and not args.no_sgd:
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'

@@ -128,6 +128,18 @@ int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
                        const int64_t* d_iz, const int64_t* d_pair_off, int32_t n_shards,
                        int64_t max_pairs, int32_t dtype, int32_t pred, uint64_t* d_out,
                        void* stream);
+/* The same counts as tw_count_pairs_idx with the compares on the 16-bit rank codes of
+ * tw_count_pairs_rng_ws held in LDS (shard s spans d_x_off[s]..d_x_off[s+1] and
+ * d_z_off[s]..d_z_off[s+1]; an index outside its shard's span compares the scores), so the
+ * kernel streams only the indices.  d_work holds tw_count_pairs_rng_work_bytes(n_shards,
+ * max_nx, max_nz, dtype, pred) bytes; when that is 0 (shards of >= 65536 values, int64 SUBGT) or
+ * d_work == NULL this call runs tw_count_pairs_idx. */
+int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                          const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                          int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,
+                          const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype,
+                          int32_t pred, void* d_work, int64_t work_bytes, uint64_t* d_out,
+                          void* stream);
 
 /* ---- Row A5/A8, device-RNG mode: B pairs per shard drawn on the device ----------------
  * Philox4x32-10(key = seed, counter = (q lo, q hi, shard_base + s, 0)) gives the 4 words

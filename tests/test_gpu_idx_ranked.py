@@ -1,0 +1,118 @@
+"""Parity of tw_count_pairs_idx_ws (explicit index pairs compared on LDS rank codes) with the
+plain index kernel tw_count_pairs_idx and with a NumPy count of the same pairs.
+
+Replay mode of UB / UnNB (compute_stats.py:37-42, :104-123): the indices are NumPy randint
+draws, absolute positions in the concatenated shard arrays.  Counts are integers: bit-exact.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _np_count(x, z, ix, iz, pair_off, mode):
+    out = []
+    for s in range(len(pair_off) - 1):
+        a = x[ix[pair_off[s]:pair_off[s + 1]]]
+        b = z[iz[pair_off[s]:pair_off[s + 1]]]
+        if mode == "gt":
+            out.append(int(np.sum(a > b)))
+        elif mode == "half":
+            out.append(int(np.sum(a > b)) + int(np.sum(a >= b)))
+        else:  # subgt: (a - b) > 0 with int64 wrap
+            with np.errstate(over="ignore"):
+                out.append(int(np.sum((a - b) > 0)))
+    return np.array(out, dtype=np.uint64)
+
+
+def _sample(kind, rng):
+    if kind == "gauss":
+        nx = [3000, 2999, 1, 4096, 0, 700]
+        nz = [2500, 3001, 5, 4096, 17, 0]
+        x = rng.normal(0.5, 1, sum(nx))
+        z = rng.normal(0, 1, sum(nz))
+    elif kind == "edge_float":
+        nx, nz = [400] * 5, [300] * 5
+        vals = np.array([np.nan, -0.0, 0.0, np.inf, -np.inf, 1.0, 1.0, -1.0, 5e-324])
+        x = rng.choice(vals, sum(nx))
+        z = rng.choice(vals, sum(nz))
+    elif kind == "ties_int":
+        nx, nz = [5000, 4000, 20000], [6000, 3000, 20000]
+        x = rng.integers(0, 7, sum(nx)).astype(np.int64)
+        z = rng.integers(0, 7, sum(nz)).astype(np.int64)
+    elif kind == "int64_wrap":
+        nx, nz = [1000, 1000], [1000, 1000]
+        big = np.array([2 ** 62, -(2 ** 62), 2 ** 63 - 1, -(2 ** 63), 0, 1], dtype=np.int64)
+        x = rng.choice(big, sum(nx))
+        z = rng.choice(big, sum(nz))
+    elif kind == "large_shard":  # nz >= 65536: codes do not apply, the plain kernel runs
+        nx, nz = [70000], [70000]
+        x = rng.normal(0.5, 1, sum(nx))
+        z = rng.normal(0, 1, sum(nz))
+    else:
+        raise ValueError(kind)
+    x_off = np.concatenate([[0], np.cumsum(nx)]).astype(np.int64)
+    z_off = np.concatenate([[0], np.cumsum(nz)]).astype(np.int64)
+    return x, x_off, z, z_off
+
+
+def _pairs(x_off, z_off, B, rng, stray=False):
+    ix, iz, po = [], [], [0]
+    for s in range(len(x_off) - 1):
+        nx, nz = x_off[s + 1] - x_off[s], z_off[s + 1] - z_off[s]
+        if nx == 0 or nz == 0:
+            po.append(po[-1])
+            continue
+        a = x_off[s] + rng.integers(0, nx, B)
+        b = z_off[s] + rng.integers(0, nz, B)
+        if stray:  # indices outside the shard's span (allowed by tw_count_pairs_idx)
+            a[::7] = rng.integers(0, x_off[-1], len(a[::7]))
+            b[::5] = rng.integers(0, z_off[-1], len(b[::5]))
+        ix.append(a)
+        iz.append(b)
+        po.append(po[-1] + B)
+    return (np.concatenate(ix).astype(np.int64), np.concatenate(iz).astype(np.int64),
+            np.array(po, dtype=np.int64))
+
+
+@pytest.mark.parametrize("kind", ["gauss", "edge_float", "ties_int", "int64_wrap",
+                                  "large_shard"])
+@pytest.mark.parametrize("stray", [False, True])
+def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray):
+    from tuplewise import _engine as E, _lib as L
+    rng = np.random.default_rng(zlib.crc32(f"{kind}{stray}".encode()))
+    x, x_off, z, z_off = _sample(kind, rng)
+    ix, iz, po = _pairs(x_off, z_off, 20011, rng, stray)
+    code = L.TW_F64 if x.dtype == np.float64 else L.TW_I64
+    xd, zd = L.to_device(x), L.to_device(z)
+    xo, zo = L.to_device(x_off), L.to_device(z_off)
+    max_nx, max_nz = int(np.diff(x_off).max()), int(np.diff(z_off).max())
+    modes = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}
+    for mode, pred in modes.items():
+        want = _np_count(x, z, ix, iz, po, mode)
+        plain = E.count_indexed_dev(xd, zd, code, ix, iz, po, pred).cpu().numpy().view(np.uint64)
+        ranked = E.count_indexed_ranked_dev(xd, xo, zd, zo, max_nx, max_nz, code, ix, iz, po,
+                                            pred).cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(plain, want, err_msg=f"plain {kind} {mode}")
+        np.testing.assert_array_equal(ranked, want, err_msg=f"ranked {kind} {mode}")
+
+
+def test_idx_ranked_codes_sorted_path(gpu):
+    """The sort + binary-search rank codes (tw_count_rng_set_codes(0)) give the same counts."""
+    from tuplewise import _engine as E, _lib as L
+    rng = np.random.default_rng(5)
+    x, x_off, z, z_off = _sample("gauss", rng)
+    ix, iz, po = _pairs(x_off, z_off, 9999, rng)
+    xd, zd = L.to_device(x), L.to_device(z)
+    xo, zo = L.to_device(x_off), L.to_device(z_off)
+    want = _np_count(x, z, ix, iz, po, "half")
+    L.call("tw_count_rng_set_codes", 0)
+    try:
+        got = E.count_indexed_ranked_dev(xd, xo, zd, zo, int(np.diff(x_off).max()),
+                                         int(np.diff(z_off).max()), L.TW_F64, ix, iz, po,
+                                         L.TW_PRED_HALF).cpu().numpy().view(np.uint64)
+    finally:
+        L.call("tw_count_rng_set_codes", 1)
+    np.testing.assert_array_equal(got, want)

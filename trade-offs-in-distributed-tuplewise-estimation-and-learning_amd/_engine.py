@@ -204,6 +204,30 @@ def count_indexed_dev(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarra
     return out
 
 
+def count_indexed_ranked_dev(x_dev, x_off_dev, z_dev, z_off_dev, max_nx: int, max_nz: int,
+                             dtype_code: int, ix, iz, pair_off: np.ndarray, pred: int,
+                             pair_off_dev=None, work=None):
+    """count_indexed_dev for shard-contiguous samples (shard s = x[x_off[s]:x_off[s+1]]): the
+    same integers, compared on 16-bit rank codes in LDS (tw_count_pairs_idx_ws; it runs the
+    plain kernel where codes do not apply).  `work` may be a cached uint8 device buffer of
+    tw_count_pairs_rng_work_bytes bytes."""
+    t = L.torch()
+    n = len(pair_off) - 1
+    ixd, izd = _idx_dev(ix), _idx_dev(iz)
+    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
+    max_pairs = int(np.diff(pair_off).max()) if n else 0
+    wpred = L.TW_PRED_GT if (pred == L.TW_PRED_SUBGT and dtype_code == L.TW_F64) else pred
+    wb = int(L.lib().tw_count_pairs_rng_work_bytes(n, max_nx, max_nz, dtype_code, wpred))
+    if wb > 0 and (work is None or work.numel() < wb):
+        work = L.empty((wb,), t.uint8)
+    out = L.empty((max(n, 1),), t.int64)[:n]
+    L.call("tw_count_pairs_idx_ws", L.ptr(x_dev), L.ptr(x_off_dev), L.ptr(z_dev),
+           L.ptr(z_off_dev), n, max_nx, max_nz, L.ptr(ixd), L.ptr(izd), L.ptr(pod), max_pairs,
+           dtype_code, pred, L.ptr(work if wb > 0 else None), wb, L.ptr(out),
+           L.stream_handle())
+    return out
+
+
 def count_indexed(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray,
                   mode: str = "gt", pair_off_dev=None) -> np.ndarray:
     """Per-shard counts over explicit (absolute) index pairs (host or device index arrays)."""

@@ -462,6 +462,77 @@ __global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
   }
 }
 
+// Incomplete count on explicit index pairs (UB replay: NumPy's randint draws, compute_stats.py:
+// 22-42) through the rank codes: a block stages its shard's 16-bit codes in LDS, so the two
+// per-pair gathers are LDS reads and only the 16 B of indices per pair stream from HBM (the plain
+// k_count_idx pulls an L2 line per gathered score).  Indices are absolute; one outside its
+// shard's range (allowed by tw_count_pairs_idx) compares the scores themselves.
+template <typename T, int PRED>
+__global__ __launch_bounds__(kRngThreads) void k_count_idx_ranked(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, const uint16_t* __restrict__ cx,
+    const uint16_t* __restrict__ cx2, const uint16_t* __restrict__ pz, int64_t max_nx,
+    int64_t max_nz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz,
+    const int64_t* __restrict__ pair_off, int parts, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t codes[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);  // a shard's parts share one L2
+  const int s = lb / parts;
+  const int part = lb - s * parts;
+  const int64_t xb = x_off[s], zb = z_off[s];
+  const uint64_t nx = (uint64_t)(x_off[s + 1] - xb), nz = (uint64_t)(z_off[s + 1] - zb);
+  uint16_t* lx = codes;
+  uint16_t* lx2 = codes + nx;
+  uint16_t* lz = codes + (PRED == TW_PRED_HALF ? 2 : 1) * nx;
+  if (nx > 0 && nz > 0) {
+    for (int64_t i = threadIdx.x; i < (int64_t)nx; i += kRngThreads) {
+      lx[i] = cx[(int64_t)s * max_nx + i];
+      if (PRED == TW_PRED_HALF) lx2[i] = cx2[(int64_t)s * max_nx + i];
+    }
+    for (int64_t j = threadIdx.x; j < (int64_t)nz; j += kRngThreads)
+      lz[j] = pz[(int64_t)s * max_nz + j];
+  }
+  __syncthreads();
+  const int64_t pb = pair_off[s], pe = pair_off[s + 1];
+  const int64_t per = (pe - pb + parts - 1) / parts;
+  const int64_t q0 = pb + (int64_t)part * per;
+  const int64_t q1 = std::min<int64_t>(pe, q0 + per);
+  unsigned acc = 0;
+  constexpr int U = 4;  // index loads in flight per thread
+  for (int64_t p0 = q0 + threadIdx.x; p0 < q1; p0 += (int64_t)U * kRngThreads) {
+    int64_t a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + (int64_t)u * kRngThreads;
+      a[u] = p < q1 ? ix[p] : xb;
+      b[u] = p < q1 ? iz[p] : zb;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p0 + (int64_t)u * kRngThreads >= q1) break;
+      const uint64_t i = (uint64_t)(a[u] - xb), j = (uint64_t)(b[u] - zb);
+      if (i < nx && j < nz) {
+        const unsigned pj = lz[j];
+        acc += (unsigned)lx[i] > pj;
+        if (PRED == TW_PRED_HALF) acc += (unsigned)lx2[i] > pj;
+      } else {
+        const T xv = x[a[u]], zv = z[b[u]];
+        acc += xv > zv;
+        if (PRED == TW_PRED_HALF) acc += xv >= zv;
+      }
+    }
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part_sum[kRngThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part_sum[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long sum = 0;
+    for (int w = 0; w < kRngThreads / kWave; ++w) sum += part_sum[w];
+    if (sum) atomicAdd(out + s, sum);
+  }
+}
+
 static int g_rng_codes_by_bucket = 1;  // tw_count_rng_set_codes: 0 = sort + binary search
 
 struct RngRankPlan {
@@ -497,11 +568,13 @@ static RngRankPlan plan_rng_ranked(int32_t n_shards, int64_t max_nx, int64_t max
   return p;
 }
 
+// Rank codes of every shard into the work buffer (plan_rng_ranked's layout): bucket codes for
+// shards of <= kBucketMaxZ z-values, else sort + binary search.  Shared by the device-RNG and the
+// replay (explicit index) draw-and-count kernels.
 template <typename T, int PRED>
-int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
-                      int32_t n_shards, int64_t max_nx, int64_t max_nz, int64_t B, uint64_t seed,
-                      uint64_t sid, const RngRankPlan& p, void* work, uint64_t* out,
-                      hipStream_t st) {
+int launch_codes(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                 int32_t n_shards, int64_t max_nx, int64_t max_nz, const RngRankPlan& p,
+                 void* work, hipStream_t st) {
   static bool attrs_set = false;
   if (!attrs_set) {
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<T, 4>,
@@ -520,9 +593,6 @@ int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const 
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)(sizeof(T) * kBucketMaxZ +
                                            sizeof(unsigned) * (2 * kBucketNB + 1))));
-    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_ranked<PRED>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024 - 1024));
     attrs_set = true;
   }
   char* w = (char*)work;
@@ -555,9 +625,54 @@ int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const 
                      p.tiles, max_nx, max_nz, cx, cx2, pz);
   }
   TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+template <typename T, int PRED>
+int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                      int32_t n_shards, int64_t max_nx, int64_t max_nz, int64_t B, uint64_t seed,
+                      uint64_t sid, const RngRankPlan& p, void* work, uint64_t* out,
+                      hipStream_t st) {
+  static bool attrs_set = false;
+  if (!attrs_set) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_ranked<PRED>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 1024));
+    attrs_set = true;
+  }
+  const int rc = launch_codes<T, PRED>(x, x_off, z, z_off, n_shards, max_nx, max_nz, p, work, st);
+  if (rc != TW_OK) return rc;
+  char* w = (char*)work;
+  uint16_t* cx = (uint16_t*)(w + p.cx_off);
+  uint16_t* cx2 = (uint16_t*)(w + p.cx2_off);
+  uint16_t* pz = (uint16_t*)(w + p.pz_off);
   hipLaunchKernelGGL((k_count_rng_ranked<PRED>), dim3(n_shards * p.parts), dim3(kRngThreads),
                      p.lds, st, x_off, z_off, cx, cx2, pz, max_nx, max_nz, B, p.parts,
                      (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
+                     (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+template <typename T, int PRED>
+int launch_idx_ranked(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                      int32_t n_shards, int64_t max_nx, int64_t max_nz, const int64_t* ix,
+                      const int64_t* iz, const int64_t* pair_off, const RngRankPlan& p,
+                      void* work, uint64_t* out, hipStream_t st) {
+  static bool attrs_set = false;
+  if (!attrs_set) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_idx_ranked<T, PRED>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 1024));
+    attrs_set = true;
+  }
+  const int rc = launch_codes<T, PRED>(x, x_off, z, z_off, n_shards, max_nx, max_nz, p, work, st);
+  if (rc != TW_OK) return rc;
+  char* w = (char*)work;
+  hipLaunchKernelGGL((k_count_idx_ranked<T, PRED>), dim3(n_shards * p.parts), dim3(kRngThreads),
+                     p.lds, st, (const T*)x, x_off, (const T*)z, z_off,
+                     (const uint16_t*)(w + p.cx_off), (const uint16_t*)(w + p.cx2_off),
+                     (const uint16_t*)(w + p.pz_off), max_nx, max_nz, ix, iz, pair_off, p.parts,
                      (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
@@ -646,4 +761,40 @@ extern "C" int tw_count_sorted_set_bucket(int32_t by_bucket) {
   TW_ARG_CHECK(by_bucket == 0 || by_bucket == 1, "tw_count_sorted_set_bucket: 0 or 1");
   g_sorted_by_bucket = by_bucket;
   return TW_OK;
+}
+
+extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
+                                  const int64_t* d_iz, const int64_t* d_pair_off,
+                                  int32_t n_shards, int64_t max_pairs, int32_t dtype,
+                                  int32_t pred, uint64_t* d_out, void* stream);
+
+extern "C" int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                     const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                     int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,
+                                     const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype,
+                                     int32_t pred, void* d_work, int64_t work_bytes,
+                                     uint64_t* d_out, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && max_nx >= 0 && max_nz >= 0 && max_pairs >= 0,
+               "tw_count_pairs_idx_ws: bad sizes");
+  // SUBGT on doubles is GT ((x - z) > 0 == x > z without FTZ); on int64 it wraps: plain kernel
+  const int32_t pr = (pred == TW_PRED_SUBGT && dtype == TW_F64) ? TW_PRED_GT : pred;
+  // plan_rng_ranked's part count from the pair count (its B), so ~512 blocks fill the chip
+  const RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pr, max_pairs);
+  if (!p.ok || (dtype != TW_F64 && dtype != TW_I64) || max_pairs == 0 || d_work == nullptr ||
+      work_bytes < p.total)  // not applicable: the plain kernel gives the same counts
+    return tw_count_pairs_idx(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, dtype,
+                              pred, d_out, stream);
+  TW_ARG_CHECK((int64_t)n_shards * p.parts < (1ll << 31) && (int64_t)n_shards * p.tiles < (1ll << 31) &&
+                   (int64_t)n_shards * p.chunks < (1ll << 31),
+               "tw_count_pairs_idx_ws: grid too large");
+  hipStream_t st = (hipStream_t)stream;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  if (dtype == TW_F64) {
+    if (pr == TW_PRED_HALF)
+      return launch_idx_ranked<double, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
+    return launch_idx_ranked<double, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
+  }
+  if (pr == TW_PRED_HALF)
+    return launch_idx_ranked<long long, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
+  return launch_idx_ranked<long long, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
 }
