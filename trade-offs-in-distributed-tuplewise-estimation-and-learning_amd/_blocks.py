@@ -187,16 +187,32 @@ class Incomplete(BlockSpec):
         if rs > 1:  # X[ind] - Z[ind] on rows: element pairs (r*rs + c, r'*rs + c)
             ixa = (ixa[:, None] * rs + np.arange(rs)).reshape(-1)
             iza = (iza[:, None] * rs + np.arange(rs)).reshape(-1)
-        return indexed_values(xs, zs, ixa, iza, np.array(offs, dtype=np.int64), self.kernel)
+        return indexed_values(xs, zs, ixa, iza, np.array(offs, dtype=np.int64), self.kernel,
+                              spans=_slice_spans(blocks) if rs == 1 else None)
+
+
+def _slice_spans(blocks):
+    """(x_off, z_off) when every block is a slice and the slices follow one another (SWOR and
+    prop-SWOR plans), else None: the shard spans of the rank-code count."""
+    if not blocks or not all(isinstance(b.x, tuple) and isinstance(b.z, tuple) for b in blocks):
+        return None
+    for a, b in zip(blocks, blocks[1:]):
+        if a.x[1] != b.x[0] or a.z[1] != b.z[0]:
+            return None
+    return ([b.x[0] for b in blocks] + [blocks[-1].x[1]],
+            [b.z[0] for b in blocks] + [blocks[-1].z[1]])
 
 
 def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,
-                   pair_off: np.ndarray, kernel: str, margin: float = 0.0) -> list:
-    """Per-shard means of `kernel` over index pairs (UB_indices semantics, compute_stats.py:22-30)."""
+                   pair_off: np.ndarray, kernel: str, margin: float = 0.0,
+                   spans=None) -> list:
+    """Per-shard means of `kernel` over index pairs (UB_indices semantics, compute_stats.py:22-30).
+    spans: optional shard spans for the rank-code count (E.count_indexed)."""
     npairs = np.diff(pair_off)
     if kernel == "AUC":
         xx, zz, code, mode = E.subtract_gt_operands(x, z)
-        counts = E.count_indexed(L.to_device(xx), L.to_device(zz), code, ix, iz, pair_off, mode)
+        counts = E.count_indexed(L.to_device(xx), L.to_device(zz), code, ix, iz, pair_off, mode,
+                                 spans=spans)
         return [E.ratio(c, p) for c, p in zip(counts, npairs)]
     kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI, "hinge": L.TW_KERN_HINGE,
             "logistic": L.TW_KERN_LOGISTIC}[kernel]

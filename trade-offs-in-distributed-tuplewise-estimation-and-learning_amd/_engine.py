@@ -229,15 +229,26 @@ def count_indexed_ranked_dev(x_dev, x_off_dev, z_dev, z_off_dev, max_nx: int, ma
 
 
 def count_indexed(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray,
-                  mode: str = "gt", pair_off_dev=None) -> np.ndarray:
-    """Per-shard counts over explicit (absolute) index pairs (host or device index arrays)."""
+                  mode: str = "gt", pair_off_dev=None, spans=None) -> np.ndarray:
+    """Per-shard counts over explicit (absolute) index pairs (host or device index arrays).
+    spans = (x_off, z_off): shard s draws mostly from x[x_off[s]:x_off[s+1]] and
+    z[z_off[s]:z_off[s+1]] (UB on slice blocks); the counts then run on LDS rank codes
+    (count_indexed_ranked_dev) — the same integers for any indices."""
     n = len(pair_off) - 1
     if n == 0:
         return np.zeros(0, dtype=np.uint64)
     ixd, izd = _idx_dev(ix), _idx_dev(iz)
     pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
+    if spans is not None:
+        xo, zo = (np.asarray(a, dtype=np.int64) for a in spans)
+        xod, zod = L.to_device(xo), L.to_device(zo)
+        mx, mz = int(np.diff(xo).max()), int(np.diff(zo).max())
 
     def run(pred):
+        if spans is not None:
+            return _counts_to_host(count_indexed_ranked_dev(x_dev, xod, z_dev, zod, mx, mz,
+                                                            dtype_code, ixd, izd, pair_off,
+                                                            pred, pod))
         return _counts_to_host(count_indexed_dev(x_dev, z_dev, dtype_code, ixd, izd, pair_off,
                                                  pred, pod))
 
