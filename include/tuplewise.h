@@ -134,6 +134,8 @@ int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
  * kernel streams only the indices.  d_work holds tw_count_pairs_rng_work_bytes(n_shards,
  * max_nx, max_nz, dtype, pred) bytes; when that is 0 (shards of >= 65536 values, int64 SUBGT) or
  * d_work == NULL this call runs tw_count_pairs_idx. */
+/* Tuning hook of tw_count_pairs_idx_ws: blocks of 1024 threads per shard (0 = the plan's). */
+int tw_count_idx_set_parts(int32_t parts);
 int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,

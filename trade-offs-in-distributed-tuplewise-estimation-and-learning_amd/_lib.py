@@ -38,6 +38,7 @@ _SIGNATURES = {
     "tw_count_sorted_set_chunk": [_i64],
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],
     "tw_count_pairs_idx": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _vp],
+    "tw_count_idx_set_parts": [_i32],
     "tw_count_pairs_idx_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _i64, _i32,
                               _i32, _vp, _i64, _vp, _vp],
     "tw_count_pairs_rng": [_vp, _vp, _vp, _vp, _i32, _i64, _u64, _u64, _i32, _i32, _vp, _vp],

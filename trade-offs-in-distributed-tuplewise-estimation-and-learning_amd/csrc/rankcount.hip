@@ -768,6 +768,14 @@ extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_
                                   int32_t n_shards, int64_t max_pairs, int32_t dtype,
                                   int32_t pred, uint64_t* d_out, void* stream);
 
+static int g_idx_parts = 0;  // tw_count_idx_set_parts: blocks per shard (0 = plan)
+
+extern "C" int tw_count_idx_set_parts(int32_t parts) {
+  TW_ARG_CHECK(parts >= 0 && parts <= 4096, "tw_count_idx_set_parts: 0..4096");
+  g_idx_parts = parts;
+  return TW_OK;
+}
+
 extern "C" int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                                      const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                                      int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,
@@ -779,7 +787,8 @@ extern "C" int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, co
   // SUBGT on doubles is GT ((x - z) > 0 == x > z without FTZ); on int64 it wraps: plain kernel
   const int32_t pr = (pred == TW_PRED_SUBGT && dtype == TW_F64) ? TW_PRED_GT : pred;
   // plan_rng_ranked's part count from the pair count (its B), so ~512 blocks fill the chip
-  const RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pr, max_pairs);
+  RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pr, max_pairs);
+  if (g_idx_parts > 0) p.parts = g_idx_parts;
   if (!p.ok || (dtype != TW_F64 && dtype != TW_I64) || max_pairs == 0 || d_work == nullptr ||
       work_bytes < p.total)  // not applicable: the plain kernel gives the same counts
     return tw_count_pairs_idx(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, dtype,
