@@ -345,19 +345,23 @@ def pmc_traffic():
 
 def incomplete_replay(X, Z, shards, B, reps=20):
     """UnNB in replay mode (compute_stats.py:37-42 via UB): B explicit index pairs per shard,
-    as NumPy's randint would hand them over, already resident as int64 (16 B per pair), counted
-    by k_count_idx (tw_count_pairs_idx).  HBM-bound: the 16 B of indices per pair stream from
-    HBM, the gathered scores (16 MB) stay in L2 / Infinity Cache.  Indices are drawn on the
-    device here (uniform within each shard's contiguous range); the kernel sees the same
-    layout as the drop-in UB/UnNB path."""
+    as NumPy's randint hands them over after the drop-in's bound check narrows them to int32
+    (8 B per pair), already resident in HBM, counted by tw_count_pairs_idx32_ws:
+    16-bit rank codes of both samples (k_rank_codes_bucket), then k_count_idx_ranked streams
+    the indices and compares codes held in LDS.  HBM-bound on the index streams.  Indices are
+    drawn on the device here (uniform within each shard's contiguous range); the kernel sees the
+    same layout as the drop-in UB/UnNB path.  The plain gather kernel (tw_count_pairs_idx32,
+    the fallback for shards of >= 65536 values) and the int64-index call are timed beside it."""
     import torch
     from tuplewise import _engine, _lib as L
     n = X.numel()
     k = n // shards
     g = torch.Generator(device="cuda").manual_seed(4321)
     base = (torch.arange(shards, device="cuda", dtype=torch.int64) * k).repeat_interleave(B)
-    ix = base + torch.randint(0, k, (shards * B,), device="cuda", generator=g)
-    iz = base + torch.randint(0, k, (shards * B,), device="cuda", generator=g)
+    ix64 = base + torch.randint(0, k, (shards * B,), device="cuda", generator=g)
+    iz64 = base + torch.randint(0, k, (shards * B,), device="cuda", generator=g)
+    ix, iz = ix64.to(torch.int32), iz64.to(torch.int32)
+    del base
     pair_off = np.arange(shards + 1, dtype=np.int64) * B
     pod = L.to_device(pair_off)
 
@@ -370,6 +374,10 @@ def incomplete_replay(X, Z, shards, B, reps=20):
 
     def ranked():
         return _engine.count_indexed_ranked_dev(X, off, Z, off, k, k, L.TW_F64, ix, iz,
+                                                pair_off, L.TW_PRED_GT, pod, work)
+
+    def ranked64():
+        return _engine.count_indexed_ranked_dev(X, off, Z, off, k, k, L.TW_F64, ix64, iz64,
                                                 pair_off, L.TW_PRED_GT, pod, work)
 
     def timed(launch):
@@ -388,27 +396,32 @@ def incomplete_replay(X, Z, shards, B, reps=20):
         return out, dt, float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     out_p, dt_p, kms_p = timed(plain)
+    out64, dt64, kms64 = timed(ranked64)
     out, dt, kms = timed(ranked)
-    # spot check against a torch gather-compare of shard 0's pairs (exact integer)
-    s0 = int((X[ix[:B]] > Z[iz[:B]]).sum())
+    # every shard against a torch gather-compare of its pairs (exact integers)
+    want = (X[ix64] > Z[iz64]).view(shards, B).sum(1)
     pairs = shards * B
-    return {"note": "UnNB replay mode: B explicit int64 index pairs per shard resident in HBM "
-                    "(NumPy-drawn in the drop-in path; device-drawn here); tw_count_pairs_idx_ws:"
-                    " rank codes of both samples, then k_count_idx_ranked compares codes held in"
-                    " LDS; the plain gather kernel k_count_idx timed beside it",
+    bpp = 8  # algorithmic bytes per pair: two int32 indices
+    return {"note": "UnNB replay mode: B explicit int32 index pairs per shard resident in HBM "
+                    "(NumPy-drawn and narrowed after the bound check in the drop-in path; "
+                    "device-drawn here); tw_count_pairs_idx32_ws: rank codes of both samples, "
+                    "then k_count_idx_ranked compares codes held in LDS",
             "B_per_shard": B, "value": pairs * reps / dt, "unit": "pairs/s",
             "ms_per_call": dt / reps * 1e3,
             "counts_identical_to_plain": bool(torch.equal(out, out_p)),
-            "shard0_count_matches_torch": int(out[0].item()) == s0,
-            "plain_k_count_idx": {"value": pairs * reps / dt_p, "ms_per_call": dt_p / reps * 1e3,
-                                  "kernel_ms": kms_p,
-                                  "GBps_indices": 16 * pairs / (kms_p * 1e-3) / 1e9},
+            "counts_identical_to_int64": bool(torch.equal(out, out64)),
+            "all_shards_match_torch": bool(torch.equal(out, want)),
+            "plain_k_count_idx_int32": {"value": pairs * reps / dt_p,
+                                        "ms_per_call": dt_p / reps * 1e3, "kernel_ms": kms_p,
+                                        "GBps_indices": bpp * pairs / (kms_p * 1e-3) / 1e9},
+            "ranked_int64_indices": {"value": pairs * reps / dt64, "kernel_ms": kms64,
+                                     "GBps_indices": 16 * pairs / (kms64 * 1e-3) / 1e9},
             "roofline": {"bound": "hbm", "kernel": "k_rank_codes_bucket + k_count_idx_ranked",
-                         "achieved": 16 * pairs / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": 16 * pairs / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "achieved": bpp * pairs / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": bpp * pairs / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "kernel_ms": kms,
-                         "note": "16 algorithmic bytes per pair (two int64 indices); kernel_ms ="
-                                 " the whole call (codes + draw-and-count)"}}
+                         "note": "8 algorithmic bytes per pair (two int32 indices, SURVEY.md "
+                                 "§8(d)); kernel_ms = the whole call (rank codes + count)"}}
 
 
 def main():

@@ -117,7 +117,8 @@ int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, const void* d
                           uint64_t* d_out, void* stream);
 /* Shards with nz <= 16384 (default 1): the count comes from value buckets of z in LDS (an
  * LDS histogram, prefix and scatter, then one bucket scanned per x) instead of sorted chunks +
- * binary searches; the same integers.  0 = always sort + search (A/B, tests). */
+ * binary searches; the same integers.  1 = equal-depth buckets (the value-range histogram's
+ * CDF refines the map), 2 = value-range buckets only, 0 = always sort + search (A/B, tests). */
 int tw_count_sorted_set_bucket(int32_t by_bucket);
 
 /* ---- Row A3/A4/A5/A8: incomplete count on given index pairs (replay mode) -------------
@@ -136,12 +137,31 @@ int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
  * d_work == NULL this call runs tw_count_pairs_idx. */
 /* Tuning hook of tw_count_pairs_idx_ws: blocks of 1024 threads per shard (0 = the plan's). */
 int tw_count_idx_set_parts(int32_t parts);
+/* Tuning hook of the int32-index ranked count: 0 = four 16-B loads of each index stream in
+ * flight per thread (default), 1 = the same as nontemporal loads, 2/3 = eight loads (plain /
+ * nontemporal), 4/5 = two loads.  Process-global; results do not depend on it. */
+int tw_count_idx_set_variant(int32_t v);
 int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,
                           const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype,
                           int32_t pred, void* d_work, int64_t work_bytes, uint64_t* d_out,
                           void* stream);
+/* int32-index variants — the 8 B/pair replay contract of SURVEY.md §8(d): the same counts as
+ * tw_count_pairs_idx / tw_count_pairs_idx_ws with d_ix / d_iz int32 (absolute positions below
+ * 2^31).  They replace the same reference lines (compute_stats.py:22-42); the Python layer
+ * narrows NumPy's int64 randint output after its bound check (UB_indices' indexing,
+ * compute_stats.py:26-30) whenever both samples have fewer than 2^31 elements. */
+int tw_count_pairs_idx32(const void* d_x, const void* d_z, const int32_t* d_ix,
+                         const int32_t* d_iz, const int64_t* d_pair_off, int32_t n_shards,
+                         int64_t max_pairs, int32_t dtype, int32_t pred, uint64_t* d_out,
+                         void* stream);
+int tw_count_pairs_idx32_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                            const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                            int64_t max_nz, const int32_t* d_ix, const int32_t* d_iz,
+                            const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype,
+                            int32_t pred, void* d_work, int64_t work_bytes, uint64_t* d_out,
+                            void* stream);
 
 /* ---- Row A5/A8, device-RNG mode: B pairs per shard drawn on the device ----------------
  * Philox4x32-10(key = seed, counter = (q lo, q hi, shard_base + s, 0)) gives the 4 words
@@ -167,8 +187,9 @@ int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,
  * d_work == NULL) this call runs tw_count_pairs_rng. */
 int64_t tw_count_pairs_rng_work_bytes(int32_t n_shards, int64_t max_nx, int64_t max_nz,
                                       int32_t dtype, int32_t pred);
-/* Rank codes of tw_count_pairs_rng_ws: 1 (default) = value buckets in LDS when every shard has
- * nz <= 16384, 0 = always sort + binary search (A/B and tests; same codes). */
+/* Rank codes of tw_count_pairs_rng_ws / tw_count_pairs_idx(32)_ws: 1 (default) = equal-depth
+ * value buckets in LDS when every shard has nz <= 16384, 2 = value-range buckets only, 0 =
+ * always sort + binary search (A/B and tests; same codes). */
 int tw_count_rng_set_codes(int32_t by_bucket);
 int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
@@ -192,6 +213,14 @@ int tw_pair_sum_idx_f64(const double* d_x, const double* d_z, const int64_t* d_i
                         const int64_t* d_iz, const int64_t* d_pair_off, int32_t n_shards,
                         int64_t max_pairs, int32_t kern, double margin, double* d_work,
                         double* d_out, void* stream);
+/* int32 indices; d_count (nullable, uint64 per shard): the same pass also counts x > z — the
+ * fixed-pair br_AUC of evaluation_step (UB_pairs(kernel="AUC"), make_exps.py:162-168) beside
+ * its hinge mean bc_AUC (conv_AUC_deter_pairs, compute_stats.py:137-144), one read of the
+ * monitor pairs for both. */
+int tw_pair_sum_idx32_f64(const double* d_x, const double* d_z, const int32_t* d_ix,
+                          const int32_t* d_iz, const int64_t* d_pair_off, int32_t n_shards,
+                          int64_t max_pairs, int32_t kern, double margin, double* d_work,
+                          double* d_out, uint64_t* d_count, void* stream);
 
 /* ---- Row L1: pairwise hinge gradient, all shards in one launch ------------------------
  * Replaces grad_inc_block(w, B, margin)(X_s, Z_s) (compute_stats.py:146-162) for every shard

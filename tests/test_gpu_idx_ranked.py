@@ -1,5 +1,6 @@
-"""Parity of tw_count_pairs_idx_ws (explicit index pairs compared on LDS rank codes) with the
-plain index kernel tw_count_pairs_idx and with a NumPy count of the same pairs.
+"""Parity of tw_count_pairs_idx(32)_ws (explicit index pairs compared on LDS rank codes) with
+the plain index kernels tw_count_pairs_idx(32) and with a NumPy count of the same pairs, for
+int32 and int64 indices, aligned (16-B vector loads) and misaligned (scalar loads) streams.
 
 Replay mode of UB / UnNB (compute_stats.py:37-42, :104-123): the indices are NumPy randint
 draws, absolute positions in the concatenated shard arrays.  Counts are integers: bit-exact.
@@ -77,14 +78,25 @@ def _pairs(x_off, z_off, B, rng, stray=False):
             np.array(po, dtype=np.int64))
 
 
+def _idx(L, a, width, misalign):
+    """Device index column of the given width; misalign = start 1 element into the buffer, so
+    the base pointer is not 16-B aligned and the kernel takes its scalar-load path."""
+    dt = np.int32 if width == 32 else np.int64
+    if not misalign:
+        return L.to_device(a, dt)
+    return L.to_device(np.concatenate([[0], a]), dt)[1:]
+
+
 @pytest.mark.parametrize("kind", ["gauss", "edge_float", "ties_int", "int64_wrap",
                                   "large_shard"])
 @pytest.mark.parametrize("stray", [False, True])
-def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray):
+@pytest.mark.parametrize("width,misalign", [(32, False), (64, False), (32, True)])
+def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray, width, misalign):
     from tuplewise import _engine as E, _lib as L
     rng = np.random.default_rng(zlib.crc32(f"{kind}{stray}".encode()))
     x, x_off, z, z_off = _sample(kind, rng)
     ix, iz, po = _pairs(x_off, z_off, 20011, rng, stray)
+    ixd, izd = _idx(L, ix, width, misalign), _idx(L, iz, width, misalign)
     code = L.TW_F64 if x.dtype == np.float64 else L.TW_I64
     xd, zd = L.to_device(x), L.to_device(z)
     xo, zo = L.to_device(x_off), L.to_device(z_off)
@@ -92,11 +104,37 @@ def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray):
     modes = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}
     for mode, pred in modes.items():
         want = _np_count(x, z, ix, iz, po, mode)
-        plain = E.count_indexed_dev(xd, zd, code, ix, iz, po, pred).cpu().numpy().view(np.uint64)
-        ranked = E.count_indexed_ranked_dev(xd, xo, zd, zo, max_nx, max_nz, code, ix, iz, po,
+        plain = E.count_indexed_dev(xd, zd, code, ixd, izd, po, pred).cpu().numpy().view(np.uint64)
+        ranked = E.count_indexed_ranked_dev(xd, xo, zd, zo, max_nx, max_nz, code, ixd, izd, po,
                                             pred).cpu().numpy().view(np.uint64)
         np.testing.assert_array_equal(plain, want, err_msg=f"plain {kind} {mode}")
         np.testing.assert_array_equal(ranked, want, err_msg=f"ranked {kind} {mode}")
+
+
+@pytest.mark.parametrize("parts", [0, 8, 32])
+def test_idx_ranked_bench_shape(gpu, parts):
+    """The bench / C3 shape: 64 shards of 15625 x 15625, 1e6 int32 index pairs per shard, a
+    512-block grid through xcd_block; every shard against a torch gather-compare."""
+    import torch
+    from tuplewise import _engine as E, _lib as L
+    k, N, B = 15625, 64, 1_000_000
+    g = torch.Generator(device="cuda").manual_seed(77 + parts)
+    X = torch.randn(N * k, dtype=torch.float64, device="cuda", generator=g) + 0.5
+    Z = torch.randn(N * k, dtype=torch.float64, device="cuda", generator=g)
+    base = (torch.arange(N, device="cuda", dtype=torch.int64) * k).repeat_interleave(B)
+    ix = (base + torch.randint(0, k, (N * B,), device="cuda", generator=g)).to(torch.int32)
+    iz = (base + torch.randint(0, k, (N * B,), device="cuda", generator=g)).to(torch.int32)
+    off = np.arange(N + 1, dtype=np.int64) * k
+    po = np.arange(N + 1, dtype=np.int64) * B
+    offd = L.to_device(off)
+    want = (X[ix.long()] > Z[iz.long()]).view(N, B).sum(1).cpu().numpy().astype(np.uint64)
+    L.call("tw_count_idx_set_parts", parts)
+    try:
+        got = E.count_indexed_ranked_dev(X, offd, Z, offd, k, k, L.TW_F64, ix, iz, po,
+                                         L.TW_PRED_GT).cpu().numpy().view(np.uint64)
+    finally:
+        L.call("tw_count_idx_set_parts", 0)
+    np.testing.assert_array_equal(got, want)
 
 
 def test_idx_ranked_codes_sorted_path(gpu):

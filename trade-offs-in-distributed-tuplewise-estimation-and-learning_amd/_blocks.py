@@ -171,44 +171,58 @@ class Incomplete(BlockSpec):
         return ix, iz
 
     def evaluate(self, X, Z, blocks):
-        ix_abs, iz_abs, offs = [], [], [0]
-        xs = _flat(X)
-        zs = _flat(Z)
         rs = _row_size(X)
         if _row_size(Z) != rs:
             raise ValueError("UB on rows of different widths cannot broadcast")
-        # absolute row positions: slices are offsets into X/Z, resampled blocks map through idx
+        # X[ind] - Z[ind] on rows of rs elements compares element pairs (r*rs + c, r'*rs + c):
+        # blocks and draws become element blocks and element-local indices
+        eb = _elements(_elements(blocks, "x", rs), "z", rs)
+        ix_loc, iz_loc = [], []
         for b in blocks:
             ix, iz = b.aux
-            ix_abs.append(ix + b.x[0] if isinstance(b.x, tuple) else np.asarray(b.x)[ix])
-            iz_abs.append(iz + b.z[0] if isinstance(b.z, tuple) else np.asarray(b.z)[iz])
-            offs.append(offs[-1] + len(ix) * rs)
-        ixa, iza = np.concatenate(ix_abs), np.concatenate(iz_abs)
-        if rs > 1:  # X[ind] - Z[ind] on rows: element pairs (r*rs + c, r'*rs + c)
-            ixa = (ixa[:, None] * rs + np.arange(rs)).reshape(-1)
-            iza = (iza[:, None] * rs + np.arange(rs)).reshape(-1)
-        return indexed_values(xs, zs, ixa, iza, np.array(offs, dtype=np.int64), self.kernel,
-                              spans=_slice_spans(blocks) if rs == 1 else None)
+            if rs > 1:
+                ix = (np.asarray(ix)[:, None] * rs + np.arange(rs)).reshape(-1)
+                iz = (np.asarray(iz)[:, None] * rs + np.arange(rs)).reshape(-1)
+            ix_loc.append(np.asarray(ix, dtype=np.int64))
+            iz_loc.append(np.asarray(iz, dtype=np.int64))
+        return block_indexed_values(_flat(X), _flat(Z), eb, ix_loc, iz_loc, self.kernel)
 
 
-def _slice_spans(blocks):
-    """(x_off, z_off) when every block is a slice and the slices follow one another (SWOR and
-    prop-SWOR plans), else None: the shard spans of the rank-code count."""
-    if not blocks or not all(isinstance(b.x, tuple) and isinstance(b.z, tuple) for b in blocks):
-        return None
-    for a, b in zip(blocks, blocks[1:]):
-        if a.x[1] != b.x[0] or a.z[1] != b.z[0]:
-            return None
-    return ([b.x[0] for b in blocks] + [blocks[-1].x[1]],
-            [b.z[0] for b in blocks] + [blocks[-1].z[1]])
+def block_indexed_values(x: np.ndarray, z: np.ndarray, blocks: list, ix_loc: list,
+                         iz_loc: list, kernel: str) -> list:
+    """UB_indices (compute_stats.py:22-30) of every block, block b drawing ix_loc[b] /
+    iz_loc[b] (block-local positions).  The blocks are laid out as consecutive spans of one
+    device array per sample (slice plans point straight into the shuffled sample, resampled
+    prop-SWR blocks are gathered on the device), so every AUC count runs on the LDS rank codes
+    (tw_count_pairs_idx32_ws) with int32 absolute indices (8 B per pair)."""
+    offs = np.concatenate([[0], np.cumsum([len(a) for a in ix_loc])]).astype(np.int64)
+    if kernel == "AUC":
+        xx, zz, code, mode = E.subtract_gt_operands(x, z)
+    else:
+        xx, zz, code, mode = (x.astype(np.float64, copy=False), z.astype(np.float64, copy=False),
+                              L.TW_F64, None)
+    xa, xo = _layout(L.to_device(xx), blocks, "x")
+    za, zo = _layout(L.to_device(zz), blocks, "z")
+    ix = np.concatenate([a + o for a, o in zip(ix_loc, xo[:-1])]) if ix_loc else np.zeros(0, np.int64)
+    iz = np.concatenate([a + o for a, o in zip(iz_loc, zo[:-1])]) if iz_loc else np.zeros(0, np.int64)
+    npairs = np.diff(offs)
+    if kernel == "AUC":
+        counts = E.count_indexed(xa, za, code, ix, iz, offs, mode, spans=(xo, zo))
+        return [E.ratio(c, p) for c, p in zip(counts, npairs)]
+    kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI}[kernel]
+    sums = E.pair_sum_indexed(xa, za, ix, iz, offs, kern)
+    return [np.float64(s / np.float64(p)) for s, p in zip(sums, npairs)]
 
 
 def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,
                    pair_off: np.ndarray, kernel: str, margin: float = 0.0,
                    spans=None) -> list:
-    """Per-shard means of `kernel` over index pairs (UB_indices semantics, compute_stats.py:22-30).
-    spans: optional shard spans for the rank-code count (E.count_indexed)."""
+    """Per-shard means of `kernel` over absolute index pairs (UB_indices semantics,
+    compute_stats.py:22-30).  spans: the shard spans for the rank-code count (E.count_indexed);
+    None = one shard spanning both whole arrays (UB_indices / UB_pairs)."""
     npairs = np.diff(pair_off)
+    if spans is None and len(pair_off) == 2:
+        spans = ([0, x.shape[0]], [0, z.shape[0]])
     if kernel == "AUC":
         xx, zz, code, mode = E.subtract_gt_operands(x, z)
         counts = E.count_indexed(L.to_device(xx), L.to_device(zz), code, ix, iz, pair_off, mode,

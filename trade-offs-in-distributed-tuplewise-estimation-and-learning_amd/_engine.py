@@ -181,26 +181,52 @@ def count_complete(sh: Shards, mode: str = "gt", algo: str = "auto") -> np.ndarr
     return _counts_to_host(run(pred))
 
 
-def _idx_dev(a):
-    """int64 index array on the device: device tensors pass through (callers cache them)."""
+_I32_LIMIT = 2 ** 31  # arrays up to this many elements take int32 pair indices
+
+
+def _idx_dev(a, bound=None):
+    """Pair-index array on the device.  Device tensors pass through (callers cache them);
+    host arrays go up as int32 when every valid index fits (bound = the indexed array's
+    length, <= 2^31; the indices were bound-checked or drawn in range by the caller), which is
+    the 8 B/pair replay contract and halves the upload, else as int64."""
     t = L.torch()
     if isinstance(a, t.Tensor):
         return a
-    return L.to_device(np.asarray(a, dtype=np.int64))
+    a = np.asarray(a)
+    if bound is not None and bound <= _I32_LIMIT:
+        return L.to_device(a, np.int32)
+    return L.to_device(a, np.int64)
+
+
+def _idx_pair(ix, iz, bx=None, bz=None):
+    """(ixd, izd) of one index width: int32 when both fit, else both int64."""
+    t = L.torch()
+    ixd, izd = _idx_dev(ix, bx), _idx_dev(iz, bz)
+    if ixd.dtype != izd.dtype:
+        ixd, izd = ixd.to(t.int64), izd.to(t.int64)
+    if ixd.dtype not in (t.int32, t.int64):
+        raise TypeError(f"pair indices must be int32 or int64, not {ixd.dtype}")
+    return ixd, izd
+
+
+def _off_dev(pair_off, pair_off_dev):
+    return pair_off_dev if pair_off_dev is not None else L.to_device(
+        np.asarray(pair_off, dtype=np.int64))
 
 
 def count_indexed_dev(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray, pred: int,
                       pair_off_dev=None):
-    """Per-shard counts over index pairs, enqueued only: the (n_shards,) int64 device tensor
-    (uint64 semantics)."""
+    """Per-shard counts over index pairs gathered from the scores (no shard spans), enqueued
+    only: the (n_shards,) int64 device tensor (uint64 semantics)."""
     t = L.torch()
     n = len(pair_off) - 1
-    ixd, izd = _idx_dev(ix), _idx_dev(iz)
-    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
-    max_pairs = int(np.diff(pair_off).max())
-    out = L.empty((n,), t.int64)
-    L.call("tw_count_pairs_idx", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd),
-           L.ptr(pod), n, max_pairs, dtype_code, pred, L.ptr(out), L.stream_handle())
+    ixd, izd = _idx_pair(ix, iz, x_dev.numel(), z_dev.numel())
+    pod = _off_dev(pair_off, pair_off_dev)
+    max_pairs = int(np.diff(pair_off).max()) if n else 0
+    out = L.empty((max(n, 1),), t.int64)[:n]
+    name = "tw_count_pairs_idx32" if ixd.dtype == t.int32 else "tw_count_pairs_idx"
+    L.call(name, L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd), L.ptr(pod), n, max_pairs,
+           dtype_code, pred, L.ptr(out), L.stream_handle())
     return out
 
 
@@ -208,37 +234,37 @@ def count_indexed_ranked_dev(x_dev, x_off_dev, z_dev, z_off_dev, max_nx: int, ma
                              dtype_code: int, ix, iz, pair_off: np.ndarray, pred: int,
                              pair_off_dev=None, work=None):
     """count_indexed_dev for shard-contiguous samples (shard s = x[x_off[s]:x_off[s+1]]): the
-    same integers, compared on 16-bit rank codes in LDS (tw_count_pairs_idx_ws; it runs the
+    same integers, compared on 16-bit rank codes in LDS (tw_count_pairs_idx(32)_ws; it runs the
     plain kernel where codes do not apply).  `work` may be a cached uint8 device buffer of
     tw_count_pairs_rng_work_bytes bytes."""
     t = L.torch()
     n = len(pair_off) - 1
-    ixd, izd = _idx_dev(ix), _idx_dev(iz)
-    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
+    ixd, izd = _idx_pair(ix, iz, x_dev.numel(), z_dev.numel())
+    pod = _off_dev(pair_off, pair_off_dev)
     max_pairs = int(np.diff(pair_off).max()) if n else 0
     wpred = L.TW_PRED_GT if (pred == L.TW_PRED_SUBGT and dtype_code == L.TW_F64) else pred
     wb = int(L.lib().tw_count_pairs_rng_work_bytes(n, max_nx, max_nz, dtype_code, wpred))
     if wb > 0 and (work is None or work.numel() < wb):
         work = L.empty((wb,), t.uint8)
     out = L.empty((max(n, 1),), t.int64)[:n]
-    L.call("tw_count_pairs_idx_ws", L.ptr(x_dev), L.ptr(x_off_dev), L.ptr(z_dev),
-           L.ptr(z_off_dev), n, max_nx, max_nz, L.ptr(ixd), L.ptr(izd), L.ptr(pod), max_pairs,
-           dtype_code, pred, L.ptr(work if wb > 0 else None), wb, L.ptr(out),
-           L.stream_handle())
+    name = "tw_count_pairs_idx32_ws" if ixd.dtype == t.int32 else "tw_count_pairs_idx_ws"
+    L.call(name, L.ptr(x_dev), L.ptr(x_off_dev), L.ptr(z_dev), L.ptr(z_off_dev), n, max_nx,
+           max_nz, L.ptr(ixd), L.ptr(izd), L.ptr(pod), max_pairs, dtype_code, pred,
+           L.ptr(work if wb > 0 else None), wb, L.ptr(out), L.stream_handle())
     return out
 
 
 def count_indexed(x_dev, z_dev, dtype_code: int, ix, iz, pair_off: np.ndarray,
                   mode: str = "gt", pair_off_dev=None, spans=None) -> np.ndarray:
     """Per-shard counts over explicit (absolute) index pairs (host or device index arrays).
-    spans = (x_off, z_off): shard s draws mostly from x[x_off[s]:x_off[s+1]] and
-    z[z_off[s]:z_off[s+1]] (UB on slice blocks); the counts then run on LDS rank codes
-    (count_indexed_ranked_dev) — the same integers for any indices."""
+    spans = (x_off, z_off): shard s draws (mostly) from x[x_off[s]:x_off[s+1]] and
+    z[z_off[s]:z_off[s+1]]; the counts then run on LDS rank codes (count_indexed_ranked_dev),
+    the same integers for any indices.  Without spans the pairs gather the scores."""
     n = len(pair_off) - 1
     if n == 0:
         return np.zeros(0, dtype=np.uint64)
-    ixd, izd = _idx_dev(ix), _idx_dev(iz)
-    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
+    ixd, izd = _idx_pair(ix, iz, x_dev.numel(), z_dev.numel())
+    pod = _off_dev(pair_off, pair_off_dev)
     if spans is not None:
         xo, zo = (np.asarray(a, dtype=np.int64) for a in spans)
         xod, zod = L.to_device(xo), L.to_device(zo)
@@ -291,18 +317,28 @@ def pair_sum_indexed(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 
 
 
 def pair_sum_indexed_dev(x_dev, z_dev, ix, iz, pair_off, kern: int, margin: float = 0.0,
-                         pair_off_dev=None):
-    """pair_sum_indexed, enqueued only: the (n_shards,) float64 device tensor."""
+                         pair_off_dev=None, count_out=None):
+    """pair_sum_indexed, enqueued only: the (n_shards,) float64 device tensor.  count_out
+    (int32 indices only): an (n_shards,) int64 device tensor that receives #{x > z} over the
+    same pairs from the same pass (tw_pair_sum_idx32_f64)."""
     n = len(pair_off) - 1
     t = L.torch()
-    ixd, izd = _idx_dev(ix), _idx_dev(iz)
-    pod = pair_off_dev if pair_off_dev is not None else _idx_dev(pair_off)
+    ixd, izd = _idx_pair(ix, iz, x_dev.numel(), z_dev.numel())
+    pod = _off_dev(pair_off, pair_off_dev)
     max_pairs = int(np.diff(pair_off).max())
     per = int(L.lib().tw_pair_sum_idx_work_per_shard(max_pairs))
     work = L.empty((per * n,), t.float64)
     out = L.empty((n,), t.float64)
-    L.call("tw_pair_sum_idx_f64", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd), L.ptr(pod),
-           n, max_pairs, kern, float(margin), L.ptr(work), L.ptr(out), L.stream_handle())
+    if ixd.dtype == t.int32:
+        L.call("tw_pair_sum_idx32_f64", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd),
+               L.ptr(pod), n, max_pairs, kern, float(margin), L.ptr(work), L.ptr(out),
+               L.ptr(count_out), L.stream_handle())
+    else:
+        if count_out is not None:
+            raise ValueError("count_out needs int32 pair indices")
+        L.call("tw_pair_sum_idx_f64", L.ptr(x_dev), L.ptr(z_dev), L.ptr(ixd), L.ptr(izd),
+               L.ptr(pod), n, max_pairs, kern, float(margin), L.ptr(work), L.ptr(out),
+               L.stream_handle())
     return out
 
 

@@ -39,8 +39,12 @@ _SIGNATURES = {
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],
     "tw_count_pairs_idx": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _vp],
     "tw_count_idx_set_parts": [_i32],
+    "tw_count_idx_set_variant": [_i32],
     "tw_count_pairs_idx_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _i64, _i32,
                               _i32, _vp, _i64, _vp, _vp],
+    "tw_count_pairs_idx32": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _vp],
+    "tw_count_pairs_idx32_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _vp, _i64, _i32,
+                                _i32, _vp, _i64, _vp, _vp],
     "tw_count_pairs_rng": [_vp, _vp, _vp, _vp, _i32, _i64, _u64, _u64, _i32, _i32, _vp, _vp],
     "tw_count_pairs_rng_work_bytes": [_i32, _i64, _i64, _i32, _i32],
     "tw_count_rng_set_codes": [_i32],
@@ -51,6 +55,8 @@ _SIGNATURES = {
     "tw_pair_sum_f64": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _f64, _vp, _vp, _vp],
     "tw_pair_sum_idx_work_per_shard": [_i64],
     "tw_pair_sum_idx_f64": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _f64, _vp, _vp, _vp],
+    "tw_pair_sum_idx32_f64": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _f64, _vp, _vp, _vp,
+                              _vp],
     "tw_hinge_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64,
                       _vp, _vp],
     "tw_pair_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64, _i32,

@@ -271,11 +271,12 @@ __global__ __launch_bounds__(kBlock) void k_count_complete(
 }
 
 // Incomplete count on explicit index pairs (replay of NumPy's randint draws).
-template <typename T, int PRED, int PPT>
+// I: int64_t (NumPy's randint dtype) or int32_t (narrowed by the host after its bound check).
+template <typename T, int PRED, int PPT, typename I>
 __global__ __launch_bounds__(kBlock) void k_count_idx(const T* __restrict__ x,
                                                       const T* __restrict__ z,
-                                                      const int64_t* __restrict__ ix,
-                                                      const int64_t* __restrict__ iz,
+                                                      const I* __restrict__ ix,
+                                                      const I* __restrict__ iz,
                                                       const int64_t* __restrict__ pair_off,
                                                       int blocks_per_shard,
                                                       unsigned long long* __restrict__ out) {
@@ -487,13 +488,13 @@ int dispatch_complete(int32_t pred, const void* x, const int64_t* x_off, const v
 
 constexpr int kPPT = 8;  // pairs per thread in the incomplete kernels
 
-template <typename T, int PRED>
-int launch_idx(const void* x, const void* z, const int64_t* ix, const int64_t* iz,
+template <typename T, int PRED, typename I>
+int launch_idx(const void* x, const void* z, const I* ix, const I* iz,
                const int64_t* pair_off, int32_t n_shards, int64_t max_pairs, uint64_t* out,
                hipStream_t st) {
   const int64_t bps = std::max<int64_t>(1, ceil_div(max_pairs, (int64_t)kBlock * kPPT));
   TW_ARG_CHECK(bps * n_shards < (1ll << 31), "tw_count_pairs_idx: grid too large");
-  hipLaunchKernelGGL((k_count_idx<T, PRED, kPPT>), dim3((unsigned)(bps * n_shards)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL((k_count_idx<T, PRED, kPPT, I>), dim3((unsigned)(bps * n_shards)), dim3(kBlock), 0, st,
                      (const T*)x, (const T*)z, ix, iz, pair_off, (int)bps, (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
@@ -618,16 +619,17 @@ extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, cons
   return dispatch_complete<long long>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, nxt, st);
 }
 
-extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
-                                  const int64_t* d_iz, const int64_t* d_pair_off,
-                                  int32_t n_shards, int64_t max_pairs, int32_t dtype,
-                                  int32_t pred, uint64_t* d_out, void* stream) {
+namespace tw {
+template <typename I>
+int count_idx(const void* d_x, const void* d_z, const I* d_ix, const I* d_iz,
+              const int64_t* d_pair_off, int32_t n_shards, int64_t max_pairs, int32_t dtype,
+              int32_t pred, uint64_t* d_out, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && max_pairs >= 0, "tw_count_pairs_idx: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
   TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (max_pairs == 0) return TW_OK;
-#define TW_IDX(T, P) return launch_idx<T, P>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, d_out, st)
+#define TW_IDX(T, P) return launch_idx<T, P, I>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, d_out, st)
   if (dtype == TW_F64) {
     if (pred == TW_PRED_GT || pred == TW_PRED_SUBGT) TW_IDX(double, TW_PRED_GT);
     if (pred == TW_PRED_HALF) TW_IDX(double, TW_PRED_HALF);
@@ -639,6 +641,23 @@ extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_
 #undef TW_IDX
   set_error("tw_count_pairs_idx: unknown dtype %d / predicate %d", dtype, pred);
   return TW_ERR_ARG;
+}
+}  // namespace tw
+
+extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_t* d_ix,
+                                  const int64_t* d_iz, const int64_t* d_pair_off,
+                                  int32_t n_shards, int64_t max_pairs, int32_t dtype,
+                                  int32_t pred, uint64_t* d_out, void* stream) {
+  return count_idx<int64_t>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, dtype, pred,
+                            d_out, stream);
+}
+
+extern "C" int tw_count_pairs_idx32(const void* d_x, const void* d_z, const int32_t* d_ix,
+                                    const int32_t* d_iz, const int64_t* d_pair_off,
+                                    int32_t n_shards, int64_t max_pairs, int32_t dtype,
+                                    int32_t pred, uint64_t* d_out, void* stream) {
+  return count_idx<int32_t>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, dtype, pred,
+                            d_out, stream);
 }
 
 extern "C" int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const void* d_z,

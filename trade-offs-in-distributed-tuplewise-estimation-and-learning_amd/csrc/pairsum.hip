@@ -93,28 +93,41 @@ __global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ 
   if (threadIdx.x == 0) work[blockIdx.x] = b;
 }
 
-template <int K, int PPT>
+// I: int64_t or int32_t indices.  COUNT: the same pass also counts x > z per shard into
+// count[s] (evaluation_step's br_AUC = UB_pairs(kernel="AUC") on the monitor pairs whose hinge
+// mean it computes, make_exps.py:162-168): one read of the index streams for both statistics.
+template <int K, int PPT, typename I, bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_pair_sum_idx(const double* __restrict__ x,
                                                          const double* __restrict__ z,
-                                                         const int64_t* __restrict__ ix,
-                                                         const int64_t* __restrict__ iz,
+                                                         const I* __restrict__ ix,
+                                                         const I* __restrict__ iz,
                                                          const int64_t* __restrict__ pair_off,
                                                          int blocks_per_shard, double margin,
-                                                         double* __restrict__ work) {
+                                                         double* __restrict__ work,
+                                                         unsigned long long* __restrict__ count) {
   const int s = blockIdx.x / blocks_per_shard;
   const int bi = blockIdx.x - s * blocks_per_shard;
   const int64_t pb = pair_off[s], pe = pair_off[s + 1];
   const int64_t p0 = pb + (int64_t)bi * (kBlock * PPT);
   double acc = 0.0;
+  unsigned cnt = 0;
   if (p0 < pe) {
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const int64_t p = p0 + k * kBlock + threadIdx.x;
-      if (p < pe) acc += fkern<K>(x[ix[p]], z[iz[p]], margin);
+      if (p < pe) {
+        const double xv = x[ix[p]], zv = z[iz[p]];
+        acc += fkern<K>(xv, zv, margin);
+        if (COUNT) cnt += xv > zv;
+      }
     }
   }
   const double b = block_sum_f64(acc);
   if (threadIdx.x == 0) work[blockIdx.x] = b;
+  if constexpr (COUNT) {
+    const unsigned long long w = wave_sum_u64((unsigned long long)cnt);
+    if ((threadIdx.x & (kWave - 1)) == 0 && w) atomicAdd(count + s, w);
+  }
 }
 
 // out[s] = ordered sum of work[s*per : (s+1)*per]; one wave per shard, lane-strided partial
@@ -165,23 +178,51 @@ extern "C" int tw_pair_sum_f64(const double* d_x, const int64_t* d_x_off, const 
   return TW_OK;
 }
 
+namespace tw {
+template <typename I, bool COUNT>
+int pair_sum_idx(const double* d_x, const double* d_z, const I* d_ix, const I* d_iz,
+                 const int64_t* d_pair_off, int32_t n_shards, int64_t max_pairs, int32_t kern,
+                 double margin, double* d_work, double* d_out, uint64_t* d_count,
+                 hipStream_t st) {
+  const int64_t per = tw_pair_sum_idx_work_per_shard(max_pairs);
+  TW_ARG_CHECK(per * n_shards < (1ll << 31), "tw_pair_sum_idx_f64: grid too large");
+  dim3 g((unsigned)(per * n_shards)), b(kBlock);
+  unsigned long long* cnt = (unsigned long long*)d_count;
+  if (kern == TW_KERN_PROD) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_PROD, kSumPPT, I, COUNT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work, cnt);
+  else if (kern == TW_KERN_GINI) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_GINI, kSumPPT, I, COUNT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work, cnt);
+  else if (kern == TW_KERN_HINGE) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_HINGE, kSumPPT, I, COUNT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work, cnt);
+  else hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_LOGISTIC, kSumPPT, I, COUNT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work, cnt);
+  TW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_reduce_partials, dim3(n_shards), dim3(kWave), 0, st, d_work, (int)per, d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+}  // namespace tw
+
 extern "C" int tw_pair_sum_idx_f64(const double* d_x, const double* d_z, const int64_t* d_ix,
                                    const int64_t* d_iz, const int64_t* d_pair_off,
                                    int32_t n_shards, int64_t max_pairs, int32_t kern,
                                    double margin, double* d_work, double* d_out, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && max_pairs >= 0, "tw_pair_sum_idx_f64: bad sizes");
   TW_ARG_CHECK(kern >= TW_KERN_PROD && kern <= TW_KERN_LOGISTIC, "tw_pair_sum_idx_f64: unknown kernel %d", kern);
+  if (n_shards == 0) return TW_OK;
+  return pair_sum_idx<int64_t, false>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, kern,
+                                      margin, d_work, d_out, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int tw_pair_sum_idx32_f64(const double* d_x, const double* d_z, const int32_t* d_ix,
+                                     const int32_t* d_iz, const int64_t* d_pair_off,
+                                     int32_t n_shards, int64_t max_pairs, int32_t kern,
+                                     double margin, double* d_work, double* d_out,
+                                     uint64_t* d_count, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && max_pairs >= 0, "tw_pair_sum_idx32_f64: bad sizes");
+  TW_ARG_CHECK(kern >= TW_KERN_PROD && kern <= TW_KERN_LOGISTIC, "tw_pair_sum_idx32_f64: unknown kernel %d", kern);
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
-  const int64_t per = tw_pair_sum_idx_work_per_shard(max_pairs);
-  TW_ARG_CHECK(per * n_shards < (1ll << 31), "tw_pair_sum_idx_f64: grid too large");
-  dim3 g((unsigned)(per * n_shards)), b(kBlock);
-  if (kern == TW_KERN_PROD) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_PROD, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
-  else if (kern == TW_KERN_GINI) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_GINI, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
-  else if (kern == TW_KERN_HINGE) hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_HINGE, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
-  else hipLaunchKernelGGL((k_pair_sum_idx<TW_KERN_LOGISTIC, kSumPPT>), g, b, 0, st, d_x, d_z, d_ix, d_iz, d_pair_off, (int)per, margin, d_work);
-  TW_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_reduce_partials, dim3(n_shards), dim3(kWave), 0, st, d_work, (int)per, d_out);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+  if (d_count == nullptr)
+    return pair_sum_idx<int32_t, false>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs,
+                                        kern, margin, d_work, d_out, nullptr, st);
+  TW_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t) * n_shards, st));
+  return pair_sum_idx<int32_t, true>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, kern,
+                                     margin, d_work, d_out, d_count, st);
 }

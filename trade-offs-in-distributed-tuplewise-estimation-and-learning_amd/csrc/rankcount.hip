@@ -20,6 +20,24 @@
 #include <algorithm>
 #include <type_traits>
 
+// Phase timestamps for kernel studies (tools/phase_codes.py builds a separate library with
+// -DTW_PHASE_TIMING; the product build compiles them out).
+#ifdef TW_PHASE_TIMING
+__device__ unsigned long long g_tw_phase[1 << 16];
+#define TW_PHASE(k)                                                                    \
+  do {                                                                                 \
+    if (threadIdx.x == 0) g_tw_phase[((size_t)blockIdx.x * 8 + (k)) & 0xFFFF] = clock64(); \
+  } while (0)
+extern "C" int tw_debug_phases(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tw_phase), sizeof(unsigned long long) * n) ==
+                 hipSuccess ? 0 : 2;
+}
+#else
+#define TW_PHASE(k) \
+  do {              \
+  } while (0)
+#endif
+
 namespace tw {
 
 constexpr int kXPerThread = 4;
@@ -97,37 +115,74 @@ inline RankPlan plan_rank(int64_t max_nx, int64_t max_nz) {
 }
 
 // Rank codes without a sort (shards with nz <= kBucketMaxZ): the block loads the shard's z
-// into LDS, buckets it by VALUE — b(v) = clamp(int((v - zmin) * NB / (zmax - zmin)), 0, NB-1)
-// over the finite z, a monotone map (every IEEE step in it is monotone), so bucket order is
-// value order — with an LDS histogram, prefix sum and scatter, and then a code is
-//   (#z in lower buckets) + (#z in its own bucket below / at most v)
-// by a scan of one bucket (~nz / NB values for smooth data).  Exact for any data: ties share
-// a bucket; NaN z sit in no bucket (their p is the count of non-NaN z, above every x code),
-// NaN x get code 0, +-inf clamp to the end buckets; degenerate or very skewed data only make
-// the scans longer.  Every block of a shard rebuilds the buckets (O(nz) LDS work) and codes
-// its share of the shard's x and z.  Replaces k_sort_chunks + k_rank_codes (41 + 78 us at
-// the bench shape).
+// into LDS, buckets it by VALUE with an LDS histogram, prefix sum and scatter, and then a code
+// is (#z in lower buckets) + (#z in its own bucket below / at most v), by a scan of one bucket.
+// Bucket map, two levels, both monotone (every IEEE step in them is monotone), so bucket order
+// is value order:
+//   coarse  u = (v - zmin) * NB / (zmax - zmin) over the finite z, b = clamp(floor(u)), and the
+//           position t = clamp(u - b, 0, 1) inside the bucket;
+//   fine    (refine = 1) the coarse histogram's prefix cs turns it into an equal-depth map,
+//           f = min(NB - 1, floor((cs[b] + t * (cs[b+1] - cs[b])) * NB / n)): the piecewise-linear
+//           empirical CDF of z, so every fine bucket holds ~n / NB values whatever the shape of
+//           the data (Gaussian scores put ~25 values in the central coarse buckets of a
+//           15625-value shard and ~8 in a fine one; the scans are the kernel's main cost).
+// Exact for any data: ties share a bucket; NaN z sit in no bucket (their p is the count of
+// non-NaN z, above every x code), NaN x get code 0, +-inf clamp to the end buckets; degenerate
+// or very skewed data only make the scans longer.  Every block of a shard rebuilds the buckets
+// (O(nz) LDS work) and codes its share of the shard's x and z.  Replaces k_sort_chunks +
+// k_rank_codes (41 + 78 us at the bench shape).
 constexpr int kBucketNB = 2048;
 constexpr int64_t kBucketMaxZ = 16384;  // 128 KiB of z in LDS
-constexpr int kBucketParts = 4;
+constexpr size_t kBucketLds = sizeof(double) * kBucketMaxZ + sizeof(unsigned) * (3 * kBucketNB + 2);
 
 template <typename T>
 __device__ __forceinline__ double bucket_value(T v) { return (double)v; }
 
+constexpr int kZPer = (int)(kBucketMaxZ / kSortThreads);  // z-values per thread (registers)
+constexpr int kEPer = 8;  // code elements per thread per round, loads issued together
+
+// Exclusive prefix of cnt[0 .. NB) into st[0 .. NB] (st[NB] = total), two buckets per thread.
+__device__ __forceinline__ void bucket_prefix(const unsigned* cnt, unsigned* st,
+                                              unsigned* wave_tot) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const int i0 = 2 * tid;  // kBucketNB == 2 * kSortThreads
+  const unsigned a = cnt[i0], b = cnt[i0 + 1];
+  unsigned v = a + b;
+  for (int o = 1; o < kWave; o <<= 1) {  // inclusive wave scan
+    const unsigned t = __shfl_up(v, o, kWave);
+    if (lane >= o) v += t;
+  }
+  if (lane == kWave - 1) wave_tot[wid] = v;
+  __syncthreads();
+  unsigned base = 0;
+  for (int w = 0; w < wid; ++w) base += wave_tot[w];
+  const unsigned excl = base + v - (a + b);
+  st[i0] = excl;
+  st[i0 + 1] = excl + a;
+  if (tid == kSortThreads - 1) st[kBucketNB] = excl + a + b;
+  __syncthreads();
+}
+
 // COUNT = true: the complete count instead of codes (tw_count_pairs_sorted): the same
 // buckets, only the x-values, and the block's sum of their codes (#z < x, plus #z <= x for
 // half-ties) added to out[s] — the integer of k_count_complete / k_rank_count.
+// The shard's z is loaded ONCE into registers (kZPer per thread, all loads in flight
+// together) and the range, histogram and scatter passes read the registers; the first round
+// of this block's code elements is loaded beside it.  Bucket scans read four values per trip.
+// Codes are written with row strides sx / sz (multiples of 8, so rows are 16-B aligned).
 template <typename T, int PRED, bool COUNT = false>
 __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
-    const int64_t* __restrict__ z_off, int parts, int64_t max_nx, int64_t max_nz,
+    const int64_t* __restrict__ z_off, int parts, int refine, int64_t sx, int64_t sz,
     uint16_t* __restrict__ cx, uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz,
     unsigned long long* __restrict__ out = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* zb = (T*)smem;                                       // z by bucket (kBucketMaxZ)
-  unsigned* start = (unsigned*)(smem + sizeof(T) * kBucketMaxZ);  // NB + 1 bucket starts
-  unsigned* cur = start + kBucketNB + 1;                  // NB fill cursors / counts
+  T* zb = (T*)smem;                                                 // z by bucket
+  unsigned* cs = (unsigned*)(smem + sizeof(double) * kBucketMaxZ);  // NB + 1 coarse prefix
+  unsigned* fst = cs + kBucketNB + 1;                               // NB + 1 fine starts
+  unsigned* cur = fst + kBucketNB + 1;                              // NB counts / cursors
   __shared__ double red_min[kSortThreads / kWave], red_max[kSortThreads / kWave];
+  __shared__ unsigned wave_tot[kSortThreads / kWave];
   __shared__ unsigned nan_z;
   const int lb = xcd_block(blockIdx.x, gridDim.x);
   const int s = lb / parts;
@@ -135,11 +190,29 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
   const int64_t xb = x_off[s], nx = x_off[s + 1] - xb;
   const int64_t zo = z_off[s], nz = z_off[s + 1] - zo;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  // this block's share of the shard's elements (x first, then z; COUNT: x only)
+  const int64_t tot = COUNT ? nx : nx + nz, per = (tot + parts - 1) / parts;
+  const int64_t e0 = (int64_t)part * per, e1 = e0 + per < tot ? e0 + per : tot;
+  auto elem = [&](int64_t e) -> T { return e < nx ? x[xb + e] : z[zo + (e - nx)]; };
+  TW_PHASE(0);
+  // 0. all loads of the first phase in flight at once: the shard's z, the first code round
+  T zr[kZPer], er[kEPer];
+#pragma unroll
+  for (int r = 0; r < kZPer; ++r) {
+    const int64_t j = tid + (int64_t)r * kSortThreads;
+    zr[r] = j < nz ? z[zo + j] : (T)0;
+  }
+#pragma unroll
+  for (int r = 0; r < kEPer; ++r) {
+    const int64_t e = e0 + tid + (int64_t)r * kSortThreads;
+    er[r] = e < e1 ? elem(e) : (T)0;
+  }
   // 1. range of the finite z
   double mn = __builtin_inf(), mx = -__builtin_inf();
-  for (int64_t j = tid; j < nz; j += kSortThreads) {
-    const double v = bucket_value<T>(z[zo + j]);
-    if (v - v == 0.0) {  // finite (not NaN, not inf)
+#pragma unroll
+  for (int r = 0; r < kZPer; ++r) {
+    const double v = bucket_value<T>(zr[r]);
+    if (tid + (int64_t)r * kSortThreads < nz && v - v == 0.0) {  // finite (not NaN, not inf)
       mn = v < mn ? v : mn;
       mx = v > mx ? v : mx;
     }
@@ -156,6 +229,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     red_max[wid] = mx;
   }
   __syncthreads();
+  TW_PHASE(1);
   mn = red_min[0];
   mx = red_max[0];
   for (int w = 1; w < kSortThreads / kWave; ++w) {
@@ -163,78 +237,111 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     mx = red_max[w] > mx ? red_max[w] : mx;
   }
   const double scale = mx > mn ? (double)kBucketNB / (mx - mn) : 0.0;
-  auto bucket = [&](double v) -> int {
-    const double t = (v - mn) * scale;  // NaN when v == mn and scale == inf: bucket 0
-    return (int)__builtin_fmin(__builtin_fmax(t, 0.0), (double)(kBucketNB - 1));
+  // coarse bucket of v and its position t in [0, 1] inside it (NaN u -> bucket 0, t = 0)
+  auto coarse = [&](double v, double& t) -> int {
+    const double u = (v - mn) * scale;
+    const int b = (int)__builtin_fmin(__builtin_fmax(u, 0.0), (double)(kBucketNB - 1));
+    t = __builtin_fmin(__builtin_fmax(u - (double)b, 0.0), 1.0);
+    return b;
   };
-  // 2. histogram (NaN z counted apart)
-  for (int64_t j = tid; j < nz; j += kSortThreads) {
-    const T v = z[zo + j];
-    if (is_nan_score<T>(v)) atomicAdd(&nan_z, 1u);
-    else atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u);
+  // 2. coarse histogram (NaN z counted apart) and its prefix
+  bool zin[kZPer];
+  int zbk[kZPer];
+#pragma unroll
+  for (int r = 0; r < kZPer; ++r) {
+    zin[r] = tid + (int64_t)r * kSortThreads < nz && !is_nan_score<T>(zr[r]);
+    double t;
+    zbk[r] = coarse(bucket_value<T>(zr[r]), t);
+    if (zin[r]) atomicAdd(&cur[zbk[r]], 1u);
+    else if (tid + (int64_t)r * kSortThreads < nz) atomicAdd(&nan_z, 1u);
   }
   __syncthreads();
-  // 3. exclusive prefix over NB buckets (two per thread, then a block scan of the pairs)
-  {
-    const int i0 = 2 * tid;  // kBucketNB == 2 * kSortThreads
-    const unsigned a = cur[i0], b = cur[i0 + 1];
-    unsigned v = a + b;
-    for (int o = 1; o < kWave; o <<= 1) {  // inclusive wave scan
-      const unsigned t = __shfl_up(v, o, kWave);
-      if (lane >= o) v += t;
-    }
-    __shared__ unsigned wave_tot[kSortThreads / kWave];
-    if (lane == kWave - 1) wave_tot[wid] = v;
+  bucket_prefix(cur, cs, wave_tot);
+  TW_PHASE(2);
+  const unsigned n_valid = cs[kBucketNB];
+  const double fscale = (double)kBucketNB / (double)n_valid;
+  auto bucket = [&](double v) -> int {
+    double t;
+    const int b = coarse(v, t);
+    if (!refine) return b;
+    const unsigned c0 = cs[b], c1 = cs[b + 1];
+    const double pos = (double)c0 + t * (double)(c1 - c0);
+    return (int)__builtin_fmin(pos * fscale, (double)(kBucketNB - 1));  // NaN (n = 0): NB - 1
+  };
+  const unsigned* st = cs;  // bucket starts of the map in use
+  if (refine) {  // 3. fine (equal-depth) histogram and its prefix
+    for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = 0;
     __syncthreads();
-    unsigned base = 0;
-    for (int w = 0; w < wid; ++w) base += wave_tot[w];
-    const unsigned excl = base + v - (a + b);
-    start[i0] = excl;
-    start[i0 + 1] = excl + a;
-    if (tid == kSortThreads - 1) start[kBucketNB] = excl + a + b;
-    __syncthreads();
-    cur[i0] = excl;
-    cur[i0 + 1] = excl + a;
-  }
-  __syncthreads();
-  // 4. scatter z into bucket order
-  for (int64_t j = tid; j < nz; j += kSortThreads) {
-    const T v = z[zo + j];
-    if (!is_nan_score<T>(v)) zb[atomicAdd(&cur[bucket(bucket_value<T>(v))], 1u)] = v;
-  }
-  __syncthreads();
-  const unsigned n_valid = start[kBucketNB];
-  // 5. codes of this block's share of the shard's x and z (COUNT: of its x only)
-  const int64_t tot = COUNT ? nx : nx + nz, per = (tot + parts - 1) / parts;
-  const int64_t e0 = (int64_t)part * per, e1 = e0 + per < tot ? e0 + per : tot;
-  unsigned long long acc = 0;
-  for (int64_t e = e0 + tid; e < e1; e += kSortThreads) {
-    const bool isx = e < nx;
-    const T v = isx ? x[xb + e] : z[zo + (e - nx)];
-    unsigned lo = 0, hi = 0;
-    if (is_nan_score<T>(v)) {
-      lo = isx ? 0u : n_valid;  // NaN x: below every p; NaN z: above every c
-      hi = lo;
-    } else {
-      const int b = bucket(bucket_value<T>(v));
-      const unsigned b0 = start[b], b1 = start[b + 1];
-      lo = b0;
-      hi = b0;
-      for (unsigned q = b0; q < b1; ++q) {
-        const T w = zb[q];
-        lo += w < v;
-        hi += w <= v;
+#pragma unroll
+    for (int r = 0; r < kZPer; ++r) {
+      if (zin[r]) {
+        zbk[r] = bucket(bucket_value<T>(zr[r]));
+        atomicAdd(&cur[zbk[r]], 1u);
       }
     }
-    if constexpr (COUNT) {
-      acc += lo + (PRED == TW_PRED_HALF ? hi : 0u);
-    } else if (isx) {
-      cx[(int64_t)s * max_nx + e] = (uint16_t)lo;
-      if (PRED == TW_PRED_HALF) cx2[(int64_t)s * max_nx + e] = (uint16_t)hi;
-    } else {
-      pz[(int64_t)s * max_nz + (e - nx)] = (uint16_t)lo;
+    __syncthreads();
+    bucket_prefix(cur, fst, wave_tot);
+    st = fst;
+  }
+  TW_PHASE(3);
+  // 4. scatter z into bucket order
+  for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = st[i];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kZPer; ++r)
+    if (zin[r]) zb[atomicAdd(&cur[zbk[r]], 1u)] = zr[r];
+  __syncthreads();
+  TW_PHASE(4);
+  // 5. codes of this block's share (rounds of kEPer elements per thread; the first is loaded)
+  unsigned long long acc = 0;
+  for (int64_t r0 = e0; r0 < e1; r0 += (int64_t)kEPer * kSortThreads) {
+    if (r0 != e0) {
+#pragma unroll
+      for (int r = 0; r < kEPer; ++r) {
+        const int64_t e = r0 + tid + (int64_t)r * kSortThreads;
+        er[r] = e < e1 ? elem(e) : (T)0;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kEPer; ++r) {
+      const int64_t e = r0 + tid + (int64_t)r * kSortThreads;
+      if (e >= e1) continue;
+      const bool isx = e < nx;
+      const T v = er[r];
+      unsigned lo = 0, hi = 0;
+      if (is_nan_score<T>(v)) {
+        lo = isx ? 0u : n_valid;  // NaN x: below every p; NaN z: above every c
+        hi = lo;
+      } else {
+        const int b = bucket(bucket_value<T>(v));
+        const unsigned b0 = st[b], b1 = st[b + 1];
+        lo = b0;
+        hi = b0;
+        unsigned q = b0;
+        for (; q + 4 <= b1; q += 4) {  // four independent LDS reads per trip
+          const T w0 = zb[q], w1 = zb[q + 1], w2 = zb[q + 2], w3 = zb[q + 3];
+          lo += (unsigned)(w0 < v) + (unsigned)(w1 < v) + (unsigned)(w2 < v) + (unsigned)(w3 < v);
+          if (PRED == TW_PRED_HALF)
+            hi += (unsigned)(w0 <= v) + (unsigned)(w1 <= v) + (unsigned)(w2 <= v) +
+                  (unsigned)(w3 <= v);
+        }
+        for (; q < b1; ++q) {
+          const T w = zb[q];
+          lo += w < v;
+          if (PRED == TW_PRED_HALF) hi += w <= v;
+        }
+      }
+      if constexpr (COUNT) {
+        acc += lo + (PRED == TW_PRED_HALF ? hi : 0u);
+      } else if (isx) {
+        cx[(int64_t)s * sx + e] = (uint16_t)lo;
+        if (PRED == TW_PRED_HALF) cx2[(int64_t)s * sx + e] = (uint16_t)hi;
+      } else {
+        pz[(int64_t)s * sz + (e - nx)] = (uint16_t)lo;
+      }
     }
   }
+  TW_PHASE(5);
   if constexpr (COUNT) {
     acc = wave_sum_u64(acc);
     __shared__ unsigned long long part_acc[kSortThreads / kWave];
@@ -248,12 +355,14 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
   }
 }
 
-static int g_sorted_by_bucket = 1;  // tw_count_sorted_set_bucket: 0 = sort + binary search
+// tw_count_sorted_set_bucket: 0 = sort + binary search, 1 = equal-depth buckets (default),
+// 2 = coarse (value-range) buckets only
+static int g_sorted_by_bucket = 1;
 
 template <typename T, int PRED>
 int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                         int32_t n_shards, int64_t max_nx, uint64_t* out, hipStream_t st) {
-  const size_t lds_b = sizeof(T) * kBucketMaxZ + sizeof(unsigned) * (2 * kBucketNB + 1);
+  const size_t lds_b = kBucketLds;
   static bool attr = false;
   if (!attr) {
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_codes_bucket<T, PRED, true>,
@@ -267,7 +376,8 @@ int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, cons
   TW_ARG_CHECK((int64_t)n_shards * parts < (1ll << 31), "tw_count_pairs_sorted: grid too large");
   hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED, true>), dim3(n_shards * parts),
                      dim3(kSortThreads), lds_b, st, (const T*)x, x_off, (const T*)z, z_off, parts,
-                     max_nx, (int64_t)0, nullptr, nullptr, nullptr, (unsigned long long*)out);
+                     (int)(g_sorted_by_bucket == 1), max_nx, (int64_t)0, nullptr, nullptr, nullptr,
+                     (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -408,11 +518,43 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes(
   }
 }
 
+// Code rows in the work buffer and in LDS have strides rounded up to 8 codes, so a shard's
+// codes are staged with 16-B loads (2 per thread for a 15625-value shard pair) issued
+// together, instead of one dependent u16 load per loop trip.
+__device__ __forceinline__ int64_t al8(int64_t n) { return (n + 7) & ~(int64_t)7; }
+
+template <int PRED>
+__device__ __forceinline__ void stage_codes(uint16_t* __restrict__ lds, const uint16_t* __restrict__ cx,
+                                            const uint16_t* __restrict__ cx2,
+                                            const uint16_t* __restrict__ pz, int64_t nx,
+                                            int64_t nz) {
+  constexpr int NC = PRED == TW_PRED_HALF ? 2 : 1;
+  const int64_t vx = al8(nx) / 8, vz = al8(nz) / 8, tot = NC * vx + vz;
+  const uint4* sx = (const uint4*)cx;
+  const uint4* sx2 = (const uint4*)cx2;
+  const uint4* sz = (const uint4*)pz;
+  uint4* d = (uint4*)lds;  // [x codes | (x codes, >=) | z codes], each al8 long
+  constexpr int U = 4;
+  for (int64_t i0 = threadIdx.x; i0 < tot; i0 += (int64_t)U * blockDim.x) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < tot) v[u] = i < vx ? sx[i] : (NC == 2 && i < 2 * vx) ? sx2[i - vx] : sz[i - NC * vx];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < tot) d[i] = v[u];
+    }
+  }
+}
+
 template <int PRED>
 __global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
     const int64_t* __restrict__ x_off, const int64_t* __restrict__ z_off,
     const uint16_t* __restrict__ cx, const uint16_t* __restrict__ cx2,
-    const uint16_t* __restrict__ pz, int64_t max_nx, int64_t max_nz, int64_t B, int parts,
+    const uint16_t* __restrict__ pz, int64_t sx, int64_t sz, int64_t B, int parts,
     uint32_t k0, uint32_t k1, uint32_t sid, unsigned long long* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint16_t codes[];
   const int lb = xcd_block(blockIdx.x, gridDim.x);  // a shard's parts share one L2
@@ -422,13 +564,10 @@ __global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
   unsigned acc = 0;
   if (nx > 0 && nz > 0) {
     uint16_t* lx = codes;
-    uint16_t* lx2 = codes + nx;
-    uint16_t* lz = codes + (PRED == TW_PRED_HALF ? 2 : 1) * nx;
-    for (int64_t i = threadIdx.x; i < nx; i += kRngThreads) {
-      lx[i] = cx[(int64_t)s * max_nx + i];
-      if (PRED == TW_PRED_HALF) lx2[i] = cx2[(int64_t)s * max_nx + i];
-    }
-    for (int64_t j = threadIdx.x; j < nz; j += kRngThreads) lz[j] = pz[(int64_t)s * max_nz + j];
+    uint16_t* lx2 = codes + al8(nx);
+    uint16_t* lz = codes + (PRED == TW_PRED_HALF ? 2 : 1) * al8(nx);
+    stage_codes<PRED>(codes, cx + (int64_t)s * sx, cx2 + (int64_t)s * sx, pz + (int64_t)s * sz,
+                      nx, nz);
     __syncthreads();
     const uint32_t ss = (uint32_t)s + sid;
     const int64_t nq = (B + 1) / 2;
@@ -462,82 +601,182 @@ __global__ __launch_bounds__(kRngThreads) void k_count_rng_ranked(
   }
 }
 
+// 16-byte vectors of pair indices: 4 int32 or 2 int64 per load.
+template <typename I> struct IdxVec;
+typedef int32_t tw_i32x4 __attribute__((ext_vector_type(4)));
+typedef int64_t tw_i64x2 __attribute__((ext_vector_type(2)));
+template <> struct IdxVec<int32_t> {
+  using V = int4;
+  using NVec = tw_i32x4;  // clang vector of the same 16 bytes (nontemporal builtin operand)
+  static constexpr int N = 4;
+  __device__ static __forceinline__ int32_t at(const V& v, int e) {
+    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+  }
+};
+template <> struct IdxVec<int64_t> {
+  using V = longlong2;
+  using NVec = tw_i64x2;
+  static constexpr int N = 2;
+  __device__ static __forceinline__ int64_t at(const V& v, int e) { return e == 0 ? v.x : v.y; }
+};
+
 // Incomplete count on explicit index pairs (UB replay: NumPy's randint draws, compute_stats.py:
 // 22-42) through the rank codes: a block stages its shard's 16-bit codes in LDS, so the two
-// per-pair gathers are LDS reads and only the 16 B of indices per pair stream from HBM (the plain
-// k_count_idx pulls an L2 line per gathered score).  Indices are absolute; one outside its
-// shard's range (allowed by tw_count_pairs_idx) compares the scores themselves.
-template <typename T, int PRED>
-__global__ __launch_bounds__(kRngThreads) void k_count_idx_ranked(
+// per-pair gathers are LDS reads and only the indices stream from HBM — 8 B per pair with int32
+// indices, 16 B with int64 (the plain k_count_idx pulls an L2 line per
+// gathered score).  Indices are absolute; one outside its shard's span (allowed by
+// tw_count_pairs_idx) compares the scores themselves.
+// The index streams are read as 16-B vectors (VEC: the host checked the pointers' alignment;
+// unaligned heads/tails of a part go through scalar loads), U vectors of each stream per
+// thread and batch, the first batch issued BEFORE the codes are staged so its latency hides
+// behind the staging.  PIPE: each later batch is issued before the previous one is compared
+// (two register buffers); otherwise after it (one buffer; the other waves hide the latency).
+// int32 indices use 32-bit offset arithmetic.  Two 1024-thread blocks per CU (62.5 KiB of
+// codes each) need <= 64 VGPRs: __launch_bounds__(1024, 8) = 8 waves per SIMD.
+template <typename T, int PRED, typename I, bool VEC, int UV = 2, bool NT = false,
+          bool PIPE = true>
+__global__ __launch_bounds__(kRngThreads, 8) void k_count_idx_ranked(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, const uint16_t* __restrict__ cx,
-    const uint16_t* __restrict__ cx2, const uint16_t* __restrict__ pz, int64_t max_nx,
-    int64_t max_nz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz,
-    const int64_t* __restrict__ pair_off, int parts, unsigned long long* __restrict__ out) {
+    const uint16_t* __restrict__ cx2, const uint16_t* __restrict__ pz, int64_t sx, int64_t sz,
+    const I* __restrict__ ix, const I* __restrict__ iz, const int64_t* __restrict__ pair_off,
+    int parts, unsigned long long* __restrict__ out) {
+  using IV = IdxVec<I>;
+  using V = typename IV::V;
+  constexpr int NV = VEC ? IV::N : 1;  // pairs per load
+  constexpr int U = VEC ? UV : 4;      // loads of each stream per thread and batch
   extern __shared__ __attribute__((aligned(16))) uint16_t codes[];
   const int lb = xcd_block(blockIdx.x, gridDim.x);  // a shard's parts share one L2
   const int s = lb / parts;
   const int part = lb - s * parts;
+  const int tid = threadIdx.x;
   const int64_t xb = x_off[s], zb = z_off[s];
-  const uint64_t nx = (uint64_t)(x_off[s + 1] - xb), nz = (uint64_t)(z_off[s + 1] - zb);
-  uint16_t* lx = codes;
-  uint16_t* lx2 = codes + nx;
-  uint16_t* lz = codes + (PRED == TW_PRED_HALF ? 2 : 1) * nx;
-  if (nx > 0 && nz > 0) {
-    for (int64_t i = threadIdx.x; i < (int64_t)nx; i += kRngThreads) {
-      lx[i] = cx[(int64_t)s * max_nx + i];
-      if (PRED == TW_PRED_HALF) lx2[i] = cx2[(int64_t)s * max_nx + i];
-    }
-    for (int64_t j = threadIdx.x; j < (int64_t)nz; j += kRngThreads)
-      lz[j] = pz[(int64_t)s * max_nz + j];
-  }
-  __syncthreads();
+  const int64_t nx = x_off[s + 1] - xb, nz = z_off[s + 1] - zb;
+  const uint16_t* lx = codes;
+  const uint16_t* lx2 = codes + al8(nx);
+  const uint16_t* lz = codes + (PRED == TW_PRED_HALF ? 2 : 1) * al8(nx);
   const int64_t pb = pair_off[s], pe = pair_off[s + 1];
   const int64_t per = (pe - pb + parts - 1) / parts;
-  const int64_t q0 = pb + (int64_t)part * per;
+  const int64_t q0 = std::min<int64_t>(pe, pb + (int64_t)part * per);
   const int64_t q1 = std::min<int64_t>(pe, q0 + per);
-  unsigned acc = 0;
-  constexpr int U = 4;  // index loads in flight per thread
-  for (int64_t p0 = q0 + threadIdx.x; p0 < q1; p0 += (int64_t)U * kRngThreads) {
-    int64_t a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t p = p0 + (int64_t)u * kRngThreads;
-      a[u] = p < q1 ? ix[p] : xb;
-      b[u] = p < q1 ? iz[p] : zb;
+  // [a0, a1): the NV-aligned body of [q0, q1), loaded as vectors
+  const int64_t a0 = std::min<int64_t>(q1, (q0 + NV - 1) / NV * NV);
+  const int64_t a1 = std::max<int64_t>(a0, q1 / NV * NV);
+  const int nv = (int)((a1 - a0) / NV);
+  auto one = [&](I a, I b) -> unsigned {
+    bool in;
+    uint32_t i, j;
+    if constexpr (sizeof(I) == 4) {  // 32-bit offsets: the arrays hold < 2^31 elements
+      i = (uint32_t)(a - (int32_t)xb);
+      j = (uint32_t)(b - (int32_t)zb);
+      in = i < (uint32_t)nx && j < (uint32_t)nz;
+    } else {
+      const uint64_t i64 = (uint64_t)(a - xb), j64 = (uint64_t)(b - zb);
+      in = i64 < (uint64_t)nx && j64 < (uint64_t)nz;
+      i = (uint32_t)i64;
+      j = (uint32_t)j64;
     }
+    if (in) {
+      const unsigned pj = lz[j];
+      unsigned r = (unsigned)lx[i] > pj;
+      if (PRED == TW_PRED_HALF) r += (unsigned)lx2[i] > pj;
+      return r;
+    }
+    const T xv = x[a], zv = z[b];
+    return (unsigned)(xv > zv) + (PRED == TW_PRED_HALF ? (unsigned)(xv >= zv) : 0u);
+  };
+  const I* __restrict__ px = ix + a0;
+  const I* __restrict__ pzi = iz + a0;
+  auto load = [&](const I* p, int v) -> V {
+    if constexpr (VEC && NT) {
+      const typename IV::NVec r = __builtin_nontemporal_load(((const typename IV::NVec*)p) + v);
+      return __builtin_bit_cast(V, r);
+    } else if constexpr (VEC) {
+      return ((const V*)p)[v];
+    } else {
+      V r;
+      r.x = p[v];
+      return r;
+    }
+  };
+  auto compare = [&](const V (&A)[U], const V (&Bv)[U], int v0) -> unsigned {
+    unsigned c = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (p0 + (int64_t)u * kRngThreads >= q1) break;
-      const uint64_t i = (uint64_t)(a[u] - xb), j = (uint64_t)(b[u] - zb);
-      if (i < nx && j < nz) {
-        const unsigned pj = lz[j];
-        acc += (unsigned)lx[i] > pj;
-        if (PRED == TW_PRED_HALF) acc += (unsigned)lx2[i] > pj;
-      } else {
-        const T xv = x[a[u]], zv = z[b[u]];
-        acc += xv > zv;
-        if (PRED == TW_PRED_HALF) acc += xv >= zv;
+      if (v0 + u * kRngThreads < nv) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) c += one(IV::at(A[u], e), IV::at(Bv[u], e));
+      }
+    }
+    return c;
+  };
+  V A[U], Bv[U];
+  constexpr int step = U * kRngThreads;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int v = tid + u * kRngThreads;
+    if (v < nv) {
+      A[u] = load(px, v);
+      Bv[u] = load(pzi, v);
+    }
+  }
+  if (nx > 0 && nz > 0)
+    stage_codes<PRED>(codes, cx + (int64_t)s * sx, cx2 + (int64_t)s * sx, pz + (int64_t)s * sz,
+                      nx, nz);
+  __syncthreads();
+  unsigned acc = 0;
+  // scalar head [q0, a0) and tail [a1, q1) (fewer than NV pairs each)
+  if (tid < a0 - q0) acc += one(ix[q0 + tid], iz[q0 + tid]);
+  if (tid < q1 - a1) acc += one(ix[a1 + tid], iz[a1 + tid]);
+  for (int v0 = tid; v0 < nv; v0 += step) {
+    if constexpr (PIPE) {
+      V A2[U], B2[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // next batch in flight while this one is compared
+        const int v = v0 + step + u * kRngThreads;
+        if (v < nv) {
+          A2[u] = load(px, v);
+          B2[u] = load(pzi, v);
+        }
+      }
+      acc += compare(A, Bv, v0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        A[u] = A2[u];
+        Bv[u] = B2[u];
+      }
+    } else {
+      acc += compare(A, Bv, v0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int v = v0 + step + u * kRngThreads;
+        if (v < nv) {
+          A[u] = load(px, v);
+          Bv[u] = load(pzi, v);
+        }
       }
     }
   }
   unsigned long long tot = wave_sum_u64((unsigned long long)acc);
   __shared__ unsigned long long part_sum[kRngThreads / kWave];
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int lane = tid & (kWave - 1), wid = tid / kWave;
   if (lane == 0) part_sum[wid] = tot;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     unsigned long long sum = 0;
     for (int w = 0; w < kRngThreads / kWave; ++w) sum += part_sum[w];
     if (sum) atomicAdd(out + s, sum);
   }
 }
 
-static int g_rng_codes_by_bucket = 1;  // tw_count_rng_set_codes: 0 = sort + binary search
+// tw_count_rng_set_codes: 0 = sort + binary search, 1 = equal-depth buckets (default),
+// 2 = coarse (value-range) buckets only
+static int g_rng_codes_by_bucket = 1;
 
 struct RngRankPlan {
   bool ok;
-  int C, chunks, tiles, parts;
+  int C, chunks, tiles, parts, code_parts;
+  int64_t sx, sz;  // code row strides (multiples of 8 codes: 16-B aligned rows)
   int64_t keys_bytes, cx_off, cx2_off, pz_off, total;
   size_t lds;
 };
@@ -553,18 +792,25 @@ static RngRankPlan plan_rng_ranked(int32_t n_shards, int64_t max_nx, int64_t max
   p.chunks = rp.chunks;
   p.tiles = (int)ceil_div(max_nx + max_nz, (int64_t)kSortThreads * kCodeElems);
   const int nc = pred == TW_PRED_HALF ? 2 : 1;
-  p.lds = (size_t)(nc * max_nx + max_nz) * sizeof(uint16_t);
+  p.sx = (max_nx + 7) / 8 * 8;
+  p.sz = (max_nz + 7) / 8 * 8;
+  p.lds = (size_t)(nc * p.sx + p.sz) * sizeof(uint16_t);
   p.ok = p.lds <= 160 * 1024 - 1024;
   // ~2 blocks of 1024 threads per CU over the whole grid, >= 8192 draws per block
   const int64_t nq = std::max<int64_t>(1, (B + 1) / 2);
   p.parts = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(512, n_shards),
                                                         ceil_div(nq, 8192)));
+  // bucket-code blocks per shard: each rebuilds the shard's buckets and codes a share of one
+  // or more rounds of kEPer elements per thread; >= 256 blocks over the grid when possible
+  p.code_parts = (int)std::max<int64_t>(
+      1, std::min<int64_t>(ceil_div(256, n_shards),
+                           ceil_div(max_nx + max_nz, (int64_t)kSortThreads * kEPer)));
   auto al = [](int64_t b) { return ceil_div(b, 256) * 256; };
   p.keys_bytes = al((int64_t)n_shards * p.chunks * p.C * 8);
   p.cx_off = p.keys_bytes;
-  p.cx2_off = p.cx_off + al((int64_t)n_shards * max_nx * 2);
-  p.pz_off = p.cx2_off + (pred == TW_PRED_HALF ? al((int64_t)n_shards * max_nx * 2) : 0);
-  p.total = p.pz_off + al((int64_t)n_shards * max_nz * 2);
+  p.cx2_off = p.cx_off + al((int64_t)n_shards * p.sx * 2);
+  p.pz_off = p.cx2_off + (pred == TW_PRED_HALF ? al((int64_t)n_shards * p.sx * 2) : 0);
+  p.total = p.pz_off + al((int64_t)n_shards * p.sz * 2);
   return p;
 }
 
@@ -591,8 +837,7 @@ int launch_codes(const void* x, const int64_t* x_off, const void* z, const int64
                                      (int)(sizeof(uint64_t) * kMaxChunk)));
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_rank_codes_bucket<T, PRED>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)(sizeof(T) * kBucketMaxZ +
-                                           sizeof(unsigned) * (2 * kBucketNB + 1))));
+                                     (int)kBucketLds));
     attrs_set = true;
   }
   char* w = (char*)work;
@@ -601,10 +846,9 @@ int launch_codes(const void* x, const int64_t* x_off, const void* z, const int64
   uint16_t* cx2 = (uint16_t*)(w + p.cx2_off);
   uint16_t* pz = (uint16_t*)(w + p.pz_off);
   if (max_nz <= kBucketMaxZ && g_rng_codes_by_bucket) {
-    const size_t lds_b = sizeof(T) * kBucketMaxZ + sizeof(unsigned) * (2 * kBucketNB + 1);
-    hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED>), dim3(n_shards * kBucketParts),
-                       dim3(kSortThreads), lds_b, st, (const T*)x, x_off, (const T*)z, z_off,
-                       kBucketParts, max_nx, max_nz, cx, cx2, pz);
+    hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED>), dim3(n_shards * p.code_parts),
+                       dim3(kSortThreads), kBucketLds, st, (const T*)x, x_off, (const T*)z, z_off,
+                       p.code_parts, (int)(g_rng_codes_by_bucket == 1), p.sx, p.sz, cx, cx2, pz);
   } else {
   const size_t lds_sort = sizeof(uint64_t) * p.C;
   const size_t lds_codes = sizeof(uint64_t) * std::min<int64_t>((int64_t)p.chunks * p.C, kMaxChunk);
@@ -622,7 +866,7 @@ int launch_codes(const void* x, const int64_t* x_off, const void* z, const int64
   TW_LAUNCH_CHECK();
   hipLaunchKernelGGL((k_rank_codes<T, PRED>), dim3(n_shards * p.tiles), dim3(kSortThreads),
                      lds_codes, st, (const T*)x, x_off, (const T*)z, z_off, keys, p.chunks, p.C,
-                     p.tiles, max_nx, max_nz, cx, cx2, pz);
+                     p.tiles, p.sx, p.sz, cx, cx2, pz);
   }
   TW_LAUNCH_CHECK();
   return TW_OK;
@@ -647,35 +891,67 @@ int launch_rng_ranked(const void* x, const int64_t* x_off, const void* z, const 
   uint16_t* cx2 = (uint16_t*)(w + p.cx2_off);
   uint16_t* pz = (uint16_t*)(w + p.pz_off);
   hipLaunchKernelGGL((k_count_rng_ranked<PRED>), dim3(n_shards * p.parts), dim3(kRngThreads),
-                     p.lds, st, x_off, z_off, cx, cx2, pz, max_nx, max_nz, B, p.parts,
+                     p.lds, st, x_off, z_off, cx, cx2, pz, p.sx, p.sz, B, p.parts,
                      (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
                      (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
 
-template <typename T, int PRED>
-int launch_idx_ranked(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
-                      int32_t n_shards, int64_t max_nx, int64_t max_nz, const int64_t* ix,
-                      const int64_t* iz, const int64_t* pair_off, const RngRankPlan& p,
-                      void* work, uint64_t* out, hipStream_t st) {
+template <typename T, int PRED, typename I, bool VEC, int UV = 2, bool NT = false,
+          bool PIPE = true>
+int launch_idx_ranked_v(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                        int32_t n_shards, int64_t max_nx, int64_t max_nz, const I* ix,
+                        const I* iz, const int64_t* pair_off, const RngRankPlan& p, void* work,
+                        uint64_t* out, hipStream_t st) {
   static bool attrs_set = false;
   if (!attrs_set) {
-    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_idx_ranked<T, PRED>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024 - 1024));
+    TW_HIP_CHECK(hipFuncSetAttribute(
+        (const void*)k_count_idx_ranked<T, PRED, I, VEC, UV, NT, PIPE>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
     attrs_set = true;
   }
   const int rc = launch_codes<T, PRED>(x, x_off, z, z_off, n_shards, max_nx, max_nz, p, work, st);
   if (rc != TW_OK) return rc;
   char* w = (char*)work;
-  hipLaunchKernelGGL((k_count_idx_ranked<T, PRED>), dim3(n_shards * p.parts), dim3(kRngThreads),
-                     p.lds, st, (const T*)x, x_off, (const T*)z, z_off,
-                     (const uint16_t*)(w + p.cx_off), (const uint16_t*)(w + p.cx2_off),
-                     (const uint16_t*)(w + p.pz_off), max_nx, max_nz, ix, iz, pair_off, p.parts,
-                     (unsigned long long*)out);
+  hipLaunchKernelGGL((k_count_idx_ranked<T, PRED, I, VEC, UV, NT, PIPE>),
+                     dim3(n_shards * p.parts), dim3(kRngThreads), p.lds, st, (const T*)x, x_off,
+                     (const T*)z, z_off, (const uint16_t*)(w + p.cx_off),
+                     (const uint16_t*)(w + p.cx2_off), (const uint16_t*)(w + p.pz_off), p.sx,
+                     p.sz, ix, iz, pair_off, p.parts, (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
+}
+
+// tw_count_idx_set_variant: int32 index streams, 0 = two 16-B loads per stream and batch,
+// pipelined (default), 1 = the same as nontemporal loads, 2/3 = four loads, one buffer
+// (plain / nontemporal), 4/5 = four loads pipelined (plain / nontemporal)
+static int g_idx_variant = 0;
+
+template <typename T, int PRED, typename I>
+int launch_idx_ranked(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                      int32_t n_shards, int64_t max_nx, int64_t max_nz, const I* ix, const I* iz,
+                      const int64_t* pair_off, const RngRankPlan& p, void* work, uint64_t* out,
+                      hipStream_t st) {
+  // 16-B vector loads of the index streams need 16-B aligned base pointers
+  if ((((uintptr_t)ix | (uintptr_t)iz) & 15) == 0) {
+    if constexpr (sizeof(I) == 4) {  // tuning variants (tw_count_idx_set_variant)
+#define TW_V(U, N, P) return launch_idx_ranked_v<T, PRED, I, true, U, N, P>(x, x_off, z, z_off, n_shards, max_nx, max_nz, ix, iz, pair_off, p, work, out, st)
+      switch (g_idx_variant) {
+        case 1: TW_V(2, true, true);
+        case 2: TW_V(4, false, false);
+        case 3: TW_V(4, true, false);
+        case 4: TW_V(4, false, true);
+        case 5: TW_V(4, true, true);
+        default: break;
+      }
+#undef TW_V
+    }
+    return launch_idx_ranked_v<T, PRED, I, true>(x, x_off, z, z_off, n_shards, max_nx, max_nz, ix,
+                                                 iz, pair_off, p, work, out, st);
+  }
+  return launch_idx_ranked_v<T, PRED, I, false>(x, x_off, z, z_off, n_shards, max_nx, max_nz, ix,
+                                                iz, pair_off, p, work, out, st);
 }
 
 }  // namespace tw
@@ -752,13 +1028,13 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
 }
 
 extern "C" int tw_count_rng_set_codes(int32_t by_bucket) {
-  TW_ARG_CHECK(by_bucket == 0 || by_bucket == 1, "tw_count_rng_set_codes: 0 or 1");
+  TW_ARG_CHECK(by_bucket >= 0 && by_bucket <= 2, "tw_count_rng_set_codes: 0, 1 or 2");
   g_rng_codes_by_bucket = by_bucket;
   return TW_OK;
 }
 
 extern "C" int tw_count_sorted_set_bucket(int32_t by_bucket) {
-  TW_ARG_CHECK(by_bucket == 0 || by_bucket == 1, "tw_count_sorted_set_bucket: 0 or 1");
+  TW_ARG_CHECK(by_bucket >= 0 && by_bucket <= 2, "tw_count_sorted_set_bucket: 0, 1 or 2");
   g_sorted_by_bucket = by_bucket;
   return TW_OK;
 }
@@ -767,8 +1043,18 @@ extern "C" int tw_count_pairs_idx(const void* d_x, const void* d_z, const int64_
                                   const int64_t* d_iz, const int64_t* d_pair_off,
                                   int32_t n_shards, int64_t max_pairs, int32_t dtype,
                                   int32_t pred, uint64_t* d_out, void* stream);
+extern "C" int tw_count_pairs_idx32(const void* d_x, const void* d_z, const int32_t* d_ix,
+                                    const int32_t* d_iz, const int64_t* d_pair_off,
+                                    int32_t n_shards, int64_t max_pairs, int32_t dtype,
+                                    int32_t pred, uint64_t* d_out, void* stream);
 
 static int g_idx_parts = 0;  // tw_count_idx_set_parts: blocks per shard (0 = plan)
+
+extern "C" int tw_count_idx_set_variant(int32_t v) {
+  TW_ARG_CHECK(v >= 0 && v <= 5, "tw_count_idx_set_variant: 0..5");
+  g_idx_variant = v;
+  return TW_OK;
+}
 
 extern "C" int tw_count_idx_set_parts(int32_t parts) {
   TW_ARG_CHECK(parts >= 0 && parts <= 4096, "tw_count_idx_set_parts: 0..4096");
@@ -776,12 +1062,23 @@ extern "C" int tw_count_idx_set_parts(int32_t parts) {
   return TW_OK;
 }
 
-extern "C" int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
-                                     const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
-                                     int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,
-                                     const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype,
-                                     int32_t pred, void* d_work, int64_t work_bytes,
-                                     uint64_t* d_out, void* stream) {
+namespace tw {
+inline int count_idx_plain(const void* x, const void* z, const int64_t* ix, const int64_t* iz,
+                           const int64_t* po, int32_t n, int64_t mp, int32_t dt, int32_t pr,
+                           uint64_t* out, void* st) {
+  return tw_count_pairs_idx(x, z, ix, iz, po, n, mp, dt, pr, out, st);
+}
+inline int count_idx_plain(const void* x, const void* z, const int32_t* ix, const int32_t* iz,
+                           const int64_t* po, int32_t n, int64_t mp, int32_t dt, int32_t pr,
+                           uint64_t* out, void* st) {
+  return tw_count_pairs_idx32(x, z, ix, iz, po, n, mp, dt, pr, out, st);
+}
+
+template <typename I>
+int count_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z, const int64_t* d_z_off,
+                 int32_t n_shards, int64_t max_nx, int64_t max_nz, const I* d_ix, const I* d_iz,
+                 const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype, int32_t pred,
+                 void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && max_nx >= 0 && max_nz >= 0 && max_pairs >= 0,
                "tw_count_pairs_idx_ws: bad sizes");
   // SUBGT on doubles is GT ((x - z) > 0 == x > z without FTZ); on int64 it wraps: plain kernel
@@ -791,19 +1088,44 @@ extern "C" int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, co
   if (g_idx_parts > 0) p.parts = g_idx_parts;
   if (!p.ok || (dtype != TW_F64 && dtype != TW_I64) || max_pairs == 0 || d_work == nullptr ||
       work_bytes < p.total)  // not applicable: the plain kernel gives the same counts
-    return tw_count_pairs_idx(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, dtype,
-                              pred, d_out, stream);
-  TW_ARG_CHECK((int64_t)n_shards * p.parts < (1ll << 31) && (int64_t)n_shards * p.tiles < (1ll << 31) &&
-                   (int64_t)n_shards * p.chunks < (1ll << 31),
+    return count_idx_plain(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, dtype, pred,
+                           d_out, stream);
+  TW_ARG_CHECK((int64_t)n_shards * p.parts < (1ll << 31) &&
+                   (int64_t)n_shards * p.tiles < (1ll << 31) &&
+                   (int64_t)n_shards * p.chunks < (1ll << 31) &&
+                   (int64_t)n_shards * p.code_parts < (1ll << 31),
                "tw_count_pairs_idx_ws: grid too large");
   hipStream_t st = (hipStream_t)stream;
   TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+#define TW_IR(T, P) return launch_idx_ranked<T, P, I>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st)
   if (dtype == TW_F64) {
-    if (pr == TW_PRED_HALF)
-      return launch_idx_ranked<double, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
-    return launch_idx_ranked<double, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
+    if (pr == TW_PRED_HALF) TW_IR(double, TW_PRED_HALF);
+    TW_IR(double, TW_PRED_GT);
   }
-  if (pr == TW_PRED_HALF)
-    return launch_idx_ranked<long long, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
-  return launch_idx_ranked<long long, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st);
+  if (pr == TW_PRED_HALF) TW_IR(long long, TW_PRED_HALF);
+  TW_IR(long long, TW_PRED_GT);
+#undef TW_IR
+}
+}  // namespace tw
+
+extern "C" int tw_count_pairs_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                     const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                     int64_t max_nz, const int64_t* d_ix, const int64_t* d_iz,
+                                     const int64_t* d_pair_off, int64_t max_pairs, int32_t dtype,
+                                     int32_t pred, void* d_work, int64_t work_bytes,
+                                     uint64_t* d_out, void* stream) {
+  return count_idx_ws<int64_t>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz,
+                               d_pair_off, max_pairs, dtype, pred, d_work, work_bytes, d_out,
+                               stream);
+}
+
+extern "C" int tw_count_pairs_idx32_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                       const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                       int64_t max_nz, const int32_t* d_ix, const int32_t* d_iz,
+                                       const int64_t* d_pair_off, int64_t max_pairs,
+                                       int32_t dtype, int32_t pred, void* d_work,
+                                       int64_t work_bytes, uint64_t* d_out, void* stream) {
+  return count_idx_ws<int32_t>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz,
+                               d_pair_off, max_pairs, dtype, pred, d_work, work_bytes, d_out,
+                               stream);
 }

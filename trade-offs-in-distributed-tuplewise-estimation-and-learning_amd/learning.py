@@ -589,10 +589,14 @@ _CACHE = _EvalCache()
 
 
 def _pairs_dev(pairs):
+    """The monitor pairs as device index columns: int32 when they fit (8 B per pair), which
+    lets evaluation read them once for both statistics (tw_pair_sum_idx32_f64 with a count)."""
     a = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
     off = np.array([0, a.shape[0]], dtype=np.int64)
-    return (L.to_device(np.ascontiguousarray(a[:, 0])), L.to_device(np.ascontiguousarray(a[:, 1])),
-            off, L.to_device(off))
+    fits = a.size == 0 or (int(a.min()) >= -2 ** 31 and int(a.max()) < 2 ** 31)
+    dt = np.int32 if fits else np.int64
+    return (L.to_device(np.ascontiguousarray(a[:, 0]), dt),
+            L.to_device(np.ascontiguousarray(a[:, 1]), dt), off, L.to_device(off))
 
 
 def _scores(A_dev, wd):
@@ -639,10 +643,16 @@ def _eval_device(wd, p_learn, loss, margin, fixed):
         ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
         n_pairs = int(off[1])
         sx, sz = _scores(tX, wd), _scores(tZ, wd)
-        parts += [E.pair_sum_indexed_dev(sx, sz, ixd, izd, off, kern, float(margin),
-                                         pair_off_dev=offd),
-                  E.count_indexed_dev(sx, sz, L.TW_F64, ixd, izd, off, L.TW_PRED_GT,
-                                      pair_off_dev=offd).view(t.float64)]
+        if ixd.dtype == t.int32:  # one pass over the pairs: hinge sum and AUC count
+            cnt = L.empty((1,), t.int64)
+            parts += [E.pair_sum_indexed_dev(sx, sz, ixd, izd, off, kern, float(margin),
+                                             pair_off_dev=offd, count_out=cnt),
+                      cnt.view(t.float64)]
+        else:
+            parts += [E.pair_sum_indexed_dev(sx, sz, ixd, izd, off, kern, float(margin),
+                                             pair_off_dev=offd),
+                      E.count_indexed_dev(sx, sz, L.TW_F64, ixd, izd, off, L.TW_PRED_GT,
+                                          pair_off_dev=offd).view(t.float64)]
     else:
         parts.append(t.zeros((2,), dtype=t.float64, device=wd.device))
     eX = _CACHE.get("test_X", p_learn["test_X"],
