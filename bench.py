@@ -43,6 +43,9 @@ N_SHARDS = 64
 PEAK_LANE_OPS = 256 * 64 * 2.4e9  # 3.93e13 f64 vector lane-ops/s (MI355X_MICROARCH chip table)
 HBM_PEAK_GBS = 8000.0
 INC_LANE_OPS = 53  # algorithmic lane-ops per device-RNG incomplete pair
+# 32-bit integer VOP2 ops (v_xor/v_and/v_lshrrev_b32) issue at 1.60-1.63 wave-instructions/
+# cycle/CU (profiles/r01_microbench_valu_issue2.log): 6.3e13 lane-op/s measured at 2.4 GHz
+INT_LANE_OPS_MEASURED = 6.29e13
 
 
 class EventPool:
@@ -84,7 +87,10 @@ class EventPool:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the run; without WORLD_SIZE in the environment, N > 1 "
+                         "spawns N ranks of this script (no torchrun needed); with WORLD_SIZE "
+                         "it must agree")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=N_PER_CLASS)
@@ -95,6 +101,10 @@ def parse():
                     help="pairs per shard of the incomplete-statistic line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sgd", action="store_true", help="skip the SGD steps/s secondary")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the strong-scaling C3 line (n = 1e6/class, 64 shards in total)")
+    ap.add_argument("--strong-T", type=int, default=4,
+                    help="repartitions per estimate of the strong-scaling C3 line (UnNT's T)")
     ap.add_argument("--cpu-inc-shards", type=int, default=16,
                     help="shards of the incomplete CPU-baseline sample")
     ap.add_argument("--cpu-shards", type=int, default=N_SHARDS,
@@ -424,12 +434,113 @@ def incomplete_replay(X, Z, shards, B, reps=20):
                                  "§8(d)); kernel_ms = the whole call (rank codes + count)"}}
 
 
+def spawn_ranks(n: int, script: str | None = None, argv: list | None = None) -> int:
+    """`python bench.py --gpus N` without a launcher: start N ranks of this script as child
+    processes (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set as torch.distributed.run
+    would, rendezvous on 127.0.0.1) before this process touches any GPU; rank 0 prints the JSON
+    line.  Returns the exit code (non-zero if any rank failed; the others are then stopped)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        cmd = [sys.executable, script or os.path.abspath(__file__)]
+        cmd += sys.argv[1:] if argv is None else argv
+        procs.append(subprocess.Popen(cmd, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        for pr in list(procs):
+            code = pr.poll()
+            if code is None:
+                continue
+            procs.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code
+                for other in procs:  # one rank failed: the collectives would hang
+                    other.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def resolve_world(args) -> int:
+    """World size from WORLD_SIZE (launcher) or --gpus (self-spawn); a disagreement is an
+    error, not a silent one-rank run."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is None:
+        return args.gpus if args.gpus is not None else 1
+    world = int(env)
+    if args.gpus is not None and args.gpus != world:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
+        sys.exit(2)
+    return world
+
+
+def strong_c3(args, group, rank, world, barrier, torch, dist):
+    """BASELINE configs[2] as strong scaling: n = 1e6/class and N = 64 shards IN TOTAL, so each
+    of G ranks holds n/G scores per class and 64/G shards (8 per GPU at G = 8, the survey's
+    '8 GPUs x 8 shards'); est.UnNT / cs.UnNBT steps with T repartitions per estimate.  The
+    global permutation, hence every shard's count and every estimate, does not depend on G."""
+    from tuplewise.device import ShardedSample
+    n_tot, N_tot = N_PER_CLASS, N_SHARDS
+    if N_tot % world or n_tot % world:
+        return {"skipped": f"n={n_tot}, N={N_tot} do not divide over {world} ranks"}
+    n_loc, N_loc = n_tot // world, N_tot // world
+    gen = torch.Generator(device="cuda").manual_seed(5000 + rank)
+    X = torch.randn(n_loc, dtype=torch.float64, device="cuda", generator=gen) + 0.5
+    Z = torch.randn(n_loc, dtype=torch.float64, device="cuda", generator=gen)
+    S = ShardedSample(X, Z, N_loc, group=group, algo="pairs")
+    k = n_tot // N_tot
+    T = max(1, args.strong_T)
+    reps = max(1, args.steps // T)
+
+    def timed(fn):
+        fn(90_000)  # warm: same shapes, other keys
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ests = [fn(r * T) for r in range(reps)]
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if group is not None:
+            tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+            dt = float(tt.item())
+        return dt, ests[-1]
+
+    dt_c, est_c = timed(lambda k0: S.UnNT(T, k0))
+    B = args.incomplete_B
+    dt_i, est_i = timed(lambda k0: float(np.mean(S.UnNB_many(B, 777 + k0, range(k0, k0 + T)))))
+    pairs_c = N_tot * k * k * T * reps
+    pairs_i = N_tot * B * T * reps
+    return {"note": "BASELINE configs[2] strong scaling: n=1e6/class and N=64 prop-SWOR shards in "
+                    "total (64/G shards and 1e6/G scores per class per rank), T repartitions per "
+                    "estimate (UnNT complete, UnNBT incomplete with device-drawn pairs); value = "
+                    "pairs of all ranks / max-over-ranks wall time",
+            "scaling": "strong", "n_per_class_total": n_tot, "shards_total": N_tot,
+            "shards_per_rank": N_loc, "T": T, "estimates": reps,
+            "complete": {"value": pairs_c / dt_c, "unit": "pairs/s",
+                         "ms_per_estimate": dt_c / reps * 1e3, "estimate_last": float(est_c)},
+            "incomplete": {"B_per_shard": B, "value": pairs_i / dt_i, "unit": "pairs/s",
+                           "ms_per_estimate": dt_i / reps * 1e3, "estimate_last": float(est_i)}}
+
+
 def main():
     args = parse()
+    world = resolve_world(args)
+    if world > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(world))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -550,6 +661,7 @@ def main():
     ops.count_rng = ops.count_rng.__wrapped__
     inc_pairs_rank = args.shards * B_inc
     inc_replay = incomplete_replay(X, Z, args.shards, B_inc)
+    strong = None if args.no_strong else strong_c3(args, group, rank, world, barrier, torch, dist)
 
     # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
     # estimation-experiment/main.py:29-31), 1e10 pairs per launch; no repartition
@@ -609,8 +721,10 @@ def main():
                                "main.py:72-74) + device repartition per step",
                    "n_per_class_per_gpu": n, "shards_per_gpu": args.shards,
                    "pairs_per_step_per_gpu": pairs_per_step_rank,
-                   "parallelism": f"dp{world}: shards over ranks, RCCL all-to-all repartition "
-                                  f"+ all-reduce of counts"},
+                   "parallelism": (f"dp{world}: shards over ranks, RCCL all-to-all repartition "
+                                   f"+ all-reduce of counts" if world > 1 else
+                                   "dp1: one GPU, device Feistel repartition fused into the "
+                                   "count launch")},
         "roofline": {"bound": "valu", "kernel": "k_count_complete",
                      "achieved": achieved / 1e12, "peak": PEAK_LANE_OPS / 1e12,
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
@@ -641,7 +755,10 @@ def main():
             "unit": "pairs/s", "ms_per_step": dt_inc / args.steps * 1e3,
             "estimate_last_step": float(est_inc),
             "roofline": {"bound": "valu",
-                         "kernel": "k_sort_chunks + k_rank_codes + k_count_rng_ranked",
+                         "kernel": "k_rank_codes_bucket + k_count_rng_ranked",
+                         "frac_vs_int32_op_peak": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3)
+                         / INT_LANE_OPS_MEASURED,
+                         "int32_op_peak": INT_LANE_OPS_MEASURED / 1e12,
                          "achieved": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3) / 1e12,
                          "peak": PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
                          "frac": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3)
@@ -649,9 +766,13 @@ def main():
                          "kernel_ms": kms_inc,
                          "note": f"{INC_LANE_OPS} lane-ops per pair (SURVEY.md §8(d) contract "
                                  "constant: 2 Philox4x32-10 words + 2 range maps + 1 compare); "
-                                 "kernel_ms = the whole tw_count_pairs_rng_ws call (z sort, "
-                                 "rank codes, draw-and-count)"}},
+                                 "kernel_ms = the whole tw_count_pairs_rng_ws call (bucket "
+                                 "rank codes, draw-and-count); frac is against the f64 lane-op "
+                                 "peak of the contract, frac_vs_int32_op_peak against the "
+                                 "measured 32-bit integer VOP2 issue rate (the Philox work is "
+                                 "32-bit integer)"}},
         "incomplete_replay": inc_replay,
+        "strong_C3": strong,
     }
     if world == 1 and not args.no_sgd:
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'
@@ -672,9 +793,13 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
-        # the box's CPU share is 16 cores per GPU (os.cpu_count() shows the whole machine)
-        out["cpu_baseline"]["all_cores"] = cpu_baseline_all_cores(
-            n, args.shards, min(16, len(os.sched_getaffinity(0))))
+        # the box's CPU share is 16 cores per GPU (os.cpu_count() and the affinity mask show
+        # the whole machine): the all-cores figure uses that share, and says so
+        share = min(16, len(os.sched_getaffinity(0)))
+        allc = cpu_baseline_all_cores(n, args.shards, share)
+        allc["label"] = (f"{share} of {len(os.sched_getaffinity(0))} host cores (the GPU box's "
+                         f"CPU share per GPU)")
+        out["cpu_baseline"]["all_cores"] = allc
         out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, args.shards, B_inc,
                                                                     args.cpu_inc_shards)
     if rank == 0:

@@ -16,13 +16,18 @@ CSRC = ROOT / "trade-offs-in-distributed-tuplewise-estimation-and-learning_amd" 
 OUT = ROOT / "tools" / "_dbg" / "libtw_phase.so"
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
+    # extra -D flags: python tools/phase_codes.py build [-DTW_IDX_STREAM_ONLY ...] [name]
+    flags = [a for a in sys.argv[2:] if a.startswith("-D")]
+    names = [a for a in sys.argv[2:] if not a.startswith("-D")]
+    if names:
+        OUT = OUT.with_name(f"libtw_{names[0]}.so")
     OUT.parent.mkdir(exist_ok=True)
     objs = []
     for src in ("capi.hip", "count.hip", "rankcount.hip"):
-        o = OUT.parent / (src + ".o")
+        o = OUT.parent / (OUT.stem + "_" + src + ".o")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
-                        "-std=c++17", "-ffp-contract=off", "-DTW_PHASE_TIMING", "-c",
-                        str(CSRC / src), "-o", str(o)], check=True)
+                        "-std=c++17", "-ffp-contract=off", "-DTW_PHASE_TIMING"] + flags +
+                       ["-c", str(CSRC / src), "-o", str(o)], check=True)
         objs.append(str(o))
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     str(OUT)] + objs, check=True)
@@ -30,6 +35,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "build":
 
 import torch  # noqa: E402  (before the dlopen: one HIP runtime)
 
+if len(sys.argv) > 1 and sys.argv[1] != "build":
+    OUT = OUT.with_name(f"libtw_{sys.argv[1]}.so")
 lib = ctypes.CDLL(str(OUT))
 vp = ctypes.c_void_p
 k, N, B = 15625, 64, 1_000_000
@@ -67,3 +74,21 @@ for mode in (1, 2):
     print(f"mode {mode}: median cycles per phase {np.median(d, axis=0).tolist()} "
           f"total median {np.median(tot):.0f} max {tot.max()}  block start spread "
           f"{a[:, 0].max() - a[:, 0].min()} (clock64 ticks; per-CU counters)", flush=True)
+
+# whole-call time of the int32 replay count with this build (HIP events), per load variant
+lib.tw_count_rng_set_codes(1)
+lib.tw_count_idx_set_variant.argtypes = [ctypes.c_int32]
+for var in range(6):
+    lib.tw_count_idx_set_variant(var)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(20)]
+    for e0, e1 in ev:
+        e0.record()
+        fn(X.data_ptr(), off.data_ptr(), Z.data_ptr(), off.data_ptr(), N, k, k, ix.data_ptr(),
+           iz.data_ptr(), po.data_ptr(), B, 0, 0, work.data_ptr(), wb, out.data_ptr(), None)
+        e1.record()
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    print(f"{OUT.name} variant {var}: whole call {ms * 1e3:.1f} us = "
+          f"{8 * N * B / (ms * 1e-3) / 1e12:.2f} TB/s of int32 indices", flush=True)
+lib.tw_count_idx_set_variant(0)

@@ -115,23 +115,25 @@ inline RankPlan plan_rank(int64_t max_nx, int64_t max_nz) {
 }
 
 // Rank codes without a sort (shards with nz <= kBucketMaxZ): the block loads the shard's z
-// into LDS, buckets it by VALUE with an LDS histogram, prefix sum and scatter, and then a code
-// is (#z in lower buckets) + (#z in its own bucket below / at most v), by a scan of one bucket.
-// Bucket map, two levels, both monotone (every IEEE step in them is monotone), so bucket order
-// is value order:
-//   coarse  u = (v - zmin) * NB / (zmax - zmin) over the finite z, b = clamp(floor(u)), and the
-//           position t = clamp(u - b, 0, 1) inside the bucket;
-//   fine    (refine = 1) the coarse histogram's prefix cs turns it into an equal-depth map,
-//           f = min(NB - 1, floor((cs[b] + t * (cs[b+1] - cs[b])) * NB / n)): the piecewise-linear
-//           empirical CDF of z, so every fine bucket holds ~n / NB values whatever the shape of
-//           the data (Gaussian scores put ~25 values in the central coarse buckets of a
-//           15625-value shard and ~8 in a fine one; the scans are the kernel's main cost).
-// Exact for any data: ties share a bucket; NaN z sit in no bucket (their p is the count of
-// non-NaN z, above every x code), NaN x get code 0, +-inf clamp to the end buckets; degenerate
-// or very skewed data only make the scans longer.  Every block of a shard rebuilds the buckets
-// (O(nz) LDS work) and codes its share of the shard's x and z.  Replaces k_sort_chunks +
-// k_rank_codes (41 + 78 us at the bench shape).
+// into LDS in bucket order (a counting sort by bucket), and then a code is
+// (#z in lower buckets) + (#z in its own bucket below / at most v), by a scan of one bucket.
+// Bucket maps, both monotone (every IEEE step in them is monotone), so bucket order is value
+// order:
+//   refine = 0  value range: f = clamp(floor((v - zmin) * NB / (zmax - zmin))) over the finite z;
+//   refine = 1  equal depth: a histogram of a 1024-value sample of z over kBucketNC value-range
+//               bins, whose piecewise-linear CDF maps v to (cs[b] + t * (cs[b+1] - cs[b])) * NB / n
+//               (t = the position of v inside bin b): every bucket then holds ~nz / NB values
+//               whatever the shape of the data (Gaussian scores put ~25 values in the central
+//               value-range buckets of a 15625-value shard; the scans are the main cost).
+// The counting sort takes ONE pass of LDS atomics: the atomicAdd that counts z in its bucket
+// returns z's slot inside the bucket, so after the prefix z is stored without a second atomic.
+// Exact for any data and any map: ties share a bucket; NaN z sit in no bucket (their p is the
+// count of non-NaN z, above every x code), NaN x get code 0, +-inf clamp to the end buckets; a
+// poor map (skewed data, an unrepresentative sample) only makes scans longer.  Every block of a
+// shard rebuilds the buckets and codes its share of the shard's x and z.  Replaces
+// k_sort_chunks + k_rank_codes (41 + 78 us at the bench shape).
 constexpr int kBucketNB = 2048;
+constexpr int kBucketNC = 256;          // value-range bins of the sampled CDF (refine = 1)
 constexpr int64_t kBucketMaxZ = 16384;  // 128 KiB of z in LDS
 constexpr size_t kBucketLds = sizeof(double) * kBucketMaxZ + sizeof(unsigned) * (3 * kBucketNB + 2);
 
@@ -167,8 +169,8 @@ __device__ __forceinline__ void bucket_prefix(const unsigned* cnt, unsigned* st,
 // buckets, only the x-values, and the block's sum of their codes (#z < x, plus #z <= x for
 // half-ties) added to out[s] — the integer of k_count_complete / k_rank_count.
 // The shard's z is loaded ONCE into registers (kZPer per thread, all loads in flight
-// together) and the range, histogram and scatter passes read the registers; the first round
-// of this block's code elements is loaded beside it.  Bucket scans read four values per trip.
+// together); the first round of this block's code elements is loaded beside it.  Bucket scans
+// read four values per trip.
 // Codes are written with row strides sx / sz (multiples of 8, so rows are 16-B aligned).
 template <typename T, int PRED, bool COUNT = false>
 __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
@@ -178,9 +180,9 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     unsigned long long* __restrict__ out = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* zb = (T*)smem;                                                 // z by bucket
-  unsigned* cs = (unsigned*)(smem + sizeof(double) * kBucketMaxZ);  // NB + 1 coarse prefix
-  unsigned* fst = cs + kBucketNB + 1;                               // NB + 1 fine starts
-  unsigned* cur = fst + kBucketNB + 1;                              // NB counts / cursors
+  unsigned* cs = (unsigned*)(smem + sizeof(double) * kBucketMaxZ);  // NB + 1 sample prefix
+  unsigned* st = cs + kBucketNB + 1;                                // NB + 1 bucket starts
+  unsigned* cur = st + kBucketNB + 1;                               // NB counts
   __shared__ double red_min[kSortThreads / kWave], red_max[kSortThreads / kWave];
   __shared__ unsigned wave_tot[kSortThreads / kWave];
   __shared__ unsigned nan_z;
@@ -236,62 +238,64 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     mn = red_min[w] < mn ? red_min[w] : mn;
     mx = red_max[w] > mx ? red_max[w] : mx;
   }
-  const double scale = mx > mn ? (double)kBucketNB / (mx - mn) : 0.0;
-  // coarse bucket of v and its position t in [0, 1] inside it (NaN u -> bucket 0, t = 0)
+  const int nbin = refine ? kBucketNC : kBucketNB;
+  const double scale = mx > mn ? (double)nbin / (mx - mn) : 0.0;
+  // value-range bin of v and its position t in [0, 1] inside it (NaN u -> bin 0, t = 0)
   auto coarse = [&](double v, double& t) -> int {
     const double u = (v - mn) * scale;
-    const int b = (int)__builtin_fmin(__builtin_fmax(u, 0.0), (double)(kBucketNB - 1));
+    const int b = (int)__builtin_fmin(__builtin_fmax(u, 0.0), (double)(nbin - 1));
     t = __builtin_fmin(__builtin_fmax(u - (double)b, 0.0), 1.0);
     return b;
   };
-  // 2. coarse histogram (NaN z counted apart) and its prefix
-  bool zin[kZPer];
-  int zbk[kZPer];
+  // 2. refine: the sampled CDF.  Thread t samples z[t + (t mod 16) * 1024], spread over the
+  // whole shard whatever its order.
+  double fscale = 0.0;
+  if (refine) {
+    const int rs = tid & (kZPer - 1);
+    T sv = zr[0];
 #pragma unroll
-  for (int r = 0; r < kZPer; ++r) {
-    zin[r] = tid + (int64_t)r * kSortThreads < nz && !is_nan_score<T>(zr[r]);
+    for (int r = 1; r < kZPer; ++r) sv = rs == r ? zr[r] : sv;
+    const bool sin = tid + (int64_t)rs * kSortThreads < nz && !is_nan_score<T>(sv);
     double t;
-    zbk[r] = coarse(bucket_value<T>(zr[r]), t);
-    if (zin[r]) atomicAdd(&cur[zbk[r]], 1u);
-    else if (tid + (int64_t)r * kSortThreads < nz) atomicAdd(&nan_z, 1u);
+    if (sin) atomicAdd(&cur[coarse(bucket_value<T>(sv), t)], 1u);
+    __syncthreads();
+    bucket_prefix(cur, cs, wave_tot);  // bins >= kBucketNC are empty
+    fscale = (double)kBucketNB / (double)cs[kBucketNB];
+    for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = 0;
+    __syncthreads();
   }
-  __syncthreads();
-  bucket_prefix(cur, cs, wave_tot);
   TW_PHASE(2);
-  const unsigned n_valid = cs[kBucketNB];
-  const double fscale = (double)kBucketNB / (double)n_valid;
   auto bucket = [&](double v) -> int {
     double t;
     const int b = coarse(v, t);
     if (!refine) return b;
     const unsigned c0 = cs[b], c1 = cs[b + 1];
     const double pos = (double)c0 + t * (double)(c1 - c0);
-    return (int)__builtin_fmin(pos * fscale, (double)(kBucketNB - 1));  // NaN (n = 0): NB - 1
+    return (int)__builtin_fmin(pos * fscale, (double)(kBucketNB - 1));  // NaN (no sample): NB-1
   };
-  const unsigned* st = cs;  // bucket starts of the map in use
-  if (refine) {  // 3. fine (equal-depth) histogram and its prefix
-    for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = 0;
-    __syncthreads();
+  // 3. counting sort of z by bucket: one returning atomic per z gives its slot in the bucket
+  int zbk[kZPer];
+  unsigned zslot[kZPer];
 #pragma unroll
-    for (int r = 0; r < kZPer; ++r) {
-      if (zin[r]) {
-        zbk[r] = bucket(bucket_value<T>(zr[r]));
-        atomicAdd(&cur[zbk[r]], 1u);
-      }
+  for (int r = 0; r < kZPer; ++r) {
+    const bool live = tid + (int64_t)r * kSortThreads < nz;
+    zbk[r] = -1;
+    if (live && !is_nan_score<T>(zr[r])) {
+      zbk[r] = bucket(bucket_value<T>(zr[r]));
+      zslot[r] = atomicAdd(&cur[zbk[r]], 1u);
+    } else if (live) {
+      atomicAdd(&nan_z, 1u);
     }
-    __syncthreads();
-    bucket_prefix(cur, fst, wave_tot);
-    st = fst;
   }
-  TW_PHASE(3);
-  // 4. scatter z into bucket order
-  for (int i = tid; i < kBucketNB; i += kSortThreads) cur[i] = st[i];
   __syncthreads();
+  bucket_prefix(cur, st, wave_tot);
+  TW_PHASE(3);
 #pragma unroll
   for (int r = 0; r < kZPer; ++r)
-    if (zin[r]) zb[atomicAdd(&cur[zbk[r]], 1u)] = zr[r];
+    if (zbk[r] >= 0) zb[st[zbk[r]] + zslot[r]] = zr[r];
   __syncthreads();
   TW_PHASE(4);
+  const unsigned n_valid = st[kBucketNB];
   // 5. codes of this block's share (rounds of kEPer elements per thread; the first is loaded)
   unsigned long long acc = 0;
   for (int64_t r0 = e0; r0 < e1; r0 += (int64_t)kEPer * kSortThreads) {
@@ -663,27 +667,33 @@ __global__ __launch_bounds__(kRngThreads, 8) void k_count_idx_ranked(
   const int64_t a0 = std::min<int64_t>(q1, (q0 + NV - 1) / NV * NV);
   const int64_t a1 = std::max<int64_t>(a0, q1 / NV * NV);
   const int nv = (int)((a1 - a0) / NV);
-  auto one = [&](I a, I b) -> unsigned {
-    bool in;
-    uint32_t i, j;
+  // span test of one pair: block-local offsets i, j (32-bit) and whether both lie in the shard
+  auto local = [&](I a, I b, uint32_t& i, uint32_t& j) -> bool {
     if constexpr (sizeof(I) == 4) {  // 32-bit offsets: the arrays hold < 2^31 elements
       i = (uint32_t)(a - (int32_t)xb);
       j = (uint32_t)(b - (int32_t)zb);
-      in = i < (uint32_t)nx && j < (uint32_t)nz;
+      return i < (uint32_t)nx && j < (uint32_t)nz;
     } else {
       const uint64_t i64 = (uint64_t)(a - xb), j64 = (uint64_t)(b - zb);
-      in = i64 < (uint64_t)nx && j64 < (uint64_t)nz;
       i = (uint32_t)i64;
       j = (uint32_t)j64;
+      return i64 < (uint64_t)nx && j64 < (uint64_t)nz;
     }
-    if (in) {
+  };
+  // an index outside its shard's span compares the scores themselves
+  auto gathered = [&](I a, I b) -> unsigned {
+    const T xv = x[a], zv = z[b];
+    return (unsigned)(xv > zv) + (PRED == TW_PRED_HALF ? (unsigned)(xv >= zv) : 0u);
+  };
+  auto one = [&](I a, I b) -> unsigned {
+    uint32_t i, j;
+    if (local(a, b, i, j)) {
       const unsigned pj = lz[j];
       unsigned r = (unsigned)lx[i] > pj;
       if (PRED == TW_PRED_HALF) r += (unsigned)lx2[i] > pj;
       return r;
     }
-    const T xv = x[a], zv = z[b];
-    return (unsigned)(xv > zv) + (PRED == TW_PRED_HALF ? (unsigned)(xv >= zv) : 0u);
+    return gathered(a, b);
   };
   const I* __restrict__ px = ix + a0;
   const I* __restrict__ pzi = iz + a0;
@@ -699,27 +709,62 @@ __global__ __launch_bounds__(kRngThreads, 8) void k_count_idx_ranked(
       return r;
     }
   };
-  auto compare = [&](const V (&A)[U], const V (&Bv)[U], int v0) -> unsigned {
+  // the batch's U x NV pairs without branches: out-of-span pairs read code 0 and count nothing,
+  // and only when some lane of the wave has one (never, for slice plans) the scores are gathered
+  auto compare = [&](const V (&A)[U], const V (&Bv)[U], int base) -> unsigned {
     unsigned c = 0;
+#ifdef TW_IDX_STREAM_ONLY  // kernel study (tools/phase_codes.py): the index streams alone
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < NV; ++e) c += (unsigned)(IV::at(A[u], e) ^ IV::at(Bv[u], e)) & 1u;
+    return c;
+#endif
+    bool bad = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (v0 + u * kRngThreads < nv) {
+      const bool live = base + tid + u * kRngThreads < nv;
 #pragma unroll
-        for (int e = 0; e < NV; ++e) c += one(IV::at(A[u], e), IV::at(Bv[u], e));
+      for (int e = 0; e < NV; ++e) {
+        uint32_t i, j;
+        const bool in = local(IV::at(A[u], e), IV::at(Bv[u], e), i, j) && live;
+        bad |= live && !in;
+        i = in ? i : 0u;
+        j = in ? j : 0u;
+        const unsigned pj = lz[j];
+        unsigned r = (unsigned)lx[i] > pj;
+        if (PRED == TW_PRED_HALF) r += (unsigned)lx2[i] > pj;
+        c += in ? r : 0u;
+      }
+    }
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool live = base + tid + u * kRngThreads < nv;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          uint32_t i, j;
+          const I a = IV::at(A[u], e), b = IV::at(Bv[u], e);
+          if (live && !local(a, b, i, j)) c += gathered(a, b);
+        }
       }
     }
     return c;
   };
-  V A[U], Bv[U];
-  constexpr int step = U * kRngThreads;
+  // one batch of U vectors per stream, unconditionally (positions past the end re-read the
+  // last vector and count nothing): branch-free loads keep the compiler's wait counts exact
+  auto load_batch = [&](V (&A)[U], V (&Bv)[U], int base) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int v = tid + u * kRngThreads;
-    if (v < nv) {
+    for (int u = 0; u < U; ++u) {
+      const int v = min(base + tid + u * kRngThreads, nv - 1);
       A[u] = load(px, v);
       Bv[u] = load(pzi, v);
     }
-  }
+  };
+  constexpr int step = U * kRngThreads;
+  const int nb = (nv + step - 1) / step;  // batches (block-uniform)
+  V A[U], Bv[U];
+  if (nb > 0) load_batch(A, Bv, 0);  // in flight while the codes are staged
   if (nx > 0 && nz > 0)
     stage_codes<PRED>(codes, cx + (int64_t)s * sx, cx2 + (int64_t)s * sx, pz + (int64_t)s * sz,
                       nx, nz);
@@ -728,33 +773,20 @@ __global__ __launch_bounds__(kRngThreads, 8) void k_count_idx_ranked(
   // scalar head [q0, a0) and tail [a1, q1) (fewer than NV pairs each)
   if (tid < a0 - q0) acc += one(ix[q0 + tid], iz[q0 + tid]);
   if (tid < q1 - a1) acc += one(ix[a1 + tid], iz[a1 + tid]);
-  for (int v0 = tid; v0 < nv; v0 += step) {
-    if constexpr (PIPE) {
-      V A2[U], B2[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {  // next batch in flight while this one is compared
-        const int v = v0 + step + u * kRngThreads;
-        if (v < nv) {
-          A2[u] = load(px, v);
-          B2[u] = load(pzi, v);
-        }
-      }
-      acc += compare(A, Bv, v0);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        A[u] = A2[u];
-        Bv[u] = B2[u];
-      }
-    } else {
-      acc += compare(A, Bv, v0);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int v = v0 + step + u * kRngThreads;
-        if (v < nv) {
-          A[u] = load(px, v);
-          Bv[u] = load(pzi, v);
-        }
-      }
+  if constexpr (PIPE) {
+    // two register buffers used in turn (no copies between them, which would make the
+    // compiler wait for the in-flight batch): batch k+1 loads while batch k is compared
+    V A2[U], B2[U];
+    for (int k = 0; k < nb; k += 2) {
+      load_batch(A2, B2, (k + 1) * step);
+      acc += compare(A, Bv, k * step);
+      load_batch(A, Bv, (k + 2) * step);
+      acc += compare(A2, B2, (k + 1) * step);
+    }
+  } else {
+    for (int k = 0; k < nb; ++k) {
+      acc += compare(A, Bv, k * step);
+      load_batch(A, Bv, (k + 1) * step);
     }
   }
   unsigned long long tot = wave_sum_u64((unsigned long long)acc);
