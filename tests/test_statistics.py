@@ -83,3 +83,76 @@ def test_device_rng_rejection_path_matches_oracle(gpu):
     assert int(out[0]) == int(np.sum(i >= n // 2))
     del X
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------ repartition and SWR draws
+# The device repartition (csrc/permute.hip, restated by oracle.feistel_perm bit for bit) and
+# the learning loop's device draws (tw_swr_rows_rng / tw_pair_grad_rng, oracle._sgd_draw) stand
+# in for NumPy's shuffle (compute_stats.py:66-67) and randint (:52-53, :155-156).  Their
+# restatements are checked here for the properties those reference calls have.
+
+@pytest.mark.parametrize("n", [10, 1000, 4099])
+def test_feistel_positions_uniform_over_keys(n):
+    """Over many keys, where element 0 lands and where (0, 1) land jointly are uniform."""
+    keys = 6000
+    p0, p1 = np.empty(keys, np.int64), np.empty(keys, np.int64)
+    for k in range(keys):
+        p0[k], p1[k] = O.feistel_perm(np.array([0, 1]), n, 0x51ED + 7919 * k)
+    assert np.all(p0 != p1)
+    bins = min(n, 20)
+    h = np.bincount(p0 * bins // n, minlength=bins)
+    assert stats.chisquare(h).pvalue > 1e-4
+    if n <= 16:  # the ordered pair (perm(0), perm(1)) uniform over the n(n-1) cells
+        cells = np.bincount(p0 * n + p1, minlength=n * n).reshape(n, n)
+        assert stats.chisquare(cells[~np.eye(n, dtype=bool)]).pvalue > 1e-4
+    else:  # coarse bins: distinctness is a negligible dependence
+        tab = np.histogram2d(p0, p1, bins=(8, 8), range=((0, n), (0, n)))[0]
+        assert stats.chi2_contingency(tab).pvalue > 1e-4
+
+
+def test_feistel_full_permutation_bias_small_n_documented():
+    """Limitation kept visible: on the tiniest domains the keyed Feistel
+    family is NOT uniform over all n! permutations (n = 3 is, n = 4 measurably is not), while
+    its low-order marginals stay uniform (above).  No keyed family can reach all n!
+    permutations once n! > 2^64 (n >= 21) anyway; the estimators depend on the shard
+    composition, whose distribution the variance tests (tests/test_gpu_variance.py) check."""
+    from collections import Counter
+    c3 = Counter(tuple(O.feistel_perm(np.arange(3), 3, k * 2654435761 + 17)) for k in range(6000))
+    assert len(c3) == 6 and stats.chisquare(list(c3.values())).pvalue > 1e-4
+    c4 = Counter(tuple(O.feistel_perm(np.arange(4), 4, k * 2654435761 + 17)) for k in range(24000))
+    assert len(c4) == 24 and stats.chisquare(list(c4.values())).pvalue < 1e-6
+
+
+def test_feistel_is_a_bijection_and_keys_independent():
+    n = 100_003
+    a = O.feistel_perm(np.arange(n), n, 123)
+    b = O.feistel_perm(np.arange(n), n, 124)
+    assert np.array_equal(np.sort(a), np.arange(n)) and np.array_equal(np.sort(b), np.arange(n))
+    assert np.array_equal(O.feistel_perm_inv(a, n, 123), np.arange(n))
+    # consecutive keys give unrelated permutations (the repartitions of UnNT's T steps)
+    assert abs(stats.spearmanr(a, b).correlation) < 0.02
+    assert abs(stats.spearmanr(np.arange(n), a).correlation) < 0.02
+    # the fraction of a shard that stays in the same shard is the hypergeometric mean 1/N
+    N = 64
+    same = np.mean(a * N // n == np.arange(n) * N // n)
+    assert abs(same - 1 / N) < 0.003, same
+
+
+def test_sgd_device_draws_uniform_and_independent():
+    """SWR_divide rows (tag 0x40000000) and grad_inc_block pairs (tag 0x80000000) drawn on the
+    device: uniform over their ranges, independent across shards and steps."""
+    seed, n, k = 0xABC, 9117, 20_000
+    rows = [O._mulhi64(O._sgd_draw(seed, 0, np.arange(k), s, 0x40000000)[0], n)
+            for s in range(3)]
+    for r in rows:
+        assert r.min() >= 0 and r.max() < n
+        assert stats.chisquare(np.bincount(r * 50 // n, minlength=50)).pvalue > 1e-4
+    tab = np.histogram2d(rows[0], rows[1], bins=(8, 8), range=((0, n), (0, n)))[0]
+    assert stats.chi2_contingency(tab).pvalue > 1e-4
+    u0, v0 = O._sgd_draw(seed, 5, np.arange(k), 2, 0x80000000)
+    u1, _ = O._sgd_draw(seed, 6, np.arange(k), 2, 0x80000000)
+    i0, j0, i1 = O._mulhi64(u0, 91), O._mulhi64(v0, 7), O._mulhi64(u1, 91)
+    assert stats.chisquare(np.bincount(i0, minlength=91)).pvalue > 1e-4
+    assert stats.chisquare(np.bincount(j0, minlength=7)).pvalue > 1e-4
+    assert stats.chi2_contingency(np.histogram2d(i0, j0, bins=(7, 7))[0]).pvalue > 1e-4
+    assert stats.chi2_contingency(np.histogram2d(i0, i1, bins=(7, 7))[0]).pvalue > 1e-4
