@@ -357,11 +357,12 @@ def incomplete_replay(X, Z, shards, B, reps=20):
     """UnNB in replay mode (compute_stats.py:37-42 via UB): B explicit index pairs per shard,
     as NumPy's randint hands them over after the drop-in's bound check narrows them to int32
     (8 B per pair), already resident in HBM, counted by tw_count_pairs_idx32_ws:
-    16-bit rank codes of both samples (k_rank_codes_bucket), then k_count_idx_ranked streams
-    the indices and compares codes held in LDS.  HBM-bound on the index streams.  Indices are
+    k_count_idx_img stages each shard's float32 score images in LDS and streams the index pairs
+    (pairs with equal images are decided on the scores).  HBM-bound on the index streams.  Indices are
     drawn on the device here (uniform within each shard's contiguous range); the kernel sees the
     same layout as the drop-in UB/UnNB path.  The plain gather kernel (tw_count_pairs_idx32,
-    the fallback for shards of >= 65536 values) and the int64-index call are timed beside it."""
+    the fallback for shard pairs too large for LDS) and the int64-index call are timed beside
+    it."""
     import torch
     from tuplewise import _engine, _lib as L
     n = X.numel()
@@ -414,8 +415,8 @@ def incomplete_replay(X, Z, shards, B, reps=20):
     bpp = 8  # algorithmic bytes per pair: two int32 indices
     return {"note": "UnNB replay mode: B explicit int32 index pairs per shard resident in HBM "
                     "(NumPy-drawn and narrowed after the bound check in the drop-in path; "
-                    "device-drawn here); tw_count_pairs_idx32_ws: rank codes of both samples, "
-                    "then k_count_idx_ranked compares codes held in LDS",
+                    "device-drawn here); tw_count_pairs_idx32_ws: k_count_idx_img compares "
+                    "float32 score images held in LDS (equal images decided on the scores)",
             "B_per_shard": B, "value": pairs * reps / dt, "unit": "pairs/s",
             "ms_per_call": dt / reps * 1e3,
             "counts_identical_to_plain": bool(torch.equal(out, out_p)),
@@ -426,12 +427,14 @@ def incomplete_replay(X, Z, shards, B, reps=20):
                                         "GBps_indices": bpp * pairs / (kms_p * 1e-3) / 1e9},
             "ranked_int64_indices": {"value": pairs * reps / dt64, "kernel_ms": kms64,
                                      "GBps_indices": 16 * pairs / (kms64 * 1e-3) / 1e9},
-            "roofline": {"bound": "hbm", "kernel": "k_rank_codes_bucket + k_count_idx_ranked",
+            "roofline": {"bound": "hbm", "kernel": "k_count_idx_img",
                          "achieved": bpp * pairs / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": bpp * pairs / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "kernel_ms": kms,
                          "note": "8 algorithmic bytes per pair (two int32 indices, SURVEY.md "
-                                 "§8(d)); kernel_ms = the whole call (rank codes + count)"}}
+                                 "§8(d)); kernel_ms = the whole call: one kernel that stages "
+                                 "each shard's float32 score images in LDS and streams the "
+                                 "index pairs (csrc/imagecount.hip)"}}
 
 
 def spawn_ranks(n: int, script: str | None = None, argv: list | None = None) -> int:
@@ -750,12 +753,12 @@ def main():
         "incomplete": {
             "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
                     "drawn pairs per shard (Philox4x32-10, two pairs per block, Lemire maps) "
-                    "counted per step on 16-bit rank codes in LDS",
+                    "counted per step on float32 score images in LDS",
             "B_per_shard": B_inc, "value": inc_pairs_rank * world * args.steps / dt_inc,
             "unit": "pairs/s", "ms_per_step": dt_inc / args.steps * 1e3,
             "estimate_last_step": float(est_inc),
             "roofline": {"bound": "valu",
-                         "kernel": "k_rank_codes_bucket + k_count_rng_ranked",
+                         "kernel": "k_count_rng_img",
                          "frac_vs_int32_op_peak": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3)
                          / INT_LANE_OPS_MEASURED,
                          "int32_op_peak": INT_LANE_OPS_MEASURED / 1e12,
@@ -766,8 +769,9 @@ def main():
                          "kernel_ms": kms_inc,
                          "note": f"{INC_LANE_OPS} lane-ops per pair (SURVEY.md §8(d) contract "
                                  "constant: 2 Philox4x32-10 words + 2 range maps + 1 compare); "
-                                 "kernel_ms = the whole tw_count_pairs_rng_ws call (bucket "
-                                 "rank codes, draw-and-count); frac is against the f64 lane-op "
+                                 "kernel_ms = the whole tw_count_pairs_rng_ws call (one "
+                                 "kernel: float32 score images in LDS, Philox draws, compares); "
+                                 "frac is against the f64 lane-op "
                                  "peak of the contract, frac_vs_int32_op_peak against the "
                                  "measured 32-bit integer VOP2 issue rate (the Philox work is "
                                  "32-bit integer)"}},

@@ -191,6 +191,15 @@ int64_t tw_count_pairs_rng_work_bytes(int32_t n_shards, int64_t max_nx, int64_t 
  * value buckets in LDS when every shard has nz <= 16384, 2 = value-range buckets only, 0 =
  * always sort + binary search (A/B and tests; same codes). */
 int tw_count_rng_set_codes(int32_t by_bucket);
+/* Default mode 3 of tw_count_rng_set_codes (csrc/imagecount.hip): instead of rank codes, each
+ * block stages the float32 images of its shard's scores in LDS (round to nearest: monotone) and
+ * decides x > z on them, gathering the scores only for pairs whose images are equal (ties, -0/+0,
+ * values within a float ulp): the same counts, no codes kernel, no workspace.  Applies when a
+ * shard pair's images fit in LDS (4 * (nx + nz) bytes <= 159 KiB) and pred is GT or HALF (or
+ * SUBGT on doubles); otherwise the codes path runs (and past it the plain kernel).  Tuning hook:
+ * blocks per shard (0 = plan) and 16-B index vectors per stream and batch (1, 2, 4; + 8 =
+ * nontemporal index loads; default 9). */
+int tw_count_img_set_plan(int32_t parts, int32_t u);
 int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, int64_t B, uint64_t seed, uint64_t shard_base,

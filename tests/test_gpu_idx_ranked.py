@@ -91,8 +91,18 @@ def _idx(L, a, width, misalign):
                                   "large_shard"])
 @pytest.mark.parametrize("stray", [False, True])
 @pytest.mark.parametrize("width,misalign", [(32, False), (64, False), (32, True)])
-def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray, width, misalign):
+@pytest.mark.parametrize("codes", [3, 2])
+def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray, width, misalign, codes):
+    """codes 3: float32 images in LDS (default); 2: 16-bit rank codes (value buckets)."""
     from tuplewise import _engine as E, _lib as L
+    L.call("tw_count_rng_set_codes", codes)
+    try:
+        _check_idx(E, L, kind, stray, width, misalign)
+    finally:
+        L.call("tw_count_rng_set_codes", 3)
+
+
+def _check_idx(E, L, kind, stray, width, misalign):
     rng = np.random.default_rng(zlib.crc32(f"{kind}{stray}".encode()))
     x, x_off, z, z_off = _sample(kind, rng)
     ix, iz, po = _pairs(x_off, z_off, 20011, rng, stray)
@@ -111,8 +121,8 @@ def test_idx_ranked_matches_plain_and_numpy(gpu, kind, stray, width, misalign):
         np.testing.assert_array_equal(ranked, want, err_msg=f"ranked {kind} {mode}")
 
 
-@pytest.mark.parametrize("parts", [0, 8, 32])
-def test_idx_ranked_bench_shape(gpu, parts):
+@pytest.mark.parametrize("codes,parts", [(3, 0), (3, 2), (3, 8), (2, 0), (2, 8), (2, 32)])
+def test_idx_ranked_bench_shape(gpu, codes, parts):
     """The bench / C3 shape: 64 shards of 15625 x 15625, 1e6 int32 index pairs per shard, a
     512-block grid through xcd_block; every shard against a torch gather-compare."""
     import torch
@@ -128,12 +138,16 @@ def test_idx_ranked_bench_shape(gpu, parts):
     po = np.arange(N + 1, dtype=np.int64) * B
     offd = L.to_device(off)
     want = (X[ix.long()] > Z[iz.long()]).view(N, B).sum(1).cpu().numpy().astype(np.uint64)
+    L.call("tw_count_rng_set_codes", codes)
     L.call("tw_count_idx_set_parts", parts)
+    L.call("tw_count_img_set_plan", parts, 2 if parts == 2 else 9)
     try:
         got = E.count_indexed_ranked_dev(X, offd, Z, offd, k, k, L.TW_F64, ix, iz, po,
                                          L.TW_PRED_GT).cpu().numpy().view(np.uint64)
     finally:
         L.call("tw_count_idx_set_parts", 0)
+        L.call("tw_count_img_set_plan", 0, 9)
+        L.call("tw_count_rng_set_codes", 3)
     np.testing.assert_array_equal(got, want)
 
 
@@ -152,5 +166,5 @@ def test_idx_ranked_codes_sorted_path(gpu):
                                          int(np.diff(z_off).max()), L.TW_F64, ix, iz, po,
                                          L.TW_PRED_HALF).cpu().numpy().view(np.uint64)
     finally:
-        L.call("tw_count_rng_set_codes", 1)
+        L.call("tw_count_rng_set_codes", 3)
     np.testing.assert_array_equal(got, want)

@@ -48,6 +48,7 @@ _SIGNATURES = {
     "tw_count_pairs_rng": [_vp, _vp, _vp, _vp, _i32, _i64, _u64, _u64, _i32, _i32, _vp, _vp],
     "tw_count_pairs_rng_work_bytes": [_i32, _i64, _i64, _i32, _i32],
     "tw_count_rng_set_codes": [_i32],
+    "tw_count_img_set_plan": [_i32, _i32],
     "tw_count_sorted_set_bucket": [_i32],
     "tw_count_pairs_rng_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _u64, _u64, _i32, _i32,
                               _vp, _i64, _vp, _vp],

@@ -1,0 +1,399 @@
+// imagecount.hip — incomplete counts on float32 images of the scores held in LDS (rows A5/A8:
+// cs.UB / UnNB / UnNBT, compute_stats.py:37-42, :104-123, in replay and device-RNG mode).
+//
+// The explicit-index (replay) and device-drawn pairs of a shard compare x[i] > z[j] at random
+// positions.  A 15625 + 15625-value shard pair is 250 KB of doubles, too much for a CU's
+// 160 KB of LDS, but its float32 images are 125 KB: one block per CU stages its shard's images
+// once and every pair then reads two LDS words instead of two random L2 lines.  The compare is
+// exact:
+//   f(v) = (float)v rounds to nearest, a monotone non-decreasing map (for doubles and for int64),
+//   so f(x) > f(z) implies x > z and f(x) < f(z) implies x < z;
+//   only f(x) == f(z) is undecided — ties, -0 vs +0, values within half a float ulp of each
+//   other, both beyond the float range, subnormals — and those pairs are decided on the scores
+//   themselves (two gathers), only in the waves where they occur;
+//   NaN images are NaN: every compare is false and they are never "equal", so a pair with a NaN
+//   counts nothing, as in NumPy.
+// Half-ties (TW_PRED_HALF) add x >= z: f(x) > f(z) gives 2, f(x) < f(z) gives 0.
+// No precomputed rank codes (the codes kernel of the 16-bit path cost 28 us of a 130 us replay
+// call at the bench shape), no workspace.  Scores with many exact ties between the samples
+// (small integers) take the gather for every tied pair: correct, slower.
+#include "imagecount.h"
+#include <algorithm>
+
+namespace tw {
+
+constexpr int kImgThreads = 1024;
+
+// the shard's images into LDS: eight loads in flight per thread, then the conversions
+template <typename T>
+__device__ __forceinline__ void stage_images(float* __restrict__ dst, const T* __restrict__ src,
+                                             int64_t n) {
+  constexpr int U = 8;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)U * kImgThreads) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * kImgThreads;
+      v[u] = i < n ? src[i] : (T)0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * kImgThreads;
+      if (i < n) dst[i] = (float)v[u];
+    }
+  }
+}
+
+__device__ __forceinline__ int64_t al4(int64_t n) { return (n + 3) & ~(int64_t)3; }
+
+// pair outcome from the images: r = the count to add when decided, und = undecided (equal
+// images: the scores decide)
+template <int PRED>
+__device__ __forceinline__ unsigned image_cmp(float xf, float zf, bool& und) {
+  und = xf == zf;
+  return (xf > zf) ? (PRED == TW_PRED_HALF ? 2u : 1u) : 0u;
+}
+
+template <typename T, int PRED>
+__device__ __forceinline__ unsigned exact_cmp(T xv, T zv) {
+  return (unsigned)(xv > zv) + (PRED == TW_PRED_HALF ? (unsigned)(xv >= zv) : 0u);
+}
+
+template <typename I> struct ImgVec;
+typedef int32_t img_i32x4 __attribute__((ext_vector_type(4)));
+typedef int64_t img_i64x2 __attribute__((ext_vector_type(2)));
+template <> struct ImgVec<int32_t> {
+  using V = int4;
+  using NVec = img_i32x4;  // the same 16 bytes as a clang vector (nontemporal builtin operand)
+  static constexpr int N = 4;
+  __device__ static __forceinline__ int32_t at(const V& v, int e) {
+    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+  }
+};
+template <> struct ImgVec<int64_t> {
+  using V = longlong2;
+  using NVec = img_i64x2;
+  static constexpr int N = 2;
+  __device__ static __forceinline__ int64_t at(const V& v, int e) { return e == 0 ? v.x : v.y; }
+};
+
+// Replay: explicit absolute index pairs (as tw_count_pairs_idx); an index outside its shard's
+// span compares the scores.  Index streams as 16-B vectors (VEC: aligned base pointers), U per
+// stream and batch, two register buffers used in turn (batch k+1 in flight while batch k is
+// compared; the first batch is issued before the images are staged).  Loads are unconditional
+// (clamped to the last vector) so the compiler's wait counts stay exact.
+template <typename T, int PRED, typename I, bool VEC, int U, bool NT>
+__global__ __launch_bounds__(kImgThreads) void k_count_idx_img(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, const I* __restrict__ ix, const I* __restrict__ iz,
+    const int64_t* __restrict__ pair_off, int parts, unsigned long long* __restrict__ out) {
+  using IV = ImgVec<I>;
+  using V = typename IV::V;
+  constexpr int NV = VEC ? IV::N : 1;
+  extern __shared__ __attribute__((aligned(16))) float img[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);  // a shard's parts share one L2
+  const int s = lb / parts;
+  const int part = lb - s * parts;
+  const int tid = threadIdx.x;
+  const int64_t xb = x_off[s], zb = z_off[s];
+  const int64_t nx = x_off[s + 1] - xb, nz = z_off[s + 1] - zb;
+  float* lx = img;
+  float* lz = img + al4(nx);
+  const int64_t pb = pair_off[s], pe = pair_off[s + 1];
+  const int64_t per = (pe - pb + parts - 1) / parts;
+  const int64_t q0 = std::min<int64_t>(pe, pb + (int64_t)part * per);
+  const int64_t q1 = std::min<int64_t>(pe, q0 + per);
+  const int64_t a0 = std::min<int64_t>(q1, (q0 + NV - 1) / NV * NV);
+  const int64_t a1 = std::max<int64_t>(a0, q1 / NV * NV);
+  const int nv = (int)((a1 - a0) / NV);
+  auto local = [&](I a, I b, uint32_t& i, uint32_t& j) -> bool {
+    if constexpr (sizeof(I) == 4) {  // 32-bit offsets: the arrays hold < 2^31 elements
+      i = (uint32_t)(a - (int32_t)xb);
+      j = (uint32_t)(b - (int32_t)zb);
+      return i < (uint32_t)nx && j < (uint32_t)nz;
+    } else {
+      const uint64_t i64 = (uint64_t)(a - xb), j64 = (uint64_t)(b - zb);
+      i = (uint32_t)i64;
+      j = (uint32_t)j64;
+      return i64 < (uint64_t)nx && j64 < (uint64_t)nz;
+    }
+  };
+  auto one = [&](I a, I b) -> unsigned {  // scalar heads / tails
+    uint32_t i, j;
+    bool und = true;
+    unsigned r = 0;
+    if (local(a, b, i, j)) r = image_cmp<PRED>(lx[i], lz[j], und);
+    return und ? exact_cmp<T, PRED>(x[a], z[b]) : r;
+  };
+  const I* __restrict__ px = ix + a0;
+  const I* __restrict__ pzi = iz + a0;
+  auto load = [&](const I* p, int v) -> V {
+    if constexpr (VEC && NT) {  // streamed once: nontemporal
+      return __builtin_bit_cast(
+          V, __builtin_nontemporal_load(((const typename IV::NVec*)p) + v));
+    } else if constexpr (VEC) {
+      return ((const V*)p)[v];
+    } else {
+      V r;
+      r.x = p[v];
+      return r;
+    }
+  };
+  // a batch without branches; pairs whose images tie or that leave the shard's span are
+  // counted from the scores, in the waves that have one
+  auto compare = [&](const V (&A)[U], const V (&Bv)[U], int base) -> unsigned {
+    unsigned c = 0;
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = base + tid + u * kImgThreads < nv;
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        uint32_t i, j;
+        const bool in = local(IV::at(A[u], e), IV::at(Bv[u], e), i, j) && live;
+        bool und;
+        const unsigned r = image_cmp<PRED>(lx[in ? i : 0u], lz[in ? j : 0u], und);
+        bad |= live && (!in || und);
+        c += (in && !und) ? r : 0u;
+      }
+    }
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool live = base + tid + u * kImgThreads < nv;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          uint32_t i, j;
+          const I a = IV::at(A[u], e), b = IV::at(Bv[u], e);
+          bool und = true;
+          if (live && local(a, b, i, j)) image_cmp<PRED>(lx[i], lz[j], und);
+          if (live && und) c += exact_cmp<T, PRED>(x[a], z[b]);
+        }
+      }
+    }
+    return c;
+  };
+  auto load_batch = [&](V (&A)[U], V (&Bv)[U], int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = min(base + tid + u * kImgThreads, nv - 1);
+      A[u] = load(px, v);
+      Bv[u] = load(pzi, v);
+    }
+  };
+  constexpr int step = U * kImgThreads;
+  const int nb = (nv + step - 1) / step;
+  V A[U], Bv[U], A2[U], B2[U];
+  if (nb > 0) load_batch(A, Bv, 0);  // in flight while the images are staged
+  stage_images<T>(lx, x + xb, nx);
+  stage_images<T>(lz, z + zb, nz);
+  __syncthreads();
+  unsigned acc = 0;
+  if (tid < a0 - q0) acc += one(ix[q0 + tid], iz[q0 + tid]);
+  if (tid < q1 - a1) acc += one(ix[a1 + tid], iz[a1 + tid]);
+  for (int k = 0; k < nb; k += 2) {
+    load_batch(A2, B2, (k + 1) * step);
+    acc += compare(A, Bv, k * step);
+    load_batch(A, Bv, (k + 2) * step);
+    acc += compare(A2, B2, (k + 1) * step);
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part_sum[kImgThreads / kWave];
+  const int lane = tid & (kWave - 1), wid = tid / kWave;
+  if (lane == 0) part_sum[wid] = tot;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long sum = 0;
+    for (int w = 0; w < kImgThreads / kWave; ++w) sum += part_sum[w];
+    if (sum) atomicAdd(out + s, sum);
+  }
+}
+
+// Device RNG: the draws of tw_count_pairs_rng (Philox block q -> pairs 2q and 2q+1, Lemire
+// maps; csrc/count.hip k_count_rng) compared on the images.
+template <typename T, int PRED>
+__global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
+    const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
+    const int64_t* __restrict__ z_off, int64_t B, int parts, uint32_t k0, uint32_t k1,
+    uint32_t sid, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float img[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int s = lb / parts;
+  const int part = lb - s * parts;
+  const int64_t xb = x_off[s], zb = z_off[s];
+  const int64_t nx = x_off[s + 1] - xb, nz = z_off[s + 1] - zb;
+  unsigned acc = 0;
+  if (nx > 0 && nz > 0) {
+    float* lx = img;
+    float* lz = img + al4(nx);
+    stage_images<T>(lx, x + xb, nx);
+    stage_images<T>(lz, z + zb, nz);
+    __syncthreads();
+    const uint32_t ss = (uint32_t)s + sid;
+    const int64_t nq = (B + 1) / 2;
+    const int64_t per = (nq + parts - 1) / parts;
+    const int64_t q0 = (int64_t)part * per, q1 = std::min<int64_t>(nq, q0 + per);
+    // trip count uniform over the block (q1 - q0 is), so the ballot below is wave-uniform
+    for (int64_t qb = q0; qb < q1; qb += kImgThreads) {
+      const int64_t q = qb + threadIdx.x;
+      const bool live = q < q1;
+      uint32_t i0 = 0, j0 = 0, i1 = 0, j1 = 0;
+      bool two = false;
+      if (live) {
+        const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
+        i0 = lemire_index(r.a, (uint32_t)nx, q, ss, 0, k0, k1);
+        j0 = lemire_index(r.b, (uint32_t)nz, q, ss, 1, k0, k1);
+        two = 2 * q + 1 < B;
+        if (two) {
+          i1 = lemire_index(r.c, (uint32_t)nx, q, ss, 2, k0, k1);
+          j1 = lemire_index(r.d, (uint32_t)nz, q, ss, 3, k0, k1);
+        }
+      }
+      bool u0, u1;
+      const unsigned r0 = image_cmp<PRED>(lx[i0], lz[j0], u0);
+      const unsigned r1 = image_cmp<PRED>(lx[i1], lz[j1], u1);
+      u0 = u0 && live;
+      u1 = u1 && two;
+      acc += (live && !u0 ? r0 : 0u) + (two && !u1 ? r1 : 0u);
+      if (__builtin_expect(__ballot(u0 || u1) != 0, 0)) {
+        if (u0) acc += exact_cmp<T, PRED>(x[xb + i0], z[zb + j0]);
+        if (u1) acc += exact_cmp<T, PRED>(x[xb + i1], z[zb + j1]);
+      }
+    }
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part_sum[kImgThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part_sum[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < kImgThreads / kWave; ++w) b += part_sum[w];
+    if (b) atomicAdd(out + s, b);
+  }
+}
+
+static int g_img_parts = 0;  // tuning: blocks per shard (0 = plan)
+static int g_img_u = 1;      // tuning: index vectors per stream and batch (1, 2, 4)
+static int g_img_nt = 1;     // tuning: nontemporal index loads (default on: streamed once)
+
+ImgPlan plan_images(int32_t n_shards, int64_t max_nx, int64_t max_nz, int32_t pred,
+                    int64_t pairs) {
+  ImgPlan p{};
+  p.lds = (size_t)(al4h(max_nx) + max_nz) * sizeof(float);
+  p.ok = n_shards > 0 && max_nx > 0 && max_nz > 0 &&
+         (pred == TW_PRED_GT || pred == TW_PRED_HALF) && p.lds <= 160 * 1024 - 1024;
+  // one 1024-thread block per CU (up to 125 KB of images each): ~256 blocks over the grid,
+  // at least 16384 pairs per block
+  p.parts = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(256, n_shards),
+                                                        ceil_div(std::max<int64_t>(pairs, 1),
+                                                                 16384)));
+  if (g_img_parts > 0) p.parts = g_img_parts;
+  p.ok = p.ok && (int64_t)n_shards * p.parts < (1ll << 31);
+  return p;
+}
+
+template <typename T, int PRED, typename I, bool VEC, int U, bool NT>
+static int launch_idx_img_v(const void* x, const int64_t* x_off, const void* z,
+                            const int64_t* z_off, int32_t n_shards, const I* ix, const I* iz,
+                            const int64_t* pair_off, const ImgPlan& p, uint64_t* out,
+                            hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_idx_img<T, PRED, I, VEC, U, NT>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_count_idx_img<T, PRED, I, VEC, U, NT>), dim3(n_shards * p.parts),
+                     dim3(kImgThreads), p.lds, st, (const T*)x, x_off, (const T*)z, z_off, ix, iz,
+                     pair_off, p.parts, (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+template <typename T, int PRED, typename I>
+static int launch_idx_img_t(const void* x, const int64_t* x_off, const void* z,
+                            const int64_t* z_off, int32_t n_shards, const I* ix, const I* iz,
+                            const int64_t* pair_off, const ImgPlan& p, uint64_t* out,
+                            hipStream_t st) {
+  if ((((uintptr_t)ix | (uintptr_t)iz) & 15) != 0)
+    return launch_idx_img_v<T, PRED, I, false, 4, false>(x, x_off, z, z_off, n_shards, ix, iz,
+                                                         pair_off, p, out, st);
+#define TW_IMG(U, NT) return launch_idx_img_v<T, PRED, I, true, U, NT>(x, x_off, z, z_off, n_shards, ix, iz, pair_off, p, out, st)
+  if (g_img_nt) {
+    if (g_img_u == 2) TW_IMG(2, true);
+    if (g_img_u == 4) TW_IMG(4, true);
+    TW_IMG(1, true);
+  }
+  if (g_img_u == 2) TW_IMG(2, false);
+  if (g_img_u == 4) TW_IMG(4, false);
+  TW_IMG(1, false);
+#undef TW_IMG
+}
+
+template <typename I>
+int launch_idx_images(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                      int32_t n_shards, const I* ix, const I* iz, const int64_t* pair_off,
+                      int32_t dtype, int32_t pred, const ImgPlan& p, uint64_t* out,
+                      hipStream_t st) {
+  if (dtype == TW_F64) {
+    if (pred == TW_PRED_HALF)
+      return launch_idx_img_t<double, TW_PRED_HALF, I>(x, x_off, z, z_off, n_shards, ix, iz, pair_off, p, out, st);
+    return launch_idx_img_t<double, TW_PRED_GT, I>(x, x_off, z, z_off, n_shards, ix, iz, pair_off, p, out, st);
+  }
+  if (pred == TW_PRED_HALF)
+    return launch_idx_img_t<long long, TW_PRED_HALF, I>(x, x_off, z, z_off, n_shards, ix, iz, pair_off, p, out, st);
+  return launch_idx_img_t<long long, TW_PRED_GT, I>(x, x_off, z, z_off, n_shards, ix, iz, pair_off, p, out, st);
+}
+template int launch_idx_images<int32_t>(const void*, const int64_t*, const void*, const int64_t*,
+                                        int32_t, const int32_t*, const int32_t*, const int64_t*,
+                                        int32_t, int32_t, const ImgPlan&, uint64_t*, hipStream_t);
+template int launch_idx_images<int64_t>(const void*, const int64_t*, const void*, const int64_t*,
+                                        int32_t, const int64_t*, const int64_t*, const int64_t*,
+                                        int32_t, int32_t, const ImgPlan&, uint64_t*, hipStream_t);
+
+template <typename T, int PRED>
+static int launch_rng_img_t(const void* x, const int64_t* x_off, const void* z,
+                            const int64_t* z_off, int32_t n_shards, int64_t B, uint64_t seed,
+                            uint64_t sid, const ImgPlan& p, uint64_t* out, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_img<T, PRED>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_count_rng_img<T, PRED>), dim3(n_shards * p.parts), dim3(kImgThreads),
+                     p.lds, st, (const T*)x, x_off, (const T*)z, z_off, B, p.parts,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
+                     (unsigned long long*)out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+int launch_rng_images(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
+                      int32_t n_shards, int64_t B, uint64_t seed, uint64_t sid, int32_t dtype,
+                      int32_t pred, const ImgPlan& p, uint64_t* out, hipStream_t st) {
+  if (dtype == TW_F64) {
+    if (pred == TW_PRED_HALF)
+      return launch_rng_img_t<double, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+    return launch_rng_img_t<double, TW_PRED_GT>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+  }
+  if (pred == TW_PRED_HALF)
+    return launch_rng_img_t<long long, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+  return launch_rng_img_t<long long, TW_PRED_GT>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+}
+
+}  // namespace tw
+
+extern "C" int tw_count_img_set_plan(int32_t parts, int32_t u) {
+  // u: 1, 2 or 4 index vectors per stream and batch; + 8: nontemporal index loads
+  TW_ARG_CHECK(parts >= 0 && parts <= 4096 && ((u & 7) == 1 || (u & 7) == 2 || (u & 7) == 4) &&
+                   u < 16,
+               "tw_count_img_set_plan: parts 0..4096, u in {1, 2, 4} (+ 8: nontemporal)");
+  tw::g_img_parts = parts;
+  tw::g_img_u = u & 7;
+  tw::g_img_nt = u >> 3;
+  return TW_OK;
+}

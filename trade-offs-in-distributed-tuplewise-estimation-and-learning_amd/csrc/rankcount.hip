@@ -17,6 +17,7 @@
 //   (log2(C) + 1 dependent ds_read_b64 per x, branchless); u32 -> u64 -> block sum -> one
 //   atomic per block.  Padding keys (max) are never < a non-NaN x key.
 #include "sortkeys.h"
+#include "imagecount.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -801,9 +802,10 @@ __global__ __launch_bounds__(kRngThreads, 8) void k_count_idx_ranked(
   }
 }
 
-// tw_count_rng_set_codes: 0 = sort + binary search, 1 = equal-depth buckets (default),
-// 2 = coarse (value-range) buckets only
-static int g_rng_codes_by_bucket = 1;
+// tw_count_rng_set_codes: 3 = float32 score images in LDS, no codes (default; falls back to
+// the codes when a shard pair's images do not fit); codes by 0 = sort + binary search,
+// 1 = equal-depth buckets, 2 = value-range buckets
+static int g_rng_codes_by_bucket = 3;
 
 struct RngRankPlan {
   bool ok;
@@ -1039,6 +1041,17 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
                                      void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && B >= 0 && max_nx >= 0 && max_nz >= 0,
                "tw_count_pairs_rng_ws: bad sizes");
+  if (g_rng_codes_by_bucket == 3 && B > 0 && (dtype == TW_F64 || dtype == TW_I64)) {
+    // float32 images in LDS (csrc/imagecount.hip): no codes, no workspace
+    const int32_t pr = (pred == TW_PRED_SUBGT && dtype == TW_F64) ? TW_PRED_GT : pred;
+    const ImgPlan ip = plan_images(n_shards, max_nx, max_nz, pr, (B + 1) / 2);
+    if (ip.ok) {
+      hipStream_t st = (hipStream_t)stream;
+      TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+      return launch_rng_images(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, dtype,
+                               pr, ip, d_out, st);
+    }
+  }
   const RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pred, B);
   if (!p.ok || (dtype != TW_F64 && dtype != TW_I64) || B == 0 || d_work == nullptr ||
       work_bytes < p.total)  // not applicable: the plain kernel draws the same pairs
@@ -1060,7 +1073,7 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
 }
 
 extern "C" int tw_count_rng_set_codes(int32_t by_bucket) {
-  TW_ARG_CHECK(by_bucket >= 0 && by_bucket <= 2, "tw_count_rng_set_codes: 0, 1 or 2");
+  TW_ARG_CHECK(by_bucket >= 0 && by_bucket <= 3, "tw_count_rng_set_codes: 0, 1, 2 or 3");
   g_rng_codes_by_bucket = by_bucket;
   return TW_OK;
 }
@@ -1115,6 +1128,16 @@ int count_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z, const
                "tw_count_pairs_idx_ws: bad sizes");
   // SUBGT on doubles is GT ((x - z) > 0 == x > z without FTZ); on int64 it wraps: plain kernel
   const int32_t pr = (pred == TW_PRED_SUBGT && dtype == TW_F64) ? TW_PRED_GT : pred;
+  if (g_rng_codes_by_bucket == 3 && max_pairs > 0 && (dtype == TW_F64 || dtype == TW_I64)) {
+    // float32 images in LDS (csrc/imagecount.hip): no codes, no workspace
+    const ImgPlan ip = plan_images(n_shards, max_nx, max_nz, pr, max_pairs);
+    if (ip.ok) {
+      hipStream_t st = (hipStream_t)stream;
+      TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+      return launch_idx_images<I>(d_x, d_x_off, d_z, d_z_off, n_shards, d_ix, d_iz, d_pair_off,
+                                  dtype, pr, ip, d_out, st);
+    }
+  }
   // plan_rng_ranked's part count from the pair count (its B), so ~512 blocks fill the chip
   RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pr, max_pairs);
   if (g_idx_parts > 0) p.parts = g_idx_parts;
