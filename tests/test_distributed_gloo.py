@@ -207,3 +207,52 @@ def test_multirank_repartition_is_G_invariant(G, fused):
     want = [float(S1.UnN(k)) for k in keys]
     assert vals == want
     assert inc == float(S1.UnNB(B, seed=77))
+
+
+def _overflow_worker(rank, G, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(G, 600, 450)
+    S = ShardedSample(torch.from_numpy(X[rank * 600:(rank + 1) * 600].copy()),
+                      torch.from_numpy(Z[rank * 450:(rank + 1) * 450].copy()), 3,
+                      group=dist.group.WORLD, ops=OracleOpsFixed())
+    cap = 10  # far below the ~525 records of a bucket: every bucket overflows
+    S._xf = {"cap": cap, "cursor": torch.zeros((G,), dtype=torch.int64),
+             "flag": torch.zeros((1,), dtype=torch.int32),
+             "send": torch.empty((G * (cap + 1), 2), dtype=torch.int64),
+             "recv": torch.empty((G * (cap + 1), 2), dtype=torch.int64)}
+    raised = []
+    for _ in range(2):  # the flag is sticky: a later repartition raises too
+        try:
+            S.repartition(5)
+            raised.append(False)
+        except RuntimeError:
+            raised.append(True)
+    S.repartition(6, check=False)  # the pipelined estimators' form: no check here...
+    try:
+        S.values(S.global_counts(S.local_counts()))  # ...but values() refuses the arrays
+        raised.append(False)
+    except RuntimeError:
+        raised.append(True)
+    q.put((rank, raised))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exchange_overflow_raises_at_repartition():
+    """a fixed-capacity exchange that overflows must not leave X/Z silently
+    corrupt — repartition() raises on every rank (and keeps raising: the flag is sticky)."""
+    import tuplewise  # noqa: F401
+    G = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, G, port, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(G))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(got[r] == [True, True, True] for r in range(G)), got

@@ -264,7 +264,9 @@ class ShardedSample:
         return self._xf
 
     def check_exchange(self):
-        """Raise if a fixed-capacity repartition overflowed a bucket (host sync)."""
+        """Raise if a fixed-capacity repartition overflowed a bucket (host sync).  The flag is
+        sticky: records past a bucket's capacity were dropped, so the arrays stay invalid for
+        every later step of this sample (a later repartition only permutes them)."""
         if self._xf is not None and int(self._xf["flag"].item()):
             raise RuntimeError("repartition: an exchange bucket overflowed its capacity; the "
                                "arrays are invalid (use ShardedSample(..., exchange='exact'))")
@@ -290,8 +292,16 @@ class ShardedSample:
         probe hook for timing the multi-rank orchestration on one GPU)."""
         return self.G > 1 or getattr(self, "_force_multi", False)
 
-    def repartition(self, key: int):
-        """One repartition: new random shards for both samples (key = any 64-bit integer)."""
+    def repartition(self, key: int, check: bool = True):
+        """One repartition: new random shards for both samples (key = any 64-bit integer).
+        With several ranks and the fixed-capacity exchange, check=True waits for the exchange
+        and raises if a bucket overflowed, so X and Z are never read corrupt; the pipelined
+        estimators pass check=False (no host sync per step) and check once in values()."""
+        self._repartition(key)
+        if check and self._multi():
+            self.check_exchange()
+
+    def _repartition(self, key: int):
         kx, kz = (key * 2) & (2 ** 64 - 1), (key * 2 + 1) & (2 ** 64 - 1)
         if not self._multi():
             self.X, self.Z = self.ops.permute_pair(self.X, kx, self.Z, kz)
@@ -347,7 +357,7 @@ class ShardedSample:
         local = []
         if not self._multi() and fusable and hasattr(self.ops, "count_step"):
             # each launch counts step i and, on spare blocks, repartitions for step i+1
-            self.repartition(keys[0])
+            self._repartition(keys[0])
             out = t.zeros((self.N,), dtype=t.int64, device=self.X.device)
             for i in range(len(keys)):
                 last = i + 1 == len(keys)
@@ -367,7 +377,7 @@ class ShardedSample:
                     self.X, self.Z, out = Xn, Zn, out_n
         elif not self._multi():
             for i, k in enumerate(keys):
-                self.repartition(k)
+                self._repartition(k)
                 local.append(count_local(i))
         else:
             main = t.cuda.current_stream()
@@ -382,7 +392,7 @@ class ShardedSample:
                 self.X.record_stream(side)  # old arrays are read on side before being dropped
                 self.Z.record_stream(side)
                 with t.cuda.stream(side):
-                    self.repartition(k)
+                    self._repartition(k)
 
             # all-pairs counts go into one buffer zeroed up front: one count launch per step
             # on main, no per-step fill kernel between the counts
