@@ -417,6 +417,24 @@ int tw_row_pack(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo, int64
                 double* d_send, void* stream);
 int tw_row_unpack(const double* d_rec, int64_t m, int64_t d, double* d_out, void* stream);
 
+/* ---- (e) single-process multi-device communicator (RCCL over xGMI) --------------------
+ * The reference's workers are one serial in-process loop (compute_stats.py:71-91,
+ * estimation-experiment/main.py:48-68), so the drop-in API drives all of the node's GPUs
+ * from ONE process: a call's blocks are spread over the devices and their
+ * per-block integers combined by an all-gather.  RCCL is bound at run time (the copy already
+ * in the process, else the system librccl.so.1); without it tw_comm_init returns TW_ERR_HIP
+ * and the caller gathers on the host (same integers).
+ * tw_comm_init: one communicator over ndev distinct devices (ncclCommInitAll) -> *out_comm.
+ * tw_allgather_u64 / _f64: for every k, device devs[k] sends count words from d_send[k] and
+ *   receives ndev*count words (rank order) into d_recv[k], on streams[k] (hipStream_t of
+ *   device k); pointer arrays are host arrays of ndev device pointers. */
+int tw_comm_init(int32_t ndev, const int32_t* devs, int32_t* out_comm);
+int tw_comm_destroy(int32_t comm);
+int tw_allgather_u64(int32_t comm, const uint64_t* const* d_send, uint64_t* const* d_recv,
+                     int64_t count, void* const* streams);
+int tw_allgather_f64(int32_t comm, const double* const* d_send, double* const* d_recv,
+                     int64_t count, void* const* streams);
+
 /* ---- f2: bulk draws of NumPy's legacy global RNG (host code, no GPU) ------------------
  * key (624 words) / pos: the MT19937 state of np.random.get_state(), advanced in place.
  * tw_np_randint_batch: n_calls consecutive RandomState.randint(low[c], high[c], cnt[c]) calls

@@ -119,3 +119,27 @@ def test_load_preprocess_constant_column_raises(tw):
     y = np.where(np.arange(100) % 10 == 0, 1, -1)
     with pytest.raises(ValueError, match="constant var"):
         lr.load_preprocess_data({"X": X, "y": y})
+
+
+def test_multi_device_split_and_device_list(monkeypatch):
+    """tuplewise._multi (single-process multi-device drop-in path): contiguous, balanced block
+    groups; the device list from set_devices / TW_DEVICES."""
+    from tuplewise import _multi as M
+    w = [5, 1, 1, 1, 5, 1, 1, 1, 5, 1]
+    g = M.split(w, 3)
+    assert g[0][0] == 0 and g[-1][1] == len(w)
+    assert all(a[1] == b[0] for a, b in zip(g, g[1:]))
+    loads = [sum(w[a:b]) for a, b in g]
+    assert max(loads) - min(loads) <= 5
+    assert M.split([], 4) == [(0, 0)] * 4
+    assert [b - a for a, b in M.split([1, 1], 4)].count(0) == 2
+    monkeypatch.setenv("TW_DEVICES", "0,0,1")
+    assert M.devices() == [0, 0, 1]
+    M.set_devices([2, 3])
+    try:
+        assert M.devices() == [2, 3]
+        assert M.slots_for(10, 5) is None  # below MIN_WORK: one device
+        assert M.slots_for(1 << 40, 1) is None  # one block: nothing to spread
+        assert M.slots_for(1 << 40, 5) == [2, 3]
+    finally:
+        M.set_devices(None)

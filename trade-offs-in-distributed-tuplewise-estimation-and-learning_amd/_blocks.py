@@ -17,6 +17,7 @@ import numpy as np
 
 from . import _engine as E
 from . import _lib as L
+from . import _multi as M
 
 
 class Block:
@@ -87,6 +88,24 @@ def _layout(arr_dev, blocks, side: str):
     return gathered, off
 
 
+def _upload_blocks(host, blocks, side: str):
+    """The part of a host array a group of blocks reads, on the current device, + int64 offsets
+    (len(blocks)+1): one contiguous slice for consecutive slice blocks (no host copy), else the
+    blocks' selections concatenated on the host.  (Multi-device path: each slot uploads only
+    its group's data.)"""
+    parts = [getattr(b, side) for b in blocks]
+    if all(isinstance(p, tuple) for p in parts) and all(
+            a[1] == b[0] for a, b in zip(parts, parts[1:])):
+        lo, hi = parts[0][0], parts[-1][1]
+        off = np.array([p[0] - lo for p in parts] + [hi - lo], dtype=np.int64)
+        return L.to_device(np.ascontiguousarray(host[lo:hi])), off
+    pieces = [host[p[0]:p[1]] if isinstance(p, tuple) else host[np.asarray(p, dtype=np.int64)]
+              for p in parts]
+    off = np.concatenate([[0], np.cumsum([len(q) for q in pieces])]).astype(np.int64)
+    cat = np.concatenate(pieces) if pieces else host[:0]
+    return L.to_device(np.ascontiguousarray(cat)), off
+
+
 class BlockSpec:
     """Descriptor of a package block function (see module docstring)."""
 
@@ -123,10 +142,26 @@ class CompleteCount(BlockSpec):
     def evaluate(self, X, Z, blocks):
         x, z, code, mode = self.operands(_flat(X), _flat(Z))
         blocks = _elements(_elements(blocks, "x", _row_size(X)), "z", _row_size(Z))
-        xd, zd = L.to_device(x), L.to_device(z)
-        xa, xo = _layout(xd, blocks, "x")
-        za, zo = _layout(zd, blocks, "z")
-        counts = E.count_complete(E.Shards(xa, xo, za, zo, code), mode)
+        work = sum(b.nx() * b.nz() for b in blocks)
+        if mode != "ne" and M.slots_for(work, len(blocks)):
+            pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}[mode]
+
+            def enqueue(sub):  # this slot's blocks: upload their data, count (in flight)
+                xa, xo = _upload_blocks(x, sub, "x")
+                za, zo = _upload_blocks(z, sub, "z")
+                sh = E.Shards(xa, xo, za, zo, code)
+                xod, zod = sh.offsets_dev()
+                mx, mz = int(sh.nx.max()), int(sh.nz.max())
+                return E.count_launch(xa, xod, za, zod, len(sub), mx, mz, code, pred,
+                                      E.pick_algo("auto", mx, mz, mode))
+
+            counts = M.gather(M.spread(blocks, lambda b: b.nx() * b.nz(), enqueue))
+            counts = counts.astype(np.int64).view(np.uint64)
+        else:
+            xd, zd = L.to_device(x), L.to_device(z)
+            xa, xo = _layout(xd, blocks, "x")
+            za, zo = _layout(zd, blocks, "z")
+            counts = E.count_complete(E.Shards(xa, xo, za, zo, code), mode)
         out = []
         for b, c in zip(blocks, counts):
             pairs = b.nx() * b.nz()
@@ -146,10 +181,20 @@ class CompleteSum(BlockSpec):
         x = _flat(X).astype(np.float64, copy=False)
         z = _flat(Z).astype(np.float64, copy=False)
         blocks = _elements(_elements(blocks, "x", _row_size(X)), "z", _row_size(Z))
-        xd, zd = L.to_device(x), L.to_device(z)
-        xa, xo = _layout(xd, blocks, "x")
-        za, zo = _layout(zd, blocks, "z")
-        sums = E.pair_sum_complete(E.Shards(xa, xo, za, zo, L.TW_F64), self.kern, self.margin)
+        if M.slots_for(sum(b.nx() * b.nz() for b in blocks), len(blocks)):
+            def enqueue(sub):
+                xa, xo = _upload_blocks(x, sub, "x")
+                za, zo = _upload_blocks(z, sub, "z")
+                return E.pair_sum_complete_dev(E.Shards(xa, xo, za, zo, L.TW_F64), self.kern,
+                                               self.margin)
+
+            sums = M.gather(M.spread(blocks, lambda b: b.nx() * b.nz(), enqueue))
+        else:
+            xd, zd = L.to_device(x), L.to_device(z)
+            xa, xo = _layout(xd, blocks, "x")
+            za, zo = _layout(zd, blocks, "z")
+            sums = E.pair_sum_complete(E.Shards(xa, xo, za, zo, L.TW_F64), self.kern,
+                                       self.margin)
         # NumPy returns the mean in the operands' float type (float32 stays float32); the
         # device accumulates in float64, so float32 results are the better-rounded value.
         rt = np.result_type(np.asarray(X).dtype, np.asarray(Z).dtype)
@@ -201,6 +246,30 @@ def block_indexed_values(x: np.ndarray, z: np.ndarray, blocks: list, ix_loc: lis
     else:
         xx, zz, code, mode = (x.astype(np.float64, copy=False), z.astype(np.float64, copy=False),
                               L.TW_F64, None)
+    npairs = np.diff(offs)
+    if mode != "ne" and M.slots_for(int(offs[-1]) * 8, len(blocks)):
+        pos = {id(b): i for i, b in enumerate(blocks)}
+
+        def enqueue(sub):  # this slot's blocks, their draws shifted into the uploaded spans
+            i0 = pos[id(sub[0])]
+            xa, xo = _upload_blocks(xx, sub, "x")
+            za, zo = _upload_blocks(zz, sub, "z")
+            ixs = np.concatenate([ix_loc[i0 + k] + xo[k] for k in range(len(sub))])
+            izs = np.concatenate([iz_loc[i0 + k] + zo[k] for k in range(len(sub))])
+            po = offs[i0:i0 + len(sub) + 1] - offs[i0]
+            if kernel == "AUC":
+                pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF,
+                        "subgt": L.TW_PRED_SUBGT}[mode]
+                return E.count_indexed_ranked_dev(xa, L.to_device(xo), za, L.to_device(zo),
+                                                  int(np.diff(xo).max()), int(np.diff(zo).max()),
+                                                  code, ixs, izs, po, pred)
+            kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI}[kernel]
+            return E.pair_sum_indexed_dev(xa, za, ixs, izs, po, kern)
+
+        vals = M.gather(M.spread(blocks, lambda b: npairs[pos[id(b)]], enqueue))
+        if kernel == "AUC":
+            return [E.ratio(c, p) for c, p in zip(vals.astype(np.int64).view(np.uint64), npairs)]
+        return [np.float64(v / np.float64(p)) for v, p in zip(vals, npairs)]
     xa, xo = _layout(L.to_device(xx), blocks, "x")
     za, zo = _layout(L.to_device(zz), blocks, "z")
     ix = np.concatenate([a + o for a, o in zip(ix_loc, xo[:-1])]) if ix_loc else np.zeros(0, np.int64)

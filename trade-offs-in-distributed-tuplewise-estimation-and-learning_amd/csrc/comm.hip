@@ -1,0 +1,136 @@
+// comm.hip — single-process multi-device communicator (SURVEY.md §5 "Distributed comm
+// backend": one process driving the node's GPUs, ncclCommInitAll; §8(b) tw_comm_init /
+// tw_allgather_u64).
+//
+// The reference's N workers are a serial in-process loop (learning-experiment/compute_stats.py:
+// 71-91, estimation-experiment/main.py:48-68), so its drop-in API runs in ONE process; the
+// package spreads a call's blocks over the visible devices and combines their per-block
+// integers here: an all-gather over RCCL (xGMI peer links), after which one device holds every
+// block's count and the host copies them back once.
+//
+// RCCL is bound at run time (dlopen): the copy the host process already has loaded (PyTorch
+// ships one) is preferred, so the process never holds two RCCL runtimes; otherwise the
+// system's librccl.so.1 is loaded.  A process without RCCL gets TW_ERR_HIP from tw_comm_init
+// and the Python layer gathers on the host instead — the same integers either way.
+#include "tw_common.h"
+#include <dlfcn.h>
+#include <mutex>
+#include <vector>
+
+namespace tw {
+
+typedef struct ncclComm* ncclComm_t;
+typedef int ncclResult_t;  // 0 = ncclSuccess
+constexpr int kNcclUint64 = 5;
+constexpr int kNcclFloat64 = 8;
+
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*initAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*allGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*groupStart)() = nullptr;
+  ncclResult_t (*groupEnd)() = nullptr;
+  const char* (*errStr)(ncclResult_t) = nullptr;
+};
+
+static Rccl g_rccl;
+static std::mutex g_mu;
+static std::vector<std::vector<ncclComm_t>> g_comms;  // handle -> one comm per device
+
+static bool load_rccl() {
+  if (g_rccl.h) return true;
+  // an RCCL already in the process first (by soname or by the name PyTorch linked), then the
+  // system one
+  const char* names[] = {"librccl.so.1", "librccl.so"};
+  void* h = nullptr;
+  for (const char* n : names)
+    if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD)) != nullptr) break;
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return false;
+  Rccl r;
+  r.h = h;
+  r.initAll = (decltype(r.initAll))dlsym(h, "ncclCommInitAll");
+  r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+  r.allGather = (decltype(r.allGather))dlsym(h, "ncclAllGather");
+  r.groupStart = (decltype(r.groupStart))dlsym(h, "ncclGroupStart");
+  r.groupEnd = (decltype(r.groupEnd))dlsym(h, "ncclGroupEnd");
+  r.errStr = (decltype(r.errStr))dlsym(h, "ncclGetErrorString");
+  if (!r.initAll || !r.destroy || !r.allGather || !r.groupStart || !r.groupEnd) return false;
+  g_rccl = r;
+  return true;
+}
+
+static const char* nccl_err(ncclResult_t e) {
+  return g_rccl.errStr ? g_rccl.errStr(e) : "RCCL error";
+}
+
+static int allgather(int32_t comm, const void* const* send, void* const* recv, int64_t count,
+                     int dtype, void* const* streams) {
+  std::vector<ncclComm_t> cs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    TW_ARG_CHECK(comm >= 0 && comm < (int32_t)g_comms.size() && !g_comms[comm].empty(),
+                 "tw_allgather: unknown communicator %d", comm);
+    cs = g_comms[comm];
+  }
+  TW_ARG_CHECK(count >= 0 && send && recv && streams, "tw_allgather: bad arguments");
+  if (count == 0) return TW_OK;
+  ncclResult_t e = g_rccl.groupStart();
+  for (size_t k = 0; k < cs.size() && e == 0; ++k)
+    e = g_rccl.allGather(send[k], recv[k], (size_t)count, dtype, cs[k], (hipStream_t)streams[k]);
+  const ncclResult_t e2 = g_rccl.groupEnd();
+  if (e == 0) e = e2;
+  if (e != 0) {
+    set_error("tw_allgather: %s", nccl_err(e));
+    return TW_ERR_HIP;
+  }
+  return TW_OK;
+}
+
+}  // namespace tw
+
+using namespace tw;
+
+extern "C" int tw_comm_init(int32_t ndev, const int32_t* devs, int32_t* out_comm) {
+  TW_ARG_CHECK(ndev >= 1 && ndev <= 64 && devs && out_comm, "tw_comm_init: 1..64 devices");
+  for (int i = 0; i < ndev; ++i)
+    for (int j = 0; j < i; ++j)
+      TW_ARG_CHECK(devs[i] != devs[j], "tw_comm_init: device %d listed twice", devs[i]);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!load_rccl()) {
+    set_error("tw_comm_init: RCCL (librccl.so.1) is not available");
+    return TW_ERR_HIP;
+  }
+  std::vector<int> dl(devs, devs + ndev);
+  std::vector<ncclComm_t> cs(ndev);
+  const ncclResult_t e = g_rccl.initAll(cs.data(), ndev, dl.data());
+  if (e != 0) {
+    set_error("tw_comm_init: ncclCommInitAll: %s", nccl_err(e));
+    return TW_ERR_HIP;
+  }
+  g_comms.push_back(cs);
+  *out_comm = (int32_t)g_comms.size() - 1;
+  return TW_OK;
+}
+
+extern "C" int tw_comm_destroy(int32_t comm) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TW_ARG_CHECK(comm >= 0 && comm < (int32_t)g_comms.size() && !g_comms[comm].empty(),
+               "tw_comm_destroy: unknown communicator %d", comm);
+  for (ncclComm_t c : g_comms[comm]) g_rccl.destroy(c);
+  g_comms[comm].clear();
+  return TW_OK;
+}
+
+extern "C" int tw_allgather_u64(int32_t comm, const uint64_t* const* d_send,
+                                uint64_t* const* d_recv, int64_t count, void* const* streams) {
+  return allgather(comm, (const void* const*)d_send, (void* const*)d_recv, count, kNcclUint64,
+                   streams);
+}
+
+extern "C" int tw_allgather_f64(int32_t comm, const double* const* d_send, double* const* d_recv,
+                                int64_t count, void* const* streams) {
+  return allgather(comm, (const void* const*)d_send, (void* const*)d_recv, count, kNcclFloat64,
+                   streams);
+}
