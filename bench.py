@@ -297,7 +297,17 @@ def sgd_replay_steps_per_s(steps):
     lr.learning_process(X, Z, p)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # hinge-filter sign audit, untimed: the device's S against NumPy/BLAS's on
+    # every pair of 300 replay steps of the same run
+    audit = []
+    np.random.seed(0)
+    lr.learning_process(X, Z, dict(p, n_it=300), sign_audit=audit)
     return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+            "sign_audit": {"steps": len(audit), "pairs": sum(a["pairs"] for a in audit),
+                           "near_zero_S": sum(a["near_zero"] for a in audit),
+                           "filter_flips": sum(a["flips"] for a in audit),
+                           "note": "pairs whose |S| is within the dot product's rounding bound, "
+                                   "and pairs whose hinge filter differs from NumPy's"},
             "config": {"n_X": 9117, "n_Z": 702, "d": 10, "N": 100, "B": 100,
                        "reshuffle_mod": 25, "rng": "replay (NumPy legacy MT19937, bit-exact)",
                        "steps": steps}}

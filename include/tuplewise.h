@@ -251,6 +251,17 @@ int tw_pair_grad(const double* d_X, const double* d_Z, int64_t d, const int64_t*
                  const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
                  double margin, int32_t loss, double* d_out, void* stream);
 
+/* Sign audit (SURVEY.md §7 "count and report" the hinge-filter flips): tw_pair_grad plus
+ * d_scores[s*B + b] = S_b = diff_b . w + margin exactly as the kernel computed it (the generic
+ * kernel; its narrow and wide paths sum the dot product in the orders of the streaming and fused
+ * kernels).  The reference decides the filter on BLAS's S (compute_stats.py:158-159); the
+ * caller compares the signs (tuplewise.learning.learning_process(..., sign_audit=[])). */
+int tw_pair_grad_audit(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                       int64_t kx, const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix,
+                       const int64_t* d_iz, int32_t n_shards, int64_t B, const double* d_w,
+                       double margin, int32_t loss, double* d_out, double* d_scores,
+                       void* stream);
+
 /* ---- Complete-block gradient (extension; BASELINE.json north_star item (2)) -------------
  * The same surrogate's gradient over ALL kx*kz pairs of each shard, computed as per-point
  * pair-coefficient reductions followed by X^T c (csrc/complete_grad.hip):

@@ -182,6 +182,21 @@ def main():
                      if isinstance(v, (int, float)) and not isinstance(v, bool)}
     meta["learn"]["seed"] = 2024
 
+    # ------------------------------------------- 5b. learning with SAME_AS_BATCH monitoring
+    # evaluation_step's other branch (make_exps.py:154-160): the block statistics on the
+    # current shards instead of the fixed monitor pairs; the module constant switched for this
+    # run only
+    me.TYPE_TRAIN_MONITOR = "SAME_AS_BATCH"
+    p_sab = {k: v for k, v in p_learn.items()
+             if k not in ("iter", "norm_w", "bc_AUC", "br_AUC", "tr_AUC", "tc_AUC")}
+    p_sab["n_it"] = 120
+    np.random.seed(2025)
+    me.learning_process(lx, lz, p_sab)
+    me.TYPE_TRAIN_MONITOR = "FIXED_PAIRS"
+    for k in ("iter", "norm_w", "bc_AUC", "br_AUC", "tr_AUC", "tc_AUC"):
+        put(f"learn_sab/{k}", np.array(p_sab[k]))
+    meta["learn_sab"] = {"seed": 2025, "n_it": 120, "TYPE_TRAIN_MONITOR": "SAME_AS_BATCH"}
+
     # ---------------------------------------------------------------- 7. data preprocessing
     # load_preprocess_data (make_exps.py:51-93) on a synthetic shuttle-like pickle written to
     # a temp dir (the real dataset is a download, absent offline).  Written by us, read by the

@@ -42,6 +42,29 @@ def test_trajectory_matches_reference(gpu, golden):
         np.testing.assert_allclose(p[k], golden[f"learn/{k}"], rtol=0, atol=1e-12)
 
 
+def test_trajectory_sign_audit(gpu, golden):
+    """count and report the hinge-filter decisions that could differ from the
+    reference's BLAS order.  The 300-step golden run with the audit on: the same trajectory,
+    zero filter flips, and the near-zero count reported (it bounds how many could flip)."""
+    import tuplewise.learning as lr
+    p = _p_learn(golden)
+    audit = []
+    logging.disable(logging.CRITICAL)
+    np.random.seed(2024)
+    traj = []
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p, trajectory=traj,
+                        sign_audit=audit)
+    ref = golden["learn/ws"]
+    assert np.abs(np.stack(traj) - ref).max() / np.abs(ref).max() < 1e-10
+    assert len(audit) == ref.shape[0]
+    pairs = sum(a["pairs"] for a in audit)
+    near = sum(a["near_zero"] for a in audit)
+    flips = sum(a["flips"] for a in audit)
+    print(f"sign audit: {pairs} pairs, {near} with |S| within the rounding bound, {flips} flips")
+    assert flips == 0 and flips <= near
+    assert pairs == ref.shape[0] * p["N"] * p["B"]
+
+
 def test_sgd_optimizer_and_assert(gpu, golden):
     import tuplewise.learning as lr
     from oracle import oracle as O
@@ -315,3 +338,49 @@ def test_fused_sgd_step_equals_grad_plus_update(gpu, golden, loss, optim):
             got = run(True, mode, graphs)
             assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), \
                 (mode, graphs)
+
+
+def test_same_as_batch_monitor_matches_reference(gpu, golden, monkeypatch):
+    """evaluation_step's SAME_AS_BATCH branch (make_exps.py:154-160) on the device, against the
+    reference's own run with TYPE_TRAIN_MONITOR = "SAME_AS_BATCH" (tests/golden/make_golden.py
+    section 5b): bc/br on the current shards, tr/tc on the test set."""
+    import tuplewise.learning as lr
+    monkeypatch.setattr(lr, "TYPE_TRAIN_MONITOR", "SAME_AS_BATCH")
+    p = _p_learn(golden)
+    p["n_it"] = 120
+    logging.disable(logging.CRITICAL)
+    np.random.seed(2025)
+    lr.learning_process(golden["learn/X"], golden["learn/Z"], p)
+    for k in ("iter", "norm_w"):
+        np.testing.assert_allclose(p[k], golden[f"learn_sab/{k}"], rtol=1e-10)
+    for k in ("bc_AUC", "tc_AUC"):
+        np.testing.assert_allclose(p[k], golden[f"learn_sab/{k}"], rtol=1e-9)
+    for k in ("br_AUC", "tr_AUC"):
+        np.testing.assert_allclose(p[k], golden[f"learn_sab/{k}"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("layout", ["replicated", "partitioned"])
+def test_same_as_batch_device_rng_equals_host_formula(gpu, golden, monkeypatch, layout):
+    """Device-RNG mode: the device SAME_AS_BATCH statistics equal the reference formula
+    (UN_split of conv_AUC / Un over X_s.dot(w)) evaluated on the same shards and w."""
+    import torch
+    import tuplewise.compute_stats as cs
+    import tuplewise.learning as lr
+    from oracle import oracle as O
+    X, Z = golden["learn/X"], golden["learn/Z"]
+    w = golden["learn/w0"]
+    eng = lr.SGDEngine(X, Z, w, 10, 20, 1, 0.05, 0.01, "momentum", x_layout=layout)
+    eng.enable_device_rng(321)
+    eng.reshuffle_device()
+    torch.cuda.synchronize()
+    bc, br = lr._same_as_batch_device(eng.batch_view(), eng.w, 1, "hinge")
+    if layout == "partitioned":
+        rx, rz = eng.rows_all_x.cpu().numpy(), eng.rows_all_z.cpu().numpy()
+    else:
+        rx, rz = eng.rows_x.cpu().numpy(), eng.rows_z.cpu().numpy()
+    sc_X = [X[r].dot(w) for r in rx]
+    sc_Z = [Z[r].dot(w) for r in rz]
+    want_bc = O.UN_split(sc_X, sc_Z, O.conv_AUC(1))
+    want_br = O.UN_split(sc_X, sc_Z, lambda x, z: O.cs_Un(x, z, kernel="AUC"))
+    assert np.isclose(bc, want_bc, rtol=1e-12) and abs(br - want_br) < 1e-12
+    assert 0.0 <= br <= 1.0 and cs.Un is not None

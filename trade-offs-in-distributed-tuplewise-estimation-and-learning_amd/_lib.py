@@ -62,6 +62,8 @@ _SIGNATURES = {
                       _vp, _vp],
     "tw_pair_grad": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64, _i32,
                      _vp, _vp],
+    "tw_pair_grad_audit": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _f64,
+                           _i32, _vp, _vp, _vp],
     "tw_pair_grad_complete_work_bytes": [_i32, _i64, _i64, _i64],
     "tw_pair_grad_complete_set_search": [_i32],
     "tw_pair_grad_complete": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _f64, _i32, _vp,

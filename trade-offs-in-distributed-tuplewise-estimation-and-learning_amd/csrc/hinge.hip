@@ -42,7 +42,10 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     int CH, const double* __restrict__ w, double margin, double* __restrict__ out,
-    uint64_t seed, const uint64_t* __restrict__ d_step, uint32_t shard_base) {
+    uint64_t seed, const uint64_t* __restrict__ d_step, uint32_t shard_base,
+    double* __restrict__ s_out = nullptr) {
+  // s_out (tw_pair_grad_audit): S_b = diff_b . w + margin of every pair, as this kernel
+  // computed it, at s_out[s * B + b] — the value whose sign is the hinge filter
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* diff = (double*)smem;                             // CH * d
   int64_t* rx = (int64_t*)(smem + sizeof(double) * CH * d);  // CH
@@ -85,6 +88,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
           part += v * w[j];
         }
         flag[t] = pair_weight<LOSS>(part + margin);
+        if (s_out) s_out[p] = part + margin;
       } else {
         rx[t] = rxt;
         rz[t] = rzt;
@@ -120,6 +124,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
       }
       part = wave_sum_f64(part);
       if (lane == 0) flag[t] = pair_weight<LOSS>(part + margin);
+      if (lane == 0 && s_out) s_out[(int64_t)s * B + b0 + t] = part + margin;
     }
     __syncthreads();
     // column sums over the filtered rows, in row order
@@ -602,14 +607,27 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
                         int64_t kx, const int64_t* rows_z, int64_t kz, const int64_t* ix,
                         const int64_t* iz, int32_t n_shards, int64_t B, const double* w,
                         double margin, uint64_t seed, const uint64_t* d_step,
-                        uint32_t shard_base, double* out, hipStream_t st) {
+                        uint32_t shard_base, double* out, hipStream_t st,
+                        double* s_out = nullptr) {
   // per staged pair: d diff doubles + two row indices + one weight, <= 64 KiB in all
   const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / (d + 3)));
   const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(double) * CH;
+  if (s_out) {  // audit: the generic kernel (its narrow and wide paths compute S in the same
+                // orders as the streaming / fused kernels) with the scores written out
+    if (d <= 32)
+      hipLaunchKernelGGL((k_hinge_grad<kBlock, LOSS>), dim3(n_shards), dim3(kBlock), lds, st, X,
+                         Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed,
+                         d_step, shard_base, s_out);
+    else
+      hipLaunchKernelGGL((k_hinge_grad<kWideBlock, LOSS>), dim3(n_shards), dim3(kWideBlock), lds,
+                         st, X, Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out,
+                         seed, d_step, shard_base, s_out);
+    return;
+  }
   if (d <= 32)
     hipLaunchKernelGGL((k_hinge_grad<kBlock, LOSS>), dim3(n_shards), dim3(kBlock), lds, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
-                       shard_base);
+                       shard_base, nullptr);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 0)
     hipLaunchKernelGGL(k_hinge_grad_stream<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
@@ -621,20 +639,20 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
   else
     hipLaunchKernelGGL((k_hinge_grad<kWideBlock, LOSS>), dim3(n_shards), dim3(kWideBlock), lds, st,
                        X, Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed,
-                       d_step, shard_base);
+                       d_step, shard_base, nullptr);
 }
 
 int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* rows_x, int64_t kx,
                  const int64_t* rows_z, int64_t kz, const int64_t* ix, const int64_t* iz,
                  int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
                  const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st,
-                 int32_t loss = TW_LOSS_HINGE) {
+                 int32_t loss = TW_LOSS_HINGE, double* s_out = nullptr) {
   if (loss == TW_LOSS_LOGISTIC)
     launch_grad_kernel<TW_LOSS_LOGISTIC>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                         margin, seed, d_step, shard_base, out, st);
+                                         margin, seed, d_step, shard_base, out, st, s_out);
   else
     launch_grad_kernel<TW_LOSS_HINGE>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                      margin, seed, d_step, shard_base, out, st);
+                                      margin, seed, d_step, shard_base, out, st, s_out);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -661,6 +679,21 @@ extern "C" int tw_pair_grad(const double* d_X, const double* d_Z, int64_t d,
   TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_hinge_grad: pair indices required");
   return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
                       margin, 0, nullptr, 0, d_out, st, loss);
+}
+
+extern "C" int tw_pair_grad_audit(const double* d_X, const double* d_Z, int64_t d,
+                                  const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                                  int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                                  int32_t n_shards, int64_t B, const double* d_w, double margin,
+                                  int32_t loss, double* d_out, double* d_scores, void* stream) {
+  TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_pair_grad_audit: d=%lld outside [1, %d]", (long long)d,
+               kMaxD);
+  TW_ARG_CHECK(n_shards >= 0 && B >= 1 && d_scores != nullptr, "tw_pair_grad_audit: bad args");
+  TW_ARG_CHECK(d_ix != nullptr && d_iz != nullptr, "tw_pair_grad_audit: pair indices required");
+  if (int rc = check_loss(loss)) return rc;
+  if (n_shards == 0) return TW_OK;
+  return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, n_shards, B, d_w,
+                      margin, 0, nullptr, 0, d_out, (hipStream_t)stream, loss, d_scores);
 }
 
 extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,

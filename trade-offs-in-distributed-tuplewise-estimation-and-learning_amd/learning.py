@@ -229,15 +229,23 @@ class SGDEngine:
                L.ptr(self.grads_loc), L.stream_handle())
         self._update()
 
-    def step(self, ix, iz):
+    def step(self, ix, iz, scores=None):
         """Replay mode: ix, iz are the (N, B) NumPy draws of every shard (host arrays or
-        device tensors)."""
+        device tensors).  scores: an (N_loc, B) float64 device tensor that receives every
+        pair's S = diff . w + margin as the kernel computed it (tw_pair_grad_audit)."""
         t = self.t
         ixd = self._local(ix) if isinstance(ix, t.Tensor) else L.to_device(self._local(ix))
         izd = self._local(iz) if isinstance(iz, t.Tensor) else L.to_device(self._local(iz))
-        L.call("tw_pair_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x), self.kx,
-               L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N_loc, self.B,
-               L.ptr(self.w), self.margin, self.loss, L.ptr(self.grads_loc), L.stream_handle())
+        if scores is not None:
+            L.call("tw_pair_grad_audit", L.ptr(self.X), L.ptr(self.Z), self.d,
+                   L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ixd),
+                   L.ptr(izd), self.N_loc, self.B, L.ptr(self.w), self.margin, self.loss,
+                   L.ptr(self.grads_loc), L.ptr(scores), L.stream_handle())
+        else:
+            L.call("tw_pair_grad", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
+                   self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ixd), L.ptr(izd), self.N_loc,
+                   self.B, L.ptr(self.w), self.margin, self.loss, L.ptr(self.grads_loc),
+                   L.stream_handle())
         self._update()
 
     def run_replay_segment(self, draws_dev, nsteps: int, graphs: bool = True, tag=0):
@@ -279,6 +287,15 @@ class SGDEngine:
                 steps()
             self._replay_graphs[key] = g
         g.replay()
+
+    def batch_view(self):
+        """The current shards as evaluation_step's SAME_AS_BATCH reads them: (X, Z, row tables
+        or None, N, kx, kz) on the device (one process only; None with several ranks)."""
+        if self.G > 1 or self.rows_x is None:
+            return None
+        if self.layout == "partitioned":  # X / Z hold the shards' rows in draw order
+            return (self.X, self.Z, None, None, self.N, self.kx, self.kz)
+        return (self.X, self.Z, self.rows_x, self.rows_z, self.N, self.kx, self.kz)
 
     def w_host(self) -> np.ndarray:
         return self.w.cpu().numpy().reshape(self.w_shape)
@@ -447,6 +464,7 @@ class _ReplayDraws:
             self.done[k].synchronize()
         h = self.hnp[k]
         self.rng.pairs(self.N, self.kx, self.kz, self.B, h[0], h[1])
+        self.last = h  # the host draws of this step (valid until the buffer's reuse)
         # stream-ordered: dev[k]'s previous reader (two steps back) precedes this copy
         self.dev[k].copy_(self.host[k], non_blocking=True)
         if self.done[k] is None:
@@ -455,9 +473,28 @@ class _ReplayDraws:
         return self.dev[k][0], self.dev[k][1]
 
 
+def sign_audit_step(X, Z, rows_x, rows_z, ix, iz, w, margin, scores) -> dict:
+    """One replay step's hinge-filter audit: the reference filters on
+    S = diff.dot(w) + margin with BLAS's summation order (compute_stats.py:157-159), the device
+    on its own order.  near_zero: pairs whose |S| is within the dot product's rounding bound
+    d * eps * (sum |diff_j w_j| + |margin|), where the two orders may disagree; flips: pairs
+    whose filter actually differs."""
+    near = flips = 0
+    w = np.asarray(w, dtype=np.float64).reshape(-1, 1)
+    d = w.shape[0]
+    for s in range(len(rows_x)):
+        diff = Z[rows_z[s][iz[s]]] - X[rows_x[s][ix[s]]]
+        S = (diff.dot(w) + margin).ravel()
+        bound = d * np.finfo(np.float64).eps * (np.abs(diff * w.ravel()).sum(axis=1)
+                                                + abs(margin))
+        near += int(np.sum(np.abs(S) <= bound))
+        flips += int(np.sum((S > 0) != (scores[s] > 0)))
+    return {"pairs": int(len(rows_x) * ix.shape[1]), "near_zero": near, "flips": flips}
+
+
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                      rng_mode="replay", graphs=True, group=None, x_layout="replicated",
-                     loss="hinge", gradient="incomplete"):
+                     loss="hinge", gradient="incomplete", sign_audit=None):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference; the
@@ -474,7 +511,10 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     loss: "hinge" (the reference) or "logistic" (SURVEY.md §8 row L3 extension: pairwise
     logistic loss softplus(diff . w + margin); evaluation reports its surrogate too).
     gradient: "incomplete" (the reference: B sampled pairs per shard) or "complete" (extension:
-    all pairs of every shard via per-point pair coefficients + X^T c; draws no pairs)."""
+    all pairs of every shard via per-point pair coefficients + X^T c; draws no pairs).
+    sign_audit: a list (replay mode, one process, replicated X) that receives, per step,
+    sign_audit_step's counts of near-zero scores and of hinge-filter disagreements between the
+    device's S and NumPy/BLAS's S; the steps then run one at a time."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -501,6 +541,15 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     if rng_mode != "replay":
         raise ValueError(f"rng_mode must be 'replay' or 'device', not {rng_mode!r}")
     draws = _ReplayDraws(N, eng.kx, eng.kz, B)
+    audit_scores = None
+    if sign_audit is not None:
+        if eng.complete or eng.G > 1 or eng.layout != "replicated":
+            raise ValueError("sign_audit needs the incomplete gradient on one process with "
+                             "replicated X")
+        audit_scores = L.empty((eng.N_loc, B), eng.t.float64)
+        if trajectory is None:
+            trajectory = []  # the audit runs the steps one at a time
+        Xh, Zh = np.asarray(X, dtype=np.float64), np.asarray(Z, dtype=np.float64)
     with draws.rng:  # the global RNG state lives natively until the loop ends
         rows_x, rows_z = draws.swr_rows(n_X, n_Z)  # the reference's redundant draw (:119)
         eng.set_shards(rows_x, rows_z)
@@ -519,7 +568,13 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                     eng.step_complete()
                 else:
                     ix, iz = draws.pairs()
-                    eng.step(ix, iz)
+                    eng.step(ix, iz, scores=audit_scores)
+                    if audit_scores is not None:
+                        hx, hz = draws.last[0].copy(), draws.last[1].copy()
+                        rec = sign_audit_step(Xh, Zh, rows_x, rows_z, hx, hz, trajectory[-1],
+                                              margin, audit_scores.cpu().numpy())
+                        rec["step"] = i
+                        sign_audit.append(rec)
                 i += 1
                 continue
             # The steps up to the next reshuffle / evaluation draw nothing else from the RNG
@@ -539,12 +594,14 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
 
 def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs):
     """evaluation_step at step i of the replay loop (make_exps.py:127-128)."""
+    X_s = Z_s = batch = None  # FIXED_PAIRS evaluation does not read the shards
     if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
-        X_s = [X[r] for r in rows_x]
-        Z_s = [Z[r] for r in rows_z]
-    else:
-        X_s = Z_s = None  # FIXED_PAIRS evaluation does not read the shards
-    evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss, _w_dev=eng.w, _graph=graphs)
+        batch = eng.batch_view()
+        if batch is None:  # several ranks: the host formula on the global shards
+            X_s = [X[r] for r in rows_x]
+            Z_s = [Z[r] for r in rows_z]
+    evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss, _w_dev=eng.w, _graph=graphs,
+                    _batch=batch)
 
 
 def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
@@ -554,18 +611,26 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
         graphs = False
     i = 0
     while i < n_it:
+        resh = i % mod == 0
         if i % eval_mod == 0:
+            batch = None
+            if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
+                # the reference reshuffles before it evaluates (make_exps.py:123-128)
+                if resh:
+                    eng.reshuffle_device()
+                    resh = False
+                batch = eng.batch_view()
             evaluation_step(i, None, None, eng.w_host(), p_learn, loss=loss, _w_dev=eng.w,
-                            _graph=graphs)
+                            _graph=graphs, _batch=batch)
         if trajectory is not None:  # one step at a time, recording w
-            if i % mod == 0:
+            if resh:
                 eng.reshuffle_device()
             trajectory.append(eng.w_host())
             eng.step_device()
             i += 1
             continue
         nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod)
-        eng.run_segment(nxt - i, i % mod == 0, graphs)
+        eng.run_segment(nxt - i, resh, graphs)
         i = nxt
     return None
 
@@ -670,7 +735,43 @@ def _eval_device(wd, p_learn, loss, margin, fixed):
     return t.cat([v.reshape(-1) for v in parts]), n_pairs, n * m
 
 
-def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _graph=True):
+def _same_as_batch_device(batch, wd, margin, loss):
+    """evaluation_step's SAME_AS_BATCH statistics (make_exps.py:154-160) on the device: the
+    scores of the current shards (one GEMV per sample over the resident rows, gathered through
+    the shard row tables), every shard's complete surrogate sum and AUC count in one launch
+    each, and the reference's UN_split averages (np.mean over shards of the per-shard means)
+    on the host.  batch = (X, Z, rows_x | None, rows_z | None, N, kx, kz) on the device."""
+    t = L.torch()
+    Xd, Zd, rx, rz, N, kx, kz = batch
+    sx, sz = _scores(Xd, wd), _scores(Zd, wd)
+    if rx is not None:
+        sx = sx.index_select(0, rx.reshape(-1))
+        sz = sz.index_select(0, rz.reshape(-1))
+    xo, zo, xod, zod = _shard_offsets(N, kx, kz)
+    sh = E.Shards(sx, xo, sz, zo, L.TW_F64)
+    sh._x_off_dev, sh._z_off_dev = xod, zod
+    kern = cs._loss_codes(loss)[0]
+    sums = E.pair_sum_complete_dev(sh, kern, float(margin))
+    cnt = E.count_launch(sx, xod, sz, zod, N, kx, kz, L.TW_F64, L.TW_PRED_GT,
+                         E.pick_algo("auto", kx, kz, "gt"))
+    res = t.cat([sums, cnt.view(t.float64)]).cpu().numpy()
+    pairs = kx * kz
+    bc = np.mean([np.float64(v / np.float64(pairs)) for v in res[:N]], axis=0)
+    br = np.mean([E.ratio(c, pairs) for c in res[N:].view(np.uint64)], axis=0)
+    return bc, br
+
+
+def _shard_offsets(N, kx, kz):
+    key = ("shards", N, kx, kz)
+    if key not in _OFFSETS:
+        xo = np.arange(N + 1, dtype=np.int64) * kx
+        zo = np.arange(N + 1, dtype=np.int64) * kz
+        _OFFSETS[key] = (xo, zo, L.to_device(xo), L.to_device(zo))
+    return _OFFSETS[key]
+
+
+def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _graph=True,
+                    _batch=None):
     """
         Modify the value of p_learn to add to the evaluation.  (make_exps.py:143-190)
         Monitored values, added in p_learn:
@@ -684,10 +785,16 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
     reg_term = p_learn["reg"] * (np.linalg.norm(w) ** 2) / 2
     t = L.torch()
     if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
-        sc_X = [x.dot(w) for x in X_s]
-        sc_Z = [z.dot(w) for z in Z_s]
-        bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin, loss=loss)) + reg_term
-        br_AUC = cs.UN_split(sc_X, sc_Z, lambda x, z: cs.Un(x, z, kernel="AUC"))
+        if _batch is not None:  # the learning loop's shards, resident on the device
+            wd = _w_dev if _w_dev is not None else L.to_device(
+                np.asarray(w, np.float64).reshape(-1))
+            bc, br_AUC = _same_as_batch_device(_batch, wd, margin, loss)
+            bc_AUC = bc + reg_term
+        else:
+            sc_X = [x.dot(w) for x in X_s]
+            sc_Z = [z.dot(w) for z in Z_s]
+            bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin, loss=loss)) + reg_term
+            br_AUC = cs.UN_split(sc_X, sc_Z, lambda x, z: cs.Un(x, z, kernel="AUC"))
     fixed = TYPE_TRAIN_MONITOR == "FIXED_PAIRS"
     if _w_dev is not None and _graph:  # the learning loop: w resident, device work one graph
         # one cached graph: valid while p_learn holds the same objects; w reaches it through
