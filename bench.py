@@ -204,6 +204,56 @@ def plumbing_C1(with_cpu, reps=200):
     return out
 
 
+def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
+    """The user-visible drop-in at BASELINE configs[2]'s size: est.UnNT(X, Z, 64, 4, "prop-SWOR")
+    (estimation-experiment/main.py:76-79) on HOST arrays of n = 1e6 per class, exactly as a
+    reference script calls it: NumPy's in-place shuffles in the reference's RNG order, the T
+    snapshots uploaded, all T x N blocks counted in one launch.  ms split into the host half
+    (shuffles, snapshots, concatenation), the H2D copy and the count kernel."""
+    import torch
+    import tuplewise.estimation as est
+    from tuplewise import _engine as E, _lib as L
+    rng = np.random.RandomState(0)
+    X, Z = rng.normal(0.5, 1, n), rng.normal(0, 1, n)
+    np.random.seed(1)
+    est.UnNT(X, Z, N, T, "prop-SWOR")  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        v = est.UnNT(X, Z, N, T, "prop-SWOR")
+    dt = (time.perf_counter() - t0) / reps
+    # the three parts, timed alone on the same shapes
+    t0 = time.perf_counter()
+    snaps = []
+    for _ in range(T):
+        np.random.shuffle(X)
+        np.random.shuffle(Z)
+        snaps.append((X.copy(), Z.copy()))
+    xs = np.concatenate([a for a, _ in snaps])
+    zs = np.concatenate([b for _, b in snaps])
+    host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    xd, zd = L.to_device(xs), L.to_device(zs)
+    torch.cuda.synchronize()
+    h2d = time.perf_counter() - t0
+    k = n // N
+    off = np.arange(T * N + 1, dtype=np.int64) * k
+    offd = L.to_device(off)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    E.count_launch(xd, offd, zd, offd, T * N, k, k, L.TW_F64, L.TW_PRED_GT, "pairs")
+    e0.record()
+    E.count_launch(xd, offd, zd, offd, T * N, k, k, L.TW_F64, L.TW_PRED_GT, "pairs")
+    e1.record()
+    torch.cuda.synchronize()
+    pairs = T * N * k * k
+    return {"note": "est.UnNT(X, Z, 64, 4, 'prop-SWOR') on host arrays, n=1e6/class (the drop-in "
+                    "as a reference script calls it); parts timed alone on the same shapes",
+            "ms_per_call": dt * 1e3, "value": pairs / dt, "unit": "pairs/s",
+            "host_shuffle_snapshot_ms": host * 1e3, "h2d_ms": h2d * 1e3,
+            "kernel_ms": e0.elapsed_time(e1), "last_value": float(v)}
+
+
 def cpu_baseline_incomplete(n, N, B, shards):
     """The reference's UnNB(kernel="AUC") restated (oracle.UB per block: two randint draws and
     a fancy-indexed compare, compute_stats.py:37-42), single-threaded, on `shards` of the N
@@ -816,6 +866,14 @@ def main():
         out["cpu_baseline"]["all_cores"] = allc
         out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, args.shards, B_inc,
                                                                     args.cpu_inc_shards)
+    if rank == 0 and world == 1:
+        d3 = drop_in_C3()
+        if "cpu_baseline" in out:  # the reference restated: T x one est.UnN of this run
+            unn_s = out["cpu_baseline"]["value"]
+            d3["cpu_port_ms_per_call"] = 4 * N_SHARDS * (n // N_SHARDS) ** 2 / unn_s * 1e3
+            d3["cpu_port_note"] = ("4 x the cpu_baseline est.UnN time (same blocks, NumPy "
+                                   "broadcast compare, 1 core); not rerun here (~23 s)")
+        out["drop_in_C3"] = d3
     if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:
