@@ -341,6 +341,29 @@ int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* 
                 double lr, double momentum, double* d_w_out, double* d_dw_out,
                 double* d_grads_out, void* stream);
 
+/* ---- Rows L1 + L2, wide rows (32 < d <= 512): a whole segment of nsteps SGD steps in ONE
+ * persistent launch (grid = min(n_shards, resident blocks), one block per CU; two grid barriers
+ * per step on d_ctl[0]).  Replaces nsteps x (tw_pair_grad(_rng) + tw_sgd_update) of
+ * learning-experiment/make_exps.py:126-141 with the same bits.  Draws: replay (d_ix / d_iz of
+ * step k at + k*draw_stride elements) or device RNG at *d_step + k (the counter advances by
+ * nsteps).  d_w / d_dw are updated in place; d_grads holds the last step's shard gradients.
+ * d_ctl: two uint32 words, the caller zeroes them once; the launch zeroes d_ctl[0]; d_ctl[1]
+ * is a sticky abort word — non-zero after a launch whose barrier wait timed out (2 s: blocks
+ * not co-resident), the SGD state is then invalid.
+ * tw_sgd_segment_set_grid(m): cap the grid at m blocks (tests; 0 = resident capacity);
+ * tw_sgd_segment_set_prefetch(1|0): prefetch the next step's first 32 pairs as rows (1, the
+ * default) or as row indices only (0) while the barriers run. */
+int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
+int tw_sgd_segment_set_grid(int32_t max_blocks);
+int tw_sgd_segment_set_prefetch(int32_t rows);
+int tw_sgd_segment(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
+                   int64_t kx, const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix,
+                   const int64_t* d_iz, int64_t draw_stride, int32_t n_shards, int64_t B,
+                   double margin, int32_t loss, uint64_t seed, uint64_t* d_step,
+                   int32_t shard_base, int32_t nsteps, double* d_w, double* d_dw,
+                   double* d_grads, double reg, double lr, double momentum, uint32_t* d_ctl,
+                   void* stream);
+
 /* ---- f1: scores = A @ w for a row-major (n, d) matrix (evaluation_step, make_exps.py:163,
  * :170-171).  Row dot products in index order. */
 int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w, double* d_out,

@@ -8,4 +8,7 @@ cfg = {"c4": (9117, 702, 10, 100, 100, 25, 2000, 1),
        "c5b": (1_000_000, 1_000_000, 512, 256, 4096, 25, 50, 1),
        "c5full": (5_000_000, 5_000_000, 512, 256, 100, 25, 500, 1)}[sys.argv[1]]
 torch.cuda.set_device(0)
+if "perstep" in sys.argv[2:]:  # per-step launches instead of the persistent segment kernel
+    import tuplewise.learning as lr
+    lr.SEGMENT_KERNEL = False
 print(json.dumps(bench.sgd_steps_per_s(*cfg)))

@@ -16,25 +16,15 @@
 //
 // Layout: one block per shard; the block streams its B pairs in chunks of CH pairs whose diff
 // rows are staged in LDS (CH*d doubles <= 64 KiB), so every X/Z row is read from HBM once.
-#include "tw_common.h"
+#include "sgd_common.h"
 #include <algorithm>
 
 namespace tw {
 
 constexpr int kLdsDoubles = 8192;  // 64 KiB of diff rows per block
 constexpr int kMaxColsPerThread = 16;  // d <= 16 * block size
-constexpr int kWideBlock = 1024;      // d > 32: 16 waves = 16 diff rows in flight per CU
 constexpr int kMaxD = 4096;
 
-// Device-RNG mode counters: Philox4x32-10 keyed by the run's seed; counter words
-// (index, shard, step lo, tag | step hi).  Tags separate the three draw streams.
-constexpr uint32_t kTagPairs = 0x80000000u, kTagRowsX = 0x40000000u, kTagRowsZ = 0x20000000u;
-
-__device__ __forceinline__ u32x4 sgd_draw(uint64_t seed, uint64_t step, uint32_t idx,
-                                          uint32_t shard, uint32_t tag) {
-  return philox4x32_10(u32x4{idx, shard, (uint32_t)step, tag | (uint32_t)(step >> 32)},
-                       (uint32_t)seed, (uint32_t)(seed >> 32));
-}
 
 template <int BS, int LOSS>
 __global__ __launch_bounds__(BS) void k_hinge_grad(
@@ -168,9 +158,6 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
 // row-order sums from +0.0), so both kernels give identical bits.
 constexpr int kWidePW = 2;
 constexpr int kWideCH = (kWideBlock / kWave) * kWidePW;  // 32 pairs per chunk
-constexpr int kWideCols = 8;                             // columns per lane
-constexpr int kWideMaxD = kWideCols * kWave;             // 512
-constexpr int kIdxPhase = 1024;
 
 template <int LOSS>
 __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
@@ -281,7 +268,6 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
 // which every thread finished before chunk k's barrier.  Same arithmetic and order as
 // k_hinge_grad_wide (per pair: lane partial dots over the same 8 columns + the same butterfly;
 // column sums in row order), so identical bits.
-constexpr int kStreamCH = kWideBlock / kWave;  // 16 pairs per chunk
 
 template <int LOSS>
 __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(

@@ -27,6 +27,7 @@ from . import compute_stats as cs
 from .numpy_rng import Session
 
 SEED_SHUFFLE = 42
+SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
 SIZE_TRAIN_MONITOR = 450000
@@ -106,6 +107,33 @@ class SGDEngine:
         self.fused = (self.G == 1 and not self.complete
                       and bool(L.lib().tw_sgd_step_fusable(self.d, self.N_loc)))
         self._slot1 = None
+        # wide rows on one GPU: a whole segment of steps in one persistent launch
+        # (tw_sgd_segment: grid barriers between the gradient and the update of every step)
+        self.segment = (SEGMENT_KERNEL and self.G == 1 and not self.complete and not self.fused
+                        and bool(L.lib().tw_sgd_segment_ok(self.d, self.N_loc)))
+        self._ctl = t.zeros((2,), dtype=t.int32, device=self.w.device) if self.segment else None
+
+    def _segment(self, nsteps: int, draws_dev=None):
+        """nsteps steps as ONE tw_sgd_segment launch (same bits as step()/step_device() +
+        _update() per step); draws_dev: the replay draws (S, 2, N, B) or None (device RNG)."""
+        ix = iz = None
+        stride = 0
+        if draws_dev is not None:
+            ix, iz = draws_dev[0, 0], draws_dev[0, 1]
+            stride = int(draws_dev.stride(0))
+        seed = getattr(self, "seed", 0) if draws_dev is None else 0
+        L.call("tw_sgd_segment", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
+               self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix), L.ptr(iz), stride, self.N_loc,
+               self.B, self.margin, self.loss, seed, L.ptr(self.step_ctr), self.shard_base,
+               nsteps, L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.reg, self.lr,
+               self.momentum, L.ptr(self._ctl), L.stream_handle())
+
+    def check(self):
+        """Raise if a persistent segment launch gave up waiting at a grid barrier (its bounded
+        spin expired: the blocks were not co-resident); the state is then invalid."""
+        if self._ctl is not None and int(self._ctl[1].item()) != 0:
+            raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
+                               "co-resident); the SGD state is invalid")
 
     def _fused_steps(self, nsteps: int, draws_dev=None):
         """nsteps steps as nsteps tw_sgd_step launches + one tw_sgd_update_to (ping-pong
@@ -260,7 +288,9 @@ class SGDEngine:
                 self.step(draws_dev[st, 0], draws_dev[st, 1])
 
         def steps():
-            if self.fused:
+            if self.segment:
+                self._segment(nsteps, draws_dev)
+            elif self.fused:
                 self._fused_steps(nsteps, draws_dev)
             else:
                 for st in range(nsteps):
@@ -298,6 +328,7 @@ class SGDEngine:
         return (self.X, self.Z, self.rows_x, self.rows_z, self.N, self.kx, self.kz)
 
     def w_host(self) -> np.ndarray:
+        self.check()
         return self.w.cpu().numpy().reshape(self.w_shape)
 
     def w_host_async(self):
@@ -312,6 +343,7 @@ class SGDEngine:
 
         def wait():
             self._w_event.synchronize()
+            self.check()
             return self._w_pinned.numpy().reshape(self.w_shape).copy()
         return wait
 
@@ -364,7 +396,9 @@ class SGDEngine:
             reshuffle_first = False
 
         def steps(n):
-            if self.fused:
+            if self.segment:
+                self._segment(n)
+            elif self.fused:
                 self._fused_steps(n)
             else:
                 for _ in range(n):
@@ -589,6 +623,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                 _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
             eng.run_replay_segment(buf, nxt - i, graphs, tag)
             i = nxt
+    eng.check()
     return None
 
 
@@ -632,6 +667,7 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
         nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod)
         eng.run_segment(nxt - i, resh, graphs)
         i = nxt
+    eng.check()
     return None
 
 
