@@ -552,8 +552,9 @@ __global__ __launch_bounds__(kBlock) void k_sgd_update(const double* w_in, const
       }
     }
     __syncthreads();
-    if (threadIdx.x < nc) {  // shard order kept; 8 LDS reads in flight per batch
+    if (threadIdx.x < nc) {  // shard order kept; 4 batches of 8 LDS reads scheduled ahead
       int r = 0;
+#pragma unroll 4
       for (; r + 8 <= ns; r += 8) {
         double v[8];
 #pragma unroll
