@@ -207,9 +207,11 @@ def plumbing_C1(with_cpu, reps=200):
 def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
     """The user-visible drop-in at BASELINE configs[2]'s size: est.UnNT(X, Z, 64, 4, "prop-SWOR")
     (estimation-experiment/main.py:76-79) on HOST arrays of n = 1e6 per class, exactly as a
-    reference script calls it: NumPy's in-place shuffles in the reference's RNG order, the T
-    snapshots uploaded, all T x N blocks counted in one launch.  ms split into the host half
-    (shuffles, snapshots, concatenation), the H2D copy and the count kernel."""
+    reference script calls it: the in-place shuffles in the reference's RNG order (the native
+    restatement of np.random.shuffle, numpy_rng.shuffle_pair: same draws, same arrays, X's swaps
+    on a second thread), the T snapshots uploaded, all T x N blocks counted in one launch.  ms
+    split into the host half (shuffles, snapshots, concatenation), the H2D copy and the count
+    kernel; NumPy's own shuffles timed beside them."""
     import torch
     import tuplewise.estimation as est
     from tuplewise import _engine as E, _lib as L
@@ -223,15 +225,20 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
         v = est.UnNT(X, Z, N, T, "prop-SWOR")
     dt = (time.perf_counter() - t0) / reps
     # the three parts, timed alone on the same shapes
+    from tuplewise.numpy_rng import shuffle_pair
     t0 = time.perf_counter()
     snaps = []
     for _ in range(T):
-        np.random.shuffle(X)
-        np.random.shuffle(Z)
+        shuffle_pair(X, Z)
         snaps.append((X.copy(), Z.copy()))
     xs = np.concatenate([a for a, _ in snaps])
     zs = np.concatenate([b for _, b in snaps])
     host = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(T):
+        np.random.shuffle(X)
+        np.random.shuffle(Z)
+    np_shuffles = time.perf_counter() - t0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     xd, zd = L.to_device(xs), L.to_device(zs)
@@ -250,7 +257,8 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
     return {"note": "est.UnNT(X, Z, 64, 4, 'prop-SWOR') on host arrays, n=1e6/class (the drop-in "
                     "as a reference script calls it); parts timed alone on the same shapes",
             "ms_per_call": dt * 1e3, "value": pairs / dt, "unit": "pairs/s",
-            "host_shuffle_snapshot_ms": host * 1e3, "h2d_ms": h2d * 1e3,
+            "host_shuffle_snapshot_ms": host * 1e3, "numpy_shuffles_ms": np_shuffles * 1e3,
+            "h2d_ms": h2d * 1e3,
             "kernel_ms": e0.elapsed_time(e1), "last_value": float(v)}
 
 

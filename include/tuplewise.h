@@ -483,6 +483,14 @@ int tw_np_mt_next32(uint32_t* key, int32_t* pos, int64_t cnt, uint32_t* out);
  * into ix[s*B..] then randint(0,kz,B) into iz[s*B..].  Returns 1 if kx or kz <= 0. */
 int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
                         int64_t B, int64_t* ix, int64_t* iz);
+/* np.random.shuffle(x); np.random.shuffle(z) — the in-place shuffles of UN
+ * (compute_stats.py:66-67, estimation-experiment/main.py:46-47) — on C-contiguous arrays of
+ * nx / nz items of isx / isz bytes (rows of a 2-D array are items): legacy RandomState's
+ * _shuffle_raw restated (i = n-1 down to 1: j = masked-rejection draw on [0, i], swap), the same
+ * draws from the same stream and the same final arrays; x's swaps run on a second thread while
+ * z's draws and swaps run.  jbuf: nx + nz int64 of scratch.  Returns 2 on bad arguments. */
+int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t isx, void* z,
+                       int64_t nz, int64_t isz, int64_t* jbuf);
 
 #ifdef __cplusplus
 }

@@ -2,9 +2,10 @@
 // host RNG restatement can be built and exercised under AddressSanitizer + UBSan
 // (csrc/Makefile target `sanitize`, tests/test_sanitize.py), on the AVX2 and the portable paths.
 //
-// stdin:  mode ("batch" | "pairs"), pos, 624 key words, then
+// stdin:  mode ("batch" | "pairs" | "shuffle"), pos, 624 key words, then
 //   batch: n_calls, then n_calls lines "low high cnt"
 //   pairs: "N kx kz B"
+//   shuffle: "nx nz": shuffles arange(nx) then arange(nz) (int64 items) in place
 // stdout: the draws (one per line), then the final pos and the 624 key words.
 #include <cstdint>
 #include <cstdio>
@@ -16,6 +17,8 @@ extern "C" int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls,
                                    int64_t* out);
 extern "C" int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx,
                                    int64_t kz, int64_t B, int64_t* ix, int64_t* iz);
+extern "C" int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t isx,
+                                  void* z, int64_t nz, int64_t isz, int64_t* jbuf);
 
 int main() {
   char mode[16];
@@ -38,6 +41,15 @@ int main() {
     }
     out.resize(tot);
     rc = tw_np_randint_batch(key.data(), &pos, n, lo.data(), hi.data(), cnt.data(), out.data());
+  } else if (std::string(mode) == "shuffle") {
+    long long nx, nz;
+    if (scanf("%lld %lld", &nx, &nz) != 2) return 2;
+    std::vector<int64_t> x(nx), z(nz), j(nx + nz + 1);
+    for (long long i = 0; i < nx; ++i) x[i] = i;
+    for (long long i = 0; i < nz; ++i) z[i] = i;
+    rc = tw_np_shuffle_pair(key.data(), &pos, x.data(), nx, 8, z.data(), nz, 8, j.data());
+    out.insert(out.end(), x.begin(), x.end());
+    out.insert(out.end(), z.begin(), z.end());
   } else {
     long long N, kx, kz, B;
     if (scanf("%lld %lld %lld %lld", &N, &kx, &kz, &B) != 4) return 2;

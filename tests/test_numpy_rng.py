@@ -95,3 +95,48 @@ def test_scalar_path_matches_numpy(tw):
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
+
+
+@pytest.mark.parametrize("nx,nz,shape,dtype", [
+    (1000, 700, None, np.float64), (1, 5, None, np.float64), (0, 3, None, np.float64),
+    (17, 1, None, np.int64), (300000, 200000, None, np.float64), (1000, 50, "col", np.float64),
+    (999, 88, "rows", np.float64), (5000, 3000, None, np.float32), (4097, 4095, None, np.int8),
+    (2 ** 20 + 5, 1025, None, np.float64)])
+def test_shuffle_pair_matches_numpy(tw, nx, nz, shape, dtype):
+    """numpy_rng.shuffle_pair == np.random.shuffle(X); np.random.shuffle(Z): arrays (1-D, (n, 1),
+    rows of a 2-D array), every dtype width, and the RNG state after (a probe draw)."""
+    from tuplewise.numpy_rng import shuffle_pair
+    rs = np.random.RandomState(nx)
+    X = rs.normal(size=nx).astype(dtype)
+    Z = rs.normal(size=nz).astype(dtype)
+    if shape == "col":
+        X, Z = X.reshape(-1, 1), Z.reshape(-1, 1)
+    elif shape == "rows":
+        X, Z = np.repeat(X[:, None], 3, 1).copy(), np.repeat(Z[:, None], 3, 1).copy()
+    for seed in (1, 123):
+        X1, Z1, X2, Z2 = X.copy(), Z.copy(), X.copy(), Z.copy()
+        np.random.seed(seed)
+        np.random.randint(0, 5, 3)
+        np.random.shuffle(X1)
+        np.random.shuffle(Z1)
+        want = np.random.randint(0, 2 ** 31, 4)
+        np.random.seed(seed)
+        np.random.randint(0, 5, 3)
+        shuffle_pair(X2, Z2)
+        assert np.array_equal(X2, X1) and np.array_equal(Z2, Z1)
+        assert np.array_equal(np.random.randint(0, 2 ** 31, 4), want)
+
+
+def test_shuffle_pair_views_fall_back_to_numpy(tw):
+    """A strided view is shuffled by np.random.shuffle itself (the buffer path is restated only
+    for contiguous arrays): same result either way."""
+    from tuplewise.numpy_rng import shuffle_pair
+    base = np.arange(2000.0)
+    X, Z = base[::2], np.arange(300.0)
+    Xr, Zr = X.copy(), Z.copy()
+    np.random.seed(4)
+    np.random.shuffle(Xr)
+    np.random.shuffle(Zr)
+    np.random.seed(4)
+    shuffle_pair(X, Z)
+    assert np.array_equal(X, Xr) and np.array_equal(Z, Zr)

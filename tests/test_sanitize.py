@@ -69,3 +69,20 @@ def test_randint_pairs_sanitized_equals_numpy(driver, scalar):
     assert rc == 0 and np.array_equal(got, want)
     _, wkey, wpos, _, _ = rs.get_state()
     assert pos == wpos and np.array_equal(key, wkey)
+
+
+@pytest.mark.parametrize("scalar", [False, True])
+@pytest.mark.parametrize("nx,nz", [(1, 1), (2, 17), (1000, 3), (70000, 65537), (300001, 20)])
+def test_shuffle_pair_sanitized_equals_numpy(driver, scalar, nx, nz):
+    """tw_np_shuffle_pair (the draws, the AVX2 sure-accept batches, the threaded swaps) under
+    ASan/UBSan against RandomState.shuffle itself."""
+    rs = np.random.RandomState(77 + nx)
+    rs.randint(0, 10, 3)
+    script = _state_script("shuffle", rs) + f"{nx} {nz}\n"
+    rc, got, pos, key = _run(driver, script, scalar)
+    x, z = np.arange(nx), np.arange(nz)
+    rs.shuffle(x)
+    rs.shuffle(z)
+    assert rc == 0 and np.array_equal(got, np.concatenate([x, z]))
+    _, wkey, wpos, _, _ = rs.get_state()
+    assert pos == wpos and np.array_equal(key, wkey)

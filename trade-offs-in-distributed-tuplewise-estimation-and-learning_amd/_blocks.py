@@ -18,6 +18,7 @@ import numpy as np
 from . import _engine as E
 from . import _lib as L
 from . import _multi as M
+from .numpy_rng import shuffle_pair
 
 
 class Block:
@@ -311,8 +312,7 @@ def plan_un(X, Z, N, spec, sampling_type, variant: str) -> list:
     reference in order.  Returns the plan [("val", Block) | ("zero",)] in append order."""
     X_rem = X
     Z_rem = Z
-    np.random.shuffle(X_rem)
-    np.random.shuffle(Z_rem)
+    shuffle_pair(X_rem, Z_rem)  # np.random.shuffle(X); np.random.shuffle(Z), bit for bit
     n_X = X_rem.shape[0]
     n_Z = Z_rem.shape[0]
     tau = int((n_X + n_Z) / N)
@@ -360,8 +360,7 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
     :33-69, variant "est").  Keeps the in-place shuffle and every RNG draw in order."""
     spec = getattr(f_block, "_tw_block", None)
     if spec is None:  # user block function: the reference protocol, block by block
-        np.random.shuffle(X)
-        np.random.shuffle(Z)
+        shuffle_pair(X, Z)
         n_X, n_Z = X.shape[0], Z.shape[0]
         return _run_un_python(X, Z, N, f_block, sampling_type, variant, n_X, n_Z,
                               int((n_X + n_Z) / N))

@@ -108,6 +108,7 @@ _SIGNATURES = {
     "tw_np_randint_batch": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],
+    "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
 }
 _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,

@@ -25,6 +25,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <thread>
 
 #define TW_INLINE inline __attribute__((always_inline))
 
@@ -226,6 +227,106 @@ __attribute__((target("avx2,popcnt"))) void pairs_avx2(uint32_t* key, int32_t* p
   pairs_body<true>(key, pos, N, kx, kz, B, ix, iz);
 }
 
+// RandomState.shuffle's index draws (legacy _shuffle_raw + random_interval): for i = n-1 down
+// to 1, j[i] = the first v = next & mask(i) with v <= i (32-bit draws while i <= 2^32-1,
+// 64-bit above).  Branch-free: every raw draw is written to j[i], i moves on only on accept.
+// 8 raw draws at a time while the bound i is large: lane k is accepted iff v_k <= i - (accepts
+// in lanes < k), so v <= i - 7 is a sure accept and v > i a sure reject; a batch of only sure
+// lanes is left-packed and stored reversed at j[i-7 .. i] (j[i - r] = r-th accept; the lanes
+// past the accepts land on lower slots that later draws overwrite).  Any unsure lane: the
+// batch is left to the scalar loop.  Returns the new p (i updated).
+__attribute__((target("avx2,popcnt"))) inline int shuffle8_avx2(const uint32_t* tmp, int p,
+                                                               uint32_t mask, int64_t lo,
+                                                               int64_t& i, int64_t* j) {
+  const __m256i vm = _mm256_set1_epi32((int)mask);
+  const __m256i sign = _mm256_set1_epi32((int)0x80000000u);
+  const __m256i rev = _mm256_setr_epi32(7, 6, 5, 4, 3, 2, 1, 0);
+  while (p + 8 <= kN && i - 8 > lo && i >= 8) {
+    const __m256i v = _mm256_and_si256(_mm256_loadu_si256((const __m256i*)(tmp + p)), vm);
+    const __m256i vs = _mm256_xor_si256(v, sign);
+    const __m256i rej = _mm256_cmpgt_epi32(vs, _mm256_set1_epi32((int)((uint32_t)i ^ 0x80000000u)));
+    const __m256i unsure = _mm256_andnot_si256(
+        rej, _mm256_cmpgt_epi32(vs, _mm256_set1_epi32((int)((uint32_t)(i - 7) ^ 0x80000000u))));
+    if (!_mm256_testz_si256(unsure, unsure)) break;
+    const int acc = ~_mm256_movemask_ps(_mm256_castsi256_ps(rej)) & 0xFF;
+    const __m256i packed = _mm256_permutevar8x32_epi32(
+        v, _mm256_loadu_si256((const __m256i*)g_pack.idx[acc]));
+    const __m256i r = _mm256_permutevar8x32_epi32(packed, rev);  // lane l = accept 7 - l
+    _mm256_storeu_si256((__m256i*)(j + i - 7), _mm256_cvtepu32_epi64(_mm256_castsi256_si128(r)));
+    _mm256_storeu_si256((__m256i*)(j + i - 3),
+                        _mm256_cvtepu32_epi64(_mm256_extracti128_si256(r, 1)));
+    i -= __builtin_popcount((unsigned)acc);
+    p += 8;
+  }
+  return p;
+}
+
+template <bool kAvx2>
+void shuffle_draws(MT& mt, int64_t n, int64_t* j) {
+  int64_t i = n - 1;
+  while (i >= 1 && (uint64_t)i > 0xFFFFFFFFull) {
+    const uint64_t mask = gen_mask((uint64_t)i);
+    uint64_t v;
+    while ((v = (mt.next64() & mask)) > (uint64_t)i) {
+    }
+    j[i--] = (int64_t)v;
+  }
+  while (i >= 1) {
+    const uint32_t mask = (uint32_t)gen_mask((uint64_t)i);
+    const int64_t lo = (int64_t)(mask >> 1);  // this mask serves i in (mask/2, mask]
+    if (mt.pos >= kN) mt.generate();
+    mt.temper_rest();
+    int p = mt.pos;
+    for (;;) {
+      if (kAvx2) p = shuffle8_avx2(mt.tmp, p, mask, lo, i, j);
+      // scalar: until the block or the mask range ends, or (AVX2) 8 words have passed
+      const int stop = kAvx2 ? (p + 8 < kN ? p + 8 : kN) : kN;
+      while (p < stop && i > lo) {
+        const uint32_t v = mt.tmp[p++] & mask;
+        j[i] = (int64_t)v;
+        i -= (int64_t)(v <= (uint32_t)i);
+      }
+      if (p >= kN || i <= lo) break;
+    }
+    mt.pos = p;
+  }
+}
+
+// the swaps of _shuffle_raw for items of `itemsize` bytes, i = n-1 down to 1, with the random
+// side prefetched a few swaps ahead
+void shuffle_apply(char* data, int64_t n, int64_t itemsize, const int64_t* j) {
+  constexpr int64_t kAhead = 24;
+  if (itemsize == 8) {
+    uint64_t* a = (uint64_t*)data;
+    for (int64_t i = n - 1; i >= 1; --i) {
+      if (i - kAhead >= 1) __builtin_prefetch(a + j[i - kAhead], 1);
+      const int64_t k = j[i];
+      const uint64_t t = a[k];
+      a[k] = a[i];
+      a[i] = t;
+    }
+    return;
+  }
+  char buf[256];
+  for (int64_t i = n - 1; i >= 1; --i) {
+    if (i - kAhead >= 1) __builtin_prefetch(data + j[i - kAhead] * itemsize, 1);
+    const int64_t k = j[i];
+    if (k == i) continue;
+    char* pk = data + k * itemsize;
+    char* pi = data + i * itemsize;
+    for (int64_t o = 0; o < itemsize; o += 256) {
+      const int64_t c = itemsize - o < 256 ? itemsize - o : 256;
+      memcpy(buf, pk + o, c);
+      memcpy(pk + o, pi + o, c);
+      memcpy(pi + o, buf, c);
+    }
+  }
+}
+
+__attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t n, int64_t* j) {
+  shuffle_draws<true>(mt, n, j);
+}
+
 // TW_NP_RNG_SCALAR=1 forces the portable path (tests compare both)
 bool use_avx2() {
   static const int v = [] {
@@ -260,6 +361,46 @@ int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int6
     pairs_avx2(key, pos, N, kx, kz, B, ix, iz);
   else
     pairs_generic(key, pos, N, kx, kz, B, ix, iz);
+  return 0;
+}
+
+// np.random.shuffle(x); np.random.shuffle(z) on C-contiguous arrays of nx / nz items of isx /
+// isz bytes (rows of a 2-D array are items): the same draws from the same stream, the same
+// swaps, the same final state.  x's draws come first; x's swaps then run on a second thread
+// while z's draws and swaps run here.  jbuf: nx + nz int64 of scratch.  nz == 0 / z == NULL:
+// x alone.
+int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t isx, void* z,
+                       int64_t nz, int64_t isz, int64_t* jbuf) {
+  if (nx < 0 || nz < 0 || (nx > 1 && !x) || (nz > 1 && !z) || isx < 1 || isz < 1) return 2;
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  int64_t* jx = jbuf;
+  int64_t* jz = jbuf + (nx > 0 ? nx : 0);
+  const bool avx2 = use_avx2();
+  auto draws = [&](int64_t n, int64_t* j) {
+    if (avx2)
+      shuffle_draws_avx2(mt, n, j);
+    else
+      shuffle_draws<false>(mt, n, j);
+  };
+  if (nx > 1) draws(nx, jx);
+  std::thread tx;
+  bool threaded = false;
+  if (nx > 1) {
+    if (nz > 1 && nx >= 65536) {
+      tx = std::thread(shuffle_apply, (char*)x, nx, isx, (const int64_t*)jx);
+      threaded = true;
+    } else {
+      shuffle_apply((char*)x, nx, isx, jx);
+    }
+  }
+  if (nz > 1) {
+    draws(nz, jz);
+    shuffle_apply((char*)z, nz, isz, jz);
+  }
+  if (threaded) tx.join();
+  *pos = mt.pos;
   return 0;
 }
 

@@ -40,6 +40,40 @@ def randint_batch(calls) -> list:
     return [out[offs[i]:offs[i + 1]] for i in range(len(cnt))]
 
 
+def _shuffle_items(a):
+    """(items, item bytes) when np.random.shuffle(a) is the buffer path this module restates:
+    a C-contiguous, non-object ndarray (rows of a 2-D array are items); else None."""
+    if not isinstance(a, np.ndarray) or a.ndim == 0 or a.dtype.hasobject:
+        return None
+    if not a.flags.c_contiguous or a.size == 0:
+        return None
+    return a.shape[0], a.itemsize * (a.size // a.shape[0])
+
+
+def shuffle_pair(X, Z) -> None:
+    """np.random.shuffle(X); np.random.shuffle(Z) (compute_stats.py:66-67, estimation-experiment/
+    main.py:46-47): the same index draws from the same legacy MT19937 stream, the same swaps,
+    the same final RNG state — the swaps of X on a second native thread while Z's draws and
+    swaps run.  Arrays the buffer path does not cover (views, object arrays, other RNGs) go
+    to np.random.shuffle itself."""
+    ix, iz = _shuffle_items(X), _shuffle_items(Z)
+    state = np.random.get_state(legacy=True)
+    if ix is None or iz is None or state[0] != "MT19937":
+        np.random.shuffle(X)
+        np.random.shuffle(Z)
+        return
+    name, key, pos, has_gauss, gauss = state
+    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+    pos_c = ctypes.c_int32(int(pos))
+    jbuf = np.empty(ix[0] + iz[0], dtype=np.int64)
+    rc = L.lib().tw_np_shuffle_pair(key.ctypes.data, ctypes.byref(pos_c), X.ctypes.data,
+                                    ix[0], ix[1], Z.ctypes.data, iz[0], iz[1],
+                                    jbuf.ctypes.data)
+    if rc:
+        raise RuntimeError(f"tw_np_shuffle_pair failed ({rc})")
+    np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
+
+
 class Session:
     """NumPy's legacy global MT19937 state held in native code for a run of draws.
 
