@@ -77,8 +77,11 @@ def test_session_flat_draws_commit_and_reacquire(tw):
     assert np.random.random() == end
 
 
-def test_scalar_path_matches_numpy(tw):
-    """The portable (non-AVX2) compaction, forced in a fresh process, against np.random."""
+@pytest.mark.parametrize("env", [{"TW_NP_RNG_SCALAR": "1"}, {"TW_NP_RNG_ISA": "avx2"}])
+def test_scalar_path_matches_numpy(tw, env):
+    """The portable compaction and the AVX2 path (the in-process tests run the widest level the
+    CPU has, AVX-512 where present), each forced in a fresh process, against np.random —
+    randint pairs and the in-place shuffles."""
     import os
     import subprocess
     import sys
@@ -89,8 +92,13 @@ def test_scalar_path_matches_numpy(tw):
         "np.random.seed(3); ix=np.empty((40,100),np.int64); iz=np.empty((40,100),np.int64)\n"
         "s=Session(); s.pairs(40,91,7,100,ix,iz); s.commit()\n"
         "assert np.array_equal(ix, np.stack(w[0::2])) and np.array_equal(iz, np.stack(w[1::2]))\n"
+        "from tuplewise.numpy_rng import shuffle_pair\n"
+        "X=np.arange(70001.0); Z=np.arange(3000.0); X1=X.copy(); Z1=Z.copy()\n"
+        "np.random.seed(8); np.random.shuffle(X1); np.random.shuffle(Z1); p=np.random.rand()\n"
+        "np.random.seed(8); shuffle_pair(X, Z)\n"
+        "assert np.array_equal(X, X1) and np.array_equal(Z, Z1) and np.random.rand() == p\n"
         "print('ok')\n")
-    env = dict(os.environ, TW_NP_RNG_SCALAR="1")
+    env = dict(os.environ, **env)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True,
                        text=True, timeout=120)

@@ -1,8 +1,8 @@
 """The host C++ of the C ABI under AddressSanitizer + UBSan (SURVEY.md §5 'Race detection /
 sanitizers').  csrc/numpy_rng.cpp (MT19937 + masked-rejection randint,
 an AVX2 left-pack with a 256-entry LUT) is built with -fsanitize=address,undefined
-(`make -C csrc sanitize`, tests/native/numpy_rng_driver.cpp) and run on both the AVX2 and the
-portable paths; every draw and the advanced state must equal np.random's own, and any
+(`make -C csrc sanitize`, tests/native/numpy_rng_driver.cpp) and run on the AVX-512 (where the
+CPU has it), AVX2 and portable paths; every draw and the advanced state must equal np.random's own, and any
 sanitizer report aborts the driver (non-zero exit)."""
 import os
 import pathlib
@@ -25,9 +25,12 @@ def driver():
 
 
 def _run(exe, script, scalar):
+    """scalar: False (widest SIMD level of the CPU), True (portable), or "avx2" (capped)."""
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
-    if scalar:
+    if scalar == "avx2":
+        env["TW_NP_RNG_ISA"] = "avx2"
+    elif scalar:
         env["TW_NP_RNG_SCALAR"] = "1"
     r = subprocess.run([str(exe)], input=script, capture_output=True, text=True, timeout=300,
                        env=env)
@@ -41,7 +44,7 @@ def _state_script(mode, rs):
     return f"{mode}\n{pos}\n" + " ".join(str(int(k)) for k in key) + "\n"
 
 
-@pytest.mark.parametrize("scalar", [False, True])
+@pytest.mark.parametrize("scalar", [False, "avx2", True])
 def test_randint_batch_sanitized_equals_numpy(driver, scalar):
     rs = np.random.RandomState(2024)
     rs.randint(0, 10, 7)  # a mid-block position
@@ -57,7 +60,7 @@ def test_randint_batch_sanitized_equals_numpy(driver, scalar):
     assert pos == wpos and np.array_equal(key, wkey)
 
 
-@pytest.mark.parametrize("scalar", [False, True])
+@pytest.mark.parametrize("scalar", [False, "avx2", True])
 def test_randint_pairs_sanitized_equals_numpy(driver, scalar):
     """grad_inc_block's draws for every shard of one step (compute_stats.py:155-156)."""
     rs = np.random.RandomState(7)
@@ -71,7 +74,7 @@ def test_randint_pairs_sanitized_equals_numpy(driver, scalar):
     assert pos == wpos and np.array_equal(key, wkey)
 
 
-@pytest.mark.parametrize("scalar", [False, True])
+@pytest.mark.parametrize("scalar", [False, "avx2", True])
 @pytest.mark.parametrize("nx,nz", [(1, 1), (2, 17), (1000, 3), (70000, 65537), (300001, 20)])
 def test_shuffle_pair_sanitized_equals_numpy(driver, scalar, nx, nz):
     """tw_np_shuffle_pair (the draws, the AVX2 sure-accept batches, the threaded swaps) under

@@ -19,8 +19,9 @@
 // Parity is pinned by tests/test_numpy_rng.py against np.random itself.
 //
 // Speed: the 624-word block is generated and tempered with vector loops, and the masked
-// rejection is a left-pack of accepted draws (8 lanes at a time with AVX2, chosen at run time
-// by __builtin_cpu_supports; scalar branch-free compaction otherwise).
+// rejection is a left-pack of accepted draws (16 lanes with AVX-512 compress, 8 with an AVX2
+// permutation LUT, chosen at run time by __builtin_cpu_supports; scalar branch-free compaction
+// otherwise).
 #include <immintrin.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -136,7 +137,29 @@ __attribute__((target("avx2,popcnt"))) inline int pack8_avx2(const uint32_t* tmp
   return p;
 }
 
-template <bool kAvx2>
+// the same with 16 lanes (AVX-512: compare to a mask register, compress the accepted lanes)
+__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) inline int pack16_avx512(
+    const uint32_t* tmp, int p, uint32_t mask, uint32_t r32, int64_t low, int64_t cnt,
+    int64_t* out, int64_t& o) {
+  const __m512i vm = _mm512_set1_epi32((int)mask);
+  const __m512i vr = _mm512_set1_epi32((int)r32);
+  const __m512i vlow = _mm512_set1_epi64(low);
+  while (p + 16 <= kN && cnt - o >= 16) {
+    const __m512i v = _mm512_and_si512(_mm512_loadu_si512((const void*)(tmp + p)), vm);
+    const __mmask16 acc = _mm512_cmple_epu32_mask(v, vr);
+    const __m512i packed = _mm512_maskz_compress_epi32(acc, v);
+    const __m512i lo8 = _mm512_cvtepu32_epi64(_mm512_castsi512_si256(packed));
+    const __m512i hi8 = _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(packed, 1));
+    _mm512_storeu_si512((void*)(out + o), _mm512_add_epi64(lo8, vlow));
+    _mm512_storeu_si512((void*)(out + o + 8), _mm512_add_epi64(hi8, vlow));
+    o += __builtin_popcount((unsigned)acc);
+    p += 16;
+  }
+  return p;
+}
+
+// kIsa: 0 portable, 1 AVX2, 2 AVX-512 (+ AVX2 for the 8-lane remainder)
+template <int kIsa>
 TW_INLINE void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) {
   const uint64_t rng = (uint64_t)(high - 1) - (uint64_t)low;
   if (rng == 0) {
@@ -157,7 +180,8 @@ TW_INLINE void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int6
       if (mt.pos >= kN) mt.generate();
       mt.temper_rest();
       int p = mt.pos;
-      if (kAvx2) p = pack8_avx2(mt.tmp, p, mask, r32, low, cnt, out, o);
+      if (kIsa >= 2) p = pack16_avx512(mt.tmp, p, mask, r32, low, cnt, out, o);
+      if (kIsa >= 1) p = pack8_avx2(mt.tmp, p, mask, r32, low, cnt, out, o);
       while (p < kN && o < cnt) {
         const uint32_t v = mt.tmp[p++] & mask;
         out[o] = (int64_t)((uint64_t)low + v);
@@ -176,7 +200,7 @@ TW_INLINE void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int6
   }
 }
 
-template <bool kAvx2>
+template <int kIsa>
 TW_INLINE int batch_body(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
                          const int64_t* high, const int64_t* cnt, int64_t* out) {
   MT mt;
@@ -188,43 +212,53 @@ TW_INLINE int batch_body(uint32_t* key, int32_t* pos, int32_t n_calls, const int
       *pos = mt.pos;
       return 1;
     }
-    randint_fill<kAvx2>(mt, low[c], high[c], cnt[c], out + o);
+    randint_fill<kIsa>(mt, low[c], high[c], cnt[c], out + o);
     o += cnt[c];
   }
   *pos = mt.pos;
   return 0;
 }
 
-template <bool kAvx2>
+template <int kIsa>
 TW_INLINE void pairs_body(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
                           int64_t B, int64_t* ix, int64_t* iz) {
   MT mt;
   mt.key = key;
   mt.pos = *pos;
   for (int32_t s = 0; s < N; ++s) {
-    randint_fill<kAvx2>(mt, 0, kx, B, ix + (int64_t)s * B);
-    randint_fill<kAvx2>(mt, 0, kz, B, iz + (int64_t)s * B);
+    randint_fill<kIsa>(mt, 0, kx, B, ix + (int64_t)s * B);
+    randint_fill<kIsa>(mt, 0, kz, B, iz + (int64_t)s * B);
   }
   *pos = mt.pos;
 }
 
 int batch_generic(uint32_t* key, int32_t* pos, int32_t n, const int64_t* lo, const int64_t* hi,
                   const int64_t* cnt, int64_t* out) {
-  return batch_body<false>(key, pos, n, lo, hi, cnt, out);
+  return batch_body<0>(key, pos, n, lo, hi, cnt, out);
 }
 __attribute__((target("avx2,popcnt"))) int batch_avx2(uint32_t* key, int32_t* pos, int32_t n,
                                                       const int64_t* lo, const int64_t* hi,
                                                       const int64_t* cnt, int64_t* out) {
-  return batch_body<true>(key, pos, n, lo, hi, cnt, out);
+  return batch_body<1>(key, pos, n, lo, hi, cnt, out);
+}
+__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) int batch_avx512(
+    uint32_t* key, int32_t* pos, int32_t n, const int64_t* lo, const int64_t* hi,
+    const int64_t* cnt, int64_t* out) {
+  return batch_body<2>(key, pos, n, lo, hi, cnt, out);
 }
 void pairs_generic(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B,
                    int64_t* ix, int64_t* iz) {
-  pairs_body<false>(key, pos, N, kx, kz, B, ix, iz);
+  pairs_body<0>(key, pos, N, kx, kz, B, ix, iz);
 }
 __attribute__((target("avx2,popcnt"))) void pairs_avx2(uint32_t* key, int32_t* pos, int32_t N,
                                                        int64_t kx, int64_t kz, int64_t B,
                                                        int64_t* ix, int64_t* iz) {
-  pairs_body<true>(key, pos, N, kx, kz, B, ix, iz);
+  pairs_body<1>(key, pos, N, kx, kz, B, ix, iz);
+}
+__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) void pairs_avx512(
+    uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B, int64_t* ix,
+    int64_t* iz) {
+  pairs_body<2>(key, pos, N, kx, kz, B, ix, iz);
 }
 
 // RandomState.shuffle's index draws (legacy _shuffle_raw + random_interval): for i = n-1 down
@@ -261,7 +295,30 @@ __attribute__((target("avx2,popcnt"))) inline int shuffle8_avx2(const uint32_t* 
   return p;
 }
 
-template <bool kAvx2>
+// the same with 16 lanes (sure accept v <= i - 15)
+__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) inline int shuffle16_avx512(
+    const uint32_t* tmp, int p, uint32_t mask, int64_t lo, int64_t& i, int64_t* j) {
+  const __m512i vm = _mm512_set1_epi32((int)mask);
+  const __m512i rev = _mm512_setr_epi32(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
+  while (p + 16 <= kN && i - 16 > lo && i >= 16) {
+    const __m512i v = _mm512_and_si512(_mm512_loadu_si512((const void*)(tmp + p)), vm);
+    const __mmask16 rej = _mm512_cmpgt_epu32_mask(v, _mm512_set1_epi32((int)(uint32_t)i));
+    const __mmask16 unsure =
+        (__mmask16)(~rej & _mm512_cmpgt_epu32_mask(v, _mm512_set1_epi32((int)(uint32_t)(i - 15))));
+    if (unsure) break;
+    const __mmask16 acc = (__mmask16)~rej;
+    const __m512i packed = _mm512_maskz_compress_epi32(acc, v);
+    const __m512i r = _mm512_permutexvar_epi32(rev, packed);  // lane l = accept 15 - l
+    _mm512_storeu_si512((void*)(j + i - 15), _mm512_cvtepu32_epi64(_mm512_castsi512_si256(r)));
+    _mm512_storeu_si512((void*)(j + i - 7),
+                        _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(r, 1)));
+    i -= __builtin_popcount((unsigned)acc);
+    p += 16;
+  }
+  return p;
+}
+
+template <int kIsa>
 void shuffle_draws(MT& mt, int64_t n, int64_t* j) {
   int64_t i = n - 1;
   while (i >= 1 && (uint64_t)i > 0xFFFFFFFFull) {
@@ -278,9 +335,10 @@ void shuffle_draws(MT& mt, int64_t n, int64_t* j) {
     mt.temper_rest();
     int p = mt.pos;
     for (;;) {
-      if (kAvx2) p = shuffle8_avx2(mt.tmp, p, mask, lo, i, j);
-      // scalar: until the block or the mask range ends, or (AVX2) 8 words have passed
-      const int stop = kAvx2 ? (p + 8 < kN ? p + 8 : kN) : kN;
+      if (kIsa >= 2) p = shuffle16_avx512(mt.tmp, p, mask, lo, i, j);
+      if (kIsa >= 1) p = shuffle8_avx2(mt.tmp, p, mask, lo, i, j);
+      // scalar: until the block or the mask range ends, or (SIMD) 8 words have passed
+      const int stop = kIsa ? (p + 8 < kN ? p + 8 : kN) : kN;
       while (p < stop && i > lo) {
         const uint32_t v = mt.tmp[p++] & mask;
         j[i] = (int64_t)v;
@@ -324,18 +382,28 @@ void shuffle_apply(char* data, int64_t n, int64_t itemsize, const int64_t* j) {
 }
 
 __attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t n, int64_t* j) {
-  shuffle_draws<true>(mt, n, j);
+  shuffle_draws<1>(mt, n, j);
+}
+__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) void shuffle_draws_avx512(MT& mt,
+                                                                                  int64_t n,
+                                                                                  int64_t* j) {
+  shuffle_draws<2>(mt, n, j);
 }
 
-// TW_NP_RNG_SCALAR=1 forces the portable path (tests compare both)
-bool use_avx2() {
+// SIMD level chosen once at run time: 2 AVX-512 (F + VL), 1 AVX2, 0 portable.
+// TW_NP_RNG_SCALAR=1 forces the portable path, TW_NP_RNG_ISA=avx2 caps it at AVX2 (tests run
+// every level against NumPy).
+int isa_level() {
   static const int v = [] {
     const char* e = getenv("TW_NP_RNG_SCALAR");
     if (e && e[0] == '1') return 0;
     __builtin_cpu_init();
-    return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("popcnt") ? 1 : 0;
+    if (!__builtin_cpu_supports("avx2") || !__builtin_cpu_supports("popcnt")) return 0;
+    const char* cap = getenv("TW_NP_RNG_ISA");
+    if (cap && strcmp(cap, "avx2") == 0) return 1;
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") ? 2 : 1;
   }();
-  return v != 0;
+  return v;
 }
 
 }  // namespace
@@ -348,7 +416,9 @@ extern "C" {
 // ValueError "high <= low"), leaving the state where the failing call would have started.
 int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
                         const int64_t* high, const int64_t* cnt, int64_t* out) {
-  return use_avx2() ? batch_avx2(key, pos, n_calls, low, high, cnt, out)
+  const int isa = isa_level();
+  return isa == 2   ? batch_avx512(key, pos, n_calls, low, high, cnt, out)
+         : isa == 1 ? batch_avx2(key, pos, n_calls, low, high, cnt, out)
                     : batch_generic(key, pos, n_calls, low, high, cnt, out);
 }
 
@@ -357,7 +427,10 @@ int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int6
 int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
                         int64_t B, int64_t* ix, int64_t* iz) {
   if (kx <= 0 || kz <= 0) return 1;
-  if (use_avx2())
+  const int isa = isa_level();
+  if (isa == 2)
+    pairs_avx512(key, pos, N, kx, kz, B, ix, iz);
+  else if (isa == 1)
     pairs_avx2(key, pos, N, kx, kz, B, ix, iz);
   else
     pairs_generic(key, pos, N, kx, kz, B, ix, iz);
@@ -377,12 +450,14 @@ int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t
   mt.pos = *pos;
   int64_t* jx = jbuf;
   int64_t* jz = jbuf + (nx > 0 ? nx : 0);
-  const bool avx2 = use_avx2();
+  const int isa = isa_level();
   auto draws = [&](int64_t n, int64_t* j) {
-    if (avx2)
+    if (isa == 2)
+      shuffle_draws_avx512(mt, n, j);
+    else if (isa == 1)
       shuffle_draws_avx2(mt, n, j);
     else
-      shuffle_draws<false>(mt, n, j);
+      shuffle_draws<0>(mt, n, j);
   };
   if (nx > 1) draws(nx, jx);
   std::thread tx;
