@@ -421,6 +421,25 @@ def pmc_traffic():
     return d.get("hbm_bytes_per_launch"), plain
 
 
+def pmc_replay_traffic():
+    """HBM bytes per launch of k_count_idx_img from the committed rocprofv3 --pmc summary
+    (profiles/*replay_img_pmc*.json): FETCH_SIZE doubled — the index streams are 16-B/lane
+    coalesced reads, which gfx950's FETCH_SIZE reports at exactly half (MI355X_MICROARCH.md
+    §HBM) — plus WRITE_SIZE; the raw sum beside it."""
+    import re
+    cands = sorted(ROOT.glob("profiles/*replay_img_pmc*.json"),
+                   key=lambda p: [int(v) for v in re.findall(r"\d+", p.name)])
+    if not cands:
+        return None, None
+    try:
+        d = json.loads(cands[-1].read_text())
+        g = d["by_grid"][d.get("timed_grid") or next(iter(d["by_grid"]))]
+        return (2 * g["FETCH_SIZE"] + g["WRITE_SIZE"]) * 1024, \
+            (g["FETCH_SIZE"] + g["WRITE_SIZE"]) * 1024
+    except Exception:
+        return None, None
+
+
 def incomplete_replay(X, Z, shards, B, reps=20):
     """UnNB in replay mode (compute_stats.py:37-42 via UB): B explicit index pairs per shard,
     as NumPy's randint hands them over after the drop-in's bound check narrows them to int32
@@ -481,6 +500,7 @@ def incomplete_replay(X, Z, shards, B, reps=20):
     want = (X[ix64] > Z[iz64]).view(shards, B).sum(1)
     pairs = shards * B
     bpp = 8  # algorithmic bytes per pair: two int32 indices
+    traffic, traffic_raw = pmc_replay_traffic()
     return {"note": "UnNB replay mode: B explicit int32 index pairs per shard resident in HBM "
                     "(NumPy-drawn and narrowed after the bound check in the drop-in path; "
                     "device-drawn here); tw_count_pairs_idx32_ws: k_count_idx_img compares "
@@ -498,11 +518,16 @@ def incomplete_replay(X, Z, shards, B, reps=20):
             "roofline": {"bound": "hbm", "kernel": "k_count_idx_img",
                          "achieved": bpp * pairs / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": bpp * pairs / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "kernel_ms": kms,
+                         "kernel_ms": kms, "traffic": traffic, "traffic_raw": traffic_raw,
+                         "algorithmic_bytes": bpp * pairs,
                          "note": "8 algorithmic bytes per pair (two int32 indices, SURVEY.md "
                                  "§8(d)); kernel_ms = the whole call: one kernel that stages "
                                  "each shard's float32 score images in LDS and streams the "
-                                 "index pairs (csrc/imagecount.hip)"}}
+                                 "index pairs (csrc/imagecount.hip); traffic = HBM bytes per "
+                                 "launch from the committed rocprofv3 --pmc summary "
+                                 "(profiles/r02_replay_img_pmc.json): FETCH_SIZE x2 (16-B/lane "
+                                 "streaming reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE; "
+                                 "traffic_raw uncorrected"}}
 
 
 def spawn_ranks(n: int, script: str | None = None, argv: list | None = None) -> int:
