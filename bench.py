@@ -411,11 +411,16 @@ def pmc_traffic():
     # newest round/session first: natural order of the numbers in the name (r01s27 > r01s5)
     cands = sorted(ROOT.glob("profiles/*count_pmc*.json"),
                    key=lambda p: [int(v) for v in re.findall(r"\d+", p.name)])
-    if not cands:
-        return None, None
-    try:
-        d = json.loads(cands[-1].read_text())
-    except Exception:
+    d = None
+    for c in reversed(cands):  # the newest summary OF THIS KERNEL (other kernels' files match)
+        try:
+            e = json.loads(c.read_text())
+        except Exception:
+            continue
+        if str(e.get("kernel", "")).startswith("k_count_complete"):
+            d = e
+            break
+    if d is None:
         return None, None
     plain = d.get("by_grid", {}).get(d.get("plain_grid") or "", {}).get("hbm_bytes_per_launch")
     return d.get("hbm_bytes_per_launch"), plain
