@@ -822,8 +822,11 @@ def main():
                                "main.py:72-74) + device repartition per step",
                    "n_per_class_per_gpu": n, "shards_per_gpu": args.shards,
                    "pairs_per_step_per_gpu": pairs_per_step_rank,
-                   "parallelism": (f"dp{world}: shards over ranks, RCCL all-to-all repartition "
-                                   f"+ all-reduce of counts" if world > 1 else
+                   "parallelism": (f"dp{world}: shards over ranks, "
+                                   + ("RCCL" if os.environ.get("TW_BENCH_BACKEND", "nccl")
+                                      == "nccl" else "gloo (rehearsal)")
+                                   + " all-to-all repartition + all-reduce of counts"
+                                   if world > 1 else
                                    "dp1: one GPU, device Feistel repartition fused into the "
                                    "count launch")},
         "roofline": {"bound": "valu", "kernel": "k_count_complete",
