@@ -19,6 +19,25 @@
 #include "sgd_common.h"
 #include <algorithm>
 
+// Per-block timestamps of the streaming wide kernel for studies (tools/phase_hinge.py builds
+// a separate library with -DTW_HINGE_TIMING; the product build compiles them out): thread 0
+// stamps the 100 MHz wall clock at 0 entry, 1 rows resolved, 2 first chunk reduced, 3 exit.
+#ifdef TW_HINGE_TIMING
+__device__ unsigned long long g_hg_t[1 << 14];
+#define HG_STAMP(p)                                                                        \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_hg_t[((size_t)blockIdx.x * 4 + (p)) & 0x3FFF] = wall_clock64(); \
+  } while (0)
+extern "C" int tw_debug_hinge_times(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hg_t), sizeof(unsigned long long) * n) ==
+                 hipSuccess ? 0 : 2;
+}
+#else
+#define HG_STAMP(p) \
+  do {              \
+  } while (0)
+#endif
+
 namespace tw {
 
 constexpr int kLdsDoubles = 8192;  // 64 KiB of diff rows per block
@@ -292,6 +311,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
   double acc = 0.0;  // thread j < d: column j
   double zv[2][kWideCols], xv[2][kWideCols];
 
+  HG_STAMP(0);
   for (int64_t P0 = 0; P0 < B; P0 += kIdxPhase) {
     const int np = (int)std::min<int64_t>(kIdxPhase, B - P0);
     __syncthreads();  // the previous phase's readers of prx/prz and diff/flag are done
@@ -310,6 +330,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
       prz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
     }
     __syncthreads();
+    if (P0 == 0) HG_STAMP(1);
 
     auto load = [&](int st, int c0) {  // this wave's pair of the chunk at c0 into stage st
       const int t = c0 + wid;
@@ -343,6 +364,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
       }
       if (c0 + 2 * kStreamCH < np) load(st, c0 + 2 * kStreamCH);  // refill: chunk k+2
       __syncthreads();
+      if (P0 == 0 && c0 == 0) HG_STAMP(2);
       if (threadIdx.x < dd) {
         const int j = threadIdx.x;
         double a = acc;
@@ -368,6 +390,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     if (c0 < np) chunk(0, c0);
   }
   if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
+  HG_STAMP(3);
 }
 
 // One whole SGD step for narrow rows (d <= 32, C4) in ONE launch: the update of the PREVIOUS
