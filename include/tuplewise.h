@@ -200,6 +200,9 @@ int tw_count_rng_set_codes(int32_t by_bucket);
  * blocks per shard (0 = plan) and 16-B index vectors per stream and batch (1, 2, 4; + 8 =
  * nontemporal index loads; default 9). */
 int tw_count_img_set_plan(int32_t parts, int32_t u);
+/* Tuning hook: Philox blocks each thread of the device-RNG image kernel draws per iteration
+ * (1, 2 — the default — or 4; independent chains for the scheduler).  No effect on results. */
+int tw_count_rng_img_set_unroll(int32_t qu);
 int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d_z,
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, int64_t B, uint64_t seed, uint64_t shard_base,

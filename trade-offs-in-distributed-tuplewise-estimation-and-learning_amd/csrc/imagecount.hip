@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kImgThreads) void k_count_idx_img(
 
 // Device RNG: the draws of tw_count_pairs_rng (Philox block q -> pairs 2q and 2q+1, Lemire
 // maps; csrc/count.hip k_count_rng) compared on the images.
-template <typename T, int PRED>
+template <typename T, int PRED, int QU>
 __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, int64_t B, int parts, uint32_t k0, uint32_t k1,
@@ -233,31 +233,40 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
     const int64_t nq = (B + 1) / 2;
     const int64_t per = (nq + parts - 1) / parts;
     const int64_t q0 = (int64_t)part * per, q1 = std::min<int64_t>(nq, q0 + per);
-    // trip count uniform over the block (q1 - q0 is), so the ballot below is wave-uniform
-    for (int64_t qb = q0; qb < q1; qb += kImgThreads) {
-      const int64_t q = qb + threadIdx.x;
-      const bool live = q < q1;
-      uint32_t i0 = 0, j0 = 0, i1 = 0, j1 = 0;
-      bool two = false;
-      if (live) {
-        const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
-        i0 = lemire_index(r.a, (uint32_t)nx, q, ss, 0, k0, k1);
-        j0 = lemire_index(r.b, (uint32_t)nz, q, ss, 1, k0, k1);
-        two = 2 * q + 1 < B;
-        if (two) {
-          i1 = lemire_index(r.c, (uint32_t)nx, q, ss, 2, k0, k1);
-          j1 = lemire_index(r.d, (uint32_t)nz, q, ss, 3, k0, k1);
-        }
+    // trip count uniform over the block (q1 - q0 is), so the ballot below is wave-uniform.
+    // QU Philox blocks per thread and iteration, computed unconditionally (a dead lane's draw
+    // is discarded): independent chains the scheduler interleaves (16 waves per CU only).
+    for (int64_t qb = q0; qb < q1; qb += (int64_t)QU * kImgThreads) {
+      u32x4 r[QU];
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int64_t q = qb + (int64_t)u * kImgThreads + threadIdx.x;
+        r[u] = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
       }
-      bool u0, u1;
-      const unsigned r0 = image_cmp<PRED>(lx[i0], lz[j0], u0);
-      const unsigned r1 = image_cmp<PRED>(lx[i1], lz[j1], u1);
-      u0 = u0 && live;
-      u1 = u1 && two;
-      acc += (live && !u0 ? r0 : 0u) + (two && !u1 ? r1 : 0u);
-      if (__builtin_expect(__ballot(u0 || u1) != 0, 0)) {
-        if (u0) acc += exact_cmp<T, PRED>(x[xb + i0], z[zb + j0]);
-        if (u1) acc += exact_cmp<T, PRED>(x[xb + i1], z[zb + j1]);
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int64_t q = qb + (int64_t)u * kImgThreads + threadIdx.x;
+        const bool live = q < q1;
+        const bool two = live && 2 * q + 1 < B;
+        uint32_t i0 = 0, j0 = 0, i1 = 0, j1 = 0;
+        if (live) {
+          i0 = lemire_index(r[u].a, (uint32_t)nx, q, ss, 0, k0, k1);
+          j0 = lemire_index(r[u].b, (uint32_t)nz, q, ss, 1, k0, k1);
+          if (two) {
+            i1 = lemire_index(r[u].c, (uint32_t)nx, q, ss, 2, k0, k1);
+            j1 = lemire_index(r[u].d, (uint32_t)nz, q, ss, 3, k0, k1);
+          }
+        }
+        bool u0, u1;
+        const unsigned r0 = image_cmp<PRED>(lx[i0], lz[j0], u0);
+        const unsigned r1 = image_cmp<PRED>(lx[i1], lz[j1], u1);
+        u0 = u0 && live;
+        u1 = u1 && two;
+        acc += (live && !u0 ? r0 : 0u) + (two && !u1 ? r1 : 0u);
+        if (__builtin_expect(__ballot(u0 || u1) != 0, 0)) {
+          if (u0) acc += exact_cmp<T, PRED>(x[xb + i0], z[zb + j0]);
+          if (u1) acc += exact_cmp<T, PRED>(x[xb + i1], z[zb + j1]);
+        }
       }
     }
   }
@@ -353,23 +362,36 @@ template int launch_idx_images<int64_t>(const void*, const int64_t*, const void*
                                         int32_t, const int64_t*, const int64_t*, const int64_t*,
                                         int32_t, int32_t, const ImgPlan&, uint64_t*, hipStream_t);
 
-template <typename T, int PRED>
-static int launch_rng_img_t(const void* x, const int64_t* x_off, const void* z,
+template <typename T, int PRED, int QU>
+static int launch_rng_img_q(const void* x, const int64_t* x_off, const void* z,
                             const int64_t* z_off, int32_t n_shards, int64_t B, uint64_t seed,
                             uint64_t sid, const ImgPlan& p, uint64_t* out, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_img<T, PRED>,
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_img<T, PRED, QU>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024 - 1024));
     attr = true;
   }
-  hipLaunchKernelGGL((k_count_rng_img<T, PRED>), dim3(n_shards * p.parts), dim3(kImgThreads),
-                     p.lds, st, (const T*)x, x_off, (const T*)z, z_off, B, p.parts,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
+  hipLaunchKernelGGL((k_count_rng_img<T, PRED, QU>), dim3(n_shards * p.parts),
+                     dim3(kImgThreads), p.lds, st, (const T*)x, x_off, (const T*)z, z_off, B,
+                     p.parts, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
                      (unsigned long long*)out);
   TW_LAUNCH_CHECK();
   return TW_OK;
+}
+
+static int g_img_rng_qu = 2;  // tuning: Philox blocks per thread and iteration (1, 2, 4)
+
+template <typename T, int PRED>
+static int launch_rng_img_t(const void* x, const int64_t* x_off, const void* z,
+                            const int64_t* z_off, int32_t n_shards, int64_t B, uint64_t seed,
+                            uint64_t sid, const ImgPlan& p, uint64_t* out, hipStream_t st) {
+  if (g_img_rng_qu == 4)
+    return launch_rng_img_q<T, PRED, 4>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+  if (g_img_rng_qu == 2)
+    return launch_rng_img_q<T, PRED, 2>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+  return launch_rng_img_q<T, PRED, 1>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
 }
 
 int launch_rng_images(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
@@ -386,6 +408,12 @@ int launch_rng_images(const void* x, const int64_t* x_off, const void* z, const 
 }
 
 }  // namespace tw
+
+extern "C" int tw_count_rng_img_set_unroll(int32_t qu) {
+  TW_ARG_CHECK(qu == 1 || qu == 2 || qu == 4, "tw_count_rng_img_set_unroll: 1, 2 or 4");
+  tw::g_img_rng_qu = qu;
+  return TW_OK;
+}
 
 extern "C" int tw_count_img_set_plan(int32_t parts, int32_t u) {
   // u: 1, 2 or 4 index vectors per stream and batch; + 8: nontemporal index loads
