@@ -707,7 +707,8 @@ def test_grad_complete_block_drop_in(gpu):
 @pytest.mark.parametrize("dtype_name", ["f64", "i64"])
 @pytest.mark.parametrize("pred_name", ["gt", "half"])
 @pytest.mark.parametrize("zmax,codes", [(20000, "sort"), (16384, "bucket"), (16384, "sort"),
-                                        (16384, "images"), (20000, "images")])
+                                        (16384, "images"), (20000, "images"), (16384, "images1"),
+                                        (16384, "images4")])
 def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name, zmax, codes):
     """tw_count_pairs_rng_ws (float32 images or rank codes in LDS) == tw_count_pairs_rng (score
     gathers) == oracle, on tie-heavy shards with NaN, -0.0/+0.0, +-inf and ragged sizes (incl.
@@ -718,7 +719,9 @@ def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name, 
     from tuplewise.device import HipOps
     rng = np.random.RandomState(21)
     nxs, nzs = [1000, 1, 0, 4097, 3000, 500], [700, 5, 9, zmax, 1, 600]
-    L.call("tw_count_rng_set_codes", {"bucket": 1, "sort": 0, "images": 3}[codes])
+    L.call("tw_count_rng_set_codes", {"bucket": 1, "sort": 0}.get(codes, 3))
+    # images1 / images4: 1 or 4 Philox blocks per thread and iteration (default 2)
+    L.call("tw_count_rng_img_set_unroll", int(codes[6:]) if codes[6:] else 2)
     if dtype_name == "f64":
         xs = [rng.randint(-20, 20, n).astype(np.float64) for n in nxs]
         zs = [rng.randint(-20, 20, n).astype(np.float64) for n in nzs]
@@ -746,6 +749,7 @@ def test_device_rng_ranked_matches_plain_and_oracle(gpu, dtype_name, pred_name, 
         ranked = ops.count_rng(*args, max_nx=max(nxs), max_nz=max(nzs)).cpu().numpy()
     finally:
         L.call("tw_count_rng_set_codes", 3)
+        L.call("tw_count_rng_img_set_unroll", 2)
     plain = ops.count_rng(*args).cpu().numpy()
     assert np.array_equal(ranked, plain)
     for s in range(len(nxs)):
