@@ -106,3 +106,56 @@ def test_rccl_communicator_one_device(gpu):
     with pytest.raises(ValueError):
         two = (ctypes.c_int32 * 2)(0, 0)
         L.call("tw_comm_init", 2, two, ctypes.byref(c))
+
+
+# ------------------------------------------------------------ learning over device slots
+def _learn_p(golden, n_it=60):
+    return {"n_it": n_it, "margin": 1, "N": 10, "B": 20, "reshuffle_mod": 5, "reg": 0.05,
+            "learning_rate": 0.01, "eval_mod": 25, "w_init": golden["learn/w0"],
+            "test_X": golden["learn/test_X"], "test_Z": golden["learn/test_Z"],
+            "train_mon_pairs": [tuple(p) for p in golden["learn/mon"]],
+            "train_X": golden["learn/X"], "train_Z": golden["learn/Z"]}
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+@pytest.mark.parametrize("per_step", [False, True])
+def test_learning_process_over_slots_equals_one_device(gpu, golden, mode, per_step):
+    """learning_process(devices=[0, 0]): two slots (own streams) own 5 shards each, gather the
+    shard gradients in shard order and apply the same update — the evaluation history and the
+    w trajectory are identical to one device, in replay and device-RNG mode, per step and in
+    segments."""
+    import tuplewise.learning as lr
+    X, Z = golden["learn/X"], golden["learn/Z"]
+    out = []
+    for devices in (None, [0, 0]):
+        p = _learn_p(golden)
+        traj = [] if per_step else None
+        np.random.seed(11)
+        lr.learning_process(X, Z, p, rng_mode=mode, trajectory=traj, devices=devices)
+        out.append((p["norm_w"], p["bc_AUC"], p["tr_AUC"], traj,
+                    np.random.randint(0, 2 ** 31)))
+    a, b = out
+    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2] and a[4] == b[4]
+    if per_step:
+        assert len(a[3]) == len(b[3]) and all(np.array_equal(u, v) for u, v in zip(a[3], b[3]))
+
+
+def test_learning_devices_wide_rows_over_three_slots(gpu):
+    """d = 64 wide rows, N = 9 shards over the slots [0, 0, 0], device RNG, against one
+    device: the same history."""
+    import tuplewise.learning as lr
+    rng = np.random.RandomState(4)
+    n, d = 3000, 64
+    X = rng.normal(0.3, 1.0, size=(n, d))
+    Z = rng.normal(0.0, 1.0, size=(n, d))
+    hist = []
+    for devices in (None, [0, 0, 0]):
+        mon = np.random.RandomState(1)
+        p = {"N": 9, "B": 64, "margin": 1.0, "reg": 0.01, "learning_rate": 0.05, "n_it": 40,
+             "reshuffle_mod": 10, "eval_mod": 20, "w_init": np.full((d, 1), 0.01),
+             "test_X": X[:500], "test_Z": Z[:500], "train_X": X, "train_Z": Z,
+             "train_mon_pairs": list(zip(mon.randint(0, n, 300), mon.randint(0, n, 300)))}
+        np.random.seed(7)
+        lr.learning_process(X, Z, p, rng_mode="device", devices=devices)
+        hist.append((p["norm_w"], p["tr_AUC"]))
+    assert hist[0] == hist[1]

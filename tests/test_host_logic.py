@@ -143,3 +143,23 @@ def test_multi_device_split_and_device_list(monkeypatch):
         assert M.slots_for(1 << 40, 5) == [2, 3]
     finally:
         M.set_devices(None)
+
+
+def test_learning_engine_device_selection(monkeypatch):
+    """learning_process's device choice (learning._engine_devices): explicit lists are used
+    (trimmed so the shards split evenly), the automatic choice spreads only steps that gather
+    >= 1 GiB of rows, and partitioned / complete / multi-rank runs stay on one device."""
+    import tuplewise.learning as lr
+    from tuplewise import _multi as M
+    f = lr._engine_devices
+    assert f([0, 1], 10, 20, 10, None, "replicated", "incomplete") == [0, 1]
+    assert f([0, 1, 2], 10, 20, 10, None, "replicated", "incomplete") == [0, 1]  # 10 % 3
+    assert f([0], 10, 20, 10, None, "replicated", "incomplete") is None
+    with pytest.raises(ValueError):
+        f([0, 1], 10, 20, 10, None, "partitioned", "incomplete")
+    assert f(None, 10, 20, 10, None, "replicated", "complete") is None
+    monkeypatch.setattr(M, "_DEVICES", [0, 1, 2, 3, 4, 5, 6, 7])
+    # C5 at B = 100: 256*100*512*16 B = 0.2 GB per step -> one device; at B = 4096: 8.6 GB
+    assert f(None, 256, 100, 512, None, "replicated", "incomplete") is None
+    assert f(None, 256, 4096, 512, None, "replicated", "incomplete") == list(range(8))
+    assert f(None, 100, 4096, 512, None, "replicated", "incomplete") == [0, 1, 2, 3, 4]

@@ -16,6 +16,7 @@ the value the reference passes to grad_inc_block at make_exps.py:130.
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 
 import numpy as np
@@ -51,12 +52,20 @@ class SGDEngine:
     through an identity row table, so the arithmetic — and the trajectory — is unchanged."""
 
     def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None,
-                 x_layout="replicated", loss="hinge", gradient="incomplete"):
-        """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is)."""
+                 x_layout="replicated", loss="hinge", gradient="incomplete", vgroup=None):
+        """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is).
+        vgroup=(G, r): slot r of G on ONE process (MultiDeviceSGD): shards as rank r, but the
+        shard gradients are gathered and the update applied by the driver (_apply_update)."""
         t = L.torch()
         self.t = t
         self.group = group
-        if group is not None:
+        self.vgroup = vgroup
+        if vgroup is not None:
+            if group is not None:
+                raise ValueError("vgroup and group are exclusive")
+            self.dist = None
+            self.G, self.rank = int(vgroup[0]), int(vgroup[1])
+        elif group is not None:
             import torch.distributed as dist
             self.dist = dist
             self.G, self.rank = dist.get_world_size(group), dist.get_rank(group)
@@ -237,11 +246,16 @@ class SGDEngine:
         L.call("tw_row_unpack", L.ptr(recv), m, d, L.ptr(out), s)
 
     def _update(self):
-        s = L.stream_handle()
+        if self.vgroup is not None:  # MultiDeviceSGD gathers the slots' gradients, then updates
+            return
         if self.G > 1:
             self.dist.all_gather_into_tensor(self.grads, self.grads_loc, group=self.group)
+        self._apply_update()
+
+    def _apply_update(self):
         L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
-               self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr), s)
+               self.d, self.reg, self.lr, self.momentum, L.ptr(self.step_ctr),
+               L.stream_handle())
 
     def step_complete(self):
         """One step with the complete-block gradient (all kx*kz pairs of every local shard,
@@ -257,13 +271,17 @@ class SGDEngine:
                L.ptr(self.grads_loc), L.stream_handle())
         self._update()
 
-    def step(self, ix, iz, scores=None):
+    def step(self, ix, iz, scores=None, local=False):
         """Replay mode: ix, iz are the (N, B) NumPy draws of every shard (host arrays or
-        device tensors).  scores: an (N_loc, B) float64 device tensor that receives every
-        pair's S = diff . w + margin as the kernel computed it (tw_pair_grad_audit)."""
+        device tensors; local=True: already this engine's (N_loc, B) rows, on its device).
+        scores: an (N_loc, B) float64 device tensor that receives every pair's
+        S = diff . w + margin as the kernel computed it (tw_pair_grad_audit)."""
         t = self.t
-        ixd = self._local(ix) if isinstance(ix, t.Tensor) else L.to_device(self._local(ix))
-        izd = self._local(iz) if isinstance(iz, t.Tensor) else L.to_device(self._local(iz))
+        if local:
+            ixd, izd = ix, iz
+        else:
+            ixd = self._local(ix) if isinstance(ix, t.Tensor) else L.to_device(self._local(ix))
+            izd = self._local(iz) if isinstance(iz, t.Tensor) else L.to_device(self._local(iz))
         if scores is not None:
             L.call("tw_pair_grad_audit", L.ptr(self.X), L.ptr(self.Z), self.d,
                    L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ixd),
@@ -433,6 +451,181 @@ class SGDEngine:
             reshuffle_first = False
 
 
+class MultiDeviceSGD:
+    """learning_process's engine over several devices of ONE process (the
+    reference's N workers are a serial in-process loop, make_exps.py:126-141 calling UN_split,
+    compute_stats.py:44-46).  Slot r (one SGDEngine per device, its own stream) owns shards
+    [r*N/G, (r+1)*N/G) with replicated X and Z; every step each slot computes its shards'
+    gradients, the (N/G, d) blocks are all-gathered in shard order — RCCL (tw_allgather_f64)
+    when the devices are distinct, stream-ordered device copies otherwise — and every slot
+    applies the same shard-ordered update, so w (hence the trajectory) is identical to one
+    device bit for bit.  Eager launches (no graphs); replicated layout, incomplete gradient.
+    Device lists may repeat a device (tests run [0, 0] on a one-GPU box)."""
+
+    def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, devices,
+                 loss="hinge"):
+        from . import _multi as M
+        t = L.torch()
+        self.t, self.M = t, M
+        devs = [int(v) for v in devices]
+        self.G = len(devs)
+        if self.G < 2 or int(N) % self.G:
+            raise ValueError(f"N={N} shards do not split over {self.G} devices")
+        self.slots = [M._Slot(dev, k) for k, dev in enumerate(devs)]
+        self.subs = []
+        for r, slot in enumerate(self.slots):
+            with slot:
+                self.subs.append(SGDEngine(X, Z, w_init, N, B, margin, reg, learning_rate,
+                                           optim_type, loss=loss, vgroup=(self.G, r)))
+        e0 = self.subs[0]
+        self.N, self.B, self.d, self.kx, self.kz = e0.N, e0.B, e0.d, e0.kx, e0.kz
+        self.N_loc, self.complete, self.layout, self.fused = e0.N_loc, False, "replicated", False
+        self.comm = M._comm(tuple(devs)) if len(set(devs)) == len(devs) else None
+        self.rows_x = None
+
+    # ---------------------------------------------------------------- per step
+    def _gather_update(self):
+        """All slots' (N_loc, d) gradients -> every slot's (N, d) buffer, then the update."""
+        t, subs, slots = self.t, self.subs, self.slots
+        if self.comm is not None:
+            P = ctypes.c_void_p * self.G
+            L.call("tw_allgather_f64", self.comm, P(*[e.grads_loc.data_ptr() for e in subs]),
+                   P(*[e.grads.data_ptr() for e in subs]), self.N_loc * self.d,
+                   P(*[sl.stream.cuda_stream for sl in slots]))
+        else:
+            evs = []
+            for sl in slots:
+                with sl:
+                    ev = t.cuda.Event()
+                    ev.record()
+                    evs.append(ev)
+            for sl, e in zip(slots, subs):
+                with sl:
+                    for ev in evs:
+                        t.cuda.current_stream().wait_event(ev)
+                    for r, o in enumerate(subs):
+                        e.grads[r * self.N_loc:(r + 1) * self.N_loc].copy_(o.grads_loc)
+        for sl, e in zip(slots, subs):
+            with sl:
+                e._apply_update()
+        # a slot's next gradients overwrite grads_loc, which the others' copies read
+        if self.comm is None:
+            evs = []
+            for sl in slots:
+                with sl:
+                    ev = t.cuda.Event()
+                    ev.record()
+                    evs.append(ev)
+            for sl in slots:
+                with sl:
+                    for ev in evs:
+                        t.cuda.current_stream().wait_event(ev)
+
+    def step(self, ix, iz, scores=None):
+        if scores is not None:
+            raise ValueError("sign_audit runs on one device")
+        for sl, e in zip(self.slots, self.subs):
+            with sl:
+                e.step(ix, iz)
+        self._gather_update()
+
+    def set_shards(self, rows_x, rows_z):
+        for sl, e in zip(self.slots, self.subs):
+            with sl:
+                e.set_shards(rows_x, rows_z)
+        self.rows_x = True
+
+    def run_replay_segment(self, draws_dev, nsteps: int, graphs: bool = True, tag=0):
+        """nsteps replay steps, eagerly: each slot gets its shards' draws on its device."""
+        t = self.t
+        caller = t.cuda.current_stream()  # the draws were uploaded on it
+        loc = []
+        for sl, e in zip(self.slots, self.subs):
+            with sl:
+                t.cuda.current_stream().wait_stream(caller)
+                a = e.shard_base
+                loc.append(draws_dev[:nsteps, :, a:a + e.N_loc].to(L.device(), non_blocking=True)
+                           .contiguous())
+        for sl in self.slots:  # the draw buffer is refilled on the caller's stream later
+            caller.wait_stream(sl.stream)
+        for st in range(nsteps):
+            for sl, e, dl in zip(self.slots, self.subs, loc):
+                with sl:
+                    e.step(dl[st, 0], dl[st, 1], local=True)
+            self._gather_update()
+
+    # ---------------------------------------------------------------- device RNG
+    def enable_device_rng(self, seed: int):
+        for sl, e in zip(self.slots, self.subs):
+            with sl:
+                e.enable_device_rng(seed)
+        self.rows_x = True
+
+    def reshuffle_device(self):
+        for sl, e in zip(self.slots, self.subs):
+            with sl:
+                e.reshuffle_device()
+
+    def step_device(self):
+        for sl, e in zip(self.slots, self.subs):
+            with sl:
+                e.step_device()
+        self._gather_update()
+
+    def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True):
+        if reshuffle_first:
+            self.reshuffle_device()
+        for _ in range(nsteps):
+            self.step_device()
+
+    # ---------------------------------------------------------------- w
+    @property
+    def w(self):
+        """Slot 0's w, ordered after slot 0's queued steps on the caller's current stream."""
+        self.t.cuda.current_stream().wait_stream(self.slots[0].stream)
+        return self.subs[0].w
+
+    def w_host(self) -> np.ndarray:
+        with self.slots[0]:
+            return self.subs[0].w_host()
+
+    def w_host_async(self):
+        with self.slots[0]:
+            return self.subs[0].w_host_async()
+
+    def batch_view(self):
+        return None
+
+    def check(self):
+        pass
+
+
+MULTI_DEVICE_MIN_BYTES = 1 << 30  # gathered row bytes per step below which one device is used
+
+
+def _engine_devices(devices, N, B, d, group, x_layout, gradient):
+    """The device list learning_process spreads over, or None (one device): explicit
+    `devices`, else TW_DEVICES / every visible device once a step gathers >= 1 GiB of rows."""
+    from . import _multi as M
+    if group is not None or x_layout != "replicated" or gradient != "incomplete":
+        if devices is not None and len(devices) > 1:
+            raise ValueError("devices= needs group=None, x_layout='replicated' and the "
+                             "incomplete gradient")
+        return None
+    if devices is None:
+        devs = M.devices()
+        if len(devs) < 2 or 16 * N * B * d < MULTI_DEVICE_MIN_BYTES:
+            return None
+        devices = devs
+    devices = list(devices)
+    if len(devices) < 2:
+        return None
+    G = len(devices)
+    while G > 1 and N % G:
+        G -= 1
+    return devices[:G] if G > 1 else None
+
+
 def _dev_f64(a):
     t = L.torch()
     if isinstance(a, t.Tensor):
@@ -528,7 +721,7 @@ def sign_audit_step(X, Z, rows_x, rows_z, ix, iz, w, margin, scores) -> dict:
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                      rng_mode="replay", graphs=True, group=None, x_layout="replicated",
-                     loss="hinge", gradient="incomplete", sign_audit=None):
+                     loss="hinge", gradient="incomplete", sign_audit=None, devices=None):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference; the
@@ -548,7 +741,10 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     all pairs of every shard via per-point pair coefficients + X^T c; draws no pairs).
     sign_audit: a list (replay mode, one process, replicated X) that receives, per step,
     sign_audit_step's counts of near-zero scores and of hinge-filter disagreements between the
-    device's S and NumPy/BLAS's S; the steps then run one at a time."""
+    device's S and NumPy/BLAS's S; the steps then run one at a time.
+    devices: a list of devices for ONE process to spread the shards over (MultiDeviceSGD:
+    bit-identical trajectory); default None = TW_DEVICES / every visible device when a step
+    gathers >= 1 GiB of rows (C5 at large B), else one device."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -567,8 +763,14 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     logging.info("pairs_per_clust: %d ", (n_X / N) * (n_Z / N))
     logging.info("#eval_pairs_before_reshuffle: %d ", B * p_learn["reshuffle_mod"])
 
-    eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
-                    group=group, x_layout=x_layout, loss=loss, gradient=gradient)
+    devs = None if sign_audit is not None else _engine_devices(
+        devices, N, B, int(np.asarray(w).size), group, x_layout, gradient)
+    if devs is not None:
+        eng = MultiDeviceSGD(X, Z, w, N, B, margin, p_learn["reg"], learning_rate,
+                             optim_type, devs, loss=loss)
+    else:
+        eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
+                        group=group, x_layout=x_layout, loss=loss, gradient=gradient)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss)
