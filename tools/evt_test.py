@@ -1,3 +1,6 @@
+"""Clock warm-up probe for bench.py's settle phase (GPU box): times the one-launch UnN step
+(count_step, HIP events) over successive K-step runs from a cold start, showing the first ~10 ms
+of load run ~3 % slower."""
 import sys, time, pathlib
 sys.path.insert(0, "/root/repo")
 import torch, numpy as np
