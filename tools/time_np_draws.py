@@ -1,0 +1,24 @@
+"""Host speed of the replay draws (numpy_rng: one C4 step = 2 x 100 randint calls of 100 draws,
+kx = 91, kz = 7) per SIMD level, in fresh processes (TW_NP_RNG_ISA / TW_NP_RNG_SCALAR are read
+once per process).  Run on the GPU box: its host CPU is what the replay loop runs on."""
+import os
+import subprocess
+import sys
+
+CODE = r'''
+import sys, time; sys.path.insert(0, ".")
+import numpy as np
+from tuplewise.numpy_rng import Session
+np.random.seed(0)
+s = Session()
+out = np.empty((25, 2, 100, 100), np.int64)
+best = 1e9
+for _ in range(30):
+    t0 = time.perf_counter(); s.pairs_steps(25, 100, 91, 7, 100, out); best = min(best, time.perf_counter() - t0)
+print("%.2f us/step" % (best / 25 * 1e6))
+'''
+for label, env in (("widest", {}), ("avx2", {"TW_NP_RNG_ISA": "avx2"}),
+                   ("portable", {"TW_NP_RNG_SCALAR": "1"})):
+    r = subprocess.run([sys.executable, "-c", CODE], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=120)
+    print(label, r.stdout.strip() or r.stderr[-300:], flush=True)

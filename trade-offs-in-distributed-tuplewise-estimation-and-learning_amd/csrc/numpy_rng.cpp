@@ -86,6 +86,77 @@ struct MT {
   }
 };
 
+// The 624-word twist with explicit vectors (the auto-vectorised loop above runs at ~1 ns per
+// word, as much as all the rest of a draw): key[i] = key[i+397] ^ twist(key[i], key[i+1]) for
+// i < 227 (reads only old words), then key[i] = key[i-227] ^ twist(...) for 227 <= i < 623
+// (key[i-227] is new; 227 exceeds the vector width, so lanes never read a word this same
+// vector writes), then the last word.  Same words as MT::generate.
+template <int W>
+struct TwistVec;
+template <>
+struct TwistVec<16> {
+  __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) static inline void step(uint32_t* key, int i,
+                                                                            int off) {
+    const __m512i up = _mm512_set1_epi32((int)kUpper), lo = _mm512_set1_epi32((int)kLower);
+    const __m512i one = _mm512_set1_epi32(1), ma = _mm512_set1_epi32((int)kMatrixA);
+    const __m512i a = _mm512_loadu_si512((const void*)(key + i));
+    const __m512i b = _mm512_loadu_si512((const void*)(key + i + 1));
+    const __m512i y = _mm512_or_si512(_mm512_and_si512(a, up), _mm512_and_si512(b, lo));
+    const __m512i mag = _mm512_and_si512(_mm512_sub_epi32(_mm512_setzero_si512(),
+                                                          _mm512_and_si512(y, one)), ma);
+    const __m512i src = _mm512_loadu_si512((const void*)(key + i + off));
+    _mm512_storeu_si512((void*)(key + i),
+                        _mm512_xor_si512(_mm512_xor_si512(src, _mm512_srli_epi32(y, 1)), mag));
+  }
+};
+template <>
+struct TwistVec<8> {
+  __attribute__((target("avx2"))) static inline void step(uint32_t* key, int i, int off) {
+    const __m256i up = _mm256_set1_epi32((int)kUpper), lo = _mm256_set1_epi32((int)kLower);
+    const __m256i one = _mm256_set1_epi32(1), ma = _mm256_set1_epi32((int)kMatrixA);
+    const __m256i a = _mm256_loadu_si256((const __m256i*)(key + i));
+    const __m256i b = _mm256_loadu_si256((const __m256i*)(key + i + 1));
+    const __m256i y = _mm256_or_si256(_mm256_and_si256(a, up), _mm256_and_si256(b, lo));
+    const __m256i mag = _mm256_and_si256(_mm256_sub_epi32(_mm256_setzero_si256(),
+                                                          _mm256_and_si256(y, one)), ma);
+    const __m256i src = _mm256_loadu_si256((const __m256i*)(key + i + off));
+    _mm256_storeu_si256((__m256i*)(key + i),
+                        _mm256_xor_si256(_mm256_xor_si256(src, _mm256_srli_epi32(y, 1)), mag));
+  }
+};
+
+template <int W>
+TW_INLINE void twist_vec(uint32_t* key) {
+  int i = 0;
+  for (; i + W <= kN - kM; i += W) TwistVec<W>::step(key, i, kM);  // 0 .. 227 (old words)
+  for (; i < kN - kM; ++i) {
+    const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+    key[i] = key[i + kM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+  }
+  for (; i + W <= kN - 1; i += W) TwistVec<W>::step(key, i, kM - kN);  // 227 .. 623
+  for (; i < kN - 1; ++i) {
+    const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+    key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+  }
+  const uint32_t y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+  key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+}
+
+// the twist for SIMD level kIsa (2: 16 lanes, 1: 8 lanes, 0: MT::generate's loops)
+template <int kIsa>
+TW_INLINE void generate_isa(MT& mt) {
+  if (kIsa == 2)
+    twist_vec<16>(mt.key);
+  else if (kIsa == 1)
+    twist_vec<8>(mt.key);
+  else {
+    mt.generate();
+    return;
+  }
+  mt.pos = 0;
+  mt.tempered_upto = 0;
+}
+
 inline uint64_t gen_mask(uint64_t max) {
   uint64_t m = max;
   m |= m >> 1;
@@ -138,7 +209,7 @@ __attribute__((target("avx2,popcnt"))) inline int pack8_avx2(const uint32_t* tmp
 }
 
 // the same with 16 lanes (AVX-512: compare to a mask register, compress the accepted lanes)
-__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) inline int pack16_avx512(
+__attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) inline int pack16_avx512(
     const uint32_t* tmp, int p, uint32_t mask, uint32_t r32, int64_t low, int64_t cnt,
     int64_t* out, int64_t& o) {
   const __m512i vm = _mm512_set1_epi32((int)mask);
@@ -158,7 +229,49 @@ __attribute__((target("avx2,avx512f,avx512vl,popcnt"))) inline int pack16_avx512
   return p;
 }
 
-// kIsa: 0 portable, 1 AVX2, 2 AVX-512 (+ AVX2 for the 8-lane remainder)
+// A whole masked-rejection call with 16-lane AVX-512 batches and no scalar tail: a batch past
+// the end of the 624-word block is a masked load, and the last batch of the call keeps only
+// the lowest `cnt - o` accepted lanes (pdep) and consumes the words up to the last of them —
+// NumPy stops drawing at the cnt-th accepted value.
+__attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) inline void fill_masked16(
+    MT& mt, uint32_t mask, uint32_t r32, int64_t low, int64_t cnt, int64_t* out) {
+  const __m512i vm = _mm512_set1_epi32((int)mask);
+  const __m512i vr = _mm512_set1_epi32((int)r32);
+  const __m512i vlow = _mm512_set1_epi64(low);
+  int64_t o = 0;
+  while (o < cnt) {
+    if (mt.pos >= kN) generate_isa<2>(mt);
+    mt.temper_rest();
+    int p = mt.pos;
+    while (p < kN && o < cnt) {
+      const int avail = kN - p;
+      const __mmask16 lm = avail >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << avail) - 1u);
+      const __m512i v = _mm512_and_si512(_mm512_maskz_loadu_epi32(lm, mt.tmp + p), vm);
+      uint32_t acc = (uint32_t)_mm512_mask_cmple_epu32_mask(lm, v, vr);
+      const int64_t rem = cnt - o;
+      int na = __builtin_popcount(acc);
+      int used = avail >= 16 ? 16 : avail;
+      if (na >= rem) {  // the call ends inside this batch: at its rem-th accepted word
+        if (na > rem) acc = _pdep_u32((1u << rem) - 1u, acc);
+        na = (int)rem;
+        used = 32 - __builtin_clz(acc);
+      }
+      const __m512i packed = _mm512_maskz_compress_epi32((__mmask16)acc, v);
+      const __m512i lo8 = _mm512_add_epi64(_mm512_cvtepu32_epi64(_mm512_castsi512_si256(packed)),
+                                           vlow);
+      const __m512i hi8 = _mm512_add_epi64(
+          _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(packed, 1)), vlow);
+      const uint32_t sm = (1u << na) - 1u;
+      _mm512_mask_storeu_epi64((void*)(out + o), (__mmask8)(sm & 0xFF), lo8);
+      _mm512_mask_storeu_epi64((void*)(out + o + 8), (__mmask8)(sm >> 8), hi8);
+      o += na;
+      p += used;
+    }
+    mt.pos = p;
+  }
+}
+
+// kIsa: 0 portable, 1 AVX2, 2 AVX-512 (+ BMI2)
 template <int kIsa>
 TW_INLINE void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int64_t* out) {
   const uint64_t rng = (uint64_t)(high - 1) - (uint64_t)low;
@@ -175,9 +288,13 @@ TW_INLINE void randint_fill(MT& mt, int64_t low, int64_t high, int64_t cnt, int6
     // accepted; raw draws come from a pre-tempered 624-word block
     const uint32_t mask = (uint32_t)gen_mask(rng);
     const uint32_t r32 = (uint32_t)rng;
+    if (kIsa == 2) {
+      fill_masked16(mt, mask, r32, low, cnt, out);
+      return;
+    }
     int64_t o = 0;
     while (o < cnt) {
-      if (mt.pos >= kN) mt.generate();
+      if (mt.pos >= kN) generate_isa<kIsa>(mt);
       mt.temper_rest();
       int p = mt.pos;
       if (kIsa >= 2) p = pack16_avx512(mt.tmp, p, mask, r32, low, cnt, out, o);
@@ -241,7 +358,7 @@ __attribute__((target("avx2,popcnt"))) int batch_avx2(uint32_t* key, int32_t* po
                                                       const int64_t* cnt, int64_t* out) {
   return batch_body<1>(key, pos, n, lo, hi, cnt, out);
 }
-__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) int batch_avx512(
+__attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) int batch_avx512(
     uint32_t* key, int32_t* pos, int32_t n, const int64_t* lo, const int64_t* hi,
     const int64_t* cnt, int64_t* out) {
   return batch_body<2>(key, pos, n, lo, hi, cnt, out);
@@ -255,7 +372,7 @@ __attribute__((target("avx2,popcnt"))) void pairs_avx2(uint32_t* key, int32_t* p
                                                        int64_t* ix, int64_t* iz) {
   pairs_body<1>(key, pos, N, kx, kz, B, ix, iz);
 }
-__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) void pairs_avx512(
+__attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) void pairs_avx512(
     uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B, int64_t* ix,
     int64_t* iz) {
   pairs_body<2>(key, pos, N, kx, kz, B, ix, iz);
@@ -296,7 +413,7 @@ __attribute__((target("avx2,popcnt"))) inline int shuffle8_avx2(const uint32_t* 
 }
 
 // the same with 16 lanes (sure accept v <= i - 15)
-__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) inline int shuffle16_avx512(
+__attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) inline int shuffle16_avx512(
     const uint32_t* tmp, int p, uint32_t mask, int64_t lo, int64_t& i, int64_t* j) {
   const __m512i vm = _mm512_set1_epi32((int)mask);
   const __m512i rev = _mm512_setr_epi32(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
@@ -331,7 +448,7 @@ void shuffle_draws(MT& mt, int64_t n, int64_t* j) {
   while (i >= 1) {
     const uint32_t mask = (uint32_t)gen_mask((uint64_t)i);
     const int64_t lo = (int64_t)(mask >> 1);  // this mask serves i in (mask/2, mask]
-    if (mt.pos >= kN) mt.generate();
+    if (mt.pos >= kN) generate_isa<kIsa>(mt);
     mt.temper_rest();
     int p = mt.pos;
     for (;;) {
@@ -384,13 +501,13 @@ void shuffle_apply(char* data, int64_t n, int64_t itemsize, const int64_t* j) {
 __attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t n, int64_t* j) {
   shuffle_draws<1>(mt, n, j);
 }
-__attribute__((target("avx2,avx512f,avx512vl,popcnt"))) void shuffle_draws_avx512(MT& mt,
+__attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) void shuffle_draws_avx512(MT& mt,
                                                                                   int64_t n,
                                                                                   int64_t* j) {
   shuffle_draws<2>(mt, n, j);
 }
 
-// SIMD level chosen once at run time: 2 AVX-512 (F + VL), 1 AVX2, 0 portable.
+// SIMD level chosen once at run time: 2 AVX-512 (F + VL) + BMI2, 1 AVX2, 0 portable.
 // TW_NP_RNG_SCALAR=1 forces the portable path, TW_NP_RNG_ISA=avx2 caps it at AVX2 (tests run
 // every level against NumPy).
 int isa_level() {
@@ -401,7 +518,10 @@ int isa_level() {
     if (!__builtin_cpu_supports("avx2") || !__builtin_cpu_supports("popcnt")) return 0;
     const char* cap = getenv("TW_NP_RNG_ISA");
     if (cap && strcmp(cap, "avx2") == 0) return 1;
-    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") ? 2 : 1;
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+                   __builtin_cpu_supports("bmi2")
+               ? 2
+               : 1;
   }();
   return v;
 }
