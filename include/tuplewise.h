@@ -368,9 +368,13 @@ int tw_sgd_segment(const double* d_X, const double* d_Z, int64_t d, const int64_
                    void* stream);
 
 /* ---- f1: scores = A @ w for a row-major (n, d) matrix (evaluation_step, make_exps.py:163,
- * :170-171).  Row dot products in index order. */
+ * :170-171).  d <= 32: row dot products in index order; d > 32: see tw_gemv_set_variant. */
 int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w, double* d_out,
                 void* stream);
+/* Tuning hook: 1 (default) computes rows of d > 32 one wave per row (lane-strided partial dots
+ * + a fixed butterfly, coalesced 16-B loads; 16-B aligned A and w), 0 = a thread per row in
+ * index order.  Scores may differ in the last ulp between the two (BLAS's order differs too). */
+int tw_gemv_set_variant(int32_t rows);
 
 /* ---- Row A6/A9/(e): repartition on the device ----------------------------------------
  * Keyed pseudo-random permutation of [0, n): a 6-round Feistel network over the smallest

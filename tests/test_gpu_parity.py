@@ -833,3 +833,32 @@ def test_sorted_count_bucket_equals_sort(gpu, dtype_name, mode):
         if mode == "half":
             want = 2 * want + int((x.reshape(-1, 1) == z.reshape(1, -1)).sum())
         assert int(got[0][s]) == want, s
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (1000, 10), (999, 33), (5000, 64), (3001, 101),
+                                 (2000, 512), (700, 1000)])
+@pytest.mark.parametrize("variant", [1, 0])
+def test_gemv_scores_match_numpy(gpu, n, d, variant):
+    """tw_gemv_f64 (evaluation_step's X.dot(w), make_exps.py:163, :170-171): a thread per row
+    in index order (d <= 32, or variant 0) or one wave per row (d > 32) — both within a few
+    ulp-scale of NumPy's BLAS product; odd d, d > 512 and an unaligned view included."""
+    import torch
+    from tuplewise import _lib as L
+    rng = np.random.RandomState(n + d)
+    A = rng.normal(size=(n, d))
+    w = rng.normal(size=d)
+    want = A.dot(w)
+    L.call("tw_gemv_set_variant", variant)
+    try:
+        Ad, wd = torch.from_numpy(A).cuda(), torch.from_numpy(w).cuda()
+        out = torch.empty(n, dtype=torch.float64, device="cuda")
+        L.call("tw_gemv_f64", L.ptr(Ad), n, d, L.ptr(wd), L.ptr(out), L.stream_handle())
+        scale = np.abs(A) @ np.abs(w)  # the dot product's rounding scale
+        assert np.all(np.abs(out.cpu().numpy() - want) <= 1e-13 * d * scale + 1e-300)
+        # an 8-B-aligned (not 16-B) view of the rows takes the thread-per-row kernel
+        big = torch.from_numpy(np.concatenate([[0.0], A.reshape(-1)])).cuda()
+        view = big[1:].view(n, d)
+        L.call("tw_gemv_f64", L.ptr(view), n, d, L.ptr(wd), L.ptr(out), L.stream_handle())
+        assert np.all(np.abs(out.cpu().numpy() - want) <= 1e-13 * d * scale + 1e-300)
+    finally:
+        L.call("tw_gemv_set_variant", 1)

@@ -86,6 +86,7 @@ _SIGNATURES = {
     "tw_sgd_segment": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i64, _f64,
                        _i32, _u64, _vp, _i32, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
+    "tw_gemv_set_variant": [_i32],
     "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],
     "tw_permute_pair": [_vp, _vp, _i64, _u64, _vp, _vp, _i64, _u64, _vp],
     "tw_perm_index": [_vp, _i64, _i64, _i64, _u64, _vp],

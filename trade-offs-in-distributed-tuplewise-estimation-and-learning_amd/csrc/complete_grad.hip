@@ -65,6 +65,16 @@ __global__ __launch_bounds__(kBlock) void k_row_scores(const double* __restrict_
   }
 }
 
+// A @ w for a row-major (n, d) matrix, one wave per row (tw_gemv_f64 for d > 32)
+int launch_row_scores(const double* A, int64_t d, int64_t n, const double* w, double* out,
+                      hipStream_t st) {
+  const int blocks = (int)std::min<int64_t>(256 * 16, ceil_div(n, kBlock / kWave));
+  hipLaunchKernelGGL(k_row_scores, dim3(blocks), dim3(kBlock), 0, st, A, d,
+                     (const int64_t*)nullptr, n, w, out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 // SIDE 0: coef of x-point i = sum_j phi'(sz_j - sx_i + m); SIDE 1: of z-point j, over i.
 template <int LOSS, int SIDE>
 __global__ __launch_bounds__(kBlock) void k_pair_coef(const double* __restrict__ s_own,

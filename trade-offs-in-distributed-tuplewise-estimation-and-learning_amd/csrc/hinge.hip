@@ -832,11 +832,23 @@ extern "C" int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d,
   return TW_OK;
 }
 
+static int g_gemv_rows = 1;  // tw_gemv_set_variant: 1 = wave per row for d > 32
+
+extern "C" int tw_gemv_set_variant(int32_t rows) {
+  TW_ARG_CHECK(rows == 0 || rows == 1, "tw_gemv_set_variant: 0 or 1");
+  g_gemv_rows = rows;
+  return TW_OK;
+}
+
 extern "C" int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w,
                            double* d_out, void* stream) {
   TW_ARG_CHECK(n >= 0 && d >= 1, "tw_gemv_f64: bad sizes");
   if (n == 0) return TW_OK;
   hipStream_t st = (hipStream_t)stream;
+  // wide rows: one wave per row, coalesced 16-B loads (a thread per row reads 64 rows per wave
+  // instruction, one line each); rows must be 16-B aligned for the double2 loads
+  if (d > 32 && g_gemv_rows && ((uintptr_t)d_A & 15) == 0 && ((uintptr_t)d_w & 15) == 0)
+    return launch_row_scores(d_A, d, n, d_w, d_out, st);
   const int blocks = (int)std::min<int64_t>(4096, ceil_div(n, kBlock));
   hipLaunchKernelGGL(k_gemv, dim3(blocks), dim3(kBlock), 0, st, d_A, n, d, d_w, d_out);
   TW_LAUNCH_CHECK();

@@ -23,4 +23,8 @@ constexpr int kWideMaxD = kWideCols * kWave;     // 512
 constexpr int kIdxPhase = 1024;                  // pairs whose rows are resolved per phase
 constexpr int kStreamCH = kWideBlock / kWave;    // 16 pairs per streaming chunk
 
+// csrc/complete_grad.hip: A @ w, one wave per row (lane-strided partial dot + fixed butterfly)
+int launch_row_scores(const double* A, int64_t d, int64_t n, const double* w, double* out,
+                      hipStream_t st);
+
 }  // namespace tw
