@@ -367,6 +367,20 @@ int tw_sgd_segment(const double* d_X, const double* d_Z, int64_t d, const int64_
                    double* d_grads, double reg, double lr, double momentum, uint32_t* d_ctl,
                    void* stream);
 
+/* ---- The hinge surrogate over ALL pairs of each shard in O((n + m) log m) (f64 scores):
+ * d_out[s] = sum_{i,j} max(fl(fl(z_j - x_i) + margin), 0) — cs.conv_AUC's sum
+ * (compute_stats.py:129-135) as evaluation_step's tc_AUC (make_exps.py:167-168) and
+ * SAME_AS_BATCH's bc_AUC (:154-157) need it.  For each x the positive terms are the top c of
+ * the shard's sorted z (a binary search with the exact predicate), summed from double-double
+ * prefix sums: the exact sum of the terms rounded once (vs NumPy's pairwise sum of rounded
+ * terms: ~1e-15 relative).  NaN / +-inf follow NumPy's elementwise semantics (NaN or +inf
+ * results).  Empty shards give 0.  d_work: tw_pair_hinge_sum_sorted_work_bytes bytes. */
+int64_t tw_pair_hinge_sum_sorted_work_bytes(int32_t n_shards, int64_t max_nx, int64_t max_nz);
+int tw_pair_hinge_sum_sorted(const double* d_x, const int64_t* d_x_off, const double* d_z,
+                             const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                             int64_t max_nz, double margin, void* d_work, double* d_out,
+                             void* stream);
+
 /* ---- f1: scores = A @ w for a row-major (n, d) matrix (evaluation_step, make_exps.py:163,
  * :170-171).  d <= 32: row dot products in index order; d > 32: see tw_gemv_set_variant. */
 int tw_gemv_f64(const double* d_A, int64_t n, int64_t d, const double* d_w, double* d_out,

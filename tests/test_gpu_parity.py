@@ -862,3 +862,65 @@ def test_gemv_scores_match_numpy(gpu, n, d, variant):
         assert np.all(np.abs(out.cpu().numpy() - want) <= 1e-13 * d * scale + 1e-300)
     finally:
         L.call("tw_gemv_set_variant", 1)
+
+
+def _hinge_both(xs, zs, margin):
+    from tuplewise import _engine as E, _lib as L
+    sh = E.Shards.from_blocks(xs, zs, L.TW_F64)
+    srt = E.pair_sum_complete_dev(sh, L.TW_KERN_HINGE, margin, "sorted").cpu().numpy()
+    prs = E.pair_sum_complete_dev(sh, L.TW_KERN_HINGE, margin, "pairs").cpu().numpy()
+    return srt, prs
+
+
+@pytest.mark.parametrize("sizes", [[(300, 77)], [(5000, 9000), (0, 10), (10, 0), (4096, 4097)],
+                                   [(1, 1), (17000, 3), (3, 12289), (1234, 5678)]])
+def test_hinge_sorted_equals_pairs(gpu, sizes):
+    """tw_pair_hinge_sum_sorted (top-c sums over sorted z, double-double prefix sums) vs the
+    all-pairs kernel and the oracle's conv_AUC (compute_stats.py:129-135) times the pair count,
+    on ragged and empty shards, partial sorted chunks and several x-tiles.  Tolerance: rtol
+    1e-12 (three summation orders of the same rounded-once terms; see hingesort.hip)."""
+    rng = np.random.RandomState(len(sizes) * 31 + sizes[0][0])
+    xs = [rng.normal(0.1, 1, nx) for nx, _ in sizes]
+    zs = [rng.normal(0, 1, nz) for _, nz in sizes]
+    for margin in (1.0, 0.0, -0.5):
+        srt, prs = _hinge_both(xs, zs, margin)
+        np.testing.assert_allclose(srt, prs, rtol=1e-12, atol=0)
+        for s, (x, z) in enumerate(zip(xs, zs)):
+            want = O.conv_AUC(margin)(x, z) * len(x) * len(z) if len(x) and len(z) else 0.0
+            np.testing.assert_allclose(srt[s], want, rtol=1e-12, atol=1e-300)
+
+
+def test_hinge_sorted_ties_exact(gpu):
+    """Integer-valued scores: S = fl(z - x) + margin is exactly 0 for many pairs (the boundary
+    of max(S, 0)) and every partial sum is an exact integer, so sorted == all-pairs == NumPy bit
+    for bit; several chunks of equal keys."""
+    rng = np.random.RandomState(5)
+    xs = [rng.randint(-6, 7, 9000).astype(np.float64), rng.randint(-2, 3, 300).astype(np.float64)]
+    zs = [rng.randint(-6, 7, 13000).astype(np.float64), np.zeros(5000)]
+    for margin in (0.0, 1.0, 3.0, -2.0):
+        srt, prs = _hinge_both(xs, zs, margin)
+        assert np.array_equal(srt, prs)
+        for s in range(2):
+            want = np.maximum(zs[s][None, :] - xs[s][:, None] + margin, 0).sum()
+            assert srt[s] == want
+
+
+def test_hinge_sorted_nonfinite(gpu):
+    """NaN / +-inf scores: the sorted path decides NumPy's elementwise outcome from counts (a NaN
+    term -> NaN, an infinite term -> +inf, zero terms from x = +inf or z = -inf), one shard per
+    case, next to finite shards that must stay exact."""
+    inf, nan = np.inf, np.nan
+    base_x, base_z = np.array([0.5, -1.0, 2.0]), np.array([1.0, 0.25, -3.0, 4.0])
+    cases = [([], []), ([nan], []), ([], [nan]), ([], [inf]), ([-inf], []), ([inf], []),
+             ([], [-inf]), ([inf], [inf]), ([-inf], [-inf]), ([inf], [-inf]), ([-inf], [inf])]
+    xs = [np.concatenate([base_x, np.array(a, dtype=np.float64)]) for a, _ in cases]
+    zs = [np.concatenate([base_z, np.array(b, dtype=np.float64)]) for _, b in cases]
+    xs.append(np.array([inf, inf]))  # all x = +inf: every term 0
+    zs.append(np.array([1.0, 2.0]))
+    for margin in (1.0, 0.0):
+        srt, prs = _hinge_both(xs, zs, margin)
+        with np.errstate(invalid="ignore"):
+            want = np.array([np.maximum(z[None, :] - x[:, None] + margin, 0).sum()
+                             for x, z in zip(xs, zs)])
+        np.testing.assert_array_equal(srt, want)
+        np.testing.assert_array_equal(prs, want)

@@ -294,12 +294,27 @@ def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
     return pair_sum_complete_dev(sh, kern, margin).cpu().numpy()
 
 
-def pair_sum_complete_dev(sh: Shards, kern: int, margin: float = 0.0):
-    """pair_sum_complete, enqueued only: the (n_shards,) float64 device tensor."""
+# hinge sums of shards with at least this many pairs use the O((n+m) log m) path
+HINGE_SORTED_MIN_PAIRS = 1 << 27
+
+
+def pair_sum_complete_dev(sh: Shards, kern: int, margin: float = 0.0, algo: str = "auto"):
+    """pair_sum_complete, enqueued only: the (n_shards,) float64 device tensor.  The hinge
+    kernel on float64 scores takes the sorted path (tw_pair_hinge_sum_sorted: top-c sums from
+    double-double prefix sums of the sorted z) when a shard has >= HINGE_SORTED_MIN_PAIRS
+    pairs (algo="auto") or always (algo="sorted"); algo="pairs" forces the all-pairs kernel."""
     n = sh.n_shards
     t = L.torch()
     xo, zo = sh.offsets_dev()
     max_nx, max_nz = int(sh.nx.max()), int(sh.nz.max())
+    if (kern == L.TW_KERN_HINGE and sh.dtype == L.TW_F64 and algo != "pairs"
+            and (algo == "sorted" or max_nx * max_nz >= HINGE_SORTED_MIN_PAIRS)):
+        nb = int(L.lib().tw_pair_hinge_sum_sorted_work_bytes(n, max_nx, max_nz))
+        work = L.empty((max(nb, 1),), t.uint8)
+        out = L.empty((n,), t.float64)
+        L.call("tw_pair_hinge_sum_sorted", L.ptr(sh.x), L.ptr(xo), L.ptr(sh.z), L.ptr(zo), n,
+               max_nx, max_nz, float(margin), L.ptr(work), L.ptr(out), L.stream_handle())
+        return out
     per = int(L.lib().tw_pair_sum_work_per_shard(max_nx, max_nz))
     work = L.empty((per * n,), t.float64)
     out = L.empty((n,), t.float64)

@@ -87,6 +87,8 @@ _SIGNATURES = {
                        _i32, _u64, _vp, _i32, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
     "tw_gemv_set_variant": [_i32],
+    "tw_pair_hinge_sum_sorted_work_bytes": [_i32, _i64, _i64],
+    "tw_pair_hinge_sum_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _f64, _vp, _vp, _vp],
     "tw_permute_scatter": [_vp, _vp, _i64, _u64, _vp],
     "tw_permute_pair": [_vp, _vp, _i64, _u64, _vp, _vp, _i64, _u64, _vp],
     "tw_perm_index": [_vp, _i64, _i64, _i64, _u64, _vp],
@@ -119,6 +121,7 @@ _RESTYPES = {
     "tw_pair_sum_work_per_shard": ctypes.c_int64,
     "tw_pair_sum_idx_work_per_shard": ctypes.c_int64,
     "tw_pair_grad_complete_work_bytes": ctypes.c_int64,
+    "tw_pair_hinge_sum_sorted_work_bytes": ctypes.c_int64,
 }
 
 _lib = None

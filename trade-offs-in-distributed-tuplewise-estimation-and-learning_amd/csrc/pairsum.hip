@@ -17,7 +17,10 @@ template <int K>
 __device__ __forceinline__ double fkern(double x, double z, double margin) {
   if constexpr (K == TW_KERN_PROD) return x * z;
   else if constexpr (K == TW_KERN_GINI) return fabs(x - z);
-  else if constexpr (K == TW_KERN_HINGE) return fmax(z - x + margin, 0.0);
+  else if constexpr (K == TW_KERN_HINGE) {  // np.maximum(t, 0): a NaN t stays NaN (not fmax)
+    const double t = z - x + margin;
+    return !(t <= 0.0) ? t : 0.0;
+  }
   else {  // TW_KERN_LOGISTIC: softplus as NumPy's logaddexp(0, t) evaluates it
     const double t = z - x + margin;
     return t == 0.0 ? 0.6931471805599453 : fmax(t, 0.0) + log1p(exp(-fabs(t)));
@@ -46,6 +49,22 @@ __device__ __forceinline__ double block_sum_f64(double v) {
   double b = 0.0;
   if (threadIdx.x == 0) b = (part[0] + part[1]) + (part[2] + part[3]);
   return b;
+}
+
+// bit 0: NaN, bit 1: +inf, bit 2: -inf
+__device__ __forceinline__ int nonfinite_bits(double v) {
+  const double inf = __longlong_as_double(0x7FF0000000000000ll);
+  return (v != v ? 1 : 0) | (v == inf ? 2 : 0) | (v == -inf ? 4 : 0);
+}
+
+// The all-pairs block sums the hinge with fmax (one v_max_f64 per pair; it drops NaN terms)
+// and restores NumPy's NaN afterwards: a pair's t = fl(z - x) + margin is NaN iff x or z is
+// NaN or both are infinite with the same sign, so the block's (x tile, z chunk) holds a NaN
+// term iff its non-finite bits say so.
+template <int K>
+__device__ __forceinline__ double fkern_loop(double x, double z, double margin) {
+  if constexpr (K == TW_KERN_HINGE) return fmax(z - x + margin, 0.0);
+  else return fkern<K>(x, z, margin);
 }
 
 template <int K>
@@ -84,13 +103,30 @@ __global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ 
   for (int j = 0; j < nz; ++j) {
     const double zv = zp[j];
 #pragma unroll
-    for (int r = 0; r < kSumR; ++r) acc[r] += fkern<K>(xv[r], zv, margin);
+    for (int r = 0; r < kSumR; ++r) acc[r] += fkern_loop<K>(xv[r], zv, margin);
   }
   double t = 0.0;
 #pragma unroll
   for (int r = 0; r < kSumR; ++r) t += valid[r] ? acc[r] : 0.0;
+  int xbits = 0, zbits = 0;
+  if constexpr (K == TW_KERN_HINGE) {
+#pragma unroll
+    for (int r = 0; r < kSumR; ++r) xbits |= valid[r] ? nonfinite_bits(xv[r]) : 0;
+    for (int j = threadIdx.x; j < nz; j += kBlock) zbits |= nonfinite_bits(zp[j]);
+  }
   const double b = block_sum_f64(t);
-  if (threadIdx.x == 0) work[blockIdx.x] = b;
+  if constexpr (K == TW_KERN_HINGE) {
+    xbits = __syncthreads_or(xbits & 1) | (__syncthreads_or(xbits & 2) ? 2 : 0) |
+            (__syncthreads_or(xbits & 4) ? 4 : 0);
+    zbits = __syncthreads_or(zbits & 1) | (__syncthreads_or(zbits & 2) ? 2 : 0) |
+            (__syncthreads_or(zbits & 4) ? 4 : 0);
+    if (threadIdx.x == 0)
+      work[blockIdx.x] = ((xbits | zbits) & 1) || (xbits & zbits & 6)
+                             ? __longlong_as_double(0x7FF8000000000000ll)
+                             : b;
+  } else {
+    if (threadIdx.x == 0) work[blockIdx.x] = b;
+  }
 }
 
 // I: int64_t or int32_t indices.  COUNT: the same pass also counts x > z per shard into

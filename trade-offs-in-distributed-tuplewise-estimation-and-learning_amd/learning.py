@@ -938,10 +938,8 @@ def _eval_device(wd, p_learn, loss, margin, fixed):
     parts = []
     n_pairs = 0
     if fixed:
-        tX = _CACHE.get("train_X", p_learn["train_X"],
-                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-        tZ = _CACHE.get("train_Z", p_learn["train_Z"],
-                        lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+        tX = _CACHE.get("train_X", p_learn["train_X"], _dev_f64)  # NumPy or device arrays
+        tZ = _CACHE.get("train_Z", p_learn["train_Z"], _dev_f64)
         # the monitor pairs live on the device for as long as p_learn holds the same list
         ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
         n_pairs = int(off[1])
@@ -958,10 +956,8 @@ def _eval_device(wd, p_learn, loss, margin, fixed):
                                           pair_off_dev=offd).view(t.float64)]
     else:
         parts.append(t.zeros((2,), dtype=t.float64, device=wd.device))
-    eX = _CACHE.get("test_X", p_learn["test_X"],
-                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
-    eZ = _CACHE.get("test_Z", p_learn["test_Z"],
-                    lambda a: L.to_device(np.asarray(a, dtype=np.float64)))
+    eX = _CACHE.get("test_X", p_learn["test_X"], _dev_f64)
+    eZ = _CACHE.get("test_Z", p_learn["test_Z"], _dev_f64)
     sxt, szt = _scores(eX, wd), _scores(eZ, wd)
     n, m = sxt.shape[0], szt.shape[0]
     xo, zo, xod, zod = _offsets(n, m)
