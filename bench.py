@@ -207,33 +207,43 @@ def plumbing_C1(with_cpu, reps=200):
 def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
     """The user-visible drop-in at BASELINE configs[2]'s size: est.UnNT(X, Z, 64, 4, "prop-SWOR")
     (estimation-experiment/main.py:76-79) on HOST arrays of n = 1e6 per class, exactly as a
-    reference script calls it: the in-place shuffles in the reference's RNG order (the native
-    restatement of np.random.shuffle, numpy_rng.shuffle_pair: same draws, same arrays, X's swaps
-    on a second thread), the T snapshots uploaded, all T x N blocks counted in one launch.  ms
-    split into the host half (shuffles, snapshots, concatenation), the H2D copy and the count
-    kernel; NumPy's own shuffles timed beside them."""
+    reference script calls it.  Default path: the host makes every draw in the reference's RNG
+    order (the T shuffles' index draws by the native restatement, numpy_rng.shuffle_draws32),
+    X and Z go up once, the device applies the T shuffles' swaps keeping every state
+    (csrc/devshuffle.hip), all T x N blocks are counted in one launch and the caller's arrays
+    receive the last state.  The host-swap path (shuffle_pair + T snapshots uploaded) is timed
+    beside it, and the parts of the default path alone on the same shapes."""
     import torch
     import tuplewise.estimation as est
-    from tuplewise import _engine as E, _lib as L
+    from tuplewise import _blocks as Bk, _engine as E, _lib as L
+    from tuplewise.numpy_rng import shuffle_draws32
     rng = np.random.RandomState(0)
     X, Z = rng.normal(0.5, 1, n), rng.normal(0, 1, n)
-    np.random.seed(1)
-    est.UnNT(X, Z, N, T, "prop-SWOR")  # warm
-    torch.cuda.synchronize()
+
+    def timed(min_items):
+        old = Bk.DEVICE_SHUFFLE_MIN
+        Bk.DEVICE_SHUFFLE_MIN = min_items
+        try:
+            Xc, Zc = X.copy(), Z.copy()  # both paths from the same arrays and RNG state
+            np.random.seed(1)
+            est.UnNT(Xc, Zc, N, T, "prop-SWOR")  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                v = est.UnNT(Xc, Zc, N, T, "prop-SWOR")
+            return (time.perf_counter() - t0) / reps, v
+        finally:
+            Bk.DEVICE_SHUFFLE_MIN = old
+
+    dt, v = timed(Bk.DEVICE_SHUFFLE_MIN)
+    dt_host, v_host = timed(1 << 62)
+    # the parts of the default path, timed alone on the same shapes
     t0 = time.perf_counter()
-    for _ in range(reps):
-        v = est.UnNT(X, Z, N, T, "prop-SWOR")
-    dt = (time.perf_counter() - t0) / reps
-    # the three parts, timed alone on the same shapes
-    from tuplewise.numpy_rng import shuffle_pair
-    t0 = time.perf_counter()
-    snaps = []
+    jx, jz = [], []
     for _ in range(T):
-        shuffle_pair(X, Z)
-        snaps.append((X.copy(), Z.copy()))
-    xs = np.concatenate([a for a, _ in snaps])
-    zs = np.concatenate([b for _, b in snaps])
-    host = time.perf_counter() - t0
+        jx.append(shuffle_draws32(n))
+        jz.append(shuffle_draws32(n))
+    draws = time.perf_counter() - t0
     t0 = time.perf_counter()
     for _ in range(T):
         np.random.shuffle(X)
@@ -241,24 +251,41 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
     np_shuffles = time.perf_counter() - t0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    xd, zd = L.to_device(xs), L.to_device(zs)
+    xd0, zd0 = L.to_device(X), L.to_device(Z)
     torch.cuda.synchronize()
     h2d = time.perf_counter() - t0
+    E.shuffle_snapshots_device(xd0, zd0, jx, jz)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    xs, zs = E.shuffle_snapshots_device(xd0, zd0, jx, jz)
+    torch.cuda.synchronize()
+    dev_shuffle = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    X[...] = xs[T - 1].cpu().numpy()
+    Z[...] = zs[T - 1].cpu().numpy()
+    d2h = time.perf_counter() - t0
     k = n // N
     off = np.arange(T * N + 1, dtype=np.int64) * k
     offd = L.to_device(off)
+    algo = E.pick_algo("auto", k, k, "gt")
+    xf, zf = xs.reshape(-1), zs.reshape(-1)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    E.count_launch(xd, offd, zd, offd, T * N, k, k, L.TW_F64, L.TW_PRED_GT, "pairs")
+    E.count_launch(xf, offd, zf, offd, T * N, k, k, L.TW_F64, L.TW_PRED_GT, algo)
     e0.record()
-    E.count_launch(xd, offd, zd, offd, T * N, k, k, L.TW_F64, L.TW_PRED_GT, "pairs")
+    E.count_launch(xf, offd, zf, offd, T * N, k, k, L.TW_F64, L.TW_PRED_GT, algo)
     e1.record()
     torch.cuda.synchronize()
     pairs = T * N * k * k
     return {"note": "est.UnNT(X, Z, 64, 4, 'prop-SWOR') on host arrays, n=1e6/class (the drop-in "
-                    "as a reference script calls it); parts timed alone on the same shapes",
+                    "as a reference script calls it): host draws in the reference's order, the "
+                    "shuffles' swaps on the device (csrc/devshuffle.hip), the caller's arrays "
+                    "written back; parts timed alone on the same shapes",
             "ms_per_call": dt * 1e3, "value": pairs / dt, "unit": "pairs/s",
-            "host_shuffle_snapshot_ms": host * 1e3, "numpy_shuffles_ms": np_shuffles * 1e3,
-            "h2d_ms": h2d * 1e3,
+            "host_swap_path_ms_per_call": dt_host * 1e3,
+            "same_value_both_paths": bool(v == v_host),
+            "host_draws_ms": draws * 1e3, "numpy_shuffles_ms": np_shuffles * 1e3,
+            "h2d_ms": h2d * 1e3, "device_shuffles_ms": dev_shuffle * 1e3,
+            "d2h_ms": d2h * 1e3, "count_algo": algo,
             "kernel_ms": e0.elapsed_time(e1), "last_value": float(v)}
 
 

@@ -512,6 +512,27 @@ int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int6
  * z's draws and swaps run.  jbuf: nx + nz int64 of scratch.  Returns 2 on bad arguments. */
 int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t isx, void* z,
                        int64_t nz, int64_t isz, int64_t* jbuf);
+/* The index draws of np.random.shuffle on n <= 2^31 items WITHOUT the swaps (j[i] for
+ * i = n-1 down to 1; j[0] untouched), advancing the state as the shuffle would: the host half
+ * of the device shuffle below.  Returns 2 on bad arguments. */
+int tw_np_shuffle_draws32(uint32_t* key, int32_t* pos, int64_t n, uint32_t* j);
+
+/* ---- Device shuffle swaps (csrc/devshuffle.hip): the swaps of np.random.shuffle(x) and
+ * np.random.shuffle(z) (UN's in-place shuffles, compute_stats.py:66-67,
+ * estimation-experiment/main.py:46-47) on 8-byte items in HBM, from the host's draws
+ * (tw_np_shuffle_draws32): for i = n-1 down to 1, swap a[i] and a[j[i]] — run as parallel
+ * rounds with deterministic reservations, giving the sequential loop's permutation bit for bit.
+ * One call enqueues tw_shuffle_swaps_rounds(nx, nz) rounds (first = 1, round0 = 0 on the first
+ * call; later calls: first = 0, round0 += rounds) and writes the number of iterations still
+ * pending to *d_pending (device u32); the caller repeats while it is non-zero (one call
+ * suffices w.h.p.).  nx + nz < 2^31.  d_work: tw_shuffle_swaps_work_bytes bytes. */
+int64_t tw_shuffle_swaps_work_bytes(int64_t nx, int64_t nz);
+int32_t tw_shuffle_swaps_rounds(int64_t nx, int64_t nz);
+/* rounds per batch (0 = the default 4.5 ln n + 24; at least 17): a test hook that forces resumed batches */
+int tw_shuffle_swaps_set_rounds(int32_t rounds);
+int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz, const uint32_t* d_jx,
+                     const uint32_t* d_jz, int32_t first, int32_t round0, void* d_work,
+                     uint32_t* d_pending, void* stream);
 
 #ifdef __cplusplus
 }

@@ -97,6 +97,13 @@ def test_scalar_path_matches_numpy(tw, env):
         "np.random.seed(8); np.random.shuffle(X1); np.random.shuffle(Z1); p=np.random.rand()\n"
         "np.random.seed(8); shuffle_pair(X, Z)\n"
         "assert np.array_equal(X, X1) and np.array_equal(Z, Z1) and np.random.rand() == p\n"
+        "from tuplewise.numpy_rng import shuffle_draws32\n"
+        "np.random.seed(8); jx=shuffle_draws32(70001); jz=shuffle_draws32(3000)\n"
+        "assert np.random.rand() == p\n"
+        "X=np.arange(70001.0); Z=np.arange(3000.0)\n"
+        "for a, j in ((X, jx), (Z, jz)):\n"
+        "    for i in range(len(a) - 1, 0, -1): a[i], a[j[i]] = a[j[i]], a[i]\n"
+        "assert np.array_equal(X, X1) and np.array_equal(Z, Z1)\n"
         "print('ok')\n")
     env = dict(os.environ, **env)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -148,3 +155,34 @@ def test_shuffle_pair_views_fall_back_to_numpy(tw):
     np.random.seed(4)
     shuffle_pair(X, Z)
     assert np.array_equal(X, Xr) and np.array_equal(Z, Zr)
+
+
+def _apply_swaps(a, j):
+    """_shuffle_raw's swaps (i = n-1 down to 1: swap a[i], a[j[i]]) in plain Python."""
+    for i in range(len(a) - 1, 0, -1):
+        k = j[i]
+        a[i], a[k] = a[k], a[i]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 17, 1000, 65537, 200003])
+def test_shuffle_draws32_are_numpy_shuffle_draws(tw, n):
+    """numpy_rng.shuffle_draws32 (the host half of the device shuffle): the draws of
+    np.random.shuffle on n items — applying them in _shuffle_raw's order gives NumPy's
+    permutation, every j[i] <= i, and the RNG state after is the shuffle's."""
+    from tuplewise.numpy_rng import shuffle_draws32
+    for seed in (4, 77):
+        a = np.arange(n, dtype=np.int64)
+        np.random.seed(seed)
+        np.random.random(3)
+        np.random.shuffle(a)
+        probe = np.random.randint(0, 2 ** 31, 3)
+        np.random.seed(seed)
+        np.random.random(3)
+        j = shuffle_draws32(n)
+        assert np.array_equal(np.random.randint(0, 2 ** 31, 3), probe)
+        assert j.dtype == np.uint32 and len(j) == n
+        if n > 1:
+            assert np.all(j[1:].astype(np.int64) <= np.arange(1, n))
+        b = list(range(n))
+        _apply_swaps(b, j.tolist())
+        assert np.array_equal(np.array(b, dtype=np.int64), a)

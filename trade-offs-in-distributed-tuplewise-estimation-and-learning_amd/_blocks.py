@@ -170,6 +170,20 @@ class CompleteCount(BlockSpec):
         return out
 
 
+    def evaluate_device(self, xd, zd, blocks):
+        """evaluate() on float64 device arrays (the device-shuffle path of run_un_repeated):
+        `X > Z` and the literal `(X - Z) > 0` are the same ordered comparison on doubles."""
+        mode = "half" if self.tie_mode == "half" else "gt"
+        xa, xo = _layout(xd, blocks, "x")
+        za, zo = _layout(zd, blocks, "z")
+        counts = E.count_complete(E.Shards(xa, xo, za, zo, L.TW_F64), mode)
+        out = []
+        for b, c in zip(blocks, counts):
+            pairs = b.nx() * b.nz()
+            out.append(E.ratio(c, 2 * pairs) if mode == "half" else E.ratio(c, pairs))
+        return out
+
+
 class CompleteSum(BlockSpec):
     """cs.Un prod/gini (compute_stats.py:15-18) and conv_AUC (compute_stats.py:129-135):
     mean over all pairs of a float kernel."""
@@ -202,6 +216,13 @@ class CompleteSum(BlockSpec):
         cast = rt.type if rt.kind == "f" else np.float64
         return [cast(s / np.float64(b.nx() * b.nz())) for b, s in zip(blocks, sums)]
 
+    def evaluate_device(self, xd, zd, blocks):
+        """evaluate() on float64 device arrays (the device-shuffle path of run_un_repeated)."""
+        xa, xo = _layout(xd, blocks, "x")
+        za, zo = _layout(zd, blocks, "z")
+        sums = E.pair_sum_complete(E.Shards(xa, xo, za, zo, L.TW_F64), self.kern, self.margin)
+        return [np.float64(s / np.float64(b.nx() * b.nz())) for b, s in zip(blocks, sums)]
+
 
 class Incomplete(BlockSpec):
     """cs.UB (compute_stats.py:37-42): B pairs drawn with replacement by two randint calls
@@ -232,6 +253,24 @@ class Incomplete(BlockSpec):
             ix_loc.append(np.asarray(ix, dtype=np.int64))
             iz_loc.append(np.asarray(iz, dtype=np.int64))
         return block_indexed_values(_flat(X), _flat(Z), eb, ix_loc, iz_loc, self.kernel)
+
+    def evaluate_device(self, xd, zd, blocks):
+        """evaluate() on float64 device arrays of 1-D samples (the device-shuffle path of
+        run_un_repeated): the blocks laid out as in block_indexed_values, the draws shifted."""
+        ix_loc = [np.asarray(b.aux[0], dtype=np.int64) for b in blocks]
+        iz_loc = [np.asarray(b.aux[1], dtype=np.int64) for b in blocks]
+        offs = np.concatenate([[0], np.cumsum([len(a) for a in ix_loc])]).astype(np.int64)
+        npairs = np.diff(offs)
+        xa, xo = _layout(xd, blocks, "x")
+        za, zo = _layout(zd, blocks, "z")
+        ix = np.concatenate([a + o for a, o in zip(ix_loc, xo[:-1])])
+        iz = np.concatenate([a + o for a, o in zip(iz_loc, zo[:-1])])
+        if self.kernel == "AUC":
+            counts = E.count_indexed(xa, za, L.TW_F64, ix, iz, offs, "gt", spans=(xo, zo))
+            return [E.ratio(c, p) for c, p in zip(counts, npairs)]
+        kern = {"prod": L.TW_KERN_PROD, "gini": L.TW_KERN_GINI}[self.kernel]
+        sums = E.pair_sum_indexed(xa, za, ix, iz, offs, kern)
+        return [np.float64(s / np.float64(p)) for s, p in zip(sums, npairs)]
 
 
 def block_indexed_values(x: np.ndarray, z: np.ndarray, blocks: list, ix_loc: list,
@@ -306,13 +345,14 @@ def indexed_values(x: np.ndarray, z: np.ndarray, ix: np.ndarray, iz: np.ndarray,
     return [np.float64(s / np.float64(p)) for s, p in zip(sums, npairs)]
 
 
-def plan_un(X, Z, N, spec, sampling_type, variant: str) -> list:
+def plan_un(X, Z, N, spec, sampling_type, variant: str, shuffle=shuffle_pair) -> list:
     """The host half of UN (compute_stats.py:56-92 "cs", estimation-experiment/main.py:33-69
     "est"): shuffle X and Z in place, then walk the N blocks making every RNG draw of the
-    reference in order.  Returns the plan [("val", Block) | ("zero",)] in append order."""
+    reference in order.  Returns the plan [("val", Block) | ("zero",)] in append order.
+    shuffle(X, Z): the in-place shuffles (or, for the device path, only their draws)."""
     X_rem = X
     Z_rem = Z
-    shuffle_pair(X_rem, Z_rem)  # np.random.shuffle(X); np.random.shuffle(Z), bit for bit
+    shuffle(X_rem, Z_rem)  # np.random.shuffle(X); np.random.shuffle(Z), bit for bit
     n_X = X_rem.shape[0]
     n_Z = Z_rem.shape[0]
     tau = int((n_X + n_Z) / N)
@@ -364,6 +404,9 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
         n_X, n_Z = X.shape[0], Z.shape[0]
         return _run_un_python(X, Z, N, f_block, sampling_type, variant, n_X, n_Z,
                               int((n_X + n_Z) / N))
+    if (isinstance(X, np.ndarray) and isinstance(Z, np.ndarray)
+            and _device_shuffle_ok(X, Z, spec)):
+        return _run_un_repeated_device(X, Z, N, spec, sampling_type, variant, 1)
     plan = plan_un(X, Z, N, spec, sampling_type, variant)
     blocks = [p[1] for p in plan if p[0] == "val"]
     return finish_un(plan, spec.evaluate(X, Z, blocks) if blocks else [])
@@ -378,6 +421,8 @@ def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
         return None  # the in-place shuffles must act on the caller's own objects
     if any(a.ndim > 2 or (a.ndim == 2 and a.shape[1] != 1) for a in (X, Z)):
         return None
+    if _device_shuffle_ok(X, Z, spec):
+        return _run_un_repeated_device(X, Z, N, spec, sampling_type, variant, T)
     plans, jobs = [], []
     for t in range(T):
         plan = plan_un(X, Z, N, spec, sampling_type, variant)
@@ -387,6 +432,62 @@ def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
         plans.append(plan)
     vals = evaluate_many(spec, jobs) if jobs else []
     return np.mean([finish_un(p, v) for p, v in zip(plans, vals)])
+
+
+# samples of at least this many items (per array) take the device shuffles in UnNT / UnNBT
+DEVICE_SHUFFLE_MIN = 1 << 16
+
+
+def _device_shuffle_ok(X, Z, spec) -> bool:
+    """The repeated UN's shuffles and blocks can stay on the device: 1-D C-contiguous float64
+    samples (8-byte items whose comparison / kernel operands are the scores themselves), a spec
+    with a device evaluation, the legacy MT19937 global state, one device."""
+    return (X.ndim == 1 and Z.ndim == 1 and X.dtype == np.float64 and Z.dtype == np.float64
+            and X.flags.c_contiguous and Z.flags.c_contiguous and X.flags.writeable
+            and Z.flags.writeable and max(X.shape[0], Z.shape[0]) >= DEVICE_SHUFFLE_MIN
+            and X.shape[0] + Z.shape[0] < 2 ** 31 and hasattr(spec, "evaluate_device")
+            and np.random.get_state(legacy=True)[0] == "MT19937" and len(M.devices()) < 2)
+
+
+def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
+    """run_un_repeated with the shuffles' swaps on the device: the host makes every draw in the
+    reference's order (the T shuffles' index draws, numpy_rng.shuffle_draws32, interleaved with
+    the block draws), the device applies the T shuffles to one upload of X and Z keeping every
+    state (_engine.shuffle_snapshots_device: the sequential swaps' permutation, bit for bit),
+    the T x N blocks are counted on those states in one launch, and the caller's arrays receive
+    the last state (the in-place side effect of the T np.random.shuffle calls)."""
+    from .numpy_rng import shuffle_draws32
+    plans = []
+    ds = E.DeviceShuffles(L.to_device(X), L.to_device(Z), T)
+
+    def draws(a, b):  # shuffle k's draws into pinned memory; the device swaps it meanwhile
+        shuffle_draws32(a.shape[0], out=ds.draw_x())
+        shuffle_draws32(b.shape[0], out=ds.draw_z())
+        ds.push()
+
+    for _ in range(T):
+        plans.append(plan_un(X, Z, N, spec, sampling_type, variant, shuffle=draws))
+    nx, nz = X.shape[0], Z.shape[0]
+    xs, zs = ds.finish()
+    blocks, counts = [], []
+    for k, plan in enumerate(plans):
+        blks = [p[1] for p in plan if p[0] == "val"]
+        for b in blks:
+            bx = (b.x[0] + k * nx, b.x[1] + k * nx) if isinstance(b.x, tuple) \
+                else np.asarray(b.x) + k * nx
+            bz = (b.z[0] + k * nz, b.z[1] + k * nz) if isinstance(b.z, tuple) \
+                else np.asarray(b.z) + k * nz
+            blocks.append(Block(bx, bz, b.aux))
+        counts.append(len(blks))
+    vals = spec.evaluate_device(xs.reshape(-1), zs.reshape(-1), blocks) if blocks else []
+    # the in-place side effect: the caller's arrays end in the last shuffled state
+    X[...] = xs[T - 1].cpu().numpy()
+    Z[...] = zs[T - 1].cpu().numpy()
+    out, i = [], 0
+    for p, c in zip(plans, counts):
+        out.append(finish_un(p, vals[i:i + c]))
+        i += c
+    return np.mean(out)
 
 
 def evaluate_many(spec, jobs) -> list:

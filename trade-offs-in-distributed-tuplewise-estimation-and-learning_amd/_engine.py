@@ -294,6 +294,85 @@ def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
     return pair_sum_complete_dev(sh, kern, margin).cpu().numpy()
 
 
+class DeviceShuffles:
+    """T successive np.random.shuffle's of two device arrays of 8-byte items, every state kept:
+    xs[k] = x0 after the swaps of shuffles 0..k (likewise zs).  The host draws each shuffle's
+    indices in NumPy's order (numpy_rng.shuffle_draws32) straight into pinned buffers (draw_x,
+    draw_z); push() uploads them asynchronously and enqueues that shuffle's swap rounds
+    (csrc/devshuffle.hip: the sequential loop's permutation, bit for bit), so the device swaps
+    shuffle k while the host draws shuffle k+1.  finish() reads the pending counts (one sync);
+    a shuffle whose batch of rounds did not finish (rare) is resumed and the shuffles after it
+    are redone.  Returns the (T, nx) and (T, nz) device tensors."""
+
+    def __init__(self, x0, z0, T: int):
+        t = L.torch()
+        lib = L.lib()
+        assert x0.element_size() == 8 and z0.element_size() == 8
+        self.x0, self.z0 = x0.reshape(-1), z0.reshape(-1)
+        self.T = T
+        self.nx, self.nz = int(x0.numel()), int(z0.numel())
+        self.xs = L.empty((T, self.nx), x0.dtype)
+        self.zs = L.empty((T, self.nz), z0.dtype)
+        self.hx = t.empty((T, self.nx), dtype=t.int32, pin_memory=True)
+        self.hz = t.empty((T, self.nz), dtype=t.int32, pin_memory=True)
+        self.jx = L.empty((T, self.nx), t.int32)
+        self.jz = L.empty((T, self.nz), t.int32)
+        nb = max(int(lib.tw_shuffle_swaps_work_bytes(self.nx, self.nz)), 1)
+        self.rounds = int(lib.tw_shuffle_swaps_rounds(self.nx, self.nz))
+        self.work = L.empty((T, nb), t.uint8)
+        self.pend = L.empty((max(T, 1),), t.int32)
+        self.k = 0
+
+    def draw_x(self):
+        return self.hx[self.k].numpy()
+
+    def draw_z(self):
+        return self.hz[self.k].numpy()
+
+    def push(self) -> None:
+        k = self.k
+        self.jx[k].copy_(self.hx[k], non_blocking=True)
+        self.jz[k].copy_(self.hz[k], non_blocking=True)
+        self._start(k)
+        self.k += 1
+
+    def _run(self, k, first, round0):
+        L.call("tw_shuffle_swaps", L.ptr(self.xs[k]), self.nx, L.ptr(self.zs[k]), self.nz,
+               L.ptr(self.jx[k]), L.ptr(self.jz[k]), int(first), round0, L.ptr(self.work[k]),
+               L.ptr(self.pend[k:k + 1]), L.stream_handle())
+
+    def _start(self, k):
+        self.xs[k].copy_(self.x0 if k == 0 else self.xs[k - 1])
+        self.zs[k].copy_(self.z0 if k == 0 else self.zs[k - 1])
+        self._run(k, True, 0)
+
+    def finish(self):
+        T = self.T
+        assert self.k == T, "every shuffle must be pushed before finish()"
+        left = np.nonzero(self.pend[:T].cpu().numpy())[0]
+        if len(left):  # rare: finish shuffle k, then redo the later ones one at a time
+            k = int(left[0])
+            while k < T:
+                r0 = self.rounds
+                while int(self.pend[k].item()):
+                    self._run(k, False, r0)
+                    r0 += self.rounds
+                k += 1
+                if k < T:
+                    self._start(k)
+        return self.xs, self.zs
+
+
+def shuffle_snapshots_device(x0, z0, jx, jz):
+    """DeviceShuffles over draws already made (uint32 host arrays, one per shuffle)."""
+    ds = DeviceShuffles(x0, z0, len(jx))
+    for a, b in zip(jx, jz):
+        ds.draw_x()[...] = np.asarray(a).view(np.int32)
+        ds.draw_z()[...] = np.asarray(b).view(np.int32)
+        ds.push()
+    return ds.finish()
+
+
 # hinge sums of shards with at least this many pairs use the O((n+m) log m) path
 HINGE_SORTED_MIN_PAIRS = 1 << 27
 

@@ -113,6 +113,11 @@ _SIGNATURES = {
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
+    "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],
+    "tw_shuffle_swaps_work_bytes": [_i64, _i64],
+    "tw_shuffle_swaps_rounds": [_i64, _i64],
+    "tw_shuffle_swaps_set_rounds": [_i32],
+    "tw_shuffle_swaps": [_vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp],
 }
 _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,
@@ -122,6 +127,7 @@ _RESTYPES = {
     "tw_pair_sum_idx_work_per_shard": ctypes.c_int64,
     "tw_pair_grad_complete_work_bytes": ctypes.c_int64,
     "tw_pair_hinge_sum_sorted_work_bytes": ctypes.c_int64,
+    "tw_shuffle_swaps_work_bytes": ctypes.c_int64,
 }
 
 _lib = None

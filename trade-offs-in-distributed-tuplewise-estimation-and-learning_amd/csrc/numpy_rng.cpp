@@ -386,9 +386,10 @@ __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) void pairs_avx512(
 // lanes is left-packed and stored reversed at j[i-7 .. i] (j[i - r] = r-th accept; the lanes
 // past the accepts land on lower slots that later draws overwrite).  Any unsure lane: the
 // batch is left to the scalar loop.  Returns the new p (i updated).
+template <typename J>
 __attribute__((target("avx2,popcnt"))) inline int shuffle8_avx2(const uint32_t* tmp, int p,
                                                                uint32_t mask, int64_t lo,
-                                                               int64_t& i, int64_t* j) {
+                                                               int64_t& i, J* j) {
   const __m256i vm = _mm256_set1_epi32((int)mask);
   const __m256i sign = _mm256_set1_epi32((int)0x80000000u);
   const __m256i rev = _mm256_setr_epi32(7, 6, 5, 4, 3, 2, 1, 0);
@@ -403,9 +404,14 @@ __attribute__((target("avx2,popcnt"))) inline int shuffle8_avx2(const uint32_t* 
     const __m256i packed = _mm256_permutevar8x32_epi32(
         v, _mm256_loadu_si256((const __m256i*)g_pack.idx[acc]));
     const __m256i r = _mm256_permutevar8x32_epi32(packed, rev);  // lane l = accept 7 - l
-    _mm256_storeu_si256((__m256i*)(j + i - 7), _mm256_cvtepu32_epi64(_mm256_castsi256_si128(r)));
-    _mm256_storeu_si256((__m256i*)(j + i - 3),
-                        _mm256_cvtepu32_epi64(_mm256_extracti128_si256(r, 1)));
+    if constexpr (sizeof(J) == 8) {
+      _mm256_storeu_si256((__m256i*)(j + i - 7),
+                          _mm256_cvtepu32_epi64(_mm256_castsi256_si128(r)));
+      _mm256_storeu_si256((__m256i*)(j + i - 3),
+                          _mm256_cvtepu32_epi64(_mm256_extracti128_si256(r, 1)));
+    } else {
+      _mm256_storeu_si256((__m256i*)(j + i - 7), r);
+    }
     i -= __builtin_popcount((unsigned)acc);
     p += 8;
   }
@@ -413,8 +419,9 @@ __attribute__((target("avx2,popcnt"))) inline int shuffle8_avx2(const uint32_t* 
 }
 
 // the same with 16 lanes (sure accept v <= i - 15)
+template <typename J>
 __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) inline int shuffle16_avx512(
-    const uint32_t* tmp, int p, uint32_t mask, int64_t lo, int64_t& i, int64_t* j) {
+    const uint32_t* tmp, int p, uint32_t mask, int64_t lo, int64_t& i, J* j) {
   const __m512i vm = _mm512_set1_epi32((int)mask);
   const __m512i rev = _mm512_setr_epi32(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
   while (p + 16 <= kN && i - 16 > lo && i >= 16) {
@@ -426,24 +433,30 @@ __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) inline int shuffle1
     const __mmask16 acc = (__mmask16)~rej;
     const __m512i packed = _mm512_maskz_compress_epi32(acc, v);
     const __m512i r = _mm512_permutexvar_epi32(rev, packed);  // lane l = accept 15 - l
-    _mm512_storeu_si512((void*)(j + i - 15), _mm512_cvtepu32_epi64(_mm512_castsi512_si256(r)));
-    _mm512_storeu_si512((void*)(j + i - 7),
-                        _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(r, 1)));
+    if constexpr (sizeof(J) == 8) {
+      _mm512_storeu_si512((void*)(j + i - 15),
+                          _mm512_cvtepu32_epi64(_mm512_castsi512_si256(r)));
+      _mm512_storeu_si512((void*)(j + i - 7),
+                          _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(r, 1)));
+    } else {
+      _mm512_storeu_si512((void*)(j + i - 15), r);
+    }
     i -= __builtin_popcount((unsigned)acc);
     p += 16;
   }
   return p;
 }
 
-template <int kIsa>
-void shuffle_draws(MT& mt, int64_t n, int64_t* j) {
+// J = int64_t (the host swaps) or uint32_t (the device swaps: n <= 2^31, so 32-bit draws only)
+template <int kIsa, typename J>
+void shuffle_draws(MT& mt, int64_t n, J* j) {
   int64_t i = n - 1;
-  while (i >= 1 && (uint64_t)i > 0xFFFFFFFFull) {
+  while (sizeof(J) == 8 && i >= 1 && (uint64_t)i > 0xFFFFFFFFull) {
     const uint64_t mask = gen_mask((uint64_t)i);
     uint64_t v;
     while ((v = (mt.next64() & mask)) > (uint64_t)i) {
     }
-    j[i--] = (int64_t)v;
+    j[i--] = (J)v;
   }
   while (i >= 1) {
     const uint32_t mask = (uint32_t)gen_mask((uint64_t)i);
@@ -458,7 +471,7 @@ void shuffle_draws(MT& mt, int64_t n, int64_t* j) {
       const int stop = kIsa ? (p + 8 < kN ? p + 8 : kN) : kN;
       while (p < stop && i > lo) {
         const uint32_t v = mt.tmp[p++] & mask;
-        j[i] = (int64_t)v;
+        j[i] = (J)v;
         i -= (int64_t)(v <= (uint32_t)i);
       }
       if (p >= kN || i <= lo) break;
@@ -498,13 +511,25 @@ void shuffle_apply(char* data, int64_t n, int64_t itemsize, const int64_t* j) {
   }
 }
 
-__attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t n, int64_t* j) {
+template <typename J>
+__attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t n, J* j) {
   shuffle_draws<1>(mt, n, j);
 }
+template <typename J>
 __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) void shuffle_draws_avx512(MT& mt,
                                                                                   int64_t n,
-                                                                                  int64_t* j) {
+                                                                                  J* j) {
   shuffle_draws<2>(mt, n, j);
+}
+
+template <typename J>
+void shuffle_draws_isa(MT& mt, int64_t n, J* j, int isa) {
+  if (isa == 2)
+    shuffle_draws_avx512(mt, n, j);
+  else if (isa == 1)
+    shuffle_draws_avx2(mt, n, j);
+  else
+    shuffle_draws<0>(mt, n, j);
 }
 
 // SIMD level chosen once at run time: 2 AVX-512 (F + VL) + BMI2, 1 AVX2, 0 portable.
@@ -571,14 +596,7 @@ int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t
   int64_t* jx = jbuf;
   int64_t* jz = jbuf + (nx > 0 ? nx : 0);
   const int isa = isa_level();
-  auto draws = [&](int64_t n, int64_t* j) {
-    if (isa == 2)
-      shuffle_draws_avx512(mt, n, j);
-    else if (isa == 1)
-      shuffle_draws_avx2(mt, n, j);
-    else
-      shuffle_draws<0>(mt, n, j);
-  };
+  auto draws = [&](int64_t n, int64_t* j) { shuffle_draws_isa(mt, n, j, isa); };
   if (nx > 1) draws(nx, jx);
   std::thread tx;
   bool threaded = false;
@@ -595,6 +613,19 @@ int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t
     shuffle_apply((char*)z, nz, isz, jz);
   }
   if (threaded) tx.join();
+  *pos = mt.pos;
+  return 0;
+}
+
+// The index draws of np.random.shuffle on n items (n <= 2^31) without the swaps: j[i] for
+// i = n-1 down to 1 (j[0] untouched), as uint32, for the device swaps (devshuffle.hip).  The
+// state advances exactly as the shuffle's would.
+int tw_np_shuffle_draws32(uint32_t* key, int32_t* pos, int64_t n, uint32_t* j) {
+  if (n < 0 || n > (1ll << 31) || (n > 1 && !j)) return 2;
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  if (n > 1) shuffle_draws_isa(mt, n, j, isa_level());
   *pos = mt.pos;
   return 0;
 }

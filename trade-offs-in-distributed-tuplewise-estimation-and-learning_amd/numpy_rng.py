@@ -74,6 +74,32 @@ def shuffle_pair(X, Z) -> None:
     np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
 
 
+def shuffle_draws32(n: int, out=None) -> np.ndarray:
+    """The index draws np.random.shuffle makes on n items (n <= 2^31), without the swaps: a
+    uint32 array j with j[i] for i = n-1 down to 1 (j[0] = 0), the global legacy state advanced
+    exactly as the shuffle would advance it (the host half of _engine.DeviceShuffles).
+    out: a C-contiguous 4-byte array of n entries to draw into (e.g. pinned memory)."""
+    name, key, pos, has_gauss, gauss = np.random.get_state(legacy=True)
+    if name != "MT19937":
+        raise ValueError("shuffle_draws32 restates the legacy MT19937 RandomState only")
+    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+    pos_c = ctypes.c_int32(int(pos))
+    if out is None:
+        j = np.zeros(max(int(n), 0), dtype=np.uint32)
+    else:
+        j = out.view(np.uint32)
+        if j.shape != (max(int(n), 0),) or not j.flags.c_contiguous:
+            raise ValueError("shuffle_draws32: out must be a contiguous array of n 4-byte items")
+        if n > 0:
+            j[0] = 0
+    rc = L.lib().tw_np_shuffle_draws32(key.ctypes.data, ctypes.byref(pos_c), int(n),
+                                       j.ctypes.data)
+    if rc:
+        raise ValueError(f"tw_np_shuffle_draws32 failed ({rc}) for n = {n}")
+    np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
+    return j
+
+
 class Session:
     """NumPy's legacy global MT19937 state held in native code for a run of draws.
 
