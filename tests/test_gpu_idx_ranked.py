@@ -23,7 +23,7 @@ def _np_count(x, z, ix, iz, pair_off, mode):
         elif mode == "half":
             out.append(int(np.sum(a > b)) + int(np.sum(a >= b)))
         else:  # subgt: (a - b) > 0 with int64 wrap
-            with np.errstate(over="ignore"):
+            with np.errstate(over="ignore", invalid="ignore"):  # inf - inf in the float cases
                 out.append(int(np.sum((a - b) > 0)))
     return np.array(out, dtype=np.uint64)
 
