@@ -641,14 +641,17 @@ def test_complete_hinge_search_equals_pair_sums(gpu, kx, kz):
 
 def test_complete_logistic_large_scores(gpu):
     """Scores beyond +-350 send their (tile, chunk) to the direct-formula path of
-    k_logistic_coef (the separated factors could leave the normal range); the gradient still
-    matches the oracle, incl. saturated sigmas (S of several hundred)."""
+    k_logistic_coef (the separated factors could leave the normal range), scores beyond +-40
+    to the per-sigma reciprocals (no batched inversion); the gradient still matches the
+    oracle, incl. saturated sigmas (S of several hundred)."""
     from tuplewise import _lib as L, _learn
     rng = np.random.RandomState(12)
-    N, d, kx, kz = 3, 4, 5000, 1300
+    N, d, kx, kz = 4, 4, 5000, 1300
     X, Z = rng.normal(size=(kx * N, d)), rng.normal(0.3, 1, size=(kz * N, d))
     X[: kx, :] *= 300.0  # shard 0: |scores| up to ~1000 on the x side
     Z[kz:2 * kz, :] *= 250.0  # shard 1: on the z side
+    X[3 * kx:, :] *= 30.0  # shard 3: |scores| in (40, 350] for some tiles (no batched sigmas)
+    Z[3 * kz:, :] *= 30.0
     w = np.array([1.0, -0.5, 0.25, 0.8])
     g = _learn.complete_grads_device(L.to_device(X), L.to_device(Z), d, None, kx, None, kz, N,
                                      L.to_device(w), 0.7, L.TW_LOSS_LOGISTIC).cpu().numpy()

@@ -24,6 +24,7 @@
 //   k_wcolsum_final  chunk partials added in chunk order, / (kx kz)
 #include "sortkeys.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace tw {
 
@@ -179,11 +180,11 @@ __global__ __launch_bounds__(kSortThreads) void k_hinge_coef(const double* __res
 //   b_i += sigma(S_ij)              per lane, in j order (registers)
 //   a_j  = sum over the tile's x    lane butterfly, then the 8 waves in wave order (LDS),
 // writing one partial of a_j per (tile, j); k_apart_final adds the tiles in tile order.
-// Deterministic.  With the separated exponent (below) a sigma is an FMA and a division.
+// Deterministic.  With the separated exponent (below) a sigma is an FMA and a reciprocal.
 constexpr int kLgR = 16;
 constexpr int kLgThreads = 256;
 constexpr int kLgChunk = 512;
-__global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __restrict__ sx,
+__global__ __launch_bounds__(kLgThreads, 2) void k_logistic_coef(const double* __restrict__ sx,
                                                               int64_t kx,
                                                               const double* __restrict__ sz,
                                                               int64_t kz, double margin,
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __re
   // only by the rare direct-formula chunks), so 16 x-values per lane fit
   double b[kLgR], ea[kLgR];
   unsigned valid = 0;  // bit r: x-value r of this lane exists
-  int tile_sep = 1;
+  int tile_sep = 1, tile_sep40 = 1;
   const double* xs = sx + (int64_t)s * kx + (int64_t)tile * (kLgThreads * kLgR) + threadIdx.x;
 #pragma unroll
   for (int r = 0; r < kLgR; ++r) {
@@ -215,38 +216,116 @@ __global__ __launch_bounds__(kLgThreads) void k_logistic_coef(const double* __re
     const double u = (ok ? xs[r * kLgThreads] : 0.0) - margin;
     b[r] = 0.0;
     tile_sep &= __builtin_fabs(u) <= 350.0;
+    tile_sep40 &= __builtin_fabs(u) <= 40.0;
     ea[r] = exp(u);
   }
   tile_sep = __syncthreads_and(tile_sep);
+  tile_sep40 = __syncthreads_and(tile_sep40);
+  const int tile_full = __syncthreads_and(valid == (1u << kLgR) - 1u);
   const double* zs = sz + (int64_t)s * kz;
   double* ap = apart + ((int64_t)s * tiles + tile) * kz;
   for (int64_t c0 = 0; c0 < kz; c0 += kLgChunk) {
     const int n = (int)std::min<int64_t>(kLgChunk, kz - c0);
     __syncthreads();
-    int chunk_sep = tile_sep;
+    int chunk_sep = tile_sep, chunk_sep40 = 1;
     for (int j = threadIdx.x; j < n; j += kLgThreads) {
       const double zj = zs[c0 + j];
       zc[j] = zj;
       eb[j] = exp(-zj);
       chunk_sep &= __builtin_fabs(zj) <= 350.0;
+      chunk_sep40 &= __builtin_fabs(zj) <= 40.0;
     }
     chunk_sep = __syncthreads_and(chunk_sep);  // block-uniform
-    if (chunk_sep) {
-      for (int j = 0; j < n; ++j) {
-        const double ej = eb[j];
-        double t = 0.0;
+    chunk_sep40 = __syncthreads_and(chunk_sep40);
+    // a block whose x-values all exist (every tile but a shard's last) adds y to t without a
+    // select: 8 VALU per pair instead of 10 (the same sums in the same order)
+    // sigma = 1 / q, q = 1 + e^(sx_i - m) e^(-sz_j), from v_rcp_f64 (2^-24 relative on gfx950)
+    // plus ONE Newton step (<= 10 ulp; tools/mb_rcp.hip, profiles/r02_mb_rcp_accuracy.log).
+    // BATCH: when every factor's exponent is within +-40 (q <= 1 + e^80), the reciprocals of
+    // 8 q's come from one (Montgomery's batch inversion): prefix products P_k = q_0...q_k
+    // (<= e^640, a normal double), I = 1 / P_7, then y_k = I_k P_(k-1), I_(k-1) = I_k q_k —
+    // 3.4 multiplies per sigma instead of a quarter-rate reciprocal and its Newton step.
+    // Relative error <= ~20 ulp per sigma either way (the oracle tolerance is 1e-10).
+    auto sep_chunk = [&](auto all_valid, auto batch) {
+      // NJ z-values at a time: independent chains interleave (2 waves per SIMD at this
+      // register count); every sum still takes its terms in the same order
+      auto step = [&](auto nj, int j0) {
+        constexpr int NJ = decltype(nj)::value;
+        double ejv[NJ], t[NJ];
 #pragma unroll
-        for (int r = 0; r < kLgR; ++r) {
-          const double q = __builtin_fma(ea[r], ej, 1.0);  // 1 + e^-S in [1, e^700]
-          double y = __builtin_amdgcn_rcp(q);
-          y = __builtin_fma(__builtin_fma(-q, y, 1.0), y, y);
-          y = __builtin_fma(__builtin_fma(-q, y, 1.0), y, y);
-          b[r] += y;
-          t += (valid >> r) & 1u ? y : 0.0;
+        for (int u = 0; u < NJ; ++u) {
+          ejv[u] = eb[j0 + u];
+          t[u] = 0.0;
         }
-        t = wave_sum_f64(t);
-        if (lane == 0) wpart[wid][j] = t;
-      }
+        if constexpr (decltype(batch)::value) {
+#pragma unroll
+          for (int g = 0; g < kLgR; g += 8) {
+            double q[NJ][8], P[NJ][7], I[NJ], tg[NJ];
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) q[u][k] = __builtin_fma(ea[g + k], ejv[u], 1.0);
+              P[u][0] = q[u][0];
+#pragma unroll
+              for (int k = 1; k < 7; ++k) P[u][k] = P[u][k - 1] * q[u][k];
+              const double P7 = P[u][6] * q[u][7];
+              I[u] = __builtin_amdgcn_rcp(P7);
+              I[u] = __builtin_fma(__builtin_fma(-P7, I[u], 1.0), I[u], I[u]);
+              tg[u] = 0.0;  // the group's sigmas are consumed as they appear (k = 7 .. 0)
+            }
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+#pragma unroll
+              for (int u = 0; u < NJ; ++u) {
+                const double y = k ? I[u] * P[u][k - 1] : I[u];
+                if (k) I[u] = I[u] * q[u][k];
+                b[g + k] += y;
+                if constexpr (decltype(all_valid)::value)
+                  tg[u] += y;
+                else
+                  tg[u] += (valid >> (g + k)) & 1u ? y : 0.0;
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) t[u] += tg[u];
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < NJ; ++u) {
+#pragma unroll
+            for (int r = 0; r < kLgR; ++r) {
+              const double q = __builtin_fma(ea[r], ejv[u], 1.0);  // 1 + e^-S in [1, e^700]
+              double y = __builtin_amdgcn_rcp(q);
+              y = __builtin_fma(__builtin_fma(-q, y, 1.0), y, y);
+              b[r] += y;
+              if constexpr (decltype(all_valid)::value)
+                t[u] += y;
+              else
+                t[u] += (valid >> r) & 1u ? y : 0.0;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+          const double tt = wave_sum_dpp_f64(t[u]);
+          if (lane == 0) wpart[wid][j0 + u] = tt;
+        }
+      };
+      int j = 0;
+      for (; j + 1 < n; j += 2) step(std::integral_constant<int, 2>{}, j);
+      if (j < n) step(std::integral_constant<int, 1>{}, j);
+    };
+    if (chunk_sep) {
+      // both block-uniform (the wave sums inside need every lane)
+      const bool batch = tile_sep40 && chunk_sep40;
+      if (tile_full && batch)
+        sep_chunk(std::true_type{}, std::true_type{});
+      else if (tile_full)
+        sep_chunk(std::true_type{}, std::false_type{});
+      else if (batch)
+        sep_chunk(std::false_type{}, std::true_type{});
+      else
+        sep_chunk(std::false_type{}, std::false_type{});
     } else {
       for (int j = 0; j < n; ++j) {
         const double zj = zc[j];

@@ -64,6 +64,33 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// One DPP move of a double (both 32-bit halves).  Lanes outside row_mask receive an undefined
+// value (no "old" operand to materialise): callers only use lanes the pattern defines.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, ROW_MASK, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Wave sum of a double through DPP lane moves (no LDS round trip, unlike __shfl_xor's
+// ds_bpermute): quad xor 1, quad xor 2, half-row mirror, row mirror, then row_bcast15 /
+// row_bcast31 fold the four rows into lane 63 (other lanes end with partial or undefined
+// sums), which is broadcast.  Fixed order (deterministic).
+__device__ __forceinline__ double wave_sum_dpp_f64(double v) {
+  v += dpp_f64<0xB1>(v);        // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);        // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);       // row_half_mirror: sums of 8
+  v += dpp_f64<0x140>(v);       // row_mirror: sums of 16
+  v += dpp_f64<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3
+  v += dpp_f64<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3: lane 63 holds the total
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // Pair weights of the gradient sum.  TW_LOSS_HINGE: grad_inc_block's filter 1{S > 0}
 // (compute_stats.py:158-161), applied as a branch so unfiltered rows are skipped exactly as
 // diff[filt] skips them.  TW_LOSS_LOGISTIC (extension, SURVEY.md §8 row L3 — not in the
