@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kBlock) void k_row_scores(const double* __restrict_
         p0 += v.x * ww.x;
         p1 += v.y * ww.y;
       }
-      const double p = wave_sum_f64(p0 + p1);
+      const double p = wave_sum_dpp_f64(p0 + p1);
       if (lane == 0) out[r] = p;
     }
     return;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kBlock) void k_row_scores(const double* __restrict_
     const double* a = A + (rows ? rows[r] : r) * d;
     double p = 0.0;
     for (int64_t j = lane; j < d; j += kWave) p += a[j] * w[j];
-    p = wave_sum_f64(p);
+    p = wave_sum_dpp_f64(p);
     if (lane == 0) out[r] = p;
   }
 }
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void k_logistic_coef(const double* _
           b[r] += p;
           t += ok ? p : 0.0;
         }
-        t = wave_sum_f64(t);
+        t = wave_sum_dpp_f64(t);
         if (lane == 0) wpart[wid][j] = t;
       }
     }

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
           }
         }
       }
-      part = wave_sum_f64(part);
+      part = wave_sum_dpp_f64(part);
       if (lane == 0) flag[t] = pair_weight<LOSS>(part + margin);
       if (lane == 0 && s_out) s_out[(int64_t)s * B + b0 + t] = part + margin;
     }
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
               part += v * wv[c];
             }
           }
-          part = wave_sum_f64(part);
+          part = wave_sum_dpp_f64(part);
           if (lane == 0) flag[t] = pair_weight<LOSS>(part + margin);
         }
       }
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
             part += v * wv[c];
           }
         }
-        part = wave_sum_f64(part);
+        part = wave_sum_dpp_f64(part);
         if (lane == 0) flag[st][t] = pair_weight<LOSS>(part + margin);
       }
       if (c0 + 2 * kStreamCH < np) load(st, c0 + 2 * kStreamCH);  // refill: chunk k+2

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kWideBlock) void k_sgd_segment_wide(
           }
         }
       }
-      part = wave_sum_f64(part);
+      part = wave_sum_dpp_f64(part);
       if (lane == 0) flag[st][wid] = pair_weight<LOSS>(part + margin);
     }
     if (c0 + 2 * kStreamCH < np) load(st, c0 + 2 * kStreamCH, np);  // refill: chunk k+2
