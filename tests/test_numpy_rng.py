@@ -186,3 +186,40 @@ def test_shuffle_draws32_are_numpy_shuffle_draws(tw, n):
         b = list(range(n))
         _apply_swaps(b, j.tolist())
         assert np.array_equal(np.array(b, dtype=np.int64), a)
+
+
+@pytest.mark.parametrize("in_place", [True, False])
+def test_state_in_place_and_copied_paths(tw, in_place, monkeypatch):
+    """The native draws advance NumPy's own MT19937 struct in place (numpy_rng._mt_state) or,
+    where that is unavailable, a get_state copy committed with set_state: both give NumPy's
+    draws and final state, incl. a foreign draw between two Session phases."""
+    from tuplewise import numpy_rng as R
+    if not in_place:
+        monkeypatch.setattr(R, "_mt_state", lambda: None)
+    np.random.seed(21)
+    a = np.random.randint(0, 97, 50)
+    X, W = np.arange(5000.0), np.arange(300.0)
+    np.random.shuffle(X)
+    np.random.shuffle(W)
+    g = np.random.normal()
+    b = np.random.randint(-4, 9, 30)
+    j = np.arange(700)
+    np.random.shuffle(j)
+    end = np.random.random()
+    np.random.seed(21)
+    got_a = R.randint_batch([(0, 97, 50)])[0]
+    Y, V = np.arange(5000.0), np.arange(300.0)
+    R.shuffle_pair(Y, V)
+    s = R.Session()
+    gg = np.random.normal()  # foreign draw (touches has_gauss)
+    s.acquire()
+    got_b = s.randint_flat([-4], [9], [30])
+    s.commit()
+    jj = R.shuffle_draws32(700)
+    k = np.arange(700)
+    for i in range(699, 0, -1):
+        k[i], k[jj[i]] = k[jj[i]], k[i]
+    assert np.array_equal(got_a, a) and np.array_equal(Y, X) and np.array_equal(V, W)
+    assert gg == g
+    assert np.array_equal(got_b, b) and np.array_equal(k, j)
+    assert np.random.random() == end

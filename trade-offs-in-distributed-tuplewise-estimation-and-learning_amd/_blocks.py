@@ -69,6 +69,19 @@ def _elements(blocks, side: str, rs: int) -> list:
     return out
 
 
+def _slice_offsets(blocks, side: str):
+    """int64 offsets (len(blocks)+1) when the blocks' parts are consecutive slices of one
+    array (the usual SWOR / prop-SWOR plan), else None."""
+    parts = [getattr(b, side) for b in blocks]
+    if not parts or not all(isinstance(p, tuple) for p in parts):
+        return None
+    starts = np.array([p[0] for p in parts], dtype=np.int64)
+    stops = np.array([p[1] for p in parts], dtype=np.int64)
+    if not np.all(starts[1:] == stops[:-1]):
+        return None
+    return np.concatenate([starts[:1], stops]).astype(np.int64)
+
+
 def _layout(arr_dev, blocks, side: str):
     """Device array + int64 offsets (len(blocks)+1) for the blocks' x or z parts."""
     parts = [getattr(b, side) for b in blocks]
@@ -159,10 +172,17 @@ class CompleteCount(BlockSpec):
             counts = M.gather(M.spread(blocks, lambda b: b.nx() * b.nz(), enqueue))
             counts = counts.astype(np.int64).view(np.uint64)
         else:
-            xd, zd = L.to_device(x), L.to_device(z)
-            xa, xo = _layout(xd, blocks, "x")
-            za, zo = _layout(zd, blocks, "z")
-            counts = E.count_complete(E.Shards(xa, xo, za, zo, code), mode)
+            xo, zo = _slice_offsets(blocks, "x"), _slice_offsets(blocks, "z")
+            if xo is not None and zo is not None:  # the usual plan: one upload for all four
+                xa, za, xod, zod = L.to_device_many([x, z, xo, zo])
+                sh = E.Shards(xa, xo, za, zo, code)
+                sh._x_off_dev, sh._z_off_dev = xod, zod
+            else:
+                xd, zd = L.to_device(x), L.to_device(z)
+                xa, xo = _layout(xd, blocks, "x")
+                za, zo = _layout(zd, blocks, "z")
+                sh = E.Shards(xa, xo, za, zo, code)
+            counts = E.count_complete(sh, mode)
         out = []
         for b, c in zip(blocks, counts):
             pairs = b.nx() * b.nz()

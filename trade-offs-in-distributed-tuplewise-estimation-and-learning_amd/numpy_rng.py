@@ -13,28 +13,73 @@ import numpy as np
 
 from . import _lib as L
 
+_RK_STATE_LEN = 624
+_MT = {"bg": None, "ptrs": None}
+
+
+def _mt_state():
+    """(key, pos) pointers into the global legacy RandomState's MT19937 state — NumPy's own
+    mt19937_state struct (uint32 key[624]; int pos), which the native draws then advance IN
+    PLACE, with no get_state/set_state copies (~40 us a pair).  The layout is checked once
+    against get_state.  None when the global generator is not an MT19937."""
+    bg = getattr(np.random.mtrand._rand, "_bit_generator", None)
+    if type(bg) is not np.random.MT19937:
+        return None
+    if _MT["bg"] is not bg:
+        addr = int(bg.ctypes.state_address)
+        key = np.ctypeslib.as_array((ctypes.c_uint32 * _RK_STATE_LEN).from_address(addr))
+        pos = ctypes.c_int.from_address(addr + 4 * _RK_STATE_LEN)
+        name, k, p = np.random.get_state(legacy=True)[:3]
+        if name != "MT19937" or p != pos.value or not np.array_equal(k, key):
+            return None
+        _MT.update(bg=bg, ptrs=(ctypes.c_void_p(addr),
+                                ctypes.c_void_p(addr + 4 * _RK_STATE_LEN)))
+    return _MT["ptrs"]
+
+
+class _CopiedState:
+    """get_state/set_state around a native call: the fallback when _mt_state() is None."""
+
+    def __init__(self):
+        name, key, pos, self.has_gauss, self.gauss = np.random.get_state(legacy=True)
+        if name != "MT19937":
+            raise NotImplementedError("only the MT19937 legacy RandomState is supported")
+        self.key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+        self.pos = ctypes.c_int32(int(pos))
+
+    def ptrs(self):
+        return ctypes.c_void_p(self.key.ctypes.data), ctypes.byref(self.pos)
+
+    def commit(self):
+        np.random.set_state(("MT19937", self.key, self.pos.value, self.has_gauss, self.gauss))
+
+
+def _native_draws(fn):
+    """Run fn(key_ptr, pos_ptr) on the global MT19937 state (in place when possible) and
+    return its status; the state is committed even on error (NumPy would have consumed the
+    draws made before the failing call)."""
+    ptrs = _mt_state()
+    if ptrs is not None:
+        return fn(*ptrs)
+    st = _CopiedState()
+    rc = fn(*st.ptrs())
+    st.commit()
+    return rc
+
 
 def randint_batch(calls) -> list:
     """[np.random.randint(lo, hi, n) for lo, hi, n in calls], one native call."""
     calls = list(calls)
     if not calls:
         return []
-    name, key, pos, has_gauss, gauss = np.random.get_state(legacy=True)
-    if name != "MT19937":
-        raise NotImplementedError("only the MT19937 legacy RandomState is supported")
-    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
-    pos_c = ctypes.c_int32(int(pos))
     low = np.array([c[0] for c in calls], dtype=np.int64)
     high = np.array([c[1] for c in calls], dtype=np.int64)
     cnt = np.array([int(c[2]) for c in calls], dtype=np.int64)
     out = np.empty(int(cnt.sum()), dtype=np.int64)
-    rc = L.lib().tw_np_randint_batch(key.ctypes.data, ctypes.byref(pos_c), len(calls),
-                                     low.ctypes.data, high.ctypes.data, cnt.ctypes.data,
-                                     out.ctypes.data)
-    bad = rc != 0
-    # commit the advanced state (even on error: NumPy has consumed the earlier calls' draws)
-    np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
-    if bad:
+    rc = _native_draws(lambda key, pos: L.lib().tw_np_randint_batch(
+        key, pos, len(calls), low.ctypes.data, high.ctypes.data, cnt.ctypes.data,
+        out.ctypes.data))
+    if rc:
         raise ValueError("high <= low")
     offs = np.concatenate([[0], np.cumsum(cnt)])
     return [out[offs[i]:offs[i + 1]] for i in range(len(cnt))]
@@ -57,21 +102,16 @@ def shuffle_pair(X, Z) -> None:
     swaps run.  Arrays the buffer path does not cover (views, object arrays, other RNGs) go
     to np.random.shuffle itself."""
     ix, iz = _shuffle_items(X), _shuffle_items(Z)
-    state = np.random.get_state(legacy=True)
-    if ix is None or iz is None or state[0] != "MT19937":
+    if ix is None or iz is None or (
+            _mt_state() is None and np.random.get_state(legacy=True)[0] != "MT19937"):
         np.random.shuffle(X)
         np.random.shuffle(Z)
         return
-    name, key, pos, has_gauss, gauss = state
-    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
-    pos_c = ctypes.c_int32(int(pos))
     jbuf = np.empty(ix[0] + iz[0], dtype=np.int64)
-    rc = L.lib().tw_np_shuffle_pair(key.ctypes.data, ctypes.byref(pos_c), X.ctypes.data,
-                                    ix[0], ix[1], Z.ctypes.data, iz[0], iz[1],
-                                    jbuf.ctypes.data)
+    rc = _native_draws(lambda key, pos: L.lib().tw_np_shuffle_pair(
+        key, pos, X.ctypes.data, ix[0], ix[1], Z.ctypes.data, iz[0], iz[1], jbuf.ctypes.data))
     if rc:
         raise RuntimeError(f"tw_np_shuffle_pair failed ({rc})")
-    np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
 
 
 def shuffle_draws32(n: int, out=None) -> np.ndarray:
@@ -79,11 +119,6 @@ def shuffle_draws32(n: int, out=None) -> np.ndarray:
     uint32 array j with j[i] for i = n-1 down to 1 (j[0] = 0), the global legacy state advanced
     exactly as the shuffle would advance it (the host half of _engine.DeviceShuffles).
     out: a C-contiguous 4-byte array of n entries to draw into (e.g. pinned memory)."""
-    name, key, pos, has_gauss, gauss = np.random.get_state(legacy=True)
-    if name != "MT19937":
-        raise ValueError("shuffle_draws32 restates the legacy MT19937 RandomState only")
-    key = np.ascontiguousarray(key, dtype=np.uint32).copy()
-    pos_c = ctypes.c_int32(int(pos))
     if out is None:
         j = np.zeros(max(int(n), 0), dtype=np.uint32)
     else:
@@ -92,34 +127,33 @@ def shuffle_draws32(n: int, out=None) -> np.ndarray:
             raise ValueError("shuffle_draws32: out must be a contiguous array of n 4-byte items")
         if n > 0:
             j[0] = 0
-    rc = L.lib().tw_np_shuffle_draws32(key.ctypes.data, ctypes.byref(pos_c), int(n),
-                                       j.ctypes.data)
+    rc = _native_draws(lambda key, pos: L.lib().tw_np_shuffle_draws32(key, pos, int(n),
+                                                                       j.ctypes.data))
     if rc:
         raise ValueError(f"tw_np_shuffle_draws32 failed ({rc}) for n = {n}")
-    np.random.set_state((name, key, pos_c.value, has_gauss, gauss))
     return j
 
 
 class Session:
     """NumPy's legacy global MT19937 state held in native code for a run of draws.
 
-    While a session is open nothing else may draw from np.random; commit() writes the
-    advanced state back (and is called on exit).  acquire() re-reads it after foreign draws.
-    Every draw equals the corresponding np.random.randint call bit for bit."""
+    The draws advance NumPy's own MT19937 state in place (_mt_state), so foreign draws between
+    them need nothing; where that is unavailable the session holds a copy, nothing else may
+    draw from np.random while it is open, commit() writes it back (and is called on exit) and
+    acquire() re-reads it after foreign draws.  Every draw equals the corresponding
+    np.random.randint call bit for bit."""
 
     def __init__(self):
         self.acquire()
 
     def acquire(self):
-        name, key, pos, self._has_gauss, self._gauss = np.random.get_state(legacy=True)
-        if name != "MT19937":
-            raise NotImplementedError("only the MT19937 legacy RandomState is supported")
-        self._key = np.ascontiguousarray(key, dtype=np.uint32).copy()
-        self._pos = ctypes.c_int32(int(pos))
+        ptrs = _mt_state()
+        self._copy = None if ptrs is not None else _CopiedState()
+        self._key, self._pos = ptrs if ptrs is not None else self._copy.ptrs()
 
     def commit(self):
-        np.random.set_state(("MT19937", self._key, self._pos.value, self._has_gauss,
-                             self._gauss))
+        if self._copy is not None:
+            self._copy.commit()
 
     def __enter__(self):
         return self
@@ -135,9 +169,8 @@ class Session:
         cnt = np.ascontiguousarray(cnt, dtype=np.int64)
         if out is None:
             out = np.empty(int(cnt.sum()), dtype=np.int64)
-        rc = L.lib().tw_np_randint_batch(self._key.ctypes.data, ctypes.byref(self._pos),
-                                         len(cnt), low.ctypes.data, high.ctypes.data,
-                                         cnt.ctypes.data, out.ctypes.data)
+        rc = L.lib().tw_np_randint_batch(self._key, self._pos, len(cnt), low.ctypes.data,
+                                         high.ctypes.data, cnt.ctypes.data, out.ctypes.data)
         if rc:
             raise ValueError("high <= low")
         return out
@@ -145,9 +178,8 @@ class Session:
     def pairs(self, N, kx, kz, B, ix, iz):
         """grad_inc_block's draws of all N shards into int64 arrays ix, iz of shape (N, B)."""
         assert ix.flags.c_contiguous and iz.flags.c_contiguous
-        rc = L.lib().tw_np_randint_pairs(self._key.ctypes.data, ctypes.byref(self._pos),
-                                         int(N), int(kx), int(kz), int(B), ix.ctypes.data,
-                                         iz.ctypes.data)
+        rc = L.lib().tw_np_randint_pairs(self._key, self._pos, int(N), int(kx), int(kz),
+                                         int(B), ix.ctypes.data, iz.ctypes.data)
         if rc:
             raise ValueError("high <= low")
 
@@ -156,7 +188,7 @@ class Session:
         int64 each) receive step s's X and Z indices, in the reference's draw order."""
         assert out.flags.c_contiguous and out.shape[0] >= S
         lib = L.lib()
-        key, pos = self._key.ctypes.data, ctypes.byref(self._pos)
+        key, pos = self._key, self._pos
         for st in range(S):
             rc = lib.tw_np_randint_pairs(key, pos, int(N), int(kx), int(kz), int(B),
                                          out[st, 0].ctypes.data, out[st, 1].ctypes.data)
