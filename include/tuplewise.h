@@ -504,6 +504,10 @@ int tw_np_mt_next32(uint32_t* key, int32_t* pos, int64_t cnt, uint32_t* out);
  * into ix[s*B..] then randint(0,kz,B) into iz[s*B..].  Returns 1 if kx or kz <= 0. */
 int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
                         int64_t B, int64_t* ix, int64_t* iz);
+/* S consecutive steps of those draws (the replay loop's segment between two reshuffles):
+ * out is (S, 2, N, B) int64 — out[s][0] the step's X indices, out[s][1] its Z indices. */
+int tw_np_randint_pairs_steps(uint32_t* key, int32_t* pos, int32_t S, int32_t N, int64_t kx,
+                              int64_t kz, int64_t B, int64_t* out);
 /* np.random.shuffle(x); np.random.shuffle(z) — the in-place shuffles of UN
  * (compute_stats.py:66-67, estimation-experiment/main.py:46-47) — on C-contiguous arrays of
  * nx / nz items of isx / isz bytes (rows of a 2-D array are items): legacy RandomState's

@@ -223,3 +223,22 @@ def test_state_in_place_and_copied_paths(tw, in_place, monkeypatch):
     assert gg == g
     assert np.array_equal(got_b, b) and np.array_equal(k, j)
     assert np.random.random() == end
+
+
+def test_session_pairs_steps_match_per_step_draws(tw):
+    """Session.pairs_steps (one native call for S steps, tw_np_randint_pairs_steps) == S
+    steps of grad_inc_block's per-shard randint(0,kx,B), randint(0,kz,B) calls."""
+    from tuplewise.numpy_rng import Session
+    S, N, kx, kz, B = 7, 5, 91, 7, 33
+    np.random.seed(17)
+    want = np.empty((S, 2, N, B), np.int64)
+    for st in range(S):
+        for s in range(N):
+            want[st, 0, s] = np.random.randint(0, kx, B)
+            want[st, 1, s] = np.random.randint(0, kz, B)
+    probe = np.random.random()
+    np.random.seed(17)
+    out = np.empty((S + 2, 2, N, B), np.int64)
+    with Session() as sess:
+        sess.pairs_steps(S, N, kx, kz, B, out)
+    assert np.array_equal(out[:S], want) and np.random.random() == probe

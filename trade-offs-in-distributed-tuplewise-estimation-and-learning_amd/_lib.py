@@ -112,6 +112,7 @@ _SIGNATURES = {
     "tw_np_randint_batch": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],
+    "tw_np_randint_pairs_steps": [_vp, _vp, _i32, _i32, _i64, _i64, _i64, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],
     "tw_shuffle_swaps_work_bytes": [_i64, _i64],

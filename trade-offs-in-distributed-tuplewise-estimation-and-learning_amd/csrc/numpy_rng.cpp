@@ -582,6 +582,20 @@ int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int6
   return 0;
 }
 
+// S consecutive steps of grad_inc_block's draws: out is (S, 2, N, B) int64, out[s][0] the
+// step's X indices of all N shards and out[s][1] its Z indices (tw_np_randint_pairs per step).
+int tw_np_randint_pairs_steps(uint32_t* key, int32_t* pos, int32_t S, int32_t N, int64_t kx,
+                              int64_t kz, int64_t B, int64_t* out) {
+  if (kx <= 0 || kz <= 0 || S < 0 || N < 0 || B < 0) return 1;
+  const int64_t per = (int64_t)N * B;
+  for (int32_t st = 0; st < S; ++st) {
+    int64_t* o = out + (int64_t)st * 2 * per;
+    const int rc = tw_np_randint_pairs(key, pos, N, kx, kz, B, o, o + per);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 // np.random.shuffle(x); np.random.shuffle(z) on C-contiguous arrays of nx / nz items of isx /
 // isz bytes (rows of a 2-D array are items): the same draws from the same stream, the same
 // swaps, the same final state.  x's draws come first; x's swaps then run on a second thread

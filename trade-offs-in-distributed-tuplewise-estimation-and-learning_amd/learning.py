@@ -187,7 +187,7 @@ class SGDEngine:
         # copied into persistent tables (captured replay graphs keep valid pointers) through a
         # pinned staging buffer, asynchronously: the host does not wait for queued steps
         t = self.t
-        rx, rz = np.stack(self._local(rows_x)), np.stack(self._local(rows_z))
+        rx, rz = np.asarray(self._local(rows_x)), np.asarray(self._local(rows_z))
         if self.rows_x is None or tuple(self.rows_x.shape) != rx.shape:
             self.rows_x = L.empty(rx.shape, t.int64)
             self.rows_z = L.empty(rz.shape, t.int64)
@@ -651,8 +651,14 @@ class _ReplayDraws:
 
     def swr_rows(self, n_X, n_Z):
         N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
-        flat = self.rng.randint_flat([0] * (2 * N), [n_X] * N + [n_Z] * N, [kx] * N + [kz] * N)
-        return list(flat[:N * kx].reshape(N, kx)), list(flat[N * kx:].reshape(N, kz))
+        if getattr(self, "_swr_args", (None,))[0] != (N, n_X, n_Z, kx, kz):
+            self._swr_args = ((N, n_X, n_Z, kx, kz), np.zeros(2 * N, np.int64),
+                              np.array([n_X] * N + [n_Z] * N, np.int64),
+                              np.array([kx] * N + [kz] * N, np.int64))
+        flat = self.rng.randint_flat(*self._swr_args[1:])
+        # (N, kx) and (N, kz) arrays: row s is shard s's draw (indexable like the list of
+        # arrays SWR_divide returns)
+        return flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, kz)
 
     def segment_capacity(self) -> int:
         """Steps per drawn segment: <= 256, and <= 64 MiB of int64 draws per buffer."""

@@ -187,10 +187,8 @@ class Session:
         """S consecutive steps of grad_inc_block's draws: out[s, 0] and out[s, 1] ((N, B)
         int64 each) receive step s's X and Z indices, in the reference's draw order."""
         assert out.flags.c_contiguous and out.shape[0] >= S
-        lib = L.lib()
-        key, pos = self._key, self._pos
-        for st in range(S):
-            rc = lib.tw_np_randint_pairs(key, pos, int(N), int(kx), int(kz), int(B),
-                                         out[st, 0].ctypes.data, out[st, 1].ctypes.data)
-            if rc:
-                raise ValueError("high <= low")
+        assert out.shape[1:] == (2, N, B) and out.dtype == np.int64
+        rc = L.lib().tw_np_randint_pairs_steps(self._key, self._pos, int(S), int(N), int(kx),
+                                               int(kz), int(B), out.ctypes.data)
+        if rc:
+            raise ValueError("high <= low")
