@@ -4,6 +4,7 @@ an AVX2 left-pack with a 256-entry LUT) is built with -fsanitize=address,undefin
 (`make -C csrc sanitize`, tests/native/numpy_rng_driver.cpp) and run on the AVX-512 (where the
 CPU has it), AVX2 and portable paths; every draw and the advanced state must equal np.random's own, and any
 sanitizer report aborts the driver (non-zero exit)."""
+import fcntl
 import os
 import pathlib
 import subprocess
@@ -18,8 +19,12 @@ EXE = ROOT / "tests" / "native" / "build" / "numpy_rng_asan"
 
 @pytest.fixture(scope="module")
 def driver():
-    r = subprocess.run(["make", "-s", "-C", str(CSRC), "sanitize"], capture_output=True,
-                       text=True, timeout=300)
+    # one build at a time: pytest-xdist workers would otherwise relink the driver under a run
+    EXE.parent.mkdir(parents=True, exist_ok=True)
+    with open(EXE.parent / ".build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", str(CSRC), "sanitize"], capture_output=True,
+                           text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     return EXE
 
