@@ -771,6 +771,7 @@ def main():
     # incomplete U-statistic (BASELINE config C3: B pairs per shard + a repartition per step;
     # cs.UnNBT's loop, device-RNG draws): pairs/s and the k_count_rng roofline
     ops.count_rng = kernel_ms.wrap(ops.count_rng)
+    ops.count_rng_step = kernel_ms.wrap(ops.count_rng_step)  # count + next repartition
     B_inc = args.incomplete_B
     S.UnNB_many(B_inc, 5, range(30_000, 30_000 + args.warmup))
     torch.cuda.synchronize()
@@ -787,6 +788,7 @@ def main():
         dt_inc = float(tt.item())
     kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
     ops.count_rng = ops.count_rng.__wrapped__
+    ops.count_rng_step = ops.count_rng_step.__wrapped__
     inc_pairs_rank = args.shards * B_inc
     inc_replay = incomplete_replay(X, Z, args.shards, B_inc)
     strong = None if args.no_strong else strong_c3(args, group, rank, world, barrier, torch, dist)
@@ -881,7 +883,8 @@ def main():
         "incomplete": {
             "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
                     "drawn pairs per shard (Philox4x32-10, two pairs per block, Lemire maps) "
-                    "counted per step on float32 score images in LDS",
+                    "counted per step on float32 score images in LDS; one launch per step "
+                    "(the next repartition rides in the count threads)",
             "B_per_shard": B_inc, "value": inc_pairs_rank * world * args.steps / dt_inc,
             "unit": "pairs/s", "ms_per_step": dt_inc / args.steps * 1e3,
             "estimate_last_step": float(est_inc),
@@ -897,8 +900,9 @@ def main():
                          "kernel_ms": kms_inc,
                          "note": f"{INC_LANE_OPS} lane-ops per pair (SURVEY.md §8(d) contract "
                                  "constant: 2 Philox4x32-10 words + 2 range maps + 1 compare); "
-                                 "kernel_ms = the whole tw_count_pairs_rng_ws call (one "
-                                 "kernel: float32 score images in LDS, Philox draws, compares); "
+                                 "kernel_ms = the whole tw_count_pairs_rng_step call (one "
+                                 "kernel: float32 score images in LDS, Philox draws, compares, "
+                                 "and the next repartition's gathers in the same threads); "
                                  "frac is against the f64 lane-op "
                                  "peak of the contract, frac_vs_int32_op_peak against the "
                                  "measured 32-bit integer VOP2 issue rate (the Philox work is "

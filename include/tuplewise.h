@@ -208,6 +208,21 @@ int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, const void* d
                           int64_t max_nz, int64_t B, uint64_t seed, uint64_t shard_base,
                           int32_t dtype, int32_t pred, void* d_work, int64_t work_bytes,
                           uint64_t* d_out, void* stream);
+/* One step of cs.UnNBT's loop (compute_stats.py:119-123) in device-RNG mode: the counts of
+ * tw_count_pairs_rng_ws for the current partition — except that d_out must already be zero
+ * (accumulated into) — and the NEXT repartition: d_x_next = the n_x scores of d_x permuted
+ * with key_x, d_z_next likewise (as tw_permute_pair), d_out_next[0 .. n_next_shards) zeroed.
+ * On the float32-image path (above) the next repartition's gathers ride in the count threads
+ * of the same launch; otherwise the count, tw_permute_pair and a memset run in turn.
+ * d_x_next == NULL: count only.  Replaces the repartition + UB loop of compute_stats.py:104-110
+ * as tw_count_pairs_step does for est.UnNT. */
+int tw_count_pairs_rng_step(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                            const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                            int64_t max_nz, int64_t B, uint64_t seed, uint64_t shard_base,
+                            int32_t dtype, int32_t pred, void* d_work, int64_t work_bytes,
+                            uint64_t* d_out, int64_t n_x, void* d_x_next, uint64_t key_x,
+                            int64_t n_z, void* d_z_next, uint64_t key_z, uint64_t* d_out_next,
+                            int32_t n_next_shards, void* stream);
 
 /* ---- Row A2 (prod/gini) and f1 (conv_AUC): float pair sums, complete -------------------
  * d_out[s] (double) = sum over all pairs of shard s of kern(x_i, z_j).  Deterministic: fixed

@@ -441,6 +441,56 @@ def test_count_pairs_step_fused_repartition(gpu, dtype, mode):
     assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 12))
 
 
+@pytest.mark.parametrize("dtype,mode,big", [("f64", "gt", False), ("f64", "half", False),
+                                            ("i64", "gt", False), ("f64", "gt", True)])
+def test_count_pairs_rng_step_fused_repartition(gpu, dtype, mode, big):
+    """tw_count_pairs_rng_step: counts == tw_count_pairs_rng_ws (the same draws) on ragged
+    shards incl. empty ones, and the same call writes the next repartition (== the oracle
+    permutation) and zeroes the next counters — on the float32-image path, where the
+    permutation's gathers ride in the count threads (B small and large: the gathers issued in
+    the Philox loop or left to the tail), and past it (big: a shard too large for LDS images,
+    count + tw_permute_pair + memset)."""
+    import torch
+    from tuplewise import _engine as E, _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(22)
+    nx = [0, 1, 5, 257, 3000, 1, 4096 + 3, 700] + ([41_000] if big else [])
+    nz = [3, 0, 9, 1000, 2049, 1, 513, 700] + ([1_000] if big else [])
+    if dtype == "f64":
+        xs = [rng.normal(size=k).round(1) for k in nx]
+        zs = [rng.normal(size=k).round(1) for k in nz]
+        code = L.TW_F64
+    else:
+        xs = [rng.randint(-50, 50, k) for k in nx]
+        zs = [rng.randint(-50, 50, k) for k in nz]
+        code = L.TW_I64
+    sh = E.Shards.from_blocks(xs, zs, code)
+    xo, zo = sh.offsets_dev()
+    pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF}[mode]
+    ops = HipOps()
+    for B in (1, 7, 5000, 300_001):
+        want = ops.count_rng(sh.x, xo, sh.z, zo, len(nx), B, 99 + B, 3, code, pred,
+                             max_nx=max(nx), max_nz=max(nz))
+        out = torch.zeros(len(nx), dtype=torch.int64, device="cuda")
+        out_next = torch.full((5,), 77, dtype=torch.int64, device="cuda")
+        xn, zn = torch.empty_like(sh.x), torch.empty_like(sh.z)
+        ops.count_rng_step(sh.x, xo, sh.z, zo, len(nx), B, 99 + B, 3, code, pred, max(nx),
+                           max(nz), out, xn, 11 + B, zn, 12 + B, out_next)
+        assert torch.equal(out, want), B
+        assert not out_next.cpu().numpy().any()
+        assert np.array_equal(xn.cpu().numpy(), O.permute_scatter(sh.x.cpu().numpy(), 11 + B))
+        assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 12 + B))
+    # count only (no next arrays): the counts alone, out_next zeroed by a memset
+    out = torch.zeros(len(nx), dtype=torch.int64, device="cuda")
+    out_next = torch.full((3,), 5, dtype=torch.int64, device="cuda")
+    L.call("tw_count_pairs_rng_step", L.ptr(sh.x), L.ptr(xo), L.ptr(sh.z), L.ptr(zo), len(nx),
+           max(nx), max(nz), 4000, 5, 0, code, pred, None, 0, L.ptr(out), 0, None, 0, 0, None,
+           0, L.ptr(out_next), 3, L.stream_handle())
+    want = ops.count_rng(sh.x, xo, sh.z, zo, len(nx), 4000, 5, 0, code, pred,
+                         max_nx=max(nx), max_nz=max(nz))
+    assert torch.equal(out, want) and not out_next.cpu().numpy().any()
+
+
 def test_device_sigmoid_accuracy(gpu):
     """The device sigma (tw_common.h pair_weight: 1 / (1 + exp(-S)) with the device exp) within 4 ulp of
     NumPy's 1 / (1 + exp(-S)) over the whole range, incl. saturation, +-inf and NaN: one

@@ -2,6 +2,7 @@
 // called by the tw_count_pairs_idx(32)_ws / tw_count_pairs_rng_ws entry points (rankcount.hip).
 #pragma once
 #include "tw_common.h"
+#include "nextstep.h"
 
 namespace tw {
 
@@ -22,8 +23,10 @@ int launch_idx_images(const void* x, const int64_t* x_off, const void* z, const 
                       int32_t dtype, int32_t pred, const ImgPlan& p, uint64_t* out,
                       hipStream_t st);
 
+// nxt: the next repartition carried by the count threads (nxt.blocks == 0: none)
 int launch_rng_images(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                       int32_t n_shards, int64_t B, uint64_t seed, uint64_t sid, int32_t dtype,
-                      int32_t pred, const ImgPlan& p, uint64_t* out, hipStream_t st);
+                      int32_t pred, const ImgPlan& p, uint64_t* out, const NextStep& nxt,
+                      hipStream_t st);
 
 }  // namespace tw

@@ -18,6 +18,7 @@
 // call at the bench shape), no workspace.  Scores with many exact ties between the samples
 // (small integers) take the gather for every tied pair: correct, slower.
 #include "imagecount.h"
+#include "nextstep.h"
 #include <algorithm>
 
 namespace tw {
@@ -211,17 +212,63 @@ __global__ __launch_bounds__(kImgThreads) void k_count_idx_img(
 
 // Device RNG: the draws of tw_count_pairs_rng (Philox block q -> pairs 2q and 2q+1, Lemire
 // maps; csrc/count.hip k_count_rng) compared on the images.
+// The next repartition riding in the count blocks (tw_count_pairs_rng_step): a block's LDS
+// holds its shard's images, so no spare block of the same launch could share a CU with it;
+// instead every count thread carries ~8 of the next permutation's gathers (nextstep.h's
+// out[p] = in[perm^-1(p)]), one issued every `every` iterations of its Philox loop and stored
+// when the next is issued, so the random reads' latency hides behind the VALU-bound draws.
+struct NextSlice {
+  const NextStep& nx;
+  int64_t e0, stride, tot;
+  int k = 0, kmax;
+  uint64_t v = 0;
+  int64_t p = -1;
+  __device__ NextSlice(const NextStep& n) : nx(n) {
+    e0 = (int64_t)blockIdx.x * kImgThreads + threadIdx.x;
+    stride = (int64_t)gridDim.x * kImgThreads;
+    tot = n.nx + n.nz;
+    kmax = n.blocks ? (int)((tot + stride - 1) / stride) : 0;
+  }
+  __device__ __forceinline__ void commit() {
+    if (p >= 0 && p < nx.nx)
+      nx.x_out[p] = v;
+    else if (p >= nx.nx && p < tot)
+      nx.z_out[p - nx.nx] = v;
+  }
+  __device__ __forceinline__ void issue() {  // commits the previous gather, issues the next
+    commit();
+    p = e0 + (int64_t)k * stride;
+    ++k;
+    if (p < nx.nx)
+      v = nx.x_in[feistel_perm_inv(nx.fx, (uint64_t)p, (uint64_t)nx.nx)];
+    else if (p < tot)
+      v = nx.z_in[feistel_perm_inv(nx.fz, (uint64_t)(p - nx.nx), (uint64_t)nx.nz)];
+  }
+  __device__ __forceinline__ void finish() {
+    while (k < kmax) issue();
+    commit();
+    p = -1;
+  }
+};
+
 template <typename T, int PRED, int QU>
 __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, int64_t B, int parts, uint32_t k0, uint32_t k1,
-    uint32_t sid, unsigned long long* __restrict__ out) {
+    uint32_t sid, unsigned long long* __restrict__ out, NextStep nxt) {
   extern __shared__ __attribute__((aligned(16))) float img[];
   const int lb = xcd_block(blockIdx.x, gridDim.x);
   const int s = lb / parts;
   const int part = lb - s * parts;
   const int64_t xb = x_off[s], zb = z_off[s];
   const int64_t nx = x_off[s + 1] - xb, nz = z_off[s + 1] - zb;
+  NextSlice ns(nxt);
+  if (nxt.nzero > 0) {  // the next step's counters
+    for (int64_t i = (int64_t)blockIdx.x * kImgThreads + threadIdx.x; i < nxt.nzero;
+         i += (int64_t)gridDim.x * kImgThreads)
+      nxt.zero[i] = 0;
+  }
+  if (ns.kmax > 0) ns.issue();  // in flight while the images are staged
   unsigned acc = 0;
   if (nx > 0 && nz > 0) {
     float* lx = img;
@@ -233,10 +280,18 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
     const int64_t nq = (B + 1) / 2;
     const int64_t per = (nq + parts - 1) / parts;
     const int64_t q0 = (int64_t)part * per, q1 = std::min<int64_t>(nq, q0 + per);
+    // next-step gathers: one every `every` iterations (block-uniform)
+    const int64_t nit = (q1 - q0 + (int64_t)QU * kImgThreads - 1) / ((int64_t)QU * kImgThreads);
+    const int every = ns.kmax > 1 ? (int)std::max<int64_t>(1, nit / ns.kmax) : 0;
+    int it = 0;
     // trip count uniform over the block (q1 - q0 is), so the ballot below is wave-uniform.
     // QU Philox blocks per thread and iteration, computed unconditionally (a dead lane's draw
     // is discarded): independent chains the scheduler interleaves (16 waves per CU only).
     for (int64_t qb = q0; qb < q1; qb += (int64_t)QU * kImgThreads) {
+      if (every && ++it == every) {
+        it = 0;
+        if (ns.k < ns.kmax) ns.issue();
+      }
       u32x4 r[QU];
 #pragma unroll
       for (int u = 0; u < QU; ++u) {
@@ -270,6 +325,7 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
       }
     }
   }
+  ns.finish();
   unsigned long long tot = wave_sum_u64((unsigned long long)acc);
   __shared__ unsigned long long part_sum[kImgThreads / kWave];
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -365,7 +421,8 @@ template int launch_idx_images<int64_t>(const void*, const int64_t*, const void*
 template <typename T, int PRED, int QU>
 static int launch_rng_img_q(const void* x, const int64_t* x_off, const void* z,
                             const int64_t* z_off, int32_t n_shards, int64_t B, uint64_t seed,
-                            uint64_t sid, const ImgPlan& p, uint64_t* out, hipStream_t st) {
+                            uint64_t sid, const ImgPlan& p, uint64_t* out, const NextStep& nxt,
+                            hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_img<T, PRED, QU>,
@@ -376,7 +433,7 @@ static int launch_rng_img_q(const void* x, const int64_t* x_off, const void* z,
   hipLaunchKernelGGL((k_count_rng_img<T, PRED, QU>), dim3(n_shards * p.parts),
                      dim3(kImgThreads), p.lds, st, (const T*)x, x_off, (const T*)z, z_off, B,
                      p.parts, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)sid,
-                     (unsigned long long*)out);
+                     (unsigned long long*)out, nxt);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -386,25 +443,27 @@ static int g_img_rng_qu = 2;  // tuning: Philox blocks per thread and iteration 
 template <typename T, int PRED>
 static int launch_rng_img_t(const void* x, const int64_t* x_off, const void* z,
                             const int64_t* z_off, int32_t n_shards, int64_t B, uint64_t seed,
-                            uint64_t sid, const ImgPlan& p, uint64_t* out, hipStream_t st) {
+                            uint64_t sid, const ImgPlan& p, uint64_t* out, const NextStep& nxt,
+                            hipStream_t st) {
   if (g_img_rng_qu == 4)
-    return launch_rng_img_q<T, PRED, 4>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+    return launch_rng_img_q<T, PRED, 4>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
   if (g_img_rng_qu == 2)
-    return launch_rng_img_q<T, PRED, 2>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
-  return launch_rng_img_q<T, PRED, 1>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+    return launch_rng_img_q<T, PRED, 2>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
+  return launch_rng_img_q<T, PRED, 1>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
 }
 
 int launch_rng_images(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                       int32_t n_shards, int64_t B, uint64_t seed, uint64_t sid, int32_t dtype,
-                      int32_t pred, const ImgPlan& p, uint64_t* out, hipStream_t st) {
+                      int32_t pred, const ImgPlan& p, uint64_t* out, const NextStep& nxt,
+                      hipStream_t st) {
   if (dtype == TW_F64) {
     if (pred == TW_PRED_HALF)
-      return launch_rng_img_t<double, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
-    return launch_rng_img_t<double, TW_PRED_GT>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+      return launch_rng_img_t<double, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
+    return launch_rng_img_t<double, TW_PRED_GT>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
   }
   if (pred == TW_PRED_HALF)
-    return launch_rng_img_t<long long, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
-  return launch_rng_img_t<long long, TW_PRED_GT>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, st);
+    return launch_rng_img_t<long long, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
+  return launch_rng_img_t<long long, TW_PRED_GT>(x, x_off, z, z_off, n_shards, B, seed, sid, p, out, nxt, st);
 }
 
 }  // namespace tw

@@ -1,9 +1,8 @@
 // nextstep.h — the next repartition of est.UnNT's loop carried by spare blocks of a count launch
 // (k_count_complete via tw_count_pairs_step): the keyed permutation of both samples as a
-// gather and the zeroing of the next step's counters.  (Tried and dropped for the ranked
-// incomplete count: its draw-and-count blocks fill every CU's LDS and wave slots, so spare
-// blocks could only run after them, with less parallelism than the standalone permute:
-// 0.150 -> 0.158 ms per UnNBT step.)
+// gather and the zeroing of the next step's counters.  (The device-RNG image count carries the
+// same gathers in its count threads instead — csrc/imagecount.hip NextSlice — since its LDS
+// footprint leaves no room for spare blocks beside its own.)
 #pragma once
 #include "feistel.h"
 

@@ -1049,7 +1049,7 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
       hipStream_t st = (hipStream_t)stream;
       TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
       return launch_rng_images(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, dtype,
-                               pr, ip, d_out, st);
+                               pr, ip, d_out, NextStep{}, st);
     }
   }
   const RngRankPlan p = plan_rng_ranked(n_shards, max_nx, max_nz, pred, B);
@@ -1070,6 +1070,59 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
   if (pred == TW_PRED_HALF)
     return launch_rng_ranked<long long, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
   return launch_rng_ranked<long long, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
+}
+
+extern "C" int tw_permute_pair(const void* d_x_in, void* d_x_out, int64_t n, uint64_t key_x,
+                               const void* d_z_in, void* d_z_out, int64_t m, uint64_t key_z,
+                               void* stream);
+
+// One UnNBT step (compute_stats.py:119-123, device-RNG mode): the counts of the current
+// partition into d_out (zero on entry) and the next repartition of both samples into
+// d_x_next / d_z_next (as tw_permute_pair) with d_out_next zeroed.  On the float32-image path
+// the next repartition's gathers ride in the count threads (csrc/imagecount.hip NextSlice):
+// one launch per step.  Elsewhere: the count call, then tw_permute_pair and a memset.
+extern "C" int tw_count_pairs_rng_step(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                       const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                                       int64_t max_nz, int64_t B, uint64_t seed,
+                                       uint64_t stream_id, int32_t dtype, int32_t pred,
+                                       void* d_work, int64_t work_bytes, uint64_t* d_out,
+                                       int64_t n_x, void* d_x_next, uint64_t key_x, int64_t n_z,
+                                       void* d_z_next, uint64_t key_z, uint64_t* d_out_next,
+                                       int32_t n_next_shards, void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && B >= 0 && max_nx >= 0 && max_nz >= 0 && n_x >= 0 && n_z >= 0 &&
+                   n_x < (1ll << 60) && n_z < (1ll << 60) && n_next_shards >= 0,
+               "tw_count_pairs_rng_step: bad sizes");
+  TW_ARG_CHECK(d_x_next == nullptr || ((n_x == 0 || d_x_next != d_x) &&
+                                       (n_z == 0 || (d_z_next != nullptr && d_z_next != d_z))),
+               "tw_count_pairs_rng_step: next arrays must be distinct buffers");
+  hipStream_t st = (hipStream_t)stream;
+  if (g_rng_codes_by_bucket == 3 && B > 0 && n_shards > 0 && (dtype == TW_F64 || dtype == TW_I64)) {
+    const int32_t pr = (pred == TW_PRED_SUBGT && dtype == TW_F64) ? TW_PRED_GT : pred;
+    const ImgPlan ip = plan_images(n_shards, max_nx, max_nz, pr, (B + 1) / 2);
+    if (ip.ok) {
+      NextStep nxt{};
+      if (d_x_next != nullptr)
+        nxt = NextStep{(const uint64_t*)d_x, (uint64_t*)d_x_next, n_x, (const uint64_t*)d_z,
+                       (uint64_t*)d_z_next, n_z, (unsigned long long*)d_out_next,
+                       d_out_next ? (int64_t)n_next_shards : 0,
+                       make_feistel(std::max<int64_t>(n_x, 1), key_x),
+                       make_feistel(std::max<int64_t>(n_z, 1), key_z), 1, 0, 0};
+      else if (d_out_next != nullptr && n_next_shards > 0)
+        TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+      return launch_rng_images(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, dtype,
+                               pr, ip, d_out, nxt, st);
+    }
+  }
+  int rc = tw_count_pairs_rng_ws(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed,
+                                 stream_id, dtype, pred, d_work, work_bytes, d_out, stream);
+  if (rc != TW_OK) return rc;
+  if (d_x_next != nullptr && n_x + n_z > 0) {
+    rc = tw_permute_pair(d_x, d_x_next, n_x, key_x, d_z, d_z_next, n_z, key_z, stream);
+    if (rc != TW_OK) return rc;
+  }
+  if (d_out_next != nullptr && n_next_shards > 0)
+    TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+  return TW_OK;
 }
 
 extern "C" int tw_count_rng_set_codes(int32_t by_bucket) {

@@ -151,6 +151,22 @@ class HipOps:
                    L.ptr(out), L.stream_handle())
         return out
 
+    def count_rng_step(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype,
+                       pred, max_nx, max_nz, out, x_next, key_x, z_next, key_z, out_next):
+        """Device-RNG incomplete counts of the current partition into `out` (already zero) and
+        the next repartition into x_next / z_next with out_next zeroed, in one launch where the
+        float32-image kernel applies (tw_count_pairs_rng_step)."""
+        wb = int(L.lib().tw_count_pairs_rng_work_bytes(int(n_shards), int(max_nx), int(max_nz),
+                                                       int(dtype), int(pred)))
+        work = L.empty((max(wb, 1),), self.t.uint8)
+        L.call("tw_count_pairs_rng_step", L.ptr(x), L.ptr(x_off_dev), L.ptr(z),
+               L.ptr(z_off_dev), int(n_shards), int(max_nx), int(max_nz), int(B), int(seed),
+               int(shard_base), int(dtype), int(pred), L.ptr(work), wb, L.ptr(out),
+               int(x.numel()), L.ptr(x_next), int(key_x), int(z.numel()), L.ptr(z_next),
+               int(key_z), L.ptr(out_next),
+               int(out_next.numel()) if out_next is not None else 0, L.stream_handle())
+        return out
+
     def to_dev(self, arr):
         return L.to_device(arr)
 
@@ -345,18 +361,20 @@ class ShardedSample:
             self.repartition(key)
         return np.mean(self.values(self.global_counts(self.local_counts())))
 
-    def _run_steps(self, keys, count_local, fusable):
+    def _run_steps(self, keys, count_local, fusable, step=None):
         """One repartition + one count of all local shards per key, with no host round trip
         per step; returns the (T, G*N) device counts in global shard order (one all-reduce).
-        One GPU and a fusable (all-pairs) count: one launch per step counts step i and, on
-        spare blocks of the same grid, repartitions both samples for step i+1
-        (tw_count_pairs_step).  Several GPUs: repartition i+1 (pack kernels, the split-size
-        copy, the RCCL all-to-all) is issued on a side stream while the counts of step i run.
-        count_local(i) enqueues step i's count on the current stream."""
+        One GPU and a one-launch step (step(i, out, X_next, key_x, Z_next, key_z, out_next):
+        tw_count_pairs_step for the all-pairs count, tw_count_pairs_rng_step for the
+        device-RNG incomplete count): each launch counts step i and repartitions both samples
+        for step i+1.  Several GPUs: repartition i+1 (pack kernels, the split-size copy, the
+        RCCL all-to-all) is issued on a side stream while the counts of step i run.
+        count_local(i) enqueues step i's count on the current stream; fusable: the all-pairs
+        count (its multi-GPU launches accumulate into one zeroed buffer)."""
         t = self.t
         local = []
-        if not self._multi() and fusable and hasattr(self.ops, "count_step"):
-            # each launch counts step i and, on spare blocks, repartitions for step i+1
+        if not self._multi() and step is not None:
+            # each launch counts step i and repartitions for step i+1
             self._repartition(keys[0])
             out = t.zeros((self.N,), dtype=t.int64, device=self.X.device)
             for i in range(len(keys)):
@@ -369,9 +387,7 @@ class ShardedSample:
                     out_n = t.empty((self.N,), dtype=t.int64, device=self.X.device)
                     kx = (keys[i + 1] * 2) & (2 ** 64 - 1)
                     kz = (keys[i + 1] * 2 + 1) & (2 ** 64 - 1)
-                self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
-                                    self.max_nx, self.max_nz, self.dtype, self.pred, out, Xn, kx,
-                                    Zn, kz, out_n)
+                step(i, out, Xn, kx, Zn, kz, out_n)
                 local.append(out)
                 if not last:
                     self.X, self.Z, out = Xn, Zn, out_n
@@ -431,7 +447,14 @@ class ShardedSample:
             return []
         if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
             return [self.UnN(k) for k in keys]
-        counts = self._run_steps(keys, lambda i: self.local_counts(), self.algo == "pairs")
+        fusable = self.algo == "pairs"
+        step = None
+        if fusable and hasattr(self.ops, "count_step"):
+            def step(i, out, Xn, kx, Zn, kz, out_n):
+                self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                    self.max_nx, self.max_nz, self.dtype, self.pred, out, Xn, kx,
+                                    Zn, kz, out_n)
+        counts = self._run_steps(keys, lambda i: self.local_counts(), fusable, step)
         return [np.mean(v) for v in self.values(counts)]
 
     def UnNT(self, T: int, key0: int = 0) -> np.float64:
@@ -461,5 +484,11 @@ class ShardedSample:
             return []
         if not self.X.is_cuda:
             return [self.UnNB(B, sd, k) for sd, k in zip(seeds, keys)]
-        counts = self._run_steps(keys, lambda i: self._count_rng(B, seeds[i]), False)
+        step = None
+        if hasattr(self.ops, "count_rng_step"):
+            def step(i, out, Xn, kx, Zn, kz, out_n):
+                self.ops.count_rng_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                        B, seeds[i], self.rank * self.N, self.dtype, self.pred,
+                                        self.max_nx, self.max_nz, out, Xn, kx, Zn, kz, out_n)
+        counts = self._run_steps(keys, lambda i: self._count_rng(B, seeds[i]), False, step)
         return [np.mean(v) for v in self.values(counts, pairs=B)]
