@@ -705,6 +705,7 @@ def main():
     ops = S.ops
     ops.count = kernel_ms.wrap(ops.count)
     ops.count_step = kernel_ms.wrap(ops.count_step)  # count + next repartition on spare blocks
+    ops.count_sorted_step = kernel_ms.wrap(ops.count_sorted_step)  # sorted count + next
 
     def barrier():
         if group is not None:
@@ -874,8 +875,9 @@ def main():
         "sorted_count": {
             "note": "same UnN steps with the exact O((n+m) log m)-class count (algo='sorted':"
                     " value buckets of z in LDS for shards of <= 16384, else sort + binary "
-                    "search; bit-identical estimates); pairs are logical, not compared one by "
-                    "one",
+                    "search; bit-identical estimates; one launch per step, the next "
+                    "repartition's gathers in the count threads); pairs are logical, not "
+                    "compared one by one",
             "value": total_pairs / dt_sorted, "unit": "logical pairs/s",
             "ms_per_step": dt_sorted / args.steps * 1e3, "count_kernels_ms": kms_sorted,
             "estimate_last_step": float(est_sorted),

@@ -115,6 +115,19 @@ int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, const void* d
                           const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
                           int64_t max_nz, int32_t dtype, int32_t pred, void* d_work,
                           uint64_t* d_out, void* stream);
+/* One step of est.UnNT's loop with the exact sorted count: the counts of tw_count_pairs_sorted
+ * for the current partition — except that d_out must already be zero (accumulated into) — and
+ * the NEXT repartition: d_x_next / d_z_next = the scores permuted with key_x / key_z (as
+ * tw_permute_pair), d_out_next[0 .. n_next_shards) zeroed.  On the bucket path (every shard's
+ * nz <= 16384) the permutation's gathers ride in the count threads of the same launch;
+ * otherwise the count, tw_permute_pair and a memset run in turn.  d_x_next == NULL: count only.
+ * Replaces the shuffle + UN loop of estimation-experiment/main.py:43-79 like tw_count_pairs_step. */
+int tw_count_pairs_sorted_step(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                               const int64_t* d_z_off, int32_t n_shards, int64_t max_nx,
+                               int64_t max_nz, int32_t dtype, int32_t pred, void* d_work,
+                               uint64_t* d_out, int64_t n_x, void* d_x_next, uint64_t key_x,
+                               int64_t n_z, void* d_z_next, uint64_t key_z,
+                               uint64_t* d_out_next, int32_t n_next_shards, void* stream);
 /* Shards with nz <= 16384 (default 1): the count comes from value buckets of z in LDS (an
  * LDS histogram, prefix and scatter, then one bucket scanned per x) instead of sorted chunks +
  * binary searches; the same integers.  1 = equal-depth buckets (the value-range histogram's

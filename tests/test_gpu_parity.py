@@ -491,6 +491,43 @@ def test_count_pairs_rng_step_fused_repartition(gpu, dtype, mode, big):
     assert torch.equal(out, want) and not out_next.cpu().numpy().any()
 
 
+@pytest.mark.parametrize("dtype,mode,big", [("f64", "gt", False), ("f64", "half", False),
+                                            ("i64", "gt", False), ("f64", "gt", True)])
+def test_count_pairs_sorted_step_fused_repartition(gpu, dtype, mode, big):
+    """tw_count_pairs_sorted_step: counts == the exact all-pairs counts on ragged shards incl.
+    empty ones (NaN-free ties: rounded scores / small integers), and the same launch writes the
+    next repartition (== the oracle permutation) and zeroes the next counters — on the bucket
+    path (gathers in the count threads) and past it (big: a shard with nz > 16384, sort +
+    search, then tw_permute_pair and a memset)."""
+    import torch
+    from tuplewise import _engine as E, _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(23)
+    nx = [0, 1, 5, 257, 3000, 1, 4096 + 3, 700, 9000] + ([2_000] if big else [])
+    nz = [3, 0, 9, 1000, 2049, 1, 513, 700, 16384] + ([20_000] if big else [])
+    if dtype == "f64":
+        xs = [rng.normal(size=k).round(1) for k in nx]
+        zs = [rng.normal(size=k).round(1) for k in nz]
+        code = L.TW_F64
+    else:
+        xs = [rng.randint(-50, 50, k) for k in nx]
+        zs = [rng.randint(-50, 50, k) for k in nz]
+        code = L.TW_I64
+    sh = E.Shards.from_blocks(xs, zs, code)
+    want = E.count_complete(sh, mode, algo="pairs")
+    xo, zo = sh.offsets_dev()
+    pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF}[mode]
+    out = torch.zeros(len(nx), dtype=torch.int64, device="cuda")
+    out_next = torch.full((5,), 77, dtype=torch.int64, device="cuda")
+    xn, zn = torch.empty_like(sh.x), torch.empty_like(sh.z)
+    HipOps().count_sorted_step(sh.x, xo, sh.z, zo, len(nx), max(nx), max(nz), code, pred, out,
+                               xn, 31, zn, 32, out_next)
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want)
+    assert not out_next.cpu().numpy().any()
+    assert np.array_equal(xn.cpu().numpy(), O.permute_scatter(sh.x.cpu().numpy(), 31))
+    assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 32))
+
+
 def test_device_sigmoid_accuracy(gpu):
     """The device sigma (tw_common.h pair_weight: 1 / (1 + exp(-S)) with the device exp) within 4 ulp of
     NumPy's 1 / (1 + exp(-S)) over the whole range, incl. saturation, +-inf and NaN: one

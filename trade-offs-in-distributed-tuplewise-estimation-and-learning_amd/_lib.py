@@ -52,6 +52,8 @@ _SIGNATURES = {
     "tw_count_sorted_set_bucket": [_i32],
     "tw_count_pairs_rng_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _u64, _u64, _i32, _i32,
                               _vp, _i64, _vp, _vp],
+    "tw_count_pairs_sorted_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp,
+                                   _i64, _vp, _u64, _i64, _vp, _u64, _vp, _i32, _vp],
     "tw_count_pairs_rng_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _u64, _u64, _i32,
                                 _i32, _vp, _i64, _vp, _i64, _vp, _u64, _i64, _vp, _u64, _vp,
                                 _i32, _vp],

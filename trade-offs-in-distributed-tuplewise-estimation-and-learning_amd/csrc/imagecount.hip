@@ -212,45 +212,6 @@ __global__ __launch_bounds__(kImgThreads) void k_count_idx_img(
 
 // Device RNG: the draws of tw_count_pairs_rng (Philox block q -> pairs 2q and 2q+1, Lemire
 // maps; csrc/count.hip k_count_rng) compared on the images.
-// The next repartition riding in the count blocks (tw_count_pairs_rng_step): a block's LDS
-// holds its shard's images, so no spare block of the same launch could share a CU with it;
-// instead every count thread carries ~8 of the next permutation's gathers (nextstep.h's
-// out[p] = in[perm^-1(p)]), one issued every `every` iterations of its Philox loop and stored
-// when the next is issued, so the random reads' latency hides behind the VALU-bound draws.
-struct NextSlice {
-  const NextStep& nx;
-  int64_t e0, stride, tot;
-  int k = 0, kmax;
-  uint64_t v = 0;
-  int64_t p = -1;
-  __device__ NextSlice(const NextStep& n) : nx(n) {
-    e0 = (int64_t)blockIdx.x * kImgThreads + threadIdx.x;
-    stride = (int64_t)gridDim.x * kImgThreads;
-    tot = n.nx + n.nz;
-    kmax = n.blocks ? (int)((tot + stride - 1) / stride) : 0;
-  }
-  __device__ __forceinline__ void commit() {
-    if (p >= 0 && p < nx.nx)
-      nx.x_out[p] = v;
-    else if (p >= nx.nx && p < tot)
-      nx.z_out[p - nx.nx] = v;
-  }
-  __device__ __forceinline__ void issue() {  // commits the previous gather, issues the next
-    commit();
-    p = e0 + (int64_t)k * stride;
-    ++k;
-    if (p < nx.nx)
-      v = nx.x_in[feistel_perm_inv(nx.fx, (uint64_t)p, (uint64_t)nx.nx)];
-    else if (p < tot)
-      v = nx.z_in[feistel_perm_inv(nx.fz, (uint64_t)(p - nx.nx), (uint64_t)nx.nz)];
-  }
-  __device__ __forceinline__ void finish() {
-    while (k < kmax) issue();
-    commit();
-    p = -1;
-  }
-};
-
 template <typename T, int PRED, int QU>
 __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
@@ -262,12 +223,12 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
   const int part = lb - s * parts;
   const int64_t xb = x_off[s], zb = z_off[s];
   const int64_t nx = x_off[s + 1] - xb, nz = z_off[s + 1] - zb;
-  NextSlice ns(nxt);
-  if (nxt.nzero > 0) {  // the next step's counters
-    for (int64_t i = (int64_t)blockIdx.x * kImgThreads + threadIdx.x; i < nxt.nzero;
-         i += (int64_t)gridDim.x * kImgThreads)
-      nxt.zero[i] = 0;
-  }
+  // the next repartition riding in the count threads (tw_count_pairs_rng_step): a block's
+  // LDS holds its shard's images, so no spare block of the same launch could share a CU with
+  // it; each thread carries ~8 of the next permutation's gathers, one issued every `every`
+  // iterations of its Philox loop, so the random reads' latency hides behind the draws
+  NextSlice<kImgThreads> ns(nxt);
+  next_step_zero<kImgThreads>(nxt);
   if (ns.kmax > 0) ns.issue();  // in flight while the images are staged
   unsigned acc = 0;
   if (nx > 0 && nz > 0) {

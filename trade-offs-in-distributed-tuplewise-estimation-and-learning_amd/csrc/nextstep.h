@@ -54,4 +54,76 @@ __device__ __forceinline__ void next_step_part(const NextStep& nx, int b) {
   }
 }
 
+// The next repartition carried by the COUNT threads of a launch whose blocks leave no room for
+// spare blocks (LDS-resident shards): thread t of block b owns elements e = b*BS + t + k*stride
+// (stride = grid threads), k < kmax, of the next permutation (next_step_part's gather).
+// NextSlice keeps ONE gather in flight — issue() stores the previous value and issues the next
+// — for kernels with a long loop to spread them over; NextBatch issues up to KB at once and
+// stores them at commit(), for kernels whose middle phases are LDS-bound.
+template <int BS>
+struct NextSlice {
+  const NextStep& nx;
+  int64_t e0, stride, tot;
+  int k = 0, kmax;
+  uint64_t v = 0;
+  int64_t p = -1;
+  __device__ NextSlice(const NextStep& n) : nx(n) {
+    e0 = (int64_t)blockIdx.x * BS + threadIdx.x;
+    stride = (int64_t)gridDim.x * BS;
+    tot = n.nx + n.nz;
+    kmax = n.blocks ? (int)((tot + stride - 1) / stride) : 0;
+  }
+  __device__ __forceinline__ uint64_t gather(int64_t q) const {
+    if (q < nx.nx) return nx.x_in[feistel_perm_inv(nx.fx, (uint64_t)q, (uint64_t)nx.nx)];
+    if (q < tot) return nx.z_in[feistel_perm_inv(nx.fz, (uint64_t)(q - nx.nx), (uint64_t)nx.nz)];
+    return 0;
+  }
+  __device__ __forceinline__ void store(int64_t q, uint64_t val) const {
+    if (q >= 0 && q < nx.nx)
+      nx.x_out[q] = val;
+    else if (q >= nx.nx && q < tot)
+      nx.z_out[q - nx.nx] = val;
+  }
+  __device__ __forceinline__ void issue() {  // stores the previous gather, issues the next
+    store(p, v);
+    p = e0 + (int64_t)k * stride;
+    ++k;
+    v = gather(p);
+  }
+  __device__ __forceinline__ void finish() {
+    while (k < kmax) issue();
+    store(p, v);
+    p = -1;
+  }
+};
+
+template <int BS, int KB>
+struct NextBatch {
+  NextSlice<BS> sl;
+  uint64_t v[KB];
+  __device__ NextBatch(const NextStep& n) : sl(n) {}
+  __device__ __forceinline__ void issue() {
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+      if (k < sl.kmax) v[k] = sl.gather(sl.e0 + (int64_t)k * sl.stride);
+  }
+  __device__ __forceinline__ void commit() {
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+      if (k < sl.kmax) sl.store(sl.e0 + (int64_t)k * sl.stride, v[k]);
+    for (int k = KB; k < sl.kmax; ++k) {  // beyond the batch: one at a time
+      const int64_t q = sl.e0 + (int64_t)k * sl.stride;
+      sl.store(q, sl.gather(q));
+    }
+  }
+};
+
+// zero the next step's counters (grid-stride over the launch)
+template <int BS>
+__device__ __forceinline__ void next_step_zero(const NextStep& nx) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < nx.nzero;
+       i += (int64_t)gridDim.x * BS)
+    nx.zero[i] = 0;
+}
+
 }  // namespace tw

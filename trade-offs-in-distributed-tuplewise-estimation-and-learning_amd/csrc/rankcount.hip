@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, int parts, int refine, int64_t sx, int64_t sz,
     uint16_t* __restrict__ cx, uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz,
-    unsigned long long* __restrict__ out = nullptr) {
+    unsigned long long* __restrict__ out, NextStep nxt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* zb = (T*)smem;                                                 // z by bucket
   unsigned* cs = (unsigned*)(smem + sizeof(double) * kBucketMaxZ);  // NB + 1 sample prefix
@@ -205,10 +205,19 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     const int64_t j = tid + (int64_t)r * kSortThreads;
     zr[r] = j < nz ? z[zo + j] : (T)0;
   }
+  // the next repartition (tw_count_pairs_sorted_step): this thread's gathers in flight
+  // through the whole kernel (the z loads above go first), stored at the end; the count
+  // path's first code round is then loaded in phase 5, so the batch's registers fit
+  NextBatch<kSortThreads, 8> nb(nxt);
+  if (COUNT) {
+    next_step_zero<kSortThreads>(nxt);
+    nb.issue();
+  } else {
 #pragma unroll
-  for (int r = 0; r < kEPer; ++r) {
-    const int64_t e = e0 + tid + (int64_t)r * kSortThreads;
-    er[r] = e < e1 ? elem(e) : (T)0;
+    for (int r = 0; r < kEPer; ++r) {
+      const int64_t e = e0 + tid + (int64_t)r * kSortThreads;
+      er[r] = e < e1 ? elem(e) : (T)0;
+    }
   }
   // 1. range of the finite z
   double mn = __builtin_inf(), mx = -__builtin_inf();
@@ -239,6 +248,8 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     mn = red_min[w] < mn ? red_min[w] : mn;
     mx = red_max[w] > mx ? red_max[w] : mx;
   }
+  // the next repartition (tw_count_pairs_sorted_step): this thread's gathers in flight
+  // through the LDS-bound bucketing and coding phases, stored at the end
   const int nbin = refine ? kBucketNC : kBucketNB;
   const double scale = mx > mn ? (double)nbin / (mx - mn) : 0.0;
   // value-range bin of v and its position t in [0, 1] inside it (NaN u -> bin 0, t = 0)
@@ -300,7 +311,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
   // 5. codes of this block's share (rounds of kEPer elements per thread; the first is loaded)
   unsigned long long acc = 0;
   for (int64_t r0 = e0; r0 < e1; r0 += (int64_t)kEPer * kSortThreads) {
-    if (r0 != e0) {
+    if (COUNT || r0 != e0) {
 #pragma unroll
       for (int r = 0; r < kEPer; ++r) {
         const int64_t e = r0 + tid + (int64_t)r * kSortThreads;
@@ -348,6 +359,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
   }
   TW_PHASE(5);
   if constexpr (COUNT) {
+    nb.commit();
     acc = wave_sum_u64(acc);
     __shared__ unsigned long long part_acc[kSortThreads / kWave];
     if (lane == 0) part_acc[wid] = acc;
@@ -366,7 +378,8 @@ static int g_sorted_by_bucket = 1;
 
 template <typename T, int PRED>
 int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
-                        int32_t n_shards, int64_t max_nx, uint64_t* out, hipStream_t st) {
+                        int32_t n_shards, int64_t max_nx, uint64_t* out, const NextStep& nxt,
+                        hipStream_t st) {
   const size_t lds_b = kBucketLds;
   static bool attr = false;
   if (!attr) {
@@ -382,7 +395,7 @@ int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, cons
   hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED, true>), dim3(n_shards * parts),
                      dim3(kSortThreads), lds_b, st, (const T*)x, x_off, (const T*)z, z_off, parts,
                      (int)(g_sorted_by_bucket == 1), max_nx, (int64_t)0, nullptr, nullptr, nullptr,
-                     (unsigned long long*)out);
+                     (unsigned long long*)out, nxt);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -393,8 +406,10 @@ int launch_rank(const void* x, const int64_t* x_off, const void* z, const int64_
                 uint64_t* out, hipStream_t st) {
   if (max_nz <= kBucketMaxZ && g_sorted_by_bucket) {
     if (pred == TW_PRED_HALF)
-      return launch_bucket_count<T, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, max_nx, out, st);
-    return launch_bucket_count<T, TW_PRED_GT>(x, x_off, z, z_off, n_shards, max_nx, out, st);
+      return launch_bucket_count<T, TW_PRED_HALF>(x, x_off, z, z_off, n_shards, max_nx, out,
+                                                  NextStep{}, st);
+    return launch_bucket_count<T, TW_PRED_GT>(x, x_off, z, z_off, n_shards, max_nx, out,
+                                              NextStep{}, st);
   }
   const RankPlan p = plan_rank(max_nx, max_nz);
   TW_ARG_CHECK((int64_t)n_shards * p.chunks < (1ll << 31) &&
@@ -882,7 +897,8 @@ int launch_codes(const void* x, const int64_t* x_off, const void* z, const int64
   if (max_nz <= kBucketMaxZ && g_rng_codes_by_bucket) {
     hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED>), dim3(n_shards * p.code_parts),
                        dim3(kSortThreads), kBucketLds, st, (const T*)x, x_off, (const T*)z, z_off,
-                       p.code_parts, (int)(g_rng_codes_by_bucket == 1), p.sx, p.sz, cx, cx2, pz);
+                       p.code_parts, (int)(g_rng_codes_by_bucket == 1), p.sx, p.sz, cx, cx2, pz,
+                       nullptr, NextStep{});
   } else {
   const size_t lds_sort = sizeof(uint64_t) * p.C;
   const size_t lds_codes = sizeof(uint64_t) * std::min<int64_t>((int64_t)p.chunks * p.C, kMaxChunk);
@@ -992,6 +1008,10 @@ int launch_idx_ranked(const void* x, const int64_t* x_off, const void* z, const 
 
 using namespace tw;
 
+extern "C" int tw_permute_pair(const void* d_x_in, void* d_x_out, int64_t n, uint64_t key_x,
+                               const void* d_z_in, void* d_z_out, int64_t m, uint64_t key_z,
+                               void* stream);
+
 extern "C" int tw_count_sorted_set_chunk(int64_t cap) {
   TW_ARG_CHECK(cap >= 1024 && cap <= kMaxChunk && (cap & (cap - 1)) == 0,
                "tw_count_sorted_set_chunk: cap must be a power of two in [1024, 16384]");
@@ -1019,6 +1039,60 @@ extern "C" int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, co
   if (dtype == TW_I64) return launch_rank<long long>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, pred, d_work, d_out, st);
   set_error("tw_count_pairs_sorted: unknown dtype %d", dtype);
   return TW_ERR_ARG;
+}
+
+// One est.UnNT step with the exact sorted count (the bucket path, shards with nz <= 16384):
+// the counts of the current partition into d_out (zero on entry) and the next repartition into
+// d_x_next / d_z_next (as tw_permute_pair) with d_out_next zeroed, in one launch — the
+// permutation's gathers ride in the count threads (NextBatch).  Elsewhere: the count call,
+// tw_permute_pair and a memset in turn.
+extern "C" int tw_count_pairs_sorted_step(const void* d_x, const int64_t* d_x_off, const void* d_z,
+                                          const int64_t* d_z_off, int32_t n_shards,
+                                          int64_t max_nx, int64_t max_nz, int32_t dtype,
+                                          int32_t pred, void* d_work, uint64_t* d_out,
+                                          int64_t n_x, void* d_x_next, uint64_t key_x,
+                                          int64_t n_z, void* d_z_next, uint64_t key_z,
+                                          uint64_t* d_out_next, int32_t n_next_shards,
+                                          void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && max_nx >= 0 && max_nz >= 0 && n_x >= 0 && n_z >= 0 &&
+                   n_x < (1ll << 60) && n_z < (1ll << 60) && n_next_shards >= 0,
+               "tw_count_pairs_sorted_step: bad sizes");
+  TW_ARG_CHECK(pred == TW_PRED_GT || pred == TW_PRED_HALF,
+               "tw_count_pairs_sorted_step: predicate must be TW_PRED_GT or TW_PRED_HALF");
+  TW_ARG_CHECK(d_x_next == nullptr || ((n_x == 0 || d_x_next != d_x) &&
+                                       (n_z == 0 || (d_z_next != nullptr && d_z_next != d_z))),
+               "tw_count_pairs_sorted_step: next arrays must be distinct buffers");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_shards > 0 && max_nx > 0 && max_nz > 0 && max_nz <= kBucketMaxZ && g_sorted_by_bucket &&
+      (dtype == TW_F64 || dtype == TW_I64)) {
+    NextStep nxt{};
+    if (d_x_next != nullptr)
+      nxt = NextStep{(const uint64_t*)d_x, (uint64_t*)d_x_next, n_x, (const uint64_t*)d_z,
+                     (uint64_t*)d_z_next, n_z, (unsigned long long*)d_out_next,
+                     d_out_next ? (int64_t)n_next_shards : 0,
+                     make_feistel(std::max<int64_t>(n_x, 1), key_x),
+                     make_feistel(std::max<int64_t>(n_z, 1), key_z), 1, 0, 0};
+    else if (d_out_next != nullptr && n_next_shards > 0)
+      TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+#define TW_BSTEP(T, P) return launch_bucket_count<T, P>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, d_out, nxt, st)
+    if (dtype == TW_F64) {
+      if (pred == TW_PRED_HALF) TW_BSTEP(double, TW_PRED_HALF);
+      TW_BSTEP(double, TW_PRED_GT);
+    }
+    if (pred == TW_PRED_HALF) TW_BSTEP(long long, TW_PRED_HALF);
+    TW_BSTEP(long long, TW_PRED_GT);
+#undef TW_BSTEP
+  }
+  int rc = tw_count_pairs_sorted(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, dtype,
+                                 pred, d_work, d_out, stream);
+  if (rc != TW_OK) return rc;
+  if (d_x_next != nullptr && n_x + n_z > 0) {
+    rc = tw_permute_pair(d_x, d_x_next, n_x, key_x, d_z, d_z_next, n_z, key_z, stream);
+    if (rc != TW_OK) return rc;
+  }
+  if (d_out_next != nullptr && n_next_shards > 0)
+    TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+  return TW_OK;
 }
 
 extern "C" int64_t tw_count_pairs_rng_work_bytes(int32_t n_shards, int64_t max_nx,
@@ -1071,10 +1145,6 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
     return launch_rng_ranked<long long, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
   return launch_rng_ranked<long long, TW_PRED_GT>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
 }
-
-extern "C" int tw_permute_pair(const void* d_x_in, void* d_x_out, int64_t n, uint64_t key_x,
-                               const void* d_z_in, void* d_z_out, int64_t m, uint64_t key_z,
-                               void* stream);
 
 // One UnNBT step (compute_stats.py:119-123, device-RNG mode): the counts of the current
 // partition into d_out (zero on entry) and the next repartition of both samples into

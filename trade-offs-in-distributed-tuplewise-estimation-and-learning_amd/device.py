@@ -151,6 +151,21 @@ class HipOps:
                    L.ptr(out), L.stream_handle())
         return out
 
+    def count_sorted_step(self, x, x_off_dev, z, z_off_dev, n_shards, max_nx, max_nz, dtype,
+                          pred, out, x_next, key_x, z_next, key_z, out_next):
+        """Exact sorted counts of the current partition into `out` (already zero) and the next
+        repartition into x_next / z_next with out_next zeroed, in one launch on the bucket
+        path (tw_count_pairs_sorted_step)."""
+        work = L.empty((max(1, int(L.lib().tw_count_pairs_sorted_work_bytes(int(n_shards),
+                                                                             int(max_nz)))),),
+                       self.t.uint8)
+        L.call("tw_count_pairs_sorted_step", L.ptr(x), L.ptr(x_off_dev), L.ptr(z),
+               L.ptr(z_off_dev), int(n_shards), int(max_nx), int(max_nz), int(dtype), int(pred),
+               L.ptr(work), L.ptr(out), int(x.numel()), L.ptr(x_next), int(key_x),
+               int(z.numel()), L.ptr(z_next), int(key_z), L.ptr(out_next),
+               int(out_next.numel()) if out_next is not None else 0, L.stream_handle())
+        return out
+
     def count_rng_step(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype,
                        pred, max_nx, max_nz, out, x_next, key_x, z_next, key_z, out_next):
         """Device-RNG incomplete counts of the current partition into `out` (already zero) and
@@ -454,6 +469,12 @@ class ShardedSample:
                 self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
                                     self.max_nx, self.max_nz, self.dtype, self.pred, out, Xn, kx,
                                     Zn, kz, out_n)
+        elif (self.algo == "sorted" and self.pred != L.TW_PRED_SUBGT
+              and hasattr(self.ops, "count_sorted_step")):
+            def step(i, out, Xn, kx, Zn, kz, out_n):
+                self.ops.count_sorted_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                           self.max_nx, self.max_nz, self.dtype, self.pred, out,
+                                           Xn, kx, Zn, kz, out_n)
         counts = self._run_steps(keys, lambda i: self.local_counts(), fusable, step)
         return [np.mean(v) for v in self.values(counts)]
 
