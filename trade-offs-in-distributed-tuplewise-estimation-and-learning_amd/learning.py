@@ -1106,8 +1106,8 @@ def load_preprocess_data(data=None):
             data = pickle.load(fh)
     X = data["X"]
     y = data["y"]
-    Z_tot = X[y == +1]  # Minority class is the anomaly class, i.e. y = +1
-    X_tot = X[y == -1]
+    # label +1 (the rare class) is the Z sample, -1 the X sample
+    Z_tot, X_tot = X[y == +1], X[y == -1]
 
     np.random.seed(SEED_SHUFFLE)
     ind_X_test = np.random.choice(X_tot.shape[0], size=int(PROP_TEST * X_tot.shape[0]),
