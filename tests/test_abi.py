@@ -45,6 +45,20 @@ def test_argument_errors_without_gpu(tw):
     with pytest.raises(ValueError):
         L.call("tw_count_set_plan", 3, 0)
     assert lib.tw_pair_sum_idx_work_per_shard(10_000) == 5
+    # the one-launch step entries validate before touching a device
+    with pytest.raises(ValueError, match="bad sizes"):
+        L.call("tw_count_pairs_rng_step", None, None, None, None, -1, 0, 0, 1, 0, 0, L.TW_F64,
+               L.TW_PRED_GT, None, 0, None, 0, None, 0, 0, None, 0, None, 0, None)
+    buf = ctypes.create_string_buffer(8)
+    with pytest.raises(ValueError, match="distinct buffers"):  # next array == current array
+        L.call("tw_count_pairs_rng_step", buf, None, buf, None, 1, 1, 1, 1, 0, 0, L.TW_F64,
+               L.TW_PRED_GT, None, 0, None, 1, buf, 0, 1, buf, 0, None, 0, None)
+    with pytest.raises(ValueError, match="predicate"):
+        L.call("tw_count_pairs_sorted_step", None, None, None, None, 1, 1, 1, L.TW_F64,
+               L.TW_PRED_SUBGT, None, None, 0, None, 0, 0, None, 0, None, 0, None)
+    with pytest.raises(ValueError, match="distinct buffers"):
+        L.call("tw_count_pairs_sorted_step", buf, None, buf, None, 1, 1, 1, L.TW_F64,
+               L.TW_PRED_GT, None, None, 1, buf, 0, 1, buf, 0, None, 0, None)
 
 
 def test_no_device_raises(tw):

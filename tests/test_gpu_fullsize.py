@@ -46,6 +46,37 @@ def test_c3_full_size_device_rng(gpu):
             assert int(c[s]) == want, (t, s)
 
 
+def test_c3_full_size_complete_one_launch_steps(gpu):
+    """The bench's step at its size: UnN_many over T = 4 keys, n = 1e6 per class, N = 64, by
+    the all-pairs count (tw_count_pairs_step) and by the exact sorted count
+    (tw_count_pairs_sorted_step) — both carry the next repartition in the count launch.  Same
+    estimates; the arrays after the last step equal the oracle's chain of permutations; every
+    shard's count of the last partition equals an exact searchsorted count."""
+    import torch
+    from tuplewise.device import ShardedSample
+    n, N = 1_000_000, 64
+    k = n // N
+    rng = np.random.RandomState(35)
+    X, Z = rng.normal(0.5, 1, n).round(3), rng.normal(0, 1, n).round(3)  # with ties
+    keys = [101, 102, 103, 104]
+    res = {}
+    for algo in ("pairs", "sorted"):
+        S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N, algo=algo)
+        res[algo] = (S.UnN_many(keys), S.X.cpu().numpy(), S.Z.cpu().numpy())
+    assert res["pairs"][0] == res["sorted"][0]
+    Xp, Zp = X, Z
+    for key in keys:  # ShardedSample._repartition's key split
+        Xp = O.permute_scatter(Xp, (2 * key) % 2 ** 64)
+        Zp = O.permute_scatter(Zp, (2 * key + 1) % 2 ** 64)
+    for algo in ("pairs", "sorted"):
+        assert np.array_equal(res[algo][1], Xp) and np.array_equal(res[algo][2], Zp), algo
+    vals = []
+    for s in range(N):
+        zs = np.sort(Zp[s * k:(s + 1) * k])
+        vals.append(np.searchsorted(zs, Xp[s * k:(s + 1) * k], side="left").sum() / (k * k))
+    assert res["pairs"][0][-1] == np.mean(np.array(vals, dtype=np.float64))
+
+
 def test_c3_full_size_replay_drop_in(gpu):
     import tuplewise.compute_stats as cs
     n, N, B, T = 1_000_000, 64, 1_000_000, 2
