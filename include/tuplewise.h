@@ -128,6 +128,24 @@ int tw_count_pairs_sorted_step(const void* d_x, const int64_t* d_x_off, const vo
                                uint64_t* d_out, int64_t n_x, void* d_x_next, uint64_t key_x,
                                int64_t n_z, void* d_z_next, uint64_t key_z,
                                uint64_t* d_out_next, int32_t n_next_shards, void* stream);
+/* T steps of est.UnNT's loop (estimation-experiment/main.py:76-79) with the exact sorted count
+ * in ONE call: step t repartitions both samples with keys_x[t] / keys_z[t] (host arrays; step 0
+ * starts from d_x / d_z in position order) and counts every shard into d_out[t * n_shards ..]
+ * (zeroed by the call); the last partition is written to d_x_out / d_z_out (distinct from the
+ * inputs).  Between steps the partition lives in d_work as records {value, position} grouped by
+ * destination shard, so a repartition is a streaming pass (csrc/records.h) instead of one random
+ * gather per score.  The layout must be prop-SWOR's: d_x_off[s] = min(s * kx, n_x),
+ * d_z_off[s] = min(s * kz, n_z).  tw_count_pairs_sorted_steps_work_bytes() returns 0 where the
+ * path does not apply (then use tw_count_pairs_sorted_step per step). */
+int64_t tw_count_pairs_sorted_steps_work_bytes(int64_t n_x, int64_t n_z, int32_t n_shards,
+                                               int64_t max_nz, int32_t dtype, int32_t pred);
+int tw_count_pairs_sorted_steps(const void* d_x, const void* d_z, int64_t n_x, int64_t n_z,
+                                const int64_t* d_x_off, const int64_t* d_z_off, int32_t n_shards,
+                                int64_t kx, int64_t kz, int64_t max_nx, int64_t max_nz,
+                                int32_t dtype, int32_t pred, const uint64_t* keys_x,
+                                const uint64_t* keys_z, int32_t T, void* d_work,
+                                int64_t work_bytes, uint64_t* d_out, void* d_x_out,
+                                void* d_z_out, void* stream);
 /* Shards with nz <= 16384 (default 1): the count comes from value buckets of z in LDS (an
  * LDS histogram, prefix and scatter, then one bucket scanned per x) instead of sorted chunks +
  * binary searches; the same integers.  1 = equal-depth buckets (the value-range histogram's

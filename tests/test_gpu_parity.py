@@ -528,6 +528,44 @@ def test_count_pairs_sorted_step_fused_repartition(gpu, dtype, mode, big):
     assert np.array_equal(zn.cpu().numpy(), O.permute_scatter(sh.z.cpu().numpy(), 32))
 
 
+@pytest.mark.parametrize("n,m,N,tie,dt", [(300_000, 250_000, 16, "strict", "f64"),
+                                          (100_003, 90_001, 7, "half", "f64"),
+                                          (60_000, 70_000, 5, "strict", "i64"),
+                                          (5_000, 20, 3, "half", "i64")])
+def test_sorted_steps_records_path(gpu, n, m, N, tie, dt):
+    """UnN_many with the sorted count through tw_count_pairs_sorted_steps (the partition kept
+    as destination-bucketed records between steps, csrc/records.h): per-step estimates equal
+    the step-at-a-time path (tw_permute_pair + the sorted count), and the arrays after the last
+    step equal the oracle's chain of permutations — with tails that belong to no shard
+    (n, m not multiples of the shard sizes), ties, int64, T = 1, 2, 5."""
+    import torch
+    from tuplewise.device import HipOps, ShardedSample
+
+    class OneStep(HipOps):  # without the records entry: one repartition + count per step
+        @property
+        def count_sorted_steps(self):
+            raise AttributeError
+
+    rng = np.random.RandomState(n % 97)
+    if dt == "f64":
+        X, Z = rng.normal(0.3, 1, n).round(2), rng.normal(0, 1, m).round(2)
+    else:
+        X, Z = rng.randint(-40, 40, n), rng.randint(-40, 40, m)
+    for keys in ([7], [7, 8], [3, 1, 4, 1, 5]):
+        S1 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
+                           tie_mode=tie, algo="sorted", ops=OneStep())
+        S2 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
+                           tie_mode=tie, algo="sorted")
+        want = S1.UnN_many(keys)
+        got = S2.UnN_many(keys)
+        assert got == want, (keys, got, want)
+        Xp, Zp = X, Z
+        for k in keys:
+            Xp = O.permute_scatter(Xp, (2 * k) % 2 ** 64)
+            Zp = O.permute_scatter(Zp, (2 * k + 1) % 2 ** 64)
+        assert np.array_equal(S2.X.cpu().numpy(), Xp) and np.array_equal(S2.Z.cpu().numpy(), Zp)
+
+
 def test_device_sigmoid_accuracy(gpu):
     """The device sigma (tw_common.h pair_weight: 1 / (1 + exp(-S)) with the device exp) within 4 ulp of
     NumPy's 1 / (1 + exp(-S)) over the whole range, incl. saturation, +-inf and NaN: one

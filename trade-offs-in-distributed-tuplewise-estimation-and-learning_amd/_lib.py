@@ -52,6 +52,9 @@ _SIGNATURES = {
     "tw_count_sorted_set_bucket": [_i32],
     "tw_count_pairs_rng_ws": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _u64, _u64, _i32, _i32,
                               _vp, _i64, _vp, _vp],
+    "tw_count_pairs_sorted_steps_work_bytes": [_i64, _i64, _i32, _i64, _i32, _i32],
+    "tw_count_pairs_sorted_steps": [_vp, _vp, _i64, _i64, _vp, _vp, _i32, _i64, _i64, _i64, _i64,
+                                    _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "tw_count_pairs_sorted_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp,
                                    _i64, _vp, _u64, _i64, _vp, _u64, _vp, _i32, _vp],
     "tw_count_pairs_rng_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _u64, _u64, _i32,
@@ -129,6 +132,7 @@ _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,
     "tw_count_pairs_sorted_work_bytes": ctypes.c_int64,
     "tw_count_pairs_rng_work_bytes": ctypes.c_int64,
+    "tw_count_pairs_sorted_steps_work_bytes": ctypes.c_int64,
     "tw_pair_sum_work_per_shard": ctypes.c_int64,
     "tw_pair_sum_idx_work_per_shard": ctypes.c_int64,
     "tw_pair_grad_complete_work_bytes": ctypes.c_int64,

@@ -18,6 +18,7 @@
 //   atomic per block.  Padding keys (max) are never < a non-NaN x key.
 #include "sortkeys.h"
 #include "imagecount.h"
+#include "records.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
     const T* __restrict__ x, const int64_t* __restrict__ x_off, const T* __restrict__ z,
     const int64_t* __restrict__ z_off, int parts, int refine, int64_t sx, int64_t sz,
     uint16_t* __restrict__ cx, uint16_t* __restrict__ cx2, uint16_t* __restrict__ pz,
-    unsigned long long* __restrict__ out, NextStep nxt) {
+    unsigned long long* __restrict__ out, NextStep nxt, EmitStep em) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* zb = (T*)smem;                                                 // z by bucket
   unsigned* cs = (unsigned*)(smem + sizeof(double) * kBucketMaxZ);  // NB + 1 sample prefix
@@ -369,6 +370,62 @@ __global__ __launch_bounds__(kSortThreads) void k_rank_codes_bucket(
       for (int w = 0; w < kSortThreads / kWave; ++w) b += part_acc[w];
       if (b) atomicAdd(out + s, b);
     }
+    if (em.active) {  // the next repartition as records (records.h): this block's x share
+                      // and a 1/parts share of the shard's z in one staged round (the LDS of
+                      // the z buckets is free now), then its stride of the tails
+      const int64_t zper = (nz + parts - 1) / parts;
+      const int64_t za = zo + std::min<int64_t>(nz, (int64_t)part * zper);
+      const int64_t zbnd = zo + std::min<int64_t>(nz, (int64_t)(part + 1) * zper);
+      const int N = em.n_shards;
+      if (lb == 0)
+        for (int i = tid; i <= N; i += kSortThreads) {
+          if (em.zero_x) em.zero_x[i] = 0;
+          if (em.zero_z) em.zero_z[i] = 0;
+        }
+      if ((e1 - e0) + (zbnd - za) <= (int64_t)kSortThreads * 8 && 2 * N + 2 <= kBucketNB) {
+        char* lds = smem;  // zb's 128 KiB: 8192 staged records (8 + 4 + 2 B)
+        uint64_t* sv = (uint64_t*)lds;
+        uint32_t* sq = (uint32_t*)(lds + 8 * kSortThreads * 8);
+        uint16_t* sbk = (uint16_t*)(lds + 12 * kSortThreads * 8);
+        emit_block_staged<kSortThreads>(em, xb + e0, xb + e1, za, zbnd, cur, cs, st, sv, sq,
+                                        sbk, wave_tot);
+      } else {
+        emit_range<kSortThreads, 8>(em.xv, em.xp, xb + e0, xb + e1, em.nx, em.fx, em.kx, em.dx,
+                                    N, em.x_off, em.cur_x, em.nxv, em.nxp, cs, st);
+        emit_range<kSortThreads, 8>(em.zv, em.zp, za, zbnd, em.nz, em.fz, em.kz, em.dz, N,
+                                    em.z_off, em.cur_z, em.nzv, em.nzp, cs, st);
+      }
+      emit_tails<kSortThreads>(em, lb, (int)gridDim.x, cs, st);
+    }
+  }
+}
+
+// The first records of a tw_count_pairs_sorted_steps call: the arrays in position order
+// (implicit positions) appended to their buckets under the first step's permutation.
+__global__ __launch_bounds__(kSortThreads) void k_emit_records(EmitStep em) {
+  __shared__ unsigned hist[kBucketNB + 1], base[kBucketNB + 1];
+  constexpr int64_t C = (int64_t)kSortThreads * 8;
+  for (int64_t c = (int64_t)blockIdx.x * C; c < em.nx; c += (int64_t)gridDim.x * C)
+    emit_range<kSortThreads, 8>(em.xv, em.xp, c, c + C < em.nx ? c + C : em.nx, em.nx, em.fx,
+                                em.kx, em.dx, em.n_shards, em.x_off, em.cur_x, em.nxv, em.nxp,
+                                hist, base);
+  for (int64_t c = (int64_t)blockIdx.x * C; c < em.nz; c += (int64_t)gridDim.x * C)
+    emit_range<kSortThreads, 8>(em.zv, em.zp, c, c + C < em.nz ? c + C : em.nz, em.nz, em.fz,
+                                em.kz, em.dz, em.n_shards, em.z_off, em.cur_z, em.nzv, em.nzp,
+                                hist, base);
+}
+
+// After the last step: the records written back in position order.
+__global__ __launch_bounds__(kBlock) void k_records_to_arrays(
+    const uint64_t* __restrict__ xv, const uint32_t* __restrict__ xp, int64_t nx,
+    const uint64_t* __restrict__ zv, const uint32_t* __restrict__ zp, int64_t nz,
+    uint64_t* __restrict__ x_out, uint64_t* __restrict__ z_out) {
+  for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < nx + nz;
+       e += (int64_t)gridDim.x * kBlock) {
+    if (e < nx)
+      x_out[xp[e]] = xv[e];
+    else
+      z_out[zp[e - nx]] = zv[e - nx];
   }
 }
 
@@ -379,7 +436,7 @@ static int g_sorted_by_bucket = 1;
 template <typename T, int PRED>
 int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, const int64_t* z_off,
                         int32_t n_shards, int64_t max_nx, uint64_t* out, const NextStep& nxt,
-                        hipStream_t st) {
+                        hipStream_t st, const EmitStep& em = EmitStep{}) {
   const size_t lds_b = kBucketLds;
   static bool attr = false;
   if (!attr) {
@@ -395,7 +452,7 @@ int launch_bucket_count(const void* x, const int64_t* x_off, const void* z, cons
   hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED, true>), dim3(n_shards * parts),
                      dim3(kSortThreads), lds_b, st, (const T*)x, x_off, (const T*)z, z_off, parts,
                      (int)(g_sorted_by_bucket == 1), max_nx, (int64_t)0, nullptr, nullptr, nullptr,
-                     (unsigned long long*)out, nxt);
+                     (unsigned long long*)out, nxt, em);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -898,7 +955,7 @@ int launch_codes(const void* x, const int64_t* x_off, const void* z, const int64
     hipLaunchKernelGGL((k_rank_codes_bucket<T, PRED>), dim3(n_shards * p.code_parts),
                        dim3(kSortThreads), kBucketLds, st, (const T*)x, x_off, (const T*)z, z_off,
                        p.code_parts, (int)(g_rng_codes_by_bucket == 1), p.sx, p.sz, cx, cx2, pz,
-                       nullptr, NextStep{});
+                       nullptr, NextStep{}, EmitStep{});
   } else {
   const size_t lds_sort = sizeof(uint64_t) * p.C;
   const size_t lds_codes = sizeof(uint64_t) * std::min<int64_t>((int64_t)p.chunks * p.C, kMaxChunk);
@@ -1092,6 +1149,128 @@ extern "C" int tw_count_pairs_sorted_step(const void* d_x, const int64_t* d_x_of
   }
   if (d_out_next != nullptr && n_next_shards > 0)
     TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+  return TW_OK;
+}
+
+// ---- T steps of est.UnNT with the sorted count, the partition kept as records (records.h)
+namespace tw {
+struct StepsWork {
+  uint64_t* xv[2];
+  uint64_t* zv[2];
+  uint32_t* xp[2];
+  uint32_t* zp[2];
+  unsigned* cx[2];
+  unsigned* cz[2];
+  int64_t total;
+};
+
+static StepsWork steps_layout(char* w, int64_t n_x, int64_t n_z, int32_t n_shards) {
+  StepsWork L{};
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    char* r = w ? w + o : nullptr;
+    o += (bytes + 255) / 256 * 256;
+    return r;
+  };
+  for (int k = 0; k < 2; ++k) {
+    L.xv[k] = (uint64_t*)take(8 * std::max<int64_t>(n_x, 1));
+    L.zv[k] = (uint64_t*)take(8 * std::max<int64_t>(n_z, 1));
+    L.xp[k] = (uint32_t*)take(4 * std::max<int64_t>(n_x, 1));
+    L.zp[k] = (uint32_t*)take(4 * std::max<int64_t>(n_z, 1));
+  }
+  char* c0 = w ? w + o : nullptr;
+  for (int k = 0; k < 2; ++k) {
+    L.cx[k] = (unsigned*)take(4 * ((int64_t)n_shards + 1));
+    L.cz[k] = (unsigned*)take(4 * ((int64_t)n_shards + 1));
+  }
+  (void)c0;
+  L.total = o;
+  return L;
+}
+
+static bool steps_ok(int64_t n_x, int64_t n_z, int32_t n_shards, int64_t max_nz, int32_t dtype,
+                     int32_t pred) {
+  return n_shards >= 1 && n_shards + 1 <= kBucketNB + 1 && max_nz <= kBucketMaxZ &&
+         g_sorted_by_bucket && (dtype == TW_F64 || dtype == TW_I64) &&
+         (pred == TW_PRED_GT || pred == TW_PRED_HALF) && n_x >= 1 && n_z >= 1 &&
+         n_x < (1ll << 32) && n_z < (1ll << 32);
+}
+}  // namespace tw
+
+extern "C" int64_t tw_count_pairs_sorted_steps_work_bytes(int64_t n_x, int64_t n_z,
+                                                          int32_t n_shards, int64_t max_nz,
+                                                          int32_t dtype, int32_t pred) {
+  if (!steps_ok(n_x, n_z, n_shards, max_nz, dtype, pred)) return 0;
+  return steps_layout(nullptr, n_x, n_z, n_shards).total;
+}
+
+extern "C" int tw_count_pairs_sorted_steps(const void* d_x, const void* d_z, int64_t n_x,
+                                           int64_t n_z, const int64_t* d_x_off,
+                                           const int64_t* d_z_off, int32_t n_shards, int64_t kx,
+                                           int64_t kz, int64_t max_nx, int64_t max_nz,
+                                           int32_t dtype, int32_t pred, const uint64_t* keys_x,
+                                           const uint64_t* keys_z, int32_t T, void* d_work,
+                                           int64_t work_bytes, uint64_t* d_out, void* d_x_out,
+                                           void* d_z_out, void* stream) {
+  TW_ARG_CHECK(T >= 1 && keys_x != nullptr && keys_z != nullptr && kx >= 0 && kz >= 0 &&
+                   max_nx >= 0 && max_nz >= 0,
+               "tw_count_pairs_sorted_steps: bad sizes");
+  TW_ARG_CHECK(steps_ok(n_x, n_z, n_shards, max_nz, dtype, pred),
+               "tw_count_pairs_sorted_steps: not applicable (see _work_bytes)");
+  const StepsWork W = steps_layout((char*)d_work, n_x, n_z, n_shards);
+  TW_ARG_CHECK(d_work != nullptr && work_bytes >= W.total,
+               "tw_count_pairs_sorted_steps: work buffer too small");
+  TW_ARG_CHECK(d_x_out != d_x && d_z_out != d_z && d_x_out != nullptr && d_z_out != nullptr,
+               "tw_count_pairs_sorted_steps: outputs must be distinct buffers");
+  hipStream_t st = (hipStream_t)stream;
+  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * (size_t)T * n_shards, st));
+  TW_HIP_CHECK(hipMemsetAsync(W.cx[0], 0, (char*)d_work + W.total - (char*)W.cx[0], st));
+  const FastDiv dx = make_fastdiv((uint64_t)std::max<int64_t>(kx, 1));
+  const FastDiv dz = make_fastdiv((uint64_t)std::max<int64_t>(kz, 1));
+  auto emit = [&](const uint64_t* xv, const uint32_t* xp, const uint64_t* zv, const uint32_t* zp,
+                  int to, unsigned* zx, unsigned* zz, int t) {
+    EmitStep e{};
+    e.xv = xv; e.xp = xp; e.nx = n_x;
+    e.zv = zv; e.zp = zp; e.nz = n_z;
+    e.nxv = W.xv[to]; e.nxp = W.xp[to]; e.nzv = W.zv[to]; e.nzp = W.zp[to];
+    e.cur_x = W.cx[to]; e.cur_z = W.cz[to];
+    e.zero_x = zx; e.zero_z = zz;
+    e.fx = make_feistel(n_x, keys_x[t]);
+    e.fz = make_feistel(n_z, keys_z[t]);
+    e.dx = dx; e.dz = dz; e.kx = kx; e.kz = kz;
+    e.x_off = d_x_off; e.z_off = d_z_off; e.n_shards = n_shards; e.active = 1;
+    return e;
+  };
+  // step 0's partition: the arrays (position order) appended to their buckets
+  {
+    const EmitStep e = emit((const uint64_t*)d_x, nullptr, (const uint64_t*)d_z, nullptr, 0,
+                            nullptr, nullptr, 0);
+    const int blocks = (int)std::min<int64_t>(1024, ceil_div(n_x + n_z, (int64_t)kSortThreads * 8));
+    hipLaunchKernelGGL(k_emit_records, dim3(std::max(blocks, 1)), dim3(kSortThreads), 0, st, e);
+    TW_LAUNCH_CHECK();
+  }
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    EmitStep e{};
+    if (t + 1 < T)
+      e = emit(W.xv[cur], W.xp[cur], W.zv[cur], W.zp[cur], nxt, W.cx[cur], W.cz[cur], t + 1);
+    int rc;
+    if (dtype == TW_F64)
+      rc = pred == TW_PRED_HALF
+               ? launch_bucket_count<double, TW_PRED_HALF>(W.xv[cur], d_x_off, W.zv[cur], d_z_off, n_shards, max_nx, d_out + (size_t)t * n_shards, NextStep{}, st, e)
+               : launch_bucket_count<double, TW_PRED_GT>(W.xv[cur], d_x_off, W.zv[cur], d_z_off, n_shards, max_nx, d_out + (size_t)t * n_shards, NextStep{}, st, e);
+    else
+      rc = pred == TW_PRED_HALF
+               ? launch_bucket_count<long long, TW_PRED_HALF>(W.xv[cur], d_x_off, W.zv[cur], d_z_off, n_shards, max_nx, d_out + (size_t)t * n_shards, NextStep{}, st, e)
+               : launch_bucket_count<long long, TW_PRED_GT>(W.xv[cur], d_x_off, W.zv[cur], d_z_off, n_shards, max_nx, d_out + (size_t)t * n_shards, NextStep{}, st, e);
+    if (rc != TW_OK) return rc;
+  }
+  const int last = (T - 1) & 1;
+  const int blocks = (int)std::min<int64_t>(4096, ceil_div(n_x + n_z, (int64_t)kBlock));
+  hipLaunchKernelGGL(k_records_to_arrays, dim3(blocks), dim3(kBlock), 0, st, W.xv[last],
+                     W.xp[last], n_x, W.zv[last], W.zp[last], n_z, (uint64_t*)d_x_out,
+                     (uint64_t*)d_z_out);
+  TW_LAUNCH_CHECK();
   return TW_OK;
 }
 

@@ -166,6 +166,29 @@ class HipOps:
                int(out_next.numel()) if out_next is not None else 0, L.stream_handle())
         return out
 
+    def count_sorted_steps(self, X, Z, x_off_dev, z_off_dev, n_shards, kx, kz, max_nx, max_nz,
+                           dtype, pred, keys):
+        """T UnN steps with the exact sorted count, the partition kept as destination-bucketed
+        records between steps (tw_count_pairs_sorted_steps): returns the (T, N) counts and
+        the last partition's arrays, or None where the records path does not apply."""
+        t = self.t
+        n, m = int(X.numel()), int(Z.numel())
+        wb = int(L.lib().tw_count_pairs_sorted_steps_work_bytes(n, m, int(n_shards),
+                                                                int(max_nz), int(dtype),
+                                                                int(pred)))
+        if wb <= 0:
+            return None
+        work = L.empty((wb,), t.uint8)
+        out = L.empty((len(keys), int(n_shards)), t.int64)
+        Xo, Zo = t.empty_like(X), t.empty_like(Z)
+        kxs = np.array([(2 * k) & (2 ** 64 - 1) for k in keys], dtype=np.uint64)
+        kzs = np.array([(2 * k + 1) & (2 ** 64 - 1) for k in keys], dtype=np.uint64)
+        L.call("tw_count_pairs_sorted_steps", L.ptr(X), L.ptr(Z), n, m, L.ptr(x_off_dev),
+               L.ptr(z_off_dev), int(n_shards), int(kx), int(kz), int(max_nx), int(max_nz),
+               int(dtype), int(pred), kxs.ctypes.data, kzs.ctypes.data, len(keys), L.ptr(work),
+               wb, L.ptr(out), L.ptr(Xo), L.ptr(Zo), L.stream_handle())
+        return out, Xo, Zo
+
     def count_rng_step(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype,
                        pred, max_nx, max_nz, out, x_next, key_x, z_next, key_z, out_next):
         """Device-RNG incomplete counts of the current partition into `out` (already zero) and
@@ -462,6 +485,18 @@ class ShardedSample:
             return []
         if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
             return [self.UnN(k) for k in keys]
+        if (self.algo == "sorted" and not self._multi() and self.N > 0
+                and hasattr(self.ops, "count_sorted_steps")):
+            # the whole sequence in one call: records between steps (csrc/records.h)
+            n, m = self.n_loc, self.m_loc
+            kx = int(n / self.N)
+            r = self.ops.count_sorted_steps(self.X, self.Z, self.x_off_dev, self.z_off_dev,
+                                            self.N, kx, int((n + m) / self.N) - kx,
+                                            self.max_nx, self.max_nz, self.dtype, self.pred,
+                                            keys)
+            if r is not None:
+                counts, self.X, self.Z = r
+                return [np.mean(v) for v in self.values(counts)]
         fusable = self.algo == "pairs"
         step = None
         if fusable and hasattr(self.ops, "count_step"):
