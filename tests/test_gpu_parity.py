@@ -531,7 +531,12 @@ def test_count_pairs_sorted_step_fused_repartition(gpu, dtype, mode, big):
 @pytest.mark.parametrize("n,m,N,tie,dt", [(300_000, 250_000, 16, "strict", "f64"),
                                           (100_003, 90_001, 7, "half", "f64"),
                                           (60_000, 70_000, 5, "strict", "i64"),
-                                          (5_000, 20, 3, "half", "i64")])
+                                          (5_000, 20, 3, "half", "i64"),
+                                          # one block per shard with > 8192 records to append:
+                                          # the unstaged emission
+                                          (600 * 7_000, 600 * 7_000 + 11, 600, "strict", "f64"),
+                                          # 2N + 2 > 2048 buckets: the unstaged emission
+                                          (1_100 * 200 + 5, 1_100 * 150, 1_100, "half", "f64")])
 def test_sorted_steps_records_path(gpu, n, m, N, tie, dt):
     """UnN_many with the sorted count through tw_count_pairs_sorted_steps (the partition kept
     as destination-bucketed records between steps, csrc/records.h): per-step estimates equal
@@ -551,7 +556,7 @@ def test_sorted_steps_records_path(gpu, n, m, N, tie, dt):
         X, Z = rng.normal(0.3, 1, n).round(2), rng.normal(0, 1, m).round(2)
     else:
         X, Z = rng.randint(-40, 40, n), rng.randint(-40, 40, m)
-    for keys in ([7], [7, 8], [3, 1, 4, 1, 5]):
+    for keys in ([7], [7, 8], [3, 1, 4, 1, 5]) if n < 10 ** 6 else ([7, 8],):
         S1 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
                            tie_mode=tie, algo="sorted", ops=OneStep())
         S2 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
