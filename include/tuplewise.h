@@ -402,6 +402,25 @@ int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* 
  * tw_sgd_segment_set_grid(m): cap the grid at m blocks (tests; 0 = resident capacity);
  * tw_sgd_segment_set_prefetch(1|0): prefetch the next step's first 32 pairs as rows (1, the
  * default) or as row indices only (0) while the barriers run. */
+/* A segment of nsteps narrow-row SGD steps (d <= 32; the steps tw_sgd_step launches one by
+ * one) in ONE persistent launch (csrc/sgdseg.hip k_sgd_segment_narrow): one block per shard,
+ * all co-resident, one grid barrier per step, the update recomputed in every block from the
+ * published shard gradients (slots d_grads0 / d_grads1 by step parity).  On return d_w_out /
+ * d_dw_out hold the state after the segment's last update and the last step's gradients are
+ * in slot (nsteps-1) & 1: apply them with tw_sgd_update_to(d_w_out, d_dw_out -> w, dw,
+ * step_inc = nsteps).  Draws: d_ix/d_iz + step k * draw_stride (replay) or device RNG at
+ * *d_step + k.  d_ctl: 2 words (arrival counter, zeroed here; sticky abort word, zeroed once
+ * by the caller: set when a bounded barrier wait expired).  Same bits as tw_sgd_step per step.
+ * make_exps.py:122-141 with compute_stats.py:146-162. */
+int tw_sgd_segment_narrow_ok(int64_t d, int32_t n_shards, int64_t B);
+int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
+                          const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z, int64_t kz,
+                          const int64_t* d_ix, const int64_t* d_iz, int64_t draw_stride,
+                          int32_t n_shards, int64_t B, double margin, int32_t loss, uint64_t seed,
+                          const uint64_t* d_step, int32_t shard_base, int32_t nsteps,
+                          const double* d_w_in, const double* d_dw_in, double reg, double lr,
+                          double momentum, double* d_grads0, double* d_grads1, double* d_w_out,
+                          double* d_dw_out, uint32_t* d_ctl, void* stream);
 int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
 int tw_sgd_segment_set_grid(int32_t max_blocks);
 int tw_sgd_segment_set_prefetch(int32_t rows);

@@ -1,4 +1,5 @@
-"""C4 SGD steps/s (bench.sgd_steps_per_s, sgd_replay_steps_per_s) on their own (GPU box)."""
+"""C4 SGD steps/s (bench.sgd_steps_per_s, sgd_replay_steps_per_s) on their own (GPU box),
+with the persistent narrow segment kernel (learning.NARROW_SEGMENT) and without it."""
 import json
 import pathlib
 import sys
@@ -8,9 +9,13 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
+import tuplewise.learning as lr  # noqa: E402
+
 torch.cuda.set_device(0)
-for _ in range(2):
+for seg in (True, False, True):
+    lr.NARROW_SEGMENT = seg
     a = bench.sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2)
     b = bench.sgd_replay_steps_per_s(2000)
-    print(json.dumps({"device_steps_per_s": a["steps_per_s"],
+    print(json.dumps({"narrow_segment": seg, "device_steps_per_s": a["steps_per_s"],
                       "replay_steps_per_s": b["steps_per_s"]}), flush=True)
+lr.NARROW_SEGMENT = True

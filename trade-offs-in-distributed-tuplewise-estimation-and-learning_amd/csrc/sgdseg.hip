@@ -334,6 +334,124 @@ __global__ __launch_bounds__(kWideBlock) void k_sgd_segment_wide(
   }
 }
 
+// ---- narrow rows (d <= 32, C4): a segment of k_sgd_step_narrow steps in ONE launch --------
+// One block per shard (all co-resident), ONE grid barrier per step: the update is recomputed
+// redundantly by every block from the published shard gradients (k_sgd_step_narrow's
+// prologue), so no second barrier publishes w.  Per step:
+//   1. the pair chain of step k (draws -> row tables -> rows -> diff rows in LDS) — independent
+//      of w, so it runs BEFORE the barrier and overlaps the wait for the slowest block;
+//   2. k > 0: wait until every block has published step k-1 (arrivals >= k*G), load the N x d
+//      shard gradients of slot (k-1)&1 (agent scope), update w, dw in shard order exactly as
+//      k_sgd_update / k_sgd_step_narrow;
+//   3. S = diff . w + margin (sequential j), weights, column sums in row order from +0.0 ->
+//      grads slot k&1 (agent-scope stores), arrive.
+// Two gradient slots suffice: a block writes slot k&1 at step k only after barrier k, which
+// needs every block to have finished step k-1 — and with it its reads of slot (k-2)&1.
+// The state after the segment's last update goes to w_out / dw_out (block 0); the last step's
+// gradients (slot (nsteps-1)&1) are applied by the caller's tw_sgd_update_to, as in the
+// one-launch-per-step path.  Same arithmetic and order: same bits.
+constexpr int kNarrowMaxD = 32, kNarrowMaxGrads = 4096;
+
+template <int LOSS>
+__global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
+    const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
+    const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
+    int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz,
+    int64_t draw_stride, int64_t B, double margin, uint64_t seed,
+    const uint64_t* __restrict__ d_step, uint32_t shard_base, int n_shards, int nsteps,
+    const double* __restrict__ w_in, const double* __restrict__ dw_in, double reg, double lr,
+    double momentum, double* grads0, double* grads1, double* __restrict__ w_out,
+    double* __restrict__ dw_out, uint32_t* ctl) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* diff = (double*)smem;         // B * d
+  double* flag = diff + B * d;          // B pair weights
+  double* wsh = flag + B;               // kNarrowMaxD: this step's w
+  double* gt = wsh + kNarrowMaxD;       // n_shards * d: the previous step's shard gradients
+  __shared__ int s_ok;
+  const int s = blockIdx.x, tid = threadIdx.x, dd = (int)d, G = gridDim.x;
+  const int ng = n_shards * dd;
+  const uint64_t step0 = d_step ? *d_step : 0;
+  double wj = 0.0, dwj = 0.0;  // thread tid < d: column tid of w and dw
+  if (tid < dd) {
+    wj = w_in[tid];
+    dwj = dw_in[tid];
+    wsh[tid] = wj;
+  }
+  for (int k = 0; k < nsteps; ++k) {
+    // 1. this step's pairs -> diff rows (independent of w)
+    for (int t = tid; t < B; t += kBlock) {
+      int64_t ax, az;
+      if (ix) {
+        ax = ix[(int64_t)k * draw_stride + (int64_t)s * B + t];
+        az = iz[(int64_t)k * draw_stride + (int64_t)s * B + t];
+      } else {
+        const u32x4 r = sgd_draw(seed, step0 + (uint64_t)k, (uint32_t)t,
+                                 shard_base + (uint32_t)s, kTagPairs);
+        ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
+        az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
+      }
+      const int64_t rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+      const int64_t rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      const double* zr = Z + rzt * d;
+      const double* xr = X + rxt * d;
+      double* dr = diff + (int64_t)t * d;
+#pragma unroll 4
+      for (int j = 0; j < dd; ++j) dr[j] = zr[j] - xr[j];
+    }
+    // 2. the previous step's update, once every block has published its gradients
+    if (k > 0) {
+      if (!seg_wait(ctl, (uint32_t)k * (uint32_t)G, &s_ok)) return;
+      const double* gin = ((k - 1) & 1) ? grads1 : grads0;
+      for (int e = tid; e < ng; e += kBlock) gt[e] = ld_agent(gin + e);
+      __syncthreads();
+      if (tid < dd) {
+        double sum = 0.0;  // shard order, as np.mean(axis=0) / k_sgd_update
+        int r = 0;
+        for (; r + 8 <= n_shards; r += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = gt[(r + u) * dd + tid];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sum += v[u];
+        }
+        for (; r < n_shards; ++r) sum += gt[r * dd + tid];
+        const double g = sum / (double)n_shards + reg * wj;
+        const double st = momentum >= 0.0 ? momentum * dwj + lr * g : lr * g;
+        wj = wj - st;
+        dwj = st;
+        wsh[tid] = wj;
+      }
+    }
+    __syncthreads();
+    // 3. S = diff . w + margin, weights, column sums in row order
+    for (int t = tid; t < B; t += kBlock) {
+      const double* dr = diff + (int64_t)t * d;
+      double part = 0.0;
+      for (int j = 0; j < dd; ++j) part += dr[j] * wsh[j];
+      flag[t] = pair_weight<LOSS>(part + margin);
+    }
+    __syncthreads();
+    if (tid < dd) {
+      double a = 0.0;
+      int t = 0;
+      for (; t + 8 <= B; t += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = weighted<LOSS>(flag[t + u], diff[(t + u) * dd + tid]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+      }
+      for (; t < B; ++t) a += weighted<LOSS>(flag[t], diff[t * dd + tid]);
+      st_agent(((k & 1) ? grads1 : grads0) + (int64_t)s * d + tid, a / (double)B);
+    }
+    seg_arrive(ctl);  // also: every thread is done with diff / flag / gt of this step
+  }
+  if (s == 0 && tid < dd) {
+    w_out[tid] = wj;
+    dw_out[tid] = dwj;
+  }
+}
+
 static int g_seg_grid = 0;      // tw_sgd_segment_set_grid: 0 = resident capacity
 static int g_seg_prefetch = 1;  // tw_sgd_segment_set_prefetch: 1 = rows, 0 = indices only
 
@@ -356,6 +474,66 @@ static int seg_capacity() {
 }  // namespace tw
 
 using namespace tw;
+
+static size_t narrow_lds(int64_t d, int32_t n_shards, int64_t B) {
+  return sizeof(double) * ((size_t)B * d + B + kNarrowMaxD + (size_t)n_shards * d);
+}
+
+// every block resident at once (the kernel's grid barriers), within 64 KiB of LDS per block
+extern "C" int tw_sgd_segment_narrow_ok(int64_t d, int32_t n_shards, int64_t B) {
+  if (d < 1 || d > kNarrowMaxD || n_shards < 1 || (int64_t)n_shards * d > kNarrowMaxGrads ||
+      B < 1 || narrow_lds(d, n_shards, B) > 64 * 1024)
+    return 0;
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_segment_narrow<TW_LOSS_HINGE>,
+                                                   kBlock, narrow_lds(d, n_shards, B)) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (int64_t)std::min(per_cu, 1) * cus >= n_shards;  // one block per CU at most
+}
+
+extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
+                                     const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                                     int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                                     int64_t draw_stride, int32_t n_shards, int64_t B,
+                                     double margin, int32_t loss, uint64_t seed,
+                                     const uint64_t* d_step, int32_t shard_base, int32_t nsteps,
+                                     const double* d_w_in, const double* d_dw_in, double reg,
+                                     double lr, double momentum, double* d_grads0,
+                                     double* d_grads1, double* d_w_out, double* d_dw_out,
+                                     uint32_t* d_ctl, void* stream) {
+  TW_ARG_CHECK(tw_sgd_segment_narrow_ok(d, n_shards, B),
+               "tw_sgd_segment_narrow: d=%lld, n_shards=%d, B=%lld unsupported", (long long)d,
+               n_shards, (long long)B);
+  TW_ARG_CHECK(kx >= 1 && kz >= 1 && shard_base >= 0 && nsteps >= 0 && nsteps <= (1 << 20) &&
+                   draw_stride >= 0,
+               "tw_sgd_segment_narrow: bad kx/kz/shard_base/nsteps/draw_stride");
+  TW_ARG_CHECK((d_ix == nullptr) == (d_iz == nullptr), "tw_sgd_segment_narrow: ix and iz go together");
+  TW_ARG_CHECK(d_ix != nullptr || d_step != nullptr, "tw_sgd_segment_narrow: device draws need d_step");
+  TW_ARG_CHECK(d_w_in && d_dw_in && d_grads0 && d_grads1 && d_w_out && d_dw_out && d_ctl,
+               "tw_sgd_segment_narrow: w, dw, both gradient slots, outputs and ctl required");
+  TW_ARG_CHECK(loss == TW_LOSS_HINGE || loss == TW_LOSS_LOGISTIC, "unknown loss %d", loss);
+  if (nsteps == 0) return TW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  TW_HIP_CHECK(hipMemsetAsync(d_ctl, 0, sizeof(uint32_t), st));  // the arrival counter only
+  const size_t lds = narrow_lds(d, n_shards, B);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x, kx,
+                       d_rows_z, kz, d_ix, d_iz, draw_stride, B, margin, seed, d_step,
+                       (uint32_t)shard_base, (int)n_shards, (int)nsteps, d_w_in, d_dw_in, reg,
+                       lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl);
+  };
+  if (loss == TW_LOSS_LOGISTIC)
+    go(k_sgd_segment_narrow<TW_LOSS_LOGISTIC>);
+  else
+    go(k_sgd_segment_narrow<TW_LOSS_HINGE>);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
 
 extern "C" int tw_sgd_segment_ok(int64_t d, int32_t n_shards) {
   return d > 32 && d <= kWideMaxD && n_shards >= 1;

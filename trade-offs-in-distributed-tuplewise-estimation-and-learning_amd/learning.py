@@ -28,6 +28,9 @@ from . import compute_stats as cs
 from .numpy_rng import Session
 
 SEED_SHUFFLE = 42
+# narrow rows (C4): a segment of fused steps in ONE persistent launch (tw_sgd_segment_narrow:
+# one grid barrier per step, the update recomputed in every block); off: one launch per step
+NARROW_SEGMENT = True
 SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
@@ -120,7 +123,10 @@ class SGDEngine:
         # (tw_sgd_segment: grid barriers between the gradient and the update of every step)
         self.segment = (SEGMENT_KERNEL and self.G == 1 and not self.complete and not self.fused
                         and bool(L.lib().tw_sgd_segment_ok(self.d, self.N_loc)))
-        self._ctl = t.zeros((2,), dtype=t.int32, device=self.w.device) if self.segment else None
+        self.narrow_seg = (NARROW_SEGMENT and self.fused
+                           and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N_loc, self.B)))
+        self._ctl = (t.zeros((2,), dtype=t.int32, device=self.w.device)
+                     if self.segment or self.narrow_seg else None)
 
     def _segment(self, nsteps: int, draws_dev=None):
         """nsteps steps as ONE tw_sgd_segment launch (same bits as step()/step_device() +
@@ -154,6 +160,24 @@ class SGDEngine:
         W, DW, Gs = zip((self.w, self.dw, self.grads), self._slot1)
         s = L.stream_handle()
         seed = getattr(self, "seed", 0) if draws_dev is None else 0
+        if self.narrow_seg and nsteps > 1:
+            # the whole segment in one persistent launch; then the last step's update, as below
+            ix = iz = None
+            stride = 0
+            if draws_dev is not None:
+                ix, iz = draws_dev[0, 0], draws_dev[0, 1]
+                stride = int(draws_dev.stride(0))
+            L.call("tw_sgd_segment_narrow", L.ptr(self.X), L.ptr(self.Z), self.d,
+                   L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix), L.ptr(iz),
+                   stride, self.N_loc, self.B, self.margin, self.loss, seed,
+                   L.ptr(self.step_ctr), self.shard_base, nsteps, L.ptr(W[0]), L.ptr(DW[0]),
+                   self.reg, self.lr, self.momentum, L.ptr(Gs[0]), L.ptr(Gs[1]), L.ptr(W[1]),
+                   L.ptr(DW[1]), L.ptr(self._ctl), s)
+            last = (nsteps - 1) & 1
+            L.call("tw_sgd_update_to", L.ptr(W[1]), L.ptr(DW[1]), L.ptr(W[0]), L.ptr(DW[0]),
+                   L.ptr(Gs[last]), self.N, self.d, self.reg, self.lr, self.momentum,
+                   L.ptr(self.step_ctr), nsteps, s)
+            return
         for k in range(nsteps):
             a, b = (k - 1) & 1, k & 1
             ix = iz = None
