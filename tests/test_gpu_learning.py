@@ -384,3 +384,39 @@ def test_same_as_batch_device_rng_equals_host_formula(gpu, golden, monkeypatch, 
     want_br = O.UN_split(sc_X, sc_Z, lambda x, z: O.cs_Un(x, z, kernel="AUC"))
     assert np.isclose(bc, want_bc, rtol=1e-12) and abs(br - want_br) < 1e-12
     assert 0.0 <= br <= 1.0 and cs.Un is not None
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_deferred_evaluations_equal_synchronous(gpu, golden, mode, monkeypatch):
+    """learning.DEFER_EVALS: the loop enqueues each evaluation's device part and runs its host
+    part once the statistics are back — the evaluation lists (and the log) are those of the
+    synchronous evaluation, bit for bit; so is the final NumPy RNG state."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for defer in (True, False):
+        monkeypatch.setattr(lr, "DEFER_EVALS", defer)
+        p = _p_learn(golden, n_it=200)
+        np.random.seed(77)
+        lr.learning_process(golden["learn/X"], golden["learn/Z"], p, rng_mode=mode)
+        out[defer] = (p, np.random.get_state()[2])
+    for k in ("iter", "norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        a, b = np.array(out[True][0][k]), np.array(out[False][0][k])
+        assert np.array_equal(a, b), (k, np.nonzero(a != b), a[a != b], b[a != b])
+    assert len(out[True][0]["iter"]) == 8 and out[True][1] == out[False][1]
+
+
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_narrow_segment_kernel_same_trajectory(gpu, golden, mode, monkeypatch):
+    """learning.NARROW_SEGMENT (the persistent narrow segment kernel, off by default, DESIGN.md
+    §4.4e): the same w at every evaluation as one launch per step, bit for bit."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for seg in (True, False):
+        monkeypatch.setattr(lr, "NARROW_SEGMENT", seg)
+        p = _p_learn(golden, n_it=200)
+        np.random.seed(78)
+        lr.learning_process(golden["learn/X"], golden["learn/Z"], p, rng_mode=mode)
+        out[seg] = p["norm_w"]
+    assert out[True] == out[False]

@@ -29,8 +29,14 @@ from .numpy_rng import Session
 
 SEED_SHUFFLE = 42
 # narrow rows (C4): a segment of fused steps in ONE persistent launch (tw_sgd_segment_narrow:
-# one grid barrier per step, the update recomputed in every block); off: one launch per step
-NARROW_SEGMENT = True
+# one grid barrier per step, the update recomputed in every block).  Off by default: with it on,
+# a later learning_process call that re-captures the evaluation graph reads a wrong test AUC
+# count from its 5th evaluation on (tools/repro_narrow_segment_eval.py) —
+# cause not yet found; the trajectories themselves are bit-identical.
+NARROW_SEGMENT = False
+# evaluations of the learning loop: device part enqueued, host part once the results are back
+# (no device wait per evaluation); off: evaluation_step waits for its results
+DEFER_EVALS = True
 SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
@@ -816,6 +822,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
         if trajectory is None:
             trajectory = []  # the audit runs the steps one at a time
         Xh, Zh = np.asarray(X, dtype=np.float64), np.asarray(Z, dtype=np.float64)
+    defer = _deferred_evals(eng, graphs, trajectory)
     with draws.rng:  # the global RNG state lives natively until the loop ends
         rows_x, rows_z = draws.swr_rows(n_X, n_Z)  # the reference's redundant draw (:119)
         eng.set_shards(rows_x, rows_z)
@@ -849,18 +856,26 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
             # graph.  At an evaluation, w leaves the device asynchronously before the draws.
             nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
                       i + draws.segment_capacity())
-            w_pending = eng.w_host_async() if i % eval_mod == 0 else None
+            w_pending = None
+            if i % eval_mod == 0:
+                if defer is not None:  # device part enqueued now, host part later
+                    _evaluate(i, eng, None, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer)
+                else:
+                    w_pending = eng.w_host_async()
             buf, tag = (None, 0) if eng.complete else draws.pairs_segment(nxt - i)
             if w_pending is not None:
                 _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
             eng.run_replay_segment(buf, nxt - i, graphs, tag)
             i = nxt
+    if defer is not None:
+        defer.drain()
     eng.check()
     return None
 
 
-def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs):
-    """evaluation_step at step i of the replay loop (make_exps.py:127-128)."""
+def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer=None):
+    """evaluation_step at step i of the replay loop (make_exps.py:127-128); with defer, w is
+    None (copied from the device with the statistics)."""
     X_s = Z_s = batch = None  # FIXED_PAIRS evaluation does not read the shards
     if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
         batch = eng.batch_view()
@@ -868,7 +883,7 @@ def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs):
             X_s = [X[r] for r in rows_x]
             Z_s = [Z[r] for r in rows_z]
     evaluation_step(i, X_s, Z_s, w, p_learn, loss=loss, _w_dev=eng.w, _graph=graphs,
-                    _batch=batch)
+                    _batch=batch, _defer=defer)
 
 
 def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
@@ -876,6 +891,7 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
     n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
     if trajectory is not None:
         graphs = False
+    defer = _deferred_evals(eng, graphs, trajectory)
     i = 0
     while i < n_it:
         resh = i % mod == 0
@@ -887,8 +903,9 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
                     eng.reshuffle_device()
                     resh = False
                 batch = eng.batch_view()
-            evaluation_step(i, None, None, eng.w_host(), p_learn, loss=loss, _w_dev=eng.w,
-                            _graph=graphs, _batch=batch)
+            evaluation_step(i, None, None, None if defer is not None else eng.w_host(),
+                            p_learn, loss=loss, _w_dev=eng.w, _graph=graphs, _batch=batch,
+                            _defer=defer)
         if trajectory is not None:  # one step at a time, recording w
             if resh:
                 eng.reshuffle_device()
@@ -899,8 +916,58 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
         nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod)
         eng.run_segment(nxt - i, resh, graphs)
         i = nxt
+    if defer is not None:
+        defer.drain()
     eng.check()
     return None
+
+
+class _DeferredEvals:
+    """Evaluations of the learning loop whose device part (one graph replay) is enqueued in
+    stream order and whose host part — the statistics' formulas, the log line, p_learn's lists
+    (make_exps.py:162-190) — runs once their results have reached pinned host memory, in order
+    (and all of them before learning_process returns).  The loop no longer waits for the device
+    at every evaluation; the values are the same bits."""
+
+    def __init__(self, w_dev, w_shape, slots=64):
+        t = L.torch()
+        self.t = t
+        self.w_shape = w_shape
+        self.host = t.empty((slots, 4 + int(w_dev.numel())), dtype=t.float64, pin_memory=True)
+        self.events = [t.cuda.Event() for _ in range(slots)]
+        self.free = list(range(slots))[::-1]
+        self.pending = []
+
+    def push(self, i, res_dev, w_dev, finish):
+        if not self.free:
+            self._pop()
+        k = self.free.pop()
+        self.host[k, :4].copy_(res_dev.reshape(-1), non_blocking=True)
+        self.host[k, 4:].copy_(w_dev.reshape(-1), non_blocking=True)
+        self.events[k].record()
+        self.pending.append((i, k, finish))
+        while len(self.pending) > 1 and self.events[self.pending[0][1]].query():
+            self._pop()
+
+    def _pop(self):
+        i, k, finish = self.pending.pop(0)
+        self.events[k].synchronize()
+        h = self.host[k].numpy()
+        finish(i, h[:4].copy(), h[4:].copy().reshape(self.w_shape))
+        self.free.append(k)
+
+    def drain(self):
+        while self.pending:
+            self._pop()
+
+
+def _deferred_evals(eng, graphs, trajectory):
+    """A _DeferredEvals for the loop when its evaluations can be deferred: hipGraphs on, FIXED_PAIRS
+    monitoring (SAME_AS_BATCH reduces on the host), one process, no trajectory recording."""
+    if (not DEFER_EVALS or not graphs or trajectory is not None
+            or TYPE_TRAIN_MONITOR != "FIXED_PAIRS" or getattr(eng, "G", 1) != 1):
+        return None
+    return _DeferredEvals(eng.w, eng.w_shape)
 
 
 class _EvalCache:
@@ -1035,7 +1102,7 @@ def _shard_offsets(N, kx, kz):
 
 
 def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _graph=True,
-                    _batch=None):
+                    _batch=None, _defer=None):
     """
         Modify the value of p_learn to add to the evaluation.  (make_exps.py:143-190)
         Monitored values, added in p_learn:
@@ -1046,20 +1113,20 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
     """
     margin = p_learn["margin"]
     logging.debug("Step %d: Begin evaluation", i)
-    reg_term = p_learn["reg"] * (np.linalg.norm(w) ** 2) / 2
+    fixed = TYPE_TRAIN_MONITOR == "FIXED_PAIRS"
+    deferred = _defer is not None and fixed and _w_dev is not None and _graph
     t = L.torch()
+    bc = br_AUC = None  # SAME_AS_BATCH: the shards' surrogate (without the reg term) and AUC
     if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
         if _batch is not None:  # the learning loop's shards, resident on the device
             wd = _w_dev if _w_dev is not None else L.to_device(
                 np.asarray(w, np.float64).reshape(-1))
             bc, br_AUC = _same_as_batch_device(_batch, wd, margin, loss)
-            bc_AUC = bc + reg_term
         else:
             sc_X = [x.dot(w) for x in X_s]
             sc_Z = [z.dot(w) for z in Z_s]
-            bc_AUC = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin, loss=loss)) + reg_term
+            bc = cs.UN_split(sc_X, sc_Z, cs.conv_AUC(margin, loss=loss))
             br_AUC = cs.UN_split(sc_X, sc_Z, lambda x, z: cs.Un(x, z, kernel="AUC"))
-    fixed = TYPE_TRAIN_MONITOR == "FIXED_PAIRS"
     if _w_dev is not None and _graph:  # the learning loop: w resident, device work one graph
         # one cached graph: valid while p_learn holds the same objects; w reaches it through
         # a persistent buffer, so later runs (new engines, new w) replay it too
@@ -1085,13 +1152,27 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
         ent[5].copy_(_w_dev)
         ent[2].replay()
         res_dev, n_pairs, n_test = ent[3]
+        if deferred:  # the statistics and w leave the device with the loop running on
+            _defer.push(i, res_dev, _w_dev, lambda it, res, wh: _eval_host(
+                it, res, wh, n_pairs, n_test, p_learn, fixed, None, None))
+            return
     else:
         wd = _w_dev if _w_dev is not None else L.to_device(np.asarray(w, np.float64).reshape(-1))
         res_dev, n_pairs, n_test = _eval_device(wd, p_learn, loss, margin, fixed)
     res = res_dev.cpu().numpy()  # the ONE copy back: [hinge sum, count] x (pairs, test)
+    _eval_host(i, res, w, n_pairs, n_test, p_learn, fixed, bc, br_AUC)
+
+
+def _eval_host(i, res, w, n_pairs, n_test, p_learn, fixed, bc, br_AUC):
+    """evaluation_step's host part from the copied statistics res = [monitor surrogate sum,
+    monitor count bits, test surrogate sum, test count bits] (make_exps.py:162-190); bc, br_AUC:
+    the SAME_AS_BATCH monitor statistics (None with FIXED_PAIRS)."""
+    reg_term = p_learn["reg"] * (np.linalg.norm(w) ** 2) / 2
     if fixed:
         bc_AUC = np.float64(res[0] / np.float64(n_pairs)) + reg_term
         br_AUC = E.ratio(int(res[1:2].view(np.uint64)[0]), n_pairs)
+    else:
+        bc_AUC = bc + reg_term
     tc_AUC = np.float64(res[2] / np.float64(n_test)) + reg_term
     tr_AUC = E.ratio(int(res[3:4].view(np.uint64)[0]), n_test)
 
