@@ -446,9 +446,15 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     }
     seg_arrive(ctl);  // also: every thread is done with diff / flag / gt of this step
   }
-  if (s == 0 && tid < dd) {
-    w_out[tid] = wj;
-    dw_out[tid] = dwj;
+  if (s == 0) {
+    if (tid < dd) {
+      w_out[tid] = wj;
+      dw_out[tid] = dwj;
+    }
+    // leave the arrival counter at zero for the next launch (no memset node): block 0 waits
+    // for the last arrivals of this launch, after which no block touches the counter
+    if (nsteps > 0 && seg_wait(ctl, (uint32_t)nsteps * (uint32_t)G, &s_ok) && tid == 0)
+      __hip_atomic_store(ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -519,7 +525,6 @@ extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64
   TW_ARG_CHECK(loss == TW_LOSS_HINGE || loss == TW_LOSS_LOGISTIC, "unknown loss %d", loss);
   if (nsteps == 0) return TW_OK;
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_ctl, 0, sizeof(uint32_t), st));  // the arrival counter only
   const size_t lds = narrow_lds(d, n_shards, B);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x, kx,
