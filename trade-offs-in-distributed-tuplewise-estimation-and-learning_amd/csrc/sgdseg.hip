@@ -512,7 +512,11 @@ extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64
                                      double lr, double momentum, double* d_grads0,
                                      double* d_grads1, double* d_w_out, double* d_dw_out,
                                      uint32_t* d_ctl, void* stream) {
-  TW_ARG_CHECK(tw_sgd_segment_narrow_ok(d, n_shards, B),
+  // shape limits only: the residency query (tw_sgd_segment_narrow_ok) is a HIP API call the
+  // caller makes once, before any stream capture — this entry runs inside captured graphs
+  TW_ARG_CHECK(d >= 1 && d <= kNarrowMaxD && n_shards >= 1 &&
+                   (int64_t)n_shards * d <= kNarrowMaxGrads && B >= 1 &&
+                   narrow_lds(d, n_shards, B) <= 64 * 1024,
                "tw_sgd_segment_narrow: d=%lld, n_shards=%d, B=%lld unsupported", (long long)d,
                n_shards, (long long)B);
   TW_ARG_CHECK(kx >= 1 && kz >= 1 && shard_base >= 0 && nsteps >= 0 && nsteps <= (1 << 20) &&
