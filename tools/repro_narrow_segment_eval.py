@@ -1,10 +1,8 @@
-"""Repro (GPU box) of the open issue behind learning.NARROW_SEGMENT = False:
-with the persistent narrow segment kernel on, a second learning_process call whose evaluation
-graph is re-captured (new p_learn objects) reads a wrong evaluation count (~7e13 instead of an
-AUC) from its 5th evaluation on — the test AUC while the kernel reset its arrival counter with a
-captured hipMemsetAsync, the monitor AUC (in the deferred-evaluation test) once it no longer
-does — while the trajectory and the other statistics stay right; with the kernel off, or the
-first engine kept alive, everything agrees."""
+"""Regression check (GPU box) for DESIGN.md §4.4e: with the persistent narrow segment kernel on,
+a second learning_process call whose evaluation graph is re-captured used to read a wrong
+evaluation count (~7e13) from its 5th evaluation on — a count output zeroed by a captured
+hipMemsetAsync node whose zeroing did not take effect.  Every entry point now zeroes with a
+kernel (tw_common.h tw_zero_async); every line below must print the same values."""
 import sys, logging, pathlib, gc
 sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
 import numpy as np, torch

@@ -539,7 +539,7 @@ extern "C" int tw_count_pairs(const void* d_x, const int64_t* d_x_off, const voi
   TW_ARG_CHECK(max_nx >= 0 && max_nz >= 0, "tw_count_pairs: negative shard size");
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (max_nx == 0 || max_nz == 0) return TW_OK;
   const NextStep none{};
   if (dtype == TW_F64) return dispatch_complete<double>(pred, d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_out, none, st);
@@ -606,7 +606,7 @@ extern "C" int tw_count_pairs_step(const void* d_x, const int64_t* d_x_off, cons
         (int64_t)(ng - 1) * nxt.every + kXcds > p.blocks + nxt.blocks)
       nxt.every = kXcds;  // leading blocks
   } else if (d_out_next != nullptr && n_next_shards > 0) {
-    TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+    TW_HIP_CHECK(tw_zero_async(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
   }
   if (n_shards == 0 || max_nx == 0 || max_nz == 0) {  // nothing to count: only the next step
     if (nxt.blocks == 0) return TW_OK;
@@ -627,7 +627,7 @@ int count_idx(const void* d_x, const void* d_z, const I* d_ix, const I* d_iz,
   TW_ARG_CHECK(n_shards >= 0 && max_pairs >= 0, "tw_count_pairs_idx: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (max_pairs == 0) return TW_OK;
 #define TW_IDX(T, P) return launch_idx<T, P, I>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, d_out, st)
   if (dtype == TW_F64) {
@@ -667,7 +667,7 @@ extern "C" int tw_count_pairs_rng(const void* d_x, const int64_t* d_x_off, const
   TW_ARG_CHECK(n_shards >= 0 && B >= 0, "tw_count_pairs_rng: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (B == 0) return TW_OK;
 #define TW_RNG(T, P) return launch_rng<T, P>(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, d_out, st)
   if (dtype == TW_F64) {

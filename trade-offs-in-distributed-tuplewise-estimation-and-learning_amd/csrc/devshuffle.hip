@@ -218,7 +218,7 @@ extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_
   const int64_t total = nx + nz;
   hipStream_t st = (hipStream_t)stream;
   if (nx <= 1 && nz <= 1) {  // no iteration at all
-    TW_HIP_CHECK(hipMemsetAsync(d_pending, 0, 4, st));
+    TW_HIP_CHECK(tw_zero_async(d_pending, 0, 4, st));
     return TW_OK;
   }
   const ShPlan p = plan_sh(nx, nz);
@@ -238,14 +238,14 @@ extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_
   ch.pz = nz > 1 ? ceil_div(nz - 1, kShWindows) : 0;
   const double per = (double)total / kShWindows;
   if (first) {
-    TW_HIP_CHECK(hipMemsetAsync(w, 0, (size_t)p.bytes, st));
+    TW_HIP_CHECK(tw_zero_async(w, 0, (size_t)p.bytes, st));
     hipLaunchKernelGGL(k_sh_reserve0, dim3(grid_for(per)), dim3(kShThreads), 0, st, d_jx, d_jz,
                        ch, R[0]);
   } else {
     // continue: the previous batch's last list (parity of its last round) is round0's input;
     // its count moves to slot 0
     TW_HIP_CHECK(hipMemcpyAsync(cnt, cnt + p.rounds, 4, hipMemcpyDeviceToDevice, st));
-    TW_HIP_CHECK(hipMemsetAsync(cnt + 1, 0, (size_t)p.rounds * 4, st));
+    TW_HIP_CHECK(tw_zero_async(cnt + 1, 0, (size_t)p.rounds * 4, st));
   }
   for (int k = 0; k < p.rounds; ++k) {
     const int r = round0 + k;

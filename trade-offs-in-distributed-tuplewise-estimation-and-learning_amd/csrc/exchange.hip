@@ -123,7 +123,7 @@ extern "C" int tw_row_route_counts(const int64_t* d_rows, int64_t M, int64_t M_q
   TW_ARG_CHECK(d_counts != nullptr && (M == 0 || d_rows != nullptr),
                "tw_row_route_counts: null pointer");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int64_t) * G, st));
+  TW_HIP_CHECK(tw_zero_async(d_counts, 0, sizeof(int64_t) * G, st));
   if (M == 0) return TW_OK;
   hipLaunchKernelGGL(k_route_counts, dim3((unsigned)ceil_div(M, kChunk)), dim3(kBlock), 0, st,
                      d_rows, M, M_q, lo, hi, (int)G, (unsigned long long*)d_counts);
@@ -141,7 +141,7 @@ extern "C" int tw_row_pack(const int64_t* d_rows, int64_t M, int64_t M_q, int64_
   TW_ARG_CHECK(lo >= 0 && hi >= lo, "tw_row_pack: bad owned range");
   TW_ARG_CHECK(d_start != nullptr && d_cursor != nullptr, "tw_row_pack: null pointer");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_cursor, 0, sizeof(int64_t) * G, st));
+  TW_HIP_CHECK(tw_zero_async(d_cursor, 0, sizeof(int64_t) * G, st));
   if (M == 0 || hi == lo) return TW_OK;
   TW_ARG_CHECK(d_rows && d_part && d_send, "tw_row_pack: null pointer");
   hipLaunchKernelGGL(k_row_pack, dim3((unsigned)ceil_div(M, kChunk)), dim3(kBlock), 0, st,

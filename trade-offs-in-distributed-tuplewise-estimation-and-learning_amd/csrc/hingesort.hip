@@ -299,7 +299,7 @@ extern "C" int tw_pair_hinge_sum_sorted(const double* d_x, const int64_t* d_x_of
   double* P_lo = P_hi + (int64_t)n_shards * p.chunks * (kHsC + 1);
   double* part = (double*)(w + p.part);
   int* counts = (int*)(w + p.counts);
-  TW_HIP_CHECK(hipMemsetAsync(counts, 0, (size_t)n_shards * kHsCounts * 4, st));
+  TW_HIP_CHECK(tw_zero_async(counts, 0, (size_t)n_shards * kHsCounts * 4, st));
   static bool attr = false;
   if (!attr) {
     TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_sort_chunks<double, 4>,

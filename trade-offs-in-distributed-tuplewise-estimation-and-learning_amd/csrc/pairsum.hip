@@ -258,7 +258,7 @@ extern "C" int tw_pair_sum_idx32_f64(const double* d_x, const double* d_z, const
   if (d_count == nullptr)
     return pair_sum_idx<int32_t, false>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs,
                                         kern, margin, d_work, d_out, nullptr, st);
-  TW_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_count, 0, sizeof(uint64_t) * n_shards, st));
   return pair_sum_idx<int32_t, true>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, kern,
                                      margin, d_work, d_out, d_count, st);
 }

@@ -379,7 +379,7 @@ extern "C" int tw_rank_histogram(const int64_t* d_perm, int64_t n, int64_t n_loc
                                  uint64_t* d_counts, void* stream) {
   TW_ARG_CHECK(G >= 1 && G <= kMaxG && n >= 0 && n_loc >= 1, "tw_rank_histogram: bad sizes");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * G, st));
+  TW_HIP_CHECK(tw_zero_async(d_counts, 0, sizeof(uint64_t) * G, st));
   if (n == 0) return TW_OK;
   const int blocks = (int)std::min<int64_t>(256 * 4, ceil_div(n, kBlock));
   hipLaunchKernelGGL(k_rank_histogram, dim3(blocks), dim3(kBlock), 0, st, d_perm, n, n_loc, (int)G,
@@ -394,7 +394,7 @@ extern "C" int tw_source_histogram(int64_t n, int64_t base, int64_t n_total, uin
                    base + n <= n_total && n_total <= n_loc * (int64_t)G && n_total < (1ll << 60),
                "tw_source_histogram: bad sizes");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * G, st));
+  TW_HIP_CHECK(tw_zero_async(d_counts, 0, sizeof(uint64_t) * G, st));
   if (n == 0) return TW_OK;
   const Feistel f = make_feistel(n_total, key);
   const int blocks = (int)std::min<int64_t>(256 * 4, ceil_div(n, kBlock));
@@ -411,7 +411,7 @@ extern "C" int tw_bucket_scatter(const int64_t* d_perm, const void* d_vals, int6
   TW_ARG_CHECK(G >= 1 && G <= kMaxG && n >= 0 && n_loc >= 1 && pos_base >= 0,
                "tw_bucket_scatter: bad sizes");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_cursor, 0, sizeof(uint64_t) * G, st));
+  TW_HIP_CHECK(tw_zero_async(d_cursor, 0, sizeof(uint64_t) * G, st));
   if (n == 0) return TW_OK;
   const int blocks = (int)std::min<int64_t>(256 * 4, ceil_div(n, kScatChunk));
   hipLaunchKernelGGL(k_bucket_scatter, dim3(blocks), dim3(kBlock), 0, st, d_perm,
@@ -444,7 +444,7 @@ extern "C" int tw_exchange_counts(int64_t n_loc, int64_t m_loc, int32_t rank, in
                "tw_exchange_counts: bad sizes");
   TW_ARG_CHECK(d_counts && d_cursor, "tw_exchange_counts: null pointer");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * 4 * G, st));
+  TW_HIP_CHECK(tw_zero_async(d_counts, 0, sizeof(uint64_t) * 4 * G, st));
   const Feistel fx = make_feistel(n_loc * (int64_t)G, key_x);
   const Feistel fz = make_feistel(m_loc * (int64_t)G, key_z);
   const int blocks = (int)std::min<int64_t>(exchange_grid(256 * 4), ceil_div(n_loc + m_loc, kBlock));

@@ -1090,7 +1090,7 @@ extern "C" int tw_count_pairs_sorted(const void* d_x, const int64_t* d_x_off, co
                "tw_count_pairs_sorted: predicate must be TW_PRED_GT or TW_PRED_HALF");
   hipStream_t st = (hipStream_t)stream;
   if (n_shards == 0) return TW_OK;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (max_nx == 0 || max_nz == 0) return TW_OK;
   if (dtype == TW_F64) return launch_rank<double>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, pred, d_work, d_out, st);
   if (dtype == TW_I64) return launch_rank<long long>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, pred, d_work, d_out, st);
@@ -1130,7 +1130,7 @@ extern "C" int tw_count_pairs_sorted_step(const void* d_x, const int64_t* d_x_of
                      make_feistel(std::max<int64_t>(n_x, 1), key_x),
                      make_feistel(std::max<int64_t>(n_z, 1), key_z), 1, 0, 0};
     else if (d_out_next != nullptr && n_next_shards > 0)
-      TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+      TW_HIP_CHECK(tw_zero_async(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
 #define TW_BSTEP(T, P) return launch_bucket_count<T, P>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, d_out, nxt, st)
     if (dtype == TW_F64) {
       if (pred == TW_PRED_HALF) TW_BSTEP(double, TW_PRED_HALF);
@@ -1148,7 +1148,7 @@ extern "C" int tw_count_pairs_sorted_step(const void* d_x, const int64_t* d_x_of
     if (rc != TW_OK) return rc;
   }
   if (d_out_next != nullptr && n_next_shards > 0)
-    TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+    TW_HIP_CHECK(tw_zero_async(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
   return TW_OK;
 }
 
@@ -1223,8 +1223,8 @@ extern "C" int tw_count_pairs_sorted_steps(const void* d_x, const void* d_z, int
   TW_ARG_CHECK(d_x_out != d_x && d_z_out != d_z && d_x_out != nullptr && d_z_out != nullptr,
                "tw_count_pairs_sorted_steps: outputs must be distinct buffers");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * (size_t)T * n_shards, st));
-  TW_HIP_CHECK(hipMemsetAsync(W.cx[0], 0, (char*)d_work + W.total - (char*)W.cx[0], st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)T * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(W.cx[0], 0, (char*)d_work + W.total - (char*)W.cx[0], st));
   const FastDiv dx = make_fastdiv((uint64_t)std::max<int64_t>(kx, 1));
   const FastDiv dz = make_fastdiv((uint64_t)std::max<int64_t>(kz, 1));
   auto emit = [&](const uint64_t* xv, const uint32_t* xp, const uint64_t* zv, const uint32_t* zp,
@@ -1300,7 +1300,7 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
     const ImgPlan ip = plan_images(n_shards, max_nx, max_nz, pr, (B + 1) / 2);
     if (ip.ok) {
       hipStream_t st = (hipStream_t)stream;
-      TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+      TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
       return launch_rng_images(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, dtype,
                                pr, ip, d_out, NextStep{}, st);
     }
@@ -1314,7 +1314,7 @@ extern "C" int tw_count_pairs_rng_ws(const void* d_x, const int64_t* d_x_off, co
                    (int64_t)n_shards * p.chunks < (1ll << 31),
                "tw_count_pairs_rng_ws: grid too large");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
   if (dtype == TW_F64) {
     if (pred == TW_PRED_HALF)
       return launch_rng_ranked<double, TW_PRED_HALF>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, B, seed, stream_id, p, d_work, d_out, st);
@@ -1357,7 +1357,7 @@ extern "C" int tw_count_pairs_rng_step(const void* d_x, const int64_t* d_x_off, 
                        make_feistel(std::max<int64_t>(n_x, 1), key_x),
                        make_feistel(std::max<int64_t>(n_z, 1), key_z), 1, 0, 0};
       else if (d_out_next != nullptr && n_next_shards > 0)
-        TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+        TW_HIP_CHECK(tw_zero_async(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
       return launch_rng_images(d_x, d_x_off, d_z, d_z_off, n_shards, B, seed, stream_id, dtype,
                                pr, ip, d_out, nxt, st);
     }
@@ -1370,7 +1370,7 @@ extern "C" int tw_count_pairs_rng_step(const void* d_x, const int64_t* d_x_off, 
     if (rc != TW_OK) return rc;
   }
   if (d_out_next != nullptr && n_next_shards > 0)
-    TW_HIP_CHECK(hipMemsetAsync(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
+    TW_HIP_CHECK(tw_zero_async(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
   return TW_OK;
 }
 
@@ -1435,7 +1435,7 @@ int count_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z, const
     const ImgPlan ip = plan_images(n_shards, max_nx, max_nz, pr, max_pairs);
     if (ip.ok) {
       hipStream_t st = (hipStream_t)stream;
-      TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+      TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
       return launch_idx_images<I>(d_x, d_x_off, d_z, d_z_off, n_shards, d_ix, d_iz, d_pair_off,
                                   dtype, pr, ip, d_out, st);
     }
@@ -1453,7 +1453,7 @@ int count_idx_ws(const void* d_x, const int64_t* d_x_off, const void* d_z, const
                    (int64_t)n_shards * p.code_parts < (1ll << 31),
                "tw_count_pairs_idx_ws: grid too large");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(uint64_t) * n_shards, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * n_shards, st));
 #define TW_IR(T, P) return launch_idx_ranked<T, P, I>(d_x, d_x_off, d_z, d_z_off, n_shards, max_nx, max_nz, d_ix, d_iz, d_pair_off, p, d_work, d_out, st)
   if (dtype == TW_F64) {
     if (pr == TW_PRED_HALF) TW_IR(double, TW_PRED_HALF);

@@ -583,7 +583,7 @@ extern "C" int tw_sgd_segment(const double* d_X, const double* d_Z, int64_t d,
   int grid = std::min(n_shards, cap);
   if (g_seg_grid > 0) grid = std::min(grid, g_seg_grid);
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(hipMemsetAsync(d_ctl, 0, sizeof(uint32_t), st));  // the arrival counter only
+  TW_HIP_CHECK(tw_zero_async(d_ctl, 0, sizeof(uint32_t), st));  // the arrival counter only
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWideBlock), 0, st, d_X, d_Z, d, d_rows_x, kx,
                        d_rows_z, kz, d_ix, d_iz, draw_stride, (int)n_shards, B, margin, seed,

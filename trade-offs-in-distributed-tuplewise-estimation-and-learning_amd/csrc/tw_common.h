@@ -1,5 +1,6 @@
 // tw_common.h — shared helpers for libtuplewise.so (gfx950 only).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
@@ -36,6 +37,30 @@ constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWave = 64;
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Zeroing of device buffers by a kernel rather than hipMemsetAsync: every entry point may be
+// captured into a hipGraph, and a captured memset node was seen not to take effect in one
+// graph-replay sequence; a kernel node is an ordinary launch.
+static __global__ __launch_bounds__(256) void k_zero_fill(unsigned char* __restrict__ p,
+                                                          size_t n) {
+  const size_t tid = blockIdx.x * (size_t)256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
+  if ((((uintptr_t)p | n) & 7) == 0) {
+    unsigned long long* q = (unsigned long long*)p;
+    for (size_t i = tid; i < n / 8; i += stride) q[i] = 0ull;
+  } else {
+    for (size_t i = tid; i < n; i += stride) p[i] = 0;
+  }
+}
+
+// same signature as hipMemsetAsync; value must be 0
+static inline hipError_t tw_zero_async(void* p, int value, size_t bytes, hipStream_t st) {
+  if (value != 0) return hipErrorInvalidValue;
+  if (bytes == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>(1024, (bytes + 256 * 8 * 4 - 1) / (256 * 8 * 4));
+  hipLaunchKernelGGL(k_zero_fill, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0, st,
+                     (unsigned char*)p, bytes);
+  return hipGetLastError();
+}
 
 // XCD-aware block order.  The dispatcher deals workgroups round-robin over the 8 XCDs
 // (blocks b and b+8 share one XCD and its 4 MiB L2; MI355X_MICROARCH.md "Workgroup dispatch").

@@ -29,12 +29,8 @@ from .numpy_rng import Session
 
 SEED_SHUFFLE = 42
 # narrow rows (C4): a segment of fused steps in ONE persistent launch (tw_sgd_segment_narrow:
-# one grid barrier per step, the update recomputed in every block).  Off by default: with it on,
-# a later learning_process call that re-captures the evaluation graph reads a wrong evaluation
-# count (test AUC, or with the kernel's memset node removed the monitor AUC) from its 5th
-# evaluation on (tools/repro_narrow_segment_eval.py) — cause not yet found;
-# the trajectories themselves are bit-identical.
-NARROW_SEGMENT = False
+# one grid barrier per step, the update recomputed in every block); off: one launch per step
+NARROW_SEGMENT = True
 # evaluations of the learning loop: device part enqueued, host part once the results are back
 # (no device wait per evaluation); off: evaluation_step waits for its results
 DEFER_EVALS = True
