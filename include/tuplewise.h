@@ -409,8 +409,10 @@ int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* 
  * d_dw_out hold the state after the segment's last update and the last step's gradients are
  * in slot (nsteps-1) & 1: apply them with tw_sgd_update_to(d_w_out, d_dw_out -> w, dw,
  * step_inc = nsteps).  Draws: d_ix/d_iz + step k * draw_stride (replay) or device RNG at
- * *d_step + k.  d_ctl: 2 words (arrival counter, zeroed here; sticky abort word, zeroed once
- * by the caller: set when a bounded barrier wait expired).  Same bits as tw_sgd_step per step.
+ * *d_step + k.  d_ctl: 2 words, zeroed once by the caller — the arrival counter (the kernel
+ * leaves it at zero again) and a sticky abort word (set when a bounded barrier wait expired).
+ * The residency check (tw_sgd_segment_narrow_ok) is the caller's, once, outside any stream
+ * capture: this entry only checks shapes.  Same bits as tw_sgd_step per step.
  * make_exps.py:122-141 with compute_stats.py:146-162. */
 int tw_sgd_segment_narrow_ok(int64_t d, int32_t n_shards, int64_t B);
 int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
