@@ -81,3 +81,14 @@ def test_single_hip_runtime_whatever_the_import_order():
                          timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().splitlines()[-1] == "1"
+
+
+def test_no_captured_memset_nodes():
+    """Every entry point may run inside a captured hipGraph; a captured hipMemsetAsync node was
+    seen not to take effect in one replay sequence, so the sources zero
+    device buffers with a kernel (tw_common.h tw_zero_async) only."""
+    import pathlib
+    csrc = pathlib.Path(__file__).resolve().parents[1] / \
+        "trade-offs-in-distributed-tuplewise-estimation-and-learning_amd" / "csrc"
+    bad = [f.name for f in csrc.glob("*.hip") if "hipMemsetAsync(" in f.read_text()]
+    assert not bad, bad
