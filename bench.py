@@ -338,13 +338,17 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
     run(steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    eng.check()  # a persistent segment that gave up at a barrier invalidates the run
+    launches = ("one persistent launch per segment" if eng.narrow_seg else
+                "one launch per step" if eng.fused else
+                "one segment kernel per segment" if eng.segment else "gradient + update per step")
     out = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
            "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
            "gather_GBps": N * B * 16 * d * steps / dt / 1e9,
            "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B,
                       "reshuffle_mod": reshuffle_mod, "optim": "momentum",
                       "rng": "device (Philox)", "graphs": True, "steps": steps,
-                      "x_layout": layout}}
+                      "x_layout": layout, "launches": launches}}
     if layout == "partitioned":
         reps = 3
         torch.cuda.synchronize()
