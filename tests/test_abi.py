@@ -92,3 +92,16 @@ def test_no_captured_memset_nodes():
         "trade-offs-in-distributed-tuplewise-estimation-and-learning_amd" / "csrc"
     bad = [f.name for f in csrc.glob("*.hip") if "hipMemsetAsync(" in f.read_text()]
     assert not bad, bad
+
+
+def test_lazy_learning_attribute():
+    """tuplewise.learning is imported lazily; both access forms must resolve it (the first
+    version of the package __getattr__ recursed on `from tuplewise import learning`)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from tuplewise import learning as a; "
+            "import tuplewise; assert tuplewise.learning is a; print(a.__name__)") % str(ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "tuplewise.learning"

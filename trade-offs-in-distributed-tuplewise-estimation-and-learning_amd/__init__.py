@@ -18,6 +18,8 @@ __all__ = ["compute_stats", "estimation", "device", "learning"]
 
 def __getattr__(name):
     if name == "learning":  # imports logging config helpers lazily
-        from . import learning
-        return learning
+        # importlib, not "from . import": that form probes hasattr(package, "learning") first,
+        # which would re-enter this function
+        import importlib
+        return importlib.import_module(__name__ + ".learning")
     raise AttributeError(name)
