@@ -408,7 +408,7 @@ def test_deferred_evaluations_equal_synchronous(gpu, golden, mode, monkeypatch):
 
 @pytest.mark.parametrize("mode", ["replay", "device"])
 def test_narrow_segment_kernel_same_trajectory(gpu, golden, mode, monkeypatch):
-    """learning.NARROW_SEGMENT (the persistent narrow segment kernel, off by default, DESIGN.md
+    """learning.NARROW_SEGMENT (the persistent narrow segment kernel, on by default, DESIGN.md
     §4.4e): the same w at every evaluation as one launch per step, bit for bit."""
     import tuplewise.learning as lr
     logging.disable(logging.CRITICAL)
@@ -420,3 +420,23 @@ def test_narrow_segment_kernel_same_trajectory(gpu, golden, mode, monkeypatch):
         lr.learning_process(golden["learn/X"], golden["learn/Z"], p, rng_mode=mode)
         out[seg] = p["norm_w"]
     assert out[True] == out[False]
+
+
+def test_deferred_evals_slot_reuse(gpu):
+    """_DeferredEvals with fewer pinned slots than evaluations in flight: every host part runs
+    once, in push order, with the values the device held at its push (slots are reused only
+    after their copy has landed)."""
+    import torch
+    import tuplewise.learning as lr
+    w = torch.zeros(5, dtype=torch.float64, device="cuda")
+    res = torch.zeros(4, dtype=torch.float64, device="cuda")
+    d = lr._DeferredEvals(w, (5,), slots=3)
+    seen = []
+    for i in range(20):
+        res.fill_(float(i))
+        w.fill_(-float(i))
+        d.push(i, res, w, lambda j, r, ww: seen.append((j, r.tolist(), ww.tolist())))
+    d.drain()
+    assert [s[0] for s in seen] == list(range(20))
+    for j, r, ww in seen:
+        assert r == [float(j)] * 4 and ww == [-float(j)] * 5
