@@ -719,6 +719,7 @@ def main():
     ops = S.ops
     ops.count = kernel_ms.wrap(ops.count)
     ops.count_step = kernel_ms.wrap(ops.count_step)  # count + next repartition on spare blocks
+    ops.count_rank_step = kernel_ms.wrap(ops.count_rank_step)  # the same on rank images
     ops.count_sorted_step = kernel_ms.wrap(ops.count_sorted_step)  # sorted count + next
     ops.count_sorted_steps = kernel_ms.wrap(ops.count_sorted_steps)  # all K sorted steps
 

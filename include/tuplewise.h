@@ -103,6 +103,36 @@ int tw_count_set_scalar_mix(int32_t on);
  * and z-chunk length per block (0 = automatic).  Process-global; results do not depend on it. */
 int tw_count_set_plan(int32_t R, int64_t z_chunk);
 
+/* ---- A1/A6/A7 on rank images (round 3, csrc/rankimage.hip): the all-pairs count of
+ * est.UnN / UnNT (estimation-experiment/main.py:29-31, :72-79) on packed f32 images.
+ * tw_rank_images gives every score an 8-B record {low word: f32 image, high word: its index in
+ * d_x / d_z}: x image = #{z < x}, z image = -(its position among the stably sorted z), so that
+ * for any pair x > z <=> x_image + z_image >= 1, NaN and -0 == +0 included (strict predicate,
+ * float64 or int64 scores; int64 SUBGT / half ties stay on tw_count_pairs).  One stable radix
+ * sort of X u Z per call; needs n_z < 2^24 (tw_rank_images_work_bytes returns -1 otherwise).
+ * d_work: device scratch of tw_rank_images_work_bytes(n_x, n_z) bytes. */
+int64_t tw_rank_images_work_bytes(int64_t n_x, int64_t n_z);
+int tw_rank_images(const void* d_x, int64_t n_x, const void* d_z, int64_t n_z, int32_t dtype,
+                   void* d_work, int64_t work_bytes, uint64_t* d_x_rec, uint64_t* d_z_rec,
+                   void* stream);
+/* tw_count_pairs_step on records: counts every shard of the current partition of d_x_rec /
+ * d_z_rec into d_out (already zero) — per pair one packed clamp-add and one packed add — and,
+ * when d_x_next is given, permutes both record arrays for the next step with the keyed Feistel
+ * bijection (as tw_count_pairs_step permutes scores) and zeroes d_out_next, in the same launch.
+ * Counts are identical to tw_count_pairs(..., TW_PRED_GT) on the scores the records index. */
+int tw_count_pairs_rank_step(const uint64_t* d_x_rec, const int64_t* d_x_off,
+                             const uint64_t* d_z_rec, const int64_t* d_z_off, int32_t n_shards,
+                             int64_t max_nx, int64_t max_nz, uint64_t* d_out, int64_t n_x,
+                             uint64_t* d_x_next, uint64_t key_x, int64_t n_z, uint64_t* d_z_next,
+                             uint64_t key_z, uint64_t* d_out_next, int32_t n_next_shards,
+                             void* stream);
+/* The scores in record order: d_out[p] = d_in[d_rec[p] >> 32] (8-B values; in != out). */
+int tw_gather_records(const void* d_in, const uint64_t* d_rec, int64_t n, void* d_out,
+                      void* stream);
+/* Tuning hook for tw_count_pairs_rank_step: x-images per lane R (8 or 16; 0 = automatic) and
+ * z-chunk length (0 = automatic).  Process-global; results do not depend on it. */
+int tw_count_rank_set_plan(int32_t R, int64_t z_chunk);
+
 /* ---- f4: the same counts in O((n+m) log m): sort each z-chunk (<= 16384 keys) in LDS as
  * order-preserving u64 keys, then binary-search every x (csrc/rankcount.hip).  Bit-identical
  * to tw_count_pairs for TW_PRED_GT and TW_PRED_HALF (not SUBGT).  d_work: device scratch of

@@ -358,6 +358,43 @@ def feistel_perm_inv(pos, n: int, key: int) -> np.ndarray:
         v[bad] = once_inv(v[bad])
 
 
+def order_keys(v) -> np.ndarray:
+    """Restates csrc/sortkeys.h order_key: order-preserving uint64 keys (NaN above every
+    value, -0.0 == +0.0; int64 by flipping the sign bit)."""
+    v = np.asarray(v).reshape(-1)
+    if v.dtype == np.int64:
+        return v.view(np.uint64) ^ np.uint64(1 << 63)
+    v = v.astype(np.float64)
+    b = v.view(np.uint64).copy()
+    b[v == 0] = 0
+    neg = (b >> np.uint64(63)) == 1
+    k = np.where(neg, ~b, b | np.uint64(1 << 63))
+    k[np.isnan(v)] = np.uint64(2 ** 64 - 1)
+    return k
+
+
+def rank_records(X, Z):
+    """Restates csrc/rankimage.hip tw_rank_images (the round-3 all-pairs count on packed f32
+    images; not a reference function): sort X u Z stably by order key, x before z; an
+    element's image is the number of z sorted before it (NaN x: -2^25); z images are stored
+    negated.  Records: low word the f32 image bits, high word the element's index.  For every
+    pair, X_i > Z_j  <=>  x_image + z_image >= 1."""
+    X, Z = np.asarray(X).reshape(-1), np.asarray(Z).reshape(-1)
+    n, m = X.size, Z.size
+    keys = np.concatenate([order_keys(X), order_keys(Z)])
+    order = np.argsort(keys, kind="stable")
+    isz = (order >= n).astype(np.int64)
+    img = np.empty(n + m, np.float32)
+    img[order] = (np.cumsum(isz) - isz).astype(np.float32)
+    gx, gz = img[:n].copy(), img[n:]
+    if X.dtype != np.int64:
+        gx[np.isnan(X)] = np.float32(-2.0 ** 25)
+    xr = gx.view(np.uint32).astype(np.uint64) | (np.arange(n, dtype=np.uint64) << np.uint64(32))
+    zr = (-gz).view(np.uint32).astype(np.uint64) | (np.arange(m, dtype=np.uint64)
+                                                    << np.uint64(32))
+    return xr.view(np.int64), zr.view(np.int64)
+
+
 def permute_scatter(vals: np.ndarray, key: int) -> np.ndarray:
     """out[perm(i)] = vals[i] (tw_permute_scatter)."""
     out = np.empty_like(vals)

@@ -466,6 +466,7 @@ def _device_shuffle_ok(X, Z, spec) -> bool:
             and X.flags.c_contiguous and Z.flags.c_contiguous and X.flags.writeable
             and Z.flags.writeable and max(X.shape[0], Z.shape[0]) >= DEVICE_SHUFFLE_MIN
             and X.shape[0] + Z.shape[0] < 2 ** 31 and hasattr(spec, "evaluate_device")
+            and not np.shares_memory(X, Z)  # separate uploads would lose the aliasing
             and np.random.get_state(legacy=True)[0] == "MT19937" and len(M.devices()) < 2)
 
 

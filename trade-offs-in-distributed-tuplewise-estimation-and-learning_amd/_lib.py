@@ -34,6 +34,12 @@ _SIGNATURES = {
     "tw_count_step_set_plan": [_i32, _i32, _i32],
     "tw_count_set_scalar_mix": [_i32],
     "tw_count_set_plan": [_i32, _i64],
+    "tw_rank_images_work_bytes": [_i64, _i64],
+    "tw_rank_images": [_vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp],
+    "tw_count_pairs_rank_step": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _vp, _i64, _vp, _u64,
+                                 _i64, _vp, _u64, _vp, _i32, _vp],
+    "tw_gather_records": [_vp, _vp, _i64, _vp, _vp],
+    "tw_count_rank_set_plan": [_i32, _i64],
     "tw_count_pairs_sorted_work_bytes": [_i32, _i64],
     "tw_count_sorted_set_chunk": [_i64],
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],
@@ -135,6 +141,7 @@ _SIGNATURES = {
 _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,
     "tw_count_pairs_sorted_work_bytes": ctypes.c_int64,
+    "tw_rank_images_work_bytes": ctypes.c_int64,
     "tw_count_pairs_rng_work_bytes": ctypes.c_int64,
     "tw_count_pairs_sorted_steps_work_bytes": ctypes.c_int64,
     "tw_pair_sum_work_per_shard": ctypes.c_int64,

@@ -21,6 +21,10 @@ import numpy as np
 from . import _engine as E
 from . import _lib as L
 
+# UnN_many's all-pairs steps on rank images (csrc/rankimage.hip; A/B switch: False keeps the
+# double-compare kernel of csrc/count.hip)
+RANK_IMAGES = True
+
 
 def prop_swor_layout(n_X: int, n_Z: int, N: int):
     """Block bounds of UN(..., sampling_type="prop-SWOR") on already-shuffled arrays
@@ -127,6 +131,40 @@ class HipOps:
                int(n_shards), int(max_nx), int(max_nz), int(dtype), int(pred), L.ptr(out),
                int(x.numel()), L.ptr(x_next), int(key_x), int(z.numel()), L.ptr(z_next),
                int(key_z), L.ptr(out_next), int(out_next.numel()) if out_next is not None else 0,
+               L.stream_handle())
+        return out
+
+    def rank_images(self, X, Z, dtype):
+        """Rank-image records of both samples (tw_rank_images, csrc/rankimage.hip): int64
+        tensors whose low word is the f32 image and high word the score's index; None where
+        the path does not apply (n_z >= 2^24)."""
+        n, m = int(X.numel()), int(Z.numel())
+        wb = int(L.lib().tw_rank_images_work_bytes(n, m))
+        if wb < 0:
+            return None
+        work = L.empty((max(wb, 1),), self.t.uint8)
+        xr = L.empty((n,), self.t.int64)
+        zr = L.empty((m,), self.t.int64)
+        L.call("tw_rank_images", L.ptr(X), n, L.ptr(Z), m, int(dtype), L.ptr(work), wb,
+               L.ptr(xr), L.ptr(zr), L.stream_handle())
+        return xr, zr
+
+    def count_rank_step(self, xr, x_off_dev, zr, z_off_dev, n_shards, max_nx, max_nz, out,
+                        x_next, key_x, z_next, key_z, out_next):
+        """tw_count_pairs_step on rank-image records (tw_count_pairs_rank_step): the counts of
+        the current partition into `out` (already zero), the next repartition of the records
+        into x_next / z_next and the zeroing of out_next in the same launch."""
+        L.call("tw_count_pairs_rank_step", L.ptr(xr), L.ptr(x_off_dev), L.ptr(zr),
+               L.ptr(z_off_dev), int(n_shards), int(max_nx), int(max_nz), L.ptr(out),
+               int(xr.numel()), L.ptr(x_next), int(key_x), int(zr.numel()), L.ptr(z_next),
+               int(key_z), L.ptr(out_next), int(out_next.numel()) if out_next is not None else 0,
+               L.stream_handle())
+        return out
+
+    def gather_records(self, vals, rec):
+        """The scores in record order (tw_gather_records): out[p] = vals[rec[p] >> 32]."""
+        out = self.t.empty_like(vals)
+        L.call("tw_gather_records", L.ptr(vals), L.ptr(rec), int(rec.numel()), L.ptr(out),
                L.stream_handle())
         return out
 
@@ -498,6 +536,10 @@ class ShardedSample:
                 counts, self.X, self.Z = r
                 return [np.mean(v) for v in self.values(counts)]
         fusable = self.algo == "pairs"
+        if fusable and self._rank_path_ok():
+            r = self._unn_many_rank(keys)
+            if r is not None:
+                return r
         step = None
         if fusable and hasattr(self.ops, "count_step"):
             def step(i, out, Xn, kx, Zn, kz, out_n):
@@ -511,6 +553,39 @@ class ShardedSample:
                                            self.max_nx, self.max_nz, self.dtype, self.pred, out,
                                            Xn, kx, Zn, kz, out_n)
         counts = self._run_steps(keys, lambda i: self.local_counts(), fusable, step)
+        return [np.mean(v) for v in self.values(counts)]
+
+    def _rank_path_ok(self) -> bool:
+        """The all-pairs steps on rank images (csrc/rankimage.hip) apply on one GPU to the
+        strict predicate (SUBGT on doubles is the same predicate; int64 SUBGT wraps and stays
+        on the score compare) with fewer than 2^24 Z-scores."""
+        return (RANK_IMAGES and not self._multi() and self.N > 0 and self.max_nx > 0
+                and self.max_nz > 0 and hasattr(self.ops, "rank_images")
+                and (self.pred == L.TW_PRED_GT
+                     or (self.pred == L.TW_PRED_SUBGT and self.dtype == L.TW_F64))
+                and self.m_loc < (1 << 24) and self.n_loc + self.m_loc < (1 << 31))
+
+    def _unn_many_rank(self, keys):
+        """UnN_many on rank images: ONE ranking of X u Z per call (the multiset of scores is
+        the same at every step), then one launch per step that counts the current partition on
+        packed f32 images and permutes the 8-B records {image, index} for the next step (the
+        same keyed permutations as the score path); the scores are gathered into the final
+        order once at the end.  Same counts, same arrays as the score path."""
+        r = self.ops.rank_images(self.X, self.Z, self.dtype)
+        if r is None:
+            return None
+        X0, Z0 = self.X, self.Z
+        self.X, self.Z = r
+
+        def step(i, out, Xn, kx, Zn, kz, out_n):
+            self.ops.count_rank_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                     self.max_nx, self.max_nz, out, Xn, kx, Zn, kz, out_n)
+        try:
+            counts = self._run_steps(keys, None, False, step)
+        finally:
+            xr, zr = self.X, self.Z
+            self.X = self.ops.gather_records(X0, xr)
+            self.Z = self.ops.gather_records(Z0, zr)
         return [np.mean(v) for v in self.values(counts)]
 
     def UnNT(self, T: int, key0: int = 0) -> np.float64:

@@ -551,9 +551,31 @@ class MultiDeviceSGD:
     def step(self, ix, iz, scores=None):
         if scores is not None:
             raise ValueError("sign_audit runs on one device")
+        t = self.t
+        if not isinstance(ix, t.Tensor):  # host draws: each slot uploads its own rows
+            for sl, e in zip(self.slots, self.subs):
+                with sl:
+                    e.step(ix, iz)
+            self._gather_update()
+            return
+        # device draws live on the caller's device, written on the caller's stream (a
+        # non-blocking upload): each slot orders its stream after it, takes a copy of its rows
+        # on its own device, and the caller's stream waits for those copies before the draw
+        # buffer can be refilled (as run_replay_segment does)
+        caller = t.cuda.current_stream()
+        loc = []
         for sl, e in zip(self.slots, self.subs):
             with sl:
-                e.step(ix, iz)
+                t.cuda.current_stream().wait_stream(caller)
+                a = e.shard_base
+                # copy=True: on a repeated device .to() would return a view of the buffer
+                loc.append((ix[a:a + e.N_loc].to(L.device(), non_blocking=True, copy=True),
+                            iz[a:a + e.N_loc].to(L.device(), non_blocking=True, copy=True)))
+        for sl in self.slots:
+            caller.wait_stream(sl.stream)
+        for sl, e, (lx, lz) in zip(self.slots, self.subs, loc):
+            with sl:
+                e.step(lx, lz, local=True)
         self._gather_update()
 
     def set_shards(self, rows_x, rows_z):
@@ -864,9 +886,9 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                 _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
             eng.run_replay_segment(buf, nxt - i, graphs, tag)
             i = nxt
+    eng.check()  # before the deferred evaluations write their history
     if defer is not None:
         defer.drain()
-    eng.check()
     return None
 
 
@@ -884,6 +906,12 @@ def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer=None
 
 
 def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
+    if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH" and (isinstance(eng, MultiDeviceSGD)
+                                                   or getattr(eng, "G", 1) > 1):
+        # the device-drawn shards exist only as per-slot / per-rank row tables
+        raise ValueError("TYPE_TRAIN_MONITOR='SAME_AS_BATCH' with rng_mode='device' runs on "
+                         "one device and one rank; use rng_mode='replay' (the host formula "
+                         "over the global shards) for several")
     eng.enable_device_rng(int(np.random.randint(0, 2 ** 63 - 1, dtype=np.int64)))
     n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
     if trajectory is not None:
@@ -913,9 +941,9 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
         nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod)
         eng.run_segment(nxt - i, resh, graphs)
         i = nxt
+    eng.check()  # before the deferred evaluations write their history
     if defer is not None:
         defer.drain()
-    eng.check()
     return None
 
 
@@ -926,10 +954,11 @@ class _DeferredEvals:
     (and all of them before learning_process returns).  The loop no longer waits for the device
     at every evaluation; the values are the same bits."""
 
-    def __init__(self, w_dev, w_shape, slots=64):
+    def __init__(self, w_dev, w_shape, slots=64, check=None):
         t = L.torch()
         self.t = t
         self.w_shape = w_shape
+        self.check = check  # the engine's abort-word check, run before any history is written
         self.host = t.empty((slots, 4 + int(w_dev.numel())), dtype=t.float64, pin_memory=True)
         self.events = [t.cuda.Event() for _ in range(slots)]
         self.free = list(range(slots))[::-1]
@@ -949,6 +978,10 @@ class _DeferredEvals:
     def _pop(self):
         i, k, finish = self.pending.pop(0)
         self.events[k].synchronize()
+        if self.check is not None:
+            # a persistent segment that gave up at its grid barrier left w invalid: raise
+            # before its statistics reach p_learn or the log
+            self.check()
         h = self.host[k].numpy()
         finish(i, h[:4].copy(), h[4:].copy().reshape(self.w_shape))
         self.free.append(k)
@@ -964,7 +997,7 @@ def _deferred_evals(eng, graphs, trajectory):
     if (not DEFER_EVALS or not graphs or trajectory is not None
             or TYPE_TRAIN_MONITOR != "FIXED_PAIRS" or getattr(eng, "G", 1) != 1):
         return None
-    return _DeferredEvals(eng.w, eng.w_shape)
+    return _DeferredEvals(eng.w, eng.w_shape, check=eng.check)
 
 
 class _EvalCache:

@@ -102,7 +102,9 @@ def shuffle_pair(X, Z) -> None:
     swaps run.  Arrays the buffer path does not cover (views, object arrays, other RNGs) go
     to np.random.shuffle itself."""
     ix, iz = _shuffle_items(X), _shuffle_items(Z)
-    if ix is None or iz is None or (
+    # aliasing X and Z (the same array or overlapping views): the second shuffle must see the
+    # first one's swaps, which the concurrent native path does not give
+    if ix is None or iz is None or np.shares_memory(X, Z) or (
             _mt_state() is None and np.random.get_state(legacy=True)[0] != "MT19937"):
         np.random.shuffle(X)
         np.random.shuffle(Z)
