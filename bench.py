@@ -5,21 +5,23 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[2] shape, one GPU's share): every rank holds n = 1e6 X-scores
-and 1e6 Z-scores (float64, synthetic N(0.5,1) / N(0,1)) resident in HBM, cut into N = 64
-prop-SWOR shards of 15625 x 15625 pairs.  One step = one block-wise complete U-statistic
-UnN (estimation-experiment/main.py:72-74): a fresh device repartition of BOTH samples (one
-global keyed permutation; at G > 1 one RCCL all-to-all moves every score to its new owner)
-and the exact pair count of all shards in one launch.  The K steps run as est.UnNT's loop
-(ShardedSample.UnN_many): repartition i+1 is issued on a side stream while step i counts,
-and the per-shard counts of all K steps are combined by one RCCL all-reduce and the host's
-np.mean at the end.  Weak scaling: per-GPU work is fixed (1.5625e10 pairs).
+Workload (BASELINE.json configs[2]): n = 1e6 X-scores and 1e6 Z-scores (float64, synthetic
+N(0.5,1) / N(0,1)) resident in HBM, cut into N = 64 prop-SWOR shards of 15625 x 15625 pairs —
+in total over the G ranks (strong scaling, the default: n/G scores per class and 64/G shards
+per rank), or per rank with --scaling weak (the nested `weak_C3` line at G > 1).  One step = one
+block-wise complete U-statistic UnN (estimation-experiment/main.py:72-74): a fresh device
+repartition of BOTH samples (one global keyed permutation; at G > 1 one RCCL all-to-all moves
+every element to its new owner) and the exact pair count of all shards.  The K steps run as
+est.UnNT's loop (ShardedSample.UnN_many): one ranking of X u Z per call (rank images,
+csrc/rankimage.hip), then per step one launch that counts on packed f32 images and carries the
+next repartition (one GPU) or the count beside the exchange on a side stream (several), the
+per-shard counts of all K steps combined by one all-reduce and the host's np.mean at the end.
 
 value = pairs compared by all ranks / max-over-ranks wall time of the K timed steps.
-roofline: the count kernel (k_count_complete, launched as the one-launch step that also
-carries the next repartition), VALU-bound: 1 compare lane-op per pair against the f64
-vector-op peak 3.93e13 lane-op/s (256 CU x 64 lanes x 2.4 GHz); its duration
-is measured live with HIP events on the stream it runs on.
+roofline: the count kernel (k_count_rank, the one-launch step that also carries the next
+repartition), VALU-bound: 1 compared pair = 1 lane-op against the f64 vector lane-op peak
+3.93e13/s (256 CU x 64 lanes x 2.4 GHz); its duration is measured live with
+HIP events on the stream it runs on.
 cpu_baseline: the CPU port of the reference (oracle/oracle.py, identical NumPy operations to
 est.UnN) timed on rank 0 at N=1 on one full UnN of the same configuration.
 """
@@ -85,6 +87,31 @@ class EventPool:
         return timed
 
 
+class Span:
+    """Max-over-ranks wall time of a region: barrier + synchronize on both sides (the driver's
+    timing contract), the slowest rank's seconds all-reduced."""
+
+    def __init__(self, torch, dist, group, barrier):
+        self.torch, self.dist, self.group, self.barrier = torch, dist, group, barrier
+
+    def __call__(self, fn):
+        t = self.torch
+        t.cuda.synchronize()
+        self.barrier()
+        t.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        t.cuda.synchronize()
+        self.barrier()
+        t.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if self.group is not None:
+            tt = t.tensor([dt], dtype=t.float64, device="cuda")
+            self.dist.all_reduce(tt, op=self.dist.ReduceOp.MAX, group=self.group)
+            dt = float(tt.item())
+        return dt, out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -103,6 +130,12 @@ def parse():
     ap.add_argument("--no-sgd", action="store_true", help="skip the SGD steps/s secondary")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the strong-scaling C3 line (n = 1e6/class, 64 shards in total)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="headline at N > 1 GPUs: strong = BASELINE configs[2]'s fixed problem "
+                         "(--n per class and --shards in total over the ranks), weak = --n per "
+                         "class and --shards per rank")
+    ap.add_argument("--no-tradeoff", action="store_true",
+                    help="skip the reshuffle_mod trade-off curve of the learning lines")
     ap.add_argument("--strong-T", type=int, default=4,
                     help="repartitions per estimate of the strong-scaling C3 line (UnNT's T)")
     ap.add_argument("--cpu-inc-shards", type=int, default=16,
@@ -309,54 +342,96 @@ def cpu_baseline_incomplete(n, N, B, shards):
                       f"B={B} randint pairs each), n={n}/class, {dt:.2f} s"}
 
 
-def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="replicated"):
-    """Pairwise-hinge SGD steps/s (BASELINE metric, second half): learning_process's loop
-    (make_exps.py:122-141) without evaluation, device-RNG mode, hipGraph-replayed segments.
-    Synthetic data of the given shape generated on the device.  layout="partitioned" also
-    times one reshuffle's row exchange (route + pack + unpack; at N=1 GPU the all_to_all is
-    the identity, so this is the HBM side of the exchange)."""
+def sgd_data(n_X, n_Z, d):
+    """Synthetic learning rows generated on the device (the same on every rank: one seed)."""
     import torch
-    from tuplewise.learning import SGDEngine
     g = torch.Generator(device="cuda").manual_seed(7)
     X = torch.randn((n_X, d), dtype=torch.float64, device="cuda", generator=g)
     Z = torch.randn((n_Z, d), dtype=torch.float64, device="cuda", generator=g) + 0.3
     w0 = torch.randn((d, 1), dtype=torch.float64, device="cuda", generator=g)
+    return X, Z, w0
+
+
+def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="replicated",
+                    group=None, span=None, data=None, check_prefix=0):
+    """Pairwise-hinge SGD steps/s (BASELINE metric, second half): learning_process's loop
+    (make_exps.py:122-141) without evaluation, device-RNG mode, hipGraph-replayed segments.
+    Synthetic data of the given shape generated on the device.  layout="partitioned" also
+    times one reshuffle's row exchange (route + pack + unpack; at N=1 GPU the all_to_all is
+    the identity, so this is the HBM side of the exchange).  group: the ranks of the run (each
+    owns N/G shards; one all-gather of the shard gradients per step); check_prefix > 0: the
+    first steps' w is compared with a one-rank engine's on rank 0 (bit for bit)."""
+    import torch
+    from tuplewise.learning import SGDEngine
+    X, Z, w0 = data if data is not None else sgd_data(n_X, n_Z, d)
     eng = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
-                    optim_type="momentum", x_layout=layout)
+                    optim_type="momentum", x_layout=layout, group=group)
     eng.enable_device_rng(12345)
 
-    def run(k):
+    def run(e, k):
         i = 0
         while i < k:
             nxt = min(k, (i // reshuffle_mod + 1) * reshuffle_mod)
-            eng.run_segment(nxt - i, i % reshuffle_mod == 0, graphs=True)
+            e.run_segment(nxt - i, i % reshuffle_mod == 0, graphs=True)
             i = nxt
 
-    run(max(warmup * reshuffle_mod, reshuffle_mod))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(steps)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    # warm: the timed schedule itself once (the same segment lengths, so every hipGraph the
+    # timed run replays is captured here), then `warmup` more reshuffle periods
+    run(eng, steps)
+    run(eng, warmup * min(reshuffle_mod, steps))
+    if span is None:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(eng, steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    else:
+        dt, _ = span(lambda: run(eng, steps))
     eng.check()  # a persistent segment that gave up at a barrier invalidates the run
+    same_1rank = None
+    if check_prefix and group is not None:
+        # the trajectory does not depend on G: a fresh engine over the ranks and a one-rank
+        # engine on rank 0, same seed, the same first steps, w compared bit for bit
+        e_g = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
+                        optim_type="momentum", x_layout=layout, group=group)
+        e_g.enable_device_rng(777)
+        run(e_g, check_prefix)
+        w_g = e_g.w_host()
+        if torch.distributed.get_rank(group) == 0:
+            e_1 = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
+                            optim_type="momentum")
+            e_1.enable_device_rng(777)
+            run(e_1, check_prefix)
+            same_1rank = bool(np.array_equal(w_g, e_1.w_host()))
+            del e_1
+        del e_g
     launches = ("one persistent launch per segment" if eng.narrow_seg else
                 "one launch per step" if eng.fused else
                 "one segment kernel per segment" if eng.segment else "gradient + update per step")
+    G = 1 if group is None else torch.distributed.get_world_size(group)
     out = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
            "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
            "gather_GBps": N * B * 16 * d * steps / dt / 1e9,
            "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B,
                       "reshuffle_mod": reshuffle_mod, "optim": "momentum",
                       "rng": "device (Philox)", "graphs": True, "steps": steps,
-                      "x_layout": layout, "launches": launches}}
+                      "x_layout": layout, "launches": launches, "ranks": G}}
+    if same_1rank is not None:
+        out["trajectory_equal_1rank"] = {"steps": check_prefix, "equal": same_1rank}
     if layout == "partitioned":
         reps = 3
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            eng.reshuffle_device()
-        torch.cuda.synchronize()
-        rs = (time.perf_counter() - t0) / reps
+
+        def resh():
+            for _ in range(reps):
+                eng.reshuffle_device()
+        if span is None:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            resh()
+            torch.cuda.synchronize()
+            rs = (time.perf_counter() - t0) / reps
+        else:
+            rs = span(resh)[0] / reps
         rows = N * (eng.kx + eng.kz)
         moved = rows * 8 * (2 * d + 2 * (d + 1))  # pack: read row, write record; unpack: back
         out["reshuffle_exchange"] = {"ms": rs * 1e3, "rows": rows, "bytes": moved,
@@ -364,50 +439,76 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
     return out
 
 
-def sgd_replay_steps_per_s(steps):
-    """learning_process in replay mode (NumPy's own draws, bit-identical to the reference)
-    at the C4 shape, no evaluation: host RNG (one native MT19937 batch per step) + index
-    upload + two kernels per step."""
-    import logging
-    import torch
-    import tuplewise.learning as lr
+def c4_problem():
     rng = np.random.RandomState(3)
     X = np.hstack([rng.normal(size=(9117, 9)), np.ones((9117, 1))])
     Z = np.hstack([rng.normal(0.5, 1, size=(702, 9)), np.ones((702, 1))])
-    p = {"n_it": steps, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": 25, "reg": 0.05,
-         "learning_rate": 0.01, "eval_mod": 10 ** 9, "w_init": rng.normal(size=(10, 1)),
+    return X, Z, rng.normal(size=(10, 1))
+
+
+def sgd_replay_steps_per_s(steps, mod=25, group=None, span=None, runs=3, audit=True):
+    """learning_process in replay mode (NumPy's own draws, bit-identical to the reference)
+    at the C4 shape, no evaluation: host RNG (one native MT19937 batch per segment) + index
+    upload + the persistent segment kernel.  group: every rank makes the full draw sequence
+    and uses its shards (make_exps.py:122-141 over the ranks)."""
+    import logging
+    import torch
+    import tuplewise.learning as lr
+    X, Z, w0 = c4_problem()
+    p = {"n_it": steps, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": mod, "reg": 0.05,
+         "learning_rate": 0.01, "eval_mod": 10 ** 9, "w_init": w0,
          "test_X": X[:10], "test_Z": Z[:10], "train_mon_pairs": [(0, 0)], "train_X": X,
          "train_Z": Z}
     logging.disable(logging.CRITICAL)
     np.random.seed(0)
-    lr.learning_process(X, Z, dict(p, n_it=50))  # warm
-    # host-bound (NumPy-exact draws on the box's shared host cores): the median of 3 runs
-    runs = []
-    for _ in range(3):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        lr.learning_process(X, Z, p)
-        torch.cuda.synchronize()
-        runs.append(time.perf_counter() - t0)
-    dt = float(np.median(runs))
-    # hinge-filter sign audit (SURVEY.md §7), untimed: the device's S against NumPy/BLAS's on
-    # every pair of 300 replay steps of the same run
-    audit = []
+    lr.learning_process(X, Z, dict(p, n_it=50), group=group)  # warm
+    # host-bound (NumPy-exact draws on the box's shared host cores): the median of the runs
+    ts = []
+    for _ in range(runs):
+        if span is None:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            lr.learning_process(X, Z, p, group=group)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        else:
+            ts.append(span(lambda: lr.learning_process(X, Z, p, group=group))[0])
+    dt = float(np.median(ts))
+    out = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
+           "runs_steps_per_s": [steps / r for r in ts],
+           "config": {"n_X": 9117, "n_Z": 702, "d": 10, "N": 100, "B": 100,
+                      "reshuffle_mod": mod, "rng": "replay (NumPy legacy MT19937, bit-exact)",
+                      "steps": steps,
+                      "ranks": 1 if group is None else torch.distributed.get_world_size(group)}}
+    if audit and group is None:
+        # hinge-filter sign audit (SURVEY.md §7), untimed: the device's S against NumPy/BLAS's
+        # on every pair of 300 replay steps of the same run
+        aud = []
+        np.random.seed(0)
+        lr.learning_process(X, Z, dict(p, n_it=300), sign_audit=aud)
+        out["sign_audit"] = {"steps": len(aud), "pairs": sum(a["pairs"] for a in aud),
+                             "near_zero_S": sum(a["near_zero"] for a in aud),
+                             "filter_flips": sum(a["flips"] for a in aud),
+                             "note": "pairs whose |S| is within the dot product's rounding "
+                                     "bound, and pairs whose hinge filter differs from NumPy's"}
+    return out
+
+
+def cpu_port_c4(mod, steps=150):
+    """The reference loop restated with its own NumPy operations (oracle.learning_trajectory:
+    SWR_divide every reshuffle_mod steps, grad_inc_block per shard, momentum update;
+    make_exps.py:122-141 without evaluation), single-threaded, at the C4 shape."""
+    from oracle import oracle as O
+    X, Z, w0 = c4_problem()
+    p = {"n_it": steps, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": mod, "reg": 0.05,
+         "learning_rate": 0.01, "w_init": w0}
     np.random.seed(0)
-    lr.learning_process(X, Z, dict(p, n_it=300), sign_audit=audit)
-    return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
-            "runs_steps_per_s": [steps / r for r in runs],
-            "sign_audit": {"steps": len(audit), "pairs": sum(a["pairs"] for a in audit),
-                           "near_zero_S": sum(a["near_zero"] for a in audit),
-                           "filter_flips": sum(a["flips"] for a in audit),
-                           "note": "pairs whose |S| is within the dot product's rounding bound, "
-                                   "and pairs whose hinge filter differs from NumPy's"},
-            "config": {"n_X": 9117, "n_Z": 702, "d": 10, "N": 100, "B": 100,
-                       "reshuffle_mod": 25, "rng": "replay (NumPy legacy MT19937, bit-exact)",
-                       "steps": steps}}
+    t0 = time.perf_counter()
+    O.learning_trajectory(X, Z, p, capture_every=10 ** 9)
+    return steps / (time.perf_counter() - t0)
 
 
-def learning_end_to_end(steps, rng_mode):
+def learning_end_to_end(steps, rng_mode, group=None, span=None):
     """learning_process at the C4 shape WITH its evaluation every 25 steps (make_exps.py:
     122-141, 143-190): shuttle-shaped synthetic train/test sets, 450k fixed monitor pairs
     (make_exps.py:216-224).  The reference spends ~2.6 ms per step and 158 ms per evaluation
@@ -426,25 +527,30 @@ def learning_end_to_end(steps, rng_mode):
          "test_X": Xe, "test_Z": Ze, "train_mon_pairs": mon, "train_X": X, "train_Z": Z}
     logging.disable(logging.CRITICAL)
     np.random.seed(0)
-    lr.learning_process(X, Z, dict(p, n_it=50), rng_mode=rng_mode)  # warm (captures graphs)
+    lr.learning_process(X, Z, dict(p, n_it=50), rng_mode=rng_mode, group=group)  # warm
     runs = []
     for _ in range(3):  # the median of 3 runs (the replay draws run on shared host cores)
         p["iter"] = []
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        lr.learning_process(X, Z, p, rng_mode=rng_mode)
-        torch.cuda.synchronize()
-        runs.append(time.perf_counter() - t0)
+        if span is None:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            lr.learning_process(X, Z, p, rng_mode=rng_mode)
+            torch.cuda.synchronize()
+            runs.append(time.perf_counter() - t0)
+        else:
+            runs.append(span(lambda: lr.learning_process(X, Z, p, rng_mode=rng_mode,
+                                                         group=group))[0])
     dt = float(np.median(runs))
     return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
             "runs_steps_per_s": [steps / r for r in runs],
             "evaluations": len(p["iter"]),
             "config": {"n_X": 9117, "n_Z": 702, "d": 10, "N": 100, "B": 100,
                        "reshuffle_mod": 25, "eval_mod": 25, "monitor_pairs": 450000,
-                       "test": "2279 x 175", "rng": rng_mode, "steps": steps}}
+                       "test": "2279 x 175", "rng": rng_mode, "steps": steps,
+                       "ranks": 1 if group is None else torch.distributed.get_world_size(group)}}
 
 
-def pmc_traffic():
+def pmc_traffic(kernel="k_count_complete"):
     """HBM bytes per launch of the count kernel from the committed rocprofv3 --pmc summary of
     this workload (profiles/*count_pmc*.json, FETCH_SIZE + WRITE_SIZE): the timed one-launch
     step (count + next repartition) and, when present, a plain count launch."""
@@ -458,7 +564,7 @@ def pmc_traffic():
             e = json.loads(c.read_text())
         except Exception:
             continue
-        if str(e.get("kernel", "")).startswith("k_count_complete"):
+        if str(e.get("kernel", "")).startswith(kernel):
             d = e
             break
     if d is None:
@@ -675,6 +781,67 @@ def strong_c3(args, group, rank, world, barrier, torch, dist):
                            "ms_per_estimate": dt_i / reps * 1e3, "estimate_last": float(est_i)}}
 
 
+RESHUFFLE_MODS = (1, 5, 25, 125, 10000)  # learning-experiment/main.py:20
+
+
+def tradeoff_curve(args, group, span, with_cpu):
+    """The paper's trade-off axis: SGD steps/s for every reshuffle_mod of the reference's sweep
+    (learning-experiment/main.py:20; a reshuffle = a new SWR draw of every shard, make_exps.py:
+    123-125).  C4 (shuttle shape) with device and replay draws; C5 (d = 512, n = 1e7, N = 256,
+    B = 100) with X replicated (a reshuffle is new row tables, no data moves) and row-partitioned
+    (a reshuffle moves every drawn row to its shard's rank: the communication side of the
+    trade-off); the reference loop restated on one CPU core beside the C4 points."""
+    import torch
+    out = {"note": "steps/s per reshuffle_mod (learning-experiment/main.py:20); device = "
+                   "Philox draws + hipGraph segments, replay = NumPy's own MT19937 draws "
+                   "(bit-exact); C5 partitioned: every reshuffle exchanges the drawn rows",
+           "reshuffle_mod": list(RESHUFFLE_MODS)}
+    c4d, c4r, cpu = {}, {}, {}
+    for mod in RESHUFFLE_MODS:
+        c4d[mod] = sgd_steps_per_s(9117, 702, 10, 100, 100, mod, 2000, 1, group=group,
+                                   span=span)["steps_per_s"]
+        c4r[mod] = sgd_replay_steps_per_s(1000, mod, group=group, span=span, runs=1,
+                                          audit=False)["steps_per_s"]
+        if with_cpu:
+            cpu[mod] = cpu_port_c4(mod)
+    out["C4_device"], out["C4_replay"] = c4d, c4r
+    if cpu:
+        out["C4_cpu_port_1core"] = cpu
+    data = sgd_data(C5_N, C5_N, 512)
+    c5r, c5p = {}, {}
+    for mod in RESHUFFLE_MODS:
+        c5r[mod] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, mod, 200, 1, group=group,
+                                   span=span, data=data)["steps_per_s"]
+        # a partitioned reshuffle moves ~n rows (41 GB at G = 1): few steps at mod 1
+        steps_p = 10 if mod == 1 else 50 if mod == 5 else 100
+        c5p[mod] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, mod, steps_p, 1,
+                                   layout="partitioned", group=group, span=span,
+                                   data=data)["steps_per_s"]
+    del data
+    torch.cuda.empty_cache()
+    out["C5_B100_replicated"], out["C5_B100_partitioned"] = c5r, c5p
+    return out
+
+
+def weak_c3(args, group, rank, world, span, torch):
+    """The weak-scaling form of the headline: n = 1e6/class and N = 64 shards PER GPU (the
+    per-GPU work of the one-GPU run), K UnN steps over all ranks."""
+    from tuplewise.device import ShardedSample
+    gen = torch.Generator(device="cuda").manual_seed(3000 + rank)
+    X = torch.randn(N_PER_CLASS, dtype=torch.float64, device="cuda", generator=gen) + 0.5
+    Z = torch.randn(N_PER_CLASS, dtype=torch.float64, device="cuda", generator=gen)
+    S = ShardedSample(X, Z, N_SHARDS, group=group, algo="pairs")
+    S.UnN_many(range(70_000, 70_000 + args.warmup + 1))
+    dt, ests = span(lambda: S.UnN_many(range(args.warmup, args.warmup + args.steps)))
+    k = N_PER_CLASS // N_SHARDS
+    pairs = world * N_SHARDS * k * k * args.steps
+    return {"note": "weak scaling: n=1e6/class and N=64 prop-SWOR shards PER GPU (8e6/class and "
+                    "512 shards at 8 GPUs), one global repartition per step",
+            "scaling": "weak", "value": pairs / dt, "unit": "pairs/s",
+            "ms_per_step": dt / args.steps * 1e3, "n_per_class_per_gpu": N_PER_CLASS,
+            "shards_per_gpu": N_SHARDS, "estimate_last_step": float(ests[-1])}
+
+
 def main():
     args = parse()
     world = resolve_world(args)
@@ -703,13 +870,22 @@ def main():
     import tuplewise  # noqa: F401
     from tuplewise.device import ShardedSample
 
+    # the headline's problem: strong (default) = BASELINE configs[2]'s fixed n per class and
+    # N shards IN TOTAL over the ranks; weak = n and N per rank
+    if args.scaling == "strong":
+        if args.n % world or args.shards % world:
+            sys.stderr.write(f"bench.py: n={args.n}, N={args.shards} do not split over {world} "
+                             "ranks\n")
+            sys.exit(2)
+        n, shards = args.n // world, args.shards // world
+    else:
+        n, shards = args.n, args.shards
     gen = torch.Generator(device="cuda").manual_seed(1000 + rank)
-    n = args.n
     X = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) + 0.5
     Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
-    S = ShardedSample(X, Z, args.shards, group=group, algo="pairs")
-    k = n // args.shards
-    pairs_per_step_rank = args.shards * k * k
+    S = ShardedSample(X, Z, shards, group=group, algo="pairs")
+    k = n // shards
+    pairs_per_step_rank = shards * k * k
 
     # live kernel timing: HIP events on the stream the C ABI launches on (torch's current
     # stream), created before the timed regions (creating them inside the loop stalled the
@@ -720,6 +896,9 @@ def main():
     ops.count = kernel_ms.wrap(ops.count)
     ops.count_step = kernel_ms.wrap(ops.count_step)  # count + next repartition on spare blocks
     ops.count_rank_step = kernel_ms.wrap(ops.count_rank_step)  # the same on rank images
+    rank_ms = EventPool(torch, 8)  # the once-per-call ranking of X u Z (tw_rank_images)
+    ops.rank_images = rank_ms.wrap(ops.rank_images)
+    rank_path = S._rank_path_ok()
     ops.count_sorted_step = kernel_ms.wrap(ops.count_sorted_step)  # sorted count + next
     ops.count_sorted_steps = kernel_ms.wrap(ops.count_sorted_steps)  # all K sorted steps
 
@@ -729,6 +908,8 @@ def main():
                 dist.barrier(device_ids=[local])
             else:
                 dist.barrier()
+
+    span = Span(torch, dist, group, barrier)
 
     # settle: untimed steps for >= settle_ms so the timed steps run at the steady-state clock
     # (the chip raises its clock over the first ~10 ms of load; measured 3 % on this step)
@@ -749,6 +930,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    X_start, Z_start = S.X.clone(), S.Z.clone()  # the score-kernel line replays the same steps
     kernel_ms.clear(sample)
     t0 = time.perf_counter()
     # K UnN steps (est.UnNT's loop): repartition i+1 overlaps the counts of step i
@@ -763,6 +945,36 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()] or [float("nan")]))
+    rank_call_ms = float(np.mean([a.elapsed_time(b) for a, b in rank_ms.used()] or [0.0]))
+
+    # the same steps with the score-compare kernel (csrc/count.hip: v_cmp_f64 + VALU/SALU
+    # counting), for comparison: identical estimates
+    score_line = None
+    if rank_path:
+        from tuplewise import device as Dv
+        Dv.RANK_IMAGES = False
+        try:
+            S.UnN_many(range(60_000, 60_000 + args.warmup))
+            S.X, S.Z = X_start, Z_start
+            torch.cuda.synchronize()
+            barrier()
+            kernel_ms.clear(sample)
+            t5 = time.perf_counter()
+            ests_score = S.UnN_many(range(args.warmup, args.warmup + args.steps))
+            torch.cuda.synchronize()
+            barrier()
+            dt_score = time.perf_counter() - t5
+            kms_score = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
+        finally:
+            Dv.RANK_IMAGES = True
+        score_line = {
+            "note": "the same K steps (same keys, same estimates) with the score-compare kernel "
+                    "k_count_complete (csrc/count.hip): one v_cmp_f64 per 64 pairs, counted "
+                    "half on the VALU (carry-add) and half on the scalar unit (s_bcnt1)",
+            "value": pairs_per_step_rank * world * args.steps / dt_score, "unit": "pairs/s",
+            "ms_per_step": dt_score / args.steps * 1e3, "kernel_ms": kms_score,
+            "frac": pairs_per_step_rank / (kms_score * 1e-3) / PEAK_LANE_OPS,
+            "same_estimates": bool(ests_score == ests)}
 
     # same workload, exact sort + binary-search count (csrc/rankcount.hip): logical pairs/s
     same_counts = bool(torch.equal(S.local_counts(), (setattr(S, "algo", "sorted"),
@@ -807,8 +1019,8 @@ def main():
     kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
     ops.count_rng = ops.count_rng.__wrapped__
     ops.count_rng_step = ops.count_rng_step.__wrapped__
-    inc_pairs_rank = args.shards * B_inc
-    inc_replay = incomplete_replay(X, Z, args.shards, B_inc)
+    inc_pairs_rank = shards * B_inc
+    inc_replay = incomplete_replay(X, Z, shards, B_inc)
     strong = None if args.no_strong else strong_c3(args, group, rank, world, barrier, torch, dist)
 
     # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
@@ -846,13 +1058,14 @@ def main():
     # the T repetitions), n = 1000/class, N = 10, T = 4; the reference restated on the CPU
     c1 = plumbing_C1(rank == 0 and world == 1 and not args.no_cpu_baseline)
 
-    traffic, traffic_plain = pmc_traffic()
+    count_kernel = "k_count_rank" if rank_path else "k_count_complete"
+    traffic, traffic_plain = pmc_traffic(count_kernel)
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
     achieved = pairs_per_step_rank / (kms * 1e-3)  # lane-ops/s, 1 compare per pair (strict)
     out = {
         "metric": "pair comparisons/sec (node) for sharded AUC U-stat at n=1e6/class (UnN, "
-                  "N=64 prop-SWOR shards per GPU, device repartition each step)",
+                  "N=64 prop-SWOR shards, device repartition each step)",
         "value": value,
         "unit": "pairs/s",
         "n_gpus": world,
@@ -861,13 +1074,16 @@ def main():
         "settle_ms": args.settle_ms,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: X~N(0.5,1), Z~N(0,1) float64 scores generated on the device",
         "config": {"workload": "UnN sharded complete AUC U-statistic (estimation-experiment/"
-                               "main.py:72-74) + device repartition per step",
-                   "n_per_class_per_gpu": n, "shards_per_gpu": args.shards,
+                               "main.py:72-74) + device repartition per step, K steps as "
+                               "est.UnNT's loop (BASELINE configs[2])",
+                   "n_per_class_total": n * world if args.scaling == "weak" else args.n,
+                   "shards_total": shards * world,
+                   "n_per_class_per_gpu": n, "shards_per_gpu": shards,
                    "pairs_per_step_per_gpu": pairs_per_step_rank,
                    "parallelism": (f"dp{world}: shards over ranks, "
                                    + ("RCCL" if os.environ.get("TW_BENCH_BACKEND", "nccl")
@@ -876,16 +1092,24 @@ def main():
                                    if world > 1 else
                                    "dp1: one GPU, device Feistel repartition fused into the "
                                    "count launch")},
-        "roofline": {"bound": "valu", "kernel": "k_count_complete",
+        "roofline": {"bound": "valu", "kernel": count_kernel,
                      "achieved": achieved / 1e12, "peak": PEAK_LANE_OPS / 1e12,
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
                      "count_kernel_ms": kms, "traffic": traffic,
                      "traffic_count_only": traffic_plain,
-                     "note": "1 v_cmp_f64 lane-op per pair; the timed launch also carries the "
-                             "next repartition on its tail blocks (tw_count_pairs_step); "
-                             "traffic = HBM bytes/launch (FETCH_SIZE+WRITE_SIZE) from the "
-                             "committed rocprofv3 --pmc summary: the timed launch, and a plain "
-                             "count launch (algorithmic: 16 MB of scores)"},
+                     "ranking_ms_per_call": rank_call_ms if rank_path else None,
+                     "note": ("1 compared pair = 1 lane-op of the contract (f64 vector "
+                              "lane-op peak); k_count_rank compares packed f32 rank images of "
+                              "the scores (two pairs per lane per instruction: a clamped "
+                              "v_pk_add_f32 and an accumulating one; csrc/rankimage.hip), "
+                              "exact by construction; the ranking of X u Z runs once per "
+                              "UnN_many call inside the timed region (ranking_ms_per_call) "
+                              if rank_path else "1 v_cmp_f64 lane-op per pair; ")
+                             + "the timed launch also carries the next repartition on its tail "
+                               "blocks; traffic = HBM bytes/launch (FETCH_SIZE+WRITE_SIZE) from "
+                               "the committed rocprofv3 --pmc summary of this kernel: the timed "
+                               "launch, and a launch without the repartition"},
+        "score_compare_kernel": score_line,
         "estimate_last_step": float(est),
         "plumbing_C1": c1,
         "single_shard_C2": single,
@@ -930,33 +1154,56 @@ def main():
         "incomplete_replay": inc_replay,
         "strong_C3": strong,
     }
-    if world == 1 and not args.no_sgd:
-        # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5'
-        out["secondary"] = {
+    if world > 1:
+        # the weak-scaling form of the headline (per-GPU work of the one-GPU run)
+        out["weak_C3"] = weak_c3(args, group, rank, world, span, torch)
+    if not args.no_sgd:
+        # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5';
+        # at G > 1 every line runs over the ranks (shards split, one all-gather of the shard
+        # gradients per step; SGDEngine(group=)), C4/C5 checked against a one-rank run
+        chk = 20 if world > 1 else 0
+        g = group
+        sec = {
             "metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)",
-            "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2),
-            "C4_shuttle_shape_replay": sgd_replay_steps_per_s(2000),
-            "C4_end_to_end_with_evaluation_replay": learning_end_to_end(2000, "replay"),
-            "C4_end_to_end_with_evaluation_device": learning_end_to_end(2000, "device"),
-            "C5_scaled_d512": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2),
-            "C5_scaled_d512_B4096": sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1),
-            "C5_scaled_d512_complete_gradient": sgd_complete_steps_per_s(C5_N, C5_N, 512,
-                                                                          256, 3),
-            "C5_scaled_d512_complete_gradient_logistic": sgd_complete_steps_per_s(
-                C5_N, C5_N, 512, 256, 2, loss="logistic"),
-            "C5_scaled_d512_partitioned": sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,
-                                                          1, layout="partitioned"),
+            "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2, group=g,
+                                                span=span, check_prefix=chk),
+            "C4_shuttle_shape_partitioned": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 2000,
+                                                            2, layout="partitioned", group=g,
+                                                            span=span, check_prefix=chk),
+            "C4_shuttle_shape_replay": sgd_replay_steps_per_s(2000, group=g, span=span),
+            "C4_end_to_end_with_evaluation_replay": learning_end_to_end(2000, "replay", g, span),
+            "C4_end_to_end_with_evaluation_device": learning_end_to_end(2000, "device", g, span),
         }
+        c5 = sgd_data(C5_N, C5_N, 512)
+        sec["C5_scaled_d512"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2, group=g,
+                                                span=span, data=c5, check_prefix=chk)
+        sec["C5_scaled_d512_B4096"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1,
+                                                      group=g, span=span, data=c5)
+        sec["C5_scaled_d512_partitioned"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,
+                                                            1, layout="partitioned", group=g,
+                                                            span=span, data=c5,
+                                                            check_prefix=chk)
+        del c5
+        torch.cuda.empty_cache()
+        if world == 1:  # one-GPU extensions (north_star item (2)): the complete-block gradient
+            sec["C5_scaled_d512_complete_gradient"] = sgd_complete_steps_per_s(
+                C5_N, C5_N, 512, 256, 3)
+            sec["C5_scaled_d512_complete_gradient_logistic"] = sgd_complete_steps_per_s(
+                C5_N, C5_N, 512, 256, 2, loss="logistic")
+        out["secondary"] = sec
+        if not args.no_tradeoff:
+            out["tradeoff_reshuffle_mod"] = tradeoff_curve(
+                args, group, span, rank == 0 and world == 1 and not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.shards, args.cpu_shards)
+        out["cpu_baseline"] = cpu_baseline(n, shards, args.cpu_shards)
         # the box's CPU share is 16 cores per GPU (os.cpu_count() and the affinity mask show
         # the whole machine): the all-cores figure uses that share, and says so
         share = min(16, len(os.sched_getaffinity(0)))
-        allc = cpu_baseline_all_cores(n, args.shards, share)
+        allc = cpu_baseline_all_cores(n, shards, share)
         allc["label"] = (f"{share} of {len(os.sched_getaffinity(0))} host cores (the GPU box's "
                          f"CPU share per GPU)")
         out["cpu_baseline"]["all_cores"] = allc
-        out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, args.shards, B_inc,
+        out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, shards, B_inc,
                                                                     args.cpu_inc_shards)
     if rank == 0 and world == 1:
         d3 = drop_in_C3()

@@ -227,6 +227,32 @@ def main():
     np.random.shuffle(perm)
     put("rng/shuffle50_seed9", perm)
 
+    # ------------------------- 5c. learning at the reference's own shape and reshuffle sweep
+    # p_learn defaults of make_exps.py:210-214 (N = 100, B = 100, margin 1, reg 0.05, lr 0.01,
+    # eval_mod 25) on shuttle-shaped synthetic rows (9117 x 10 / 702 x 10 train, 2279 x 10 /
+    # 175 x 10 test: the sizes the `~ind` split gives on ODDS shuttle), at the
+    # two ends of the paper's reshuffle sweep (learning-experiment/main.py:20): reshuffle_mod 1
+    # (a new SWR draw before every step) and 10000 (one draw for the whole run).  The rows come
+    # from the in-repo generator tests/golden/shapes.py (seeded legacy RandomState), so only
+    # the trajectories and the evaluation lists are stored.
+    from shapes import shuttle_problem
+    sx, sz, stx, stz, sw0, smon = shuttle_problem()
+    for mod in (1, 10000):
+        p_sh = {"n_it": 250, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": mod,
+                "reg": 0.05, "learning_rate": 0.01, "eval_mod": 25, "w_init": sw0,
+                "test_X": stx, "test_Z": stz, "train_mon_pairs": smon, "train_X": sx,
+                "train_Z": sz}
+        captured = []
+        cs.grad_inc_block = hook
+        np.random.seed(3000 + mod)
+        me.learning_process(sx, sz, p_sh)
+        cs.grad_inc_block = orig
+        put(f"shuttle_mod{mod}/ws", np.stack(captured))
+        for k in ("iter", "norm_w", "bc_AUC", "br_AUC", "tr_AUC", "tc_AUC"):
+            put(f"shuttle_mod{mod}/{k}", np.array(p_sh[k]))
+        meta[f"shuttle_mod{mod}"] = {"seed": 3000 + mod, "n_it": 250, "N": 100, "B": 100,
+                                     "reshuffle_mod": mod, "eval_mod": 25}
+
     np.savez_compressed(OUT / "golden.npz", **arrays)
     (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1, default=float))
     print(f"wrote {len(arrays)} arrays to {OUT / 'golden.npz'}")

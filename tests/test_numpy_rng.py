@@ -157,6 +157,29 @@ def test_shuffle_pair_views_fall_back_to_numpy(tw):
     assert np.array_equal(X, Xr) and np.array_equal(Z, Zr)
 
 
+@pytest.mark.parametrize("alias", ["same", "overlap"])
+def test_shuffle_pair_aliased_samples(tw, alias):
+    """X and Z sharing memory (the same array, or overlapping contiguous views): the second
+    shuffle sees the first one's swaps, exactly as two np.random.shuffle calls in turn — the
+    concurrent native path is not taken."""
+    from tuplewise.numpy_rng import shuffle_pair
+    for n in (1000, 70_000):  # below and above the two-thread size
+        base = np.random.RandomState(n).normal(size=2 * n)
+        ref = base.copy()
+        if alias == "same":
+            X, Z, Xr, Zr = base, base, ref, ref
+        else:
+            X, Z, Xr, Zr = base[:n + n // 2], base[n // 2:], ref[:n + n // 2], ref[n // 2:]
+        np.random.seed(8)
+        np.random.shuffle(Xr)
+        np.random.shuffle(Zr)
+        want = np.random.randint(0, 2 ** 31, 4)
+        np.random.seed(8)
+        shuffle_pair(X, Z)
+        assert np.array_equal(base, ref)
+        assert np.array_equal(np.random.randint(0, 2 ** 31, 4), want)
+
+
 def _apply_swaps(a, j):
     """_shuffle_raw's swaps (i = n-1 down to 1: swap a[i], a[j[i]]) in plain Python."""
     for i in range(len(a) - 1, 0, -1):

@@ -196,3 +196,18 @@ def test_complete_gradient_factorisation():
                    for e in np.eye(5)])
     np.testing.assert_allclose(O.grad_complete_block(w, 0.4, "logistic")(X, Z).ravel(), fd,
                                rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("mod", [1, 10000])
+def test_learning_trajectory_reference_shape(golden, mod):
+    """The reference's own p_learn shape (make_exps.py:210-214: N = 100, B = 100) on the
+    shuttle-shaped rows of tests/golden/shapes.py at both ends of the reshuffle sweep
+    (learning-experiment/main.py:20): the oracle's loop reproduces the reference's w at every
+    step bit for bit."""
+    from golden.shapes import shuttle_problem
+    X, Z, _, _, w0, _ = shuttle_problem()
+    p = {"n_it": 250, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": mod, "reg": 0.05,
+         "learning_rate": 0.01, "w_init": w0}
+    np.random.seed(3000 + mod)
+    ws, _ = O.learning_trajectory(X, Z, p)
+    assert np.array_equal(np.stack(ws), golden[f"shuttle_mod{mod}/ws"])

@@ -4,6 +4,7 @@
 set -e
 export TMPDIR=/tmp
 R=${1:-r01}
+K=${2:-k_count_rank}  # the count kernel of the bench's timed steps
 B="python3 bench.py --steps 5 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-sgd"
 O=gpurun_out/pmc_$R
 mkdir -p $O
@@ -12,4 +13,4 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/p1 -o r
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/p2 -o run -- $B > $O.p2.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_SMEM --output-format csv -d $O/p3 -o run -- $B > $O.p3.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU --output-format csv -d $O/p4 -o run -- $B > $O.p4.log 2>&1
-python3 tools/pmc_summary.py $O/count_pmc.json k_count_complete $O/p1 $O/p2 $O/p3 $O/p4
+python3 tools/pmc_summary.py $O/count_pmc.json $K $O/p1 $O/p2 $O/p3 $O/p4

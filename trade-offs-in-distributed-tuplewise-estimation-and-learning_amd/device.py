@@ -163,7 +163,7 @@ class HipOps:
 
     def gather_records(self, vals, rec):
         """The scores in record order (tw_gather_records): out[p] = vals[rec[p] >> 32]."""
-        out = self.t.empty_like(vals)
+        out = self.t.empty(rec.shape, dtype=vals.dtype, device=rec.device)
         L.call("tw_gather_records", L.ptr(vals), L.ptr(rec), int(rec.numel()), L.ptr(out),
                L.stream_handle())
         return out
@@ -437,7 +437,7 @@ class ShardedSample:
             self.repartition(key)
         return np.mean(self.values(self.global_counts(self.local_counts())))
 
-    def _run_steps(self, keys, count_local, fusable, step=None):
+    def _run_steps(self, keys, count_local, fusable, step=None, count_into=None):
         """One repartition + one count of all local shards per key, with no host round trip
         per step; returns the (T, G*N) device counts in global shard order (one all-reduce).
         One GPU and a one-launch step (step(i, out, X_next, key_x, Z_next, key_z, out_next):
@@ -446,7 +446,8 @@ class ShardedSample:
         for step i+1.  Several GPUs: repartition i+1 (pack kernels, the split-size copy, the
         RCCL all-to-all) is issued on a side stream while the counts of step i run.
         count_local(i) enqueues step i's count on the current stream; fusable: the all-pairs
-        count (its multi-GPU launches accumulate into one zeroed buffer)."""
+        count (its multi-GPU launches accumulate into one zeroed buffer) — count_into(out) its
+        launch into a zeroed row (default: tw_count_pairs_step without a next step)."""
         t = self.t
         local = []
         if not self._multi() and step is not None:
@@ -489,16 +490,19 @@ class ShardedSample:
             # all-pairs counts go into one buffer zeroed up front: one count launch per step
             # on main, no per-step fill kernel between the counts
             pre = None
-            if fusable and hasattr(self.ops, "count_step"):
+            if count_into is None and fusable and hasattr(self.ops, "count_step"):
+                def count_into(row):
+                    self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                        self.max_nx, self.max_nz, self.dtype, self.pred, row,
+                                        None, 0, None, 0, None)
+            if count_into is not None:
                 pre = t.zeros((len(keys), self.N), dtype=t.int64, device=self.X.device)
             side.wait_stream(main)
             repartition_on_side(keys[0])
             for i in range(len(keys)):
                 main.wait_stream(side)  # repartition i (only it is queued on side so far)
                 if pre is not None:
-                    self.ops.count_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
-                                        self.max_nx, self.max_nz, self.dtype, self.pred, pre[i],
-                                        None, 0, None, 0, None)
+                    count_into(pre[i])
                     local.append(pre[i])
                 else:
                     local.append(count_local(i))
@@ -556,14 +560,15 @@ class ShardedSample:
         return [np.mean(v) for v in self.values(counts)]
 
     def _rank_path_ok(self) -> bool:
-        """The all-pairs steps on rank images (csrc/rankimage.hip) apply on one GPU to the
-        strict predicate (SUBGT on doubles is the same predicate; int64 SUBGT wraps and stays
-        on the score compare) with fewer than 2^24 Z-scores."""
-        return (RANK_IMAGES and not self._multi() and self.N > 0 and self.max_nx > 0
+        """The all-pairs steps on rank images (csrc/rankimage.hip) apply to the strict
+        predicate (SUBGT on doubles is the same predicate; int64 SUBGT wraps and stays on the
+        score compare) with fewer than 2^24 Z-scores in all."""
+        G = self.G
+        return (RANK_IMAGES and self.N > 0 and self.max_nx > 0
                 and self.max_nz > 0 and hasattr(self.ops, "rank_images")
                 and (self.pred == L.TW_PRED_GT
                      or (self.pred == L.TW_PRED_SUBGT and self.dtype == L.TW_F64))
-                and self.m_loc < (1 << 24) and self.n_loc + self.m_loc < (1 << 31))
+                and G * self.m_loc < (1 << 24) and G * (self.n_loc + self.m_loc) < (1 << 31))
 
     def _unn_many_rank(self, keys):
         """UnN_many on rank images: ONE ranking of X u Z per call (the multiset of scores is
@@ -571,22 +576,47 @@ class ShardedSample:
         packed f32 images and permutes the 8-B records {image, index} for the next step (the
         same keyed permutations as the score path); the scores are gathered into the final
         order once at the end.  Same counts, same arrays as the score path."""
-        r = self.ops.rank_images(self.X, self.Z, self.dtype)
-        if r is None:
-            return None
-        X0, Z0 = self.X, self.Z
-        self.X, self.Z = r
+        if self.G > 1:
+            # several ranks: every rank ranks the WHOLE sample (one all-gather of both samples
+            # per call), keeps its own elements' records — whose high words are then global
+            # indices — and the exchanges move 8-B records as they moved scores
+            X0, Z0 = self._all_gather(self.X), self._all_gather(self.Z)
+            r = self.ops.rank_images(X0, Z0, self.dtype)
+            if r is None:
+                return None
+            a, b = self.rank * self.n_loc, self.rank * self.m_loc
+            self.X, self.Z = r[0][a:a + self.n_loc].clone(), r[1][b:b + self.m_loc].clone()
+        else:
+            r = self.ops.rank_images(self.X, self.Z, self.dtype)
+            if r is None:
+                return None
+            X0, Z0 = self.X, self.Z
+            self.X, self.Z = r
 
         def step(i, out, Xn, kx, Zn, kz, out_n):
             self.ops.count_rank_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
                                      self.max_nx, self.max_nz, out, Xn, kx, Zn, kz, out_n)
+
+        def count_into(row):
+            self.ops.count_rank_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                     self.max_nx, self.max_nz, row, None, 0, None, 0, None)
         try:
-            counts = self._run_steps(keys, None, False, step)
+            counts = self._run_steps(keys, None, True, step, count_into)
         finally:
             xr, zr = self.X, self.Z
             self.X = self.ops.gather_records(X0, xr)
             self.Z = self.ops.gather_records(Z0, zr)
         return [np.mean(v) for v in self.values(counts)]
+
+    def _all_gather(self, A):
+        """The G ranks' local arrays concatenated in rank order (one collective)."""
+        t, dist = self.t, self.dist
+        out = t.empty((self.G * A.numel(),), dtype=A.dtype, device=A.device)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, A.contiguous(), group=self.group)
+        else:
+            dist.all_gather(list(out.chunk(self.G)), A.contiguous(), group=self.group)
+        return out
 
     def UnNT(self, T: int, key0: int = 0) -> np.float64:
         """T repartitions, averaged (est.UnNT, estimation-experiment/main.py:76-79)."""
