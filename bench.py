@@ -134,6 +134,9 @@ def parse():
                     help="headline at N > 1 GPUs: strong = BASELINE configs[2]'s fixed problem "
                          "(--n per class and --shards in total over the ranks), weak = --n per "
                          "class and --shards per rank")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the C5 learning lines (41 GB of rows per rank; for gloo "
+                         "rehearsals, where every exchange is staged through host memory)")
     ap.add_argument("--no-tradeoff", action="store_true",
                     help="skip the reshuffle_mod trade-off curve of the learning lines")
     ap.add_argument("--strong-T", type=int, default=4,
@@ -807,6 +810,8 @@ def tradeoff_curve(args, group, span, with_cpu):
     out["C4_device"], out["C4_replay"] = c4d, c4r
     if cpu:
         out["C4_cpu_port_1core"] = cpu
+    if args.no_c5:
+        return out
     data = sgd_data(C5_N, C5_N, 512)
     c5r, c5p = {}, {}
     for mod in RESHUFFLE_MODS:
@@ -845,6 +850,10 @@ def weak_c3(args, group, rank, world, span, torch):
 def main():
     args = parse()
     world = resolve_world(args)
+    if args.scaling == "strong" and (args.n % world or args.shards % world):
+        sys.stderr.write(f"bench.py: n={args.n}, N={args.shards} do not split over {world} ranks "
+                         "(strong scaling; --scaling weak runs them per rank)\n")
+        sys.exit(2)
     if world > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(world))
     import torch
@@ -873,10 +882,6 @@ def main():
     # the headline's problem: strong (default) = BASELINE configs[2]'s fixed n per class and
     # N shards IN TOTAL over the ranks; weak = n and N per rank
     if args.scaling == "strong":
-        if args.n % world or args.shards % world:
-            sys.stderr.write(f"bench.py: n={args.n}, N={args.shards} do not split over {world} "
-                             "ranks\n")
-            sys.exit(2)
         n, shards = args.n // world, args.shards // world
     else:
         n, shards = args.n, args.shards
@@ -932,6 +937,7 @@ def main():
     torch.cuda.synchronize()
     X_start, Z_start = S.X.clone(), S.Z.clone()  # the score-kernel line replays the same steps
     kernel_ms.clear(sample)
+    rank_ms.clear()
     t0 = time.perf_counter()
     # K UnN steps (est.UnNT's loop): repartition i+1 overlaps the counts of step i
     ests = S.UnN_many(range(args.warmup, args.warmup + args.steps))
@@ -1174,18 +1180,20 @@ def main():
             "C4_end_to_end_with_evaluation_replay": learning_end_to_end(2000, "replay", g, span),
             "C4_end_to_end_with_evaluation_device": learning_end_to_end(2000, "device", g, span),
         }
-        c5 = sgd_data(C5_N, C5_N, 512)
-        sec["C5_scaled_d512"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2, group=g,
-                                                span=span, data=c5, check_prefix=chk)
-        sec["C5_scaled_d512_B4096"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100, 1,
-                                                      group=g, span=span, data=c5)
-        sec["C5_scaled_d512_partitioned"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 100,
-                                                            1, layout="partitioned", group=g,
-                                                            span=span, data=c5,
-                                                            check_prefix=chk)
-        del c5
-        torch.cuda.empty_cache()
-        if world == 1:  # one-GPU extensions (north_star item (2)): the complete-block gradient
+        c5 = None if args.no_c5 else sgd_data(C5_N, C5_N, 512)
+        if c5 is not None:
+            sec["C5_scaled_d512"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2,
+                                                    group=g, span=span, data=c5,
+                                                    check_prefix=chk)
+            sec["C5_scaled_d512_B4096"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 4096, 25, 100,
+                                                          1, group=g, span=span, data=c5)
+            sec["C5_scaled_d512_partitioned"] = sgd_steps_per_s(
+                C5_N, C5_N, 512, 256, 100, 25, 100, 1, layout="partitioned", group=g,
+                span=span, data=c5, check_prefix=chk)
+            del c5
+            torch.cuda.empty_cache()
+        if world == 1 and not args.no_c5:
+            # one-GPU extensions (north_star item (2)): the complete-block gradient
             sec["C5_scaled_d512_complete_gradient"] = sgd_complete_steps_per_s(
                 C5_N, C5_N, 512, 256, 3)
             sec["C5_scaled_d512_complete_gradient_logistic"] = sgd_complete_steps_per_s(

@@ -69,3 +69,12 @@ def test_bench_rejects_mismatched_world():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_strong_split_checked_before_any_rank_starts():
+    """The strong-scaling headline cuts n per class and the 64 shards over the ranks: a world
+    size that does not divide them is refused up front (exit 2), before ranks are spawned."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3"],
+                       env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"},
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "do not split over 3 ranks" in r.stderr
