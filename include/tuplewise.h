@@ -106,10 +106,11 @@ int tw_count_set_plan(int32_t R, int64_t z_chunk);
 /* ---- A1/A6/A7 on rank images (round 3, csrc/rankimage.hip): the all-pairs count of
  * est.UnN / UnNT (estimation-experiment/main.py:29-31, :72-79) on packed f32 images.
  * tw_rank_images gives every score an 8-B record {low word: f32 image, high word: its index in
- * d_x / d_z}: x image = #{z < x}, z image = -(its position among the stably sorted z), so that
- * for any pair x > z <=> x_image + z_image >= 1, NaN and -0 == +0 included (strict predicate,
- * float64 or int64 scores; int64 SUBGT / half ties stay on tw_count_pairs).  One stable radix
- * sort of X u Z per call; needs n_z < 2^24 (tw_rank_images_work_bytes returns -1 otherwise).
+ * d_x / d_z}: image g(v) = #{z in d_z : z < v} (x: g, z: -g; a NaN x: -2^25), so that for any
+ * pair x > z <=> x_image + z_image >= 1, NaN and -0 == +0 included (strict predicate, float64
+ * or int64 scores; int64 SUBGT / half ties stay on tw_count_pairs).  One bucketed ranking of
+ * X u Z per call (sampled splitters, per-bucket LDS sorts of the z keys); needs n_z < 2^24
+ * (tw_rank_images_work_bytes returns -1 otherwise).
  * d_work: device scratch of tw_rank_images_work_bytes(n_x, n_z) bytes. */
 int64_t tw_rank_images_work_bytes(int64_t n_x, int64_t n_z);
 int tw_rank_images(const void* d_x, int64_t n_x, const void* d_z, int64_t n_z, int32_t dtype,
@@ -586,6 +587,15 @@ int tw_allgather_u64(int32_t comm, const uint64_t* const* d_send, uint64_t* cons
                      int64_t count, void* const* streams);
 int tw_allgather_f64(int32_t comm, const double* const* d_send, double* const* d_recv,
                      int64_t count, void* const* streams);
+/* Failure detection (the one entry point here that waits): block until the
+ * collectives enqueued on streams[k] (one per device of the communicator) complete, polling
+ * ncclCommGetAsyncError on every device's communicator; an RCCL error, a failed stream or
+ * timeout_ms (<= 0: the tw_comm_set_timeout default, 60 s) aborts the communicator
+ * (ncclCommAbort) and returns TW_ERR_HIP — later calls on the handle fail at once, and the
+ * caller gathers on the host instead.  Replaces the wait the reference never needed: its
+ * workers are a serial loop (compute_stats.py:71-92). */
+int tw_comm_wait(int32_t comm, void* const* streams, int64_t timeout_ms);
+int tw_comm_set_timeout(int64_t ms);
 
 /* ---- f2: bulk draws of NumPy's legacy global RNG (host code, no GPU) ------------------
  * key (624 words) / pos: the MT19937 state of np.random.get_state(), advanced in place.

@@ -375,18 +375,15 @@ def order_keys(v) -> np.ndarray:
 
 def rank_records(X, Z):
     """Restates csrc/rankimage.hip tw_rank_images (the round-3 all-pairs count on packed f32
-    images; not a reference function): sort X u Z stably by order key, x before z; an
-    element's image is the number of z sorted before it (NaN x: -2^25); z images are stored
-    negated.  Records: low word the f32 image bits, high word the element's index.  For every
-    pair, X_i > Z_j  <=>  x_image + z_image >= 1."""
+    images; not a reference function): every element's image is the number of Z-scores whose
+    order key is below its own, g(v) = #{z : key(z) < key(v)} (NaN x: -2^25); z images are
+    stored negated.  Records: low word the f32 image bits, high word the element's index.  For
+    every pair, X_i > Z_j  <=>  x_image + z_image >= 1."""
     X, Z = np.asarray(X).reshape(-1), np.asarray(Z).reshape(-1)
     n, m = X.size, Z.size
-    keys = np.concatenate([order_keys(X), order_keys(Z)])
-    order = np.argsort(keys, kind="stable")
-    isz = (order >= n).astype(np.int64)
-    img = np.empty(n + m, np.float32)
-    img[order] = (np.cumsum(isz) - isz).astype(np.float32)
-    gx, gz = img[:n].copy(), img[n:]
+    zk = np.sort(order_keys(Z))
+    gx = np.searchsorted(zk, order_keys(X), side="left").astype(np.float32)
+    gz = np.searchsorted(zk, order_keys(Z), side="left").astype(np.float32)
     if X.dtype != np.int64:
         gx[np.isnan(X)] = np.float32(-2.0 ** 25)
     xr = gx.view(np.uint32).astype(np.uint64) | (np.arange(n, dtype=np.uint64) << np.uint64(32))

@@ -1,0 +1,62 @@
+"""RCCL failure detection of the single-process communicator (csrc/comm.hip) on
+CPU: a stub library (tests/native/rccl_stub.cpp, bound through TW_RCCL_LIB) reports a failed
+peer or a collective that never completes; tw_comm_wait must return an error instead of
+hanging, abort every device's communicator, and leave the handle dead for later calls.  Each
+case runs in a fresh process (the library binds RCCL once per process)."""
+import ctypes
+import json
+import os
+import pathlib
+import subprocess
+import sys
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+_CHILD = r"""
+import ctypes, json, sys
+sys.path.insert(0, sys.argv[1])
+from tuplewise import _lib as L
+lib = L.lib()
+stub = ctypes.CDLL(sys.argv[2])
+comm = ctypes.c_int32(-1)
+devs = (ctypes.c_int32 * 2)(0, 1)
+out = {"init": lib.tw_comm_init(2, devs, ctypes.byref(comm))}
+P = ctypes.c_void_p * 2
+streams = P(None, None)
+bufs = P(None, None)
+out["gather"] = lib.tw_allgather_u64(comm.value, bufs, bufs, 4, streams)
+out["wait"] = lib.tw_comm_wait(comm.value, streams, 2000)
+out["msg"] = lib.tw_last_error().decode()
+out["aborts"] = stub.stub_aborts()
+out["again"] = lib.tw_allgather_u64(comm.value, bufs, bufs, 4, streams)
+out["again_msg"] = lib.tw_last_error().decode()
+out["gathers"] = stub.stub_gathers()
+print(json.dumps(out))
+"""
+
+
+@pytest.fixture(scope="module")
+def stub(tmp_path_factory):
+    so = tmp_path_factory.mktemp("rccl") / "librccl_stub.so"
+    subprocess.run(["g++", "-O1", "-shared", "-fPIC", "-o", str(so),
+                    str(ROOT / "tests" / "native" / "rccl_stub.cpp")], check=True)
+    return so
+
+
+@pytest.mark.parametrize("mode", ["error", "inprogress"])
+def test_comm_wait_fails_instead_of_hanging(stub, mode):
+    env = dict(os.environ, TW_RCCL_LIB=str(stub), STUB_MODE=mode, HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-c", _CHILD, str(ROOT), str(stub)], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["init"] == 0 and out["gather"] == 0 and out["gathers"] == 2
+    assert out["wait"] == 2  # TW_ERR_HIP, returned (no hang)
+    if mode == "error":
+        assert "asynchronous error" in out["msg"] and "stub: system error" in out["msg"]
+    else:  # the collective never reports completion: the stream query or the deadline ends it
+        assert "aborted" in out["msg"]
+    assert out["aborts"] == 2  # both devices' communicators
+    assert out["again"] == 2 and "aborted after an RCCL failure" in out["again_msg"]

@@ -27,7 +27,8 @@ def _edge_sample(rng, n, kind):
 
 
 @pytest.mark.parametrize("kind", ["gauss", "edge", "i64"])
-@pytest.mark.parametrize("n,m", [(1, 1), (0, 5), (7, 0), (300, 257), (5000, 4099)])
+@pytest.mark.parametrize("n,m", [(1, 1), (0, 5), (7, 0), (300, 257), (5000, 4099),
+                                 (200_001, 150_000)])
 def test_rank_images_equal_oracle(gpu, kind, n, m):
     """tw_rank_images == oracle.rank_records bit for bit, and every pair satisfies
     x > z  <=>  x_image + z_image >= 1 (NaN, +-0, +-inf, subnormals, ties, int64)."""
@@ -40,11 +41,39 @@ def test_rank_images_equal_oracle(gpu, kind, n, m):
     xr, zr = HipOps().rank_images(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), code)
     wx, wz = O.rank_records(X, Z)
     assert np.array_equal(xr.cpu().numpy(), wx) and np.array_equal(zr.cpu().numpy(), wz)
-    if n and m and n * m <= 5000 * 5000:
+    if n and m and n * m <= 5000 * 5000:  # the pair property itself, on all pairs
         gx = (wx.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32)
         nz = (wz.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32)
         with np.errstate(invalid="ignore"):
             assert np.array_equal(gx[:, None] + nz[None, :] >= 1, X[:, None] > Z[None, :])
+
+
+def test_rank_images_bucket_paths(gpu):
+    """The bucketed ranking's three per-bucket paths against the oracle: heavy ties (every
+    sampled splitter the same few values: equality buckets), and an interval bucket holding
+    more z keys than its LDS sort takes (the sample sees only one value, every other z falls
+    into the top interval: the tiled counting path)."""
+    import torch
+    from tuplewise import _lib as L
+    from tuplewise.device import HipOps
+    ops = HipOps()
+    rng = np.random.RandomState(17)
+    # heavy ties: 3 values make 95 % of both samples, the rest continuous
+    X = np.where(rng.rand(300_000) < 0.95, rng.choice([-1.0, 0.0, 2.5], 300_000),
+                 rng.normal(size=300_000))
+    Z = np.where(rng.rand(250_000) < 0.95, rng.choice([-1.0, -0.0, 2.5], 250_000),
+                 rng.normal(size=250_000))
+    # the adversarial layout: Z's sampled positions (i * m // cs) all hold 0.0, every other z a
+    # distinct value in (0, 1)
+    m, cs = 40_000, 8192
+    Za = rng.uniform(1e-6, 1.0, m)
+    Za[(np.arange(cs) * m) // cs] = 0.0
+    Xa = rng.uniform(-0.5, 1.5, 30_000)
+    for Xc, Zc in ((X, Z), (Xa, Za)):
+        xr, zr = ops.rank_images(torch.from_numpy(Xc).cuda(), torch.from_numpy(Zc).cuda(),
+                                 L.TW_F64)
+        wx, wz = O.rank_records(Xc, Zc)
+        assert np.array_equal(xr.cpu().numpy(), wx) and np.array_equal(zr.cpu().numpy(), wz)
 
 
 @pytest.mark.parametrize("kind", ["gauss", "edge", "i64"])

@@ -127,6 +127,8 @@ _SIGNATURES = {
     "tw_comm_destroy": [_i32],
     "tw_allgather_u64": [_i32, _vp, _vp, _i64, _vp],
     "tw_allgather_f64": [_i32, _vp, _vp, _i64, _vp],
+    "tw_comm_wait": [_i32, _vp, _i64],
+    "tw_comm_set_timeout": [_i64],
     "tw_np_randint_batch": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],

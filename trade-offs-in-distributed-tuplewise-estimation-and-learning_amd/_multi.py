@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 
 import numpy as np
 
@@ -150,8 +151,20 @@ def gather(parts) -> np.ndarray:
             streams.append(slot.stream.cuda_stream)
     P = ctypes.c_void_p * len(parts)
     fn = "tw_allgather_f64" if dt == t.float64 else "tw_allgather_u64"
-    L.call(fn, comm, P(*[a.data_ptr() for a in send]), P(*[a.data_ptr() for a in recv]), M,
-           P(*streams))
+    try:
+        L.call(fn, comm, P(*[a.data_ptr() for a in send]), P(*[a.data_ptr() for a in recv]), M,
+               P(*streams))
+        # bounded wait: an RCCL failure (a peer that never answers) aborts the communicator
+        # and raises here instead of hanging the copy below (tw_comm_wait)
+        L.call("tw_comm_wait", comm, P(*streams), 0)
+    except (L.TuplewiseError, ValueError) as err:
+        _COMMS[devs] = None  # this device set gathers on the host from now on
+        warnings.warn(f"RCCL all-gather failed ({err}); gathering on the host", RuntimeWarning)
+        vals = []
+        for slot, v, n in parts:
+            with slot:
+                vals.append(v[:n].cpu().numpy())
+        return np.concatenate(vals)
     with parts[0][0]:
         allv = recv[0].cpu().numpy().reshape(len(parts), M)
     return np.concatenate([allv[k, :n] for k, (_, _, n) in enumerate(parts)])

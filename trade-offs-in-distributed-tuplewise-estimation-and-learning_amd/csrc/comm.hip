@@ -10,11 +10,21 @@
 //
 // RCCL is bound at run time (dlopen): the copy the host process already has loaded (PyTorch
 // ships one) is preferred, so the process never holds two RCCL runtimes; otherwise the
-// system's librccl.so.1 is loaded.  A process without RCCL gets TW_ERR_HIP from tw_comm_init
-// and the Python layer gathers on the host instead — the same integers either way.
+// system's librccl.so.1 is loaded (TW_RCCL_LIB names another library: the tests' failure
+// stub).  A process without RCCL gets TW_ERR_HIP from tw_comm_init and the Python layer
+// gathers on the host instead — the same integers either way.
+//
+// Failure detection: a collective whose peer fails never completes, so the
+// caller that needs its result waits through tw_comm_wait — bounded, polling
+// ncclCommGetAsyncError on every device's communicator and the streams' progress; an RCCL
+// error or the deadline aborts the communicator (ncclCommAbort, so its kernels stop holding
+// the GPUs) and returns TW_ERR_HIP; the handle is then dead and later calls on it fail at once.
 #include "tw_common.h"
+#include <chrono>
+#include <cstdlib>
 #include <dlfcn.h>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace tw {
@@ -23,6 +33,7 @@ typedef struct ncclComm* ncclComm_t;
 typedef int ncclResult_t;  // 0 = ncclSuccess
 constexpr int kNcclUint64 = 5;
 constexpr int kNcclFloat64 = 8;
+constexpr ncclResult_t kNcclInProgress = 7;
 
 struct Rccl {
   void* h = nullptr;
@@ -32,11 +43,15 @@ struct Rccl {
   ncclResult_t (*groupStart)() = nullptr;
   ncclResult_t (*groupEnd)() = nullptr;
   const char* (*errStr)(ncclResult_t) = nullptr;
+  ncclResult_t (*asyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*abort)(ncclComm_t) = nullptr;
 };
 
 static Rccl g_rccl;
 static std::mutex g_mu;
 static std::vector<std::vector<ncclComm_t>> g_comms;  // handle -> one comm per device
+static std::vector<char> g_dead;                      // handle -> aborted after a failure
+static int64_t g_wait_ms = 60000;                     // tw_comm_set_timeout
 
 static bool load_rccl() {
   if (g_rccl.h) return true;
@@ -44,9 +59,14 @@ static bool load_rccl() {
   // system one
   const char* names[] = {"librccl.so.1", "librccl.so"};
   void* h = nullptr;
-  for (const char* n : names)
-    if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD)) != nullptr) break;
-  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  const char* over = std::getenv("TW_RCCL_LIB");
+  if (over && *over) {
+    h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
+  } else {
+    for (const char* n : names)
+      if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD)) != nullptr) break;
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  }
   if (!h) return false;
   Rccl r;
   r.h = h;
@@ -56,7 +76,11 @@ static bool load_rccl() {
   r.groupStart = (decltype(r.groupStart))dlsym(h, "ncclGroupStart");
   r.groupEnd = (decltype(r.groupEnd))dlsym(h, "ncclGroupEnd");
   r.errStr = (decltype(r.errStr))dlsym(h, "ncclGetErrorString");
-  if (!r.initAll || !r.destroy || !r.allGather || !r.groupStart || !r.groupEnd) return false;
+  r.asyncError = (decltype(r.asyncError))dlsym(h, "ncclCommGetAsyncError");
+  r.abort = (decltype(r.abort))dlsym(h, "ncclCommAbort");
+  if (!r.initAll || !r.destroy || !r.allGather || !r.groupStart || !r.groupEnd ||
+      !r.asyncError || !r.abort)
+    return false;
   g_rccl = r;
   return true;
 }
@@ -72,6 +96,10 @@ static int allgather(int32_t comm, const void* const* send, void* const* recv, i
     std::lock_guard<std::mutex> lk(g_mu);
     TW_ARG_CHECK(comm >= 0 && comm < (int32_t)g_comms.size() && !g_comms[comm].empty(),
                  "tw_allgather: unknown communicator %d", comm);
+    if (g_dead[comm]) {
+      set_error("tw_allgather: communicator %d was aborted after an RCCL failure", comm);
+      return TW_ERR_HIP;
+    }
     cs = g_comms[comm];
   }
   TW_ARG_CHECK(count >= 0 && send && recv && streams, "tw_allgather: bad arguments");
@@ -86,6 +114,58 @@ static int allgather(int32_t comm, const void* const* send, void* const* recv, i
     return TW_ERR_HIP;
   }
   return TW_OK;
+}
+
+// abort every device's communicator of a handle (caller holds g_mu)
+static void abort_comm(int32_t comm) {
+  for (ncclComm_t c : g_comms[comm]) g_rccl.abort(c);
+  g_dead[comm] = 1;
+}
+
+static int wait_comm(int32_t comm, void* const* streams, int64_t timeout_ms) {
+  std::vector<ncclComm_t> cs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    TW_ARG_CHECK(comm >= 0 && comm < (int32_t)g_comms.size() && !g_comms[comm].empty(),
+                 "tw_comm_wait: unknown communicator %d", comm);
+    if (g_dead[comm]) {
+      set_error("tw_comm_wait: communicator %d was aborted after an RCCL failure", comm);
+      return TW_ERR_HIP;
+    }
+    cs = g_comms[comm];
+  }
+  TW_ARG_CHECK(streams != nullptr, "tw_comm_wait: streams");
+  const int64_t limit = timeout_ms > 0 ? timeout_ms : g_wait_ms;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto fail = [&](const char* what, const char* detail) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    abort_comm(comm);
+    set_error("tw_comm_wait: %s (%s); communicator %d aborted", what, detail, comm);
+    return TW_ERR_HIP;
+  };
+  for (;;) {
+    // an RCCL error on any device's communicator (a peer that failed, a broken link)
+    for (ncclComm_t c : cs) {
+      ncclResult_t ae = 0;
+      const ncclResult_t e = g_rccl.asyncError(c, &ae);
+      if (e != 0) return fail("ncclCommGetAsyncError failed", nccl_err(e));
+      if (ae != 0 && ae != kNcclInProgress) return fail("RCCL asynchronous error", nccl_err(ae));
+    }
+    bool done = true;
+    for (size_t k = 0; k < cs.size(); ++k) {
+      const hipError_t q = hipStreamQuery((hipStream_t)streams[k]);
+      if (q == hipErrorNotReady) {
+        done = false;
+      } else if (q != hipSuccess) {
+        return fail("stream query failed", hipGetErrorString(q));
+      }
+    }
+    if (done) return TW_OK;
+    const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                           std::chrono::steady_clock::now() - t0).count();
+    if (ms > limit) return fail("collective did not complete in time", "deadline");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
 }
 
 }  // namespace tw
@@ -110,6 +190,7 @@ extern "C" int tw_comm_init(int32_t ndev, const int32_t* devs, int32_t* out_comm
     return TW_ERR_HIP;
   }
   g_comms.push_back(cs);
+  g_dead.push_back(0);
   *out_comm = (int32_t)g_comms.size() - 1;
   return TW_OK;
 }
@@ -118,8 +199,19 @@ extern "C" int tw_comm_destroy(int32_t comm) {
   std::lock_guard<std::mutex> lk(g_mu);
   TW_ARG_CHECK(comm >= 0 && comm < (int32_t)g_comms.size() && !g_comms[comm].empty(),
                "tw_comm_destroy: unknown communicator %d", comm);
-  for (ncclComm_t c : g_comms[comm]) g_rccl.destroy(c);
+  if (!g_dead[comm])
+    for (ncclComm_t c : g_comms[comm]) g_rccl.destroy(c);
   g_comms[comm].clear();
+  return TW_OK;
+}
+
+extern "C" int tw_comm_wait(int32_t comm, void* const* streams, int64_t timeout_ms) {
+  return wait_comm(comm, streams, timeout_ms);
+}
+
+extern "C" int tw_comm_set_timeout(int64_t ms) {
+  TW_ARG_CHECK(ms > 0, "tw_comm_set_timeout: ms > 0");
+  g_wait_ms = ms;
   return TW_OK;
 }
 

@@ -17,30 +17,28 @@
 //
 // The images.  Over ONE call (est.UnNT's T repartitions) the multiset of scores does not change,
 // only which shard holds which score.  So the images are computed once per call from the whole
-// sample: sort X ∪ Z by the order key (NaN last, -0 == +0), stably, every x before every z (the
-// input order), and give every element the number of z-elements sorted before it:
-//     gx(x_i) = #{z : key(z) < key(x_i)}   (equal z come after x: never counted)
-//     gz(z_j) = #{z before z_j in the sort} (equal z get distinct consecutive values)
-// Then for any x, z:  x > z  <=>  gx > gz  <=>  gx - gz >= 1.  (key(x) > key(z): every z with
-// key <= key(z) — z itself included — precedes x, so gx >= gz + 1.  key(x) <= key(z): the z
-// counted in gx all precede z, so gx <= gz.)  NaN x get -2^25 (never greater); a NaN z sorts
-// after every non-NaN x, so gz >= gx of every such x (never less).  Images are integers
-// <= m < 2^24, so every f32 sum gx - gz is exact; sentinels are exact powers of two and keep
-// their sign.  Per pair the count is the reference's integer, bit for bit.
+// sample: every element v (of X or of Z) gets
+//     g(v) = #{z in Z : key(z) < key(v)}      (order keys: NaN last, -0 == +0)
+// Then for any x, z:  x > z  <=>  g(x) > g(z)  <=>  g(x) - g(z) >= 1.  (x > z: every z' <= z
+// is < x, z itself included, so g(x) >= g(z) + 1.  x <= z: every z' < x is < z, so
+// g(x) <= g(z).)  NaN x get -2^25 (never greater); a NaN z has g = #non-NaN z >= every g(x)
+// (never less).  Images are integers <= m < 2^24, so every f32 sum g(x) - g(z) is exact;
+// the sentinel is an exact power of two and keeps its sign.  Per pair the count is the
+// reference's integer, bit for bit.
 //
-// State between steps.  An element is an 8-B record: low word = its f32 image, high word = its
-// index in the call's input array.  The repartition permutes records exactly as it permuted
-// doubles (nextstep.h: the next step's gather rides on the tail blocks of the count launch, the
-// same 8 B per element), and at the end of the call one gather writes the doubles in the final
-// order (tw_gather_records).
+// State between steps.  An element is an 8-B record: low word = its f32 image (negated for z),
+// high word = its index in the call's input array.  The repartition permutes records exactly as
+// it permuted doubles (nextstep.h: the next step's gather rides on the tail blocks of the count
+// launch, the same 8 B per element), and at the end of the call one gather writes the doubles in
+// the final order (tw_gather_records).
 //
-// Sort and scan: rocPRIM's device radix sort (stable LSD, 64-bit keys) and lookback scan, once
-// per call; the per-step kernel below is the hot path.
+// The ranking (once per call) is a bucket count, not a sort of all n + m elements: a sorted
+// sample of Z gives B - 1 splitters; every element goes to the interval bucket between two
+// splitters or to the EQUALITY bucket of a splitter (heavy ties land there, where g is the same
+// for every element); per bucket the z keys are sorted in LDS and every element's g is the z
+// count of the lower buckets plus a binary search in its own.  See tw_rank_images below.
 #include "nextstep.h"
 #include "sortkeys.h"
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 namespace tw {
 
@@ -48,79 +46,294 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr float kImgNever = -33554432.0f;  // -2^25: NaN x and padded lanes, never greater
 
 // ----------------------------------------------------------------------------- images
+// g(v) = #{z : key(z) < key(v)} for all n + m elements, from a structure over Z alone:
+//  1. an evenly spaced sample of Z, sorted in one block: B - 1 splitter keys;
+//  2. z -> bucket: 2j for the keys strictly between splitters j-1 and j, 2j + 1 for keys EQUAL
+//     to splitter j (heavy ties land there: no z of such a bucket is below any of its values);
+//     per-block histograms, their prefix per bucket, and the z keys scattered bucket by bucket;
+//  3. per interval bucket, a counting sort of its z keys over 2048 sub-buckets by a key-linear
+//     map between its bounding splitters (monotone, so sub(z) < sub(v) => z < v), into a second
+//     key array, with the sub-bucket prefix table;
+//  4. every element, in input order (coalesced record stores): bucket by splitter search, then
+//     g = z count below the bucket + below its sub-bucket + a scan of its own sub-bucket (about
+//     one key for smooth data; ties or clusters only lengthen the scan, never change g).
+constexpr int kRkThreads = 256;
+constexpr int kRkPer = 16;                         // elements per thread in the bucket passes
+constexpr int kRkTile = kRkThreads * kRkPer;       // 4096 elements per block
+constexpr int kRkSample = 2048;                    // sampled z keys (one k_sort_chunks block)
+constexpr int kRkMaxB = 256;                       // splitter intervals (511 buckets max)
+constexpr int kRkSub = 2048;                       // sub-buckets per interval bucket
+
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_rank_keys(const T* __restrict__ x, int64_t n,
-                                                      const T* __restrict__ z, int64_t m,
-                                                      uint64_t* __restrict__ keys,
-                                                      uint32_t* __restrict__ ids) {
-  const int64_t tot = n + m;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < tot;
-       i += (int64_t)gridDim.x * kBlock) {
-    keys[i] = order_key<T>(i < n ? x[i] : z[i - n]);
-    ids[i] = (uint32_t)i;  // x first: the stable sort keeps every x before an equal z
-  }
+__global__ __launch_bounds__(kBlock) void k_rank_sample(const T* __restrict__ z, int64_t m,
+                                                        int cs, T* __restrict__ samp) {
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < cs; i += gridDim.x * kBlock)
+    samp[i] = z[((int64_t)i * m) / cs];  // evenly spaced over Z (i * m < 2^35)
 }
 
-struct IsZ {
-  uint32_t n;
-  __host__ __device__ uint32_t operator()(uint32_t id) const { return id >= n ? 1u : 0u; }
+// bucket of a key: 2j for the interval below splitter j (j = #splitters < key), 2j + 1 for a key
+// equal to splitter j; bucket order is key order
+__device__ __forceinline__ int rank_bucket(const uint64_t* sp, int nsp, uint64_t k) {
+  int lo = 0, n = nsp;  // lower_bound over sp[0..nsp)
+  while (n > 0) {
+    const int h = n >> 1;
+    if (sp[lo + h] < k) {
+      lo += h + 1;
+      n -= h + 1;
+    } else {
+      n = h;
+    }
+  }
+  return 2 * lo + ((lo < nsp && sp[lo] == k) ? 1 : 0);
+}
+
+struct RankGeo {
+  int64_t n, m, tot;
+  int B, NB, nblk, cs;
 };
 
-// records: x_rec[i] = (image bits | i << 32), z_rec[j] = (-image bits | j << 32)
-__global__ __launch_bounds__(kBlock) void k_rank_records(const uint64_t* __restrict__ keys_s,
-                                                         const uint32_t* __restrict__ ids_s,
-                                                         const uint32_t* __restrict__ cz,
-                                                         int64_t n, int64_t tot, bool x_nan_key,
-                                                         uint64_t* __restrict__ x_rec,
-                                                         uint64_t* __restrict__ z_rec) {
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < tot;
-       p += (int64_t)gridDim.x * kBlock) {
-    const uint32_t id = ids_s[p];
-    const float g = (float)cz[p];  // exact: cz <= m < 2^24
-    if ((int64_t)id < n) {
-      const float img = (x_nan_key && keys_s[p] == ~0ull) ? kImgNever : g;
-      x_rec[id] = (uint64_t)__float_as_uint(img) | ((uint64_t)id << 32);
-    } else {
-      const uint32_t j = id - (uint32_t)n;
-      z_rec[j] = (uint64_t)__float_as_uint(-g) | ((uint64_t)j << 32);
+// splitter j = the sample's ((j + 1) * cs / B)-th key; loaded into LDS by every pass
+__device__ __forceinline__ int load_splitters(const uint64_t* __restrict__ ss, const RankGeo& g,
+                                              uint64_t* sp) {
+  const int nsp = g.B - 1;
+  for (int j = threadIdx.x; j < nsp; j += blockDim.x)
+    sp[j] = ss[(int)(((int64_t)(j + 1) * g.cs) / g.B)];
+  __syncthreads();
+  return nsp;
+}
+
+// pass 1: per-block bucket histogram of Z (column blk of rel[b][*])
+template <typename T>
+__global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ z, RankGeo g,
+                                                          const uint64_t* __restrict__ ss,
+                                                          uint32_t* __restrict__ rel) {
+  __shared__ uint64_t sp[kRkMaxB];
+  __shared__ uint32_t h[2 * kRkMaxB];
+  for (int b = threadIdx.x; b < g.NB; b += kRkThreads) h[b] = 0;
+  const int nsp = load_splitters(ss, g, sp);
+  const int64_t e0 = (int64_t)blockIdx.x * kRkTile;
+#pragma unroll 4
+  for (int k = 0; k < kRkPer; ++k) {
+    const int64_t e = e0 + k * kRkThreads + threadIdx.x;
+    if (e < g.m) atomicAdd(&h[rank_bucket(sp, nsp, order_key<T>(z[e]))], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
+    rel[(int64_t)b * g.nblk + blockIdx.x] = h[b];
+}
+
+// pass 2a: one wave per bucket: exclusive prefix of its row over the blocks (in place), total
+__global__ __launch_bounds__(kBlock) void k_rank_rows(RankGeo g, uint32_t* __restrict__ rel,
+                                                      uint32_t* __restrict__ total) {
+  const int b = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  if (b >= g.NB) return;
+  uint32_t* row = rel + (int64_t)b * g.nblk;
+  uint32_t carry = 0;
+  for (int c0 = 0; c0 < g.nblk; c0 += kWave) {
+    const int c = c0 + lane;
+    const uint32_t v = c < g.nblk ? row[c] : 0u;
+    uint32_t inc = v;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += t;
+    }
+    if (c < g.nblk) row[c] = carry + inc - v;
+    carry += __shfl(inc, kWave - 1, kWave);
+  }
+  if (lane == 0) total[b] = carry;
+}
+
+// pass 2b: bucket starts = the z count below every bucket (one block, NB <= 1024)
+__global__ __launch_bounds__(1024) void k_rank_starts(RankGeo g, const uint32_t* __restrict__ total,
+                                                      uint32_t* __restrict__ start) {
+  __shared__ uint32_t a[1024];
+  const int t = threadIdx.x;
+  a[t] = t < g.NB ? total[t] : 0u;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = t >= o ? a[t - o] : 0u;
+    __syncthreads();
+    a[t] += v;
+    __syncthreads();
+  }
+  if (t < g.NB) start[t] = a[t] - total[t];
+}
+
+// pass 3: the z keys into their buckets' slots (order inside a bucket is free)
+template <typename T>
+__global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict__ z, RankGeo g,
+                                                             const uint64_t* __restrict__ ss,
+                                                             const uint32_t* __restrict__ rel,
+                                                             const uint32_t* __restrict__ start,
+                                                             uint64_t* __restrict__ bkeys) {
+  __shared__ uint64_t sp[kRkMaxB];
+  __shared__ uint32_t cur[2 * kRkMaxB];
+  for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
+    cur[b] = start[b] + rel[(int64_t)b * g.nblk + blockIdx.x];
+  const int nsp = load_splitters(ss, g, sp);
+  const int64_t e0 = (int64_t)blockIdx.x * kRkTile;
+#pragma unroll 4
+  for (int k = 0; k < kRkPer; ++k) {
+    const int64_t e = e0 + k * kRkThreads + threadIdx.x;
+    if (e < g.m) {
+      const uint64_t key = order_key<T>(z[e]);
+      bkeys[atomicAdd(&cur[rank_bucket(sp, nsp, key)], 1u)] = key;
     }
   }
 }
 
+// the key-linear sub-bucket map of interval bucket 2j: bounds = its splitters (the sample's
+// first / last key at the open ends), clamped, so it is monotone over all keys
+struct SubMap {
+  uint64_t lo;
+  int shift;
+  __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
+    if (k <= lo) return 0;
+    const uint64_t d = (k - lo) >> shift;
+    return d >= (uint64_t)kRkSub ? (uint32_t)(kRkSub - 1) : (uint32_t)d;
+  }
+};
+__device__ __forceinline__ SubMap sub_map(const uint64_t* __restrict__ ss, const RankGeo& g,
+                                          int j) {
+  const int nsp = g.B - 1;
+  const uint64_t lo = j > 0 ? ss[(int)(((int64_t)j * g.cs) / g.B)] : ss[0];
+  const uint64_t hi = j < nsp ? ss[(int)(((int64_t)(j + 1) * g.cs) / g.B)] : ss[g.cs - 1];
+  const uint64_t r = hi > lo ? hi - lo : 0;
+  const int bits = r ? 64 - __builtin_clzll(r) : 0;  // r < 2^bits
+  return SubMap{lo, bits > 11 ? bits - 11 : 0};
+}
+
+// pass 4: one block per interval bucket: counting sort of its z keys over kRkSub sub-buckets
+// (histogram, prefix, scatter into skeys), prefix table subp[b][0 .. kRkSub]
+__global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
+    RankGeo g, const uint64_t* __restrict__ ss, const uint32_t* __restrict__ start,
+    const uint32_t* __restrict__ total, const uint64_t* __restrict__ bkeys,
+    uint64_t* __restrict__ skeys, uint32_t* __restrict__ subp, SubMap* __restrict__ maps) {
+  __shared__ uint32_t h[kRkSub + 1];
+  const int b = 2 * blockIdx.x;  // interval buckets only
+  const uint32_t s0 = start[b], c = total[b];
+  const SubMap f = sub_map(ss, g, blockIdx.x);
+  if (threadIdx.x == 0) maps[blockIdx.x] = f;
+  for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) h[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) atomicAdd(&h[f(bkeys[s0 + i])], 1u);
+  __syncthreads();
+  if (threadIdx.x < kWave) {  // exclusive prefix of the 2048 counts: one wave, 32 per lane
+    const int lane = threadIdx.x;
+    constexpr int per = kRkSub / kWave;
+    uint32_t loc[per], sum = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+      loc[k] = h[lane * per + k];
+      sum += loc[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += t;
+    }
+    uint32_t run = inc - sum;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+      h[lane * per + k] = run;
+      run += loc[k];
+    }
+    if (lane == kWave - 1) h[kRkSub] = run;
+  }
+  __syncthreads();
+  uint32_t* sp_out = subp + (int64_t)blockIdx.x * (kRkSub + 1);
+  for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) sp_out[i] = h[i];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
+    const uint64_t k = bkeys[s0 + i];
+    skeys[s0 + atomicAdd(&h[f(k)], 1u)] = k;
+  }
+}
+
+// pass 5: every element in input order, one per thread (the chain splitters -> bucket map ->
+// sub-bucket prefix -> keys is three dependent loads; many waves hide them): its image and its
+// record (coalesced stores)
+template <typename T>
+__global__ __launch_bounds__(kRkThreads) void k_rank_records(
+    const T* __restrict__ x, const T* __restrict__ z, RankGeo g, const uint64_t* __restrict__ ss,
+    const uint32_t* __restrict__ start, const uint32_t* __restrict__ total,
+    const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ subp,
+    const SubMap* __restrict__ maps, uint64_t* __restrict__ x_rec,
+    uint64_t* __restrict__ z_rec) {
+  __shared__ uint64_t sp[kRkMaxB];
+  const int64_t e = (int64_t)blockIdx.x * kRkThreads + threadIdx.x;
+  const bool isx = e < g.n;
+  uint64_t key = 0;
+  if (e < g.tot) key = order_key<T>(isx ? x[e] : z[e - g.n]);  // issued before the barrier
+  const int nsp = load_splitters(ss, g, sp);
+  if (e >= g.tot) return;
+  const int b = rank_bucket(sp, nsp, key);
+  uint32_t gv = start[b];  // every z of the lower buckets is below key
+  if ((b & 1) == 0 && total[b] != 0) {  // interval bucket: sub-buckets below + a scan
+    const SubMap f = maps[b >> 1];
+    const uint32_t sb = f(key);
+    const uint32_t* pt = subp + (int64_t)(b >> 1) * (kRkSub + 1);
+    const uint32_t lo = pt[sb], hi = pt[sb + 1];
+    const uint64_t* q = skeys + gv;
+    uint32_t below = lo;
+    for (uint32_t i = lo; i < hi; ++i) below += q[i] < key ? 1u : 0u;
+    gv += below;
+  }
+  if (isx) {
+    const float img = (std::is_floating_point<T>::value && key == ~0ull) ? kImgNever : (float)gv;
+    x_rec[e] = (uint64_t)__float_as_uint(img) | ((uint64_t)e << 32);
+  } else {
+    const int64_t j = e - g.n;
+    z_rec[j] = (uint64_t)__float_as_uint(-(float)gv) | ((uint64_t)j << 32);
+  }
+}
+
 struct RankWork {
-  uint64_t *keys_in, *keys_out;
-  uint32_t *ids_in, *ids_out, *cz;
-  void* temp;
-  size_t temp_bytes;
-  size_t total;
+  void* samp;
+  uint64_t *ss, *bkeys, *skeys;
+  uint32_t *rel, *total, *start, *subp;
+  SubMap* maps;
+  size_t total_bytes;
 };
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-static int rank_work(int64_t n, int64_t m, char* base, RankWork* w) {
-  const int64_t tot = n + m;
-  size_t sort_b = 0, scan_b = 0;
-  TW_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, sort_b, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                         (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)tot, 0,
-                                         64));
-  auto flags = rocprim::make_transform_iterator((const uint32_t*)nullptr, IsZ{(uint32_t)n});
-  TW_HIP_CHECK(rocprim::exclusive_scan(nullptr, scan_b, flags, (uint32_t*)nullptr, 0u,
-                                       (size_t)tot, rocprim::plus<uint32_t>()));
+static RankGeo rank_geo(int64_t n, int64_t m) {
+  RankGeo g{};
+  g.n = n;
+  g.m = m;
+  g.tot = n + m;
+  int B = 1;
+  while (B < kRkMaxB && (int64_t)B * 2048 < m) B <<= 1;  // >= ~2048 z per interval
+  g.B = B;
+  g.NB = 2 * B;
+  g.nblk = (int)std::max<int64_t>(1, ceil_div(m, kRkTile));
+  g.cs = (int)std::min<int64_t>(m, kRkSample);
+  return g;
+}
+
+static RankWork rank_work(const RankGeo& g, char* base) {
+  RankWork w{};
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
     off += align256(bytes);
     return base ? (void*)(base + o) : nullptr;
   };
-  w->keys_in = (uint64_t*)take(8 * (size_t)tot);
-  w->keys_out = (uint64_t*)take(8 * (size_t)tot);
-  w->ids_in = (uint32_t*)take(4 * (size_t)tot);
-  w->ids_out = (uint32_t*)take(4 * (size_t)tot);
-  w->cz = (uint32_t*)take(4 * (size_t)tot);
-  w->temp_bytes = std::max(sort_b, scan_b);
-  w->temp = take(w->temp_bytes);
-  w->total = off;
-  return TW_OK;
+  w.samp = take(8 * (size_t)kRkSample);
+  w.ss = (uint64_t*)take(8 * (size_t)kRkSample);
+  w.rel = (uint32_t*)take(4 * (size_t)g.NB * g.nblk);
+  w.total = (uint32_t*)take(4 * (size_t)g.NB);
+  w.start = (uint32_t*)take(4 * (size_t)g.NB);
+  w.subp = (uint32_t*)take(4 * (size_t)g.B * (kRkSub + 1));
+  w.maps = (SubMap*)take(sizeof(SubMap) * (size_t)g.B);
+  w.bkeys = (uint64_t*)take(8 * (size_t)std::max<int64_t>(g.m, 1));
+  w.skeys = (uint64_t*)take(8 * (size_t)std::max<int64_t>(g.m, 1));
+  w.total_bytes = off;
+  return w;
 }
 
 static bool rank_sizes_ok(int64_t n, int64_t m) {
@@ -315,10 +528,40 @@ using namespace tw;
 
 extern "C" int64_t tw_rank_images_work_bytes(int64_t n_x, int64_t n_z) {
   if (!rank_sizes_ok(n_x, n_z)) return -1;
-  RankWork w{};
-  if (rank_work(n_x, n_z, nullptr, &w) != TW_OK) return -1;
-  return (int64_t)w.total;
+  return (int64_t)rank_work(rank_geo(n_x, n_z), nullptr).total_bytes;
 }
+
+namespace tw {
+template <typename T>
+static int rank_images_t(const T* x, int64_t n, const T* z, int64_t m, const RankWork& w,
+                         const RankGeo& g, uint64_t* x_rec, uint64_t* z_rec, hipStream_t st) {
+  if (m > 0) {  // the sample: evenly spaced z, sorted (k_sort_chunks pads with ~0 past cs)
+    hipLaunchKernelGGL((k_rank_sample<T>), dim3(8), dim3(kBlock), 0, st, z, m, g.cs, (T*)w.samp);
+    hipLaunchKernelGGL((k_sort_chunks<T, 4>), dim3(1), dim3(kRkSample / 4), kRkSample * 8, st,
+                       (const T*)w.samp, nullptr, 1, kRkSample, w.ss, (int64_t)g.cs);
+    TW_LAUNCH_CHECK();
+    hipLaunchKernelGGL((k_rank_hist<T>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g, w.ss,
+                       w.rel);
+    hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
+                       dim3(kBlock), 0, st, g, w.rel, w.total);
+    hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
+    hipLaunchKernelGGL((k_rank_scatter<T>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g, w.ss,
+                       w.rel, w.start, w.bkeys);
+    hipLaunchKernelGGL(k_rank_subsort, dim3(g.B), dim3(kRkThreads), 0, st, g, w.ss, w.start,
+                       w.total, w.bkeys, w.skeys, w.subp, w.maps);
+    TW_LAUNCH_CHECK();
+  } else {  // no z: every image is 0
+    TW_HIP_CHECK(tw_zero_async(w.start, 0, 4 * (size_t)g.NB, st));
+    TW_HIP_CHECK(tw_zero_async(w.total, 0, 4 * (size_t)g.NB, st));
+    TW_HIP_CHECK(tw_zero_async(w.ss, 0, 8 * (size_t)kRkSample, st));
+  }
+  hipLaunchKernelGGL((k_rank_records<T>), dim3((unsigned)ceil_div(g.tot, kRkThreads)),
+                     dim3(kRkThreads), 0, st, x, z, g, w.ss, w.start, w.total, w.skeys, w.subp,
+                     w.maps, x_rec, z_rec);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+}  // namespace tw
 
 extern "C" int tw_rank_images(const void* d_x, int64_t n_x, const void* d_z, int64_t n_z,
                               int32_t dtype, void* d_work, int64_t work_bytes, uint64_t* d_x_rec,
@@ -328,34 +571,17 @@ extern "C" int tw_rank_images(const void* d_x, int64_t n_x, const void* d_z, int
                (long long)n_x, (long long)n_z);
   TW_ARG_CHECK(dtype == TW_F64 || dtype == TW_I64, "tw_rank_images: unknown dtype %d", dtype);
   hipStream_t st = (hipStream_t)stream;
-  const int64_t tot = n_x + n_z;
-  if (tot == 0) return TW_OK;
-  RankWork w{};
-  if (rank_work(n_x, n_z, (char*)d_work, &w) != TW_OK) return TW_ERR_HIP;
-  TW_ARG_CHECK(d_work != nullptr && work_bytes >= (int64_t)w.total,
+  if (n_x + n_z == 0) return TW_OK;
+  const RankGeo g = rank_geo(n_x, n_z);
+  const RankWork w = rank_work(g, (char*)d_work);
+  TW_ARG_CHECK(d_work != nullptr && work_bytes >= (int64_t)w.total_bytes,
                "tw_rank_images: work buffer of %lld bytes, %lld needed", (long long)work_bytes,
-               (long long)w.total);
-  const unsigned grid = (unsigned)std::min<int64_t>(4096, ceil_div(tot, kBlock));
+               (long long)w.total_bytes);
   if (dtype == TW_F64)
-    hipLaunchKernelGGL(k_rank_keys<double>, dim3(grid), dim3(kBlock), 0, st, (const double*)d_x,
-                       n_x, (const double*)d_z, n_z, w.keys_in, w.ids_in);
-  else
-    hipLaunchKernelGGL(k_rank_keys<long long>, dim3(grid), dim3(kBlock), 0, st,
-                       (const long long*)d_x, n_x, (const long long*)d_z, n_z, w.keys_in,
-                       w.ids_in);
-  TW_LAUNCH_CHECK();
-  size_t tb = w.temp_bytes;
-  TW_HIP_CHECK(rocprim::radix_sort_pairs(w.temp, tb, w.keys_in, w.keys_out, w.ids_in, w.ids_out,
-                                         (size_t)tot, 0, 64, st));
-  tb = w.temp_bytes;
-  auto flags = rocprim::make_transform_iterator((const uint32_t*)w.ids_out,
-                                                IsZ{(uint32_t)n_x});
-  TW_HIP_CHECK(rocprim::exclusive_scan(w.temp, tb, flags, w.cz, 0u, (size_t)tot,
-                                       rocprim::plus<uint32_t>(), st));
-  hipLaunchKernelGGL(k_rank_records, dim3(grid), dim3(kBlock), 0, st, w.keys_out, w.ids_out,
-                     w.cz, n_x, tot, dtype == TW_F64, d_x_rec, d_z_rec);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+    return rank_images_t<double>((const double*)d_x, n_x, (const double*)d_z, n_z, w, g, d_x_rec,
+                                 d_z_rec, st);
+  return rank_images_t<long long>((const long long*)d_x, n_x, (const long long*)d_z, n_z, w, g,
+                                  d_x_rec, d_z_rec, st);
 }
 
 extern "C" int tw_count_rank_set_plan(int32_t R, int64_t z_chunk) {
