@@ -273,6 +273,15 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
 
     dt, v = timed(Bk.DEVICE_SHUFFLE_MIN)
     dt_host, v_host = timed(1 << 62)
+    # the same call with two device slots visible (a multi-GPU node's default device list;
+    # slots [0, 0] on one GPU): the blocks' sorted count stays below the spreading threshold,
+    # so the device-shuffle path is kept
+    from tuplewise import _multi as M
+    M.set_devices([0, 0])
+    try:
+        dt_slots, v_slots = timed(Bk.DEVICE_SHUFFLE_MIN)
+    finally:
+        M.set_devices(None)
     # the parts of the default path, timed alone on the same shapes
     t0 = time.perf_counter()
     jx, jz = [], []
@@ -319,6 +328,8 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
             "ms_per_call": dt * 1e3, "value": pairs / dt, "unit": "pairs/s",
             "host_swap_path_ms_per_call": dt_host * 1e3,
             "same_value_both_paths": bool(v == v_host),
+            "slots_0_0_ms_per_call": dt_slots * 1e3,
+            "slots_0_0_same_value": bool(v_slots == v),
             "host_draws_ms": draws * 1e3, "numpy_shuffles_ms": np_shuffles * 1e3,
             "h2d_ms": h2d * 1e3, "device_shuffles_ms": dev_shuffle * 1e3,
             "d2h_ms": d2h * 1e3, "count_algo": algo,

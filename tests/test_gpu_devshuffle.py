@@ -99,3 +99,32 @@ def test_drop_in_device_shuffles_equal_host_path(gpu, name, make):
     assert dev[0] == host[0] and type(dev[0]) is type(host[0])
     for a, b in zip(dev[1:], host[1:]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["est.UnNT prop-SWOR", "cs.UnNBT AUC"])
+def test_device_shuffles_kept_with_several_devices(gpu, name, monkeypatch):
+    """With several device slots visible (slots [0, 0] on the one-GPU box, as TW_DEVICES=0,0
+    gives), est.UnNT / cs.UnNBT at >= 2^16 items per sample keep the device-shuffle path (the
+    sorted count of their blocks is far below the multi-device threshold): it
+    runs, and gives the one-device value, post-call arrays and RNG state bit for bit."""
+    import tuplewise.compute_stats as cs
+    import tuplewise.estimation as est
+    from tuplewise import _blocks as Bk, _multi as M
+    fn = dict(CASES)[name](est, cs)
+    rs = np.random.RandomState(4)
+    X = rs.normal(0.3, 1, 1 << 17)
+    Z = rs.normal(0, 1, (1 << 16) + 5)
+    one = _call(fn, X, Z, 31)
+    taken = []
+    orig = Bk._run_un_repeated_device
+    monkeypatch.setattr(Bk, "_run_un_repeated_device",
+                        lambda *a, **k: taken.append(1) or orig(*a, **k))
+    M.set_devices([0, 0])
+    try:
+        two = _call(fn, X, Z, 31)
+    finally:
+        M.set_devices(None)
+    assert taken, "the device-shuffle path was not taken with two slots"
+    assert two[0] == one[0]
+    for a, b in zip(two[1:], one[1:]):
+        assert np.array_equal(a, b)

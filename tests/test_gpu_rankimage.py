@@ -49,10 +49,10 @@ def test_rank_images_equal_oracle(gpu, kind, n, m):
 
 
 def test_rank_images_bucket_paths(gpu):
-    """The bucketed ranking's three per-bucket paths against the oracle: heavy ties (every
-    sampled splitter the same few values: equality buckets), and an interval bucket holding
-    more z keys than its LDS sort takes (the sample sees only one value, every other z falls
-    into the top interval: the tiled counting path)."""
+    """The bucketed ranking against the oracle on the layouts that exercise its paths: heavy
+    ties (every sampled splitter one of a few values: equality buckets), a sample that sees only
+    one value (every other z in the top interval bucket), heavy tails with subnormals (the
+    order-key sub-bucket map), and full-range int64 keys."""
     import torch
     from tuplewise import _lib as L
     from tuplewise.device import HipOps
@@ -69,9 +69,13 @@ def test_rank_images_bucket_paths(gpu):
     Za = rng.uniform(1e-6, 1.0, m)
     Za[(np.arange(cs) * m) // cs] = 0.0
     Xa = rng.uniform(-0.5, 1.5, 30_000)
-    for Xc, Zc in ((X, Z), (Xa, Za)):
-        xr, zr = ops.rank_images(torch.from_numpy(Xc).cuda(), torch.from_numpy(Zc).cuda(),
-                                 L.TW_F64)
+    # heavy tails (the order-key sub-bucket map) and a sample straddling 0 with subnormals
+    Xc_, Zc_ = rng.standard_cauchy(200_000), rng.standard_cauchy(180_000)
+    Zc_[::1000] = 5e-324
+    Xi, Zi = rng.randint(-2 ** 62, 2 ** 62, 100_000), rng.randint(-2 ** 62, 2 ** 62, 90_000)
+    for Xc, Zc in ((X, Z), (Xa, Za), (Xc_, Zc_), (Xi, Zi)):
+        code = L.TW_I64 if Xc.dtype == np.int64 else L.TW_F64
+        xr, zr = ops.rank_images(torch.from_numpy(Xc).cuda(), torch.from_numpy(Zc).cuda(), code)
         wx, wz = O.rank_records(Xc, Zc)
         assert np.array_equal(xr.cpu().numpy(), wx) and np.array_equal(zr.cpu().numpy(), wz)
 

@@ -130,6 +130,11 @@ class BlockSpec:
     def evaluate(self, X: np.ndarray, Z: np.ndarray, blocks: list) -> list:
         raise NotImplementedError
 
+    def work(self, nx: int, nz: int, dtype) -> int:
+        """Device work of one block in all-pairs compare equivalents (what the multi-device
+        split weighs; default: every pair once)."""
+        return nx * nz
+
 
 class CompleteCount(BlockSpec):
     """Un-type block: exact count of a comparison predicate over all pairs, divided by nx*nz.
@@ -153,10 +158,20 @@ class CompleteCount(BlockSpec):
             mode = "half"
         return x, z, code, mode
 
+    def _mode(self, dtype) -> str:
+        if self.literal_sub and np.issubdtype(np.dtype(dtype), np.integer):
+            return "subgt"  # int64 wrap-around: all pairs only
+        return "half" if self.tie_mode == "half" else "gt"
+
+    def work(self, nx, nz, dtype):
+        """the count 'auto' runs: (nx + nz) sorted-element steps or nx*nz compares"""
+        return E.count_work(nx, nz, self._mode(dtype))
+
     def evaluate(self, X, Z, blocks):
         x, z, code, mode = self.operands(_flat(X), _flat(Z))
         blocks = _elements(_elements(blocks, "x", _row_size(X)), "z", _row_size(Z))
-        work = sum(b.nx() * b.nz() for b in blocks)
+        wmode = mode if mode != "ne" else "gt"
+        work = sum(E.count_work(b.nx(), b.nz(), wmode) for b in blocks)
         if mode != "ne" and M.slots_for(work, len(blocks)):
             pred = {"gt": L.TW_PRED_GT, "half": L.TW_PRED_HALF, "subgt": L.TW_PRED_SUBGT}[mode]
 
@@ -169,7 +184,8 @@ class CompleteCount(BlockSpec):
                 return E.count_launch(xa, xod, za, zod, len(sub), mx, mz, code, pred,
                                       E.pick_algo("auto", mx, mz, mode))
 
-            counts = M.gather(M.spread(blocks, lambda b: b.nx() * b.nz(), enqueue))
+            counts = M.gather(M.spread(blocks, lambda b: E.count_work(b.nx(), b.nz(), wmode),
+                                       enqueue))
             counts = counts.astype(np.int64).view(np.uint64)
         else:
             xo, zo = _slice_offsets(blocks, "x"), _slice_offsets(blocks, "z")
@@ -257,6 +273,10 @@ class Incomplete(BlockSpec):
         iz = np.random.randint(0, nz, self.B)
         return ix, iz
 
+    def work(self, nx, nz, dtype):
+        """B indexed pairs (two random gathers each: ~50 compares of the all-pairs kernel)"""
+        return 50 * self.B
+
     def evaluate(self, X, Z, blocks):
         rs = _row_size(X)
         if _row_size(Z) != rs:
@@ -307,7 +327,7 @@ def block_indexed_values(x: np.ndarray, z: np.ndarray, blocks: list, ix_loc: lis
         xx, zz, code, mode = (x.astype(np.float64, copy=False), z.astype(np.float64, copy=False),
                               L.TW_F64, None)
     npairs = np.diff(offs)
-    if mode != "ne" and M.slots_for(int(offs[-1]) * 8, len(blocks)):
+    if mode != "ne" and M.slots_for(int(offs[-1]) * 50, len(blocks)):  # ~50 compares a pair
         pos = {id(b): i for i, b in enumerate(blocks)}
 
         def enqueue(sub):  # this slot's blocks, their draws shifted into the uploaded spans
@@ -441,7 +461,7 @@ def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
         return None  # the in-place shuffles must act on the caller's own objects
     if any(a.ndim > 2 or (a.ndim == 2 and a.shape[1] != 1) for a in (X, Z)):
         return None
-    if _device_shuffle_ok(X, Z, spec):
+    if _device_shuffle_ok(X, Z, spec, N, T):
         return _run_un_repeated_device(X, Z, N, spec, sampling_type, variant, T)
     plans, jobs = [], []
     for t in range(T):
@@ -458,16 +478,25 @@ def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
 DEVICE_SHUFFLE_MIN = 1 << 16
 
 
-def _device_shuffle_ok(X, Z, spec) -> bool:
+def _device_shuffle_ok(X, Z, spec, N: int = 1, T: int = 1) -> bool:
     """The repeated UN's shuffles and blocks can stay on the device: 1-D C-contiguous float64
     samples (8-byte items whose comparison / kernel operands are the scores themselves), a spec
-    with a device evaluation, the legacy MT19937 global state, one device."""
-    return (X.ndim == 1 and Z.ndim == 1 and X.dtype == np.float64 and Z.dtype == np.float64
-            and X.flags.c_contiguous and Z.flags.c_contiguous and X.flags.writeable
-            and Z.flags.writeable and max(X.shape[0], Z.shape[0]) >= DEVICE_SHUFFLE_MIN
-            and X.shape[0] + Z.shape[0] < 2 ** 31 and hasattr(spec, "evaluate_device")
-            and not np.shares_memory(X, Z)  # separate uploads would lose the aliasing
-            and np.random.get_state(legacy=True)[0] == "MT19937" and len(M.devices()) < 2)
+    with a device evaluation, the legacy MT19937 global state, and blocks whose work does not
+    call for spreading over several devices (the multi-device split weighs the algorithm that
+    will run: the sorted count of est.UnNT's blocks is ~0.1 ms, so a node with 8 GPUs keeps
+    the one-device shuffles — DESIGN.md §6)."""
+    ok = (X.ndim == 1 and Z.ndim == 1 and X.dtype == np.float64 and Z.dtype == np.float64
+          and X.flags.c_contiguous and Z.flags.c_contiguous and X.flags.writeable
+          and Z.flags.writeable and max(X.shape[0], Z.shape[0]) >= DEVICE_SHUFFLE_MIN
+          and X.shape[0] + Z.shape[0] < 2 ** 31 and hasattr(spec, "evaluate_device")
+          and not np.shares_memory(X, Z)  # separate uploads would lose the aliasing
+          and np.random.get_state(legacy=True)[0] == "MT19937")
+    if not ok or len(M.devices()) < 2:
+        return ok
+    nb = max(1, int(N)) * max(1, int(T))
+    per = spec.work(max(1, X.shape[0] // max(1, N)), max(1, Z.shape[0] // max(1, N)),
+                    np.float64)
+    return M.slots_for(per * nb, nb) is None
 
 
 def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):

@@ -140,6 +140,20 @@ def pick_algo(algo: str, max_nx: int, max_nz: int, mode: str) -> str:
     return algo
 
 
+# one element of the sorted count (LDS buckets / sort + search, csrc/rankcount.hip) costs about
+# as much device time as 750 compares of the all-pairs kernel (measured at the C3 shape:
+# 2e6 elements in ~45 us against 3.3e13 compared pairs/s)
+SORTED_ELEMENT_COST = 750
+
+
+def count_work(nx: int, nz: int, mode: str) -> int:
+    """Device work of one block's count in all-pairs compare equivalents, for the algorithm
+    'auto' picks: nx*nz compares, or (nx + nz) sorted-element steps."""
+    if pick_algo("auto", nx, nz, mode) == "sorted":
+        return (nx + nz) * SORTED_ELEMENT_COST
+    return nx * nz
+
+
 def count_launch(x_dev, x_off_dev, z_dev, z_off_dev, n, max_nx, max_nz, dtype, pred, algo):
     """Enqueue one count of all shards (no host sync); returns the int64 device tensor."""
     t = L.torch()

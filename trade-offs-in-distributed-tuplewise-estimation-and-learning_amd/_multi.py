@@ -24,7 +24,10 @@ import numpy as np
 
 from . import _lib as L
 
-MIN_WORK = 1 << 27  # pair compares below which a call is not worth spreading
+# work (all-pairs compare equivalents, BlockSpec.work) below which a call stays on one device:
+# 2^33 is ~0.25 ms of one MI355X's count kernel, about what spreading costs (per-device
+# uploads, launches, the gather)
+MIN_WORK = 1 << 33
 _DEVICES = None
 _STREAMS = {}
 _COMMS = {}

@@ -51,9 +51,9 @@ constexpr float kImgNever = -33554432.0f;  // -2^25: NaN x and padded lanes, nev
 //  2. z -> bucket: 2j for the keys strictly between splitters j-1 and j, 2j + 1 for keys EQUAL
 //     to splitter j (heavy ties land there: no z of such a bucket is below any of its values);
 //     per-block histograms, their prefix per bucket, and the z keys scattered bucket by bucket;
-//  3. per interval bucket, a counting sort of its z keys over 2048 sub-buckets by a key-linear
-//     map between its bounding splitters (monotone, so sub(z) < sub(v) => z < v), into a second
-//     key array, with the sub-bucket prefix table;
+//  3. per interval bucket, a counting sort of its z keys over 2048 sub-buckets by a monotone map
+//     (linear in the value or in the order key, whichever spreads the bucket's z better; so
+//     sub(z) < sub(v) => z < v), into a second key array, with the sub-bucket prefix table;
 //  4. every element, in input order (coalesced record stores): bucket by splitter search, then
 //     g = z count below the bucket + below its sub-bucket + a scan of its own sub-bucket (about
 //     one key for smooth data; ties or clusters only lengthen the scan, never change g).
@@ -184,43 +184,80 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict
   }
 }
 
-// the key-linear sub-bucket map of interval bucket 2j: bounds = its splitters (the sample's
-// first / last key at the open ends), clamped, so it is monotone over all keys
+// The sub-bucket map of an interval bucket, one of two monotone maps (sub(z) < sub(v) => z < v),
+// whichever spreads the bucket's z better (the smaller sum of squared sub-bucket counts, i.e.
+// the shorter expected scan):
+//  * linear in the VALUE between the bucket's smallest and largest finite z:
+//    fl(fl(v - lo) * scale) never decreases as v grows; right for bulk buckets, and for the
+//    bucket that straddles 0, where every tiny magnitude lies between the two signs' keys;
+//  * linear in the ORDER KEY between the bucket's smallest and largest non-NaN z key (a log
+//    scale in the magnitude): right for heavy tails (Cauchy-like scores), where a value-linear
+//    map crowds the bucket's inner edge into one sub-bucket.
+// Both clamp; NaN goes last.
 struct SubMap {
-  uint64_t lo;
-  int shift;
-  __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
-    if (k <= lo) return 0;
-    const uint64_t d = (k - lo) >> shift;
-    return d >= (uint64_t)kRkSub ? (uint32_t)(kRkSub - 1) : (uint32_t)d;
+  double lo, scale;
+  uint64_t klo;
+  int kshift, bykey;
+  __device__ __forceinline__ uint32_t operator()(double v, uint64_t k) const {
+    if (bykey) {
+      if (k <= klo) return 0;
+      const uint64_t d = (k - klo) >> kshift;
+      return d >= (uint64_t)(kRkSub - 1) ? (uint32_t)(kRkSub - 1) : (uint32_t)d;
+    }
+    if (v != v) return kRkSub - 1;
+    const double d = (v - lo) * scale;
+    if (!(d > 0.0)) return 0;
+    return d >= (double)(kRkSub - 1) ? (uint32_t)(kRkSub - 1) : (uint32_t)d;
   }
 };
-__device__ __forceinline__ SubMap sub_map(const uint64_t* __restrict__ ss, const RankGeo& g,
-                                          int j) {
-  const int nsp = g.B - 1;
-  const uint64_t lo = j > 0 ? ss[(int)(((int64_t)j * g.cs) / g.B)] : ss[0];
-  const uint64_t hi = j < nsp ? ss[(int)(((int64_t)(j + 1) * g.cs) / g.B)] : ss[g.cs - 1];
-  const uint64_t r = hi > lo ? hi - lo : 0;
-  const int bits = r ? 64 - __builtin_clzll(r) : 0;  // r < 2^bits
-  return SubMap{lo, bits > 11 ? bits - 11 : 0};
+
+template <typename T>
+__device__ __forceinline__ double key_value(uint64_t k);
+template <>
+__device__ __forceinline__ double key_value<double>(uint64_t k) {
+  return key_to_double(k);
+}
+template <>
+__device__ __forceinline__ double key_value<long long>(uint64_t k) {
+  return (double)(long long)(k ^ 0x8000000000000000ull);
 }
 
-// pass 4: one block per interval bucket: counting sort of its z keys over kRkSub sub-buckets
-// (histogram, prefix, scatter into skeys), prefix table subp[b][0 .. kRkSub]
-__global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
-    RankGeo g, const uint64_t* __restrict__ ss, const uint32_t* __restrict__ start,
-    const uint32_t* __restrict__ total, const uint64_t* __restrict__ bkeys,
-    uint64_t* __restrict__ skeys, uint32_t* __restrict__ subp, SubMap* __restrict__ maps) {
-  __shared__ uint32_t h[kRkSub + 1];
-  const int b = 2 * blockIdx.x;  // interval buckets only
-  const uint32_t s0 = start[b], c = total[b];
-  const SubMap f = sub_map(ss, g, blockIdx.x);
-  if (threadIdx.x == 0) maps[blockIdx.x] = f;
-  for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) h[i] = 0;
+// block-wide min / max (all threads get the result)
+__device__ __forceinline__ void block_minmax(double& lo, double& hi, uint64_t& klo,
+                                             uint64_t& khi, double* sd, uint64_t* sk) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, kWave));
+    hi = fmax(hi, __shfl_xor(hi, o, kWave));
+    const uint64_t a = __shfl_xor(klo, o, kWave), b = __shfl_xor(khi, o, kWave);
+    klo = a < klo ? a : klo;
+    khi = b > khi ? b : khi;
+  }
+  const int wid = threadIdx.x / kWave;
+  constexpr int W = kRkThreads / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    sd[wid] = lo;
+    sd[W + wid] = hi;
+    sk[wid] = klo;
+    sk[W + wid] = khi;
+  }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) atomicAdd(&h[f(bkeys[s0 + i])], 1u);
-  __syncthreads();
-  if (threadIdx.x < kWave) {  // exclusive prefix of the 2048 counts: one wave, 32 per lane
+  lo = sd[0];
+  hi = sd[W];
+  klo = sk[0];
+  khi = sk[W];
+#pragma unroll
+  for (int w = 1; w < W; ++w) {
+    lo = fmin(lo, sd[w]);
+    hi = fmax(hi, sd[W + w]);
+    klo = sk[w] < klo ? sk[w] : klo;
+    khi = sk[W + w] > khi ? sk[W + w] : khi;
+  }
+}
+
+// exclusive prefix of h[0 .. kRkSub) by wave 0 (32 entries per lane), total in h[kRkSub]
+__device__ __forceinline__ void sub_prefix(uint32_t* h) {
+  if (threadIdx.x < kWave) {
     const int lane = threadIdx.x;
     constexpr int per = kRkSub / kWave;
     uint32_t loc[per], sum = 0;
@@ -243,13 +280,76 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
     }
     if (lane == kWave - 1) h[kRkSub] = run;
   }
+}
+
+// pass 4: one block per interval bucket: the two candidate maps, their histograms, the better
+// one's prefix table subp[b][0 .. kRkSub] and the z keys sorted by it into skeys
+template <typename T>
+__global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
+    RankGeo g, const uint32_t* __restrict__ start, const uint32_t* __restrict__ total,
+    const uint64_t* __restrict__ bkeys, uint64_t* __restrict__ skeys,
+    uint32_t* __restrict__ subp, SubMap* __restrict__ maps) {
+  __shared__ uint32_t hv[kRkSub + 1], hk[kRkSub + 1];
+  __shared__ double sd[2 * kRkThreads / kWave];
+  __shared__ uint64_t sk[2 * kRkThreads / kWave];
+  __shared__ unsigned long long cost[2];
+  const int b = 2 * blockIdx.x;  // interval buckets only
+  const uint32_t s0 = start[b], c = total[b];
+  double lo = __builtin_inf(), hi = -__builtin_inf();
+  uint64_t klo = ~0ull, khi = 0;
+  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
+    const uint64_t k = bkeys[s0 + i];
+    const double v = key_value<T>(k);
+    if (v - v == 0.0) {  // finite
+      lo = fmin(lo, v);
+      hi = fmax(hi, v);
+    }
+    if (k != ~0ull) {  // not NaN
+      klo = k < klo ? k : klo;
+      khi = k > khi ? k : khi;
+    }
+  }
+  for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) hv[i] = hk[i] = 0;
+  if (threadIdx.x < 2) cost[threadIdx.x] = 0;
+  block_minmax(lo, hi, klo, khi, sd, sk);
+  SubMap fv{0.0, 0.0, 0, 0, 0}, fk{0.0, 0.0, 0, 0, 1};
+  if (hi > lo) {
+    const double scale = (double)kRkSub / (hi - lo);
+    if (scale - scale == 0.0) fv.lo = lo, fv.scale = scale;  // a finite span
+  }
+  if (khi > klo) {
+    const uint64_t r = khi - klo;
+    const int bits = 64 - __builtin_clzll(r);  // r < 2^bits
+    fk.klo = klo;
+    fk.kshift = bits > 11 ? bits - 11 : 0;
+  }
+  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
+    const uint64_t k = bkeys[s0 + i];
+    const double v = key_value<T>(k);
+    atomicAdd(&hv[fv(v, k)], 1u);
+    atomicAdd(&hk[fk(v, k)], 1u);
+  }
+  __syncthreads();
+  unsigned long long cv = 0, ck = 0;
+  for (int i = threadIdx.x; i < kRkSub; i += kRkThreads) {
+    cv += (unsigned long long)hv[i] * hv[i];
+    ck += (unsigned long long)hk[i] * hk[i];
+  }
+  atomicAdd(&cost[0], cv);
+  atomicAdd(&cost[1], ck);
+  __syncthreads();
+  const bool bykey = cost[1] < cost[0];
+  const SubMap f = bykey ? fk : fv;
+  uint32_t* h = bykey ? hk : hv;
+  if (threadIdx.x == 0) maps[blockIdx.x] = f;
+  sub_prefix(h);
   __syncthreads();
   uint32_t* sp_out = subp + (int64_t)blockIdx.x * (kRkSub + 1);
   for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) sp_out[i] = h[i];
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
     const uint64_t k = bkeys[s0 + i];
-    skeys[s0 + atomicAdd(&h[f(k)], 1u)] = k;
+    skeys[s0 + atomicAdd(&h[f(key_value<T>(k), k)], 1u)] = k;
   }
 }
 
@@ -266,15 +366,16 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_records(
   __shared__ uint64_t sp[kRkMaxB];
   const int64_t e = (int64_t)blockIdx.x * kRkThreads + threadIdx.x;
   const bool isx = e < g.n;
-  uint64_t key = 0;
-  if (e < g.tot) key = order_key<T>(isx ? x[e] : z[e - g.n]);  // issued before the barrier
+  T v = 0;
+  if (e < g.tot) v = isx ? x[e] : z[e - g.n];  // issued before the barrier
+  const uint64_t key = order_key<T>(v);
   const int nsp = load_splitters(ss, g, sp);
   if (e >= g.tot) return;
   const int b = rank_bucket(sp, nsp, key);
   uint32_t gv = start[b];  // every z of the lower buckets is below key
   if ((b & 1) == 0 && total[b] != 0) {  // interval bucket: sub-buckets below + a scan
     const SubMap f = maps[b >> 1];
-    const uint32_t sb = f(key);
+    const uint32_t sb = f((double)v, key);
     const uint32_t* pt = subp + (int64_t)(b >> 1) * (kRkSub + 1);
     const uint32_t lo = pt[sb], hi = pt[sb + 1];
     const uint64_t* q = skeys + gv;
@@ -547,7 +648,7 @@ static int rank_images_t(const T* x, int64_t n, const T* z, int64_t m, const Ran
     hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
     hipLaunchKernelGGL((k_rank_scatter<T>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g, w.ss,
                        w.rel, w.start, w.bkeys);
-    hipLaunchKernelGGL(k_rank_subsort, dim3(g.B), dim3(kRkThreads), 0, st, g, w.ss, w.start,
+    hipLaunchKernelGGL((k_rank_subsort<T>), dim3(g.B), dim3(kRkThreads), 0, st, g, w.start,
                        w.total, w.bkeys, w.skeys, w.subp, w.maps);
     TW_LAUNCH_CHECK();
   } else {  // no z: every image is 0
