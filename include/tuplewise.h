@@ -615,6 +615,18 @@ int tw_np_randint_pairs(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int6
  * out is (S, 2, N, B) int64 — out[s][0] the step's X indices, out[s][1] its Z indices. */
 int tw_np_randint_pairs_steps(uint32_t* key, int32_t* pos, int32_t S, int32_t N, int64_t kx,
                               int64_t kz, int64_t B, int64_t* out);
+/* The same draws narrowed to uint16 (needs kx, kz <= 65536): a quarter of the bytes for the
+ * replay loop's host-to-device copy; tw_widen_u16 restores the int64 indices on the device. */
+int tw_np_randint_pairs_steps_u16(uint32_t* key, int32_t* pos, int32_t S, int32_t N,
+                                  int64_t kx, int64_t kz, int64_t B, uint16_t* out);
+/* d_out[i] = d_in[i] (uint16 -> int64) for i < n, on `stream`; d_in may be the device address
+ * of pinned host memory (tw_host_device_pointer): the kernel then reads it over PCIe. */
+int tw_widen_u16(const uint16_t* d_in, int64_t n, int64_t* d_out, void* stream);
+/* n 8-byte words d_in -> d_out on `stream` (d_in may be mapped host memory, as above). */
+int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
+/* The device address of pinned, mapped host memory (hipHostGetDevicePointer); TW_ERR_ARG when
+ * `host` is not such memory. */
+int tw_host_device_pointer(void* host, void** out_dev);
 /* np.random.shuffle(x); np.random.shuffle(z) — the in-place shuffles of UN
  * (compute_stats.py:66-67, estimation-experiment/main.py:46-47) — on C-contiguous arrays of
  * nx / nz items of isx / isz bytes (rows of a 2-D array are items): legacy RandomState's

@@ -112,3 +112,22 @@ def test_reference_shape_device_rng_segments(gpu, golden, mod, monkeypatch):
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert out[True][k] == out[False][k], k
         assert len(out[True][k]) == 10 and np.all(np.isfinite(out[True][k]))
+
+
+@pytest.mark.parametrize("mod", MODS)
+def test_reference_shape_draw_ahead_equals_sequential(gpu, golden, mod, monkeypatch):
+    """learning.DRAW_AHEAD (the replay draws made two segments ahead by a worker thread): the
+    same evaluation lists and final NumPy RNG state as the sequential loop, bit for bit."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for ahead in (True, False):
+        monkeypatch.setattr(lr, "DRAW_AHEAD", ahead)
+        X, Z, p = _p(mod)
+        np.random.seed(3000 + mod)
+        lr.learning_process(X, Z, p)
+        _check_lists(p, golden, mod)
+        out[ahead] = (p, np.random.get_state()[1].copy())
+    for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        assert out[True][0][k] == out[False][0][k], k
+    assert np.array_equal(out[True][1], out[False][1])

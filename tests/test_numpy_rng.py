@@ -265,3 +265,24 @@ def test_session_pairs_steps_match_per_step_draws(tw):
     with Session() as sess:
         sess.pairs_steps(S, N, kx, kz, B, out)
     assert np.array_equal(out[:S], want) and np.random.random() == probe
+
+
+@pytest.mark.parametrize("kx,kz", [(91, 7), (65536, 3), (40000, 65535)])
+def test_session_pairs_steps_u16_match_int64(tw, kx, kz):
+    """Session.pairs_steps_u16 (the replay loop's narrowed draws, tw_np_randint_pairs_steps_u16)
+    == the int64 draws of pairs_steps, value for value, and leaves the same RNG state; ranges
+    beyond 65536 are refused."""
+    from tuplewise.numpy_rng import Session
+    S, N, B = 5, 4, 37
+    np.random.seed(23)
+    want = np.empty((S, 2, N, B), np.int64)
+    with Session() as sess:
+        sess.pairs_steps(S, N, kx, kz, B, want)
+    probe = np.random.random()
+    np.random.seed(23)
+    got = np.empty((S, 2, N, B), np.uint16)
+    with Session() as sess:
+        sess.pairs_steps_u16(S, N, kx, kz, B, got)
+    assert np.array_equal(got.astype(np.int64), want) and np.random.random() == probe
+    with Session() as sess, pytest.raises(ValueError):
+        sess.pairs_steps_u16(1, N, 65537, kz, B, got)

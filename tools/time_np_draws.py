@@ -16,6 +16,11 @@ best = 1e9
 for _ in range(30):
     t0 = time.perf_counter(); s.pairs_steps(25, 100, 91, 7, 100, out); best = min(best, time.perf_counter() - t0)
 print("%.2f us/step" % (best / 25 * 1e6))
+o16 = np.empty((25, 2, 100, 100), np.uint16)
+best = 1e9
+for _ in range(30):
+    t0 = time.perf_counter(); s.pairs_steps_u16(25, 100, 91, 7, 100, o16); best = min(best, time.perf_counter() - t0)
+print("uint16 %.2f us/step" % (best / 25 * 1e6))
 '''
 for label, env in (("widest", {}), ("avx2", {"TW_NP_RNG_ISA": "avx2"}),
                    ("portable", {"TW_NP_RNG_SCALAR": "1"})):

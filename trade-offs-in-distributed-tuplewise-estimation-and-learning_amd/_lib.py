@@ -133,6 +133,10 @@ _SIGNATURES = {
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],
     "tw_np_randint_pairs_steps": [_vp, _vp, _i32, _i32, _i64, _i64, _i64, _vp],
+    "tw_np_randint_pairs_steps_u16": [_vp, _vp, _i32, _i32, _i64, _i64, _i64, _vp],
+    "tw_widen_u16": [_vp, _i64, _vp, _vp],
+    "tw_copy_words": [_vp, _i64, _vp, _vp],
+    "tw_host_device_pointer": [_vp, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],
     "tw_shuffle_swaps_work_bytes": [_i64, _i64],
@@ -217,6 +221,14 @@ def device():
 
 def stream_handle():
     return ctypes.c_void_p(torch().cuda.current_stream().cuda_stream)
+
+
+def host_device_pointer(t):
+    """The device address of a pinned host tensor's storage (None when it is not mapped)."""
+    out = ctypes.c_void_p()
+    if lib().tw_host_device_pointer(ctypes.c_void_p(t.data_ptr()), ctypes.byref(out)) != TW_OK:
+        return None
+    return out.value
 
 
 def ptr(t) -> ctypes.c_void_p:

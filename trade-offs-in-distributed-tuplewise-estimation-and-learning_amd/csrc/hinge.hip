@@ -715,6 +715,41 @@ extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
                       margin, TW_LOSS_HINGE, d_out, stream);
 }
 
+// Replay draws arrive narrowed to uint16 (tw_np_randint_pairs_steps_u16): widened here, in
+// stream order, into the int64 buffer the segment graphs read.
+static __global__ __launch_bounds__(256) void k_widen_u16(const uint16_t* __restrict__ in,
+                                                          int64_t n, int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = (int64_t)in[i];
+}
+
+extern "C" int tw_widen_u16(const uint16_t* d_in, int64_t n, int64_t* d_out, void* stream) {
+  TW_ARG_CHECK(n >= 0, "tw_widen_u16: n < 0");
+  if (n == 0) return TW_OK;
+  const unsigned g = (unsigned)std::min<int64_t>(2048, ceil_div(n, 256));
+  hipLaunchKernelGGL(k_widen_u16, dim3(g), dim3(256), 0, (hipStream_t)stream, d_in, n, d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+// 8-byte words from a (host-mapped) staging buffer into device memory: the replay loop's SWR
+// row tables, read by the kernel straight from pinned host memory.
+static __global__ __launch_bounds__(256) void k_copy_words(const uint64_t* __restrict__ in,
+                                                           int64_t n, uint64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = in[i];
+}
+
+extern "C" int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream) {
+  TW_ARG_CHECK(n >= 0, "tw_copy_words: n < 0");
+  if (n == 0) return TW_OK;
+  const unsigned g = (unsigned)std::min<int64_t>(1024, ceil_div(n, 256));
+  hipLaunchKernelGGL(k_copy_words, dim3(g), dim3(256), 0, (hipStream_t)stream,
+                     (const uint64_t*)d_in, n, (uint64_t*)d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 extern "C" int tw_hinge_set_variant(int32_t legacy_wide) {
   TW_ARG_CHECK(legacy_wide >= 0 && legacy_wide <= 2, "tw_hinge_set_variant: 0, 1 or 2");
   g_hinge_legacy_wide = legacy_wide;

@@ -27,6 +27,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <thread>
+#include <vector>
 
 #define TW_INLINE inline __attribute__((always_inline))
 
@@ -532,6 +533,61 @@ void shuffle_draws_isa(MT& mt, int64_t n, J* j, int isa) {
     shuffle_draws<0>(mt, n, j);
 }
 
+// grad_inc_block's draws straight into uint16 outputs (ranges <= 65536) with AVX-512 VBMI2:
+// the masked words of a 16-lane batch are narrowed (vpmovdw), the accepted lanes compressed in
+// a register (vpcompressw) and stored with a lane mask — no int64 widening and no narrowing pass
+// afterwards.  Same words consumed, same values as fill_masked16.
+__attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) inline void
+fill_masked16_u16(MT& mt, uint32_t mask, uint32_t r32, int64_t cnt, uint16_t* out) {
+  const __m512i vm = _mm512_set1_epi32((int)mask);
+  const __m512i vr = _mm512_set1_epi32((int)r32);
+  int64_t o = 0;
+  while (o < cnt) {
+    if (mt.pos >= kN) generate_isa<2>(mt);
+    mt.temper_rest();
+    int p = mt.pos;
+    while (p < kN && o < cnt) {
+      const int avail = kN - p;
+      const __mmask16 lm = avail >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << avail) - 1u);
+      const __m512i v = _mm512_and_si512(_mm512_maskz_loadu_epi32(lm, mt.tmp + p), vm);
+      uint32_t acc = (uint32_t)_mm512_mask_cmple_epu32_mask(lm, v, vr);
+      const int64_t rem = cnt - o;
+      int na = __builtin_popcount(acc);
+      int used = avail >= 16 ? 16 : avail;
+      if (na >= rem) {  // the call ends inside this batch: at its rem-th accepted word
+        if (na > rem) acc = _pdep_u32((1u << rem) - 1u, acc);
+        na = (int)rem;
+        used = 32 - __builtin_clz(acc);
+      }
+      const __m256i packed = _mm256_maskz_compress_epi16((__mmask16)acc, _mm512_cvtepi32_epi16(v));
+      _mm256_mask_storeu_epi16((void*)(out + o), (__mmask16)((1u << na) - 1u), packed);
+      o += na;
+      p += used;
+    }
+    mt.pos = p;
+  }
+}
+
+__attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) void
+pairs_u16_avx512(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B,
+                 uint16_t* ix, uint16_t* iz) {
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  for (int32_t s = 0; s < N; ++s) {
+    for (int side = 0; side < 2; ++side) {
+      const uint64_t rng = (uint64_t)((side ? kz : kx) - 1);
+      uint16_t* o = (side ? iz : ix) + (int64_t)s * B;
+      if (rng == 0) {  // randint(0, 1): no draw, all zeros (as randint_fill)
+        for (int64_t i = 0; i < B; ++i) o[i] = 0;
+      } else {
+        fill_masked16_u16(mt, (uint32_t)gen_mask(rng), (uint32_t)rng, B, o);
+      }
+    }
+  }
+  *pos = mt.pos;
+}
+
 // SIMD level chosen once at run time: 2 AVX-512 (F + VL) + BMI2, 1 AVX2, 0 portable.
 // TW_NP_RNG_SCALAR=1 forces the portable path, TW_NP_RNG_ISA=avx2 caps it at AVX2 (tests run
 // every level against NumPy).
@@ -548,6 +604,14 @@ int isa_level() {
                ? 2
                : 1;
   }();
+  return v;
+}
+
+// the uint16 pair draws above (AVX-512 level plus BW + VBMI2; TW_NP_RNG_ISA / _SCALAR caps
+// apply through isa_level)
+bool has_vbmi2() {
+  static const bool v = isa_level() == 2 && __builtin_cpu_supports("avx512bw") &&
+                        __builtin_cpu_supports("avx512vbmi2");
   return v;
 }
 
@@ -592,6 +656,32 @@ int tw_np_randint_pairs_steps(uint32_t* key, int32_t* pos, int32_t S, int32_t N,
     int64_t* o = out + (int64_t)st * 2 * per;
     const int rc = tw_np_randint_pairs(key, pos, N, kx, kz, B, o, o + per);
     if (rc) return rc;
+  }
+  return 0;
+}
+
+// The same S steps narrowed to uint16 (kx, kz <= 65536: every index < 65536), for a quarter
+// of the bytes on the way to the device (the replay loop's H2D copy; tw_widen_u16 restores
+// int64 there).  Each step is drawn into a thread-local int64 scratch, then narrowed.
+int tw_np_randint_pairs_steps_u16(uint32_t* key, int32_t* pos, int32_t S, int32_t N, int64_t kx,
+                                  int64_t kz, int64_t B, uint16_t* out) {
+  if (kx <= 0 || kz <= 0 || kx > 65536 || kz > 65536 || S < 0 || N < 0 || B < 0) return 1;
+  const int64_t per = (int64_t)N * B;
+  if (has_vbmi2()) {
+    for (int32_t st = 0; st < S; ++st) {
+      uint16_t* o = out + (int64_t)st * 2 * per;
+      pairs_u16_avx512(key, pos, N, kx, kz, B, o, o + per);
+    }
+    return 0;
+  }
+  static thread_local std::vector<int64_t> scratch;
+  scratch.resize((size_t)(2 * per));
+  for (int32_t st = 0; st < S; ++st) {
+    const int rc = tw_np_randint_pairs(key, pos, N, kx, kz, B, scratch.data(),
+                                       scratch.data() + per);
+    if (rc) return rc;
+    uint16_t* o = out + (int64_t)st * 2 * per;
+    for (int64_t i = 0; i < 2 * per; ++i) o[i] = (uint16_t)scratch[(size_t)i];
   }
   return 0;
 }

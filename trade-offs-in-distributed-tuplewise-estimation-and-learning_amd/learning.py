@@ -31,6 +31,9 @@ SEED_SHUFFLE = 42
 # narrow rows (C4): a segment of fused steps in ONE persistent launch (tw_sgd_segment_narrow:
 # one grid barrier per step, the update recomputed in every block); off: one launch per step
 NARROW_SEGMENT = True
+# replay loop: the host's NumPy-exact draws made two segments ahead by a worker thread
+# (_replay_pipelined); False keeps the sequential loop (A/B, tests)
+DRAW_AHEAD = True
 # evaluations of the learning loop: device part enqueued, host part once the results are back
 # (no device wait per evaluation); off: evaluation_step waits for its results
 DEFER_EVALS = True
@@ -230,6 +233,29 @@ class SGDEngine:
         self.rows_z.copy_(hz, non_blocking=True)
         self._rows_done = t.cuda.Event()
         self._rows_done.record()
+
+    def set_shards_staged(self, staged):
+        """set_shards from rows already in pinned host tensors (the pipelined replay loop's
+        staging ring, flat (N*kx + N*kz,)): two asynchronous copies of this engine's shards
+        into the persistent tables; the caller keeps the staging buffer until they have run.
+        False where the layout needs the host path (set_shards)."""
+        if self.layout == "partitioned" or self.rows_x is None:
+            return False
+        flat, hdev = staged
+        nx = self.N * self.kx
+        a = self.shard_base
+        if hdev is not None:  # the copy kernel reads the pinned buffer in place
+            st = L.stream_handle()
+            L.call("tw_copy_words", ctypes.c_void_p(hdev + 8 * a * self.kx),
+                   self.N_loc * self.kx, L.ptr(self.rows_x), st)
+            L.call("tw_copy_words", ctypes.c_void_p(hdev + 8 * (nx + a * self.kz)),
+                   self.N_loc * self.kz, L.ptr(self.rows_z), st)
+            return True
+        self.rows_x.view(-1).copy_(flat[a * self.kx:(a + self.N_loc) * self.kx],
+                                   non_blocking=True)
+        self.rows_z.view(-1).copy_(flat[nx + a * self.kz:nx + (a + self.N_loc) * self.kz],
+                                   non_blocking=True)
+        return True
 
     def _records(self, name, rows, expect):
         """Persistent (rows, d+1) record buffer for the row exchange, kept across reshuffles
@@ -698,16 +724,45 @@ class _ReplayDraws:
         self.k = 0
         self.rng = Session()
 
-    def swr_rows(self, n_X, n_Z):
+    def _swr_setup(self, n_X, n_Z):
+        """SWR_divide's randint arguments: N calls on [0, n_X) of kx draws, then N on [0, n_Z)."""
         N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
         if getattr(self, "_swr_args", (None,))[0] != (N, n_X, n_Z, kx, kz):
             self._swr_args = ((N, n_X, n_Z, kx, kz), np.zeros(2 * N, np.int64),
                               np.array([n_X] * N + [n_Z] * N, np.int64),
                               np.array([kx] * N + [kz] * N, np.int64))
-        flat = self.rng.randint_flat(*self._swr_args[1:])
+        return self._swr_args[1:]
+
+    def swr_rows(self, n_X, n_Z):
+        N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
+        flat = self.rng.randint_flat(*self._swr_setup(n_X, n_Z))
         # (N, kx) and (N, kz) arrays: row s is shard s's draw (indexable like the list of
         # arrays SWR_divide returns)
         return flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, kz)
+
+    def swr_rows_staged(self, k, n_X, n_Z):
+        """swr_rows drawn straight into pinned row buffer k of the pipelined loop (ring of 3,
+        reused once the upload out of it has finished): (rows_x, rows_z) host views and the
+        pinned tensors."""
+        t = L.torch()
+        N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
+        if getattr(self, "rows3", None) is None or self.rows3[0][0].shape != (N * kx + N * kz,):
+            self.rows3 = [(t.empty((N * kx + N * kz,), dtype=t.int64, pin_memory=True),
+                           t.cuda.Event()) for _ in range(3)]
+            self.rows3_used = [False] * 3
+            self.rows3_hdev = [L.host_device_pointer(b) for b, _ in self.rows3]
+        buf, ev = self.rows3[k]
+        if self.rows3_used[k]:
+            ev.synchronize()
+        flat = buf.numpy()
+        self.rng.randint_flat(*self._swr_setup(n_X, n_Z), out=flat)
+        return (flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, kz)), (buf,
+                                                                             self.rows3_hdev[k])
+
+    def rows_uploaded(self, k):
+        """Main side: the upload out of pinned row buffer k has been enqueued."""
+        self.rows3[k][1].record()
+        self.rows3_used[k] = True
 
     def segment_capacity(self) -> int:
         """Steps per drawn segment: <= 256, and <= 64 MiB of int64 draws per buffer."""
@@ -737,6 +792,60 @@ class _ReplayDraws:
             self.seg_done[k] = t.cuda.Event()
         self.seg_done[k].record()
         return self.seg_dev[k], k
+
+    def _seg_buffers(self, nbuf):
+        """Pinned draw buffers of the pipelined loop: uint16 when every index fits (a quarter
+        of the H2D bytes: at C4 a 25-step segment's draws are 4 MB as int64, the copy then
+        as long as the segment's kernels), widened on the device into the int64 buffers the
+        segment graphs read."""
+        t = L.torch()
+        if getattr(self, "seg3_host", None) is None:
+            cap = self.segment_capacity()
+            shape = (cap, 2, self.N, self.B)
+            self.seg3_u16 = self.kx <= 65536 and self.kz <= 65536
+            hdt = t.int16 if self.seg3_u16 else t.int64  # int16 storage holds the uint16 bits
+            self.seg3_host = [t.empty(shape, dtype=hdt, pin_memory=True) for _ in range(nbuf)]
+            self.seg3_np = [h.numpy().view(np.uint16) if self.seg3_u16 else h.numpy()
+                            for h in self.seg3_host]
+            self.seg3_stage = ([L.empty(shape, t.int16) for _ in range(nbuf)]
+                               if self.seg3_u16 else None)
+            self.seg3_dev = [L.empty(shape, t.int64) for _ in range(nbuf)]
+            self.seg3_done = [t.cuda.Event() for _ in range(nbuf)]
+            self.seg3_used = [False] * nbuf
+            # the widening kernel reads the pinned buffers in place (mapped host memory): one
+            # launch per segment instead of a copy call and a launch
+            self.seg3_hdev = [L.host_device_pointer(h) if self.seg3_u16 else None
+                              for h in self.seg3_host]
+
+    def fill_segment(self, k, S):
+        """Worker side of the pipelined replay loop: the next S steps' draws into pinned
+        buffer k, once the copy out of it (three segments back) has finished."""
+        self._seg_buffers(3)
+        if self.seg3_used[k]:
+            self.seg3_done[k].synchronize()
+        if self.seg3_u16:
+            self.rng.pairs_steps_u16(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
+        else:
+            self.rng.pairs_steps(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
+        return k
+
+    def ship_segment(self, k, S):
+        """Main side: the asynchronous H2D copy of buffer k (stream-ordered after the graph
+        that read its device copy three segments back), widened on the device when narrowed;
+        returns the int64 device buffer."""
+        if self.seg3_u16 and self.seg3_hdev[k] is not None:
+            L.call("tw_widen_u16", ctypes.c_void_p(self.seg3_hdev[k]),
+                   int(S) * 2 * self.N * self.B, L.ptr(self.seg3_dev[k]), L.stream_handle())
+        elif self.seg3_u16:
+            st = self.seg3_stage[k]
+            st[:S].copy_(self.seg3_host[k][:S], non_blocking=True)
+            L.call("tw_widen_u16", L.ptr(st), int(S) * 2 * self.N * self.B,
+                   L.ptr(self.seg3_dev[k]), L.stream_handle())
+        else:
+            self.seg3_dev[k][:S].copy_(self.seg3_host[k][:S], non_blocking=True)
+        self.seg3_done[k].record()
+        self.seg3_used[k] = True
+        return self.seg3_dev[k]
 
     def pairs(self):
         t = L.torch()
@@ -846,6 +955,10 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
         rows_x, rows_z = draws.swr_rows(n_X, n_Z)  # the reference's redundant draw (:119)
         eng.set_shards(rows_x, rows_z)
         n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
+        assert optim_type in ["SGD", "momentum"]
+        if trajectory is None and not eng.complete and DRAW_AHEAD:
+            _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, rows_z)
+            n_it = 0  # done
         i = 0
         while i < n_it:
             if i % mod == 0:
@@ -890,6 +1003,61 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     if defer is not None:
         defer.drain()
     return None
+
+
+def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, rows_z):
+    """The replay loop's segments (runs of steps up to the next reshuffle / evaluation, at most
+    segment_capacity() steps) with the host's NumPy-exact draws made AHEAD by a worker thread:
+    the draws of segment j + 2 (its SWR rows, make_exps.py:123-125, then its steps' pairs,
+    compute_stats.py:155-156 — the reference's order, one MT19937 stream) run in native code
+    (ctypes releases the GIL) while this thread uploads the row tables, evaluates and launches
+    segment j.  Three pinned draw buffers: the worker refills buffer k only after the H2D copy
+    of the segment that used it three segments back has finished.  Same draws, same
+    trajectory as the sequential loop (tests/test_gpu_learning*.py)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n_X, n_Z = X.shape[0], Z.shape[0]
+    n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
+    segs, i = [], 0
+    while i < n_it:
+        nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
+                  i + draws.segment_capacity())
+        segs.append((i, nxt, i % mod == 0))
+        i = nxt
+
+    staged = isinstance(eng, SGDEngine) and eng.layout == "replicated"
+
+    def work(idx):
+        a, b, resh = segs[idx]
+        rows = None
+        if resh:
+            rows = (draws.swr_rows_staged(idx % 3, n_X, n_Z) if staged
+                    else (draws.swr_rows(n_X, n_Z), None))
+        return rows, draws.fill_segment(idx % 3, b - a)
+
+    ahead = 2
+    draws._seg_buffers(3)  # on this thread: its current device and stream
+    with ThreadPoolExecutor(max_workers=1) as pool:
+        futs = [pool.submit(work, j) for j in range(min(ahead, len(segs)))]
+        for idx, (i, nxt, resh) in enumerate(segs):
+            rows, k = futs[idx].result()
+            if idx + ahead < len(segs):
+                futs.append(pool.submit(work, idx + ahead))
+            if rows is not None:
+                (rows_x, rows_z), pinned = rows
+                if pinned is not None and eng.set_shards_staged(pinned):
+                    draws.rows_uploaded(idx % 3)
+                else:
+                    eng.set_shards(rows_x, rows_z)
+            w_pending = None
+            if i % eval_mod == 0:
+                if defer is not None:  # device part enqueued now, host part later
+                    _evaluate(i, eng, None, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer)
+                else:
+                    w_pending = eng.w_host_async()
+            buf = draws.ship_segment(k, nxt - i)
+            if w_pending is not None:
+                _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
+            eng.run_replay_segment(buf, nxt - i, graphs, k)
 
 
 def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer=None):
