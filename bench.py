@@ -204,9 +204,21 @@ def sgd_complete_steps_per_s(n_X, n_Z, d, N, steps, loss="hinge"):
     dt = time.perf_counter() - t0
     pairs = N * eng.kx * eng.kz
     rows_bytes = 2 * N * (eng.kx + eng.kz) * d * 8  # scores pass + weighted column sums
+    # step floor = the two row passes at the HBM peak + the coefficient work at the f64 lane-op
+    # peak (hinge: binary searches, ~log2(k) lane-ops per point, negligible; logistic: 7.5 VALU
+    # per sigma, PMC-counted) -- serial phases, so the floors add
+    lane_ops = 7.5 * pairs if loss == "logistic" else 2 * N * (eng.kx + eng.kz) * 15
+    floor_s = rows_bytes / (HBM_PEAK_GBS * 1e9) + lane_ops / PEAK_LANE_OPS
+    t_step = dt / steps
     return {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
             "pairs_per_step": pairs, "pairs_per_s": pairs * steps / dt,
             "row_GBps": rows_bytes * steps / dt / 1e9,
+            "roofline": {"bound": "valu" if loss == "logistic" else "hbm",
+                         "floor_ms": floor_s * 1e3, "frac": floor_s / t_step,
+                         "hbm_bytes_per_step": rows_bytes, "lane_ops_per_step": lane_ops,
+                         "note": "frac = (row bytes / HBM peak + coefficient lane-ops / f64 "
+                                 "lane-op peak) / measured step; logistic counts 7.5 VALU per "
+                                 "sigma (PMC), hinge ~15 per point (binary searches)"},
             "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "loss": loss,
                        "gradient": "complete (per-point pair coefficients + X^T c)",
                        "steps": steps}}
@@ -325,7 +337,9 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
                     "as a reference script calls it): host draws in the reference's order, the "
                     "shuffles' swaps on the device (csrc/devshuffle.hip), the caller's arrays "
                     "written back; parts timed alone on the same shapes",
-            "ms_per_call": dt * 1e3, "value": pairs / dt, "unit": "pairs/s",
+            "ms_per_call": dt * 1e3, "value": pairs / dt,
+            # the sorted count decides every pair without comparing it: logical pairs
+            "unit": "logical pairs/s" if algo == "sorted" else "pairs/s",
             "host_swap_path_ms_per_call": dt_host * 1e3,
             "same_value_both_paths": bool(v == v_host),
             "slots_0_0_ms_per_call": dt_slots * 1e3,
@@ -1140,7 +1154,18 @@ def main():
             "value": total_pairs / dt_sorted, "unit": "logical pairs/s",
             "ms_per_step": dt_sorted / args.steps * 1e3, "count_kernels_ms": kms_sorted,
             "estimate_last_step": float(est_sorted),
-            "counts_identical_to_all_pairs": same_counts},
+            "counts_identical_to_all_pairs": same_counts,
+            # algorithmic bytes per step: every record {8-B value, 4-B position} of both samples
+            # read once and written once to its next bucket (csrc/records.h)
+            # (one GPU: the K steps are one records launch; over ranks the count is per step)
+            "roofline": None if world > 1 else {
+                         "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "bytes_per_element": 24,
+                         "achieved": 24 * 2 * n / (kms_sorted * 1e-3) / 1e9,
+                         "frac": 24 * 2 * n / (kms_sorted * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "count_kernels_ms per step against 24 B per element; the step "
+                                 "is latency-bound (Feistel + load/atomic/store chain, DESIGN "
+                                 "4.6), not bandwidth-bound"}},
         "incomplete": {
             "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
                     "drawn pairs per shard (Philox4x32-10, two pairs per block, Lemire maps) "

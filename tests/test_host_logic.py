@@ -143,6 +143,13 @@ def test_multi_device_split_and_device_list(monkeypatch):
         assert M.slots_for(1 << 40, 5) == [2, 3]
     finally:
         M.set_devices(None)
+    # one rank of a torchrun job: only its own GPU, never the other ranks'
+    monkeypatch.delenv("TW_DEVICES")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    import torch
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 5)
+    assert M.devices() == [5]
+    assert M.slots_for(1 << 40, 5) is None
 
 
 def test_learning_engine_device_selection(monkeypatch):

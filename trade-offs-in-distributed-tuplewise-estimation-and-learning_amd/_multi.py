@@ -11,7 +11,8 @@ are distinct devices (tw_allgather_u64 / _f64, csrc/comm.hip), else by host copi
 are identical to one device: every block is computed by the same kernel on the same data.
 
 Devices: set_devices([...]) or TW_DEVICES="0,1,..." (a device may repeat: two slots on one GPU
-get two streams — how the path is tested on a one-GPU box); default: all visible devices.
+get two streams — how the path is tested on a one-GPU box); default: all visible devices, or
+only the current one inside a multi-process launch (LOCAL_WORLD_SIZE / WORLD_SIZE > 1).
 Calls whose work is below MIN_WORK (pair compares) stay on the current device.
 """
 from __future__ import annotations
@@ -48,6 +49,9 @@ def devices() -> list:
     env = os.environ.get("TW_DEVICES")
     if env:
         return [int(v) for v in env.split(",") if v.strip()]
+    if int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))) > 1:
+        # one process per GPU (torchrun): the other GPUs belong to the other ranks
+        return [L.torch().cuda.current_device()]
     n = L.torch().cuda.device_count()
     return list(range(n)) if n > 0 else [0]
 
