@@ -619,9 +619,15 @@ int tw_np_randint_pairs_steps(uint32_t* key, int32_t* pos, int32_t S, int32_t N,
  * replay loop's host-to-device copy; tw_widen_u16 restores the int64 indices on the device. */
 int tw_np_randint_pairs_steps_u16(uint32_t* key, int32_t* pos, int32_t S, int32_t N,
                                   int64_t kx, int64_t kz, int64_t B, uint16_t* out);
+/* The same draws narrowed to uint8 (needs kx, kz <= 256): half the bytes of the uint16 form. */
+int tw_np_randint_pairs_steps_u8(uint32_t* key, int32_t* pos, int32_t S, int32_t N,
+                                 int64_t kx, int64_t kz, int64_t B, uint8_t* out);
 /* d_out[i] = d_in[i] (uint16 -> int64) for i < n, on `stream`; d_in may be the device address
- * of pinned host memory (tw_host_device_pointer): the kernel then reads it over PCIe. */
+ * of pinned host memory (tw_host_device_pointer): the kernel then reads it over PCIe, 16 B per
+ * lane when d_in is 16-B aligned. */
 int tw_widen_u16(const uint16_t* d_in, int64_t n, int64_t* d_out, void* stream);
+/* The same for uint8 indices. */
+int tw_widen_u8(const uint8_t* d_in, int64_t n, int64_t* d_out, void* stream);
 /* n 8-byte words d_in -> d_out on `stream` (d_in may be mapped host memory, as above). */
 int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
 /* The device address of pinned, mapped host memory (hipHostGetDevicePointer); TW_ERR_ARG when

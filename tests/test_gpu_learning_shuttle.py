@@ -131,3 +131,49 @@ def test_reference_shape_draw_ahead_equals_sequential(gpu, golden, mod, monkeypa
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert out[True][0][k] == out[False][0][k], k
     assert np.array_equal(out[True][1], out[False][1])
+
+
+def test_engine_cache_reuse(gpu, golden, monkeypatch):
+    """learning.ENGINE_CACHE: a second replay call of the same shapes reuses the engine (its
+    buffers, draw buffers and captured segment graphs) and still gives the reference's lists;
+    a call on other rows of the same shapes equals a fresh engine's bit for bit, also after a
+    device-RNG run and a call of other shapes in between."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    monkeypatch.setattr(lr, "ENGINE_CACHE", True)
+    mod = 10000
+    X, Z, p = _p(mod)
+    np.random.seed(3000 + mod)
+    lr.learning_process(X, Z, p)
+    _check_lists(p, golden, mod)
+    eng = lr._ENGINE["eng"]
+    assert eng is not None and getattr(eng, "_draws", None) is not None
+    X, Z, p = _p(mod)
+    np.random.seed(3000 + mod)
+    lr.learning_process(X, Z, p)
+    _check_lists(p, golden, mod)
+    assert lr._ENGINE["eng"] is eng
+
+    def other(seed):
+        X, Z, p = _p(mod)
+        r = np.random.RandomState(seed)
+        X2, Z2 = X + 0.1 * r.normal(size=X.shape), Z - 0.1 * r.normal(size=Z.shape)
+        p = dict(p, train_X=X2, train_Z=Z2, w_init=p["w_init"] * 0.5)
+        np.random.seed(seed)
+        lr.learning_process(X2, Z2, p)
+        return p, np.random.get_state()[1].copy()
+
+    a = other(7)
+    assert lr._ENGINE["eng"] is eng
+    X, Z, p = _p(mod)
+    np.random.seed(8)
+    lr.learning_process(X, Z, p, rng_mode="device")
+    Xs, Zs, ps = _p(mod, n_it=30)
+    np.random.seed(9)
+    lr.learning_process(Xs[:5000], Zs[:500], dict(ps, N=50, B=20))
+    b = other(7)
+    monkeypatch.setattr(lr, "ENGINE_CACHE", False)
+    c = other(7)
+    for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        assert a[0][k] == b[0][k] == c[0][k], k
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[1], c[1])

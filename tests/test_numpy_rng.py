@@ -92,6 +92,10 @@ def test_scalar_path_matches_numpy(tw, env):
         "np.random.seed(3); ix=np.empty((40,100),np.int64); iz=np.empty((40,100),np.int64)\n"
         "s=Session(); s.pairs(40,91,7,100,ix,iz); s.commit()\n"
         "assert np.array_equal(ix, np.stack(w[0::2])) and np.array_equal(iz, np.stack(w[1::2]))\n"
+        "np.random.seed(3); o8=np.empty((4,2,10,100),np.uint8); o16=np.empty((4,2,10,100),np.uint16)\n"
+        "s=Session(); s.pairs_steps_u8(4,10,91,7,100,o8); s.commit()\n"
+        "np.random.seed(3); s=Session(); s.pairs_steps_u16(4,10,91,7,100,o16); s.commit()\n"
+        "assert np.array_equal(o8[:, 0].reshape(40, 100), ix) and np.array_equal(o16, o8)\n"
         "from tuplewise.numpy_rng import shuffle_pair\n"
         "X=np.arange(70001.0); Z=np.arange(3000.0); X1=X.copy(); Z1=Z.copy()\n"
         "np.random.seed(8); np.random.shuffle(X1); np.random.shuffle(Z1); p=np.random.rand()\n"
@@ -286,3 +290,24 @@ def test_session_pairs_steps_u16_match_int64(tw, kx, kz):
     assert np.array_equal(got.astype(np.int64), want) and np.random.random() == probe
     with Session() as sess, pytest.raises(ValueError):
         sess.pairs_steps_u16(1, N, 65537, kz, B, got)
+
+
+@pytest.mark.parametrize("kx,kz", [(91, 7), (256, 1), (2, 256), (200, 129)])
+def test_session_pairs_steps_u8_match_int64(tw, kx, kz):
+    """Session.pairs_steps_u8 (the replay loop's uint8 draws, tw_np_randint_pairs_steps_u8, the
+    C4 shape's default) == the int64 draws of pairs_steps, value for value, and leaves the same
+    RNG state; ranges beyond 256 are refused."""
+    from tuplewise.numpy_rng import Session
+    S, N, B = 5, 4, 37
+    np.random.seed(29)
+    want = np.empty((S, 2, N, B), np.int64)
+    with Session() as sess:
+        sess.pairs_steps(S, N, kx, kz, B, want)
+    probe = np.random.random()
+    np.random.seed(29)
+    got = np.empty((S, 2, N, B), np.uint8)
+    with Session() as sess:
+        sess.pairs_steps_u8(S, N, kx, kz, B, got)
+    assert np.array_equal(got.astype(np.int64), want) and np.random.random() == probe
+    with Session() as sess, pytest.raises(ValueError):
+        sess.pairs_steps_u8(1, N, 257, kz, B, got)

@@ -45,6 +45,20 @@ lr.learning_process(X, Z, dict(p, n_it=50))
 full, ts = timed(lambda: lr.learning_process(X, Z, p))
 print(f"full      {STEPS / full:9.0f} steps/s  {full * 1e3:7.2f} ms  runs "
       + " ".join(f"{STEPS / t:.0f}" for t in ts), flush=True)
+lr.NARROW_DRAWS_U8 = False
+u16, ts = timed(lambda: lr.learning_process(X, Z, p))
+print(f"u16       {STEPS / u16:9.0f} steps/s  {u16 * 1e3:7.2f} ms  runs "
+      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (NARROW_DRAWS_U8 off)", flush=True)
+lr.NARROW_DRAWS_U8 = True
+lr.ENGINE_CACHE = False
+off, ts = timed(lambda: lr.learning_process(X, Z, p))
+print(f"fresh     {STEPS / off:9.0f} steps/s  {off * 1e3:7.2f} ms  runs "
+      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (ENGINE_CACHE off: a new engine per call)",
+      flush=True)
+one, _ = timed(lambda: lr.learning_process(X, Z, dict(p, n_it=1)))
+print(f"fresh one n_it=1:  {one * 1e3:7.3f} ms per call", flush=True)
+lr.ENGINE_CACHE = True
+lr.learning_process(X, Z, p)
 short, _ = timed(lambda: lr.learning_process(X, Z, dict(p, n_it=25)))
 print(f"short     n_it=25: {short * 1e3:7.3f} ms per call", flush=True)
 one, _ = timed(lambda: lr.learning_process(X, Z, dict(p, n_it=1)))

@@ -715,21 +715,44 @@ extern "C" int tw_hinge_grad(const double* d_X, const double* d_Z, int64_t d,
                       margin, TW_LOSS_HINGE, d_out, stream);
 }
 
-// Replay draws arrive narrowed to uint16 (tw_np_randint_pairs_steps_u16): widened here, in
-// stream order, into the int64 buffer the segment graphs read.
-static __global__ __launch_bounds__(256) void k_widen_u16(const uint16_t* __restrict__ in,
-                                                          int64_t n, int64_t* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+// Replay draws arrive narrowed to uint16 / uint8 (tw_np_randint_pairs_steps_u16 / _u8): widened
+// here, in stream order, into the int64 buffer the segment graphs read.  The source is usually
+// pinned host memory read in place over PCIe, so every lane reads 16 B (8 or 16 indices): few,
+// wide requests; a tail of < 16 B (or a misaligned source) goes element by element.
+template <typename T>
+static __global__ __launch_bounds__(256) void k_widen(const T* __restrict__ in, int64_t n,
+                                                      int64_t* __restrict__ out) {
+  constexpr int kPer = 16 / (int)sizeof(T);
+  const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  const int64_t nv = vec ? n / kPer : 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
+    const uint4 v = reinterpret_cast<const uint4*>(in)[i];
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) out[i * kPer + k] = (int64_t)e[k];
+  }
+  for (int64_t i = nv * kPer + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
     out[i] = (int64_t)in[i];
+}
+
+template <typename T>
+static int widen(const T* d_in, int64_t n, int64_t* d_out, void* stream) {
+  if (n == 0) return TW_OK;
+  const unsigned g = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256 * (16 / (int64_t)sizeof(T)))));
+  hipLaunchKernelGGL(k_widen<T>, dim3(g), dim3(256), 0, (hipStream_t)stream, d_in, n, d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
 }
 
 extern "C" int tw_widen_u16(const uint16_t* d_in, int64_t n, int64_t* d_out, void* stream) {
   TW_ARG_CHECK(n >= 0, "tw_widen_u16: n < 0");
-  if (n == 0) return TW_OK;
-  const unsigned g = (unsigned)std::min<int64_t>(2048, ceil_div(n, 256));
-  hipLaunchKernelGGL(k_widen_u16, dim3(g), dim3(256), 0, (hipStream_t)stream, d_in, n, d_out);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+  return widen(d_in, n, d_out, stream);
+}
+
+extern "C" int tw_widen_u8(const uint8_t* d_in, int64_t n, int64_t* d_out, void* stream) {
+  TW_ARG_CHECK(n >= 0, "tw_widen_u8: n < 0");
+  return widen(d_in, n, d_out, stream);
 }
 
 // 8-byte words from a (host-mapped) staging buffer into device memory: the replay loop's SWR

@@ -588,6 +588,59 @@ pairs_u16_avx512(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz,
   *pos = mt.pos;
 }
 
+// fill_masked16_u16 with uint8 output (every value < 256): the same words consumed, the same
+// values, a byte compress instead of a word compress.
+__attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) inline void
+fill_masked16_u8(MT& mt, uint32_t mask, uint32_t r32, int64_t cnt, uint8_t* out) {
+  const __m512i vm = _mm512_set1_epi32((int)mask);
+  const __m512i vr = _mm512_set1_epi32((int)r32);
+  int64_t o = 0;
+  while (o < cnt) {
+    if (mt.pos >= kN) generate_isa<2>(mt);
+    mt.temper_rest();
+    int p = mt.pos;
+    while (p < kN && o < cnt) {
+      const int avail = kN - p;
+      const __mmask16 lm = avail >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << avail) - 1u);
+      const __m512i v = _mm512_and_si512(_mm512_maskz_loadu_epi32(lm, mt.tmp + p), vm);
+      uint32_t acc = (uint32_t)_mm512_mask_cmple_epu32_mask(lm, v, vr);
+      const int64_t rem = cnt - o;
+      int na = __builtin_popcount(acc);
+      int used = avail >= 16 ? 16 : avail;
+      if (na >= rem) {  // the call ends inside this batch: at its rem-th accepted word
+        if (na > rem) acc = _pdep_u32((1u << rem) - 1u, acc);
+        na = (int)rem;
+        used = 32 - __builtin_clz(acc);
+      }
+      const __m128i packed = _mm_maskz_compress_epi8((__mmask16)acc, _mm512_cvtepi32_epi8(v));
+      _mm_mask_storeu_epi8((void*)(out + o), (__mmask16)((1u << na) - 1u), packed);
+      o += na;
+      p += used;
+    }
+    mt.pos = p;
+  }
+}
+
+__attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) void
+pairs_u8_avx512(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B,
+                uint8_t* ix, uint8_t* iz) {
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  for (int32_t s = 0; s < N; ++s) {
+    for (int side = 0; side < 2; ++side) {
+      const uint64_t rng = (uint64_t)((side ? kz : kx) - 1);
+      uint8_t* o = (side ? iz : ix) + (int64_t)s * B;
+      if (rng == 0) {  // randint(0, 1): no draw, all zeros (as randint_fill)
+        for (int64_t i = 0; i < B; ++i) o[i] = 0;
+      } else {
+        fill_masked16_u8(mt, (uint32_t)gen_mask(rng), (uint32_t)rng, B, o);
+      }
+    }
+  }
+  *pos = mt.pos;
+}
+
 // SIMD level chosen once at run time: 2 AVX-512 (F + VL) + BMI2, 1 AVX2, 0 portable.
 // TW_NP_RNG_SCALAR=1 forces the portable path, TW_NP_RNG_ISA=avx2 caps it at AVX2 (tests run
 // every level against NumPy).
@@ -682,6 +735,30 @@ int tw_np_randint_pairs_steps_u16(uint32_t* key, int32_t* pos, int32_t S, int32_
     if (rc) return rc;
     uint16_t* o = out + (int64_t)st * 2 * per;
     for (int64_t i = 0; i < 2 * per; ++i) o[i] = (uint16_t)scratch[(size_t)i];
+  }
+  return 0;
+}
+
+// The same S steps narrowed to uint8 (kx, kz <= 256): half the bytes of the uint16 form.
+int tw_np_randint_pairs_steps_u8(uint32_t* key, int32_t* pos, int32_t S, int32_t N, int64_t kx,
+                                 int64_t kz, int64_t B, uint8_t* out) {
+  if (kx <= 0 || kz <= 0 || kx > 256 || kz > 256 || S < 0 || N < 0 || B < 0) return 1;
+  const int64_t per = (int64_t)N * B;
+  if (has_vbmi2()) {
+    for (int32_t st = 0; st < S; ++st) {
+      uint8_t* o = out + (int64_t)st * 2 * per;
+      pairs_u8_avx512(key, pos, N, kx, kz, B, o, o + per);
+    }
+    return 0;
+  }
+  static thread_local std::vector<int64_t> scratch;
+  scratch.resize((size_t)(2 * per));
+  for (int32_t st = 0; st < S; ++st) {
+    const int rc = tw_np_randint_pairs(key, pos, N, kx, kz, B, scratch.data(),
+                                       scratch.data() + per);
+    if (rc) return rc;
+    uint8_t* o = out + (int64_t)st * 2 * per;
+    for (int64_t i = 0; i < 2 * per; ++i) o[i] = (uint8_t)scratch[(size_t)i];
   }
   return 0;
 }

@@ -143,7 +143,10 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t 
     const uint64_t p0 = (uint64_t)M0 * ctr.a, p1 = (uint64_t)M1 * ctr.c;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    ctr = u32x4{hi1 ^ ctr.b ^ k0, lo1, hi0 ^ ctr.d ^ k1, lo0};
+    // a ^ b ^ c in ONE gfx950 three-input bitwise op (v_bitop3_b32, truth table 0x96; the
+    // compiler emits two v_xor_b32 for the plain expression): 20 instead of 40 xors per block
+    ctr = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, ctr.b, k0, 0x96), lo1,
+                (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, ctr.d, k1, 0x96), lo0};
     k0 += W0;
     k1 += W1;
   }

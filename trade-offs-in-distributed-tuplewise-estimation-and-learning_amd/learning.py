@@ -37,6 +37,17 @@ DRAW_AHEAD = True
 # evaluations of the learning loop: device part enqueued, host part once the results are back
 # (no device wait per evaluation); off: evaluation_step waits for its results
 DEFER_EVALS = True
+# pipelined replay loop: draws shipped as uint8 when every index is < 256 (C4: kx = 91, kz = 7),
+# else uint16; the device widens them (the H2D bytes are read over PCIe by the widen kernel)
+NARROW_DRAWS_U8 = True
+# learning_process keeps its engine (device buffers, captured segment graphs, replay draw
+# buffers) for the next call of the same shapes and hyper-parameters on host arrays — the
+# reference's make_exps calls learning_process once per configuration and repetition — so that
+# call loads its X, Z and w into the same buffers and replays the graphs already captured
+# instead of capturing new ones.  Problems up to ENGINE_CACHE_MAX_BYTES of rows only.
+ENGINE_CACHE = True
+ENGINE_CACHE_MAX_BYTES = 256 << 20
+_ENGINE = {"key": None, "eng": None}
 SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
@@ -133,6 +144,20 @@ class SGDEngine:
                            and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N_loc, self.B)))
         self._ctl = (t.zeros((2,), dtype=t.int32, device=self.w.device)
                      if self.segment or self.narrow_seg else None)
+
+    def reload(self, X, Z, w_init):
+        """A new run on this engine (learning_process's engine cache): X, Z (host arrays of
+        this engine's shapes) and w_init into the existing buffers, momentum and the abort word
+        zeroed; captured graphs stay valid (same addresses, same scalars)."""
+        t = self.t
+        for dst, src in ((self.X, X), (self.Z, Z)):
+            dst.copy_(t.from_numpy(np.ascontiguousarray(src, dtype=np.float64)).reshape(
+                dst.shape))
+        self.w_shape = tuple(w_init.shape)
+        self.w.copy_(t.from_numpy(np.ascontiguousarray(w_init, dtype=np.float64)).reshape(-1))
+        self.dw.zero_()
+        if self._ctl is not None:
+            self._ctl.zero_()
 
     def _segment(self, nsteps: int, draws_dev=None):
         """nsteps steps as ONE tw_sgd_segment launch (same bits as step()/step_device() +
@@ -678,6 +703,34 @@ class MultiDeviceSGD:
 MULTI_DEVICE_MIN_BYTES = 1 << 30  # gathered row bytes per step below which one device is used
 
 
+def _engine_for(X, Z, w, N, B, margin, reg, learning_rate, optim_type, group, x_layout, loss,
+                gradient, rng_mode, plain):
+    """learning_process's one-device engine: the cached one when this call matches it (replay
+    mode on host arrays, same shapes and hyper-parameters; ENGINE_CACHE), else a new one
+    (cached in turn when the call qualifies).  Device-RNG runs are not cached: their graphs
+    hold the run's seed."""
+    cacheable = (ENGINE_CACHE and plain and rng_mode == "replay" and group is None
+                 and x_layout == "replicated"
+                 and isinstance(X, np.ndarray) and isinstance(Z, np.ndarray)
+                 and X.ndim == 2 and Z.ndim == 2
+                 and 8 * (X.shape[0] + Z.shape[0]) * X.shape[1] <= ENGINE_CACHE_MAX_BYTES)
+    key = None
+    if cacheable:
+        key = (X.shape, Z.shape, int(np.asarray(w).size), int(N), int(B), float(margin),
+               float(reg), float(learning_rate), optim_type, loss, gradient,
+               L.torch().cuda.current_device(), NARROW_SEGMENT, SEGMENT_KERNEL)
+        eng = _ENGINE["eng"]
+        if _ENGINE["key"] == key:
+            eng.reload(X, Z, np.asarray(w, dtype=np.float64))
+            return eng
+    eng = SGDEngine(X, Z, w, N, B, margin, reg, learning_rate, optim_type, group=group,
+                    x_layout=x_layout, loss=loss, gradient=gradient)
+    if cacheable:
+        _ENGINE["key"], _ENGINE["eng"] = None, None  # release the previous engine first
+        _ENGINE["key"], _ENGINE["eng"] = key, eng
+    return eng
+
+
 def _engine_devices(devices, N, B, d, group, x_layout, gradient):
     """The device list learning_process spreads over, or None (one device): explicit
     `devices`, else TW_DEVICES / every visible device once a step gathers >= 1 GiB of rows."""
@@ -794,27 +847,29 @@ class _ReplayDraws:
         return self.seg_dev[k], k
 
     def _seg_buffers(self, nbuf):
-        """Pinned draw buffers of the pipelined loop: uint16 when every index fits (a quarter
-        of the H2D bytes: at C4 a 25-step segment's draws are 4 MB as int64, the copy then
-        as long as the segment's kernels), widened on the device into the int64 buffers the
-        segment graphs read."""
+        """Pinned draw buffers of the pipelined loop, narrowed when every index fits — uint8
+        (kx, kz <= 256; NARROW_DRAWS_U8) or uint16 (<= 65536): an eighth / a quarter of the
+        int64 bytes (a 25-step C4 segment is 4 MB as int64) — and widened on the device into
+        the int64 buffers the segment graphs read."""
         t = L.torch()
         if getattr(self, "seg3_host", None) is None:
             cap = self.segment_capacity()
             shape = (cap, 2, self.N, self.B)
-            self.seg3_u16 = self.kx <= 65536 and self.kz <= 65536
-            hdt = t.int16 if self.seg3_u16 else t.int64  # int16 storage holds the uint16 bits
+            self.seg3_w = (1 if NARROW_DRAWS_U8 and self.kx <= 256 and self.kz <= 256
+                           else 2 if self.kx <= 65536 and self.kz <= 65536 else 8)
+            # torch storage of the narrow bits (viewed unsigned on the host)
+            hdt, npv = {1: (t.uint8, np.uint8), 2: (t.int16, np.uint16),
+                        8: (t.int64, np.int64)}[self.seg3_w]
             self.seg3_host = [t.empty(shape, dtype=hdt, pin_memory=True) for _ in range(nbuf)]
-            self.seg3_np = [h.numpy().view(np.uint16) if self.seg3_u16 else h.numpy()
-                            for h in self.seg3_host]
-            self.seg3_stage = ([L.empty(shape, t.int16) for _ in range(nbuf)]
-                               if self.seg3_u16 else None)
+            self.seg3_np = [h.numpy().view(npv) for h in self.seg3_host]
+            self.seg3_stage = ([L.empty(shape, hdt) for _ in range(nbuf)]
+                               if self.seg3_w < 8 else None)
             self.seg3_dev = [L.empty(shape, t.int64) for _ in range(nbuf)]
             self.seg3_done = [t.cuda.Event() for _ in range(nbuf)]
             self.seg3_used = [False] * nbuf
             # the widening kernel reads the pinned buffers in place (mapped host memory): one
             # launch per segment instead of a copy call and a launch
-            self.seg3_hdev = [L.host_device_pointer(h) if self.seg3_u16 else None
+            self.seg3_hdev = [L.host_device_pointer(h) if self.seg3_w < 8 else None
                               for h in self.seg3_host]
 
     def fill_segment(self, k, S):
@@ -823,24 +878,24 @@ class _ReplayDraws:
         self._seg_buffers(3)
         if self.seg3_used[k]:
             self.seg3_done[k].synchronize()
-        if self.seg3_u16:
-            self.rng.pairs_steps_u16(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
-        else:
-            self.rng.pairs_steps(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
+        fill = {1: self.rng.pairs_steps_u8, 2: self.rng.pairs_steps_u16,
+                8: self.rng.pairs_steps}[self.seg3_w]
+        fill(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
         return k
 
     def ship_segment(self, k, S):
         """Main side: the asynchronous H2D copy of buffer k (stream-ordered after the graph
         that read its device copy three segments back), widened on the device when narrowed;
         returns the int64 device buffer."""
-        if self.seg3_u16 and self.seg3_hdev[k] is not None:
-            L.call("tw_widen_u16", ctypes.c_void_p(self.seg3_hdev[k]),
-                   int(S) * 2 * self.N * self.B, L.ptr(self.seg3_dev[k]), L.stream_handle())
-        elif self.seg3_u16:
+        n = int(S) * 2 * self.N * self.B
+        widen = "tw_widen_u8" if self.seg3_w == 1 else "tw_widen_u16"
+        if self.seg3_w < 8 and self.seg3_hdev[k] is not None:
+            L.call(widen, ctypes.c_void_p(self.seg3_hdev[k]), n, L.ptr(self.seg3_dev[k]),
+                   L.stream_handle())
+        elif self.seg3_w < 8:
             st = self.seg3_stage[k]
             st[:S].copy_(self.seg3_host[k][:S], non_blocking=True)
-            L.call("tw_widen_u16", L.ptr(st), int(S) * 2 * self.N * self.B,
-                   L.ptr(self.seg3_dev[k]), L.stream_handle())
+            L.call(widen, L.ptr(st), n, L.ptr(self.seg3_dev[k]), L.stream_handle())
         else:
             self.seg3_dev[k][:S].copy_(self.seg3_host[k][:S], non_blocking=True)
         self.seg3_done[k].record()
@@ -933,14 +988,20 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
         eng = MultiDeviceSGD(X, Z, w, N, B, margin, p_learn["reg"], learning_rate,
                              optim_type, devs, loss=loss)
     else:
-        eng = SGDEngine(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
-                        group=group, x_layout=x_layout, loss=loss, gradient=gradient)
+        eng = _engine_for(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
+                          group, x_layout, loss, gradient, rng_mode, sign_audit is None)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss)
     if rng_mode != "replay":
         raise ValueError(f"rng_mode must be 'replay' or 'device', not {rng_mode!r}")
-    draws = _ReplayDraws(N, eng.kx, eng.kz, B)
+    draws = getattr(eng, "_draws", None)
+    if draws is None or sign_audit is not None:
+        draws = _ReplayDraws(N, eng.kx, eng.kz, B)
+        if _ENGINE["eng"] is eng:
+            eng._draws = draws  # kept with the engine: its buffers' addresses are in the graphs
+    else:
+        draws.rng.acquire()  # NumPy's global state as it is now
     audit_scores = None
     if sign_audit is not None:
         if eng.complete or eng.G > 1 or eng.layout != "replicated":

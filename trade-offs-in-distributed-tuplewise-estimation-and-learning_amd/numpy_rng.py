@@ -194,6 +194,15 @@ class Session:
         if rc:
             raise ValueError("high <= low or an index range beyond 65536")
 
+    def pairs_steps_u8(self, S, N, kx, kz, B, out):
+        """pairs_steps into a uint8 array (kx, kz <= 256): the same indices, narrowed."""
+        assert out.flags.c_contiguous and out.shape[0] >= S
+        assert out.shape[1:] == (2, N, B) and out.dtype == np.uint8
+        rc = L.lib().tw_np_randint_pairs_steps_u8(self._key, self._pos, int(S), int(N),
+                                                  int(kx), int(kz), int(B), out.ctypes.data)
+        if rc:
+            raise ValueError("high <= low or an index range beyond 256")
+
     def pairs_steps(self, S, N, kx, kz, B, out):
         """S consecutive steps of grad_inc_block's draws: out[s, 0] and out[s, 1] ((N, B)
         int64 each) receive step s's X and Z indices, in the reference's draw order."""
