@@ -628,6 +628,14 @@ int tw_np_randint_pairs_steps_u8(uint32_t* key, int32_t* pos, int32_t S, int32_t
 int tw_widen_u16(const uint16_t* d_in, int64_t n, int64_t* d_out, void* stream);
 /* The same for uint8 indices. */
 int tw_widen_u8(const uint8_t* d_in, int64_t n, int64_t* d_out, void* stream);
+/* The replay loop's segment upload in one launch: widen n narrowed draws (width 1 = uint8,
+ * 2 = uint16) d_in -> d_out as above, and copy nx + nz 8-byte row indices d_rows ->
+ * d_rows_x[0:nx], d_rows_z[0:nz] (a reshuffle's SWR tables; nx = nz = 0: none).  Either
+ * source may be mapped host memory.  Replaces learning-experiment/make_exps.py:123-125's
+ * SWR_divide hand-off + compute_stats.py:155-156's draws for one segment of steps. */
+int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
+                  const void* d_rows, int64_t nx, int64_t* d_rows_x, int64_t nz,
+                  int64_t* d_rows_z, void* stream);
 /* n 8-byte words d_in -> d_out on `stream` (d_in may be mapped host memory, as above). */
 int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
 /* The device address of pinned, mapped host memory (hipHostGetDevicePointer); TW_ERR_ARG when

@@ -45,6 +45,18 @@ lr.learning_process(X, Z, dict(p, n_it=50))
 full, ts = timed(lambda: lr.learning_process(X, Z, p))
 print(f"full      {STEPS / full:9.0f} steps/s  {full * 1e3:7.2f} ms  runs "
       + " ".join(f"{STEPS / t:.0f}" for t in ts), flush=True)
+lr.PIPE_STATS = []
+lr.learning_process(X, Z, p)
+w = np.array(lr.PIPE_STATS) * 1e6
+lr.PIPE_STATS = None
+print(f"waits     main thread waited for the draws: {w.sum() / 1e3:.2f} ms over {len(w)} segments "
+      f"(median {np.median(w):.1f} us, max {w.max():.1f} us)", flush=True)
+lr.FUSED_SHIP = False
+fs, ts = timed(lambda: lr.learning_process(X, Z, p))
+print(f"unfused   {STEPS / fs:9.0f} steps/s  {fs * 1e3:7.2f} ms  runs "
+      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (FUSED_SHIP off: widen + 2 row copies)",
+      flush=True)
+lr.FUSED_SHIP = True
 lr.NARROW_DRAWS_U8 = False
 u16, ts = timed(lambda: lr.learning_process(X, Z, p))
 print(f"u16       {STEPS / u16:9.0f} steps/s  {u16 * 1e3:7.2f} ms  runs "

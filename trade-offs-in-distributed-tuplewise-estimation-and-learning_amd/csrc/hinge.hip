@@ -755,6 +755,66 @@ extern "C" int tw_widen_u8(const uint8_t* d_in, int64_t n, int64_t* d_out, void*
   return widen(d_in, n, d_out, stream);
 }
 
+// The replay loop's per-segment upload in ONE launch: blocks [0, gw) widen the narrowed draws
+// (as k_widen), the rest copy a reshuffle's SWR row tables (nx words to rows_x, then nz to
+// rows_z, from one source) — both sources usually pinned host memory read over PCIe.  One
+// launch instead of three: each launch on the segment's critical path costs its own gap.
+template <typename T>
+static __global__ __launch_bounds__(256) void k_ship(const T* __restrict__ in, int64_t n,
+                                                     int64_t* __restrict__ out,
+                                                     const uint64_t* __restrict__ rin,
+                                                     int64_t nx, uint64_t* __restrict__ rx,
+                                                     int64_t nz, uint64_t* __restrict__ rz,
+                                                     int gw) {
+  if ((int)blockIdx.x < gw) {
+    constexpr int kPer = 16 / (int)sizeof(T);
+    const int64_t nv = (reinterpret_cast<uintptr_t>(in) & 15) == 0 ? n / kPer : 0;
+    const int64_t stride = (int64_t)gw * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
+      const uint4 v = reinterpret_cast<const uint4*>(in)[i];
+      const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) out[i * kPer + k] = (int64_t)e[k];
+    }
+    for (int64_t i = nv * kPer + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+      out[i] = (int64_t)in[i];
+    return;
+  }
+  const int64_t stride = (int64_t)(gridDim.x - gw) * 256;
+  for (int64_t i = (int64_t)(blockIdx.x - gw) * 256 + threadIdx.x; i < nx + nz; i += stride) {
+    const uint64_t v = rin[i];
+    if (i < nx)
+      rx[i] = v;
+    else
+      rz[i - nx] = v;
+  }
+}
+
+extern "C" int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
+                             const void* d_rows, int64_t nx, int64_t* d_rows_x, int64_t nz,
+                             int64_t* d_rows_z, void* stream) {
+  TW_ARG_CHECK(width == 1 || width == 2, "tw_ship_draws: width must be 1 or 2");
+  TW_ARG_CHECK(n >= 0 && nx >= 0 && nz >= 0, "tw_ship_draws: negative size");
+  TW_ARG_CHECK(n == 0 || (d_in != nullptr && d_out != nullptr), "tw_ship_draws: null draws");
+  TW_ARG_CHECK(nx + nz == 0 || (d_rows != nullptr && (nx == 0 || d_rows_x != nullptr) &&
+                                (nz == 0 || d_rows_z != nullptr)),
+               "tw_ship_draws: null row tables");
+  const int64_t per = 256 * (16 / (int64_t)width);
+  const int gw = n > 0 ? (int)std::min<int64_t>(1024, ceil_div(n, per)) : 0;
+  const int gr = nx + nz > 0 ? (int)std::min<int64_t>(256, ceil_div(nx + nz, 256)) : 0;
+  if (gw + gr == 0) return TW_OK;
+  if (width == 1)
+    hipLaunchKernelGGL(k_ship<uint8_t>, dim3(gw + gr), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_in, n, d_out, (const uint64_t*)d_rows, nx,
+                       (uint64_t*)d_rows_x, nz, (uint64_t*)d_rows_z, gw);
+  else
+    hipLaunchKernelGGL(k_ship<uint16_t>, dim3(gw + gr), dim3(256), 0, (hipStream_t)stream,
+                       (const uint16_t*)d_in, n, d_out, (const uint64_t*)d_rows, nx,
+                       (uint64_t*)d_rows_x, nz, (uint64_t*)d_rows_z, gw);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 // 8-byte words from a (host-mapped) staging buffer into device memory: the replay loop's SWR
 // row tables, read by the kernel straight from pinned host memory.
 static __global__ __launch_bounds__(256) void k_copy_words(const uint64_t* __restrict__ in,

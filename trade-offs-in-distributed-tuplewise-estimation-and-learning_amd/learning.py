@@ -48,6 +48,10 @@ NARROW_DRAWS_U8 = True
 ENGINE_CACHE = True
 ENGINE_CACHE_MAX_BYTES = 256 << 20
 _ENGINE = {"key": None, "eng": None}
+# pipelined replay loop: each segment's narrowed draws and a reshuffle's row tables go up in ONE
+# launch (tw_ship_draws) instead of a widen and two row copies
+FUSED_SHIP = True
+PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each segment's draws
 SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
@@ -281,6 +285,19 @@ class SGDEngine:
         self.rows_z.view(-1).copy_(flat[nx + a * self.kz:nx + (a + self.N_loc) * self.kz],
                                    non_blocking=True)
         return True
+
+    def rows_ship_args(self, staged):
+        """tw_ship_draws' row-table arguments for a reshuffle whose rows sit in a mapped pinned
+        staging buffer (the pipelined replay loop; one process, replicated layout): (source
+        device address, nx, rows_x, nz, rows_z), or None where set_shards_staged / set_shards
+        must do it."""
+        if self.layout == "partitioned" or self.rows_x is None or self.N_loc != self.N:
+            return None
+        flat, hdev = staged
+        if hdev is None:
+            return None
+        return (hdev, self.N * self.kx, L.ptr(self.rows_x), self.N * self.kz,
+                L.ptr(self.rows_z))
 
     def _records(self, name, rows, expect):
         """Persistent (rows, d+1) record buffer for the row exchange, kept across reshuffles
@@ -883,13 +900,21 @@ class _ReplayDraws:
         fill(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
         return k
 
-    def ship_segment(self, k, S):
+    def ship_segment(self, k, S, rows=None):
         """Main side: the asynchronous H2D copy of buffer k (stream-ordered after the graph
         that read its device copy three segments back), widened on the device when narrowed;
-        returns the int64 device buffer."""
+        returns the int64 device buffer.  rows: SGDEngine.rows_ship_args of a reshuffle — its
+        row tables go up in the same launch (tw_ship_draws; narrowed, mapped draws only)."""
         n = int(S) * 2 * self.N * self.B
         widen = "tw_widen_u8" if self.seg3_w == 1 else "tw_widen_u16"
-        if self.seg3_w < 8 and self.seg3_hdev[k] is not None:
+        if rows is not None or (FUSED_SHIP and self.seg3_w < 8
+                                and self.seg3_hdev[k] is not None):
+            assert self.seg3_w < 8 and self.seg3_hdev[k] is not None
+            src, nx, dx, nz, dz = rows if rows is not None else (None, 0, None, 0, None)
+            L.call("tw_ship_draws", ctypes.c_void_p(self.seg3_hdev[k]), self.seg3_w, n,
+                   L.ptr(self.seg3_dev[k]), ctypes.c_void_p(src), nx, dx, nz, dz,
+                   L.stream_handle())
+        elif self.seg3_w < 8 and self.seg3_hdev[k] is not None:
             L.call(widen, ctypes.c_void_p(self.seg3_hdev[k]), n, L.ptr(self.seg3_dev[k]),
                    L.stream_handle())
         elif self.seg3_w < 8:
@@ -1100,22 +1125,37 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
     with ThreadPoolExecutor(max_workers=1) as pool:
         futs = [pool.submit(work, j) for j in range(min(ahead, len(segs)))]
         for idx, (i, nxt, resh) in enumerate(segs):
-            rows, k = futs[idx].result()
+            if PIPE_STATS is not None:  # study hook (tools/time_replay_parts.py)
+                import time
+                t0 = time.perf_counter()
+                rows, k = futs[idx].result()
+                PIPE_STATS.append(time.perf_counter() - t0)
+            else:
+                rows, k = futs[idx].result()
             if idx + ahead < len(segs):
                 futs.append(pool.submit(work, idx + ahead))
+            rargs = None
             if rows is not None:
                 (rows_x, rows_z), pinned = rows
-                if pinned is not None and eng.set_shards_staged(pinned):
+                if pinned is not None and FUSED_SHIP:
+                    rargs = eng.rows_ship_args(pinned)
+                if rargs is not None:
+                    pass  # the row tables go up with the segment's draws, in one launch
+                elif pinned is not None and eng.set_shards_staged(pinned):
                     draws.rows_uploaded(idx % 3)
                 else:
                     eng.set_shards(rows_x, rows_z)
+            # the segment's upload before its evaluation: the reference reshuffles, then
+            # evaluates (make_exps.py:123-128)
+            buf = draws.ship_segment(k, nxt - i, rargs)
+            if rargs is not None:
+                draws.rows_uploaded(idx % 3)
             w_pending = None
             if i % eval_mod == 0:
                 if defer is not None:  # device part enqueued now, host part later
                     _evaluate(i, eng, None, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer)
                 else:
                     w_pending = eng.w_host_async()
-            buf = draws.ship_segment(k, nxt - i)
             if w_pending is not None:
                 _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
             eng.run_replay_segment(buf, nxt - i, graphs, k)
