@@ -636,6 +636,23 @@ int tw_widen_u8(const uint8_t* d_in, int64_t n, int64_t* d_out, void* stream);
 int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
                   const void* d_rows, int64_t nx, int64_t* d_rows_x, int64_t nz,
                   int64_t* d_rows_z, void* stream);
+/* The replay loop's draws made ahead on a native thread (csrc/drawpipe.hip): segment j of
+ * n_seg (seg_steps[j] steps; seg_resh[j] != 0: a reshuffle first) is drawn from NumPy's
+ * MT19937 state (key/pos, advanced in place) into ring buffer j % nbuf: the SWR rows of a
+ * reshuffle (make_exps.py:123-125, compute_stats.py:48-54: N randint calls on [0, n_X) of
+ * n_X / N values, then N on [0, n_Z)) into row_bufs[k] (int64), then the steps' pairs
+ * (compute_stats.py:155-156) into seg_bufs[k] as (S, 2, N, B) values of `width` bytes (1, 2
+ * or 8).  tw_draw_pipe_wait blocks until segment j is drawn; tw_draw_pipe_shipped records
+ * that the uploads reading its buffers are enqueued on `stream` (the worker refills them only
+ * after they have run); tw_draw_pipe_stop cancels what is not drawn, joins and frees.
+ * Nothing else may use NumPy's global RNG between start and stop. */
+int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg, const int32_t* seg_steps,
+                       const uint8_t* seg_resh, int32_t N, int64_t kx, int64_t kz, int64_t B,
+                       int64_t n_X, int64_t n_Z, int32_t width, int32_t nbuf,
+                       void* const* seg_bufs, int64_t* const* row_bufs, void** out_handle);
+int tw_draw_pipe_wait(void* handle, int32_t j);
+int tw_draw_pipe_shipped(void* handle, int32_t j, void* stream);
+int tw_draw_pipe_stop(void* handle);
 /* n 8-byte words d_in -> d_out on `stream` (d_in may be mapped host memory, as above). */
 int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
 /* The device address of pinned, mapped host memory (hipHostGetDevicePointer); TW_ERR_ARG when

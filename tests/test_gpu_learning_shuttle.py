@@ -177,3 +177,89 @@ def test_engine_cache_reuse(gpu, golden, monkeypatch):
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert a[0][k] == b[0][k] == c[0][k], k
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[1], c[1])
+
+
+@pytest.mark.parametrize("mod", MODS)
+def test_native_draw_worker_equals_python_worker(gpu, golden, mod, monkeypatch):
+    """learning.NATIVE_DRAWS (the replay draws made ahead by tw_draw_pipe, csrc/drawpipe.hip)
+    against the Python worker thread, and learning.FUSED_SHIP (the upload captured in the
+    segment graph) against separate launches: the same lists and NumPy RNG state, bit for
+    bit, and the reference's lists."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for native, fused in ((True, True), (False, True), (True, False)):
+        monkeypatch.setattr(lr, "NATIVE_DRAWS", native)
+        monkeypatch.setattr(lr, "FUSED_SHIP", fused)
+        X, Z, p = _p(mod)
+        np.random.seed(3000 + mod)
+        lr.learning_process(X, Z, p)
+        _check_lists(p, golden, mod)
+        out[native, fused] = (p, np.random.get_state()[1].copy(), np.random.get_state()[2])
+    ref = out[True, True]
+    for key, (p, st, pos) in out.items():
+        for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+            assert p[k] == ref[0][k], (key, k)
+        assert np.array_equal(st, ref[1]) and pos == ref[2], key
+
+
+def test_native_draw_pipe_protocol(gpu):
+    """tw_draw_pipe_*: the segments come out in NumPy's order (== Session.pairs_steps_u8 on the
+    same state), a reshuffle's rows first; a pipe stopped before its last segment joins
+    without hanging (its worker blocked on a buffer the main thread never shipped); a width
+    the indices do not fit is refused."""
+    import torch
+    import tuplewise.learning as lr
+    from tuplewise import _lib as L
+    from tuplewise.numpy_rng import Session
+    N, kx, kz, B = 7, 91, 7, 13
+    n_X, n_Z = N * kx, N * kz
+    segs = [(0, 3, True), (3, 5, False), (5, 9, True), (9, 10, False), (10, 12, True)]
+    np.random.seed(11)
+    want = []
+    with Session() as s:
+        for a, b, r in segs:
+            rows = s.randint_flat(np.zeros(2 * N, np.int64),
+                                  np.array([n_X] * N + [n_Z] * N, np.int64),
+                                  np.array([kx] * N + [kz] * N, np.int64)) if r else None
+            o = np.empty((b - a, 2, N, B), np.uint8)
+            s.pairs_steps_u8(b - a, N, kx, kz, B, o)
+            want.append((rows, o))
+    state = np.random.get_state()
+    np.random.seed(11)
+    d = lr._ReplayDraws(N, kx, kz, B)
+    with d.rng:
+        pipe = d.native_pipe(segs, n_X, n_Z)
+        try:
+            for j, (a, b, r) in enumerate(segs):
+                rows, k = pipe.wait(j)
+                got = d.seg3_np[k][:b - a].copy()
+                assert np.array_equal(got, want[j][1]), j
+                if r:
+                    (rx, rz), _ = rows
+                    assert np.array_equal(np.concatenate([rx.ravel(), rz.ravel()]), want[j][0])
+                else:
+                    assert rows is None
+                pipe.shipped(j)
+        finally:
+            pipe.stop()
+    assert np.array_equal(np.random.get_state()[1], state[1])
+    assert np.random.get_state()[2] == state[2]
+    torch.cuda.synchronize()
+    # stopped early: the worker waits for segment 0's buffer to be shipped, which never happens
+    d2 = lr._ReplayDraws(N, kx, kz, B)
+    with d2.rng:
+        pipe = d2.native_pipe(segs, n_X, n_Z)
+        pipe.wait(0)
+        pipe.stop()
+    with pytest.raises(ValueError):
+        h = ctypes_handle()
+        P = __import__("ctypes").c_void_p * 3
+        L.call("tw_draw_pipe_start", d2.rng._key, d2.rng._pos, 1,
+               np.array([1], np.int32).ctypes.data, np.array([0], np.uint8).ctypes.data,
+               N, 300, kz, B, 300 * N, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), h)
+
+
+def ctypes_handle():
+    import ctypes
+    return ctypes.byref(ctypes.c_void_p())

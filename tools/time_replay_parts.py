@@ -51,12 +51,22 @@ w = np.array(lr.PIPE_STATS) * 1e6
 lr.PIPE_STATS = None
 print(f"waits     main thread waited for the draws: {w.sum() / 1e3:.2f} ms over {len(w)} segments "
       f"(median {np.median(w):.1f} us, max {w.max():.1f} us)", flush=True)
+eg, ts = timed(lambda: lr.learning_process(X, Z, p, graphs=False))
+print(f"eager     {STEPS / eg:9.0f} steps/s  {eg * 1e3:7.2f} ms  runs "
+      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (graphs=False: the segment kernels "
+      "launched eagerly)", flush=True)
 lr.FUSED_SHIP = False
 fs, ts = timed(lambda: lr.learning_process(X, Z, p))
 print(f"unfused   {STEPS / fs:9.0f} steps/s  {fs * 1e3:7.2f} ms  runs "
-      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (FUSED_SHIP off: widen + 2 row copies)",
-      flush=True)
+      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (FUSED_SHIP off: widen + 2 row copies, "
+      "eager before the graph)", flush=True)
 lr.FUSED_SHIP = True
+lr.NATIVE_DRAWS = False
+nd, ts = timed(lambda: lr.learning_process(X, Z, p))
+print(f"pyworker  {STEPS / nd:9.0f} steps/s  {nd * 1e3:7.2f} ms  runs "
+      + " ".join(f"{STEPS / t:.0f}" for t in ts) + "  (NATIVE_DRAWS off: Python worker thread)",
+      flush=True)
+lr.NATIVE_DRAWS = True
 lr.NARROW_DRAWS_U8 = False
 u16, ts = timed(lambda: lr.learning_process(X, Z, p))
 print(f"u16       {STEPS / u16:9.0f} steps/s  {u16 * 1e3:7.2f} ms  runs "

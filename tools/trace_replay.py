@@ -1,5 +1,6 @@
 """Replay-mode learning_process at the C4 shape (as bench sgd_replay_steps_per_s), 5 calls, for
-a rocprofv3 --kernel-trace run: the device timeline of the segments (kernels, gaps)."""
+a rocprofv3 --kernel-trace run: the device timeline of the segments (kernels, gaps).
+Argument "eager": graphs=False."""
 import logging
 import pathlib
 import sys
@@ -18,7 +19,8 @@ p = {"n_it": 2000, "margin": 1, "N": 100, "B": 100, "reshuffle_mod": 25, "reg": 
      "train_Z": Z}
 logging.disable(logging.CRITICAL)
 np.random.seed(0)
+eager = "eager" in sys.argv[1:]  # graphs=False: the segment kernels launched eagerly
 for _ in range(6):
-    lr.learning_process(X, Z, p)
+    lr.learning_process(X, Z, p, graphs=not eager)
     torch.cuda.synchronize()
 print("done", flush=True)

@@ -138,6 +138,11 @@ _SIGNATURES = {
     "tw_np_randint_pairs_steps_u8": [_vp, _vp, _i32, _i32, _i64, _i64, _i64, _vp],
     "tw_widen_u8": [_vp, _i64, _vp, _vp],
     "tw_ship_draws": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp],
+    "tw_draw_pipe_start": [_vp, _vp, _i32, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32,
+                           _i32, _vp, _vp, _vp],
+    "tw_draw_pipe_wait": [_vp, _i32],
+    "tw_draw_pipe_shipped": [_vp, _i32, _vp],
+    "tw_draw_pipe_stop": [_vp],
     "tw_copy_words": [_vp, _i64, _vp, _vp],
     "tw_host_device_pointer": [_vp, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],

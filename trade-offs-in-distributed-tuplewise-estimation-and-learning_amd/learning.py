@@ -51,6 +51,9 @@ _ENGINE = {"key": None, "eng": None}
 # pipelined replay loop: each segment's narrowed draws and a reshuffle's row tables go up in ONE
 # launch (tw_ship_draws) instead of a widen and two row copies
 FUSED_SHIP = True
+# pipelined replay loop: the draws made ahead by a native thread (csrc/drawpipe.hip) rather
+# than a Python worker thread
+NATIVE_DRAWS = True
 PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each segment's draws
 SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
@@ -389,11 +392,14 @@ class SGDEngine:
                    L.stream_handle())
         self._update()
 
-    def run_replay_segment(self, draws_dev, nsteps: int, graphs: bool = True, tag=0):
+    def run_replay_segment(self, draws_dev, nsteps: int, graphs: bool = True, tag=0,
+                           upload=None):
         """nsteps replay steps whose NumPy draws sit in draws_dev[s] ((2, N, B) int64 on the
         device): one gradient + one update launch per step, replayed from a hipGraph captured
         per (tag, nsteps) — tag names the draw buffer, whose address the graph holds — or
-        launched eagerly (graphs=False, or a collective in the step)."""
+        launched eagerly (graphs=False, or a collective in the step).  upload: (key, fn) — fn
+        enqueues the segment's upload (tw_ship_draws), captured in the same graph (one graph
+        launch per segment); key names its arguments."""
         def one(st):
             if self.complete:
                 self.step_complete()
@@ -409,13 +415,18 @@ class SGDEngine:
                 for st in range(nsteps):
                     one(st)
 
-        if not graphs or self.G > 1:
+        # a persistent narrow segment is two launches (plus the upload): eager launches cost
+        # ~1.5 us per boundary on the stream, a graph launch ~12 (kernel traces r03s31/s32)
+        if not graphs or self.G > 1 or (self.narrow_seg and nsteps > 1 and not self.complete):
+            if upload is not None:
+                upload[1]()
             steps()
             return
         t = self.t
         if not hasattr(self, "_replay_graphs"):
             self._replay_graphs = {}
-        key = (tag, nsteps, draws_dev.data_ptr() if draws_dev is not None else 0)
+        key = (tag, nsteps, draws_dev.data_ptr() if draws_dev is not None else 0,
+               None if upload is None else upload[0])
         g = self._replay_graphs.get(key)
         if g is None:
             if self.complete and self._cwork is None:  # allocated outside the capture
@@ -427,6 +438,8 @@ class SGDEngine:
                                t.empty_like(self.grads))
             g = t.cuda.CUDAGraph()
             with t.cuda.graph(g):
+                if upload is not None:
+                    upload[1]()
                 steps()
             self._replay_graphs[key] = g
         g.replay()
@@ -814,13 +827,7 @@ class _ReplayDraws:
         """swr_rows drawn straight into pinned row buffer k of the pipelined loop (ring of 3,
         reused once the upload out of it has finished): (rows_x, rows_z) host views and the
         pinned tensors."""
-        t = L.torch()
-        N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
-        if getattr(self, "rows3", None) is None or self.rows3[0][0].shape != (N * kx + N * kz,):
-            self.rows3 = [(t.empty((N * kx + N * kz,), dtype=t.int64, pin_memory=True),
-                           t.cuda.Event()) for _ in range(3)]
-            self.rows3_used = [False] * 3
-            self.rows3_hdev = [L.host_device_pointer(b) for b, _ in self.rows3]
+        N, kx, kz = self._rows_buffers(n_X, n_Z)
         buf, ev = self.rows3[k]
         if self.rows3_used[k]:
             ev.synchronize()
@@ -828,6 +835,35 @@ class _ReplayDraws:
         self.rng.randint_flat(*self._swr_setup(n_X, n_Z), out=flat)
         return (flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, kz)), (buf,
                                                                              self.rows3_hdev[k])
+
+    def _rows_buffers(self, n_X, n_Z):
+        """The ring of three pinned SWR row buffers (flat N*kx + N*kz int64, mapped)."""
+        t = L.torch()
+        N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
+        if getattr(self, "rows3", None) is None or self.rows3[0][0].shape != (N * kx + N * kz,):
+            self.rows3 = [(t.empty((N * kx + N * kz,), dtype=t.int64, pin_memory=True),
+                           t.cuda.Event()) for _ in range(3)]
+            self.rows3_used = [False] * 3
+            self.rows3_hdev = [L.host_device_pointer(b) for b, _ in self.rows3]
+        return N, kx, kz
+
+    def native_pipe(self, segs, n_X, n_Z):
+        """The loop's draws made ahead by a native thread (tw_draw_pipe_*, csrc/drawpipe.hip)
+        into the ring of pinned segment and row buffers: segs = [(i, nxt, reshuffle)]."""
+        t = L.torch()
+        self._seg_buffers(3)
+        N, kx, kz = self._rows_buffers(n_X, n_Z)
+        t.cuda.current_stream().synchronize()  # earlier uploads out of the ring have run
+        steps = np.array([b - a for a, b, _ in segs], dtype=np.int32)
+        resh = np.array([bool(r) for _, _, r in segs], dtype=np.uint8)
+        P = ctypes.c_void_p * 3
+        segp = P(*[h.data_ptr() for h in self.seg3_host])
+        rowp = P(*[b.data_ptr() for b, _ in self.rows3])
+        h = ctypes.c_void_p()
+        L.call("tw_draw_pipe_start", self.rng._key, self.rng._pos, len(segs),
+               steps.ctypes.data, resh.ctypes.data, N, self.kx, self.kz, self.B, int(n_X),
+               int(n_Z), self.seg3_w, 3, segp, rowp, ctypes.byref(h))
+        return _NativeDraws(self, h, segs, N, kx, kz, (steps, resh, segp, rowp))
 
     def rows_uploaded(self, k):
         """Main side: the upload out of pinned row buffer k has been enqueued."""
@@ -900,7 +936,7 @@ class _ReplayDraws:
         fill(S, self.N, self.kx, self.kz, self.B, self.seg3_np[k])
         return k
 
-    def ship_segment(self, k, S, rows=None):
+    def ship_segment(self, k, S, rows=None, record=True):
         """Main side: the asynchronous H2D copy of buffer k (stream-ordered after the graph
         that read its device copy three segments back), widened on the device when narrowed;
         returns the int64 device buffer.  rows: SGDEngine.rows_ship_args of a reshuffle — its
@@ -923,9 +959,14 @@ class _ReplayDraws:
             L.call(widen, L.ptr(st), n, L.ptr(self.seg3_dev[k]), L.stream_handle())
         else:
             self.seg3_dev[k][:S].copy_(self.seg3_host[k][:S], non_blocking=True)
+        if record:  # (record=False inside a graph capture: the caller records after the replay)
+            self.shipped_out(k)
+        return self.seg3_dev[k]
+
+    def shipped_out(self, k):
+        """The upload out of pinned buffer k is enqueued (on the current stream)."""
         self.seg3_done[k].record()
         self.seg3_used[k] = True
-        return self.seg3_dev[k]
 
     def pairs(self):
         t = L.torch()
@@ -942,6 +983,37 @@ class _ReplayDraws:
             self.done[k] = t.cuda.Event()
         self.done[k].record()
         return self.dev[k][0], self.dev[k][1]
+
+
+class _NativeDraws:
+    """Handle of a running tw_draw_pipe (the pipelined replay loop's native draw worker)."""
+
+    def __init__(self, draws, h, segs, N, kx, kz, keep):
+        self.draws, self.h, self.segs = draws, h, segs
+        self.N, self.kx, self.kz = N, kx, kz
+        self._keep = keep  # the arrays the native side reads
+
+    def wait(self, j):
+        """Block (interpreter lock released) until segment j is drawn: (rows, k) as the
+        Python worker returns them — rows = ((rows_x, rows_z) views, (pinned, device
+        address)) for a reshuffle, else None; k = the ring slot."""
+        L.call("tw_draw_pipe_wait", self.h, j)
+        k = j % 3
+        if not self.segs[j][2]:
+            return None, k
+        buf = self.draws.rows3[k][0]
+        flat = buf.numpy()
+        N, kx = self.N, self.kx
+        return ((flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, self.kz)),
+                (buf, self.draws.rows3_hdev[k])), k
+
+    def shipped(self, j):
+        L.call("tw_draw_pipe_shipped", self.h, j, L.stream_handle())
+
+    def stop(self):
+        if self.h is not None:
+            L.call("tw_draw_pipe_stop", self.h)
+            self.h = None
 
 
 def sign_audit_step(X, Z, rows_x, rows_z, ix, iz, w, margin, scores) -> dict:
@@ -1093,14 +1165,14 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
 
 def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, rows_z):
     """The replay loop's segments (runs of steps up to the next reshuffle / evaluation, at most
-    segment_capacity() steps) with the host's NumPy-exact draws made AHEAD by a worker thread:
-    the draws of segment j + 2 (its SWR rows, make_exps.py:123-125, then its steps' pairs,
-    compute_stats.py:155-156 — the reference's order, one MT19937 stream) run in native code
-    (ctypes releases the GIL) while this thread uploads the row tables, evaluates and launches
-    segment j.  Three pinned draw buffers: the worker refills buffer k only after the H2D copy
-    of the segment that used it three segments back has finished.  Same draws, same
-    trajectory as the sequential loop (tests/test_gpu_learning*.py)."""
-    from concurrent.futures import ThreadPoolExecutor
+    segment_capacity() steps) with the host's NumPy-exact draws made AHEAD by a worker: the
+    draws of later segments (their SWR rows, make_exps.py:123-125, then their steps' pairs,
+    compute_stats.py:155-156 — the reference's order, one MT19937 stream) run while this thread
+    uploads the row tables, evaluates and launches segment j.  NATIVE_DRAWS: a native thread
+    (tw_draw_pipe, csrc/drawpipe.hip) filling a ring of three pinned buffers, each refilled once
+    the upload out of it has run; else a Python worker thread two segments ahead (ctypes
+    releases the GIL during the draws).  Same draws, same trajectory as the sequential loop
+    (tests/test_gpu_learning*.py)."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
     segs, i = [], 0
@@ -1110,6 +1182,18 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
         segs.append((i, nxt, i % mod == 0))
         i = nxt
 
+    def run(wait, shipped):
+        _replay_segments(eng, draws, segs, wait, shipped, X, Z, p_learn, loss, graphs, defer,
+                         rows_x, rows_z)
+
+    if NATIVE_DRAWS:
+        pipe = draws.native_pipe(segs, n_X, n_Z)
+        try:
+            run(pipe.wait, pipe.shipped)
+        finally:
+            pipe.stop()
+        return
+    from concurrent.futures import ThreadPoolExecutor
     staged = isinstance(eng, SGDEngine) and eng.layout == "replicated"
 
     def work(idx):
@@ -1124,41 +1208,80 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
     draws._seg_buffers(3)  # on this thread: its current device and stream
     with ThreadPoolExecutor(max_workers=1) as pool:
         futs = [pool.submit(work, j) for j in range(min(ahead, len(segs)))]
-        for idx, (i, nxt, resh) in enumerate(segs):
-            if PIPE_STATS is not None:  # study hook (tools/time_replay_parts.py)
-                import time
-                t0 = time.perf_counter()
-                rows, k = futs[idx].result()
-                PIPE_STATS.append(time.perf_counter() - t0)
-            else:
-                rows, k = futs[idx].result()
+
+        def wait(idx):
+            r = futs[idx].result()
             if idx + ahead < len(segs):
                 futs.append(pool.submit(work, idx + ahead))
-            rargs = None
-            if rows is not None:
-                (rows_x, rows_z), pinned = rows
-                if pinned is not None and FUSED_SHIP:
-                    rargs = eng.rows_ship_args(pinned)
-                if rargs is not None:
-                    pass  # the row tables go up with the segment's draws, in one launch
-                elif pinned is not None and eng.set_shards_staged(pinned):
-                    draws.rows_uploaded(idx % 3)
-                else:
-                    eng.set_shards(rows_x, rows_z)
-            # the segment's upload before its evaluation: the reference reshuffles, then
-            # evaluates (make_exps.py:123-128)
-            buf = draws.ship_segment(k, nxt - i, rargs)
+            return r
+
+        run(wait, None)
+
+
+def _replay_segments(eng, draws, segs, wait, shipped, X, Z, p_learn, loss, graphs, defer,
+                     rows_x, rows_z):
+    """The main thread's side of _replay_pipelined: per segment, its draws (wait(j) -> (rows,
+    ring slot)), a reshuffle's row tables, the upload, the evaluation, the steps."""
+    eval_mod = p_learn["eval_mod"]
+    for idx, (i, nxt, resh) in enumerate(segs):
+        if PIPE_STATS is not None:  # study hook (tools/time_replay_parts.py)
+            import time
+            t0 = time.perf_counter()
+            rows, k = wait(idx)
+            PIPE_STATS.append(time.perf_counter() - t0)
+        else:
+            rows, k = wait(idx)
+        rargs = None
+        if rows is not None:
+            (rows_x, rows_z), pinned = rows
+            staged = pinned is not None and isinstance(eng, SGDEngine)
+            if staged and FUSED_SHIP:
+                rargs = eng.rows_ship_args(pinned)
             if rargs is not None:
-                draws.rows_uploaded(idx % 3)
-            w_pending = None
-            if i % eval_mod == 0:
-                if defer is not None:  # device part enqueued now, host part later
-                    _evaluate(i, eng, None, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer)
-                else:
-                    w_pending = eng.w_host_async()
-            if w_pending is not None:
-                _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
+                pass  # the row tables go up with the segment's draws, in one launch
+            elif staged and eng.set_shards_staged(pinned):
+                if shipped is None:
+                    draws.rows_uploaded(k)
+            else:
+                eng.set_shards(rows_x, rows_z)
+        evaluating = i % eval_mod == 0
+        # the upload rides in the segment's graph when nothing enqueued between them reads
+        # the new rows: no evaluation here, or FIXED_PAIRS monitoring (its statistics read w
+        # and the fixed pairs only); otherwise it goes first — the reference reshuffles, then
+        # evaluates (make_exps.py:123-128)
+        upload = None
+        if (graphs and FUSED_SHIP and isinstance(eng, SGDEngine) and eng.G == 1
+                and (rows is None or rargs is not None)
+                and draws.seg3_w < 8 and draws.seg3_hdev[k] is not None
+                and (not evaluating or TYPE_TRAIN_MONITOR == "FIXED_PAIRS")):
+            buf = draws.seg3_dev[k]
+            upload = ((k, nxt - i, rargs is not None),
+                      lambda k=k, S=nxt - i, r=rargs: draws.ship_segment(k, S, r, record=False))
+        else:
+            # (the native worker keeps its own event per ring slot: no torch event records)
+            buf = draws.ship_segment(k, nxt - i, rargs, record=shipped is None)
+            if shipped is None and rargs is not None:
+                draws.rows_uploaded(k)
+            if shipped is not None:
+                shipped(idx)
+        w_pending = None
+        if evaluating:
+            if defer is not None:  # device part enqueued now, host part later
+                _evaluate(i, eng, None, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer)
+            else:
+                w_pending = eng.w_host_async()
+        if w_pending is not None:
+            _evaluate(i, eng, w_pending(), rows_x, rows_z, X, Z, p_learn, loss, graphs)
+        if upload is None:
             eng.run_replay_segment(buf, nxt - i, graphs, k)
+        else:
+            eng.run_replay_segment(buf, nxt - i, graphs, k, upload=upload)
+            if shipped is None:
+                draws.shipped_out(k)
+                if rargs is not None:
+                    draws.rows_uploaded(k)
+            else:
+                shipped(idx)
 
 
 def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer=None):
