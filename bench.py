@@ -396,7 +396,21 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
                     optim_type="momentum", x_layout=layout, group=group)
     eng.enable_device_rng(12345)
 
+    import tuplewise.learning as lr
+    swr = lr.SWR_IN_KERNEL and eng.swr_segments_ok()
+
     def run(e, k):
+        if swr and k > 1:
+            # the persistent narrow segment draws every reshuffle's rows itself: segments are
+            # not cut at reshuffles (learning_process cuts them at evaluations only)
+            i = 0
+            while i < k:
+                n = min(k - i, 4096)
+                if k - i - n == 1:
+                    n -= 1  # never leave a one-step tail
+                e.run_segment(n, False, graphs=True, swr_mod=reshuffle_mod)
+                i += n
+            return
         i = 0
         while i < k:
             nxt = min(k, (i // reshuffle_mod + 1) * reshuffle_mod)
@@ -433,7 +447,9 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
             same_1rank = bool(np.array_equal(w_g, e_1.w_host()))
             del e_1
         del e_g
-    launches = ("one persistent launch per segment" if eng.narrow_seg else
+    launches = ("one persistent launch per run of <= 4096 steps, reshuffles drawn in the "
+                "kernel" if swr else
+                "one persistent launch per segment" if eng.narrow_seg else
                 "one launch per step" if eng.fused else
                 "one segment kernel per segment" if eng.segment else "gradient + update per step")
     G = 1 if group is None else torch.distributed.get_world_size(group)

@@ -454,6 +454,19 @@ int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
                           const double* d_w_in, const double* d_dw_in, double reg, double lr,
                           double momentum, double* d_grads0, double* d_grads1, double* d_w_out,
                           double* d_dw_out, uint32_t* d_ctl, void* stream);
+/* tw_sgd_segment_narrow in device-RNG mode with the SWR row tables drawn IN the kernel: the
+ * row of draw position a of shard s at step counter c is the one tw_swr_rows_rng drew at the
+ * last reshuffle, counter rc = c - (c - swr_base) % swr_mod (reshuffles every swr_mod steps
+ * from swr_base: make_exps.py:123-125), so one launch runs through any number of reshuffles.
+ * Same bits as tw_swr_rows_rng at every reshuffle + tw_sgd_segment_narrow between them. */
+int tw_sgd_segment_narrow_swr(const double* d_X, const double* d_Z, int64_t d, int64_t n_X,
+                              int64_t n_Z, int64_t kx, int64_t kz, int32_t n_shards, int64_t B,
+                              double margin, int32_t loss, uint64_t seed, const uint64_t* d_step,
+                              int32_t shard_base, int32_t nsteps, int64_t swr_mod,
+                              uint64_t swr_base, const double* d_w_in, const double* d_dw_in,
+                              double reg, double lr, double momentum, double* d_grads0,
+                              double* d_grads1, double* d_w_out, double* d_dw_out,
+                              uint32_t* d_ctl, void* stream);
 int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
 int tw_sgd_segment_set_grid(int32_t max_blocks);
 int tw_sgd_segment_set_prefetch(int32_t rows);

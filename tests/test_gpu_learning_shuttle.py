@@ -263,3 +263,26 @@ def test_native_draw_pipe_protocol(gpu):
 def ctypes_handle():
     import ctypes
     return ctypes.byref(ctypes.c_void_p())
+
+
+@pytest.mark.parametrize("mod,eval_mod,n_it", [(1, 25, 101), (7, 25, 101), (10000, 25, 76),
+                                               (3, 2, 41)])
+def test_swr_in_kernel_equals_row_tables(gpu, golden, mod, eval_mod, n_it, monkeypatch):
+    """learning.SWR_IN_KERNEL (device RNG: the persistent narrow segment draws each reshuffle's
+    SWR rows itself, segments cut at evaluations only) against the row-table path (a
+    tw_swr_rows_rng launch and a new segment per reshuffle): the same statistics bit for bit,
+    with reshuffles inside segments, one-step tails whose tables a segment left stale, and
+    two-step segments."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for swr in (True, False):
+        monkeypatch.setattr(lr, "SWR_IN_KERNEL", swr)
+        X, Z, p = _p(mod, n_it=n_it)
+        p["eval_mod"] = eval_mod
+        np.random.seed(45)
+        lr.learning_process(X, Z, p, rng_mode="device")
+        out[swr] = p
+    for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        assert out[True][k] == out[False][k], k
+    assert len(out[True]["norm_w"]) == (n_it + eval_mod - 1) // eval_mod

@@ -367,7 +367,8 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     const uint64_t* __restrict__ d_step, uint32_t shard_base, int n_shards, int nsteps,
     const double* __restrict__ w_in, const double* __restrict__ dw_in, double reg, double lr,
     double momentum, double* grads0, double* grads1, double* __restrict__ w_out,
-    double* __restrict__ dw_out, uint32_t* ctl) {
+    double* __restrict__ dw_out, uint32_t* ctl, int64_t n_X, int64_t n_Z, uint64_t swr_mod,
+    uint64_t swr_base) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* diff = (double*)smem;         // B * d
   double* flag = diff + B * d;          // B pair weights
@@ -396,8 +397,20 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
         ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
         az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
       }
-      const int64_t rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-      const int64_t rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      int64_t rxt, rzt;
+      if (swr_mod) {
+        // the SWR row tables in the kernel (device RNG): the rows k_swr_rows drew at this
+        // step's last reshuffle, counter c - (c - base) % mod — one Philox per side, so a
+        // segment runs through its reshuffles without a table-drawing launch
+        const uint64_t c = step0 + (uint64_t)k, rc = c - (c - swr_base) % swr_mod;
+        const u32x4 qx = sgd_draw(seed, rc, (uint32_t)ax, shard_base + (uint32_t)s, kTagRowsX);
+        const u32x4 qz = sgd_draw(seed, rc, (uint32_t)az, shard_base + (uint32_t)s, kTagRowsZ);
+        rxt = (int64_t)mulhi_u64(((uint64_t)qx.b << 32) | qx.a, (uint64_t)n_X);
+        rzt = (int64_t)mulhi_u64(((uint64_t)qz.b << 32) | qz.a, (uint64_t)n_Z);
+      } else {
+        rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+        rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      }
       const double* zr = Z + rzt * d;
       const double* xr = X + rxt * d;
       double* dr = diff + (int64_t)t * d;
@@ -508,16 +521,16 @@ extern "C" int tw_sgd_segment_narrow_ok(int64_t d, int32_t n_shards, int64_t B) 
   return (int64_t)std::min(per_cu, 1) * cus >= n_shards;  // one block per CU at most
 }
 
-extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
-                                     const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
-                                     int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
-                                     int64_t draw_stride, int32_t n_shards, int64_t B,
-                                     double margin, int32_t loss, uint64_t seed,
-                                     const uint64_t* d_step, int32_t shard_base, int32_t nsteps,
-                                     const double* d_w_in, const double* d_dw_in, double reg,
-                                     double lr, double momentum, double* d_grads0,
-                                     double* d_grads1, double* d_w_out, double* d_dw_out,
-                                     uint32_t* d_ctl, void* stream) {
+static int segment_narrow(const double* d_X, const double* d_Z, int64_t d,
+                          const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                          int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                          int64_t draw_stride, int32_t n_shards, int64_t B, double margin,
+                          int32_t loss, uint64_t seed, const uint64_t* d_step,
+                          int32_t shard_base, int32_t nsteps, const double* d_w_in,
+                          const double* d_dw_in, double reg, double lr, double momentum,
+                          double* d_grads0, double* d_grads1, double* d_w_out, double* d_dw_out,
+                          uint32_t* d_ctl, int64_t n_X, int64_t n_Z, uint64_t swr_mod,
+                          uint64_t swr_base, void* stream) {
   // shape limits only: the residency query (tw_sgd_segment_narrow_ok) is a HIP API call the
   // caller makes once, before any stream capture — this entry runs inside captured graphs
   TW_ARG_CHECK(d >= 1 && d <= kNarrowMaxD && n_shards >= 1 &&
@@ -540,7 +553,8 @@ extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64
     hipLaunchKernelGGL(kern, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x, kx,
                        d_rows_z, kz, d_ix, d_iz, draw_stride, B, margin, seed, d_step,
                        (uint32_t)shard_base, (int)n_shards, (int)nsteps, d_w_in, d_dw_in, reg,
-                       lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl);
+                       lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl, n_X, n_Z,
+                       swr_mod, swr_base);
   };
   if (loss == TW_LOSS_LOGISTIC)
     go(k_sgd_segment_narrow<TW_LOSS_LOGISTIC>);
@@ -548,6 +562,40 @@ extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64
     go(k_sgd_segment_narrow<TW_LOSS_HINGE>);
   TW_LAUNCH_CHECK();
   return TW_OK;
+}
+
+extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
+                                     const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                                     int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                                     int64_t draw_stride, int32_t n_shards, int64_t B,
+                                     double margin, int32_t loss, uint64_t seed,
+                                     const uint64_t* d_step, int32_t shard_base, int32_t nsteps,
+                                     const double* d_w_in, const double* d_dw_in, double reg,
+                                     double lr, double momentum, double* d_grads0,
+                                     double* d_grads1, double* d_w_out, double* d_dw_out,
+                                     uint32_t* d_ctl, void* stream) {
+  return segment_narrow(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, draw_stride,
+                        n_shards, B, margin, loss, seed, d_step, shard_base, nsteps, d_w_in,
+                        d_dw_in, reg, lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl,
+                        1, 1, 0, 0, stream);
+}
+
+extern "C" int tw_sgd_segment_narrow_swr(const double* d_X, const double* d_Z, int64_t d,
+                                         int64_t n_X, int64_t n_Z, int64_t kx, int64_t kz,
+                                         int32_t n_shards, int64_t B, double margin,
+                                         int32_t loss, uint64_t seed, const uint64_t* d_step,
+                                         int32_t shard_base, int32_t nsteps, int64_t swr_mod,
+                                         uint64_t swr_base, const double* d_w_in,
+                                         const double* d_dw_in, double reg, double lr,
+                                         double momentum, double* d_grads0, double* d_grads1,
+                                         double* d_w_out, double* d_dw_out, uint32_t* d_ctl,
+                                         void* stream) {
+  TW_ARG_CHECK(swr_mod >= 1 && n_X >= 1 && n_Z >= 1 && d_step != nullptr,
+               "tw_sgd_segment_narrow_swr: swr_mod, n_X, n_Z >= 1 and d_step required");
+  return segment_narrow(d_X, d_Z, d, nullptr, kx, nullptr, kz, nullptr, nullptr, 0, n_shards,
+                        B, margin, loss, seed, d_step, shard_base, nsteps, d_w_in, d_dw_in, reg,
+                        lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl, n_X, n_Z,
+                        (uint64_t)swr_mod, swr_base, stream);
 }
 
 extern "C" int tw_sgd_segment_ok(int64_t d, int32_t n_shards) {

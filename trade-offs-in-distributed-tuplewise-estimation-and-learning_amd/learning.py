@@ -51,6 +51,10 @@ _ENGINE = {"key": None, "eng": None}
 # pipelined replay loop: each segment's narrowed draws and a reshuffle's row tables go up in ONE
 # launch (tw_ship_draws) instead of a widen and two row copies
 FUSED_SHIP = True
+# device-RNG loop: persistent narrow segments run through their reshuffles, the kernel drawing
+# each reshuffle's SWR rows (tw_sgd_segment_narrow_swr) instead of a row-table launch and a new
+# segment per reshuffle
+SWR_IN_KERNEL = True
 # pipelined replay loop: the draws made ahead by a native thread (csrc/drawpipe.hip) rather
 # than a Python worker thread
 NATIVE_DRAWS = True
@@ -188,7 +192,7 @@ class SGDEngine:
             raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
                                "co-resident); the SGD state is invalid")
 
-    def _fused_steps(self, nsteps: int, draws_dev=None):
+    def _fused_steps(self, nsteps: int, draws_dev=None, swr_mod=0):
         """nsteps steps as nsteps tw_sgd_step launches + one tw_sgd_update_to (ping-pong
         slots for w/dw/grads; slot 0 = self.w/self.dw/self.grads holds the state before and
         after).  Same bits as step()/step_device() + _update() per step."""
@@ -205,12 +209,20 @@ class SGDEngine:
             if draws_dev is not None:
                 ix, iz = draws_dev[0, 0], draws_dev[0, 1]
                 stride = int(draws_dev.stride(0))
-            L.call("tw_sgd_segment_narrow", L.ptr(self.X), L.ptr(self.Z), self.d,
-                   L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix), L.ptr(iz),
-                   stride, self.N_loc, self.B, self.margin, self.loss, seed,
-                   L.ptr(self.step_ctr), self.shard_base, nsteps, L.ptr(W[0]), L.ptr(DW[0]),
-                   self.reg, self.lr, self.momentum, L.ptr(Gs[0]), L.ptr(Gs[1]), L.ptr(W[1]),
-                   L.ptr(DW[1]), L.ptr(self._ctl), s)
+            if swr_mod:  # device RNG: the segment draws its reshuffles' rows itself
+                L.call("tw_sgd_segment_narrow_swr", L.ptr(self.X), L.ptr(self.Z), self.d,
+                       self.n_X, self.n_Z, self.kx, self.kz, self.N_loc, self.B, self.margin,
+                       self.loss, seed, L.ptr(self.step_ctr), self.shard_base, nsteps,
+                       int(swr_mod), 0, L.ptr(W[0]), L.ptr(DW[0]), self.reg, self.lr,
+                       self.momentum, L.ptr(Gs[0]), L.ptr(Gs[1]), L.ptr(W[1]), L.ptr(DW[1]),
+                       L.ptr(self._ctl), s)
+            else:
+                L.call("tw_sgd_segment_narrow", L.ptr(self.X), L.ptr(self.Z), self.d,
+                       L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix),
+                       L.ptr(iz), stride, self.N_loc, self.B, self.margin, self.loss, seed,
+                       L.ptr(self.step_ctr), self.shard_base, nsteps, L.ptr(W[0]),
+                       L.ptr(DW[0]), self.reg, self.lr, self.momentum, L.ptr(Gs[0]),
+                       L.ptr(Gs[1]), L.ptr(W[1]), L.ptr(DW[1]), L.ptr(self._ctl), s)
             last = (nsteps - 1) & 1
             L.call("tw_sgd_update_to", L.ptr(W[1]), L.ptr(DW[1]), L.ptr(W[0]), L.ptr(DW[0]),
                    L.ptr(Gs[last]), self.N, self.d, self.reg, self.lr, self.momentum,
@@ -490,8 +502,26 @@ class SGDEngine:
             self.rows_z = t.empty((self.N_loc, self.kz), dtype=t.int64, device=self.w.device)
         self._graphs = {}
 
-    def reshuffle_device(self):
+    def swr_segments_ok(self) -> bool:
+        """run_segment(swr_mod=) applies: device RNG, one process, replicated rows, the
+        persistent narrow segment, the incomplete gradient."""
+        return (getattr(self, "seed", None) is not None and self.G == 1 and self.narrow_seg
+                and self.layout == "replicated" and not self.complete)
+
+    def reshuffle_device(self, counter=None):
+        """New SWR row tables from the device RNG at the current step counter, or at `counter`
+        (the step of an earlier reshuffle: the tables a swr segment left stale)."""
         s = L.stream_handle()
+        if counter is not None:
+            t = self.t
+            if getattr(self, "_swr_ctr", None) is None:
+                self._swr_ctr = t.zeros((1,), dtype=t.int64, device=self.w.device)
+            self._swr_ctr.copy_(t.tensor([int(counter)], dtype=t.int64))
+            for side, rows, k, n in ((0, self.rows_x, self.kx, self.n_X),
+                                     (1, self.rows_z, self.kz, self.n_Z)):
+                L.call("tw_swr_rows_rng", L.ptr(rows), self.N_loc, k, n, self.seed,
+                       L.ptr(self._swr_ctr), side, self.shard_base, s)
+            return
         if self.layout == "partitioned":
             L.call("tw_swr_rows_rng", L.ptr(self.rows_all_x), self.N, self.kx, self.n_X,
                    self.seed, L.ptr(self.step_ctr), 0, 0, s)
@@ -514,9 +544,21 @@ class SGDEngine:
                L.ptr(self.grads_loc), L.stream_handle())
         self._update()
 
-    def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True):
+    def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True,
+                    swr_mod: int = 0):
         """nsteps device-RNG steps (reshuffling first if asked), replayed from a captured
-        hipGraph per distinct segment shape (eager when the step holds a collective)."""
+        hipGraph per distinct segment shape (eager when the step holds a collective).
+        swr_mod: the persistent narrow segment draws the SWR rows of every reshuffle (one every
+        swr_mod steps from step counter 0) itself (tw_sgd_segment_narrow_swr) — the device
+        row tables are then NOT updated (swr_segments_ok says when this applies)."""
+        if swr_mod:
+            assert self.swr_segments_ok() and nsteps > 1 and not reshuffle_first
+            if self.fused and self._slot1 is None:
+                t = self.t
+                self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw),
+                               t.empty_like(self.grads))
+            self._fused_steps(nsteps, swr_mod=swr_mod)
+            return
         if reshuffle_first and self.layout == "partitioned":
             self.reshuffle_device()  # the exchange sizes its buffers on the host: not captured
             reshuffle_first = False
@@ -1309,9 +1351,29 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
     if trajectory is not None:
         graphs = False
     defer = _deferred_evals(eng, graphs, trajectory)
+    # segments through their reshuffles (the kernel draws the rows) where nothing reads the
+    # device row tables: FIXED_PAIRS monitoring, no per-step trajectory
+    swr = (SWR_IN_KERNEL and trajectory is None and TYPE_TRAIN_MONITOR == "FIXED_PAIRS"
+           and isinstance(eng, SGDEngine) and eng.swr_segments_ok())
+    stale = False  # the device tables lag behind a swr segment's reshuffles
     i = 0
     while i < n_it:
         resh = i % mod == 0
+        if swr:
+            if i % eval_mod == 0:
+                evaluation_step(i, None, None, None if defer is not None else eng.w_host(),
+                                p_learn, loss=loss, _w_dev=eng.w, _graph=graphs, _defer=defer)
+            nxt = min(n_it, (i // eval_mod + 1) * eval_mod)
+            if nxt - i > 1:
+                eng.run_segment(nxt - i, False, graphs, swr_mod=mod)
+                stale = True
+            else:  # one step: the row tables, drawn at this step's last reshuffle
+                if resh or stale:
+                    eng.reshuffle_device(counter=None if resh else i - i % mod)
+                    stale = False
+                eng.run_segment(1, False, graphs)
+            i = nxt
+            continue
         if i % eval_mod == 0:
             batch = None
             if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
