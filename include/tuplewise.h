@@ -467,6 +467,21 @@ int tw_sgd_segment_narrow_swr(const double* d_X, const double* d_Z, int64_t d, i
                               double reg, double lr, double momentum, double* d_grads0,
                               double* d_grads1, double* d_w_out, double* d_dw_out,
                               uint32_t* d_ctl, void* stream);
+/* evaluation_step's FIXED_PAIRS statistics (make_exps.py:143-190) for small problems in two
+ * launches: the scores A @ w of train X (n_trX x d), train Z, test X, test Z into d_scores
+ * (concatenated, k_gemv's arithmetic), then the monitor pairs' surrogate sum and AUC count
+ * (d_ix/d_iz: n_pairs int32 row indices; d_offs = {0, n_pairs, 0, n_teX, 0, n_teZ} on the
+ * device) and all test pairs' surrogate sum and AUC count, reduced in one launch: d_out =
+ * {monitor sum, monitor count (uint64 bits), test sum, test count (uint64 bits)} — the same
+ * values as tw_gemv_f64 + tw_pair_sum_idx32_f64 + tw_pair_sum_f64 + tw_count_pairs.  d_work /
+ * d_cwork: tw_eval_small_work(...) entries each; d_ticket: one zeroed word (left zero). */
+int64_t tw_eval_small_work(int64_t n_pairs, int64_t n_test_x, int64_t n_test_z);
+int tw_eval_small(const double* d_trX, int64_t n_trX, const double* d_trZ, int64_t n_trZ,
+                  const double* d_teX, int64_t n_teX, const double* d_teZ, int64_t n_teZ,
+                  int64_t d, const double* d_w, const int32_t* d_ix, const int32_t* d_iz,
+                  int64_t n_pairs, const int64_t* d_offs, int32_t kern, double margin,
+                  double* d_scores, double* d_work, uint64_t* d_cwork, uint32_t* d_ticket,
+                  double* d_out, void* stream);
 int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
 int tw_sgd_segment_set_grid(int32_t max_blocks);
 int tw_sgd_segment_set_prefetch(int32_t rows);

@@ -440,3 +440,36 @@ def test_deferred_evals_slot_reuse(gpu):
     assert [s[0] for s in seen] == list(range(20))
     for j, r, ww in seen:
         assert r == [float(j)] * 4 and ww == [-float(j)] * 5
+
+
+@pytest.mark.parametrize("loss", ["hinge", "logistic"])
+@pytest.mark.parametrize("mode", ["replay", "device"])
+def test_fused_evaluation_equals_separate_launches(gpu, golden, loss, mode, monkeypatch):
+    """learning.EVAL_FUSED (evaluation_step's FIXED_PAIRS statistics in two launches,
+    tw_eval_small) against the separate GEMV / pair-sum / count launches: the same lists bit
+    for bit (the fused kernel runs the same blocks and reduces in the same order); the replay
+    hinge run also against the reference's golden lists.  Out-of-range monitor pairs raise
+    IndexError instead of reading past the scores."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(lr, "EVAL_FUSED", fused)
+        p = _p_learn(golden)
+        np.random.seed(2024)
+        lr.learning_process(p["train_X"], p["train_Z"], p, rng_mode=mode, loss=loss)
+        out[fused] = p
+    for k in ("iter", "norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        assert out[True][k] == out[False][k], k
+    if mode == "replay" and loss == "hinge":
+        q = out[True]
+        np.testing.assert_allclose(q["norm_w"], golden["learn/norm_w"], rtol=1e-10)
+        for k in ("bc_AUC", "tc_AUC"):
+            np.testing.assert_allclose(q[k], golden[f"learn/{k}"], rtol=1e-9)
+        for k in ("br_AUC", "tr_AUC"):
+            np.testing.assert_allclose(q[k], golden[f"learn/{k}"], rtol=0, atol=1e-12)
+    monkeypatch.setattr(lr, "EVAL_FUSED", True)
+    p = _p_learn(golden, n_it=3)
+    p["train_mon_pairs"] = [(0, 0), (len(p["train_X"]), 0)]
+    with pytest.raises(IndexError):
+        lr.evaluation_step(0, None, None, p["w_init"], p)

@@ -140,6 +140,9 @@ _SIGNATURES = {
     "tw_widen_u16": [_vp, _i64, _vp, _vp],
     "tw_np_randint_pairs_steps_u8": [_vp, _vp, _i32, _i32, _i64, _i64, _i64, _vp],
     "tw_widen_u8": [_vp, _i64, _vp, _vp],
+    "tw_eval_small_work": [_i64, _i64, _i64],
+    "tw_eval_small": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _i64,
+                      _vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "tw_ship_draws": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp],
     "tw_draw_pipe_start": [_vp, _vp, _i32, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32,
                            _i32, _vp, _vp, _vp],
@@ -166,6 +169,7 @@ _RESTYPES = {
     "tw_pair_grad_complete_work_bytes": ctypes.c_int64,
     "tw_pair_hinge_sum_sorted_work_bytes": ctypes.c_int64,
     "tw_shuffle_swaps_work_bytes": ctypes.c_int64,
+    "tw_eval_small_work": ctypes.c_int64,
 }
 
 _lib = None

@@ -67,16 +67,30 @@ __device__ __forceinline__ double fkern_loop(double x, double z, double margin) 
   else return fkern<K>(x, z, margin);
 }
 
-template <int K>
-__global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ x,
-                                                     const int64_t* __restrict__ x_off,
-                                                     const double* __restrict__ z,
-                                                     const int64_t* __restrict__ z_off,
-                                                     int tiles_x, int zchunks, double margin,
-                                                     double* __restrict__ work) {
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v) {
+  v = wave_sum_u64(v);
+  __shared__ unsigned long long partc[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) partc[wid] = v;
+  __syncthreads();
+  unsigned long long b = 0;
+  if (threadIdx.x == 0) b = (partc[0] + partc[1]) + (partc[2] + partc[3]);
+  return b;
+}
+
+// One block of k_pair_sum — (shard, x tile, z chunk) number `bid` — returning its partial (on
+// thread 0).  CNT: also #{x > z} over the block's pairs into *cnt (thread 0; a NaN compares
+// false, as k_count_complete's v_cmp_gt_f64).
+template <int K, bool CNT>
+__device__ __forceinline__ double pair_sum_block(const double* __restrict__ x,
+                                                 const int64_t* __restrict__ x_off,
+                                                 const double* __restrict__ z,
+                                                 const int64_t* __restrict__ z_off, int tiles_x,
+                                                 int zchunks, double margin, int bid,
+                                                 unsigned long long* cnt) {
   const int per_shard = tiles_x * zchunks;
-  const int s = blockIdx.x / per_shard;
-  const int rem = blockIdx.x - s * per_shard;
+  const int s = bid / per_shard;
+  const int rem = bid - s * per_shard;
   const int cz = rem / tiles_x;
   const int tx = rem - cz * tiles_x;
   const int64_t xb = x_off[s], xe = x_off[s + 1];
@@ -84,8 +98,8 @@ __global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ 
   const int64_t x0 = xb + (int64_t)tx * (kBlock * kSumR);
   const int64_t z0 = zb + (int64_t)cz * kSumZChunk;
   if (x0 >= xe || z0 >= ze) {  // block-uniform; the slot must still be written
-    if (threadIdx.x == 0) work[blockIdx.x] = 0.0;
-    return;
+    if (CNT) *cnt = 0;
+    return 0.0;
   }
   const int64_t z1 = std::min(ze, z0 + kSumZChunk);
   double xv[kSumR], acc[kSumR];
@@ -99,15 +113,25 @@ __global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ 
   }
   const double* __restrict__ zp = z + z0;
   const int nz = (int)(z1 - z0);
+  unsigned cr[kSumR] = {};
 #pragma unroll 4
   for (int j = 0; j < nz; ++j) {
     const double zv = zp[j];
 #pragma unroll
-    for (int r = 0; r < kSumR; ++r) acc[r] += fkern_loop<K>(xv[r], zv, margin);
+    for (int r = 0; r < kSumR; ++r) {
+      acc[r] += fkern_loop<K>(xv[r], zv, margin);
+      if (CNT) cr[r] += xv[r] > zv;
+    }
   }
   double t = 0.0;
 #pragma unroll
   for (int r = 0; r < kSumR; ++r) t += valid[r] ? acc[r] : 0.0;
+  if (CNT) {
+    unsigned long long c = 0;
+#pragma unroll
+    for (int r = 0; r < kSumR; ++r) c += valid[r] ? cr[r] : 0u;
+    *cnt = block_sum_u64(c);
+  }
   int xbits = 0, zbits = 0;
   if constexpr (K == TW_KERN_HINGE) {
 #pragma unroll
@@ -120,29 +144,37 @@ __global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ 
             (__syncthreads_or(xbits & 4) ? 4 : 0);
     zbits = __syncthreads_or(zbits & 1) | (__syncthreads_or(zbits & 2) ? 2 : 0) |
             (__syncthreads_or(zbits & 4) ? 4 : 0);
-    if (threadIdx.x == 0)
-      work[blockIdx.x] = ((xbits | zbits) & 1) || (xbits & zbits & 6)
-                             ? __longlong_as_double(0x7FF8000000000000ll)
-                             : b;
-  } else {
-    if (threadIdx.x == 0) work[blockIdx.x] = b;
+    return ((xbits | zbits) & 1) || (xbits & zbits & 6)
+               ? __longlong_as_double(0x7FF8000000000000ll)
+               : b;
   }
+  return b;
 }
 
-// I: int64_t or int32_t indices.  COUNT: the same pass also counts x > z per shard into
-// count[s] (evaluation_step's br_AUC = UB_pairs(kernel="AUC") on the monitor pairs whose hinge
-// mean it computes, make_exps.py:162-168): one read of the index streams for both statistics.
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_pair_sum(const double* __restrict__ x,
+                                                     const int64_t* __restrict__ x_off,
+                                                     const double* __restrict__ z,
+                                                     const int64_t* __restrict__ z_off,
+                                                     int tiles_x, int zchunks, double margin,
+                                                     double* __restrict__ work) {
+  const double b = pair_sum_block<K, false>(x, x_off, z, z_off, tiles_x, zchunks, margin,
+                                            (int)blockIdx.x, nullptr);
+  if (threadIdx.x == 0) work[blockIdx.x] = b;
+}
+
+// One block of k_pair_sum_idx, number `bid`: its partial (thread 0) and, COUNT, its pairs'
+// #{x > z} (every lane's own count; the caller reduces them)
 template <int K, int PPT, typename I, bool COUNT>
-__global__ __launch_bounds__(kBlock) void k_pair_sum_idx(const double* __restrict__ x,
-                                                         const double* __restrict__ z,
-                                                         const I* __restrict__ ix,
-                                                         const I* __restrict__ iz,
-                                                         const int64_t* __restrict__ pair_off,
-                                                         int blocks_per_shard, double margin,
-                                                         double* __restrict__ work,
-                                                         unsigned long long* __restrict__ count) {
-  const int s = blockIdx.x / blocks_per_shard;
-  const int bi = blockIdx.x - s * blocks_per_shard;
+__device__ __forceinline__ double pair_sum_idx_block(const double* __restrict__ x,
+                                                     const double* __restrict__ z,
+                                                     const I* __restrict__ ix,
+                                                     const I* __restrict__ iz,
+                                                     const int64_t* __restrict__ pair_off,
+                                                     int blocks_per_shard, double margin,
+                                                     int bid, unsigned* lane_cnt) {
+  const int s = bid / blocks_per_shard;
+  const int bi = bid - s * blocks_per_shard;
   const int64_t pb = pair_off[s], pe = pair_off[s + 1];
   const int64_t p0 = pb + (int64_t)bi * (kBlock * PPT);
   double acc = 0.0;
@@ -158,9 +190,29 @@ __global__ __launch_bounds__(kBlock) void k_pair_sum_idx(const double* __restric
       }
     }
   }
-  const double b = block_sum_f64(acc);
+  if (COUNT) *lane_cnt = cnt;
+  return block_sum_f64(acc);
+}
+
+// I: int64_t or int32_t indices.  COUNT: the same pass also counts x > z per shard into
+// count[s] (evaluation_step's br_AUC = UB_pairs(kernel="AUC") on the monitor pairs whose hinge
+// mean it computes, make_exps.py:162-168): one read of the index streams for both statistics.
+template <int K, int PPT, typename I, bool COUNT>
+__global__ __launch_bounds__(kBlock) void k_pair_sum_idx(const double* __restrict__ x,
+                                                         const double* __restrict__ z,
+                                                         const I* __restrict__ ix,
+                                                         const I* __restrict__ iz,
+                                                         const int64_t* __restrict__ pair_off,
+                                                         int blocks_per_shard, double margin,
+                                                         double* __restrict__ work,
+                                                         unsigned long long* __restrict__ count) {
+  unsigned cnt = 0;
+  const double b = pair_sum_idx_block<K, PPT, I, COUNT>(x, z, ix, iz, pair_off,
+                                                        blocks_per_shard, margin,
+                                                        (int)blockIdx.x, &cnt);
   if (threadIdx.x == 0) work[blockIdx.x] = b;
   if constexpr (COUNT) {
+    const int s = (int)blockIdx.x / blocks_per_shard;
     const unsigned long long w = wave_sum_u64((unsigned long long)cnt);
     if ((threadIdx.x & (kWave - 1)) == 0 && w) atomicAdd(count + s, w);
   }
@@ -178,6 +230,91 @@ __global__ __launch_bounds__(kWave) void k_reduce_partials(const double* __restr
 }
 
 constexpr int kSumPPT = 8;
+
+// ---------------------------------------------------------------- fused evaluation (round 3)
+// evaluation_step's FIXED_PAIRS statistics for small problems (make_exps.py:143-190: the C4
+// loop evaluates every 25 steps) in TWO launches instead of a dozen: k_eval_scores computes the
+// four score vectors (train X, train Z, test X, test Z) with k_gemv's per-row arithmetic;
+// k_eval_pairs runs the blocks of k_pair_sum_idx (the monitor pairs: surrogate sum + AUC count)
+// and of k_pair_sum (all test pairs: surrogate sum + AUC count) side by side, and the block
+// that arrives last reduces both partial arrays with k_reduce_partials' order.  Same bits as
+// the separate launches (tests/test_gpu_learning.py).  Hand-off: every block's thread 0 stores
+// its partials write-through (sc1), waits for them (vmcnt(0)) and takes a ticket; the last
+// ticket's block reads them with sc1 loads (MI355X_MICROARCH.md "Valid forms", row 1).
+__device__ __forceinline__ void st_sc1_u64(void* p, unsigned long long v) {
+  __hip_atomic_store((unsigned long long*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const void* p) {
+  return __hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kBlock) void k_eval_scores(const double* __restrict__ a0, int64_t n0,
+                                                        const double* __restrict__ a1, int64_t n1,
+                                                        const double* __restrict__ a2, int64_t n2,
+                                                        const double* __restrict__ a3, int64_t n3,
+                                                        int64_t d, const double* __restrict__ w,
+                                                        double* __restrict__ out) {
+  const int64_t tot = n0 + n1 + n2 + n3;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * kBlock) {
+    const double* row = i < n0             ? a0 + i * d
+                        : i < n0 + n1      ? a1 + (i - n0) * d
+                        : i < n0 + n1 + n2 ? a2 + (i - n0 - n1) * d
+                                           : a3 + (i - n0 - n1 - n2) * d;
+    double a = 0.0;  // k_gemv's order: j = 0 .. d-1, multiply then add (no contraction)
+    for (int64_t j = 0; j < d; ++j) a += row[j] * w[j];
+    out[i] = a;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_eval_pairs(
+    const double* __restrict__ sx, const double* __restrict__ sz, const int32_t* __restrict__ ix,
+    const int32_t* __restrict__ iz, const int64_t* __restrict__ offs, int per_idx,
+    const double* __restrict__ tx, const double* __restrict__ tz, int tiles_x, int zchunks,
+    double margin, double* work, unsigned long long* cwork, unsigned* ticket, double* out) {
+  const int nb = per_idx + tiles_x * zchunks;
+  double v;
+  unsigned long long c = 0;
+  if ((int)blockIdx.x < per_idx) {
+    unsigned lc = 0;
+    v = pair_sum_idx_block<K, kSumPPT, int32_t, true>(sx, sz, ix, iz, offs, per_idx, margin,
+                                                      (int)blockIdx.x, &lc);
+    c = block_sum_u64(lc);
+  } else {
+    v = pair_sum_block<K, true>(tx, offs + 2, tz, offs + 4, tiles_x, zchunks, margin,
+                                (int)blockIdx.x - per_idx, &c);
+  }
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    st_sc1_u64(work + blockIdx.x, __double_as_longlong(v));
+    st_sc1_u64(cwork + blockIdx.x, c);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)nb - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  if (wid < 2) {  // wave 0: the monitor pairs' partials, wave 1: the test pairs'
+    const int base = wid == 0 ? 0 : per_idx, per = wid == 0 ? per_idx : nb - per_idx;
+    double sum = 0.0;
+    unsigned long long cc = 0;
+    for (int i = lane; i < per; i += kWave) {
+      sum += __longlong_as_double(ld_sc1_u64(work + base + i));
+      cc += ld_sc1_u64(cwork + base + i);
+    }
+    sum = wave_sum_f64(sum);
+    cc = wave_sum_u64(cc);
+    if (lane == 0) {
+      out[2 * wid] = sum;
+      out[2 * wid + 1] = __longlong_as_double((long long)cc);
+    }
+  }
+  if (threadIdx.x == 0)  // the next launch starts from zero (no memset node in its graph)
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 }  // namespace tw
 
@@ -261,4 +398,47 @@ extern "C" int tw_pair_sum_idx32_f64(const double* d_x, const double* d_z, const
   TW_HIP_CHECK(tw_zero_async(d_count, 0, sizeof(uint64_t) * n_shards, st));
   return pair_sum_idx<int32_t, true>(d_x, d_z, d_ix, d_iz, d_pair_off, n_shards, max_pairs, kern,
                                      margin, d_work, d_out, d_count, st);
+}
+
+extern "C" int64_t tw_eval_small_work(int64_t n_pairs, int64_t n_test_x, int64_t n_test_z) {
+  const SumPlan p = plan_sum(n_test_x, n_test_z);
+  return tw_pair_sum_idx_work_per_shard(n_pairs) + (int64_t)p.tiles_x * p.zchunks;
+}
+
+extern "C" int tw_eval_small(const double* d_trX, int64_t n_trX, const double* d_trZ,
+                             int64_t n_trZ, const double* d_teX, int64_t n_teX,
+                             const double* d_teZ, int64_t n_teZ, int64_t d, const double* d_w,
+                             const int32_t* d_ix, const int32_t* d_iz, int64_t n_pairs,
+                             const int64_t* d_offs, int32_t kern, double margin,
+                             double* d_scores, double* d_work, uint64_t* d_cwork,
+                             uint32_t* d_ticket, double* d_out, void* stream) {
+  TW_ARG_CHECK(n_trX >= 1 && n_trZ >= 1 && n_teX >= 1 && n_teZ >= 1 && d >= 1 && n_pairs >= 1,
+               "tw_eval_small: empty operand");
+  TW_ARG_CHECK(kern == TW_KERN_HINGE || kern == TW_KERN_LOGISTIC,
+               "tw_eval_small: hinge or logistic only (kernel %d)", kern);
+  const SumPlan p = plan_sum(n_teX, n_teZ);
+  const int64_t per_idx = tw_pair_sum_idx_work_per_shard(n_pairs);
+  const int64_t nb = per_idx + (int64_t)p.tiles_x * p.zchunks;
+  TW_ARG_CHECK(nb < (1ll << 31), "tw_eval_small: grid too large");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rows = n_trX + n_trZ + n_teX + n_teZ;
+  const int gs = (int)std::min<int64_t>(4096, ceil_div(rows, kBlock));
+  hipLaunchKernelGGL(k_eval_scores, dim3(gs), dim3(kBlock), 0, st, d_trX, n_trX, d_trZ, n_trZ,
+                     d_teX, n_teX, d_teZ, n_teZ, d, d_w, d_scores);
+  TW_LAUNCH_CHECK();
+  const double* sx = d_scores;
+  const double* sz = sx + n_trX;
+  const double* tx = sz + n_trZ;
+  const double* tz = tx + n_teX;
+  auto go = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, sx, sz, d_ix, d_iz,
+                       d_offs, (int)per_idx, tx, tz, p.tiles_x, p.zchunks, margin, d_work,
+                       (unsigned long long*)d_cwork, d_ticket, d_out);
+  };
+  if (kern == TW_KERN_HINGE)
+    go(k_eval_pairs<TW_KERN_HINGE>);
+  else
+    go(k_eval_pairs<TW_KERN_LOGISTIC>);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
 }

@@ -55,6 +55,9 @@ FUSED_SHIP = True
 # each reshuffle's SWR rows (tw_sgd_segment_narrow_swr) instead of a row-table launch and a new
 # segment per reshuffle
 SWR_IN_KERNEL = True
+# evaluation_step (FIXED_PAIRS) on small problems: scores, monitor and test statistics in two
+# launches (tw_eval_small) instead of a dozen, same values
+EVAL_FUSED = True
 # pipelined replay loop: the draws made ahead by a native thread (csrc/drawpipe.hip) rather
 # than a Python worker thread
 NATIVE_DRAWS = True
@@ -1483,6 +1486,14 @@ def _pairs_dev(pairs):
             L.to_device(np.ascontiguousarray(a[:, 1]), dt), off, L.to_device(off))
 
 
+def _pairs_range(pairs):
+    """(min x, max x, min z, max z) of the monitor pairs ((0, -1, 0, -1) when empty)."""
+    a = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    if a.size == 0:
+        return 0, -1, 0, -1
+    return int(a[:, 0].min()), int(a[:, 0].max()), int(a[:, 1].min()), int(a[:, 1].max())
+
+
 def _scores(A_dev, wd):
     """A @ w on the device (tw_gemv_f64); wd: w as a (d,) float64 device tensor."""
     t = L.torch()
@@ -1516,6 +1527,16 @@ def _eval_device(wd, p_learn, loss, margin, fixed):
     bits, test surrogate sum, test count bits], #monitor pairs, #test pairs)."""
     t = L.torch()
     kern = cs._loss_codes(loss)[0]
+    if fixed:  # the monitor pairs index the training scores (make_exps.py:162-168)
+        lo_x, hi_x, lo_z, hi_z = _CACHE.get("pairs_range", p_learn["train_mon_pairs"],
+                                            _pairs_range)
+        nx, nz = len(p_learn["train_X"]), len(p_learn["train_Z"])
+        if lo_x < 0 or lo_z < 0 or hi_x >= nx or hi_z >= nz:
+            raise IndexError(f"train_mon_pairs index out of range for {nx} x {nz} rows "
+                             f"(x in [{lo_x}, {hi_x}], z in [{lo_z}, {hi_z}])")
+    small = _eval_small(wd, p_learn, kern, margin) if fixed and EVAL_FUSED else None
+    if small is not None:
+        return small
     parts = []
     n_pairs = 0
     if fixed:
@@ -1548,6 +1569,44 @@ def _eval_device(wd, p_learn, loss, margin, fixed):
               E.count_launch(sxt, xod, szt, zod, 1, n, m, L.TW_F64, L.TW_PRED_GT,
                              E.pick_algo("auto", n, m, "gt")).view(t.float64)]
     return t.cat([v.reshape(-1) for v in parts]), n_pairs, n * m
+
+
+def _eval_small(wd, p_learn, kern, margin):
+    """_eval_device's FIXED_PAIRS statistics in two launches (tw_eval_small) when the problem
+    is small enough for the all-pairs test statistics (the paths _eval_device would take
+    anyway) and the monitor pairs are int32: the same values, or None."""
+    t = L.torch()
+    if kern not in (L.TW_KERN_HINGE, L.TW_KERN_LOGISTIC):
+        return None
+    tX = _CACHE.get("train_X", p_learn["train_X"], _dev_f64)
+    tZ = _CACHE.get("train_Z", p_learn["train_Z"], _dev_f64)
+    eX = _CACHE.get("test_X", p_learn["test_X"], _dev_f64)
+    eZ = _CACHE.get("test_Z", p_learn["test_Z"], _dev_f64)
+    ixd, izd, off, offd = _CACHE.get("pairs", p_learn["train_mon_pairs"], _pairs_dev)
+    mats = (tX, tZ, eX, eZ)
+    if any(a.dim() != 2 or a.shape[1] != wd.numel() or a.shape[0] == 0 for a in mats):
+        return None
+    n, m, n_pairs = eX.shape[0], eZ.shape[0], int(off[1])
+    if (ixd.dtype != t.int32 or wd.numel() > 32 or n_pairs == 0 or len(off) != 2
+            or n * m >= E.HINGE_SORTED_MIN_PAIRS
+            or E.pick_algo("auto", n, m, "gt") != "pairs"):
+        return None
+    key = ("eval_small",) + tuple(a.shape[0] for a in mats) + (n_pairs, wd.numel())
+    bufs = _CACHE.dev.get(key)
+    if bufs is None:  # made outside any capture (evaluation_step warms before capturing)
+        nw = int(L.lib().tw_eval_small_work(n_pairs, n, m))
+        rows = sum(a.shape[0] for a in mats)
+        bufs = (L.empty((rows,), t.float64), L.empty((nw,), t.float64),
+                L.empty((nw,), t.int64), t.zeros((1,), dtype=t.int32, device=wd.device),
+                L.to_device(np.array([0, n_pairs, 0, n, 0, m], dtype=np.int64)))
+        _CACHE.dev[key] = bufs
+    scores, work, cwork, ticket, offs = bufs
+    out = L.empty((4,), t.float64)
+    L.call("tw_eval_small", L.ptr(tX), tX.shape[0], L.ptr(tZ), tZ.shape[0], L.ptr(eX), n,
+           L.ptr(eZ), m, wd.numel(), L.ptr(wd), L.ptr(ixd), L.ptr(izd), n_pairs, L.ptr(offs),
+           kern, float(margin), L.ptr(scores), L.ptr(work), L.ptr(cwork), L.ptr(ticket),
+           L.ptr(out), L.stream_handle())
+    return out, n_pairs, n * m
 
 
 def _same_as_batch_device(batch, wd, margin, loss):
