@@ -482,6 +482,14 @@ int tw_eval_small(const double* d_trX, int64_t n_trX, const double* d_trZ, int64
                   int64_t n_pairs, const int64_t* d_offs, int32_t kern, double margin,
                   double* d_scores, double* d_work, uint64_t* d_cwork, uint32_t* d_ticket,
                   double* d_out, void* stream);
+/* tw_pair_grad_rng with the SWR rows drawn in the kernel (reshuffles every swr_mod steps from
+ * counter swr_base; the rows of tw_swr_rows_rng at the last reshuffle): the per-step gradient
+ * of wide rows (C5) needs no row tables and no table-drawing launch per reshuffle. */
+int tw_pair_grad_rng_swr(const double* d_X, const double* d_Z, int64_t d, int64_t n_X,
+                         int64_t n_Z, int64_t kx, int64_t kz, int32_t n_shards, int64_t B,
+                         const double* d_w, double margin, int32_t loss, uint64_t seed,
+                         const uint64_t* d_step, int32_t shard_base, int64_t swr_mod,
+                         uint64_t swr_base, double* d_out, void* stream);
 int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
 int tw_sgd_segment_set_grid(int32_t max_blocks);
 int tw_sgd_segment_set_prefetch(int32_t rows);

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     int CH, const double* __restrict__ w, double margin, double* __restrict__ out,
     uint64_t seed, const uint64_t* __restrict__ d_step, uint32_t shard_base,
-    double* __restrict__ s_out = nullptr) {
+    double* __restrict__ s_out, SwrMap swr) {
   // s_out (tw_pair_grad_audit): S_b = diff_b . w + margin of every pair, as this kernel
   // computed it, at s_out[s * B + b] — the value whose sign is the hinge filter
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -83,8 +83,8 @@ __global__ __launch_bounds__(BS) void k_hinge_grad(
         ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
         az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
       }
-      const int64_t rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-      const int64_t rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      int64_t rxt, rzt;
+      swr_rows_of(swr, rows_x, kx, rows_z, kz, s, shard_base, ax, az, seed, step, rxt, rzt);
       if (d <= 32) {  // narrow rows: this thread stages its own pair right away (no barrier)
         const double* zr = Z + rzt * d;
         const double* xr = X + rxt * d;
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
-    const uint64_t* __restrict__ d_step, uint32_t shard_base) {
+    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr) {
   __shared__ double diff[kWideCH * kWideMaxD];  // 128 KiB
   __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
   __shared__ double flag[kWideCH];  // pair weights
@@ -215,8 +215,8 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
         ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
         az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
       }
-      prx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-      prz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      swr_rows_of(swr, rows_x, kx, rows_z, kz, s, shard_base, ax, az, seed, step, prx[t],
+                  prz[t]);
     }
     __syncthreads();
 
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
-    const uint64_t* __restrict__ d_step, uint32_t shard_base) {
+    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr) {
   __shared__ double diff[2][kStreamCH * kWideMaxD];  // 128 KiB
   __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
   __shared__ double flag[2][kStreamCH];
@@ -326,8 +326,8 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
         ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
         az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
       }
-      prx[t] = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-      prz[t] = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+      swr_rows_of(swr, rows_x, kx, rows_z, kz, s, shard_base, ax, az, seed, step, prx[t],
+                  prz[t]);
     }
     __syncthreads();
     if (P0 == 0) HG_STAMP(1);
@@ -618,7 +618,7 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
                         const int64_t* iz, int32_t n_shards, int64_t B, const double* w,
                         double margin, uint64_t seed, const uint64_t* d_step,
                         uint32_t shard_base, double* out, hipStream_t st,
-                        double* s_out = nullptr) {
+                        double* s_out = nullptr, SwrMap swr = SwrMap{0, 0, 1, 1}) {
   // per staged pair: d diff doubles + two row indices + one weight, <= 64 KiB in all
   const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / (d + 3)));
   const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(double) * CH;
@@ -627,42 +627,43 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
     if (d <= 32)
       hipLaunchKernelGGL((k_hinge_grad<kBlock, LOSS>), dim3(n_shards), dim3(kBlock), lds, st, X,
                          Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed,
-                         d_step, shard_base, s_out);
+                         d_step, shard_base, s_out, swr);
     else
       hipLaunchKernelGGL((k_hinge_grad<kWideBlock, LOSS>), dim3(n_shards), dim3(kWideBlock), lds,
                          st, X, Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out,
-                         seed, d_step, shard_base, s_out);
+                         seed, d_step, shard_base, s_out, swr);
     return;
   }
   if (d <= 32)
     hipLaunchKernelGGL((k_hinge_grad<kBlock, LOSS>), dim3(n_shards), dim3(kBlock), lds, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
-                       shard_base, nullptr);
+                       shard_base, nullptr, swr);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 0)
     hipLaunchKernelGGL(k_hinge_grad_stream<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
-                       shard_base);
+                       shard_base, swr);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 2)
     hipLaunchKernelGGL(k_hinge_grad_wide<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
-                       shard_base);
+                       shard_base, swr);
   else
     hipLaunchKernelGGL((k_hinge_grad<kWideBlock, LOSS>), dim3(n_shards), dim3(kWideBlock), lds, st,
                        X, Z, d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed,
-                       d_step, shard_base, nullptr);
+                       d_step, shard_base, nullptr, swr);
 }
 
 int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* rows_x, int64_t kx,
                  const int64_t* rows_z, int64_t kz, const int64_t* ix, const int64_t* iz,
                  int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
                  const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st,
-                 int32_t loss = TW_LOSS_HINGE, double* s_out = nullptr) {
+                 int32_t loss = TW_LOSS_HINGE, double* s_out = nullptr,
+                 SwrMap swr = SwrMap{0, 0, 1, 1}) {
   if (loss == TW_LOSS_LOGISTIC)
     launch_grad_kernel<TW_LOSS_LOGISTIC>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                         margin, seed, d_step, shard_base, out, st, s_out);
+                                         margin, seed, d_step, shard_base, out, st, s_out, swr);
   else
     launch_grad_kernel<TW_LOSS_HINGE>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                      margin, seed, d_step, shard_base, out, st, s_out);
+                                      margin, seed, d_step, shard_base, out, st, s_out, swr);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -856,6 +857,25 @@ extern "C" int tw_pair_grad_rng(const double* d_X, const double* d_Z, int64_t d,
   TW_ARG_CHECK(shard_base >= 0, "tw_hinge_grad_rng: shard_base < 0");
   return launch_hinge(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, nullptr, nullptr, n_shards, B,
                       d_w, margin, seed, d_step, (uint32_t)shard_base, d_out, st, loss);
+}
+
+extern "C" int tw_pair_grad_rng_swr(const double* d_X, const double* d_Z, int64_t d,
+                                    int64_t n_X, int64_t n_Z, int64_t kx, int64_t kz,
+                                    int32_t n_shards, int64_t B, const double* d_w,
+                                    double margin, int32_t loss, uint64_t seed,
+                                    const uint64_t* d_step, int32_t shard_base, int64_t swr_mod,
+                                    uint64_t swr_base, double* d_out, void* stream) {
+  TW_ARG_CHECK(d >= 1 && d <= kMaxD, "tw_pair_grad_rng_swr: d=%lld outside [1, %d]",
+               (long long)d, kMaxD);
+  TW_ARG_CHECK(n_shards >= 0 && B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1 &&
+                   n_X >= 1 && n_Z >= 1 && swr_mod >= 1 && shard_base >= 0,
+               "tw_pair_grad_rng_swr: bad sizes");
+  TW_ARG_CHECK(d_step != nullptr, "tw_pair_grad_rng_swr: step counter required");
+  if (int rc = check_loss(loss)) return rc;
+  if (n_shards == 0) return TW_OK;
+  return launch_hinge(d_X, d_Z, d, nullptr, kx, nullptr, kz, nullptr, nullptr, n_shards, B, d_w,
+                      margin, seed, d_step, (uint32_t)shard_base, d_out, (hipStream_t)stream,
+                      loss, nullptr, SwrMap{(uint64_t)swr_mod, swr_base, n_X, n_Z});
 }
 
 extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,

@@ -17,6 +17,33 @@ __device__ __forceinline__ u32x4 sgd_draw(uint64_t seed, uint64_t step, uint32_t
                        (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// Device-RNG SWR rows drawn IN the gradient kernel (round 3): with reshuffles every `mod` steps
+// from counter `base`, the row of draw position a in shard s at step counter c is the one
+// k_swr_rows drew at the last reshuffle, counter c - (c - base) % mod — one Philox block per
+// side instead of a table read, and no table-drawing launch per reshuffle.  mod == 0: tables.
+struct SwrMap {
+  uint64_t mod, base;
+  int64_t n_x, n_z;
+};
+
+// rows of pair (ax, az) of local shard s (global shard_base + s) at step counter `step`
+__device__ __forceinline__ void swr_rows_of(const SwrMap& m, const int64_t* __restrict__ rows_x,
+                                            int64_t kx, const int64_t* __restrict__ rows_z,
+                                            int64_t kz, int s, uint32_t shard_base, int64_t ax,
+                                            int64_t az, uint64_t seed, uint64_t step,
+                                            int64_t& rx, int64_t& rz) {
+  if (m.mod) {
+    const uint64_t rc = step - (step - m.base) % m.mod;
+    const u32x4 qx = sgd_draw(seed, rc, (uint32_t)ax, shard_base + (uint32_t)s, kTagRowsX);
+    const u32x4 qz = sgd_draw(seed, rc, (uint32_t)az, shard_base + (uint32_t)s, kTagRowsZ);
+    rx = (int64_t)mulhi_u64(((uint64_t)qx.b << 32) | qx.a, (uint64_t)m.n_x);
+    rz = (int64_t)mulhi_u64(((uint64_t)qz.b << 32) | qz.a, (uint64_t)m.n_z);
+  } else {
+    rx = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
+    rz = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+  }
+}
+
 // Wide rows (32 < d <= 512): a wave holds one pair's two rows, 8 columns per lane.
 constexpr int kWideCols = 8;                     // columns per lane
 constexpr int kWideMaxD = kWideCols * kWave;     // 512

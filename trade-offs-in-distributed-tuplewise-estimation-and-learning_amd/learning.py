@@ -505,11 +505,16 @@ class SGDEngine:
             self.rows_z = t.empty((self.N_loc, self.kz), dtype=t.int64, device=self.w.device)
         self._graphs = {}
 
-    def swr_segments_ok(self) -> bool:
-        """run_segment(swr_mod=) applies: device RNG, one process, replicated rows, the
-        persistent narrow segment, the incomplete gradient."""
-        return (getattr(self, "seed", None) is not None and self.G == 1 and self.narrow_seg
-                and self.layout == "replicated" and not self.complete)
+    def swr_segments_ok(self, nsteps: int = 2) -> bool:
+        """run_segment(nsteps, swr_mod=) applies: device RNG, one process, replicated rows,
+        the incomplete gradient, and a kernel that draws the rows — the persistent narrow
+        segment (nsteps > 1) or the per-step gradient launches of wide rows."""
+        if (getattr(self, "seed", None) is None or self.G != 1 or self.layout != "replicated"
+                or self.complete):
+            return False
+        if self.narrow_seg:
+            return nsteps > 1
+        return not self.fused and not self.segment
 
     def reshuffle_device(self, counter=None):
         """New SWR row tables from the device RNG at the current step counter, or at `counter`
@@ -538,9 +543,16 @@ class SGDEngine:
         L.call("tw_swr_rows_rng", L.ptr(self.rows_z), self.N_loc, self.kz, self.n_Z, self.seed,
                L.ptr(self.step_ctr), 1, self.shard_base, s)
 
-    def step_device(self):
+    def step_device(self, swr_mod: int = 0):
         if self.complete:
             return self.step_complete()
+        if swr_mod:  # the rows of the step's last reshuffle, drawn in the kernel
+            L.call("tw_pair_grad_rng_swr", L.ptr(self.X), L.ptr(self.Z), self.d, self.n_X,
+                   self.n_Z, self.kx, self.kz, self.N_loc, self.B, L.ptr(self.w), self.margin,
+                   self.loss, self.seed, L.ptr(self.step_ctr), self.shard_base, int(swr_mod), 0,
+                   L.ptr(self.grads_loc), L.stream_handle())
+            self._update()
+            return
         L.call("tw_pair_grad_rng", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
                self.kx, L.ptr(self.rows_z), self.kz, self.N_loc, self.B, L.ptr(self.w),
                self.margin, self.loss, self.seed, L.ptr(self.step_ctr), self.shard_base,
@@ -551,23 +563,27 @@ class SGDEngine:
                     swr_mod: int = 0):
         """nsteps device-RNG steps (reshuffling first if asked), replayed from a captured
         hipGraph per distinct segment shape (eager when the step holds a collective).
-        swr_mod: the persistent narrow segment draws the SWR rows of every reshuffle (one every
-        swr_mod steps from step counter 0) itself (tw_sgd_segment_narrow_swr) — the device
-        row tables are then NOT updated (swr_segments_ok says when this applies)."""
+        swr_mod: the kernels draw the SWR rows of every reshuffle (one every swr_mod steps from
+        step counter 0) themselves (tw_sgd_segment_narrow_swr, tw_pair_grad_rng_swr) — the
+        device row tables are then NOT updated (swr_segments_ok says when this applies)."""
+        t = self.t
         if swr_mod:
-            assert self.swr_segments_ok() and nsteps > 1 and not reshuffle_first
+            assert self.swr_segments_ok(nsteps) and not reshuffle_first
             if self.fused and self._slot1 is None:
-                t = self.t
                 self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw),
                                t.empty_like(self.grads))
-            self._fused_steps(nsteps, swr_mod=swr_mod)
-            return
+            if self.narrow_seg and nsteps > 1:  # one persistent launch, eager (§4.4e)
+                self._fused_steps(nsteps, swr_mod=swr_mod)
+                return
         if reshuffle_first and self.layout == "partitioned":
             self.reshuffle_device()  # the exchange sizes its buffers on the host: not captured
             reshuffle_first = False
 
         def steps(n):
-            if self.segment:
+            if swr_mod:
+                for _ in range(n):
+                    self.step_device(swr_mod=swr_mod)
+            elif self.segment:
                 self._segment(n)
             elif self.fused:
                 self._fused_steps(n)
@@ -580,12 +596,11 @@ class SGDEngine:
                 self.reshuffle_device()
             steps(nsteps)
             return
-        t = self.t
         if self.fused and self._slot1 is None:  # allocated outside any capture
             self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw), t.empty_like(self.grads))
         while nsteps > 0:
             n = min(nsteps, 256)
-            key = (n, reshuffle_first)
+            key = (n, reshuffle_first, swr_mod)
             g = self._graphs.get(key)
             if g is None:
                 g = t.cuda.CUDAGraph()
@@ -1367,7 +1382,7 @@ def _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss="hinge"):
                 evaluation_step(i, None, None, None if defer is not None else eng.w_host(),
                                 p_learn, loss=loss, _w_dev=eng.w, _graph=graphs, _defer=defer)
             nxt = min(n_it, (i // eval_mod + 1) * eval_mod)
-            if nxt - i > 1:
+            if eng.swr_segments_ok(nxt - i):
                 eng.run_segment(nxt - i, False, graphs, swr_mod=mod)
                 stale = True
             else:  # one step: the row tables, drawn at this step's last reshuffle
