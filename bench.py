@@ -1135,7 +1135,12 @@ def main():
                    "parallelism": (f"dp{world}: shards over ranks, "
                                    + ("RCCL" if os.environ.get("TW_BENCH_BACKEND", "nccl")
                                       == "nccl" else "gloo (rehearsal)")
-                                   + " all-to-all repartition + all-reduce of counts"
+                                   + (" all-gather of the sample once per call, every rank "
+                                      "applies each global repartition to all records (no "
+                                      "per-step collective)" if S._rank_path_ok()
+                                      and S._replicated_ok() else
+                                      " all-to-all repartition")
+                                   + " + all-reduce of counts"
                                    if world > 1 else
                                    "dp1: one GPU, device Feistel repartition fused into the "
                                    "count launch")},

@@ -133,6 +133,10 @@ int tw_gather_records(const void* d_in, const uint64_t* d_rec, int64_t n, void* 
 /* Tuning hook for tw_count_pairs_rank_step: x-images per lane R (8 or 16; 0 = automatic) and
  * z-chunk length (0 = automatic).  Process-global; results do not depend on it. */
 int tw_count_rank_set_plan(int32_t R, int64_t z_chunk);
+/* Tuning hook for tw_count_pairs_rank_step's fused next repartition: its spare blocks are the
+ * last blocks of the grid (front = 0, the default) or the first (front = 1).  Process-global;
+ * results do not depend on it. */
+int tw_count_rank_set_next(int32_t front);
 
 /* ---- f4: the same counts in O((n+m) log m): sort each z-chunk (<= 16384 keys) in LDS as
  * order-preserving u64 keys, then binary-search every x (csrc/rankcount.hip).  Bit-identical

@@ -140,7 +140,35 @@ class OracleOpsFixed(OracleOps):
         return out
 
 
-_OPS = {"plain": OracleOps, "fused": OracleOpsFused, "fixed": OracleOpsFixed}
+class OracleOpsRank(OracleOpsFixed):
+    """Adds the rank-image step chain (tw_rank_images / tw_count_pairs_rank_step /
+    tw_gather_records) restated, so UnN_many takes the replicated rank path on host tensors."""
+
+    def rank_images(self, X, Z, dtype):
+        xr, zr = O.rank_records(X.numpy(), Z.numpy())
+        return torch.from_numpy(xr), torch.from_numpy(zr)
+
+    def count_rank_step(self, xr, x_off_dev, zr, z_off_dev, n_shards, max_nx, max_nz, out,
+                        x_next, key_x, z_next, key_z, out_next):
+        img = lambda r: (r.numpy() & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
+        gx, nz = img(xr), img(zr)  # z images stored negated: x > z <=> gx + nz >= 1
+        xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
+        for s in range(n_shards):
+            a, b = gx[xo[s]:xo[s + 1]], nz[zo[s]:zo[s + 1]]
+            out[s] += int((a[:, None] + b[None, :] >= 1).sum())
+        if x_next is not None:
+            x_next.copy_(torch.from_numpy(O.permute_scatter(xr.numpy(), key_x)))
+            z_next.copy_(torch.from_numpy(O.permute_scatter(zr.numpy(), key_z)))
+        if out_next is not None:
+            out_next.zero_()
+        return out
+
+    def gather_records(self, vals, rec):
+        return vals[rec >> 32]
+
+
+_OPS = {"plain": OracleOps, "fused": OracleOpsFused, "fixed": OracleOpsFixed,
+        "rank": OracleOpsRank}
 
 
 def _free_port():
@@ -207,6 +235,60 @@ def test_multirank_repartition_is_G_invariant(G, fused):
     want = [float(S1.UnN(k)) for k in keys]
     assert vals == want
     assert inc == float(S1.UnNB(B, seed=77))
+
+
+def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(G, n_loc, m_loc)
+    S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
+                      torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
+                      group=dist.group.WORLD, ops=OracleOpsRank())
+    assert S.algo == "pairs" and S._rank_path_ok()
+    vals = [float(v) for v in S.UnN_many(keys)]
+    Xg = [torch.empty_like(S.X) for _ in range(G)]
+    Zg = [torch.empty_like(S.Z) for _ in range(G)]
+    dist.all_gather(Xg, S.X)
+    dist.all_gather(Zg, S.Z)
+    if rank == 0:
+        q.put((vals, torch.cat(Xg).numpy(), torch.cat(Zg).numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_replicated_rank_steps_are_G_invariant(G):
+    """UnN_many's collective-free multi-rank chain (device.REPLICATED_RANK_STEPS): every rank
+    ranks the all-gathered sample, repartitions the whole record arrays with the global keys and
+    counts only its own shards; one all-reduce of the counts per call.  The estimates equal the
+    one-process score path's (est.UnNT's loop) and the ranks' final arrays, concatenated, equal
+    the global permutation chain."""
+    import tuplewise  # noqa: F401
+    from tuplewise import device as D
+    assert D.REPLICATED_RANK_STEPS
+    from tuplewise.device import ShardedSample
+    n_loc, m_loc, N, keys = 600, 450, 3, [5, 6, 9]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, G, port, n_loc, m_loc, N, keys, q))
+             for r in range(G)]
+    for p in procs:
+        p.start()
+    vals, Xg, Zg = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X, Z = _global_data(G, n_loc, m_loc)
+    S1 = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
+                       ops=OracleOps())
+    assert vals == [float(S1.UnN(k)) for k in keys]  # the score path, key by key
+    assert np.array_equal(Xg, S1.X.numpy()) and np.array_equal(Zg, S1.Z.numpy())
+    S1r = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
+                        ops=OracleOpsRank())  # the one-process rank chain
+    assert [float(v) for v in S1r.UnN_many(keys)] == vals
+    assert np.array_equal(S1r.X.numpy(), Xg)
 
 
 def _overflow_worker(rank, G, port, q):

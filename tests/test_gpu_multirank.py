@@ -71,30 +71,37 @@ def test_learning_two_ranks_equals_one(gpu, mode, layout):
     assert np.array_equal(got, np.stack(ref))
 
 
-def _est_worker(rank, port, G, q, exchange="fixed"):
+def _est_worker(rank, port, G, q, exchange="fixed", replicated=True):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     torch.cuda.set_device(0)
+    from tuplewise import device as D
     from tuplewise.device import ShardedSample
+    D.REPLICATED_RANK_STEPS = replicated  # False: the per-step all-to-all of records
     rng = np.random.RandomState(3)
     n_loc, N = 40_000, 8
     X = rng.normal(0.3, 1, G * n_loc)
     Z = rng.normal(0, 1, G * n_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(),
                       torch.from_numpy(Z[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(), N,
-                      group=dist.group.WORLD, exchange=exchange)
+                      group=dist.group.WORLD, exchange=exchange, algo="pairs")
     vals = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
-    vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # the side-stream pipeline
+    vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # rank images: the replicated chain
+    Xg = [torch.empty(S.X.shape, dtype=S.X.dtype) for _ in range(G)]
+    Zg = [torch.empty(S.Z.shape, dtype=S.Z.dtype) for _ in range(G)]
+    dist.all_gather(Xg, S.X.cpu())
+    dist.all_gather(Zg, S.Z.cpu())
     if rank == 0:
-        q.put(vals)
+        q.put((vals, torch.cat(Xg).numpy(), torch.cat(Zg).numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["fixed", "exact"])
-def test_sharded_sample_two_ranks_equals_one(gpu, exchange):
+@pytest.mark.parametrize("exchange,replicated", [("fixed", True), ("fixed", False),
+                                                  ("exact", False)])
+def test_sharded_sample_two_ranks_equals_one(gpu, exchange, replicated):
     import torch
     import torch.multiprocessing as mp
     from tuplewise.device import ShardedSample
@@ -102,17 +109,21 @@ def test_sharded_sample_two_ranks_equals_one(gpu, exchange):
     rng = np.random.RandomState(3)
     X = rng.normal(0.3, 1, G * n_loc)
     Z = rng.normal(0, 1, G * n_loc)
-    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), G * N)
+    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), G * N,
+                      algo="pairs")
     want = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
     want += [float(v) for v in S.UnN_many([5, 6, 7])]
+    assert S._rank_path_ok() and S.algo == "pairs"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q, exchange)) for r in range(G)]
+    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q, exchange, replicated))
+             for r in range(G)]
     for pr in procs:
         pr.start()
-    got = q.get(timeout=300)
+    got, Xg, Zg = q.get(timeout=300)
     for pr in procs:
         pr.join(timeout=120)
         assert pr.exitcode == 0
     assert got == want
+    assert np.array_equal(Xg, S.X.cpu().numpy()) and np.array_equal(Zg, S.Z.cpu().numpy())

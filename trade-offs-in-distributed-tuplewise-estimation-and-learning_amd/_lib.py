@@ -40,6 +40,7 @@ _SIGNATURES = {
                                  _i64, _vp, _u64, _vp, _i32, _vp],
     "tw_gather_records": [_vp, _vp, _i64, _vp, _vp],
     "tw_count_rank_set_plan": [_i32, _i64],
+    "tw_count_rank_set_next": [_i32],
     "tw_count_pairs_sorted_work_bytes": [_i32, _i64],
     "tw_count_sorted_set_chunk": [_i64],
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],

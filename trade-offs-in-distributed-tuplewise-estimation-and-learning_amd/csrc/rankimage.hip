@@ -525,12 +525,17 @@ __global__ __launch_bounds__(kBlock) void k_count_rank(
     const uint64_t* __restrict__ zr, const int64_t* __restrict__ z_off, int n_shards,
     int tiles_x, int zchunks, int64_t z_chunk, unsigned long long* __restrict__ out,
     NextStep nxt) {
-  if (nxt.blocks && (int)blockIdx.x >= (int)gridDim.x - nxt.blocks) {
-    next_step_part<kBlock>(nxt, (int)blockIdx.x - ((int)gridDim.x - nxt.blocks));
+  // spare blocks: the last nxt.blocks of the grid (tail = 1) or the first (tail = 0: dispatched
+  // beside the count blocks from the start, for count grids of a few waves per SIMD)
+  const int nb = nxt.blocks;
+  const int sb = nxt.tail ? (int)blockIdx.x - ((int)gridDim.x - nb) : (int)blockIdx.x;
+  if (nb && sb >= 0 && sb < nb) {
+    next_step_part<kBlock>(nxt, sb);
     return;
   }
   const int per_shard = tiles_x * zchunks;
-  const int lb = xcd_block(blockIdx.x, gridDim.x - nxt.blocks);  // whole shards per XCD
+  // whole shards per XCD (nb is a multiple of kXcds, so front spares keep the XCD order)
+  const int lb = xcd_block(nxt.tail ? blockIdx.x : blockIdx.x - nb, gridDim.x - nb);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x & (kWave - 1);
   const int item = lb * (kBlock / kWave) + wid;
@@ -588,11 +593,12 @@ struct RankPlan {
   int64_t z_chunk, blocks;
 };
 static int g_rank_R = 0;          // tuning hooks (tw_count_rank_set_plan); 0 = automatic
+static int g_rank_next_front = 0;  // tw_count_rank_set_next: spare blocks first (1) or last (0)
 static int64_t g_rank_zchunk = 0;
 
 // R in {16, 8}: least padded x-slots (ties to 16: half the z loads per compare); z chunks of
 // ~1024 records (tools/mb_pk.hip: 528 is too short for R = 8, >= 2048 leaves the tail ragged).
-static RankPlan plan_rank(int64_t max_nx, int64_t max_nz, int32_t n_shards) {
+static RankPlan plan_rank(int64_t max_nx, int64_t max_nz, int32_t n_shards, bool fused) {
   RankPlan p{16, 1, 1, max_nz, 0};
   int64_t best = -1;
   for (int R : {16, 8}) {
@@ -605,9 +611,15 @@ static RankPlan plan_rank(int64_t max_nx, int64_t max_nz, int32_t n_shards) {
   }
   p.tiles_x = (int)ceil_div(max_nx, (int64_t)kWave * p.R);
   int64_t zc = g_rank_zchunk > 0 ? g_rank_zchunk : 1024;
-  // enough work items to fill the chip when shards are few / short
-  const int64_t target = 256 * 16 * (kBlock / kWave);
+  // enough work items to fill the chip when shards are few / short: 16 per SIMD; but a count
+  // with a fused next repartition and under 4 items per SIMD at 1024-long chunks (8 shards of
+  // 15625 + 15625, the strong-scaling shape at G = 8) aims at 4, so the whole count grid is
+  // resident at once and the spare blocks behind it start at once (tools/replicated_probe.py:
+  // 80.4 -> 72.5 us per step there)
   const int64_t base = (int64_t)p.tiles_x * n_shards;
+  const int64_t few = 256 * 4 * (kBlock / kWave);
+  const int64_t target =
+      fused && base * ceil_div(max_nz, (int64_t)1024) < few ? few : 256 * 16 * (kBlock / kWave);
   if (g_rank_zchunk <= 0 && base * ceil_div(max_nz, zc) < target)
     zc = std::max<int64_t>(256, ceil_div(max_nz, std::max<int64_t>(1, target / base)));
   zc = std::min<int64_t>(zc, (int64_t)1 << 24);  // f32 lane counters stay exact
@@ -685,6 +697,12 @@ extern "C" int tw_rank_images(const void* d_x, int64_t n_x, const void* d_z, int
                                   d_x_rec, d_z_rec, st);
 }
 
+extern "C" int tw_count_rank_set_next(int32_t front) {
+  TW_ARG_CHECK(front == 0 || front == 1, "tw_count_rank_set_next: front in {0, 1}");
+  g_rank_next_front = front;
+  return TW_OK;
+}
+
 extern "C" int tw_count_rank_set_plan(int32_t R, int64_t z_chunk) {
   TW_ARG_CHECK(R == 0 || R == 8 || R == 16, "tw_count_rank_set_plan: R in {0, 8, 16}");
   TW_ARG_CHECK(z_chunk >= 0 && z_chunk <= (1ll << 24), "tw_count_rank_set_plan: bad z_chunk");
@@ -714,7 +732,7 @@ extern "C" int tw_count_pairs_rank_step(const uint64_t* d_x_rec, const int64_t* 
                    (unsigned long long*)d_out_next, d_out_next ? (int64_t)n_next_shards : 0,
                    make_feistel(std::max<int64_t>(n_x, 1), key_x),
                    make_feistel(std::max<int64_t>(n_z, 1), key_z), next_rank_blocks(n_x + n_z),
-                   0, 1};
+                   0, g_rank_next_front ? 0 : 1};
   } else if (d_out_next != nullptr && n_next_shards > 0) {
     TW_HIP_CHECK(tw_zero_async(d_out_next, 0, sizeof(uint64_t) * n_next_shards, st));
   }
@@ -726,7 +744,7 @@ extern "C" int tw_count_pairs_rank_step(const uint64_t* d_x_rec, const int64_t* 
     TW_LAUNCH_CHECK();
     return TW_OK;
   }
-  const RankPlan p = plan_rank(max_nx, max_nz, n_shards);
+  const RankPlan p = plan_rank(max_nx, max_nz, n_shards, nxt.blocks > 0);
   TW_ARG_CHECK((p.blocks + nxt.blocks) * (kBlock / kWave) < (1ll << 31),
                "tw_count_pairs_rank_step: grid too large");
   dim3 g((unsigned)(p.blocks + nxt.blocks)), b(kBlock);

@@ -13,6 +13,9 @@ every element is sent to the rank owning its new position with a single all-to-a
 {value, position} records, and the receiver scatters them into place.  The resulting global
 array — hence every shard's integer count and the final np.mean — is identical for any G.
 Per-shard counts are combined with one all-reduce (sum of a zero-padded int64 vector; exact).
+UnN_many on rank images (est.UnNT's loop, the bench's strong-scaling problem) needs no
+exchange at all while the whole sample is small: every rank all-gathers it once per call,
+keeps all the records and applies each global permutation itself, counting only its shards.
 """
 from __future__ import annotations
 
@@ -24,6 +27,14 @@ from . import _lib as L
 # UnN_many's all-pairs steps on rank images (csrc/rankimage.hip; A/B switch: False keeps the
 # double-compare kernel of csrc/count.hip)
 RANK_IMAGES = True
+# UnN_many on rank images over several ranks: every rank keeps the WHOLE sample's records (16 MB
+# at 1e6 + 1e6) and applies each global repartition itself, counting only its own shards — no
+# collective per step (False: the fixed-capacity all-to-all of _repartition_multi per step).
+# Taken up to REPLICATED_MAX_RECORDS records in all: every rank permutes all of them each step
+# (~25 us per 2e6 on one MI355X, mostly hidden beside the count; tools/replicated_probe.py), so
+# the weak-scaling form (1e6/class PER rank: 2e6*G records) keeps the exchange from G = 4 on.
+REPLICATED_RANK_STEPS = True
+REPLICATED_MAX_RECORDS = 1 << 22
 
 
 def prop_swor_layout(n_X: int, n_Z: int, N: int):
@@ -382,6 +393,8 @@ class ShardedSample:
     def _multi(self) -> bool:
         """The exchange path (always with G > 1; at G = 1 only when _force_multi is set, a
         probe hook for timing the multi-rank orchestration on one GPU)."""
+        if getattr(self, "_replicated", False):  # _unn_many_rank's replicated steps
+            return False
         return self.G > 1 or getattr(self, "_force_multi", False)
 
     def repartition(self, key: int, check: bool = True):
@@ -525,7 +538,10 @@ class ShardedSample:
         keys = list(keys)
         if not keys:
             return []
-        if not self.X.is_cuda:  # host tensors (CPU rehearsal of the orchestration)
+        if not self.X.is_cuda and not (self.algo == "pairs" and self._rank_path_ok()
+                                       and (self.G == 1 or self._replicated_ok())):
+            # host tensors (CPU rehearsal of the orchestration): the stream-pipelined paths
+            # need a device; the rank-image chain (no side stream) runs as it is
             return [self.UnN(k) for k in keys]
         if (self.algo == "sorted" and not self._multi() and self.N > 0
                 and hasattr(self.ops, "count_sorted_steps")):
@@ -578,12 +594,15 @@ class ShardedSample:
         order once at the end.  Same counts, same arrays as the score path."""
         if self.G > 1:
             # several ranks: every rank ranks the WHOLE sample (one all-gather of both samples
-            # per call), keeps its own elements' records — whose high words are then global
-            # indices — and the exchanges move 8-B records as they moved scores
+            # per call); its records' high words are then global indices
             X0, Z0 = self._all_gather(self.X), self._all_gather(self.Z)
             r = self.ops.rank_images(X0, Z0, self.dtype)
             if r is None:
                 return None
+            if self._replicated_ok():
+                return self._unn_many_replicated(keys, X0, Z0, r)
+            # ... keeps its own elements' records and the exchanges move 8-B records as they
+            # moved scores
             a, b = self.rank * self.n_loc, self.rank * self.m_loc
             self.X, self.Z = r[0][a:a + self.n_loc].clone(), r[1][b:b + self.m_loc].clone()
         else:
@@ -604,6 +623,39 @@ class ShardedSample:
             counts = self._run_steps(keys, None, True, step, count_into)
         finally:
             xr, zr = self.X, self.Z
+            self.X = self.ops.gather_records(X0, xr)
+            self.Z = self.ops.gather_records(Z0, zr)
+        return [np.mean(v) for v in self.values(counts)]
+
+    def _replicated_ok(self) -> bool:
+        return (REPLICATED_RANK_STEPS
+                and self.G * (self.n_loc + self.m_loc) <= REPLICATED_MAX_RECORDS)
+
+    def _unn_many_replicated(self, keys, X0, Z0, rec):
+        """UnN_many on rank images over G ranks with NO collective per step: every rank holds
+        the whole sample's records (rec, from the all-gathered X0 / Z0) and runs the one-GPU
+        step chain on them — each launch counts this rank's N shards of the global layout
+        (global positions r*n_loc + x_off, r*m_loc + z_off) and applies the next GLOBAL keyed
+        repartition to all records, the same permutation chain every rank evaluates and the
+        exchange path distributes.  The counts meet in _run_steps' one all-reduce per call;
+        the rank's final arrays are its slices of the permuted global arrays, gathered back
+        into scores.  Same counts and arrays as the exchange path (and as one GPU)."""
+        r, n, m = self.rank, self.n_loc, self.m_loc
+        offs = (self.x_off_dev, self.z_off_dev)
+        self.x_off_dev = self.ops.to_dev(self.x_off + r * n)
+        self.z_off_dev = self.ops.to_dev(self.z_off + r * m)
+        self.X, self.Z = rec
+
+        def step(i, out, Xn, kx, Zn, kz, out_n):
+            self.ops.count_rank_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
+                                     self.max_nx, self.max_nz, out, Xn, kx, Zn, kz, out_n)
+        self._replicated = True  # _multi() is False: the one-GPU chain of _run_steps
+        try:
+            counts = self._run_steps(keys, None, True, step)
+        finally:
+            self._replicated = False
+            self.x_off_dev, self.z_off_dev = offs
+            xr, zr = self.X[r * n:(r + 1) * n], self.Z[r * m:(r + 1) * m]
             self.X = self.ops.gather_records(X0, xr)
             self.Z = self.ops.gather_records(Z0, zr)
         return [np.mean(v) for v in self.values(counts)]
