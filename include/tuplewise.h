@@ -695,6 +695,11 @@ int tw_draw_pipe_shipped(void* handle, int32_t j, void* stream);
 int tw_draw_pipe_stop(void* handle);
 /* n 8-byte words d_in -> d_out on `stream` (d_in may be mapped host memory, as above). */
 int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
+/* learning_process's deferred evaluations (make_exps.py:143-190): one evaluation's nres
+ * statistics, the nw words of w and (d_ctl not null) the SGD engine's abort word, written in one
+ * launch into h_out, pinned host memory of nres + nw + 1 8-byte words. */
+int tw_stage_eval(const void* d_res, int32_t nres, const void* d_w, int32_t nw,
+                  const uint32_t* d_ctl, void* h_out, void* stream);
 /* The device address of pinned, mapped host memory (hipHostGetDevicePointer); TW_ERR_ARG when
  * `host` is not such memory. */
 int tw_host_device_pointer(void* host, void** out_dev);

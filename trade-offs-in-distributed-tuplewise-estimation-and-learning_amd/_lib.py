@@ -153,6 +153,7 @@ _SIGNATURES = {
     "tw_draw_pipe_shipped": [_vp, _i32, _vp],
     "tw_draw_pipe_stop": [_vp],
     "tw_copy_words": [_vp, _i64, _vp, _vp],
+    "tw_stage_eval": [_vp, _i32, _vp, _i32, _vp, _vp, _vp],
     "tw_host_device_pointer": [_vp, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],

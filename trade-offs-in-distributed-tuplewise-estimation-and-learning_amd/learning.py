@@ -1426,12 +1426,21 @@ class _DeferredEvals:
     (and all of them before learning_process returns).  The loop no longer waits for the device
     at every evaluation; the values are the same bits."""
 
-    def __init__(self, w_dev, w_shape, slots=64, check=None):
+    def __init__(self, w_dev, w_shape, slots=64, check=None, ctl=None):
         t = L.torch()
         self.t = t
         self.w_shape = w_shape
-        self.check = check  # the engine's abort-word check, run before any history is written
-        self.host = t.empty((slots, 4 + int(w_dev.numel())), dtype=t.float64, pin_memory=True)
+        # the engine's abort word (ctl, a 1-element device tensor), copied beside each
+        # evaluation's results and checked before its history is written; without it, the
+        # engine's blocking check() runs instead
+        self.check = check
+        self.ctl = ctl
+        # slot k: [4 statistics | w | abort word], written by ONE tw_stage_eval launch
+        self.nw = int(w_dev.numel())
+        self.host = t.zeros((slots, 4 + self.nw + 1), dtype=t.float64, pin_memory=True)
+        self.host_dev = L.host_device_pointer(self.host)  # the kernel's address of slot 0
+        if self.host_dev is None:
+            raise RuntimeError("deferred evaluations: pinned host slots are not device-mapped")
         self.events = [t.cuda.Event() for _ in range(slots)]
         self.free = list(range(slots))[::-1]
         self.pending = []
@@ -1440,8 +1449,12 @@ class _DeferredEvals:
         if not self.free:
             self._pop()
         k = self.free.pop()
-        self.host[k, :4].copy_(res_dev.reshape(-1), non_blocking=True)
-        self.host[k, 4:].copy_(w_dev.reshape(-1), non_blocking=True)
+        res = res_dev.reshape(-1)
+        assert res.dtype == self.t.float64 and res.numel() == 4 and res.is_contiguous()
+        assert w_dev.dtype == self.t.float64 and w_dev.numel() == self.nw and w_dev.is_contiguous()
+        L.call("tw_stage_eval", L.ptr(res), 4, L.ptr(w_dev), self.nw,
+               L.ptr(self.ctl),
+               ctypes.c_void_p(self.host_dev + k * 8 * (4 + self.nw + 1)), L.stream_handle())
         self.events[k].record()
         self.pending.append((i, k, finish))
         while len(self.pending) > 1 and self.events[self.pending[0][1]].query():
@@ -1450,12 +1463,17 @@ class _DeferredEvals:
     def _pop(self):
         i, k, finish = self.pending.pop(0)
         self.events[k].synchronize()
-        if self.check is not None:
-            # a persistent segment that gave up at its grid barrier left w invalid: raise
-            # before its statistics reach p_learn or the log
+        # a persistent segment that gave up at its grid barrier left w invalid: raise before
+        # its statistics reach p_learn or the log (the word is sticky, so the copy taken with
+        # this evaluation covers every segment before it, without a device-wide wait here)
+        if self.ctl is not None:
+            if int(self.host[k, 4 + self.nw:].numpy().view(np.int64)[0]) != 0:
+                raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
+                                   "co-resident); the SGD state is invalid")
+        elif self.check is not None:
             self.check()
         h = self.host[k].numpy()
-        finish(i, h[:4].copy(), h[4:].copy().reshape(self.w_shape))
+        finish(i, h[:4].copy(), h[4:4 + self.nw].copy().reshape(self.w_shape))
         self.free.append(k)
 
     def drain(self):
@@ -1469,7 +1487,9 @@ def _deferred_evals(eng, graphs, trajectory):
     if (not DEFER_EVALS or not graphs or trajectory is not None
             or TYPE_TRAIN_MONITOR != "FIXED_PAIRS" or getattr(eng, "G", 1) != 1):
         return None
-    return _DeferredEvals(eng.w, eng.w_shape, check=eng.check)
+    ctl = getattr(eng, "_ctl", None)
+    return _DeferredEvals(eng.w, eng.w_shape, check=eng.check,
+                          ctl=ctl[1:2] if ctl is not None else None)
 
 
 class _EvalCache:
@@ -1707,13 +1727,33 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
                          (("train_X", "train_Z", "pairs") if fixed else ()))
             ent = (key, srcs, g, out, held, wbuf)
             _CACHE.dev["eval_graph"] = ent
+        res_dev, n_pairs, n_test = ent[3]
+        if deferred:
+            # the evaluation runs on a side stream BESIDE the next segment of steps: w is
+            # snapshotted into the graph's buffer on the loop's stream (after the previous
+            # evaluation has read it), the graph and the staging of its results follow on the
+            # side stream; the persistent segment holds N CUs, the evaluation's blocks take the
+            # others.  The statistics and the snapshot leave the device as before (same bits).
+            main = t.cuda.current_stream()
+            side = _CACHE.dev.get("eval_side")
+            if side is None:
+                side = _CACHE.dev["eval_side"] = t.cuda.Stream()
+            main.wait_stream(side)
+            wbuf = ent[5]
+            if (_w_dev.dtype == t.float64 and _w_dev.is_contiguous()
+                    and wbuf.is_contiguous()):
+                L.call("tw_copy_words", L.ptr(_w_dev), int(_w_dev.numel()), L.ptr(wbuf),
+                       L.stream_handle())
+            else:
+                wbuf.copy_(_w_dev)
+            side.wait_stream(main)
+            with t.cuda.stream(side):
+                ent[2].replay()
+                _defer.push(i, res_dev, wbuf, lambda it, res, wh: _eval_host(
+                    it, res, wh, n_pairs, n_test, p_learn, fixed, None, None))
+            return
         ent[5].copy_(_w_dev)
         ent[2].replay()
-        res_dev, n_pairs, n_test = ent[3]
-        if deferred:  # the statistics and w leave the device with the loop running on
-            _defer.push(i, res_dev, _w_dev, lambda it, res, wh: _eval_host(
-                it, res, wh, n_pairs, n_test, p_learn, fixed, None, None))
-            return
     else:
         wd = _w_dev if _w_dev is not None else L.to_device(np.asarray(w, np.float64).reshape(-1))
         res_dev, n_pairs, n_test = _eval_device(wd, p_learn, loss, margin, fixed)
