@@ -112,6 +112,17 @@ class Span:
         return dt, out
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """One line per bench section on stderr (rank 0), so a long multi-GPU run shows it is alive;
+    stdout carries only the JSON line."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.perf_counter() - _T_START:7.1f} s] {msg}", file=sys.stderr,
+              flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -842,6 +853,7 @@ def tradeoff_curve(args, group, span, with_cpu):
            "reshuffle_mod": list(RESHUFFLE_MODS)}
     c4d, c4r, cpu = {}, {}, {}
     for mod in RESHUFFLE_MODS:
+        progress(f"trade-off curve C4, reshuffle_mod {mod}")
         c4d[mod] = sgd_steps_per_s(9117, 702, 10, 100, 100, mod, 2000, 1, group=group,
                                    span=span)["steps_per_s"]
         c4r[mod] = sgd_replay_steps_per_s(1000, mod, group=group, span=span, runs=1,
@@ -856,6 +868,7 @@ def tradeoff_curve(args, group, span, with_cpu):
     data = sgd_data(C5_N, C5_N, 512)
     c5r, c5p = {}, {}
     for mod in RESHUFFLE_MODS:
+        progress(f"trade-off curve C5, reshuffle_mod {mod}")
         c5r[mod] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, mod, 200, 1, group=group,
                                    span=span, data=data)["steps_per_s"]
         # a partitioned reshuffle moves ~n rows (41 GB at G = 1): few steps at mod 1
@@ -957,6 +970,7 @@ def main():
 
     span = Span(torch, dist, group, barrier)
 
+    progress(f"headline: {args.steps} UnN steps on {world} rank(s)")
     # settle: untimed steps for >= settle_ms so the timed steps run at the steady-state clock
     # (the chip raises its clock over the first ~10 ms of load; measured 3 % on this step)
     # one untimed run at the timed run's length first: the first K-step UnN_many of a process
@@ -1067,7 +1081,9 @@ def main():
     ops.count_rng = ops.count_rng.__wrapped__
     ops.count_rng_step = ops.count_rng_step.__wrapped__
     inc_pairs_rank = shards * B_inc
+    progress("incomplete replay")
     inc_replay = incomplete_replay(X, Z, shards, B_inc)
+    progress("strong C3")
     strong = None if args.no_strong else strong_c3(args, group, rank, world, barrier, torch, dist)
 
     # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
@@ -1103,6 +1119,7 @@ def main():
     # BASELINE.json configs[0] (C1, plumbing): estimation-experiment/main.py's UnNT on host
     # arrays through the drop-in API (host shuffles as the reference, one device launch for
     # the T repetitions), n = 1000/class, N = 10, T = 4; the reference restated on the CPU
+    progress("plumbing C1")
     c1 = plumbing_C1(rank == 0 and world == 1 and not args.no_cpu_baseline)
 
     count_kernel = "k_count_rank" if rank_path else "k_count_complete"
@@ -1219,6 +1236,7 @@ def main():
     }
     if world > 1:
         # the weak-scaling form of the headline (per-GPU work of the one-GPU run)
+        progress("weak C3")
         out["weak_C3"] = weak_c3(args, group, rank, world, span, torch)
     if not args.no_sgd:
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5';
@@ -1226,19 +1244,22 @@ def main():
         # gradients per step; SGDEngine(group=)), C4/C5 checked against a one-rank run
         chk = 20 if world > 1 else 0
         g = group
-        sec = {
-            "metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)",
-            "C4_shuttle_shape": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2, group=g,
-                                                span=span, check_prefix=chk),
-            "C4_shuttle_shape_partitioned": sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 2000,
-                                                            2, layout="partitioned", group=g,
-                                                            span=span, check_prefix=chk),
-            "C4_shuttle_shape_replay": sgd_replay_steps_per_s(2000, group=g, span=span),
-            "C4_end_to_end_with_evaluation_replay": learning_end_to_end(2000, "replay", g, span),
-            "C4_end_to_end_with_evaluation_device": learning_end_to_end(2000, "device", g, span),
-        }
+        sec = {"metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)"}
+        progress("C4 device RNG")
+        sec["C4_shuttle_shape"] = sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2, group=g,
+                                                  span=span, check_prefix=chk)
+        progress("C4 partitioned")
+        sec["C4_shuttle_shape_partitioned"] = sgd_steps_per_s(
+            9117, 702, 10, 100, 100, 25, 2000, 2, layout="partitioned", group=g, span=span,
+            check_prefix=chk)
+        progress("C4 replay")
+        sec["C4_shuttle_shape_replay"] = sgd_replay_steps_per_s(2000, group=g, span=span)
+        progress("C4 end to end (replay, device)")
+        sec["C4_end_to_end_with_evaluation_replay"] = learning_end_to_end(2000, "replay", g, span)
+        sec["C4_end_to_end_with_evaluation_device"] = learning_end_to_end(2000, "device", g, span)
         c5 = None if args.no_c5 else sgd_data(C5_N, C5_N, 512)
         if c5 is not None:
+            progress("C5 B = 100, 4096, partitioned")
             sec["C5_scaled_d512"] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, 25, 500, 2,
                                                     group=g, span=span, data=c5,
                                                     check_prefix=chk)
@@ -1251,6 +1272,7 @@ def main():
             torch.cuda.empty_cache()
         if world == 1 and not args.no_c5:
             # one-GPU extensions (north_star item (2)): the complete-block gradient
+            progress("C5 complete-block gradients")
             sec["C5_scaled_d512_complete_gradient"] = sgd_complete_steps_per_s(
                 C5_N, C5_N, 512, 256, 3)
             sec["C5_scaled_d512_complete_gradient_logistic"] = sgd_complete_steps_per_s(
@@ -1260,6 +1282,7 @@ def main():
             out["tradeoff_reshuffle_mod"] = tradeoff_curve(
                 args, group, span, rank == 0 and world == 1 and not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baselines")
         out["cpu_baseline"] = cpu_baseline(n, shards, args.cpu_shards)
         # the box's CPU share is 16 cores per GPU (os.cpu_count() and the affinity mask show
         # the whole machine): the all-cores figure uses that share, and says so
@@ -1271,6 +1294,7 @@ def main():
         out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, shards, B_inc,
                                                                     args.cpu_inc_shards)
     if rank == 0 and world == 1:
+        progress("drop-in C3")
         d3 = drop_in_C3()
         if "cpu_baseline" in out:  # the reference restated: T x one est.UnN of this run
             unn_s = out["cpu_baseline"]["value"]

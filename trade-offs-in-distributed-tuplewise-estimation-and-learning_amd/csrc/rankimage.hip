@@ -110,13 +110,17 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ 
   __shared__ uint64_t sp[kRkMaxB];
   __shared__ uint32_t h[2 * kRkMaxB];
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads) h[b] = 0;
-  const int nsp = load_splitters(ss, g, sp);
-  const int64_t e0 = (int64_t)blockIdx.x * kRkTile;
-#pragma unroll 4
+  const int64_t e0 = (int64_t)blockIdx.x * kRkTile + threadIdx.x;
+  T zv[kRkPer];  // all of the thread's loads in flight at once (a block per 4096 z: few waves)
+#pragma unroll
   for (int k = 0; k < kRkPer; ++k) {
-    const int64_t e = e0 + k * kRkThreads + threadIdx.x;
-    if (e < g.m) atomicAdd(&h[rank_bucket(sp, nsp, order_key<T>(z[e]))], 1u);
+    const int64_t e = e0 + k * kRkThreads;
+    zv[k] = e < g.m ? z[e] : (T)0;
   }
+  const int nsp = load_splitters(ss, g, sp);
+#pragma unroll
+  for (int k = 0; k < kRkPer; ++k)
+    if (e0 + k * kRkThreads < g.m) atomicAdd(&h[rank_bucket(sp, nsp, order_key<T>(zv[k]))], 1u);
   __syncthreads();
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
     rel[(int64_t)b * g.nblk + blockIdx.x] = h[b];
@@ -172,13 +176,18 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict
   __shared__ uint32_t cur[2 * kRkMaxB];
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
     cur[b] = start[b] + rel[(int64_t)b * g.nblk + blockIdx.x];
-  const int nsp = load_splitters(ss, g, sp);
-  const int64_t e0 = (int64_t)blockIdx.x * kRkTile;
-#pragma unroll 4
+  const int64_t e0 = (int64_t)blockIdx.x * kRkTile + threadIdx.x;
+  T zv[kRkPer];
+#pragma unroll
   for (int k = 0; k < kRkPer; ++k) {
-    const int64_t e = e0 + k * kRkThreads + threadIdx.x;
-    if (e < g.m) {
-      const uint64_t key = order_key<T>(z[e]);
+    const int64_t e = e0 + k * kRkThreads;
+    zv[k] = e < g.m ? z[e] : (T)0;
+  }
+  const int nsp = load_splitters(ss, g, sp);
+#pragma unroll
+  for (int k = 0; k < kRkPer; ++k) {
+    if (e0 + k * kRkThreads < g.m) {
+      const uint64_t key = order_key<T>(zv[k]);
       bkeys[atomicAdd(&cur[rank_bucket(sp, nsp, key)], 1u)] = key;
     }
   }
@@ -222,7 +231,8 @@ __device__ __forceinline__ double key_value<long long>(uint64_t k) {
   return (double)(long long)(k ^ 0x8000000000000000ull);
 }
 
-// block-wide min / max (all threads get the result)
+// block-wide min / max over NT threads (all threads get the result)
+template <int NT>
 __device__ __forceinline__ void block_minmax(double& lo, double& hi, uint64_t& klo,
                                              uint64_t& khi, double* sd, uint64_t* sk) {
 #pragma unroll
@@ -234,7 +244,7 @@ __device__ __forceinline__ void block_minmax(double& lo, double& hi, uint64_t& k
     khi = b > khi ? b : khi;
   }
   const int wid = threadIdx.x / kWave;
-  constexpr int W = kRkThreads / kWave;
+  constexpr int W = NT / kWave;
   if ((threadIdx.x & (kWave - 1)) == 0) {
     sd[wid] = lo;
     sd[W + wid] = hi;
@@ -284,20 +294,21 @@ __device__ __forceinline__ void sub_prefix(uint32_t* h) {
 
 // pass 4: one block per interval bucket: the two candidate maps, their histograms, the better
 // one's prefix table subp[b][0 .. kRkSub] and the z keys sorted by it into skeys
+constexpr int kSubThreads = 1024;  // ~4000 z per bucket: four per thread and pass
 template <typename T>
-__global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
+__global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
     RankGeo g, const uint32_t* __restrict__ start, const uint32_t* __restrict__ total,
     const uint64_t* __restrict__ bkeys, uint64_t* __restrict__ skeys,
     uint32_t* __restrict__ subp, SubMap* __restrict__ maps) {
   __shared__ uint32_t hv[kRkSub + 1], hk[kRkSub + 1];
-  __shared__ double sd[2 * kRkThreads / kWave];
-  __shared__ uint64_t sk[2 * kRkThreads / kWave];
+  __shared__ double sd[2 * kSubThreads / kWave];
+  __shared__ uint64_t sk[2 * kSubThreads / kWave];
   __shared__ unsigned long long cost[2];
   const int b = 2 * blockIdx.x;  // interval buckets only
   const uint32_t s0 = start[b], c = total[b];
   double lo = __builtin_inf(), hi = -__builtin_inf();
   uint64_t klo = ~0ull, khi = 0;
-  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
+  for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) {
     const uint64_t k = bkeys[s0 + i];
     const double v = key_value<T>(k);
     if (v - v == 0.0) {  // finite
@@ -309,9 +320,9 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
       khi = k > khi ? k : khi;
     }
   }
-  for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) hv[i] = hk[i] = 0;
+  for (int i = threadIdx.x; i <= kRkSub; i += kSubThreads) hv[i] = hk[i] = 0;
   if (threadIdx.x < 2) cost[threadIdx.x] = 0;
-  block_minmax(lo, hi, klo, khi, sd, sk);
+  block_minmax<kSubThreads>(lo, hi, klo, khi, sd, sk);
   SubMap fv{0.0, 0.0, 0, 0, 0}, fk{0.0, 0.0, 0, 0, 1};
   if (hi > lo) {
     const double scale = (double)kRkSub / (hi - lo);
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
     fk.klo = klo;
     fk.kshift = bits > 11 ? bits - 11 : 0;
   }
-  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
+  for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) {
     const uint64_t k = bkeys[s0 + i];
     const double v = key_value<T>(k);
     atomicAdd(&hv[fv(v, k)], 1u);
@@ -331,7 +342,7 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
   }
   __syncthreads();
   unsigned long long cv = 0, ck = 0;
-  for (int i = threadIdx.x; i < kRkSub; i += kRkThreads) {
+  for (int i = threadIdx.x; i < kRkSub; i += kSubThreads) {
     cv += (unsigned long long)hv[i] * hv[i];
     ck += (unsigned long long)hk[i] * hk[i];
   }
@@ -345,9 +356,9 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_subsort(
   sub_prefix(h);
   __syncthreads();
   uint32_t* sp_out = subp + (int64_t)blockIdx.x * (kRkSub + 1);
-  for (int i = threadIdx.x; i <= kRkSub; i += kRkThreads) sp_out[i] = h[i];
+  for (int i = threadIdx.x; i <= kRkSub; i += kSubThreads) sp_out[i] = h[i];
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < c; i += kRkThreads) {
+  for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) {
     const uint64_t k = bkeys[s0 + i];
     skeys[s0 + atomicAdd(&h[f(key_value<T>(k), k)], 1u)] = k;
   }
@@ -660,7 +671,7 @@ static int rank_images_t(const T* x, int64_t n, const T* z, int64_t m, const Ran
     hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
     hipLaunchKernelGGL((k_rank_scatter<T>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g, w.ss,
                        w.rel, w.start, w.bkeys);
-    hipLaunchKernelGGL((k_rank_subsort<T>), dim3(g.B), dim3(kRkThreads), 0, st, g, w.start,
+    hipLaunchKernelGGL((k_rank_subsort<T>), dim3(g.B), dim3(kSubThreads), 0, st, g, w.start,
                        w.total, w.bkeys, w.skeys, w.subp, w.maps);
     TW_LAUNCH_CHECK();
   } else {  // no z: every image is 0
@@ -668,6 +679,8 @@ static int rank_images_t(const T* x, int64_t n, const T* z, int64_t m, const Ran
     TW_HIP_CHECK(tw_zero_async(w.total, 0, 4 * (size_t)g.NB, st));
     TW_HIP_CHECK(tw_zero_async(w.ss, 0, 8 * (size_t)kRkSample, st));
   }
+  // (one element per thread: 128 .. 1024 threads per block and four elements per thread
+  // measured the same or slower, profiles/r03s53_time_ranking.log)
   hipLaunchKernelGGL((k_rank_records<T>), dim3((unsigned)ceil_div(g.tot, kRkThreads)),
                      dim3(kRkThreads), 0, st, x, z, g, w.ss, w.start, w.total, w.skeys, w.subp,
                      w.maps, x_rec, z_rec);
