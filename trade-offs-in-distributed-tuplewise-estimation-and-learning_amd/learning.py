@@ -1752,6 +1752,9 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
                 _defer.push(i, res_dev, wbuf, lambda it, res, wh: _eval_host(
                     it, res, wh, n_pairs, n_test, p_learn, fixed, None, None))
             return
+        side = _CACHE.dev.get("eval_side")
+        if side is not None:  # a deferred evaluation may still read the graph's buffers
+            t.cuda.current_stream().wait_stream(side)
         ent[5].copy_(_w_dev)
         ent[2].replay()
     else:
