@@ -729,6 +729,9 @@ int64_t tw_shuffle_swaps_work_bytes(int64_t nx, int64_t nz);
 int32_t tw_shuffle_swaps_rounds(int64_t nx, int64_t nz);
 /* rounds per batch (0 = the default 4.5 ln n + 24; at least 17): a test hook that forces resumed batches */
 int tw_shuffle_swaps_set_rounds(int32_t rounds);
+/* 1 (default): the tail rounds of a batch (every chunk entered, a short pending list) run in
+ * one workgroup launch; 0: one launch per round.  Process-global; results do not depend on it. */
+int tw_shuffle_swaps_set_tail(int32_t on);
 int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz, const uint32_t* d_jx,
                      const uint32_t* d_jz, int32_t first, int32_t round0, void* d_work,
                      uint32_t* d_pending, void* stream);

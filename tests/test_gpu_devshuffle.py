@@ -23,11 +23,12 @@ def _numpy_snapshots(X, Z, T, seed):
                                          (2, 3, np.int64), (1000, 17, np.float64),
                                          (65537, 4099, np.int64),
                                          (1_000_000, 1_000_000, np.float64)])
-@pytest.mark.parametrize("rounds", [0, 17])
-def test_device_shuffle_snapshots_match_numpy(gpu, nx, nz, dtype, rounds):
+@pytest.mark.parametrize("rounds,tail", [(0, 1), (0, 0), (17, 1), (40, 1)])
+def test_device_shuffle_snapshots_match_numpy(gpu, nx, nz, dtype, rounds, tail):
     """T = 3 chained shuffles of X and Z on the device == NumPy's sequential in-place
     shuffles with the same stream, every state; rounds = 17 (the least allowed) forces
-    resumed batches."""
+    resumed batches, 40 resumed batches that end in the one-workgroup tail; tail = 0 one
+    launch per round throughout."""
     from tuplewise import _engine as E, _lib as L
     from tuplewise.numpy_rng import shuffle_draws32
     rs = np.random.RandomState(nx + nz)
@@ -43,10 +44,12 @@ def test_device_shuffle_snapshots_match_numpy(gpu, nx, nz, dtype, rounds):
         jz.append(shuffle_draws32(nz))
     assert np.array_equal(np.random.randint(0, 2 ** 31, 3), probe)
     L.call("tw_shuffle_swaps_set_rounds", rounds)
+    L.call("tw_shuffle_swaps_set_tail", tail)
     try:
         xs, zs = E.shuffle_snapshots_device(L.to_device(X), L.to_device(Z), jx, jz)
     finally:
         L.call("tw_shuffle_swaps_set_rounds", 0)
+        L.call("tw_shuffle_swaps_set_tail", 1)
     for k in range(3):
         assert np.array_equal(xs[k].cpu().numpy(), want_x[k])
         assert np.array_equal(zs[k].cpu().numpy(), want_z[k])

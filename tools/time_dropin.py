@@ -47,3 +47,23 @@ for rep in range(2):
     a = xs[T - 1].cpu().numpy()
     b = zs[T - 1].cpu().numpy()
     t0 = tick("write-back D2H", t0)
+
+# A/B of the one-workgroup tail of the swap rounds (tw_shuffle_swaps_set_tail)
+for tail in (0, 1, 0, 1):
+    L.call("tw_shuffle_swaps_set_tail", tail)
+    est.UnNT(X, Z, N, T, "prop-SWOR")
+    ts = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        est.UnNT(X, Z, N, T, "prop-SWOR")
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    xs, zs = E.shuffle_snapshots_device(xd, zd, jx, jz)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    xs, zs = E.shuffle_snapshots_device(xd, zd, jx, jz)
+    torch.cuda.synchronize()
+    print(f"tail {tail}: est.UnNT {np.median(ts) * 1e3:.2f} ms/call (median of 5), "
+          f"shuffle_snapshots_device {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+L.call("tw_shuffle_swaps_set_tail", 1)

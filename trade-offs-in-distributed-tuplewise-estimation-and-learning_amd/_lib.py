@@ -160,6 +160,7 @@ _SIGNATURES = {
     "tw_shuffle_swaps_work_bytes": [_i64, _i64],
     "tw_shuffle_swaps_rounds": [_i64, _i64],
     "tw_shuffle_swaps_set_rounds": [_i32],
+    "tw_shuffle_swaps_set_tail": [_i32],
     "tw_shuffle_swaps": [_vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp],
 }
 _RESTYPES = {

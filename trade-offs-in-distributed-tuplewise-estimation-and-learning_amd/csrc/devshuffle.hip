@@ -157,12 +157,82 @@ __global__ __launch_bounds__(kShThreads) void k_sh_round(
   }
 }
 
+// The tail of a batch in ONE workgroup: once every chunk has entered, only the pending list is
+// left and it shrinks geometrically (x0.8 per round), so the last ~40 rounds of a 1e6-item
+// shuffle are a few thousand iterations each — a launch apiece cost more than the work.  Rounds
+// [r0, r1) run here back to back with workgroup barriers between them: the same per-iteration
+// step as k_sh_round (same reservations, same lists and counters), one CU, so plain loads and
+// stores of the arrays and lists stay coherent through its L1; the reservations, written by
+// L2 atomics, are read with agent-scope loads (not L1).  Stops early once a round leaves no
+// pending iteration (cnt_final = 0); otherwise cnt_final = the count after round r1 - 1, as
+// after a batch of launches.
+constexpr int kShFinThreads = 1024;
+__global__ __launch_bounds__(kShFinThreads) void k_sh_finish(
+    int r0, int r1, uint64_t* __restrict__ x, uint64_t* __restrict__ z,
+    const uint32_t* __restrict__ jx, const uint32_t* __restrict__ jz, int64_t nx,
+    uint32_t* __restrict__ L0, uint32_t* __restrict__ L1, unsigned* __restrict__ cnt,
+    unsigned long long* __restrict__ R0, unsigned long long* __restrict__ R1,
+    unsigned* __restrict__ cnt_final) {
+  __shared__ unsigned s_n;
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int r = r0; r < r1; ++r) {
+    // round r reads the list of round r-1 and counter cnt[r - r0], writes the other list and
+    // cnt[r - r0 + 1] (the caller's cnt points at the counter of round r0's input)
+    if (threadIdx.x == 0)
+      s_n = __hip_atomic_load(cnt + (r - r0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int64_t n_list = s_n;
+    if (n_list == 0) {
+      if (threadIdx.x == 0) *cnt_final = 0u;
+      return;
+    }
+    const uint32_t* list_in = (r & 1) ? L0 : L1;  // L[(r + 1) & 1]
+    uint32_t* list_out = (r & 1) ? L1 : L0;       // L[r & 1]
+    const unsigned long long* Rcur = (r & 1) ? R1 : R0;
+    unsigned long long* Rnext = (r & 1) ? R0 : R1;
+    unsigned* cnt_out = cnt + (r - r0) + 1;
+    for (int64_t base = threadIdx.x - lane; base < n_list; base += kShFinThreads) {
+      const int64_t t = base + lane;
+      bool pending = false;
+      int64_t g = 0;
+      if (t < n_list) {
+        g = (int64_t)list_in[t];
+        const ShItem it = sh_item(g, x, z, jx, jz, nx);
+        const unsigned long long k = sh_key(r, g);
+        const unsigned long long a = __hip_atomic_load(Rcur + it.gi, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_load(Rcur + it.gj, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        if (a == k && b == k) {
+          const uint64_t vi = it.a[it.i], vj = it.a[it.j];
+          it.a[it.j] = vi;
+          it.a[it.i] = vj;
+        } else {
+          sh_reserve(Rnext, it.gi, it.gj, sh_key(r + 1, g));
+          pending = true;
+        }
+      }
+      const unsigned long long m = __ballot(pending);
+      if (m) {
+        unsigned at = 0;
+        if (lane == 0) at = atomicAdd(cnt_out, (unsigned)__popcll(m));
+        at = __shfl(at, 0, kWave);
+        if (pending) list_out[at + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)g;
+      }
+    }
+    __syncthreads();  // this round's swaps, reservations and list entries before the next
+  }
+  if (threadIdx.x == 0)
+    *cnt_final = __hip_atomic_load(cnt + (r1 - r0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct ShPlan {
   int rounds;                       // rounds per batch
   int64_t R, list, cnt, bytes;      // workspace offsets
 };
 
 static int g_sh_rounds = 0;  // tw_shuffle_swaps_set_rounds (tests: force resumed batches)
+static int g_sh_tail = 1;    // tw_shuffle_swaps_set_tail: the one-workgroup tail (k_sh_finish)
 
 inline ShPlan plan_sh(int64_t nx, int64_t nz) {
   ShPlan p{};
@@ -193,6 +263,13 @@ extern "C" int64_t tw_shuffle_swaps_work_bytes(int64_t nx, int64_t nz) {
 extern "C" int tw_shuffle_swaps_set_rounds(int32_t rounds) {
   TW_ARG_CHECK(rounds >= 0 && rounds < (1 << 20), "tw_shuffle_swaps_set_rounds: bad count");
   g_sh_rounds = rounds;
+  return TW_OK;
+}
+
+// 1: the tail rounds of a batch in one workgroup (default); 0: one launch per round (A/B, tests)
+extern "C" int tw_shuffle_swaps_set_tail(int32_t on) {
+  TW_ARG_CHECK(on == 0 || on == 1, "tw_shuffle_swaps_set_tail: 0 or 1");
+  g_sh_tail = on;
   return TW_OK;
 }
 
@@ -247,16 +324,33 @@ extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_
     TW_HIP_CHECK(hipMemcpyAsync(cnt, cnt + p.rounds, 4, hipMemcpyDeviceToDevice, st));
     TW_HIP_CHECK(tw_zero_async(cnt + 1, 0, (size_t)p.rounds * 4, st));
   }
+  // rounds of the whole grid while chunks enter and the list is long, then the tail in one
+  // workgroup (k_sh_finish) once the expected list is under ~kShFinThreads * 8 iterations
+  const double tail_items = (double)kShFinThreads * 8;
+  int k_fin = p.rounds;
   for (int k = 0; k < p.rounds; ++k) {
     const int r = round0 + k;
-    // round r reads the list of round r-1 (L[(r+1)&1]) and writes L[r&1]
     const double est =
         r < kShWindows ? 2.0 * per : 2.0 * per * std::pow(0.8, (double)(r - kShWindows + 1));
+    if (g_sh_tail && r > kShWindows && est < tail_items) {
+      k_fin = k;
+      break;
+    }
+    // round r reads the list of round r-1 (L[(r+1)&1]) and writes L[r&1]
     hipLaunchKernelGGL(k_sh_round, dim3(grid_for(est)), dim3(kShThreads), 0, st, r, d_x, d_z,
                        d_jx, d_jz, ch, L[(r + 1) & 1], cnt + k, L[r & 1], cnt + k + 1, R[r & 1],
                        R[(r + 1) & 1]);
   }
   TW_LAUNCH_CHECK();
+  if (k_fin < p.rounds) {
+    hipLaunchKernelGGL(k_sh_finish, dim3(1), dim3(kShFinThreads), 0, st, round0 + k_fin,
+                       round0 + p.rounds, d_x, d_z, d_jx, d_jz, (int64_t)nx, L[0], L[1],
+                       cnt + k_fin, R[0], R[1], d_pending);
+    TW_LAUNCH_CHECK();
+    // the next batch (if any) starts from cnt[p.rounds]
+    TW_HIP_CHECK(hipMemcpyAsync(cnt + p.rounds, d_pending, 4, hipMemcpyDeviceToDevice, st));
+    return TW_OK;
+  }
   TW_HIP_CHECK(hipMemcpyAsync(d_pending, cnt + p.rounds, 4, hipMemcpyDeviceToDevice, st));
   return TW_OK;
 }
