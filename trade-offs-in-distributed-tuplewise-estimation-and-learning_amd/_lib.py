@@ -240,7 +240,11 @@ def device():
 
 
 def stream_handle():
-    return ctypes.c_void_p(torch().cuda.current_stream().cuda_stream)
+    """The current HIP stream of the current device as a raw handle (the C ABI's `stream`): the
+    raw-stream accessor, not a torch.cuda.Stream object per call (~4x less host time in the
+    learning loop's launches)."""
+    C = torch()._C
+    return ctypes.c_void_p(C._cuda_getCurrentRawStream(C._cuda_getDevice()))
 
 
 def host_device_pointer(t):
