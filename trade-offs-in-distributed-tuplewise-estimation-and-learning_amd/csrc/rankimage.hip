@@ -384,8 +384,11 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_records(
   if (e >= g.tot) return;
   const int b = rank_bucket(sp, nsp, key);
   uint32_t gv = start[b];  // every z of the lower buckets is below key
-  if ((b & 1) == 0 && total[b] != 0) {  // interval bucket: sub-buckets below + a scan
-    const SubMap f = maps[b >> 1];
+  const uint32_t tb = total[b];
+  // issued with start / total (in bounds for every bucket; used for interval buckets only), so
+  // the chain is splitters -> {start, total, map} -> sub-bucket prefix -> keys
+  const SubMap f = maps[b >> 1];
+  if ((b & 1) == 0 && tb != 0) {  // interval bucket: sub-buckets below + a scan
     const uint32_t sb = f((double)v, key);
     const uint32_t* pt = subp + (int64_t)(b >> 1) * (kRkSub + 1);
     const uint32_t lo = pt[sb], hi = pt[sb + 1];
