@@ -59,6 +59,7 @@ class EventPool:
     def __init__(self, torch, n):
         self._ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     for _ in range(n)]
+        self._w = [1] * n
         self._i = 0
         self._calls = 0
         self._stride = 1
@@ -71,13 +72,20 @@ class EventPool:
     def used(self):
         return self._ev[:self._i]
 
-    def wrap(self, fn):
+    def ms_per_unit(self):
+        """Mean milliseconds per unit of work over the recorded calls (weight = units per call,
+        e.g. the steps one chain count launch carries)."""
+        ms = [a.elapsed_time(b) for a, b in self.used()]
+        return sum(ms) / max(1, sum(self._w[:self._i])) if ms else float("nan")
+
+    def wrap(self, fn, weight=None):
         def timed(*a, **kw):
             c = self._calls
             self._calls += 1
             if self._i >= len(self._ev) or c % self._stride:
                 return fn(*a, **kw)
             e0, e1 = self._ev[self._i]
+            self._w[self._i] = weight(*a, **kw) if weight else 1
             self._i += 1
             e0.record()
             out = fn(*a, **kw)
@@ -955,8 +963,16 @@ def main():
     ops.count = kernel_ms.wrap(ops.count)
     ops.count_step = kernel_ms.wrap(ops.count_step)  # count + next repartition on spare blocks
     ops.count_rank_step = kernel_ms.wrap(ops.count_rank_step)  # the same on rank images
+    # the step chains (csrc/chain.hip): one count launch per chunk of steps (weight: its steps)
+    # and the chunk's emission
+    chain_ms = EventPool(torch, 64)
+    ops.count_chain = chain_ms.wrap(ops.count_chain, weight=lambda *a, **kw: a[5])
+    emit_ms = EventPool(torch, 64)
+    ops.chain_emit = emit_ms.wrap(ops.chain_emit, weight=lambda *a, **kw: len(a[8]))
+    chain_path = S._chain_ok()
     rank_ms = EventPool(torch, 8)  # the once-per-call ranking of X u Z (tw_rank_images)
     ops.rank_images = rank_ms.wrap(ops.rank_images)
+    ops.rank_images_query = rank_ms.wrap(ops.rank_images_query)
     rank_path = S._rank_path_ok()
     ops.count_sorted_step = kernel_ms.wrap(ops.count_sorted_step)  # sorted count + next
     ops.count_sorted_steps = kernel_ms.wrap(ops.count_sorted_steps)  # all K sorted steps
@@ -993,6 +1009,8 @@ def main():
     X_start, Z_start = S.X.clone(), S.Z.clone()  # the score-kernel line replays the same steps
     kernel_ms.clear(sample)
     rank_ms.clear()
+    chain_ms.clear()
+    emit_ms.clear()
     t0 = time.perf_counter()
     # K UnN steps (est.UnNT's loop): repartition i+1 overlaps the counts of step i
     ests = S.UnN_many(range(args.warmup, args.warmup + args.steps))
@@ -1006,6 +1024,11 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()] or [float("nan")]))
+    chain_launch_ms = float(np.mean([a.elapsed_time(b) for a, b in chain_ms.used()]
+                                    or [float("nan")]))
+    if chain_path:  # per-step device time of the chain count launches
+        kms = chain_ms.ms_per_unit()
+    emit_step_ms = emit_ms.ms_per_unit() if chain_path else None
     rank_call_ms = float(np.mean([a.elapsed_time(b) for a, b in rank_ms.used()] or [0.0]))
 
     # the same steps with the score-compare kernel (csrc/count.hip: v_cmp_f64 + VALU/SALU
@@ -1122,7 +1145,8 @@ def main():
     progress("plumbing C1")
     c1 = plumbing_C1(rank == 0 and world == 1 and not args.no_cpu_baseline)
 
-    count_kernel = "k_count_rank" if rank_path else "k_count_complete"
+    count_kernel = ("k_count_chain" if chain_path else "k_count_rank" if rank_path
+                    else "k_count_complete")
     traffic, traffic_plain = pmc_traffic(count_kernel)
     total_pairs = pairs_per_step_rank * world * args.steps
     value = total_pairs / dt
@@ -1152,11 +1176,11 @@ def main():
                    "parallelism": (f"dp{world}: shards over ranks, "
                                    + ("RCCL" if os.environ.get("TW_BENCH_BACKEND", "nccl")
                                       == "nccl" else "gloo (rehearsal)")
-                                   + (" all-gather of the sample once per call, every rank "
-                                      "applies each global repartition to all records (no "
-                                      "per-step collective)" if S._rank_path_ok()
-                                      and S._replicated_ok() else
-                                      " all-to-all repartition")
+                                   + (" step chains: all-gather of the sample once per call, "
+                                      "each rank walks its own elements' repartitions, one "
+                                      "all-to-all of {image, position} records per chunk of "
+                                      "<= 32 steps, every step of a chunk counted in one launch"
+                                      if S._chain_ok() else " all-to-all repartition")
                                    + " + all-reduce of counts"
                                    if world > 1 else
                                    "dp1: one GPU, device Feistel repartition fused into the "
@@ -1166,18 +1190,27 @@ def main():
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
                      "count_kernel_ms": kms, "traffic": traffic,
                      "traffic_count_only": traffic_plain,
-                     "ranking_ms_per_call": rank_call_ms if rank_path else None,
+                     "ranking_ms_per_call": rank_call_ms if rank_path or chain_path else None,
+                     "chain_count_launch_ms": chain_launch_ms if chain_path else None,
+                     "chain_emit_ms_per_step": emit_step_ms,
                      "note": ("1 compared pair = 1 lane-op of the contract (f64 vector "
-                              "lane-op peak); k_count_rank compares packed f32 rank images of "
+                              "lane-op peak); the count compares packed f32 rank images of "
                               "the scores (two pairs per lane per instruction: a clamped "
-                              "v_pk_add_f32 and an accumulating one; csrc/rankimage.hip), "
-                              "exact by construction; the ranking of X u Z runs once per "
-                              "UnN_many call inside the timed region (ranking_ms_per_call) "
-                              if rank_path else "1 v_cmp_f64 lane-op per pair; ")
-                             + "the timed launch also carries the next repartition on its tail "
-                               "blocks; traffic = HBM bytes/launch (FETCH_SIZE+WRITE_SIZE) from "
-                               "the committed rocprofv3 --pmc summary of this kernel: the timed "
-                               "launch, and a launch without the repartition"},
+                              "v_pk_add_f32 and an accumulating one), exact by construction; "
+                              "the ranking of X u Z runs once per UnN_many call inside the "
+                              "timed region (ranking_ms_per_call) "
+                              if rank_path or chain_path else "1 v_cmp_f64 lane-op per pair; ")
+                             + ("step chains (csrc/chain.hip): every element walks the call's "
+                                "repartitions once (k_chain_emit, chain_emit_ms_per_step) and "
+                                "ONE k_count_chain launch counts all steps of a chunk "
+                                "(chain_count_launch_ms); count_kernel_ms = that launch per "
+                                "step; traffic = HBM bytes per step of the count launch "
+                                "(FETCH_SIZE+WRITE_SIZE) from the committed rocprofv3 --pmc "
+                                "summary" if chain_path else
+                                "the timed launch also carries the next repartition on its tail "
+                                "blocks; traffic = HBM bytes/launch (FETCH_SIZE+WRITE_SIZE) from "
+                                "the committed rocprofv3 --pmc summary of this kernel: the timed "
+                                "launch, and a launch without the repartition")},
         "score_compare_kernel": score_line,
         "estimate_last_step": float(est),
         "plumbing_C1": c1,

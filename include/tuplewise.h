@@ -137,6 +137,76 @@ int tw_count_rank_set_plan(int32_t R, int64_t z_chunk);
  * last blocks of the grid (front = 0, the default) or the first (front = 1).  Process-global;
  * results do not depend on it. */
 int tw_count_rank_set_next(int32_t front);
+/* Tuning hook for tw_rank_images / tw_rank_images_query: sampled z keys for the splitters (512,
+ * 1024 or 2048) and z per thread in the bucket passes (4, 8 or 16).  Process-global; results
+ * do not depend on it (the workspace size does: query it after setting). */
+int tw_rank_set_plan(int32_t sample, int32_t per);
+/* tw_rank_images over several ranks (and for half ties): the images are counted against the Z
+ * of d_z_all (the all-gathered sample, n_z_all < 2^24) but written only for the n_x + n_z
+ * elements of d_x / d_z (this rank's share; d_z may be d_z_all).  half = 1: each X record's
+ * high word is h(x) = #{z in d_z_all : z <= x} as f32 bits (NaN x: -2^25) instead of the index.
+ * d_work: tw_rank_images_work_bytes(n_x, n_z_all) bytes. */
+int tw_rank_images_query(const void* d_z_all, int64_t n_z_all, const void* d_x, int64_t n_x,
+                         const void* d_z, int64_t n_z, int32_t dtype, int32_t half,
+                         void* d_work, int64_t work_bytes, uint64_t* d_x_rec, uint64_t* d_z_rec,
+                         void* stream);
+
+/* ---- A7 / (e) step chains (round 4, csrc/chain.hip): the repartition loop of est.UnNT
+ * (estimation-experiment/main.py:76-79; each repartition = the keyed Feistel bijection of
+ * tw_permute_pair with keys 2k / 2k+1) walked per element.  A rank holds n_x + n_z elements
+ * whose global indices start at rank * n_x / rank * n_z in samples of world * n_x / world * n_z;
+ * every rank's local layout is prop-SWOR shards of x_shard / z_shard positions (n_shards of
+ * them, clamped at the array ends, then a tail in no shard).
+ * tw_chain_emit walks `steps` (<= 32) repartitions (host arrays keys_x / keys_z of the Feistel
+ * keys) for every element of d_x_rec / d_z_rec (rank-image records; half = 1: X records carry
+ * {g, h}), its global position kept in d_x_pos / d_z_pos (u32; first = 1: start from the
+ * element's global index).  world == 1: for each step c the images are appended to the bags
+ * d_x_bag [steps][n_x] (f32, or {g, h} f32 pairs when half) / d_z_bag [steps][n_z] (f32), each
+ * shard's slot range holding exactly its images in an arbitrary order; d_cursors: scratch of
+ * steps * 2 * (n_shards + 1) u32.  world > 1: records go to d_send, per destination rank g a
+ * chunk of steps buckets of (cap + 1) * W u64 words (W = 1 + half; word 0 of a bucket = its
+ * count), each record {image word(s), local position (Z: n_x + position)}; a bucket past cap
+ * sets *d_flag (the record is dropped). */
+int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec, int64_t n_z,
+                  int32_t half, uint32_t* d_x_pos, uint32_t* d_z_pos, int32_t first,
+                  int32_t rank, int32_t world, const uint64_t* keys_x, const uint64_t* keys_z,
+                  int32_t steps, int64_t x_shard, int64_t z_shard, int32_t n_shards,
+                  void* d_x_bag, void* d_z_bag, uint32_t* d_cursors, uint64_t* d_send,
+                  int64_t cap, int32_t* d_flag, void* stream);
+/* The receiving side of tw_chain_emit's buckets after an equal-split all-to-all (d_recv: world
+ * chunks in source order): every record into the bags at its position; a count past cap sets
+ * *d_flag. */
+int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
+                    int32_t half, int64_t n_x, int64_t n_z, void* d_x_bag, void* d_z_bag,
+                    int32_t* d_flag, void* stream);
+/* The all-pairs counts of `steps` x n_shards bags in ONE launch: bag (c, s) = x images
+ * [c * x_stride + d_x_off[s], c * x_stride + d_x_off[s + 1]) against z images likewise;
+ * d_out[c * n_shards + s] (zeroed here) = #{x > z} (half = 1: 2 #{x > z} + #{x == z}, the
+ * tw_count_pairs TW_PRED_HALF units).  Identical to tw_count_pairs on the scores. */
+int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off, int64_t x_stride,
+                         const void* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
+                         int32_t n_shards, int32_t steps, int64_t max_nx, int64_t max_nz,
+                         int32_t half, uint64_t* d_out, void* stream);
+/* Tuning hook for tw_chain_emit: elements per thread (2, 4 or 8) and steps per reservation
+ * round (1 or 16 / elements per thread); 0 = automatic.  Process-global; results do not depend
+ * on it (the order inside a bag does). */
+int tw_chain_set_emit(int32_t epr, int32_t steps_per_round);
+/* Tuning hook for tw_count_pairs_chain: x-images per lane (8 or 16; 0 = automatic) and z-chunk
+ * length (0 = automatic).  Process-global; results do not depend on it. */
+int tw_count_chain_set_plan(int32_t R, int64_t z_chunk);
+/* The scores in their final order after the chains (one process): d_x_out[d_x_pos[e]] =
+ * d_x[e] (8-B values), likewise for Z. */
+int tw_chain_scatter(const void* d_x, const uint32_t* d_x_pos, int64_t n_x, const void* d_z,
+                     const uint32_t* d_z_pos, int64_t n_z, void* d_x_out, void* d_z_out,
+                     void* stream);
+/* The same over ranks: this rank's final positions [x_base, x_base + n_x) of the n_x_all-long
+ * X (and Z likewise) walked back through all `steps` repartitions (inverse Feistel, last step
+ * first) and gathered from the all-gathered samples d_x_all / d_z_all.  d_work: n_x + n_z u32
+ * when steps > 32. */
+int tw_chain_gather(const void* d_x_all, const void* d_z_all, int64_t x_base, int64_t n_x,
+                    int64_t n_x_all, int64_t z_base, int64_t n_z, int64_t n_z_all,
+                    const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
+                    uint32_t* d_work, void* d_x_out, void* d_z_out, void* stream);
 
 /* ---- f4: the same counts in O((n+m) log m): sort each z-chunk (<= 16384 keys) in LDS as
  * order-preserving u64 keys, then binary-search every x (csrc/rankcount.hip).  Bit-identical

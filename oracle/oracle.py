@@ -373,20 +373,29 @@ def order_keys(v) -> np.ndarray:
     return k
 
 
-def rank_records(X, Z):
+def rank_records(X, Z, half=False, Z_all=None):
     """Restates csrc/rankimage.hip tw_rank_images (the round-3 all-pairs count on packed f32
     images; not a reference function): every element's image is the number of Z-scores whose
     order key is below its own, g(v) = #{z : key(z) < key(v)} (NaN x: -2^25); z images are
     stored negated.  Records: low word the f32 image bits, high word the element's index.  For
-    every pair, X_i > Z_j  <=>  x_image + z_image >= 1."""
+    every pair, X_i > Z_j  <=>  x_image + z_image >= 1.
+    tw_rank_images_query: Z_all (default Z) is the Z the images count; half=True puts
+    h(x) = #{z : key(z) <= key(x)} (NaN x: -2^25) in the X records' high word instead of the
+    index, so that X_i >= Z_j  <=>  h_image + z_image >= 1."""
     X, Z = np.asarray(X).reshape(-1), np.asarray(Z).reshape(-1)
     n, m = X.size, Z.size
-    zk = np.sort(order_keys(Z))
+    zk = np.sort(order_keys(Z if Z_all is None else np.asarray(Z_all).reshape(-1)))
     gx = np.searchsorted(zk, order_keys(X), side="left").astype(np.float32)
     gz = np.searchsorted(zk, order_keys(Z), side="left").astype(np.float32)
+    hi = np.arange(n, dtype=np.uint64)
+    if half:
+        hx = np.searchsorted(zk, order_keys(X), side="right").astype(np.float32)
+        if X.dtype != np.int64:
+            hx[np.isnan(X)] = np.float32(-2.0 ** 25)
+        hi = hx.view(np.uint32).astype(np.uint64)
     if X.dtype != np.int64:
         gx[np.isnan(X)] = np.float32(-2.0 ** 25)
-    xr = gx.view(np.uint32).astype(np.uint64) | (np.arange(n, dtype=np.uint64) << np.uint64(32))
+    xr = gx.view(np.uint32).astype(np.uint64) | (hi << np.uint64(32))
     zr = (-gz).view(np.uint32).astype(np.uint64) | (np.arange(m, dtype=np.uint64)
                                                     << np.uint64(32))
     return xr.view(np.int64), zr.view(np.int64)

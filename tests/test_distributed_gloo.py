@@ -167,8 +167,106 @@ class OracleOpsRank(OracleOpsFixed):
         return vals[rec >> 32]
 
 
+class OracleOpsChain(OracleOpsRank):
+    """Adds the step chains (tw_rank_images_query / tw_chain_emit / tw_chain_unpack /
+    tw_count_pairs_chain / tw_chain_scatter / tw_chain_gather, csrc/chain.hip) restated, so
+    UnN_many takes the chain path on host tensors (bags written at exact positions, one valid
+    arrangement of the device's shard multisets)."""
+
+    def rank_images_query(self, Z_all, X, Z, dtype, half=False):
+        xr, zr = O.rank_records(X.numpy(), Z.numpy(), half=half, Z_all=Z_all.numpy())
+        return torch.from_numpy(xr), torch.from_numpy(zr)
+
+    def chain_emit(self, xr, zr, half, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
+                   n_shards, x_bag=None, z_bag=None, cursors=None, send=None, cap=0, flag=None):
+        n, m = xr.numel(), zr.numel()
+        W = 2 if half else 1
+        steps = len(keys_x)
+        buckets = {}
+        for side, (rec, pos, keys, nl) in enumerate(((xr, xpos, keys_x, n), (zr, zpos, keys_z, m))):
+            r = rec.numpy().view(np.uint64)
+            val = r if (half and side == 0) else r & np.uint64(0xFFFFFFFF)
+            p = (np.arange(rank * nl, (rank + 1) * nl) if first
+                 else pos.numpy().view(np.uint32).astype(np.int64))
+            for c, key in enumerate(keys):
+                p = O.feistel_perm(p, world * nl, int(key))
+                if world == 1:
+                    bag = (x_bag if side == 0 else z_bag)[c].numpy()
+                    bag.view(np.uint64 if (half and side == 0) else np.uint32)[p] = val
+                else:
+                    dst = p // nl
+                    loc = p - dst * nl + (n if side else 0)
+                    for g in range(world):
+                        sel = dst == g
+                        buckets.setdefault((g, c), []).append((val[sel], loc[sel]))
+            pos.numpy()[:] = p.astype(np.uint32).view(np.int32)
+        if world > 1:
+            buf = send.numpy().view(np.uint64)
+            for g in range(world):
+                for c in range(steps):
+                    v = np.concatenate([a for a, _ in buckets[(g, c)]])
+                    q = np.concatenate([b for _, b in buckets[(g, c)]]).astype(np.uint64)
+                    b0 = (g * steps + c) * (cap + 1) * W
+                    buf[b0] = len(v)
+                    if len(v) > cap:
+                        flag.numpy()[0] = 1
+                        v, q = v[:cap], q[:cap]
+                    recs = buf[b0 + W:b0 + W * (1 + len(v))].reshape(-1, W)
+                    if W == 1:
+                        recs[:, 0] = v | (q << np.uint64(32))
+                    else:
+                        recs[:, 0], recs[:, 1] = v, q
+
+    def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag):
+        W = 2 if half else 1
+        buf = recv.numpy().view(np.uint64)
+        for b in range(world * steps):
+            c = b % steps
+            b0 = b * (cap + 1) * W
+            cnt = int(buf[b0] & np.uint64(0xFFFFFFFF))
+            if cnt > cap:
+                flag.numpy()[0] = 1
+            recs = buf[b0 + W:b0 + W * (1 + min(cnt, cap))].reshape(-1, W)
+            v = recs[:, 0] if W == 2 else recs[:, 0] & np.uint64(0xFFFFFFFF)
+            p = (recs[:, 1] if W == 2 else recs[:, 0] >> np.uint64(32)).astype(np.int64)
+            isx = p < n
+            x_bag[c].numpy().view(np.uint64 if half else np.uint32)[p[isx]] = v[isx]
+            z_bag[c].numpy().view(np.uint32)[p[~isx] - n] = v[~isx]
+
+    def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
+                    z_stride, max_nx, max_nz, half, out):
+        xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
+        for c in range(steps):
+            xb = x_bag[c].numpy().view(np.float32)
+            nz = z_bag[c].numpy().view(np.float32)
+            for s in range(n_shards):
+                b = nz[zo[s]:zo[s + 1]]
+                if half:  # {g, h} pairs: [x > z] + [x >= z]
+                    a = xb.reshape(-1, 2)[xo[s]:xo[s + 1]]
+                    cnt = (a[:, 0, None] + b >= 1).sum() + (a[:, 1, None] + b >= 1).sum()
+                else:
+                    cnt = (xb[xo[s]:xo[s + 1], None] + b >= 1).sum()
+                out[c, s] = int(cnt)
+        return out
+
+    def chain_scatter(self, X, xpos, Z, zpos):
+        Xo, Zo = torch.empty_like(X), torch.empty_like(Z)
+        Xo.numpy()[xpos.numpy().view(np.uint32)] = X.numpy()
+        Zo.numpy()[zpos.numpy().view(np.uint32)] = Z.numpy()
+        return Xo, Zo
+
+    def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z):
+        out = []
+        for A, base, cnt, keys in ((X_all, x_base, n, keys_x), (Z_all, z_base, m, keys_z)):
+            p = np.arange(base, base + cnt)
+            for key in reversed(keys):
+                p = O.feistel_perm_inv(p, A.numel(), int(key))
+            out.append(torch.from_numpy(A.numpy()[p].copy()))
+        return out[0], out[1]
+
+
 _OPS = {"plain": OracleOps, "fused": OracleOpsFused, "fixed": OracleOpsFixed,
-        "rank": OracleOpsRank}
+        "rank": OracleOpsRank, "chain": OracleOpsChain}
 
 
 def _free_port():
@@ -237,15 +335,16 @@ def test_multirank_repartition_is_G_invariant(G, fused):
     assert inc == float(S1.UnNB(B, seed=77))
 
 
-def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q):
+def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     from tuplewise.device import ShardedSample
     X, Z = _global_data(G, n_loc, m_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
                       torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
-                      group=dist.group.WORLD, ops=OracleOpsRank())
-    assert S.algo == "pairs" and S._rank_path_ok()
+                      group=dist.group.WORLD, ops=OracleOpsChain(), tie_mode=tie_mode,
+                      algo="pairs")
+    assert S.algo == "pairs" and S._chain_ok()
     vals = [float(v) for v in S.UnN_many(keys)]
     Xg = [torch.empty_like(S.X) for _ in range(G)]
     Zg = [torch.empty_like(S.Z) for _ in range(G)]
@@ -257,22 +356,24 @@ def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("G", [2, 4, 8])
-def test_replicated_rank_steps_are_G_invariant(G):
-    """UnN_many's collective-free multi-rank chain (device.REPLICATED_RANK_STEPS): every rank
-    ranks the all-gathered sample, repartitions the whole record arrays with the global keys and
-    counts only its own shards; one all-reduce of the counts per call.  The estimates equal the
-    one-process score path's (est.UnNT's loop) and the ranks' final arrays, concatenated, equal
-    the global permutation chain."""
+@pytest.mark.parametrize("G,tie_mode", [(2, "strict"), (4, "strict"), (8, "strict"),
+                                        (2, "half")])
+def test_chain_steps_are_G_invariant(G, tie_mode):
+    """UnN_many's step chains over G ranks (csrc/chain.hip, restated): every rank images its
+    own elements against the all-gathered Z, walks their chains into per-(rank, step) buckets,
+    one all-to-all per chunk, counts its bags; one all-reduce of the counts per call.  The
+    estimates equal the one-process score path's (est.UnNT's loop, key by key) and the ranks'
+    final arrays, concatenated, equal the global permutation chain."""
     import tuplewise  # noqa: F401
     from tuplewise import device as D
-    assert D.REPLICATED_RANK_STEPS
+    assert D.CHAIN_STEPS
     from tuplewise.device import ShardedSample
     n_loc, m_loc, N, keys = 600, 450, 3, [5, 6, 9]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_worker, args=(r, G, port, n_loc, m_loc, N, keys, q))
+    procs = [ctx.Process(target=_rank_worker,
+                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode))
              for r in range(G)]
     for p in procs:
         p.start()
@@ -282,13 +383,13 @@ def test_replicated_rank_steps_are_G_invariant(G):
         assert p.exitcode == 0
     X, Z = _global_data(G, n_loc, m_loc)
     S1 = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
-                       ops=OracleOps())
+                       ops=OracleOps(), tie_mode=tie_mode, algo="pairs")
     assert vals == [float(S1.UnN(k)) for k in keys]  # the score path, key by key
     assert np.array_equal(Xg, S1.X.numpy()) and np.array_equal(Zg, S1.Z.numpy())
-    S1r = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
-                        ops=OracleOpsRank())  # the one-process rank chain
-    assert [float(v) for v in S1r.UnN_many(keys)] == vals
-    assert np.array_equal(S1r.X.numpy(), Xg)
+    S1c = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
+                        ops=OracleOpsChain(), tie_mode=tie_mode, algo="pairs")
+    assert [float(v) for v in S1c.UnN_many(keys)] == vals  # the one-process chain
+    assert np.array_equal(S1c.X.numpy(), Xg)
 
 
 def _overflow_worker(rank, G, port, q):

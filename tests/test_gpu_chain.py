@@ -1,0 +1,281 @@
+"""Step chains (csrc/chain.hip, round 4): est.UnNT's repartition loop walked per element, the
+(step, shard) image bags of a chunk of steps counted in one launch.  Checked against the oracle:
+the bags hold exactly the images of the oracle's permutation chain shard by shard, the counts
+equal the reference predicate on the oracle's permuted arrays (strict and half ties), the
+simulated multi-rank exchange (send buckets, an all-to-all done by hand, unpack) gives the
+one-process bags, and UnN_many through the chains equals the one-launch-per-step paths
+(estimates and final arrays).  Bar: bit-exact (every value is an integer count)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+M64 = 2 ** 64 - 1
+
+
+def _sample(rng, n, kind):
+    if kind == "i64":
+        return rng.randint(-40, 40, n).astype(np.int64)
+    v = rng.normal(size=n).round(2)
+    if kind == "edge" and n > 12:
+        v[::7] = np.nan
+        v[1::9] = 0.0
+        v[2::11] = -0.0
+        v[3::13] = np.inf
+        v[4::17] = -np.inf
+        v[5::19] = 5e-324
+    return v
+
+
+def _chain(a, keys, odd):
+    """The oracle's permutation chain: the arrays after each repartition."""
+    out = []
+    for k in keys:
+        a = O.permute_scatter(a, (2 * k + odd) & M64)
+        out.append(a)
+    return out
+
+
+def _layout(n, m, N):
+    from tuplewise.device import prop_swor_layout
+    x_off, z_off, _ = prop_swor_layout(n, m, N)
+    return x_off, z_off
+
+
+@pytest.mark.parametrize("kind", ["gauss", "edge", "i64"])
+@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("n,m,N", [(5000, 4099, 7), (20_000, 30_000, 1), (3000, 700, 64),
+                                   (1, 1, 1), (4097, 2, 3)])
+def test_chain_bags_and_counts_equal_oracle(gpu, kind, half, n, m, N):
+    """tw_chain_emit (one process) + tw_count_pairs_chain: each (step, shard) bag is the
+    multiset of the oracle's images at that shard's positions after the step's repartition; the
+    counts equal the reference predicate (strict: #{x > z}; half: 2 #{x > z} + #{x == z}) on the
+    oracle's permuted scores; the chain state after the last step gives the final arrays."""
+    import torch
+    from tuplewise import _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(n + 3 * m + N)
+    X, Z = _sample(rng, n, kind), _sample(rng, m, kind)
+    code = L.TW_I64 if kind == "i64" else L.TW_F64
+    ops = HipOps()
+    Xd, Zd = torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda()
+    xr, zr = ops.rank_images_query(Zd, Xd, Zd, code, half)
+    wx, wz = O.rank_records(X, Z, half=half)
+    assert np.array_equal(xr.cpu().numpy(), wx) and np.array_equal(zr.cpu().numpy(), wz)
+    keys = [11, 12, 13, 14, 15]
+    T = len(keys)
+    kx, kz = int(n / N), int((n + m) / N) - int(n / N)
+    x_off, z_off = _layout(n, m, N)
+    x_bag = torch.empty((T, n), dtype=torch.int64 if half else torch.float32, device="cuda")
+    z_bag = torch.empty((T, m), dtype=torch.float32, device="cuda")
+    xpos = torch.empty(n, dtype=torch.int32, device="cuda")
+    zpos = torch.empty(m, dtype=torch.int32, device="cuda")
+    cur = torch.empty(T * 2 * (N + 1), dtype=torch.int32, device="cuda")
+    kxs = [(2 * k) & M64 for k in keys]
+    kzs = [(2 * k + 1) & M64 for k in keys]
+    # two emissions (3 steps, then 2) through the chain state
+    ops.chain_emit(xr, zr, half, xpos, zpos, True, 0, 1, kxs[:3], kzs[:3], kx, kz, N,
+                   x_bag=x_bag, z_bag=z_bag, cursors=cur)
+    ops.chain_emit(xr, zr, half, xpos, zpos, False, 0, 1, kxs[3:], kzs[3:], kx, kz, N,
+                   x_bag=x_bag[3:], z_bag=z_bag[3:], cursors=cur)
+    xo, zo = torch.from_numpy(x_off).cuda(), torch.from_numpy(z_off).cuda()
+    out = torch.full((T, N), 7, dtype=torch.int64, device="cuda")
+    ops.count_chain(x_bag, xo, z_bag, zo, N, 3, n, m, kx, kz, half, out[:3])
+    ops.count_chain(x_bag[3:], xo, z_bag[3:], zo, N, 2, n, m, kx, kz, half, out[3:])
+    xb = x_bag.cpu().numpy()
+    zb = z_bag.cpu().numpy()
+    got = out.cpu().numpy().view(np.uint64)
+    xs, zs = _chain(X, keys, 0), _chain(Z, keys, 1)
+    wxs, wzs = _chain(wx, keys, 0), _chain(wz, keys, 1)
+    for c in range(T):
+        wimg_x = wxs[c] if half else (wxs[c].view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        wimg_z = (wzs[c].view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        gx = xb[c].view(np.int64) if half else xb[c].view(np.uint32)
+        gz = zb[c].view(np.uint32)
+        for s in range(N):
+            a, b = x_off[s], x_off[s + 1]
+            assert np.array_equal(np.sort(gx[a:b]), np.sort(wimg_x[a:b]))
+            a, b = z_off[s], z_off[s + 1]
+            assert np.array_equal(np.sort(gz[a:b]), np.sort(wimg_z[a:b]))
+            xa, za = xs[c][x_off[s]:x_off[s + 1]], zs[c][z_off[s]:z_off[s + 1]]
+            if xa.dtype.kind == "f":
+                xa = xa[~np.isnan(xa)]  # a NaN x is greater than / equal to nothing
+            want = O.count_half_sorted(xa, za) if half else O.count_gt_sorted(xa, za)
+            assert int(got[c, s]) == want, (c, s)
+    Xo, Zo = ops.chain_scatter(Xd, xpos, Zd, zpos)
+    assert np.array_equal(Xo.cpu().numpy(), xs[-1], equal_nan=kind != "i64")
+    assert np.array_equal(Zo.cpu().numpy(), zs[-1], equal_nan=kind != "i64")
+
+
+@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("G", [2, 3])
+def test_chain_exchange_simulated_ranks(gpu, G, half):
+    """Several ranks in one process: each rank images its own elements against the whole Z
+    (tw_rank_images_query), walks its chains into send buckets (tw_chain_emit, world = G), the
+    all-to-all is done by hand (rank r receives every source's chunk for r), tw_chain_unpack
+    fills its bags, tw_count_pairs_chain counts them; the ranks' counts equal one process on the
+    global layout of G*N shards, and tw_chain_gather's final arrays equal the oracle chain."""
+    import torch
+    from tuplewise import _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(9 + G)
+    n_loc, m_loc, N = 3000, 2100, 4
+    X, Z = rng.normal(0.3, 1, G * n_loc).round(3), rng.normal(0, 1, G * m_loc).round(3)
+    ops = HipOps()
+    Zall = torch.from_numpy(Z).cuda()
+    Xall = torch.from_numpy(X).cuda()
+    keys = [21, 22, 23]
+    T = len(keys)
+    kxs = [(2 * k) & M64 for k in keys]
+    kzs = [(2 * k + 1) & M64 for k in keys]
+    kx, kz = int(n_loc / N), int((n_loc + m_loc) / N) - int(n_loc / N)
+    tot = n_loc + m_loc
+    cap = tot // G + tot // (8 * G) + 1024
+    W = 2 if half else 1
+    sends = []
+    for r in range(G):
+        xq = Xall[r * n_loc:(r + 1) * n_loc]
+        zq = Zall[r * m_loc:(r + 1) * m_loc]
+        xr, zr = ops.rank_images_query(Zall, xq, zq, L.TW_F64, half)
+        wx, wz = O.rank_records(X[r * n_loc:(r + 1) * n_loc], Z[r * m_loc:(r + 1) * m_loc],
+                                half=half, Z_all=Z)
+        assert np.array_equal(xr.cpu().numpy(), wx) and np.array_equal(zr.cpu().numpy(), wz)
+        xpos = torch.empty(n_loc, dtype=torch.int32, device="cuda")
+        zpos = torch.empty(m_loc, dtype=torch.int32, device="cuda")
+        send = torch.empty(G * T * (cap + 1) * W, dtype=torch.int64, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ops.chain_emit(xr, zr, half, xpos, zpos, True, r, G, kxs, kzs, kx, kz, N, send=send,
+                       cap=cap, flag=flag)
+        assert int(flag.item()) == 0
+        sends.append(send.view(G, -1))
+    x_off, z_off = _layout(n_loc, m_loc, N)
+    xo, zo = torch.from_numpy(x_off).cuda(), torch.from_numpy(z_off).cuda()
+    counts = []
+    for r in range(G):
+        recv = torch.cat([sends[g][r] for g in range(G)])
+        x_bag = torch.empty((T, n_loc), dtype=torch.int64 if half else torch.float32,
+                            device="cuda")
+        z_bag = torch.empty((T, m_loc), dtype=torch.float32, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ops.chain_unpack(recv, G, T, cap, half, n_loc, m_loc, x_bag, z_bag, flag)
+        out = torch.empty((T, N), dtype=torch.int64, device="cuda")
+        ops.count_chain(x_bag, xo, z_bag, zo, N, T, n_loc, m_loc, kx, kz, half, out)
+        counts.append(out.cpu().numpy())
+        assert int(flag.item()) == 0
+        # exact positions: the receiver's bags are the oracle's permuted images in order
+        wx, wz = O.rank_records(X, Z, half=half)
+        wxs, wzs = _chain(wx, keys, 0), _chain(wz, keys, 1)
+        for c in range(T):
+            ex = wxs[c][r * n_loc:(r + 1) * n_loc]
+            ez = wzs[c][r * m_loc:(r + 1) * m_loc]
+            if half:
+                assert np.array_equal(x_bag[c].cpu().numpy(), ex)
+            else:
+                assert np.array_equal(x_bag[c].cpu().numpy().view(np.uint32),
+                                      (ex.view(np.uint64) & np.uint64(0xFFFFFFFF))
+                                      .astype(np.uint32))
+            assert np.array_equal(z_bag[c].cpu().numpy().view(np.uint32),
+                                  (ez.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+        Xo, Zo = ops.chain_gather(Xall, Zall, r * n_loc, n_loc, r * m_loc, m_loc, kxs, kzs)
+        xs, zs = _chain(X, keys, 0), _chain(Z, keys, 1)
+        assert np.array_equal(Xo.cpu().numpy(), xs[-1][r * n_loc:(r + 1) * n_loc])
+        assert np.array_equal(Zo.cpu().numpy(), zs[-1][r * m_loc:(r + 1) * m_loc])
+    got = np.concatenate(counts, axis=1).view(np.uint64)
+    xs, zs = _chain(X, keys, 0), _chain(Z, keys, 1)
+    for c in range(T):
+        for g in range(G):
+            for s in range(N):
+                xa = xs[c][g * n_loc + x_off[s]:g * n_loc + x_off[s + 1]]
+                za = zs[c][g * m_loc + z_off[s]:g * m_loc + z_off[s + 1]]
+                want = (2 * O.un_count(xa, za) + int((xa[:, None] == za[None, :]).sum())
+                        if half else O.un_count(xa, za))
+                assert int(got[c, g * N + s]) == want
+
+
+def test_chain_gather_many_steps(gpu):
+    """tw_chain_gather over more than 32 steps (chunks walked back through its work array)."""
+    import torch
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(4)
+    G, n_loc, m_loc = 2, 1000, 700
+    X, Z = rng.normal(size=G * n_loc), rng.normal(size=G * m_loc)
+    keys = list(range(100, 170))
+    kxs = [(2 * k) & M64 for k in keys]
+    kzs = [(2 * k + 1) & M64 for k in keys]
+    xs, zs = _chain(X, keys, 0)[-1], _chain(Z, keys, 1)[-1]
+    ops = HipOps()
+    for r in range(G):
+        Xo, Zo = ops.chain_gather(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(),
+                                  r * n_loc, n_loc, r * m_loc, m_loc, kxs, kzs)
+        assert np.array_equal(Xo.cpu().numpy(), xs[r * n_loc:(r + 1) * n_loc])
+        assert np.array_equal(Zo.cpu().numpy(), zs[r * m_loc:(r + 1) * m_loc])
+
+
+@pytest.mark.parametrize("case", ["gauss", "ties_i64", "edge_ragged", "one_shard", "long"])
+@pytest.mark.parametrize("tie_mode", ["strict", "half"])
+def test_unn_many_chain_equals_step_paths(gpu, case, tie_mode):
+    """ShardedSample.UnN_many through the step chains == the one-launch-per-step paths (rank
+    images for strict, the score compare for half ties): estimates and final arrays bit for
+    bit; "long" crosses the 32-step chunk boundary."""
+    import torch
+    from tuplewise import device as D
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(5)
+    keys = [3, 4, 5, 6]
+    if case == "gauss":
+        X, Z, N = rng.normal(0.3, 1, 300_000), rng.normal(0, 1, 250_000), 16
+    elif case == "ties_i64":
+        X, Z, N = rng.randint(0, 50, 160_003), rng.randint(0, 50, 120_000), 12
+    elif case == "edge_ragged":
+        X, Z, N = _sample(rng, 100_001, "edge"), _sample(rng, 77_777, "edge"), 7
+    elif case == "one_shard":
+        X, Z, N = rng.normal(0.5, 1, 20_000), rng.normal(0, 1, 30_000), 1
+    else:
+        X, Z, N = rng.normal(0.5, 1, 40_000).round(2), rng.normal(0, 1, 30_000).round(2), 5
+        keys = list(range(40, 110))
+    got = {}
+    for chain in (True, False):
+        old = D.CHAIN_STEPS
+        D.CHAIN_STEPS = chain
+        try:
+            S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
+                              algo="pairs", tie_mode=tie_mode)
+            assert S._chain_ok() == chain
+            got[chain] = (S.UnN_many(keys), S.X.cpu().numpy(), S.Z.cpu().numpy())
+        finally:
+            D.CHAIN_STEPS = old
+    assert got[True][0] == got[False][0]
+    eqn = X.dtype.kind == "f"
+    assert np.array_equal(got[True][1], got[False][1], equal_nan=eqn)
+    assert np.array_equal(got[True][2], got[False][2], equal_nan=eqn)
+    xa, za = _chain(X, keys, 0)[-1], _chain(Z, keys, 1)[-1]
+    assert np.array_equal(got[True][1], xa, equal_nan=eqn)
+    assert np.array_equal(got[True][2], za, equal_nan=eqn)
+
+
+def test_chain_overflow_flag(gpu):
+    """A send bucket past its capacity sets the flag (records dropped, never written out of
+    place) and the unpack flags a count past cap."""
+    import torch
+    from tuplewise import _lib as L
+    from tuplewise.device import HipOps
+    rng = np.random.RandomState(1)
+    G, n, m = 2, 500, 400
+    X, Z = rng.normal(size=G * n), rng.normal(size=G * m)
+    ops = HipOps()
+    Zall = torch.from_numpy(Z).cuda()
+    xr, zr = ops.rank_images_query(Zall, torch.from_numpy(X[:n]).cuda(), Zall[:m], L.TW_F64)
+    cap = 10
+    send = torch.zeros(G * 1 * (cap + 1), dtype=torch.int64, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    xpos = torch.empty(n, dtype=torch.int32, device="cuda")
+    zpos = torch.empty(m, dtype=torch.int32, device="cuda")
+    ops.chain_emit(xr, zr, False, xpos, zpos, True, 0, G, [5], [6], 50, 40, 10, send=send,
+                   cap=cap, flag=flag)
+    assert int(flag.item()) == 1
+    flag.zero_()
+    x_bag = torch.zeros((1, n), dtype=torch.float32, device="cuda")
+    z_bag = torch.zeros((1, m), dtype=torch.float32, device="cuda")
+    ops.chain_unpack(send, G, 1, cap, False, n, m, x_bag, z_bag, flag)
+    assert int(flag.item()) == 1

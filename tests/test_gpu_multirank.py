@@ -71,7 +71,7 @@ def test_learning_two_ranks_equals_one(gpu, mode, layout):
     assert np.array_equal(got, np.stack(ref))
 
 
-def _est_worker(rank, port, G, q, exchange="fixed", replicated=True):
+def _est_worker(rank, port, G, q, exchange="fixed", chain=True):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -79,7 +79,7 @@ def _est_worker(rank, port, G, q, exchange="fixed", replicated=True):
     torch.cuda.set_device(0)
     from tuplewise import device as D
     from tuplewise.device import ShardedSample
-    D.REPLICATED_RANK_STEPS = replicated  # False: the per-step all-to-all of records
+    D.CHAIN_STEPS = chain  # False: the per-step all-to-all of rank-image records
     rng = np.random.RandomState(3)
     n_loc, N = 40_000, 8
     X = rng.normal(0.3, 1, G * n_loc)
@@ -88,7 +88,7 @@ def _est_worker(rank, port, G, q, exchange="fixed", replicated=True):
                       torch.from_numpy(Z[rank * n_loc:(rank + 1) * n_loc].copy()).cuda(), N,
                       group=dist.group.WORLD, exchange=exchange, algo="pairs")
     vals = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
-    vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # rank images: the replicated chain
+    vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # rank images: the step chains
     Xg = [torch.empty(S.X.shape, dtype=S.X.dtype) for _ in range(G)]
     Zg = [torch.empty(S.Z.shape, dtype=S.Z.dtype) for _ in range(G)]
     dist.all_gather(Xg, S.X.cpu())
@@ -99,9 +99,8 @@ def _est_worker(rank, port, G, q, exchange="fixed", replicated=True):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange,replicated", [("fixed", True), ("fixed", False),
-                                                  ("exact", False)])
-def test_sharded_sample_two_ranks_equals_one(gpu, exchange, replicated):
+@pytest.mark.parametrize("exchange,chain", [("fixed", True), ("fixed", False), ("exact", False)])
+def test_sharded_sample_two_ranks_equals_one(gpu, exchange, chain):
     import torch
     import torch.multiprocessing as mp
     from tuplewise.device import ShardedSample
@@ -113,11 +112,11 @@ def test_sharded_sample_two_ranks_equals_one(gpu, exchange, replicated):
                       algo="pairs")
     want = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
     want += [float(v) for v in S.UnN_many([5, 6, 7])]
-    assert S._rank_path_ok() and S.algo == "pairs"
+    assert S._chain_ok() and S.algo == "pairs"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q, exchange, replicated))
+    procs = [ctx.Process(target=_est_worker, args=(r, port, G, q, exchange, chain))
              for r in range(G)]
     for pr in procs:
         pr.start()

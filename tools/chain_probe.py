@@ -1,0 +1,137 @@
+"""Probe the step chains (csrc/chain.hip) on ONE GPU: (1) one UnN_many call of K steps at the
+bench shape (n = 1e6/class, N = 64) through the chains against the one-launch-per-step path, and
+(2) what rank r of G does in one strong-scaling call (1e6/class and 64 shards in total, 64/G
+shards per rank), the ranking included: the Z structure of the whole Z and the images of the
+rank's own 1/G of the elements (tw_rank_images_query), the chain emission into G send buckets,
+a device copy of the send buffer standing in for the all-to-all (the same bytes; RCCL's xGMI
+transfer is not simulated), the unpack, one count launch of K x 64/G bags and the inverse-chain
+gather of the rank's final arrays.  Reports ms per call and the efficiency against the one-GPU
+call / G.  Run on the GPU box:
+    python tools/chain_probe.py [K ...]"""
+import pathlib
+import sys
+import time
+
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+import numpy as np
+import torch
+
+import tuplewise  # noqa: F401
+from tuplewise import _lib as L
+from tuplewise import device as D
+from tuplewise.device import HipOps, ShardedSample, prop_swor_layout
+
+torch.cuda.set_device(0)
+gen = torch.Generator(device="cuda").manual_seed(1)
+n, N = 1_000_000, 64
+Ks = [int(a) for a in sys.argv[1:]] or [20, 4, 100]
+X = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) + 0.5
+Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+M64 = 2 ** 64 - 1
+
+
+def ev_time(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, (time.perf_counter() - t0) / reps * 1e3
+
+
+def one_gpu_call(K, chain):
+    D.CHAIN_STEPS = chain
+    S = ShardedSample(X.clone(), Z.clone(), N, algo="pairs")
+    base = [1000]
+
+    def call():
+        base[0] += K
+        S.UnN_many(range(base[0], base[0] + K))
+    try:
+        return ev_time(call, 5)
+    finally:
+        D.CHAIN_STEPS = True
+
+
+def rank_call(G, r, K, parts=False):
+    """Rank r's device work in one call of the strong problem split over G ranks."""
+    ops = HipOps()
+    nl, Nl = n // G, N // G
+    x_off, z_off, _ = prop_swor_layout(nl, nl, Nl)
+    xo, zo = torch.from_numpy(x_off).cuda(), torch.from_numpy(z_off).cuda()
+    kx = int(nl / Nl)
+    kz = int(2 * nl / Nl) - kx
+    xq, zq = X[r * nl:(r + 1) * nl], Z[r * nl:(r + 1) * nl]
+    C = min(K, D.CHAIN_MAX)
+    tot = 2 * nl
+    cap = max(1, tot // G + tot // (8 * G) + 1024)
+    send = torch.empty(G * C * (cap + 1), dtype=torch.int64, device="cuda")
+    recv = torch.empty_like(send)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    x_bag = torch.empty((C, nl), dtype=torch.float32, device="cuda")
+    z_bag = torch.empty((C, nl), dtype=torch.float32, device="cuda")
+    xpos = torch.empty(nl, dtype=torch.int32, device="cuda")
+    zpos = torch.empty(nl, dtype=torch.int32, device="cuda")
+    counts = torch.empty((K, Nl), dtype=torch.int64, device="cuda")
+    cur = torch.empty(C * 2 * (Nl + 1), dtype=torch.int32, device="cuda")
+    keys = list(range(500, 500 + K))
+    kxs = [(2 * k) & M64 for k in keys]
+    kzs = [(2 * k + 1) & M64 for k in keys]
+    t = {}
+
+    def mark(name, fn):
+        if not parts:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn()
+        e1.record()
+        t.setdefault(name, []).append((e0, e1))
+        return out
+
+    def call():
+        xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
+        for i0 in range(0, K, C):
+            c = min(C, K - i0)
+            if G == 1:  # one process: straight into the bags
+                mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, 0, 1,
+                                                    kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
+                                                    x_bag=x_bag, z_bag=z_bag, cursors=cur))
+            else:
+                mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, r, G,
+                                                    kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
+                                                    send=send, cap=cap, flag=flag))
+                sz = G * c * (cap + 1)
+                mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
+                mark("unpack", lambda: ops.chain_unpack(recv, G, c, cap, False, nl, nl, x_bag,
+                                                        z_bag, flag))
+            mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz,
+                                                  False, counts[i0:i0 + c]))
+        if G == 1:
+            mark("final scatter", lambda: ops.chain_scatter(X, xpos, Z, zpos))
+        else:
+            mark("final gather", lambda: ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs,
+                                                          kzs))
+    ms, host = ev_time(call, 5)
+    if parts:
+        t = {k: sum(a.elapsed_time(b) for a, b in v) / 6 for k, v in t.items()}
+    return ms, host, t
+
+
+for K in Ks:
+    ch, ch_host = one_gpu_call(K, True)
+    st, st_host = one_gpu_call(K, False)
+    print(f"K={K}: one GPU, step chains {ch:.3f} ms/call ({ch / K:.4f} ms/step; host "
+          f"{ch_host:.3f}); one launch per step {st:.3f} ms/call ({st / K:.4f} ms/step)",
+          flush=True)
+    for G in (1, 2, 4, 8):
+        ms, host, _ = rank_call(G, 0, K)
+        ms_l, _, parts = rank_call(G, G - 1, K, parts=True)
+        worst = max(ms, ms_l)
+        print(f"  G={G}: rank 0 {ms:.3f} ms/call, rank {G - 1} {ms_l:.3f}; ideal (one-GPU "
+              f"chain call / G) {ch / G:.3f}; efficiency {ch / G / worst:.3f}; parts "
+              + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()), flush=True)

@@ -41,6 +41,19 @@ _SIGNATURES = {
     "tw_gather_records": [_vp, _vp, _i64, _vp, _vp],
     "tw_count_rank_set_plan": [_i32, _i64],
     "tw_count_rank_set_next": [_i32],
+    "tw_rank_set_plan": [_i32, _i32],
+    "tw_rank_images_query": [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp,
+                             _vp],
+    "tw_chain_emit": [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32,
+                      _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
+    "tw_chain_unpack": [_vp, _i32, _i32, _i64, _i32, _i64, _i64, _vp, _vp, _vp, _vp],
+    "tw_count_pairs_chain": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i32, _vp,
+                             _vp],
+    "tw_count_chain_set_plan": [_i32, _i64],
+    "tw_chain_set_emit": [_i32, _i32],
+    "tw_chain_scatter": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
+    "tw_chain_gather": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp,
+                        _vp, _vp],
     "tw_count_pairs_sorted_work_bytes": [_i32, _i64],
     "tw_count_sorted_set_chunk": [_i64],
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],

@@ -40,7 +40,7 @@ __host__ __device__ inline uint32_t mix32(uint32_t v) {  // murmur3 finaliser
   return v;
 }
 
-inline Feistel make_feistel(int64_t n, uint64_t key) {
+__host__ __device__ inline Feistel make_feistel(int64_t n, uint64_t key) {
   Feistel f;
   int bits = 2;
   while (bits < 62 && (1ll << bits) < n) ++bits;
@@ -96,6 +96,40 @@ __host__ __device__ inline uint64_t feistel_perm_inv(const Feistel& f, uint64_t 
   uint64_t v = feistel_once_inv(f, p);
   while (v >= n) v = feistel_once_inv(f, v);
   return v;
+}
+
+// The same rounds on 32-bit words, for domains of at most 2^32 (half_bits <= 16): the step
+// chains (csrc/chain.hip) keep positions in u32 and evaluate these per element and step.
+__device__ __forceinline__ uint32_t feistel_once32(const Feistel& f, uint32_t v) {
+  uint32_t L = (v >> f.half_bits) & f.mask;
+  uint32_t R = v & f.mask;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const uint32_t nL = R;
+    R = (L ^ mix32(R * 0x9E3779B1u + f.k[i])) & f.mask;
+    L = nL;
+  }
+  return (L << f.half_bits) | R;
+}
+__device__ __forceinline__ uint32_t feistel_once_inv32(const Feistel& f, uint32_t v) {
+  uint32_t L = (v >> f.half_bits) & f.mask;
+  uint32_t R = v & f.mask;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    const uint32_t pR = L;
+    L = (R ^ mix32(pR * 0x9E3779B1u + f.k[i])) & f.mask;
+    R = pR;
+  }
+  return (L << f.half_bits) | R;
+}
+
+// v / d for v < 2^32, d < 2^32: one f64 multiply by the reciprocal (within one of the quotient)
+// and one exact correction each way
+__device__ __forceinline__ uint32_t fast_div32(uint32_t v, const FastDiv& f) {
+  uint32_t q = (uint32_t)((double)v * f.inv);
+  if ((uint64_t)q * f.d > v) --q;
+  else if ((uint64_t)(q + 1) * f.d <= v) ++q;
+  return q;
 }
 
 }  // namespace tw

@@ -38,16 +38,14 @@
 // for every element); per bucket the z keys are sorted in LDS and every element's g is the z
 // count of the lower buckets plus a binary search in its own.  See tw_rank_images below.
 #include "nextstep.h"
+#include "pkcount.h"
 #include "sortkeys.h"
 
 namespace tw {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-constexpr float kImgNever = -33554432.0f;  // -2^25: NaN x and padded lanes, never greater
-
 // ----------------------------------------------------------------------------- images
 // g(v) = #{z : key(z) < key(v)} for all n + m elements, from a structure over Z alone:
-//  1. an evenly spaced sample of Z, sorted in one block: B - 1 splitter keys;
+//  1. a sample of Z at hashed positions, sorted in one block: B - 1 splitter keys;
 //  2. z -> bucket: 2j for the keys strictly between splitters j-1 and j, 2j + 1 for keys EQUAL
 //     to splitter j (heavy ties land there: no z of such a bucket is below any of its values);
 //     per-block histograms, their prefix per bucket, and the z keys scattered bucket by bucket;
@@ -58,17 +56,25 @@ constexpr float kImgNever = -33554432.0f;  // -2^25: NaN x and padded lanes, nev
 //     g = z count below the bucket + below its sub-bucket + a scan of its own sub-bucket (about
 //     one key for smooth data; ties or clusters only lengthen the scan, never change g).
 constexpr int kRkThreads = 256;
-constexpr int kRkPer = 16;                         // elements per thread in the bucket passes
-constexpr int kRkTile = kRkThreads * kRkPer;       // 4096 elements per block
-constexpr int kRkSample = 2048;                    // sampled z keys (one k_sort_chunks block)
+constexpr int kRkSample = 2048;                    // largest sample (one k_sort_chunks block)
+// tuning hooks (tw_rank_set_plan): sample size, z per thread in the bucket passes (1024 / 8:
+// 145 us per 1e6 + 1e6 ranking against 169-172 us for 2048 / 16; profiles/r04_chain_parts.log)
+static int g_rank_cs = 1024;
+static int g_rank_per = 8;
 constexpr int kRkMaxB = 256;                       // splitter intervals (511 buckets max)
 constexpr int kRkSub = 2048;                       // sub-buckets per interval bucket
+
+// position of sample i in [0, m): a hashed, not an index-strided, sample (Z with periodic
+// structure would give an evenly spaced sample of repeated values)
+__device__ __forceinline__ int64_t sample_index(int i, int64_t m) {
+  return (int64_t)(((uint64_t)mix32((uint32_t)i * 0x9E3779B1u + 0x7F4A7C15u) * (uint64_t)m) >> 32);
+}
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_rank_sample(const T* __restrict__ z, int64_t m,
                                                         int cs, T* __restrict__ samp) {
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < cs; i += gridDim.x * kBlock)
-    samp[i] = z[((int64_t)i * m) / cs];  // evenly spaced over Z (i * m < 2^35)
+    samp[i] = z[sample_index(i, m)];
 }
 
 // bucket of a key: 2j for the interval below splitter j (j = #splitters < key), 2j + 1 for a key
@@ -87,9 +93,13 @@ __device__ __forceinline__ int rank_bucket(const uint64_t* sp, int nsp, uint64_t
   return 2 * lo + ((lo < nsp && sp[lo] == k) ? 1 : 0);
 }
 
+// m: the Z of the STRUCTURE (every z counted by g); n / mq: the X / Z elements whose images the
+// record pass writes (the same Z as the structure in one process; a rank's own share of X and Z
+// against the all-gathered Z over several ranks, tw_rank_images_query); tot = n + mq.
+// half: the X record's high word holds h(x) = #{z : key(z) <= key(x)} instead of the index.
 struct RankGeo {
-  int64_t n, m, tot;
-  int B, NB, nblk, cs;
+  int64_t n, m, tot, mq;
+  int B, NB, nblk, cs, half, per, C;  // C: the sorted sample's padded length (power of two)
 };
 
 // splitter j = the sample's ((j + 1) * cs / B)-th key; loaded into LDS by every pass
@@ -102,24 +112,24 @@ __device__ __forceinline__ int load_splitters(const uint64_t* __restrict__ ss, c
   return nsp;
 }
 
-// pass 1: per-block bucket histogram of Z (column blk of rel[b][*])
-template <typename T>
+// pass 1: per-block bucket histogram of Z (column blk of rel[b][*]); PER z per thread
+template <typename T, int PER>
 __global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ z, RankGeo g,
                                                           const uint64_t* __restrict__ ss,
                                                           uint32_t* __restrict__ rel) {
   __shared__ uint64_t sp[kRkMaxB];
   __shared__ uint32_t h[2 * kRkMaxB];
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads) h[b] = 0;
-  const int64_t e0 = (int64_t)blockIdx.x * kRkTile + threadIdx.x;
-  T zv[kRkPer];  // all of the thread's loads in flight at once (a block per 4096 z: few waves)
+  const int64_t e0 = (int64_t)blockIdx.x * kRkThreads * PER + threadIdx.x;
+  T zv[PER];  // all of the thread's loads in flight at once (few waves per CU)
 #pragma unroll
-  for (int k = 0; k < kRkPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const int64_t e = e0 + k * kRkThreads;
     zv[k] = e < g.m ? z[e] : (T)0;
   }
   const int nsp = load_splitters(ss, g, sp);
 #pragma unroll
-  for (int k = 0; k < kRkPer; ++k)
+  for (int k = 0; k < PER; ++k)
     if (e0 + k * kRkThreads < g.m) atomicAdd(&h[rank_bucket(sp, nsp, order_key<T>(zv[k]))], 1u);
   __syncthreads();
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
@@ -166,7 +176,7 @@ __global__ __launch_bounds__(1024) void k_rank_starts(RankGeo g, const uint32_t*
 }
 
 // pass 3: the z keys into their buckets' slots (order inside a bucket is free)
-template <typename T>
+template <typename T, int PER>
 __global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict__ z, RankGeo g,
                                                              const uint64_t* __restrict__ ss,
                                                              const uint32_t* __restrict__ rel,
@@ -176,16 +186,16 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict
   __shared__ uint32_t cur[2 * kRkMaxB];
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
     cur[b] = start[b] + rel[(int64_t)b * g.nblk + blockIdx.x];
-  const int64_t e0 = (int64_t)blockIdx.x * kRkTile + threadIdx.x;
-  T zv[kRkPer];
+  const int64_t e0 = (int64_t)blockIdx.x * kRkThreads * PER + threadIdx.x;
+  T zv[PER];
 #pragma unroll
-  for (int k = 0; k < kRkPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const int64_t e = e0 + k * kRkThreads;
     zv[k] = e < g.m ? z[e] : (T)0;
   }
   const int nsp = load_splitters(ss, g, sp);
 #pragma unroll
-  for (int k = 0; k < kRkPer; ++k) {
+  for (int k = 0; k < PER; ++k) {
     if (e0 + k * kRkThreads < g.m) {
       const uint64_t key = order_key<T>(zv[k]);
       bkeys[atomicAdd(&cur[rank_bucket(sp, nsp, key)], 1u)] = key;
@@ -385,21 +395,33 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_records(
   const int b = rank_bucket(sp, nsp, key);
   uint32_t gv = start[b];  // every z of the lower buckets is below key
   const uint32_t tb = total[b];
+  uint32_t hv = gv + tb;   // h(v) for an equality bucket: every z of it equals v
   // issued with start / total (in bounds for every bucket; used for interval buckets only), so
   // the chain is splitters -> {start, total, map} -> sub-bucket prefix -> keys
   const SubMap f = maps[b >> 1];
-  if ((b & 1) == 0 && tb != 0) {  // interval bucket: sub-buckets below + a scan
-    const uint32_t sb = f((double)v, key);
-    const uint32_t* pt = subp + (int64_t)(b >> 1) * (kRkSub + 1);
-    const uint32_t lo = pt[sb], hi = pt[sb + 1];
-    const uint64_t* q = skeys + gv;
-    uint32_t below = lo;
-    for (uint32_t i = lo; i < hi; ++i) below += q[i] < key ? 1u : 0u;
-    gv += below;
+  if ((b & 1) == 0) {  // interval bucket: sub-buckets below + a scan (equal keys share one)
+    hv = gv;
+    if (tb != 0) {
+      const uint32_t sb = f((double)v, key);
+      const uint32_t* pt = subp + (int64_t)(b >> 1) * (kRkSub + 1);
+      const uint32_t lo = pt[sb], hi = pt[sb + 1];
+      const uint64_t* q = skeys + gv;
+      uint32_t below = lo, eq = 0;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint64_t k = q[i];
+        below += k < key ? 1u : 0u;
+        eq += k == key ? 1u : 0u;
+      }
+      gv += below;
+      hv = gv + eq;
+    }
   }
   if (isx) {
-    const float img = (std::is_floating_point<T>::value && key == ~0ull) ? kImgNever : (float)gv;
-    x_rec[e] = (uint64_t)__float_as_uint(img) | ((uint64_t)e << 32);
+    const bool nan = std::is_floating_point<T>::value && key == ~0ull;
+    const float img = nan ? kImgNever : (float)gv;
+    const uint64_t hi = g.half ? (uint64_t)__float_as_uint(nan ? kImgNever : (float)hv)
+                               : (uint64_t)e;
+    x_rec[e] = (uint64_t)__float_as_uint(img) | (hi << 32);
   } else {
     const int64_t j = e - g.n;
     z_rec[j] = (uint64_t)__float_as_uint(-(float)gv) | ((uint64_t)j << 32);
@@ -416,17 +438,22 @@ struct RankWork {
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-static RankGeo rank_geo(int64_t n, int64_t m) {
+static RankGeo rank_geo(int64_t n, int64_t m, int64_t mq = -1, int half = 0) {
   RankGeo g{};
   g.n = n;
   g.m = m;
-  g.tot = n + m;
+  g.mq = mq < 0 ? m : mq;
+  g.tot = n + g.mq;
+  g.half = half;
   int B = 1;
   while (B < kRkMaxB && (int64_t)B * 2048 < m) B <<= 1;  // >= ~2048 z per interval
   g.B = B;
   g.NB = 2 * B;
-  g.nblk = (int)std::max<int64_t>(1, ceil_div(m, kRkTile));
-  g.cs = (int)std::min<int64_t>(m, kRkSample);
+  g.per = g_rank_per;
+  g.nblk = (int)std::max<int64_t>(1, ceil_div(m, (int64_t)kRkThreads * g.per));
+  g.cs = (int)std::min<int64_t>(m, g_rank_cs);
+  g.C = 1024;
+  while (g.C < g.cs) g.C <<= 1;
   return g;
 }
 
@@ -457,17 +484,7 @@ static bool rank_sizes_ok(int64_t n, int64_t m) {
 }
 
 // ----------------------------------------------------------------------------- the count
-// nz2: an SGPR pair holding one z record; both packed halves take its LOW word (the negated
-// image): t = clamp(x_lo + nz, x_hi + nz).
-__device__ __forceinline__ f2 gt_clamp(f2 x, uint64_t nz2) {
-  f2 t;
-  asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] clamp" : "=v"(t) : "v"(x), "s"(nz2));
-  return t;
-}
-__device__ __forceinline__ void acc_add(f2& a, f2 t) {
-  asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a) : "v"(t));
-}
-
+// (gt_clamp / acc_add: pkcount.h; a z record's LOW word is its negated image)
 __device__ __forceinline__ float rec_image(uint64_t r) { return __uint_as_float((uint32_t)r); }
 
 // One wave item: 64*R x-images (R per lane as R/2 packed pairs) against z records [z0, z1).
@@ -659,21 +676,31 @@ extern "C" int64_t tw_rank_images_work_bytes(int64_t n_x, int64_t n_z) {
 }
 
 namespace tw {
+// z / m: the structure's Z; xq / zq: the elements imaged (g.n and g.mq of them)
 template <typename T>
-static int rank_images_t(const T* x, int64_t n, const T* z, int64_t m, const RankWork& w,
+static int rank_images_t(const T* xq, const T* zq, const T* z, int64_t m, const RankWork& w,
                          const RankGeo& g, uint64_t* x_rec, uint64_t* z_rec, hipStream_t st) {
-  if (m > 0) {  // the sample: evenly spaced z, sorted (k_sort_chunks pads with ~0 past cs)
+  if (m > 0) {  // the sample: hashed positions of z, sorted (k_sort_chunks pads with ~0 past cs)
     hipLaunchKernelGGL((k_rank_sample<T>), dim3(8), dim3(kBlock), 0, st, z, m, g.cs, (T*)w.samp);
-    hipLaunchKernelGGL((k_sort_chunks<T, 4>), dim3(1), dim3(kRkSample / 4), kRkSample * 8, st,
-                       (const T*)w.samp, nullptr, 1, kRkSample, w.ss, (int64_t)g.cs);
+    hipLaunchKernelGGL((k_sort_chunks<T, 4>), dim3(1), dim3(g.C / 4), g.C * 8, st,
+                       (const T*)w.samp, nullptr, 1, g.C, w.ss, (int64_t)g.cs);
     TW_LAUNCH_CHECK();
-    hipLaunchKernelGGL((k_rank_hist<T>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g, w.ss,
-                       w.rel);
-    hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
-                       dim3(kBlock), 0, st, g, w.rel, w.total);
-    hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
-    hipLaunchKernelGGL((k_rank_scatter<T>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g, w.ss,
-                       w.rel, w.start, w.bkeys);
+    auto passes = [&](auto per) {
+      constexpr int PER = decltype(per)::value;
+      hipLaunchKernelGGL((k_rank_hist<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
+                         w.ss, w.rel);
+      hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
+                         dim3(kBlock), 0, st, g, w.rel, w.total);
+      hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
+      hipLaunchKernelGGL((k_rank_scatter<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
+                         w.ss, w.rel, w.start, w.bkeys);
+    };
+    if (g.per == 4)
+      passes(std::integral_constant<int, 4>());
+    else if (g.per == 8)
+      passes(std::integral_constant<int, 8>());
+    else
+      passes(std::integral_constant<int, 16>());
     hipLaunchKernelGGL((k_rank_subsort<T>), dim3(g.B), dim3(kSubThreads), 0, st, g, w.start,
                        w.total, w.bkeys, w.skeys, w.subp, w.maps);
     TW_LAUNCH_CHECK();
@@ -684,11 +711,28 @@ static int rank_images_t(const T* x, int64_t n, const T* z, int64_t m, const Ran
   }
   // (one element per thread: 128 .. 1024 threads per block and four elements per thread
   // measured the same or slower, profiles/r03s53_time_ranking.log)
+  if (g.tot == 0) return TW_OK;
   hipLaunchKernelGGL((k_rank_records<T>), dim3((unsigned)ceil_div(g.tot, kRkThreads)),
-                     dim3(kRkThreads), 0, st, x, z, g, w.ss, w.start, w.total, w.skeys, w.subp,
+                     dim3(kRkThreads), 0, st, xq, zq, g, w.ss, w.start, w.total, w.skeys, w.subp,
                      w.maps, x_rec, z_rec);
   TW_LAUNCH_CHECK();
   return TW_OK;
+}
+
+static int rank_images_any(const void* d_zs, int64_t m, const void* d_xq, int64_t nq_x,
+                           const void* d_zq, int64_t nq_z, int32_t dtype, int32_t half,
+                           void* d_work, int64_t work_bytes, uint64_t* d_x_rec,
+                           uint64_t* d_z_rec, hipStream_t st) {
+  const RankGeo g = rank_geo(nq_x, m, nq_z, half);
+  const RankWork w = rank_work(g, (char*)d_work);
+  TW_ARG_CHECK(d_work != nullptr && work_bytes >= (int64_t)w.total_bytes,
+               "tw_rank_images: work buffer of %lld bytes, %lld needed", (long long)work_bytes,
+               (long long)w.total_bytes);
+  if (dtype == TW_F64)
+    return rank_images_t<double>((const double*)d_xq, (const double*)d_zq, (const double*)d_zs,
+                                 m, w, g, d_x_rec, d_z_rec, st);
+  return rank_images_t<long long>((const long long*)d_xq, (const long long*)d_zq,
+                                  (const long long*)d_zs, m, w, g, d_x_rec, d_z_rec, st);
 }
 }  // namespace tw
 
@@ -699,18 +743,33 @@ extern "C" int tw_rank_images(const void* d_x, int64_t n_x, const void* d_z, int
                "tw_rank_images: needs n_z < 2^24 and n_x + n_z < 2^31 (got %lld, %lld)",
                (long long)n_x, (long long)n_z);
   TW_ARG_CHECK(dtype == TW_F64 || dtype == TW_I64, "tw_rank_images: unknown dtype %d", dtype);
-  hipStream_t st = (hipStream_t)stream;
   if (n_x + n_z == 0) return TW_OK;
-  const RankGeo g = rank_geo(n_x, n_z);
-  const RankWork w = rank_work(g, (char*)d_work);
-  TW_ARG_CHECK(d_work != nullptr && work_bytes >= (int64_t)w.total_bytes,
-               "tw_rank_images: work buffer of %lld bytes, %lld needed", (long long)work_bytes,
-               (long long)w.total_bytes);
-  if (dtype == TW_F64)
-    return rank_images_t<double>((const double*)d_x, n_x, (const double*)d_z, n_z, w, g, d_x_rec,
-                                 d_z_rec, st);
-  return rank_images_t<long long>((const long long*)d_x, n_x, (const long long*)d_z, n_z, w, g,
-                                  d_x_rec, d_z_rec, st);
+  return rank_images_any(d_z, n_z, d_x, n_x, d_z, n_z, dtype, 0, d_work, work_bytes, d_x_rec,
+                         d_z_rec, (hipStream_t)stream);
+}
+
+extern "C" int tw_rank_images_query(const void* d_z_all, int64_t n_z_all, const void* d_x,
+                                    int64_t n_x, const void* d_z, int64_t n_z, int32_t dtype,
+                                    int32_t half, void* d_work, int64_t work_bytes,
+                                    uint64_t* d_x_rec, uint64_t* d_z_rec, void* stream) {
+  TW_ARG_CHECK(rank_sizes_ok(n_x, n_z_all) && n_z >= 0 && n_x + n_z < (1ll << 31),
+               "tw_rank_images_query: needs n_z_all < 2^24 and n_x + n_z < 2^31 (got %lld, "
+               "%lld, %lld)", (long long)n_z_all, (long long)n_x, (long long)n_z);
+  TW_ARG_CHECK(dtype == TW_F64 || dtype == TW_I64, "tw_rank_images_query: unknown dtype %d",
+               dtype);
+  TW_ARG_CHECK(half == 0 || half == 1, "tw_rank_images_query: half in {0, 1}");
+  if (n_x + n_z == 0) return TW_OK;
+  return rank_images_any(d_z_all, n_z_all, d_x, n_x, d_z, n_z, dtype, half, d_work, work_bytes,
+                         d_x_rec, d_z_rec, (hipStream_t)stream);
+}
+
+extern "C" int tw_rank_set_plan(int32_t sample, int32_t per) {
+  TW_ARG_CHECK(sample == 512 || sample == 1024 || sample == 2048,
+               "tw_rank_set_plan: sample of 512, 1024 or 2048 keys");
+  TW_ARG_CHECK(per == 4 || per == 8 || per == 16, "tw_rank_set_plan: 4, 8 or 16 z per thread");
+  g_rank_cs = sample;
+  g_rank_per = per;
+  return TW_OK;
 }
 
 extern "C" int tw_count_rank_set_next(int32_t front) {

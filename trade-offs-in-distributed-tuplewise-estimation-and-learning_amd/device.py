@@ -13,9 +13,10 @@ every element is sent to the rank owning its new position with a single all-to-a
 {value, position} records, and the receiver scatters them into place.  The resulting global
 array — hence every shard's integer count and the final np.mean — is identical for any G.
 Per-shard counts are combined with one all-reduce (sum of a zero-padded int64 vector; exact).
-UnN_many on rank images (est.UnNT's loop, the bench's strong-scaling problem) needs no
-exchange at all while the whole sample is small: every rank all-gathers it once per call,
-keeps all the records and applies each global permutation itself, counting only its shards.
+UnN_many on rank images (est.UnNT's loop, the bench's problem) walks the call's repartitions as
+per-element chains of positions (csrc/chain.hip): each rank walks only its own elements, one
+equal-split all-to-all per chunk of <= 32 steps moves {image, position} records to the ranks
+that hold those positions, and all steps of a chunk are counted in one launch.
 """
 from __future__ import annotations
 
@@ -27,14 +28,12 @@ from . import _lib as L
 # UnN_many's all-pairs steps on rank images (csrc/rankimage.hip; A/B switch: False keeps the
 # double-compare kernel of csrc/count.hip)
 RANK_IMAGES = True
-# UnN_many on rank images over several ranks: every rank keeps the WHOLE sample's records (16 MB
-# at 1e6 + 1e6) and applies each global repartition itself, counting only its own shards — no
-# collective per step (False: the fixed-capacity all-to-all of _repartition_multi per step).
-# Taken up to REPLICATED_MAX_RECORDS records in all: every rank permutes all of them each step
-# (~25 us per 2e6 on one MI355X, mostly hidden beside the count; tools/replicated_probe.py), so
-# the weak-scaling form (1e6/class PER rank: 2e6*G records) keeps the exchange from G = 4 on.
-REPLICATED_RANK_STEPS = True
-REPLICATED_MAX_RECORDS = 1 << 22
+# UnN_many on rank images as step chains (csrc/chain.hip: every element walks the call's
+# repartitions once, the steps' (step, shard) bags are counted in one launch per chunk of
+# CHAIN_MAX steps; over ranks one all-to-all per chunk).  False: one launch per step that counts
+# and permutes the records for the next step (csrc/rankimage.hip), the A/B baseline.
+CHAIN_STEPS = True
+CHAIN_MAX = 32
 
 
 def prop_swor_layout(n_X: int, n_Z: int, N: int):
@@ -178,6 +177,65 @@ class HipOps:
         L.call("tw_gather_records", L.ptr(vals), L.ptr(rec), int(rec.numel()), L.ptr(out),
                L.stream_handle())
         return out
+
+    def rank_images_query(self, Z_all, X, Z, dtype, half=False):
+        """Rank-image records of this rank's X and Z counted against the Z of Z_all
+        (tw_rank_images_query); half: the X records' high word is h(x) = #{z <= x}.  None where
+        the path does not apply (|Z_all| >= 2^24)."""
+        n, m, ma = int(X.numel()), int(Z.numel()), int(Z_all.numel())
+        wb = int(L.lib().tw_rank_images_work_bytes(n, ma))
+        if wb < 0 or n + m >= (1 << 31):
+            return None
+        dev = X.device
+        work = self.t.empty((max(wb, 1),), dtype=self.t.uint8, device=dev)
+        xr = self.t.empty((n,), dtype=self.t.int64, device=dev)
+        zr = self.t.empty((m,), dtype=self.t.int64, device=dev)
+        L.call("tw_rank_images_query", L.ptr(Z_all), ma, L.ptr(X), n, L.ptr(Z), m, int(dtype),
+               int(bool(half)), L.ptr(work), wb, L.ptr(xr), L.ptr(zr), L.stream_handle())
+        return xr, zr
+
+    def chain_emit(self, xr, zr, half, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
+                   n_shards, x_bag=None, z_bag=None, cursors=None, send=None, cap=0, flag=None):
+        """Walk len(keys_x) repartitions for this rank's elements (tw_chain_emit): into the
+        step bags (one process) or the send buckets (several ranks)."""
+        kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
+        kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
+        L.call("tw_chain_emit", L.ptr(xr), int(xr.numel()), L.ptr(zr), int(zr.numel()),
+               int(bool(half)), L.ptr(xpos), L.ptr(zpos), int(bool(first)), int(rank),
+               int(world), kxa.ctypes.data, kza.ctypes.data, len(kxa), int(kx), int(kz),
+               int(n_shards), L.ptr(x_bag), L.ptr(z_bag), L.ptr(cursors), L.ptr(send),
+               int(cap), L.ptr(flag), L.stream_handle())
+
+    def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag):
+        L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
+               int(bool(half)), int(n), int(m), L.ptr(x_bag), L.ptr(z_bag), L.ptr(flag),
+               L.stream_handle())
+
+    def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
+                    z_stride, max_nx, max_nz, half, out):
+        """Counts of steps x n_shards bags in one launch into out (steps, n_shards)."""
+        L.call("tw_count_pairs_chain", L.ptr(x_bag), L.ptr(x_off_dev), int(x_stride),
+               L.ptr(z_bag), L.ptr(z_off_dev), int(z_stride), int(n_shards), int(steps),
+               int(max_nx), int(max_nz), int(bool(half)), L.ptr(out), L.stream_handle())
+        return out
+
+    def chain_scatter(self, X, xpos, Z, zpos):
+        Xo, Zo = self.t.empty_like(X), self.t.empty_like(Z)
+        L.call("tw_chain_scatter", L.ptr(X), L.ptr(xpos), int(X.numel()), L.ptr(Z),
+               L.ptr(zpos), int(Z.numel()), L.ptr(Xo), L.ptr(Zo), L.stream_handle())
+        return Xo, Zo
+
+    def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z):
+        kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
+        kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
+        dev = X_all.device
+        Xo = self.t.empty((n,), dtype=X_all.dtype, device=dev)
+        Zo = self.t.empty((m,), dtype=Z_all.dtype, device=dev)
+        work = self.t.empty((max(1, n + m),), dtype=self.t.int32, device=dev)
+        L.call("tw_chain_gather", L.ptr(X_all), L.ptr(Z_all), int(x_base), int(n),
+               int(X_all.numel()), int(z_base), int(m), int(Z_all.numel()), kxa.ctypes.data,
+               kza.ctypes.data, len(kxa), L.ptr(work), L.ptr(Xo), L.ptr(Zo), L.stream_handle())
+        return Xo, Zo
 
     def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred,
                   max_nx=None, max_nz=None):
@@ -373,6 +431,9 @@ class ShardedSample:
         if self._xf is not None and int(self._xf["flag"].item()):
             raise RuntimeError("repartition: an exchange bucket overflowed its capacity; the "
                                "arrays are invalid (use ShardedSample(..., exchange='exact'))")
+        if getattr(self, "_chain_flag", None) is not None and int(self._chain_flag.item()):
+            raise RuntimeError("UnN_many: a step-chain bucket overflowed its capacity; the "
+                               "counts and arrays are invalid")
 
     def _exchange_records(self, send, c):
         """All-to-all of the packed records (split sizes from the (4, G) host counts) and the
@@ -393,8 +454,6 @@ class ShardedSample:
     def _multi(self) -> bool:
         """The exchange path (always with G > 1; at G = 1 only when _force_multi is set, a
         probe hook for timing the multi-rank orchestration on one GPU)."""
-        if getattr(self, "_replicated", False):  # _unn_many_rank's replicated steps
-            return False
         return self.G > 1 or getattr(self, "_force_multi", False)
 
     def repartition(self, key: int, check: bool = True):
@@ -538,11 +597,12 @@ class ShardedSample:
         keys = list(keys)
         if not keys:
             return []
-        if not self.X.is_cuda and not (self.algo == "pairs" and self._rank_path_ok()
-                                       and (self.G == 1 or self._replicated_ok())):
+        if not self.X.is_cuda and not (self.algo == "pairs" and self._chain_ok()):
             # host tensors (CPU rehearsal of the orchestration): the stream-pipelined paths
-            # need a device; the rank-image chain (no side stream) runs as it is
+            # need a device; the step chains (no side stream) run as they are
             return [self.UnN(k) for k in keys]
+        if self.algo == "pairs" and self._chain_ok():
+            return self._unn_many_chain(keys)
         if (self.algo == "sorted" and not self._multi() and self.N > 0
                 and hasattr(self.ops, "count_sorted_steps")):
             # the whole sequence in one call: records between steps (csrc/records.h)
@@ -586,23 +646,32 @@ class ShardedSample:
                      or (self.pred == L.TW_PRED_SUBGT and self.dtype == L.TW_F64))
                 and G * self.m_loc < (1 << 24) and G * (self.n_loc + self.m_loc) < (1 << 31))
 
+    def _chain_ok(self) -> bool:
+        """The step chains (csrc/chain.hip) take the rank-image predicates and half ties, with
+        positions in 32 bits and at most 8191 shards per rank (the emission's LDS buckets)."""
+        G = self.G
+        return (CHAIN_STEPS and RANK_IMAGES and self.N > 0 and self.max_nx > 0
+                and self.max_nz > 0 and hasattr(self.ops, "chain_emit")
+                and (self.pred in (L.TW_PRED_GT, L.TW_PRED_HALF)
+                     or (self.pred == L.TW_PRED_SUBGT and self.dtype == L.TW_F64))
+                and G * self.m_loc < (1 << 24) and G * (self.n_loc + self.m_loc) < (1 << 31)
+                and self.N < 8191 and G <= 512)
+
     def _unn_many_rank(self, keys):
-        """UnN_many on rank images: ONE ranking of X u Z per call (the multiset of scores is
-        the same at every step), then one launch per step that counts the current partition on
-        packed f32 images and permutes the 8-B records {image, index} for the next step (the
-        same keyed permutations as the score path); the scores are gathered into the final
-        order once at the end.  Same counts, same arrays as the score path."""
+        """UnN_many on rank images, one launch per step (the A/B baseline of the step chains):
+        ONE ranking of X u Z per call (the multiset of scores is the same at every step), then
+        one launch per step that counts the current partition on packed f32 images and permutes
+        the 8-B records {image, index} for the next step (the same keyed permutations as the
+        score path); the scores are gathered into the final order once at the end.  Same counts,
+        same arrays as the score path."""
         if self.G > 1:
             # several ranks: every rank ranks the WHOLE sample (one all-gather of both samples
-            # per call); its records' high words are then global indices
+            # per call), keeps its own elements' records (high words: global indices) and the
+            # exchanges move 8-B records as they moved scores
             X0, Z0 = self._all_gather(self.X), self._all_gather(self.Z)
             r = self.ops.rank_images(X0, Z0, self.dtype)
             if r is None:
                 return None
-            if self._replicated_ok():
-                return self._unn_many_replicated(keys, X0, Z0, r)
-            # ... keeps its own elements' records and the exchanges move 8-B records as they
-            # moved scores
             a, b = self.rank * self.n_loc, self.rank * self.m_loc
             self.X, self.Z = r[0][a:a + self.n_loc].clone(), r[1][b:b + self.m_loc].clone()
         else:
@@ -627,38 +696,79 @@ class ShardedSample:
             self.Z = self.ops.gather_records(Z0, zr)
         return [np.mean(v) for v in self.values(counts)]
 
-    def _replicated_ok(self) -> bool:
-        return (REPLICATED_RANK_STEPS
-                and self.G * (self.n_loc + self.m_loc) <= REPLICATED_MAX_RECORDS)
-
-    def _unn_many_replicated(self, keys, X0, Z0, rec):
-        """UnN_many on rank images over G ranks with NO collective per step: every rank holds
-        the whole sample's records (rec, from the all-gathered X0 / Z0) and runs the one-GPU
-        step chain on them — each launch counts this rank's N shards of the global layout
-        (global positions r*n_loc + x_off, r*m_loc + z_off) and applies the next GLOBAL keyed
-        repartition to all records, the same permutation chain every rank evaluates and the
-        exchange path distributes.  The counts meet in _run_steps' one all-reduce per call;
-        the rank's final arrays are its slices of the permuted global arrays, gathered back
-        into scores.  Same counts and arrays as the exchange path (and as one GPU)."""
-        r, n, m = self.rank, self.n_loc, self.m_loc
-        offs = (self.x_off_dev, self.z_off_dev)
-        self.x_off_dev = self.ops.to_dev(self.x_off + r * n)
-        self.z_off_dev = self.ops.to_dev(self.z_off + r * m)
-        self.X, self.Z = rec
-
-        def step(i, out, Xn, kx, Zn, kz, out_n):
-            self.ops.count_rank_step(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
-                                     self.max_nx, self.max_nz, out, Xn, kx, Zn, kz, out_n)
-        self._replicated = True  # _multi() is False: the one-GPU chain of _run_steps
-        try:
-            counts = self._run_steps(keys, None, True, step)
-        finally:
-            self._replicated = False
-            self.x_off_dev, self.z_off_dev = offs
-            xr, zr = self.X[r * n:(r + 1) * n], self.Z[r * m:(r + 1) * m]
-            self.X = self.ops.gather_records(X0, xr)
-            self.Z = self.ops.gather_records(Z0, zr)
+    def _unn_many_chain(self, keys):
+        """UnN_many as step chains (csrc/chain.hip; est.UnNT's loop, estimation-experiment/
+        main.py:76-79).  One ranking per call: over ranks the Z structure of the all-gathered Z,
+        images written for this rank's own elements only.  Then per chunk of <= CHAIN_MAX steps
+        every own element walks the chunk's repartitions (one forward Feistel per step) and its
+        image lands in the (step, shard) bag holding its position — directly in one process,
+        through ONE equal-split all-to-all of {image, position} records over ranks — and one
+        launch counts all bags of the chunk.  The final arrays: a scatter by the chains' last
+        positions (one process) or the inverse chains of the rank's own positions gathered from
+        the all-gathered sample.  Same permutation chain, counts and final arrays as the
+        one-launch-per-step paths, at any G."""
+        t, ops, G, r = self.t, self.ops, self.G, self.rank
+        n, m, N = self.n_loc, self.m_loc, self.N
+        dev = self.X.device
+        half = self.pred == L.TW_PRED_HALF
+        if G > 1:
+            X0, Z0 = self._all_gather(self.X), self._all_gather(self.Z)
+        else:
+            X0, Z0 = self.X, self.Z
+        rec = ops.rank_images_query(Z0, self.X, self.Z, self.dtype, half)
+        if rec is None:
+            return [self.UnN(k) for k in keys]
+        xr, zr = rec
+        T = len(keys)
+        C = min(T, CHAIN_MAX)
+        kx = int(n / N)
+        kz = int((n + m) / N) - kx  # prop_swor_layout's shard sizes
+        M64 = 2 ** 64 - 1
+        kxs = [(2 * k) & M64 for k in keys]
+        kzs = [(2 * k + 1) & M64 for k in keys]
+        x_bag = t.empty((C, n), dtype=t.int64 if half else t.float32, device=dev)
+        z_bag = t.empty((C, m), dtype=t.float32, device=dev)
+        xpos = t.empty((n,), dtype=t.int32, device=dev)
+        zpos = t.empty((m,), dtype=t.int32, device=dev)
+        counts = t.empty((T, N), dtype=t.int64, device=dev)
+        if G > 1:
+            tot = n + m
+            cap = max(1, tot // G + tot // (8 * G) + 1024)
+            W = 2 if half else 1
+            send = t.empty((G * C * (cap + 1) * W,), dtype=t.int64, device=dev)
+            recv = t.empty_like(send)
+            if getattr(self, "_chain_flag", None) is None:
+                self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
+        else:
+            cursors = t.empty((C * 2 * (N + 1),), dtype=t.int32, device=dev)
+        for i0 in range(0, T, C):
+            c = min(C, T - i0)
+            if G > 1:
+                ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, r, G, kxs[i0:i0 + c],
+                               kzs[i0:i0 + c], kx, kz, N, send=send, cap=cap,
+                               flag=self._chain_flag)
+                sz = G * c * (cap + 1) * W
+                self._all_to_all(recv[:sz], send[:sz])
+                ops.chain_unpack(recv, G, c, cap, half, n, m, x_bag, z_bag, self._chain_flag)
+            else:
+                ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
+                               kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
+                               cursors=cursors)
+            ops.count_chain(x_bag, self.x_off_dev, z_bag, self.z_off_dev, N, c, n, m,
+                            self.max_nx, self.max_nz, half, counts[i0:i0 + c])
+        if G > 1:
+            self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
+            full = t.zeros((T, G * N), dtype=t.int64, device=dev)
+            full[:, r * N:(r + 1) * N] = counts
+            self.dist.all_reduce(full, group=self.group)
+            counts = full
+        else:
+            self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
         return [np.mean(v) for v in self.values(counts)]
+
+    def _all_to_all(self, out, inp):
+        """Equal-split all-to-all of one flat tensor (RCCL all_to_all_single; gloo on CPU)."""
+        self.dist.all_to_all_single(out, inp, group=self.group)
 
     def _all_gather(self, A):
         """The G ranks' local arrays concatenated in rank order (one collective)."""
