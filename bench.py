@@ -400,7 +400,7 @@ def sgd_data(n_X, n_Z, d):
 
 
 def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="replicated",
-                    group=None, span=None, data=None, check_prefix=0):
+                    group=None, span=None, data=None, check_prefix=0, loss="hinge"):
     """Pairwise-hinge SGD steps/s (BASELINE metric, second half): learning_process's loop
     (make_exps.py:122-141) without evaluation, device-RNG mode, hipGraph-replayed segments.
     Synthetic data of the given shape generated on the device.  layout="partitioned" also
@@ -412,7 +412,7 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
     from tuplewise.learning import SGDEngine
     X, Z, w0 = data if data is not None else sgd_data(n_X, n_Z, d)
     eng = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
-                    optim_type="momentum", x_layout=layout, group=group)
+                    optim_type="momentum", x_layout=layout, group=group, loss=loss)
     eng.enable_device_rng(12345)
 
     import tuplewise.learning as lr
@@ -454,13 +454,13 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
         # the trajectory does not depend on G: a fresh engine over the ranks and a one-rank
         # engine on rank 0, same seed, the same first steps, w compared bit for bit
         e_g = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
-                        optim_type="momentum", x_layout=layout, group=group)
+                        optim_type="momentum", x_layout=layout, group=group, loss=loss)
         e_g.enable_device_rng(777)
         run(e_g, check_prefix)
         w_g = e_g.w_host()
         if torch.distributed.get_rank(group) == 0:
             e_1 = SGDEngine(X, Z, w0, N, B, margin=1, reg=0.05, learning_rate=0.01,
-                            optim_type="momentum")
+                            optim_type="momentum", loss=loss)
             e_1.enable_device_rng(777)
             run(e_1, check_prefix)
             same_1rank = bool(np.array_equal(w_g, e_1.w_host()))
@@ -475,7 +475,7 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
     out = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
            "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
            "gather_GBps": N * B * 16 * d * steps / dt / 1e9,
-           "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B,
+           "config": {"n_X": n_X, "n_Z": n_Z, "d": d, "N": N, "B": B, "loss": loss,
                       "reshuffle_mod": reshuffle_mod, "optim": "momentum",
                       "rng": "device (Philox)", "graphs": True, "steps": steps,
                       "x_layout": layout, "launches": launches, "ranks": G}}
@@ -890,6 +890,34 @@ def tradeoff_curve(args, group, span, with_cpu):
     return out
 
 
+def half_ties_line(args, group, span, torch, X, Z, shards, pairs_per_step_rank, world):
+    """The north star's "+0.5 on ties" mode (tie_mode="half": 2 #{x > z} + #{x == z} half
+    units) on the headline's UnN steps: step chains whose x images are {g(x), h(x)} pairs, one
+    clamped packed add giving [x > z] and [x >= z] for a z — 2 lane-ops of the contract per
+    pair."""
+    from tuplewise.device import ShardedSample
+    S = ShardedSample(X.clone(), Z.clone(), shards, group=group, tie_mode="half", algo="pairs")
+    pool = EventPool(torch, 64)
+    S.ops.count_chain = pool.wrap(S.ops.count_chain, weight=lambda *a, **kw: a[5])
+    S.UnN_many(range(90_000, 90_000 + args.steps))
+    S.UnN_many(range(args.warmup))
+    pool.clear()
+    dt, ests = span(lambda: S.UnN_many(range(args.warmup, args.warmup + args.steps)))
+    kms = pool.ms_per_unit()
+    lane_ops = 2 * pairs_per_step_rank
+    return {"note": "tie_mode='half' UnN steps (same shape, same keys as the headline): "
+                    "estimates in half units 2#{x>z} + #{x==z} over 2 #pairs; step chains on "
+                    "{g, h} image pairs (csrc/chain.hip); frac counts 2 lane-ops per pair",
+            "value": pairs_per_step_rank * world * args.steps / dt, "unit": "pairs/s",
+            "ms_per_step": dt / args.steps * 1e3, "estimate_last_step": float(ests[-1]),
+            "chain_path": S._chain_ok(),
+            "roofline": {"bound": "valu", "kernel": "k_count_chain<8, half>",
+                         "count_kernel_ms": kms,
+                         "achieved": lane_ops / (kms * 1e-3) / 1e12,
+                         "peak": PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
+                         "frac": lane_ops / (kms * 1e-3) / PEAK_LANE_OPS}}
+
+
 def weak_c3(args, group, rank, world, span, torch):
     """The weak-scaling form of the headline: n = 1e6/class and N = 64 shards PER GPU (the
     per-GPU work of the one-GPU run), K UnN steps over all ranks."""
@@ -1060,6 +1088,10 @@ def main():
             "frac": pairs_per_step_rank / (kms_score * 1e-3) / PEAK_LANE_OPS,
             "same_estimates": bool(ests_score == ests)}
 
+    progress("half ties")
+    half_line = half_ties_line(args, group, span, torch, X_start, Z_start, shards,
+                               pairs_per_step_rank, world)
+
     # same workload, exact sort + binary-search count (csrc/rankcount.hip): logical pairs/s
     same_counts = bool(torch.equal(S.local_counts(), (setattr(S, "algo", "sorted"),
                                                       S.local_counts())[1]))
@@ -1110,33 +1142,51 @@ def main():
     strong = None if args.no_strong else strong_c3(args, group, rank, world, barrier, torch, dist)
 
     # BASELINE.json configs[1] (C2): complete AUC U-statistic, n = 1e5/class, ONE shard (est.Un,
-    # estimation-experiment/main.py:29-31), 1e10 pairs per launch; no repartition
+    # estimation-experiment/main.py:29-31), 1e10 pairs per call; no repartition.  One-shot
+    # counts of this size rank X u Z and count packed f32 images (ShardedSample.local_counts):
+    # the call = the ranking + one count launch, both timed
     n1 = 100_000
     g1 = torch.Generator(device="cuda").manual_seed(7 + rank)
     X1 = torch.randn(n1, dtype=torch.float64, device="cuda", generator=g1) + 0.5
     Z1 = torch.randn(n1, dtype=torch.float64, device="cuda", generator=g1)
     S1 = ShardedSample(X1, Z1, 1, algo="pairs")
-    S1.ops.count = kernel_ms.wrap(S1.ops.count)
+    c2_rank = S1._oneshot_rank_ok()
+    c2_count = EventPool(torch, 64)
+    c2_rankms = EventPool(torch, 64)
+    S1.ops.count = c2_count.wrap(S1.ops.count)
+    S1.ops.count_chain = c2_count.wrap(S1.ops.count_chain)
+    S1.ops.rank_images_query = c2_rankms.wrap(S1.ops.rank_images_query)
     for _ in range(3):
         S1.local_counts()
     torch.cuda.synchronize()
-    kernel_ms.clear()
+    c2_count.clear()
+    c2_rankms.clear()
     reps1 = 20
     t3 = time.perf_counter()
     for _ in range(reps1):
         c1 = S1.local_counts()
     torch.cuda.synchronize()
     dt1 = time.perf_counter() - t3
-    kms1 = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
+    kms1 = float(np.mean([a.elapsed_time(b) for a, b in c2_count.used()]))
+    rms1 = float(np.mean([a.elapsed_time(b) for a, b in c2_rankms.used()] or [0.0]))
     c1 = int(c1.sum())
+    call_ms = dt1 / reps1 * 1e3
     single = {"note": "BASELINE configs[1]: est.Un complete AUC, n=1e5/class, one shard "
-                      "(1e10 pairs per launch), inputs resident, per-rank",
-              "value": n1 * n1 * reps1 / dt1, "unit": "pairs/s", "ms_per_call": dt1 / reps1 * 1e3,
+                      "(1e10 pairs per call), inputs resident, per-rank; "
+                      + ("one-shot count on rank images: the ranking of X u Z "
+                         "(tw_rank_images_query, compact) + one k_count_chain launch, both "
+                         "inside the timed call" if c2_rank else
+                         "the double-compare kernel k_count_complete"),
+              "value": n1 * n1 * reps1 / dt1, "unit": "pairs/s", "ms_per_call": call_ms,
               "count": c1, "estimate": c1 / (n1 * n1),
-              "roofline": {"bound": "valu", "kernel": "k_count_complete",
+              "roofline": {"bound": "valu",
+                           "kernel": "k_count_chain" if c2_rank else "k_count_complete",
                            "achieved": n1 * n1 / (kms1 * 1e-3) / 1e12,
                            "peak": PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
-                           "frac": n1 * n1 / (kms1 * 1e-3) / PEAK_LANE_OPS, "kernel_ms": kms1}}
+                           "frac": n1 * n1 / (kms1 * 1e-3) / PEAK_LANE_OPS, "kernel_ms": kms1,
+                           "ranking_ms": rms1 if c2_rank else None,
+                           "frac_with_ranking": n1 * n1 / ((kms1 + rms1) * 1e-3) / PEAK_LANE_OPS,
+                           "frac_wall": n1 * n1 / (call_ms * 1e-3) / PEAK_LANE_OPS}}
     del S1, X1, Z1
 
     # BASELINE.json configs[0] (C1, plumbing): estimation-experiment/main.py's UnNT on host
@@ -1190,6 +1240,12 @@ def main():
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
                      "count_kernel_ms": kms, "traffic": traffic,
                      "traffic_count_only": traffic_plain,
+                     "traffic_source": ("rocprofv3 --pmc FETCH_SIZE+WRITE_SIZE of this kernel "
+                                        "at the one-GPU shape (profiles/*count_pmc*.json), "
+                                        "not measured at this run's per-rank shape"
+                                        if world > 1 else
+                                        "rocprofv3 --pmc FETCH_SIZE+WRITE_SIZE of this kernel "
+                                        "at this shape (profiles/*count_pmc*.json)"),
                      "ranking_ms_per_call": rank_call_ms if rank_path or chain_path else None,
                      "chain_count_launch_ms": chain_launch_ms if chain_path else None,
                      "chain_emit_ms_per_step": emit_step_ms,
@@ -1212,6 +1268,7 @@ def main():
                                 "the committed rocprofv3 --pmc summary of this kernel: the timed "
                                 "launch, and a launch without the repartition")},
         "score_compare_kernel": score_line,
+        "half_ties": half_line,
         "estimate_last_step": float(est),
         "plumbing_C1": c1,
         "single_shard_C2": single,
@@ -1281,6 +1338,12 @@ def main():
         progress("C4 device RNG")
         sec["C4_shuttle_shape"] = sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2, group=g,
                                                   span=span, check_prefix=chk)
+        # BASELINE configs[3] names pairwise-LOGISTIC SGD: the same loop with loss="logistic"
+        # (the weight sigma(S) per drawn pair instead of the hinge filter)
+        progress("C4 logistic")
+        sec["C4_shuttle_shape_logistic"] = sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2,
+                                                           group=g, span=span,
+                                                           check_prefix=chk, loss="logistic")
         progress("C4 partitioned")
         sec["C4_shuttle_shape_partitioned"] = sgd_steps_per_s(
             9117, 702, 10, 100, 100, 25, 2000, 2, layout="partitioned", group=g, span=span,
@@ -1314,17 +1377,20 @@ def main():
         if not args.no_tradeoff:
             out["tradeoff_reshuffle_mod"] = tradeoff_curve(
                 args, group, span, rank == 0 and world == 1 and not args.no_cpu_baseline)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # at every G (the GPU work of every rank is done; the others wait at the final barrier):
+        # the reference's est.UnN restated on 1 core, and the same blocks spread over the host
+        # cores of this run's CPU share — 16 per GPU on the pool's boxes (os.cpu_count() and the
+        # affinity mask show the whole machine, which the GPU boxes share out per GPU)
         progress("CPU baselines")
-        out["cpu_baseline"] = cpu_baseline(n, shards, args.cpu_shards)
-        # the box's CPU share is 16 cores per GPU (os.cpu_count() and the affinity mask show
-        # the whole machine): the all-cores figure uses that share, and says so
-        share = min(16, len(os.sched_getaffinity(0)))
-        allc = cpu_baseline_all_cores(n, shards, share)
-        allc["label"] = (f"{share} of {len(os.sched_getaffinity(0))} host cores (the GPU box's "
-                         f"CPU share per GPU)")
+        out["cpu_baseline"] = cpu_baseline(args.n, args.shards, args.cpu_shards)
+        aff = len(os.sched_getaffinity(0))
+        share = min(16 * world, aff)
+        allc = cpu_baseline_all_cores(args.n, args.shards, share)
+        allc["label"] = (f"{share} host cores = 16 per GPU x {world} GPU(s), the pool's CPU share "
+                         f"(affinity mask {aff}, os.cpu_count() {os.cpu_count()})")
         out["cpu_baseline"]["all_cores"] = allc
-        out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(n, shards, B_inc,
+        out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(args.n, args.shards, B_inc,
                                                                     args.cpu_inc_shards)
     if rank == 0 and world == 1:
         progress("drop-in C3")
@@ -1338,6 +1404,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:
+        barrier()  # rank 0's CPU baselines run after every rank's GPU work
         dist.destroy_process_group()
 
 

@@ -143,8 +143,10 @@ int tw_count_rank_set_next(int32_t front);
 int tw_rank_set_plan(int32_t sample, int32_t per);
 /* tw_rank_images over several ranks (and for half ties): the images are counted against the Z
  * of d_z_all (the all-gathered sample, n_z_all < 2^24) but written only for the n_x + n_z
- * elements of d_x / d_z (this rank's share; d_z may be d_z_all).  half = 1: each X record's
- * high word is h(x) = #{z in d_z_all : z <= x} as f32 bits (NaN x: -2^25) instead of the index.
+ * elements of d_x / d_z (this rank's share; d_z may be d_z_all).  half (flags): bit 0 — each X
+ * record's high word is h(x) = #{z in d_z_all : z <= x} as f32 bits (NaN x: -2^25) instead of
+ * the index; bit 1 — compact images without indices, the bag layout of tw_count_pairs_chain
+ * (d_x_rec: n_x f32, or n_x {g, h} f32 pairs with bit 0; d_z_rec: n_z f32).
  * d_work: tw_rank_images_work_bytes(n_x, n_z_all) bytes. */
 int tw_rank_images_query(const void* d_z_all, int64_t n_z_all, const void* d_x, int64_t n_x,
                          const void* d_z, int64_t n_z, int32_t dtype, int32_t half,

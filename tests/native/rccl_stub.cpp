@@ -1,7 +1,8 @@
-// Test stub standing in for librccl (tests/test_comm_failure.py, CPU only): the handful of RCCL
-// entry points csrc/comm.hip binds, with ncclCommGetAsyncError reporting a peer failure
-// (STUB_MODE=error) or a collective that never finishes (STUB_MODE=inprogress), so the
-// failure-detection path of tw_comm_wait runs without GPUs or peers.
+// Test stub standing in for librccl (tests/test_comm_failure.py): the handful of RCCL entry
+// points csrc/comm.hip binds, with ncclCommGetAsyncError reporting a peer failure
+// (STUB_MODE=error), a collective that never finishes (STUB_MODE=inprogress) or nothing wrong
+// (STUB_MODE=ok: the GPU test of a slow count queued before the collective), so the
+// failure-detection path of tw_comm_wait runs without peers.
 #include <cstdlib>
 #include <cstring>
 
@@ -10,6 +11,7 @@ typedef struct ncclComm* ncclComm_t;
 static int g_aborts = 0, g_gathers = 0;
 static int mode() {
   const char* m = std::getenv("STUB_MODE");
+  if (m && std::strcmp(m, "ok") == 0) return 0;
   return (m && std::strcmp(m, "inprogress") == 0) ? 7 : 2;  // ncclInProgress / ncclSystemError
 }
 int ncclCommInitAll(ncclComm_t* comms, int n, const int*) {

@@ -60,3 +60,45 @@ def test_comm_wait_fails_instead_of_hanging(stub, mode):
         assert "aborted" in out["msg"]
     assert out["aborts"] == 2  # both devices' communicators
     assert out["again"] == 2 and "aborted after an RCCL failure" in out["again_msg"]
+
+
+_SLOW = r"""
+import ctypes, json, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+from tuplewise import _lib as L
+lib = L.lib()
+stub = ctypes.CDLL(sys.argv[2])
+comm = ctypes.c_int32(-1)
+devs = (ctypes.c_int32 * 1)(0)
+out = {"init": lib.tw_comm_init(1, devs, ctypes.byref(comm))}
+a = torch.randn(4096, 4096, device="cuda")
+torch.cuda.synchronize()
+for _ in range(200):  # ~0.1-0.3 s of queued work before the collective
+    a = a @ a
+    a = a / a.norm()
+P = ctypes.c_void_p * 1
+streams = P(L.stream_handle().value)
+bufs = P(a.data_ptr())
+out["busy_at_gather"] = not torch.cuda.current_stream().query()
+out["gather"] = lib.tw_allgather_u64(comm.value, bufs, bufs, 4, streams)
+out["wait"] = lib.tw_comm_wait(comm.value, streams, 20)  # a 20 ms deadline
+out["msg"] = lib.tw_last_error().decode()
+out["aborts"] = stub.stub_aborts()
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_comm_wait_deadline_starts_after_prior_work(stub):
+    """tw_comm_wait's deadline covers the collective, not the work queued before it
+    on the same stream — a long queue ahead of the all-gather (here ~0.2 s against a 20 ms
+    deadline) must not be taken for an RCCL failure (no abort)."""
+    env = dict(os.environ, TW_RCCL_LIB=str(stub), STUB_MODE="ok")
+    r = subprocess.run([sys.executable, "-c", _SLOW, str(ROOT), str(stub)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["init"] == 0 and out["gather"] == 0 and out["busy_at_gather"]
+    assert out["wait"] == 0, out["msg"]
+    assert out["aborts"] == 0

@@ -279,3 +279,48 @@ def test_chain_overflow_flag(gpu):
     z_bag = torch.zeros((1, m), dtype=torch.float32, device="cuda")
     ops.chain_unpack(send, G, 1, cap, False, n, m, x_bag, z_bag, flag)
     assert int(flag.item()) == 1
+
+
+@pytest.mark.parametrize("kind", ["gauss", "edge", "i64"])
+@pytest.mark.parametrize("tie_mode", ["strict", "half"])
+def test_local_counts_on_rank_images(gpu, kind, tie_mode, monkeypatch):
+    """One-shot counts (ShardedSample.local_counts: est.Un / UnN) on compact rank images ==
+    the double-compare kernel == the oracle, shard by shard (ragged shards, NaN/+-0/+-inf,
+    int64 ties; strict and half units)."""
+    import torch
+    from tuplewise import device as D
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(77)
+    X, Z, N = _sample(rng, 50_001, kind), _sample(rng, 33_333, kind), 7
+    got = {}
+    for on in (True, False):
+        monkeypatch.setattr(D, "ONESHOT_RANK", on)
+        monkeypatch.setattr(D, "ONESHOT_RANK_MIN_PAIRS", 0)
+        S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
+                          algo="pairs", tie_mode=tie_mode)
+        assert S._oneshot_rank_ok() == on
+        got[on] = S.local_counts().cpu().numpy()
+    assert np.array_equal(got[True], got[False])
+    x_off, z_off = _layout(X.size, Z.size, N)
+    for s in range(N):
+        xa, za = X[x_off[s]:x_off[s + 1]], Z[z_off[s]:z_off[s + 1]]
+        if xa.dtype.kind == "f":
+            xa = xa[~np.isnan(xa)]
+        want = O.count_half_sorted(xa, za) if tie_mode == "half" else O.count_gt_sorted(xa, za)
+        assert int(got[True][s]) == want
+
+
+@pytest.mark.parametrize("tie_mode", ["strict", "half"])
+def test_c2_one_shard_on_rank_images(gpu, tie_mode):
+    """BASELINE configs[1] (est.Un, n = 1e5/class, one shard: 1e10 pairs) through the rank-image
+    one-shot count (taken by default at this size) == the oracle's sorted count."""
+    import torch
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(8)
+    X, Z = rng.normal(0.5, 1, 100_000).round(3), rng.normal(0, 1, 100_000).round(3)
+    S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), 1, algo="pairs",
+                      tie_mode=tie_mode)
+    assert S._oneshot_rank_ok()
+    got = int(S.local_counts()[0])
+    want = O.count_half_sorted(X, Z) if tie_mode == "half" else O.count_gt_sorted(X, Z)
+    assert got == want

@@ -159,3 +159,26 @@ def test_learning_devices_wide_rows_over_three_slots(gpu):
         lr.learning_process(X, Z, p, rng_mode="device", devices=devices)
         hist.append((p["norm_w"], p["tr_AUC"]))
     assert hist[0] == hist[1]
+
+
+@pytest.mark.parametrize("draw_ahead", [True, False])
+def test_same_as_batch_replay_over_slots_reshuffle_every_step(gpu, golden, monkeypatch,
+                                                                draw_ahead):
+    """SAME_AS_BATCH monitoring in the pipelined replay loop over two slots (no
+    batch_view: the host formula reads the SWR rows), a reshuffle and an evaluation every step:
+    the pinned ring slots are refilled by the draw worker while later segments run, so the
+    evaluation must read its own copy of the rows.  History equals the one-device run and the
+    sequential loop (DRAW_AHEAD=False)."""
+    import tuplewise.learning as lr
+    monkeypatch.setattr(lr, "TYPE_TRAIN_MONITOR", "SAME_AS_BATCH")
+    monkeypatch.setattr(lr, "DRAW_AHEAD", draw_ahead)
+    X, Z = golden["learn/X"], golden["learn/Z"]
+    out = []
+    for devices in (None, [0, 0]):
+        p = _learn_p(golden)
+        p["n_it"], p["reshuffle_mod"], p["eval_mod"] = 40, 1, 1
+        np.random.seed(13)
+        lr.learning_process(X, Z, p, rng_mode="replay", devices=devices)
+        out.append((p["norm_w"], p["bc_AUC"], p["br_AUC"], p["tr_AUC"]))
+    for a, b in zip(*out):
+        np.testing.assert_allclose(a, b, rtol=1e-12, atol=0)

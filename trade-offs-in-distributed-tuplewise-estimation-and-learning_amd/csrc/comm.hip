@@ -50,6 +50,9 @@ struct Rccl {
 static Rccl g_rccl;
 static std::mutex g_mu;
 static std::vector<std::vector<ncclComm_t>> g_comms;  // handle -> one comm per device
+static std::vector<std::vector<int>> g_devs;          // handle -> its devices
+static std::vector<std::vector<hipEvent_t>> g_pre;    // handle -> per device, recorded on the
+                                                      // stream just before the collective
 static std::vector<char> g_dead;                      // handle -> aborted after a failure
 static int64_t g_wait_ms = 60000;                     // tw_comm_set_timeout
 
@@ -89,6 +92,28 @@ static const char* nccl_err(ncclResult_t e) {
   return g_rccl.errStr ? g_rccl.errStr(e) : "RCCL error";
 }
 
+// An event per device recorded on the collective's stream right before it is enqueued:
+// tw_comm_wait's deadline starts only once the work queued before the collective (a count of
+// any length) has drained, so a slow count is never taken for an RCCL failure.  Without a
+// device (the CPU test's stub) no event exists and the deadline covers the whole stream.
+static void mark_pre(int32_t comm, void* const* streams) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::vector<hipEvent_t>& pre = g_pre[comm];
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) cur = -1;
+  for (size_t k = 0; k < pre.size(); ++k) {
+    if (hipSetDevice(g_devs[comm][k]) != hipSuccess) continue;
+    if (!pre[k] && hipEventCreateWithFlags(&pre[k], hipEventDisableTiming) != hipSuccess)
+      pre[k] = nullptr;
+    if (pre[k] && hipEventRecord(pre[k], (hipStream_t)streams[k]) != hipSuccess) {
+      (void)hipEventDestroy(pre[k]);
+      pre[k] = nullptr;
+    }
+  }
+  if (cur >= 0) (void)hipSetDevice(cur);
+  (void)hipGetLastError();  // no sticky error from a device-less process
+}
+
 static int allgather(int32_t comm, const void* const* send, void* const* recv, int64_t count,
                      int dtype, void* const* streams) {
   std::vector<ncclComm_t> cs;
@@ -104,6 +129,7 @@ static int allgather(int32_t comm, const void* const* send, void* const* recv, i
   }
   TW_ARG_CHECK(count >= 0 && send && recv && streams, "tw_allgather: bad arguments");
   if (count == 0) return TW_OK;
+  mark_pre(comm, streams);
   ncclResult_t e = g_rccl.groupStart();
   for (size_t k = 0; k < cs.size() && e == 0; ++k)
     e = g_rccl.allGather(send[k], recv[k], (size_t)count, dtype, cs[k], (hipStream_t)streams[k]);
@@ -124,6 +150,7 @@ static void abort_comm(int32_t comm) {
 
 static int wait_comm(int32_t comm, void* const* streams, int64_t timeout_ms) {
   std::vector<ncclComm_t> cs;
+  std::vector<hipEvent_t> pre;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     TW_ARG_CHECK(comm >= 0 && comm < (int32_t)g_comms.size() && !g_comms[comm].empty(),
@@ -133,24 +160,44 @@ static int wait_comm(int32_t comm, void* const* streams, int64_t timeout_ms) {
       return TW_ERR_HIP;
     }
     cs = g_comms[comm];
+    pre = g_pre[comm];
   }
   TW_ARG_CHECK(streams != nullptr, "tw_comm_wait: streams");
   const int64_t limit = timeout_ms > 0 ? timeout_ms : g_wait_ms;
-  const auto t0 = std::chrono::steady_clock::now();
   auto fail = [&](const char* what, const char* detail) {
     std::lock_guard<std::mutex> lk(g_mu);
     abort_comm(comm);
     set_error("tw_comm_wait: %s (%s); communicator %d aborted", what, detail, comm);
     return TW_ERR_HIP;
   };
-  for (;;) {
-    // an RCCL error on any device's communicator (a peer that failed, a broken link)
+  // an RCCL error on any device's communicator (a peer that failed, a broken link)
+  auto async_error = [&]() -> int {
     for (ncclComm_t c : cs) {
       ncclResult_t ae = 0;
       const ncclResult_t e = g_rccl.asyncError(c, &ae);
       if (e != 0) return fail("ncclCommGetAsyncError failed", nccl_err(e));
       if (ae != 0 && ae != kNcclInProgress) return fail("RCCL asynchronous error", nccl_err(ae));
     }
+    return TW_OK;
+  };
+  // first the work queued before the collective (no deadline: a legitimately long count)
+  for (bool before = true; before;) {
+    if (const int rc = async_error()) return rc;
+    before = false;
+    for (hipEvent_t ev : pre) {
+      if (!ev) continue;
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipErrorNotReady) {
+        before = true;
+      } else if (q != hipSuccess) {
+        return fail("event query failed", hipGetErrorString(q));
+      }
+    }
+    if (before) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  const auto t0 = std::chrono::steady_clock::now();  // the collective's own deadline
+  for (;;) {
+    if (const int rc = async_error()) return rc;
     bool done = true;
     for (size_t k = 0; k < cs.size(); ++k) {
       const hipError_t q = hipStreamQuery((hipStream_t)streams[k]);
@@ -190,6 +237,8 @@ extern "C" int tw_comm_init(int32_t ndev, const int32_t* devs, int32_t* out_comm
     return TW_ERR_HIP;
   }
   g_comms.push_back(cs);
+  g_devs.push_back(dl);
+  g_pre.push_back(std::vector<hipEvent_t>(ndev, nullptr));
   g_dead.push_back(0);
   *out_comm = (int32_t)g_comms.size() - 1;
   return TW_OK;
@@ -202,6 +251,11 @@ extern "C" int tw_comm_destroy(int32_t comm) {
   if (!g_dead[comm])
     for (ncclComm_t c : g_comms[comm]) g_rccl.destroy(c);
   g_comms[comm].clear();
+  for (hipEvent_t& ev : g_pre[comm])
+    if (ev) {
+      (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
   return TW_OK;
 }
 

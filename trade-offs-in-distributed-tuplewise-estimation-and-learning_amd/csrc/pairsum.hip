@@ -291,7 +291,9 @@ __global__ __launch_bounds__(kBlock) void k_eval_pairs(
     st_sc1_u64(work + blockIdx.x, __double_as_longlong(v));
     st_sc1_u64(cwork + blockIdx.x, c);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+    // release: this block's partials before its ticket; acquire: the last block's loads of
+    // every other block's partials after the ticket that saw them all
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
            (unsigned)nb - 1;
   }
   __syncthreads();

@@ -97,9 +97,12 @@ __device__ __forceinline__ int rank_bucket(const uint64_t* sp, int nsp, uint64_t
 // record pass writes (the same Z as the structure in one process; a rank's own share of X and Z
 // against the all-gathered Z over several ranks, tw_rank_images_query); tot = n + mq.
 // half: the X record's high word holds h(x) = #{z : key(z) <= key(x)} instead of the index.
+// compact: images without indices (x: f32, or the {g, h} f32 pair when half; z: f32), the
+// layout of tw_count_pairs_chain's bags
 struct RankGeo {
   int64_t n, m, tot, mq;
   int B, NB, nblk, cs, half, per, C;  // C: the sorted sample's padded length (power of two)
+  int compact;
 };
 
 // splitter j = the sample's ((j + 1) * cs / B)-th key; loaded into LDS by every pass
@@ -421,10 +424,16 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_records(
     const float img = nan ? kImgNever : (float)gv;
     const uint64_t hi = g.half ? (uint64_t)__float_as_uint(nan ? kImgNever : (float)hv)
                                : (uint64_t)e;
-    x_rec[e] = (uint64_t)__float_as_uint(img) | (hi << 32);
+    if (g.compact && !g.half)
+      ((uint32_t*)x_rec)[e] = __float_as_uint(img);  // the image alone, 4 B
+    else
+      x_rec[e] = (uint64_t)__float_as_uint(img) | (hi << 32);
   } else {
     const int64_t j = e - g.n;
-    z_rec[j] = (uint64_t)__float_as_uint(-(float)gv) | ((uint64_t)j << 32);
+    if (g.compact)
+      ((uint32_t*)z_rec)[j] = __float_as_uint(-(float)gv);
+    else
+      z_rec[j] = (uint64_t)__float_as_uint(-(float)gv) | ((uint64_t)j << 32);
   }
 }
 
@@ -438,13 +447,14 @@ struct RankWork {
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-static RankGeo rank_geo(int64_t n, int64_t m, int64_t mq = -1, int half = 0) {
+static RankGeo rank_geo(int64_t n, int64_t m, int64_t mq = -1, int half = 0, int compact = 0) {
   RankGeo g{};
   g.n = n;
   g.m = m;
   g.mq = mq < 0 ? m : mq;
   g.tot = n + g.mq;
   g.half = half;
+  g.compact = compact;
   int B = 1;
   while (B < kRkMaxB && (int64_t)B * 2048 < m) B <<= 1;  // >= ~2048 z per interval
   g.B = B;
@@ -723,7 +733,7 @@ static int rank_images_any(const void* d_zs, int64_t m, const void* d_xq, int64_
                            const void* d_zq, int64_t nq_z, int32_t dtype, int32_t half,
                            void* d_work, int64_t work_bytes, uint64_t* d_x_rec,
                            uint64_t* d_z_rec, hipStream_t st) {
-  const RankGeo g = rank_geo(nq_x, m, nq_z, half);
+  const RankGeo g = rank_geo(nq_x, m, nq_z, half & 1, (half >> 1) & 1);
   const RankWork w = rank_work(g, (char*)d_work);
   TW_ARG_CHECK(d_work != nullptr && work_bytes >= (int64_t)w.total_bytes,
                "tw_rank_images: work buffer of %lld bytes, %lld needed", (long long)work_bytes,
@@ -757,7 +767,7 @@ extern "C" int tw_rank_images_query(const void* d_z_all, int64_t n_z_all, const 
                "%lld, %lld)", (long long)n_z_all, (long long)n_x, (long long)n_z);
   TW_ARG_CHECK(dtype == TW_F64 || dtype == TW_I64, "tw_rank_images_query: unknown dtype %d",
                dtype);
-  TW_ARG_CHECK(half == 0 || half == 1, "tw_rank_images_query: half in {0, 1}");
+  TW_ARG_CHECK(half >= 0 && half <= 3, "tw_rank_images_query: flags in [0, 3]");
   if (n_x + n_z == 0) return TW_OK;
   return rank_images_any(d_z_all, n_z_all, d_x, n_x, d_z, n_z, dtype, half, d_work, work_bytes,
                          d_x_rec, d_z_rec, (hipStream_t)stream);

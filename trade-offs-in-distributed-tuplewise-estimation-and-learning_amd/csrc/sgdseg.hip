@@ -78,17 +78,24 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 
 // ctl[0]: arrivals (monotonic within a launch, zeroed before it); ctl[1]: abort word, sticky
 // (zeroed once by the caller: a later launch that finds it set exits at its first wait).
+// Memory-model contract of the grid barrier: every published word is an agent-scope atomic
+// store (st_agent); each storing wave waits for its own stores (s_waitcnt vmcnt(0) — the
+// block barrier's workgroup-scope release does not wait for another wave's vector stores to
+// reach the agent-coherent level), the block barrier orders them before thread 0's arrival,
+// and the arrival is an agent-scope RELEASE add; the poller's loads of the counter are
+// agent-scope ACQUIRE loads, and the block barrier after the poll orders every wave's loads of
+// the published words (ld_agent) after it.
 __device__ __forceinline__ void seg_arrive(uint32_t* ctl) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's published stores landed
   __syncthreads();
   if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // one lane: spin until the counter reaches target (false: aborted or timed out -> abort word)
 __device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  while (__hip_atomic_load(ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
     if (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
         wall_clock64() - t0 > kSegSpinTicks) {
       __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(kWideBlock) void k_sgd_segment_wide(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         SEG_STAMP(k, 6);
         if (lane == 0)
-          __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         if (!more && blk == 0 && lane == 0 && d_step) *d_step = step0 + (uint64_t)nsteps;
       }
     } else if (more && prefetch_rows) {

@@ -34,6 +34,10 @@ RANK_IMAGES = True
 # and permutes the records for the next step (csrc/rankimage.hip), the A/B baseline.
 CHAIN_STEPS = True
 CHAIN_MAX = 32
+# one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
+# images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
+ONESHOT_RANK = True
+ONESHOT_RANK_MIN_PAIRS = 1 << 32
 
 
 def prop_swor_layout(n_X: int, n_Z: int, N: int):
@@ -178,20 +182,22 @@ class HipOps:
                L.stream_handle())
         return out
 
-    def rank_images_query(self, Z_all, X, Z, dtype, half=False):
+    def rank_images_query(self, Z_all, X, Z, dtype, half=False, compact=False):
         """Rank-image records of this rank's X and Z counted against the Z of Z_all
-        (tw_rank_images_query); half: the X records' high word is h(x) = #{z <= x}.  None where
-        the path does not apply (|Z_all| >= 2^24)."""
+        (tw_rank_images_query); half: the X records' high word is h(x) = #{z <= x}; compact:
+        images without indices (x float32, or int64 {g, h} pairs when half; z float32), the bag
+        layout of count_chain.  None where the path does not apply (|Z_all| >= 2^24)."""
         n, m, ma = int(X.numel()), int(Z.numel()), int(Z_all.numel())
         wb = int(L.lib().tw_rank_images_work_bytes(n, ma))
         if wb < 0 or n + m >= (1 << 31):
             return None
-        dev = X.device
-        work = self.t.empty((max(wb, 1),), dtype=self.t.uint8, device=dev)
-        xr = self.t.empty((n,), dtype=self.t.int64, device=dev)
-        zr = self.t.empty((m,), dtype=self.t.int64, device=dev)
+        t, dev = self.t, X.device
+        work = t.empty((max(wb, 1),), dtype=t.uint8, device=dev)
+        xr = t.empty((n,), dtype=t.float32 if compact and not half else t.int64, device=dev)
+        zr = t.empty((m,), dtype=t.float32 if compact else t.int64, device=dev)
         L.call("tw_rank_images_query", L.ptr(Z_all), ma, L.ptr(X), n, L.ptr(Z), m, int(dtype),
-               int(bool(half)), L.ptr(work), wb, L.ptr(xr), L.ptr(zr), L.stream_handle())
+               int(bool(half)) | (int(bool(compact)) << 1), L.ptr(work), wb, L.ptr(xr),
+               L.ptr(zr), L.stream_handle())
         return xr, zr
 
     def chain_emit(self, xr, zr, half, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
@@ -474,9 +480,31 @@ class ShardedSample:
 
     # ------------------------------------------------------------------ estimation
     def local_counts(self):
-        """Per-local-shard exact counts (int64 device tensor; uint64 semantics)."""
+        """Per-local-shard exact counts (int64 device tensor; uint64 semantics).  Large all-pairs
+        counts (est.Un at BASELINE configs[1]: 1e10 pairs in one shard) rank X u Z once and count
+        packed f32 images (tw_rank_images_query compact + tw_count_pairs_chain, one step): the
+        ranking costs less than the double compares it replaces."""
+        if self.algo == "pairs" and self._oneshot_rank_ok():
+            half = self.pred == L.TW_PRED_HALF
+            xi, zi = self.ops.rank_images_query(self.Z, self.X, self.Z, self.dtype, half,
+                                                compact=True)
+            out = self.t.empty((1, self.N), dtype=self.t.int64, device=self.X.device)
+            self.ops.count_chain(xi, self.x_off_dev, zi, self.z_off_dev, self.N, 1,
+                                 self.n_loc, self.m_loc, self.max_nx, self.max_nz, half, out)
+            return out[0]
         return self.ops.count(self.X, self.x_off_dev, self.Z, self.z_off_dev, self.N,
                               self.max_nx, self.max_nz, self.dtype, self.pred, algo=self.algo)
+
+    def _oneshot_rank_ok(self) -> bool:
+        """One-shot counts on rank images: the step-chain predicates, a device sample of fewer
+        than 2^24 Z-scores, and at least ONESHOT_RANK_MIN_PAIRS pairs."""
+        return (ONESHOT_RANK and RANK_IMAGES and self.X.is_cuda and self.N > 0
+                and self.max_nx > 0 and self.max_nz > 0
+                and hasattr(self.ops, "rank_images_query") and hasattr(self.ops, "count_chain")
+                and (self.pred in (L.TW_PRED_GT, L.TW_PRED_HALF)
+                     or (self.pred == L.TW_PRED_SUBGT and self.dtype == L.TW_F64))
+                and self.m_loc < (1 << 24) and self.n_loc + self.m_loc < (1 << 31)
+                and int(sum(self.pairs)) >= ONESHOT_RANK_MIN_PAIRS)
 
     def global_counts(self, local):
         """All G*N shard counts, in global shard order, on every rank (one all-reduce)."""

@@ -1294,6 +1294,11 @@ def _replay_segments(eng, draws, segs, wait, shipped, X, Z, p_learn, loss, graph
         rargs = None
         if rows is not None:
             (rows_x, rows_z), pinned = rows
+            if TYPE_TRAIN_MONITOR == "SAME_AS_BATCH":
+                # a host-formula evaluation (several ranks or devices: no batch_view) reads
+                # these rows at this or a later segment, after shipped(idx) may have let the
+                # draw worker refill their ring slot with a later reshuffle: own copies
+                rows_x, rows_z = np.array(rows_x), np.array(rows_z)
             staged = pinned is not None and isinstance(eng, SGDEngine)
             if staged and FUSED_SHIP:
                 rargs = eng.rows_ship_args(pinned)
