@@ -530,6 +530,20 @@ int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64_t d,
                           const double* d_w_in, const double* d_dw_in, double reg, double lr,
                           double momentum, double* d_grads0, double* d_grads1, double* d_w_out,
                           double* d_dw_out, uint32_t* d_ctl, void* stream);
+/* tw_sgd_segment_narrow replaying through reshuffles: d_rows_x / d_rows_z are stacks of SWR
+ * row tables tab_x / tab_z words apart (>= n_shards * kx / kz), and step k of the segment
+ * reads table (tab_phase + k) / tab_mod — the segment starts at step tab_phase of a reshuffle
+ * period of tab_mod steps (0 <= tab_phase < tab_mod), table 0 being the tables in force at its
+ * start (learning_process's SWR_divide every `mod` steps, make_exps.py:123-125, without
+ * ending the segment there). */
+int tw_sgd_segment_narrow_tables(
+    const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x, int64_t kx,
+    const int64_t* d_rows_z, int64_t kz, int64_t tab_x, int64_t tab_z, int64_t tab_phase,
+    int64_t tab_mod, const int64_t* d_ix, const int64_t* d_iz, int64_t draw_stride,
+    int32_t n_shards, int64_t B, double margin, int32_t loss, uint64_t seed,
+    const uint64_t* d_step, int32_t shard_base, int32_t nsteps, const double* d_w_in,
+    const double* d_dw_in, double reg, double lr, double momentum, double* d_grads0,
+    double* d_grads1, double* d_w_out, double* d_dw_out, uint32_t* d_ctl, void* stream);
 /* tw_sgd_segment_narrow in device-RNG mode with the SWR row tables drawn IN the kernel: the
  * row of draw position a of shard s at step counter c is the one tw_swr_rows_rng drew at the
  * last reshuffle, counter rc = c - (c - swr_base) % swr_mod (reshuffles every swr_mod steps
@@ -748,20 +762,30 @@ int tw_widen_u8(const uint8_t* d_in, int64_t n, int64_t* d_out, void* stream);
 int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
                   const void* d_rows, int64_t nx, int64_t* d_rows_x, int64_t nz,
                   int64_t* d_rows_z, void* stream);
+/* tw_ship_draws for a segment running through reshuffles: d_rows holds ntab tables, each
+ * [nx x words | nz z words], copied into ntab consecutive tables of the stacks d_rows_x
+ * (nx words apart) and d_rows_z (nz apart) — the input of tw_sgd_segment_narrow_tables. */
+int tw_ship_draws_tables(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
+                         const void* d_rows, int32_t ntab, int64_t nx, int64_t* d_rows_x,
+                         int64_t nz, int64_t* d_rows_z, void* stream);
 /* The replay loop's draws made ahead on a native thread (csrc/drawpipe.hip): segment j of
- * n_seg (seg_steps[j] steps; seg_resh[j] != 0: a reshuffle first) is drawn from NumPy's
- * MT19937 state (key/pos, advanced in place) into ring buffer j % nbuf: the SWR rows of a
- * reshuffle (make_exps.py:123-125, compute_stats.py:48-54: N randint calls on [0, n_X) of
- * n_X / N values, then N on [0, n_Z)) into row_bufs[k] (int64), then the steps' pairs
- * (compute_stats.py:155-156) into seg_bufs[k] as (S, 2, N, B) values of `width` bytes (1, 2
- * or 8).  tw_draw_pipe_wait blocks until segment j is drawn; tw_draw_pipe_shipped records
+ * n_seg (seg_steps[j] steps, its first step being step seg_phase[j] of a reshuffle period of
+ * `mod` steps: a reshuffle before each of its steps k with (seg_phase[j] + k) % mod == 0) is
+ * drawn from NumPy's MT19937 state (key/pos, advanced in place) into ring buffer j % nbuf, in
+ * the reference's order: each reshuffle's SWR rows (make_exps.py:123-125,
+ * compute_stats.py:48-54: N randint calls on [0, n_X) of n_X / N values, then N on [0, n_Z))
+ * into the next of row_tabs tables of row_bufs[k] (int64, N * (n_X/N + n_Z/N) words each),
+ * then the pairs (compute_stats.py:155-156) of the steps up to the next reshuffle into
+ * seg_bufs[k] as (S, 2, N, B) values of `width` bytes (1, 2 or 8).  A segment with more
+ * reshuffles than row_tabs fails the worker.  tw_draw_pipe_wait blocks until segment j is drawn; tw_draw_pipe_shipped records
  * that the uploads reading its buffers are enqueued on `stream` (the worker refills them only
  * after they have run); tw_draw_pipe_stop cancels what is not drawn, joins and frees.
  * Nothing else may use NumPy's global RNG between start and stop. */
 int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg, const int32_t* seg_steps,
-                       const uint8_t* seg_resh, int32_t N, int64_t kx, int64_t kz, int64_t B,
-                       int64_t n_X, int64_t n_Z, int32_t width, int32_t nbuf,
-                       void* const* seg_bufs, int64_t* const* row_bufs, void** out_handle);
+                       const int32_t* seg_phase, int64_t mod, int32_t N, int64_t kx, int64_t kz,
+                       int64_t B, int64_t n_X, int64_t n_Z, int32_t width, int32_t nbuf,
+                       void* const* seg_bufs, int64_t* const* row_bufs, int32_t row_tabs,
+                       void** out_handle);
 int tw_draw_pipe_wait(void* handle, int32_t j);
 int tw_draw_pipe_shipped(void* handle, int32_t j, void* stream);
 int tw_draw_pipe_stop(void* handle);

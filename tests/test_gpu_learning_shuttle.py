@@ -67,9 +67,9 @@ def test_reference_shape_default_path(gpu, golden, mod, monkeypatch):
     seen = []
     orig = lr.SGDEngine._fused_steps
 
-    def spy(self, nsteps, draws_dev=None):
-        seen.append((nsteps, self.narrow_seg))
-        return orig(self, nsteps, draws_dev)
+    def spy(self, nsteps, draws_dev=None, swr_mod=0, tables=None):
+        seen.append((nsteps, self.narrow_seg, tables))
+        return orig(self, nsteps, draws_dev, swr_mod, tables)
 
     monkeypatch.setattr(lr.SGDEngine, "_fused_steps", spy)
     logging.disable(logging.CRITICAL)
@@ -84,10 +84,12 @@ def test_reference_shape_default_path(gpu, golden, mod, monkeypatch):
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert out[True][0][k] == out[False][0][k], k
     assert np.array_equal(out[True][1], out[False][1]) and out[True][2] == out[False][2]
-    if mod == 10000:
-        assert any(n > 1 and nseg for n, nseg in seen), seen[:5]
-    else:
-        assert all(n == 1 for n, _ in seen)
+    # segments end at evaluations only (eval_mod 25): at mod 1 they run through a reshuffle
+    # before every step, the kernel switching row tables by step
+    assert any(n > 1 and nseg for n, nseg, _ in seen), seen[:5]
+    if mod == 1:
+        assert all(tab is not None and tab[1] == 1 for n, _, tab in seen if n > 1), seen[:5]
+        assert max(n for n, _, _ in seen) == 25, seen[:5]
     X, Z, p = _p(mod)
     np.random.seed(3000 + mod)
     lr.learning_process(X, Z, p, trajectory=[])
@@ -214,7 +216,8 @@ def test_native_draw_pipe_protocol(gpu):
     from tuplewise.numpy_rng import Session
     N, kx, kz, B = 7, 91, 7, 13
     n_X, n_Z = N * kx, N * kz
-    segs = [(0, 3, True), (3, 5, False), (5, 9, True), (9, 10, False), (10, 12, True)]
+    mod = 5  # reshuffles at steps 0, 5, 10
+    segs = [(0, 3, 1), (3, 5, 0), (5, 9, 1), (9, 10, 0), (10, 12, 1)]
     np.random.seed(11)
     want = []
     with Session() as s:
@@ -229,7 +232,7 @@ def test_native_draw_pipe_protocol(gpu):
     np.random.seed(11)
     d = lr._ReplayDraws(N, kx, kz, B)
     with d.rng:
-        pipe = d.native_pipe(segs, n_X, n_Z)
+        pipe = d.native_pipe(segs, n_X, n_Z, mod)
         try:
             for j, (a, b, r) in enumerate(segs):
                 rows, k = pipe.wait(j)
@@ -246,18 +249,47 @@ def test_native_draw_pipe_protocol(gpu):
     assert np.array_equal(np.random.get_state()[1], state[1])
     assert np.random.get_state()[2] == state[2]
     torch.cuda.synchronize()
+    # segments running through reshuffles (replay_through): the same draws, a reshuffle's rows
+    # before the pairs of its step, the tables one after another in the row buffer
+    tsegs = [(0, 12, 3), (12, 13, 0), (13, 20, 1)]  # reshuffles at 0, 5, 10 | - | 15
+    np.random.seed(11)
+    d3 = lr._ReplayDraws(N, kx, kz, B)
+    with d3.rng:
+        pipe = d3.native_pipe(tsegs, n_X, n_Z, mod)
+        try:
+            tabs = []
+            for j, (a, b, r) in enumerate(tsegs):
+                pipe.wait(j, rows=False)
+                k = j % 3
+                per = N * kx + N * kz
+                tabs += [d3.rows3[k][0].numpy()[t * per:(t + 1) * per].copy() for t in range(r)]
+                if j == 0:
+                    got = d3.seg3_np[k][:12].copy()
+                    assert np.array_equal(got, np.concatenate([w[1] for w in want]))
+                pipe.shipped(j)
+        finally:
+            pipe.stop()
+    for t, w in zip(tabs[:3], (want[0][0], want[2][0], want[4][0])):
+        assert np.array_equal(t, w)
+    assert len(tabs) == 4
+    torch.cuda.synchronize()
     # stopped early: the worker waits for segment 0's buffer to be shipped, which never happens
     d2 = lr._ReplayDraws(N, kx, kz, B)
     with d2.rng:
-        pipe = d2.native_pipe(segs, n_X, n_Z)
+        pipe = d2.native_pipe(segs, n_X, n_Z, mod)
         pipe.wait(0)
         pipe.stop()
+    P = __import__("ctypes").c_void_p * 3
     with pytest.raises(ValueError):
-        h = ctypes_handle()
-        P = __import__("ctypes").c_void_p * 3
         L.call("tw_draw_pipe_start", d2.rng._key, d2.rng._pos, 1,
-               np.array([1], np.int32).ctypes.data, np.array([0], np.uint8).ctypes.data,
-               N, 300, kz, B, 300 * N, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), h)
+               np.array([1], np.int32).ctypes.data, np.array([0], np.int32).ctypes.data, 1,
+               N, 300, kz, B, 300 * N, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), 1,
+               ctypes_handle())
+    with pytest.raises(ValueError):  # a phase outside the reshuffle period
+        L.call("tw_draw_pipe_start", d2.rng._key, d2.rng._pos, 1,
+               np.array([1], np.int32).ctypes.data, np.array([5], np.int32).ctypes.data, 5,
+               N, kx, kz, B, n_X, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), 1,
+               ctypes_handle())
 
 
 def ctypes_handle():
@@ -286,3 +318,30 @@ def test_swr_in_kernel_equals_row_tables(gpu, golden, mod, eval_mod, n_it, monke
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert out[True][k] == out[False][k], k
     assert len(out[True]["norm_w"]) == (n_it + eval_mod - 1) // eval_mod
+
+
+@pytest.mark.parametrize("mod,eval_mod,n_it,monitor", [
+    (1, 25, 101, "FIXED_PAIRS"), (3, 25, 101, "FIXED_PAIRS"), (7, 10, 95, "FIXED_PAIRS"),
+    (2, 25, 60, "SAME_AS_BATCH"), (5, 7, 50, "SAME_AS_BATCH"), (40, 25, 101, "FIXED_PAIRS")])
+def test_replay_through_reshuffles_equals_cut_segments(gpu, golden, mod, eval_mod, n_it,
+                                                      monitor, monkeypatch):
+    """learning.REPLAY_THROUGH (replay segments running through their reshuffles: the SWR
+    tables shipped with the segment's draws, the kernel switching tables at the reshuffle
+    steps) against segments cut at every reshuffle: the same evaluation lists and final NumPy
+    RNG state, bit for bit — with evaluations that coincide with reshuffles (SAME_AS_BATCH reads
+    the new tables), segments that start between reshuffles, and one-step tails."""
+    import tuplewise.learning as lr
+    logging.disable(logging.CRITICAL)
+    monkeypatch.setattr(lr, "TYPE_TRAIN_MONITOR", monitor)
+    out = {}
+    for through in (True, False):
+        monkeypatch.setattr(lr, "REPLAY_THROUGH", through)
+        X, Z, p = _p(mod, n_it=n_it)
+        p["eval_mod"] = eval_mod
+        np.random.seed(46)
+        lr.learning_process(X, Z, p)
+        out[through] = (p, np.random.get_state()[1].copy(), np.random.get_state()[2])
+    for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
+        assert out[True][0][k] == out[False][0][k], k
+    assert np.array_equal(out[True][1], out[False][1]) and out[True][2] == out[False][2]
+    assert len(out[True][0]["norm_w"]) == (n_it + eval_mod - 1) // eval_mod

@@ -113,6 +113,10 @@ _SIGNATURES = {
     "tw_sgd_segment_narrow": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i64,
                               _f64, _i32, _u64, _vp, _i32, _i32, _vp, _vp, _f64, _f64, _f64, _vp,
                               _vp, _vp, _vp, _vp, _vp],
+    "tw_sgd_segment_narrow_tables": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64,
+                                     _i64, _vp, _vp, _i64, _i32, _i64, _f64, _i32, _u64, _vp,
+                                     _i32, _i32, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp,
+                                     _vp, _vp],
     "tw_pair_grad_rng_swr": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _vp, _f64,
                              _i32, _u64, _vp, _i32, _i64, _u64, _vp, _vp],
     "tw_sgd_segment_narrow_swr": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _f64,
@@ -160,8 +164,9 @@ _SIGNATURES = {
     "tw_eval_small": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _i64,
                       _vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "tw_ship_draws": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp],
-    "tw_draw_pipe_start": [_vp, _vp, _i32, _vp, _vp, _i32, _i64, _i64, _i64, _i64, _i64, _i32,
-                           _i32, _vp, _vp, _vp],
+    "tw_draw_pipe_start": [_vp, _vp, _i32, _vp, _vp, _i64, _i32, _i64, _i64, _i64, _i64, _i64,
+                           _i32, _i32, _vp, _vp, _i32, _vp],
+    "tw_ship_draws_tables": [_vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _i64, _vp, _vp],
     "tw_draw_pipe_wait": [_vp, _i32],
     "tw_draw_pipe_shipped": [_vp, _i32, _vp],
     "tw_draw_pipe_stop": [_vp],

@@ -5,11 +5,14 @@
 // compute_stats.py:48-54: N randint calls on [0, n_X) of kx values, then N on [0, n_Z)), and per
 // step grad_inc_block's pairs (compute_stats.py:155-156) — one MT19937 stream, NumPy's global
 // RandomState, advanced in place here (key/pos point into it).  The loop's segments (runs of
-// steps between reshuffles/evaluations) are drawn in order into a ring of pinned host buffers;
+// steps between evaluations) are drawn in order into a ring of pinned host buffers — a
+// segment's pairs, and the row tables of every reshuffle inside it, in the reference's draw
+// order (a reshuffle's rows before the pairs of its step);
 // the main thread waits for segment j, ships it (one upload kernel reading the pinned buffer)
 // and records that upload on its stream; the worker refills a buffer only after the upload out
 // of it has run (hipEventSynchronize on the recorded event).  A Python worker thread did the
 // same with ~60 us per 25-step segment of interpreter and GIL overhead on top of the draws.
+#include <algorithm>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -24,7 +27,9 @@ struct DrawPipe {
   uint32_t* key;
   int32_t* pos;
   std::vector<int32_t> steps;
-  std::vector<uint8_t> resh;
+  std::vector<int32_t> phase;  // step of the reshuffle period at each segment's first step
+  int64_t mod;                 // reshuffle period (steps)
+  int32_t row_tabs;            // row tables per row buffer
   int32_t N;
   int64_t kx, kz, B, n_X, n_Z;
   int32_t width, nbuf;
@@ -55,19 +60,31 @@ struct DrawPipe {
           return;
         }
       }
-      int r = 0;
-      if (resh[j])
-        r = tw_np_randint_batch(key, pos, 2 * N, row_low.data(), row_high.data(),
-                                row_cnt.data(), row_bufs[k]);
-      if (!r) {
+      int r = 0, tabs = 0;
+      const int64_t per = 2 * (int64_t)N * B, wtab = (int64_t)N * (kx + kz);
+      for (int32_t k0 = 0; k0 < steps[j] && !r;) {
+        const int64_t ph = ((int64_t)phase[j] + k0) % mod;
+        if (ph == 0) {  // a reshuffle at this step: its rows first (SWR_divide, then the pairs)
+          if (tabs == row_tabs) {
+            r = 1;
+            break;
+          }
+          r = tw_np_randint_batch(key, pos, 2 * N, row_low.data(), row_high.data(),
+                                  row_cnt.data(), row_bufs[k] + tabs * wtab);
+          ++tabs;
+          if (r) break;
+        }
+        const int32_t run = (int32_t)std::min<int64_t>(steps[j] - k0, mod - ph);
+        const int64_t at = (int64_t)k0 * per;
         if (width == 1)
-          r = tw_np_randint_pairs_steps_u8(key, pos, steps[j], N, kx, kz, B,
-                                           (uint8_t*)seg_bufs[k]);
+          r = tw_np_randint_pairs_steps_u8(key, pos, run, N, kx, kz, B,
+                                           (uint8_t*)seg_bufs[k] + at);
         else if (width == 2)
-          r = tw_np_randint_pairs_steps_u16(key, pos, steps[j], N, kx, kz, B,
-                                            (uint16_t*)seg_bufs[k]);
+          r = tw_np_randint_pairs_steps_u16(key, pos, run, N, kx, kz, B,
+                                            (uint16_t*)seg_bufs[k] + at);
         else
-          r = tw_np_randint_pairs_steps(key, pos, steps[j], N, kx, kz, B, (int64_t*)seg_bufs[k]);
+          r = tw_np_randint_pairs_steps(key, pos, run, N, kx, kz, B, (int64_t*)seg_bufs[k] + at);
+        k0 += run;
       }
       if (r) {
         finish(TW_ERR_ARG);
@@ -95,12 +112,18 @@ struct DrawPipe {
 }  // namespace tw
 
 extern "C" int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg,
-                                  const int32_t* seg_steps, const uint8_t* seg_resh, int32_t N,
-                                  int64_t kx, int64_t kz, int64_t B, int64_t n_X, int64_t n_Z,
-                                  int32_t width, int32_t nbuf, void* const* seg_bufs,
-                                  int64_t* const* row_bufs, void** out_handle) {
-  TW_ARG_CHECK(key && pos && out_handle && n_seg >= 0 && N >= 0 && B >= 0,
+                                  const int32_t* seg_steps, const int32_t* seg_phase,
+                                  int64_t mod, int32_t N, int64_t kx, int64_t kz, int64_t B,
+                                  int64_t n_X, int64_t n_Z, int32_t width, int32_t nbuf,
+                                  void* const* seg_bufs, int64_t* const* row_bufs,
+                                  int32_t row_tabs, void** out_handle) {
+  TW_ARG_CHECK(key && pos && out_handle && n_seg >= 0 && N >= 0 && B >= 0 && mod >= 1 &&
+                   row_tabs >= 1 && (n_seg == 0 || (seg_steps && seg_phase)),
                "tw_draw_pipe_start: bad arguments");
+  for (int32_t j = 0; j < n_seg; ++j)
+    TW_ARG_CHECK(seg_steps[j] >= 0 && seg_phase[j] >= 0 && seg_phase[j] < mod,
+                 "tw_draw_pipe_start: segment %d: steps %d, phase %d (mod %lld)", j,
+                 seg_steps[j], seg_phase[j], (long long)mod);
   TW_ARG_CHECK(nbuf >= 1 && nbuf <= 16 && seg_bufs && row_bufs, "tw_draw_pipe_start: buffers");
   TW_ARG_CHECK(width == 1 || width == 2 || width == 8, "tw_draw_pipe_start: width 1, 2 or 8");
   TW_ARG_CHECK(kx >= 1 && kz >= 1 && n_X >= 1 && n_Z >= 1, "tw_draw_pipe_start: empty ranges");
@@ -111,7 +134,9 @@ extern "C" int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg,
   p->key = key;
   p->pos = pos;
   p->steps.assign(seg_steps, seg_steps + n_seg);
-  p->resh.assign(seg_resh, seg_resh + n_seg);
+  p->phase.assign(seg_phase, seg_phase + n_seg);
+  p->mod = mod;
+  p->row_tabs = row_tabs;
   p->N = N;
   p->kx = kx;
   p->kz = kz;

@@ -816,6 +816,67 @@ extern "C" int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t
   return TW_OK;
 }
 
+// A replay segment through reshuffles: its narrowed pair draws widened (as k_ship) and ntab row
+// tables, laid out [x rows | z rows] per table in the mapped pinned buffer, into consecutive
+// tables of the device stacks (x tables nx words apart, z tables nz apart), in one launch.
+template <typename T>
+static __global__ __launch_bounds__(256) void k_ship_tables(
+    const T* __restrict__ in, int64_t n, int64_t* __restrict__ out,
+    const uint64_t* __restrict__ rows, int ntab, int64_t nx, uint64_t* __restrict__ rows_x,
+    int64_t nz, uint64_t* __restrict__ rows_z, int gw) {
+  if ((int)blockIdx.x < gw) {
+    constexpr int U = 16 / (int)sizeof(T);
+    const int64_t nv = n / U;
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nv;
+         v += (int64_t)gw * 256) {
+      const uint4 q = ((const uint4*)in)[v];
+      const T* e = (const T*)&q;
+#pragma unroll
+      for (int u = 0; u < U; ++u) out[v * U + u] = (int64_t)e[u];
+    }
+    for (int64_t i = nv * U + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gw * 256)
+      out[i] = (int64_t)in[i];
+    return;
+  }
+  const int64_t per = nx + nz, tot = per * ntab;
+  for (int64_t i = (int64_t)(blockIdx.x - gw) * 256 + threadIdx.x; i < tot;
+       i += (int64_t)(gridDim.x - gw) * 256) {
+    const int64_t t = i / per, j = i - t * per;
+    if (j < nx)
+      rows_x[t * nx + j] = rows[i];
+    else
+      rows_z[t * nz + (j - nx)] = rows[i];
+  }
+}
+
+extern "C" int tw_ship_draws_tables(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
+                                    const void* d_rows, int32_t ntab, int64_t nx,
+                                    int64_t* d_rows_x, int64_t nz, int64_t* d_rows_z,
+                                    void* stream) {
+  TW_ARG_CHECK(width == 1 || width == 2, "tw_ship_draws_tables: width must be 1 or 2");
+  TW_ARG_CHECK(n >= 0 && nx >= 0 && nz >= 0 && ntab >= 0, "tw_ship_draws_tables: negative size");
+  TW_ARG_CHECK(n == 0 || (d_in != nullptr && d_out != nullptr), "tw_ship_draws_tables: draws");
+  TW_ARG_CHECK(ntab == 0 || nx + nz == 0 ||
+                   (d_rows != nullptr && d_rows_x != nullptr && d_rows_z != nullptr),
+               "tw_ship_draws_tables: null row tables");
+  const int64_t per = 256 * (16 / (int64_t)width);
+  const int gw = n > 0 ? (int)std::min<int64_t>(1024, ceil_div(n, per)) : 0;
+  const int64_t tot = (nx + nz) * ntab;
+  const int gr = tot > 0 ? (int)std::min<int64_t>(512, ceil_div(tot, 256)) : 0;
+  if (gw + gr == 0) return TW_OK;
+  if (width == 1)
+    hipLaunchKernelGGL(k_ship_tables<uint8_t>, dim3(gw + gr), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_in, n, d_out, (const uint64_t*)d_rows, (int)ntab, nx,
+                       (uint64_t*)d_rows_x, nz, (uint64_t*)d_rows_z, gw);
+  else
+    hipLaunchKernelGGL(k_ship_tables<uint16_t>, dim3(gw + gr), dim3(256), 0, (hipStream_t)stream,
+                       (const uint16_t*)d_in, n, d_out, (const uint64_t*)d_rows, (int)ntab, nx,
+                       (uint64_t*)d_rows_x, nz, (uint64_t*)d_rows_z, gw);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 // 8-byte words from a (host-mapped) staging buffer into device memory: the replay loop's SWR
 // row tables, read by the kernel straight from pinned host memory.
 static __global__ __launch_bounds__(256) void k_copy_words(const uint64_t* __restrict__ in,

@@ -365,6 +365,14 @@ __global__ __launch_bounds__(kWideBlock) void k_sgd_segment_wide(
 // one-launch-per-step path.  Same arithmetic and order: same bits.
 constexpr int kNarrowMaxD = 32, kNarrowMaxGrads = 4096;
 
+// Replay segments through reshuffles (tw_sgd_segment_narrow_tables): the row tables are stacks
+// of tables x / z words apart, and step k of the segment reads table (phase + k) / mod — the
+// segment's first step is step `phase` of a reshuffle period.  mod = 0: one table.
+struct TabSteps {
+  int64_t x, z;
+  uint64_t phase, mod;
+};
+
 template <int LOSS>
 __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     const double* __restrict__ w_in, const double* __restrict__ dw_in, double reg, double lr,
     double momentum, double* grads0, double* grads1, double* __restrict__ w_out,
     double* __restrict__ dw_out, uint32_t* ctl, int64_t n_X, int64_t n_Z, uint64_t swr_mod,
-    uint64_t swr_base) {
+    uint64_t swr_base, TabSteps tab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* diff = (double*)smem;         // B * d
   double* flag = diff + B * d;          // B pair weights
@@ -392,6 +400,11 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     wsh[tid] = wj;
   }
   for (int k = 0; k < nsteps; ++k) {
+    // replay through reshuffles: the row tables of this step's last reshuffle, table
+    // (phase + k) / mod of the stacks (table 0: the tables in force when the segment starts)
+    const int64_t tk = tab.mod ? (int64_t)((tab.phase + (uint64_t)k) / tab.mod) : 0;
+    const int64_t* __restrict__ rtx = rows_x ? rows_x + tk * tab.x : nullptr;
+    const int64_t* __restrict__ rtz = rows_z ? rows_z + tk * tab.z : nullptr;
     // 1. this step's pairs -> diff rows (independent of w)
     for (int t = tid; t < B; t += kBlock) {
       int64_t ax, az;
@@ -415,8 +428,8 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
         rxt = (int64_t)mulhi_u64(((uint64_t)qx.b << 32) | qx.a, (uint64_t)n_X);
         rzt = (int64_t)mulhi_u64(((uint64_t)qz.b << 32) | qz.a, (uint64_t)n_Z);
       } else {
-        rxt = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-        rzt = rows_z ? rows_z[(int64_t)s * kz + az] : az;
+        rxt = rtx ? rtx[(int64_t)s * kx + ax] : ax;
+        rzt = rtz ? rtz[(int64_t)s * kz + az] : az;
       }
       const double* zr = Z + rzt * d;
       const double* xr = X + rxt * d;
@@ -537,7 +550,7 @@ static int segment_narrow(const double* d_X, const double* d_Z, int64_t d,
                           const double* d_dw_in, double reg, double lr, double momentum,
                           double* d_grads0, double* d_grads1, double* d_w_out, double* d_dw_out,
                           uint32_t* d_ctl, int64_t n_X, int64_t n_Z, uint64_t swr_mod,
-                          uint64_t swr_base, void* stream) {
+                          uint64_t swr_base, void* stream, TabSteps tab = TabSteps{0, 0, 0, 0}) {
   // shape limits only: the residency query (tw_sgd_segment_narrow_ok) is a HIP API call the
   // caller makes once, before any stream capture — this entry runs inside captured graphs
   TW_ARG_CHECK(d >= 1 && d <= kNarrowMaxD && n_shards >= 1 &&
@@ -561,7 +574,7 @@ static int segment_narrow(const double* d_X, const double* d_Z, int64_t d,
                        d_rows_z, kz, d_ix, d_iz, draw_stride, B, margin, seed, d_step,
                        (uint32_t)shard_base, (int)n_shards, (int)nsteps, d_w_in, d_dw_in, reg,
                        lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl, n_X, n_Z,
-                       swr_mod, swr_base);
+                       swr_mod, swr_base, tab);
   };
   if (loss == TW_LOSS_LOGISTIC)
     go(k_sgd_segment_narrow<TW_LOSS_LOGISTIC>);
@@ -585,6 +598,25 @@ extern "C" int tw_sgd_segment_narrow(const double* d_X, const double* d_Z, int64
                         n_shards, B, margin, loss, seed, d_step, shard_base, nsteps, d_w_in,
                         d_dw_in, reg, lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl,
                         1, 1, 0, 0, stream);
+}
+
+extern "C" int tw_sgd_segment_narrow_tables(
+    const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x, int64_t kx,
+    const int64_t* d_rows_z, int64_t kz, int64_t tab_x, int64_t tab_z, int64_t tab_phase,
+    int64_t tab_mod, const int64_t* d_ix, const int64_t* d_iz, int64_t draw_stride,
+    int32_t n_shards, int64_t B, double margin, int32_t loss, uint64_t seed,
+    const uint64_t* d_step, int32_t shard_base, int32_t nsteps, const double* d_w_in,
+    const double* d_dw_in, double reg, double lr, double momentum, double* d_grads0,
+    double* d_grads1, double* d_w_out, double* d_dw_out, uint32_t* d_ctl, void* stream) {
+  TW_ARG_CHECK(tab_mod >= 1 && tab_phase >= 0 && tab_phase < tab_mod &&
+                   tab_x >= (int64_t)n_shards * kx && tab_z >= (int64_t)n_shards * kz &&
+                   d_rows_x != nullptr && d_rows_z != nullptr,
+               "tw_sgd_segment_narrow_tables: bad table stacks (stride, phase, mod)");
+  return segment_narrow(d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, draw_stride,
+                        n_shards, B, margin, loss, seed, d_step, shard_base, nsteps, d_w_in,
+                        d_dw_in, reg, lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl,
+                        1, 1, 0, 0, stream,
+                        TabSteps{tab_x, tab_z, (uint64_t)tab_phase, (uint64_t)tab_mod});
 }
 
 extern "C" int tw_sgd_segment_narrow_swr(const double* d_X, const double* d_Z, int64_t d,

@@ -61,6 +61,9 @@ EVAL_FUSED = True
 # pipelined replay loop: the draws made ahead by a native thread (csrc/drawpipe.hip) rather
 # than a Python worker thread
 NATIVE_DRAWS = True
+# replay segments run through reshuffles (one process, replicated X, narrow segments): the
+# reshuffles' SWR tables ride in the segment's upload, the kernel switches tables by step
+REPLAY_THROUGH = True
 PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each segment's draws
 SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
@@ -195,7 +198,25 @@ class SGDEngine:
             raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
                                "co-resident); the SGD state is invalid")
 
-    def _fused_steps(self, nsteps: int, draws_dev=None, swr_mod=0):
+    def table_stacks(self, ntab: int):
+        """Replay segments through reshuffles (tw_sgd_segment_narrow_tables): the row tables
+        become slot 0 of stacks of 1 + ntab tables (N, kx) / (N, kz), the segment's reshuffles
+        shipped into slots 1.. (0.. when it starts at one).  Growing them moves rows_x /
+        rows_z: captured replay graphs hold the old addresses and are dropped."""
+        st = getattr(self, "_stacks", None)
+        if st is None or st[0].shape[0] < ntab + 1:
+            t = self.t
+            sx = L.empty((ntab + 1, self.N_loc, self.kx), t.int64)
+            sz = L.empty((ntab + 1, self.N_loc, self.kz), t.int64)
+            if self.rows_x is not None:
+                sx[0].copy_(self.rows_x)
+                sz[0].copy_(self.rows_z)
+            self._stacks = st = (sx, sz)
+            self.rows_x, self.rows_z = sx[0], sz[0]
+            self._replay_graphs = {}
+        return st
+
+    def _fused_steps(self, nsteps: int, draws_dev=None, swr_mod=0, tables=None):
         """nsteps steps as nsteps tw_sgd_step launches + one tw_sgd_update_to (ping-pong
         slots for w/dw/grads; slot 0 = self.w/self.dw/self.grads holds the state before and
         after).  Same bits as step()/step_device() + _update() per step."""
@@ -212,7 +233,22 @@ class SGDEngine:
             if draws_dev is not None:
                 ix, iz = draws_dev[0, 0], draws_dev[0, 1]
                 stride = int(draws_dev.stride(0))
-            if swr_mod:  # device RNG: the segment draws its reshuffles' rows itself
+            if tables is not None:  # replay through reshuffles: the stacks' tables by step
+                sx, sz = self._stacks
+                phase, mod = tables
+                L.call("tw_sgd_segment_narrow_tables", L.ptr(self.X), L.ptr(self.Z), self.d,
+                       L.ptr(sx), self.kx, L.ptr(sz), self.kz, int(sx.stride(0)),
+                       int(sz.stride(0)), int(phase), int(mod), L.ptr(ix), L.ptr(iz), stride,
+                       self.N_loc, self.B, self.margin, self.loss, seed, L.ptr(self.step_ctr),
+                       self.shard_base, nsteps, L.ptr(W[0]), L.ptr(DW[0]), self.reg, self.lr,
+                       self.momentum, L.ptr(Gs[0]), L.ptr(Gs[1]), L.ptr(W[1]), L.ptr(DW[1]),
+                       L.ptr(self._ctl), s)
+                # the last reshuffle's tables become slot 0 (evaluations, later segments)
+                last_tab = (int(phase) + nsteps - 1) // int(mod)
+                if last_tab > 0:
+                    L.call("tw_copy_words", L.ptr(sx[last_tab]), sx[0].numel(), L.ptr(sx[0]), s)
+                    L.call("tw_copy_words", L.ptr(sz[last_tab]), sz[0].numel(), L.ptr(sz[0]), s)
+            elif swr_mod:  # device RNG: the segment draws its reshuffles' rows itself
                 L.call("tw_sgd_segment_narrow_swr", L.ptr(self.X), L.ptr(self.Z), self.d,
                        self.n_X, self.n_Z, self.kx, self.kz, self.N_loc, self.B, self.margin,
                        self.loss, seed, L.ptr(self.step_ctr), self.shard_base, nsteps,
@@ -303,6 +339,12 @@ class SGDEngine:
         self.rows_z.view(-1).copy_(flat[nx + a * self.kz:nx + (a + self.N_loc) * self.kz],
                                    non_blocking=True)
         return True
+
+    def replay_through_ok(self) -> bool:
+        """Replay segments may run through reshuffles (tw_sgd_segment_narrow_tables): one
+        process, replicated X, the persistent narrow segment kernel."""
+        return (self.narrow_seg and self.G == 1 and self.layout == "replicated"
+                and not self.complete and self.N_loc == self.N and self.rows_x is not None)
 
     def rows_ship_args(self, staged):
         """tw_ship_draws' row-table arguments for a reshuffle whose rows sit in a mapped pinned
@@ -408,13 +450,14 @@ class SGDEngine:
         self._update()
 
     def run_replay_segment(self, draws_dev, nsteps: int, graphs: bool = True, tag=0,
-                           upload=None):
+                           upload=None, tables=None):
         """nsteps replay steps whose NumPy draws sit in draws_dev[s] ((2, N, B) int64 on the
         device): one gradient + one update launch per step, replayed from a hipGraph captured
         per (tag, nsteps) — tag names the draw buffer, whose address the graph holds — or
         launched eagerly (graphs=False, or a collective in the step).  upload: (key, fn) — fn
         enqueues the segment's upload (tw_ship_draws), captured in the same graph (one graph
-        launch per segment); key names its arguments."""
+        launch per segment); key names its arguments.  tables: (phase, mod) — a narrow segment
+        running through reshuffles whose row tables sit in table_stacks (replay_through)."""
         def one(st):
             if self.complete:
                 self.step_complete()
@@ -425,7 +468,7 @@ class SGDEngine:
             if self.segment:
                 self._segment(nsteps, draws_dev)
             elif self.fused:
-                self._fused_steps(nsteps, draws_dev)
+                self._fused_steps(nsteps, draws_dev, tables=tables)
             else:
                 for st in range(nsteps):
                     one(st)
@@ -891,39 +934,65 @@ class _ReplayDraws:
         buf, ev = self.rows3[k]
         if self.rows3_used[k]:
             ev.synchronize()
-        flat = buf.numpy()
+        flat = buf.numpy()[:N * kx + N * kz]
         self.rng.randint_flat(*self._swr_setup(n_X, n_Z), out=flat)
         return (flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, kz)), (buf,
                                                                              self.rows3_hdev[k])
 
-    def _rows_buffers(self, n_X, n_Z):
-        """The ring of three pinned SWR row buffers (flat N*kx + N*kz int64, mapped)."""
+    def _rows_buffers(self, n_X, n_Z, ntab=1):
+        """The ring of three pinned SWR row buffers (flat N*kx + N*kz int64 per table, ntab
+        tables; mapped)."""
         t = L.torch()
         N, kx, kz = self.N, int(n_X / self.N), int(n_Z / self.N)
-        if getattr(self, "rows3", None) is None or self.rows3[0][0].shape != (N * kx + N * kz,):
-            self.rows3 = [(t.empty((N * kx + N * kz,), dtype=t.int64, pin_memory=True),
+        per = N * kx + N * kz
+        if (getattr(self, "rows3", None) is None or self.rows3_per != per
+                or self.rows3[0][0].shape[0] < per * ntab):
+            self.rows3 = None  # release the old ring first
+            self.rows3_per = per
+            self.rows3 = [(t.empty((per * ntab,), dtype=t.int64, pin_memory=True),
                            t.cuda.Event()) for _ in range(3)]
             self.rows3_used = [False] * 3
             self.rows3_hdev = [L.host_device_pointer(b) for b, _ in self.rows3]
         return N, kx, kz
 
-    def native_pipe(self, segs, n_X, n_Z):
+    def native_pipe(self, segs, n_X, n_Z, mod):
         """The loop's draws made ahead by a native thread (tw_draw_pipe_*, csrc/drawpipe.hip)
-        into the ring of pinned segment and row buffers: segs = [(i, nxt, reshuffle)]."""
+        into the ring of pinned segment and row buffers: segs = [(i, nxt, ntab)] — ntab row
+        tables in segment [i, nxt) (its reshuffles: the steps i + k with (i + k) % mod == 0;
+        a segment cut at reshuffles has ntab 1 when it starts at one, else 0)."""
         t = L.torch()
         self._seg_buffers(3)
-        N, kx, kz = self._rows_buffers(n_X, n_Z)
+        ntab = max([1] + [int(r) for _, _, r in segs])
+        N, kx, kz = self._rows_buffers(n_X, n_Z, ntab)
         t.cuda.current_stream().synchronize()  # earlier uploads out of the ring have run
         steps = np.array([b - a for a, b, _ in segs], dtype=np.int32)
-        resh = np.array([bool(r) for _, _, r in segs], dtype=np.uint8)
+        phase = np.array([a % mod for a, _, _ in segs], dtype=np.int32)
         P = ctypes.c_void_p * 3
         segp = P(*[h.data_ptr() for h in self.seg3_host])
         rowp = P(*[b.data_ptr() for b, _ in self.rows3])
         h = ctypes.c_void_p()
         L.call("tw_draw_pipe_start", self.rng._key, self.rng._pos, len(segs),
-               steps.ctypes.data, resh.ctypes.data, N, self.kx, self.kz, self.B, int(n_X),
-               int(n_Z), self.seg3_w, 3, segp, rowp, ctypes.byref(h))
-        return _NativeDraws(self, h, segs, N, kx, kz, (steps, resh, segp, rowp))
+               steps.ctypes.data, phase.ctypes.data, int(mod), N, self.kx, self.kz, self.B,
+               int(n_X), int(n_Z), self.seg3_w, 3, segp, rowp, ntab, ctypes.byref(h))
+        return _NativeDraws(self, h, segs, N, kx, kz, (steps, phase, segp, rowp))
+
+    def ship_tables(self, k, S, ntab, slot, eng):
+        """Main side, replay through reshuffles: buffer k's S steps of draws widened on the
+        device and its ntab row tables into eng's table stacks from `slot` on, in one launch
+        (tw_ship_draws_tables); returns the int64 device draws."""
+        sx, sz = eng._stacks
+        n = int(S) * 2 * self.N * self.B
+        L.call("tw_ship_draws_tables", ctypes.c_void_p(self.seg3_hdev[k]), self.seg3_w, n,
+               L.ptr(self.seg3_dev[k]), ctypes.c_void_p(self.rows3_hdev[k]), int(ntab),
+               sx[0].numel(), L.ptr(sx[slot]), sz[0].numel(), L.ptr(sz[slot]),
+               L.stream_handle())
+        return self.seg3_dev[k]
+
+    def table_capacity(self, n_X, n_Z) -> int:
+        """Row tables per segment when replaying through reshuffles: <= 32 MiB of int64 rows
+        per ring buffer."""
+        per = 8 * (self.N * int(n_X / self.N) + self.N * int(n_Z / self.N))
+        return int(max(1, (32 << 20) // per))
 
     def rows_uploaded(self, k):
         """Main side: the upload out of pinned row buffer k has been enqueued."""
@@ -1053,13 +1122,14 @@ class _NativeDraws:
         self.N, self.kx, self.kz = N, kx, kz
         self._keep = keep  # the arrays the native side reads
 
-    def wait(self, j):
+    def wait(self, j, rows=True):
         """Block (interpreter lock released) until segment j is drawn: (rows, k) as the
         Python worker returns them — rows = ((rows_x, rows_z) views, (pinned, device
-        address)) for a reshuffle, else None; k = the ring slot."""
+        address)) for a reshuffle, else None (always None with rows=False); k = the ring
+        slot."""
         L.call("tw_draw_pipe_wait", self.h, j)
         k = j % 3
-        if not self.segs[j][2]:
+        if not rows or not self.segs[j][2]:
             return None, k
         buf = self.draws.rows3[k][0]
         flat = buf.numpy()
@@ -1235,19 +1305,39 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
     (tests/test_gpu_learning*.py)."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     n_it, mod, eval_mod = p_learn["n_it"], p_learn["reshuffle_mod"], p_learn["eval_mod"]
+    draws._seg_buffers(3)
+    through = (REPLAY_THROUGH and NATIVE_DRAWS and isinstance(eng, SGDEngine)
+               and eng.replay_through_ok() and draws.seg3_w < 8
+               and draws.seg3_hdev[0] is not None)
     segs, i = [], 0
     while i < n_it:
-        nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
-                  i + draws.segment_capacity())
-        segs.append((i, nxt, i % mod == 0))
+        if through:
+            # segments end at evaluations and at capacity only: the reshuffles inside one go
+            # up with its draws and the kernel switches tables at their steps
+            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, i + draws.segment_capacity())
+            first = (mod - i % mod) % mod  # the segment's first reshuffle, from its start
+            nxt = min(nxt, i + first + draws.table_capacity(n_X, n_Z) * mod)
+            segs.append((i, nxt, (nxt - 1) // mod - (i - 1) // mod))
+        else:
+            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
+                      i + draws.segment_capacity())
+            segs.append((i, nxt, int(i % mod == 0)))
         i = nxt
 
     def run(wait, shipped):
         _replay_segments(eng, draws, segs, wait, shipped, X, Z, p_learn, loss, graphs, defer,
                          rows_x, rows_z)
 
+    if through:
+        eng.table_stacks(max([1] + [r for _, _, r in segs]))
+        pipe = draws.native_pipe(segs, n_X, n_Z, mod)
+        try:
+            _replay_through(eng, draws, segs, pipe, mod, p_learn, loss, graphs, defer, X, Z)
+        finally:
+            pipe.stop()
+        return
     if NATIVE_DRAWS:
-        pipe = draws.native_pipe(segs, n_X, n_Z)
+        pipe = draws.native_pipe(segs, n_X, n_Z, mod)
         try:
             run(pipe.wait, pipe.shipped)
         finally:
@@ -1347,6 +1437,34 @@ def _replay_segments(eng, draws, segs, wait, shipped, X, Z, p_learn, loss, graph
                     draws.rows_uploaded(k)
             else:
                 shipped(idx)
+
+
+def _replay_through(eng, draws, segs, pipe, mod, p_learn, loss, graphs, defer, X, Z):
+    """_replay_segments for segments running through their reshuffles (REPLAY_THROUGH; one
+    process, replicated X, the persistent narrow segment): per segment, its draws and the row
+    tables of every reshuffle inside it (drawn ahead in the reference's order by the native
+    worker) go up in one launch into the engine's table stacks — slot 0 when the segment starts
+    at a reshuffle, which the reference makes before it evaluates (make_exps.py:123-128), else
+    slots 1.. — then the evaluation (SAME_AS_BATCH reads slot 0), then one persistent launch
+    that switches tables at the reshuffle steps and leaves the last one in slot 0."""
+    eval_mod = p_learn["eval_mod"]
+    for idx, (i, nxt, ntab) in enumerate(segs):
+        if PIPE_STATS is not None:  # study hook (tools/time_replay_parts.py)
+            import time
+            t0 = time.perf_counter()
+            pipe.wait(idx, rows=False)
+            PIPE_STATS.append(time.perf_counter() - t0)
+        else:
+            pipe.wait(idx, rows=False)
+        k, phase = idx % 3, i % mod
+        buf = draws.ship_tables(k, nxt - i, ntab, 0 if phase == 0 else 1, eng)
+        pipe.shipped(idx)  # the only reader of the pinned buffers has been enqueued
+        if i % eval_mod == 0:
+            if defer is not None:  # device part enqueued now, host part later
+                _evaluate(i, eng, None, None, None, X, Z, p_learn, loss, graphs, defer)
+            else:
+                _evaluate(i, eng, eng.w_host(), None, None, X, Z, p_learn, loss, graphs)
+        eng.run_replay_segment(buf, nxt - i, graphs, k, tables=(phase, mod))
 
 
 def _evaluate(i, eng, w, rows_x, rows_z, X, Z, p_learn, loss, graphs, defer=None):
