@@ -404,8 +404,8 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
     """Pairwise-hinge SGD steps/s (BASELINE metric, second half): learning_process's loop
     (make_exps.py:122-141) without evaluation, device-RNG mode, hipGraph-replayed segments.
     Synthetic data of the given shape generated on the device.  layout="partitioned" also
-    times one reshuffle's row exchange (route + pack + unpack; at N=1 GPU the all_to_all is
-    the identity, so this is the HBM side of the exchange).  group: the ranks of the run (each
+    times one reshuffle's row exchange (row tables + route + pack of the remote rows + the
+    all_to_all; at one GPU every row is owned: the tables only).  group: the ranks of the run (each
     owns N/G shards; one all-gather of the shard gradients per step); check_prefix > 0: the
     first steps' w is compared with a one-rank engine's on rank 0 (bit for bit)."""
     import torch
@@ -495,10 +495,15 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
             rs = (time.perf_counter() - t0) / reps
         else:
             rs = span(resh)[0] / reps
-        rows = N * (eng.kx + eng.kz)
-        moved = rows * 8 * (2 * d + 2 * (d + 1))  # pack: read row, write record; unpack: back
-        out["reshuffle_exchange"] = {"ms": rs * 1e3, "rows": rows, "bytes": moved,
-                                     "GBps": moved / rs / 1e9}
+        rows = eng.N_loc * (eng.kx + eng.kz)  # this rank's drawn positions
+        remote = rows * (G - 1) // G  # expected rows owned elsewhere (the only ones that move)
+        # table write per position; a remote row: read in the partition, written with its
+        # position into the send bucket (the receive side writes it in place: RCCL's bytes)
+        moved = rows * 8 + remote * 8 * (2 * d + 1)
+        out["reshuffle_exchange"] = {"ms": rs * 1e3, "rows": rows, "remote_rows": remote,
+                                     "bytes": moved, "GBps": moved / rs / 1e9,
+                                     "note": "owned rows are read in place in the partition; "
+                                             "only remote rows travel (none at G = 1)"}
     return out
 
 
@@ -857,7 +862,8 @@ def tradeoff_curve(args, group, span, with_cpu):
     import torch
     out = {"note": "steps/s per reshuffle_mod (learning-experiment/main.py:20); device = "
                    "Philox draws + hipGraph segments, replay = NumPy's own MT19937 draws "
-                   "(bit-exact); C5 partitioned: every reshuffle exchanges the drawn rows",
+                   "(bit-exact); C5 partitioned: every reshuffle exchanges the drawn rows "
+                   "owned by other ranks (at G = 1: none, only new row tables)",
            "reshuffle_mod": list(RESHUFFLE_MODS)}
     c4d, c4r, cpu = {}, {}, {}
     for mod in RESHUFFLE_MODS:
@@ -879,8 +885,9 @@ def tradeoff_curve(args, group, span, with_cpu):
         progress(f"trade-off curve C5, reshuffle_mod {mod}")
         c5r[mod] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, mod, 200, 1, group=group,
                                    span=span, data=data)["steps_per_s"]
-        # a partitioned reshuffle moves ~n rows (41 GB at G = 1): few steps at mod 1
-        steps_p = 10 if mod == 1 else 50 if mod == 5 else 100
+        # a partitioned reshuffle moves the ~n (G-1)/G remote rows: fewer steps at mod 1, G > 1
+        G = 1 if group is None else torch.distributed.get_world_size(group)
+        steps_p = 200 if G == 1 else 10 if mod == 1 else 50 if mod == 5 else 100
         c5p[mod] = sgd_steps_per_s(C5_N, C5_N, 512, 256, 100, mod, steps_p, 1,
                                    layout="partitioned", group=group, span=span,
                                    data=data)["steps_per_s"]

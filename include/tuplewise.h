@@ -695,6 +695,32 @@ int tw_row_pack(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo, int64
                 const double* d_part, int64_t d, const int64_t* d_start, int64_t* d_cursor,
                 double* d_send, void* stream);
 int tw_row_unpack(const double* d_rec, int64_t m, int64_t d, double* d_out, void* stream);
+/* Remote rows only (the learning layout's default): this rank's matrix is [partition |
+ * receive area], and its row tables point into it — owned draws at their partition row, the
+ * others where the exchange lands them.  Nothing owned is copied; at G = 1 nothing moves.
+ * tw_row_route_remote_counts: tw_row_route_counts with d_counts[me] = 0 (me: this rank).
+ * tw_row_pack_remote: requester q's bucket starts at word d_start[q] of d_send and holds
+ *   d_count[q] rows (d doubles each; order unspecified) followed by their requester-local
+ *   positions (bit-cast int64), padded by the caller to whole rows: ceil(d_count[q] / d) * d
+ *   words.  d_cursor: G int64 of scratch.
+ * tw_row_table_local: d_table[i] = d_rows[i] - lo for this rank's M_q positions whose row it
+ *   owns (d_rows: its own slice of the draws), -1 for the others.
+ * tw_row_table_remote: for the `total` records received (source g's bucket at word
+ *   d_rstart[g] of d_recv, d_rcount[g] records, d_rprefix[g] = sum of the counts before g):
+ *   d_table[position] = base + d_rstart[g] / d + j for record j — d_recv being the receive
+ *   area of the matrix at row `base` (the partition's row count). */
+int tw_row_route_remote_counts(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo,
+                               int64_t hi, int32_t G, int32_t me, int64_t* d_counts,
+                               void* stream);
+int tw_row_pack_remote(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo, int64_t hi,
+                       int32_t G, int32_t me, const double* d_part, int64_t d,
+                       const int64_t* d_start, const int64_t* d_count, int64_t* d_cursor,
+                       double* d_send, void* stream);
+int tw_row_table_local(const int64_t* d_rows, int64_t M_q, int64_t lo, int64_t hi,
+                       int64_t* d_table, void* stream);
+int tw_row_table_remote(const double* d_recv, int32_t G, const int64_t* d_rstart,
+                        const int64_t* d_rcount, const int64_t* d_rprefix, int64_t total,
+                        int64_t d, int64_t base, int64_t* d_table, void* stream);
 
 /* ---- (e) single-process multi-device communicator (RCCL over xGMI) --------------------
  * The reference's workers are one serial in-process loop (compute_stats.py:71-91,
@@ -732,6 +758,10 @@ int tw_comm_set_timeout(int64_t ms);
  * tw_np_mt_next32: the raw genrand_int32 stream. */
 int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
                         const int64_t* high, const int64_t* cnt, int64_t* out);
+/* tw_np_randint_batch narrowed to uint16, for calls on [0, high) with high <= 65536 (SWR_divide's
+ * rows for the replay loop's narrowed row tables); 1 for any other call (state untouched). */
+int tw_np_randint_batch_u16(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
+                            const int64_t* high, const int64_t* cnt, uint16_t* out);
 int tw_np_mt_next32(uint32_t* key, int32_t* pos, int64_t cnt, uint32_t* out);
 /* grad_inc_block's draws for every shard of one UN_split call: for s < N, randint(0,kx,B)
  * into ix[s*B..] then randint(0,kz,B) into iz[s*B..].  Returns 1 if kx or kz <= 0. */
@@ -763,18 +793,20 @@ int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
                   const void* d_rows, int64_t nx, int64_t* d_rows_x, int64_t nz,
                   int64_t* d_rows_z, void* stream);
 /* tw_ship_draws for a segment running through reshuffles: d_rows holds ntab tables, each
- * [nx x words | nz z words], copied into ntab consecutive tables of the stacks d_rows_x
+ * [nx x values | nz z values] of row_width bytes (8: int64, 2: uint16, widened), copied into
+ * ntab consecutive tables of the stacks d_rows_x
  * (nx words apart) and d_rows_z (nz apart) — the input of tw_sgd_segment_narrow_tables. */
 int tw_ship_draws_tables(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
-                         const void* d_rows, int32_t ntab, int64_t nx, int64_t* d_rows_x,
-                         int64_t nz, int64_t* d_rows_z, void* stream);
+                         const void* d_rows, int32_t row_width, int32_t ntab, int64_t nx,
+                         int64_t* d_rows_x, int64_t nz, int64_t* d_rows_z, void* stream);
 /* The replay loop's draws made ahead on a native thread (csrc/drawpipe.hip): segment j of
  * n_seg (seg_steps[j] steps, its first step being step seg_phase[j] of a reshuffle period of
  * `mod` steps: a reshuffle before each of its steps k with (seg_phase[j] + k) % mod == 0) is
  * drawn from NumPy's MT19937 state (key/pos, advanced in place) into ring buffer j % nbuf, in
  * the reference's order: each reshuffle's SWR rows (make_exps.py:123-125,
  * compute_stats.py:48-54: N randint calls on [0, n_X) of n_X / N values, then N on [0, n_Z))
- * into the next of row_tabs tables of row_bufs[k] (int64, N * (n_X/N + n_Z/N) words each),
+ * into the next of row_tabs tables of row_bufs[k] (N * (n_X/N + n_Z/N) values each, of
+ * row_width bytes: 8 = int64, 2 = uint16 when n_X, n_Z <= 65536),
  * then the pairs (compute_stats.py:155-156) of the steps up to the next reshuffle into
  * seg_bufs[k] as (S, 2, N, B) values of `width` bytes (1, 2 or 8).  A segment with more
  * reshuffles than row_tabs fails the worker.  tw_draw_pipe_wait blocks until segment j is drawn; tw_draw_pipe_shipped records
@@ -784,8 +816,8 @@ int tw_ship_draws_tables(const void* d_in, int32_t width, int64_t n, int64_t* d_
 int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg, const int32_t* seg_steps,
                        const int32_t* seg_phase, int64_t mod, int32_t N, int64_t kx, int64_t kz,
                        int64_t B, int64_t n_X, int64_t n_Z, int32_t width, int32_t nbuf,
-                       void* const* seg_bufs, int64_t* const* row_bufs, int32_t row_tabs,
-                       void** out_handle);
+                       void* const* seg_bufs, void* const* row_bufs, int32_t row_tabs,
+                       int32_t row_width, void** out_handle);
 int tw_draw_pipe_wait(void* handle, int32_t j);
 int tw_draw_pipe_shipped(void* handle, int32_t j, void* stream);
 int tw_draw_pipe_stop(void* handle);

@@ -252,26 +252,31 @@ def test_native_draw_pipe_protocol(gpu):
     # segments running through reshuffles (replay_through): the same draws, a reshuffle's rows
     # before the pairs of its step, the tables one after another in the row buffer
     tsegs = [(0, 12, 3), (12, 13, 0), (13, 20, 1)]  # reshuffles at 0, 5, 10 | - | 15
-    np.random.seed(11)
-    d3 = lr._ReplayDraws(N, kx, kz, B)
-    with d3.rng:
-        pipe = d3.native_pipe(tsegs, n_X, n_Z, mod)
-        try:
-            tabs = []
-            for j, (a, b, r) in enumerate(tsegs):
-                pipe.wait(j, rows=False)
-                k = j % 3
-                per = N * kx + N * kz
-                tabs += [d3.rows3[k][0].numpy()[t * per:(t + 1) * per].copy() for t in range(r)]
-                if j == 0:
-                    got = d3.seg3_np[k][:12].copy()
-                    assert np.array_equal(got, np.concatenate([w[1] for w in want]))
-                pipe.shipped(j)
-        finally:
-            pipe.stop()
-    for t, w in zip(tabs[:3], (want[0][0], want[2][0], want[4][0])):
-        assert np.array_equal(t, w)
-    assert len(tabs) == 4
+    ends = []
+    for rw, view in ((8, np.int64), (2, np.uint16)):  # int64 tables, and narrowed to uint16
+        np.random.seed(11)
+        d3 = lr._ReplayDraws(N, kx, kz, B)
+        with d3.rng:
+            pipe = d3.native_pipe(tsegs, n_X, n_Z, mod, row_width=rw)
+            try:
+                tabs = []
+                for j, (a, b, r) in enumerate(tsegs):
+                    pipe.wait(j, rows=False)
+                    k = j % 3
+                    per = N * kx + N * kz
+                    flat = d3.rows3[k][0].numpy().view(view)
+                    tabs += [flat[t * per:(t + 1) * per].astype(np.int64) for t in range(r)]
+                    if j == 0:
+                        got = d3.seg3_np[k][:12].copy()
+                        assert np.array_equal(got, np.concatenate([w[1] for w in want]))
+                    pipe.shipped(j)
+            finally:
+                pipe.stop()
+        for t, w in zip(tabs[:3], (want[0][0], want[2][0], want[4][0])):
+            assert np.array_equal(t, w), rw
+        assert len(tabs) == 4
+        ends.append(np.random.get_state())
+    assert np.array_equal(ends[0][1], ends[1][1]) and ends[0][2] == ends[1][2]
     torch.cuda.synchronize()
     # stopped early: the worker waits for segment 0's buffer to be shipped, which never happens
     d2 = lr._ReplayDraws(N, kx, kz, B)
@@ -283,12 +288,12 @@ def test_native_draw_pipe_protocol(gpu):
     with pytest.raises(ValueError):
         L.call("tw_draw_pipe_start", d2.rng._key, d2.rng._pos, 1,
                np.array([1], np.int32).ctypes.data, np.array([0], np.int32).ctypes.data, 1,
-               N, 300, kz, B, 300 * N, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), 1,
+               N, 300, kz, B, 300 * N, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), 1, 8,
                ctypes_handle())
     with pytest.raises(ValueError):  # a phase outside the reshuffle period
         L.call("tw_draw_pipe_start", d2.rng._key, d2.rng._pos, 1,
                np.array([1], np.int32).ctypes.data, np.array([5], np.int32).ctypes.data, 5,
-               N, kx, kz, B, n_X, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), 1,
+               N, kx, kz, B, n_X, n_Z, 1, 3, P(*[0, 0, 0]), P(*[0, 0, 0]), 1, 8,
                ctypes_handle())
 
 

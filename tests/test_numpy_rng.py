@@ -311,3 +311,33 @@ def test_session_pairs_steps_u8_match_int64(tw, kx, kz):
     assert np.array_equal(got.astype(np.int64), want) and np.random.random() == probe
     with Session() as sess, pytest.raises(ValueError):
         sess.pairs_steps_u8(1, N, 257, kz, B, got)
+
+
+@pytest.mark.parametrize("highs", [[9117] * 5 + [702] * 5, [65536, 1, 2, 40000], [3]])
+def test_randint_batch_u16_matches_numpy(tw, highs):
+    """tw_np_randint_batch_u16 (SWR_divide's rows narrowed for the replay loop's uint16 row
+    tables; 64-word AVX-512 VBMI2 compaction where the host has it, else the int64 path
+    narrowed) == np.random.randint call for call, leaving the same RNG state; calls beyond
+    [0, 65536) are refused with the state untouched."""
+    from tuplewise import _lib as L
+    from tuplewise.numpy_rng import Session
+    cnt = np.array([37 + 11 * i for i in range(len(highs))], np.int64)
+    low = np.zeros(len(highs), np.int64)
+    high = np.array(highs, np.int64)
+    np.random.seed(31)
+    want = np.concatenate([np.random.randint(0, h, c) for h, c in zip(highs, cnt)])
+    probe = np.random.random()
+    np.random.seed(31)
+    got = np.empty(int(cnt.sum()), np.uint16)
+    with Session() as s:
+        assert L.lib().tw_np_randint_batch_u16(s._key, s._pos, len(highs), low.ctypes.data,
+                                               high.ctypes.data, cnt.ctypes.data,
+                                               got.ctypes.data) == 0
+    assert np.array_equal(got.astype(np.int64), want) and np.random.random() == probe
+    bad = np.array([65537], np.int64)
+    np.random.seed(31)
+    with Session() as s:
+        assert L.lib().tw_np_randint_batch_u16(s._key, s._pos, 1, low.ctypes.data,
+                                               bad.ctypes.data, cnt.ctypes.data,
+                                               got.ctypes.data) == 1
+    assert np.random.randint(0, highs[0], int(cnt[0]))[0] == want[0]

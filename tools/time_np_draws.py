@@ -21,6 +21,24 @@ best = 1e9
 for _ in range(30):
     t0 = time.perf_counter(); s.pairs_steps_u16(25, 100, 91, 7, 100, o16); best = min(best, time.perf_counter() - t0)
 print("uint16 %.2f us/step" % (best / 25 * 1e6))
+o8 = np.empty((25, 2, 100, 100), np.uint8)
+best = 1e9
+for _ in range(30):
+    t0 = time.perf_counter(); s.pairs_steps_u8(25, 100, 91, 7, 100, o8); best = min(best, time.perf_counter() - t0)
+print("uint8 %.2f us/step" % (best / 25 * 1e6))
+# one reshuffle's SWR_divide rows at C4 (100 calls of 91 on [0, 9117), 100 of 7 on [0, 702))
+lo = np.zeros(200, np.int64); hi = np.array([9117] * 100 + [702] * 100, np.int64)
+cnt = np.array([91] * 100 + [7] * 100, np.int64); rows = np.empty(9800, np.int64)
+best = 1e9
+for _ in range(300):
+    t0 = time.perf_counter(); s.randint_flat(lo, hi, cnt, out=rows); best = min(best, time.perf_counter() - t0)
+print("SWR rows %.2f us/reshuffle (incl. the Python call)" % (best * 1e6))
+from tuplewise import _lib as L
+r16 = np.empty(9800, np.uint16); f = L.lib().tw_np_randint_batch_u16
+best = 1e9
+for _ in range(300):
+    t0 = time.perf_counter(); f(s._key, s._pos, 200, lo.ctypes.data, hi.ctypes.data, cnt.ctypes.data, r16.ctypes.data); best = min(best, time.perf_counter() - t0)
+print("SWR rows uint16 %.2f us/reshuffle (incl. the ctypes call)" % (best * 1e6))
 '''
 for label, env in (("widest", {}), ("avx2", {"TW_NP_RNG_ISA": "avx2"}),
                    ("portable", {"TW_NP_RNG_SCALAR": "1"})):

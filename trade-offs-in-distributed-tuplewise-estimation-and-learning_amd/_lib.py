@@ -146,6 +146,11 @@ _SIGNATURES = {
     "tw_row_route_counts": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
     "tw_row_pack": [_vp, _i64, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "tw_row_unpack": [_vp, _i64, _i64, _vp, _vp],
+    "tw_row_route_remote_counts": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp],
+    "tw_row_pack_remote": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _vp,
+                           _vp, _vp],
+    "tw_row_table_local": [_vp, _i64, _i64, _i64, _vp, _vp],
+    "tw_row_table_remote": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "tw_comm_init": [_i32, _vp, _vp],
     "tw_comm_destroy": [_i32],
     "tw_allgather_u64": [_i32, _vp, _vp, _i64, _vp],
@@ -165,8 +170,9 @@ _SIGNATURES = {
                       _vp, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "tw_ship_draws": [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp],
     "tw_draw_pipe_start": [_vp, _vp, _i32, _vp, _vp, _i64, _i32, _i64, _i64, _i64, _i64, _i64,
-                           _i32, _i32, _vp, _vp, _i32, _vp],
-    "tw_ship_draws_tables": [_vp, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _i64, _vp, _vp],
+                           _i32, _i32, _vp, _vp, _i32, _i32, _vp],
+    "tw_ship_draws_tables": [_vp, _i32, _i64, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp],
+    "tw_np_randint_batch_u16": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
     "tw_draw_pipe_wait": [_vp, _i32],
     "tw_draw_pipe_shipped": [_vp, _i32, _vp],
     "tw_draw_pipe_stop": [_vp],

@@ -30,11 +30,12 @@ struct DrawPipe {
   std::vector<int32_t> phase;  // step of the reshuffle period at each segment's first step
   int64_t mod;                 // reshuffle period (steps)
   int32_t row_tabs;            // row tables per row buffer
+  int32_t row_width;           // bytes per row value: 8 (int64) or 2 (uint16)
   int32_t N;
   int64_t kx, kz, B, n_X, n_Z;
   int32_t width, nbuf;
   std::vector<void*> seg_bufs;
-  std::vector<int64_t*> row_bufs;
+  std::vector<char*> row_bufs;
   std::vector<hipEvent_t> shipped_ev;
   std::vector<int64_t> row_low, row_high, row_cnt;
 
@@ -69,8 +70,12 @@ struct DrawPipe {
             r = 1;
             break;
           }
-          r = tw_np_randint_batch(key, pos, 2 * N, row_low.data(), row_high.data(),
-                                  row_cnt.data(), row_bufs[k] + tabs * wtab);
+          char* dst = row_bufs[k] + (int64_t)tabs * wtab * row_width;
+          r = row_width == 2
+                  ? tw_np_randint_batch_u16(key, pos, 2 * N, row_low.data(), row_high.data(),
+                                            row_cnt.data(), (uint16_t*)dst)
+                  : tw_np_randint_batch(key, pos, 2 * N, row_low.data(), row_high.data(),
+                                        row_cnt.data(), (int64_t*)dst);
           ++tabs;
           if (r) break;
         }
@@ -115,8 +120,8 @@ extern "C" int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg,
                                   const int32_t* seg_steps, const int32_t* seg_phase,
                                   int64_t mod, int32_t N, int64_t kx, int64_t kz, int64_t B,
                                   int64_t n_X, int64_t n_Z, int32_t width, int32_t nbuf,
-                                  void* const* seg_bufs, int64_t* const* row_bufs,
-                                  int32_t row_tabs, void** out_handle) {
+                                  void* const* seg_bufs, void* const* row_bufs,
+                                  int32_t row_tabs, int32_t row_width, void** out_handle) {
   TW_ARG_CHECK(key && pos && out_handle && n_seg >= 0 && N >= 0 && B >= 0 && mod >= 1 &&
                    row_tabs >= 1 && (n_seg == 0 || (seg_steps && seg_phase)),
                "tw_draw_pipe_start: bad arguments");
@@ -127,6 +132,9 @@ extern "C" int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg,
   TW_ARG_CHECK(nbuf >= 1 && nbuf <= 16 && seg_bufs && row_bufs, "tw_draw_pipe_start: buffers");
   TW_ARG_CHECK(width == 1 || width == 2 || width == 8, "tw_draw_pipe_start: width 1, 2 or 8");
   TW_ARG_CHECK(kx >= 1 && kz >= 1 && n_X >= 1 && n_Z >= 1, "tw_draw_pipe_start: empty ranges");
+  TW_ARG_CHECK(row_width == 8 || (row_width == 2 && n_X <= 65536 && n_Z <= 65536),
+               "tw_draw_pipe_start: row width %d (uint16 rows need n_X, n_Z <= 65536)",
+               row_width);
   TW_ARG_CHECK((width != 1 || (kx <= 256 && kz <= 256)) &&
                    (width != 2 || (kx <= 65536 && kz <= 65536)),
                "tw_draw_pipe_start: indices do not fit the width");
@@ -137,6 +145,7 @@ extern "C" int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg,
   p->phase.assign(seg_phase, seg_phase + n_seg);
   p->mod = mod;
   p->row_tabs = row_tabs;
+  p->row_width = row_width;
   p->N = N;
   p->kx = kx;
   p->kz = kz;
@@ -146,7 +155,7 @@ extern "C" int tw_draw_pipe_start(uint32_t* key, int32_t* pos, int32_t n_seg,
   p->width = width;
   p->nbuf = nbuf;
   p->seg_bufs.assign(seg_bufs, seg_bufs + nbuf);
-  p->row_bufs.assign(row_bufs, row_bufs + nbuf);
+  for (int k = 0; k < nbuf; ++k) p->row_bufs.push_back((char*)row_bufs[k]);
   // SWR_divide's calls: N on [0, n_X) of n_X / N values, then N on [0, n_Z) of n_Z / N
   for (int s = 0; s < 2 * N; ++s) {
     p->row_low.push_back(0);

@@ -819,11 +819,11 @@ extern "C" int tw_ship_draws(const void* d_in, int32_t width, int64_t n, int64_t
 // A replay segment through reshuffles: its narrowed pair draws widened (as k_ship) and ntab row
 // tables, laid out [x rows | z rows] per table in the mapped pinned buffer, into consecutive
 // tables of the device stacks (x tables nx words apart, z tables nz apart), in one launch.
-template <typename T>
+template <typename T, typename R>
 static __global__ __launch_bounds__(256) void k_ship_tables(
     const T* __restrict__ in, int64_t n, int64_t* __restrict__ out,
-    const uint64_t* __restrict__ rows, int ntab, int64_t nx, uint64_t* __restrict__ rows_x,
-    int64_t nz, uint64_t* __restrict__ rows_z, int gw) {
+    const R* __restrict__ rows, int ntab, int64_t nx, int64_t* __restrict__ rows_x,
+    int64_t nz, int64_t* __restrict__ rows_z, int gw) {
   if ((int)blockIdx.x < gw) {
     constexpr int U = 16 / (int)sizeof(T);
     const int64_t nv = n / U;
@@ -843,18 +843,34 @@ static __global__ __launch_bounds__(256) void k_ship_tables(
   for (int64_t i = (int64_t)(blockIdx.x - gw) * 256 + threadIdx.x; i < tot;
        i += (int64_t)(gridDim.x - gw) * 256) {
     const int64_t t = i / per, j = i - t * per;
+    const int64_t v = (int64_t)rows[i];
     if (j < nx)
-      rows_x[t * nx + j] = rows[i];
+      rows_x[t * nx + j] = v;
     else
-      rows_z[t * nz + (j - nx)] = rows[i];
+      rows_z[t * nz + (j - nx)] = v;
   }
 }
 
+template <typename R>
+static void ship_tables_launch(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
+                               const void* d_rows, int32_t ntab, int64_t nx, int64_t* d_rows_x,
+                               int64_t nz, int64_t* d_rows_z, int gw, int gr, hipStream_t st) {
+  if (width == 1)
+    hipLaunchKernelGGL((k_ship_tables<uint8_t, R>), dim3(gw + gr), dim3(256), 0, st,
+                       (const uint8_t*)d_in, n, d_out, (const R*)d_rows, (int)ntab, nx,
+                       d_rows_x, nz, d_rows_z, gw);
+  else
+    hipLaunchKernelGGL((k_ship_tables<uint16_t, R>), dim3(gw + gr), dim3(256), 0, st,
+                       (const uint16_t*)d_in, n, d_out, (const R*)d_rows, (int)ntab, nx,
+                       d_rows_x, nz, d_rows_z, gw);
+}
+
 extern "C" int tw_ship_draws_tables(const void* d_in, int32_t width, int64_t n, int64_t* d_out,
-                                    const void* d_rows, int32_t ntab, int64_t nx,
-                                    int64_t* d_rows_x, int64_t nz, int64_t* d_rows_z,
-                                    void* stream) {
+                                    const void* d_rows, int32_t row_width, int32_t ntab,
+                                    int64_t nx, int64_t* d_rows_x, int64_t nz,
+                                    int64_t* d_rows_z, void* stream) {
   TW_ARG_CHECK(width == 1 || width == 2, "tw_ship_draws_tables: width must be 1 or 2");
+  TW_ARG_CHECK(row_width == 2 || row_width == 8, "tw_ship_draws_tables: row_width 2 or 8");
   TW_ARG_CHECK(n >= 0 && nx >= 0 && nz >= 0 && ntab >= 0, "tw_ship_draws_tables: negative size");
   TW_ARG_CHECK(n == 0 || (d_in != nullptr && d_out != nullptr), "tw_ship_draws_tables: draws");
   TW_ARG_CHECK(ntab == 0 || nx + nz == 0 ||
@@ -865,14 +881,12 @@ extern "C" int tw_ship_draws_tables(const void* d_in, int32_t width, int64_t n, 
   const int64_t tot = (nx + nz) * ntab;
   const int gr = tot > 0 ? (int)std::min<int64_t>(512, ceil_div(tot, 256)) : 0;
   if (gw + gr == 0) return TW_OK;
-  if (width == 1)
-    hipLaunchKernelGGL(k_ship_tables<uint8_t>, dim3(gw + gr), dim3(256), 0, (hipStream_t)stream,
-                       (const uint8_t*)d_in, n, d_out, (const uint64_t*)d_rows, (int)ntab, nx,
-                       (uint64_t*)d_rows_x, nz, (uint64_t*)d_rows_z, gw);
+  if (row_width == 2)
+    ship_tables_launch<uint16_t>(d_in, width, n, d_out, d_rows, ntab, nx, d_rows_x, nz,
+                                 d_rows_z, gw, gr, (hipStream_t)stream);
   else
-    hipLaunchKernelGGL(k_ship_tables<uint16_t>, dim3(gw + gr), dim3(256), 0, (hipStream_t)stream,
-                       (const uint16_t*)d_in, n, d_out, (const uint64_t*)d_rows, (int)ntab, nx,
-                       (uint64_t*)d_rows_x, nz, (uint64_t*)d_rows_z, gw);
+    ship_tables_launch<uint64_t>(d_in, width, n, d_out, d_rows, ntab, nx, d_rows_x, nz,
+                                 d_rows_z, gw, gr, (hipStream_t)stream);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

@@ -702,6 +702,74 @@ fill_masked64_u8(MT& mt, uint32_t mask, uint32_t r32, int64_t cnt, uint8_t* out)
   }
 }
 
+// fill_masked64_u8 with uint16 output (every value < 65536): SWR_divide's row draws for the
+// replay loop's narrowed row tables.  Same words consumed, same values.
+__attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) inline void
+fill_masked64_u16(MT& mt, uint32_t mask, uint32_t r32, int64_t cnt, uint16_t* out) {
+  const __m512i vm = _mm512_set1_epi32((int)mask);
+  const __m512i vr = _mm512_set1_epi32((int)r32);
+  int64_t o = 0;
+  while (o < cnt) {
+    if (mt.pos >= kN) generate_isa<2>(mt);
+    mt.temper_rest();
+    int p = mt.pos;
+    while (p < kN && o < cnt) {
+      const int w = kN - p < 64 ? kN - p : 64;
+      __m512i v[4];
+      uint64_t acc = 0;
+#pragma GCC unroll 4
+      for (int g = 0; g < 4; ++g) {
+        const int lanes = w - 16 * g;
+        const __mmask16 lm = lanes >= 16  ? (__mmask16)0xFFFF
+                             : lanes > 0 ? (__mmask16)((1u << lanes) - 1u)
+                                         : (__mmask16)0;
+        v[g] = _mm512_and_si512(_mm512_maskz_loadu_epi32(lm, mt.tmp + p + 16 * g), vm);
+        acc |= (uint64_t)_mm512_mask_cmple_epu32_mask(lm, v[g], vr) << (16 * g);
+      }
+      const int64_t rem = cnt - o;
+      int na = __builtin_popcountll(acc);
+      int used = w;
+      if (na >= rem) {
+        if (na > rem) acc = _pdep_u64((1ull << rem) - 1ull, acc);
+        na = (int)rem;
+        used = 64 - __builtin_clzll(acc);
+      }
+      int off = 0;
+#pragma GCC unroll 4
+      for (int g = 0; g < 4; ++g) {
+        const __mmask16 mg = (__mmask16)(acc >> (16 * g));
+        const int cg = __builtin_popcount((unsigned)mg);
+        const __m256i packed = _mm256_maskz_compress_epi16(mg, _mm512_cvtepi32_epi16(v[g]));
+        _mm256_mask_storeu_epi16((void*)(out + o + off), (__mmask16)((1u << cg) - 1u), packed);
+        off += cg;
+      }
+      o += na;
+      p += used;
+    }
+    mt.pos = p;
+  }
+}
+
+__attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) int
+batch_u16_avx512(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* high,
+                 const int64_t* cnt, uint16_t* out) {
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  int64_t o = 0;
+  for (int32_t c = 0; c < n_calls; ++c) {
+    const uint64_t rng = (uint64_t)(high[c] - 1);
+    if (rng == 0) {
+      for (int64_t i = 0; i < cnt[c]; ++i) out[o + i] = 0;
+    } else {
+      fill_masked64_u16(mt, (uint32_t)gen_mask(rng), (uint32_t)rng, cnt[c], out + o);
+    }
+    o += cnt[c];
+  }
+  *pos = mt.pos;
+  return 0;
+}
+
 __attribute__((target("avx2,avx512f,avx512vl,avx512bw,avx512vbmi2,popcnt,bmi2"))) void
 pairs_u8_avx512(uint32_t* key, int32_t* pos, int32_t N, int64_t kx, int64_t kz, int64_t B,
                 uint8_t* ix, uint8_t* iz) {
@@ -763,6 +831,24 @@ int tw_np_randint_batch(uint32_t* key, int32_t* pos, int32_t n_calls, const int6
   return isa == 2   ? batch_avx512(key, pos, n_calls, low, high, cnt, out)
          : isa == 1 ? batch_avx2(key, pos, n_calls, low, high, cnt, out)
                     : batch_generic(key, pos, n_calls, low, high, cnt, out);
+}
+
+// tw_np_randint_batch narrowed to uint16 for calls on [0, high) with high <= 65536 (SWR_divide's
+// rows of the replay loop's narrowed row tables): the same words consumed, the same values.
+// Returns 1 for a call outside that form (state untouched).
+int tw_np_randint_batch_u16(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* low,
+                            const int64_t* high, const int64_t* cnt, uint16_t* out) {
+  for (int32_t c = 0; c < n_calls; ++c)
+    if (low[c] != 0 || high[c] < 1 || high[c] > 65536 || cnt[c] < 0) return 1;
+  if (has_vbmi2()) return batch_u16_avx512(key, pos, n_calls, high, cnt, out);
+  static thread_local std::vector<int64_t> scratch;
+  int64_t tot = 0;
+  for (int32_t c = 0; c < n_calls; ++c) tot += cnt[c];
+  scratch.resize((size_t)tot);
+  const int rc = tw_np_randint_batch(key, pos, n_calls, low, high, cnt, scratch.data());
+  if (rc) return rc;
+  for (int64_t i = 0; i < tot; ++i) out[i] = (uint16_t)scratch[(size_t)i];
+  return 0;
 }
 
 // grad_inc_block's draws for all N shards of one UN_split call (compute_stats.py:155-156):

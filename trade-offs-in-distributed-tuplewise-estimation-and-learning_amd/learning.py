@@ -126,14 +126,16 @@ class SGDEngine:
             G, r = self.G, self.rank
             self.x_own = (r * self.n_X // G, (r + 1) * self.n_X // G)
             self.z_own = (r * self.n_Z // G, (r + 1) * self.n_Z // G)
-            self.X_part = _dev_f64(X[self.x_own[0]:self.x_own[1]]).reshape(-1, self.d)
-            self.Z_part = _dev_f64(Z[self.z_own[0]:self.z_own[1]]).reshape(-1, self.d)
-            # the kernels read the shard-local matrices through identity row tables
-            self.X = L.empty((self.N_loc * self.kx, self.d), t.float64)
-            self.Z = L.empty((self.N_loc * self.kz, self.d), t.float64)
+            # each side's matrix is [this rank's partition | receive area]: owned draws are read
+            # in the partition, remote ones where the exchange lands them (csrc/exchange.hip);
+            # the row tables (partition_tables) point into it
+            self.X = self._side_matrix(X[self.x_own[0]:self.x_own[1]], self.kx)
+            self.Z = self._side_matrix(Z[self.z_own[0]:self.z_own[1]], self.kz)
+            self.X_part = self.X[:self.x_own[1] - self.x_own[0]]
+            self.Z_part = self.Z[:self.z_own[1] - self.z_own[0]]
             dev = self.X.device
-            self.ident_x = t.arange(self.N_loc * self.kx, device=dev).view(self.N_loc, self.kx)
-            self.ident_z = t.arange(self.N_loc * self.kz, device=dev).view(self.N_loc, self.kz)
+            self.tab_x = t.zeros((self.N_loc, self.kx), dtype=t.int64, device=dev)
+            self.tab_z = t.zeros((self.N_loc, self.kz), dtype=t.int64, device=dev)
         self.margin, self.reg, self.lr = float(margin), float(reg), float(learning_rate)
         self.loss = cs._loss_codes(loss)[1]
         if gradient not in ("incomplete", "complete"):
@@ -291,11 +293,9 @@ class SGDEngine:
     def set_shards(self, rows_x, rows_z):
         """Replay mode: the full SWR draw (all N shards; identical on every rank)."""
         if self.layout == "partitioned":
-            self._exchange(L.to_device(np.stack(rows_x).astype(np.int64).reshape(-1)), self.kx,
-                           self.X_part, self.x_own, self.X)
-            self._exchange(L.to_device(np.stack(rows_z).astype(np.int64).reshape(-1)), self.kz,
-                           self.Z_part, self.z_own, self.Z)
-            self.rows_x, self.rows_z = self.ident_x, self.ident_z
+            self._exchange(L.to_device(np.stack(rows_x).astype(np.int64).reshape(-1)), 0)
+            self._exchange(L.to_device(np.stack(rows_z).astype(np.int64).reshape(-1)), 1)
+            self.rows_x, self.rows_z = self.tab_x, self.tab_z
             return
         # copied into persistent tables (captured replay graphs keep valid pointers) through a
         # pinned staging buffer, asynchronously: the host does not wait for queued steps
@@ -359,46 +359,88 @@ class SGDEngine:
         return (hdev, self.N * self.kx, L.ptr(self.rows_x), self.N * self.kz,
                 L.ptr(self.rows_z))
 
-    def _records(self, name, rows, expect):
-        """Persistent (rows, d+1) record buffer for the row exchange, kept across reshuffles
-        and grown with headroom only when a draw needs more: a fresh ~n*d*8-byte allocation
-        per reshuffle made the caching allocator flush and re-map (a 1 s stall at C5)."""
+    def _side_matrix(self, part, k, remote=None):
+        """One side's device matrix of the partitioned layout: the partition's rows, then room
+        for `remote` received rows (default: the expected count with headroom, none at G = 1)
+        — a remote row takes its d doubles, each sender's positions ceil(c / d) rows more."""
+        t = self.t
+        n_own = int(part.shape[0])
+        if remote is None:
+            M_q = self.N_loc * k
+            remote = (0 if self.G == 1 else
+                      M_q * (self.G - 1) // self.G + M_q // 16 + M_q // self.d + 2 * self.G)
+        m = L.empty((n_own + remote, self.d), t.float64)
+        if isinstance(part, t.Tensor):
+            m[:n_own].copy_(part)
+        else:
+            m[:n_own].copy_(t.from_numpy(np.ascontiguousarray(part, dtype=np.float64)).reshape(
+                n_own, self.d))
+        return m
+
+    def _records(self, name, words):
+        """Persistent flat float64 send buffer for the row exchange, kept across reshuffles and
+        grown with headroom only when a draw needs more (a fresh allocation per reshuffle made
+        the caching allocator flush and re-map: a 1 s stall at C5)."""
         bufs = self.__dict__.setdefault("_xbufs", {})
         b = bufs.get(name)
-        if b is None or b.shape[0] < rows:
+        if b is None or b.shape[0] < words:
             bufs[name] = None  # release the old block first
-            cap = max(rows, expect + (expect // 16 if self.G > 1 else 0), 1)
-            b = bufs[name] = L.empty((cap, self.d + 1), self.t.float64)
-        return b[:max(rows, 1)]
+            b = bufs[name] = L.empty((max(words + words // 16, 1),), self.t.float64)
+        return b
 
-    def _exchange(self, rows, k, part, own, out):
-        """Partitioned layout: move the rows drawn for this rank's shards (rows: all N*k global
-        row indices, shard-major) from their owners into `out` (N_loc*k, d), in draw order."""
+    def _exchange(self, rows, side):
+        """Partitioned layout, at a reshuffle: this rank's row table for `side` (0 = X, 1 = Z)
+        from the global draws `rows` (all N*k global row indices, shard-major).  Owned rows are
+        read in place in the partition; only rows owned by other ranks travel (one all_to_all
+        of [rows | positions] buckets) and stay where they land in the receive area — no unpack
+        pass, and at G = 1 nothing moves (compute_stats.py:48-54's copies become tables)."""
         t, G, d = self.t, self.G, self.d
         s = L.stream_handle()
+        k = self.kx if side == 0 else self.kz
+        lo, hi = self.x_own if side == 0 else self.z_own
+        table = self.tab_x if side == 0 else self.tab_z
+        n_own = hi - lo
         M, M_q = self.N * k, self.N_loc * k
+        mine = rows[self.rank * M_q:(self.rank + 1) * M_q]
+        L.call("tw_row_table_local", L.ptr(mine), M_q, lo, hi, L.ptr(table), s)
+        if G == 1:
+            return
+        part = self.X_part if side == 0 else self.Z_part
         counts = L.empty((G,), t.int64)
-        L.call("tw_row_route_counts", L.ptr(rows), M, M_q, own[0], own[1], G, L.ptr(counts), s)
-        start = t.cumsum(counts, 0) - counts
-        sc = counts.cpu().tolist()
-        total = int(sum(sc))
-        send = self._records("send", total, M_q)
+        L.call("tw_row_route_remote_counts", L.ptr(rows), M, M_q, lo, hi, G, self.rank,
+               L.ptr(counts), s)
+        rcounts = t.empty_like(counts)
+        self.dist.all_to_all_single(rcounts, counts, group=self.group)
+        both = t.stack([counts, rcounts]).cpu().tolist()
+        sc, rc = both
+
+        def layout(cs):  # per bucket: c rows of d words, then c positions padded to rows
+            words = [c * d + -(-c // d) * d for c in cs]
+            start = np.concatenate([[0], np.cumsum(words)[:-1]]).astype(np.int64)
+            return words, start
+
+        swords, sstart = layout(sc)
+        rwords, rstart = layout(rc)
+        send = self._records("send", int(sum(swords)))
         cursor = L.empty((G,), t.int64)
-        L.call("tw_row_pack", L.ptr(rows), M, M_q, own[0], own[1], G, L.ptr(part), d,
-               L.ptr(start), L.ptr(cursor), L.ptr(send), s)
-        if G > 1:
-            rcounts = t.empty_like(counts)
-            self.dist.all_to_all_single(rcounts, counts, group=self.group)
-            rc = rcounts.cpu().tolist()
-            recv = self._records("recv", int(sum(rc)), M_q)
-            self.dist.all_to_all_single(recv[:int(sum(rc))], send[:total], output_split_sizes=rc,
-                                        input_split_sizes=sc, group=self.group)
-            m = int(sum(rc))
-        else:
-            recv, m = send, total
-        if m != M_q:
-            raise RuntimeError(f"row exchange delivered {m} rows for {M_q} positions")
-        L.call("tw_row_unpack", L.ptr(recv), m, d, L.ptr(out), s)
+        L.call("tw_row_pack_remote", L.ptr(rows), M, M_q, lo, hi, G, self.rank, L.ptr(part), d,
+               L.ptr(L.to_device(sstart)), L.ptr(counts), L.ptr(cursor), L.ptr(send), s)
+        mat = self.X if side == 0 else self.Z
+        need = n_own + int(sum(rwords)) // d
+        if need > mat.shape[0]:  # more remote rows than the receive area holds: grow it
+            mat = self._side_matrix(part, k, remote=need - n_own + need // 16)
+            if side == 0:
+                self.X, self.X_part = mat, mat[:n_own]
+            else:
+                self.Z, self.Z_part = mat, mat[:n_own]
+            self._graphs, self._replay_graphs = {}, {}  # they hold the old matrix's address
+        recv = mat.view(-1)[n_own * d:n_own * d + int(sum(rwords))]
+        self.dist.all_to_all_single(recv, send[:int(sum(swords))], output_split_sizes=rwords,
+                                    input_split_sizes=swords, group=self.group)
+        rprefix = np.concatenate([[0], np.cumsum(rc)]).astype(np.int64)
+        L.call("tw_row_table_remote", L.ptr(recv), G, L.ptr(L.to_device(rstart)),
+               L.ptr(rcounts), L.ptr(L.to_device(rprefix)), int(rprefix[-1]), d, n_own,
+               L.ptr(table), s)
 
     def _update(self):
         if self.vgroup is not None:  # MultiDeviceSGD gathers the slots' gradients, then updates
@@ -507,8 +549,6 @@ class SGDEngine:
         or None, N, kx, kz) on the device (one process only; None with several ranks)."""
         if self.G > 1 or self.rows_x is None:
             return None
-        if self.layout == "partitioned":  # X / Z hold the shards' rows in draw order
-            return (self.X, self.Z, None, None, self.N, self.kx, self.kz)
         return (self.X, self.Z, self.rows_x, self.rows_z, self.N, self.kx, self.kz)
 
     def w_host(self) -> np.ndarray:
@@ -542,7 +582,7 @@ class SGDEngine:
         if self.layout == "partitioned":  # owners need every shard's draws
             self.rows_all_x = t.empty((self.N, self.kx), dtype=t.int64, device=self.w.device)
             self.rows_all_z = t.empty((self.N, self.kz), dtype=t.int64, device=self.w.device)
-            self.rows_x, self.rows_z = self.ident_x, self.ident_z
+            self.rows_x, self.rows_z = self.tab_x, self.tab_z
         else:
             self.rows_x = t.empty((self.N_loc, self.kx), dtype=t.int64, device=self.w.device)
             self.rows_z = t.empty((self.N_loc, self.kz), dtype=t.int64, device=self.w.device)
@@ -552,8 +592,8 @@ class SGDEngine:
         """run_segment(nsteps, swr_mod=) applies: device RNG, one process, replicated rows,
         the incomplete gradient, and a kernel that draws the rows — the persistent narrow
         segment (nsteps > 1) or the per-step gradient launches of wide rows."""
-        if (getattr(self, "seed", None) is None or self.G != 1 or self.layout != "replicated"
-                or self.complete):
+        # (partitioned at G = 1: the partition is all of X and the tables are the draws)
+        if getattr(self, "seed", None) is None or self.G != 1 or self.complete:
             return False
         if self.narrow_seg:
             return nsteps > 1
@@ -578,8 +618,8 @@ class SGDEngine:
                    self.seed, L.ptr(self.step_ctr), 0, 0, s)
             L.call("tw_swr_rows_rng", L.ptr(self.rows_all_z), self.N, self.kz, self.n_Z,
                    self.seed, L.ptr(self.step_ctr), 1, 0, s)
-            self._exchange(self.rows_all_x.view(-1), self.kx, self.X_part, self.x_own, self.X)
-            self._exchange(self.rows_all_z.view(-1), self.kz, self.Z_part, self.z_own, self.Z)
+            self._exchange(self.rows_all_x.view(-1), 0)
+            self._exchange(self.rows_all_z.view(-1), 1)
             return
         L.call("tw_swr_rows_rng", L.ptr(self.rows_x), self.N_loc, self.kx, self.n_X, self.seed,
                L.ptr(self.step_ctr), 0, self.shard_base, s)
@@ -955,11 +995,12 @@ class _ReplayDraws:
             self.rows3_hdev = [L.host_device_pointer(b) for b, _ in self.rows3]
         return N, kx, kz
 
-    def native_pipe(self, segs, n_X, n_Z, mod):
+    def native_pipe(self, segs, n_X, n_Z, mod, row_width=8):
         """The loop's draws made ahead by a native thread (tw_draw_pipe_*, csrc/drawpipe.hip)
         into the ring of pinned segment and row buffers: segs = [(i, nxt, ntab)] — ntab row
         tables in segment [i, nxt) (its reshuffles: the steps i + k with (i + k) % mod == 0;
-        a segment cut at reshuffles has ntab 1 when it starts at one, else 0)."""
+        a segment cut at reshuffles has ntab 1 when it starts at one, else 0).  row_width 2:
+        the tables drawn as uint16 (n_X, n_Z <= 65536; ship_tables widens them)."""
         t = L.torch()
         self._seg_buffers(3)
         ntab = max([1] + [int(r) for _, _, r in segs])
@@ -973,7 +1014,9 @@ class _ReplayDraws:
         h = ctypes.c_void_p()
         L.call("tw_draw_pipe_start", self.rng._key, self.rng._pos, len(segs),
                steps.ctypes.data, phase.ctypes.data, int(mod), N, self.kx, self.kz, self.B,
-               int(n_X), int(n_Z), self.seg3_w, 3, segp, rowp, ntab, ctypes.byref(h))
+               int(n_X), int(n_Z), self.seg3_w, 3, segp, rowp, ntab, int(row_width),
+               ctypes.byref(h))
+        self.rows3_rw = int(row_width)
         return _NativeDraws(self, h, segs, N, kx, kz, (steps, phase, segp, rowp))
 
     def ship_tables(self, k, S, ntab, slot, eng):
@@ -983,7 +1026,8 @@ class _ReplayDraws:
         sx, sz = eng._stacks
         n = int(S) * 2 * self.N * self.B
         L.call("tw_ship_draws_tables", ctypes.c_void_p(self.seg3_hdev[k]), self.seg3_w, n,
-               L.ptr(self.seg3_dev[k]), ctypes.c_void_p(self.rows3_hdev[k]), int(ntab),
+               L.ptr(self.seg3_dev[k]), ctypes.c_void_p(self.rows3_hdev[k]), self.rows3_rw,
+               int(ntab),
                sx[0].numel(), L.ptr(sx[slot]), sz[0].numel(), L.ptr(sz[slot]),
                L.stream_handle())
         return self.seg3_dev[k]
@@ -1134,7 +1178,8 @@ class _NativeDraws:
         buf = self.draws.rows3[k][0]
         flat = buf.numpy()
         N, kx = self.N, self.kx
-        return ((flat[:N * kx].reshape(N, kx), flat[N * kx:].reshape(N, self.kz)),
+        return ((flat[:N * kx].reshape(N, kx),
+                 flat[N * kx:N * kx + N * self.kz].reshape(N, self.kz)),
                 (buf, self.draws.rows3_hdev[k])), k
 
     def shipped(self, j):
@@ -1311,16 +1356,18 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
                and draws.seg3_hdev[0] is not None)
     segs, i = [], 0
     while i < n_it:
+        # capacity, and a halving tail: the device runs the last segment after the host's last
+        # draw, unoverlapped — 256 steps there were ~10 % of a 2000-step run at C4
+        cap = min(draws.segment_capacity(), max(8, -(-(n_it - i) // 2)))
         if through:
             # segments end at evaluations and at capacity only: the reshuffles inside one go
             # up with its draws and the kernel switches tables at their steps
-            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, i + draws.segment_capacity())
+            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, i + cap)
             first = (mod - i % mod) % mod  # the segment's first reshuffle, from its start
             nxt = min(nxt, i + first + draws.table_capacity(n_X, n_Z) * mod)
             segs.append((i, nxt, (nxt - 1) // mod - (i - 1) // mod))
         else:
-            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod,
-                      i + draws.segment_capacity())
+            nxt = min(n_it, (i // eval_mod + 1) * eval_mod, (i // mod + 1) * mod, i + cap)
             segs.append((i, nxt, int(i % mod == 0)))
         i = nxt
 
@@ -1330,7 +1377,10 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
 
     if through:
         eng.table_stacks(max([1] + [r for _, _, r in segs]))
-        pipe = draws.native_pipe(segs, n_X, n_Z, mod)
+        # the tables as uint16 where every row index fits: a quarter of the host stores and
+        # of the upload, and the 64-word compaction of the draws (csrc/numpy_rng.cpp)
+        rw = 2 if n_X <= 65536 and n_Z <= 65536 else 8
+        pipe = draws.native_pipe(segs, n_X, n_Z, mod, row_width=rw)
         try:
             _replay_through(eng, draws, segs, pipe, mod, p_learn, loss, graphs, defer, X, Z)
         finally:
