@@ -386,13 +386,17 @@ def test_same_as_batch_device_rng_equals_host_formula(gpu, golden, monkeypatch, 
     assert 0.0 <= br <= 1.0 and cs.Un is not None
 
 
-@pytest.mark.parametrize("mode", ["replay", "device"])
-def test_deferred_evaluations_equal_synchronous(gpu, golden, mode, monkeypatch):
+@pytest.mark.parametrize("mode,fused", [("replay", True), ("device", True), ("replay", False),
+                                        ("device", False)])
+def test_deferred_evaluations_equal_synchronous(gpu, golden, mode, fused, monkeypatch):
     """learning.DEFER_EVALS: the loop enqueues each evaluation's device part and runs its host
     part once the statistics are back — the evaluation lists (and the log) are those of the
-    synchronous evaluation, bit for bit; so is the final NumPy RNG state."""
+    synchronous evaluation, bit for bit; so is the final NumPy RNG state.  fused=False: the
+    evaluation takes the separate launches, which run on the loop's stream instead of beside
+    the next persistent segment."""
     import tuplewise.learning as lr
     logging.disable(logging.CRITICAL)
+    monkeypatch.setattr(lr, "EVAL_FUSED", fused)
     out = {}
     for defer in (True, False):
         monkeypatch.setattr(lr, "DEFER_EVALS", defer)

@@ -1356,9 +1356,11 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
                and draws.seg3_hdev[0] is not None)
     segs, i = [], 0
     while i < n_it:
-        # capacity, and a halving tail: the device runs the last segment after the host's last
-        # draw, unoverlapped — 256 steps there were ~10 % of a 2000-step run at C4
-        cap = min(draws.segment_capacity(), max(8, -(-(n_it - i) // 2)))
+        # capacity, a doubling head and a halving tail: the device starts only once the first
+        # segment is drawn, and runs the last one after the host's last draw, unoverlapped —
+        # 256-step segments there cost ~10 % of a 2000-step run at C4 (profiles/r04s3_*)
+        cap = min(draws.segment_capacity(), 16 << min(len(segs), 8),
+                  max(8, -(-(n_it - i) // 2)))
         if through:
             # segments end at evaluations and at capacity only: the reshuffles inside one go
             # up with its draws and the kernel switches tables at their steps
@@ -1814,6 +1816,7 @@ def _eval_small(wd, p_learn, kern, margin):
            L.ptr(eZ), m, wd.numel(), L.ptr(wd), L.ptr(ixd), L.ptr(izd), n_pairs, L.ptr(offs),
            kern, float(margin), L.ptr(scores), L.ptr(work), L.ptr(cwork), L.ptr(ticket),
            L.ptr(out), L.stream_handle())
+    _eval_small.last = out.data_ptr()  # evaluation_step: this output came from the fused path
     return out, n_pairs, n * m
 
 
@@ -1892,15 +1895,29 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
             wbuf.copy_(_w_dev)
             _eval_device(wbuf, p_learn, loss, margin, fixed)  # warm: caches, allocations
             t.cuda.synchronize()
+            _eval_small.last = None
             with t.cuda.graph(g):
                 out = _eval_device(wbuf, p_learn, loss, margin, fixed)
+            # only the fused small evaluation (two short launches) runs beside a persistent
+            # segment: a larger one could hold CUs long enough for the segment's co-resident
+            # grid barrier to give up
+            small = out[0].data_ptr() == getattr(_eval_small, "last", None)
             # the entry keeps the device copies the graph reads alive, even if a later call
             # with other p_learn objects replaces them in _CACHE
             held = tuple(_CACHE.dev[k] for k in ("test_X", "test_Z") +
                          (("train_X", "train_Z", "pairs") if fixed else ()))
-            ent = (key, srcs, g, out, held, wbuf)
+            ent = (key, srcs, g, out, held, wbuf, small)
             _CACHE.dev["eval_graph"] = ent
         res_dev, n_pairs, n_test = ent[3]
+        if deferred and not ent[6]:  # serialised with the steps on the loop's stream
+            side = _CACHE.dev.get("eval_side")
+            if side is not None:
+                t.cuda.current_stream().wait_stream(side)
+            ent[5].copy_(_w_dev)
+            ent[2].replay()
+            _defer.push(i, res_dev, ent[5], lambda it, res, wh: _eval_host(
+                it, res, wh, n_pairs, n_test, p_learn, fixed, None, None))
+            return
         if deferred:
             # the evaluation runs on a side stream BESIDE the next segment of steps: w is
             # snapshotted into the graph's buffer on the loop's stream (after the previous
