@@ -638,7 +638,26 @@ def pmc_traffic(kernel="k_count_complete"):
     if d is None:
         return None, None
     plain = d.get("by_grid", {}).get(d.get("plain_grid") or "", {}).get("hbm_bytes_per_launch")
-    return d.get("hbm_bytes_per_launch"), plain
+    per = d.get("hbm_bytes_per_launch")
+    k = d.get("steps_per_launch")  # a k_count_chain launch counts every step of a chunk
+    if k and per is not None:
+        return per / k, None
+    return per, plain
+
+
+def pmc_emit_traffic():
+    """HBM bytes per step of the step chains' emission (k_chain_emit) in the bench's timed
+    K-step call, from the committed per-dispatch --pmc summary (profiles/*chain_emit_pmc.json)."""
+    import re
+    cands = sorted(ROOT.glob("profiles/*chain_emit_pmc*.json"),
+                   key=lambda p: [int(v) for v in re.findall(r"\d+", p.name)])
+    if not cands:
+        return None
+    try:
+        t = json.loads(cands[-1].read_text())["timed_call"]
+        return (t["write_MB"] + t["fetch_MB"]) * 1e6 / t["steps"]
+    except Exception:
+        return None
 
 
 def pmc_replay_traffic():
@@ -1247,6 +1266,12 @@ def main():
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
                      "count_kernel_ms": kms, "traffic": traffic,
                      "traffic_count_only": traffic_plain,
+                     "traffic_unit": ("HBM bytes per step: the chunk's k_count_chain launch / its "
+                                      "steps" if chain_path else "HBM bytes per launch"),
+                     "traffic_emit_per_step": pmc_emit_traffic() if chain_path else None,
+                     # the count reads each step's 4-B images of its n + n scores once
+                     "algorithmic_bytes_per_step": (4 * 2 * n if chain_path
+                                                    else None),
                      "traffic_source": ("rocprofv3 --pmc FETCH_SIZE+WRITE_SIZE of this kernel "
                                         "at the one-GPU shape (profiles/*count_pmc*.json), "
                                         "not measured at this run's per-rank shape"
