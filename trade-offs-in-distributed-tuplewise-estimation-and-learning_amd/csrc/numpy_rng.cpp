@@ -356,13 +356,19 @@ TW_INLINE int batch_body(uint32_t* key, int32_t* pos, int32_t n_calls, const int
   mt.key = key;
   mt.pos = *pos;
   int64_t o = 0;
-  for (int32_t c = 0; c < n_calls; ++c) {
+  for (int32_t c = 0; c < n_calls;) {
     if (high[c] <= low[c]) {
       *pos = mt.pos;
       return 1;
     }
-    randint_fill<kIsa>(mt, low[c], high[c], cnt[c], out + o);
-    o += cnt[c];
+    // consecutive calls on the same range are one call of their summed size: the masked
+    // rejection keeps no state between calls (SWR_divide's N calls per side: one fill each)
+    int32_t c2 = c + 1;
+    int64_t run = cnt[c];
+    while (c2 < n_calls && low[c2] == low[c] && high[c2] == high[c]) run += cnt[c2++];
+    randint_fill<kIsa>(mt, low[c], high[c], run, out + o);
+    o += run;
+    c = c2;
   }
   *pos = mt.pos;
   return 0;
@@ -757,14 +763,18 @@ batch_u16_avx512(uint32_t* key, int32_t* pos, int32_t n_calls, const int64_t* hi
   mt.key = key;
   mt.pos = *pos;
   int64_t o = 0;
-  for (int32_t c = 0; c < n_calls; ++c) {
+  for (int32_t c = 0; c < n_calls;) {
+    int32_t c2 = c + 1;  // consecutive calls on one range: one fill (as batch_body)
+    int64_t run = cnt[c];
+    while (c2 < n_calls && high[c2] == high[c]) run += cnt[c2++];
     const uint64_t rng = (uint64_t)(high[c] - 1);
     if (rng == 0) {
-      for (int64_t i = 0; i < cnt[c]; ++i) out[o + i] = 0;
+      for (int64_t i = 0; i < run; ++i) out[o + i] = 0;
     } else {
-      fill_masked64_u16(mt, (uint32_t)gen_mask(rng), (uint32_t)rng, cnt[c], out + o);
+      fill_masked64_u16(mt, (uint32_t)gen_mask(rng), (uint32_t)rng, run, out + o);
     }
-    o += cnt[c];
+    o += run;
+    c = c2;
   }
   *pos = mt.pos;
   return 0;

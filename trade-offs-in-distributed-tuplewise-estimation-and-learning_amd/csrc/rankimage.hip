@@ -61,6 +61,12 @@ constexpr int kRkSample = 2048;                    // largest sample (one k_sort
 // 145 us per 1e6 + 1e6 ranking against 169-172 us for 2048 / 16; profiles/r04_chain_parts.log)
 static int g_rank_cs = 1024;
 static int g_rank_per = 8;
+// small Z (m <= kRkSmallM, the one-shot C2 counts): a shorter sample (its one-block sort is a
+// serial latency chain: 15 us for 1024 keys) and shorter interval buckets (more sub-sort
+// blocks); tw_rank_set_small
+constexpr int64_t kRkSmallM = 1 << 18;
+static int g_rank_cs_small = 256;
+static int g_rank_zint_small = 2048;
 constexpr int kRkMaxB = 256;                       // splitter intervals (511 buckets max)
 constexpr int kRkSub = 2048;                       // sub-buckets per interval bucket
 
@@ -70,11 +76,17 @@ __device__ __forceinline__ int64_t sample_index(int i, int64_t m) {
   return (int64_t)(((uint64_t)mix32((uint32_t)i * 0x9E3779B1u + 0x7F4A7C15u) * (uint64_t)m) >> 32);
 }
 
+// the sample drawn and sorted in one block: keys of z at cs hashed positions, padded with ~0
+// to C (a power of two >= 256), bitonic-sorted (sortkeys.h) into ss
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_rank_sample(const T* __restrict__ z, int64_t m,
-                                                        int cs, T* __restrict__ samp) {
-  for (int i = blockIdx.x * kBlock + threadIdx.x; i < cs; i += gridDim.x * kBlock)
-    samp[i] = z[sample_index(i, m)];
+__global__ __launch_bounds__(kRkSample / 4) void k_rank_sample_sort(const T* __restrict__ z,
+                                                                    int64_t m, int cs, int C,
+                                                                    uint64_t* __restrict__ ss) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+  for (int i = threadIdx.x; i < C; i += blockDim.x)
+    keys[i] = i < cs ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+  __syncthreads();
+  sort_keys_block<4>(keys, C, ss);
 }
 
 // bucket of a key: 2j for the interval below splitter j (j = #splitters < key), 2j + 1 for a key
@@ -160,6 +172,48 @@ __global__ __launch_bounds__(kBlock) void k_rank_rows(RankGeo g, uint32_t* __res
     carry += __shfl(inc, kWave - 1, kWave);
   }
   if (lane == 0) total[b] = carry;
+}
+
+// passes 2a + 2b in one 1024-thread block when NB x nblk is small (the C2-size ranking: two
+// launches of ~2 us of work each were ~8 us): each wave scans the rows of buckets wid,
+// wid + 16, ..., then the block scans the totals
+constexpr int64_t kRkRowsOneBlock = 16384;
+__global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* __restrict__ rel,
+                                                           uint32_t* __restrict__ total,
+                                                           uint32_t* __restrict__ start) {
+  __shared__ uint32_t a[1024];
+  const int t = threadIdx.x, wid = t / kWave, lane = t & (kWave - 1);
+  a[t] = 0u;
+  __syncthreads();
+  for (int b = wid; b < g.NB; b += 1024 / kWave) {
+    uint32_t* row = rel + (int64_t)b * g.nblk;
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < g.nblk; c0 += kWave) {
+      const int c = c0 + lane;
+      const uint32_t v = c < g.nblk ? row[c] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += u;
+      }
+      if (c < g.nblk) row[c] = carry + inc - v;
+      carry += __shfl(inc, kWave - 1, kWave);
+    }
+    if (lane == 0) {
+      total[b] = carry;
+      a[b] = carry;
+    }
+  }
+  __syncthreads();
+  const uint32_t own = a[t];
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the totals
+    const uint32_t v = t >= o ? a[t - o] : 0u;
+    __syncthreads();
+    a[t] += v;
+    __syncthreads();
+  }
+  if (t < g.NB) start[t] = a[t] - own;
 }
 
 // pass 2b: bucket starts = the z count below every bucket (one block, NB <= 1024)
@@ -455,14 +509,16 @@ static RankGeo rank_geo(int64_t n, int64_t m, int64_t mq = -1, int half = 0, int
   g.tot = n + g.mq;
   g.half = half;
   g.compact = compact;
+  const bool small = m <= kRkSmallM;
+  const int64_t zint = small ? g_rank_zint_small : 2048;  // >= ~zint z per interval
+  g.cs = (int)std::min<int64_t>(m, small ? g_rank_cs_small : g_rank_cs);
   int B = 1;
-  while (B < kRkMaxB && (int64_t)B * 2048 < m) B <<= 1;  // >= ~2048 z per interval
+  while (B < kRkMaxB && 2 * B <= std::max(g.cs, 1) && (int64_t)B * zint < m) B <<= 1;
   g.B = B;
   g.NB = 2 * B;
   g.per = g_rank_per;
   g.nblk = (int)std::max<int64_t>(1, ceil_div(m, (int64_t)kRkThreads * g.per));
-  g.cs = (int)std::min<int64_t>(m, g_rank_cs);
-  g.C = 1024;
+  g.C = 256;
   while (g.C < g.cs) g.C <<= 1;
   return g;
 }
@@ -691,17 +747,21 @@ template <typename T>
 static int rank_images_t(const T* xq, const T* zq, const T* z, int64_t m, const RankWork& w,
                          const RankGeo& g, uint64_t* x_rec, uint64_t* z_rec, hipStream_t st) {
   if (m > 0) {  // the sample: hashed positions of z, sorted (k_sort_chunks pads with ~0 past cs)
-    hipLaunchKernelGGL((k_rank_sample<T>), dim3(8), dim3(kBlock), 0, st, z, m, g.cs, (T*)w.samp);
-    hipLaunchKernelGGL((k_sort_chunks<T, 4>), dim3(1), dim3(g.C / 4), g.C * 8, st,
-                       (const T*)w.samp, nullptr, 1, g.C, w.ss, (int64_t)g.cs);
+    hipLaunchKernelGGL((k_rank_sample_sort<T>), dim3(1), dim3(g.C / 4), g.C * 8, st, z, m,
+                       g.cs, g.C, w.ss);
     TW_LAUNCH_CHECK();
     auto passes = [&](auto per) {
       constexpr int PER = decltype(per)::value;
       hipLaunchKernelGGL((k_rank_hist<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
                          w.ss, w.rel);
-      hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
-                         dim3(kBlock), 0, st, g, w.rel, w.total);
-      hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
+      if ((int64_t)g.NB * g.nblk <= kRkRowsOneBlock) {  // small Z: rows and starts in one block
+        hipLaunchKernelGGL(k_rank_rows_starts, dim3(1), dim3(1024), 0, st, g, w.rel, w.total,
+                           w.start);
+      } else {
+        hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
+                           dim3(kBlock), 0, st, g, w.rel, w.total);
+        hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
+      }
       hipLaunchKernelGGL((k_rank_scatter<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
                          w.ss, w.rel, w.start, w.bkeys);
     };
@@ -779,6 +839,16 @@ extern "C" int tw_rank_set_plan(int32_t sample, int32_t per) {
   TW_ARG_CHECK(per == 4 || per == 8 || per == 16, "tw_rank_set_plan: 4, 8 or 16 z per thread");
   g_rank_cs = sample;
   g_rank_per = per;
+  return TW_OK;
+}
+
+extern "C" int tw_rank_set_small(int32_t sample, int32_t z_per_interval) {
+  TW_ARG_CHECK(sample == 256 || sample == 512 || sample == 1024 || sample == 2048,
+               "tw_rank_set_small: sample of 256, 512, 1024 or 2048 keys");
+  TW_ARG_CHECK(z_per_interval == 512 || z_per_interval == 1024 || z_per_interval == 2048,
+               "tw_rank_set_small: 512, 1024 or 2048 z per interval bucket");
+  g_rank_cs_small = sample;
+  g_rank_zint_small = z_per_interval;
   return TW_OK;
 }
 

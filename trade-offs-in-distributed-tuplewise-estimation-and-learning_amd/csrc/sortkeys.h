@@ -65,32 +65,14 @@ __device__ __forceinline__ void reg_levels(uint64_t (&v)[E], int base, int k, in
 //   j <  E          same thread          -> compare-exchange in registers
 //   E <= j < 64 E   same wave (lane ^ j/E) -> __shfl_xor, no barrier
 //   j >= 64 E       other wave           -> exchange through LDS (one barrier pair)
-// Direction: ascending iff (i & k) == 0.  C is a power of two >= 1024.
-template <typename T, int kE>
-__global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restrict__ z,
-                                                              const int64_t* __restrict__ z_off,
-                                                              int chunks, int C,
-                                                              uint64_t* __restrict__ sorted,
-                                                              int64_t stride = 0) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
-  const int s = blockIdx.x / chunks;
-  const int c = blockIdx.x - s * chunks;
-  // shard s is z[z_off[s], z_off[s+1]), or z[s*stride, (s+1)*stride) without offsets
-  const int64_t zb = z_off ? z_off[s] : (int64_t)s * stride;
-  const int64_t ze = z_off ? z_off[s + 1] : zb + stride;
-  const int64_t c0 = zb + (int64_t)c * C;
+// Direction: ascending iff (i & k) == 0.  C is a power of two >= 4 E (>= 1024 for the
+// callers that sort shard chunks; the ranking's sample sort uses C >= 256).
+// The network on C keys already in LDS (`keys`), thread t owning [E t, E t + E); the sorted
+// keys written to dst.  Every thread of the block (C / E of them) calls it.
+template <int kE>
+__device__ __forceinline__ void sort_keys_block(uint64_t* keys, int C, uint64_t* __restrict__ dst) {
   const int nthr = blockDim.x;  // == C / kE
   const int tid = threadIdx.x;
-  for (int i = tid; i < C; i += nthr) {  // coalesced load + key transform
-    const int64_t g = c0 + i;
-    keys[i] = (g < ze) ? order_key<T>(z[g]) : ~0ull;
-  }
-  __syncthreads();
-  uint64_t* dst = sorted + (int64_t)blockIdx.x * C;
-  if (c0 >= ze) {  // block-uniform: an empty chunk stays all-padding
-    for (int i = tid; i < C; i += nthr) dst[i] = ~0ull;
-    return;
-  }
   const int base = tid * kE;
   uint64_t v[kE];
 #pragma unroll
@@ -127,6 +109,34 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restric
   for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
   __syncthreads();
   for (int i = tid; i < C; i += nthr) dst[i] = keys[i];
+}
+
+template <typename T, int kE>
+__global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restrict__ z,
+                                                              const int64_t* __restrict__ z_off,
+                                                              int chunks, int C,
+                                                              uint64_t* __restrict__ sorted,
+                                                              int64_t stride = 0) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
+  const int s = blockIdx.x / chunks;
+  const int c = blockIdx.x - s * chunks;
+  // shard s is z[z_off[s], z_off[s+1]), or z[s*stride, (s+1)*stride) without offsets
+  const int64_t zb = z_off ? z_off[s] : (int64_t)s * stride;
+  const int64_t ze = z_off ? z_off[s + 1] : zb + stride;
+  const int64_t c0 = zb + (int64_t)c * C;
+  const int nthr = blockDim.x;  // == C / kE
+  const int tid = threadIdx.x;
+  for (int i = tid; i < C; i += nthr) {  // coalesced load + key transform
+    const int64_t g = c0 + i;
+    keys[i] = (g < ze) ? order_key<T>(z[g]) : ~0ull;
+  }
+  __syncthreads();
+  uint64_t* dst = sorted + (int64_t)blockIdx.x * C;
+  if (c0 >= ze) {  // block-uniform: an empty chunk stays all-padding
+    for (int i = tid; i < C; i += nthr) dst[i] = ~0ull;
+    return;
+  }
+  sort_keys_block<kE>(keys, C, dst);
 }
 
 // #{keys < k} in a sorted power-of-two array (branchless).
