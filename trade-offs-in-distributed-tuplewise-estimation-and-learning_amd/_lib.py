@@ -7,12 +7,15 @@ without a HIP device raises instead of silently computing elsewhere.
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
 
 import numpy as np
 
 _HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libtuplewise.so"
+# TW_LIB_PATH: an A/B build of the same library (tools/ab_barrier.py), never the product default
+LIB_PATH = pathlib.Path(os.environ["TW_LIB_PATH"]) if os.environ.get("TW_LIB_PATH") else (
+    _HERE / "libtuplewise.so")
 
 TW_OK, TW_ERR_ARG, TW_ERR_HIP = 0, 1, 2
 TW_F64, TW_I64 = 0, 1

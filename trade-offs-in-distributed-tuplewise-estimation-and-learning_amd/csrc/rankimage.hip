@@ -77,16 +77,40 @@ __device__ __forceinline__ int64_t sample_index(int i, int64_t m) {
 }
 
 // the sample drawn and sorted in one block: keys of z at cs hashed positions, padded with ~0
-// to C (a power of two >= 256), bitonic-sorted (sortkeys.h) into ss
+// to C (a power of two >= 256), sorted by counting — key i goes to #{j : k_j < k_i} + #{j < i :
+// k_j == k_i}, C compares per key against LDS broadcasts (a bitonic network on one block was a
+// serial chain of ~40 shuffle levels: 15 us for 1024 keys)
 template <typename T>
-__global__ __launch_bounds__(kRkSample / 4) void k_rank_sample_sort(const T* __restrict__ z,
-                                                                    int64_t m, int cs, int C,
-                                                                    uint64_t* __restrict__ ss) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];
-  for (int i = threadIdx.x; i < C; i += blockDim.x)
-    keys[i] = i < cs ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+__global__ __launch_bounds__(1024) void k_rank_sample_sort(const T* __restrict__ z, int64_t m,
+                                                           int cs, int C,
+                                                           uint64_t* __restrict__ ss) {
+  __shared__ uint64_t keys[kRkSample];
+  constexpr int kMaxPer = kRkSample / 1024;
+  const int nt = blockDim.x, per = C / nt;
+  uint64_t mine[kMaxPer];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {  // all loads issued before the first store
+    const int i = threadIdx.x + u * nt;
+    mine[u] = (u < per && i < cs) ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u)
+    if (u < per) keys[threadIdx.x + u * nt] = mine[u];
   __syncthreads();
-  sort_keys_block<4>(keys, C, ss);
+  uint32_t pos[kMaxPer];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) pos[u] = 0;
+  for (int j = 0; j < C; ++j) {
+    const uint64_t kj = keys[j];  // the same address in every lane: one broadcast read
+#pragma unroll
+    for (int u = 0; u < kMaxPer; ++u) {
+      const int i = threadIdx.x + u * nt;
+      pos[u] += (kj < mine[u] || (kj == mine[u] && j < i)) ? 1u : 0u;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u)
+    if (u < per) ss[pos[u]] = mine[u];
 }
 
 // bucket of a key: 2j for the interval below splitter j (j = #splitters < key), 2j + 1 for a key
@@ -174,43 +198,48 @@ __global__ __launch_bounds__(kBlock) void k_rank_rows(RankGeo g, uint32_t* __res
   if (lane == 0) total[b] = carry;
 }
 
-// passes 2a + 2b in one 1024-thread block when NB x nblk is small (the C2-size ranking: two
-// launches of ~2 us of work each were ~8 us): each wave scans the rows of buckets wid,
-// wid + 16, ..., then the block scans the totals
-constexpr int64_t kRkRowsOneBlock = 16384;
+// passes 2a + 2b in one 1024-thread block when every bucket row fits a wave (nblk <= 64: the
+// C2-size ranking, where two launches of ~2 us of work each took ~8 us): each wave scans the
+// rows of buckets wid, wid + 16, ..., then the block scans the totals
 __global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* __restrict__ rel,
                                                            uint32_t* __restrict__ total,
                                                            uint32_t* __restrict__ start) {
   __shared__ uint32_t a[1024];
+  constexpr int kPerWave = 2 * kRkMaxB / (1024 / kWave);  // NB <= 512 rows over 16 waves
   const int t = threadIdx.x, wid = t / kWave, lane = t & (kWave - 1);
   a[t] = 0u;
-  __syncthreads();
-  for (int b = wid; b < g.NB; b += 1024 / kWave) {
-    uint32_t* row = rel + (int64_t)b * g.nblk;
-    uint32_t carry = 0;
-    for (int c0 = 0; c0 < g.nblk; c0 += kWave) {
-      const int c = c0 + lane;
-      const uint32_t v = c < g.nblk ? row[c] : 0u;
-      uint32_t inc = v;
+  // nblk <= kWave here: one value per lane and row, every row's load issued
+  // before the first scan
+  uint32_t v[kPerWave];
 #pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t u = __shfl_up(inc, o, kWave);
-        if (lane >= o) inc += u;
-      }
-      if (c < g.nblk) row[c] = carry + inc - v;
-      carry += __shfl(inc, kWave - 1, kWave);
+  for (int r = 0; r < kPerWave; ++r) {
+    const int b = wid + r * (1024 / kWave);
+    v[r] = (b < g.NB && lane < g.nblk) ? rel[(int64_t)b * g.nblk + lane] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kPerWave; ++r) {
+    const int b = wid + r * (1024 / kWave);
+    if (b >= g.NB) break;
+    uint32_t inc = v[r];
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += u;
     }
+    if (lane < g.nblk) rel[(int64_t)b * g.nblk + lane] = inc - v[r];
+    const uint32_t tot = __shfl(inc, kWave - 1, kWave);
     if (lane == 0) {
-      total[b] = carry;
-      a[b] = carry;
+      total[b] = tot;
+      a[b] = tot;
     }
   }
   __syncthreads();
   const uint32_t own = a[t];
   for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the totals
-    const uint32_t v = t >= o ? a[t - o] : 0u;
+    const uint32_t x = t >= o ? a[t - o] : 0u;
     __syncthreads();
-    a[t] += v;
+    a[t] += x;
     __syncthreads();
   }
   if (t < g.NB) start[t] = a[t] - own;
@@ -373,10 +402,30 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
   __shared__ unsigned long long cost[2];
   const int b = 2 * blockIdx.x;  // interval buckets only
   const uint32_t s0 = start[b], c = total[b];
+  // a bucket of <= kSubK * kSubThreads keys is read once into registers and every pass reuses
+  // them (three dependent global passes were most of this kernel's time at C2 size)
+  constexpr int kSubK = 4;
+  const bool inreg = c <= (uint32_t)(kSubK * kSubThreads);  // block-uniform
+  uint64_t kr[kSubK];
+  if (inreg) {
+#pragma unroll
+    for (int u = 0; u < kSubK; ++u) {
+      const uint32_t i = threadIdx.x + u * kSubThreads;
+      kr[u] = i < c ? bkeys[s0 + i] : 0ull;
+    }
+  }
+  auto each = [&](auto&& fn) {
+    if (inreg) {
+#pragma unroll
+      for (int u = 0; u < kSubK; ++u)
+        if (threadIdx.x + u * kSubThreads < c) fn(kr[u]);
+    } else {
+      for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) fn(bkeys[s0 + i]);
+    }
+  };
   double lo = __builtin_inf(), hi = -__builtin_inf();
   uint64_t klo = ~0ull, khi = 0;
-  for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) {
-    const uint64_t k = bkeys[s0 + i];
+  each([&](uint64_t k) {
     const double v = key_value<T>(k);
     if (v - v == 0.0) {  // finite
       lo = fmin(lo, v);
@@ -386,7 +435,7 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
       klo = k < klo ? k : klo;
       khi = k > khi ? k : khi;
     }
-  }
+  });
   for (int i = threadIdx.x; i <= kRkSub; i += kSubThreads) hv[i] = hk[i] = 0;
   if (threadIdx.x < 2) cost[threadIdx.x] = 0;
   block_minmax<kSubThreads>(lo, hi, klo, khi, sd, sk);
@@ -401,12 +450,11 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
     fk.klo = klo;
     fk.kshift = bits > 11 ? bits - 11 : 0;
   }
-  for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) {
-    const uint64_t k = bkeys[s0 + i];
+  each([&](uint64_t k) {
     const double v = key_value<T>(k);
     atomicAdd(&hv[fv(v, k)], 1u);
     atomicAdd(&hk[fk(v, k)], 1u);
-  }
+  });
   __syncthreads();
   unsigned long long cv = 0, ck = 0;
   for (int i = threadIdx.x; i < kRkSub; i += kSubThreads) {
@@ -425,10 +473,7 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
   uint32_t* sp_out = subp + (int64_t)blockIdx.x * (kRkSub + 1);
   for (int i = threadIdx.x; i <= kRkSub; i += kSubThreads) sp_out[i] = h[i];
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < c; i += kSubThreads) {
-    const uint64_t k = bkeys[s0 + i];
-    skeys[s0 + atomicAdd(&h[f(key_value<T>(k), k)], 1u)] = k;
-  }
+  each([&](uint64_t k) { skeys[s0 + atomicAdd(&h[f(key_value<T>(k), k)], 1u)] = k; });
 }
 
 // pass 5: every element in input order, one per thread (the chain splitters -> bucket map ->
@@ -747,14 +792,14 @@ template <typename T>
 static int rank_images_t(const T* xq, const T* zq, const T* z, int64_t m, const RankWork& w,
                          const RankGeo& g, uint64_t* x_rec, uint64_t* z_rec, hipStream_t st) {
   if (m > 0) {  // the sample: hashed positions of z, sorted (k_sort_chunks pads with ~0 past cs)
-    hipLaunchKernelGGL((k_rank_sample_sort<T>), dim3(1), dim3(g.C / 4), g.C * 8, st, z, m,
-                       g.cs, g.C, w.ss);
+    hipLaunchKernelGGL((k_rank_sample_sort<T>), dim3(1), dim3(std::min(g.C, 1024)), 0, st, z,
+                       m, g.cs, g.C, w.ss);
     TW_LAUNCH_CHECK();
     auto passes = [&](auto per) {
       constexpr int PER = decltype(per)::value;
       hipLaunchKernelGGL((k_rank_hist<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
                          w.ss, w.rel);
-      if ((int64_t)g.NB * g.nblk <= kRkRowsOneBlock) {  // small Z: rows and starts in one block
+      if (g.nblk <= kWave) {  // small Z: rows and starts in one block
         hipLaunchKernelGGL(k_rank_rows_starts, dim3(1), dim3(1024), 0, st, g, w.rel, w.total,
                            w.start);
       } else {

@@ -82,20 +82,34 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 // store (st_agent); each storing wave waits for its own stores (s_waitcnt vmcnt(0) — the
 // block barrier's workgroup-scope release does not wait for another wave's vector stores to
 // reach the agent-coherent level), the block barrier orders them before thread 0's arrival,
-// and the arrival is an agent-scope RELEASE add; the poller's loads of the counter are
-// agent-scope ACQUIRE loads, and the block barrier after the poll orders every wave's loads of
-// the published words (ld_agent) after it.
-__device__ __forceinline__ void seg_arrive(uint32_t* ctl) {
+// and the arrival is an agent-scope RELEASE add (gfx950: buffer_wbl2 sc1 before the atomic).
+// The poller spins on RELAXED loads of the counter and, once it has seen the target, issues
+// ONE agent-scope ACQUIRE fence (buffer_inv sc1) — acquire loads in the spin itself would
+// invalidate the L2 on every iteration; the fence after the last relaxed load that read the
+// release's value gives the same synchronisation (fence-atomic rule).  The block barrier after
+// the poll orders every wave's loads of the published words (ld_agent) after the fence.
+// TW_SEG_BARRIER (A/B builds, tools/ab_barrier.py): 0 = relaxed arrival and spin, no fence
+// (round 3); 1 = acquire loads in the spin; 2 (default) = as above.
+#ifndef TW_SEG_BARRIER
+#define TW_SEG_BARRIER 2
+#endif
+// arriver: the thread that adds the arrival — the release's L2 write-back (~0.6 us on gfx950)
+// stalls only its wave, so the narrow kernel hands it to the last wave, which has no pairs in
+// the next step's chain when B <= 192 (C4: B = 100): the stall hides behind the other waves'
+// draws -> rows -> diff rows (tools/ab_barrier.py)
+__device__ __forceinline__ void seg_arrive(uint32_t* ctl, int arriver = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's published stores landed
   __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)threadIdx.x == arriver)
+    __hip_atomic_fetch_add(ctl, 1u, TW_SEG_BARRIER ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // one lane: spin until the counter reaches target (false: aborted or timed out -> abort word)
 __device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  while (__hip_atomic_load(ctl, TW_SEG_BARRIER == 1 ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT) < target) {
     if (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
         wall_clock64() - t0 > kSegSpinTicks) {
       __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -103,6 +117,7 @@ __device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  if (TW_SEG_BARRIER == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
@@ -305,7 +320,8 @@ __global__ __launch_bounds__(kWideBlock) void k_sgd_segment_wide(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         SEG_STAMP(k, 6);
         if (lane == 0)
-          __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(ctl, 1u, TW_SEG_BARRIER ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
         if (!more && blk == 0 && lane == 0 && d_step) *d_step = step0 + (uint64_t)nsteps;
       }
     } else if (more && prefetch_rows) {
@@ -483,7 +499,8 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
       for (; t < B; ++t) a += weighted<LOSS>(flag[t], diff[t * dd + tid]);
       st_agent(((k & 1) ? grads1 : grads0) + (int64_t)s * d + tid, a / (double)B);
     }
-    seg_arrive(ctl);  // also: every thread is done with diff / flag / gt of this step
+    seg_arrive(ctl, B <= kBlock - kWave ? kBlock - kWave : 0);  // also: every thread is done
+                                                                // with diff / flag / gt
   }
   if (s == 0) {
     if (tid < dd) {

@@ -1004,6 +1004,8 @@ class _ReplayDraws:
         t = L.torch()
         self._seg_buffers(3)
         ntab = max([1] + [int(r) for _, _, r in segs])
+        if ntab > 1:  # through reshuffles: room for a full segment's tables (see table_stacks)
+            ntab = max(ntab, min(self.segment_capacity(), self.table_capacity(n_X, n_Z)))
         N, kx, kz = self._rows_buffers(n_X, n_Z, ntab)
         t.cuda.current_stream().synchronize()  # earlier uploads out of the ring have run
         steps = np.array([b - a for a, b, _ in segs], dtype=np.int32)
@@ -1378,7 +1380,11 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
                          rows_x, rows_z)
 
     if through:
-        eng.table_stacks(max([1] + [r for _, _, r in segs]))
+        # the stacks and the pinned ring sized for the most tables a segment can hold, not this
+        # run's: a later call at another reshuffle_mod must not re-allocate (pinned allocations
+        # cost milliseconds inside the caller's loop)
+        cap_tabs = min(draws.segment_capacity(), draws.table_capacity(n_X, n_Z))
+        eng.table_stacks(max([cap_tabs] + [r for _, _, r in segs]))
         # the tables as uint16 where every row index fits: a quarter of the host stores and
         # of the upload, and the 64-word compaction of the draws (csrc/numpy_rng.cpp)
         rw = 2 if n_X <= 65536 and n_Z <= 65536 else 8
