@@ -1358,10 +1358,13 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
                and draws.seg3_hdev[0] is not None)
     segs, i = [], 0
     while i < n_it:
-        # capacity, a doubling head and a halving tail: the device starts only once the first
+        # capacity, a growing head and a halving tail: the device starts only once the first
         # segment is drawn, and runs the last one after the host's last draw, unoverlapped —
-        # 256-step segments there cost ~10 % of a 2000-step run at C4 (profiles/r04s3_*)
-        cap = min(draws.segment_capacity(), 16 << min(len(segs), 8),
+        # 256-step segments there cost ~10 % of a 2000-step run at C4 (profiles/r04s3_*).  The
+        # head grows by 1.25x a segment: the host draws a step in ~0.75 of the device's time
+        # (C4, mod 25), so doubling left the device idle while the next segment was drawn
+        # (profiles/r04s6_replay_timeline.log)
+        cap = min(draws.segment_capacity(), int(16 * 1.25 ** min(len(segs), 24)),
                   max(8, -(-(n_it - i) // 2)))
         if through:
             # segments end at evaluations and at capacity only: the reshuffles inside one go
