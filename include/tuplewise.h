@@ -142,9 +142,9 @@ int tw_count_rank_set_next(int32_t front);
  * do not depend on it (the workspace size does: query it after setting). */
 int tw_rank_set_plan(int32_t sample, int32_t per);
 /* Tuning hook for small Z (n_z <= 2^18: the one-shot C2 counts): the ranking's sample size
- * (256, 512, 1024 or 2048 keys; default 256) and the target z per interval bucket (512, 1024
- * or 2048; default 2048). */
-int tw_rank_set_small(int32_t sample, int32_t z_per_interval);
+ * (256, 512, 1024 or 2048 keys; default 256), the target z per interval bucket (512, 1024 or
+ * 2048; default 2048) and z per thread in the bucket passes (4, 8 or 16; default 4). */
+int tw_rank_set_small(int32_t sample, int32_t z_per_interval, int32_t per);
 /* tw_rank_images over several ranks (and for half ties): the images are counted against the Z
  * of d_z_all (the all-gathered sample, n_z_all < 2^24) but written only for the n_x + n_z
  * elements of d_x / d_z (this rank's share; d_z may be d_z_all).  half (flags): bit 0 — each X

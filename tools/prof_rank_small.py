@@ -4,7 +4,8 @@ durations):
     rocprofv3 --kernel-trace --output-format csv -d DIR -- python3 tools/prof_rank_small.py
     python3 tools/kernel_grid_stats.py DIR/.../kernel_trace.csv
 `--sweep`: HIP-event time per call for each small-Z plan (tw_rank_set_small: sample size,
-z per interval bucket), interleaved, images checked equal to the default plan's."""
+z per interval bucket, z per thread), interleaved, images checked equal to the default plan's
+(back-to-back rankings: host enqueue bound, so the trace mode is the device-time measure)."""
 import pathlib
 import sys
 
@@ -22,14 +23,17 @@ n = int(args[0]) if args else 100_000
 X = torch.randn(n, dtype=torch.float64, device="cuda", generator=g) + 0.5
 Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
 ops = HipOps()
+plan_arg = [a for a in sys.argv if a.startswith("--plan=")]
+if plan_arg:  # one small-Z plan for the trace: --plan=SAMPLE,Z_PER_INTERVAL,PER
+    L.call("tw_rank_set_small", *[int(v) for v in plan_arg[0][7:].split(",")])
 if "--sweep" not in sys.argv:
     for _ in range(20):
         ops.rank_images_query(Z, X, Z, L.TW_F64, compact=True)
     torch.cuda.synchronize()
     print("done", flush=True)
     sys.exit(0)
-plans = [(s, z) for s in (256, 512, 1024) for z in (512, 1024, 2048)]
-L.call("tw_rank_set_small", 256, 2048)
+plans = [(s, z, p) for s in (256, 512) for z in (1024, 2048) for p in (4, 8, 16)]
+L.call("tw_rank_set_small", 256, 2048, 8)
 ref = [r.clone() for r in ops.rank_images_query(Z, X, Z, L.TW_F64, compact=True)]
 times = {p: [] for p in plans}
 for rep in range(5):
@@ -47,5 +51,6 @@ for rep in range(5):
         assert all(torch.equal(u, v) for u, v in zip(out, ref)), p
 for p in plans:
     v = sorted(times[p])
-    print(f"n={n} sample={p[0]:5d} z/interval={p[1]:5d}: median {v[len(v) // 2]:7.1f} us "
+    print(f"n={n} sample={p[0]:5d} z/interval={p[1]:5d} per={p[2]:2d}: "
+          f"median {v[len(v) // 2]:7.1f} us "
           f"per ranking (min {v[0]:.1f})", flush=True)

@@ -45,7 +45,7 @@ _SIGNATURES = {
     "tw_count_rank_set_plan": [_i32, _i64],
     "tw_count_rank_set_next": [_i32],
     "tw_rank_set_plan": [_i32, _i32],
-    "tw_rank_set_small": [_i32, _i32],
+    "tw_rank_set_small": [_i32, _i32, _i32],
     "tw_rank_images_query": [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp,
                              _vp],
     "tw_chain_emit": [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32,

@@ -67,6 +67,7 @@ static int g_rank_per = 8;
 constexpr int64_t kRkSmallM = 1 << 18;
 static int g_rank_cs_small = 256;
 static int g_rank_zint_small = 2048;
+static int g_rank_per_small = 4;  // 43 vs 47 us at 1e5 + 1e5 (profiles/r04s7_rank_small_per*.log)
 constexpr int kRkMaxB = 256;                       // splitter intervals (511 buckets max)
 constexpr int kRkSub = 2048;                       // sub-buckets per interval bucket
 
@@ -76,41 +77,65 @@ __device__ __forceinline__ int64_t sample_index(int i, int64_t m) {
   return (int64_t)(((uint64_t)mix32((uint32_t)i * 0x9E3779B1u + 0x7F4A7C15u) * (uint64_t)m) >> 32);
 }
 
+// the sample of C >= 1024 keys (Z beyond kRkSmallM): drawn, then bitonic-sorted (sortkeys.h)
+// by C / 4 threads in the same launch (counting costs C compares per key: 27 us at C = 1024)
+template <typename T>
+__global__ __launch_bounds__(kRkSample / 4) void k_rank_sample_bitonic(const T* __restrict__ z,
+                                                                       int64_t m, int cs, int C,
+                                                                       uint64_t* __restrict__ ss) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t skeys_lds[];
+  for (int i = threadIdx.x; i < C; i += blockDim.x)
+    skeys_lds[i] = i < cs ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+  __syncthreads();
+  sort_keys_block<4>(skeys_lds, C, ss);
+}
+
 // the sample drawn and sorted in one block: keys of z at cs hashed positions, padded with ~0
 // to C (a power of two >= 256), sorted by counting — key i goes to #{j : k_j < k_i} + #{j < i :
-// k_j == k_i}, C compares per key against LDS broadcasts (a bitonic network on one block was a
-// serial chain of ~40 shuffle levels: 15 us for 1024 keys)
+// k_j == k_i}: 1024 threads, each counting one key against a 1 / (1024 / C) share of the keys
+// (LDS broadcasts, four independent partial counts), the shares added with LDS atomics; for
+// C <= 512 (the bitonic network on one block is a serial chain of ~40 shuffle levels: 8.8 us
+// at C = 256 against 5.6)
 template <typename T>
 __global__ __launch_bounds__(1024) void k_rank_sample_sort(const T* __restrict__ z, int64_t m,
                                                            int cs, int C,
                                                            uint64_t* __restrict__ ss) {
   __shared__ uint64_t keys[kRkSample];
+  __shared__ uint32_t cnt[kRkSample];
   constexpr int kMaxPer = kRkSample / 1024;
-  const int nt = blockDim.x, per = C / nt;
-  uint64_t mine[kMaxPer];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {  // all loads issued before the first store
-    const int i = threadIdx.x + u * nt;
-    mine[u] = (u < per && i < cs) ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
-  }
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u)
-    if (u < per) keys[threadIdx.x + u * nt] = mine[u];
-  __syncthreads();
-  uint32_t pos[kMaxPer];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) pos[u] = 0;
-  for (int j = 0; j < C; ++j) {
-    const uint64_t kj = keys[j];  // the same address in every lane: one broadcast read
-#pragma unroll
-    for (int u = 0; u < kMaxPer; ++u) {
-      const int i = threadIdx.x + u * nt;
-      pos[u] += (kj < mine[u] || (kj == mine[u] && j < i)) ? 1u : 0u;
+  const int tid = threadIdx.x;
+  const int per = C > 1024 ? C / 1024 : 1;     // keys per thread
+  const int parts = C >= 1024 ? 1 : 1024 / C;  // threads per key
+  for (int u = 0; u < per; ++u) {  // load and zero (every slot written once)
+    const int i = tid + u * 1024;
+    if (i < C) {
+      keys[i] = i < cs ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+      cnt[i] = 0;
     }
   }
+  __syncthreads();
+  const int part = tid / (C < 1024 ? C : 1024);
+  const int j0 = part * (C / parts), j1 = j0 + C / parts;
 #pragma unroll
-  for (int u = 0; u < kMaxPer; ++u)
-    if (u < per) ss[pos[u]] = mine[u];
+  for (int u = 0; u < kMaxPer; ++u) {
+    if (u >= per) break;
+    const int i = (C < 1024 ? tid % C : tid) + u * 1024;
+    const uint64_t ki = keys[i];
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (int j = j0; j < j1; j += 4) {  // C / parts is a multiple of 4
+      const uint64_t a = keys[j], b = keys[j + 1], c = keys[j + 2], d = keys[j + 3];
+      c0 += (a < ki || (a == ki && j < i)) ? 1u : 0u;
+      c1 += (b < ki || (b == ki && j + 1 < i)) ? 1u : 0u;
+      c2 += (c < ki || (c == ki && j + 2 < i)) ? 1u : 0u;
+      c3 += (d < ki || (d == ki && j + 3 < i)) ? 1u : 0u;
+    }
+    atomicAdd(&cnt[i], c0 + c1 + c2 + c3);
+  }
+  __syncthreads();
+  for (int u = 0; u < per; ++u) {
+    const int i = tid + u * 1024;
+    if (i < C) ss[cnt[i]] = keys[i];
+  }
 }
 
 // bucket of a key: 2j for the interval below splitter j (j = #splitters < key), 2j + 1 for a key
@@ -198,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void k_rank_rows(RankGeo g, uint32_t* __res
   if (lane == 0) total[b] = carry;
 }
 
-// passes 2a + 2b in one 1024-thread block when every bucket row fits a wave (nblk <= 64: the
+// passes 2a + 2b in one 1024-thread block when every bucket row fits two wave loads (nblk <= 128: the
 // C2-size ranking, where two launches of ~2 us of work each took ~8 us): each wave scans the
 // rows of buckets wid, wid + 16, ..., then the block scans the totals
 __global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* __restrict__ rel,
@@ -208,41 +233,57 @@ __global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* 
   constexpr int kPerWave = 2 * kRkMaxB / (1024 / kWave);  // NB <= 512 rows over 16 waves
   const int t = threadIdx.x, wid = t / kWave, lane = t & (kWave - 1);
   a[t] = 0u;
-  // nblk <= kWave here: one value per lane and row, every row's load issued
-  // before the first scan
-  uint32_t v[kPerWave];
+  // nblk <= 2 kWave here: two values per lane and row, every row's loads issued before the
+  // first scan
+  uint32_t v[kPerWave][2];
 #pragma unroll
   for (int r = 0; r < kPerWave; ++r) {
     const int b = wid + r * (1024 / kWave);
-    v[r] = (b < g.NB && lane < g.nblk) ? rel[(int64_t)b * g.nblk + lane] : 0u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = h * kWave + lane;
+      v[r][h] = (b < g.NB && c < g.nblk) ? rel[(int64_t)b * g.nblk + c] : 0u;
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kPerWave; ++r) {
     const int b = wid + r * (1024 / kWave);
     if (b >= g.NB) break;
-    uint32_t inc = v[r];
+    uint32_t carry = 0;
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, kWave);
-      if (lane >= o) inc += u;
+    for (int h = 0; h < 2; ++h) {
+      const int c = h * kWave + lane;
+      uint32_t inc = v[r][h];
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += u;
+      }
+      if (c < g.nblk) rel[(int64_t)b * g.nblk + c] = carry + inc - v[r][h];
+      carry += __shfl(inc, kWave - 1, kWave);
     }
-    if (lane < g.nblk) rel[(int64_t)b * g.nblk + lane] = inc - v[r];
-    const uint32_t tot = __shfl(inc, kWave - 1, kWave);
     if (lane == 0) {
-      total[b] = tot;
-      a[b] = tot;
+      total[b] = carry;
+      a[b] = carry;
     }
   }
   __syncthreads();
+  // exclusive scan of the NB <= 512 totals: a wave scan per 64, then the wave totals (two
+  // barriers; a Hillis-Steele scan over the block took twenty)
+  __shared__ uint32_t wsum[1024 / kWave];
   const uint32_t own = a[t];
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the totals
-    const uint32_t x = t >= o ? a[t - o] : 0u;
-    __syncthreads();
-    a[t] += x;
-    __syncthreads();
+  uint32_t inc = own;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += u;
   }
-  if (t < g.NB) start[t] = a[t] - own;
+  if (lane == kWave - 1) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wid; ++w) before += wsum[w];
+  if (t < g.NB) start[t] = before + inc - own;
 }
 
 // pass 2b: bucket starts = the z count below every bucket (one block, NB <= 1024)
@@ -461,8 +502,13 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
     cv += (unsigned long long)hv[i] * hv[i];
     ck += (unsigned long long)hk[i] * hk[i];
   }
-  atomicAdd(&cost[0], cv);
-  atomicAdd(&cost[1], ck);
+  // wave sums first: 1024 LDS atomics on one address serialise (most of this kernel's 18 us)
+  cv = wave_sum_u64(cv);
+  ck = wave_sum_u64(ck);
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    atomicAdd(&cost[0], cv);
+    atomicAdd(&cost[1], ck);
+  }
   __syncthreads();
   const bool bykey = cost[1] < cost[0];
   const SubMap f = bykey ? fk : fv;
@@ -561,7 +607,7 @@ static RankGeo rank_geo(int64_t n, int64_t m, int64_t mq = -1, int half = 0, int
   while (B < kRkMaxB && 2 * B <= std::max(g.cs, 1) && (int64_t)B * zint < m) B <<= 1;
   g.B = B;
   g.NB = 2 * B;
-  g.per = g_rank_per;
+  g.per = small ? g_rank_per_small : g_rank_per;
   g.nblk = (int)std::max<int64_t>(1, ceil_div(m, (int64_t)kRkThreads * g.per));
   g.C = 256;
   while (g.C < g.cs) g.C <<= 1;
@@ -792,14 +838,18 @@ template <typename T>
 static int rank_images_t(const T* xq, const T* zq, const T* z, int64_t m, const RankWork& w,
                          const RankGeo& g, uint64_t* x_rec, uint64_t* z_rec, hipStream_t st) {
   if (m > 0) {  // the sample: hashed positions of z, sorted (k_sort_chunks pads with ~0 past cs)
-    hipLaunchKernelGGL((k_rank_sample_sort<T>), dim3(1), dim3(std::min(g.C, 1024)), 0, st, z,
-                       m, g.cs, g.C, w.ss);
+    if (g.C <= 512)
+      hipLaunchKernelGGL((k_rank_sample_sort<T>), dim3(1), dim3(1024), 0, st, z, m, g.cs, g.C,
+                         w.ss);
+    else
+      hipLaunchKernelGGL((k_rank_sample_bitonic<T>), dim3(1), dim3(g.C / 4), g.C * 8, st, z, m,
+                         g.cs, g.C, w.ss);
     TW_LAUNCH_CHECK();
     auto passes = [&](auto per) {
       constexpr int PER = decltype(per)::value;
       hipLaunchKernelGGL((k_rank_hist<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
                          w.ss, w.rel);
-      if (g.nblk <= kWave) {  // small Z: rows and starts in one block
+      if (g.nblk <= 2 * kWave) {  // small Z: rows and starts in one block
         hipLaunchKernelGGL(k_rank_rows_starts, dim3(1), dim3(1024), 0, st, g, w.rel, w.total,
                            w.start);
       } else {
@@ -887,13 +937,15 @@ extern "C" int tw_rank_set_plan(int32_t sample, int32_t per) {
   return TW_OK;
 }
 
-extern "C" int tw_rank_set_small(int32_t sample, int32_t z_per_interval) {
+extern "C" int tw_rank_set_small(int32_t sample, int32_t z_per_interval, int32_t per) {
   TW_ARG_CHECK(sample == 256 || sample == 512 || sample == 1024 || sample == 2048,
                "tw_rank_set_small: sample of 256, 512, 1024 or 2048 keys");
   TW_ARG_CHECK(z_per_interval == 512 || z_per_interval == 1024 || z_per_interval == 2048,
                "tw_rank_set_small: 512, 1024 or 2048 z per interval bucket");
+  TW_ARG_CHECK(per == 4 || per == 8 || per == 16, "tw_rank_set_small: 4, 8 or 16 z per thread");
   g_rank_cs_small = sample;
   g_rank_zint_small = z_per_interval;
+  g_rank_per_small = per;
   return TW_OK;
 }
 
