@@ -86,8 +86,9 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 // The poller spins on RELAXED loads of the counter and, once it has seen the target, issues
 // ONE agent-scope ACQUIRE fence (buffer_inv sc1) — acquire loads in the spin itself would
 // invalidate the L2 on every iteration; the fence after the last relaxed load that read the
-// release's value gives the same synchronisation (fence-atomic rule).  The block barrier after
-// the poll orders every wave's loads of the published words (ld_agent) after the fence.
+// release's value gives the same synchronisation (fence-atomic rule), and s_waitcnt vmcnt(0)
+// holds the block barrier after the poll until the invalidate has completed, so every wave's
+// loads of the published words (ld_agent) come after it.
 // TW_SEG_BARRIER (A/B builds, tools/ab_barrier.py): 0 = relaxed arrival and spin, no fence
 // (round 3); 1 = acquire loads in the spin; 2 (default) = as above.
 #ifndef TW_SEG_BARRIER
@@ -117,7 +118,12 @@ __device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  if (TW_SEG_BARRIER == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (TW_SEG_BARRIER == 2) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the invalidate completes before the block barrier lets any wave load (the consumer
+    // recipe of MI355X_MICROARCH.md: relaxed poll -> acquire -> vmcnt(0) -> barrier -> loads)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   return true;
 }
 
