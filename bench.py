@@ -1412,15 +1412,19 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         # at every G (the GPU work of every rank is done; the others wait at the final barrier):
         # the reference's est.UnN restated on 1 core, and the same blocks spread over the host
-        # cores of this run's CPU share — 16 per GPU on the pool's boxes (os.cpu_count() and the
-        # affinity mask show the whole machine, which the GPU boxes share out per GPU)
+        # cores of this run's CPU share: on a whole 8-GPU node every core of the affinity mask
+        # (the node-wide figure); on the pool's smaller boxes 16 per GPU (os.cpu_count() and the
+        # affinity mask show the whole machine, which those boxes share out per GPU)
         progress("CPU baselines")
         out["cpu_baseline"] = cpu_baseline(args.n, args.shards, args.cpu_shards)
         aff = len(os.sched_getaffinity(0))
-        share = min(16 * world, aff)
+        node = world >= 8
+        share = aff if node else min(16 * world, aff)
         allc = cpu_baseline_all_cores(args.n, args.shards, share)
-        allc["label"] = (f"{share} host cores = 16 per GPU x {world} GPU(s), the pool's CPU share "
-                         f"(affinity mask {aff}, os.cpu_count() {os.cpu_count()})")
+        allc["label"] = ((f"{share} host cores = the whole affinity mask of the {world}-GPU node"
+                          if node else
+                          f"{share} host cores = 16 per GPU x {world} GPU(s), the pool's CPU "
+                          f"share") + f" (affinity mask {aff}, os.cpu_count() {os.cpu_count()})")
         out["cpu_baseline"]["all_cores"] = allc
         out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(args.n, args.shards, B_inc,
                                                                     args.cpu_inc_shards)
