@@ -121,3 +121,41 @@ def test_wide_swr_in_kernel_equals_row_tables(gpu, mod, monkeypatch):
         hist[swr] = p
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert hist[True][k] == hist[False][k], k
+
+
+@pytest.mark.parametrize("d,N,loss,optim", [(64, 8, "hinge", "momentum"),
+                                            (100, 24, "logistic", "SGD"),
+                                            (512, 40, "hinge", "momentum"),
+                                            (512, 3, "logistic", "momentum")])
+def test_update_tail_equals_separate_update(gpu, d, N, loss, optim, monkeypatch):
+    """learning.UPDATE_TAIL (wide rows, device RNG: the step's update in the gradient launch's
+    tail, tw_pair_grad_rng_swr_update — the last arrivals sum the shard gradients in shard order
+    and step w / dw) against the gradient launch + k_sgd_update: w and dw bit for bit after
+    every segment, graphs and eager, segments through reshuffles, fewer shards than updater
+    parts (N = 3) and more (N = 24, 40)."""
+    import torch
+    import tuplewise.learning as lr
+    rng = np.random.RandomState(11)
+    n = 40 * N
+    X = rng.normal(0.3, 1.0, size=(n, d))
+    Z = rng.normal(0.0, 1.0, size=(n, d))
+    w0 = rng.normal(0.0, 0.1, size=(d, 1))
+    out = {}
+    for tail in (True, False):
+        monkeypatch.setattr(lr, "UPDATE_TAIL", tail)
+        eng = lr.SGDEngine(X, Z, w0, N, 16, 1.0, 0.01, 0.05, optim, loss=loss)
+        eng.enable_device_rng(1234)
+        assert eng._tail_ok() == tail and eng.swr_segments_ok(2)
+        traj = []
+        for i, (nseg, graphs) in enumerate([(5, True), (7, False), (1, True), (12, True)]):
+            eng.run_segment(nseg, False, graphs, swr_mod=3)
+            traj.append((eng.w.cpu().numpy().copy(), eng.dw.cpu().numpy().copy()))
+        eng.check()
+        out[tail] = traj
+        assert int(eng.step_ctr.item()) == 25
+        if tail:
+            assert eng._tail_ctl.cpu().tolist()[:3] == [0, 0, 0]
+        del eng
+        torch.cuda.synchronize()
+    for (wa, da), (wb, db) in zip(out[True], out[False]):
+        assert np.array_equal(wa, wb) and np.array_equal(da, db)

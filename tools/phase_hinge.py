@@ -28,8 +28,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "build":
                         "-std=c++17", "-ffp-contract=off", "-DTW_HINGE_TIMING", "-c",
                         str(CSRC / src), "-o", str(o)], check=True)
         objs.append(str(o))
+    # the rest of the library as built (make), for the symbols hinge.hip uses from elsewhere
+    rest = [str(p) for p in sorted(CSRC.glob("*.o"))
+            if p.name not in ("capi.o", "hinge.o")]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
-                    str(OUT)] + objs, check=True)
+                    str(OUT)] + objs + rest + ["-ldl", "-pthread"], check=True)
     sys.exit(0)
 
 import torch  # noqa: E402

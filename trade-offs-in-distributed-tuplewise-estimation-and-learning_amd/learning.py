@@ -61,6 +61,9 @@ EVAL_FUSED = True
 # pipelined replay loop: the draws made ahead by a native thread (csrc/drawpipe.hip) rather
 # than a Python worker thread
 NATIVE_DRAWS = True
+# wide rows (C5), device RNG, one process: the step's update folded into the gradient launch's
+# tail (tw_pair_grad_rng_swr_update) instead of a k_sgd_update launch per step
+UPDATE_TAIL = True
 # replay segments run through reshuffles (one process, replicated X, narrow segments): the
 # reshuffles' SWR tables ride in the segment's upload, the kernel switches tables by step
 REPLAY_THROUGH = True
@@ -195,10 +198,15 @@ class SGDEngine:
 
     def check(self):
         """Raise if a persistent segment launch gave up waiting at a grid barrier (its bounded
-        spin expired: the blocks were not co-resident); the state is then invalid."""
+        spin expired: the blocks were not co-resident), or a fused update tail gave up waiting
+        for the step's gradients; the state is then invalid."""
         if self._ctl is not None and int(self._ctl[1].item()) != 0:
             raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
                                "co-resident); the SGD state is invalid")
+        tc = getattr(self, "_tail_ctl", None)
+        if tc is not None and int(tc[1].item()) != 0:
+            raise RuntimeError("tw_pair_grad_rng_swr_update: the update tail timed out waiting "
+                               "for the step's gradients; the SGD state is invalid")
 
     def table_stacks(self, ntab: int):
         """Replay segments through reshuffles (tw_sgd_segment_narrow_tables): the row tables
@@ -629,6 +637,16 @@ class SGDEngine:
     def step_device(self, swr_mod: int = 0):
         if self.complete:
             return self.step_complete()
+        if swr_mod and self._tail_ok():
+            # the update in the gradient launch's tail (one launch per step, same bits)
+            if getattr(self, "_tail_ctl", None) is None:
+                self._tail_ctl = self.t.zeros((4,), dtype=self.t.int32, device=self.w.device)
+            L.call("tw_pair_grad_rng_swr_update", L.ptr(self.X), L.ptr(self.Z), self.d,
+                   self.n_X, self.n_Z, self.kx, self.kz, self.N_loc, self.B, L.ptr(self.w),
+                   L.ptr(self.dw), self.margin, self.loss, self.seed, L.ptr(self.step_ctr),
+                   int(swr_mod), 0, self.reg, self.lr, self.momentum, L.ptr(self.grads_loc),
+                   L.ptr(self._tail_ctl), L.stream_handle())
+            return
         if swr_mod:  # the rows of the step's last reshuffle, drawn in the kernel
             L.call("tw_pair_grad_rng_swr", L.ptr(self.X), L.ptr(self.Z), self.d, self.n_X,
                    self.n_Z, self.kx, self.kz, self.N_loc, self.B, L.ptr(self.w), self.margin,
@@ -641,6 +659,18 @@ class SGDEngine:
                self.margin, self.loss, self.seed, L.ptr(self.step_ctr), self.shard_base,
                L.ptr(self.grads_loc), L.stream_handle())
         self._update()
+
+    def _tail_ok(self) -> bool:
+        """The wide-row step's update folds into the gradient launch
+        (tw_pair_grad_rng_swr_update): one process, every shard in the launch, the streaming
+        kernel (UPDATE_TAIL)."""
+        ok = getattr(self, "_tail_flag", None)
+        if ok is None:
+            ok = self._tail_flag = bool(
+                UPDATE_TAIL and self.G == 1 and self.vgroup is None and not self.complete
+                and self.N_loc == self.N
+                and L.lib().tw_pair_grad_rng_swr_update_ok(self.d, self.N_loc))
+        return ok
 
     def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True,
                     swr_mod: int = 0):
