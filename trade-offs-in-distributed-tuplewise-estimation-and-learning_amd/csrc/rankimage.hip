@@ -70,6 +70,11 @@ static int g_rank_zint_small = 2048;
 static int g_rank_per_small = 4;  // 43 vs 47 us at 1e5 + 1e5 (profiles/r04s7_rank_small_per*.log)
 constexpr int kRkMaxB = 256;                       // splitter intervals (511 buckets max)
 constexpr int kRkSub = 2048;                       // sub-buckets per interval bucket
+// sub-buckets of more than kRkSortedMin keys (ties, skew) are sorted in place by the sub-sort
+// (up to kRkSortedMax keys) and binary-searched by the record pass, whose scan of a sub-bucket
+// was otherwise unbounded (1000 copies of each of 1000 values took 3.6 ms)
+constexpr uint32_t kRkSortedMin = 32;
+constexpr uint32_t kRkSortedMax = 4096;
 
 // position of sample i in [0, m): a hashed, not an index-strided, sample (Z with periodic
 // structure would give an evenly spaced sample of repeated values)
@@ -520,6 +525,28 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
   for (int i = threadIdx.x; i <= kRkSub; i += kSubThreads) sp_out[i] = h[i];
   __syncthreads();
   each([&](uint64_t k) { skeys[s0 + atomicAdd(&h[f(key_value<T>(k), k)], 1u)] = k; });
+  // long sub-buckets sorted in place: h[i] is now the END of sub-bucket i
+  __shared__ uint16_t longs[kRkSub];
+  __shared__ int nlong;
+  if (threadIdx.x == 0) nlong = 0;
+  __syncthreads();  // also: the scatter's skeys stores are visible to the whole block
+  for (int i = threadIdx.x; i < kRkSub; i += kSubThreads) {
+    const uint32_t L = h[i] - (i ? h[i - 1] : 0u);
+    if (L > kRkSortedMin && L <= kRkSortedMax) longs[atomicAdd(&nlong, 1)] = (uint16_t)i;
+  }
+  __syncthreads();
+  const int nl = nlong;
+  if (nl == 0) return;
+  __shared__ uint64_t sbuf[kRkSortedMax];
+  for (int li = 0; li < nl; ++li) {
+    const int i = longs[li];
+    const uint32_t a = i ? h[i - 1] : 0u, L = h[i] - a;
+    for (uint32_t t = threadIdx.x; t < kRkSortedMax; t += kSubThreads)
+      sbuf[t] = t < L ? skeys[s0 + a + t] : ~0ull;
+    __syncthreads();
+    sort_keys_block<kRkSortedMax / kSubThreads>(sbuf, (int)kRkSortedMax, skeys + s0 + a, (int)L);
+    __syncthreads();
+  }
 }
 
 // pass 5: every element in input order, one per thread (the chain splitters -> bucket map ->
@@ -555,10 +582,35 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_records(
       const uint32_t lo = pt[sb], hi = pt[sb + 1];
       const uint64_t* q = skeys + gv;
       uint32_t below = lo, eq = 0;
-      for (uint32_t i = lo; i < hi; ++i) {
-        const uint64_t k = q[i];
-        below += k < key ? 1u : 0u;
-        eq += k == key ? 1u : 0u;
+      if (hi - lo > kRkSortedMin && hi - lo <= kRkSortedMax) {  // sorted by the sub-sort
+        uint32_t a = lo, n = hi - lo;  // lower_bound(key)
+        while (n > 0) {
+          const uint32_t h2 = n >> 1;
+          if (q[a + h2] < key) {
+            a += h2 + 1;
+            n -= h2 + 1;
+          } else {
+            n = h2;
+          }
+        }
+        uint32_t b2 = a, m2 = hi - a;  // upper_bound(key)
+        while (m2 > 0) {
+          const uint32_t h2 = m2 >> 1;
+          if (q[b2 + h2] <= key) {
+            b2 += h2 + 1;
+            m2 -= h2 + 1;
+          } else {
+            m2 = h2;
+          }
+        }
+        below = a;
+        eq = b2 - a;
+      } else {
+        for (uint32_t i = lo; i < hi; ++i) {
+          const uint64_t k = q[i];
+          below += k < key ? 1u : 0u;
+          eq += k == key ? 1u : 0u;
+        }
       }
       gv += below;
       hv = gv + eq;

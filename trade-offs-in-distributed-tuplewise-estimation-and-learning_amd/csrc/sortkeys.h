@@ -70,7 +70,8 @@ __device__ __forceinline__ void reg_levels(uint64_t (&v)[E], int base, int k, in
 // The network on C keys already in LDS (`keys`), thread t owning [E t, E t + E); the sorted
 // keys written to dst.  Every thread of the block (C / E of them) calls it.
 template <int kE>
-__device__ __forceinline__ void sort_keys_block(uint64_t* keys, int C, uint64_t* __restrict__ dst) {
+__device__ __forceinline__ void sort_keys_block(uint64_t* keys, int C, uint64_t* __restrict__ dst,
+                                                int n_out = -1) {
   const int nthr = blockDim.x;  // == C / kE
   const int tid = threadIdx.x;
   const int base = tid * kE;
@@ -108,7 +109,8 @@ __device__ __forceinline__ void sort_keys_block(uint64_t* keys, int C, uint64_t*
 #pragma unroll
   for (int e = 0; e < kE; ++e) keys[base + e] = v[e];
   __syncthreads();
-  for (int i = tid; i < C; i += nthr) dst[i] = keys[i];
+  const int n = n_out < 0 ? C : n_out;  // the first n sorted keys (pads sort last)
+  for (int i = tid; i < n; i += nthr) dst[i] = keys[i];
 }
 
 template <typename T, int kE>
