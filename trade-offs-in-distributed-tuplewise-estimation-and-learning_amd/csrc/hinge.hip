@@ -288,45 +288,54 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
 // k_hinge_grad_wide (per pair: lane partial dots over the same 8 columns + the same butterfly;
 // column sums in row order), so identical bits.
 
-// The step's update (make_exps.py:130-141, k_sgd_update's arithmetic) folded into the tail of
-// the streaming gradient launch (one process, all shards in the launch; tw_pair_grad_rng_swr_
-// update): every block publishes its shard gradient row and takes an arrival ticket (agent-
-// scope release); the LAST kUpdParts arrivals wait for the others (relaxed spin, one acquire
-// fence) and each updates d / kUpdParts columns — the N x cols gradient tile staged in LDS by
-// all 1024 threads, then each column summed over the shards in order from +0.0 as
-// k_sgd_update does, so the bits are those of the two launches.  A ticket is taken only after
-// the block's own reads of w are done, and the updaters wait for every ticket, so no block
-// reads a w the tail has written.  ctl[0] arrivals, ctl[1] abort word (a spin that gave up),
-// ctl[2] updaters done (the last one zeroes ctl[0] and ctl[2] for the next launch).
-struct UpdTail {
-  double* w;         // w (read at the start of every block, written by the updaters)
-  double* dw;
-  uint32_t* ctl;     // nullptr: no tail (the update runs as its own launch)
-  uint64_t* d_step;  // advanced by one by the first updater
+// The PREVIOUS step's update folded into this step's gradient launch (wide rows, one process:
+// tw_pair_grad_rng_swr_step).  The update of step t-1 and the pair chain of step t are
+// independent until S needs w, ~12 us into the block (the first chunk's rows, C5), so each
+// block — after resolving its pairs' rows and issuing the first two chunks' loads — updates
+// d / G columns (the G x cols tile of the previous launch's shard gradients staged in LDS, each
+// column summed in shard order from +0.0: k_sgd_update's arithmetic), stores them write-through
+// (agent-scope atomic stores) and drained, takes an arrival ticket, and waits at a grid barrier
+// for every block's columns (relaxed spin on a monotonic 64-bit counter: target = the ticket's
+// generation + 1, times G; one agent acquire fence) before it loads w.  All G blocks must be
+// resident at once (tw_pair_grad_rng_swr_step_ok); a spin that gives up sets ctl[2] (the
+// engine raises).  Slots: w_in / dw_in / grads_in are the previous step's (grads_in null: no
+// pending update, w_out := w_in), w_out / dw_out this step's, ping-ponged by the caller, so no
+// block overwrites what another block of the launch reads; the caller ends a run of such
+// launches with tw_sgd_update_to, as the narrow fused steps (tw_sgd_step) do.
+struct PreUpd {
+  const double* w_in;
+  const double* dw_in;
+  const double* grads_in;
+  double* w_out;
+  double* dw_out;
+  uint64_t* ctl;  // nullptr: no prologue (w read from the kernel's w argument)
   double reg, lr, momentum;
+  uint32_t step_off;  // this launch's step counter = *d_step + step_off
 };
-constexpr int kUpdParts = 16;
-constexpr uint64_t kUpdSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+constexpr uint64_t kPreSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
 template <int LOSS>
 __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
-    const double* w, double margin, double* __restrict__ out, uint64_t seed,
-    const uint64_t* d_step, uint32_t shard_base, SwrMap swr, UpdTail tail) {
+    const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
+    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr, PreUpd pre) {
   __shared__ double diff[2][kStreamCH * kWideMaxD];  // 128 KiB
   __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
   __shared__ double flag[2][kStreamCH];
+  __shared__ int s_ok;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int dd = (int)d;
-  const uint64_t step = d_step ? *d_step : 0;
+  const uint64_t step = (d_step ? *d_step : 0) + (pre.ctl ? pre.step_off : 0u);
   double wv[kWideCols];
+  if (pre.ctl == nullptr) {
 #pragma unroll
-  for (int c = 0; c < kWideCols; ++c) {
-    const int j = lane + c * kWave;
-    wv[c] = j < dd ? w[j] : 0.0;
+    for (int c = 0; c < kWideCols; ++c) {
+      const int j = lane + c * kWave;
+      wv[c] = j < dd ? w[j] : 0.0;
+    }
   }
   double acc = 0.0;  // thread j < d: column j
   double zv[2][kWideCols], xv[2][kWideCols];
@@ -402,6 +411,74 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     };
     load(0, 0);
     if (kStreamCH < np) load(1, kStreamCH);
+    if (pre.ctl && P0 == 0) {
+      // the pending update of columns [u0, u1) while the first chunks' rows are in flight
+      const int G = (int)gridDim.x;
+      const int u0 = (int)((int64_t)s * dd / G), u1 = (int)((int64_t)(s + 1) * dd / G);
+      const int nc = u1 - u0;
+      double* tile = &diff[1][0];  // idle until the second chunk: G x nc <= 16 x 512 doubles
+      if (pre.grads_in) {
+        for (int e = threadIdx.x; e < G * nc; e += kWideBlock) {
+          const int r = e / nc, c = e - r * nc;
+          tile[e] = pre.grads_in[(int64_t)r * d + u0 + c];
+        }
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < nc) {
+        const int c = threadIdx.x, j = u0 + c;
+        double wj = pre.w_in[j], dwj = pre.dw_in[j];
+        if (pre.grads_in) {
+          double sum = 0.0;  // shard order from +0.0, as k_sgd_update
+          int r = 0;
+          for (; r + 8 <= G; r += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * nc + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sum += v[u];
+          }
+          for (; r < G; ++r) sum += tile[r * nc + c];
+          const double g = sum / (double)G + pre.reg * wj;
+          const double stp = pre.momentum >= 0.0 ? pre.momentum * dwj + pre.lr * g : pre.lr * g;
+          dwj = stp;
+          wj = wj - stp;
+        }
+        __hip_atomic_store((uint64_t*)&pre.w_out[j], __builtin_bit_cast(uint64_t, wj),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((uint64_t*)&pre.dw_out[j], __builtin_bit_cast(uint64_t, dwj),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // publish: this wave's write-through stores drained, then one ticket per block; wait
+      // for the whole generation (every block of this launch), acquire, then load w
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint64_t tk =
+            __hip_atomic_fetch_add(pre.ctl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t target = (tk / (uint64_t)G + 1) * (uint64_t)G;
+        const uint64_t t0 = wall_clock64();
+        int ok = 1;
+        while (__hip_atomic_load(pre.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (__hip_atomic_load(pre.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull ||
+              wall_clock64() - t0 > kPreSpinTicks) {
+            __hip_atomic_store(pre.ctl + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_ok = ok;
+      }
+      __syncthreads();
+      if (!s_ok) return;  // the barrier gave up: the state is invalid (the engine raises)
+#pragma unroll
+      for (int c = 0; c < kWideCols; ++c) {
+        const int j = lane + c * kWave;
+        wv[c] = j < dd ? pre.w_out[j] : 0.0;
+      }
+    }
     int c0 = 0;
     for (; c0 + kStreamCH < np; c0 += 2 * kStreamCH) {  // stages alternate; constant indices
       chunk(0, c0);
@@ -411,87 +488,6 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
   }
   if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
   HG_STAMP(3);
-  if (tail.ctl == nullptr) return;
-  // ---- the update tail: publish, ticket, the last kUpdParts arrivals update the columns
-  __shared__ uint32_t s_tk;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gradient stores landed
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_tk = __hip_atomic_fetch_add(tail.ctl, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int G = (int)gridDim.x;
-  const int parts = G < kUpdParts ? G : kUpdParts;
-  const int part = (int)s_tk - (G - parts);
-  if (part < 0) return;
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = wall_clock64();
-    int ok = 1;
-    while (__hip_atomic_load(tail.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           (uint32_t)G) {
-      if (__hip_atomic_load(tail.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-          wall_clock64() - t0 > kUpdSpinTicks) {
-        __hip_atomic_store(tail.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_tk = ok;
-  }
-  __syncthreads();
-  if (!s_tk) return;  // gave up (abort word set): the state is invalid, the engine raises
-  // columns [c0, c1) of this part; the G x nc tile through the (now idle) diff buffer
-  const int c0 = (int)((int64_t)part * dd / parts), c1 = (int)((int64_t)(part + 1) * dd / parts);
-  const int nc = c1 - c0;
-  double* tile = &diff[0][0];  // 2 x 16 x 512 doubles = 128 KiB >= G x nc for G x d <= 2^14 x 16
-  const int64_t tot = (int64_t)G * nc;
-  for (int64_t e0 = 0; e0 < tot; e0 += (int64_t)kWideBlock * 8) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {  // eight loads in flight per thread, then the stores
-      const int64_t e = e0 + u * kWideBlock + threadIdx.x;
-      const int64_t r = e / nc, c = e - r * nc;
-      v[u] = e < tot ? out[r * d + c0 + c] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t e = e0 + u * kWideBlock + threadIdx.x;
-      if (e < tot) tile[e] = v[u];
-    }
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < nc) {
-    const int c = threadIdx.x;
-    double sum = 0.0;  // shard order from +0.0, as k_sgd_update
-    int r = 0;
-    for (; r + 8 <= G; r += 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = tile[(int64_t)(r + u) * nc + c];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
-    for (; r < G; ++r) sum += tile[(int64_t)r * nc + c];
-    const int j = c0 + c;
-    const double wj = tail.w[j];
-    const double g = sum / (double)G + tail.reg * wj;
-    const double stp = tail.momentum >= 0.0 ? tail.momentum * tail.dw[j] + tail.lr * g
-                                            : tail.lr * g;
-    tail.dw[j] = stp;
-    tail.w[j] = wj - stp;
-  }
-  if (part == 0 && threadIdx.x == 0 && tail.d_step) *tail.d_step += 1;
-  // the last updater to finish leaves the counters at zero for the next launch
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(tail.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          (uint32_t)parts - 1) {
-    __hip_atomic_store(tail.ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tail.ctl + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // One whole SGD step for narrow rows (d <= 32, C4) in ONE launch: the update of the PREVIOUS
@@ -720,7 +716,7 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
                         double margin, uint64_t seed, const uint64_t* d_step,
                         uint32_t shard_base, double* out, hipStream_t st,
                         double* s_out = nullptr, SwrMap swr = SwrMap{0, 0, 1, 1},
-                        UpdTail tail = UpdTail{nullptr, nullptr, nullptr, nullptr, 0, 0, 0}) {
+                        PreUpd pre = PreUpd{}) {
   // per staged pair: d diff doubles + two row indices + one weight, <= 64 KiB in all
   const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / (d + 3)));
   const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(double) * CH;
@@ -743,7 +739,7 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 0)
     hipLaunchKernelGGL(k_hinge_grad_stream<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
-                       shard_base, swr, tail);
+                       shard_base, swr, pre);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 2)
     hipLaunchKernelGGL(k_hinge_grad_wide<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
@@ -759,16 +755,14 @@ int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* row
                  int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
                  const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st,
                  int32_t loss = TW_LOSS_HINGE, double* s_out = nullptr,
-                 SwrMap swr = SwrMap{0, 0, 1, 1},
-                 UpdTail tail = UpdTail{nullptr, nullptr, nullptr, nullptr, 0, 0, 0}) {
+                 SwrMap swr = SwrMap{0, 0, 1, 1}, PreUpd pre = PreUpd{}) {
   if (loss == TW_LOSS_LOGISTIC)
     launch_grad_kernel<TW_LOSS_LOGISTIC>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
                                          margin, seed, d_step, shard_base, out, st, s_out, swr,
-                                         tail);
+                                         pre);
   else
     launch_grad_kernel<TW_LOSS_HINGE>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                      margin, seed, d_step, shard_base, out, st, s_out, swr,
-                                      tail);
+                                      margin, seed, d_step, shard_base, out, st, s_out, swr, pre);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -777,25 +771,25 @@ int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* row
 
 using namespace tw;
 
-// the fused update tail applies: the streaming kernel (32 < d <= 512, not the legacy variant),
-// every block resident at once (one 1024-thread block per CU: the updaters spin on the others),
-// and the G x (d / parts) gradient tile within the 128 KiB diff buffer
-static bool tail_shape_ok(int64_t d, int32_t n_shards) {  // no HIP call: runs in captures
+// the streaming kernel with the previous step's update in its prologue applies: 32 < d <= 512
+// (not the legacy wide variant), the G x ceil(d / G) column tile in half the diff buffer, every
+// one of the n_shards blocks resident at once (the prologue's grid barrier)
+static bool pre_shape_ok(int64_t d, int32_t n_shards) {  // no HIP call: runs in captures
   if (d <= 32 || d > kWideMaxD || g_hinge_legacy_wide != 0 || n_shards < 1) return false;
-  const int parts = n_shards < kUpdParts ? n_shards : kUpdParts;
-  const int64_t nc = ceil_div(d, (int64_t)parts);
-  return (int64_t)n_shards * nc <= 2 * kStreamCH * kWideMaxD;
+  return (int64_t)n_shards * ceil_div(d, (int64_t)n_shards) <= kStreamCH * kWideMaxD;
 }
 
-extern "C" int tw_pair_grad_rng_swr_update_ok(int64_t d, int32_t n_shards) {
-  if (!tail_shape_ok(d, n_shards)) return 0;
-  int dev = 0, cus = 0;
+extern "C" int tw_pair_grad_rng_swr_step_ok(int64_t d, int32_t n_shards) {
+  if (!pre_shape_ok(d, n_shards)) return 0;
+  int dev = 0, per_cu = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hinge_grad_stream<TW_LOSS_HINGE>,
+                                                   kWideBlock, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
     return 0;
   }
-  return n_shards <= cus;
+  return (int64_t)std::min(per_cu, 1) * cus >= n_shards;
 }
 
 static int check_loss(int32_t loss) {
@@ -1107,27 +1101,33 @@ extern "C" int tw_pair_grad_rng_swr(const double* d_X, const double* d_Z, int64_
                       loss, nullptr, SwrMap{(uint64_t)swr_mod, swr_base, n_X, n_Z});
 }
 
-// tw_pair_grad_rng_swr + tw_sgd_update in ONE launch (the update in the gradient kernel's
-// tail; same bits): for the streaming wide kernel (32 < d <= 512) over every shard of the step
-// (one process).  d_ctl: 3 zeroed uint32 words kept across launches.
-extern "C" int tw_pair_grad_rng_swr_update(
+// One learning step for wide rows in ONE launch: the previous step's update (k_sgd_update's
+// arithmetic; d_grads_in null: none pending) in the prologue of this step's device-RNG gradient
+// (tw_pair_grad_rng_swr: rows of the step's last reshuffle drawn in the kernel); see PreUpd.
+// Step k of a run uses counter *d_step + step_off; end the run with tw_sgd_update_to.
+// d_ctl: 2 uint64 words, zero before the first launch (ctl[0] only grows; ctl[1] != 0: a grid
+// barrier gave up and the state is invalid).  The residency half of
+// tw_pair_grad_rng_swr_step_ok is the caller's, made once before any stream capture.
+extern "C" int tw_pair_grad_rng_swr_step(
     const double* d_X, const double* d_Z, int64_t d, int64_t n_X, int64_t n_Z, int64_t kx,
-    int64_t kz, int32_t n_shards, int64_t B, double* d_w, double* d_dw, double margin,
-    int32_t loss, uint64_t seed, uint64_t* d_step, int64_t swr_mod, uint64_t swr_base,
-    double reg, double lr, double momentum, double* d_grads, uint32_t* d_ctl, void* stream) {
-  // (the residency half of tw_pair_grad_rng_swr_update_ok is the caller's, made once before
-  // any stream capture)
-  TW_ARG_CHECK(tail_shape_ok(d, n_shards),
-               "tw_pair_grad_rng_swr_update: d=%lld, n_shards=%d outside the fused kernel",
+    int64_t kz, int32_t n_shards, int64_t B, double margin, int32_t loss, uint64_t seed,
+    const uint64_t* d_step, int32_t step_off, int64_t swr_mod, uint64_t swr_base,
+    const double* d_w_in, const double* d_dw_in, const double* d_grads_in, double reg,
+    double lr, double momentum, double* d_w_out, double* d_dw_out, double* d_grads_out,
+    uint64_t* d_ctl, void* stream) {
+  TW_ARG_CHECK(pre_shape_ok(d, n_shards),
+               "tw_pair_grad_rng_swr_step: d=%lld, n_shards=%d outside the fused kernel",
                (long long)d, n_shards);
   TW_ARG_CHECK(B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1 && n_X >= 1 && n_Z >= 1 &&
-                   swr_mod >= 1 && d_step && d_w && d_dw && d_grads && d_ctl,
-               "tw_pair_grad_rng_swr_update: bad sizes or null pointers");
+                   swr_mod >= 1 && step_off >= 0 && d_step && d_w_in && d_dw_in && d_w_out &&
+                   d_dw_out && d_grads_out && d_ctl,
+               "tw_pair_grad_rng_swr_step: bad sizes or null pointers");
   if (int rc = check_loss(loss)) return rc;
-  return launch_hinge(d_X, d_Z, d, nullptr, kx, nullptr, kz, nullptr, nullptr, n_shards, B, d_w,
-                      margin, seed, d_step, 0, d_grads, (hipStream_t)stream, loss, nullptr,
-                      SwrMap{(uint64_t)swr_mod, swr_base, n_X, n_Z},
-                      UpdTail{d_w, d_dw, d_ctl, d_step, reg, lr, momentum});
+  return launch_hinge(d_X, d_Z, d, nullptr, kx, nullptr, kz, nullptr, nullptr, n_shards, B,
+                      nullptr, margin, seed, d_step, 0, d_grads_out, (hipStream_t)stream, loss,
+                      nullptr, SwrMap{(uint64_t)swr_mod, swr_base, n_X, n_Z},
+                      PreUpd{d_w_in, d_dw_in, d_grads_in, d_w_out, d_dw_out, d_ctl, reg, lr,
+                             momentum, (uint32_t)step_off});
 }
 
 extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,
