@@ -584,25 +584,6 @@ int tw_pair_grad_rng_swr(const double* d_X, const double* d_Z, int64_t d, int64_
                          const double* d_w, double margin, int32_t loss, uint64_t seed,
                          const uint64_t* d_step, int32_t shard_base, int64_t swr_mod,
                          uint64_t swr_base, double* d_out, void* stream);
-/* One learning step for wide rows (32 < d <= 512) in ONE launch (make_exps.py:126-141): the
- * PREVIOUS step's update (tw_sgd_update's arithmetic on d_w_in / d_dw_in / d_grads_in; grads_in
- * null: none pending, w_out := w_in) in the prologue of this step's device-RNG gradient
- * (tw_pair_grad_rng_swr at counter *d_step + step_off) — each block updates d / n_shards columns
- * while its pairs' rows load, then a grid barrier (every block resident: _ok) before S needs w.
- * Writes d_w_out / d_dw_out (this step's w) and d_grads_out.  End a run of such steps with
- * tw_sgd_update_to; the bits are those of gradient + update launches.  d_ctl: 2 int64, zero
- * before the first launch (d_ctl[1] != 0: a barrier gave up; the state is invalid).
- * tw_pair_grad_rng_swr_step_ok: 1 where it applies on the current device (call it outside
- * stream captures). */
-int tw_pair_grad_rng_swr_step(const double* d_X, const double* d_Z, int64_t d, int64_t n_X,
-                              int64_t n_Z, int64_t kx, int64_t kz, int32_t n_shards, int64_t B,
-                              double margin, int32_t loss, uint64_t seed, const uint64_t* d_step,
-                              int32_t step_off, int64_t swr_mod, uint64_t swr_base,
-                              const double* d_w_in, const double* d_dw_in,
-                              const double* d_grads_in, double reg, double lr, double momentum,
-                              double* d_w_out, double* d_dw_out, double* d_grads_out,
-                              uint64_t* d_ctl, void* stream);
-int tw_pair_grad_rng_swr_step_ok(int64_t d, int32_t n_shards);
 int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
 int tw_sgd_segment_set_grid(int32_t max_blocks);
 int tw_sgd_segment_set_prefetch(int32_t rows);

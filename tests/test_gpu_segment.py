@@ -121,41 +121,3 @@ def test_wide_swr_in_kernel_equals_row_tables(gpu, mod, monkeypatch):
         hist[swr] = p
     for k in ("norm_w", "bc_AUC", "br_AUC", "tc_AUC", "tr_AUC"):
         assert hist[True][k] == hist[False][k], k
-
-
-@pytest.mark.parametrize("d,N,loss,optim", [(64, 8, "hinge", "momentum"),
-                                            (100, 24, "logistic", "SGD"),
-                                            (512, 40, "hinge", "momentum"),
-                                            (512, 256, "logistic", "momentum"),
-                                            (33, 3, "hinge", "momentum")])
-def test_wide_fused_steps_equal_separate_update(gpu, d, N, loss, optim, monkeypatch):
-    """learning.WIDE_FUSED_STEPS (wide rows, device RNG: each step's update in the prologue of
-    the next step's gradient launch, tw_pair_grad_rng_swr_step — every block updates its
-    d / N columns while its rows load, a grid barrier, then S) against gradient + k_sgd_update
-    launches per step: w and dw bit for bit after every segment, graphs and eager, one-step
-    segments, segments through reshuffles, more shards than columns per block (N = 256 at
-    d = 512: two columns each) and fewer (N = 3)."""
-    import torch
-    import tuplewise.learning as lr
-    rng = np.random.RandomState(11)
-    n = 40 * N
-    X = rng.normal(0.3, 1.0, size=(n, d))
-    Z = rng.normal(0.0, 1.0, size=(n, d))
-    w0 = rng.normal(0.0, 0.1, size=(d, 1))
-    out = {}
-    for fused in (True, False):
-        monkeypatch.setattr(lr, "WIDE_FUSED_STEPS", fused)
-        eng = lr.SGDEngine(X, Z, w0, N, 16, 1.0, 0.01, 0.05, optim, loss=loss)
-        eng.enable_device_rng(1234)
-        assert eng._wide_step_ok() == fused and eng.swr_segments_ok(2)
-        traj = []
-        for nseg, graphs in [(5, True), (7, False), (1, True), (12, True), (5, True)]:
-            eng.run_segment(nseg, False, graphs, swr_mod=3)
-            traj.append((eng.w.cpu().numpy().copy(), eng.dw.cpu().numpy().copy()))
-        eng.check()
-        out[fused] = traj
-        assert int(eng.step_ctr.item()) == 30
-        del eng
-        torch.cuda.synchronize()
-    for (wa, da), (wb, db) in zip(out[True], out[False]):
-        assert np.array_equal(wa, wb) and np.array_equal(da, db)

@@ -7,9 +7,5 @@ import sys
 
 sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
 import bench  # noqa: E402
-import tuplewise.learning as lr  # noqa: E402
-
-if "notail" in sys.argv:  # A/B: the update as its own k_sgd_update launch
-    lr.UPDATE_TAIL = False
 r = bench.sgd_steps_per_s(bench.C5_N, bench.C5_N, 512, 256, 100, 25, 300, 1)
 print(f"C5 B=100: {r['steps_per_s']:.0f} steps/s, {r['ms_per_step'] * 1e3:.1f} us/step", flush=True)

@@ -122,11 +122,7 @@ _SIGNATURES = {
                                      _i32, _i32, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp,
                                      _vp, _vp],
     "tw_pair_grad_rng_swr": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _vp, _f64,
-                             _i32, _u64, _vp, _i32, _i64, _u64, _vp, _vp],    "tw_pair_grad_rng_swr_step": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _f64,
-                                  _i32, _u64, _vp, _i32, _i64, _u64, _vp, _vp, _vp, _f64, _f64,
-                                  _f64, _vp, _vp, _vp, _vp, _vp],
-    "tw_pair_grad_rng_swr_step_ok": [_i64, _i32],
-
+                             _i32, _u64, _vp, _i32, _i64, _u64, _vp, _vp],
     "tw_sgd_segment_narrow_swr": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _f64,
                                   _i32, _u64, _vp, _i32, _i32, _i64, _u64, _vp, _vp, _f64,
                                   _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],

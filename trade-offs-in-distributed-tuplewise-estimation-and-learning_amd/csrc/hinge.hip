@@ -288,54 +288,25 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
 // k_hinge_grad_wide (per pair: lane partial dots over the same 8 columns + the same butterfly;
 // column sums in row order), so identical bits.
 
-// The PREVIOUS step's update folded into this step's gradient launch (wide rows, one process:
-// tw_pair_grad_rng_swr_step).  The update of step t-1 and the pair chain of step t are
-// independent until S needs w, ~12 us into the block (the first chunk's rows, C5), so each
-// block — after resolving its pairs' rows and issuing the first two chunks' loads — updates
-// d / G columns (the G x cols tile of the previous launch's shard gradients staged in LDS, each
-// column summed in shard order from +0.0: k_sgd_update's arithmetic), stores them write-through
-// (agent-scope atomic stores) and drained, takes an arrival ticket, and waits at a grid barrier
-// for every block's columns (relaxed spin on a monotonic 64-bit counter: target = the ticket's
-// generation + 1, times G; one agent acquire fence) before it loads w.  All G blocks must be
-// resident at once (tw_pair_grad_rng_swr_step_ok); a spin that gives up sets ctl[2] (the
-// engine raises).  Slots: w_in / dw_in / grads_in are the previous step's (grads_in null: no
-// pending update, w_out := w_in), w_out / dw_out this step's, ping-ponged by the caller, so no
-// block overwrites what another block of the launch reads; the caller ends a run of such
-// launches with tw_sgd_update_to, as the narrow fused steps (tw_sgd_step) do.
-struct PreUpd {
-  const double* w_in;
-  const double* dw_in;
-  const double* grads_in;
-  double* w_out;
-  double* dw_out;
-  uint64_t* ctl;  // nullptr: no prologue (w read from the kernel's w argument)
-  double reg, lr, momentum;
-  uint32_t step_off;  // this launch's step counter = *d_step + step_off
-};
-constexpr uint64_t kPreSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-
 template <int LOSS>
 __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
-    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr, PreUpd pre) {
+    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr) {
   __shared__ double diff[2][kStreamCH * kWideMaxD];  // 128 KiB
   __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
   __shared__ double flag[2][kStreamCH];
-  __shared__ int s_ok;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int dd = (int)d;
-  const uint64_t step = (d_step ? *d_step : 0) + (pre.ctl ? pre.step_off : 0u);
+  const uint64_t step = d_step ? *d_step : 0;
   double wv[kWideCols];
-  if (pre.ctl == nullptr) {
 #pragma unroll
-    for (int c = 0; c < kWideCols; ++c) {
-      const int j = lane + c * kWave;
-      wv[c] = j < dd ? w[j] : 0.0;
-    }
+  for (int c = 0; c < kWideCols; ++c) {
+    const int j = lane + c * kWave;
+    wv[c] = j < dd ? w[j] : 0.0;
   }
   double acc = 0.0;  // thread j < d: column j
   double zv[2][kWideCols], xv[2][kWideCols];
@@ -411,74 +382,6 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     };
     load(0, 0);
     if (kStreamCH < np) load(1, kStreamCH);
-    if (pre.ctl && P0 == 0) {
-      // the pending update of columns [u0, u1) while the first chunks' rows are in flight
-      const int G = (int)gridDim.x;
-      const int u0 = (int)((int64_t)s * dd / G), u1 = (int)((int64_t)(s + 1) * dd / G);
-      const int nc = u1 - u0;
-      double* tile = &diff[1][0];  // idle until the second chunk: G x nc <= 16 x 512 doubles
-      if (pre.grads_in) {
-        for (int e = threadIdx.x; e < G * nc; e += kWideBlock) {
-          const int r = e / nc, c = e - r * nc;
-          tile[e] = pre.grads_in[(int64_t)r * d + u0 + c];
-        }
-      }
-      __syncthreads();
-      if ((int)threadIdx.x < nc) {
-        const int c = threadIdx.x, j = u0 + c;
-        double wj = pre.w_in[j], dwj = pre.dw_in[j];
-        if (pre.grads_in) {
-          double sum = 0.0;  // shard order from +0.0, as k_sgd_update
-          int r = 0;
-          for (; r + 8 <= G; r += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * nc + c];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) sum += v[u];
-          }
-          for (; r < G; ++r) sum += tile[r * nc + c];
-          const double g = sum / (double)G + pre.reg * wj;
-          const double stp = pre.momentum >= 0.0 ? pre.momentum * dwj + pre.lr * g : pre.lr * g;
-          dwj = stp;
-          wj = wj - stp;
-        }
-        __hip_atomic_store((uint64_t*)&pre.w_out[j], __builtin_bit_cast(uint64_t, wj),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((uint64_t*)&pre.dw_out[j], __builtin_bit_cast(uint64_t, dwj),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      // publish: this wave's write-through stores drained, then one ticket per block; wait
-      // for the whole generation (every block of this launch), acquire, then load w
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const uint64_t tk =
-            __hip_atomic_fetch_add(pre.ctl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t target = (tk / (uint64_t)G + 1) * (uint64_t)G;
-        const uint64_t t0 = wall_clock64();
-        int ok = 1;
-        while (__hip_atomic_load(pre.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-          if (__hip_atomic_load(pre.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull ||
-              wall_clock64() - t0 > kPreSpinTicks) {
-            __hip_atomic_store(pre.ctl + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = 0;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_ok = ok;
-      }
-      __syncthreads();
-      if (!s_ok) return;  // the barrier gave up: the state is invalid (the engine raises)
-#pragma unroll
-      for (int c = 0; c < kWideCols; ++c) {
-        const int j = lane + c * kWave;
-        wv[c] = j < dd ? pre.w_out[j] : 0.0;
-      }
-    }
     int c0 = 0;
     for (; c0 + kStreamCH < np; c0 += 2 * kStreamCH) {  // stages alternate; constant indices
       chunk(0, c0);
@@ -715,8 +618,7 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
                         const int64_t* iz, int32_t n_shards, int64_t B, const double* w,
                         double margin, uint64_t seed, const uint64_t* d_step,
                         uint32_t shard_base, double* out, hipStream_t st,
-                        double* s_out = nullptr, SwrMap swr = SwrMap{0, 0, 1, 1},
-                        PreUpd pre = PreUpd{}) {
+                        double* s_out = nullptr, SwrMap swr = SwrMap{0, 0, 1, 1}) {
   // per staged pair: d diff doubles + two row indices + one weight, <= 64 KiB in all
   const int CH = (int)std::max<int64_t>(1, std::min<int64_t>(B, kLdsDoubles / (d + 3)));
   const size_t lds = sizeof(double) * CH * d + 2 * sizeof(int64_t) * CH + sizeof(double) * CH;
@@ -739,7 +641,7 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 0)
     hipLaunchKernelGGL(k_hinge_grad_stream<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z,
                        d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
-                       shard_base, swr, pre);
+                       shard_base, swr);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 2)
     hipLaunchKernelGGL(k_hinge_grad_wide<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
@@ -755,14 +657,13 @@ int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* row
                  int32_t n_shards, int64_t B, const double* w, double margin, uint64_t seed,
                  const uint64_t* d_step, uint32_t shard_base, double* out, hipStream_t st,
                  int32_t loss = TW_LOSS_HINGE, double* s_out = nullptr,
-                 SwrMap swr = SwrMap{0, 0, 1, 1}, PreUpd pre = PreUpd{}) {
+                 SwrMap swr = SwrMap{0, 0, 1, 1}) {
   if (loss == TW_LOSS_LOGISTIC)
     launch_grad_kernel<TW_LOSS_LOGISTIC>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                         margin, seed, d_step, shard_base, out, st, s_out, swr,
-                                         pre);
+                                         margin, seed, d_step, shard_base, out, st, s_out, swr);
   else
     launch_grad_kernel<TW_LOSS_HINGE>(X, Z, d, rows_x, kx, rows_z, kz, ix, iz, n_shards, B, w,
-                                      margin, seed, d_step, shard_base, out, st, s_out, swr, pre);
+                                      margin, seed, d_step, shard_base, out, st, s_out, swr);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -770,27 +671,6 @@ int launch_hinge(const double* X, const double* Z, int64_t d, const int64_t* row
 }  // namespace tw
 
 using namespace tw;
-
-// the streaming kernel with the previous step's update in its prologue applies: 32 < d <= 512
-// (not the legacy wide variant), the G x ceil(d / G) column tile in half the diff buffer, every
-// one of the n_shards blocks resident at once (the prologue's grid barrier)
-static bool pre_shape_ok(int64_t d, int32_t n_shards) {  // no HIP call: runs in captures
-  if (d <= 32 || d > kWideMaxD || g_hinge_legacy_wide != 0 || n_shards < 1) return false;
-  return (int64_t)n_shards * ceil_div(d, (int64_t)n_shards) <= kStreamCH * kWideMaxD;
-}
-
-extern "C" int tw_pair_grad_rng_swr_step_ok(int64_t d, int32_t n_shards) {
-  if (!pre_shape_ok(d, n_shards)) return 0;
-  int dev = 0, per_cu = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hinge_grad_stream<TW_LOSS_HINGE>,
-                                                   kWideBlock, 0) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  return (int64_t)std::min(per_cu, 1) * cus >= n_shards;
-}
 
 static int check_loss(int32_t loss) {
   TW_ARG_CHECK(loss == TW_LOSS_HINGE || loss == TW_LOSS_LOGISTIC, "unknown loss %d", loss);
@@ -1099,35 +979,6 @@ extern "C" int tw_pair_grad_rng_swr(const double* d_X, const double* d_Z, int64_
   return launch_hinge(d_X, d_Z, d, nullptr, kx, nullptr, kz, nullptr, nullptr, n_shards, B, d_w,
                       margin, seed, d_step, (uint32_t)shard_base, d_out, (hipStream_t)stream,
                       loss, nullptr, SwrMap{(uint64_t)swr_mod, swr_base, n_X, n_Z});
-}
-
-// One learning step for wide rows in ONE launch: the previous step's update (k_sgd_update's
-// arithmetic; d_grads_in null: none pending) in the prologue of this step's device-RNG gradient
-// (tw_pair_grad_rng_swr: rows of the step's last reshuffle drawn in the kernel); see PreUpd.
-// Step k of a run uses counter *d_step + step_off; end the run with tw_sgd_update_to.
-// d_ctl: 2 uint64 words, zero before the first launch (ctl[0] only grows; ctl[1] != 0: a grid
-// barrier gave up and the state is invalid).  The residency half of
-// tw_pair_grad_rng_swr_step_ok is the caller's, made once before any stream capture.
-extern "C" int tw_pair_grad_rng_swr_step(
-    const double* d_X, const double* d_Z, int64_t d, int64_t n_X, int64_t n_Z, int64_t kx,
-    int64_t kz, int32_t n_shards, int64_t B, double margin, int32_t loss, uint64_t seed,
-    const uint64_t* d_step, int32_t step_off, int64_t swr_mod, uint64_t swr_base,
-    const double* d_w_in, const double* d_dw_in, const double* d_grads_in, double reg,
-    double lr, double momentum, double* d_w_out, double* d_dw_out, double* d_grads_out,
-    uint64_t* d_ctl, void* stream) {
-  TW_ARG_CHECK(pre_shape_ok(d, n_shards),
-               "tw_pair_grad_rng_swr_step: d=%lld, n_shards=%d outside the fused kernel",
-               (long long)d, n_shards);
-  TW_ARG_CHECK(B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1 && n_X >= 1 && n_Z >= 1 &&
-                   swr_mod >= 1 && step_off >= 0 && d_step && d_w_in && d_dw_in && d_w_out &&
-                   d_dw_out && d_grads_out && d_ctl,
-               "tw_pair_grad_rng_swr_step: bad sizes or null pointers");
-  if (int rc = check_loss(loss)) return rc;
-  return launch_hinge(d_X, d_Z, d, nullptr, kx, nullptr, kz, nullptr, nullptr, n_shards, B,
-                      nullptr, margin, seed, d_step, 0, d_grads_out, (hipStream_t)stream, loss,
-                      nullptr, SwrMap{(uint64_t)swr_mod, swr_base, n_X, n_Z},
-                      PreUpd{d_w_in, d_dw_in, d_grads_in, d_w_out, d_dw_out, d_ctl, reg, lr,
-                             momentum, (uint32_t)step_off});
 }
 
 extern "C" int tw_hinge_grad_rng(const double* d_X, const double* d_Z, int64_t d,

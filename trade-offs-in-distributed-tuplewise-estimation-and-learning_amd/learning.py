@@ -61,10 +61,6 @@ EVAL_FUSED = True
 # pipelined replay loop: the draws made ahead by a native thread (csrc/drawpipe.hip) rather
 # than a Python worker thread
 NATIVE_DRAWS = True
-# wide rows (C5), device RNG, one process: each step's update in the prologue of the next
-# step's gradient launch (tw_pair_grad_rng_swr_step), beside its pairs' row loads, instead of a
-# k_sgd_update launch per step
-WIDE_FUSED_STEPS = True
 # replay segments run through reshuffles (one process, replicated X, narrow segments): the
 # reshuffles' SWR tables ride in the segment's upload, the kernel switches tables by step
 REPLAY_THROUGH = True
@@ -198,15 +194,10 @@ class SGDEngine:
                self.momentum, L.ptr(self._ctl), L.stream_handle())
 
     def check(self):
-        """Raise if a persistent segment launch, or a wide step's update prologue, gave up
-        waiting at a grid barrier (its bounded spin expired: the blocks were not co-resident);
-        the state is then invalid."""
+        """Raise if a persistent segment launch gave up waiting at a grid barrier (its bounded
+        spin expired: the blocks were not co-resident); the state is then invalid."""
         if self._ctl is not None and int(self._ctl[1].item()) != 0:
             raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
-                               "co-resident); the SGD state is invalid")
-        wc = getattr(self, "_wide_ctl", None)
-        if wc is not None and int(wc[1].item()) != 0:
-            raise RuntimeError("tw_pair_grad_rng_swr_step: a grid barrier timed out (blocks not "
                                "co-resident); the SGD state is invalid")
 
     def table_stacks(self, ntab: int):
@@ -651,42 +642,6 @@ class SGDEngine:
                L.ptr(self.grads_loc), L.stream_handle())
         self._update()
 
-    def _wide_step_ok(self) -> bool:
-        """Wide rows, device RNG, one process: each step's update rides in the prologue of the
-        next step's gradient launch (tw_pair_grad_rng_swr_step; WIDE_FUSED_STEPS)."""
-        ok = getattr(self, "_wide_flag", None)
-        if ok is None:
-            ok = self._wide_flag = bool(
-                WIDE_FUSED_STEPS and self.G == 1 and self.vgroup is None and not self.complete
-                and not self.fused and not self.segment and self.N_loc == self.N
-                and L.lib().tw_pair_grad_rng_swr_step_ok(self.d, self.N_loc))
-        return ok
-
-    def _wide_fused_steps(self, nsteps: int, swr_mod: int):
-        """nsteps device-RNG steps of wide rows as nsteps launches (the update of step k-1 in
-        the prologue of step k's gradient launch, ping-pong slots as _fused_steps) + one
-        tw_sgd_update_to; same bits as gradient + update launches per step."""
-        t = self.t
-        if self._slot1 is None:
-            self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw), t.empty_like(self.grads))
-        if getattr(self, "_wide_ctl", None) is None:
-            self._wide_ctl = t.zeros((2,), dtype=t.int64, device=self.w.device)
-        W, DW, Gs = zip((self.w, self.dw, self.grads), self._slot1)
-        s = L.stream_handle()
-        for k in range(nsteps):
-            a, b = (k - 1) & 1, k & 1
-            pend = k > 0
-            L.call("tw_pair_grad_rng_swr_step", L.ptr(self.X), L.ptr(self.Z), self.d, self.n_X,
-                   self.n_Z, self.kx, self.kz, self.N_loc, self.B, self.margin, self.loss,
-                   self.seed, L.ptr(self.step_ctr), k, int(swr_mod), 0,
-                   L.ptr(W[a] if pend else W[0]), L.ptr(DW[a] if pend else DW[0]),
-                   L.ptr(Gs[a] if pend else None), self.reg, self.lr, self.momentum,
-                   L.ptr(W[b]), L.ptr(DW[b]), L.ptr(Gs[b]), L.ptr(self._wide_ctl), s)
-        last = (nsteps - 1) & 1
-        L.call("tw_sgd_update_to", L.ptr(W[last]), L.ptr(DW[last]), L.ptr(W[0]), L.ptr(DW[0]),
-               L.ptr(Gs[last]), self.N, self.d, self.reg, self.lr, self.momentum,
-               L.ptr(self.step_ctr), nsteps, s)
-
     def run_segment(self, nsteps: int, reshuffle_first: bool, graphs: bool = True,
                     swr_mod: int = 0):
         """nsteps device-RNG steps (reshuffling first if asked), replayed from a captured
@@ -706,17 +661,9 @@ class SGDEngine:
         if reshuffle_first and self.layout == "partitioned":
             self.reshuffle_device()  # the exchange sizes its buffers on the host: not captured
             reshuffle_first = False
-        if swr_mod and self._wide_step_ok():  # its residency query and buffers: not captured
-            if self._slot1 is None:
-                self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw),
-                               t.empty_like(self.grads))
-            if getattr(self, "_wide_ctl", None) is None:
-                self._wide_ctl = t.zeros((2,), dtype=t.int64, device=self.w.device)
 
         def steps(n):
-            if swr_mod and self._wide_step_ok():
-                self._wide_fused_steps(n, swr_mod)
-            elif swr_mod:
+            if swr_mod:
                 for _ in range(n):
                     self.step_device(swr_mod=swr_mod)
             elif self.segment:
