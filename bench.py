@@ -1247,6 +1247,10 @@ def main():
         "config": {"workload": "UnN sharded complete AUC U-statistic (estimation-experiment/"
                                "main.py:72-74) + device repartition per step, K steps as "
                                "est.UnNT's loop (BASELINE configs[2])",
+                   "repartition": ("device keyed Feistel permutation per step (a device-RNG "
+                                   "stand-in for np.random.shuffle, pinned against the oracle's "
+                                   "restatement and validated statistically, DESIGN.md §4.5); "
+                                   "the NumPy-order drop-in path is the drop_in_C3 line"),
                    "n_per_class_total": n * world if args.scaling == "weak" else args.n,
                    "shards_total": shards * world,
                    "n_per_class_per_gpu": n, "shards_per_gpu": shards,
