@@ -361,14 +361,18 @@ def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict"):
 def test_chain_steps_are_G_invariant(G, tie_mode):
     """UnN_many's step chains over G ranks (csrc/chain.hip, restated): every rank images its
     own elements against the all-gathered Z, walks their chains into per-(rank, step) buckets,
-    one all-to-all per chunk, counts its bags; one all-reduce of the counts per call.  The
+    one async all-to-all per sub-chunk, counts its bags; one all-reduce of the counts per call.
+    The
     estimates equal the one-process score path's (est.UnNT's loop, key by key) and the ranks'
     final arrays, concatenated, equal the global permutation chain."""
     import tuplewise  # noqa: F401
     from tuplewise import device as D
     assert D.CHAIN_STEPS
     from tuplewise.device import ShardedSample
-    n_loc, m_loc, N, keys = 600, 450, 3, [5, 6, 9]
+    # 12 steps: sub-chunks of D.CHAIN_SUB = 5 steps (5, 5, 2), each its own async
+    # all-to-all, unpacked and counted in order
+    n_loc, m_loc, N = 600, 450, 3
+    keys = [5, 6, 9, 11, 2, 7, 8, 13, 21, 3, 4, 17] if G != 8 else [5, 6, 9, 11, 2, 7, 8]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -34,6 +34,9 @@ RANK_IMAGES = True
 # and permutes the records for the next step (csrc/rankimage.hip), the A/B baseline.
 CHAIN_STEPS = True
 CHAIN_MAX = 32
+# several ranks: the steps of a chunk exchanged in sub-chunks of this many steps, each its own
+# (async) all-to-all, so the exchange of one sub-chunk overlaps the counts of the previous
+CHAIN_SUB = 5
 # one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
 # images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
 ONESHOT_RANK = True
@@ -760,11 +763,18 @@ class ShardedSample:
         zpos = t.empty((m,), dtype=t.int32, device=dev)
         counts = t.empty((T, N), dtype=t.int64, device=dev)
         if G > 1:
+            # a chunk's steps in sub-chunks of <= CHAIN_SUB steps, each with its own send /
+            # receive buffers and its own all-to-all (async): every sub-chunk's emission is
+            # enqueued first, then each sub-chunk waits for its records, unpacks and counts —
+            # the exchange of sub-chunk j+1 runs under the counts of sub-chunk j
             tot = n + m
             cap = max(1, tot // G + tot // (8 * G) + 1024)
             W = 2 if half else 1
-            send = t.empty((G * C * (cap + 1) * W,), dtype=t.int64, device=dev)
-            recv = t.empty_like(send)
+            Sub = max(1, min(C, CHAIN_SUB))
+            nsub = -(-C // Sub)
+            sends = [t.empty((G * Sub * (cap + 1) * W,), dtype=t.int64, device=dev)
+                     for _ in range(nsub)]
+            recvs = [t.empty_like(b) for b in sends]
             if getattr(self, "_chain_flag", None) is None:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
         else:
@@ -772,16 +782,27 @@ class ShardedSample:
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             if G > 1:
-                ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, r, G, kxs[i0:i0 + c],
-                               kzs[i0:i0 + c], kx, kz, N, send=send, cap=cap,
-                               flag=self._chain_flag)
-                sz = G * c * (cap + 1) * W
-                self._all_to_all(recv[:sz], send[:sz])
-                ops.chain_unpack(recv, G, c, cap, half, n, m, x_bag, z_bag, self._chain_flag)
-            else:
-                ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
-                               kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
-                               cursors=cursors)
+                works = []
+                for j, a in enumerate(range(0, c, Sub)):
+                    cs = min(Sub, c - a)
+                    ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0 and a == 0, r, G,
+                                   kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz, N,
+                                   send=sends[j], cap=cap, flag=self._chain_flag)
+                    sz = G * cs * (cap + 1) * W
+                    works.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
+                                                             async_op=True)))
+                for a, cs, j, work in works:
+                    if work is not None:
+                        work.wait()
+                    ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
+                                     z_bag[a:a + cs], self._chain_flag)
+                    ops.count_chain(x_bag[a:a + cs], self.x_off_dev, z_bag[a:a + cs],
+                                    self.z_off_dev, N, cs, n, m, self.max_nx, self.max_nz,
+                                    half, counts[i0 + a:i0 + a + cs])
+                continue
+            ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
+                           kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
+                           cursors=cursors)
             ops.count_chain(x_bag, self.x_off_dev, z_bag, self.z_off_dev, N, c, n, m,
                             self.max_nx, self.max_nz, half, counts[i0:i0 + c])
         if G > 1:
@@ -794,9 +815,10 @@ class ShardedSample:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
         return [np.mean(v) for v in self.values(counts)]
 
-    def _all_to_all(self, out, inp):
-        """Equal-split all-to-all of one flat tensor (RCCL all_to_all_single; gloo on CPU)."""
-        self.dist.all_to_all_single(out, inp, group=self.group)
+    def _all_to_all(self, out, inp, async_op=False):
+        """Equal-split all-to-all of one flat tensor (RCCL all_to_all_single; gloo on CPU);
+        async_op: returns the work handle (its wait() orders the caller's stream after it)."""
+        return self.dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
 
     def _all_gather(self, A):
         """The G ranks' local arrays concatenated in rank order (one collective)."""
