@@ -1,4 +1,4 @@
-"""UnN_many calls of K = 20 steps at the bench shape (1e6/class, 64 shards), for a rocprofv3
+"""UnN_many calls of K = 20 steps (or argv[1]) at the bench shape (1e6/class, 64 shards), for a rocprofv3
 --kernel-trace run; with a CSV argument instead, prints the last call's kernel timeline (start
 offsets, durations, idle gaps) to see the per-call overhead beside the K count launches.
     rocprofv3 --kernel-trace --output-format csv -d DIR -- python3 tools/trace_unn_call.py
@@ -8,7 +8,7 @@ import pathlib
 import sys
 import time
 
-if len(sys.argv) > 1:
+if len(sys.argv) > 1 and sys.argv[1].endswith(".csv"):
     rows = list(csv.DictReader(open(sys.argv[1])))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:70])
                 for r in rows)
@@ -35,10 +35,11 @@ g = torch.Generator(device="cuda").manual_seed(1)
 X = torch.randn(1_000_000, dtype=torch.float64, device="cuda", generator=g) + 0.5
 Z = torch.randn(1_000_000, dtype=torch.float64, device="cuda", generator=g)
 S = ShardedSample(X, Z, 64, algo="pairs")
+K = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 20
 for c in range(6):
     torch.cuda.synchronize()
     time.sleep(0.01)  # a gap the summary cuts on
     t0 = time.perf_counter()
-    S.UnN_many(range(100 * c, 100 * c + 20))
+    S.UnN_many(range(100 * c, 100 * c + K))
     torch.cuda.synchronize()
     print(f"call {c}: {(time.perf_counter() - t0) * 1e3:.3f} ms", flush=True)
