@@ -84,8 +84,9 @@ def test_rank_images_bucket_paths(gpu):
 def test_rank_images_sorted_and_periodic_z(gpu, m):
     """Z in sorted order and with index-periodic structure (the layouts an
     index-strided splitter sample handled worst) — the hashed sample keeps the interval buckets
-    balanced: images equal the oracle's and one ranking stays within a few times its Gaussian
-    cost (sub-bucket scans bounded), small-Z plan (m = 1e5) and large (1e6)."""
+    balanced — and Z with heavy ties: images equal the oracle's and one ranking stays within a
+    few times its Gaussian cost (sub-bucket scans bounded, long sub-buckets sorted by waves),
+    small-Z plan (m = 1e5) and large (1e6)."""
     import time
     import torch
     from tuplewise import _lib as L
@@ -95,7 +96,11 @@ def test_rank_images_sorted_and_periodic_z(gpu, m):
     X = rng.normal(size=m // 2)
     cases = {"gauss": rng.normal(size=m), "sorted": np.sort(rng.normal(size=m)),
              "periodic": np.tile(np.sort(rng.normal(size=1000)), m // 1000),
-             "sawtooth": (np.arange(m) % 4096) * 1e-3}
+             "sawtooth": (np.arange(m) % 4096) * 1e-3,
+             # heavy ties: ~m / 5000 and ~m / 1000 copies of each value (long sub-buckets,
+             # sorted by one wave each; before, ~20 sequential block sorts per bucket: 1.9 ms)
+             "ties5000": rng.randint(0, 5000, size=m).astype(np.float64),
+             "ties1000": rng.randint(0, 1000, size=m).astype(np.float64)}
     times = {}
     for name, Z in cases.items():
         Xd, Zd = torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda()

@@ -75,6 +75,7 @@ constexpr int kRkSub = 2048;                       // sub-buckets per interval b
 // was otherwise unbounded (1000 copies of each of 1000 values took 3.6 ms)
 constexpr uint32_t kRkSortedMin = 32;
 constexpr uint32_t kRkSortedMax = 4096;
+constexpr uint32_t kRkWaveSortMax = 1024;  // sorted by one wave (16 keys per lane)
 
 // position of sample i in [0, m): a hashed, not an index-strided, sample (Z with periodic
 // structure would give an evenly spaced sample of repeated values)
@@ -537,10 +538,41 @@ __global__ __launch_bounds__(kSubThreads) void k_rank_subsort(
   __syncthreads();
   const int nl = nlong;
   if (nl == 0) return;
+  // up to kRkWaveSortMax keys: one wave per sub-bucket, the block's waves on different ones at
+  // once (ties: ~200 copies of each value made every interval bucket ~20 sequential 4096-key
+  // block sorts, 1.9 ms for 1e6 + 1e6 keys of 5000 values; profiles/r04s12_rank_plan_ties.log)
+  {
+    const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    auto wave_sort = [&](auto e_const, uint64_t* q, uint32_t L) {
+      constexpr int E = decltype(e_const)::value;
+      uint64_t v[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const uint32_t t = (uint32_t)(lane * E + e);
+        v[e] = t < L ? q[t] : ~0ull;
+      }
+      wave_sort_keys<E>(v, lane);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const uint32_t t = (uint32_t)(lane * E + e);
+        if (t < L) q[t] = v[e];
+      }
+    };
+    for (int li = wid; li < nl; li += kSubThreads / kWave) {
+      const int i = __builtin_amdgcn_readfirstlane(longs[li]);
+      const uint32_t a = i ? h[i - 1] : 0u, L = h[i] - a;
+      uint64_t* q = skeys + s0 + a;
+      if (L <= 4 * kWave)
+        wave_sort(std::integral_constant<int, 4>(), q, L);
+      else if (L <= kRkWaveSortMax)
+        wave_sort(std::integral_constant<int, kRkWaveSortMax / kWave>(), q, L);
+    }
+  }
   __shared__ uint64_t sbuf[kRkSortedMax];
   for (int li = 0; li < nl; ++li) {
     const int i = longs[li];
     const uint32_t a = i ? h[i - 1] : 0u, L = h[i] - a;
+    if (L <= kRkWaveSortMax) continue;  // sorted by a wave above
     for (uint32_t t = threadIdx.x; t < kRkSortedMax; t += kSubThreads)
       sbuf[t] = t < L ? skeys[s0 + a + t] : ~0ull;
     __syncthreads();

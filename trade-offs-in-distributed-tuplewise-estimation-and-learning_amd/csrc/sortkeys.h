@@ -113,6 +113,29 @@ __device__ __forceinline__ void sort_keys_block(uint64_t* keys, int C, uint64_t*
   for (int i = tid; i < n; i += nthr) dst[i] = keys[i];
 }
 
+// The same network on kE * 64 keys held by ONE wave (lane l owning [kE l, kE l + kE)): the
+// register levels and the in-wave shuffles only, no barrier, so the waves of a block sort
+// different key runs at once (the ranking's long sub-buckets).
+template <int kE>
+__device__ __forceinline__ void wave_sort_keys(uint64_t (&v)[kE], int lane) {
+  constexpr int C = kE * kWave;
+  const int base = lane * kE;
+  for (int k = 2; k <= kE; k <<= 1) reg_levels<kE>(v, base, k, k >> 1);
+  for (int k = 2 * kE; k <= C; k <<= 1) {
+    const bool up = ((base & k) == 0);
+    for (int j = k >> 1; j >= kE; j >>= 1) {
+      const int m = j / kE;
+      const bool keep_min = (((lane & m) == 0) == up);
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const uint64_t o = __shfl_xor(v[e], m, kWave);
+        v[e] = keep_min ? (o < v[e] ? o : v[e]) : (o > v[e] ? o : v[e]);
+      }
+    }
+    reg_levels<kE>(v, base, k, kE >> 1);
+  }
+}
+
 template <typename T, int kE>
 __global__ __launch_bounds__(kSortThreads) void k_sort_chunks(const T* __restrict__ z,
                                                               const int64_t* __restrict__ z_off,
