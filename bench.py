@@ -1032,6 +1032,8 @@ def main():
     rank_path = S._rank_path_ok()
     ops.count_sorted_step = kernel_ms.wrap(ops.count_sorted_step)  # sorted count + next
     ops.count_sorted_steps = kernel_ms.wrap(ops.count_sorted_steps)  # all K sorted steps
+    # algo="sorted" on the step chains: the exact bucket count of a chunk's bags (weight: steps)
+    ops.count_chain_bucket = kernel_ms.wrap(ops.count_chain_bucket, weight=lambda *a, **kw: a[5])
 
     def barrier():
         if group is not None:
@@ -1124,10 +1126,15 @@ def main():
     same_counts = bool(torch.equal(S.local_counts(), (setattr(S, "algo", "sorted"),
                                                       S.local_counts())[1]))
     S.algo = "sorted"
+    from tuplewise import device as _D
+    sorted_chain = (S._chain_ok() and S.max_nz <= _D.CHAIN_BUCKET_MAX
+                    and hasattr(S.ops, "count_chain_bucket"))
     S.UnN_many(range(10_000, 10_000 + args.warmup))
     torch.cuda.synchronize()
     barrier()
-    kernel_ms.clear(sample)
+    kernel_ms.clear(sample if not sorted_chain else 1)
+    emit_ms.clear()
+    rank_ms.clear()
     t1 = time.perf_counter()
     # same keys as the timed all-pairs steps
     est_sorted = S.UnN_many(range(args.warmup, args.warmup + args.steps))[-1]
@@ -1138,8 +1145,16 @@ def main():
         tt = torch.tensor([dt_sorted], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt_sorted = float(tt.item())
-    # one tw_count_pairs_sorted_steps call carries all K steps: per-step device time
-    kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()])) / args.steps
+    if sorted_chain:  # per step: the bags' bucket count + the emission (+ the call's ranking)
+        sorted_parts = {"bucket_count_ms_per_step": kernel_ms.ms_per_unit(),
+                        "emission_ms_per_step": emit_ms.ms_per_unit(),
+                        "ranking_ms_per_call": float(np.mean([a.elapsed_time(b)
+                                                              for a, b in rank_ms.used()]))}
+        kms_sorted = (sorted_parts["bucket_count_ms_per_step"]
+                      + sorted_parts["emission_ms_per_step"])
+    else:  # one tw_count_pairs_sorted_steps call carries all K steps: per-step device time
+        sorted_parts = None
+        kms_sorted = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()])) / args.steps
     S.algo = "pairs"
 
     # incomplete U-statistic (BASELINE config C3: B pairs per shard + a repartition per step;
@@ -1310,7 +1325,29 @@ def main():
         "estimate_last_step": float(est),
         "plumbing_C1": c1,
         "single_shard_C2": single,
-        "sorted_count": {
+        "sorted_count": ({
+            "note": "same UnN steps with the exact O(n+m) count (algo='sorted' on the step "
+                    "chains: the call's ranking, the chains' (step, shard) image bags, each bag "
+                    "counted by a counting sort of its integer z images in LDS, "
+                    "tw_count_pairs_chain_bucket; bit-identical estimates and arrays); "
+                    "count_kernels_ms = bucket count + emission per step (the ranking once per "
+                    "call beside it); pairs are logical, not compared one by one",
+            "value": total_pairs / dt_sorted, "unit": "logical pairs/s",
+            "ms_per_step": dt_sorted / args.steps * 1e3, "count_kernels_ms": kms_sorted,
+            "parts": sorted_parts,
+            "estimate_last_step": float(est_sorted),
+            "counts_identical_to_all_pairs": same_counts,
+            # algorithmic bytes per element and step: its 4-B image appended to a bag and read
+            # back by the count (positions and records stay in registers across a chunk)
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "bytes_per_element": 8,
+                         "achieved": 8 * 2 * n / (kms_sorted * 1e-3) / 1e9,
+                         "frac": 8 * 2 * n / (kms_sorted * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "count_kernels_ms per step against 8 B per element; both "
+                                 "kernels are issue-bound (the emission's Feistel walk and LDS "
+                                 "histogram, the bucket count's LDS counting sort), not "
+                                 "bandwidth-bound"}}
+            if sorted_chain else {
             "note": "same UnN steps with the exact O((n+m) log m)-class count (algo='sorted':"
                     " value buckets of z in LDS for shards of <= 16384, else sort + binary "
                     "search; bit-identical estimates; the K steps in one call with the "
@@ -1331,7 +1368,7 @@ def main():
                          "frac": 24 * 2 * n / (kms_sorted * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "note": "count_kernels_ms per step against 24 B per element; the step "
                                  "is latency-bound (Feistel + load/atomic/store chain, DESIGN "
-                                 "4.6), not bandwidth-bound"}},
+                                 "4.6), not bandwidth-bound"}}),
         "incomplete": {
             "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
                     "drawn pairs per shard (Philox4x32-10, two pairs per block, Lemire maps) "

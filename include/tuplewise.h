@@ -193,6 +193,16 @@ int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off, int64_t x_
                          const void* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
                          int32_t n_shards, int32_t steps, int64_t max_nx, int64_t max_nz,
                          int32_t half, uint64_t* d_out, void* stream);
+/* The same counts as tw_count_pairs_chain in O(n + m) per bag (algo="sorted", SURVEY row f4;
+ * estimation-experiment/main.py:29-31's integer): each bag's z images (integers in
+ * [0, z_total], z_total = the Z count the images were ranked against) counting-sorted into
+ * <= 16384 LDS buckets, every x's g(x) (and h(x) with half) answered by the bucket prefix and a
+ * scan of its own bucket.  Bags of <= 16384 z (max_nz); d_out[c * n_shards + s] written, not
+ * accumulated. */
+int tw_count_pairs_chain_bucket(const void* d_x_bag, const int64_t* d_x_off, int64_t x_stride,
+                                const void* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
+                                int32_t n_shards, int32_t steps, int64_t max_nz,
+                                int64_t z_total, int32_t half, uint64_t* d_out, void* stream);
 /* Tuning hook for tw_chain_emit: elements per thread (2, 4 or 8) and steps per reservation
  * round (1 or 16 / elements per thread); 0 = automatic.  Process-global; results do not depend
  * on it (the order inside a bag does). */

@@ -51,7 +51,8 @@ def test_chain_bags_and_counts_equal_oracle(gpu, kind, half, n, m, N):
     """tw_chain_emit (one process) + tw_count_pairs_chain: each (step, shard) bag is the
     multiset of the oracle's images at that shard's positions after the step's repartition; the
     counts equal the reference predicate (strict: #{x > z}; half: 2 #{x > z} + #{x == z}) on the
-    oracle's permuted scores; the chain state after the last step gives the final arrays."""
+    oracle's permuted scores, and tw_count_pairs_chain_bucket's exact counts equal them; the
+    chain state after the last step gives the final arrays."""
     import torch
     from tuplewise import _lib as L
     from tuplewise.device import HipOps
@@ -83,6 +84,11 @@ def test_chain_bags_and_counts_equal_oracle(gpu, kind, half, n, m, N):
     out = torch.full((T, N), 7, dtype=torch.int64, device="cuda")
     ops.count_chain(x_bag, xo, z_bag, zo, N, 3, n, m, kx, kz, half, out[:3])
     ops.count_chain(x_bag[3:], xo, z_bag[3:], zo, N, 2, n, m, kx, kz, half, out[3:])
+    # the exact bucket count (algo="sorted") of the same bags: bags of <= 16384 z
+    outb = torch.full((T, N), 7, dtype=torch.int64, device="cuda")
+    if kz <= 16384:
+        ops.count_chain_bucket(x_bag, xo, z_bag, zo, N, T, n, m, kz, m, half, outb)
+        assert torch.equal(outb, out)
     xb = x_bag.cpu().numpy()
     zb = z_bag.cpu().numpy()
     got = out.cpu().numpy().view(np.uint64)
@@ -252,6 +258,51 @@ def test_unn_many_chain_equals_step_paths(gpu, case, tie_mode):
     xa, za = _chain(X, keys, 0)[-1], _chain(Z, keys, 1)[-1]
     assert np.array_equal(got[True][1], xa, equal_nan=eqn)
     assert np.array_equal(got[True][2], za, equal_nan=eqn)
+
+
+@pytest.mark.parametrize("case", ["gauss", "ties_i64", "edge_ragged", "one_shard", "long",
+                                  "wide"])
+@pytest.mark.parametrize("tie_mode", ["strict", "half"])
+def test_unn_many_sorted_on_chains_equals_pairs(gpu, case, tie_mode):
+    """algo="sorted" through the step chains with the exact bucket count of every bag
+    (tw_count_pairs_chain_bucket; shards of <= 16384 z) == the all-pairs chain path: estimates
+    and final arrays bit for bit, final arrays == the oracle's permutation chain; "wide" has
+    shards past 16384 z and keeps the records path (same values again)."""
+    import torch
+    from tuplewise import device as D
+    from tuplewise.device import ShardedSample
+    rng = np.random.RandomState(8)
+    keys = [3, 4, 5, 6]
+    if case == "gauss":
+        X, Z, N = rng.normal(0.3, 1, 300_000), rng.normal(0, 1, 250_000), 16
+    elif case == "ties_i64":
+        X, Z, N = rng.randint(0, 50, 160_003), rng.randint(0, 50, 120_000), 12
+    elif case == "edge_ragged":
+        X, Z, N = _sample(rng, 100_001, "edge"), _sample(rng, 77_777, "edge"), 7
+    elif case == "one_shard":
+        X, Z, N = rng.normal(0.5, 1, 20_000), rng.normal(0, 1, 16_000), 1
+    elif case == "long":
+        X, Z, N = rng.normal(0.5, 1, 40_000).round(2), rng.normal(0, 1, 30_000).round(2), 5
+        keys = list(range(40, 110))
+    else:
+        X, Z, N = rng.normal(0.5, 1, 60_000), rng.normal(0, 1, 50_000), 2
+    if tie_mode == "half" and case == "wide":
+        pytest.skip("the records path takes the strict predicate only")
+    got = {}
+    for algo in ("sorted", "pairs"):
+        S = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N, algo=algo,
+                          tie_mode=tie_mode)
+        assert S._chain_ok()
+        if algo == "sorted":
+            assert (S.max_nz <= D.CHAIN_BUCKET_MAX) == (case != "wide")
+        got[algo] = (S.UnN_many(keys), S.X.cpu().numpy(), S.Z.cpu().numpy())
+    assert got["sorted"][0] == got["pairs"][0]
+    eqn = X.dtype.kind == "f"
+    assert np.array_equal(got["sorted"][1], got["pairs"][1], equal_nan=eqn)
+    assert np.array_equal(got["sorted"][2], got["pairs"][2], equal_nan=eqn)
+    xa, za = _chain(X, keys, 0)[-1], _chain(Z, keys, 1)[-1]
+    assert np.array_equal(got["sorted"][1], xa, equal_nan=eqn)
+    assert np.array_equal(got["sorted"][2], za, equal_nan=eqn)
 
 
 def test_chain_overflow_flag(gpu):

@@ -53,6 +53,8 @@ _SIGNATURES = {
     "tw_chain_unpack": [_vp, _i32, _i32, _i64, _i32, _i64, _i64, _vp, _vp, _vp, _vp],
     "tw_count_pairs_chain": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i32, _vp,
                              _vp],
+    "tw_count_pairs_chain_bucket": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64,
+                                    _i32, _vp, _vp],
     "tw_count_chain_set_plan": [_i32, _i64],
     "tw_chain_set_emit": [_i32, _i32],
     "tw_chain_scatter": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp],

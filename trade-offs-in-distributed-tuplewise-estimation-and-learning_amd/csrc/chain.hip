@@ -723,6 +723,141 @@ extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
   return TW_OK;
 }
 
+// ----------------------------------------------------------------------------- exact count
+// The exact O(n + m) count of the bags (algo="sorted", row f4) on the rank images themselves:
+// z images are integers g in [0, z_total], so a bag's z, bucketed by g >> shift into <= 16384
+// LDS buckets (a counting sort in LDS), answer #{z : g(z) < t} as the z count of the lower
+// buckets + a scan of t's own bucket (~1 z).  Per x: t = g(x) ([x > z] <=> g(z) < g(x)); half
+// ties add t = h(x) ([x >= z] <=> g(z) < h(x)).  NaN x (image -2^25) count nothing; NaN z
+// (g = #non-NaN z) are below no t.  One block per (step, shard) bag, bags of <= 16384 z.
+constexpr int kCbMaxZ = 16384;
+constexpr int kCbBuckets = 16384;
+constexpr int kCbThreads = 1024;
+constexpr int kCbPer = kCbMaxZ / kCbThreads;  // z per thread
+
+template <bool HALF>
+__global__ __launch_bounds__(kCbThreads) void k_count_chain_bucket(
+    const void* __restrict__ xbag, const int64_t* __restrict__ x_off, int64_t x_stride,
+    const float* __restrict__ zbag, const int64_t* __restrict__ z_off, int64_t z_stride,
+    int n_shards, int shift, int nbk, unsigned long long* __restrict__ out) {
+  __shared__ uint32_t end[kCbBuckets];  // after the scatter: end of bucket b = start of b + 1
+  __shared__ uint32_t zs[kCbMaxZ];
+  __shared__ uint32_t wtot[kCbThreads / kWave];
+  __shared__ unsigned long long bsum[kCbThreads / kWave];
+  const int bag = xcd_block(blockIdx.x, gridDim.x);  // a step's shards on one XCD
+  const int c = bag / n_shards, s = bag - c * n_shards;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const int64_t z0 = z_off[s], x0 = x_off[s];
+  const int nz = (int)(z_off[s + 1] - z0);
+  const int64_t nx = x_off[s + 1] - x0;
+  const float* zp = zbag + (int64_t)c * z_stride + z0;
+  uint32_t zv[kCbPer];
+#pragma unroll
+  for (int u = 0; u < kCbPer; ++u) {  // all loads in flight before the first LDS atomic
+    const int i = tid + u * kCbThreads;
+    zv[u] = i < nz ? (uint32_t)(-zp[i]) : 0xFFFFFFFFu;  // z bags hold -g(z)
+  }
+  for (int b = tid; b < nbk; b += kCbThreads) end[b] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kCbPer; ++u)
+    if (zv[u] != 0xFFFFFFFFu) atomicAdd(&end[zv[u] >> shift], 1u);
+  __syncthreads();
+  // exclusive prefix of the counts: kCbPer consecutive buckets per thread, wave scans, then
+  // the wave totals
+  {
+    const int b0 = tid * kCbPer;
+    uint32_t loc[kCbPer], sum = 0;
+#pragma unroll
+    for (int u = 0; u < kCbPer; ++u) {
+      loc[u] = b0 + u < nbk ? end[b0 + u] : 0u;
+      sum += loc[u];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += t;
+    }
+    if (lane == kWave - 1) wtot[wid] = inc;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int w = 0; w < wid; ++w) wbase += wtot[w];
+    uint32_t run = wbase + inc - sum;
+#pragma unroll
+    for (int u = 0; u < kCbPer; ++u) {
+      if (b0 + u < nbk) end[b0 + u] = run;  // start of bucket b0 + u
+      run += loc[u];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kCbPer; ++u)  // counting-sort scatter: start -> end of every bucket
+    if (zv[u] != 0xFFFFFFFFu) zs[atomicAdd(&end[zv[u] >> shift], 1u)] = zv[u];
+  __syncthreads();
+  auto below = [&](float tf) -> uint32_t {  // #{z of the bag : g(z) < t}
+    if (!(tf > 0.0f)) return 0u;              // t <= 0 (or the NaN-x sentinel): none below
+    const uint32_t t = (uint32_t)tf;
+    const uint32_t b = t >> shift;            // < nbk: t <= z_total
+    uint32_t lo = b ? end[b - 1] : 0u;
+    const uint32_t hi = end[b];
+    uint32_t cnt = lo;
+    for (; lo < hi; ++lo) cnt += zs[lo] < t ? 1u : 0u;
+    return cnt;
+  };
+  unsigned long long acc = 0;
+  if constexpr (HALF) {
+    const uint64_t* xp = (const uint64_t*)xbag + (int64_t)c * x_stride + x0;
+    for (int64_t i = tid; i < nx; i += kCbThreads) {
+      const uint64_t v = xp[i];
+      acc += below(__uint_as_float((uint32_t)v)) + below(__uint_as_float((uint32_t)(v >> 32)));
+    }
+  } else {
+    const float* xp = (const float*)xbag + (int64_t)c * x_stride + x0;
+    for (int64_t i = tid; i < nx; i += kCbThreads) acc += below(xp[i]);
+  }
+  acc = wave_sum_u64(acc);
+  if (lane == 0) bsum[wid] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kCbThreads / kWave; ++w) t += bsum[w];
+    out[bag] = t;
+  }
+}
+
+extern "C" int tw_count_pairs_chain_bucket(const void* d_x_bag, const int64_t* d_x_off,
+                                           int64_t x_stride, const void* d_z_bag,
+                                           const int64_t* d_z_off, int64_t z_stride,
+                                           int32_t n_shards, int32_t steps, int64_t max_nz,
+                                           int64_t z_total, int32_t half, uint64_t* d_out,
+                                           void* stream) {
+  TW_ARG_CHECK(n_shards >= 0 && steps >= 0 && x_stride >= 0 && z_stride >= 0 &&
+                   (half == 0 || half == 1) && z_total >= 0 && z_total < (1ll << 24),
+               "tw_count_pairs_chain_bucket: bad sizes");
+  TW_ARG_CHECK(max_nz >= 0 && max_nz <= kCbMaxZ,
+               "tw_count_pairs_chain_bucket: bags of <= %d z (use tw_count_pairs_chain)",
+               kCbMaxZ);
+  const int64_t bags = (int64_t)n_shards * steps;
+  TW_ARG_CHECK(bags < (1ll << 31), "tw_count_pairs_chain_bucket: too many bags");
+  if (bags == 0) return TW_OK;
+  int shift = 0;
+  while ((z_total >> shift) >= kCbBuckets) ++shift;
+  const int nbk = (int)(z_total >> shift) + 1;
+  hipStream_t st = (hipStream_t)stream;
+  auto* o = (unsigned long long*)d_out;
+  if (half)
+    hipLaunchKernelGGL((k_count_chain_bucket<true>), dim3((unsigned)bags), dim3(kCbThreads), 0,
+                       st, d_x_bag, d_x_off, x_stride, (const float*)d_z_bag, d_z_off, z_stride,
+                       n_shards, shift, nbk, o);
+  else
+    hipLaunchKernelGGL((k_count_chain_bucket<false>), dim3((unsigned)bags), dim3(kCbThreads), 0,
+                       st, d_x_bag, d_x_off, x_stride, (const float*)d_z_bag, d_z_off, z_stride,
+                       n_shards, shift, nbk, o);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 extern "C" int tw_count_chain_set_plan(int32_t R, int64_t z_chunk) {
   TW_ARG_CHECK(R == 0 || R == 8 || R == 16, "tw_count_chain_set_plan: R in {0, 8, 16}");
   TW_ARG_CHECK(z_chunk >= 0 && z_chunk <= (1ll << 24), "tw_count_chain_set_plan: bad z_chunk");

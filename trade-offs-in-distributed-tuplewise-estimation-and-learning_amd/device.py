@@ -34,6 +34,10 @@ RANK_IMAGES = True
 # and permutes the records for the next step (csrc/rankimage.hip), the A/B baseline.
 CHAIN_STEPS = True
 CHAIN_MAX = 32
+# algo="sorted" on the step chains: bags of at most this many z are counted exactly in
+# O(n + m) on their integer rank images (tw_count_pairs_chain_bucket); larger shards keep the
+# records path (tw_count_pairs_sorted_steps)
+CHAIN_BUCKET_MAX = 16384
 # several ranks: the steps of a chunk exchanged in sub-chunks of this many steps, each its own
 # (async) all-to-all, so the exchange of one sub-chunk overlaps the counts of the previous
 CHAIN_SUB = 5
@@ -226,6 +230,15 @@ class HipOps:
         L.call("tw_count_pairs_chain", L.ptr(x_bag), L.ptr(x_off_dev), int(x_stride),
                L.ptr(z_bag), L.ptr(z_off_dev), int(z_stride), int(n_shards), int(steps),
                int(max_nx), int(max_nz), int(bool(half)), L.ptr(out), L.stream_handle())
+        return out
+
+    def count_chain_bucket(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps,
+                           x_stride, z_stride, max_nz, z_total, half, out):
+        """The exact O(n + m) counts of steps x n_shards bags (tw_count_pairs_chain_bucket,
+        bags of <= CHAIN_BUCKET_MAX z) into out (steps, n_shards)."""
+        L.call("tw_count_pairs_chain_bucket", L.ptr(x_bag), L.ptr(x_off_dev), int(x_stride),
+               L.ptr(z_bag), L.ptr(z_off_dev), int(z_stride), int(n_shards), int(steps),
+               int(max_nz), int(z_total), int(bool(half)), L.ptr(out), L.stream_handle())
         return out
 
     def chain_scatter(self, X, xpos, Z, zpos):
@@ -634,6 +647,10 @@ class ShardedSample:
             return [self.UnN(k) for k in keys]
         if self.algo == "pairs" and self._chain_ok():
             return self._unn_many_chain(keys)
+        if (self.algo == "sorted" and self._chain_ok() and self.max_nz <= CHAIN_BUCKET_MAX
+                and hasattr(self.ops, "count_chain_bucket")):
+            # the step chains with the exact bucket count of each bag (row f4)
+            return self._unn_many_chain(keys, bucket=True)
         if (self.algo == "sorted" and not self._multi() and self.N > 0
                 and hasattr(self.ops, "count_sorted_steps")):
             # the whole sequence in one call: records between steps (csrc/records.h)
@@ -727,7 +744,7 @@ class ShardedSample:
             self.Z = self.ops.gather_records(Z0, zr)
         return [np.mean(v) for v in self.values(counts)]
 
-    def _unn_many_chain(self, keys):
+    def _unn_many_chain(self, keys, bucket=False):
         """UnN_many as step chains (csrc/chain.hip; est.UnNT's loop, estimation-experiment/
         main.py:76-79).  One ranking per call: over ranks the Z structure of the all-gathered Z,
         images written for this rank's own elements only.  Then per chunk of <= CHAIN_MAX steps
@@ -737,7 +754,8 @@ class ShardedSample:
         launch counts all bags of the chunk.  The final arrays: a scatter by the chains' last
         positions (one process) or the inverse chains of the rank's own positions gathered from
         the all-gathered sample.  Same permutation chain, counts and final arrays as the
-        one-launch-per-step paths, at any G."""
+        one-launch-per-step paths, at any G.  bucket: the bags counted exactly in O(n + m) on
+        their integer images (algo="sorted") instead of all pairs — the same integers."""
         t, ops, G, r = self.t, self.ops, self.G, self.rank
         n, m, N = self.n_loc, self.m_loc, self.N
         dev = self.X.device
@@ -757,6 +775,15 @@ class ShardedSample:
         M64 = 2 ** 64 - 1
         kxs = [(2 * k) & M64 for k in keys]
         kzs = [(2 * k + 1) & M64 for k in keys]
+        z_total = int(Z0.numel())  # the Z the images were ranked against: images <= z_total
+
+        def count(xb, zb, steps, out):  # the bags of `steps` steps -> out (steps, N)
+            if bucket:
+                ops.count_chain_bucket(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
+                                       self.max_nz, z_total, half, out)
+            else:
+                ops.count_chain(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
+                                self.max_nx, self.max_nz, half, out)
         x_bag = t.empty((C, n), dtype=t.int64 if half else t.float32, device=dev)
         z_bag = t.empty((C, m), dtype=t.float32, device=dev)
         xpos = t.empty((n,), dtype=t.int32, device=dev)
@@ -796,15 +823,12 @@ class ShardedSample:
                         work.wait()
                     ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
                                      z_bag[a:a + cs], self._chain_flag)
-                    ops.count_chain(x_bag[a:a + cs], self.x_off_dev, z_bag[a:a + cs],
-                                    self.z_off_dev, N, cs, n, m, self.max_nx, self.max_nz,
-                                    half, counts[i0 + a:i0 + a + cs])
+                    count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs])
                 continue
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
-            ops.count_chain(x_bag, self.x_off_dev, z_bag, self.z_off_dev, N, c, n, m,
-                            self.max_nx, self.max_nz, half, counts[i0:i0 + c])
+            count(x_bag, z_bag, c, counts[i0:i0 + c])
         if G > 1:
             self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
             full = t.zeros((T, G * N), dtype=t.int64, device=dev)
