@@ -89,6 +89,8 @@ def _est_worker(rank, port, G, q, exchange="fixed", chain=True):
                       group=dist.group.WORLD, exchange=exchange, algo="pairs")
     vals = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
     vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # rank images: the step chains
+    S.algo = "sorted"  # the chains' exact bucket count of every bag (per-step path unchained)
+    vals += [float(v) for v in S.UnN_many([8, 9])]
     Xg = [torch.empty(S.X.shape, dtype=S.X.dtype) for _ in range(G)]
     Zg = [torch.empty(S.Z.shape, dtype=S.Z.dtype) for _ in range(G)]
     dist.all_gather(Xg, S.X.cpu())
@@ -113,6 +115,8 @@ def test_sharded_sample_two_ranks_equals_one(gpu, exchange, chain):
     want = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
     want += [float(v) for v in S.UnN_many([5, 6, 7])]
     assert S._chain_ok() and S.algo == "pairs"
+    S.algo = "sorted"
+    want += [float(v) for v in S.UnN_many([8, 9])]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
