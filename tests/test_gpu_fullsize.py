@@ -48,10 +48,10 @@ def test_c3_full_size_device_rng(gpu):
 
 def test_c3_full_size_complete_one_launch_steps(gpu):
     """The bench's step at its size: UnN_many over T = 4 keys, n = 1e6 per class, N = 64, by
-    the all-pairs count (tw_count_pairs_step) and by the exact sorted count
-    (tw_count_pairs_sorted_step) — both carry the next repartition in the count launch.  Same
-    estimates; the arrays after the last step equal the oracle's chain of permutations; every
-    shard's count of the last partition equals an exact searchsorted count."""
+    the all-pairs count and by the exact count (algo="sorted": since round 4 the step chains'
+    bags counted by tw_count_pairs_chain_bucket, shards of 15625 z) — same estimates; the
+    arrays after the last step equal the oracle's chain of permutations; every shard's count
+    of the last partition equals an exact searchsorted count."""
     import torch
     from tuplewise.device import ShardedSample
     n, N = 1_000_000, 64

@@ -542,13 +542,23 @@ def test_sorted_steps_records_path(gpu, n, m, N, tie, dt):
     as destination-bucketed records between steps, csrc/records.h): per-step estimates equal
     the step-at-a-time path (tw_permute_pair + the sorted count), and the arrays after the last
     step equal the oracle's chain of permutations — with tails that belong to no shard
-    (n, m not multiples of the shard sizes), ties, int64, T = 1, 2, 5."""
+    (n, m not multiples of the shard sizes), ties, int64, T = 1, 2, 5.  The default route
+    (the step chains' exact bucket count of every bag, round 4) gives the same again."""
     import torch
     from tuplewise.device import HipOps, ShardedSample
 
     class OneStep(HipOps):  # without the records entry: one repartition + count per step
         @property
         def count_sorted_steps(self):
+            raise AttributeError
+
+        @property
+        def count_chain_bucket(self):
+            raise AttributeError
+
+    class Records(HipOps):  # the records path, not the step chains' bucket count
+        @property
+        def count_chain_bucket(self):
             raise AttributeError
 
     rng = np.random.RandomState(n % 97)
@@ -560,15 +570,20 @@ def test_sorted_steps_records_path(gpu, n, m, N, tie, dt):
         S1 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
                            tie_mode=tie, algo="sorted", ops=OneStep())
         S2 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
+                           tie_mode=tie, algo="sorted", ops=Records())
+        # the default: the step chains with the bags' exact bucket count (round 4)
+        S3 = ShardedSample(torch.from_numpy(X).cuda(), torch.from_numpy(Z).cuda(), N,
                            tie_mode=tie, algo="sorted")
         want = S1.UnN_many(keys)
-        got = S2.UnN_many(keys)
-        assert got == want, (keys, got, want)
+        for S in (S2, S3):
+            got = S.UnN_many(keys)
+            assert got == want, (keys, got, want)
         Xp, Zp = X, Z
         for k in keys:
             Xp = O.permute_scatter(Xp, (2 * k) % 2 ** 64)
             Zp = O.permute_scatter(Zp, (2 * k + 1) % 2 ** 64)
-        assert np.array_equal(S2.X.cpu().numpy(), Xp) and np.array_equal(S2.Z.cpu().numpy(), Zp)
+        for S in (S2, S3):
+            assert np.array_equal(S.X.cpu().numpy(), Xp) and np.array_equal(S.Z.cpu().numpy(), Zp)
 
 
 def test_device_sigmoid_accuracy(gpu):
