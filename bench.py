@@ -1148,8 +1148,9 @@ def main():
     if sorted_chain:  # per step: the bags' bucket count + the emission (+ the call's ranking)
         sorted_parts = {"bucket_count_ms_per_step": kernel_ms.ms_per_unit(),
                         "emission_ms_per_step": emit_ms.ms_per_unit(),
-                        "ranking_ms_per_call": float(np.mean([a.elapsed_time(b)
-                                                              for a, b in rank_ms.used()]))}
+                        "ranking_ms_per_call": (float(np.mean([a.elapsed_time(b)
+                                                               for a, b in rank_ms.used()]))
+                                                if rank_ms.used() else None)}
         kms_sorted = (sorted_parts["bucket_count_ms_per_step"]
                       + sorted_parts["emission_ms_per_step"])
     else:  # one tw_count_pairs_sorted_steps call carries all K steps: per-step device time
