@@ -730,6 +730,8 @@ extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
 // buckets + a scan of t's own bucket (~1 z).  Per x: t = g(x) ([x > z] <=> g(z) < g(x)); half
 // ties add t = h(x) ([x >= z] <=> g(z) < h(x)).  NaN x (image -2^25) count nothing; NaN z
 // (g = #non-NaN z) are below no t.  One block per (step, shard) bag, bags of <= 16384 z.
+namespace tw {
+
 constexpr int kCbMaxZ = 16384;
 constexpr int kCbBuckets = 16384;
 constexpr int kCbThreads = 1024;
@@ -825,6 +827,8 @@ __global__ __launch_bounds__(kCbThreads) void k_count_chain_bucket(
     out[bag] = t;
   }
 }
+
+}  // namespace tw
 
 extern "C" int tw_count_pairs_chain_bucket(const void* d_x_bag, const int64_t* d_x_off,
                                            int64_t x_stride, const void* d_z_bag,
