@@ -981,7 +981,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     group = None
-    if world > 1:
+    # TW_BENCH_RCCL_WORLD1=1: a world-size-1 RCCL group with every multi-rank branch forced
+    # (TW_FORCE_COLLECTIVES), so each collective of the G > 1 path runs on the one GPU
+    rccl1 = world == 1 and os.environ.get("TW_BENCH_RCCL_WORLD1", "") == "1"
+    if rccl1:
+        os.environ["TW_FORCE_COLLECTIVES"] = "1"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or rccl1:
         # RCCL over xGMI; TW_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
         backend = os.environ.get("TW_BENCH_BACKEND", "nccl")
         if backend == "nccl":

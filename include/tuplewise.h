@@ -166,10 +166,12 @@ int tw_rank_images_query(const void* d_z_all, int64_t n_z_all, const void* d_x, 
  * tw_chain_emit walks `steps` (<= 32) repartitions (host arrays keys_x / keys_z of the Feistel
  * keys) for every element of d_x_rec / d_z_rec (rank-image records; half = 1: X records carry
  * {g, h}), its global position kept in d_x_pos / d_z_pos (u32; first = 1: start from the
- * element's global index).  world == 1: for each step c the images are appended to the bags
- * d_x_bag [steps][n_x] (f32, or {g, h} f32 pairs when half) / d_z_bag [steps][n_z] (f32), each
- * shard's slot range holding exactly its images in an arbitrary order; d_cursors: scratch of
- * steps * 2 * (n_shards + 1) u32.  world > 1: records go to d_send, per destination rank g a
+ * element's global index).  d_send == NULL (one process, world == 1): for each step c the
+ * images are appended to the bags d_x_bag [steps][n_x] (f32, or {g, h} f32 pairs when half) /
+ * d_z_bag [steps][n_z] (f32), each shard's slot range holding exactly its images in an
+ * arbitrary order; d_cursors: scratch of steps * 2 * (n_shards + 1) u32.  d_send given (the
+ * exchange: world > 1, or a world-size-1 group forced through its collectives): records go to
+ * d_send, per destination rank g a
  * chunk of steps buckets of (cap + 1) * W u64 words (W = 1 + half; word 0 of a bucket = its
  * count), each record {image word(s), local position (Z: n_x + position)}; a bucket past cap
  * sets *d_flag (the record is dropped). */
@@ -762,6 +764,10 @@ int tw_allgather_f64(int32_t comm, const double* const* d_send, double* const* d
  * workers are a serial loop (compute_stats.py:71-92). */
 int tw_comm_wait(int32_t comm, void* const* streams, int64_t timeout_ms);
 int tw_comm_set_timeout(int64_t ms);
+/* The deadline of the work queued on the streams BEFORE the last collective (default 600 s):
+ * tw_comm_wait waits for it first, outside the collective's own deadline, and aborts the
+ * communicator if it has not drained by then (a wedged stream ends in an error, not a hang). */
+int tw_comm_set_prior_timeout(int64_t ms);
 
 /* ---- f2: bulk draws of NumPy's legacy global RNG (host code, no GPU) ------------------
  * key (624 words) / pos: the MT19937 state of np.random.get_state(), advanced in place.

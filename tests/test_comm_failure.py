@@ -102,3 +102,46 @@ def test_comm_wait_deadline_starts_after_prior_work(stub):
     assert out["init"] == 0 and out["gather"] == 0 and out["busy_at_gather"]
     assert out["wait"] == 0, out["msg"]
     assert out["aborts"] == 0
+
+
+_WEDGED = r"""
+import ctypes, json, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+from tuplewise import _lib as L
+lib = L.lib()
+stub = ctypes.CDLL(sys.argv[2])
+comm = ctypes.c_int32(-1)
+devs = (ctypes.c_int32 * 1)(0)
+out = {"init": lib.tw_comm_init(1, devs, ctypes.byref(comm))}
+out["set"] = lib.tw_comm_set_prior_timeout(ctypes.c_int64(30))  # 30 ms for the prior work
+a = torch.randn(4096, 4096, device="cuda")
+torch.cuda.synchronize()
+for _ in range(400):  # ~0.2-0.6 s queued ahead of the collective: "wedged" against 30 ms
+    a = a @ a
+    a = a / a.norm()
+P = ctypes.c_void_p * 1
+streams = P(L.stream_handle().value)
+bufs = P(a.data_ptr())
+out["gather"] = lib.tw_allgather_u64(comm.value, bufs, bufs, 4, streams)
+out["wait"] = lib.tw_comm_wait(comm.value, streams, 60000)
+out["msg"] = lib.tw_last_error().decode()
+out["aborts"] = stub.stub_aborts()
+torch.cuda.synchronize()  # the queued work drains before the process ends
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_comm_wait_prior_work_has_its_own_deadline(stub):
+    """the work queued before a collective is waited for under its own deadline
+    (tw_comm_set_prior_timeout), so a stream that never drains ends in an error and an aborted
+    communicator instead of an unbounded wait."""
+    env = dict(os.environ, TW_RCCL_LIB=str(stub), STUB_MODE="ok")
+    r = subprocess.run([sys.executable, "-c", _WEDGED, str(ROOT), str(stub)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["init"] == 0 and out["set"] == 0 and out["gather"] == 0
+    assert out["wait"] == 2 and "prior deadline" in out["msg"], out
+    assert out["aborts"] == 1

@@ -190,7 +190,7 @@ class OracleOpsChain(OracleOpsRank):
                  else pos.numpy().view(np.uint32).astype(np.int64))
             for c, key in enumerate(keys):
                 p = O.feistel_perm(p, world * nl, int(key))
-                if world == 1:
+                if send is None:  # one process: the bags (a send buffer: the exchange)
                     bag = (x_bag if side == 0 else z_bag)[c].numpy()
                     bag.view(np.uint64 if (half and side == 0) else np.uint32)[p] = val
                 else:
@@ -200,7 +200,7 @@ class OracleOpsChain(OracleOpsRank):
                         sel = dst == g
                         buckets.setdefault((g, c), []).append((val[sel], loc[sel]))
             pos.numpy()[:] = p.astype(np.uint32).view(np.int32)
-        if world > 1:
+        if send is not None:
             buf = send.numpy().view(np.uint64)
             for g in range(world):
                 for c in range(steps):
@@ -443,3 +443,85 @@ def test_exchange_overflow_raises_at_repartition():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(got[r] == [True, True, True] for r in range(G)), got
+
+
+def _flag_worker(rank, G, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(G, 600, 450)
+    S = ShardedSample(torch.from_numpy(X[rank * 600:(rank + 1) * 600].copy()),
+                      torch.from_numpy(Z[rank * 450:(rank + 1) * 450].copy()), 3,
+                      group=dist.group.WORLD, ops=OracleOpsChain(), algo="pairs")
+    if rank == 0:  # an overflow seen by rank 0 only (a sending rank and its receiver)
+        S._chain_flag = torch.ones((1,), dtype=torch.int32)
+    try:
+        S.UnN_many([5, 6])
+        raised = False
+    except RuntimeError:
+        raised = True
+    q.put((rank, raised))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_chain_overflow_raises_on_every_rank():
+    """ADVICE r04: a step-chain bucket overflow flags only the sending and the receiving rank;
+    the flag rides in the counts' all-reduce, so EVERY rank raises in values() — none returns
+    estimates built from the corrupted counts, and the ranks agree."""
+    import tuplewise  # noqa: F401
+    G = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flag_worker, args=(r, G, port, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(G))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(got[r] for r in range(G)), got
+
+
+def _forced_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(1, 1800, 1350)
+    out = {}
+    for tie in ("strict", "half"):
+        S = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), 9,
+                          group=dist.group.WORLD, ops=OracleOpsChain(), tie_mode=tie,
+                          algo="pairs", collectives=True)
+        assert S.coll and S._multi()
+        vals = [float(v) for v in S.UnN_many([5, 6, 9, 11, 2, 7, 8])]
+        vals.append(float(S.UnN(3)))  # the fixed exchange + one all-reduce
+        out[tie] = (vals, S.X.numpy().copy(), S.Z.numpy().copy())
+    q.put(out)
+    dist.destroy_process_group()
+
+
+def test_forced_collectives_at_world_size_one_equal_one_process():
+    """VERDICT r04 item 1 on CPU: ShardedSample(collectives=True) on a world-size-1 group runs
+    the multi-rank branches (all-gathers, chain emission into send buckets, the all-to-all,
+    unpack, chain_gather, the counts' all-reduce, the fixed exchange) and must equal the
+    one-process path bit for bit; tests/test_gpu_rccl.py runs the same on RCCL."""
+    import tuplewise  # noqa: F401
+    from tuplewise.device import ShardedSample
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(_free_port(), q))
+    p.start()
+    got = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    X, Z = _global_data(1, 1800, 1350)
+    for tie in ("strict", "half"):
+        S = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), 9,
+                          ops=OracleOpsChain(), tie_mode=tie, algo="pairs")
+        want = [float(v) for v in S.UnN_many([5, 6, 9, 11, 2, 7, 8])]
+        want.append(float(S.UnN(3)))
+        vals, Xf, Zf = got[tie]
+        assert vals == want
+        assert np.array_equal(Xf, S.X.numpy()) and np.array_equal(Zf, S.Z.numpy())

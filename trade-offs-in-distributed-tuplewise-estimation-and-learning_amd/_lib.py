@@ -163,6 +163,7 @@ _SIGNATURES = {
     "tw_allgather_f64": [_i32, _vp, _vp, _i64, _vp],
     "tw_comm_wait": [_i32, _vp, _i64],
     "tw_comm_set_timeout": [_i64],
+    "tw_comm_set_prior_timeout": [_i64],
     "tw_np_randint_batch": [_vp, _vp, _i32, _vp, _vp, _vp, _vp],
     "tw_np_mt_next32": [_vp, _vp, _i64, _vp],
     "tw_np_randint_pairs": [_vp, _vp, _i32, _i64, _i64, _i64, _vp, _vp],
@@ -319,3 +320,20 @@ def to_device_many(arrays) -> list:
 
 def empty(shape, dtype):
     return torch().empty(shape, dtype=dtype, device=device())
+
+
+def collectives_default(group, G: int) -> bool:
+    """The collectives= default of ShardedSample / SGDEngine: the multi-rank branches exactly
+    when the group has several ranks, or on any group when TW_FORCE_COLLECTIVES=1 (bench.py's
+    world-size-1 RCCL rehearsal: every collective of the multi-GPU path on one GPU)."""
+    if group is None:
+        return False
+    return G > 1 or os.environ.get("TW_FORCE_COLLECTIVES", "") == "1"
+
+
+def capture(graph):
+    """torch.cuda.graph(graph) in thread-local capture mode: other host threads (the RCCL
+    process group's watchdog polling its events, the native draw thread) keep making HIP calls
+    while a stream of this thread captures — in the default global mode those calls invalidate
+    the capture and kill the watchdog (seen on a world-size-1 nccl group)."""
+    return torch().cuda.graph(graph, capture_error_mode="thread_local")

@@ -67,9 +67,10 @@ struct ChainEmit {
   void* xbag;
   uint32_t* zbag;
   unsigned* cur;
-  // several ranks: per destination g, steps buckets of 1 + cap records of W words (slot 0: the
-  // count), records {image word(s), local position (z: nx + position)}
-  int world, W;
+  // the exchange (several ranks, or one rank forced through its collectives): per destination
+  // g, steps buckets of 1 + cap records of W words (slot 0: the count), records {image
+  // word(s), local position (z: nx + position)}
+  int xchg, world, W;
   FastDiv dnx, dnz;
   uint64_t* send;
   int64_t cap;
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
     }
   }
   const int N = em.nsh;
-  const int NB = em.world > 1 ? em.world : N + 1;
+  const int NB = em.xchg ? em.world : N + 1;
   const uint32_t kb = (uint32_t)(isx ? em.kx : em.kz);
   const FastDiv dk = isx ? em.dkx : em.dkz;
   const FastDiv dn = isx ? em.dnx : em.dnz;
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
           if ((valid >> r) & 1u) {
             const uint32_t q = pos[r];
             int b;
-            if (em.world > 1) {
+            if (em.xchg) {
               const uint32_t g = fast_div32(q, dn);
               const uint32_t ql = q - g * (uint32_t)n;
               b = (int)g;
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
       const int c = c0 + s;
       const unsigned h = hist[i];
       unsigned* cu;
-      if (em.world > 1)
+      if (em.xchg)
         cu = (unsigned*)(em.send + ((int64_t)b * em.steps + c) * (em.cap + 1) * em.W);
       else
         cu = em.cur + ((int64_t)c * 2 + (isx ? 0 : 1)) * (N + 1) + b;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
     auto put = [&](int i, unsigned u, uint64_t v, uint32_t a) {
       const int s = i / NB, b = i - s * NB;
       const int c = c0 + s;
-      if (em.world > 1) {
+      if (em.xchg) {
         if ((int64_t)u >= em.cap) {
           *em.flag = 1;  // dropped, never written out of place; the host raises
           return;
@@ -571,18 +572,21 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
                "tw_chain_emit: bad sizes");
   TW_ARG_CHECK((int64_t)world * n_x < (1ll << 32) && (int64_t)world * n_z < (1ll << 32),
                "tw_chain_emit: positions must fit 32 bits");
-  TW_ARG_CHECK((world > 1 ? world : n_shards + 1) <= kEmMaxBig,
+  // the exchange mode is chosen by the send buffer, not by world > 1: a world-size-1 process
+  // group can be forced through the collectives' path (ShardedSample(collectives=True))
+  const bool xchg = d_send != nullptr;
+  TW_ARG_CHECK((xchg ? world : n_shards + 1) <= kEmMaxBig,
                "tw_chain_emit: at most %d buckets (shards + 1, or ranks)", kEmMaxBig);
   TW_ARG_CHECK(steps == 0 || (keys_x != nullptr && keys_z != nullptr),
                "tw_chain_emit: keys missing");
   if (steps == 0 || n_x + n_z == 0) return TW_OK;
   TW_ARG_CHECK(d_x_pos != nullptr && d_z_pos != nullptr, "tw_chain_emit: position state missing");
-  if (world > 1)
-    TW_ARG_CHECK(d_send != nullptr && d_flag != nullptr && cap >= 1 && world <= 1024,
-                 "tw_chain_emit: send buffer, flag and cap >= 1 needed over ranks");
+  if (xchg)
+    TW_ARG_CHECK(d_flag != nullptr && cap >= 1 && world <= 1024,
+                 "tw_chain_emit: flag and cap >= 1 needed with a send buffer");
   else
-    TW_ARG_CHECK(d_x_bag != nullptr && d_z_bag != nullptr && d_cursors != nullptr,
-                 "tw_chain_emit: bags and cursors needed in one process");
+    TW_ARG_CHECK(world == 1 && d_x_bag != nullptr && d_z_bag != nullptr && d_cursors != nullptr,
+                 "tw_chain_emit: over ranks a send buffer, in one process bags and cursors");
   hipStream_t st = (hipStream_t)stream;
   ChainEmit em{};
   em.xr = d_x_rec;
@@ -606,6 +610,7 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
   em.xbag = d_x_bag;
   em.zbag = (uint32_t*)d_z_bag;
   em.cur = d_cursors;
+  em.xchg = xchg ? 1 : 0;
   em.world = world;
   em.W = half ? 2 : 1;
   em.dnx = make_fastdiv(n_x > 0 ? n_x : 1);
@@ -613,7 +618,7 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
   em.send = d_send;
   em.cap = cap;
   em.flag = d_flag;
-  if (world > 1) {
+  if (xchg) {
     const int64_t buckets = (int64_t)world * steps;
     hipLaunchKernelGGL(k_chain_zero_heads, dim3((unsigned)ceil_div(buckets, kBlock)),
                        dim3(kBlock), 0, st, d_send, buckets, (cap + 1) * em.W);
@@ -622,7 +627,7 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
                                sizeof(unsigned) * (size_t)steps * 2 * (n_shards + 1), st));
   }
   const ChainKeys k = chain_keys(keys_x, keys_z, steps);
-  const int NB = world > 1 ? world : n_shards + 1;
+  const int NB = xchg ? world : n_shards + 1;
   auto launch = [&](auto epr, auto spr, auto staged) {
     constexpr int EPR = decltype(epr)::value, S = decltype(spr)::value;
     constexpr bool ST = decltype(staged)::value;

@@ -55,6 +55,11 @@ static std::vector<std::vector<hipEvent_t>> g_pre;    // handle -> per device, r
                                                       // stream just before the collective
 static std::vector<char> g_dead;                      // handle -> aborted after a failure
 static int64_t g_wait_ms = 60000;                     // tw_comm_set_timeout
+// the work queued on a stream BEFORE the collective gets its own, generous deadline
+// (tw_comm_set_prior_timeout): a legitimately long count must not be taken for an RCCL failure,
+// but a wedged stream (an earlier collective that never completes, a hung kernel) must still
+// end in an error rather than an unbounded wait
+static int64_t g_prior_ms = 600000;
 
 static bool load_rccl() {
   if (g_rccl.h) return true;
@@ -180,7 +185,8 @@ static int wait_comm(int32_t comm, void* const* streams, int64_t timeout_ms) {
     }
     return TW_OK;
   };
-  // first the work queued before the collective (no deadline: a legitimately long count)
+  // first the work queued before the collective, under its own deadline
+  const auto tp = std::chrono::steady_clock::now();
   for (bool before = true; before;) {
     if (const int rc = async_error()) return rc;
     before = false;
@@ -193,7 +199,13 @@ static int wait_comm(int32_t comm, void* const* streams, int64_t timeout_ms) {
         return fail("event query failed", hipGetErrorString(q));
       }
     }
-    if (before) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    if (!before) break;
+    const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                           std::chrono::steady_clock::now() - tp).count();
+    if (ms > g_prior_ms)
+      return fail("the work queued before the collective did not finish in time",
+                  "prior deadline");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   const auto t0 = std::chrono::steady_clock::now();  // the collective's own deadline
   for (;;) {
@@ -266,6 +278,12 @@ extern "C" int tw_comm_wait(int32_t comm, void* const* streams, int64_t timeout_
 extern "C" int tw_comm_set_timeout(int64_t ms) {
   TW_ARG_CHECK(ms > 0, "tw_comm_set_timeout: ms > 0");
   g_wait_ms = ms;
+  return TW_OK;
+}
+
+extern "C" int tw_comm_set_prior_timeout(int64_t ms) {
+  TW_ARG_CHECK(ms > 0, "tw_comm_set_prior_timeout: ms > 0");
+  g_prior_ms = ms;
   return TW_OK;
 }
 

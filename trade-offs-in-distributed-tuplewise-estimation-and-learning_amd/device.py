@@ -348,10 +348,14 @@ class ShardedSample:
     "auto" (sorted for large shards).
     exchange (several ranks): "fixed" (equal-size buckets, one permutation pass, no host round
     trip per repartition) or "exact" (counted buckets: a count pass, the inverse permutation and
-    a host copy of the split sizes).  Both give the same arrays."""
+    a host copy of the split sizes).  Both give the same arrays.
+    collectives: None (default) = the collective branches (exchange, all-gathers, all-reduce of
+    the counts) exactly when the group has several ranks; True forces them on a world-size-1
+    group too (every RCCL call of the multi-rank path then runs on one GPU; same integers, same
+    arrays as the one-process path); False is refused with several ranks."""
 
     def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None,
-                 algo: str = "auto", exchange: str = "fixed"):
+                 algo: str = "auto", exchange: str = "fixed", collectives=None):
         if exchange not in ("fixed", "exact"):
             raise ValueError(f"exchange must be 'fixed' or 'exact', not {exchange!r}")
         self.exchange = exchange
@@ -368,6 +372,13 @@ class ShardedSample:
         else:
             self.dist = None
             self.G, self.rank = 1, 0
+        self.coll = (L.collectives_default(group, self.G) if collectives is None
+                     else bool(collectives))
+        if self.coll and group is None:
+            raise ValueError("collectives=True needs a process group")
+        if self.G > 1 and not self.coll:
+            raise ValueError("several ranks always take the collective branches")
+        self._flag_all = None  # the ranks' overflow flags, summed by the last counts reduction
         if X.dtype == t.float64:
             self.dtype = L.TW_F64
         elif X.dtype == t.int64:
@@ -446,10 +457,39 @@ class ShardedSample:
                         "recv": t.empty((G * (cap + 1), 2), dtype=t.int64, device=dev)}
         return self._xf
 
+    def _local_flag(self):
+        """This rank's sticky overflow flags (fixed exchange + step chains) as one int64 device
+        element, or None before any exchange ran."""
+        fl = [f for f in ((self._xf or {}).get("flag"), getattr(self, "_chain_flag", None))
+              if f is not None]
+        if not fl:
+            return None
+        return sum(f.to(self.t.int64) for f in fl)
+
+    def _reduce_counts(self, counts):
+        """(T, N) local counts -> (T, G*N) global counts in shard order on every rank, with the
+        ranks' overflow flags summed in the SAME all-reduce (one extra element): a bucket that
+        overflowed on any rank is then seen by every rank in values(), so all ranks raise
+        together instead of the two involved ones only."""
+        t, G, N, r = self.t, self.G, self.N, self.rank
+        T = counts.shape[0]
+        flat = t.zeros((T * G * N + 1,), dtype=t.int64, device=counts.device)
+        flat[:-1].view(T, G * N)[:, r * N:(r + 1) * N] = counts
+        f = self._local_flag()
+        if f is not None:
+            flat[-1:] = f.reshape(1)
+        self.dist.all_reduce(flat, group=self.group)
+        self._flag_all = flat[-1:]
+        return flat[:-1].view(T, G * N)
+
     def check_exchange(self):
         """Raise if a fixed-capacity repartition overflowed a bucket (host sync).  The flag is
         sticky: records past a bucket's capacity were dropped, so the arrays stay invalid for
-        every later step of this sample (a later repartition only permutes them)."""
+        every later step of this sample (a later repartition only permutes them).  Over ranks
+        the flag read is the ranks' sum from the last counts all-reduce, so every rank raises."""
+        if self._flag_all is not None and int(self._flag_all.item()):
+            raise RuntimeError("repartition: an exchange bucket on some rank overflowed its "
+                               "capacity; the counts and arrays are invalid")
         if self._xf is not None and int(self._xf["flag"].item()):
             raise RuntimeError("repartition: an exchange bucket overflowed its capacity; the "
                                "arrays are invalid (use ShardedSample(..., exchange='exact'))")
@@ -474,17 +514,22 @@ class ShardedSample:
         self.X, self.Z = XZ[:n], XZ[n:]
 
     def _multi(self) -> bool:
-        """The exchange path (always with G > 1; at G = 1 only when _force_multi is set, a
-        probe hook for timing the multi-rank orchestration on one GPU)."""
-        return self.G > 1 or getattr(self, "_force_multi", False)
+        """The exchange path: several ranks, or a world-size-1 group with collectives=True."""
+        return self.coll
 
     def repartition(self, key: int, check: bool = True):
         """One repartition: new random shards for both samples (key = any 64-bit integer).
         With several ranks and the fixed-capacity exchange, check=True waits for the exchange
-        and raises if a bucket overflowed, so X and Z are never read corrupt; the pipelined
+        and raises if a bucket overflowed on any rank (one small all-reduce of the flags, so
+        every rank raises together), so X and Z are never read corrupt; the pipelined
         estimators pass check=False (no host sync per step) and check once in values()."""
         self._repartition(key)
         if check and self._multi():
+            f = self._local_flag()
+            if f is not None:
+                f = f.reshape(1).clone()
+                self.dist.all_reduce(f, group=self.group)
+                self._flag_all = f
             self.check_exchange()
 
     def _repartition(self, key: int):
@@ -523,14 +568,11 @@ class ShardedSample:
                 and int(sum(self.pairs)) >= ONESHOT_RANK_MIN_PAIRS)
 
     def global_counts(self, local):
-        """All G*N shard counts, in global shard order, on every rank (one all-reduce)."""
-        if self.G == 1:
+        """All G*N shard counts, in global shard order, on every rank (one all-reduce, the
+        ranks' overflow flags riding along)."""
+        if not self.coll:
             return local
-        t = self.t
-        full = t.zeros((self.G * self.N,), dtype=t.int64, device=local.device)
-        full[self.rank * self.N:(self.rank + 1) * self.N] = local
-        self.dist.all_reduce(full, group=self.group)
-        return full
+        return self._reduce_counts(local.reshape(1, -1))[0]
 
     def values(self, counts, pairs=None) -> np.ndarray:
         """Block values count / #pairs of the kept shards, in global shard order: each one
@@ -628,11 +670,8 @@ class ShardedSample:
                     repartition_on_side(keys[i + 1])
             main.wait_stream(side)
         counts = t.stack(local)  # (T, N)
-        if self.G > 1:
-            full = t.zeros((len(keys), self.G * self.N), dtype=t.int64, device=counts.device)
-            full[:, self.rank * self.N:(self.rank + 1) * self.N] = counts
-            self.dist.all_reduce(full, group=self.group)
-            counts = full
+        if self.coll:
+            counts = self._reduce_counts(counts)
         return counts
 
     def UnN_many(self, keys) -> list:
@@ -712,7 +751,7 @@ class ShardedSample:
         the 8-B records {image, index} for the next step (the same keyed permutations as the
         score path); the scores are gathered into the final order once at the end.  Same counts,
         same arrays as the score path."""
-        if self.G > 1:
+        if self.coll:
             # several ranks: every rank ranks the WHOLE sample (one all-gather of both samples
             # per call), keeps its own elements' records (high words: global indices) and the
             # exchanges move 8-B records as they moved scores
@@ -760,7 +799,8 @@ class ShardedSample:
         n, m, N = self.n_loc, self.m_loc, self.N
         dev = self.X.device
         half = self.pred == L.TW_PRED_HALF
-        if G > 1:
+        coll = self.coll  # the exchange branch (several ranks, or forced at world size 1)
+        if coll:
             X0, Z0 = self._all_gather(self.X), self._all_gather(self.Z)
         else:
             X0, Z0 = self.X, self.Z
@@ -789,7 +829,7 @@ class ShardedSample:
         xpos = t.empty((n,), dtype=t.int32, device=dev)
         zpos = t.empty((m,), dtype=t.int32, device=dev)
         counts = t.empty((T, N), dtype=t.int64, device=dev)
-        if G > 1:
+        if coll:
             # a chunk's steps in sub-chunks of <= CHAIN_SUB steps, each with its own send /
             # receive buffers and its own all-to-all (async): every sub-chunk's emission is
             # enqueued first, then each sub-chunk waits for its records, unpacks and counts —
@@ -808,7 +848,7 @@ class ShardedSample:
             cursors = t.empty((C * 2 * (N + 1),), dtype=t.int32, device=dev)
         for i0 in range(0, T, C):
             c = min(C, T - i0)
-            if G > 1:
+            if coll:
                 works = []
                 for j, a in enumerate(range(0, c, Sub)):
                     cs = min(Sub, c - a)
@@ -829,12 +869,9 @@ class ShardedSample:
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
             count(x_bag, z_bag, c, counts[i0:i0 + c])
-        if G > 1:
+        if coll:
             self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
-            full = t.zeros((T, G * N), dtype=t.int64, device=dev)
-            full[:, r * N:(r + 1) * N] = counts
-            self.dist.all_reduce(full, group=self.group)
-            counts = full
+            counts = self._reduce_counts(counts)
         else:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
         return [np.mean(v) for v in self.values(counts)]

@@ -89,10 +89,14 @@ class SGDEngine:
     through an identity row table, so the arithmetic — and the trajectory — is unchanged."""
 
     def __init__(self, X, Z, w_init, N, B, margin, reg, learning_rate, optim_type, group=None,
-                 x_layout="replicated", loss="hinge", gradient="incomplete", vgroup=None):
+                 x_layout="replicated", loss="hinge", gradient="incomplete", vgroup=None,
+                 collectives=None):
         """X, Z, w_init: NumPy arrays (copied to the device) or device tensors (used as is).
         vgroup=(G, r): slot r of G on ONE process (MultiDeviceSGD): shards as rank r, but the
-        shard gradients are gathered and the update applied by the driver (_apply_update)."""
+        shard gradients are gathered and the update applied by the driver (_apply_update).
+        collectives: None = the over-ranks step (eager launches, one all-gather per step, the
+        partitioned exchange) exactly when the group has several ranks; True forces it on a
+        world-size-1 group (every RCCL call of the path runs on one GPU, same trajectory)."""
         t = L.torch()
         self.t = t
         self.group = group
@@ -108,6 +112,13 @@ class SGDEngine:
             self.G, self.rank = dist.get_world_size(group), dist.get_rank(group)
         else:
             self.dist, self.G, self.rank = None, 1, 0
+        self.coll = (self.dist is not None
+                     and (L.collectives_default(group, self.G) if collectives is None
+                          else bool(collectives)))
+        if collectives and self.dist is None:
+            raise ValueError("collectives=True needs a process group")
+        # one process, one device, no collective: the fused / persistent / graph paths apply
+        self.solo = self.G == 1 and not self.coll
         if int(N) % self.G:
             raise ValueError(f"N={N} shards do not split evenly over {self.G} ranks")
         self.N_loc = int(N) // self.G
@@ -147,17 +158,17 @@ class SGDEngine:
         self.w = _dev_f64(w_init).reshape(-1).clone()
         self.dw = t.zeros_like(self.w)
         self.grads = L.empty((self.N, self.d), t.float64)  # all shards, global order
-        self.grads_loc = self.grads if self.G == 1 else L.empty((self.N_loc, self.d), t.float64)
+        self.grads_loc = self.grads if self.solo else L.empty((self.N_loc, self.d), t.float64)
         self.rows_x = self.rows_z = None
         self.step_ctr = None
         # one launch per step (tw_sgd_step: the previous step's update fused into the gradient
         # launch) for narrow rows on one GPU; fused=False keeps grad + update launches
-        self.fused = (self.G == 1 and not self.complete
+        self.fused = (self.solo and not self.complete
                       and bool(L.lib().tw_sgd_step_fusable(self.d, self.N_loc)))
         self._slot1 = None
         # wide rows on one GPU: a whole segment of steps in one persistent launch
         # (tw_sgd_segment: grid barriers between the gradient and the update of every step)
-        self.segment = (SEGMENT_KERNEL and self.G == 1 and not self.complete and not self.fused
+        self.segment = (SEGMENT_KERNEL and self.solo and not self.complete and not self.fused
                         and bool(L.lib().tw_sgd_segment_ok(self.d, self.N_loc)))
         self.narrow_seg = (NARROW_SEGMENT and self.fused
                            and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N_loc, self.B)))
@@ -343,7 +354,7 @@ class SGDEngine:
     def replay_through_ok(self) -> bool:
         """Replay segments may run through reshuffles (tw_sgd_segment_narrow_tables): one
         process, replicated X, the persistent narrow segment kernel."""
-        return (self.narrow_seg and self.G == 1 and self.layout == "replicated"
+        return (self.narrow_seg and self.solo and self.layout == "replicated"
                 and not self.complete and self.N_loc == self.N and self.rows_x is not None)
 
     def rows_ship_args(self, staged):
@@ -403,7 +414,7 @@ class SGDEngine:
         M, M_q = self.N * k, self.N_loc * k
         mine = rows[self.rank * M_q:(self.rank + 1) * M_q]
         L.call("tw_row_table_local", L.ptr(mine), M_q, lo, hi, L.ptr(table), s)
-        if G == 1:
+        if not self.coll:
             return
         part = self.X_part if side == 0 else self.Z_part
         counts = L.empty((G,), t.int64)
@@ -445,7 +456,7 @@ class SGDEngine:
     def _update(self):
         if self.vgroup is not None:  # MultiDeviceSGD gathers the slots' gradients, then updates
             return
-        if self.G > 1:
+        if self.coll:
             self.dist.all_gather_into_tensor(self.grads, self.grads_loc, group=self.group)
         self._apply_update()
 
@@ -517,7 +528,7 @@ class SGDEngine:
 
         # a persistent narrow segment is two launches (plus the upload): eager launches cost
         # ~1.5 us per boundary on the stream, a graph launch ~12 (kernel traces r03s31/s32)
-        if not graphs or self.G > 1 or (self.narrow_seg and nsteps > 1 and not self.complete):
+        if not graphs or not self.solo or (self.narrow_seg and nsteps > 1 and not self.complete):
             if upload is not None:
                 upload[1]()
             steps()
@@ -537,7 +548,7 @@ class SGDEngine:
                 self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw),
                                t.empty_like(self.grads))
             g = t.cuda.CUDAGraph()
-            with t.cuda.graph(g):
+            with L.capture(g):
                 if upload is not None:
                     upload[1]()
                 steps()
@@ -547,7 +558,7 @@ class SGDEngine:
     def batch_view(self):
         """The current shards as evaluation_step's SAME_AS_BATCH reads them: (X, Z, row tables
         or None, N, kx, kz) on the device (one process only; None with several ranks)."""
-        if self.G > 1 or self.rows_x is None:
+        if not self.solo or self.rows_x is None:
             return None
         return (self.X, self.Z, self.rows_x, self.rows_z, self.N, self.kx, self.kz)
 
@@ -593,7 +604,7 @@ class SGDEngine:
         the incomplete gradient, and a kernel that draws the rows — the persistent narrow
         segment (nsteps > 1) or the per-step gradient launches of wide rows."""
         # (partitioned at G = 1: the partition is all of X and the tables are the draws)
-        if getattr(self, "seed", None) is None or self.G != 1 or self.complete:
+        if getattr(self, "seed", None) is None or not self.solo or self.complete:
             return False
         if self.narrow_seg:
             return nsteps > 1
@@ -674,7 +685,7 @@ class SGDEngine:
                 for _ in range(n):
                     self.step_device()
 
-        if not graphs or self.G > 1:
+        if not graphs or not self.solo:
             if reshuffle_first:
                 self.reshuffle_device()
             steps(nsteps)
@@ -692,7 +703,7 @@ class SGDEngine:
                 with t.cuda.stream(side):  # warm the launch path outside capture
                     pass
                 t.cuda.current_stream().wait_stream(side)
-                with t.cuda.graph(g):
+                with L.capture(g):
                     if reshuffle_first:
                         self.reshuffle_device()
                     steps(n)
@@ -877,12 +888,13 @@ MULTI_DEVICE_MIN_BYTES = 1 << 30  # gathered row bytes per step below which one 
 
 
 def _engine_for(X, Z, w, N, B, margin, reg, learning_rate, optim_type, group, x_layout, loss,
-                gradient, rng_mode, plain):
+                gradient, rng_mode, plain, collectives=None):
     """learning_process's one-device engine: the cached one when this call matches it (replay
     mode on host arrays, same shapes and hyper-parameters; ENGINE_CACHE), else a new one
     (cached in turn when the call qualifies).  Device-RNG runs are not cached: their graphs
     hold the run's seed."""
     cacheable = (ENGINE_CACHE and plain and rng_mode == "replay" and group is None
+                 and not collectives
                  and x_layout == "replicated"
                  and isinstance(X, np.ndarray) and isinstance(Z, np.ndarray)
                  and X.ndim == 2 and Z.ndim == 2
@@ -897,7 +909,7 @@ def _engine_for(X, Z, w, N, B, margin, reg, learning_rate, optim_type, group, x_
             eng.reload(X, Z, np.asarray(w, dtype=np.float64))
             return eng
     eng = SGDEngine(X, Z, w, N, B, margin, reg, learning_rate, optim_type, group=group,
-                    x_layout=x_layout, loss=loss, gradient=gradient)
+                    x_layout=x_layout, loss=loss, gradient=gradient, collectives=collectives)
     if cacheable:
         _ENGINE["key"], _ENGINE["eng"] = None, None  # release the previous engine first
         _ENGINE["key"], _ENGINE["eng"] = key, eng
@@ -1214,7 +1226,8 @@ def sign_audit_step(X, Z, rows_x, rows_z, ix, iz, w, margin, scores) -> dict:
 
 def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                      rng_mode="replay", graphs=True, group=None, x_layout="replicated",
-                     loss="hinge", gradient="incomplete", sign_audit=None, devices=None):
+                     loss="hinge", gradient="incomplete", sign_audit=None, devices=None,
+                     collectives=None):
     """Learning process for our experiments.  (make_exps.py:96-141)
 
     rng_mode="replay" (default): NumPy's own draws, bit-compatible with the reference; the
@@ -1237,7 +1250,9 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
     device's S and NumPy/BLAS's S; the steps then run one at a time.
     devices: a list of devices for ONE process to spread the shards over (MultiDeviceSGD:
     bit-identical trajectory); default None = TW_DEVICES / every visible device when a step
-    gathers >= 1 GiB of rows (C5 at large B), else one device."""
+    gathers >= 1 GiB of rows (C5 at large B), else one device.
+    collectives: with group, True runs the over-ranks step even on a world-size-1 group (the
+    RCCL calls of the multi-GPU path on one GPU; same trajectory); None = only with G > 1."""
     n_X, n_Z = X.shape[0], Z.shape[0]
     N = p_learn["N"]
     B = p_learn["B"]
@@ -1263,7 +1278,8 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
                              optim_type, devs, loss=loss)
     else:
         eng = _engine_for(X, Z, w, N, B, margin, p_learn["reg"], learning_rate, optim_type,
-                          group, x_layout, loss, gradient, rng_mode, sign_audit is None)
+                          group, x_layout, loss, gradient, rng_mode, sign_audit is None,
+                          collectives)
     if rng_mode == "device":
         assert optim_type in ["SGD", "momentum"]
         return _learning_device(eng, X, Z, p_learn, trajectory, graphs, loss)
@@ -1278,7 +1294,7 @@ def learning_process(X, Z, p_learn, optim_type="momentum", *, trajectory=None,
         draws.rng.acquire()  # NumPy's global state as it is now
     audit_scores = None
     if sign_audit is not None:
-        if eng.complete or eng.G > 1 or eng.layout != "replicated":
+        if eng.complete or not eng.solo or eng.layout != "replicated":
             raise ValueError("sign_audit needs the incomplete gradient on one process with "
                              "replicated X")
         audit_scores = L.empty((eng.N_loc, B), eng.t.float64)
@@ -1466,7 +1482,7 @@ def _replay_segments(eng, draws, segs, wait, shipped, X, Z, p_learn, loss, graph
         # and the fixed pairs only); otherwise it goes first — the reference reshuffles, then
         # evaluates (make_exps.py:123-128)
         upload = None
-        if (graphs and FUSED_SHIP and isinstance(eng, SGDEngine) and eng.G == 1
+        if (graphs and FUSED_SHIP and isinstance(eng, SGDEngine) and eng.solo
                 and (rows is None or rargs is not None)
                 and draws.seg3_w < 8 and draws.seg3_hdev[k] is not None
                 and (not evaluating or TYPE_TRAIN_MONITOR == "FIXED_PAIRS")):
@@ -1905,7 +1921,7 @@ def evaluation_step(i, X_s, Z_s, w, p_learn, *, loss="hinge", _w_dev=None, _grap
             _eval_device(wbuf, p_learn, loss, margin, fixed)  # warm: caches, allocations
             t.cuda.synchronize()
             _eval_small.last = None
-            with t.cuda.graph(g):
+            with L.capture(g):
                 out = _eval_device(wbuf, p_learn, loss, margin, fixed)
             # only the fused small evaluation (two short launches) runs beside a persistent
             # segment: a larger one could hold CUs long enough for the segment's co-resident
