@@ -1290,8 +1290,12 @@ def main():
                                       if S._chain_ok() else " all-to-all repartition")
                                    + " + all-reduce of counts"
                                    if world > 1 else
-                                   "dp1: one GPU, device Feistel repartition fused into the "
-                                   "count launch")},
+                                   ("dp1: one GPU; step chains: every element walks the K "
+                                    "repartitions (k_chain_emit, one launch per chunk of <= 32 "
+                                    "steps) and one k_count_chain launch counts every shard of "
+                                    "the chunk's steps"
+                                    + (" — RCCL world-size-1 rehearsal: every multi-rank "
+                                       "collective forced" if S.coll else "")))},
         "roofline": {"bound": "valu", "kernel": count_kernel,
                      "achieved": achieved / 1e12, "peak": PEAK_LANE_OPS / 1e12,
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,

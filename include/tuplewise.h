@@ -513,18 +513,6 @@ int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* 
                 double lr, double momentum, double* d_w_out, double* d_dw_out,
                 double* d_grads_out, void* stream);
 
-/* ---- Rows L1 + L2, wide rows (32 < d <= 512): a whole segment of nsteps SGD steps in ONE
- * persistent launch (grid = min(n_shards, resident blocks), one block per CU; two grid barriers
- * per step on d_ctl[0]).  Replaces nsteps x (tw_pair_grad(_rng) + tw_sgd_update) of
- * learning-experiment/make_exps.py:126-141 with the same bits.  Draws: replay (d_ix / d_iz of
- * step k at + k*draw_stride elements) or device RNG at *d_step + k (the counter advances by
- * nsteps).  d_w / d_dw are updated in place; d_grads holds the last step's shard gradients.
- * d_ctl: two uint32 words, the caller zeroes them once; the launch zeroes d_ctl[0]; d_ctl[1]
- * is a sticky abort word — non-zero after a launch whose barrier wait timed out (2 s: blocks
- * not co-resident), the SGD state is then invalid.
- * tw_sgd_segment_set_grid(m): cap the grid at m blocks (tests; 0 = resident capacity);
- * tw_sgd_segment_set_prefetch(1|0): prefetch the next step's first 32 pairs as rows (1, the
- * default) or as row indices only (0) while the barriers run. */
 /* A segment of nsteps narrow-row SGD steps (d <= 32; the steps tw_sgd_step launches one by
  * one) in ONE persistent launch (csrc/sgdseg.hip k_sgd_segment_narrow): one block per shard,
  * all co-resident, one grid barrier per step, the update recomputed in every block from the
@@ -596,17 +584,6 @@ int tw_pair_grad_rng_swr(const double* d_X, const double* d_Z, int64_t d, int64_
                          const double* d_w, double margin, int32_t loss, uint64_t seed,
                          const uint64_t* d_step, int32_t shard_base, int64_t swr_mod,
                          uint64_t swr_base, double* d_out, void* stream);
-int tw_sgd_segment_ok(int64_t d, int32_t n_shards);
-int tw_sgd_segment_set_grid(int32_t max_blocks);
-int tw_sgd_segment_set_prefetch(int32_t rows);
-int tw_sgd_segment(const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x,
-                   int64_t kx, const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix,
-                   const int64_t* d_iz, int64_t draw_stride, int32_t n_shards, int64_t B,
-                   double margin, int32_t loss, uint64_t seed, uint64_t* d_step,
-                   int32_t shard_base, int32_t nsteps, double* d_w, double* d_dw,
-                   double* d_grads, double reg, double lr, double momentum, uint32_t* d_ctl,
-                   void* stream);
-
 /* ---- The hinge surrogate over ALL pairs of each shard in O((n + m) log m) (f64 scores):
  * d_out[s] = sum_{i,j} max(fl(fl(z_j - x_i) + margin), 0) — cs.conv_AUC's sum
  * (compute_stats.py:129-135) as evaluation_step's tc_AUC (make_exps.py:167-168) and
@@ -768,6 +745,50 @@ int tw_comm_set_timeout(int64_t ms);
  * tw_comm_wait waits for it first, outside the collective's own deadline, and aborts the
  * communicator if it has not drained by then (a wedged stream ends in an error, not a hang). */
 int tw_comm_set_prior_timeout(int64_t ms);
+
+/* ---- (e) learning over ranks: device-resident gradient exchange (round 5, csrc/peer.hip,
+ * csrc/peer.h).  Replaces the per-step all-gather of the shard partials between the gradient
+ * and the update launches (the shard mean of make_exps.py:126-141 / compute_stats.py:44-46,
+ * split over ranks) by GPU-to-GPU stores into one peer buffer per rank, IPC-mapped into the
+ * others.  tw_peer_buffer_bytes: the buffer size for n_total shards of d columns (-1: bad
+ * sizes).  tw_peer_alloc: a zeroed device buffer, uncached where the driver allows
+ * (*out_uncached = 1), else plain.  tw_peer_handle / tw_peer_open / tw_peer_close: the 64-byte
+ * IPC handle of a buffer, mapped into another process (hipIpcMemLazyEnablePeerAccess).
+ * d_peer_bases below: G device addresses in rank order (this rank's own buffer at `rank`). */
+int64_t tw_peer_buffer_bytes(int32_t n_total, int64_t d);
+int tw_peer_alloc(int64_t bytes, void** d_out, int32_t* out_uncached);
+int tw_peer_free(void* d_ptr);
+int tw_peer_handle(void* d_ptr, uint8_t* out_handle);
+int tw_peer_open(const uint8_t* handle, void** d_out);
+int tw_peer_close(void* d_ptr);
+/* Per-step form, parity par = step & 1: this rank's `words` partial words (its shards' rows,
+ * global offset offset_words) stored into every rank's slot, arrivals added to every rank's
+ * counter; then tw_peer_update waits (bounded: 20 s, *d_abort raised on timeout) until all G
+ * ranks' arrivals are in and applies tw_sgd_update's arithmetic to the n_total x d slot (same
+ * bits), d_step advanced by one when given. */
+int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t offset_words,
+                    void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total,
+                    int64_t d, int32_t par, void* stream);
+int tw_peer_update(double* d_w, double* d_dw, void* d_my_base, int32_t n_total, int64_t d,
+                   int64_t words_per_rank, int32_t G, int32_t par, double reg, double lr,
+                   double momentum, uint64_t* d_step, uint32_t* d_abort, void* stream);
+/* The narrow persistent segment (tw_sgd_segment_narrow) over ranks: this rank's n_shards
+ * blocks (global shards shard_base..) push every step's gradients into every rank's peer
+ * buffer and wait for all n_total shards on their own; the last update is applied in the
+ * launch (d_w / d_dw in place; d_step += nsteps when given).  Replay draws d_ix / d_iz: this
+ * rank's first shard's rows (draw_stride per step); device RNG: d_ix = d_iz = NULL, and
+ * swr_mod > 0 draws the SWR rows in the kernel (else the row tables d_rows_x / d_rows_z).
+ * d_ctl[1]: the abort word. */
+int tw_sgd_segment_narrow_peer(const double* d_X, const double* d_Z, int64_t d,
+                               const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
+                               int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+                               int64_t draw_stride, int32_t n_shards, int64_t B, double margin,
+                               int32_t loss, uint64_t seed, uint64_t* d_step,
+                               int32_t shard_base, int32_t nsteps, int64_t n_X, int64_t n_Z,
+                               int64_t swr_mod, double* d_w, double* d_dw, double reg,
+                               double lr, double momentum, uint32_t* d_ctl,
+                               void* const* d_peer_bases, int32_t G, int32_t rank,
+                               int32_t n_total, void* stream);
 
 /* ---- f2: bulk draws of NumPy's legacy global RNG (host code, no GPU) ------------------
  * key (624 words) / pos: the MT19937 state of np.random.get_state(), advanced in place.

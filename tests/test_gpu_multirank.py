@@ -16,6 +16,9 @@ def _port():
         return s.getsockname()[1]
 
 
+_HIST = ("norm_w", "tr_AUC", "tc_AUC", "bc_AUC")
+
+
 def _learn_worker(rank, port, G, mode, q, layout="replicated"):
     import torch
     import torch.distributed as dist
@@ -28,8 +31,13 @@ def _learn_worker(rank, port, G, mode, q, layout="replicated"):
     np.random.seed(99)
     lr.learning_process(X, Z, p, rng_mode=mode, trajectory=traj, group=dist.group.WORLD,
                         x_layout=layout)
+    # no trajectory: the segments — over ranks the persistent peer segment, whose gradient
+    # exchange runs between the two processes' kernels through IPC-mapped peer buffers
+    p2 = dict(_problem()[3], n_it=60, eval_mod=20)
+    np.random.seed(99)
+    lr.learning_process(X, Z, p2, rng_mode=mode, group=dist.group.WORLD, x_layout=layout)
     if rank == 0:
-        q.put(np.stack(traj))
+        q.put((np.stack(traj), {k: p2[k] for k in _HIST}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -57,6 +65,9 @@ def test_learning_two_ranks_equals_one(gpu, mode, layout):
     ref = []
     np.random.seed(99)
     lr.learning_process(X, Z, p, rng_mode=mode, trajectory=ref)
+    p2 = dict(_problem()[3], n_it=60, eval_mod=20)
+    np.random.seed(99)
+    lr.learning_process(X, Z, p2, rng_mode=mode)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -64,11 +75,12 @@ def test_learning_two_ranks_equals_one(gpu, mode, layout):
              for r in range(2)]
     for pr in procs:
         pr.start()
-    got = q.get(timeout=300)
+    got, hist = q.get(timeout=300)
     for pr in procs:
         pr.join(timeout=120)
         assert pr.exitcode == 0
     assert np.array_equal(got, np.stack(ref))
+    assert len(hist["norm_w"]) == 3 and hist == {k: p2[k] for k in _HIST}
 
 
 def _est_worker(rank, port, G, q, exchange="fixed", chain=True):

@@ -9,8 +9,10 @@ options with the high-priority stream), and the G > 1 branches forced through it
 * ShardedSample._run_steps (UnNB_many, UnN with a key): the fixed-capacity exchange on the
   high-priority side stream (all_to_all_single) and the counts' all-reduce; the counted
   exchange (`exchange="exact"`: all_to_all_single with split sizes);
-* SGDEngine over ranks: the per-step all_gather_into_tensor of the shard gradients (replicated
-  layout) and the partitioned layout's row exchange (all_to_all_single of counts and rows).
+* SGDEngine over ranks: the device-resident gradient exchange (csrc/peer.hip: per-step publish
+  + wait-and-update with a trajectory, the persistent peer segment without), and with
+  learning.PEER_EXCHANGE = False the per-step all_gather_into_tensor of the shard gradients;
+  the partitioned layout's row exchange (all_to_all_single of counts and rows).
 
 Each must give the estimates, final arrays and trajectories of the plain one-process path bit
 for bit (reference: the serial shard loop estimation-experiment/main.py:48-69 and the learning
@@ -95,8 +97,11 @@ def _worker(port, q):
             if not (np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])):
                 out["mismatch"].append((tag, "final arrays"))
         Xl, Zl, p = _learn_problem()
-        for mode in ("replay", "device"):
-            for layout in ("replicated", "partitioned"):
+        for peer, mode, layout in [(pe, m, la) for pe in (True, False)
+                                   for m in ("replay", "device")
+                                   for la in ("replicated", "partitioned")]:
+            lr.PEER_EXCHANGE = peer  # False: the per-step RCCL all-gather of the partials
+            if True:
                 ref, got = [], []
                 np.random.seed(99)
                 lr.learning_process(Xl, Zl, dict(p), rng_mode=mode, trajectory=ref,
@@ -104,10 +109,20 @@ def _worker(port, q):
                 np.random.seed(99)
                 lr.learning_process(Xl, Zl, dict(p), rng_mode=mode, trajectory=got, group=g,
                                     x_layout=layout, collectives=True)
-                tag = f"learning/{mode}/{layout}"
+                tag = f"learning/{'peer' if peer else 'allgather'}/{mode}/{layout}"
                 out["ran"].append(tag)
                 if len(ref) != 50 or not np.array_equal(np.stack(ref), np.stack(got)):
                     out["mismatch"].append((tag, "trajectory"))
+                # no trajectory: the segments (over ranks: the persistent peer segment); the
+                # evaluation histories come from w at steps 0, 25
+                pa, pb = dict(p), dict(p)
+                np.random.seed(99)
+                lr.learning_process(Xl, Zl, pa, rng_mode=mode, x_layout=layout)
+                np.random.seed(99)
+                lr.learning_process(Xl, Zl, pb, rng_mode=mode, group=g, x_layout=layout,
+                                    collectives=True)
+                if any(pa[k] != pb[k] for k in ("norm_w", "tr_AUC", "tc_AUC", "bc_AUC")):
+                    out["mismatch"].append((tag, "segment histories"))
         torch.cuda.synchronize()
         dist.destroy_process_group()
         q.put(("ok", out))
@@ -125,5 +140,5 @@ def test_rccl_world_size_one_equals_one_process(gpu):
     pr.join(timeout=120)
     assert status == "ok", out
     assert pr.exitcode == 0
-    assert len(out["ran"]) == 8, out["ran"]
+    assert len(out["ran"]) == 12, out["ran"]
     assert out["mismatch"] == [], out["mismatch"]

@@ -508,17 +508,24 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
     the last state (the in-place side effect of the T np.random.shuffle calls)."""
     from .numpy_rng import shuffle_draws32
     plans = []
-    ds = E.DeviceShuffles(L.to_device(X), L.to_device(Z), T)
+    # X and Z go up on a helper thread while the host draws the first shuffle
+    ds = E.DeviceShuffles(X, Z, T)
 
-    def draws(a, b):  # shuffle k's draws into pinned memory; the device swaps it meanwhile
+    def draws(a, b):  # each side's draws into pinned memory; the device swaps it meanwhile
         shuffle_draws32(a.shape[0], out=ds.draw_x())
+        ds.push_x()
         shuffle_draws32(b.shape[0], out=ds.draw_z())
-        ds.push()
+        ds.push_z()
 
     for _ in range(T):
         plans.append(plan_un(X, Z, N, spec, sampling_type, variant, shuffle=draws))
     nx, nz = X.shape[0], Z.shape[0]
+    t = L.torch()
+    # the in-place side effect, X first: its last state goes back while Z's last shuffle runs
+    t.from_numpy(X).copy_(ds.last_x())
     xs, zs = ds.finish()
+    if 0 in ds.redone:  # (rare) X's shuffles were resumed: its last state changed
+        t.from_numpy(X).copy_(xs[T - 1])
     blocks, counts = [], []
     for k, plan in enumerate(plans):
         blks = [p[1] for p in plan if p[0] == "val"]
@@ -530,9 +537,8 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
             blocks.append(Block(bx, bz, b.aux))
         counts.append(len(blks))
     vals = spec.evaluate_device(xs.reshape(-1), zs.reshape(-1), blocks) if blocks else []
-    # the in-place side effect: the caller's arrays end in the last shuffled state
-    X[...] = xs[T - 1].cpu().numpy()
-    Z[...] = zs[T - 1].cpu().numpy()
+    # the caller's Z ends in the last shuffled state too (X was written above)
+    t.from_numpy(Z).copy_(zs[T - 1])
     out, i = [], 0
     for p, c in zip(plans, counts):
         out.append(finish_un(p, vals[i:i + c]))

@@ -308,72 +308,145 @@ def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
     return pair_sum_complete_dev(sh, kern, margin).cpu().numpy()
 
 
+_SH_STREAMS = {}  # per device: the X and Z shuffle streams of DeviceShuffles
+
+
 class DeviceShuffles:
-    """T successive np.random.shuffle's of two device arrays of 8-byte items, every state kept:
-    xs[k] = x0 after the swaps of shuffles 0..k (likewise zs).  The host draws each shuffle's
-    indices in NumPy's order (numpy_rng.shuffle_draws32) straight into pinned buffers (draw_x,
-    draw_z); push() uploads them asynchronously and enqueues that shuffle's swap rounds
-    (csrc/devshuffle.hip: the sequential loop's permutation, bit for bit), so the device swaps
-    shuffle k while the host draws shuffle k+1.  finish() reads the pending counts (one sync);
-    a shuffle whose batch of rounds did not finish (rare) is resumed and the shuffles after it
-    are redone.  Returns the (T, nx) and (T, nz) device tensors."""
+    """T successive np.random.shuffle's of two arrays of 8-byte items, every state kept on the
+    device: xs[k] = x0 after the swaps of shuffles 0..k (likewise zs).  The host draws each
+    shuffle's indices in NumPy's order (numpy_rng.shuffle_draws32) straight into pinned buffers
+    (draw_x, draw_z); push_x() / push_z() upload them asynchronously and enqueue that side's
+    swap rounds (csrc/devshuffle.hip: the sequential loop's permutation, bit for bit) on the
+    side's own stream, so X's shuffle k runs while the host draws Z's, and Z's while the host
+    draws X's shuffle k+1 — the last shuffle on the critical path is Z's alone (round 5: the two
+    sides shared every launch before, and the last pair ran after the last draw).
+    x0 / z0: device tensors, or host arrays (1-D float64) uploaded by a helper thread while the
+    host makes the first draws.  finish() reads the pending counts (one sync); a side whose
+    batch of rounds did not finish (rare) is resumed and its later shuffles are redone.
+    Returns the (T, nx) and (T, nz) device tensors."""
 
     def __init__(self, x0, z0, T: int):
+        import threading
         t = L.torch()
         lib = L.lib()
-        assert x0.element_size() == 8 and z0.element_size() == 8
-        self.x0, self.z0 = x0.reshape(-1), z0.reshape(-1)
+        self.t = t
         self.T = T
-        self.nx, self.nz = int(x0.numel()), int(z0.numel())
-        self.xs = L.empty((T, self.nx), x0.dtype)
-        self.zs = L.empty((T, self.nz), z0.dtype)
+        host = not isinstance(x0, t.Tensor)
+        self.nx = int(np.asarray(x0).size if host else x0.numel())
+        self.nz = int(np.asarray(z0).size if host else z0.numel())
+        dev = t.cuda.current_device()
+        if dev not in _SH_STREAMS:
+            _SH_STREAMS[dev] = (t.cuda.Stream(), t.cuda.Stream())
+        self.sx, self.sz = _SH_STREAMS[dev]
+        main = t.cuda.current_stream()
+        self.sx.wait_stream(main)
+        self.sz.wait_stream(main)
+        self._up = None
+        if host:
+            self.x0 = L.empty((self.nx,), t.float64)
+            self.z0 = L.empty((self.nz,), t.float64)
+
+            def upload():  # pageable H2D copies, GIL released; the streams order the shuffles
+                with t.cuda.device(dev):
+                    with t.cuda.stream(self.sx):
+                        self.x0.copy_(t.from_numpy(np.ascontiguousarray(x0).reshape(-1)))
+                    with t.cuda.stream(self.sz):
+                        self.z0.copy_(t.from_numpy(np.ascontiguousarray(z0).reshape(-1)))
+            self._up = threading.Thread(target=upload)
+            self._up.start()
+        else:
+            assert x0.element_size() == 8 and z0.element_size() == 8
+            self.x0, self.z0 = x0.reshape(-1), z0.reshape(-1)
+        dt = self.x0.dtype
+        self.xs = L.empty((T, self.nx), dt)
+        self.zs = L.empty((T, self.nz), dt)
         self.hx = t.empty((T, self.nx), dtype=t.int32, pin_memory=True)
         self.hz = t.empty((T, self.nz), dtype=t.int32, pin_memory=True)
         self.jx = L.empty((T, self.nx), t.int32)
         self.jz = L.empty((T, self.nz), t.int32)
-        nb = max(int(lib.tw_shuffle_swaps_work_bytes(self.nx, self.nz)), 1)
-        self.rounds = int(lib.tw_shuffle_swaps_rounds(self.nx, self.nz))
-        self.work = L.empty((T, nb), t.uint8)
-        self.pend = L.empty((max(T, 1),), t.int32)
-        self.k = 0
+        nbx = max(int(lib.tw_shuffle_swaps_work_bytes(self.nx, 0)), 1)
+        nbz = max(int(lib.tw_shuffle_swaps_work_bytes(0, self.nz)), 1)
+        self.rounds = (int(lib.tw_shuffle_swaps_rounds(self.nx, 0)),
+                       int(lib.tw_shuffle_swaps_rounds(0, self.nz)))
+        self.work = (L.empty((T, nbx), t.uint8), L.empty((T, nbz), t.uint8))
+        self.pend = L.empty((2, max(T, 1)), t.int32)
+        self.kx = self.kz = 0
+
+    def _uploaded(self):
+        if self._up is not None:
+            self._up.join()
+            self._up = None
 
     def draw_x(self):
-        return self.hx[self.k].numpy()
+        return self.hx[self.kx].numpy()
 
     def draw_z(self):
-        return self.hz[self.k].numpy()
+        return self.hz[self.kz].numpy()
+
+    def push_x(self) -> None:
+        self._uploaded()
+        with self.t.cuda.stream(self.sx):
+            self.jx[self.kx].copy_(self.hx[self.kx], non_blocking=True)
+            self._start(0, self.kx)
+        self.kx += 1
+
+    def push_z(self) -> None:
+        self._uploaded()
+        with self.t.cuda.stream(self.sz):
+            self.jz[self.kz].copy_(self.hz[self.kz], non_blocking=True)
+            self._start(1, self.kz)
+        self.kz += 1
 
     def push(self) -> None:
-        k = self.k
-        self.jx[k].copy_(self.hx[k], non_blocking=True)
-        self.jz[k].copy_(self.hz[k], non_blocking=True)
-        self._start(k)
-        self.k += 1
+        self.push_x()
+        self.push_z()
 
-    def _run(self, k, first, round0):
-        L.call("tw_shuffle_swaps", L.ptr(self.xs[k]), self.nx, L.ptr(self.zs[k]), self.nz,
-               L.ptr(self.jx[k]), L.ptr(self.jz[k]), int(first), round0, L.ptr(self.work[k]),
-               L.ptr(self.pend[k:k + 1]), L.stream_handle())
+    def _run(self, side, k, first, round0):
+        if side == 0:
+            L.call("tw_shuffle_swaps", L.ptr(self.xs[k]), self.nx, None, 0, L.ptr(self.jx[k]),
+                   None, int(first), round0, L.ptr(self.work[0][k]),
+                   L.ptr(self.pend[0, k:k + 1]), L.stream_handle())
+        else:
+            L.call("tw_shuffle_swaps", None, 0, L.ptr(self.zs[k]), self.nz, None,
+                   L.ptr(self.jz[k]), int(first), round0, L.ptr(self.work[1][k]),
+                   L.ptr(self.pend[1, k:k + 1]), L.stream_handle())
 
-    def _start(self, k):
-        self.xs[k].copy_(self.x0 if k == 0 else self.xs[k - 1])
-        self.zs[k].copy_(self.z0 if k == 0 else self.zs[k - 1])
-        self._run(k, True, 0)
+    def _start(self, side, k):  # on the side's stream
+        xs = self.xs if side == 0 else self.zs
+        xs[k].copy_((self.x0 if side == 0 else self.z0) if k == 0 else xs[k - 1])
+        self._run(side, k, True, 0)
+
+    def last_x(self):
+        """The X side's last state, ordered on the current stream after its shuffles (a
+        caller may copy it out while Z's last shuffle runs); finish() says whether it held."""
+        self.t.cuda.current_stream().wait_stream(self.sx)
+        return self.xs[self.T - 1]
 
     def finish(self):
-        T = self.T
-        assert self.k == T, "every shuffle must be pushed before finish()"
-        left = np.nonzero(self.pend[:T].cpu().numpy())[0]
-        if len(left):  # rare: finish shuffle k, then redo the later ones one at a time
+        """Sync on the pending counts; resume the rare unfinished side.  Returns (xs, zs) and
+        leaves the current stream ordered after both sides.  self.redone: the sides whose
+        states changed after a resumption."""
+        T, t = self.T, self.t
+        assert self.kx == T and self.kz == T, "every shuffle must be pushed before finish()"
+        main = t.cuda.current_stream()
+        main.wait_stream(self.sx)
+        main.wait_stream(self.sz)
+        pend = self.pend[:, :T].cpu().numpy()
+        self.redone = set()
+        for side in (0, 1):
+            left = np.nonzero(pend[side])[0]
+            if not len(left):
+                continue
+            self.redone.add(side)
             k = int(left[0])
-            while k < T:
-                r0 = self.rounds
-                while int(self.pend[k].item()):
-                    self._run(k, False, r0)
-                    r0 += self.rounds
+            while k < T:  # finish shuffle k, then redo the later ones one at a time
+                r0 = self.rounds[side]
+                while int(self.pend[side, k].item()):
+                    self._run(side, k, False, r0)
+                    r0 += self.rounds[side]
                 k += 1
                 if k < T:
-                    self._start(k)
+                    self._start(side, k)
         return self.xs, self.zs
 
 

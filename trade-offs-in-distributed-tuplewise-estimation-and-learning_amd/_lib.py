@@ -114,7 +114,6 @@ _SIGNATURES = {
     "tw_sgd_step": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _f64, _i32, _u64,
                     _vp, _i32, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
     "tw_count_rng_img_set_unroll": [_i32],
-    "tw_sgd_segment_ok": [_i64, _i32],
     "tw_sgd_segment_narrow_ok": [_i64, _i32, _i64],
     "tw_sgd_segment_narrow": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i64,
                               _f64, _i32, _u64, _vp, _i32, _i32, _vp, _vp, _f64, _f64, _f64, _vp,
@@ -128,10 +127,18 @@ _SIGNATURES = {
     "tw_sgd_segment_narrow_swr": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _f64,
                                   _i32, _u64, _vp, _i32, _i32, _i64, _u64, _vp, _vp, _f64,
                                   _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
-    "tw_sgd_segment_set_grid": [_i32],
-    "tw_sgd_segment_set_prefetch": [_i32],
-    "tw_sgd_segment": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i64, _f64,
-                       _i32, _u64, _vp, _i32, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp],
+    "tw_peer_buffer_bytes": [_i32, _i64],
+    "tw_peer_alloc": [_i64, _vp, _vp],
+    "tw_peer_free": [_vp],
+    "tw_peer_handle": [_vp, _vp],
+    "tw_peer_open": [_vp, _vp],
+    "tw_peer_close": [_vp],
+    "tw_peer_publish": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i64, _i32, _vp],
+    "tw_peer_update": [_vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _f64, _f64, _f64, _vp, _vp,
+                       _vp],
+    "tw_sgd_segment_narrow_peer": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
+                                   _i64, _f64, _i32, _u64, _vp, _i32, _i32, _i64, _i64, _i64,
+                                   _vp, _vp, _f64, _f64, _f64, _vp, _vp, _i32, _i32, _i32, _vp],
     "tw_gemv_f64": [_vp, _i64, _i64, _vp, _vp, _vp],
     "tw_gemv_set_variant": [_i32],
     "tw_pair_hinge_sum_sorted_work_bytes": [_i32, _i64, _i64],
@@ -198,6 +205,7 @@ _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,
     "tw_count_pairs_sorted_work_bytes": ctypes.c_int64,
     "tw_rank_images_work_bytes": ctypes.c_int64,
+    "tw_peer_buffer_bytes": ctypes.c_int64,
     "tw_count_pairs_rng_work_bytes": ctypes.c_int64,
     "tw_count_pairs_sorted_steps_work_bytes": ctypes.c_int64,
     "tw_pair_sum_work_per_shard": ctypes.c_int64,

@@ -1,0 +1,205 @@
+// peer.hip — device-resident gradient exchange between ranks (round 5; SURVEY.md §8(e)
+// "Learning").  Reference: the per-step shard mean of learning-experiment/make_exps.py:126-141
+// (grads = UN_split(X_s, Z_s, grad_inc_block(w, B, margin)), compute_stats.py:44-46), which a
+// multi-GPU run splits over ranks: every rank computes its shards' partial gradients and every
+// rank needs all of them, in shard order, before the update.
+//
+// Over RCCL that is a host-enqueued all-gather between the gradient and the update launches:
+// three host launches and a collective's latency per step, against an 8-us step on one GPU
+// (C4).  Here the GPUs exchange the partials themselves, through one peer buffer per rank
+// (layout: csrc/peer.h) allocated UNCACHED and mapped into every other rank with an IPC handle
+// (xGMI peer access; HSA_ENABLE_IPC_MODE_LEGACY=0: dmabuf handles).  Two forms:
+//  * the persistent narrow segment (csrc/sgdseg.hip, tw_sgd_segment_narrow_peer): C4's
+//    segments, the exchange inside the launch;
+//  * per step (any d, any gradient kernel; C5): the gradient launch writes the rank's
+//    (N/G, d) partials as usual, tw_peer_publish pushes them into every rank's per-step slot
+//    of the step's parity and adds this launch's arrivals to every rank's parity counter, and
+//    tw_peer_update waits for all ranks' arrivals on its own counter and applies k_sgd_update's
+//    arithmetic to the slot (same bits as the one-GPU update).  No host collective per step.
+// Counter reuse of the per-step form: update(t) waits for counter[t & 1] >= P * G (P publish
+// blocks per rank); publish(t + 1) zeroes this rank's counter[t & 1] (update(t) is done: stream
+// order) BEFORE its block 0 adds its arrivals, and a rank can add to counter[t & 1] again only
+// in publish(t + 2), after its update(t + 1) saw those arrivals.  Slots likewise: slot t & 1 of
+// a rank is rewritten by publish(t + 2), after every rank's update(t) has read it.
+#include "peer.h"
+#include <algorithm>
+#include <cstring>
+
+namespace tw {
+
+constexpr int kPubBlocks = 32;  // publish blocks per rank (all ranks the same: the target)
+
+static int publish_blocks(int64_t words) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kPubBlocks, ceil_div(words, (int64_t)kBlock * 4)));
+}
+
+// this rank's (rows, d) partials -> rows [row0, row0 + rows) of every rank's slot `par`
+__global__ __launch_bounds__(kBlock) void k_peer_publish(const double* __restrict__ src,
+                                                         int64_t words, int64_t off,
+                                                         PeerSeg ps, int par,
+                                                         unsigned long long* reset) {
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(reset, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const size_t base = (size_t)par * ps.n_total + off;  // in words: ps.n_total holds N * d here
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < words;
+       i += (int64_t)gridDim.x * kBlock) {
+    const double v = src[i];
+    for (int p = 0; p < ps.G; ++p) st_sys(ps.slot[p] + base + i, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores (and the reset) done
+  __syncthreads();
+  if ((int)threadIdx.x < ps.G)
+    __hip_atomic_fetch_add(ps.ctr[threadIdx.x], 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// k_sgd_update (csrc/hinge.hip) on the slot, once every rank's arrivals are in: the same
+// shard-order sum from +0.0, /N, + reg * w, momentum — the same bits
+constexpr int kPUpdCols = 8, kPUpdRows = 1024;
+__global__ __launch_bounds__(kBlock) void k_peer_update(double* w, double* dw,
+                                                        const double* __restrict__ slot,
+                                                        const unsigned long long* ctr,
+                                                        uint64_t target, int n_shards,
+                                                        int64_t d, double reg, double lr,
+                                                        double momentum,
+                                                        uint64_t* __restrict__ d_step,
+                                                        uint32_t* abort_word) {
+  __shared__ double tile[kPUpdRows * kPUpdCols];
+  __shared__ int s_ok;
+  if (!peer_wait(ctr, target, abort_word, &s_ok)) return;
+  if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += 1;
+  const int64_t j0 = (int64_t)blockIdx.x * kPUpdCols;
+  const int nc = (int)std::min<int64_t>(kPUpdCols, d - j0);
+  double sum = 0.0;
+  for (int s0 = 0; s0 < n_shards; s0 += kPUpdRows) {
+    const int ns = std::min(kPUpdRows, n_shards - s0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * kPUpdCols; e += kBlock) {
+      const int r = e / kPUpdCols, c = e - r * kPUpdCols;
+      tile[e] = c < nc ? ld_sys(slot + (int64_t)(s0 + r) * d + j0 + c) : 0.0;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nc) {
+      int r = 0;
+      for (; r + 8 <= ns; r += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * kPUpdCols + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum += v[u];
+      }
+      for (; r < ns; ++r) sum += tile[r * kPUpdCols + threadIdx.x];
+    }
+  }
+  if ((int)threadIdx.x < nc) {
+    const int64_t j = j0 + threadIdx.x;
+    const double wj = w[j];
+    const double g = sum / (double)n_shards + reg * wj;
+    const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
+    dw[j] = step;
+    w[j] = wj - step;
+  }
+}
+
+}  // namespace tw
+
+using namespace tw;
+
+extern "C" int64_t tw_peer_buffer_bytes(int32_t n_total, int64_t d) {
+  if (n_total < 1 || d < 1) return -1;
+  return (int64_t)peer_buffer_bytes(n_total, d);
+}
+
+extern "C" int tw_peer_alloc(int64_t bytes, void** d_out, int32_t* out_uncached) {
+  TW_ARG_CHECK(bytes > 0 && d_out != nullptr, "tw_peer_alloc: bytes > 0 and an output");
+  void* p = nullptr;
+  int unc = 1;
+  if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    unc = 0;
+    TW_HIP_CHECK(hipMalloc(&p, (size_t)bytes));
+  }
+  if (hipMemset(p, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    set_error("tw_peer_alloc: zeroing the buffer failed");
+    return TW_ERR_HIP;
+  }
+  *d_out = p;
+  if (out_uncached) *out_uncached = unc;
+  return TW_OK;
+}
+
+extern "C" int tw_peer_free(void* d_ptr) {
+  if (d_ptr) TW_HIP_CHECK(hipFree(d_ptr));
+  return TW_OK;
+}
+
+extern "C" int tw_peer_handle(void* d_ptr, uint8_t* out_handle) {
+  TW_ARG_CHECK(d_ptr != nullptr && out_handle != nullptr, "tw_peer_handle: pointer and output");
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle larger than 64 bytes");
+  hipIpcMemHandle_t h;
+  TW_HIP_CHECK(hipIpcGetMemHandle(&h, d_ptr));
+  std::memset(out_handle, 0, 64);
+  std::memcpy(out_handle, &h, sizeof(h));
+  return TW_OK;
+}
+
+extern "C" int tw_peer_open(const uint8_t* handle, void** d_out) {
+  TW_ARG_CHECK(handle != nullptr && d_out != nullptr, "tw_peer_open: handle and output");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  TW_HIP_CHECK(hipIpcOpenMemHandle(d_out, h, hipIpcMemLazyEnablePeerAccess));
+  return TW_OK;
+}
+
+extern "C" int tw_peer_close(void* d_ptr) {
+  if (d_ptr) TW_HIP_CHECK(hipIpcCloseMemHandle(d_ptr));
+  return TW_OK;
+}
+
+// per-step form: this rank's `words` partial words (rows shard_base.. of the global order,
+// d columns) into every rank's per-step slot of parity `par`, arrivals added
+extern "C" int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t offset_words,
+                               void* const* d_peer_bases, int32_t G, int32_t rank,
+                               int32_t n_total, int64_t d, int32_t par, void* stream) {
+  TW_ARG_CHECK(d_peer_bases != nullptr && G >= 1 && G <= kPeerMax && rank >= 0 && rank < G &&
+                   n_total >= 1 && d >= 1 && words >= 1 && offset_words >= 0 &&
+                   offset_words + words <= (int64_t)n_total * d && (par == 0 || par == 1),
+               "tw_peer_publish: bad sizes");
+  PeerSeg ps{};
+  const size_t step_slots = kPeerHdr + sizeof(double) * peer_slots_words(n_total, d);
+  for (int p = 0; p < G; ++p) {
+    char* b = (char*)d_peer_bases[p];
+    TW_ARG_CHECK(b != nullptr, "tw_peer_publish: rank %d's buffer missing", p);
+    ps.slot[p] = (double*)(b + step_slots);
+    ps.ctr[p] = (unsigned long long*)(b + kPeerStepCtr + 64 * par);
+  }
+  ps.G = G;
+  ps.n_total = (int)((int64_t)n_total * d);  // one slot's words
+  auto* reset = (unsigned long long*)((char*)d_peer_bases[rank] + kPeerStepCtr + 64 * (1 - par));
+  hipLaunchKernelGGL(k_peer_publish, dim3(publish_blocks(words)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_grads_loc, words, offset_words, ps, par, reset);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+// per-step form: wait until every rank's publish of parity `par` is in (G ranks of
+// `words_per_rank` words each), then k_sgd_update on the slot
+extern "C" int tw_peer_update(double* d_w, double* d_dw, void* d_my_base, int32_t n_total,
+                              int64_t d, int64_t words_per_rank, int32_t G, int32_t par,
+                              double reg, double lr, double momentum, uint64_t* d_step,
+                              uint32_t* d_abort, void* stream) {
+  TW_ARG_CHECK(d_w && d_dw && d_my_base && d_abort && n_total >= 1 && d >= 1 && G >= 1 &&
+                   words_per_rank >= 1 && (par == 0 || par == 1),
+               "tw_peer_update: bad arguments");
+  char* b = (char*)d_my_base;
+  const size_t step_slots = kPeerHdr + sizeof(double) * peer_slots_words(n_total, d);
+  const double* slot = (const double*)(b + step_slots) + (size_t)par * n_total * d;
+  const auto* ctr = (const unsigned long long*)(b + kPeerStepCtr + 64 * par);
+  const uint64_t target = (uint64_t)publish_blocks(words_per_rank) * (uint64_t)G;
+  hipLaunchKernelGGL(k_peer_update, dim3((unsigned)ceil_div(d, (int64_t)kPUpdCols)), dim3(kBlock),
+                     0, (hipStream_t)stream, d_w, d_dw, slot, ctr, target, n_total, d, reg, lr,
+                     momentum, d_step, d_abort);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}

@@ -1,70 +1,35 @@
-// sgdseg.hip — a whole segment of SGD steps in ONE persistent launch (SURVEY.md §8 rows L1/L2,
-// wide rows 32 < d <= 512: the C5 shape d = 512, N = 256).
+// sgdseg.hip — a whole segment of SGD steps in ONE persistent launch (SURVEY.md §8 rows L1/L2;
+// narrow rows d <= 32: the C4 shuttle shape d = 10, N = 100).
 //
 //   for it in segment:                                    learning-experiment/make_exps.py:126-141
 //       grads = [grad_inc_block(w, B, margin) per shard]  compute_stats.py:146-162
 //       g = mean(grads, axis=0) + reg*w; dw = momentum*dw + lr*g (SGD: lr*g); w -= dw
 //
-// Launch-per-step (k_hinge_grad_stream + k_sgd_update) pays, every step, two kernel
-// boundaries, the update kernel's own latency chain and the gradient's ramp (the first rows of
-// every shard are requested only after the draws and the row tables resolve).  Here the grid is
-// one block per CU (LDS 159 KiB => 1 block/CU, grid <= resident capacity, blocks loop over
-// shards when N exceeds it) and every step is:
-//   1. wait for barrier 2k (w of step k published), read w;
-//   2. the block's shards, exactly as k_hinge_grad_stream: same chunking, same lane partials +
-//      butterfly per pair, column sums in pair order from +0.0 — identical bits;
-//   3. publish the shard gradients, arrive at barrier 2k+1;
-//   4. PREFETCH: draws, row tables and the first two chunks' rows of step k+1's first shard are
-//      issued now — they are independent of w, so they stream while the other blocks arrive;
-//      the two chunks land as diff rows in LDS (the dot products wait for w);
-//   5. wait for barrier 2k+1, update this block's columns [b*d/G, (b+1)*d/G) — shard-order sum
-//      from +0.0, /N, + reg*w, momentum: k_sgd_update's arithmetic — publish w, dw, arrive at
-//      barrier 2k+2.
+// Launch-per-step (the gradient + update launches, or tw_sgd_step) pays a kernel boundary per
+// step against a C4 step of ~8 us.  Here one block per shard (all co-resident) runs the whole
+// segment with ONE grid barrier per step (k_sgd_segment_narrow below), and over ranks the same
+// kernel exchanges the shard gradients with the other ranks' kernels through IPC-mapped peer
+// buffers instead of a host collective (PEER, csrc/peer.h).  Wide rows (d > 32, C5) run per-step
+// launches: a wide persistent segment (grid barriers between gradient and update) measured
+// slower than the launches at C5 and was removed in round 5.
 //
 // Inter-block hand-offs (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup
-// visibility", table row 1): every handed-off word (grads, w, dw) is stored and loaded with
-// agent-scope relaxed atomics (global_store/load sc1: write-through, L1-bypassing, coherent
-// across the XCDs' L2s); each storing wave waits vmcnt(0), the block barriers, then ONE lane
-// adds to the monotonic arrival counter; one lane polls it with s_sleep, then a block barrier.
-// This is the guide's sc1-hand-off form (MI355X_MICROARCH.md "Valid forms", table row 1: every
-// handed-off byte stored AND loaded sc1, each storing wave's vmcnt(0) before the workgroup
-// barrier that precedes the one-lane agent-scope add, an sc1 poll, one workgroup per CU), so no
-// release fence on the add and no acquire on the poll: on gfx950 those lower to buffer_wbl2 sc1
-// / buffer_inv sc1 at ~1.7 us each (the guide's fence table), two hand-offs per step against a
-// C4 step of ~8 us.  Any new handed-off word must keep to ld_agent / st_agent below.
+// visibility"): every handed-off word is stored and loaded with agent-scope relaxed atomics
+// (global_store/load sc1), each storing wave waits vmcnt(0), the block barriers, then ONE lane
+// adds to the monotonic arrival counter (release), and the poller's one acquire fence follows
+// its relaxed poll (the contract is spelled out at seg_arrive / seg_poll below).  Any new
+// handed-off word must keep to ld_agent / st_agent.
 // Residency: a plain launch of <= occupancy x CUs blocks is co-resident on an otherwise idle GPU
 // (the learning loop runs on one stream); every spin is still bounded (2 s of the 100 MHz wall
 // clock): a block that times out raises the abort word, every other waiter sees it and exits,
 // and the caller finds ctl[1] != 0 afterwards (the segment's results are then invalid).
+#include "peer.h"
 #include "sgd_common.h"
 #include <algorithm>
-
-// Per-step timestamps for kernel studies (tools/phase_segment.py builds a separate library with
-// -DTW_SEG_TIMING; the product build compiles them out): thread 0 of block b stamps the 100 MHz
-// wall clock at point p of step k < 32 — 0 w read, 1 gradients stored, 4 their stores landed
-// (block barrier), 2 barrier 2k+1 passed, 5 the update's gradient loads landed, 3 update
-// stored, 6 its stores landed (counter add), 7 step start (before waiting for barrier 2k).
-#ifdef TW_SEG_TIMING
-__device__ unsigned long long g_seg_t[1 << 16];
-#define SEG_STAMP(k, p)                                                                     \
-  do {                                                                                      \
-    if (threadIdx.x == 0 && (k) < 32)                                                       \
-      g_seg_t[(((size_t)blockIdx.x * 32 + (k)) * 8 + (p)) & 0xFFFF] = wall_clock64();       \
-  } while (0)
-extern "C" int tw_debug_seg_times(unsigned long long* host, int n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_seg_t), sizeof(unsigned long long) * n) ==
-                 hipSuccess ? 0 : 2;
-}
-#else
-#define SEG_STAMP(k, p) \
-  do {                  \
-  } while (0)
-#endif
 
 namespace tw {
 
 constexpr uint64_t kSegSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-constexpr int kSegStage = 1408;                   // 11 KiB: LDS total 159.3 KiB
 
 __device__ __forceinline__ double ld_agent(const double* p) {
   const uint64_t v = __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED,
@@ -134,240 +99,25 @@ __device__ __forceinline__ bool seg_wait(uint32_t* ctl, uint32_t target, int* s_
   return *s_ok != 0;
 }
 
-// FULL: d == 512 (every lane column valid: no per-column masks, fewer live SGPR masks)
-template <int LOSS, bool FULL>
-__global__ __launch_bounds__(kWideBlock) void k_sgd_segment_wide(
-    const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
-    const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
-    int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz,
-    int64_t draw_stride, int n_shards, int64_t B, double margin, uint64_t seed,
-    uint64_t* d_step, uint32_t shard_base, int nsteps, double* w, double* dw, double* grads,
-    double reg, double lr, double momentum, uint32_t* ctl, int prefetch_rows) {
-  __shared__ double diff[2][kStreamCH * kWideMaxD];  // 128 KiB
-  __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
-  __shared__ double flag[2][kStreamCH];
-  __shared__ double stage[kSegStage];                 // the update's shard-gradient staging
-  __shared__ double wsh[kWideMaxD];                   // w of the current step
-  __shared__ int s_ok;
-  const int G = gridDim.x, blk = blockIdx.x, tid = threadIdx.x;
-  const int lane = tid & (kWave - 1), wid = tid / kWave;
-  const int dd = FULL ? kWideMaxD : (int)d;
-  const uint64_t step0 = d_step ? *d_step : 0;
-  const int cA = (int)((int64_t)blk * dd / G), cB = (int)((int64_t)(blk + 1) * dd / G);
-  double zv[2][kWideCols], xv[2][kWideCols];
-  double acc = 0.0;  // thread j < d: column j of the current shard
-
-  // pair rows of phase [P0, P0 + np) of shard s at step k -> prx/prz (as k_hinge_grad_stream)
-  // absolute X / Z rows of pair b of shard s at step k (draw, then the SWR row tables)
-  auto pair_rows = [&](int s, int k, int64_t b, int64_t& rx, int64_t& rz) {
-    int64_t ax, az;
-    if (ix) {
-      ax = ix[(int64_t)k * draw_stride + (int64_t)s * B + b];
-      az = iz[(int64_t)k * draw_stride + (int64_t)s * B + b];
-    } else {
-      const u32x4 r = sgd_draw(seed, step0 + (uint64_t)k, (uint32_t)b, shard_base + (uint32_t)s,
-                               kTagPairs);
-      ax = (int64_t)mulhi_u64(((uint64_t)r.b << 32) | r.a, (uint64_t)kx);
-      az = (int64_t)mulhi_u64(((uint64_t)r.d << 32) | r.c, (uint64_t)kz);
-    }
-    rx = rows_x ? rows_x[(int64_t)s * kx + ax] : ax;
-    rz = rows_z ? rows_z[(int64_t)s * kz + az] : az;
-  };
-  // rows of phase [P0, P0 + np) of shard s at step k -> prx/prz, threads t0, t0 + ts, ...
-  auto setup = [&](int s, int k, int64_t P0, int np, int t0, int ts) {
-    for (int t = t0; t < np; t += ts) pair_rows(s, k, P0 + t, prx[t], prz[t]);
-  };
-  auto load = [&](int st, int c0, int np) {  // this wave's pair of the chunk at c0 -> stage st
-    const int t = c0 + wid;
-    if (t < np) {
-      const double* zr = Z + prz[t] * d;
-      const double* xr = X + prx[t] * d;
-#pragma unroll
-      for (int c = 0; c < kWideCols; ++c) {
-        const int j = lane + c * kWave;
-        zv[st][c] = (FULL || j < dd) ? zr[j] : 0.0;
-        xv[st][c] = (FULL || j < dd) ? xr[j] : 0.0;
-      }
-    }
-  };
-  // from_lds: the chunk's diff rows were written by the prefetch (same v, same order: bits)
-  auto chunk = [&](int st, int c0, int np, bool from_lds) {
-    const int nb = std::min(kStreamCH, np - c0);
-    if (wid < nb) {
-      double part = 0.0;
-      if (from_lds) {
-#pragma unroll
-        for (int c = 0; c < kWideCols; ++c) {
-          const int j = lane + c * kWave;
-          if (FULL || j < dd) part += diff[st][wid * dd + j] * wsh[j];
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < kWideCols; ++c) {
-          const int j = lane + c * kWave;
-          if (FULL || j < dd) {
-            const double v = zv[st][c] - xv[st][c];
-            diff[st][wid * dd + j] = v;
-            part += v * wsh[j];
-          }
-        }
-      }
-      part = wave_sum_dpp_f64(part);
-      if (lane == 0) flag[st][wid] = pair_weight<LOSS>(part + margin);
-    }
-    if (c0 + 2 * kStreamCH < np) load(st, c0 + 2 * kStreamCH, np);  // refill: chunk k+2
-    __syncthreads();
-    if (tid < dd) {
-      double a = acc;
-      int u0 = 0;
-      for (; u0 + 8 <= nb; u0 += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = weighted<LOSS>(flag[st][u0 + u], diff[st][(u0 + u) * dd + tid]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a += v[u];
-      }
-      for (; u0 < nb; ++u0) a += weighted<LOSS>(flag[st][u0], diff[st][u0 * dd + tid]);
-      acc = a;
-    }
-  };
-
-  bool pre = false;       // step k's first shard: phase 0's row indices already in prx/prz
-  bool pre_rows = false;  // ... and chunks 0/1 already as diff rows in LDS
-  for (int k = 0; k < nsteps; ++k) {
-    SEG_STAMP(k, 7);
-    if (k > 0 && !seg_wait(ctl, (uint32_t)(2 * k) * (uint32_t)G, &s_ok)) return;
-    if (tid < dd) wsh[tid] = ld_agent(w + tid);
-    __syncthreads();
-    SEG_STAMP(k, 0);
-    for (int s = blk; s < n_shards; s += G) {
-      acc = 0.0;
-      for (int64_t P0 = 0; P0 < B; P0 += kIdxPhase) {
-        const int np = (int)std::min<int64_t>(kIdxPhase, B - P0);
-        const bool lds0 = pre_rows && P0 == 0;
-        if (!(pre && P0 == 0)) {
-          __syncthreads();  // the previous phase's readers of prx/prz and diff/flag are done
-          setup(s, k, P0, np, tid, kWideBlock);
-          __syncthreads();
-        }
-        if (!lds0) {
-          load(0, 0, np);
-          if (kStreamCH < np) load(1, kStreamCH, np);
-        }
-        int c0 = 0;
-        for (; c0 + kStreamCH < np; c0 += 2 * kStreamCH) {
-          chunk(0, c0, np, lds0 && c0 == 0);
-          chunk(1, c0 + kStreamCH, np, lds0 && c0 == 0);
-        }
-        if (c0 < np) chunk(0, c0, np, lds0 && c0 == 0);
-        pre = pre_rows = false;
-      }
-      if (tid < dd) st_agent(grads + (int64_t)s * d + tid, acc / (double)B);
-    }
-    SEG_STAMP(k, 1);
-    seg_arrive(ctl);  // barrier 2k+1: every shard gradient of step k published
-    SEG_STAMP(k, 4);
-    const bool more = k + 1 < nsteps;
-    if (wid == 0) {
-      // control wave: waits for barrier 2k+1, updates columns [cA, cB), arrives at 2k+2.  It
-      // has no loads in flight, so nothing queues in front of its polls and loads.
-      int ok = 1;
-      if (lane == 0) ok = seg_poll(ctl, (uint32_t)(2 * k + 1) * (uint32_t)G) ? 1 : 0;
-      ok = __shfl(ok, 0, kWave);
-      SEG_STAMP(k, 2);
-      for (int g0 = cA; ok && g0 < cB; g0 += kWave) {  // column groups of <= 64 lanes
-        const int nc = std::min(kWave, cB - g0);
-        double wj = 0.0, dwj = 0.0;
-        if (lane < nc) {
-          wj = ld_agent(w + g0 + lane);
-          if (momentum >= 0.0) dwj = ld_agent(dw + g0 + lane);
-        }
-        const int SS = kSegStage / nc;  // shards staged per pass
-        double sum = 0.0;               // lane c < nc: column g0 + c, shard order from +0.0
-        for (int s0 = 0; s0 < n_shards; s0 += SS) {
-          const int ns = std::min(SS, n_shards - s0), tot = ns * nc;
-          for (int e0 = 0; e0 < tot; e0 += 8 * kWave) {  // 8 loads in flight per lane
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int e = e0 + u * kWave + lane, r = e / nc;
-              v[u] = e < tot ? ld_agent(grads + (int64_t)(s0 + r) * d + g0 + (e - r * nc)) : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int e = e0 + u * kWave + lane;
-              if (e < tot) stage[e] = v[u];
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-          SEG_STAMP(k, 5);
-          if (lane < nc) {
-            int r = 0;
-            for (; r + 8 <= ns; r += 8) {
-              double v[8];
-#pragma unroll
-              for (int u = 0; u < 8; ++u) v[u] = stage[(r + u) * nc + lane];
-#pragma unroll
-              for (int u = 0; u < 8; ++u) sum += v[u];
-            }
-            for (; r < ns; ++r) sum += stage[r * nc + lane];
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-        if (lane < nc) {
-          const double g = sum / (double)n_shards + reg * wj;
-          const double stp = momentum >= 0.0 ? momentum * dwj + lr * g : lr * g;
-          st_agent(dw + g0 + lane, stp);
-          st_agent(w + g0 + lane, wj - stp);
-        }
-      }
-      SEG_STAMP(k, 3);
-      if (ok) {  // barrier 2k+2: this wave's w and dw stores landed (the only stores it signals)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        SEG_STAMP(k, 6);
-        if (lane == 0)
-          __hip_atomic_fetch_add(ctl, 1u, TW_SEG_BARRIER ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-        if (!more && blk == 0 && lane == 0 && d_step) *d_step = step0 + (uint64_t)nsteps;
-      }
-    } else if (more && prefetch_rows) {
-      // waves 1..15 prefetch step k+1's first shard: the 32 pairs of chunks 0 and 1 as diff
-      // rows in LDS (wave w: pairs w-1, w+14, w+29), then phase 0's row indices (prx/prz free:
-      // seg_arrive's barrier follows their last reads)
-      const int np = (int)std::min<int64_t>(kIdxPhase, B);
-      const int npre = std::min(np, 2 * kStreamCH);
-      for (int t1 = wid - 1; t1 < npre; t1 += 2 * (kStreamCH - 1)) {
-        const int t2 = t1 + (kStreamCH - 1);
-        int64_t rx1, rz1, rx2 = 0, rz2 = 0;
-        pair_rows(blk, k + 1, t1, rx1, rz1);
-        if (t2 < npre) pair_rows(blk, k + 1, t2, rx2, rz2);
-#pragma unroll
-        for (int c = 0; c < kWideCols; ++c) {
-          const int j = lane + c * kWave;
-          const bool in = FULL || j < dd;
-          zv[0][c] = in ? Z[rz1 * d + j] : 0.0;
-          xv[0][c] = in ? X[rx1 * d + j] : 0.0;
-          zv[1][c] = (in && t2 < npre) ? Z[rz2 * d + j] : 0.0;
-          xv[1][c] = (in && t2 < npre) ? X[rx2 * d + j] : 0.0;
-        }
-#pragma unroll
-        for (int c = 0; c < kWideCols; ++c) {
-          const int j = lane + c * kWave;
-          if (FULL || j < dd) {
-            diff[t1 / kStreamCH][(t1 % kStreamCH) * dd + j] = zv[0][c] - xv[0][c];
-            if (t2 < npre) diff[t2 / kStreamCH][(t2 % kStreamCH) * dd + j] = zv[1][c] - xv[1][c];
-          }
-        }
-      }
-      setup(blk, k + 1, 0, np, tid - kWave, kWideBlock - kWave);
-    } else if (more) {  // indices only: the rows stream once w is known
-      setup(blk, k + 1, 0, (int)std::min<int64_t>(kIdxPhase, B), tid - kWave,
-            kWideBlock - kWave);
-    }
-    pre = more;
-    pre_rows = more && prefetch_rows;
-  }
-}
+// ---- peers: the narrow segment over ranks (round 5) ----------------------------------------
+// With several ranks (one process per GPU) the shard gradients of a step are exchanged IN the
+// persistent launch instead of by a host-enqueued RCCL all-gather between two launches: every
+// rank owns one peer buffer (csrc/peer.hip: device memory allocated uncached, mapped into every
+// other rank through an IPC handle), and each block pushes its shard's d gradient words into
+// EVERY rank's slot for the step (global shard order), then adds one arrival to every rank's
+// counter.  A rank's blocks wait until its own counter shows all n_total shards of the step
+// (the ranks' blocks together), read the n_total x d slot from their own memory and apply the
+// same shard-ordered update as the one-process kernel: the trajectory is the one-GPU one, bit
+// for bit.  Memory model across devices: every handed-off word (gradient words, counters) is
+// stored and loaded with SYSTEM-scope relaxed atomics on uncached memory (sc0 sc1: no cache of
+// any device keeps a line), each storing wave waits vmcnt(0) before the workgroup barrier that
+// precedes its block's counter adds, and the consumer loads only after its poll has matched
+// (the system-scope analogue of the guide's sc1 hand-off form, table row 1).
+// Slots: step e (global, counted from the rank's epoch) writes slot e & 1; a block writes it
+// on rank p only after its own counter showed every block's arrival for step e - 1, i.e. after
+// every block of every rank finished reading slot (e - 2) & 1 — two slots suffice, also across
+// launches (the epoch word continues the parity).  Counters are monotonic (64-bit): the wait
+// of step e is arrivals >= (e + 1) * n_total.
 
 // ---- narrow rows (d <= 32, C4): a segment of k_sgd_step_narrow steps in ONE launch --------
 // One block per shard (all co-resident), ONE grid barrier per step: the update is recomputed
@@ -395,7 +145,7 @@ struct TabSteps {
   uint64_t phase, mod;
 };
 
-template <int LOSS>
+template <int LOSS, bool PEER>
 __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
@@ -405,16 +155,23 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     const double* __restrict__ w_in, const double* __restrict__ dw_in, double reg, double lr,
     double momentum, double* grads0, double* grads1, double* __restrict__ w_out,
     double* __restrict__ dw_out, uint32_t* ctl, int64_t n_X, int64_t n_Z, uint64_t swr_mod,
-    uint64_t swr_base, TabSteps tab) {
+    uint64_t swr_base, TabSteps tab, PeerSeg ps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* diff = (double*)smem;         // B * d
   double* flag = diff + B * d;          // B pair weights
   double* wsh = flag + B;               // kNarrowMaxD: this step's w
-  double* gt = wsh + kNarrowMaxD;       // n_shards * d: the previous step's shard gradients
+  double* gt = wsh + kNarrowMaxD;       // n_shards * d (peers: n_total * d): the previous
+                                        // step's shard gradients
   __shared__ int s_ok;
   const int s = blockIdx.x, tid = threadIdx.x, dd = (int)d, G = gridDim.x;
-  const int ng = n_shards * dd;
+  // the shards of the update: this launch's blocks, or every rank's (peers)
+  const int n_upd = PEER ? ps.n_total : n_shards;
+  const int ng = n_upd * dd;
   const uint64_t step0 = d_step ? *d_step : 0;
+  // peers: the global step count before this launch (steps done by earlier peer launches)
+  const uint64_t ep = PEER ? __hip_atomic_load(ps.epoch, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) : 0;
+  const size_t slot_words = (size_t)ps.n_total * dd;
   double wj = 0.0, dwj = 0.0;  // thread tid < d: column tid of w and dw
   if (tid < dd) {
     wj = w_in[tid];
@@ -461,22 +218,30 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     }
     // 2. the previous step's update, once every block has published its gradients
     if (k > 0) {
-      if (!seg_wait(ctl, (uint32_t)k * (uint32_t)G, &s_ok)) return;
-      const double* gin = ((k - 1) & 1) ? grads1 : grads0;
-      for (int e = tid; e < ng; e += kBlock) gt[e] = ld_agent(gin + e);
+      if constexpr (PEER) {
+        // every rank's blocks have pushed step ep + k - 1 into this rank's slot
+        if (!peer_wait(ps.my_ctr, (ep + (uint64_t)k) * (uint64_t)ps.n_total, ctl + 1, &s_ok))
+          return;
+        const double* gin = ps.my_slot + ((ep + (uint64_t)k - 1) & 1) * slot_words;
+        for (int e = tid; e < ng; e += kBlock) gt[e] = ld_sys(gin + e);
+      } else {
+        if (!seg_wait(ctl, (uint32_t)k * (uint32_t)G, &s_ok)) return;
+        const double* gin = ((k - 1) & 1) ? grads1 : grads0;
+        for (int e = tid; e < ng; e += kBlock) gt[e] = ld_agent(gin + e);
+      }
       __syncthreads();
       if (tid < dd) {
         double sum = 0.0;  // shard order, as np.mean(axis=0) / k_sgd_update
         int r = 0;
-        for (; r + 8 <= n_shards; r += 8) {
+        for (; r + 8 <= n_upd; r += 8) {
           double v[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] = gt[(r + u) * dd + tid];
 #pragma unroll
           for (int u = 0; u < 8; ++u) sum += v[u];
         }
-        for (; r < n_shards; ++r) sum += gt[r * dd + tid];
-        const double g = sum / (double)n_shards + reg * wj;
+        for (; r < n_upd; ++r) sum += gt[r * dd + tid];
+        const double g = sum / (double)n_upd + reg * wj;
         const double st = momentum >= 0.0 ? momentum * dwj + lr * g : lr * g;
         wj = wj - st;
         dwj = st;
@@ -503,10 +268,58 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
         for (int u = 0; u < 8; ++u) a += v[u];
       }
       for (; t < B; ++t) a += weighted<LOSS>(flag[t], diff[t * dd + tid]);
-      st_agent(((k & 1) ? grads1 : grads0) + (int64_t)s * d + tid, a / (double)B);
+      if constexpr (PEER) {
+        // this shard's row of step ep + k into every rank's slot (global shard order)
+        const size_t o = ((ep + (uint64_t)k) & 1) * slot_words +
+                         (size_t)(shard_base + (uint32_t)s) * dd + tid;
+        for (int p = 0; p < ps.G; ++p) st_sys(ps.slot[p] + o, a / (double)B);
+      } else {
+        st_agent(((k & 1) ? grads1 : grads0) + (int64_t)s * d + tid, a / (double)B);
+      }
     }
-    seg_arrive(ctl, B <= kBlock - kWave ? kBlock - kWave : 0);  // also: every thread is done
-                                                                // with diff / flag / gt
+    if constexpr (PEER) {
+      // every storing wave's stores performed, then one lane per rank adds this block's
+      // arrival (the barrier also ends every thread's use of diff / flag / gt)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid < ps.G)
+        __hip_atomic_fetch_add(ps.ctr[tid], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      seg_arrive(ctl, B <= kBlock - kWave ? kBlock - kWave : 0);  // also: every thread is done
+                                                                  // with diff / flag / gt
+    }
+  }
+  if constexpr (PEER) {
+    // the last step's update in the launch (block 0): w_out / dw_out, the epoch, the step
+    // counter — every block of this launch has read epoch and step counter long before
+    if (s == 0 && nsteps > 0) {
+      const uint64_t e = ep + (uint64_t)nsteps;
+      if (!peer_wait(ps.my_ctr, e * (uint64_t)ps.n_total, ctl + 1, &s_ok)) return;
+      const double* gin = ps.my_slot + ((e - 1) & 1) * slot_words;
+      for (int i = tid; i < ng; i += kBlock) gt[i] = ld_sys(gin + i);
+      __syncthreads();
+      if (tid < dd) {
+        double sum = 0.0;
+        int r = 0;
+        for (; r + 8 <= n_upd; r += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = gt[(r + u) * dd + tid];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sum += v[u];
+        }
+        for (; r < n_upd; ++r) sum += gt[r * dd + tid];
+        const double g = sum / (double)n_upd + reg * wj;
+        const double st = momentum >= 0.0 ? momentum * dwj + lr * g : lr * g;
+        w_out[tid] = wj - st;
+        dw_out[tid] = st;
+      }
+      if (tid == 0) {
+        __hip_atomic_store(ps.epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d_step) *(uint64_t*)d_step = step0 + (uint64_t)nsteps;
+      }
+    }
+    return;
   }
   if (s == 0) {
     if (tid < dd) {
@@ -518,25 +331,6 @@ __global__ __launch_bounds__(kBlock) void k_sgd_segment_narrow(
     if (nsteps > 0 && seg_wait(ctl, (uint32_t)nsteps * (uint32_t)G, &s_ok) && tid == 0)
       __hip_atomic_store(ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-static int g_seg_grid = 0;      // tw_sgd_segment_set_grid: 0 = resident capacity
-static int g_seg_prefetch = 1;  // tw_sgd_segment_set_prefetch: 1 = rows, 0 = indices only
-
-static int seg_capacity() {
-  static int cap[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cap[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, k_sgd_segment_wide<TW_LOSS_HINGE, false>, kWideBlock, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 0;
-    // 145 KiB of LDS per block: one per CU (never trust more than that here)
-    cap[dev] = std::min(per_cu, 1) * cus;
-  }
-  return cap[dev];
 }
 
 }  // namespace tw
@@ -554,7 +348,8 @@ extern "C" int tw_sgd_segment_narrow_ok(int64_t d, int32_t n_shards, int64_t B) 
     return 0;
   int dev = 0, per_cu = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_segment_narrow<TW_LOSS_HINGE>,
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
+                                                   k_sgd_segment_narrow<TW_LOSS_HINGE, false>,
                                                    kBlock, narrow_lds(d, n_shards, B)) !=
           hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
@@ -573,7 +368,8 @@ static int segment_narrow(const double* d_X, const double* d_Z, int64_t d,
                           const double* d_dw_in, double reg, double lr, double momentum,
                           double* d_grads0, double* d_grads1, double* d_w_out, double* d_dw_out,
                           uint32_t* d_ctl, int64_t n_X, int64_t n_Z, uint64_t swr_mod,
-                          uint64_t swr_base, void* stream, TabSteps tab = TabSteps{0, 0, 0, 0}) {
+                          uint64_t swr_base, void* stream, TabSteps tab = TabSteps{0, 0, 0, 0},
+                          const PeerSeg* peer = nullptr) {
   // shape limits only: the residency query (tw_sgd_segment_narrow_ok) is a HIP API call the
   // caller makes once, before any stream capture — this entry runs inside captured graphs
   TW_ARG_CHECK(d >= 1 && d <= kNarrowMaxD && n_shards >= 1 &&
@@ -589,20 +385,31 @@ static int segment_narrow(const double* d_X, const double* d_Z, int64_t d,
   TW_ARG_CHECK(d_w_in && d_dw_in && d_grads0 && d_grads1 && d_w_out && d_dw_out && d_ctl,
                "tw_sgd_segment_narrow: w, dw, both gradient slots, outputs and ctl required");
   TW_ARG_CHECK(loss == TW_LOSS_HINGE || loss == TW_LOSS_LOGISTIC, "unknown loss %d", loss);
+  if (peer)
+    TW_ARG_CHECK(peer->n_total >= n_shards && (int64_t)peer->n_total * d <= kNarrowMaxGrads &&
+                     narrow_lds(d, peer->n_total, B) <= 64 * 1024,
+                 "tw_sgd_segment_narrow_peer: %d shards in all unsupported", peer->n_total);
   if (nsteps == 0) return TW_OK;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = narrow_lds(d, n_shards, B);
+  const size_t lds = narrow_lds(d, peer ? peer->n_total : n_shards, B);
+  const PeerSeg ps = peer ? *peer : PeerSeg{};
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(n_shards), dim3(kBlock), lds, st, d_X, d_Z, d, d_rows_x, kx,
                        d_rows_z, kz, d_ix, d_iz, draw_stride, B, margin, seed, d_step,
                        (uint32_t)shard_base, (int)n_shards, (int)nsteps, d_w_in, d_dw_in, reg,
                        lr, momentum, d_grads0, d_grads1, d_w_out, d_dw_out, d_ctl, n_X, n_Z,
-                       swr_mod, swr_base, tab);
+                       swr_mod, swr_base, tab, ps);
   };
-  if (loss == TW_LOSS_LOGISTIC)
-    go(k_sgd_segment_narrow<TW_LOSS_LOGISTIC>);
-  else
-    go(k_sgd_segment_narrow<TW_LOSS_HINGE>);
+  if (peer) {
+    if (loss == TW_LOSS_LOGISTIC)
+      go(k_sgd_segment_narrow<TW_LOSS_LOGISTIC, true>);
+    else
+      go(k_sgd_segment_narrow<TW_LOSS_HINGE, true>);
+  } else if (loss == TW_LOSS_LOGISTIC) {
+    go(k_sgd_segment_narrow<TW_LOSS_LOGISTIC, false>);
+  } else {
+    go(k_sgd_segment_narrow<TW_LOSS_HINGE, false>);
+  }
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -660,58 +467,52 @@ extern "C" int tw_sgd_segment_narrow_swr(const double* d_X, const double* d_Z, i
                         (uint64_t)swr_mod, swr_base, stream);
 }
 
-extern "C" int tw_sgd_segment_ok(int64_t d, int32_t n_shards) {
-  return d > 32 && d <= kWideMaxD && n_shards >= 1;
-}
-
-extern "C" int tw_sgd_segment_set_grid(int32_t max_blocks) {
-  TW_ARG_CHECK(max_blocks >= 0, "tw_sgd_segment_set_grid: max_blocks < 0");
-  g_seg_grid = max_blocks;
+// The narrow persistent segment over ranks (round 5; csrc/peer.h): the local shards
+// [shard_base, shard_base + n_shards) of n_total, their gradients pushed into every rank's
+// peer buffer (d_peer_bases: G device addresses in rank order — this rank's own buffer and
+// the IPC-mapped ones of the others), the update of every step from this rank's own slot, the
+// last one in the launch (w / dw in place; d_step advanced by nsteps when given).
+static int peer_seg_of(void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total,
+                       int64_t d, PeerSeg& ps) {
+  TW_ARG_CHECK(d_peer_bases != nullptr && G >= 1 && G <= kPeerMax && rank >= 0 && rank < G &&
+                   n_total >= 1,
+               "peer segment: bad ranks (G=%d, rank=%d, at most %d ranks)", G, rank, kPeerMax);
+  ps = PeerSeg{};
+  for (int p = 0; p < G; ++p) {
+    char* b = (char*)d_peer_bases[p];
+    TW_ARG_CHECK(b != nullptr, "peer segment: rank %d's buffer missing", p);
+    ps.slot[p] = (double*)(b + kPeerHdr);
+    ps.ctr[p] = (unsigned long long*)(b + kPeerSegCtr);
+  }
+  char* mine = (char*)d_peer_bases[rank];
+  ps.my_ctr = (unsigned long long*)(mine + kPeerSegCtr);
+  ps.epoch = (unsigned long long*)(mine + kPeerEpoch);
+  ps.my_slot = (const double*)(mine + kPeerHdr);
+  ps.G = G;
+  ps.n_total = n_total;
   return TW_OK;
 }
 
-extern "C" int tw_sgd_segment_set_prefetch(int32_t rows) {
-  TW_ARG_CHECK(rows == 0 || rows == 1, "tw_sgd_segment_set_prefetch: 0 or 1");
-  g_seg_prefetch = rows;
-  return TW_OK;
-}
-
-extern "C" int tw_sgd_segment(const double* d_X, const double* d_Z, int64_t d,
-                              const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z,
-                              int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
-                              int64_t draw_stride, int32_t n_shards, int64_t B, double margin,
-                              int32_t loss, uint64_t seed, uint64_t* d_step, int32_t shard_base,
-                              int32_t nsteps, double* d_w, double* d_dw, double* d_grads,
-                              double reg, double lr, double momentum, uint32_t* d_ctl,
-                              void* stream) {
-  TW_ARG_CHECK(tw_sgd_segment_ok(d, n_shards), "tw_sgd_segment: d=%lld, n_shards=%d unsupported",
-               (long long)d, n_shards);
-  TW_ARG_CHECK(B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1 && shard_base >= 0 &&
-                   nsteps >= 0 && nsteps <= (1 << 20) && draw_stride >= 0,
-               "tw_sgd_segment: bad B/kx/kz/shard_base/nsteps/draw_stride");
-  TW_ARG_CHECK((d_ix == nullptr) == (d_iz == nullptr), "tw_sgd_segment: ix and iz go together");
-  TW_ARG_CHECK(d_ix != nullptr || d_step != nullptr, "tw_sgd_segment: device draws need d_step");
-  TW_ARG_CHECK(d_w && d_dw && d_grads && d_ctl, "tw_sgd_segment: w, dw, grads, ctl required");
-  TW_ARG_CHECK(loss == TW_LOSS_HINGE || loss == TW_LOSS_LOGISTIC, "unknown loss %d", loss);
-  if (nsteps == 0) return TW_OK;
-  const int cap = seg_capacity();
-  TW_ARG_CHECK(cap >= 1, "tw_sgd_segment: no resident capacity for the segment kernel");
-  int grid = std::min(n_shards, cap);
-  if (g_seg_grid > 0) grid = std::min(grid, g_seg_grid);
-  hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(tw_zero_async(d_ctl, 0, sizeof(uint32_t), st));  // the arrival counter only
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWideBlock), 0, st, d_X, d_Z, d, d_rows_x, kx,
-                       d_rows_z, kz, d_ix, d_iz, draw_stride, (int)n_shards, B, margin, seed,
-                       d_step, (uint32_t)shard_base, (int)nsteps, d_w, d_dw, d_grads, reg, lr,
-                       momentum, d_ctl, g_seg_prefetch);
-  };
-  const bool full = d == kWideMaxD;
-  if (loss == TW_LOSS_LOGISTIC)
-    full ? go(k_sgd_segment_wide<TW_LOSS_LOGISTIC, true>)
-         : go(k_sgd_segment_wide<TW_LOSS_LOGISTIC, false>);
-  else
-    full ? go(k_sgd_segment_wide<TW_LOSS_HINGE, true>) : go(k_sgd_segment_wide<TW_LOSS_HINGE, false>);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
+extern "C" int tw_sgd_segment_narrow_peer(
+    const double* d_X, const double* d_Z, int64_t d, const int64_t* d_rows_x, int64_t kx,
+    const int64_t* d_rows_z, int64_t kz, const int64_t* d_ix, const int64_t* d_iz,
+    int64_t draw_stride, int32_t n_shards, int64_t B, double margin, int32_t loss,
+    uint64_t seed, uint64_t* d_step, int32_t shard_base, int32_t nsteps, int64_t n_X,
+    int64_t n_Z, int64_t swr_mod, double* d_w, double* d_dw, double reg, double lr,
+    double momentum, uint32_t* d_ctl, void* const* d_peer_bases, int32_t G, int32_t rank,
+    int32_t n_total, void* stream) {
+  PeerSeg ps;
+  if (const int rc = peer_seg_of(d_peer_bases, G, rank, n_total, d, ps)) return rc;
+  TW_ARG_CHECK(shard_base + n_shards <= n_total, "tw_sgd_segment_narrow_peer: shards past n_total");
+  TW_ARG_CHECK(swr_mod >= 0 && (swr_mod == 0 || (d_step != nullptr && n_X >= 1 && n_Z >= 1)),
+               "tw_sgd_segment_narrow_peer: swr_mod needs d_step, n_X, n_Z");
+  TW_ARG_CHECK(swr_mod > 0 || (d_rows_x != nullptr && d_rows_z != nullptr),
+               "tw_sgd_segment_narrow_peer: row tables or swr_mod");
+  // the gradient slots of the one-process kernel are not used: the peer slots replace them
+  return segment_narrow(d_X, d_Z, d, swr_mod ? nullptr : d_rows_x, kx,
+                        swr_mod ? nullptr : d_rows_z, kz, d_ix, d_iz, draw_stride, n_shards, B,
+                        margin, loss, seed, d_step, shard_base, nsteps, d_w, d_dw, reg, lr,
+                        momentum, d_w, d_w, d_w, d_dw, d_ctl, swr_mod ? n_X : 1,
+                        swr_mod ? n_Z : 1, (uint64_t)swr_mod, 0, stream, TabSteps{0, 0, 0, 0},
+                        &ps);
 }

@@ -65,7 +65,10 @@ NATIVE_DRAWS = True
 # reshuffles' SWR tables ride in the segment's upload, the kernel switches tables by step
 REPLAY_THROUGH = True
 PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each segment's draws
-SEGMENT_KERNEL = False  # wide rows: one persistent launch per segment (tw_sgd_segment); off: per-step launches are faster at C5
+# learning over ranks: the shard gradients exchanged by the GPUs through IPC-mapped peer buffers
+# (csrc/peer.hip: the persistent narrow segment, or per step a publish + wait-and-update launch)
+# instead of a host-enqueued RCCL all-gather per step; False keeps the all-gather (A/B)
+PEER_EXCHANGE = True
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
 SIZE_TRAIN_MONITOR = 450000
@@ -166,14 +169,16 @@ class SGDEngine:
         self.fused = (self.solo and not self.complete
                       and bool(L.lib().tw_sgd_step_fusable(self.d, self.N_loc)))
         self._slot1 = None
-        # wide rows on one GPU: a whole segment of steps in one persistent launch
-        # (tw_sgd_segment: grid barriers between the gradient and the update of every step)
-        self.segment = (SEGMENT_KERNEL and self.solo and not self.complete and not self.fused
-                        and bool(L.lib().tw_sgd_segment_ok(self.d, self.N_loc)))
         self.narrow_seg = (NARROW_SEGMENT and self.fused
                            and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N_loc, self.B)))
+        # over ranks: the device-resident gradient exchange (csrc/peer.hip), when every rank
+        # could map every other rank's peer buffer (else the per-step RCCL all-gather)
+        self.peer = _PeerBuffers.create(self) if self.coll and PEER_EXCHANGE else None
+        self._pstep = 0  # steps of the per-step peer exchange (its slot / counter parity)
+        self.peer_seg = (self.peer is not None and not self.complete
+                         and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N, self.B)))
         self._ctl = (t.zeros((2,), dtype=t.int32, device=self.w.device)
-                     if self.segment or self.narrow_seg else None)
+                     if self.narrow_seg or self.peer is not None else None)
 
     def reload(self, X, Z, w_init):
         """A new run on this engine (learning_process's engine cache): X, Z (host arrays of
@@ -189,27 +194,13 @@ class SGDEngine:
         if self._ctl is not None:
             self._ctl.zero_()
 
-    def _segment(self, nsteps: int, draws_dev=None):
-        """nsteps steps as ONE tw_sgd_segment launch (same bits as step()/step_device() +
-        _update() per step); draws_dev: the replay draws (S, 2, N, B) or None (device RNG)."""
-        ix = iz = None
-        stride = 0
-        if draws_dev is not None:
-            ix, iz = draws_dev[0, 0], draws_dev[0, 1]
-            stride = int(draws_dev.stride(0))
-        seed = getattr(self, "seed", 0) if draws_dev is None else 0
-        L.call("tw_sgd_segment", L.ptr(self.X), L.ptr(self.Z), self.d, L.ptr(self.rows_x),
-               self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix), L.ptr(iz), stride, self.N_loc,
-               self.B, self.margin, self.loss, seed, L.ptr(self.step_ctr), self.shard_base,
-               nsteps, L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.reg, self.lr,
-               self.momentum, L.ptr(self._ctl), L.stream_handle())
-
     def check(self):
-        """Raise if a persistent segment launch gave up waiting at a grid barrier (its bounded
-        spin expired: the blocks were not co-resident); the state is then invalid."""
+        """Raise if a persistent segment launch gave up waiting at a grid barrier, or a peer
+        wait of the exchange over ranks expired (its bounded spin: blocks not co-resident, or
+        a rank that stopped stepping); the state is then invalid."""
         if self._ctl is not None and int(self._ctl[1].item()) != 0:
-            raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
-                               "co-resident); the SGD state is invalid")
+            raise RuntimeError("SGD segment: a grid barrier or peer wait timed out (blocks not "
+                               "co-resident, or a rank stopped); the SGD state is invalid")
 
     def table_stacks(self, ntab: int):
         """Replay segments through reshuffles (tw_sgd_segment_narrow_tables): the row tables
@@ -456,9 +447,39 @@ class SGDEngine:
     def _update(self):
         if self.vgroup is not None:  # MultiDeviceSGD gathers the slots' gradients, then updates
             return
+        if self.peer is not None:
+            # publish this rank's partials into every rank's slot, wait for all, update
+            s, par = L.stream_handle(), self._pstep & 1
+            self._pstep += 1
+            nw = self.N_loc * self.d
+            L.call("tw_peer_publish", L.ptr(self.grads_loc), nw, self.shard_base * self.d,
+                   self.peer.bases, self.G, self.rank, self.N, self.d, par, s)
+            L.call("tw_peer_update", L.ptr(self.w), L.ptr(self.dw), self.peer.mine, self.N,
+                   self.d, nw, self.G, par, self.reg, self.lr, self.momentum,
+                   L.ptr(self.step_ctr), L.ptr(self._ctl[1:]), s)
+            return
         if self.coll:
             self.dist.all_gather_into_tensor(self.grads, self.grads_loc, group=self.group)
         self._apply_update()
+
+    def _peer_segment(self, nsteps: int, draws_dev=None, swr_mod: int = 0):
+        """nsteps steps over ranks as ONE persistent launch (tw_sgd_segment_narrow_peer): this
+        rank's shards, their gradients pushed into every rank's peer buffer in the launch, the
+        update (the last one included) applied from the rank's own — the one-GPU trajectory.
+        draws_dev: the replay draws (S, 2, N, B) of all shards, or None (device RNG)."""
+        ix = iz = None
+        stride = 0
+        if draws_dev is not None:
+            ix = draws_dev[0, 0, self.shard_base:]
+            iz = draws_dev[0, 1, self.shard_base:]
+            stride = int(draws_dev.stride(0))
+        seed = getattr(self, "seed", 0) if draws_dev is None else 0
+        L.call("tw_sgd_segment_narrow_peer", L.ptr(self.X), L.ptr(self.Z), self.d,
+               L.ptr(self.rows_x), self.kx, L.ptr(self.rows_z), self.kz, L.ptr(ix), L.ptr(iz),
+               stride, self.N_loc, self.B, self.margin, self.loss, seed, L.ptr(self.step_ctr),
+               self.shard_base, nsteps, self.n_X, self.n_Z, int(swr_mod), L.ptr(self.w),
+               L.ptr(self.dw), self.reg, self.lr, self.momentum, L.ptr(self._ctl),
+               self.peer.bases, self.G, self.rank, self.N, L.stream_handle())
 
     def _apply_update(self):
         L.call("tw_sgd_update", L.ptr(self.w), L.ptr(self.dw), L.ptr(self.grads), self.N,
@@ -518,8 +539,8 @@ class SGDEngine:
                 self.step(draws_dev[st, 0], draws_dev[st, 1])
 
         def steps():
-            if self.segment:
-                self._segment(nsteps, draws_dev)
+            if self.peer_seg:
+                self._peer_segment(nsteps, draws_dev)
             elif self.fused:
                 self._fused_steps(nsteps, draws_dev, tables=tables)
             else:
@@ -604,11 +625,14 @@ class SGDEngine:
         the incomplete gradient, and a kernel that draws the rows — the persistent narrow
         segment (nsteps > 1) or the per-step gradient launches of wide rows."""
         # (partitioned at G = 1: the partition is all of X and the tables are the draws)
+        if self.peer_seg and getattr(self, "seed", None) is not None:
+            # over ranks: the peer segment draws the rows itself (global rows: replicated X)
+            return self.layout == "replicated" or self.G == 1
         if getattr(self, "seed", None) is None or not self.solo or self.complete:
             return False
         if self.narrow_seg:
             return nsteps > 1
-        return not self.fused and not self.segment
+        return not self.fused
 
     def reshuffle_device(self, counter=None):
         """New SWR row tables from the device RNG at the current step counter, or at `counter`
@@ -663,6 +687,9 @@ class SGDEngine:
         t = self.t
         if swr_mod:
             assert self.swr_segments_ok(nsteps) and not reshuffle_first
+            if self.peer_seg:
+                self._peer_segment(nsteps, swr_mod=swr_mod)
+                return
             if self.fused and self._slot1 is None:
                 self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw),
                                t.empty_like(self.grads))
@@ -677,8 +704,8 @@ class SGDEngine:
             if swr_mod:
                 for _ in range(n):
                     self.step_device(swr_mod=swr_mod)
-            elif self.segment:
-                self._segment(n)
+            elif self.peer_seg:
+                self._peer_segment(n)
             elif self.fused:
                 self._fused_steps(n)
             else:
@@ -711,6 +738,72 @@ class SGDEngine:
             g.replay()
             nsteps -= n
             reshuffle_first = False
+
+
+class _PeerBuffers:
+    """This rank's peer buffer (csrc/peer.hip, tw_peer_alloc: counters and gradient slots of
+    the device-resident exchange) and every other rank's, mapped through IPC handles exchanged
+    once over the process group.  create() is collective: every rank learns whether all ranks
+    allocated and mapped their buffers, and all fall back to the RCCL all-gather together if
+    one could not."""
+
+    def __init__(self, mine, uncached, opened, bases):
+        self.mine = ctypes.c_void_p(mine)
+        self.uncached = uncached
+        self.opened = opened
+        self.bases = bases
+
+    @staticmethod
+    def create(eng):
+        dist, group, G, r = eng.dist, eng.group, eng.G, eng.rank
+        lib = L.lib()
+        mine, unc, handle = None, 0, None
+        try:
+            nb = int(lib.tw_peer_buffer_bytes(eng.N, eng.d))
+            p, u = ctypes.c_void_p(), ctypes.c_int32(0)
+            if G <= 16 and nb > 0:
+                L.call("tw_peer_alloc", nb, ctypes.byref(p), ctypes.byref(u))
+                mine, unc = p.value, int(u.value)
+                h = (ctypes.c_uint8 * 64)()
+                if G > 1:
+                    L.call("tw_peer_handle", ctypes.c_void_p(mine), h)
+                handle = bytes(h)
+        except Exception:  # this rank cannot take part: every rank falls back
+            handle = None
+        handles = [None] * G
+        dist.all_gather_object(handles, handle, group=group)
+        opened, bases, ok = [], [], all(hb is not None for hb in handles)
+        if ok:
+            try:
+                for q, hb in enumerate(handles):
+                    if q == r:
+                        bases.append(mine)
+                        continue
+                    v = ctypes.c_void_p()
+                    L.call("tw_peer_open", (ctypes.c_uint8 * 64).from_buffer_copy(hb),
+                           ctypes.byref(v))
+                    opened.append(v.value)
+                    bases.append(v.value)
+            except Exception:
+                ok = False
+        flags = [None] * G
+        dist.all_gather_object(flags, ok, group=group)
+        if not all(flags):
+            for v in opened:
+                lib.tw_peer_close(ctypes.c_void_p(v))
+            if mine is not None:
+                lib.tw_peer_free(ctypes.c_void_p(mine))
+            return None
+        return _PeerBuffers(mine, unc, opened, (ctypes.c_void_p * G)(*bases))
+
+    def __del__(self):
+        try:
+            lib = L.lib()
+            for v in self.opened:
+                lib.tw_peer_close(ctypes.c_void_p(v))
+            lib.tw_peer_free(self.mine)
+        except Exception:  # interpreter shutdown
+            pass
 
 
 class MultiDeviceSGD:
@@ -903,7 +996,7 @@ def _engine_for(X, Z, w, N, B, margin, reg, learning_rate, optim_type, group, x_
     if cacheable:
         key = (X.shape, Z.shape, int(np.asarray(w).size), int(N), int(B), float(margin),
                float(reg), float(learning_rate), optim_type, loss, gradient,
-               L.torch().cuda.current_device(), NARROW_SEGMENT, SEGMENT_KERNEL)
+               L.torch().cuda.current_device(), NARROW_SEGMENT)
         eng = _ENGINE["eng"]
         if _ENGINE["key"] == key:
             eng.reload(X, Z, np.asarray(w, dtype=np.float64))
