@@ -807,6 +807,9 @@ __global__ __launch_bounds__(kCbThreads) void k_count_chain_bucket(
     const uint32_t t = (uint32_t)tf;
     const uint32_t b = t >> shift;            // < nbk: t <= z_total
     uint32_t lo = b ? end[b - 1] : 0u;
+    // shift 0: every z of bucket t has image exactly t — none below it, no scan;
+    // shift > 0: a bucket spans 2^shift images and is scanned (tie-heavy bags: long buckets)
+    if (shift == 0) return lo;
     const uint32_t hi = end[b];
     uint32_t cnt = lo;
     for (; lo < hi; ++lo) cnt += zs[lo] < t ? 1u : 0u;

@@ -845,9 +845,16 @@ class ShardedSample:
             W = 2 if half else 1
             Sub = max(1, min(C, CHAIN_SUB))
             nsub = -(-C // Sub)
-            sends = [t.empty((G * Sub * (cap + 1) * W,), dtype=t.int64, device=dev)
-                     for _ in range(nsub)]
-            recvs = [t.empty_like(b) for b in sends]
+            # the send / receive ring persists on the sample across calls (fresh
+            # GB-scale allocations per call made the caching allocator flush and re-map)
+            rk = (G, Sub, cap, W, nsub)
+            ring = getattr(self, "_chain_ring", None)
+            if ring is None or ring[0] != rk:
+                self._chain_ring = None  # release the old ring first
+                sends = [t.empty((G * Sub * (cap + 1) * W,), dtype=t.int64, device=dev)
+                         for _ in range(nsub)]
+                self._chain_ring = ring = (rk, sends, [t.empty_like(b) for b in sends])
+            sends, recvs = ring[1], ring[2]
             if getattr(self, "_chain_flag", None) is None:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
         else:

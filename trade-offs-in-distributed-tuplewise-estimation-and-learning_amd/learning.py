@@ -557,8 +557,10 @@ class SGDEngine:
         t = self.t
         if not hasattr(self, "_replay_graphs"):
             self._replay_graphs = {}
+        # tables (phase, mod) in the key: a captured graph holds its table-stack phase, so a
+        # graph captured for one phase is never replayed at another
         key = (tag, nsteps, draws_dev.data_ptr() if draws_dev is not None else 0,
-               None if upload is None else upload[0])
+               None if upload is None else upload[0], tables)
         g = self._replay_graphs.get(key)
         if g is None:
             if self.complete and self._cwork is None:  # allocated outside the capture
@@ -1630,6 +1632,10 @@ def _replay_through(eng, draws, segs, pipe, mod, p_learn, loss, graphs, defer, X
             PIPE_STATS.append(time.perf_counter() - t0)
         else:
             pipe.wait(idx, rows=False)
+        # the table slots (0 at a segment that starts at a reshuffle, else 1..) and the copy of
+        # the last table into slot 0 hold only while evaluations sit at segment starts, which
+        # the segmentation guarantees: no evaluation step inside (i, nxt)
+        assert (nxt - 1) // eval_mod == i // eval_mod, (i, nxt, eval_mod)
         k, phase = idx % 3, i % mod
         buf = draws.ship_tables(k, nxt - i, ntab, 0 if phase == 0 else 1, eng)
         pipe.shipped(idx)  # the only reader of the pinned buffers has been enqueued
