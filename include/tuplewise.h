@@ -763,12 +763,13 @@ int tw_peer_open(const uint8_t* handle, void** d_out);
 int tw_peer_close(void* d_ptr);
 /* Per-step form, parity par = step & 1: this rank's `words` partial words (its shards' rows,
  * global offset offset_words) stored into every rank's slot, arrivals added to every rank's
- * counter; then tw_peer_update waits (bounded: 20 s, *d_abort raised on timeout) until all G
- * ranks' arrivals are in and applies tw_sgd_update's arithmetic to the n_total x d slot (same
- * bits), d_step advanced by one when given. */
-int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t offset_words,
-                    void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total,
-                    int64_t d, int32_t par, void* stream);
+ * counter (words_pad: the most words any rank publishes, the same on every rank — uneven shard
+ * splits); then tw_peer_update (words_per_rank = that words_pad) waits (bounded: 20 s,
+ * *d_abort raised on timeout) until all G ranks' arrivals are in and applies tw_sgd_update's
+ * arithmetic to the n_total x d slot (same bits), d_step advanced by one when given. */
+int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t words_pad,
+                    int64_t offset_words, void* const* d_peer_bases, int32_t G, int32_t rank,
+                    int32_t n_total, int64_t d, int32_t par, void* stream);
 int tw_peer_update(double* d_w, double* d_dw, void* d_my_base, int32_t n_total, int64_t d,
                    int64_t words_per_rank, int32_t G, int32_t par, double reg, double lr,
                    double momentum, uint64_t* d_step, uint32_t* d_abort, void* stream);

@@ -56,9 +56,14 @@ def _problem():
     return X, Z, w0, p
 
 
-@pytest.mark.parametrize("layout", ["replicated", "partitioned"])
-@pytest.mark.parametrize("mode", ["replay", "device"])
-def test_learning_two_ranks_equals_one(gpu, mode, layout):
+@pytest.mark.parametrize("G,mode,layout",
+                         [(2, m, la) for m in ("replay", "device")
+                          for la in ("replicated", "partitioned")]
+                         + [(3, "replay", "replicated"), (3, "device", "partitioned")])
+def test_learning_two_ranks_equals_one(gpu, G, mode, layout):
+    """G ranks (gloo) on the box's GPU equal one rank bit for bit — with a trajectory (the
+    per-step peer exchange) and without (the persistent peer segment, three evaluations).
+    G = 3: N = 8 shards split 2/3/3 (uneven splits, the reference's N = 100 over 8 GPUs)."""
     import torch.multiprocessing as mp
     import tuplewise.learning as lr
     X, Z, w0, p = _problem()
@@ -71,8 +76,8 @@ def test_learning_two_ranks_equals_one(gpu, mode, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_learn_worker, args=(r, port, 2, mode, q, layout))
-             for r in range(2)]
+    procs = [ctx.Process(target=_learn_worker, args=(r, port, G, mode, q, layout))
+             for r in range(G)]
     for pr in procs:
         pr.start()
     got, hist = q.get(timeout=300)

@@ -4,7 +4,8 @@ bench shape (n = 1e6/class, N = 64) through the chains against the one-launch-pe
 shards per rank), the ranking included: the Z structure of the whole Z and the images of the
 rank's own 1/G of the elements (tw_rank_images_query), the chain emission into G send buckets,
 a device copy of the send buffer standing in for the all-to-all (the same bytes; RCCL's xGMI
-transfer is not simulated), the unpack, one count launch of K x 64/G bags and the inverse-chain
+transfer is not simulated), the unpack, (round 5) a device copy standing in for the Z
+all-gather and the local part of the counts' reduction, one count launch of K x 64/G bags and the inverse-chain
 gather of the rank's final arrays.  Reports ms per call and the efficiency against the one-GPU
 call / G.  Run on the GPU box:
     python tools/chain_probe.py [K ...]"""
@@ -93,7 +94,13 @@ def rank_call(G, r, K, parts=False):
         t.setdefault(name, []).append((e0, e1))
         return out
 
+    Zg = torch.empty_like(Z)  # the all-gathered Z (a device copy of the same bytes)
+    full = torch.zeros(K * N + 1, dtype=torch.int64, device="cuda")
+
     def call():
+        if G > 1:  # round 5: the Z all-gather the ranking waits for, as a device copy of its
+            # bytes (the X all-gather runs asynchronously under the counts, not timed here)
+            mark("all-gather Z (device copy)", lambda: Zg.copy_(Z))
         xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
         for i0 in range(0, K, C):
             c = min(C, K - i0)
@@ -116,6 +123,9 @@ def rank_call(G, r, K, parts=False):
         else:
             mark("final gather", lambda: ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs,
                                                           kzs))
+            # the counts' all-reduce (with the overflow flag) stands in as its local fill
+            mark("counts reduce (local part)",
+                 lambda: full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
     ms, host = ev_time(call, 5)
     if parts:
         t = {k: sum(a.elapsed_time(b) for a, b in v) / 6 for k, v in t.items()}

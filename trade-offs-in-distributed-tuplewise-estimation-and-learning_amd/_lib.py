@@ -133,7 +133,7 @@ _SIGNATURES = {
     "tw_peer_handle": [_vp, _vp],
     "tw_peer_open": [_vp, _vp],
     "tw_peer_close": [_vp],
-    "tw_peer_publish": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i64, _i32, _vp],
+    "tw_peer_publish": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i64, _i32, _vp],
     "tw_peer_update": [_vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _f64, _f64, _f64, _vp, _vp,
                        _vp],
     "tw_sgd_segment_narrow_peer": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,

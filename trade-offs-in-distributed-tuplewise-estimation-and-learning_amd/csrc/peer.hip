@@ -158,12 +158,15 @@ extern "C" int tw_peer_close(void* d_ptr) {
 }
 
 // per-step form: this rank's `words` partial words (rows shard_base.. of the global order,
-// d columns) into every rank's per-step slot of parity `par`, arrivals added
-extern "C" int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t offset_words,
-                               void* const* d_peer_bases, int32_t G, int32_t rank,
-                               int32_t n_total, int64_t d, int32_t par, void* stream) {
+// d columns) into every rank's per-step slot of parity `par`, arrivals added; words_pad: the
+// most words any rank publishes (uneven shard splits), which fixes the blocks per rank
+extern "C" int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t words_pad,
+                               int64_t offset_words, void* const* d_peer_bases, int32_t G,
+                               int32_t rank, int32_t n_total, int64_t d, int32_t par,
+                               void* stream) {
   TW_ARG_CHECK(d_peer_bases != nullptr && G >= 1 && G <= kPeerMax && rank >= 0 && rank < G &&
-                   n_total >= 1 && d >= 1 && words >= 1 && offset_words >= 0 &&
+                   n_total >= 1 && d >= 1 && words >= 0 && words_pad >= words &&
+                   words_pad >= 1 && offset_words >= 0 &&
                    offset_words + words <= (int64_t)n_total * d && (par == 0 || par == 1),
                "tw_peer_publish: bad sizes");
   PeerSeg ps{};
@@ -177,14 +180,14 @@ extern "C" int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t
   ps.G = G;
   ps.n_total = (int)((int64_t)n_total * d);  // one slot's words
   auto* reset = (unsigned long long*)((char*)d_peer_bases[rank] + kPeerStepCtr + 64 * (1 - par));
-  hipLaunchKernelGGL(k_peer_publish, dim3(publish_blocks(words)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_peer_publish, dim3(publish_blocks(words_pad)), dim3(kBlock), 0,
                      (hipStream_t)stream, d_grads_loc, words, offset_words, ps, par, reset);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
 
-// per-step form: wait until every rank's publish of parity `par` is in (G ranks of
-// `words_per_rank` words each), then k_sgd_update on the slot
+// per-step form: wait until every rank's publish of parity `par` is in (G ranks, publishing
+// with words_pad = words_per_rank), then k_sgd_update on the slot
 extern "C" int tw_peer_update(double* d_w, double* d_dw, void* d_my_base, int32_t n_total,
                               int64_t d, int64_t words_per_rank, int32_t G, int32_t par,
                               double reg, double lr, double momentum, uint64_t* d_step,

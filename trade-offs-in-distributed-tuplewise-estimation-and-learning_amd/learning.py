@@ -122,10 +122,19 @@ class SGDEngine:
             raise ValueError("collectives=True needs a process group")
         # one process, one device, no collective: the fused / persistent / graph paths apply
         self.solo = self.G == 1 and not self.coll
-        if int(N) % self.G:
-            raise ValueError(f"N={N} shards do not split evenly over {self.G} ranks")
-        self.N_loc = int(N) // self.G
-        self.shard_base = self.rank * self.N_loc
+        if vgroup is not None and int(N) % self.G:
+            raise ValueError(f"N={N} shards do not split evenly over {self.G} slots")
+        if int(N) < self.G:
+            raise ValueError(f"N={N} shards cannot give each of {self.G} ranks one")
+        # rank r owns shards [r N / G, (r + 1) N / G): balanced and uneven where G does not
+        # divide N (the reference's N = 100 shuttle shards over 8 GPUs: 12 or 13 per rank);
+        # N_pad = the most any rank owns (padded per-rank layouts of the exchanges)
+        G_ = self.G
+        self.shard_bounds = [g * int(N) // G_ for g in range(G_ + 1)]
+        self.shard_base = self.shard_bounds[self.rank]
+        self.N_loc = self.shard_bounds[self.rank + 1] - self.shard_base
+        self.N_pad = -(-int(N) // G_)
+        self.even = int(N) % G_ == 0
         if x_layout not in ("replicated", "partitioned"):
             raise ValueError(f"x_layout must be 'replicated' or 'partitioned', not {x_layout!r}")
         self.layout = x_layout
@@ -161,7 +170,8 @@ class SGDEngine:
         self.w = _dev_f64(w_init).reshape(-1).clone()
         self.dw = t.zeros_like(self.w)
         self.grads = L.empty((self.N, self.d), t.float64)  # all shards, global order
-        self.grads_loc = self.grads if self.solo else L.empty((self.N_loc, self.d), t.float64)
+        # over ranks: this rank's partials (N_pad rows: the padded all-gather of uneven splits)
+        self.grads_loc = self.grads if self.solo else L.empty((self.N_pad, self.d), t.float64)
         self.rows_x = self.rows_z = None
         self.step_ctr = None
         # one launch per step (tw_sgd_step: the previous step's update fused into the gradient
@@ -402,9 +412,17 @@ class SGDEngine:
         lo, hi = self.x_own if side == 0 else self.z_own
         table = self.tab_x if side == 0 else self.tab_z
         n_own = hi - lo
-        M, M_q = self.N * k, self.N_loc * k
-        mine = rows[self.rank * M_q:(self.rank + 1) * M_q]
-        L.call("tw_row_table_local", L.ptr(mine), M_q, lo, hi, L.ptr(table), s)
+        if not self.even:
+            # uneven splits: every rank's positions padded to N_pad shards (row -1: owned by
+            # no rank, so never counted, packed or received), the kernels' equal layout
+            b, kp = self.shard_bounds, self.N_pad * k
+            pad = t.full((G * kp,), -1, dtype=t.int64, device=rows.device)
+            for g in range(G):
+                pad[g * kp:g * kp + (b[g + 1] - b[g]) * k].copy_(rows[b[g] * k:b[g + 1] * k])
+            rows = pad
+        M, M_q = G * self.N_pad * k, self.N_pad * k
+        mine = rows[self.rank * M_q:self.rank * M_q + self.N_loc * k]
+        L.call("tw_row_table_local", L.ptr(mine), self.N_loc * k, lo, hi, L.ptr(table), s)
         if not self.coll:
             return
         part = self.X_part if side == 0 else self.Z_part
@@ -451,15 +469,25 @@ class SGDEngine:
             # publish this rank's partials into every rank's slot, wait for all, update
             s, par = L.stream_handle(), self._pstep & 1
             self._pstep += 1
-            nw = self.N_loc * self.d
-            L.call("tw_peer_publish", L.ptr(self.grads_loc), nw, self.shard_base * self.d,
+            nw, npad = self.N_loc * self.d, self.N_pad * self.d
+            L.call("tw_peer_publish", L.ptr(self.grads_loc), nw, npad, self.shard_base * self.d,
                    self.peer.bases, self.G, self.rank, self.N, self.d, par, s)
             L.call("tw_peer_update", L.ptr(self.w), L.ptr(self.dw), self.peer.mine, self.N,
-                   self.d, nw, self.G, par, self.reg, self.lr, self.momentum,
+                   self.d, npad, self.G, par, self.reg, self.lr, self.momentum,
                    L.ptr(self.step_ctr), L.ptr(self._ctl[1:]), s)
             return
         if self.coll:
-            self.dist.all_gather_into_tensor(self.grads, self.grads_loc, group=self.group)
+            if self.even:
+                self.dist.all_gather_into_tensor(self.grads, self.grads_loc, group=self.group)
+            else:  # padded per-rank blocks, then the N valid rows in shard order
+                if getattr(self, "_gpad", None) is None:
+                    t, b = self.t, self.shard_bounds
+                    self._gpad = L.empty((self.G * self.N_pad, self.d), t.float64)
+                    self._gidx = L.to_device(np.concatenate(
+                        [np.arange(b[g + 1] - b[g]) + g * self.N_pad
+                         for g in range(self.G)]).astype(np.int64))
+                self.dist.all_gather_into_tensor(self._gpad, self.grads_loc, group=self.group)
+                self.t.index_select(self._gpad, 0, self._gidx, out=self.grads)
         self._apply_update()
 
     def _peer_segment(self, nsteps: int, draws_dev=None, swr_mod: int = 0):
