@@ -761,6 +761,12 @@ int tw_peer_free(void* d_ptr);
 int tw_peer_handle(void* d_ptr, uint8_t* out_handle);
 int tw_peer_open(const uint8_t* handle, void** d_out);
 int tw_peer_close(void* d_ptr);
+/* Setup handshake: tw_peer_hello stores `token` into this rank's hello word of every rank's
+ * buffer (and waits for it); after a host barrier over the ranks, tw_peer_check sets *out_ok
+ * = 1 when its own buffer's G hello words all hold `token`. */
+int tw_peer_hello(void* const* d_peer_bases, int32_t G, int32_t rank, uint64_t token,
+                  void* stream);
+int tw_peer_check(void* d_my_base, int32_t G, uint64_t token, int32_t* out_ok);
 /* Per-step form, parity par = step & 1: this rank's `words` partial words (its shards' rows,
  * global offset offset_words) stored into every rank's slot, arrivals added to every rank's
  * counter (words_pad: the most words any rank publishes, the same on every rank — uneven shard

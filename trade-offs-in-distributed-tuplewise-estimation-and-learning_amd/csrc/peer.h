@@ -9,6 +9,7 @@
 //   0    u64 segment arrival counter (monotonic; the persistent segments)
 //   64   u64 segment epoch: global steps done by this rank's persistent segments
 //   128  u64 per-step counters [2] (128, 192), by step parity (the publish / update launches)
+//   256  u64 hello words [16]: rank p's token, written by rank p at setup (tw_peer_hello)
 //   512  segment gradient slots [2][n_total][d] f64
 //   ...  per-step gradient slots [2][n_total][d] f64
 #pragma once
@@ -16,7 +17,8 @@
 
 namespace tw {
 
-constexpr size_t kPeerSegCtr = 0, kPeerEpoch = 64, kPeerStepCtr = 128, kPeerHdr = 512;
+constexpr size_t kPeerSegCtr = 0, kPeerEpoch = 64, kPeerStepCtr = 128, kPeerHello = 256,
+                 kPeerHdr = 512;
 
 __host__ __device__ inline size_t peer_slots_words(int64_t n_total, int64_t d) {
   return 2 * (size_t)n_total * (size_t)d;

@@ -101,9 +101,51 @@ __global__ __launch_bounds__(kBlock) void k_peer_update(double* w, double* dw,
   }
 }
 
+// setup handshake: lane p stores this rank's token into rank p's hello word for this rank
+__global__ void k_peer_hello(PeerSeg ps, int rank, unsigned long long token) {
+  const int p = (int)threadIdx.x;
+  if (p < ps.G) {
+    auto* w = (unsigned long long*)((char*)ps.ctr[p] + kPeerHello) + rank;
+    __hip_atomic_store(w, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace tw
 
 using namespace tw;
+
+// Setup handshake of the peer mapping: every rank writes `token` into its slot of every rank's
+// hello words (tw_peer_hello, then a host barrier over the ranks); tw_peer_check then reads its
+// own buffer's G hello words and sets *ok = 1 when each holds `token` — the IPC mappings
+// work and GPU stores through them land, before any step relies on them.
+extern "C" int tw_peer_hello(void* const* d_peer_bases, int32_t G, int32_t rank, uint64_t token,
+                             void* stream) {
+  TW_ARG_CHECK(d_peer_bases != nullptr && G >= 1 && G <= kPeerMax && rank >= 0 && rank < G,
+               "tw_peer_hello: bad ranks");
+  PeerSeg ps{};
+  for (int p = 0; p < G; ++p) {
+    TW_ARG_CHECK(d_peer_bases[p] != nullptr, "tw_peer_hello: rank %d's buffer missing", p);
+    ps.ctr[p] = (unsigned long long*)d_peer_bases[p];
+  }
+  ps.G = G;
+  hipLaunchKernelGGL(k_peer_hello, dim3(1), dim3(64), 0, (hipStream_t)stream, ps, (int)rank,
+                     (unsigned long long)token);
+  TW_LAUNCH_CHECK();
+  TW_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  return TW_OK;
+}
+
+extern "C" int tw_peer_check(void* d_my_base, int32_t G, uint64_t token, int32_t* out_ok) {
+  TW_ARG_CHECK(d_my_base != nullptr && G >= 1 && G <= kPeerMax && out_ok != nullptr,
+               "tw_peer_check: bad arguments");
+  uint64_t h[kPeerMax] = {0};
+  TW_HIP_CHECK(hipMemcpy(h, (char*)d_my_base + kPeerHello, sizeof(uint64_t) * G,
+                         hipMemcpyDeviceToHost));
+  int ok = 1;
+  for (int p = 0; p < G; ++p) ok &= h[p] == token ? 1 : 0;
+  *out_ok = ok;
+  return TW_OK;
+}
 
 extern "C" int64_t tw_peer_buffer_bytes(int32_t n_total, int64_t d) {
   if (n_total < 1 || d < 1) return -1;

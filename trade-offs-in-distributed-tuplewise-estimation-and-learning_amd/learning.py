@@ -816,6 +816,28 @@ class _PeerBuffers:
                     bases.append(v.value)
             except Exception:
                 ok = False
+        # the handshake: every rank's GPU stores a token into every rank's buffer through the
+        # mappings; each checks its own after a barrier (a mapping that opened but does not
+        # carry stores is found here, before any step relies on it)
+        token = 0x7E5E_0000_0000 + 1 + int(np.random.default_rng().integers(1 << 30))
+        tokens = [None] * G
+        dist.all_gather_object(tokens, token if ok else None, group=group)
+        ok = ok and all(tk is not None for tk in tokens)
+        token = tokens[0] if ok else 0
+        if ok:
+            try:
+                bases_arr = (ctypes.c_void_p * G)(*bases)
+                L.call("tw_peer_hello", bases_arr, G, r, token, L.stream_handle())
+            except Exception:
+                ok = False
+        dist.all_gather_object([None] * G, ok, group=group)  # the barrier: every hello landed
+        if ok:
+            good = ctypes.c_int32(0)
+            try:
+                L.call("tw_peer_check", ctypes.c_void_p(mine), G, token, ctypes.byref(good))
+                ok = bool(good.value)
+            except Exception:
+                ok = False
         flags = [None] * G
         dist.all_gather_object(flags, ok, group=group)
         if not all(flags):
