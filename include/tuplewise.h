@@ -701,7 +701,9 @@ int tw_row_unpack(const double* d_rec, int64_t m, int64_t d, double* d_out, void
  * tw_row_table_remote: for the `total` records received (source g's bucket at word
  *   d_rstart[g] of d_recv, d_rcount[g] records, d_rprefix[g] = sum of the counts before g):
  *   d_table[position] = base + d_rstart[g] / d + j for record j — d_recv being the receive
- *   area of the matrix at row `base` (the partition's row count). */
+ *   area of the matrix at row `base` (the partition's row count); a position outside
+ *   [0, table_len), or a record past recv_len words, is not used and raises *d_bad (position
+ *   + 1, or 2^62: a protocol error the caller reports; d_bad may be NULL). */
 int tw_row_route_remote_counts(const int64_t* d_rows, int64_t M, int64_t M_q, int64_t lo,
                                int64_t hi, int32_t G, int32_t me, int64_t* d_counts,
                                void* stream);
@@ -713,7 +715,8 @@ int tw_row_table_local(const int64_t* d_rows, int64_t M_q, int64_t lo, int64_t h
                        int64_t* d_table, void* stream);
 int tw_row_table_remote(const double* d_recv, int32_t G, const int64_t* d_rstart,
                         const int64_t* d_rcount, const int64_t* d_rprefix, int64_t total,
-                        int64_t d, int64_t base, int64_t* d_table, void* stream);
+                        int64_t d, int64_t base, int64_t* d_table, int64_t table_len,
+                        int64_t recv_len, int64_t* d_bad, void* stream);
 
 /* ---- (e) single-process multi-device communicator (RCCL over xGMI) --------------------
  * The reference's workers are one serial in-process loop (compute_stats.py:71-91,

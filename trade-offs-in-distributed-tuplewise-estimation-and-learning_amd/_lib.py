@@ -165,7 +165,8 @@ _SIGNATURES = {
     "tw_row_pack_remote": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _vp,
                            _vp, _vp],
     "tw_row_table_local": [_vp, _i64, _i64, _i64, _vp, _vp],
-    "tw_row_table_remote": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "tw_row_table_remote": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp,
+                            _vp],
     "tw_comm_init": [_i32, _vp, _vp],
     "tw_comm_destroy": [_i32],
     "tw_allgather_u64": [_i32, _vp, _vp, _i64, _vp],

@@ -167,11 +167,13 @@ __global__ __launch_bounds__(kBlock) void k_row_table_local(const int64_t* __res
   }
 }
 
-// received rows: record j of source g sits at row (base + rstart[g] / d + j) of the matrix
+// received rows: record j of source g sits at row (base + rstart[g] / d + j) of the matrix;
+// a position outside the table (a protocol error) is not written and raises *bad
 __global__ __launch_bounds__(kBlock) void k_row_table_remote(
     const double* __restrict__ recv, int G, const int64_t* __restrict__ rstart,
     const int64_t* __restrict__ rcount, const int64_t* __restrict__ rprefix, int64_t total,
-    int64_t d, int64_t base, int64_t* __restrict__ table) {
+    int64_t d, int64_t base, int64_t* __restrict__ table, int64_t table_len, int64_t recv_len,
+    int64_t* __restrict__ bad) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kBlock) {
     int a = 0, b = G;  // the last g with rprefix[g] <= i
@@ -180,8 +182,16 @@ __global__ __launch_bounds__(kBlock) void k_row_table_remote(
       if (rprefix[m] <= i) a = m; else b = m;
     }
     const int64_t j = i - rprefix[a];
-    const int64_t pos =
-        (int64_t)__double_as_longlong(recv[rstart[a] + rcount[a] * d + j]);
+    const int64_t at = rstart[a] + rcount[a] * d + j;
+    if (at < 0 || at >= recv_len) {  // the split sizes disagree with the counts
+      if (bad) atomicMax((unsigned long long*)bad, 1ull << 62);
+      continue;
+    }
+    const int64_t pos = (int64_t)__double_as_longlong(recv[at]);
+    if (pos < 0 || pos >= table_len) {
+      if (bad) atomicMax((unsigned long long*)bad, (unsigned long long)(pos + 1 > 0 ? pos + 1 : 1));
+      continue;
+    }
     table[pos] = base + rstart[a] / d + j;
   }
 }
@@ -298,8 +308,10 @@ extern "C" int tw_row_table_local(const int64_t* d_rows, int64_t M_q, int64_t lo
 extern "C" int tw_row_table_remote(const double* d_recv, int32_t G, const int64_t* d_rstart,
                                    const int64_t* d_rcount, const int64_t* d_rprefix,
                                    int64_t total, int64_t d, int64_t base, int64_t* d_table,
+                                   int64_t table_len, int64_t recv_len, int64_t* d_bad,
                                    void* stream) {
-  TW_ARG_CHECK(G >= 1 && G <= kMaxRanks && total >= 0 && d >= 1 && base >= 0,
+  TW_ARG_CHECK(G >= 1 && G <= kMaxRanks && total >= 0 && d >= 1 && base >= 0 &&
+                   table_len >= 0,
                "tw_row_table_remote: bad sizes");
   if (total == 0) return TW_OK;
   TW_ARG_CHECK(d_recv && d_rstart && d_rcount && d_rprefix && d_table,
@@ -307,7 +319,7 @@ extern "C" int tw_row_table_remote(const double* d_recv, int32_t G, const int64_
   const int64_t blocks = std::min<int64_t>(ceil_div(total, kBlock), 4096);
   hipLaunchKernelGGL(k_row_table_remote, dim3((unsigned)blocks), dim3(kBlock), 0,
                      (hipStream_t)stream, d_recv, (int)G, d_rstart, d_rcount, d_rprefix, total,
-                     d, base, d_table);
+                     d, base, d_table, table_len, recv_len, d_bad);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

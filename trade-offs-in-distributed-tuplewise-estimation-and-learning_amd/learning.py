@@ -443,8 +443,13 @@ class SGDEngine:
         rwords, rstart = layout(rc)
         send = self._records("send", int(sum(swords)))
         cursor = L.empty((G,), t.int64)
+        # device copies held in locals until the launches are enqueued: a temporary freed
+        # inside one call's argument list hands its block to the next temporary of the same
+        # list (the round-4 table call read its bucket starts from the prefix array — masked
+        # at G = 2, where both begin 0, 0; found at G = 3)
+        sstart_d = L.to_device(sstart)
         L.call("tw_row_pack_remote", L.ptr(rows), M, M_q, lo, hi, G, self.rank, L.ptr(part), d,
-               L.ptr(L.to_device(sstart)), L.ptr(counts), L.ptr(cursor), L.ptr(send), s)
+               L.ptr(sstart_d), L.ptr(counts), L.ptr(cursor), L.ptr(send), s)
         mat = self.X if side == 0 else self.Z
         need = n_own + int(sum(rwords)) // d
         if need > mat.shape[0]:  # more remote rows than the receive area holds: grow it
@@ -458,9 +463,16 @@ class SGDEngine:
         self.dist.all_to_all_single(recv, send[:int(sum(swords))], output_split_sizes=rwords,
                                     input_split_sizes=swords, group=self.group)
         rprefix = np.concatenate([[0], np.cumsum(rc)]).astype(np.int64)
-        L.call("tw_row_table_remote", L.ptr(recv), G, L.ptr(L.to_device(rstart)),
-               L.ptr(rcounts), L.ptr(L.to_device(rprefix)), int(rprefix[-1]), d, n_own,
-               L.ptr(table), s)
+        bad = t.zeros((1,), dtype=t.int64, device=table.device)
+        rstart_d, rprefix_d = L.to_device(rstart), L.to_device(rprefix)
+        L.call("tw_row_table_remote", L.ptr(recv), G, L.ptr(rstart_d), L.ptr(rcounts),
+               L.ptr(rprefix_d), int(rprefix[-1]), d, n_own, L.ptr(table), table.numel(),
+               recv.numel(), L.ptr(bad), s)
+        b = int(bad.item())  # (the exchange already synchronised on its split sizes)
+        if b:
+            raise RuntimeError(f"partitioned row exchange: a received position ({b - 1}) lies "
+                               f"outside this rank's {table.numel()}-entry row table "
+                               f"(side {side}, G={G}, rank {self.rank}, sc={sc}, rc={rc})")
 
     def _update(self):
         if self.vgroup is not None:  # MultiDeviceSGD gathers the slots' gradients, then updates
