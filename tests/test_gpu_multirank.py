@@ -118,12 +118,17 @@ def _est_worker(rank, port, G, q, exchange="fixed", chain=True):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange,chain", [("fixed", True), ("fixed", False), ("exact", False)])
-def test_sharded_sample_two_ranks_equals_one(gpu, exchange, chain):
+@pytest.mark.parametrize("G,exchange,chain", [(2, "fixed", True), (2, "fixed", False),
+                                               (2, "exact", False), (3, "fixed", True),
+                                               (3, "exact", False)])
+def test_sharded_sample_two_ranks_equals_one(gpu, G, exchange, chain):
+    """G ranks (gloo, real kernels) equal one process: UnN with a key, UnNB, the step chains
+    (all-pairs and exact bucket counts) and the final arrays.  G = 3: three send buckets per
+    rank (G = 2 has one remote peer only)."""
     import torch
     import torch.multiprocessing as mp
     from tuplewise.device import ShardedSample
-    G, n_loc, N = 2, 40_000, 8
+    n_loc, N = 40_000, 8
     rng = np.random.RandomState(3)
     X = rng.normal(0.3, 1, G * n_loc)
     Z = rng.normal(0, 1, G * n_loc)
