@@ -466,11 +466,16 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
             same_1rank = bool(np.array_equal(w_g, e_1.w_host()))
             del e_1
         del e_g
-    launches = ("one persistent launch per run of <= 4096 steps, reshuffles drawn in the "
+    launches = ("one persistent launch per segment over the ranks, shard gradients exchanged "
+                "GPU to GPU through IPC-mapped peer buffers (csrc/peer.hip)"
+                + (", reshuffles drawn in the kernel" if swr else "")
+                if getattr(eng, "peer_seg", False) else
+                "gradient launch + peer publish + wait-and-update per step (csrc/peer.hip)"
+                if getattr(eng, "peer", None) is not None else
+                "one persistent launch per run of <= 4096 steps, reshuffles drawn in the "
                 "kernel" if swr else
                 "one persistent launch per segment" if eng.narrow_seg else
-                "one launch per step" if eng.fused else
-                "one segment kernel per segment" if eng.segment else "gradient + update per step")
+                "one launch per step" if eng.fused else "gradient + update per step")
     G = 1 if group is None else torch.distributed.get_world_size(group)
     out = {"steps_per_s": steps / dt, "ms_per_step": dt / steps * 1e3,
            "pairs_per_step": N * B, "gathered_bytes_per_step": N * B * 16 * d,
@@ -643,6 +648,24 @@ def pmc_traffic(kernel="k_count_complete"):
     if k and per is not None:
         return per / k, None
     return per, plain
+
+
+def traced_count_chain(steps):
+    """The committed rocprofv3 kernel-trace summary of the headline count launch at this K
+    (profiles/*count_chain_traced*.json, tools/traced_chain.py): mean / min duration of the
+    K-step k_count_chain launches and the lane-op fractions they imply — the traced figure
+    printed beside the live frac."""
+    cands = sorted(ROOT.glob("profiles/*count_chain_traced*.json"),
+                   key=lambda p: p.stat().st_mtime, reverse=True)
+    for c in cands:
+        try:
+            d = json.loads(c.read_text())
+        except Exception:
+            continue
+        if int(d.get("steps_per_launch", -1)) == int(steps):
+            return {k: d[k] for k in ("mean_ms", "min_ms", "frac_mean", "frac_min", "launches")
+                    if k in d} | {"source": str(c.relative_to(ROOT))}
+    return None
 
 
 def pmc_emit_traffic():
@@ -1299,6 +1322,8 @@ def main():
         "roofline": {"bound": "valu", "kernel": count_kernel,
                      "achieved": achieved / 1e12, "peak": PEAK_LANE_OPS / 1e12,
                      "unit": "Tlane-op/s", "frac": achieved / PEAK_LANE_OPS,
+                     # the same launches under rocprofv3 --kernel-trace (committed summary)
+                     "frac_traced": traced_count_chain(args.steps) if chain_path else None,
                      "count_kernel_ms": kms, "traffic": traffic,
                      "traffic_count_only": traffic_plain,
                      "traffic_unit": ("HBM bytes per step: the chunk's k_count_chain launch / its "
