@@ -476,6 +476,15 @@ def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
 
 # samples of at least this many items (per array) take the device shuffles in UnNT / UnNBT
 DEVICE_SHUFFLE_MIN = 1 << 16
+# study hook (tools/time_dropin_parts.py): a list receives (label, perf_counter) marks of the
+# device-shuffle drop-in call
+DROPIN_MARKS = None
+
+
+def _mark(label):
+    if DROPIN_MARKS is not None:
+        import time
+        DROPIN_MARKS.append((label, time.perf_counter()))
 
 
 def _device_shuffle_ok(X, Z, spec, N: int = 1, T: int = 1) -> bool:
@@ -508,22 +517,29 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
     the last state (the in-place side effect of the T np.random.shuffle calls)."""
     from .numpy_rng import shuffle_draws32
     plans = []
+    _mark("start")
     # X and Z go up on a helper thread while the host draws the first shuffle
     ds = E.DeviceShuffles(X, Z, T)
+    _mark("setup")
 
     def draws(a, b):  # each side's draws into pinned memory; the device swaps it meanwhile
         shuffle_draws32(a.shape[0], out=ds.draw_x())
+        _mark("x drawn")
         ds.push_x()
         shuffle_draws32(b.shape[0], out=ds.draw_z())
+        _mark("z drawn")
         ds.push_z()
 
     for _ in range(T):
         plans.append(plan_un(X, Z, N, spec, sampling_type, variant, shuffle=draws))
     nx, nz = X.shape[0], Z.shape[0]
     t = L.torch()
+    _mark("pushed")
     # the in-place side effect, X first: its last state goes back while Z's last shuffle runs
     t.from_numpy(X).copy_(ds.last_x())
+    _mark("x written back")
     xs, zs = ds.finish()
+    _mark("finish")
     if 0 in ds.redone:  # (rare) X's shuffles were resumed: its last state changed
         t.from_numpy(X).copy_(xs[T - 1])
     blocks, counts = [], []
@@ -537,8 +553,10 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
             blocks.append(Block(bx, bz, b.aux))
         counts.append(len(blks))
     vals = spec.evaluate_device(xs.reshape(-1), zs.reshape(-1), blocks) if blocks else []
+    _mark("counted")
     # the caller's Z ends in the last shuffled state too (X was written above)
     t.from_numpy(Z).copy_(zs[T - 1])
+    _mark("z written back")
     out, i = [], 0
     for p, c in zip(plans, counts):
         out.append(finish_un(p, vals[i:i + c]))

@@ -215,7 +215,9 @@ __global__ __launch_bounds__(kImgThreads) void k_count_idx_img(
 // compare); 2 = + the two LDS image reads and the compare (no equal-image fallback); 3 = 2 with
 // the LDS reads at conflict-free addresses (lane-consecutive: what the random gathers' bank
 // conflicts cost); 4 = the product with the Lemire maps' four per-draw rejection branches
-// (tw_common.h lemire_index) in place of lemire4's one wave-uniform test.
+// (tw_common.h lemire_index) in place of lemire4's one wave-uniform test.  Measured (round 5,
+// profiles/r05s8_rng_img_attribution.json): product 0.0848 ms per 64 x 1e6 pairs, 1: 0.0752,
+// 2: 0.0781, 3: 0.0797, 4: 0.1010 — the round-4 gap was the per-draw branches.
 #ifndef TW_RNG_IMG_VARIANT
 #define TW_RNG_IMG_VARIANT 0
 #endif
@@ -294,6 +296,10 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
         const int64_t q = qb + (int64_t)u * kImgThreads + threadIdx.x;
         r[u] = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
       }
+      // the iteration's undecided pairs (equal images), settled on the scores after ONE
+      // wave-uniform test for all QU blocks (one ballot per iteration, not per block)
+      uint32_t ui[QU][2], uj[QU][2];
+      bool ud[QU][2];
 #pragma unroll
       for (int u = 0; u < QU; ++u) {
         const int64_t q = qb + (int64_t)u * kImgThreads + threadIdx.x;
@@ -341,12 +347,30 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
         u0 = u0 && live;
         u1 = u1 && two;
         acc += (live && !u0 ? r0 : 0u) + (two && !u1 ? r1 : 0u);
-        if (__builtin_expect(__ballot(u0 || u1) != 0, 0)) {
-          if (u0) acc += exact_cmp<T, PRED>(x[xb + i0], z[zb + j0]);
-          if (u1) acc += exact_cmp<T, PRED>(x[xb + i1], z[zb + j1]);
-        }
+        ui[u][0] = i0;
+        uj[u][0] = j0;
+        ui[u][1] = i1;
+        uj[u][1] = j1;
+        ud[u][0] = u0;
+        ud[u][1] = u1;
 #endif
       }
+#if TW_RNG_IMG_VARIANT == 0 || TW_RNG_IMG_VARIANT == 4
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < QU; ++u) any = any || ud[u][0] || ud[u][1];
+      if (__builtin_expect(__ballot(any) != 0, 0)) {
+#pragma unroll
+        for (int u = 0; u < QU; ++u)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (ud[u][h]) acc += exact_cmp<T, PRED>(x[xb + ui[u][h]], z[zb + uj[u][h]]);
+      }
+#else
+      (void)ui;
+      (void)uj;
+      (void)ud;
+#endif
     }
   }
   ns.finish();
