@@ -212,12 +212,17 @@ class CompleteCount(BlockSpec):
         mode = "half" if self.tie_mode == "half" else "gt"
         xa, xo = _layout(xd, blocks, "x")
         za, zo = _layout(zd, blocks, "z")
-        counts = E.count_complete(E.Shards(xa, xo, za, zo, L.TW_F64), mode)
-        out = []
-        for b, c in zip(blocks, counts):
-            pairs = b.nx() * b.nz()
-            out.append(E.ratio(c, 2 * pairs) if mode == "half" else E.ratio(c, pairs))
-        return out
+        sh = E.Shards(xa, xo, za, zo, L.TW_F64)
+        sh._x_off_dev, sh._z_off_dev = L.to_device_many([xo, zo])  # one upload for both
+        counts = E.count_complete(sh, mode)
+        # float64(count) / float64(pairs) per block, as E.ratio: both conversions exact
+        # (counts and pairs < 2^53 here) and one IEEE division each — the same bits, vectorised
+        pairs = np.diff(xo).astype(np.int64) * np.diff(zo).astype(np.int64)
+        if mode == "half":
+            pairs = 2 * pairs
+        if counts.size and (int(counts.max()) >= 1 << 53 or int(pairs.max()) >= 1 << 53):
+            return [E.ratio(c, p) for c, p in zip(counts, pairs)]
+        return list(counts.astype(np.float64) / pairs.astype(np.float64))
 
 
 class CompleteSum(BlockSpec):
@@ -519,7 +524,7 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
     plans = []
     _mark("start")
     # X and Z go up on a helper thread while the host draws the first shuffle
-    ds = E.DeviceShuffles(X, Z, T)
+    ds = E.DeviceShuffles(X, Z, T, reuse=True)
     _mark("setup")
 
     def draws(a, b):  # each side's draws into pinned memory; the device swaps it meanwhile
