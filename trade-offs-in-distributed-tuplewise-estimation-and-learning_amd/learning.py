@@ -184,7 +184,6 @@ class SGDEngine:
         # over ranks: the device-resident gradient exchange (csrc/peer.hip), when every rank
         # could map every other rank's peer buffer (else the per-step RCCL all-gather)
         self.peer = _PeerBuffers.create(self) if self.coll and PEER_EXCHANGE else None
-        self._pstep = 0  # steps of the per-step peer exchange (its slot / counter parity)
         self.peer_seg = (self.peer is not None and not self.complete
                          and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N, self.B)))
         self._ctl = (t.zeros((2,), dtype=t.int32, device=self.w.device)
@@ -479,8 +478,8 @@ class SGDEngine:
             return
         if self.peer is not None:
             # publish this rank's partials into every rank's slot, wait for all, update
-            s, par = L.stream_handle(), self._pstep & 1
-            self._pstep += 1
+            s, par = L.stream_handle(), self.peer.pstep & 1
+            self.peer.pstep += 1
             nw, npad = self.N_loc * self.d, self.N_pad * self.d
             L.call("tw_peer_publish", L.ptr(self.grads_loc), nw, npad, self.shard_base * self.d,
                    self.peer.bases, self.G, self.rank, self.N, self.d, par, s)
@@ -782,24 +781,39 @@ class SGDEngine:
             reshuffle_first = False
 
 
+_PEERS = {}  # (process group, G, rank, N, d) -> _PeerBuffers: one set per shape, kept
+
+
 class _PeerBuffers:
     """This rank's peer buffer (csrc/peer.hip, tw_peer_alloc: counters and gradient slots of
     the device-resident exchange) and every other rank's, mapped through IPC handles exchanged
     once over the process group.  create() is collective: every rank learns whether all ranks
     allocated and mapped their buffers, and all fall back to the RCCL all-gather together if
-    one could not."""
+    one could not (a warning names the reason).  The buffers of a (group, N, d) shape are kept
+    for the process and handed to every later engine of that shape: freeing one while a peer
+    still maps it, and mapping its successor at the same address, made the next open fail (a
+    C5 engine after a C4 one).  The persistent segments' epoch lives in the buffer and the
+    per-step exchange's parity (pstep) lives here, so a later engine continues both."""
 
     def __init__(self, mine, uncached, opened, bases):
         self.mine = ctypes.c_void_p(mine)
         self.uncached = uncached
         self.opened = opened
         self.bases = bases
+        self.pstep = 0  # steps of the per-step exchange through these buffers (its parity)
 
     @staticmethod
     def create(eng):
+        import warnings
         dist, group, G, r = eng.dist, eng.group, eng.G, eng.rank
+        key = (id(group), G, r, eng.N, eng.d)
+        have = _PEERS.get(key)
+        flags = [None] * G
+        dist.all_gather_object(flags, have is not None, group=group)
+        if all(flags):
+            return have
         lib = L.lib()
-        mine, unc, handle = None, 0, None
+        mine, unc, handle, why = None, 0, None, None
         try:
             nb = int(lib.tw_peer_buffer_bytes(eng.N, eng.d))
             p, u = ctypes.c_void_p(), ctypes.c_int32(0)
@@ -810,8 +824,10 @@ class _PeerBuffers:
                 if G > 1:
                     L.call("tw_peer_handle", ctypes.c_void_p(mine), h)
                 handle = bytes(h)
-        except Exception:  # this rank cannot take part: every rank falls back
-            handle = None
+            else:
+                why = f"{G} ranks (at most 16)"
+        except Exception as e:  # this rank cannot take part: every rank falls back
+            handle, why = None, f"allocation / handle: {e}"
         handles = [None] * G
         dist.all_gather_object(handles, handle, group=group)
         opened, bases, ok = [], [], all(hb is not None for hb in handles)
@@ -826,8 +842,8 @@ class _PeerBuffers:
                            ctypes.byref(v))
                     opened.append(v.value)
                     bases.append(v.value)
-            except Exception:
-                ok = False
+            except Exception as e:
+                ok, why = False, f"opening a peer's handle: {e}"
         # the handshake: every rank's GPU stores a token into every rank's buffer through the
         # mappings; each checks its own after a barrier (a mapping that opened but does not
         # carry stores is found here, before any step relies on it)
@@ -840,34 +856,32 @@ class _PeerBuffers:
             try:
                 bases_arr = (ctypes.c_void_p * G)(*bases)
                 L.call("tw_peer_hello", bases_arr, G, r, token, L.stream_handle())
-            except Exception:
-                ok = False
+            except Exception as e:
+                ok, why = False, f"handshake stores: {e}"
         dist.all_gather_object([None] * G, ok, group=group)  # the barrier: every hello landed
         if ok:
             good = ctypes.c_int32(0)
             try:
                 L.call("tw_peer_check", ctypes.c_void_p(mine), G, token, ctypes.byref(good))
                 ok = bool(good.value)
-            except Exception:
-                ok = False
-        flags = [None] * G
-        dist.all_gather_object(flags, ok, group=group)
-        if not all(flags):
+                if not ok:
+                    why = "handshake: a peer's token did not arrive"
+            except Exception as e:
+                ok, why = False, f"handshake check: {e}"
+        oks = [None] * G
+        dist.all_gather_object(oks, (ok, why), group=group)
+        if not all(o for o, _ in oks):
             for v in opened:
                 lib.tw_peer_close(ctypes.c_void_p(v))
             if mine is not None:
                 lib.tw_peer_free(ctypes.c_void_p(mine))
+            reasons = "; ".join(f"rank {q}: {w}" for q, (o, w) in enumerate(oks) if not o)
+            warnings.warn("learning over ranks: the device-resident gradient exchange is "
+                          f"unavailable ({reasons}); using the RCCL all-gather per step")
             return None
-        return _PeerBuffers(mine, unc, opened, (ctypes.c_void_p * G)(*bases))
-
-    def __del__(self):
-        try:
-            lib = L.lib()
-            for v in self.opened:
-                lib.tw_peer_close(ctypes.c_void_p(v))
-            lib.tw_peer_free(self.mine)
-        except Exception:  # interpreter shutdown
-            pass
+        pb = _PeerBuffers(mine, unc, opened, (ctypes.c_void_p * G)(*bases))
+        _PEERS[key] = pb
+        return pb
 
 
 class MultiDeviceSGD:
