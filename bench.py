@@ -470,7 +470,7 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
                 "GPU to GPU through IPC-mapped peer buffers (csrc/peer.hip)"
                 + (", reshuffles drawn in the kernel" if swr else "")
                 if getattr(eng, "peer_seg", False) else
-                "gradient launch + peer publish + wait-and-update per step (csrc/peer.hip)"
+                "gradient launch + one publish-wait-update launch per step (csrc/peer.hip)"
                 if getattr(eng, "peer", None) is not None else
                 "one persistent launch per run of <= 4096 steps, reshuffles drawn in the "
                 "kernel" if swr else

@@ -770,18 +770,17 @@ int tw_peer_close(void* d_ptr);
 int tw_peer_hello(void* const* d_peer_bases, int32_t G, int32_t rank, uint64_t token,
                   void* stream);
 int tw_peer_check(void* d_my_base, int32_t G, uint64_t token, int32_t* out_ok);
-/* Per-step form, parity par = step & 1: this rank's `words` partial words (its shards' rows,
- * global offset offset_words) stored into every rank's slot, arrivals added to every rank's
- * counter (words_pad: the most words any rank publishes, the same on every rank — uneven shard
- * splits); then tw_peer_update (words_per_rank = that words_pad) waits (bounded: 20 s,
- * *d_abort raised on timeout) until all G ranks' arrivals are in and applies tw_sgd_update's
- * arithmetic to the n_total x d slot (same bits), d_step advanced by one when given. */
-int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t words_pad,
-                    int64_t offset_words, void* const* d_peer_bases, int32_t G, int32_t rank,
-                    int32_t n_total, int64_t d, int32_t par, void* stream);
-int tw_peer_update(double* d_w, double* d_dw, void* d_my_base, int32_t n_total, int64_t d,
-                   int64_t words_per_rank, int32_t G, int32_t par, double reg, double lr,
-                   double momentum, uint64_t* d_step, uint32_t* d_abort, void* stream);
+/* Per-step form, ONE launch after the gradient launch, parity par = step & 1: this rank's
+ * `words` partial words (its shards' rows, global offset offset_words = shard_base * d) stored
+ * into every rank's slot and the launch's arrivals added to every rank's counter; then the
+ * launch waits (bounded: 20 s, *d_abort raised on timeout) until all G ranks' arrivals are in
+ * and applies tw_sgd_update's arithmetic to the n_total x d slot (same bits), d_step advanced
+ * by one when given.  Uneven shard splits need nothing more: the arrivals per rank depend on
+ * d only. */
+int tw_peer_step(const double* d_grads_loc, int64_t words, int64_t offset_words,
+                 void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total, int64_t d,
+                 int32_t par, double* d_w, double* d_dw, double reg, double lr, double momentum,
+                 uint64_t* d_step, uint32_t* d_abort, void* stream);
 /* The narrow persistent segment (tw_sgd_segment_narrow) over ranks: this rank's n_shards
  * blocks (global shards shard_base..) push every step's gradients into every rank's peer
  * buffer and wait for all n_total shards on their own; the last update is applied in the

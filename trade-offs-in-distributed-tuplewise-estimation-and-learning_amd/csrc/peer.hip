@@ -12,32 +12,47 @@
 //  * the persistent narrow segment (csrc/sgdseg.hip, tw_sgd_segment_narrow_peer): C4's
 //    segments, the exchange inside the launch;
 //  * per step (any d, any gradient kernel; C5): the gradient launch writes the rank's
-//    (N/G, d) partials as usual, tw_peer_publish pushes them into every rank's per-step slot
-//    of the step's parity and adds this launch's arrivals to every rank's parity counter, and
-//    tw_peer_update waits for all ranks' arrivals on its own counter and applies k_sgd_update's
-//    arithmetic to the slot (same bits as the one-GPU update).  No host collective per step.
-// Counter reuse of the per-step form: update(t) waits for counter[t & 1] >= P * G (P publish
-// blocks per rank); publish(t + 1) zeroes this rank's counter[t & 1] (update(t) is done: stream
-// order) BEFORE its block 0 adds its arrivals, and a rank can add to counter[t & 1] again only
-// in publish(t + 2), after its update(t + 1) saw those arrivals.  Slots likewise: slot t & 1 of
-// a rank is rewritten by publish(t + 2), after every rank's update(t) has read it.
+//    (N/G, d) partials as usual, then ONE tw_peer_step launch pushes them into every rank's
+//    per-step slot of the step's parity, adds its arrivals to every rank's parity counter,
+//    waits for all ranks' arrivals on its own counter and applies k_sgd_update's arithmetic
+//    to the slot (same bits as the one-GPU update).  No host collective per step.
+// Counter reuse of the per-step form: step(t) waits for counter[t & 1] >= P * G (P blocks per
+// rank, a function of d); step(t + 1) zeroes this rank's counter[t & 1] (step(t) is done:
+// stream order) in its block 0, whose arrivals on the peers come after that store (vmcnt(0)),
+// and a peer can add to counter[t & 1] again only in step(t + 2), after its step(t + 1) saw
+// all of this rank's arrivals of step t + 1 — block 0's included.  Slots likewise: slot t & 1
+// of a rank is rewritten by step(t + 2), after every rank's step(t) has read it.
 #include "peer.h"
 #include <algorithm>
 #include <cstring>
 
 namespace tw {
 
-constexpr int kPubBlocks = 32;  // publish blocks per rank (all ranks the same: the target)
+// One launch per step after the gradient launch: its blocks push this rank's partials, then
+// wait for every rank's arrivals and update.  The grid is capped (kStepBlocks, blocks looping
+// over column groups) so that every rank's blocks are resident together: a waiting block holds
+// its CU, and a rank whose blocks could not start would never arrive (ranks co-resident on one
+// GPU in rehearsals included: 128 blocks of 32 KB LDS per rank, at least 10 ranks' grids fit).
+constexpr int kStepBlocks = 128, kPUpdCols = 8, kPUpdRows = 512;
 
-static int publish_blocks(int64_t words) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>(kPubBlocks, ceil_div(words, (int64_t)kBlock * 4)));
+static int step_blocks(int64_t d) {
+  return (int)std::min<int64_t>(kStepBlocks, ceil_div(d, (int64_t)kPUpdCols));
 }
 
-// this rank's (rows, d) partials -> rows [row0, row0 + rows) of every rank's slot `par`
-__global__ __launch_bounds__(kBlock) void k_peer_publish(const double* __restrict__ src,
-                                                         int64_t words, int64_t off,
-                                                         PeerSeg ps, int par,
-                                                         unsigned long long* reset) {
+// (1) this rank's (rows, d) partials -> rows [row0, row0 + rows) of every rank's slot `par`,
+//     then one arrival per block on every rank's counter of parity `par`;
+// (2) wait for P * G arrivals on this rank's counter, then k_sgd_update (csrc/hinge.hip) on the
+//     slot: the same shard-order sum from +0.0, /N, + reg * w, momentum — the same bits
+__global__ __launch_bounds__(kBlock) void k_peer_step(const double* __restrict__ src,
+                                                      int64_t words, int64_t off, PeerSeg ps,
+                                                      int par, unsigned long long* reset,
+                                                      uint64_t target, int n_shards, int64_t d,
+                                                      double* w, double* dw, double reg,
+                                                      double lr, double momentum,
+                                                      uint64_t* __restrict__ d_step,
+                                                      uint32_t* abort_word) {
+  __shared__ double tile[kPUpdRows * kPUpdCols];
+  __shared__ int s_ok;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(reset, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const size_t base = (size_t)par * ps.n_total + off;  // in words: ps.n_total holds N * d here
@@ -51,53 +66,42 @@ __global__ __launch_bounds__(kBlock) void k_peer_publish(const double* __restric
   if ((int)threadIdx.x < ps.G)
     __hip_atomic_fetch_add(ps.ctr[threadIdx.x], 1ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
-// k_sgd_update (csrc/hinge.hip) on the slot, once every rank's arrivals are in: the same
-// shard-order sum from +0.0, /N, + reg * w, momentum — the same bits
-constexpr int kPUpdCols = 8, kPUpdRows = 1024;
-__global__ __launch_bounds__(kBlock) void k_peer_update(double* w, double* dw,
-                                                        const double* __restrict__ slot,
-                                                        const unsigned long long* ctr,
-                                                        uint64_t target, int n_shards,
-                                                        int64_t d, double reg, double lr,
-                                                        double momentum,
-                                                        uint64_t* __restrict__ d_step,
-                                                        uint32_t* abort_word) {
-  __shared__ double tile[kPUpdRows * kPUpdCols];
-  __shared__ int s_ok;
-  if (!peer_wait(ctr, target, abort_word, &s_ok)) return;
+  if (!peer_wait(ps.my_ctr, target, abort_word, &s_ok)) return;
   if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += 1;
-  const int64_t j0 = (int64_t)blockIdx.x * kPUpdCols;
-  const int nc = (int)std::min<int64_t>(kPUpdCols, d - j0);
-  double sum = 0.0;
-  for (int s0 = 0; s0 < n_shards; s0 += kPUpdRows) {
-    const int ns = std::min(kPUpdRows, n_shards - s0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < ns * kPUpdCols; e += kBlock) {
-      const int r = e / kPUpdCols, c = e - r * kPUpdCols;
-      tile[e] = c < nc ? ld_sys(slot + (int64_t)(s0 + r) * d + j0 + c) : 0.0;
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < nc) {
-      int r = 0;
-      for (; r + 8 <= ns; r += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * kPUpdCols + threadIdx.x];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) sum += v[u];
+  const double* slot = ps.my_slot + (size_t)par * ps.n_total;
+  for (int64_t j0 = (int64_t)blockIdx.x * kPUpdCols; j0 < d;
+       j0 += (int64_t)gridDim.x * kPUpdCols) {
+    const int nc = (int)std::min<int64_t>(kPUpdCols, d - j0);
+    double sum = 0.0;
+    for (int s0 = 0; s0 < n_shards; s0 += kPUpdRows) {
+      const int ns = std::min(kPUpdRows, n_shards - s0);
+      __syncthreads();
+      for (int e = threadIdx.x; e < ns * kPUpdCols; e += kBlock) {
+        const int r = e / kPUpdCols, c = e - r * kPUpdCols;
+        tile[e] = c < nc ? ld_sys(slot + (int64_t)(s0 + r) * d + j0 + c) : 0.0;
       }
-      for (; r < ns; ++r) sum += tile[r * kPUpdCols + threadIdx.x];
+      __syncthreads();
+      if ((int)threadIdx.x < nc) {
+        int r = 0;
+        for (; r + 8 <= ns; r += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * kPUpdCols + threadIdx.x];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sum += v[u];
+        }
+        for (; r < ns; ++r) sum += tile[r * kPUpdCols + threadIdx.x];
+      }
     }
-  }
-  if ((int)threadIdx.x < nc) {
-    const int64_t j = j0 + threadIdx.x;
-    const double wj = w[j];
-    const double g = sum / (double)n_shards + reg * wj;
-    const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
-    dw[j] = step;
-    w[j] = wj - step;
+    if ((int)threadIdx.x < nc) {
+      const int64_t j = j0 + threadIdx.x;
+      const double wj = w[j];
+      const double g = sum / (double)n_shards + reg * wj;
+      const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
+      dw[j] = step;
+      w[j] = wj - step;
+    }
   }
 }
 
@@ -199,52 +203,38 @@ extern "C" int tw_peer_close(void* d_ptr) {
   return TW_OK;
 }
 
-// per-step form: this rank's `words` partial words (rows shard_base.. of the global order,
-// d columns) into every rank's per-step slot of parity `par`, arrivals added; words_pad: the
-// most words any rank publishes (uneven shard splits), which fixes the blocks per rank
-extern "C" int tw_peer_publish(const double* d_grads_loc, int64_t words, int64_t words_pad,
-                               int64_t offset_words, void* const* d_peer_bases, int32_t G,
-                               int32_t rank, int32_t n_total, int64_t d, int32_t par,
-                               void* stream) {
+// per-step form, one launch after the gradient launch: this rank's `words` partial words
+// (rows shard_base.. of the global order, d columns; offset_words = shard_base * d) into every
+// rank's per-step slot of parity `par` with this launch's arrivals; then, once every rank's
+// arrivals of that parity are in, k_sgd_update's arithmetic on this rank's slot
+extern "C" int tw_peer_step(const double* d_grads_loc, int64_t words, int64_t offset_words,
+                            void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total,
+                            int64_t d, int32_t par, double* d_w, double* d_dw, double reg,
+                            double lr, double momentum, uint64_t* d_step, uint32_t* d_abort,
+                            void* stream) {
   TW_ARG_CHECK(d_peer_bases != nullptr && G >= 1 && G <= kPeerMax && rank >= 0 && rank < G &&
-                   n_total >= 1 && d >= 1 && words >= 0 && words_pad >= words &&
-                   words_pad >= 1 && offset_words >= 0 &&
+                   n_total >= 1 && d >= 1 && words >= 0 && offset_words >= 0 &&
                    offset_words + words <= (int64_t)n_total * d && (par == 0 || par == 1),
-               "tw_peer_publish: bad sizes");
+               "tw_peer_step: bad sizes");
+  TW_ARG_CHECK(d_w && d_dw && d_abort, "tw_peer_step: w, dw and the abort word required");
   PeerSeg ps{};
   const size_t step_slots = kPeerHdr + sizeof(double) * peer_slots_words(n_total, d);
   for (int p = 0; p < G; ++p) {
     char* b = (char*)d_peer_bases[p];
-    TW_ARG_CHECK(b != nullptr, "tw_peer_publish: rank %d's buffer missing", p);
+    TW_ARG_CHECK(b != nullptr, "tw_peer_step: rank %d's buffer missing", p);
     ps.slot[p] = (double*)(b + step_slots);
     ps.ctr[p] = (unsigned long long*)(b + kPeerStepCtr + 64 * par);
   }
+  char* mine = (char*)d_peer_bases[rank];
   ps.G = G;
   ps.n_total = (int)((int64_t)n_total * d);  // one slot's words
-  auto* reset = (unsigned long long*)((char*)d_peer_bases[rank] + kPeerStepCtr + 64 * (1 - par));
-  hipLaunchKernelGGL(k_peer_publish, dim3(publish_blocks(words_pad)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_grads_loc, words, offset_words, ps, par, reset);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
-}
-
-// per-step form: wait until every rank's publish of parity `par` is in (G ranks, publishing
-// with words_pad = words_per_rank), then k_sgd_update on the slot
-extern "C" int tw_peer_update(double* d_w, double* d_dw, void* d_my_base, int32_t n_total,
-                              int64_t d, int64_t words_per_rank, int32_t G, int32_t par,
-                              double reg, double lr, double momentum, uint64_t* d_step,
-                              uint32_t* d_abort, void* stream) {
-  TW_ARG_CHECK(d_w && d_dw && d_my_base && d_abort && n_total >= 1 && d >= 1 && G >= 1 &&
-                   words_per_rank >= 1 && (par == 0 || par == 1),
-               "tw_peer_update: bad arguments");
-  char* b = (char*)d_my_base;
-  const size_t step_slots = kPeerHdr + sizeof(double) * peer_slots_words(n_total, d);
-  const double* slot = (const double*)(b + step_slots) + (size_t)par * n_total * d;
-  const auto* ctr = (const unsigned long long*)(b + kPeerStepCtr + 64 * par);
-  const uint64_t target = (uint64_t)publish_blocks(words_per_rank) * (uint64_t)G;
-  hipLaunchKernelGGL(k_peer_update, dim3((unsigned)ceil_div(d, (int64_t)kPUpdCols)), dim3(kBlock),
-                     0, (hipStream_t)stream, d_w, d_dw, slot, ctr, target, n_total, d, reg, lr,
-                     momentum, d_step, d_abort);
+  ps.my_ctr = (unsigned long long*)(mine + kPeerStepCtr + 64 * par);
+  ps.my_slot = (const double*)(mine + step_slots);
+  auto* reset = (unsigned long long*)(mine + kPeerStepCtr + 64 * (1 - par));
+  const int P = step_blocks(d);  // the same on every rank: d is
+  hipLaunchKernelGGL(k_peer_step, dim3(P), dim3(kBlock), 0, (hipStream_t)stream, d_grads_loc,
+                     words, offset_words, ps, par, reset, (uint64_t)P * (uint64_t)G, n_total, d,
+                     d_w, d_dw, reg, lr, momentum, d_step, d_abort);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

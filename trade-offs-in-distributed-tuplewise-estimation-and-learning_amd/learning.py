@@ -66,7 +66,7 @@ NATIVE_DRAWS = True
 REPLAY_THROUGH = True
 PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each segment's draws
 # learning over ranks: the shard gradients exchanged by the GPUs through IPC-mapped peer buffers
-# (csrc/peer.hip: the persistent narrow segment, or per step a publish + wait-and-update launch)
+# (csrc/peer.hip: the persistent narrow segment, or per step one publish-wait-update launch)
 # instead of a host-enqueued RCCL all-gather per step; False keeps the all-gather (A/B)
 PEER_EXCHANGE = True
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
@@ -477,15 +477,13 @@ class SGDEngine:
         if self.vgroup is not None:  # MultiDeviceSGD gathers the slots' gradients, then updates
             return
         if self.peer is not None:
-            # publish this rank's partials into every rank's slot, wait for all, update
-            s, par = L.stream_handle(), self.peer.pstep & 1
+            # one launch: this rank's partials into every rank's slot, wait for all, update
+            par = self.peer.pstep & 1
             self.peer.pstep += 1
-            nw, npad = self.N_loc * self.d, self.N_pad * self.d
-            L.call("tw_peer_publish", L.ptr(self.grads_loc), nw, npad, self.shard_base * self.d,
-                   self.peer.bases, self.G, self.rank, self.N, self.d, par, s)
-            L.call("tw_peer_update", L.ptr(self.w), L.ptr(self.dw), self.peer.mine, self.N,
-                   self.d, npad, self.G, par, self.reg, self.lr, self.momentum,
-                   L.ptr(self.step_ctr), L.ptr(self._ctl[1:]), s)
+            L.call("tw_peer_step", L.ptr(self.grads_loc), self.N_loc * self.d,
+                   self.shard_base * self.d, self.peer.bases, self.G, self.rank, self.N, self.d,
+                   par, L.ptr(self.w), L.ptr(self.dw), self.reg, self.lr, self.momentum,
+                   L.ptr(self.step_ctr), L.ptr(self._ctl[1:]), L.stream_handle())
             return
         if self.coll:
             if self.even:
