@@ -7,7 +7,9 @@ a device copy of the send buffer standing in for the all-to-all (the same bytes;
 transfer is not simulated), the unpack, (round 5) a device copy standing in for the Z
 all-gather and the local part of the counts' reduction, one count launch of K x 64/G bags and the inverse-chain
 gather of the rank's final arrays.  Reports ms per call and the efficiency against the one-GPU
-call / G.  Run on the GPU box:
+call / G.  Round 5: the efficiency takes both ranks' UNinstrumented times (the per-part event
+markers of the parts run cost a G = 8 rank's K = 4 call ~0.07 ms, which the round-4 figure
+charged to rank G - 1).  Run on the GPU box:
     python tools/chain_probe.py [K ...]"""
 import pathlib
 import sys
@@ -104,12 +106,13 @@ def rank_call(G, r, K, parts=False):
         xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
         for i0 in range(0, K, C):
             c = min(C, K - i0)
+            first = i0 == 0
             if G == 1:  # one process: straight into the bags
-                mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, 0, 1,
+                mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, 0, 1,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                     x_bag=x_bag, z_bag=z_bag, cursors=cur))
             else:
-                mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, r, G,
+                mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, r, G,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                     send=send, cap=cap, flag=flag))
                 sz = G * c * (cap + 1)
@@ -133,15 +136,16 @@ def rank_call(G, r, K, parts=False):
 
 
 for K in Ks:
+    one_gpu_call(K, True)  # warm: the process's first calls run before the clock has risen
     ch, ch_host = one_gpu_call(K, True)
     st, st_host = one_gpu_call(K, False)
     print(f"K={K}: one GPU, step chains {ch:.3f} ms/call ({ch / K:.4f} ms/step; host "
           f"{ch_host:.3f}); one launch per step {st:.3f} ms/call ({st / K:.4f} ms/step)",
           flush=True)
     for G in (1, 2, 4, 8):
-        ms, host, _ = rank_call(G, 0, K)
-        ms_l, _, parts = rank_call(G, G - 1, K, parts=True)
-        worst = max(ms, ms_l)
-        print(f"  G={G}: rank 0 {ms:.3f} ms/call, rank {G - 1} {ms_l:.3f}; ideal (one-GPU "
-              f"chain call / G) {ch / G:.3f}; efficiency {ch / G / worst:.3f}; parts "
+        ms = [rank_call(G, r, K)[0] for r in sorted({0, G - 1})]
+        _, _, parts = rank_call(G, G - 1, K, parts=True)
+        print(f"  G={G}: ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
+              + f" ms/call; ideal (one-GPU chain call / G) {ch / G:.3f}; efficiency "
+              f"{ch / G / max(ms):.3f}; parts (instrumented rank {G - 1}) "
               + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()), flush=True)

@@ -45,10 +45,12 @@ namespace tw {
 
 // ----------------------------------------------------------------------------- images
 // g(v) = #{z : key(z) < key(v)} for all n + m elements, from a structure over Z alone:
-//  1. a sample of Z at hashed positions, sorted in one block: B - 1 splitter keys;
+//  1. a sample of Z at hashed positions, sorted (by counting, over C / 128 blocks from C = 1024
+//     keys): B - 1 splitter keys;
 //  2. z -> bucket: 2j for the keys strictly between splitters j-1 and j, 2j + 1 for keys EQUAL
 //     to splitter j (heavy ties land there: no z of such a bucket is below any of its values);
-//     per-block histograms, their prefix per bucket, and the z keys scattered bucket by bucket;
+//     per-block histograms (each z's bucket kept), their prefix per bucket, and the z keys
+//     scattered bucket by bucket (the bucket starts scanned in the scatter blocks);
 //  3. per interval bucket, a counting sort of its z keys over 2048 sub-buckets by a monotone map
 //     (linear in the value or in the order key, whichever spreads the bucket's z better; so
 //     sub(z) < sub(v) => z < v), into a second key array, with the sub-bucket prefix table;
@@ -83,17 +85,40 @@ __device__ __forceinline__ int64_t sample_index(int i, int64_t m) {
   return (int64_t)(((uint64_t)mix32((uint32_t)i * 0x9E3779B1u + 0x7F4A7C15u) * (uint64_t)m) >> 32);
 }
 
-// the sample of C >= 1024 keys (Z beyond kRkSmallM): drawn, then bitonic-sorted (sortkeys.h)
-// by C / 4 threads in the same launch (counting costs C compares per key: 27 us at C = 1024)
+// the sample of C >= 1024 keys (Z beyond kRkSmallM), sorted by counting over C / 128 blocks
+// (one block's bitonic network was a serial chain of ~50 shuffle levels: 16 us at C = 1024,
+// the longest of the ranking's structure launches): every block draws the whole sample into
+// LDS (cs hashed positions of z, padded with ~0) and places 128 of its keys — key i goes to
+// #{j : k_j < k_i} + #{j < i : k_j == k_i}, eight threads per key each counting a C / 8 share
+// (a wave's lanes hold different keys and read the same k_j: LDS broadcasts), the shares
+// added with LDS atomics.  The sorted array is the bitonic one's, key for key.
+constexpr int kRkSampPlace = 128;  // keys placed per block
 template <typename T>
-__global__ __launch_bounds__(kRkSample / 4) void k_rank_sample_bitonic(const T* __restrict__ z,
-                                                                       int64_t m, int cs, int C,
-                                                                       uint64_t* __restrict__ ss) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t skeys_lds[];
-  for (int i = threadIdx.x; i < C; i += blockDim.x)
-    skeys_lds[i] = i < cs ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+__global__ __launch_bounds__(1024) void k_rank_sample_count(const T* __restrict__ z, int64_t m,
+                                                            int cs, int C,
+                                                            uint64_t* __restrict__ ss) {
+  __shared__ uint64_t keys[kRkSample];
+  __shared__ uint32_t cnt[kRkSampPlace];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < C; i += 1024) keys[i] = i < cs ? order_key<T>(z[sample_index(i, m)]) : ~0ull;
+  if (tid < kRkSampPlace) cnt[tid] = 0;
   __syncthreads();
-  sort_keys_block<4>(skeys_lds, C, ss);
+  constexpr int kParts = 1024 / kRkSampPlace;
+  const int q = tid % kRkSampPlace, part = tid / kRkSampPlace;
+  const int i = (int)blockIdx.x * kRkSampPlace + q;
+  const uint64_t ki = keys[i];
+  const int span = C / kParts, j0 = part * span;  // a multiple of 4 (C >= 1024)
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  for (int j = j0; j < j0 + span; j += 4) {
+    const uint64_t a = keys[j], b = keys[j + 1], c = keys[j + 2], d = keys[j + 3];
+    c0 += (a < ki || (a == ki && j < i)) ? 1u : 0u;
+    c1 += (b < ki || (b == ki && j + 1 < i)) ? 1u : 0u;
+    c2 += (c < ki || (c == ki && j + 2 < i)) ? 1u : 0u;
+    c3 += (d < ki || (d == ki && j + 3 < i)) ? 1u : 0u;
+  }
+  atomicAdd(&cnt[q], c0 + c1 + c2 + c3);
+  __syncthreads();
+  if (tid < kRkSampPlace) ss[cnt[tid]] = keys[(int)blockIdx.x * kRkSampPlace + tid];
 }
 
 // the sample drawn and sorted in one block: keys of z at cs hashed positions, padded with ~0
@@ -186,7 +211,8 @@ __device__ __forceinline__ int load_splitters(const uint64_t* __restrict__ ss, c
 template <typename T, int PER>
 __global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ z, RankGeo g,
                                                           const uint64_t* __restrict__ ss,
-                                                          uint32_t* __restrict__ rel) {
+                                                          uint32_t* __restrict__ rel,
+                                                          uint16_t* __restrict__ bid) {
   __shared__ uint64_t sp[kRkMaxB];
   __shared__ uint32_t h[2 * kRkMaxB];
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads) h[b] = 0;
@@ -199,8 +225,14 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ 
   }
   const int nsp = load_splitters(ss, g, sp);
 #pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (e0 + k * kRkThreads < g.m) atomicAdd(&h[rank_bucket(sp, nsp, order_key<T>(zv[k]))], 1u);
+  for (int k = 0; k < PER; ++k) {
+    const int64_t e = e0 + k * kRkThreads;
+    if (e < g.m) {
+      const int b = rank_bucket(sp, nsp, order_key<T>(zv[k]));
+      atomicAdd(&h[b], 1u);
+      bid[e] = (uint16_t)b;  // the scatter pass reads it instead of searching again
+    }
+  }
   __syncthreads();
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
     rel[(int64_t)b * g.nblk + blockIdx.x] = h[b];
@@ -292,48 +324,55 @@ __global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* 
   if (t < g.NB) start[t] = before + inc - own;
 }
 
-// pass 2b: bucket starts = the z count below every bucket (one block, NB <= 1024)
-__global__ __launch_bounds__(1024) void k_rank_starts(RankGeo g, const uint32_t* __restrict__ total,
-                                                      uint32_t* __restrict__ start) {
-  __shared__ uint32_t a[1024];
-  const int t = threadIdx.x;
-  a[t] = t < g.NB ? total[t] : 0u;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t v = t >= o ? a[t - o] : 0u;
-    __syncthreads();
-    a[t] += v;
-    __syncthreads();
-  }
-  if (t < g.NB) start[t] = a[t] - total[t];
-}
-
-// pass 3: the z keys into their buckets' slots (order inside a bucket is free)
+// pass 3: the z keys into their buckets' slots (order inside a bucket is free), by the bucket
+// ids the histogram pass kept (no second splitter search).  The bucket starts — the z count
+// below every bucket, an exclusive scan of the NB <= 512 totals — are made by every block in
+// LDS (two per thread, wave scans) and stored by block 0 for the sub-sort and record passes:
+// one launch fewer than a separate scan kernel.
 template <typename T, int PER>
 __global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict__ z, RankGeo g,
-                                                             const uint64_t* __restrict__ ss,
+                                                             const uint16_t* __restrict__ bid,
                                                              const uint32_t* __restrict__ rel,
-                                                             const uint32_t* __restrict__ start,
+                                                             const uint32_t* __restrict__ total,
+                                                             uint32_t* __restrict__ start,
                                                              uint64_t* __restrict__ bkeys) {
-  __shared__ uint64_t sp[kRkMaxB];
+  static_assert(2 * kRkMaxB <= 2 * kRkThreads, "two bucket totals per thread");
   __shared__ uint32_t cur[2 * kRkMaxB];
-  for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
-    cur[b] = start[b] + rel[(int64_t)b * g.nblk + blockIdx.x];
+  __shared__ uint32_t wsum[kRkThreads / kWave];
   const int64_t e0 = (int64_t)blockIdx.x * kRkThreads * PER + threadIdx.x;
   T zv[PER];
+  uint32_t bv[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int64_t e = e0 + k * kRkThreads;
     zv[k] = e < g.m ? z[e] : (T)0;
+    bv[k] = e < g.m ? bid[e] : 0u;
   }
-  const int nsp = load_splitters(ss, g, sp);
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const uint32_t a0 = 2 * t < g.NB ? total[2 * t] : 0u;
+  const uint32_t a1 = 2 * t + 1 < g.NB ? total[2 * t + 1] : 0u;
+  uint32_t inc = a0 + a1;
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    if (e0 + k * kRkThreads < g.m) {
-      const uint64_t key = order_key<T>(zv[k]);
-      bkeys[atomicAdd(&cur[rank_bucket(sp, nsp, key)], 1u)] = key;
-    }
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += u;
   }
+  if (lane == kWave - 1) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t ex = inc - (a0 + a1);
+  for (int w = 0; w < wid; ++w) ex += wsum[w];
+  if (2 * t < g.NB) {
+    cur[2 * t] = ex + rel[(int64_t)(2 * t) * g.nblk + blockIdx.x];
+    if (blockIdx.x == 0) start[2 * t] = ex;
+  }
+  if (2 * t + 1 < g.NB) {
+    cur[2 * t + 1] = ex + a0 + rel[(int64_t)(2 * t + 1) * g.nblk + blockIdx.x];
+    if (blockIdx.x == 0) start[2 * t + 1] = ex + a0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (e0 + k * kRkThreads < g.m) bkeys[atomicAdd(&cur[bv[k]], 1u)] = order_key<T>(zv[k]);
 }
 
 // The sub-bucket map of an interval bucket, one of two monotone maps (sub(z) < sub(v) => z < v),
@@ -670,6 +709,7 @@ struct RankWork {
   void* samp;
   uint64_t *ss, *bkeys, *skeys;
   uint32_t *rel, *total, *start, *subp;
+  uint16_t* bid;  // each z's bucket (the histogram pass -> the scatter pass)
   SubMap* maps;
   size_t total_bytes;
 };
@@ -715,6 +755,7 @@ static RankWork rank_work(const RankGeo& g, char* base) {
   w.maps = (SubMap*)take(sizeof(SubMap) * (size_t)g.B);
   w.bkeys = (uint64_t*)take(8 * (size_t)std::max<int64_t>(g.m, 1));
   w.skeys = (uint64_t*)take(8 * (size_t)std::max<int64_t>(g.m, 1));
+  w.bid = (uint16_t*)take(2 * (size_t)std::max<int64_t>(g.m, 1));
   w.total_bytes = off;
   return w;
 }
@@ -926,23 +967,22 @@ static int rank_images_t(const T* xq, const T* zq, const T* z, int64_t m, const 
       hipLaunchKernelGGL((k_rank_sample_sort<T>), dim3(1), dim3(1024), 0, st, z, m, g.cs, g.C,
                          w.ss);
     else
-      hipLaunchKernelGGL((k_rank_sample_bitonic<T>), dim3(1), dim3(g.C / 4), g.C * 8, st, z, m,
-                         g.cs, g.C, w.ss);
+      hipLaunchKernelGGL((k_rank_sample_count<T>), dim3(g.C / kRkSampPlace), dim3(1024), 0, st,
+                         z, m, g.cs, g.C, w.ss);
     TW_LAUNCH_CHECK();
     auto passes = [&](auto per) {
       constexpr int PER = decltype(per)::value;
       hipLaunchKernelGGL((k_rank_hist<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
-                         w.ss, w.rel);
-      if (g.nblk <= 2 * kWave) {  // small Z: rows and starts in one block
+                         w.ss, w.rel, w.bid);
+      if (g.nblk <= 2 * kWave)  // small Z: rows (and starts) in one block
         hipLaunchKernelGGL(k_rank_rows_starts, dim3(1), dim3(1024), 0, st, g, w.rel, w.total,
                            w.start);
-      } else {
+      else
         hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
                            dim3(kBlock), 0, st, g, w.rel, w.total);
-        hipLaunchKernelGGL(k_rank_starts, dim3(1), dim3(1024), 0, st, g, w.total, w.start);
-      }
+      // the starts: made (again, for the small path) by the scatter blocks
       hipLaunchKernelGGL((k_rank_scatter<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
-                         w.ss, w.rel, w.start, w.bkeys);
+                         w.bid, w.rel, w.total, w.start, w.bkeys);
     };
     if (g.per == 4)
       passes(std::integral_constant<int, 4>());
