@@ -893,6 +893,12 @@ int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t
  * i = n-1 down to 1; j[0] untouched), advancing the state as the shuffle would: the host half
  * of the device shuffle below.  Returns 2 on bad arguments. */
 int tw_np_shuffle_draws32(uint32_t* key, int32_t* pos, int64_t n, uint32_t* j);
+/* The same draws for i = hi down to lo only (1 <= lo <= hi < n; j is the shuffle's n-entry
+ * array, other entries untouched), the state advanced past them: consecutive ranges from
+ * hi = n - 1 down to lo = 1 make exactly tw_np_shuffle_draws32's draws (the streamed last
+ * shuffle of the drop-in).  Returns 2 on bad arguments. */
+int tw_np_shuffle_draws32_range(uint32_t* key, int32_t* pos, int64_t n, int64_t hi, int64_t lo,
+                                uint32_t* j);
 
 /* ---- Device shuffle swaps (csrc/devshuffle.hip): the swaps of np.random.shuffle(x) and
  * np.random.shuffle(z) (UN's in-place shuffles, compute_stats.py:66-67,
@@ -913,6 +919,18 @@ int tw_shuffle_swaps_set_tail(int32_t on);
 int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz, const uint32_t* d_jx,
                      const uint32_t* d_jz, int32_t first, int32_t round0, void* d_work,
                      uint32_t* d_pending, void* stream);
+/* The draw windows of the rounds: iterations enter in W = tw_shuffle_swaps_windows() chunks of
+ * p = ceil((n - 1) / W) draws, window c holding i in [max(1, n - (c + 1) p), n - c p). */
+int32_t tw_shuffle_swaps_windows(void);
+/* The first batch (first = 1, round0 = 0) of tw_shuffle_swaps enqueued in parts as the draws
+ * arrive: rounds [r_begin, r_end) — round r reads windows 0 .. r + 1, so with windows [0, c)
+ * on the device r_end = c - 1 (< W); r_begin = 0 also clears the workspace and reserves round
+ * 0; last != 0 enqueues the remaining rounds, the tail and *d_pending (r_end ignored).  The
+ * parts in sequence (each r_begin = the previous r_end) equal one tw_shuffle_swaps call. */
+int tw_shuffle_swaps_part(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz,
+                          const uint32_t* d_jx, const uint32_t* d_jz, int32_t r_begin,
+                          int32_t r_end, int32_t last, void* d_work, uint32_t* d_pending,
+                          void* stream);
 
 #ifdef __cplusplus
 }

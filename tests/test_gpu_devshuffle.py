@@ -55,6 +55,32 @@ def test_device_shuffle_snapshots_match_numpy(gpu, nx, nz, dtype, rounds, tail):
         assert np.array_equal(zs[k].cpu().numpy(), want_z[k])
 
 
+@pytest.mark.parametrize("nx,nz", [(0, 1), (3, 2), (1000, 17), (4099, 65537),
+                                   (1_000_000, 1_000_000)])
+@pytest.mark.parametrize("pieces", [1, 3, 4, 16])
+def test_streamed_z_shuffle_matches_numpy(gpu, nx, nz, pieces):
+    """DeviceShuffles.draw_push_z_streamed (the drop-in's last shuffle drawn and swapped in
+    window groups: tw_np_shuffle_draws32_range + tw_shuffle_swaps_part) == NumPy's in-place
+    shuffles, every state, and the RNG state after; T = 2, both Z shuffles streamed."""
+    from tuplewise import _engine as E
+    from tuplewise.numpy_rng import shuffle_draws32
+    rs = np.random.RandomState(nx + 7 * nz)
+    X, Z = rs.normal(size=nx), rs.normal(size=nz)
+    want_x, want_z, probe = _numpy_snapshots(X, Z, 2, 13)
+    np.random.seed(13)
+    np.random.random(2)
+    ds = E.DeviceShuffles(X, Z, 2)
+    for _ in range(2):
+        shuffle_draws32(nx, out=ds.draw_x())
+        ds.push_x()
+        ds.draw_push_z_streamed(pieces)
+    assert np.array_equal(np.random.randint(0, 2 ** 31, 3), probe)
+    xs, zs = ds.finish()
+    for k in range(2):
+        assert np.array_equal(xs[k].cpu().numpy(), want_x[k])
+        assert np.array_equal(zs[k].cpu().numpy(), want_z[k])
+
+
 def _call(fn, X, Z, seed):
     X, Z = X.copy(), Z.copy()
     np.random.seed(seed)
@@ -99,6 +125,35 @@ def test_drop_in_device_shuffles_equal_host_path(gpu, name, make):
         dev = _call(fn, X, Z, 21)
     finally:
         Bk.DEVICE_SHUFFLE_MIN = old
+    assert dev[0] == host[0] and type(dev[0]) is type(host[0])
+    for a, b in zip(dev[1:], host[1:]):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("early,pieces,threaded", [(False, 0, False), (True, 0, False),
+                                                   (False, 4, False), (True, 16, False),
+                                                   (False, 0, True), (True, 4, True)])
+@pytest.mark.parametrize("name", ["est.UnNT prop-SWOR", "est.UnNT SWOR", "est.UnNT half",
+                                  "cs.UnNT AUC", "est.UnNT prop-SWR"])
+def test_drop_in_pipelining_equals_host_path(gpu, name, early, pieces, threaded, monkeypatch):
+    """The drop-in's round-5 pipelining switched on and off (_blocks.EARLY_COUNTS: step k
+    counted while step k + 1 is drawn; STREAM_LAST_SHUFFLE: the last shuffle in parts;
+    THREADED_LAUNCHES: uploads and launches on the launcher thread): the value, the post-call
+    arrays and the RNG state equal the host path's in every setting."""
+    import tuplewise.compute_stats as cs
+    import tuplewise.estimation as est
+    from tuplewise import _blocks as Bk
+    fn = dict(CASES)[name](est, cs)
+    rs = np.random.RandomState(4)
+    X = np.round(rs.normal(0.3, 1, 30001), 2)
+    Z = np.round(rs.normal(0, 1, 25000), 2)
+    monkeypatch.setattr(Bk, "DEVICE_SHUFFLE_MIN", 1 << 40)
+    host = _call(fn, X, Z, 5)
+    monkeypatch.setattr(Bk, "DEVICE_SHUFFLE_MIN", 0)
+    monkeypatch.setattr(Bk, "EARLY_COUNTS", early)
+    monkeypatch.setattr(Bk, "STREAM_LAST_SHUFFLE", pieces)
+    monkeypatch.setattr(Bk, "THREADED_LAUNCHES", threaded)
+    dev = _call(fn, X, Z, 5)
     assert dev[0] == host[0] and type(dev[0]) is type(host[0])
     for a, b in zip(dev[1:], host[1:]):
         assert np.array_equal(a, b)

@@ -215,6 +215,29 @@ def test_shuffle_draws32_are_numpy_shuffle_draws(tw, n):
         assert np.array_equal(np.array(b, dtype=np.int64), a)
 
 
+@pytest.mark.parametrize("n", [2, 3, 17, 1000, 65537, 200003])
+@pytest.mark.parametrize("cuts", [1, 2, 4, 16, 37])
+def test_shuffle_draws32_range_pieces_equal_whole(tw, n, cuts):
+    """numpy_rng.shuffle_draws32_range in consecutive ranges (hi = n - 1 down to lo = 1, the
+    streamed last shuffle of the drop-in) == one shuffle_draws32(n): the same draws and the
+    same RNG state after (cuts 37: ranges that split the mask ranges and SIMD batches)."""
+    from tuplewise.numpy_rng import shuffle_draws32, shuffle_draws32_range
+    np.random.seed(5)
+    np.random.random(7)
+    want = shuffle_draws32(n)
+    probe = np.random.randint(0, 2 ** 31, 3)
+    np.random.seed(5)
+    np.random.random(7)
+    got = np.zeros(n, dtype=np.uint32)
+    edges = sorted({int(e) for e in np.linspace(n - 1, 0, cuts + 1)})[::-1]
+    for hi, lo in zip(edges[:-1], edges[1:]):
+        hi_i = hi if hi == n - 1 else hi - 1
+        if hi_i >= max(lo, 1):
+            shuffle_draws32_range(n, hi_i, max(lo, 1), got)
+    assert np.array_equal(np.random.randint(0, 2 ** 31, 3), probe)
+    assert np.array_equal(got[1:], want[1:])
+
+
 @pytest.mark.parametrize("in_place", [True, False])
 def test_state_in_place_and_copied_paths(tw, in_place, monkeypatch):
     """The native draws advance NumPy's own MT19937 struct in place (numpy_rng._mt_state) or,

@@ -209,12 +209,51 @@ class CompleteCount(BlockSpec):
     def evaluate_device(self, xd, zd, blocks):
         """evaluate() on float64 device arrays (the device-shuffle path of run_un_repeated):
         `X > Z` and the literal `(X - Z) > 0` are the same ordered comparison on doubles."""
+        done = self.enqueue_device(xd, zd, blocks)
+        if done is not None:
+            return done()
         mode = "half" if self.tie_mode == "half" else "gt"
         xa, xo = _layout(xd, blocks, "x")
         za, zo = _layout(zd, blocks, "z")
         sh = E.Shards(xa, xo, za, zo, L.TW_F64)
         sh._x_off_dev, sh._z_off_dev = L.to_device_many([xo, zo])  # one upload for both
-        counts = E.count_complete(sh, mode)
+        return self._ratios(E.count_complete(sh, mode), xo, zo, mode)
+
+    def enqueue_device(self, xd, zd, blocks, stream=None, after=()):
+        """evaluate_device in two halves, for blocks that are consecutive slices of xd / zd
+        (the SWOR / prop-SWOR plans; None otherwise): the offsets go up on the current stream,
+        then the count is enqueued — on `stream` when given, ordered after the upload and the
+        streams in `after` (the arrays' producers); returns done() -> the values (one sync,
+        ordered after the count on the caller's current stream)."""
+        t = L.torch()
+        xo, zo = _slice_offsets(blocks, "x"), _slice_offsets(blocks, "z")
+        if xo is None or zo is None:
+            return None
+        mode = "half" if self.tie_mode == "half" else "gt"
+        xod, zod = L.to_device_many([xo, zo], pinned=stream is not None)
+        mx, mz = int(np.diff(xo).max()), int(np.diff(zo).max())
+        pred = L.TW_PRED_HALF if mode == "half" else L.TW_PRED_GT
+        algo = E.pick_algo("auto", mx, mz, mode)
+        if stream is None:
+            dev = E.count_launch(xd, xod, zd, zod, len(blocks), mx, mz, L.TW_F64, pred, algo)
+        else:
+            stream.wait_stream(t.cuda.current_stream())
+            for s in after:
+                stream.wait_stream(s)
+            with t.cuda.stream(stream):
+                for a in (xod, zod, xd, zd):
+                    a.record_stream(stream)  # read there; the caller may drop them meanwhile
+                dev = E.count_launch(xd, xod, zd, zod, len(blocks), mx, mz, L.TW_F64, pred,
+                                     algo)
+
+        def done():
+            if stream is not None:
+                t.cuda.current_stream().wait_stream(stream)
+            return self._ratios(E._counts_to_host(dev), xo, zo, mode)
+        return done
+
+    @staticmethod
+    def _ratios(counts, xo, zo, mode):
         # float64(count) / float64(pairs) per block, as E.ratio: both conversions exact
         # (counts and pairs < 2^53 here) and one IEEE division each — the same bits, vectorised
         pairs = np.diff(xo).astype(np.int64) * np.diff(zo).astype(np.int64)
@@ -484,6 +523,13 @@ DEVICE_SHUFFLE_MIN = 1 << 16
 # study hook (tools/time_dropin_parts.py): a list receives (label, perf_counter) marks of the
 # device-shuffle drop-in call
 DROPIN_MARKS = None
+# the device-shuffle drop-in's pipelining (round 5): the counts of step k enqueued while the
+# host draws step k + 1; the call's last shuffle drawn and pushed in this many parts (0: whole)
+EARLY_COUNTS = True
+STREAM_LAST_SHUFFLE = 8
+# ... and the uploads, swap-round launches and count enqueues made on a launcher thread
+# (_engine.launcher), off the thread that makes the draws
+THREADED_LAUNCHES = True
 
 
 def _mark(label):
@@ -518,55 +564,93 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
     reference's order (the T shuffles' index draws, numpy_rng.shuffle_draws32, interleaved with
     the block draws), the device applies the T shuffles to one upload of X and Z keeping every
     state (_engine.shuffle_snapshots_device: the sequential swaps' permutation, bit for bit),
-    the T x N blocks are counted on those states in one launch, and the caller's arrays receive
-    the last state (the in-place side effect of the T np.random.shuffle calls)."""
+    the blocks are counted on those states, and the caller's arrays receive the last state (the
+    in-place side effect of the T np.random.shuffle calls).  Round 5: every upload and launch
+    is made by a launcher thread while this thread draws (THREADED_LAUNCHES), the counts of
+    step k are enqueued on their own stream once step k's shuffles are (EARLY_COUNTS: they run
+    while the host draws step k + 1), the call's last shuffle is drawn and pushed in parts
+    (STREAM_LAST_SHUFFLE, DeviceShuffles.draw_push_z_streamed: its first windows' swaps run
+    while the host draws the rest), and Z's write-back runs beside the last step's count."""
     from .numpy_rng import shuffle_draws32
+    t = L.torch()
     plans = []
     _mark("start")
     # X and Z go up on a helper thread while the host draws the first shuffle
-    ds = E.DeviceShuffles(X, Z, T, reuse=True)
+    ds = E.DeviceShuffles(X, Z, T, reuse=True, threaded=THREADED_LAUNCHES)
     _mark("setup")
+    step = [0]
 
     def draws(a, b):  # each side's draws into pinned memory; the device swaps it meanwhile
         shuffle_draws32(a.shape[0], out=ds.draw_x())
         _mark("x drawn")
         ds.push_x()
-        shuffle_draws32(b.shape[0], out=ds.draw_z())
+        if step[0] == T - 1 and STREAM_LAST_SHUFFLE:
+            ds.draw_push_z_streamed(STREAM_LAST_SHUFFLE)
+        else:
+            shuffle_draws32(b.shape[0], out=ds.draw_z())
+            ds.push_z()
         _mark("z drawn")
-        ds.push_z()
 
-    for _ in range(T):
-        plans.append(plan_un(X, Z, N, spec, sampling_type, variant, shuffle=draws))
+    early = hasattr(spec, "enqueue_device") and EARLY_COUNTS
+    cs = E.side_stream("count") if early else None
+    pending = {}
     nx, nz = X.shape[0], Z.shape[0]
-    t = L.torch()
+    for k in range(T):
+        step[0] = k
+        plans.append(plan_un(X, Z, N, spec, sampling_type, variant, shuffle=draws))
+        if early and k < T - 1:  # step k's counts beside the host's next draws
+            def count(k=k):  # after step k's pushes (on the launcher thread when threaded)
+                blks = [p[1] for p in plans[k] if p[0] == "val"]
+                done = spec.enqueue_device(ds.xs[k], ds.zs[k], blks, stream=cs,
+                                           after=(ds.sx, ds.sz)) if blks else None
+                if done is not None:
+                    pending[k] = done
+            ds.submit(count)
+            _mark("counts submitted")
     _mark("pushed")
     # the in-place side effect, X first: its last state goes back while Z's last shuffle runs
     t.from_numpy(X).copy_(ds.last_x())
     _mark("x written back")
-    xs, zs = ds.finish()
+    xs, zs = ds.finish()  # (drains the launcher: every count task has run)
     _mark("finish")
     if 0 in ds.redone:  # (rare) X's shuffles were resumed: its last state changed
         t.from_numpy(X).copy_(xs[T - 1])
-    blocks, counts = [], []
-    for k, plan in enumerate(plans):
-        blks = [p[1] for p in plan if p[0] == "val"]
+    if ds.redone:  # (rare) later states changed: every step is counted again below
+        pending.clear()
+    # the steps not counted yet, in one launch (enqueued before Z's write-back runs beside it)
+    rest = [k for k in range(T) if k not in pending]
+    blocks, counts = [], {}
+    for k in rest:
+        blks = [p[1] for p in plans[k] if p[0] == "val"]
         for b in blks:
             bx = (b.x[0] + k * nx, b.x[1] + k * nx) if isinstance(b.x, tuple) \
                 else np.asarray(b.x) + k * nx
             bz = (b.z[0] + k * nz, b.z[1] + k * nz) if isinstance(b.z, tuple) \
                 else np.asarray(b.z) + k * nz
             blocks.append(Block(bx, bz, b.aux))
-        counts.append(len(blks))
-    vals = spec.evaluate_device(xs.reshape(-1), zs.reshape(-1), blocks) if blocks else []
-    _mark("counted")
-    # the caller's Z ends in the last shuffled state too (X was written above)
-    t.from_numpy(Z).copy_(zs[T - 1])
+        counts[k] = len(blks)
+    done_rest = None
+    if blocks and early:
+        done_rest = spec.enqueue_device(xs.reshape(-1), zs.reshape(-1), blocks)
+    # the caller's Z ends in the last shuffled state too (X was written above): copied out on
+    # a stream of its own, so the copy engine moves it while the last count runs
+    wb = E.side_stream("writeback")
+    ds.order_after(wb)
+    with t.cuda.stream(wb):
+        t.from_numpy(Z).copy_(zs[T - 1])
     _mark("z written back")
-    out, i = [], 0
-    for p, c in zip(plans, counts):
-        out.append(finish_un(p, vals[i:i + c]))
-        i += c
-    return np.mean(out)
+    if done_rest is not None:
+        vals = done_rest()
+    else:
+        vals = spec.evaluate_device(xs.reshape(-1), zs.reshape(-1), blocks) if blocks else []
+    _mark("counted")
+    by_step, i = {}, 0
+    for k in rest:
+        by_step[k] = vals[i:i + counts[k]]
+        i += counts[k]
+    for k, done in pending.items():
+        by_step[k] = done()
+    return np.mean([finish_un(plans[k], by_step[k]) for k in range(T)])
 
 
 def evaluate_many(spec, jobs) -> list:

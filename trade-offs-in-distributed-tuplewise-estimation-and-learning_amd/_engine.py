@@ -309,6 +309,63 @@ def pair_sum_complete(sh: Shards, kern: int, margin: float = 0.0) -> np.ndarray:
 
 
 _SH_STREAMS = {}  # per device: the X and Z shuffle streams of DeviceShuffles
+_SIDE_STREAMS = {}  # (device, name) -> a stream of the drop-in's own (counts, write-backs)
+
+
+class _Launcher:
+    """A worker thread per device that runs the drop-in's enqueue work (the draws' uploads, the
+    swap rounds' launches, the per-step counts) in submission order, so the host thread making
+    the draws (native code, GIL released) never waits for a launch: each shuffle enqueues ~20
+    kernels, ~0.1 ms of host time, and the draws are the call's critical path."""
+
+    def __init__(self, dev):
+        import queue
+        import threading
+        self.q = queue.Queue()
+        self.err = None
+        self.dev = dev
+        threading.Thread(target=self._loop, daemon=True).start()
+
+    def _loop(self):
+        L.torch().cuda.set_device(self.dev)
+        while True:
+            fn = self.q.get()
+            try:
+                if self.err is None:
+                    fn()
+            except BaseException as e:  # raised to the submitting thread at drain()
+                self.err = e
+            finally:
+                self.q.task_done()
+
+    def submit(self, fn) -> None:
+        self.q.put(fn)
+
+    def drain(self) -> None:
+        """Wait until every submitted task has run; re-raise the first failure."""
+        self.q.join()
+        if self.err is not None:
+            e, self.err = self.err, None
+            raise e
+
+
+_LAUNCHERS = {}
+
+
+def launcher(dev) -> _Launcher:
+    if dev not in _LAUNCHERS:
+        _LAUNCHERS[dev] = _Launcher(dev)
+    return _LAUNCHERS[dev]
+
+
+def side_stream(name: str):
+    """A named side stream of the current device, made once (torch.cuda.Stream)."""
+    t = L.torch()
+    key = (t.cuda.current_device(), name)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = t.cuda.Stream()
+    return _SIDE_STREAMS[key]
+
 _SH_BUFFERS = {}  # (device, nx, nz, T, dtype) -> the buffers of the last reuse=True instance
 
 
@@ -329,7 +386,7 @@ class DeviceShuffles:
     (their allocation was ~0.35 ms of a 7-ms call).
     Returns the (T, nx) and (T, nz) device tensors."""
 
-    def __init__(self, x0, z0, T: int, reuse: bool = False):
+    def __init__(self, x0, z0, T: int, reuse: bool = False, threaded: bool = False):
         import threading
         t = L.torch()
         lib = L.lib()
@@ -382,6 +439,19 @@ class DeviceShuffles:
         self.xs, self.zs, self.hx, self.hz = buf["xs"], buf["zs"], buf["hx"], buf["hz"]
         self.jx, self.jz, self.work, self.pend = buf["jx"], buf["jz"], buf["work"], buf["pend"]
         self.kx = self.kz = 0
+        # threaded: uploads and launches run on the device's launcher thread (submit), in order
+        self._launcher = launcher(dev) if threaded else None
+
+    def submit(self, fn) -> None:
+        """Run fn after every push so far (on the launcher thread when threaded)."""
+        if self._launcher is None:
+            fn()
+        else:
+            self._launcher.submit(fn)
+
+    def drain(self) -> None:
+        if self._launcher is not None:
+            self._launcher.drain()
 
     def _uploaded(self):
         if self._up is not None:
@@ -395,22 +465,73 @@ class DeviceShuffles:
         return self.hz[self.kz].numpy()
 
     def push_x(self) -> None:
-        self._uploaded()
-        with self.t.cuda.stream(self.sx):
-            self.jx[self.kx].copy_(self.hx[self.kx], non_blocking=True)
-            self._start(0, self.kx)
+        k = self.kx
         self.kx += 1
 
+        def task():
+            self._uploaded()
+            with self.t.cuda.stream(self.sx):
+                self.jx[k].copy_(self.hx[k], non_blocking=True)
+                self._start(0, k)
+        self.submit(task)
+
     def push_z(self) -> None:
-        self._uploaded()
-        with self.t.cuda.stream(self.sz):
-            self.jz[self.kz].copy_(self.hz[self.kz], non_blocking=True)
-            self._start(1, self.kz)
+        k = self.kz
         self.kz += 1
+
+        def task():
+            self._uploaded()
+            with self.t.cuda.stream(self.sz):
+                self.jz[k].copy_(self.hz[k], non_blocking=True)
+                self._start(1, k)
+        self.submit(task)
 
     def push(self) -> None:
         self.push_x()
         self.push_z()
+
+    def draw_push_z_streamed(self, pieces: int = 4) -> None:
+        """Z's next shuffle drawn AND pushed in `pieces` parts (the call's last shuffle, whose
+        swap rounds would otherwise all run after its last draw): the draws of a group of
+        windows (tw_shuffle_swaps_windows, in the host's draw order), their upload, and the
+        rounds those windows allow (tw_shuffle_swaps_part) — the device swaps the first windows
+        while the host draws the next.  Same draws, same rounds, same permutation."""
+        from .numpy_rng import shuffle_draws32_range
+        t, k, n = self.t, self.kz, self.nz
+        self.kz += 1
+        hz = self.hz[k].numpy()
+        W = int(L.lib().tw_shuffle_swaps_windows())
+        p = -(-(n - 1) // W) if n > 1 else 0
+        pieces = max(1, min(int(pieces), W))
+        r0 = 0
+        for q in range(pieces):
+            c0, c1 = q * W // pieces, (q + 1) * W // pieces
+            last = q == pieces - 1
+            hi, lo = n - c0 * p - 1, max(1, n - c1 * p)
+            if n > 1 and hi >= lo:
+                shuffle_draws32_range(n, hi, lo, hz)
+            # windows [0, c1) are up: rounds to c1 - 2 (round r reads windows <= r + 1)
+            r1 = max(r0, c1 - 1) if not last else r0
+
+            def part(q=q, hi=hi, lo=lo, r0=r0, r1=r1, last=last):
+                if q == 0:
+                    self._uploaded()
+                with t.cuda.stream(self.sz):
+                    if q == 0:
+                        self.zs[k].copy_(self.z0 if k == 0 else self.zs[k - 1])
+                    if n > 1 and hi >= lo:
+                        self.jz[k][lo:hi + 1].copy_(self.hz[k][lo:hi + 1], non_blocking=True)
+                    L.call("tw_shuffle_swaps_part", None, 0, L.ptr(self.zs[k]), n, None,
+                           L.ptr(self.jz[k]), r0, r1, int(last), L.ptr(self.work[1][k]),
+                           L.ptr(self.pend[1, k:k + 1]), L.stream_handle())
+            self.submit(part)
+            r0 = r1
+
+    def order_after(self, stream) -> None:
+        """`stream` waits for every shuffle enqueued so far (both sides; call it on the
+        launcher thread, or after drain(), to include every push)."""
+        stream.wait_stream(self.sx)
+        stream.wait_stream(self.sz)
 
     def _run(self, side, k, first, round0):
         if side == 0:
@@ -430,6 +551,7 @@ class DeviceShuffles:
     def last_x(self):
         """The X side's last state, ordered on the current stream after its shuffles (a
         caller may copy it out while Z's last shuffle runs); finish() says whether it held."""
+        self.drain()
         self.t.cuda.current_stream().wait_stream(self.sx)
         return self.xs[self.T - 1]
 
@@ -439,6 +561,7 @@ class DeviceShuffles:
         states changed after a resumption."""
         T, t = self.T, self.t
         assert self.kx == T and self.kz == T, "every shuffle must be pushed before finish()"
+        self.drain()
         main = t.cuda.current_stream()
         main.wait_stream(self.sx)
         main.wait_stream(self.sz)

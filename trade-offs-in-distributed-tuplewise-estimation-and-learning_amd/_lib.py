@@ -197,11 +197,14 @@ _SIGNATURES = {
     "tw_host_device_pointer": [_vp, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],
+    "tw_np_shuffle_draws32_range": [_vp, _vp, _i64, _i64, _i64, _vp],
     "tw_shuffle_swaps_work_bytes": [_i64, _i64],
     "tw_shuffle_swaps_rounds": [_i64, _i64],
     "tw_shuffle_swaps_set_rounds": [_i32],
     "tw_shuffle_swaps_set_tail": [_i32],
     "tw_shuffle_swaps": [_vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp],
+    "tw_shuffle_swaps_windows": [],
+    "tw_shuffle_swaps_part": [_vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
 }
 _RESTYPES = {
     "tw_last_error": ctypes.c_char_p,
@@ -307,20 +310,24 @@ def to_device(arr: np.ndarray, dtype=None):
     return t.from_numpy(a).to(device())
 
 
-def to_device_many(arrays) -> list:
+def to_device_many(arrays, pinned: bool = False) -> list:
     """Several host arrays -> contiguous device tensors of the same dtypes through ONE H2D copy
     (the small drop-in calls were bound by one copy's fixed cost per array).  Each array starts
-    at an 8-byte boundary of the staging buffer."""
+    at an 8-byte boundary of the staging buffer.  pinned: staged in page-locked memory (torch's
+    caching host allocator) and copied asynchronously on the current stream — the host does
+    not wait for the stream's earlier work (the drop-in's per-step counts)."""
     t = torch()
     arrs = [np.ascontiguousarray(a) for a in arrays]
     offs, total = [], 0
     for a in arrs:
         offs.append(total)
         total += (a.nbytes + 7) & ~7
-    buf = np.empty(max(total, 8), dtype=np.uint8)
+    host = (t.empty((max(total, 8),), dtype=t.uint8, pin_memory=True) if pinned
+            else t.from_numpy(np.empty(max(total, 8), dtype=np.uint8)))
+    buf = host.numpy()
     for a, o in zip(arrs, offs):
         buf[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
-    dev = t.from_numpy(buf).to(device())
+    dev = host.to(device(), non_blocking=pinned)
     out = []
     for a, o in zip(arrs, offs):
         td = t.from_numpy(np.empty(0, dtype=a.dtype)).dtype

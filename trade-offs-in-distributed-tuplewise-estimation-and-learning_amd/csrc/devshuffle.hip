@@ -277,25 +277,17 @@ extern "C" int32_t tw_shuffle_swaps_rounds(int64_t nx, int64_t nz) {
   return plan_sh(std::max<int64_t>(nx, 0), std::max<int64_t>(nz, 0)).rounds;
 }
 
-// Enqueue one batch of tw_shuffle_swaps_rounds rounds.  first != 0: the first batch (clears
-// the workspace, reserves round 0, round 0 runs over every iteration); round0 = 0.  Later
-// batches (first == 0, round0 = the previous round0 + rounds) continue from the previous
-// batch's pending list.  *d_pending (device) receives the number of iterations still pending
-// after the batch: the caller reads it and enqueues another batch while it is not 0 — with
-// ~3.5 ln n rounds needed and 4.5 ln n + 8 per batch, one batch finishes w.h.p.
-extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz,
-                                const uint32_t* d_jx, const uint32_t* d_jz, int32_t first,
-                                int32_t round0, void* d_work, uint32_t* d_pending,
-                                void* stream) {
-  TW_ARG_CHECK(nx >= 0 && nz >= 0 && d_work != nullptr && d_pending != nullptr && round0 >= 0,
-               "tw_shuffle_swaps: bad arguments");
-  TW_ARG_CHECK(nx + nz < (1ll << 31), "tw_shuffle_swaps: more than 2^31 items");
-  TW_ARG_CHECK((nx <= 1 || (d_x && d_jx)) && (nz <= 1 || (d_z && d_jz)),
-               "tw_shuffle_swaps: null array");
+namespace tw {
+// rounds [k_begin, k_end) of one batch (k counts from round0); k_begin = 0 also sets the batch
+// up (first: clear the workspace, reserve round 0; else continue from the previous batch's
+// list); last: the batch's remaining rounds (k_end ignored), its tail and *d_pending
+static int swaps_batch(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz,
+                       const uint32_t* d_jx, const uint32_t* d_jz, int first, int round0,
+                       int k_begin, int k_end, int last, void* d_work, uint32_t* d_pending,
+                       hipStream_t st) {
   const int64_t total = nx + nz;
-  hipStream_t st = (hipStream_t)stream;
   if (nx <= 1 && nz <= 1) {  // no iteration at all
-    TW_HIP_CHECK(tw_zero_async(d_pending, 0, 4, st));
+    if (last) TW_HIP_CHECK(tw_zero_async(d_pending, 0, 4, st));
     return TW_OK;
   }
   const ShPlan p = plan_sh(nx, nz);
@@ -314,21 +306,23 @@ extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_
   ch.px = nx > 1 ? ceil_div(nx - 1, kShWindows) : 0;
   ch.pz = nz > 1 ? ceil_div(nz - 1, kShWindows) : 0;
   const double per = (double)total / kShWindows;
-  if (first) {
-    TW_HIP_CHECK(tw_zero_async(w, 0, (size_t)p.bytes, st));
-    hipLaunchKernelGGL(k_sh_reserve0, dim3(grid_for(per)), dim3(kShThreads), 0, st, d_jx, d_jz,
-                       ch, R[0]);
-  } else {
-    // continue: the previous batch's last list (parity of its last round) is round0's input;
-    // its count moves to slot 0
-    TW_HIP_CHECK(hipMemcpyAsync(cnt, cnt + p.rounds, 4, hipMemcpyDeviceToDevice, st));
-    TW_HIP_CHECK(tw_zero_async(cnt + 1, 0, (size_t)p.rounds * 4, st));
+  if (k_begin == 0) {
+    if (first) {
+      TW_HIP_CHECK(tw_zero_async(w, 0, (size_t)p.bytes, st));
+      hipLaunchKernelGGL(k_sh_reserve0, dim3(grid_for(per)), dim3(kShThreads), 0, st, d_jx,
+                         d_jz, ch, R[0]);
+    } else {
+      // continue: the previous batch's last list (parity of its last round) is round0's
+      // input; its count moves to slot 0
+      TW_HIP_CHECK(hipMemcpyAsync(cnt, cnt + p.rounds, 4, hipMemcpyDeviceToDevice, st));
+      TW_HIP_CHECK(tw_zero_async(cnt + 1, 0, (size_t)p.rounds * 4, st));
+    }
   }
   // rounds of the whole grid while chunks enter and the list is long, then the tail in one
   // workgroup (k_sh_finish) once the expected list is under ~kShFinThreads * 8 iterations
   const double tail_items = (double)kShFinThreads * 8;
   int k_fin = p.rounds;
-  for (int k = 0; k < p.rounds; ++k) {
+  for (int k = k_begin; k < p.rounds; ++k) {
     const int r = round0 + k;
     const double est =
         r < kShWindows ? 2.0 * per : 2.0 * per * std::pow(0.8, (double)(r - kShWindows + 1));
@@ -336,12 +330,14 @@ extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_
       k_fin = k;
       break;
     }
+    if (!last && k >= k_end) return TW_OK;  // a part: the next one continues at k_end
     // round r reads the list of round r-1 (L[(r+1)&1]) and writes L[r&1]
     hipLaunchKernelGGL(k_sh_round, dim3(grid_for(est)), dim3(kShThreads), 0, st, r, d_x, d_z,
                        d_jx, d_jz, ch, L[(r + 1) & 1], cnt + k, L[r & 1], cnt + k + 1, R[r & 1],
                        R[(r + 1) & 1]);
   }
   TW_LAUNCH_CHECK();
+  if (!last) return TW_OK;
   if (k_fin < p.rounds) {
     hipLaunchKernelGGL(k_sh_finish, dim3(1), dim3(kShFinThreads), 0, st, round0 + k_fin,
                        round0 + p.rounds, d_x, d_z, d_jx, d_jz, (int64_t)nx, L[0], L[1],
@@ -353,4 +349,51 @@ extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_
   }
   TW_HIP_CHECK(hipMemcpyAsync(d_pending, cnt + p.rounds, 4, hipMemcpyDeviceToDevice, st));
   return TW_OK;
+}
+}  // namespace tw
+
+// Enqueue one batch of tw_shuffle_swaps_rounds rounds.  first != 0: the first batch (clears
+// the workspace, reserves round 0, round 0 runs over every iteration); round0 = 0.  Later
+// batches (first == 0, round0 = the previous round0 + rounds) continue from the previous
+// batch's pending list.  *d_pending (device) receives the number of iterations still pending
+// after the batch: the caller reads it and enqueues another batch while it is not 0 — with
+// ~3.5 ln n rounds needed and 4.5 ln n + 8 per batch, one batch finishes w.h.p.
+extern "C" int tw_shuffle_swaps(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz,
+                                const uint32_t* d_jx, const uint32_t* d_jz, int32_t first,
+                                int32_t round0, void* d_work, uint32_t* d_pending,
+                                void* stream) {
+  TW_ARG_CHECK(nx >= 0 && nz >= 0 && d_work != nullptr && d_pending != nullptr && round0 >= 0,
+               "tw_shuffle_swaps: bad arguments");
+  TW_ARG_CHECK(nx + nz < (1ll << 31), "tw_shuffle_swaps: more than 2^31 items");
+  TW_ARG_CHECK((nx <= 1 || (d_x && d_jx)) && (nz <= 1 || (d_z && d_jz)),
+               "tw_shuffle_swaps: null array");
+  return swaps_batch(d_x, nx, d_z, nz, d_jx, d_jz, first, round0, 0, 0, 1, d_work, d_pending,
+                     (hipStream_t)stream);
+}
+
+// The draw windows of the swap rounds: iterations enter in kShWindows chunks of
+// p = ceil((n - 1) / kShWindows) draws each, window c holding i in [max(1, n - (c + 1) p),
+// n - c p) — the order the host draws them in.
+extern "C" int32_t tw_shuffle_swaps_windows() { return kShWindows; }
+
+// The FIRST batch of tw_shuffle_swaps in parts, enqueued as the draws arrive (the streamed
+// last shuffle of the drop-in, _engine.DeviceShuffles): rounds [r_begin, r_end) — round r
+// reads the draws of windows 0 .. r + 1, so once windows [0, c) are on the device rounds up to
+// c - 2 may run (r_end = c - 1).  r_begin = 0 also clears the workspace and reserves round 0
+// (window 0 needed); last != 0 enqueues every remaining round, the tail and *d_pending
+// (r_end ignored).  The parts in sequence (r_begin = the previous r_end) are exactly
+// tw_shuffle_swaps(first = 1, round0 = 0).
+extern "C" int tw_shuffle_swaps_part(uint64_t* d_x, int64_t nx, uint64_t* d_z, int64_t nz,
+                                     const uint32_t* d_jx, const uint32_t* d_jz,
+                                     int32_t r_begin, int32_t r_end, int32_t last,
+                                     void* d_work, uint32_t* d_pending, void* stream) {
+  TW_ARG_CHECK(nx >= 0 && nz >= 0 && d_work != nullptr && d_pending != nullptr &&
+                   r_begin >= 0 && (last || (r_end >= r_begin && r_end < kShWindows)),
+               "tw_shuffle_swaps_part: bad arguments (a part ends before round %d)",
+               kShWindows);
+  TW_ARG_CHECK(nx + nz < (1ll << 31), "tw_shuffle_swaps_part: more than 2^31 items");
+  TW_ARG_CHECK((nx <= 1 || (d_x && d_jx)) && (nz <= 1 || (d_z && d_jz)),
+               "tw_shuffle_swaps_part: null array");
+  return swaps_batch(d_x, nx, d_z, nz, d_jx, d_jz, 1, 0, r_begin, r_end, last, d_work,
+                     d_pending, (hipStream_t)stream);
 }

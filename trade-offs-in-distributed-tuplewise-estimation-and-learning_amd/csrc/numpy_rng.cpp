@@ -485,20 +485,24 @@ __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) inline int shuffle1
   return p;
 }
 
-// J = int64_t (the host swaps) or uint32_t (the device swaps: n <= 2^31, so 32-bit draws only)
+// J = int64_t (the host swaps) or uint32_t (the device swaps: n <= 2^31, so 32-bit draws only).
+// The draws for i = hi down to stop (stop >= 1; the whole shuffle: hi = n - 1, stop = 1): a
+// shuffle drawn in consecutive ranges consumes the same words and makes the same draws as one
+// call (the range end only lowers the loops' bound; the SIMD batches never store below it)
 template <int kIsa, typename J>
-void shuffle_draws(MT& mt, int64_t n, J* j) {
-  int64_t i = n - 1;
-  while (sizeof(J) == 8 && i >= 1 && (uint64_t)i > 0xFFFFFFFFull) {
+void shuffle_draws(MT& mt, int64_t hi, int64_t stop, J* j) {
+  int64_t i = hi;
+  while (sizeof(J) == 8 && i >= stop && (uint64_t)i > 0xFFFFFFFFull) {
     const uint64_t mask = gen_mask((uint64_t)i);
     uint64_t v;
     while ((v = (mt.next64() & mask)) > (uint64_t)i) {
     }
     j[i--] = (J)v;
   }
-  while (i >= 1) {
+  while (i >= stop) {
     const uint32_t mask = (uint32_t)gen_mask((uint64_t)i);
-    const int64_t lo = (int64_t)(mask >> 1);  // this mask serves i in (mask/2, mask]
+    // this mask serves i in (mask/2, mask]; the range ends below stop
+    const int64_t lo = std::max<int64_t>((int64_t)(mask >> 1), stop - 1);
     if (mt.pos >= kN) generate_isa<kIsa>(mt);
     mt.temper_rest();
     int p = mt.pos;
@@ -506,8 +510,8 @@ void shuffle_draws(MT& mt, int64_t n, J* j) {
       if (kIsa >= 2) p = shuffle16_avx512(mt.tmp, p, mask, lo, i, j);
       if (kIsa >= 1) p = shuffle8_avx2(mt.tmp, p, mask, lo, i, j);
       // scalar: until the block or the mask range ends, or (SIMD) 8 words have passed
-      const int stop = kIsa ? (p + 8 < kN ? p + 8 : kN) : kN;
-      while (p < stop && i > lo) {
+      const int stop_p = kIsa ? (p + 8 < kN ? p + 8 : kN) : kN;
+      while (p < stop_p && i > lo) {
         const uint32_t v = mt.tmp[p++] & mask;
         j[i] = (J)v;
         i -= (int64_t)(v <= (uint32_t)i);
@@ -550,24 +554,27 @@ void shuffle_apply(char* data, int64_t n, int64_t itemsize, const int64_t* j) {
 }
 
 template <typename J>
-__attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t n, J* j) {
-  shuffle_draws<1>(mt, n, j);
+__attribute__((target("avx2,popcnt"))) void shuffle_draws_avx2(MT& mt, int64_t hi, int64_t stop,
+                                                               J* j) {
+  shuffle_draws<1>(mt, hi, stop, j);
 }
 template <typename J>
 __attribute__((target("avx2,avx512f,avx512vl,popcnt,bmi2"))) void shuffle_draws_avx512(MT& mt,
-                                                                                  int64_t n,
+                                                                                  int64_t hi,
+                                                                                  int64_t stop,
                                                                                   J* j) {
-  shuffle_draws<2>(mt, n, j);
+  shuffle_draws<2>(mt, hi, stop, j);
 }
 
+// the draws for i = hi down to stop (the whole shuffle of n items: hi = n - 1, stop = 1)
 template <typename J>
-void shuffle_draws_isa(MT& mt, int64_t n, J* j, int isa) {
+void shuffle_draws_isa(MT& mt, int64_t hi, int64_t stop, J* j, int isa) {
   if (isa == 2)
-    shuffle_draws_avx512(mt, n, j);
+    shuffle_draws_avx512(mt, hi, stop, j);
   else if (isa == 1)
-    shuffle_draws_avx2(mt, n, j);
+    shuffle_draws_avx2(mt, hi, stop, j);
   else
-    shuffle_draws<0>(mt, n, j);
+    shuffle_draws<0>(mt, hi, stop, j);
 }
 
 // grad_inc_block's draws straight into uint16 outputs (ranges <= 65536) with AVX-512 VBMI2:
@@ -954,7 +961,7 @@ int tw_np_shuffle_pair(uint32_t* key, int32_t* pos, void* x, int64_t nx, int64_t
   int64_t* jx = jbuf;
   int64_t* jz = jbuf + (nx > 0 ? nx : 0);
   const int isa = isa_level();
-  auto draws = [&](int64_t n, int64_t* j) { shuffle_draws_isa(mt, n, j, isa); };
+  auto draws = [&](int64_t n, int64_t* j) { shuffle_draws_isa(mt, n - 1, (int64_t)1, j, isa); };
   if (nx > 1) draws(nx, jx);
   std::thread tx;
   bool threaded = false;
@@ -983,7 +990,22 @@ int tw_np_shuffle_draws32(uint32_t* key, int32_t* pos, int64_t n, uint32_t* j) {
   MT mt;
   mt.key = key;
   mt.pos = *pos;
-  if (n > 1) shuffle_draws_isa(mt, n, j, isa_level());
+  if (n > 1) shuffle_draws_isa(mt, n - 1, (int64_t)1, j, isa_level());
+  *pos = mt.pos;
+  return 0;
+}
+
+// The same draws in consecutive ranges (the streamed last shuffle of the drop-in,
+// _engine.DeviceShuffles.push_z_part): j[i] for i = hi down to lo (1 <= lo <= hi < n <= 2^31),
+// the state advanced past them.  Ranges [hi_0 = n-1 .. lo_0], [lo_0 - 1 .. lo_1], ... down to 1
+// make exactly tw_np_shuffle_draws32's draws.
+int tw_np_shuffle_draws32_range(uint32_t* key, int32_t* pos, int64_t n, int64_t hi, int64_t lo,
+                                uint32_t* j) {
+  if (n < 2 || n > (1ll << 31) || lo < 1 || hi < lo || hi >= n || !j) return 2;
+  MT mt;
+  mt.key = key;
+  mt.pos = *pos;
+  shuffle_draws_isa(mt, hi, lo, j, isa_level());
   *pos = mt.pos;
   return 0;
 }

@@ -136,6 +136,20 @@ def shuffle_draws32(n: int, out=None) -> np.ndarray:
     return j
 
 
+def shuffle_draws32_range(n: int, hi: int, lo: int, out) -> None:
+    """shuffle_draws32's draws for i = hi down to lo only (1 <= lo <= hi < n), into out (the
+    shuffle's whole n-entry 4-byte array; other entries untouched), the global legacy state
+    advanced past them: consecutive ranges from hi = n - 1 down to lo = 1 make exactly
+    shuffle_draws32(n)'s draws (_engine.DeviceShuffles streams the drop-in's last shuffle)."""
+    j = out.view(np.uint32)
+    if j.shape != (int(n),) or not j.flags.c_contiguous:
+        raise ValueError("shuffle_draws32_range: out must be a contiguous array of n items")
+    rc = _native_draws(lambda key, pos: L.lib().tw_np_shuffle_draws32_range(
+        key, pos, int(n), int(hi), int(lo), j.ctypes.data))
+    if rc:
+        raise ValueError(f"tw_np_shuffle_draws32_range failed ({rc}) for n={n}, [{lo}, {hi}]")
+
+
 class Session:
     """NumPy's legacy global MT19937 state held in native code for a run of draws.
 
