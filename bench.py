@@ -271,14 +271,16 @@ def plumbing_C1(with_cpu, reps=200):
     return out
 
 
-def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
+def drop_in_C3(reps=10, T=4, N=64, n=N_PER_CLASS):
     """The user-visible drop-in at BASELINE configs[2]'s size: est.UnNT(X, Z, 64, 4, "prop-SWOR")
     (estimation-experiment/main.py:76-79) on HOST arrays of n = 1e6 per class, exactly as a
     reference script calls it.  Default path: the host makes every draw in the reference's RNG
     order (the T shuffles' index draws by the native restatement, numpy_rng.shuffle_draws32),
     X and Z go up once, the device applies the T shuffles' swaps keeping every state
-    (csrc/devshuffle.hip), all T x N blocks are counted in one launch and the caller's arrays
-    receive the last state.  The host-swap path (shuffle_pair + T snapshots uploaded) is timed
+    (csrc/devshuffle.hip; launches made by a launcher thread while the host draws, the last
+    shuffle streamed in window groups), each step's blocks are counted while the next step is
+    drawn, and the caller's arrays receive the last state.  ms_per_call: the median of `reps`
+    calls (mean beside it).  The host-swap path (shuffle_pair + T snapshots uploaded) is timed
     beside it, and the parts of the default path alone on the same shapes."""
     import torch
     import tuplewise.estimation as est
@@ -295,14 +297,18 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
             np.random.seed(1)
             est.UnNT(Xc, Zc, N, T, "prop-SWOR")  # warm
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
+            ts = []
             for _ in range(reps):
+                t0 = time.perf_counter()
                 v = est.UnNT(Xc, Zc, N, T, "prop-SWOR")
-            return (time.perf_counter() - t0) / reps, v
+                ts.append(time.perf_counter() - t0)
+            timed.mean = float(np.mean(ts))
+            return float(np.median(ts)), v
         finally:
             Bk.DEVICE_SHUFFLE_MIN = old
 
     dt, v = timed(Bk.DEVICE_SHUFFLE_MIN)
+    dt_mean = timed.mean
     dt_host, v_host = timed(1 << 62)
     # the same call with two device slots visible (a multi-GPU node's default device list;
     # slots [0, 0] on one GPU): the blocks' sorted count stays below the spreading threshold,
@@ -356,7 +362,8 @@ def drop_in_C3(reps=3, T=4, N=64, n=N_PER_CLASS):
                     "as a reference script calls it): host draws in the reference's order, the "
                     "shuffles' swaps on the device (csrc/devshuffle.hip), the caller's arrays "
                     "written back; parts timed alone on the same shapes",
-            "ms_per_call": dt * 1e3, "value": pairs / dt,
+            "ms_per_call": dt * 1e3, "ms_per_call_mean": dt_mean * 1e3, "calls": reps,
+            "value": pairs / dt,
             # the sorted count decides every pair without comparing it: logical pairs
             "unit": "logical pairs/s" if algo == "sorted" else "pairs/s",
             "host_swap_path_ms_per_call": dt_host * 1e3,
