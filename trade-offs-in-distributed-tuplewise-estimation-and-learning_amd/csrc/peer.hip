@@ -105,12 +105,15 @@ __global__ __launch_bounds__(kBlock) void k_peer_step(const double* __restrict__
   }
 }
 
-// setup handshake: lane p stores this rank's token into rank p's hello word for this rank
+// setup handshake: lane p swaps this rank's token into rank p's hello word for this rank —
+// a system-scope read-modify-write through the mapping, the kind of operation every step's
+// arrivals are (a peer whose remote atomics do not land fails the check, and the ranks fall
+// back to the all-gather)
 __global__ void k_peer_hello(PeerSeg ps, int rank, unsigned long long token) {
   const int p = (int)threadIdx.x;
   if (p < ps.G) {
     auto* w = (unsigned long long*)((char*)ps.ctr[p] + kPeerHello) + rank;
-    __hip_atomic_store(w, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    (void)__hip_atomic_exchange(w, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -45,7 +45,7 @@ namespace tw {
 
 // ----------------------------------------------------------------------------- images
 // g(v) = #{z : key(z) < key(v)} for all n + m elements, from a structure over Z alone:
-//  1. a sample of Z at hashed positions, sorted (by counting, over C / 128 blocks from C = 1024
+//  1. a sample of Z at hashed positions, sorted (by counting, over C / 64 blocks from C = 1024
 //     keys): B - 1 splitter keys;
 //  2. z -> bucket: 2j for the keys strictly between splitters j-1 and j, 2j + 1 for keys EQUAL
 //     to splitter j (heavy ties land there: no z of such a bucket is below any of its values);
@@ -85,14 +85,15 @@ __device__ __forceinline__ int64_t sample_index(int i, int64_t m) {
   return (int64_t)(((uint64_t)mix32((uint32_t)i * 0x9E3779B1u + 0x7F4A7C15u) * (uint64_t)m) >> 32);
 }
 
-// the sample of C >= 1024 keys (Z beyond kRkSmallM), sorted by counting over C / 128 blocks
+// the sample of C >= 1024 keys (Z beyond kRkSmallM), sorted by counting over C / 64 blocks
 // (one block's bitonic network was a serial chain of ~50 shuffle levels: 16 us at C = 1024,
-// the longest of the ranking's structure launches): every block draws the whole sample into
-// LDS (cs hashed positions of z, padded with ~0) and places 128 of its keys — key i goes to
-// #{j : k_j < k_i} + #{j < i : k_j == k_i}, eight threads per key each counting a C / 8 share
-// (a wave's lanes hold different keys and read the same k_j: LDS broadcasts), the shares
-// added with LDS atomics.  The sorted array is the bitonic one's, key for key.
-constexpr int kRkSampPlace = 128;  // keys placed per block
+// the longest of the ranking's structure launches; 8 blocks placing 128 keys each: 10 us):
+// every block draws the whole sample into LDS (cs hashed positions of z, padded with ~0) and
+// places 64 of its keys — key i goes to #{j : k_j < k_i} + #{j < i : k_j == k_i}, sixteen
+// threads per key each counting a C / 16 share (a wave's lanes hold different keys and read
+// the same k_j: LDS broadcasts), the shares added with LDS atomics.  The sorted array is the
+// bitonic one's, key for key.
+constexpr int kRkSampPlace = 64;  // keys placed per block
 template <typename T>
 __global__ __launch_bounds__(1024) void k_rank_sample_count(const T* __restrict__ z, int64_t m,
                                                             int cs, int C,
