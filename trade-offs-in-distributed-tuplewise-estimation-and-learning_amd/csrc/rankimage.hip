@@ -208,7 +208,8 @@ __device__ __forceinline__ int load_splitters(const uint64_t* __restrict__ ss, c
   return nsp;
 }
 
-// pass 1: per-block bucket histogram of Z (column blk of rel[b][*]); PER z per thread
+// pass 1: per-block bucket histogram of Z (row blk of rel[blk][b]: each block's NB counters
+// stored contiguously, and read back the same way by the scatter pass); PER z per thread
 template <typename T, int PER>
 __global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ z, RankGeo g,
                                                           const uint64_t* __restrict__ ss,
@@ -236,30 +237,50 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_hist(const T* __restrict__ 
   }
   __syncthreads();
   for (int b = threadIdx.x; b < g.NB; b += kRkThreads)
-    rel[(int64_t)b * g.nblk + blockIdx.x] = h[b];
+    rel[(int64_t)blockIdx.x * g.NB + b] = h[b];
 }
 
-// pass 2a: one wave per bucket: exclusive prefix of its row over the blocks (in place), total
-__global__ __launch_bounds__(kBlock) void k_rank_rows(RankGeo g, uint32_t* __restrict__ rel,
-                                                      uint32_t* __restrict__ total) {
-  const int b = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  if (b >= g.NB) return;
-  uint32_t* row = rel + (int64_t)b * g.nblk;
-  uint32_t carry = 0;
-  for (int c0 = 0; c0 < g.nblk; c0 += kWave) {
-    const int c = c0 + lane;
-    const uint32_t v = c < g.nblk ? row[c] : 0u;
-    uint32_t inc = v;  // inclusive wave scan
+// pass 2a: exclusive prefix of every bucket's column of rel[blk][NB] over the blocks (in
+// place) and the bucket totals.  A block takes 64 consecutive buckets (one per lane: every
+// wave-load is a 256-B run of one rel row) and splits the rows among its 16 waves: each wave
+// sums its rows, the waves' sums are scanned in LDS, then each wave walks its rows again writing
+// the running prefix — two coalesced passes instead of one strided wave per bucket.
+constexpr int kRowsWaves = 16;
+__global__ __launch_bounds__(kRowsWaves * kWave) void k_rank_rows(RankGeo g,
+                                                                  uint32_t* __restrict__ rel,
+                                                                  uint32_t* __restrict__ total) {
+  __shared__ uint32_t part[kRowsWaves][kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int b = blockIdx.x * kWave + lane;
+  const bool live = b < g.NB;
+  const int per = (g.nblk + kRowsWaves - 1) / kRowsWaves;
+  const int c0 = wid * per, c1 = min(g.nblk, c0 + per);
+  uint32_t sum = 0;
+  int c = c0;
+  for (; c + 4 <= c1; c += 4) {  // four rows' loads in flight
+    uint32_t v[4];
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, kWave);
-      if (lane >= o) inc += t;
-    }
-    if (c < g.nblk) row[c] = carry + inc - v;
-    carry += __shfl(inc, kWave - 1, kWave);
+    for (int u = 0; u < 4; ++u) v[u] = live ? rel[(int64_t)(c + u) * g.NB + b] : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sum += v[u];
   }
-  if (lane == 0) total[b] = carry;
+  for (; c < c1; ++c) sum += live ? rel[(int64_t)c * g.NB + b] : 0u;
+  part[wid][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (int w = 0; w < wid; ++w) run += part[w][lane];
+  if (wid == kRowsWaves - 1 && live) total[b] = run + sum;
+  if (!live) return;
+  for (c = c0; c < c1; c += 8) {  // eight rows' loads issued before their stores
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = c + u < c1 ? rel[(int64_t)(c + u) * g.NB + b] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (c + u < c1) rel[(int64_t)(c + u) * g.NB + b] = run;
+      run += v[u];
+    }
+  }
 }
 
 // passes 2a + 2b in one 1024-thread block when every bucket row fits two wave loads (nblk <= 128: the
@@ -281,7 +302,7 @@ __global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = h * kWave + lane;
-      v[r][h] = (b < g.NB && c < g.nblk) ? rel[(int64_t)b * g.nblk + c] : 0u;
+      v[r][h] = (b < g.NB && c < g.nblk) ? rel[(int64_t)c * g.NB + b] : 0u;
     }
   }
   __syncthreads();
@@ -299,7 +320,7 @@ __global__ __launch_bounds__(1024) void k_rank_rows_starts(RankGeo g, uint32_t* 
         const uint32_t u = __shfl_up(inc, o, kWave);
         if (lane >= o) inc += u;
       }
-      if (c < g.nblk) rel[(int64_t)b * g.nblk + c] = carry + inc - v[r][h];
+      if (c < g.nblk) rel[(int64_t)c * g.NB + b] = carry + inc - v[r][h];
       carry += __shfl(inc, kWave - 1, kWave);
     }
     if (lane == 0) {
@@ -363,11 +384,11 @@ __global__ __launch_bounds__(kRkThreads) void k_rank_scatter(const T* __restrict
   uint32_t ex = inc - (a0 + a1);
   for (int w = 0; w < wid; ++w) ex += wsum[w];
   if (2 * t < g.NB) {
-    cur[2 * t] = ex + rel[(int64_t)(2 * t) * g.nblk + blockIdx.x];
+    cur[2 * t] = ex + rel[(int64_t)blockIdx.x * g.NB + 2 * t];
     if (blockIdx.x == 0) start[2 * t] = ex;
   }
   if (2 * t + 1 < g.NB) {
-    cur[2 * t + 1] = ex + a0 + rel[(int64_t)(2 * t + 1) * g.nblk + blockIdx.x];
+    cur[2 * t + 1] = ex + a0 + rel[(int64_t)blockIdx.x * g.NB + 2 * t + 1];
     if (blockIdx.x == 0) start[2 * t + 1] = ex + a0;
   }
   __syncthreads();
@@ -979,8 +1000,8 @@ static int rank_images_t(const T* xq, const T* zq, const T* z, int64_t m, const 
         hipLaunchKernelGGL(k_rank_rows_starts, dim3(1), dim3(1024), 0, st, g, w.rel, w.total,
                            w.start);
       else
-        hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kBlock / kWave)),
-                           dim3(kBlock), 0, st, g, w.rel, w.total);
+        hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)ceil_div(g.NB, kWave)),
+                           dim3(kRowsWaves * kWave), 0, st, g, w.rel, w.total);
       // the starts: made (again, for the small path) by the scatter blocks
       hipLaunchKernelGGL((k_rank_scatter<T, PER>), dim3(g.nblk), dim3(kRkThreads), 0, st, z, g,
                          w.bid, w.rel, w.total, w.start, w.bkeys);
