@@ -670,7 +670,8 @@ def traced_count_chain(steps):
         except Exception:
             continue
         if int(d.get("steps_per_launch", -1)) == int(steps):
-            return {k: d[k] for k in ("mean_ms", "min_ms", "frac_mean", "frac_min", "launches")
+            return {k: d[k] for k in ("mean_ms", "min_ms", "frac_mean", "frac_min", "launches",
+                                      "timed_ms", "frac_timed", "launch_ms_in_order")
                     if k in d} | {"source": str(c.relative_to(ROOT))}
     return None
 
