@@ -442,8 +442,8 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
         st_agent(fz.w_out + j, wj - st);
         st_agent(fz.dw_out + j, st);
       }
-      hand_arrive(fz.ctl);  // w_out went out with sc1 stores: the fence-free hand-off
-      if (!hand_wait(fz.ctl, fz.abort_word, gridDim.x, &s_ok)) return;  // caller sees it
+      seg_arrive(fz.ctl);
+      if (!seg_wait_at(fz.ctl, fz.abort_word, gridDim.x, &s_ok)) return;  // caller sees it
 #pragma unroll
       for (int c = 0; c < kWideCols; ++c) {
         const int j = lane + c * kWave;
