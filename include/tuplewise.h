@@ -515,9 +515,9 @@ int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* 
 /* The same segment structure for wide rows (32 < d <= 512, device RNG; C5): ONE launch per
  * step whose blocks first apply the PREVIOUS step's update spread over them (block b takes
  * columns [b*cpb, (b+1)*cpb), cpb = ceil(d / n_shards)) while this step's first rows are in
- * flight, meet at a grid barrier (d_ctl: 4 words, the arrival counters of step parities 0 and
- * 1 and the abort word, zeroed once by the caller; d_ctl[2] != 0 afterwards: a block gave up
- * waiting, the state is invalid), then compute this step's gradients with the new w.  Draws at step counter
+ * flight, meet at a grid barrier (d_ctl: 4 words, [arrivals, abort] for step parities 0 and 1,
+ * zeroed once by the caller; an abort word != 0 afterwards: a block gave up waiting, the state
+ * is invalid), then compute this step's gradients with the new w.  Draws at step counter
  * *d_step + step_off: swr_mod > 0 draws the SWR rows in the kernel (tw_pair_grad_rng_swr,
  * swr base 0), else the row tables d_rows_x / d_rows_z (tw_pair_grad_rng).  Slots and the
  * closing tw_sgd_update_to as tw_sgd_step; the same bits as gradient + tw_sgd_update launches.

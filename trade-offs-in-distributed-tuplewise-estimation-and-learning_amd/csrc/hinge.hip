@@ -283,9 +283,8 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
 // gradient launch's blocks (block b updates columns [b * cpb, (b + 1) * cpb)) while the first
 // rows of this step are in flight, a grid barrier, then the gradient with the new w.
 // grads_in == nullptr: no pending update (the segment's first step reads w_in).  ctl: this
-// launch's arrival counter (by step parity); ctl_next: the other parity's, zeroed here for the
-// next launch (which starts after every block of this one has finished); abort_word: shared
-// by both parities and sticky, so the launches after a timed-out one exit at once.
+// launch's [arrivals, abort] pair; ctl_next: the other parity's arrival counter, zeroed here
+// for the next launch (which starts after every block of this one has finished).
 constexpr int kWideFuseUpd = 1536;  // n_shards * cpb staged per block (12 KiB)
 struct WideFuse {
   const double* w_in;
@@ -296,7 +295,6 @@ struct WideFuse {
   double reg, lr, momentum;
   uint32_t* ctl;
   uint32_t* ctl_next;
-  uint32_t* abort_word;
   int n_shards;
   uint32_t step_off;
 };
@@ -443,7 +441,7 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
         st_agent(fz.dw_out + j, st);
       }
       seg_arrive(fz.ctl);
-      if (!seg_wait_at(fz.ctl, fz.abort_word, gridDim.x, &s_ok)) return;  // caller sees it
+      if (!seg_wait(fz.ctl, gridDim.x, &s_ok)) return;  // gave up: the caller sees ctl[1]
 #pragma unroll
       for (int c = 0; c < kWideCols; ++c) {
         const int j = lane + c * kWave;
@@ -1163,8 +1161,8 @@ extern "C" int tw_sgd_step_wide_ok(int64_t d, int32_t n_shards) {
 // barrier, then this step's gradient (tw_pair_grad_rng's draws at step counter *d_step +
 // step_off; swr_mod > 0: the SWR rows drawn in the kernel, else the row tables) with the new
 // w into grads_out.  grads_in == NULL: no pending update (w_in is this step's w).  d_ctl: 4
-// words — the arrival counters of step parities 0 and 1, then the abort word (zeroed once by
-// the caller; d_ctl[2] != 0 afterwards means a block gave up waiting).  Same bits as
+// words, the barrier pairs [arrivals, abort] of step parities 0 and 1 (zeroed once by the
+// caller; an abort word != 0 afterwards means a block gave up waiting).  Same bits as
 // tw_pair_grad_rng(_swr) + tw_sgd_update per step.
 extern "C" int tw_sgd_step_wide(const double* d_X, const double* d_Z, int64_t d, int64_t n_X,
                                 int64_t n_Z, const int64_t* d_rows_x, int64_t kx,
@@ -1188,9 +1186,8 @@ extern "C" int tw_sgd_step_wide(const double* d_X, const double* d_Z, int64_t d,
                "tw_sgd_step_wide: a pending update needs dw_in, w_out, dw_out");
   if (int rc = check_loss(loss)) return rc;
   const int par = step_off & 1;
-  WideFuse fz{d_w_in,     d_dw_in,  d_grads_in,       d_w_out,     d_dw_out,
-              reg,        lr,       momentum,         d_ctl + par, d_ctl + (1 - par),
-              d_ctl + 2,  (int)n_shards, (uint32_t)step_off};
+  WideFuse fz{d_w_in, d_dw_in, d_grads_in, d_w_out, d_dw_out, reg, lr, momentum,
+              d_ctl + 2 * par, d_ctl + 2 * (1 - par), (int)n_shards, (uint32_t)step_off};
   const SwrMap swr = swr_mod > 0 ? SwrMap{(uint64_t)swr_mod, 0, n_X, n_Z} : SwrMap{0, 0, 1, 1};
   hipStream_t st = (hipStream_t)stream;
   if (loss == TW_LOSS_LOGISTIC)

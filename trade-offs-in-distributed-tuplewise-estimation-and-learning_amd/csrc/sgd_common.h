@@ -97,15 +97,14 @@ __device__ __forceinline__ void seg_arrive(uint32_t* ctl, int arriver = 0) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one lane: spin until *ctr reaches target (false: aborted or timed out -> *abort_word raised)
-__device__ __forceinline__ bool seg_poll_at(uint32_t* ctr, uint32_t* abort_word,
-                                            uint32_t target) {
+// one lane: spin until the counter reaches target (false: aborted or timed out -> abort word)
+__device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(ctr, TW_SEG_BARRIER == 1 ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+  while (__hip_atomic_load(ctl, TW_SEG_BARRIER == 1 ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+    if (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
         wall_clock64() - t0 > kSegSpinTicks) {
-      __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -117,19 +116,6 @@ __device__ __forceinline__ bool seg_poll_at(uint32_t* ctr, uint32_t* abort_word,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   return true;
-}
-
-// ctl[0] counter, ctl[1] abort word
-__device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
-  return seg_poll_at(ctl, ctl + 1, target);
-}
-
-// the whole block waits (thread 0 polls *ctr, abort word *abort_word)
-__device__ __forceinline__ bool seg_wait_at(uint32_t* ctr, uint32_t* abort_word,
-                                            uint32_t target, int* s_ok) {
-  if (threadIdx.x == 0) *s_ok = seg_poll_at(ctr, abort_word, target) ? 1 : 0;
-  __syncthreads();
-  return *s_ok != 0;
 }
 
 // the whole block waits (thread 0 polls)

@@ -194,7 +194,7 @@ class SGDEngine:
                      if self.narrow_seg or self.peer is not None else None)
         self.wide_fused = (WIDE_FUSED and self.solo and not self.complete and not self.fused
                            and bool(L.lib().tw_sgd_step_wide_ok(self.d, self.N_loc)))
-        # its grid barriers: the arrival counters of step parities 0 and 1, the abort word
+        # its grid barriers: [arrivals, abort] per step parity
         self._wctl = (t.zeros((4,), dtype=t.int32, device=self.w.device)
                       if self.wide_fused else None)
 
@@ -221,7 +221,7 @@ class SGDEngine:
         if self._ctl is not None and int(self._ctl[1].item()) != 0:
             raise RuntimeError("SGD segment: a grid barrier or peer wait timed out (blocks not "
                                "co-resident, or a rank stopped); the SGD state is invalid")
-        if self._wctl is not None and int(self._wctl[2].item()) != 0:
+        if self._wctl is not None and int(self._wctl[1::2].max().item()) != 0:
             raise RuntimeError("fused wide SGD step: a grid barrier timed out (blocks not "
                                "co-resident); the SGD state is invalid")
 
