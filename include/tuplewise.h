@@ -512,25 +512,6 @@ int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d, const int64_t* 
                 const double* d_w_in, const double* d_dw_in, const double* d_grads_in, double reg,
                 double lr, double momentum, double* d_w_out, double* d_dw_out,
                 double* d_grads_out, void* stream);
-/* The same segment structure for wide rows (32 < d <= 512, device RNG; C5): ONE launch per
- * step whose blocks first apply the PREVIOUS step's update spread over them (block b takes
- * columns [b*cpb, (b+1)*cpb), cpb = ceil(d / n_shards)) while this step's first rows are in
- * flight, meet at a grid barrier (d_ctl: 4 words, [arrivals, abort] for step parities 0 and 1,
- * zeroed once by the caller; an abort word != 0 afterwards: a block gave up waiting, the state
- * is invalid), then compute this step's gradients with the new w.  Draws at step counter
- * *d_step + step_off: swr_mod > 0 draws the SWR rows in the kernel (tw_pair_grad_rng_swr,
- * swr base 0), else the row tables d_rows_x / d_rows_z (tw_pair_grad_rng).  Slots and the
- * closing tw_sgd_update_to as tw_sgd_step; the same bits as gradient + tw_sgd_update launches.
- * tw_sgd_step_wide_ok: the shape qualifies and its n_shards blocks are co-resident. */
-int tw_sgd_step_wide_ok(int64_t d, int32_t n_shards);
-int tw_sgd_step_wide(const double* d_X, const double* d_Z, int64_t d, int64_t n_X, int64_t n_Z,
-                     const int64_t* d_rows_x, int64_t kx, const int64_t* d_rows_z, int64_t kz,
-                     int32_t n_shards, int64_t B, double margin, int32_t loss, uint64_t seed,
-                     const uint64_t* d_step, int32_t step_off, int32_t shard_base,
-                     int64_t swr_mod, const double* d_w_in, const double* d_dw_in,
-                     const double* d_grads_in, double reg, double lr, double momentum,
-                     double* d_w_out, double* d_dw_out, double* d_grads_out, uint32_t* d_ctl,
-                     void* stream);
 
 /* A segment of nsteps narrow-row SGD steps (d <= 32; the steps tw_sgd_step launches one by
  * one) in ONE persistent launch (csrc/sgdseg.hip k_sgd_segment_narrow): one block per shard,

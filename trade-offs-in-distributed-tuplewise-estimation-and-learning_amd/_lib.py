@@ -111,10 +111,6 @@ _SIGNATURES = {
     "tw_sgd_update": [_vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _vp],
     "tw_sgd_update_to": [_vp, _vp, _vp, _vp, _vp, _i32, _i64, _f64, _f64, _f64, _vp, _i32, _vp],
     "tw_sgd_step_fusable": [_i64, _i32],
-    "tw_sgd_step_wide_ok": [_i64, _i32],
-    "tw_sgd_step_wide": [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _f64,
-                         _i32, _u64, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _f64, _f64, _f64,
-                         _vp, _vp, _vp, _vp, _vp],
     "tw_sgd_step": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i64, _f64, _i32, _u64,
                     _vp, _i32, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
     "tw_count_rng_img_set_unroll": [_i32],

@@ -279,26 +279,6 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_wide(
   if (threadIdx.x < dd) out[(int64_t)s * d + threadIdx.x] = acc / (double)B;
 }
 
-// The fused wide step (tw_sgd_step_wide, FUSE): the PREVIOUS step's update spread over the
-// gradient launch's blocks (block b updates columns [b * cpb, (b + 1) * cpb)) while the first
-// rows of this step are in flight, a grid barrier, then the gradient with the new w.
-// grads_in == nullptr: no pending update (the segment's first step reads w_in).  ctl: this
-// launch's [arrivals, abort] pair; ctl_next: the other parity's arrival counter, zeroed here
-// for the next launch (which starts after every block of this one has finished).
-constexpr int kWideFuseUpd = 1536;  // n_shards * cpb staged per block (12 KiB)
-struct WideFuse {
-  const double* w_in;
-  const double* dw_in;
-  const double* grads_in;
-  double* w_out;
-  double* dw_out;
-  double reg, lr, momentum;
-  uint32_t* ctl;
-  uint32_t* ctl_next;
-  int n_shards;
-  uint32_t step_off;
-};
-
 // Streaming variant of k_hinge_grad_wide (the default for 32 < d <= 512): one pair per wave
 // per chunk (16-pair chunks) and TWO register stages, so the rows of chunks k+1 and k+2 are
 // in flight while chunk k is reduced — the loads form a continuous stream instead of one
@@ -308,33 +288,25 @@ struct WideFuse {
 // k_hinge_grad_wide (per pair: lane partial dots over the same 8 columns + the same butterfly;
 // column sums in row order), so identical bits.
 
-template <int LOSS, bool FUSE>
+template <int LOSS>
 __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     const double* __restrict__ X, const double* __restrict__ Z, int64_t d,
     const int64_t* __restrict__ rows_x, int64_t kx, const int64_t* __restrict__ rows_z,
     int64_t kz, const int64_t* __restrict__ ix, const int64_t* __restrict__ iz, int64_t B,
     const double* __restrict__ w, double margin, double* __restrict__ out, uint64_t seed,
-    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr, WideFuse fz) {
+    const uint64_t* __restrict__ d_step, uint32_t shard_base, SwrMap swr) {
   __shared__ double diff[2][kStreamCH * kWideMaxD];  // 128 KiB
   __shared__ int64_t prx[kIdxPhase], prz[kIdxPhase];  // 16 KiB
   __shared__ double flag[2][kStreamCH];
-  __shared__ double ug[FUSE ? kWideFuseUpd : 1];      // FUSE: this block's columns' shard grads
-  __shared__ int s_ok;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int dd = (int)d;
-  const uint64_t step = (d_step ? *d_step : 0) + (FUSE ? fz.step_off : 0u);
-  const bool pend = FUSE && fz.grads_in != nullptr;  // the previous step's update comes first
-  if (FUSE && blockIdx.x == 0 && threadIdx.x == 0)  // the next launch's barrier counter
-    __hip_atomic_store(fz.ctl_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t step = d_step ? *d_step : 0;
   double wv[kWideCols];
-  if (!pend) {
-    const double* wsrc = FUSE ? fz.w_in : w;
 #pragma unroll
-    for (int c = 0; c < kWideCols; ++c) {
-      const int j = lane + c * kWave;
-      wv[c] = j < dd ? wsrc[j] : 0.0;
-    }
+  for (int c = 0; c < kWideCols; ++c) {
+    const int j = lane + c * kWave;
+    wv[c] = j < dd ? w[j] : 0.0;
   }
   double acc = 0.0;  // thread j < d: column j
   double zv[2][kWideCols], xv[2][kWideCols];
@@ -410,44 +382,6 @@ __global__ __launch_bounds__(kWideBlock) void k_hinge_grad_stream(
     };
     load(0, 0);
     if (kStreamCH < np) load(1, kStreamCH);
-    if (FUSE && pend && P0 == 0) {
-      // the previous step's update (k_sgd_update's arithmetic) for this block's columns while
-      // the first rows are in flight, published with agent-scope stores; then every block
-      // waits for all blocks' columns and loads the new w
-      const int cpb = (dd + (int)gridDim.x - 1) / (int)gridDim.x;
-      const int c_lo = (int)blockIdx.x * cpb, nc = max(0, min(cpb, dd - c_lo));
-      const int nsh = fz.n_shards;
-      for (int e = threadIdx.x; e < nsh * nc; e += kWideBlock) {
-        const int r = e / nc, c = e - r * nc;
-        ug[e] = fz.grads_in[(int64_t)r * dd + c_lo + c];
-      }
-      __syncthreads();
-      if ((int)threadIdx.x < nc) {
-        const int j = c_lo + (int)threadIdx.x;
-        double sum = 0.0;  // shard order, as np.mean(axis=0) / k_sgd_update
-        int r = 0;
-        for (; r + 8 <= nsh; r += 8) {
-          double v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = ug[(r + u) * nc + threadIdx.x];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) sum += v[u];
-        }
-        for (; r < nsh; ++r) sum += ug[r * nc + threadIdx.x];
-        const double wj = fz.w_in[j], dwj = fz.dw_in[j];
-        const double g = sum / (double)nsh + fz.reg * wj;
-        const double st = fz.momentum >= 0.0 ? fz.momentum * dwj + fz.lr * g : fz.lr * g;
-        st_agent(fz.w_out + j, wj - st);
-        st_agent(fz.dw_out + j, st);
-      }
-      seg_arrive(fz.ctl);
-      if (!seg_wait(fz.ctl, gridDim.x, &s_ok)) return;  // gave up: the caller sees ctl[1]
-#pragma unroll
-      for (int c = 0; c < kWideCols; ++c) {
-        const int j = lane + c * kWave;
-        wv[c] = j < dd ? ld_agent(fz.w_out + j) : 0.0;
-      }
-    }
     int c0 = 0;
     for (; c0 + kStreamCH < np; c0 += 2 * kStreamCH) {  // stages alternate; constant indices
       chunk(0, c0);
@@ -705,9 +639,9 @@ void launch_grad_kernel(const double* X, const double* Z, int64_t d, const int64
                        d, rows_x, kx, rows_z, kz, ix, iz, B, CH, w, margin, out, seed, d_step,
                        shard_base, nullptr, swr);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 0)
-    hipLaunchKernelGGL((k_hinge_grad_stream<LOSS, false>), dim3(n_shards), dim3(kWideBlock), 0,
-                       st, X, Z, d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed,
-                       d_step, shard_base, swr, WideFuse{});
+    hipLaunchKernelGGL(k_hinge_grad_stream<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z,
+                       d, rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
+                       shard_base, swr);
   else if (d <= kWideMaxD && g_hinge_legacy_wide == 2)
     hipLaunchKernelGGL(k_hinge_grad_wide<LOSS>, dim3(n_shards), dim3(kWideBlock), 0, st, X, Z, d,
                        rows_x, kx, rows_z, kz, ix, iz, B, w, margin, out, seed, d_step,
@@ -1135,71 +1069,6 @@ extern "C" int tw_sgd_step(const double* d_X, const double* d_Z, int64_t d,
                        d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, d_ix, d_iz, B, CH, margin, seed,
                        d_step, (uint32_t)step_off, (uint32_t)shard_base, (int)n_shards, d_w_in,
                        d_dw_in, d_grads_in, reg, lr, momentum, d_w_out, d_dw_out, d_grads_out);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
-}
-
-// The fused wide step: co-residency of the n_shards blocks (the grid barrier) and the staged
-// update slice bound it
-extern "C" int tw_sgd_step_wide_ok(int64_t d, int32_t n_shards) {
-  if (d <= 32 || d > kWideMaxD || n_shards < 1 ||
-      (int64_t)n_shards * ((d + n_shards - 1) / n_shards) > kWideFuseUpd)
-    return 0;
-  int dev = 0, per_cu = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, k_hinge_grad_stream<TW_LOSS_HINGE, true>, kWideBlock, 0) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  return (int64_t)per_cu * cus >= n_shards;
-}
-
-// One wide SGD step (32 < d <= 512) in ONE launch: the previous step's update (grads_in: its
-// shard gradients, w_in / dw_in -> w_out / dw_out) spread over the blocks behind a grid
-// barrier, then this step's gradient (tw_pair_grad_rng's draws at step counter *d_step +
-// step_off; swr_mod > 0: the SWR rows drawn in the kernel, else the row tables) with the new
-// w into grads_out.  grads_in == NULL: no pending update (w_in is this step's w).  d_ctl: 4
-// words, the barrier pairs [arrivals, abort] of step parities 0 and 1 (zeroed once by the
-// caller; an abort word != 0 afterwards means a block gave up waiting).  Same bits as
-// tw_pair_grad_rng(_swr) + tw_sgd_update per step.
-extern "C" int tw_sgd_step_wide(const double* d_X, const double* d_Z, int64_t d, int64_t n_X,
-                                int64_t n_Z, const int64_t* d_rows_x, int64_t kx,
-                                const int64_t* d_rows_z, int64_t kz, int32_t n_shards,
-                                int64_t B, double margin, int32_t loss, uint64_t seed,
-                                const uint64_t* d_step, int32_t step_off, int32_t shard_base,
-                                int64_t swr_mod, const double* d_w_in, const double* d_dw_in,
-                                const double* d_grads_in, double reg, double lr,
-                                double momentum, double* d_w_out, double* d_dw_out,
-                                double* d_grads_out, uint32_t* d_ctl, void* stream) {
-  TW_ARG_CHECK(d > 32 && d <= kWideMaxD && n_shards >= 1 &&
-                   (int64_t)n_shards * ((d + n_shards - 1) / n_shards) <= kWideFuseUpd,
-               "tw_sgd_step_wide: d=%lld, n_shards=%d unsupported", (long long)d, n_shards);
-  TW_ARG_CHECK(B >= 1 && B < (1ll << 32) && kx >= 1 && kz >= 1 && step_off >= 0 &&
-                   shard_base >= 0 && swr_mod >= 0 && d_step != nullptr && d_ctl != nullptr,
-               "tw_sgd_step_wide: bad B/kx/kz/step_off/shard_base/swr_mod/step/ctl");
-  TW_ARG_CHECK(swr_mod > 0 ? (n_X >= 1 && n_Z >= 1) : (d_rows_x && d_rows_z),
-               "tw_sgd_step_wide: row tables, or n_X / n_Z with swr_mod");
-  TW_ARG_CHECK(d_w_in && d_grads_out &&
-                   (d_grads_in == nullptr || (d_dw_in && d_w_out && d_dw_out)),
-               "tw_sgd_step_wide: a pending update needs dw_in, w_out, dw_out");
-  if (int rc = check_loss(loss)) return rc;
-  const int par = step_off & 1;
-  WideFuse fz{d_w_in, d_dw_in, d_grads_in, d_w_out, d_dw_out, reg, lr, momentum,
-              d_ctl + 2 * par, d_ctl + 2 * (1 - par), (int)n_shards, (uint32_t)step_off};
-  const SwrMap swr = swr_mod > 0 ? SwrMap{(uint64_t)swr_mod, 0, n_X, n_Z} : SwrMap{0, 0, 1, 1};
-  hipStream_t st = (hipStream_t)stream;
-  if (loss == TW_LOSS_LOGISTIC)
-    hipLaunchKernelGGL((k_hinge_grad_stream<TW_LOSS_LOGISTIC, true>), dim3(n_shards),
-                       dim3(kWideBlock), 0, st, d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, nullptr,
-                       nullptr, B, nullptr, margin, d_grads_out, seed, d_step,
-                       (uint32_t)shard_base, swr, fz);
-  else
-    hipLaunchKernelGGL((k_hinge_grad_stream<TW_LOSS_HINGE, true>), dim3(n_shards),
-                       dim3(kWideBlock), 0, st, d_X, d_Z, d, d_rows_x, kx, d_rows_z, kz, nullptr,
-                       nullptr, B, nullptr, margin, d_grads_out, seed, d_step,
-                       (uint32_t)shard_base, swr, fz);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

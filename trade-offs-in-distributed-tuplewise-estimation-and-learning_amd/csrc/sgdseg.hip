@@ -29,8 +29,75 @@
 
 namespace tw {
 
-// the grid-barrier helpers (ld_agent / st_agent, seg_arrive / seg_poll / seg_wait) live in
-// sgd_common.h: the fused wide step (csrc/hinge.hip) uses them too
+constexpr uint64_t kSegSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ double ld_agent(const double* p) {
+  const uint64_t v = __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ctl[0]: arrivals (monotonic within a launch, zeroed before it); ctl[1]: abort word, sticky
+// (zeroed once by the caller: a later launch that finds it set exits at its first wait).
+// Memory-model contract of the grid barrier: every published word is an agent-scope atomic
+// store (st_agent); each storing wave waits for its own stores (s_waitcnt vmcnt(0) — the
+// block barrier's workgroup-scope release does not wait for another wave's vector stores to
+// reach the agent-coherent level), the block barrier orders them before thread 0's arrival,
+// and the arrival is an agent-scope RELEASE add (gfx950: buffer_wbl2 sc1 before the atomic).
+// The poller spins on RELAXED loads of the counter and, once it has seen the target, issues
+// ONE agent-scope ACQUIRE fence (buffer_inv sc1) — acquire loads in the spin itself would
+// invalidate the L2 on every iteration; the fence after the last relaxed load that read the
+// release's value gives the same synchronisation (fence-atomic rule), and s_waitcnt vmcnt(0)
+// holds the block barrier after the poll until the invalidate has completed, so every wave's
+// loads of the published words (ld_agent) come after it.
+// TW_SEG_BARRIER (A/B builds, tools/ab_barrier.py): 0 = relaxed arrival and spin, no fence
+// (round 3); 1 = acquire loads in the spin; 2 (default) = as above.
+#ifndef TW_SEG_BARRIER
+#define TW_SEG_BARRIER 2
+#endif
+// arriver: the thread that adds the arrival — the release's L2 write-back (~0.6 us on gfx950)
+// stalls only its wave, so the narrow kernel hands it to the last wave, which has no pairs in
+// the next step's chain when B <= 192 (C4: B = 100): the stall hides behind the other waves'
+// draws -> rows -> diff rows (tools/ab_barrier.py)
+__device__ __forceinline__ void seg_arrive(uint32_t* ctl, int arriver = 0) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's published stores landed
+  __syncthreads();
+  if ((int)threadIdx.x == arriver)
+    __hip_atomic_fetch_add(ctl, 1u, TW_SEG_BARRIER ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane: spin until the counter reaches target (false: aborted or timed out -> abort word)
+__device__ __forceinline__ bool seg_poll(uint32_t* ctl, uint32_t target) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(ctl, TW_SEG_BARRIER == 1 ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+        wall_clock64() - t0 > kSegSpinTicks) {
+      __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (TW_SEG_BARRIER == 2) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the invalidate completes before the block barrier lets any wave load (the consumer
+    // recipe of MI355X_MICROARCH.md: relaxed poll -> acquire -> vmcnt(0) -> barrier -> loads)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  return true;
+}
+
+// the whole block waits (thread 0 polls)
+__device__ __forceinline__ bool seg_wait(uint32_t* ctl, uint32_t target, int* s_ok) {
+  if (threadIdx.x == 0) *s_ok = seg_poll(ctl, target) ? 1 : 0;
+  __syncthreads();
+  return *s_ok != 0;
+}
 
 // ---- peers: the narrow segment over ranks (round 5) ----------------------------------------
 // With several ranks (one process per GPU) the shard gradients of a step are exchanged IN the

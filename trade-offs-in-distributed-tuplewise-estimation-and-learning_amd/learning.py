@@ -31,10 +31,6 @@ SEED_SHUFFLE = 42
 # narrow rows (C4): a segment of fused steps in ONE persistent launch (tw_sgd_segment_narrow:
 # one grid barrier per step, the update recomputed in every block); off: one launch per step
 NARROW_SEGMENT = True
-# wide rows (32 < d <= 512, C5) on one GPU: one launch per device-RNG step (tw_sgd_step_wide:
-# the previous step's update spread over the gradient launch's blocks behind a grid barrier,
-# overlapping this step's first row loads) instead of a gradient and an update launch
-WIDE_FUSED = True
 # replay loop: the host's NumPy-exact draws made two segments ahead by a worker thread
 # (_replay_pipelined); False keeps the sequential loop (A/B, tests)
 DRAW_AHEAD = True
@@ -192,11 +188,6 @@ class SGDEngine:
                          and bool(L.lib().tw_sgd_segment_narrow_ok(self.d, self.N, self.B)))
         self._ctl = (t.zeros((2,), dtype=t.int32, device=self.w.device)
                      if self.narrow_seg or self.peer is not None else None)
-        self.wide_fused = (WIDE_FUSED and self.solo and not self.complete and not self.fused
-                           and bool(L.lib().tw_sgd_step_wide_ok(self.d, self.N_loc)))
-        # its grid barriers: [arrivals, abort] per step parity
-        self._wctl = (t.zeros((4,), dtype=t.int32, device=self.w.device)
-                      if self.wide_fused else None)
 
     def reload(self, X, Z, w_init):
         """A new run on this engine (learning_process's engine cache): X, Z (host arrays of
@@ -211,8 +202,6 @@ class SGDEngine:
         self.dw.zero_()
         if self._ctl is not None:
             self._ctl.zero_()
-        if self._wctl is not None:
-            self._wctl.zero_()
 
     def check(self):
         """Raise if a persistent segment launch gave up waiting at a grid barrier, or a peer
@@ -221,9 +210,6 @@ class SGDEngine:
         if self._ctl is not None and int(self._ctl[1].item()) != 0:
             raise RuntimeError("SGD segment: a grid barrier or peer wait timed out (blocks not "
                                "co-resident, or a rank stopped); the SGD state is invalid")
-        if self._wctl is not None and int(self._wctl[1::2].max().item()) != 0:
-            raise RuntimeError("fused wide SGD step: a grid barrier timed out (blocks not "
-                               "co-resident); the SGD state is invalid")
 
     def table_stacks(self, ntab: int):
         """Replay segments through reshuffles (tw_sgd_segment_narrow_tables): the row tables
@@ -307,32 +293,6 @@ class SGDEngine:
                    L.ptr(DW[a] if pend else None), L.ptr(Gs[a] if pend else None), self.reg,
                    self.lr, self.momentum, L.ptr(W[b] if pend else None),
                    L.ptr(DW[b] if pend else None), L.ptr(Gs[b]), s)
-        last = (nsteps - 1) & 1
-        L.call("tw_sgd_update_to", L.ptr(W[last]), L.ptr(DW[last]), L.ptr(W[0]), L.ptr(DW[0]),
-               L.ptr(Gs[last]), self.N, self.d, self.reg, self.lr, self.momentum,
-               L.ptr(self.step_ctr), nsteps, s)
-
-    def _wide_steps(self, nsteps: int, swr_mod: int = 0):
-        """nsteps device-RNG steps of wide rows as nsteps tw_sgd_step_wide launches (step k's
-        launch applies step k-1's update across its blocks, then computes step k's gradient)
-        + one tw_sgd_update_to; ping-pong slots as _fused_steps.  Same bits as step_device()
-        per step."""
-        t = self.t
-        if self._slot1 is None:
-            self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw), t.empty_like(self.grads))
-        W, DW, Gs = zip((self.w, self.dw, self.grads), self._slot1)
-        s = L.stream_handle()
-        for k in range(nsteps):
-            a, b = (k - 1) & 1, k & 1
-            pend = k > 0
-            L.call("tw_sgd_step_wide", L.ptr(self.X), L.ptr(self.Z), self.d, self.n_X, self.n_Z,
-                   L.ptr(self.rows_x) if not swr_mod else None, self.kx,
-                   L.ptr(self.rows_z) if not swr_mod else None, self.kz, self.N_loc, self.B,
-                   self.margin, self.loss, self.seed, L.ptr(self.step_ctr), k, self.shard_base,
-                   int(swr_mod), L.ptr(W[a] if pend else W[0]), L.ptr(DW[a] if pend else None),
-                   L.ptr(Gs[a] if pend else None), self.reg, self.lr, self.momentum,
-                   L.ptr(W[b] if pend else None), L.ptr(DW[b] if pend else None),
-                   L.ptr(Gs[b]), L.ptr(self._wctl), s)
         last = (nsteps - 1) & 1
         L.call("tw_sgd_update_to", L.ptr(W[last]), L.ptr(DW[last]), L.ptr(W[0]), L.ptr(DW[0]),
                L.ptr(Gs[last]), self.N, self.d, self.reg, self.lr, self.momentum,
@@ -780,9 +740,7 @@ class SGDEngine:
             reshuffle_first = False
 
         def steps(n):
-            if self.wide_fused:
-                self._wide_steps(n, swr_mod)
-            elif swr_mod:
+            if swr_mod:
                 for _ in range(n):
                     self.step_device(swr_mod=swr_mod)
             elif self.peer_seg:
@@ -798,7 +756,7 @@ class SGDEngine:
                 self.reshuffle_device()
             steps(nsteps)
             return
-        if (self.fused or self.wide_fused) and self._slot1 is None:  # outside any capture
+        if self.fused and self._slot1 is None:  # allocated outside any capture
             self._slot1 = (t.empty_like(self.w), t.empty_like(self.dw), t.empty_like(self.grads))
         while nsteps > 0:
             n = min(nsteps, 256)
