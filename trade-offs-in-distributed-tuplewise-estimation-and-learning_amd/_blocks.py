@@ -584,6 +584,8 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
         shuffle_draws32(a.shape[0], out=ds.draw_x())
         _mark("x drawn")
         ds.push_x()
+        if step[0] == T - 1 and THREADED_LAUNCHES:
+            ds.write_back_x_async(X)  # X's last state goes back while Z's last draws are made
         if step[0] == T - 1 and STREAM_LAST_SHUFFLE:
             ds.draw_push_z_streamed(STREAM_LAST_SHUFFLE)
         else:
@@ -609,7 +611,11 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
             _mark("counts submitted")
     _mark("pushed")
     # the in-place side effect, X first: its last state goes back while Z's last shuffle runs
-    t.from_numpy(X).copy_(ds.last_x())
+    # (threaded: already on its way since X's last push)
+    if THREADED_LAUNCHES:
+        ds.drain_write_back()
+    else:
+        t.from_numpy(X).copy_(ds.last_x())
     _mark("x written back")
     xs, zs = ds.finish()  # (drains the launcher: every count task has run)
     _mark("finish")

@@ -352,10 +352,11 @@ class _Launcher:
 _LAUNCHERS = {}
 
 
-def launcher(dev) -> _Launcher:
-    if dev not in _LAUNCHERS:
-        _LAUNCHERS[dev] = _Launcher(dev)
-    return _LAUNCHERS[dev]
+def launcher(dev, name: str = "launch") -> _Launcher:
+    """The device's worker thread of that name (made once)."""
+    if (dev, name) not in _LAUNCHERS:
+        _LAUNCHERS[(dev, name)] = _Launcher(dev)
+    return _LAUNCHERS[(dev, name)]
 
 
 def side_stream(name: str):
@@ -416,8 +417,11 @@ class DeviceShuffles:
                         self.x0.copy_(t.from_numpy(np.ascontiguousarray(x0).reshape(-1)))
                     with t.cuda.stream(self.sz):
                         self.z0.copy_(t.from_numpy(np.ascontiguousarray(z0).reshape(-1)))
-            self._up = threading.Thread(target=upload)
-            self._up.start()
+            if threaded:  # the launcher's first task: before every push, beside the draws
+                launcher(dev).submit(upload)
+            else:
+                self._up = threading.Thread(target=upload)
+                self._up.start()
         else:
             assert x0.element_size() == 8 and z0.element_size() == 8
             self.x0, self.z0 = x0.reshape(-1), z0.reshape(-1)
@@ -547,6 +551,34 @@ class DeviceShuffles:
         xs = self.xs if side == 0 else self.zs
         xs[k].copy_((self.x0 if side == 0 else self.z0) if k == 0 else xs[k - 1])
         self._run(side, k, True, 0)
+
+    def write_back_x_async(self, x_host) -> None:
+        """Copy X's last state into the host array x_host on the device's write-back thread, as
+        soon as X's last shuffle has run — while this thread draws Z's last shuffle (threaded
+        only; drain_write_back() waits for it)."""
+        t, T = self.t, self.T
+        wb = launcher(self._launcher.dev, "writeback")
+        stream = side_stream("x-writeback")
+        out = t.from_numpy(x_host).reshape(-1)
+
+        def record():  # on the launcher thread, after X's last push was enqueued
+            ev = t.cuda.Event()
+            ev.record(self.sx)
+
+            def copy():
+                stream.wait_event(ev)
+                with t.cuda.stream(stream):
+                    out.copy_(self.xs[T - 1])
+            wb.submit(copy)
+        self.submit(record)
+        self._wb = wb
+
+    def drain_write_back(self) -> None:
+        wb = getattr(self, "_wb", None)
+        if wb is not None:
+            self.drain()  # the record task ran, so the copy is queued
+            wb.drain()
+            self._wb = None
 
     def last_x(self):
         """The X side's last state, ordered on the current stream after its shuffles (a
