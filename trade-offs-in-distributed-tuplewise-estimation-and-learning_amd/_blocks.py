@@ -524,9 +524,11 @@ DEVICE_SHUFFLE_MIN = 1 << 16
 # device-shuffle drop-in call
 DROPIN_MARKS = None
 # the device-shuffle drop-in's pipelining (round 5): the counts of step k enqueued while the
-# host draws step k + 1; the call's last shuffle drawn and pushed in this many parts (0: whole)
-EARLY_COUNTS = True
-STREAM_LAST_SHUFFLE = 8
+# host draws step k + 1 (off: measured slower once the launches moved to the launcher thread —
+# its enqueue work there competes with the drawing thread; profiles/r05s28_dropin_*.log); the
+# call's last shuffle drawn and pushed in this many parts (0: whole)
+EARLY_COUNTS = False
+STREAM_LAST_SHUFFLE = 4
 # ... and the uploads, swap-round launches and count enqueues made on a launcher thread
 # (_engine.launcher), off the thread that makes the draws
 THREADED_LAUNCHES = True
@@ -584,8 +586,6 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
         shuffle_draws32(a.shape[0], out=ds.draw_x())
         _mark("x drawn")
         ds.push_x()
-        if step[0] == T - 1 and THREADED_LAUNCHES:
-            ds.write_back_x_async(X)  # X's last state goes back while Z's last draws are made
         if step[0] == T - 1 and STREAM_LAST_SHUFFLE:
             ds.draw_push_z_streamed(STREAM_LAST_SHUFFLE)
         else:
@@ -611,15 +611,17 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
             _mark("counts submitted")
     _mark("pushed")
     # the in-place side effect, X first: its last state goes back while Z's last shuffle runs
-    # (threaded: already on its way since X's last push)
+    # (threaded: on the write-back thread, beside this thread's wait for Z and Z's write-back;
+    # not earlier — beside the last draws it slowed them)
     if THREADED_LAUNCHES:
-        ds.drain_write_back()
+        ds.write_back_x_async(X)
     else:
         t.from_numpy(X).copy_(ds.last_x())
     _mark("x written back")
     xs, zs = ds.finish()  # (drains the launcher: every count task has run)
     _mark("finish")
     if 0 in ds.redone:  # (rare) X's shuffles were resumed: its last state changed
+        ds.drain_write_back()
         t.from_numpy(X).copy_(xs[T - 1])
     if ds.redone:  # (rare) later states changed: every step is counted again below
         pending.clear()
@@ -644,6 +646,7 @@ def _run_un_repeated_device(X, Z, N, spec, sampling_type, variant: str, T: int):
     ds.order_after(wb)
     with t.cuda.stream(wb):
         t.from_numpy(Z).copy_(zs[T - 1])
+    ds.drain_write_back()  # X's copy (threaded) has landed too
     _mark("z written back")
     if done_rest is not None:
         vals = done_rest()
