@@ -38,8 +38,9 @@ CHAIN_MAX = 32
 # O(n + m) on their integer rank images (tw_count_pairs_chain_bucket); larger shards keep the
 # records path (tw_count_pairs_sorted_steps)
 CHAIN_BUCKET_MAX = 16384
-# several ranks: the steps of a chunk exchanged in sub-chunks of this many steps, each its own
-# (async) all-to-all, so the exchange of one sub-chunk overlaps the counts of the previous
+# several ranks: the steps of a chunk exchanged in sub-chunks of at most this many steps (and
+# at least two sub-chunks), each its own (async) all-to-all, so the exchange of one sub-chunk
+# overlaps the counts of the previous
 CHAIN_SUB = 5
 # one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
 # images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
@@ -843,7 +844,9 @@ class ShardedSample:
             tot = n + m
             cap = max(1, tot // G + tot // (8 * G) + 1024)
             W = 2 if half else 1
-            Sub = max(1, min(C, CHAIN_SUB))
+            # (at least two sub-chunks per chunk: with one, est.UnNT's T = 4 left its whole
+            # exchange exposed before the first count)
+            Sub = max(1, min(CHAIN_SUB, -(-C // 2)))
             nsub = -(-C // Sub)
             # the send / receive ring persists on the sample across calls (fresh
             # GB-scale allocations per call made the caching allocator flush and re-map)
