@@ -817,11 +817,27 @@ class ShardedSample:
         xr, zr = rec
         T = len(keys)
         C = min(T, CHAIN_MAX)
-        kx = int(n / N)
-        kz = int((n + m) / N) - kx  # prop_swor_layout's shard sizes
         M64 = 2 ** 64 - 1
         kxs = [(2 * k) & M64 for k in keys]
         kzs = [(2 * k + 1) & M64 for k in keys]
+        final = None
+        if coll and self.X.is_cuda:
+            # the final arrays depend on the keys and the all-gathered sample only: gathered on
+            # a side stream beside the emission, exchanges and counts (not after them)
+            main = t.cuda.current_stream()
+            if getattr(self, "_final_stream", None) is None:
+                self._final_stream = t.cuda.Stream()
+            fs = self._final_stream
+            fs.wait_stream(main)
+            with t.cuda.stream(fs):
+                if x_work is not None:
+                    x_work.wait()
+                    x_work = None
+                final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
+                for a in final:
+                    a.record_stream(main)
+        kx = int(n / N)
+        kz = int((n + m) / N) - kx  # prop_swor_layout's shard sizes
         z_total = int(Z0.numel())  # the Z the images were ranked against: images <= z_total
 
         def count(xb, zb, steps, out):  # the bags of `steps` steps -> out (steps, N)
@@ -886,9 +902,13 @@ class ShardedSample:
                            cursors=cursors)
             count(x_bag, z_bag, c, counts[i0:i0 + c])
         if coll:
-            if x_work is not None:
-                x_work.wait()
-            self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
+            if final is not None:
+                t.cuda.current_stream().wait_stream(self._final_stream)
+                self.X, self.Z = final
+            else:
+                if x_work is not None:
+                    x_work.wait()
+                self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
             counts = self._reduce_counts(counts)
         else:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
