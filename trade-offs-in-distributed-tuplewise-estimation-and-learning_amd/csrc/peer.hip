@@ -59,7 +59,8 @@ __global__ __launch_bounds__(kBlock) void k_peer_step(const double* __restrict__
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < words;
        i += (int64_t)gridDim.x * kBlock) {
     const double v = src[i];
-    for (int p = 0; p < ps.G; ++p) st_sys(ps.slot[p] + base + i, v);
+    for (int p = 0; p < ps.G; ++p)  // the peers' slots; this rank reads its own rows from src
+      if (ps.slot[p] != ps.my_slot) st_sys(ps.slot[p] + base + i, v);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores (and the reset) done
   __syncthreads();
@@ -79,7 +80,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_step(const double* __restrict__
       __syncthreads();
       for (int e = threadIdx.x; e < ns * kPUpdCols; e += kBlock) {
         const int r = e / kPUpdCols, c = e - r * kPUpdCols;
-        tile[e] = c < nc ? ld_sys(slot + (int64_t)(s0 + r) * d + j0 + c) : 0.0;
+        const int64_t at = (int64_t)(s0 + r) * d + j0 + c;  // word of the global slot
+        tile[e] = c >= nc ? 0.0 : (at >= off && at < off + words) ? src[at - off]
+                                                                   : ld_sys(slot + at);
       }
       __syncthreads();
       if ((int)threadIdx.x < nc) {
