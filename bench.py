@@ -480,7 +480,9 @@ def sgd_steps_per_s(n_X, n_Z, d, N, B, reshuffle_mod, steps, warmup, layout="rep
                 "gradient launch + one publish-wait-update launch per step (csrc/peer.hip)"
                 if getattr(eng, "peer", None) is not None else
                 "one persistent launch per run of <= 4096 steps, reshuffles drawn in the "
-                "kernel" if swr else
+                "kernel" if swr and eng.narrow_seg else
+                "gradient + update launch per step (hipGraph-replayed segments), each "
+                "reshuffle's rows drawn in the gradient kernel" if swr else
                 "one persistent launch per segment" if eng.narrow_seg else
                 "one launch per step" if eng.fused else "gradient + update per step")
     G = 1 if group is None else torch.distributed.get_world_size(group)
