@@ -54,10 +54,18 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 // release's value gives the same synchronisation (fence-atomic rule), and s_waitcnt vmcnt(0)
 // holds the block barrier after the poll until the invalidate has completed, so every wave's
 // loads of the published words (ld_agent) come after it.
-// TW_SEG_BARRIER (A/B builds, tools/ab_barrier.py): 0 = relaxed arrival and spin, no fence
-// (round 3); 1 = acquire loads in the spin; 2 (default) = as above.
+// TW_SEG_BARRIER (A/B builds, tools/ab_barrier.py): 0 (default since round 5) = relaxed
+// arrival and spin, no fence; 1 = acquire loads in the spin; 2 = the release/acquire form
+// above (round 4).  Form 0 is the fence-free hand-off of MI355X_MICROARCH.md §Workgroup
+// dispatch, "Valid forms": EVERY handed-off word goes out as an sc1 store (st_agent) and comes
+// back as an sc1 load (ld_agent), each storing wave drains them (s_waitcnt vmcnt(0)) before the
+// workgroup barrier and ONE lane's agent-scope atomic add, and the consumer polls with sc1
+// loads and joins a workgroup barrier before loading — no L2 write-back per arrival and no
+// invalidate per poll (the peer segment has used the same form at system scope all round).
+// C4: 124-125k steps/s with form 2 against 132k with form 0 (profiles/
+// r04s8_ab_barrier_fence_wait.log).
 #ifndef TW_SEG_BARRIER
-#define TW_SEG_BARRIER 2
+#define TW_SEG_BARRIER 0
 #endif
 // arriver: the thread that adds the arrival — the release's L2 write-back (~0.6 us on gfx950)
 // stalls only its wave, so the narrow kernel hands it to the last wave, which has no pairs in
