@@ -182,10 +182,14 @@ int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec,
                   void* d_x_bag, void* d_z_bag, uint32_t* d_cursors, uint64_t* d_send,
                   int64_t cap, int32_t* d_flag, void* stream);
 /* The receiving side of tw_chain_emit's buckets after an equal-split all-to-all (d_recv: world
- * chunks in source order): every record into the bags at its position; a count past cap sets
- * *d_flag. */
+ * chunks in source order): every record appended to the bag region of its (step, side, shard)
+ * — shard b of a side holds positions [min(b k, n), min((b+1) k, n)), k = x_shard / z_shard,
+ * b = n_shards the tail — in runs reserved on d_cursors (steps x 2 (n_shards + 1) u32, zeroed
+ * here); a bag holds its shard's multiset, in no particular order (what the counts read).  A
+ * count past cap sets *d_flag. */
 int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
-                    int32_t half, int64_t n_x, int64_t n_z, void* d_x_bag, void* d_z_bag,
+                    int32_t half, int64_t n_x, int64_t n_z, int64_t x_shard, int64_t z_shard,
+                    int32_t n_shards, void* d_x_bag, void* d_z_bag, uint32_t* d_cursors,
                     int32_t* d_flag, void* stream);
 /* The all-pairs counts of `steps` x n_shards bags in ONE launch: bag (c, s) = x images
  * [c * x_stride + d_x_off[s], c * x_stride + d_x_off[s + 1]) against z images likewise;

@@ -217,7 +217,9 @@ class OracleOpsChain(OracleOpsRank):
                     else:
                         recs[:, 0], recs[:, 1] = v, q
 
-    def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag):
+    def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx=0, kz=0,
+                     n_shards=0):
+        # (positions kept: the device appends each shard's records in runs, in any order)
         W = 2 if half else 1
         buf = recv.numpy().view(np.uint64)
         for b in range(world * steps):

@@ -164,7 +164,9 @@ def test_chain_exchange_simulated_ranks(gpu, G, half):
                             device="cuda")
         z_bag = torch.empty((T, m_loc), dtype=torch.float32, device="cuda")
         flag = torch.zeros(1, dtype=torch.int32, device="cuda")
-        ops.chain_unpack(recv, G, T, cap, half, n_loc, m_loc, x_bag, z_bag, flag)
+        ops.chain_unpack(recv, G, T, cap, half, n_loc, m_loc, x_bag, z_bag, flag, kx, kz, N)
+        assert int(flag.item()) == 0
+        # (the bags hold their shards' multisets in no particular order: the counts check them)
         out = torch.empty((T, N), dtype=torch.int64, device="cuda")
         ops.count_chain(x_bag, xo, z_bag, zo, N, T, n_loc, m_loc, kx, kz, half, out)
         counts.append(out.cpu().numpy())
@@ -328,7 +330,7 @@ def test_chain_overflow_flag(gpu):
     flag.zero_()
     x_bag = torch.zeros((1, n), dtype=torch.float32, device="cuda")
     z_bag = torch.zeros((1, m), dtype=torch.float32, device="cuda")
-    ops.chain_unpack(send, G, 1, cap, False, n, m, x_bag, z_bag, flag)
+    ops.chain_unpack(send, G, 1, cap, False, n, m, x_bag, z_bag, flag, 50, 40, 10)
     assert int(flag.item()) == 1
 
 

@@ -118,7 +118,7 @@ def rank_call(G, r, K, parts=False):
                 sz = G * c * (cap + 1)
                 mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
                 mark("unpack", lambda: ops.chain_unpack(recv, G, c, cap, False, nl, nl, x_bag,
-                                                        z_bag, flag))
+                                                        z_bag, flag, kx, kz, Nl))
             mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz,
                                                   False, counts[i0:i0 + c]))
         if G == 1:

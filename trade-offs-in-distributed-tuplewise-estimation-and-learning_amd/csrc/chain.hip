@@ -16,7 +16,8 @@
 //    (step, shard) and block, runs written coalesced (records.h's staging).  Over several ranks a
 //    rank walks only ITS OWN elements and appends {image, local position} records to one
 //    fixed-capacity bucket per (destination rank, step); ONE equal-split all-to-all per chunk
-//    moves them and k_chain_unpack writes them into the receiver's bags at their positions.
+//    moves them and k_chain_unpack appends them to the receiver's (step, shard) bags (runs
+//    reserved per block: a bag's multiset is what the count needs, not positions).
 //  * k_count_chain: the C x N (step, shard) bags counted in one launch (k_count_rank's packed
 //    f32 compare-and-count, its work items, XCD order and epilogue), counts [C][N].
 //  * at the end of the call the scores in their final order: one scatter by the chains' last
@@ -280,17 +281,24 @@ __global__ __launch_bounds__(kBlock) void k_chain_zero_heads(uint64_t* __restric
     send[i * stride] = 0;
 }
 
-// Receiver side: every record of bucket (source g, step c) into the step's bags at its
-// position.  Logical blocks are step-major and dealt to the XCDs in contiguous ranges
-// (xcd_block), so one step's bag region (a few MB) is written through ONE L2, where the
-// partial-line writes of its scattered positions merge before they reach HBM.
-__global__ __launch_bounds__(kBlock) void k_chain_unpack(const uint64_t* __restrict__ recv,
-                                                         int world, int steps, int parts,
-                                                         int64_t cap, int W, int half,
-                                                         int64_t nx, int64_t nz,
-                                                         void* __restrict__ xbag,
-                                                         uint32_t* __restrict__ zbag,
-                                                         int* __restrict__ flag) {
+// Receiver side: every record of bucket (source g, step c) appended to its (step, side, shard)
+// bag region.  The count needs each bag's multiset, not the positions inside it, so a block
+// histograms its records over the step's 2 (nsh + 1) regions in LDS, reserves one run per
+// (block, region) with one global atomic on the step's cursors, and writes each record into
+// its run — whole lines per run, where one scattered 4-B store per record at its position
+// (round 4) made every line a partial write: 0.37 ms per 20 steps at G = 2, whose 4-MB step
+// bags overflow an XCD's L2.  Region b of a side starts at min(b k, n) (em_region: shard b,
+// and b = nsh the tail that belongs to no shard).  Logical blocks are step-major and dealt to
+// the XCDs in contiguous ranges (xcd_block), so one step's runs meet in one L2.
+constexpr int kUnpackPer = 4;  // records per thread and round
+__global__ __launch_bounds__(kBlock) void k_chain_unpack(
+    const uint64_t* __restrict__ recv, int world, int steps, int parts, int64_t cap, int W,
+    int half, int64_t nx, int64_t nz, int64_t kx, int64_t kz, int nsh, void* __restrict__ xbag,
+    uint32_t* __restrict__ zbag, unsigned* __restrict__ cursors, int* __restrict__ flag) {
+  extern __shared__ unsigned un_lds[];  // hist[NB], base[NB]
+  const int NB = 2 * (nsh + 1);
+  unsigned* hist = un_lds;
+  unsigned* base = un_lds + NB;
   const int lb = xcd_block(blockIdx.x, gridDim.x);
   const int c = lb / (world * parts);
   const int rem = lb - c * world * parts;
@@ -299,18 +307,57 @@ __global__ __launch_bounds__(kBlock) void k_chain_unpack(const uint64_t* __restr
   const int64_t cnt0 = (int64_t)(uint32_t)b[0];
   if (cnt0 > cap && part == 0 && threadIdx.x == 0) *flag = 1;
   const int64_t cnt = cnt0 < cap ? cnt0 : cap;
-  for (int64_t i = (int64_t)part * kBlock + threadIdx.x; i < cnt; i += (int64_t)parts * kBlock) {
-    const uint64_t* r = b + (1 + i) * W;
-    const uint64_t v = W == 1 ? (r[0] & 0xFFFFFFFFull) : r[0];
-    const int64_t p = W == 1 ? (int64_t)(r[0] >> 32) : (int64_t)r[1];
-    if (p < nx) {
-      if (half)
-        ((uint64_t*)xbag)[(int64_t)c * nx + p] = v;
-      else
-        ((uint32_t*)xbag)[(int64_t)c * nx + p] = (uint32_t)v;
-    } else if (p < nx + nz) {
-      zbag[(int64_t)c * nz + (p - nx)] = (uint32_t)v;
+  unsigned* cur = cursors + (int64_t)c * NB;
+  for (int j = threadIdx.x; j < NB; j += kBlock) hist[j] = 0;
+  __syncthreads();
+  constexpr int64_t kRound = (int64_t)kBlock * kUnpackPer;
+  for (int64_t i0 = (int64_t)part * kRound; i0 < cnt; i0 += (int64_t)parts * kRound) {
+    uint64_t v[kUnpackPer];
+    int bk[kUnpackPer];
+    unsigned slot[kUnpackPer];
+#pragma unroll
+    for (int u = 0; u < kUnpackPer; ++u) {
+      const int64_t i = i0 + (int64_t)u * kBlock + threadIdx.x;
+      bk[u] = -1;
+      v[u] = 0;
+      slot[u] = 0;
+      if (i < cnt) {
+        const uint64_t* r = b + (1 + i) * W;
+        v[u] = W == 1 ? (r[0] & 0xFFFFFFFFull) : r[0];
+        const int64_t p = W == 1 ? (int64_t)(r[0] >> 32) : (int64_t)r[1];
+        if (p < nx) {
+          bk[u] = kx > 0 ? (int)min<int64_t>(p / kx, nsh) : nsh;
+        } else if (p < nx + nz) {
+          const int64_t q = p - nx;
+          bk[u] = (nsh + 1) + (kz > 0 ? (int)min<int64_t>(q / kz, nsh) : nsh);
+        }
+        if (bk[u] >= 0) slot[u] = atomicAdd(&hist[bk[u]], 1u);
+      }
     }
+    __syncthreads();
+    for (int j = threadIdx.x; j < NB; j += kBlock) {
+      const unsigned h = hist[j];
+      base[j] = h ? atomicAdd(cur + j, h) : 0u;
+      hist[j] = 0;  // for the next round (its atomics come after the next barrier)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kUnpackPer; ++u) {
+      if (bk[u] < 0) continue;
+      const bool isx = bk[u] <= nsh;
+      const int rb = isx ? bk[u] : bk[u] - (nsh + 1);
+      const int64_t o = em_region(rb, (uint32_t)(isx ? kx : kz), isx ? nx : nz) + base[bk[u]] +
+                        slot[u];
+      if (isx) {
+        if (half)
+          ((uint64_t*)xbag)[(int64_t)c * nx + o] = v[u];
+        else
+          ((uint32_t*)xbag)[(int64_t)c * nx + o] = (uint32_t)v[u];
+      } else {
+        zbag[(int64_t)c * nz + o] = (uint32_t)v[u];
+      }
+    }
+    __syncthreads();  // base[] is rewritten by the next round
   }
 }
 
@@ -677,17 +724,24 @@ extern "C" int tw_chain_set_emit(int32_t epr, int32_t steps_per_round) {
 }
 
 extern "C" int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
-                               int32_t half, int64_t n_x, int64_t n_z, void* d_x_bag,
-                               void* d_z_bag, int32_t* d_flag, void* stream) {
+                               int32_t half, int64_t n_x, int64_t n_z, int64_t x_shard,
+                               int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
+                               uint32_t* d_cursors, int32_t* d_flag, void* stream) {
   TW_ARG_CHECK(world >= 1 && steps >= 0 && steps <= kChainMax && cap >= 1 && n_x >= 0 &&
-                   n_z >= 0 && (half == 0 || half == 1) && (int64_t)world * steps < 65536,
+                   n_z >= 0 && (half == 0 || half == 1) && (int64_t)world * steps < 65536 &&
+                   x_shard >= 0 && z_shard >= 0 && n_shards >= 0 && n_shards < kEmMaxBig,
                "tw_chain_unpack: bad sizes");
   if (steps == 0 || n_x + n_z == 0) return TW_OK;
-  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(cap, (int64_t)kBlock * 4),
-                                                                  64));
-  hipLaunchKernelGGL(k_chain_unpack, dim3((unsigned)(parts * world * steps)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_recv, (int)world, (int)steps, parts, cap,
-                     half ? 2 : 1, (int)half, n_x, n_z, d_x_bag, (uint32_t*)d_z_bag, d_flag);
+  TW_ARG_CHECK(d_cursors != nullptr && d_flag != nullptr, "tw_chain_unpack: cursors and flag");
+  hipStream_t st = (hipStream_t)stream;
+  const int NB = 2 * (n_shards + 1);
+  TW_HIP_CHECK(tw_zero_async(d_cursors, 0, sizeof(uint32_t) * (size_t)NB * steps, st));
+  const int parts = (int)std::max<int64_t>(
+      1, std::min<int64_t>(ceil_div(cap, (int64_t)kBlock * kUnpackPer), 64));
+  hipLaunchKernelGGL(k_chain_unpack, dim3((unsigned)(parts * world * steps)), dim3(kBlock),
+                     sizeof(unsigned) * 2 * (size_t)NB, st, d_recv, (int)world, (int)steps, parts,
+                     cap, half ? 2 : 1, (int)half, n_x, n_z, x_shard, z_shard, (int)n_shards,
+                     d_x_bag, (uint32_t*)d_z_bag, (unsigned*)d_cursors, d_flag);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

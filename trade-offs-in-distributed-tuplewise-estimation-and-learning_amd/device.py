@@ -220,10 +220,20 @@ class HipOps:
                int(n_shards), L.ptr(x_bag), L.ptr(z_bag), L.ptr(cursors), L.ptr(send),
                int(cap), L.ptr(flag), L.stream_handle())
 
-    def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag):
+    def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx, kz,
+                     n_shards):
+        """The received records appended to their (step, shard) bags (tw_chain_unpack)."""
+        cur = self._unpack_cursors(int(steps) * 2 * (int(n_shards) + 1), x_bag.device)
         L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
-               int(bool(half)), int(n), int(m), L.ptr(x_bag), L.ptr(z_bag), L.ptr(flag),
-               L.stream_handle())
+               int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
+               L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
+
+    def _unpack_cursors(self, words, dev):
+        # one buffer per HipOps, grown as needed; unpacks on one stream reuse it in order
+        c = getattr(self, "_cursors", None)
+        if c is None or c.numel() < words:
+            self._cursors = c = self.t.empty((max(words, 1024),), dtype=self.t.int32, device=dev)
+        return c
 
     def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
                     z_stride, max_nx, max_nz, half, out):
@@ -894,7 +904,7 @@ class ShardedSample:
                     if work is not None:
                         work.wait()
                     ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
-                                     z_bag[a:a + cs], self._chain_flag)
+                                     z_bag[a:a + cs], self._chain_flag, kx, kz, N)
                     count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs])
                 continue
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
