@@ -60,8 +60,12 @@ def one_gpu_call(K, chain):
         D.CHAIN_STEPS = True
 
 
-def rank_call(G, r, K, parts=False):
-    """Rank r's device work in one call of the strong problem split over G ranks."""
+def rank_call(G, r, K, parts=False, product=False):
+    """Rank r's device work in one call of the strong problem split over G ranks.  product:
+    the product's schedule at G > 1 (device.py _unn_many_chain, round 5): the chunk in >= 2
+    sub-chunks, each sub-chunk's emission and exchange copy on a side stream (sub-chunk j+1's
+    emission beside sub-chunk j's count), unpack + count on the main stream, the final gather
+    on another side stream beside the counts."""
     ops = HipOps()
     nl, Nl = n // G, N // G
     x_off, z_off, _ = prop_swor_layout(nl, nl, Nl)
@@ -98,6 +102,43 @@ def rank_call(G, r, K, parts=False):
 
     Zg = torch.empty_like(Z)  # the all-gathered Z (a device copy of the same bytes)
     full = torch.zeros(K * N + 1, dtype=torch.int64, device="cuda")
+    Sub = max(1, min(D.CHAIN_SUB, -(-C // 2)))
+    nsub = -(-C // Sub)
+    sends = [torch.empty(G * Sub * (cap + 1), dtype=torch.int64, device="cuda")
+             for _ in range(nsub)]
+    recvs = [torch.empty_like(b) for b in sends]
+    es, fs = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def call_product():
+        main = torch.cuda.current_stream()
+        Zg.copy_(Z)
+        xr, zr = ops.rank_images_query(Z, xq, zq, L.TW_F64)
+        fs.wait_stream(main)
+        with torch.cuda.stream(fs):
+            ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs, kzs)
+        for i0 in range(0, K, C):
+            c = min(C, K - i0)
+            es.wait_stream(main)
+            evs = []
+            with torch.cuda.stream(es):
+                for j, a in enumerate(range(0, c, Sub)):
+                    cs = min(Sub, c - a)
+                    ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0 and a == 0, r, G,
+                                   kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz, Nl,
+                                   send=sends[j], cap=cap, flag=flag)
+                    sz = G * cs * (cap + 1)
+                    recvs[j][:sz].copy_(sends[j][:sz])
+                    ev = torch.cuda.Event()
+                    ev.record(es)
+                    evs.append((a, cs, j, ev))
+            for a, cs, j, ev in evs:
+                main.wait_event(ev)
+                ops.chain_unpack(recvs[j], G, cs, cap, False, nl, nl, x_bag[a:a + cs],
+                                 z_bag[a:a + cs], flag, kx, kz, Nl)
+                ops.count_chain(x_bag[a:a + cs], xo, z_bag[a:a + cs], zo, Nl, cs, nl, nl, kx,
+                                kz, False, counts[i0 + a:i0 + a + cs])
+        main.wait_stream(fs)
+        full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts)
 
     def call():
         if G > 1:  # round 5: the Z all-gather the ranking waits for, as a device copy of its
@@ -129,7 +170,7 @@ def rank_call(G, r, K, parts=False):
             # the counts' all-reduce (with the overflow flag) stands in as its local fill
             mark("counts reduce (local part)",
                  lambda: full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
-    ms, host = ev_time(call, 5)
+    ms, host = ev_time(call_product if (product and G > 1) else call, 5)
     if parts:
         t = {k: sum(a.elapsed_time(b) for a, b in v) / 6 for k, v in t.items()}
     return ms, host, t
@@ -144,8 +185,11 @@ for K in Ks:
           flush=True)
     for G in (1, 2, 4, 8):
         ms = [rank_call(G, r, K)[0] for r in sorted({0, G - 1})]
+        mp = [rank_call(G, r, K, product=True)[0] for r in sorted({0, G - 1})]
         _, _, parts = rank_call(G, G - 1, K, parts=True)
-        print(f"  G={G}: ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
-              + f" ms/call; ideal (one-GPU chain call / G) {ch / G:.3f}; efficiency "
-              f"{ch / G / max(ms):.3f}; parts (instrumented rank {G - 1}) "
-              + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()), flush=True)
+        print(f"  G={G}: serial ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
+              + f" ms/call, efficiency {ch / G / max(ms):.3f}; product schedule "
+              + "/".join(f"{v:.3f}" for v in mp) + f" ms/call, efficiency {ch / G / max(mp):.3f}"
+              f"; ideal (one-GPU chain call / G) {ch / G:.3f}; parts (serial, instrumented "
+              f"rank {G - 1}) " + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()),
+              flush=True)

@@ -20,6 +20,8 @@ that hold those positions, and all steps of a chunk are counted in one launch.
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 
 from . import _engine as E
@@ -891,15 +893,26 @@ class ShardedSample:
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             if coll:
+                # the emissions (and the all-to-alls issued behind them) on a side stream, so
+                # sub-chunk j+1's emission runs beside sub-chunk j's count; the side stream
+                # first waits for the main stream (the previous chunk's unpacks and counts are
+                # done with these send / receive buffers)
+                es = None
+                if self.X.is_cuda:
+                    if getattr(self, "_emit_stream", None) is None:
+                        self._emit_stream = t.cuda.Stream()
+                    es = self._emit_stream
+                    es.wait_stream(t.cuda.current_stream())
                 works = []
-                for j, a in enumerate(range(0, c, Sub)):
-                    cs = min(Sub, c - a)
-                    ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0 and a == 0, r, G,
-                                   kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz, N,
-                                   send=sends[j], cap=cap, flag=self._chain_flag)
-                    sz = G * cs * (cap + 1) * W
-                    works.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
-                                                             async_op=True)))
+                with (t.cuda.stream(es) if es is not None else contextlib.nullcontext()):
+                    for j, a in enumerate(range(0, c, Sub)):
+                        cs = min(Sub, c - a)
+                        ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0 and a == 0, r, G,
+                                       kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz,
+                                       N, send=sends[j], cap=cap, flag=self._chain_flag)
+                        sz = G * cs * (cap + 1) * W
+                        works.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
+                                                                 async_op=True)))
                 for a, cs, j, work in works:
                     if work is not None:
                         work.wait()
