@@ -337,10 +337,12 @@ def test_multirank_repartition_is_G_invariant(G, fused):
     assert inc == float(S1.UnNB(B, seed=77))
 
 
-def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict"):
+def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise import device as D
     from tuplewise.device import ShardedSample
+    D.CHAIN_SUB = sub
     X, Z = _global_data(G, n_loc, m_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
                       torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
@@ -358,28 +360,27 @@ def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("G,tie_mode", [(2, "strict"), (4, "strict"), (8, "strict"),
-                                        (2, "half")])
-def test_chain_steps_are_G_invariant(G, tie_mode):
+@pytest.mark.parametrize("G,tie_mode,sub", [(2, "strict", 0), (4, "strict", 0), (8, "strict", 0),
+                                            (2, "half", 0), (4, "strict", 5)])
+def test_chain_steps_are_G_invariant(G, tie_mode, sub):
     """UnN_many's step chains over G ranks (csrc/chain.hip, restated): every rank images its
     own elements against the all-gathered Z, walks their chains into per-(rank, step) buckets,
-    one async all-to-all per sub-chunk, counts its bags; one all-reduce of the counts per call.
-    The
-    estimates equal the one-process score path's (est.UnNT's loop, key by key) and the ranks'
+    one all-to-all per chunk (sub > 0: per sub-chunk of <= sub steps, async), counts its bags;
+    one all-reduce of the counts per call.  The estimates equal the one-process score path's (est.UnNT's loop, key by key) and the ranks'
     final arrays, concatenated, equal the global permutation chain."""
     import tuplewise  # noqa: F401
     from tuplewise import device as D
     assert D.CHAIN_STEPS
     from tuplewise.device import ShardedSample
-    # 12 steps: sub-chunks of D.CHAIN_SUB = 5 steps (5, 5, 2), each its own async
-    # all-to-all, unpacked and counted in order
+    # 12 steps: with sub = 5, sub-chunks of (5, 5, 2) steps, each its own async all-to-all,
+    # unpacked and counted in order
     n_loc, m_loc, N = 600, 450, 3
     keys = [5, 6, 9, 11, 2, 7, 8, 13, 21, 3, 4, 17] if G != 8 else [5, 6, 9, 11, 2, 7, 8]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_rank_worker,
-                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode))
+                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode, sub))
              for r in range(G)]
     for p in procs:
         p.start()

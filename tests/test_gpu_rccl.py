@@ -5,7 +5,8 @@ options with the high-priority stream), and the G > 1 branches forced through it
 
 * ShardedSample._unn_many_chain: all_gather_into_tensor of both samples (`_all_gather`'s nccl
   branch), the chain emission into send buckets, the async all_to_all_single + work.wait()
-  per sub-chunk, chain_unpack, chain_gather, the counts' all-reduce with the overflow flag;
+  per chunk (and per sub-chunk with device.CHAIN_SUB > 0), chain_unpack, chain_gather, the
+  counts' all-reduce with the overflow flag;
 * ShardedSample._run_steps (UnNB_many, UnN with a key): the fixed-capacity exchange on the
   high-priority side stream (all_to_all_single) and the counts' all-reduce; the counted
   exchange (`exchange="exact"`: all_to_all_single with split sizes);
@@ -49,7 +50,7 @@ def _learn_problem():
 
 def _estimates(S, ties):
     """The estimator calls whose multi-rank branches hold RCCL calls, in a fixed order."""
-    vals = [float(v) for v in S.UnN_many(range(5, 45))]  # 40 steps: two chunks, sub-chunks
+    vals = [float(v) for v in S.UnN_many(range(5, 45))]  # 40 steps: two chunks
     vals.append(float(S.UnN(3)))  # one repartition (exchange) + global counts
     if not ties:
         vals += [float(v) for v in S.UnNB_many(700, 11, [8, 9, 10])]  # side-stream exchange
@@ -96,6 +97,18 @@ def _worker(port, q):
                 out["mismatch"].append((tag, "estimates"))
             if not (np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])):
                 out["mismatch"].append((tag, "final arrays"))
+        import tuplewise.device as D
+        X, Z = data["f64"]  # the chunks' sub-chunks (CHAIN_SUB > 0: emissions on a side stream)
+        a = _estimates(ShardedSample(X.clone(), Z.clone(), 8, algo="pairs"), False)
+        D.CHAIN_SUB = 5
+        try:
+            b = _estimates(ShardedSample(X.clone(), Z.clone(), 8, group=g, algo="pairs",
+                                         collectives=True), False)
+        finally:
+            D.CHAIN_SUB = 0
+        out["ran"].append("f64/strict/fixed/sub-chunks")
+        if a[0] != b[0] or not (np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])):
+            out["mismatch"].append(("f64/strict/fixed/sub-chunks", "estimates or arrays"))
         Xl, Zl, p = _learn_problem()
         for peer, mode, layout in [(pe, m, la) for pe in (True, False)
                                    for m in ("replay", "device")
@@ -140,5 +153,5 @@ def test_rccl_world_size_one_equals_one_process(gpu):
     pr.join(timeout=120)
     assert status == "ok", out
     assert pr.exitcode == 0
-    assert len(out["ran"]) == 12, out["ran"]
+    assert len(out["ran"]) == 13, out["ran"]
     assert out["mismatch"] == [], out["mismatch"]

@@ -60,12 +60,14 @@ def one_gpu_call(K, chain):
         D.CHAIN_STEPS = True
 
 
-def rank_call(G, r, K, parts=False, product=False):
-    """Rank r's device work in one call of the strong problem split over G ranks.  product:
-    the product's schedule at G > 1 (device.py _unn_many_chain, round 5): the chunk in >= 2
+def rank_call(G, r, K, parts=False, product=False, side=True):
+    """Rank r's device work in one call of the strong problem split over G ranks: by default
+    the product's schedule (device.CHAIN_SUB = 0: one exchange, unpack and count per chunk).
+    product: the CHAIN_SUB = 5 schedule at G > 1 (device.py _unn_many_chain): the chunk in >= 2
     sub-chunks, each sub-chunk's emission and exchange copy on a side stream (sub-chunk j+1's
     emission beside sub-chunk j's count), unpack + count on the main stream, the final gather
-    on another side stream beside the counts."""
+    on another side stream beside the counts.  side=False: the same sub-chunks all on the
+    main stream (every sub-chunk's emission + copy first, then its unpack + count)."""
     ops = HipOps()
     nl, Nl = n // G, N // G
     x_off, z_off, _ = prop_swor_layout(nl, nl, Nl)
@@ -102,7 +104,7 @@ def rank_call(G, r, K, parts=False, product=False):
 
     Zg = torch.empty_like(Z)  # the all-gathered Z (a device copy of the same bytes)
     full = torch.zeros(K * N + 1, dtype=torch.int64, device="cuda")
-    Sub = max(1, min(D.CHAIN_SUB, -(-C // 2)))
+    Sub = max(1, min(5, -(-C // 2)))  # device.CHAIN_SUB = 5
     nsub = -(-C // Sub)
     sends = [torch.empty(G * Sub * (cap + 1), dtype=torch.int64, device="cuda")
              for _ in range(nsub)]
@@ -118,9 +120,10 @@ def rank_call(G, r, K, parts=False, product=False):
             ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs, kzs)
         for i0 in range(0, K, C):
             c = min(C, K - i0)
-            es.wait_stream(main)
+            st = es if side else main
+            st.wait_stream(main)
             evs = []
-            with torch.cuda.stream(es):
+            with torch.cuda.stream(st):
                 for j, a in enumerate(range(0, c, Sub)):
                     cs = min(Sub, c - a)
                     ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0 and a == 0, r, G,
@@ -128,11 +131,14 @@ def rank_call(G, r, K, parts=False, product=False):
                                    send=sends[j], cap=cap, flag=flag)
                     sz = G * cs * (cap + 1)
                     recvs[j][:sz].copy_(sends[j][:sz])
-                    ev = torch.cuda.Event()
-                    ev.record(es)
+                    ev = None
+                    if side:
+                        ev = torch.cuda.Event()
+                        ev.record(es)
                     evs.append((a, cs, j, ev))
             for a, cs, j, ev in evs:
-                main.wait_event(ev)
+                if ev is not None:
+                    main.wait_event(ev)
                 ops.chain_unpack(recvs[j], G, cs, cap, False, nl, nl, x_bag[a:a + cs],
                                  z_bag[a:a + cs], flag, kx, kz, Nl)
                 ops.count_chain(x_bag[a:a + cs], xo, z_bag[a:a + cs], zo, Nl, cs, nl, nl, kx,
@@ -186,10 +192,12 @@ for K in Ks:
     for G in (1, 2, 4, 8):
         ms = [rank_call(G, r, K)[0] for r in sorted({0, G - 1})]
         mp = [rank_call(G, r, K, product=True)[0] for r in sorted({0, G - 1})]
+        mm = [rank_call(G, r, K, product=True, side=False)[0] for r in sorted({0, G - 1})]
         _, _, parts = rank_call(G, G - 1, K, parts=True)
-        print(f"  G={G}: serial ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
-              + f" ms/call, efficiency {ch / G / max(ms):.3f}; product schedule "
-              + "/".join(f"{v:.3f}" for v in mp) + f" ms/call, efficiency {ch / G / max(mp):.3f}"
+        print(f"  G={G}: product (one exchange per chunk) ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
+              + f" ms/call, efficiency {ch / G / max(ms):.3f}; sub-chunks of 5, side stream "
+              + "/".join(f"{v:.3f}" for v in mp) + f" ms/call, efficiency {ch / G / max(mp):.3f}; sub-chunks on one stream "
+              + "/".join(f"{v:.3f}" for v in mm) + f" ms/call, efficiency {ch / G / max(mm):.3f}"
               f"; ideal (one-GPU chain call / G) {ch / G:.3f}; parts (serial, instrumented "
               f"rank {G - 1}) " + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()),
               flush=True)

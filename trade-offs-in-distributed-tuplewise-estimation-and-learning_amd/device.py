@@ -40,10 +40,14 @@ CHAIN_MAX = 32
 # O(n + m) on their integer rank images (tw_count_pairs_chain_bucket); larger shards keep the
 # records path (tw_count_pairs_sorted_steps)
 CHAIN_BUCKET_MAX = 16384
-# several ranks: the steps of a chunk exchanged in sub-chunks of at most this many steps (and
-# at least two sub-chunks), each its own (async) all-to-all, so the exchange of one sub-chunk
-# overlaps the counts of the previous
-CHAIN_SUB = 5
+# several ranks: 0 (default) — one all-to-all per chunk, its unpack and ONE count launch
+# behind it; n > 0 — the chunk's steps in sub-chunks of at most n steps (and at least two),
+# each its own async all-to-all with its emission on a side stream, so one sub-chunk's exchange
+# runs under the previous sub-chunk's count.  Round 5 (tools/chain_probe.py,
+# profiles/r05s36_chain_probe.log): the sub-chunks' extra launches (emission, unpack, count
+# tail, cross-stream waits) cost a G = 8 rank 0.05-0.09 ms per call at T = 4 and 0.13-0.15 ms
+# at T = 20 — more than the exchange they hide (~0.03 / ~0.08 ms over xGMI)
+CHAIN_SUB = 0
 # one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
 # images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
 ONESHOT_RANK = True
@@ -865,16 +869,14 @@ class ShardedSample:
         zpos = t.empty((m,), dtype=t.int32, device=dev)
         counts = t.empty((T, N), dtype=t.int64, device=dev)
         if coll:
-            # a chunk's steps in sub-chunks of <= CHAIN_SUB steps, each with its own send /
-            # receive buffers and its own all-to-all (async): every sub-chunk's emission is
-            # enqueued first, then each sub-chunk waits for its records, unpacks and counts —
-            # the exchange of sub-chunk j+1 runs under the counts of sub-chunk j
+            # one all-to-all per chunk (CHAIN_SUB = 0), or the chunk's steps in sub-chunks of
+            # <= CHAIN_SUB steps, each with its own send / receive buffers and its own async
+            # all-to-all: every sub-chunk's emission is enqueued first, then each sub-chunk
+            # waits for its records, unpacks and counts
             tot = n + m
             cap = max(1, tot // G + tot // (8 * G) + 1024)
             W = 2 if half else 1
-            # (at least two sub-chunks per chunk: with one, est.UnNT's T = 4 left its whole
-            # exchange exposed before the first count)
-            Sub = max(1, min(CHAIN_SUB, -(-C // 2)))
+            Sub = max(1, min(CHAIN_SUB, -(-C // 2))) if CHAIN_SUB > 0 else C
             nsub = -(-C // Sub)
             # the send / receive ring persists on the sample across calls (fresh
             # GB-scale allocations per call made the caching allocator flush and re-map)
@@ -893,12 +895,12 @@ class ShardedSample:
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             if coll:
-                # the emissions (and the all-to-alls issued behind them) on a side stream, so
-                # sub-chunk j+1's emission runs beside sub-chunk j's count; the side stream
-                # first waits for the main stream (the previous chunk's unpacks and counts are
-                # done with these send / receive buffers)
+                # with sub-chunks, the emissions (and the all-to-alls issued behind them) on a
+                # side stream, so sub-chunk j+1's emission runs beside sub-chunk j's count; the
+                # side stream first waits for the main stream (the previous chunk's unpacks and
+                # counts are done with these send / receive buffers)
                 es = None
-                if self.X.is_cuda:
+                if self.X.is_cuda and c > Sub:
                     if getattr(self, "_emit_stream", None) is None:
                         self._emit_stream = t.cuda.Stream()
                     es = self._emit_stream
