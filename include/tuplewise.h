@@ -191,17 +191,6 @@ int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t steps, int64_
                     int32_t half, int64_t n_x, int64_t n_z, int64_t x_shard, int64_t z_shard,
                     int32_t n_shards, void* d_x_bag, void* d_z_bag, uint32_t* d_cursors,
                     int32_t* d_flag, void* stream);
-/* The bags of `steps` (<= 32) steps over ranks WITHOUT the records' exchange (round 5): with
- * every rank's images all-gathered into d_img_all (world blocks of n_x + n_z words in rank
- * order: half = 0 u32 — the low words of the X / Z rank-image records; half = 1 u64 — the X
- * records {g, h} and the Z records, low word used), the element at this rank's position i after
- * step c (c = 0 .. steps - 1 of the call, keys as tw_chain_emit's) is found by the inverse
- * chain of steps c .. 0 and its image written at d_x_bag[c][i] / d_z_bag[c][i]: the bags in
- * position order, the same multisets as tw_chain_emit + all-to-all + tw_chain_unpack.  Cannot
- * overflow (no capacity).  world * n_x and world * n_z < 2^32. */
-int tw_chain_fetch(const void* d_img_all, int32_t world, int32_t rank, int64_t n_x, int64_t n_z,
-                   int32_t half, const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
-                   void* d_x_bag, void* d_z_bag, void* stream);
 /* The all-pairs counts of `steps` x n_shards bags in ONE launch: bag (c, s) = x images
  * [c * x_stride + d_x_off[s], c * x_stride + d_x_off[s + 1]) against z images likewise;
  * d_out[c * n_shards + s] (zeroed here) = #{x > z} (half = 1: 2 #{x > z} + #{x == z}, the

@@ -235,20 +235,6 @@ class OracleOpsChain(OracleOpsRank):
             x_bag[c].numpy().view(np.uint64 if half else np.uint32)[p[isx]] = v[isx]
             z_bag[c].numpy().view(np.uint32)[p[~isx] - n] = v[~isx]
 
-    def chain_fetch(self, img_all, world, rank, n, m, half, keys_x, keys_z, x_bag, z_bag):
-        # position i of this rank after step c: its inverse chain through steps c .. 0
-        a = img_all.numpy().view(np.uint64 if half else np.uint32).reshape(world, n + m)
-        for side, (keys, nl, bag) in enumerate(((keys_x, n, x_bag), (keys_z, m, z_bag))):
-            for c in range(len(keys)):
-                p = np.arange(rank * nl, (rank + 1) * nl)
-                for key in reversed(keys[:c + 1]):
-                    p = O.feistel_perm_inv(p, world * nl, int(key))
-                v = a[p // nl, (n if side else 0) + p % nl]
-                if side == 0:
-                    bag[c].numpy().view(np.uint64 if half else np.uint32)[:] = v
-                else:
-                    bag[c].numpy().view(np.uint32)[:] = (v & 0xFFFFFFFF).astype(np.uint32)
-
     def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
                     z_stride, max_nx, max_nz, half, out):
         xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
@@ -351,13 +337,12 @@ def test_multirank_repartition_is_G_invariant(G, fused):
     assert inc == float(S1.UnNB(B, seed=77))
 
 
-def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub=0, fetch=32):
+def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     from tuplewise import device as D
     from tuplewise.device import ShardedSample
     D.CHAIN_SUB = sub
-    D.CHAIN_FETCH_MAX = fetch
     X, Z = _global_data(G, n_loc, m_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
                       torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
@@ -375,16 +360,13 @@ def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("G,tie_mode,sub,fetch", [
-    (2, "strict", 0, 32), (4, "strict", 0, 32), (8, "strict", 0, 32), (2, "half", 0, 32),
-    (2, "strict", 0, 0), (2, "half", 0, 0), (4, "strict", 5, 0)])
-def test_chain_steps_are_G_invariant(G, tie_mode, sub, fetch):
+@pytest.mark.parametrize("G,tie_mode,sub", [(2, "strict", 0), (4, "strict", 0), (8, "strict", 0),
+                                            (2, "half", 0), (4, "strict", 5)])
+def test_chain_steps_are_G_invariant(G, tie_mode, sub):
     """UnN_many's step chains over G ranks (csrc/chain.hip, restated): every rank images its
-    own elements against the all-gathered Z; fetch (calls of <= fetch steps): the images
-    all-gathered and every rank's bags filled by inverse chains (tw_chain_fetch); otherwise the
-    rank walks its elements' chains into per-(rank, step) buckets, one all-to-all per chunk
-    (sub > 0: per sub-chunk of <= sub steps, async) and the unpack.  Then the counts of its
-    bags and one all-reduce of the counts per call.  The estimates equal the one-process score path's (est.UnNT's loop, key by key) and the ranks'
+    own elements against the all-gathered Z, walks their chains into per-(rank, step) buckets,
+    one all-to-all per chunk (sub > 0: per sub-chunk of <= sub steps, async), counts its bags;
+    one all-reduce of the counts per call.  The estimates equal the one-process score path's (est.UnNT's loop, key by key) and the ranks'
     final arrays, concatenated, equal the global permutation chain."""
     import tuplewise  # noqa: F401
     from tuplewise import device as D
@@ -398,7 +380,7 @@ def test_chain_steps_are_G_invariant(G, tie_mode, sub, fetch):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_rank_worker,
-                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode, sub, fetch))
+                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode, sub))
              for r in range(G)]
     for p in procs:
         p.start()
@@ -508,20 +490,17 @@ def test_chain_overflow_raises_on_every_rank():
 def _forced_worker(port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=0, world_size=1)
-    from tuplewise import device as D
     from tuplewise.device import ShardedSample
     X, Z = _global_data(1, 1800, 1350)
     out = {}
     for tie in ("strict", "half"):
-        for fetch in (32, 0):  # the fetched bags; the emission + all-to-all + unpack
-            D.CHAIN_FETCH_MAX = fetch
-            S = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), 9,
-                              group=dist.group.WORLD, ops=OracleOpsChain(), tie_mode=tie,
-                              algo="pairs", collectives=True)
-            assert S.coll and S._multi()
-            vals = [float(v) for v in S.UnN_many([5, 6, 9, 11, 2, 7, 8])]
-            vals.append(float(S.UnN(3)))  # the fixed exchange + one all-reduce
-            out[(tie, fetch)] = (vals, S.X.numpy().copy(), S.Z.numpy().copy())
+        S = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), 9,
+                          group=dist.group.WORLD, ops=OracleOpsChain(), tie_mode=tie,
+                          algo="pairs", collectives=True)
+        assert S.coll and S._multi()
+        vals = [float(v) for v in S.UnN_many([5, 6, 9, 11, 2, 7, 8])]
+        vals.append(float(S.UnN(3)))  # the fixed exchange + one all-reduce
+        out[tie] = (vals, S.X.numpy().copy(), S.Z.numpy().copy())
     q.put(out)
     dist.destroy_process_group()
 
@@ -546,7 +525,6 @@ def test_forced_collectives_at_world_size_one_equal_one_process():
                           ops=OracleOpsChain(), tie_mode=tie, algo="pairs")
         want = [float(v) for v in S.UnN_many([5, 6, 9, 11, 2, 7, 8])]
         want.append(float(S.UnN(3)))
-        for fetch in (32, 0):
-            vals, Xf, Zf = got[(tie, fetch)]
-            assert vals == want
-            assert np.array_equal(Xf, S.X.numpy()) and np.array_equal(Zf, S.Z.numpy())
+        vals, Xf, Zf = got[tie]
+        assert vals == want
+        assert np.array_equal(Xf, S.X.numpy()) and np.array_equal(Zf, S.Z.numpy())

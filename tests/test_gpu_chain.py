@@ -210,63 +210,6 @@ def test_chain_exchange_simulated_ranks(gpu, G, half):
                 assert int(got[c, g * N + s]) == want
 
 
-@pytest.mark.parametrize("half", [False, True])
-@pytest.mark.parametrize("G,T", [(2, 3), (3, 7), (8, 32)])
-def test_chain_fetch_simulated_ranks(gpu, G, T, half):
-    """tw_chain_fetch: every rank's image words all-gathered (by hand: concatenated in rank
-    order), each rank's bags filled by inverse chains — in POSITION order, so the bags equal
-    the oracle's permuted images of the rank's positions exactly (the emission's bags are the
-    same multisets); the counts equal one process on the global layout."""
-    import torch
-    from tuplewise import _lib as L
-    from tuplewise.device import HipOps
-    rng = np.random.RandomState(31 + G)
-    n_loc, m_loc, N = 2500, 1900, 4
-    X, Z = rng.normal(0.3, 1, G * n_loc).round(3), rng.normal(0, 1, G * m_loc).round(3)
-    ops = HipOps()
-    Zall = torch.from_numpy(Z).cuda()
-    Xall = torch.from_numpy(X).cuda()
-    keys = list(range(40, 40 + T))
-    kxs = [(2 * k) & M64 for k in keys]
-    kzs = [(2 * k + 1) & M64 for k in keys]
-    kx, kz = int(n_loc / N), int((n_loc + m_loc) / N) - int(n_loc / N)
-    words = []
-    for r in range(G):
-        xr, zr = ops.rank_images_query(Zall, Xall[r * n_loc:(r + 1) * n_loc],
-                                       Zall[r * m_loc:(r + 1) * m_loc], L.TW_F64, half)
-        own = torch.cat([xr.view(torch.int64), zr.view(torch.int64)])
-        words.append(own if half else own.view(torch.int32)[0::2].contiguous())
-    img_all = torch.cat(words)
-    wx, wz = O.rank_records(X, Z, half=half)
-    wxs, wzs = _chain(wx, keys, 0), _chain(wz, keys, 1)
-    x_off, z_off = _layout(n_loc, m_loc, N)
-    xo, zo = torch.from_numpy(x_off).cuda(), torch.from_numpy(z_off).cuda()
-    xs, zs = _chain(X, keys, 0), _chain(Z, keys, 1)
-    for r in range(G):
-        x_bag = torch.empty((T, n_loc), dtype=torch.int64 if half else torch.float32,
-                            device="cuda")
-        z_bag = torch.empty((T, m_loc), dtype=torch.float32, device="cuda")
-        ops.chain_fetch(img_all, G, r, n_loc, m_loc, half, kxs, kzs, x_bag, z_bag)
-        xb = x_bag.cpu().numpy().view(np.uint64 if half else np.uint32)
-        zb = z_bag.cpu().numpy().view(np.uint32)
-        lo = np.uint64(0xFFFFFFFF)
-        for c in range(T):
-            ex = wxs[c][r * n_loc:(r + 1) * n_loc].view(np.uint64)
-            ez = wzs[c][r * m_loc:(r + 1) * m_loc].view(np.uint64)
-            assert np.array_equal(xb[c], ex if half else (ex & lo).astype(np.uint32))
-            assert np.array_equal(zb[c], (ez & lo).astype(np.uint32))
-        out = torch.empty((T, N), dtype=torch.int64, device="cuda")
-        ops.count_chain(x_bag, xo, z_bag, zo, N, T, n_loc, m_loc, kx, kz, half, out)
-        got = out.cpu().numpy().view(np.uint64)
-        for c in (0, T - 1):
-            for s in range(N):
-                xa = xs[c][r * n_loc + x_off[s]:r * n_loc + x_off[s + 1]]
-                za = zs[c][r * m_loc + z_off[s]:r * m_loc + z_off[s + 1]]
-                want = (2 * O.un_count(xa, za) + int((xa[:, None] == za[None, :]).sum())
-                        if half else O.un_count(xa, za))
-                assert int(got[c, s]) == want
-
-
 def test_chain_gather_many_steps(gpu):
     """tw_chain_gather over more than 32 steps (chunks walked back through its work array)."""
     import torch

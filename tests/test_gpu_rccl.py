@@ -5,8 +5,7 @@ options with the high-priority stream), and the G > 1 branches forced through it
 
 * ShardedSample._unn_many_chain: all_gather_into_tensor of both samples (`_all_gather`'s nccl
   branch), the chain emission into send buckets, the async all_to_all_single + work.wait()
-  per chunk (and per sub-chunk with device.CHAIN_SUB > 0), chain_unpack; for calls of <=
-  CHAIN_FETCH_MAX steps the all-gather of the images and chain_fetch; chain_gather, the
+  per chunk (and per sub-chunk with device.CHAIN_SUB > 0), chain_unpack, chain_gather, the
   counts' all-reduce with the overflow flag;
 * ShardedSample._run_steps (UnNB_many, UnN with a key): the fixed-capacity exchange on the
   high-priority side stream (all_to_all_single) and the counts' all-reduce; the counted
@@ -52,7 +51,7 @@ def _learn_problem():
 def _estimates(S, ties):
     """The estimator calls whose multi-rank branches hold RCCL calls, in a fixed order."""
     vals = [float(v) for v in S.UnN_many(range(5, 45))]  # 40 steps: two chunks, emitted
-    vals += [float(v) for v in S.UnN_many(range(50, 54))]  # 4 steps: the fetched bags
+    vals += [float(v) for v in S.UnN_many(range(50, 54))]  # est.UnNT's own T = 4
     vals.append(float(S.UnN(3)))  # one repartition (exchange) + global counts
     if not ties:
         vals += [float(v) for v in S.UnNB_many(700, 11, [8, 9, 10])]  # side-stream exchange

@@ -60,7 +60,7 @@ def one_gpu_call(K, chain):
         D.CHAIN_STEPS = True
 
 
-def rank_call(G, r, K, parts=False, product=False, side=True, fetch=False):
+def rank_call(G, r, K, parts=False, product=False, side=True):
     """Rank r's device work in one call of the strong problem split over G ranks: by default
     the product's schedule (device.CHAIN_SUB = 0: one exchange, unpack and count per chunk).
     product: the CHAIN_SUB = 5 schedule at G > 1 (device.py _unn_many_chain): the chunk in >= 2
@@ -146,32 +146,6 @@ def rank_call(G, r, K, parts=False, product=False, side=True, fetch=False):
         main.wait_stream(fs)
         full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts)
 
-    img_all = torch.empty(G * (nl + nl) * (1), dtype=torch.int32, device="cuda")
-
-    def call_fetch():
-        """The fetched bags (device.CHAIN_FETCH_MAX): the images' all-gather as a device copy
-        of its bytes (every rank's n + m image words), tw_chain_fetch, one count launch; the
-        final gather on a side stream as in the product."""
-        main = torch.cuda.current_stream()
-        mark("all-gather Z (device copy)", lambda: Zg.copy_(Z))
-        xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
-        fs.wait_stream(main)
-        with torch.cuda.stream(fs):
-            ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs, kzs)
-
-        def gather_images():
-            own = torch.cat([xr.view(torch.int64), zr.view(torch.int64)])
-            own = own.view(torch.int32)[0::2]
-            img_all.view(G, -1).copy_(own.expand(G, -1))
-        mark("images all-gather (device copy)", gather_images)
-        mark("fetch", lambda: ops.chain_fetch(img_all, G, r, nl, nl, False, kxs, kzs, x_bag,
-                                              z_bag))
-        mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, K, nl, nl, kx, kz,
-                                              False, counts))
-        main.wait_stream(fs)
-        mark("counts reduce (local part)",
-             lambda: full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
-
     def call():
         if G > 1:  # round 5: the Z all-gather the ranking waits for, as a device copy of its
             # bytes (the X all-gather runs asynchronously under the counts, not timed here)
@@ -202,13 +176,7 @@ def rank_call(G, r, K, parts=False, product=False, side=True, fetch=False):
             # the counts' all-reduce (with the overflow flag) stands in as its local fill
             mark("counts reduce (local part)",
                  lambda: full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
-    fn = call
-    if G > 1 and product:
-        fn = call_product
-    elif G > 1 and fetch:
-        assert K <= C
-        fn = call_fetch
-    ms, host = ev_time(fn, 5)
+    ms, host = ev_time(call_product if (product and G > 1) else call, 5)
     if parts:
         t = {k: sum(a.elapsed_time(b) for a, b in v) / 6 for k, v in t.items()}
     return ms, host, t
@@ -225,15 +193,8 @@ for K in Ks:
         ms = [rank_call(G, r, K)[0] for r in sorted({0, G - 1})]
         mp = [rank_call(G, r, K, product=True)[0] for r in sorted({0, G - 1})]
         mm = [rank_call(G, r, K, product=True, side=False)[0] for r in sorted({0, G - 1})]
-        if G > 1 and K <= D.CHAIN_MAX:
-            mf = [rank_call(G, r, K, fetch=True)[0] for r in sorted({0, G - 1})]
-            _, _, fparts = rank_call(G, G - 1, K, parts=True, fetch=True)
-            print(f"  G={G}: FETCHED BAGS ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in mf)
-                  + f" ms/call, efficiency {ch / G / max(mf):.3f}; parts (instrumented rank "
-                  f"{G - 1}) " + ", ".join(f"{k} {v:.3f}" for k, v in fparts.items()),
-                  flush=True)
         _, _, parts = rank_call(G, G - 1, K, parts=True)
-        print(f"  G={G}: emission (one exchange per chunk) ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
+        print(f"  G={G}: product (one exchange per chunk) ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
               + f" ms/call, efficiency {ch / G / max(ms):.3f}; sub-chunks of 5, side stream "
               + "/".join(f"{v:.3f}" for v in mp) + f" ms/call, efficiency {ch / G / max(mp):.3f}; sub-chunks on one stream "
               + "/".join(f"{v:.3f}" for v in mm) + f" ms/call, efficiency {ch / G / max(mm):.3f}"

@@ -50,7 +50,6 @@ _SIGNATURES = {
                              _vp],
     "tw_chain_emit": [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32,
                       _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
-    "tw_chain_fetch": [_vp, _i32, _i32, _i64, _i64, _i32, _vp, _vp, _i32, _vp, _vp, _vp],
     "tw_chain_unpack": [_vp, _i32, _i32, _i64, _i32, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp,
                         _vp],
     "tw_count_pairs_chain": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i32, _vp,

@@ -556,56 +556,6 @@ __global__ __launch_bounds__(kBlock) void k_chain_inverse(
   }
 }
 
-// ----------------------------------------------------------------------------- fetched bags
-// Over ranks, the bags filled from the receiving side (round 5, tw_chain_fetch): with every
-// element's image all-gathered (img: world blocks of n_x + n_z words, rank order), the element
-// at this rank's position i after step s is found by walking i back through steps s .. 0 —
-// s + 1 inverse Feistels, no emission, no exchange of records, no unpack, no capacity.  One
-// thread per (position, step); blockIdx.y = s, so a wave's lanes walk equally deep.  The bag
-// slot of position i is i itself (a shard's slots are its positions), so bags come out in
-// position order: the same multisets as the emitted ones.
-__global__ __launch_bounds__(kBlock) void k_chain_fetch(
-    const void* __restrict__ img, int64_t nx, int64_t nz, int half, int64_t xbase,
-    int64_t zbase, int64_t NX, int64_t NZ, FastDiv dnx, FastDiv dnz, ChainKeys keys, int steps,
-    void* __restrict__ xbag, uint32_t* __restrict__ zbag) {
-  __shared__ Feistel fs[2 * kChainMax];
-  const int s = (int)blockIdx.y;
-  if ((int)threadIdx.x < 2 * (s + 1)) {
-    const int t = threadIdx.x;
-    fs[t] = t <= s ? make_feistel(NX > 1 ? NX : 1, keys.kx[t])
-                   : make_feistel(NZ > 1 ? NZ : 1, keys.kz[t - (s + 1)]);
-  }
-  __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= nx + nz) return;
-  const bool isx = i < nx;
-  const int64_t loc = isx ? i : i - nx;
-  const uint32_t Nt = (uint32_t)(isx ? NX : NZ);
-  const Feistel* F = fs + (isx ? 0 : s + 1);
-  uint32_t p = (uint32_t)((isx ? xbase : zbase) + loc);
-  for (int c = s; c >= 0; --c) {
-    p = feistel_once_inv32(F[c], p);
-    while (p >= Nt) p = feistel_once_inv32(F[c], p);
-  }
-  // p: the element's global index; its image in the block of the rank that holds it
-  const int64_t nside = isx ? nx : nz;
-  const uint32_t g = fast_div32(p, isx ? dnx : dnz);
-  const int64_t src = (int64_t)g * (nx + nz) + (isx ? 0 : nx) + (p - (int64_t)g * nside);
-  if (half) {
-    const uint64_t v = ((const uint64_t*)img)[src];
-    if (isx)
-      ((uint64_t*)xbag)[(int64_t)s * nx + loc] = v;
-    else
-      zbag[(int64_t)s * nz + loc] = (uint32_t)v;
-  } else {
-    const uint32_t v = ((const uint32_t*)img)[src];
-    if (isx)
-      ((uint32_t*)xbag)[(int64_t)s * nx + loc] = v;
-    else
-      zbag[(int64_t)s * nz + loc] = v;
-  }
-}
-
 // ----------------------------------------------------------------------------- plan
 struct ChainPlan {
   int R, tiles_x, zchunks;
@@ -770,30 +720,6 @@ extern "C" int tw_chain_set_emit(int32_t epr, int32_t steps_per_round) {
                "tw_chain_set_emit: steps per round 0, 1 or 16 / elements per thread");
   g_emit_epr = epr;
   g_emit_s = steps_per_round;
-  return TW_OK;
-}
-
-extern "C" int tw_chain_fetch(const void* d_img_all, int32_t world, int32_t rank, int64_t n_x,
-                              int64_t n_z, int32_t half, const uint64_t* keys_x,
-                              const uint64_t* keys_z, int32_t steps, void* d_x_bag,
-                              void* d_z_bag, void* stream) {
-  TW_ARG_CHECK(world >= 1 && rank >= 0 && rank < world && n_x >= 0 && n_z >= 0 && steps >= 0 &&
-                   steps <= kChainMax && (half == 0 || half == 1) &&
-                   (int64_t)world * n_x < (1ll << 32) && (int64_t)world * n_z < (1ll << 32),
-               "tw_chain_fetch: bad sizes");
-  if (steps == 0 || n_x + n_z == 0) return TW_OK;
-  TW_ARG_CHECK(d_img_all != nullptr && keys_x != nullptr && keys_z != nullptr &&
-                   d_x_bag != nullptr && d_z_bag != nullptr,
-               "tw_chain_fetch: null pointer");
-  const ChainKeys k = chain_keys(keys_x, keys_z, steps);
-  const dim3 grid((unsigned)ceil_div(n_x + n_z, (int64_t)kBlock), (unsigned)steps);
-  hipLaunchKernelGGL(k_chain_fetch, grid, dim3(kBlock), 0, (hipStream_t)stream, d_img_all, n_x,
-                     n_z, (int)half, (int64_t)rank * n_x, (int64_t)rank * n_z,
-                     (int64_t)world * n_x, (int64_t)world * n_z,
-                     make_fastdiv(n_x > 0 ? (uint64_t)n_x : 1),
-                     make_fastdiv(n_z > 0 ? (uint64_t)n_z : 1), k, (int)steps, d_x_bag,
-                     (uint32_t*)d_z_bag);
-  TW_LAUNCH_CHECK();
   return TW_OK;
 }
 

@@ -48,10 +48,6 @@ CHAIN_BUCKET_MAX = 16384
 # tail, cross-stream waits) cost a G = 8 rank 0.05-0.09 ms per call at T = 4 and 0.13-0.15 ms
 # at T = 20 — more than the exchange they hide (~0.03 / ~0.08 ms over xGMI)
 CHAIN_SUB = 0
-# several ranks, calls of at most this many steps (<= CHAIN_MAX): every rank's images
-# all-gathered and each rank's bags fetched by inverse chains (tw_chain_fetch) instead of the
-# emission, the records' all-to-all and the unpack; 0 = always the emission
-CHAIN_FETCH_MAX = 32
 # one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
 # images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
 ONESHOT_RANK = True
@@ -237,15 +233,6 @@ class HipOps:
         L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
                int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
                L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
-
-    def chain_fetch(self, img_all, world, rank, n, m, half, keys_x, keys_z, x_bag, z_bag):
-        """The bags of len(keys_x) steps filled by inverse chains from the all-gathered images
-        (tw_chain_fetch): no emission, exchange of records or unpack."""
-        kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
-        kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
-        L.call("tw_chain_fetch", L.ptr(img_all), int(world), int(rank), int(n), int(m),
-               int(bool(half)), kxa.ctypes.data, kza.ctypes.data, len(kxa), L.ptr(x_bag),
-               L.ptr(z_bag), L.stream_handle())
 
     def _unpack_cursors(self, words, dev):
         # one buffer per HipOps, grown as needed; unpacks on one stream reuse it in order
@@ -881,15 +868,7 @@ class ShardedSample:
         xpos = t.empty((n,), dtype=t.int32, device=dev)
         zpos = t.empty((m,), dtype=t.int32, device=dev)
         counts = t.empty((T, N), dtype=t.int64, device=dev)
-        fetch = coll and T <= min(CHAIN_FETCH_MAX, CHAIN_MAX)
-        if fetch:
-            # ONE chunk: the rank's image words (strict: the records' low words; half: the
-            # 8-B records) all-gathered in rank order, the bags fetched by inverse chains
-            own = t.cat([xr.view(t.int64), zr.view(t.int64)])
-            if not half:
-                own = own.view(t.int32)[0::2].contiguous()
-            img_all = self._all_gather(own)
-        elif coll:
+        if coll:
             # one all-to-all per chunk (CHAIN_SUB = 0), or the chunk's steps in sub-chunks of
             # <= CHAIN_SUB steps, each with its own send / receive buffers and its own async
             # all-to-all: every sub-chunk's emission is enqueued first, then each sub-chunk
@@ -915,10 +894,6 @@ class ShardedSample:
             cursors = t.empty((C * 2 * (N + 1),), dtype=t.int32, device=dev)
         for i0 in range(0, T, C):
             c = min(C, T - i0)
-            if fetch:
-                ops.chain_fetch(img_all, G, r, n, m, half, kxs, kzs, x_bag, z_bag)
-                count(x_bag, z_bag, c, counts)
-                continue
             if coll:
                 # with sub-chunks, the emissions (and the all-to-alls issued behind them) on a
                 # side stream, so sub-chunk j+1's emission runs beside sub-chunk j's count; the
