@@ -295,7 +295,10 @@ def drop_in_C3(reps=10, T=4, N=64, n=N_PER_CLASS):
         try:
             Xc, Zc = X.copy(), Z.copy()  # both paths from the same arrays and RNG state
             np.random.seed(1)
-            est.UnNT(Xc, Zc, N, T, "prop-SWOR")  # warm
+            for _ in range(3):  # warm (a reference script calls it in a loop: steady state;
+                # after one warm call the first series still ran ~0.3 ms/call slower than a later
+                # one on the same path, profiles/r05s19_bench.json / r05s38_bench.json)
+                est.UnNT(Xc, Zc, N, T, "prop-SWOR")
             torch.cuda.synchronize()
             ts = []
             for _ in range(reps):
