@@ -528,3 +528,65 @@ def test_forced_collectives_at_world_size_one_equal_one_process():
         vals, Xf, Zf = got[tie]
         assert vals == want
         assert np.array_equal(Xf, S.X.numpy()) and np.array_equal(Zf, S.Z.numpy())
+
+
+def _carry_worker(rank, G, port, q, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise.device import ShardedSample
+    n_loc, m_loc, N = 600, 450, 3  # shards that tile the global layout rank by rank
+    X, Z = _global_data(G, n_loc, m_loc)
+    S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
+                      torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
+                      group=dist.group.WORLD, ops=OracleOpsChain(), algo="pairs")
+    out = {"vals": [], "carried": []}
+    try:
+        for keys in ([3, 4, 5], [6, 7], [8, 9, 10, 11]):
+            if mode == "inplace" and keys[0] == 8:
+                S.Z.mul_(1)  # an in-place change on every rank: the images are recomputed
+            if mode == "one_rank" and keys[0] == 8 and rank == 0:
+                S.Z.mul_(1)  # on rank 0 alone: the ranks disagree, every rank raises
+            out["carried"].append(S._carried(False) is not None)
+            out["vals"] += [float(v) for v in S.UnN_many(keys)]
+        Xg = [torch.empty_like(S.X) for _ in range(G)]
+        Zg = [torch.empty_like(S.Z) for _ in range(G)]
+        dist.all_gather(Xg, S.X)
+        dist.all_gather(Zg, S.Z)
+        out["X"], out["Z"] = torch.cat(Xg).numpy(), torch.cat(Zg).numpy()
+    except RuntimeError as e:
+        out["raised"] = str(e)
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G,mode", [(2, "carry"), (3, "carry"), (2, "inplace"), (3, "one_rank")])
+def test_carried_images_over_ranks(G, mode):
+    """device.CARRY_IMAGES over ranks: the second and later UnN_many calls carry every rank's
+    records through the inverse chains (all-gathered records, chain_gather) instead of ranking
+    again; estimates and final arrays equal the one-process score path call after call.  An
+    in-place change of the sample on every rank drops the carried images; on one rank alone the
+    ranks disagree and every rank raises in values()."""
+    import tuplewise  # noqa: F401
+    from tuplewise.device import ShardedSample
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_carry_worker, args=(r, G, port, q, mode)) for r in range(G)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(G))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if mode == "one_rank":
+        assert all("disagree" in got[r].get("raised", "") for r in range(G)), got
+        return
+    out = got[0]
+    assert out["carried"] == [False, True, mode == "carry"]
+    X, Z = _global_data(G, 600, 450)
+    S1 = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * 3,
+                       ops=OracleOps(), algo="pairs")
+    want = [float(S1.UnN(k)) for k in [3, 4, 5, 6, 7, 8, 9, 10, 11]]
+    assert out["vals"] == want
+    assert np.array_equal(out["X"], S1.X.numpy()) and np.array_equal(out["Z"], S1.Z.numpy())

@@ -386,3 +386,42 @@ def test_c2_one_shard_on_rank_images(gpu, tie_mode):
     got = int(S.local_counts()[0])
     want = O.count_half_sorted(X, Z) if tie_mode == "half" else O.count_gt_sorted(X, Z)
     assert got == want
+
+
+@pytest.mark.parametrize("tie_mode,algo", [("strict", "pairs"), ("half", "pairs"),
+                                           ("strict", "sorted")])
+def test_carried_images_equal_fresh_ranking(gpu, tie_mode, algo):
+    """device.CARRY_IMAGES: consecutive UnN_many calls on one sample carry the records of the
+    final arrays (tw_chain_scatter of the records by the chains' last positions) and skip the
+    ranking; every call's estimates and final arrays equal the same calls with a fresh ranking
+    each time.  An in-place change of X (its version counter) or an assignment drops them."""
+    import torch
+    from tuplewise import device as D
+    from tuplewise.device import ShardedSample
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    n = 70_000
+    X = (torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) + 0.3).round(
+        decimals=2)
+    Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen).round(decimals=2)
+    calls = [range(3, 7), range(10, 13), range(20, 40), range(50, 54)]
+
+    def run(carry):
+        D.CARRY_IMAGES = carry
+        try:
+            S = ShardedSample(X.clone(), Z.clone(), 16, tie_mode=tie_mode, algo=algo)
+            out, seen = [], []
+            for i, ks in enumerate(calls):
+                if i == 3:
+                    S.X.add_(0.0)  # in place: the carried images are dropped
+                seen.append(S._carried(tie_mode == "half") is not None)
+                out.append(([float(v) for v in S.UnN_many(ks)], S.X.cpu().numpy(),
+                            S.Z.cpu().numpy()))
+            return out, seen
+        finally:
+            D.CARRY_IMAGES = True
+    got, seen = run(True)
+    want, _ = run(False)
+    assert seen == [False, True, True, False]
+    for (gv, gx, gz), (wv, wx, wz) in zip(got, want):
+        assert gv == wv
+        assert np.array_equal(gx, wx) and np.array_equal(gz, wz)

@@ -9,7 +9,12 @@ all-gather and the local part of the counts' reduction, one count launch of K x 
 gather of the rank's final arrays.  Reports ms per call and the efficiency against the one-GPU
 call / G.  Round 5: the efficiency takes both ranks' UNinstrumented times (the per-part event
 markers of the parts run cost a G = 8 rank's K = 4 call ~0.07 ms, which the round-4 figure
-charged to rank G - 1).  Run on the GPU box:
+charged to rank G - 1); and every G is timed twice — a sample's FIRST call (the ranking, the Z
+all-gather it waits for) and its later calls with the images carried (device.CARRY_IMAGES: no
+ranking; the all-gathers of both samples and of both record arrays, as device copies, and the
+inverse-chain gathers of scores and records on a side stream beside the counts), each against
+the one-GPU call of the same kind / G.  The sub-chunk schedules of the round-5 study are in
+profiles/r05s36_chain_probe.log.  Run on the GPU box:
     python tools/chain_probe.py [K ...]"""
 import pathlib
 import sys
@@ -46,8 +51,9 @@ def ev_time(fn, reps):
     return e0.elapsed_time(e1) / reps, (time.perf_counter() - t0) / reps * 1e3
 
 
-def one_gpu_call(K, chain):
+def one_gpu_call(K, chain, carry):
     D.CHAIN_STEPS = chain
+    D.CARRY_IMAGES = carry
     S = ShardedSample(X.clone(), Z.clone(), N, algo="pairs")
     base = [1000]
 
@@ -58,16 +64,19 @@ def one_gpu_call(K, chain):
         return ev_time(call, 5)
     finally:
         D.CHAIN_STEPS = True
+        D.CARRY_IMAGES = True
 
 
-def rank_call(G, r, K, parts=False, product=False, side=True):
-    """Rank r's device work in one call of the strong problem split over G ranks: by default
-    the product's schedule (device.CHAIN_SUB = 0: one exchange, unpack and count per chunk).
-    product: the CHAIN_SUB = 5 schedule at G > 1 (device.py _unn_many_chain): the chunk in >= 2
-    sub-chunks, each sub-chunk's emission and exchange copy on a side stream (sub-chunk j+1's
-    emission beside sub-chunk j's count), unpack + count on the main stream, the final gather
-    on another side stream beside the counts.  side=False: the same sub-chunks all on the
-    main stream (every sub-chunk's emission + copy first, then its unpack + count)."""
+# every element's records (one ranking of the whole sample): the carried records all ranks hold
+XR, ZR = HipOps().rank_images_query(Z, X, Z, L.TW_F64)
+
+
+def rank_call(G, r, K, parts=False, carried=False):
+    """Rank r's device work in one call of the strong problem split over G ranks, the
+    product's schedule (device.CHAIN_SUB = 0: one exchange, unpack and count per chunk).
+    carried: a later call of the sample (device.CARRY_IMAGES): no Z all-gather to wait for and
+    no ranking; the all-gathers (device copies) and the final gathers of scores and records on
+    a side stream."""
     ops = HipOps()
     nl, Nl = n // G, N // G
     x_off, z_off, _ = prop_swor_layout(nl, nl, Nl)
@@ -102,55 +111,36 @@ def rank_call(G, r, K, parts=False, product=False, side=True):
         t.setdefault(name, []).append((e0, e1))
         return out
 
-    Zg = torch.empty_like(Z)  # the all-gathered Z (a device copy of the same bytes)
+    # the all-gathered arrays (device copies of the same bytes)
+    Xg, Zg, RXg, RZg = (torch.empty_like(a) for a in (X, Z, XR, ZR))
     full = torch.zeros(K * N + 1, dtype=torch.int64, device="cuda")
-    Sub = max(1, min(5, -(-C // 2)))  # device.CHAIN_SUB = 5
-    nsub = -(-C // Sub)
-    sends = [torch.empty(G * Sub * (cap + 1), dtype=torch.int64, device="cuda")
-             for _ in range(nsub)]
-    recvs = [torch.empty_like(b) for b in sends]
-    es, fs = torch.cuda.Stream(), torch.cuda.Stream()
+    fs = torch.cuda.Stream()
+    xr_c, zr_c = XR[r * nl:(r + 1) * nl], ZR[r * nl:(r + 1) * nl]
 
-    def call_product():
+    def side_work():
+        # the product: the async all-gathers, then the inverse-chain gathers of the scores
+        # (and of the records when they are carried) on a side stream beside the counts
         main = torch.cuda.current_stream()
-        Zg.copy_(Z)
-        xr, zr = ops.rank_images_query(Z, xq, zq, L.TW_F64)
         fs.wait_stream(main)
         with torch.cuda.stream(fs):
-            ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs, kzs)
-        for i0 in range(0, K, C):
-            c = min(C, K - i0)
-            st = es if side else main
-            st.wait_stream(main)
-            evs = []
-            with torch.cuda.stream(st):
-                for j, a in enumerate(range(0, c, Sub)):
-                    cs = min(Sub, c - a)
-                    ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0 and a == 0, r, G,
-                                   kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz, Nl,
-                                   send=sends[j], cap=cap, flag=flag)
-                    sz = G * cs * (cap + 1)
-                    recvs[j][:sz].copy_(sends[j][:sz])
-                    ev = None
-                    if side:
-                        ev = torch.cuda.Event()
-                        ev.record(es)
-                    evs.append((a, cs, j, ev))
-            for a, cs, j, ev in evs:
-                if ev is not None:
-                    main.wait_event(ev)
-                ops.chain_unpack(recvs[j], G, cs, cap, False, nl, nl, x_bag[a:a + cs],
-                                 z_bag[a:a + cs], flag, kx, kz, Nl)
-                ops.count_chain(x_bag[a:a + cs], xo, z_bag[a:a + cs], zo, Nl, cs, nl, nl, kx,
-                                kz, False, counts[i0 + a:i0 + a + cs])
-        main.wait_stream(fs)
-        full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts)
+            Xg.copy_(X)
+            if carried:
+                Zg.copy_(Z)
+            ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs)
+            RXg.copy_(XR)
+            RZg.copy_(ZR)
+            ops.chain_gather(RXg, RZg, r * nl, nl, r * nl, nl, kxs, kzs)
 
     def call():
-        if G > 1:  # round 5: the Z all-gather the ranking waits for, as a device copy of its
-            # bytes (the X all-gather runs asynchronously under the counts, not timed here)
-            mark("all-gather Z (device copy)", lambda: Zg.copy_(Z))
-        xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
+        main = torch.cuda.current_stream()
+        if carried:
+            xr, zr = xr_c, zr_c
+        else:
+            if G > 1:  # the Z all-gather the ranking waits for
+                mark("all-gather Z (device copy)", lambda: Zg.copy_(Z))
+            xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
+        if G > 1:
+            side_work()
         for i0 in range(0, K, C):
             c = min(C, K - i0)
             first = i0 == 0
@@ -169,35 +159,34 @@ def rank_call(G, r, K, parts=False, product=False, side=True):
             mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz,
                                                   False, counts[i0:i0 + c]))
         if G == 1:
-            mark("final scatter", lambda: ops.chain_scatter(X, xpos, Z, zpos))
+            mark("final scatter (scores, records)",
+                 lambda: (ops.chain_scatter(X, xpos, Z, zpos),
+                          ops.chain_scatter(xr, xpos, zr, zpos)))
         else:
-            mark("final gather", lambda: ops.chain_gather(X, Z, r * nl, nl, r * nl, nl, kxs,
-                                                          kzs))
+            main.wait_stream(fs)
             # the counts' all-reduce (with the overflow flag) stands in as its local fill
             mark("counts reduce (local part)",
                  lambda: full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
-    ms, host = ev_time(call_product if (product and G > 1) else call, 5)
+    ms, host = ev_time(call, 5)
     if parts:
         t = {k: sum(a.elapsed_time(b) for a, b in v) / 6 for k, v in t.items()}
     return ms, host, t
 
 
 for K in Ks:
-    one_gpu_call(K, True)  # warm: the process's first calls run before the clock has risen
-    ch, ch_host = one_gpu_call(K, True)
-    st, st_host = one_gpu_call(K, False)
-    print(f"K={K}: one GPU, step chains {ch:.3f} ms/call ({ch / K:.4f} ms/step; host "
-          f"{ch_host:.3f}); one launch per step {st:.3f} ms/call ({st / K:.4f} ms/step)",
-          flush=True)
+    one_gpu_call(K, True, True)  # warm: the process's first calls run before the clock has risen
+    ch, ch_host = one_gpu_call(K, True, True)
+    chf, _ = one_gpu_call(K, True, False)
+    st, st_host = one_gpu_call(K, False, True)
+    print(f"K={K}: one GPU, step chains {ch:.3f} ms/call with carried images ({ch / K:.4f} "
+          f"ms/step; host {ch_host:.3f}), {chf:.3f} ranking every call; one launch per step "
+          f"{st:.3f} ms/call ({st / K:.4f} ms/step)", flush=True)
     for G in (1, 2, 4, 8):
-        ms = [rank_call(G, r, K)[0] for r in sorted({0, G - 1})]
-        mp = [rank_call(G, r, K, product=True)[0] for r in sorted({0, G - 1})]
-        mm = [rank_call(G, r, K, product=True, side=False)[0] for r in sorted({0, G - 1})]
-        _, _, parts = rank_call(G, G - 1, K, parts=True)
-        print(f"  G={G}: product (one exchange per chunk) ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
-              + f" ms/call, efficiency {ch / G / max(ms):.3f}; sub-chunks of 5, side stream "
-              + "/".join(f"{v:.3f}" for v in mp) + f" ms/call, efficiency {ch / G / max(mp):.3f}; sub-chunks on one stream "
-              + "/".join(f"{v:.3f}" for v in mm) + f" ms/call, efficiency {ch / G / max(mm):.3f}"
-              f"; ideal (one-GPU chain call / G) {ch / G:.3f}; parts (serial, instrumented "
-              f"rank {G - 1}) " + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()),
-              flush=True)
+        for carried, ideal, label in ((False, chf, "first call (ranking)"),
+                                      (True, ch, "later calls (carried images)")):
+            ms = [rank_call(G, r, K, carried=carried)[0] for r in sorted({0, G - 1})]
+            _, _, parts = rank_call(G, G - 1, K, parts=True, carried=carried)
+            print(f"  G={G} {label}: ranks 0/{G - 1} " + "/".join(f"{v:.3f}" for v in ms)
+                  + f" ms/call, efficiency {ideal / G / max(ms):.3f} (ideal: the one-GPU call "
+                  f"/ G = {ideal / G:.3f}); parts (instrumented rank {G - 1}) "
+                  + ", ".join(f"{k} {v:.3f}" for k, v in parts.items()), flush=True)

@@ -48,6 +48,12 @@ CHAIN_BUCKET_MAX = 16384
 # tail, cross-stream waits) cost a G = 8 rank 0.05-0.09 ms per call at T = 4 and 0.13-0.15 ms
 # at T = 20 — more than the exchange they hide (~0.03 / ~0.08 ms over xGMI)
 CHAIN_SUB = 0
+# UnN_many on the step chains carries the rank-image records of the final arrays to the next
+# call: a repartition permutes the sample and never changes its multiset, so the images (ranks
+# against the whole Z) stay valid while the arrays are the ones the chains left — the next call
+# skips the ranking (and over ranks the Z all-gather it waits for).  Any assignment of X / Z or
+# an in-place change (the tensors' version counters) drops them.
+CARRY_IMAGES = True
 # one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
 # images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
 ONESHOT_RANK = True
@@ -371,6 +377,38 @@ class ShardedSample:
     group too (every RCCL call of the multi-rank path then runs on one GPU; same integers, same
     arrays as the one-process path); False is refused with several ranks."""
 
+    # X / Z: every assignment drops the step chains' carried images (CARRY_IMAGES)
+    @property
+    def X(self):
+        return self._X
+
+    @X.setter
+    def X(self, v):
+        self._X = v
+        self._carry = None
+
+    @property
+    def Z(self):
+        return self._Z
+
+    @Z.setter
+    def Z(self, v):
+        self._Z = v
+        self._carry = None
+
+    def _carried(self, half):
+        """The records {image, ...} of the current own elements carried from the last chain
+        call, or None: valid while X / Z are the tensors that call left (same objects, same
+        version counters) with the same tie mode."""
+        c = getattr(self, "_carry", None)
+        if not CARRY_IMAGES or c is None:
+            return None
+        X, Z, vx, vz, h, xr, zr = c
+        if (X is self._X and Z is self._Z and X._version == vx and Z._version == vz
+                and h == half):
+            return xr, zr
+        return None
+
     def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None,
                  algo: str = "auto", exchange: str = "fixed", collectives=None):
         if exchange not in ("fixed", "exact"):
@@ -396,6 +434,7 @@ class ShardedSample:
         if self.G > 1 and not self.coll:
             raise ValueError("several ranks always take the collective branches")
         self._flag_all = None  # the ranks' overflow flags, summed by the last counts reduction
+        self._carry_all = None  # the ranks' carried-images bits, summed by the same reduction
         if X.dtype == t.float64:
             self.dtype = L.TW_F64
         elif X.dtype == t.int64:
@@ -483,21 +522,28 @@ class ShardedSample:
             return None
         return sum(f.to(self.t.int64) for f in fl)
 
-    def _reduce_counts(self, counts):
+    def _reduce_counts(self, counts, carried=None):
         """(T, N) local counts -> (T, G*N) global counts in shard order on every rank, with the
         ranks' overflow flags summed in the SAME all-reduce (one extra element): a bucket that
         overflowed on any rank is then seen by every rank in values(), so all ranks raise
-        together instead of the two involved ones only."""
+        together instead of the two involved ones only.  carried (the step
+        chains): whether this rank used carried images — summed in a second extra element, so a
+        rank whose sample changed alone (its images recomputed while the others carried theirs)
+        makes every rank raise in values()."""
         t, G, N, r = self.t, self.G, self.N, self.rank
         T = counts.shape[0]
-        flat = t.zeros((T * G * N + 1,), dtype=t.int64, device=counts.device)
-        flat[:-1].view(T, G * N)[:, r * N:(r + 1) * N] = counts
+        extra = 1 if carried is None else 2
+        flat = t.zeros((T * G * N + extra,), dtype=t.int64, device=counts.device)
+        flat[:T * G * N].view(T, G * N)[:, r * N:(r + 1) * N] = counts
         f = self._local_flag()
         if f is not None:
             flat[-1:] = f.reshape(1)
+        if carried:
+            flat[-2:-1] = 1
         self.dist.all_reduce(flat, group=self.group)
         self._flag_all = flat[-1:]
-        return flat[:-1].view(T, G * N)
+        self._carry_all = None if carried is None else flat[-2:-1]
+        return flat[:T * G * N].view(T, G * N)
 
     def check_exchange(self):
         """Raise if a fixed-capacity repartition overflowed a bucket (host sync).  The flag is
@@ -513,6 +559,10 @@ class ShardedSample:
         if getattr(self, "_chain_flag", None) is not None and int(self._chain_flag.item()):
             raise RuntimeError("UnN_many: a step-chain bucket overflowed its capacity; the "
                                "counts and arrays are invalid")
+        if self._carry_all is not None and int(self._carry_all.item()) not in (0, self.G):
+            raise RuntimeError("UnN_many: the ranks disagree on the carried rank images (a "
+                               "rank's sample was changed on that rank alone); the counts are "
+                               "invalid")
 
     def _exchange_records(self, send, c):
         """All-to-all of the packed records (split sizes from the (4, G) host counts) and the
@@ -817,20 +867,37 @@ class ShardedSample:
         dev = self.X.device
         half = self.pred == L.TW_PRED_HALF
         coll = self.coll  # the exchange branch (several ranks, or forced at world size 1)
-        x_work = None
+        works = []  # the asynchronous all-gathers the final arrays wait for
+        rec = self._carried(half)
+        carried = rec is not None
         if coll:
-            # the ranking needs the whole Z now; the whole X only for the final arrays
-            # (chain_gather), so its all-gather runs asynchronously under the chunks' counts
-            Z0 = self._all_gather(self.Z)
-            X0, x_work = self._all_gather(self.X, async_op=True)
+            # the ranking needs the whole Z now (unless the images are carried); the whole X
+            # only for the final arrays (chain_gather), so its all-gather runs asynchronously
+            # under the chunks' counts
+            if carried:
+                Z0, w = self._all_gather(self.Z, async_op=True)
+                works.append(w)
+            else:
+                Z0 = self._all_gather(self.Z)
+            X0, w = self._all_gather(self.X, async_op=True)
+            works.append(w)
         else:
             X0, Z0 = self.X, self.Z
-        rec = ops.rank_images_query(Z0, self.X, self.Z, self.dtype, half)
+        if not carried:
+            rec = ops.rank_images_query(Z0, self.X, self.Z, self.dtype, half)
         if rec is None:
-            if x_work is not None:
-                x_work.wait()
+            for w in works:
+                w.wait()
             return [self.UnN(k) for k in keys]
         xr, zr = rec
+        RX = RZ = None
+        if coll and CARRY_IMAGES:
+            # the records follow their elements: gathered by the same inverse chains as the
+            # scores, from every rank's records (asynchronous, under the counts)
+            RX, w = self._all_gather(xr, async_op=True)
+            works.append(w)
+            RZ, w = self._all_gather(zr, async_op=True)
+            works.append(w)
         T = len(keys)
         C = min(T, CHAIN_MAX)
         M64 = 2 ** 64 - 1
@@ -846,10 +913,13 @@ class ShardedSample:
             fs = self._final_stream
             fs.wait_stream(main)
             with t.cuda.stream(fs):
-                if x_work is not None:
-                    x_work.wait()
-                    x_work = None
+                for w in works:
+                    if w is not None:
+                        w.wait()
+                works = []
                 final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
+                if RX is not None:
+                    final = final + ops.chain_gather(RX, RZ, r * n, n, r * m, m, kxs, kzs)
                 for a in final:
                     a.record_stream(main)
         kx = int(n / N)
@@ -905,7 +975,7 @@ class ShardedSample:
                         self._emit_stream = t.cuda.Stream()
                     es = self._emit_stream
                     es.wait_stream(t.cuda.current_stream())
-                works = []
+                xchg = []
                 with (t.cuda.stream(es) if es is not None else contextlib.nullcontext()):
                     for j, a in enumerate(range(0, c, Sub)):
                         cs = min(Sub, c - a)
@@ -913,9 +983,9 @@ class ShardedSample:
                                        kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz,
                                        N, send=sends[j], cap=cap, flag=self._chain_flag)
                         sz = G * cs * (cap + 1) * W
-                        works.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
-                                                                 async_op=True)))
-                for a, cs, j, work in works:
+                        xchg.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
+                                                                async_op=True)))
+                for a, cs, j, work in xchg:
                     if work is not None:
                         work.wait()
                     ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
@@ -926,17 +996,28 @@ class ShardedSample:
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
             count(x_bag, z_bag, c, counts[i0:i0 + c])
+        carry = None
         if coll:
             if final is not None:
                 t.cuda.current_stream().wait_stream(self._final_stream)
-                self.X, self.Z = final
             else:
-                if x_work is not None:
-                    x_work.wait()
-                self.X, self.Z = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
-            counts = self._reduce_counts(counts)
+                for w in works:
+                    if w is not None:
+                        w.wait()
+                final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
+                if RX is not None:
+                    final = final + ops.chain_gather(RX, RZ, r * n, n, r * m, m, kxs, kzs)
+            self.X, self.Z = final[0], final[1]
+            if RX is not None:
+                carry = (final[2], final[3])
+            counts = self._reduce_counts(counts, carried=carried)
         else:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
+            if CARRY_IMAGES:
+                carry = ops.chain_scatter(xr, xpos, zr, zpos)
+        if carry is not None:  # after the assignments above (they drop the old ones)
+            self._carry = (self._X, self._Z, self._X._version, self._Z._version, half,
+                           carry[0], carry[1])
         return [np.mean(v) for v in self.values(counts)]
 
     def _all_to_all(self, out, inp, async_op=False):
