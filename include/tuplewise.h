@@ -174,41 +174,31 @@ int tw_rank_images_query(const void* d_z_all, int64_t n_z_all, const void* d_x, 
  * d_send, per destination rank g a
  * chunk of steps buckets of (cap + 1) * W u64 words (W = 1 + half; word 0 of a bucket = its
  * count), each record {image word(s), local position (Z: n_x + position)}; a bucket past cap
- * sets *d_flag (the record is dropped).  heads_zero = 1: the buckets' count words are already
- * zero (tw_chain_unpack's d_send_reset after the exchange), no zeroing launch.  d_zero /
- * zero_words (round 5): u32 words a LATER launch needs zeroed and this one never touches (the
- * unpack's cursors, the count's output), zeroed by this launch's threads (0 words: none). */
+ * sets *d_flag (the record is dropped). */
 int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec, int64_t n_z,
                   int32_t half, uint32_t* d_x_pos, uint32_t* d_z_pos, int32_t first,
                   int32_t rank, int32_t world, const uint64_t* keys_x, const uint64_t* keys_z,
                   int32_t steps, int64_t x_shard, int64_t z_shard, int32_t n_shards,
                   void* d_x_bag, void* d_z_bag, uint32_t* d_cursors, uint64_t* d_send,
-                  int64_t cap, int32_t* d_flag, uint32_t* d_zero, int64_t zero_words,
-                  int32_t heads_zero, void* stream);
+                  int64_t cap, int32_t* d_flag, void* stream);
 /* The receiving side of tw_chain_emit's buckets after an equal-split all-to-all (d_recv: world
  * chunks in source order): every record appended to the bag region of its (step, side, shard)
  * — shard b of a side holds positions [min(b k, n), min((b+1) k, n)), k = x_shard / z_shard,
  * b = n_shards the tail — in runs reserved on d_cursors (steps x 2 (n_shards + 1) u32, zeroed
- * here unless cursors_zero = 1: zeroed by the emission's d_zero); a bag holds its shard's
- * multiset, in no particular order (what the counts read).  A count past cap sets *d_flag.
- * Zeroed by this launch for later ones (round 5): d_zero_out[0 .. zero_out_words) (the count's
- * output) and the count words of send_buckets buckets of d_send_reset (stride (cap + 1) W: the
- * send buffer whose exchange is complete, for the next emission's heads_zero). */
+ * here); a bag holds its shard's multiset, in no particular order (what the counts read).  A
+ * count past cap sets *d_flag. */
 int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
                     int32_t half, int64_t n_x, int64_t n_z, int64_t x_shard, int64_t z_shard,
                     int32_t n_shards, void* d_x_bag, void* d_z_bag, uint32_t* d_cursors,
-                    int32_t* d_flag, int32_t cursors_zero, uint64_t* d_zero_out,
-                    int64_t zero_out_words, uint64_t* d_send_reset, int64_t send_buckets,
-                    void* stream);
+                    int32_t* d_flag, void* stream);
 /* The all-pairs counts of `steps` x n_shards bags in ONE launch: bag (c, s) = x images
  * [c * x_stride + d_x_off[s], c * x_stride + d_x_off[s + 1]) against z images likewise;
- * d_out[c * n_shards + s] (zeroed here unless out_zero = 1: zeroed by the launch before) =
- * #{x > z} (half = 1: 2 #{x > z} + #{x == z}, the tw_count_pairs TW_PRED_HALF units).
- * Identical to tw_count_pairs on the scores. */
+ * d_out[c * n_shards + s] (zeroed here) = #{x > z} (half = 1: 2 #{x > z} + #{x == z}, the
+ * tw_count_pairs TW_PRED_HALF units).  Identical to tw_count_pairs on the scores. */
 int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off, int64_t x_stride,
                          const void* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
                          int32_t n_shards, int32_t steps, int64_t max_nx, int64_t max_nz,
-                         int32_t half, uint64_t* d_out, int32_t out_zero, void* stream);
+                         int32_t half, uint64_t* d_out, void* stream);
 /* The same counts as tw_count_pairs_chain in O(n + m) per bag (algo="sorted", SURVEY row f4;
  * estimation-experiment/main.py:29-31's integer): each bag's z images (integers in
  * [0, z_total], z_total = the Z count the images were ranked against) counting-sorted into

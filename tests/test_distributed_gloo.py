@@ -178,10 +178,7 @@ class OracleOpsChain(OracleOpsRank):
         return torch.from_numpy(xr), torch.from_numpy(zr)
 
     def chain_emit(self, xr, zr, half, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
-                   n_shards, x_bag=None, z_bag=None, cursors=None, send=None, cap=0, flag=None,
-                   zero=None, heads_zero=False):
-        if zero is not None:  # a later launch's memory, zeroed here (tw_chain_emit's d_zero)
-            zero.zero_()
+                   n_shards, x_bag=None, z_bag=None, cursors=None, send=None, cap=0, flag=None):
         n, m = xr.numel(), zr.numel()
         W = 2 if half else 1
         steps = len(keys_x)
@@ -221,13 +218,9 @@ class OracleOpsChain(OracleOpsRank):
                         recs[:, 0], recs[:, 1] = v, q
 
     def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx=0, kz=0,
-                     n_shards=0, cursors_zero=False, zero_out=None, send_reset=None):
+                     n_shards=0):
         # (positions kept: the device appends each shard's records in runs, in any order)
         W = 2 if half else 1
-        if zero_out is not None:
-            zero_out.zero_()
-        if send_reset is not None:  # the send buckets' heads, for the next emission
-            send_reset.view(-1, (cap + 1) * W)[:, 0] = 0
         buf = recv.numpy().view(np.uint64)
         for b in range(world * steps):
             c = b % steps
@@ -243,7 +236,7 @@ class OracleOpsChain(OracleOpsRank):
             z_bag[c].numpy().view(np.uint32)[p[~isx] - n] = v[~isx]
 
     def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
-                    z_stride, max_nx, max_nz, half, out, out_zero=False):
+                    z_stride, max_nx, max_nz, half, out):
         xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
         for c in range(steps):
             xb = x_bag[c].numpy().view(np.float32)

@@ -87,7 +87,7 @@ def rank_call(G, r, K, parts=False, carried=False):
     C = min(K, D.CHAIN_MAX)
     tot = 2 * nl
     cap = max(1, tot // G + tot // (8 * G) + 1024)
-    send = torch.zeros(G * C * (cap + 1), dtype=torch.int64, device="cuda")  # heads zero
+    send = torch.empty(G * C * (cap + 1), dtype=torch.int64, device="cuda")
     recv = torch.empty_like(send)
     flag = torch.zeros(1, dtype=torch.int32, device="cuda")
     x_bag = torch.empty((C, nl), dtype=torch.float32, device="cuda")
@@ -144,28 +144,20 @@ def rank_call(G, r, K, parts=False, carried=False):
         for i0 in range(0, K, C):
             c = min(C, K - i0)
             first = i0 == 0
-            # the product's zeroing (device.py): the count's output zeroed by the launch
-            # before it, the unpack's cursors by the emission, the send heads by the unpack
             if G == 1:  # one process: straight into the bags
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, 0, 1,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
-                                                    x_bag=x_bag, z_bag=z_bag, cursors=cur,
-                                                    zero=counts[i0:i0 + c]))
+                                                    x_bag=x_bag, z_bag=z_bag, cursors=cur))
             else:
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, r, G,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
-                                                    send=send, cap=cap, flag=flag,
-                                                    zero=ops.unpack_cursors(c, Nl, "cuda"),
-                                                    heads_zero=True))
+                                                    send=send, cap=cap, flag=flag))
                 sz = G * c * (cap + 1)
                 mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
                 mark("unpack", lambda: ops.chain_unpack(recv, G, c, cap, False, nl, nl, x_bag,
-                                                        z_bag, flag, kx, kz, Nl,
-                                                        cursors_zero=True,
-                                                        zero_out=counts[i0:i0 + c],
-                                                        send_reset=send))
+                                                        z_bag, flag, kx, kz, Nl))
             mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz,
-                                                  False, counts[i0:i0 + c], out_zero=True))
+                                                  False, counts[i0:i0 + c]))
         if G == 1:
             mark("final scatter (scores, records)",
                  lambda: (ops.chain_scatter(X, xpos, Z, zpos),

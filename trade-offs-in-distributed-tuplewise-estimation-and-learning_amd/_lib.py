@@ -49,11 +49,11 @@ _SIGNATURES = {
     "tw_rank_images_query": [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _vp, _vp,
                              _vp],
     "tw_chain_emit": [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32,
-                      _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _vp],
+                      _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp],
     "tw_chain_unpack": [_vp, _i32, _i32, _i64, _i32, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp,
-                        _i32, _vp, _i64, _vp, _i64, _vp],
+                        _vp],
     "tw_count_pairs_chain": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i32, _vp,
-                             _i32, _vp],
+                             _vp],
     "tw_count_pairs_chain_bucket": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64,
                                     _i32, _vp, _vp],
     "tw_count_chain_set_plan": [_i32, _i64],

@@ -77,11 +77,6 @@ struct ChainEmit {
   int64_t cap;
   int* flag;
   int bx;  // blocks of X tiles; the rest are Z tiles
-  // memory a LATER launch needs zeroed and this one never touches (the unpack's cursors over
-  // ranks, the count's output in one process): zeroed by this launch's threads, one launch
-  // fewer on the stream
-  uint32_t* zero;
-  int64_t nzero;
 };
 
 __device__ __forceinline__ int64_t em_region(int b, uint32_t k, int64_t n) {
@@ -168,9 +163,6 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
   const FastDiv dk = isx ? em.dkx : em.dkz;
   const FastDiv dn = isx ? em.dnx : em.dnz;
   const int cnt = (int)min<int64_t>(TILE, n - (int64_t)tile * TILE);
-  for (int64_t i = (int64_t)blockIdx.x * kEmThreads + threadIdx.x; i < em.nzero;
-       i += (int64_t)gridDim.x * kEmThreads)
-    em.zero[i] = 0u;
   for (int i = threadIdx.x; i < S * NB && i < MB; i += kEmThreads) hist[i] = 0;
   __syncthreads();  // fs, hist
   for (int c0 = 0; c0 < em.steps; c0 += S) {
@@ -281,12 +273,6 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
   }
 }
 
-// n u64 words at p, p + stride, ... zeroed by a launch for a later one (none: n = 0)
-struct ZeroU64 {
-  uint64_t* p;
-  int64_t n, stride;
-};
-
 // the count slots of every (destination, step) bucket of a send buffer
 __global__ __launch_bounds__(kBlock) void k_chain_zero_heads(uint64_t* __restrict__ send,
                                                              int64_t buckets, int64_t stride) {
@@ -308,18 +294,8 @@ constexpr int kUnpackPer = 4;  // records per thread and round
 __global__ __launch_bounds__(kBlock) void k_chain_unpack(
     const uint64_t* __restrict__ recv, int world, int steps, int parts, int64_t cap, int W,
     int half, int64_t nx, int64_t nz, int64_t kx, int64_t kz, int nsh, void* __restrict__ xbag,
-    uint32_t* __restrict__ zbag, unsigned* __restrict__ cursors, int* __restrict__ flag,
-    ZeroU64 z1, ZeroU64 z2) {
+    uint32_t* __restrict__ zbag, unsigned* __restrict__ cursors, int* __restrict__ flag) {
   extern __shared__ unsigned un_lds[];  // hist[NB], base[NB]
-  // memory later launches need zeroed, untouched here: the count's output and the send
-  // buckets' heads of the next emission (the exchange that read them is complete)
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < z1.n + z2.n;
-       i += (int64_t)gridDim.x * kBlock) {
-    if (i < z1.n)
-      z1.p[i * z1.stride] = 0ull;
-    else
-      z2.p[(i - z1.n) * z2.stride] = 0ull;
-  }
   const int NB = 2 * (nsh + 1);
   unsigned* hist = un_lds;
   unsigned* base = un_lds + NB;
@@ -636,8 +612,7 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
                              const uint64_t* keys_z, int32_t steps, int64_t x_shard,
                              int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
                              uint32_t* d_cursors, uint64_t* d_send, int64_t cap,
-                             int32_t* d_flag, uint32_t* d_zero, int64_t zero_words,
-                             int32_t heads_zero, void* stream) {
+                             int32_t* d_flag, void* stream) {
   TW_ARG_CHECK(n_x >= 0 && n_z >= 0 && world >= 1 && rank >= 0 && rank < world &&
                    steps >= 0 && steps <= kChainMax && n_shards >= 0 && x_shard >= 0 &&
                    z_shard >= 0 && (half == 0 || half == 1) && (first == 0 || first == 1),
@@ -651,14 +626,7 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
                "tw_chain_emit: at most %d buckets (shards + 1, or ranks)", kEmMaxBig);
   TW_ARG_CHECK(steps == 0 || (keys_x != nullptr && keys_z != nullptr),
                "tw_chain_emit: keys missing");
-  TW_ARG_CHECK(zero_words >= 0 && (zero_words == 0 || d_zero != nullptr) &&
-                   (heads_zero == 0 || heads_zero == 1),
-               "tw_chain_emit: bad zero range");
-  hipStream_t st0 = (hipStream_t)stream;
-  if (steps == 0 || n_x + n_z == 0) {
-    if (zero_words > 0) TW_HIP_CHECK(tw_zero_async(d_zero, 0, sizeof(uint32_t) * zero_words, st0));
-    return TW_OK;
-  }
+  if (steps == 0 || n_x + n_z == 0) return TW_OK;
   TW_ARG_CHECK(d_x_pos != nullptr && d_z_pos != nullptr, "tw_chain_emit: position state missing");
   if (xchg)
     TW_ARG_CHECK(d_flag != nullptr && cap >= 1 && world <= 1024,
@@ -697,13 +665,10 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
   em.send = d_send;
   em.cap = cap;
   em.flag = d_flag;
-  em.zero = d_zero;
-  em.nzero = zero_words;
   if (xchg) {
     const int64_t buckets = (int64_t)world * steps;
-    if (!heads_zero)  // (heads_zero: the previous unpack reset them, tw_chain_unpack)
-      hipLaunchKernelGGL(k_chain_zero_heads, dim3((unsigned)ceil_div(buckets, kBlock)),
-                         dim3(kBlock), 0, st, d_send, buckets, (cap + 1) * em.W);
+    hipLaunchKernelGGL(k_chain_zero_heads, dim3((unsigned)ceil_div(buckets, kBlock)),
+                       dim3(kBlock), 0, st, d_send, buckets, (cap + 1) * em.W);
   } else {
     TW_HIP_CHECK(tw_zero_async(d_cursors, 0,
                                sizeof(unsigned) * (size_t)steps * 2 * (n_shards + 1), st));
@@ -761,39 +726,22 @@ extern "C" int tw_chain_set_emit(int32_t epr, int32_t steps_per_round) {
 extern "C" int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
                                int32_t half, int64_t n_x, int64_t n_z, int64_t x_shard,
                                int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
-                               uint32_t* d_cursors, int32_t* d_flag, int32_t cursors_zero,
-                               uint64_t* d_zero_out, int64_t zero_out_words,
-                               uint64_t* d_send_reset, int64_t send_buckets, void* stream) {
+                               uint32_t* d_cursors, int32_t* d_flag, void* stream) {
   TW_ARG_CHECK(world >= 1 && steps >= 0 && steps <= kChainMax && cap >= 1 && n_x >= 0 &&
                    n_z >= 0 && (half == 0 || half == 1) && (int64_t)world * steps < 65536 &&
                    x_shard >= 0 && z_shard >= 0 && n_shards >= 0 && n_shards < kEmMaxBig,
                "tw_chain_unpack: bad sizes");
-  TW_ARG_CHECK((cursors_zero == 0 || cursors_zero == 1) && zero_out_words >= 0 &&
-                   (zero_out_words == 0 || d_zero_out != nullptr) && send_buckets >= 0 &&
-                   (send_buckets == 0 || d_send_reset != nullptr),
-               "tw_chain_unpack: bad zero ranges");
-  hipStream_t st = (hipStream_t)stream;
-  if (steps == 0 || n_x + n_z == 0) {
-    if (zero_out_words > 0)
-      TW_HIP_CHECK(tw_zero_async(d_zero_out, 0, sizeof(uint64_t) * zero_out_words, st));
-    if (send_buckets > 0)
-      hipLaunchKernelGGL(k_chain_zero_heads, dim3((unsigned)ceil_div(send_buckets, kBlock)),
-                         dim3(kBlock), 0, st, d_send_reset, send_buckets,
-                         (cap + 1) * (half ? 2 : 1));
-    return TW_OK;
-  }
+  if (steps == 0 || n_x + n_z == 0) return TW_OK;
   TW_ARG_CHECK(d_cursors != nullptr && d_flag != nullptr, "tw_chain_unpack: cursors and flag");
+  hipStream_t st = (hipStream_t)stream;
   const int NB = 2 * (n_shards + 1);
-  if (!cursors_zero)  // (cursors_zero: the emission zeroed them, tw_chain_emit's d_zero)
-    TW_HIP_CHECK(tw_zero_async(d_cursors, 0, sizeof(uint32_t) * (size_t)NB * steps, st));
+  TW_HIP_CHECK(tw_zero_async(d_cursors, 0, sizeof(uint32_t) * (size_t)NB * steps, st));
   const int parts = (int)std::max<int64_t>(
       1, std::min<int64_t>(ceil_div(cap, (int64_t)kBlock * kUnpackPer), 64));
   hipLaunchKernelGGL(k_chain_unpack, dim3((unsigned)(parts * world * steps)), dim3(kBlock),
                      sizeof(unsigned) * 2 * (size_t)NB, st, d_recv, (int)world, (int)steps, parts,
                      cap, half ? 2 : 1, (int)half, n_x, n_z, x_shard, z_shard, (int)n_shards,
-                     d_x_bag, (uint32_t*)d_z_bag, (unsigned*)d_cursors, d_flag,
-                     ZeroU64{d_zero_out, zero_out_words, 1},
-                     ZeroU64{d_send_reset, send_buckets, (cap + 1) * (half ? 2 : 1)});
+                     d_x_bag, (uint32_t*)d_z_bag, (unsigned*)d_cursors, d_flag);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
@@ -802,7 +750,7 @@ extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
                                     int64_t x_stride, const void* d_z_bag,
                                     const int64_t* d_z_off, int64_t z_stride, int32_t n_shards,
                                     int32_t steps, int64_t max_nx, int64_t max_nz, int32_t half,
-                                    uint64_t* d_out, int32_t out_zero, void* stream) {
+                                    uint64_t* d_out, void* stream) {
   TW_ARG_CHECK(n_shards >= 0 && steps >= 0 && max_nx >= 0 && max_nz >= 0 && x_stride >= 0 &&
                    z_stride >= 0 && (half == 0 || half == 1),
                "tw_count_pairs_chain: bad sizes");
@@ -810,9 +758,7 @@ extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
   hipStream_t st = (hipStream_t)stream;
   const int64_t bags = (int64_t)n_shards * steps;
   if (bags == 0) return TW_OK;
-  TW_ARG_CHECK(out_zero == 0 || out_zero == 1, "tw_count_pairs_chain: out_zero 0 or 1");
-  if (!out_zero)  // (out_zero: zeroed by the launch before, tw_chain_emit / tw_chain_unpack)
-    TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)bags, st));
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)bags, st));
   if (max_nx == 0 || max_nz == 0) return TW_OK;
   const ChainPlan p = plan_chain(max_nx, max_nz, bags, half != 0);
   TW_ARG_CHECK(p.blocks * (kBlock / kWave) < (1ll << 31) && bags < (1ll << 31),

@@ -221,42 +221,24 @@ class HipOps:
         return xr, zr
 
     def chain_emit(self, xr, zr, half, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
-                   n_shards, x_bag=None, z_bag=None, cursors=None, send=None, cap=0, flag=None,
-                   zero=None, heads_zero=False):
+                   n_shards, x_bag=None, z_bag=None, cursors=None, send=None, cap=0, flag=None):
         """Walk len(keys_x) repartitions for this rank's elements (tw_chain_emit): into the
-        step bags (one process) or the send buckets (several ranks).  zero: a tensor a later
-        launch needs zeroed (the unpack's cursors, the count's output), zeroed by this one;
-        heads_zero: the send buckets' heads are already zero (reset by the last unpack)."""
+        step bags (one process) or the send buckets (several ranks)."""
         kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
         kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
-        zw = 0 if zero is None else zero.numel() * zero.element_size() // 4
         L.call("tw_chain_emit", L.ptr(xr), int(xr.numel()), L.ptr(zr), int(zr.numel()),
                int(bool(half)), L.ptr(xpos), L.ptr(zpos), int(bool(first)), int(rank),
                int(world), kxa.ctypes.data, kza.ctypes.data, len(kxa), int(kx), int(kz),
                int(n_shards), L.ptr(x_bag), L.ptr(z_bag), L.ptr(cursors), L.ptr(send),
-               int(cap), L.ptr(flag), L.ptr(zero), int(zw), int(bool(heads_zero)),
-               L.stream_handle())
+               int(cap), L.ptr(flag), L.stream_handle())
 
     def chain_unpack(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx, kz,
-                     n_shards, cursors_zero=False, zero_out=None, send_reset=None):
-        """The received records appended to their (step, shard) bags (tw_chain_unpack).
-        cursors_zero: the emission zeroed this HipOps' cursors (unpack_cursors); zero_out (the
-        count's output) and send_reset (a send buffer whose bucket heads the next emission
-        needs zero) are zeroed by this launch."""
-        cur = self.unpack_cursors(steps, n_shards, x_bag.device)
-        sb = 0 if send_reset is None else send_reset.numel() // ((int(cap) + 1) * (2 if half
-                                                                                    else 1))
+                     n_shards):
+        """The received records appended to their (step, shard) bags (tw_chain_unpack)."""
+        cur = self._unpack_cursors(int(steps) * 2 * (int(n_shards) + 1), x_bag.device)
         L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
                int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
-               L.ptr(z_bag), L.ptr(cur), L.ptr(flag), int(bool(cursors_zero)), L.ptr(zero_out),
-               0 if zero_out is None else int(zero_out.numel()), L.ptr(send_reset), int(sb),
-               L.stream_handle())
-
-    def unpack_cursors(self, steps, n_shards, dev):
-        """The cursors tw_chain_unpack uses for `steps` steps of n_shards shards (a view of
-        this HipOps' buffer: unpacks on one stream reuse it in order)."""
-        words = int(steps) * 2 * (int(n_shards) + 1)
-        return self._unpack_cursors(words, dev)[:words]
+               L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
 
     def _unpack_cursors(self, words, dev):
         # one buffer per HipOps, grown as needed; unpacks on one stream reuse it in order
@@ -266,13 +248,11 @@ class HipOps:
         return c
 
     def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
-                    z_stride, max_nx, max_nz, half, out, out_zero=False):
-        """Counts of steps x n_shards bags in one launch into out (steps, n_shards); out_zero:
-        out was zeroed by the launch before (the emission's or the unpack's zero range)."""
+                    z_stride, max_nx, max_nz, half, out):
+        """Counts of steps x n_shards bags in one launch into out (steps, n_shards)."""
         L.call("tw_count_pairs_chain", L.ptr(x_bag), L.ptr(x_off_dev), int(x_stride),
                L.ptr(z_bag), L.ptr(z_off_dev), int(z_stride), int(n_shards), int(steps),
-               int(max_nx), int(max_nz), int(bool(half)), L.ptr(out), int(bool(out_zero)),
-               L.stream_handle())
+               int(max_nx), int(max_nz), int(bool(half)), L.ptr(out), L.stream_handle())
         return out
 
     def count_chain_bucket(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps,
@@ -950,11 +930,9 @@ class ShardedSample:
             if bucket:
                 ops.count_chain_bucket(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
                                        self.max_nz, z_total, half, out)
-            else:  # (out zeroed by the launch before: the emission's or the unpack's range)
+            else:
                 ops.count_chain(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
-                                self.max_nx, self.max_nz, half, out, out_zero=True)
-        # the all-pairs count accumulates: its output is zeroed by the launch before it
-        zero_out = (lambda a, b: None) if bucket else (lambda a, b: counts[a:b])
+                                self.max_nx, self.max_nz, half, out)
         x_bag = t.empty((C, n), dtype=t.int64 if half else t.float32, device=dev)
         z_bag = t.empty((C, m), dtype=t.float32, device=dev)
         xpos = t.empty((n,), dtype=t.int32, device=dev)
@@ -976,13 +954,10 @@ class ShardedSample:
             ring = getattr(self, "_chain_ring", None)
             if ring is None or ring[0] != rk:
                 self._chain_ring = None  # release the old ring first
-                # zeroed once: every bucket head zero; each unpack resets its send buffer's
-                # heads for the next emission (heads_ok[j])
-                sends = [t.zeros((G * Sub * (cap + 1) * W,), dtype=t.int64, device=dev)
+                sends = [t.empty((G * Sub * (cap + 1) * W,), dtype=t.int64, device=dev)
                          for _ in range(nsub)]
-                self._chain_ring = ring = (rk, sends, [t.empty_like(b) for b in sends],
-                                           [True] * nsub)
-            sends, recvs, heads_ok = ring[1], ring[2], ring[3]
+                self._chain_ring = ring = (rk, sends, [t.empty_like(b) for b in sends])
+            sends, recvs = ring[1], ring[2]
             if getattr(self, "_chain_flag", None) is None:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
         else:
@@ -1000,19 +975,13 @@ class ShardedSample:
                         self._emit_stream = t.cuda.Stream()
                     es = self._emit_stream
                     es.wait_stream(t.cuda.current_stream())
-                # one stream: the emission zeroes the unpack's cursors (no memset launch;
-                # with sub-chunks an emission would run beside the previous unpack)
-                fuse = es is None and hasattr(ops, "unpack_cursors")
                 xchg = []
                 with (t.cuda.stream(es) if es is not None else contextlib.nullcontext()):
                     for j, a in enumerate(range(0, c, Sub)):
                         cs = min(Sub, c - a)
                         ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0 and a == 0, r, G,
                                        kxs[i0 + a:i0 + a + cs], kzs[i0 + a:i0 + a + cs], kx, kz,
-                                       N, send=sends[j], cap=cap, flag=self._chain_flag,
-                                       zero=ops.unpack_cursors(cs, N, dev) if fuse else None,
-                                       heads_zero=heads_ok[j])
-                        heads_ok[j] = False  # until this sub-chunk's unpack resets them
+                                       N, send=sends[j], cap=cap, flag=self._chain_flag)
                         sz = G * cs * (cap + 1) * W
                         xchg.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
                                                                 async_op=True)))
@@ -1020,15 +989,12 @@ class ShardedSample:
                     if work is not None:
                         work.wait()
                     ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
-                                     z_bag[a:a + cs], self._chain_flag, kx, kz, N,
-                                     cursors_zero=fuse,
-                                     zero_out=zero_out(i0 + a, i0 + a + cs), send_reset=sends[j])
-                    heads_ok[j] = True
+                                     z_bag[a:a + cs], self._chain_flag, kx, kz, N)
                     count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs])
                 continue
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
-                           cursors=cursors, zero=zero_out(i0, i0 + c))
+                           cursors=cursors)
             count(x_bag, z_bag, c, counts[i0:i0 + c])
         carry = None
         if coll:
