@@ -38,9 +38,12 @@ Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
 M64 = 2 ** 64 - 1
 
 
-def ev_time(fn, reps):
+def ev_time(fn, reps, warm=3):
+    # (warm: a sample's first calls allocate; one warm call left the one-GPU product call
+    # ~0.1 ms above its steady 1.89 ms at K = 4, profiles/r05s43_sync_probe.log)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
+    for _ in range(warm):
+        fn()
     torch.cuda.synchronize()
     e0.record()
     t0 = time.perf_counter()
@@ -61,7 +64,7 @@ def one_gpu_call(K, chain, carry):
         base[0] += K
         S.UnN_many(range(base[0], base[0] + K))
     try:
-        return ev_time(call, 5)
+        return ev_time(call, 10)
     finally:
         D.CHAIN_STEPS = True
         D.CARRY_IMAGES = True
@@ -169,7 +172,7 @@ def rank_call(G, r, K, parts=False, carried=False):
                  lambda: full[:-1].view(K, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
     ms, host = ev_time(call, 5)
     if parts:
-        t = {k: sum(a.elapsed_time(b) for a, b in v) / 6 for k, v in t.items()}
+        t = {k: sum(a.elapsed_time(b) for a, b in v) / 8 for k, v in t.items()}
     return ms, host, t
 
 
