@@ -3,9 +3,10 @@ bench.py's live `roofline.frac`): from a rocprofv3 --kernel-trace CSV of `bench.
 the strict k_count_chain launches of the largest grid (the K-step chunks of the headline's
 UnN_many calls; the strong_C3 and half-ties lines launch smaller grids or the HALF kernel),
 their mean and minimum duration, and the lane-op fraction they imply; in time order the first
-is the bench's untimed warm-up call (a cold chip: its clock is still rising) and the LAST the
+is the bench's untimed warm-up call (a cold chip: its clock is still rising), the SECOND the
 timed call whose HIP-event duration gives the live `frac` — `timed_ms` / `frac_timed` is that
-same launch as the tracer saw it.
+same launch as the tracer saw it — and (round 5, late) a third the `first_call_ranking` line's
+call of the same steps.
     python3 tools/traced_chain.py TRACE.csv K OUT.json"""
 import csv
 import json
@@ -26,7 +27,8 @@ res = {"kernel": rows[0]["Kernel_Name"].split("(")[0], "grid": g, "launches": le
        "steps_per_launch": K, "mean_ms": mean, "min_ms": lo,
        "frac_mean": K * PAIRS_PER_STEP / (mean * 1e-3) / PEAK,
        "frac_min": K * PAIRS_PER_STEP / (lo * 1e-3) / PEAK, "launch_ms_in_order": ds,
-       "timed_ms": ds[-1], "frac_timed": K * PAIRS_PER_STEP / (ds[-1] * 1e-3) / PEAK,
+       "timed_ms": ds[min(1, len(ds) - 1)],
+       "frac_timed": K * PAIRS_PER_STEP / (ds[min(1, len(ds) - 1)] * 1e-3) / PEAK,
        "source": path}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
