@@ -543,6 +543,7 @@ class ShardedSample:
         self.dist.all_reduce(flat, group=self.group)
         self._flag_all = flat[-1:]
         self._carry_all = None if carried is None else flat[-2:-1]
+        self._flag_tail = flat[-2:]
         return flat[:T * G * N].view(T, G * N)
 
     def check_exchange(self):
@@ -550,7 +551,13 @@ class ShardedSample:
         sticky: records past a bucket's capacity were dropped, so the arrays stay invalid for
         every later step of this sample (a later repartition only permutes them).  Over ranks
         the flag read is the ranks' sum from the last counts all-reduce, so every rank raises."""
-        if self._flag_all is not None and int(self._flag_all.item()):
+        carry_sum = None
+        if self._carry_all is not None:  # both extra elements of the reduction in one read
+            carry_sum, flag_sum = (int(v) for v in self._flag_tail.cpu().tolist())
+            if flag_sum:
+                raise RuntimeError("repartition: an exchange bucket on some rank overflowed "
+                                   "its capacity; the counts and arrays are invalid")
+        elif self._flag_all is not None and int(self._flag_all.item()):
             raise RuntimeError("repartition: an exchange bucket on some rank overflowed its "
                                "capacity; the counts and arrays are invalid")
         if self._xf is not None and int(self._xf["flag"].item()):
@@ -559,7 +566,7 @@ class ShardedSample:
         if getattr(self, "_chain_flag", None) is not None and int(self._chain_flag.item()):
             raise RuntimeError("UnN_many: a step-chain bucket overflowed its capacity; the "
                                "counts and arrays are invalid")
-        if self._carry_all is not None and int(self._carry_all.item()) not in (0, self.G):
+        if carry_sum is not None and carry_sum not in (0, self.G):
             raise RuntimeError("UnN_many: the ranks disagree on the carried rank images (a "
                                "rank's sample was changed on that rank alone); the counts are "
                                "invalid")
@@ -597,6 +604,7 @@ class ShardedSample:
                 f = f.reshape(1).clone()
                 self.dist.all_reduce(f, group=self.group)
                 self._flag_all = f
+                self._carry_all = None  # (this reduction carries no carried-images bit)
             self.check_exchange()
 
     def _repartition(self, key: int):
