@@ -565,8 +565,13 @@ static int g_chain_R = 0;  // tuning hooks (tw_count_chain_set_plan); 0 = automa
 static int64_t g_chain_zchunk = 0;
 
 // strict: R in {16, 8} x-images per lane, least padded slots (ties to 16); half: R = 8 {g, h}
-// pairs (the same 8 packed registers per lane); z chunks of ~1024 images, shorter when the
-// bags are too few to give 16 items per SIMD
+// pairs (the same 8 packed registers per lane).  z chunks: as many as give ~150 work items per
+// SIMD (kChainItems), each of >= 512 images — long items amortise a wave's x loads and
+// epilogue, enough of them keep the tail short.  Round 5 (tools/count_plan_ab.py, profiles/
+// r05s49_count_plan_ab.log, interleaved A/B): against round 4's fixed 1024-image chunks the
+// headline K = 20 launch 8.54 -> 8.31 ms, K = 32 13.68 -> 13.34, half ties 17.02 -> 16.54,
+// every per-rank shape of the strong problem 0.3-2.4 % faster, C2 within 1 %
+constexpr int64_t kChainItems = 256 * 4 * 150;
 static ChainPlan plan_chain(int64_t max_nx, int64_t max_nz, int64_t n_bags, bool half) {
   ChainPlan p{half ? 8 : 16, 1, 1, max_nz, 0};
   if (!half) {
@@ -581,11 +586,11 @@ static ChainPlan plan_chain(int64_t max_nx, int64_t max_nz, int64_t n_bags, bool
     }
   }
   p.tiles_x = (int)ceil_div(max_nx, (int64_t)kWave * p.R);
-  int64_t zc = g_chain_zchunk > 0 ? g_chain_zchunk : 1024;
   const int64_t base = (int64_t)p.tiles_x * n_bags;
-  const int64_t target = 256 * 16 * (kBlock / kWave);
-  if (g_chain_zchunk <= 0 && base * ceil_div(max_nz, zc) < target)
-    zc = std::max<int64_t>(256, ceil_div(max_nz, std::max<int64_t>(1, target / base)));
+  int64_t zc = g_chain_zchunk;
+  if (zc <= 0)
+    zc = std::max<int64_t>(
+        512, ceil_div(max_nz, std::max<int64_t>(1, ceil_div(kChainItems, std::max<int64_t>(1, base)))));
   zc = std::min<int64_t>(zc, (int64_t)1 << 24);  // f32 lane counters stay exact
   p.z_chunk = ceil_div(std::min<int64_t>(zc, max_nz), 8) * 8;
   p.zchunks = (int)ceil_div(max_nz, p.z_chunk);
