@@ -941,10 +941,10 @@ class ShardedSample:
             else:
                 ops.count_chain(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
                                 self.max_nx, self.max_nz, half, out)
-        x_bag = t.empty((C, n), dtype=t.int64 if half else t.float32, device=dev)
-        z_bag = t.empty((C, m), dtype=t.float32, device=dev)
-        xpos = t.empty((n,), dtype=t.int32, device=dev)
-        zpos = t.empty((m,), dtype=t.int32, device=dev)
+        x_bag = self._work("x_bag", (C, n), t.int64 if half else t.float32)
+        z_bag = self._work("z_bag", (C, m), t.float32)
+        xpos = self._work("xpos", (n,), t.int32)
+        zpos = self._work("zpos", (m,), t.int32)
         counts = t.empty((T, N), dtype=t.int64, device=dev)
         if coll:
             # one all-to-all per chunk (CHAIN_SUB = 0), or the chunk's steps in sub-chunks of
@@ -969,7 +969,7 @@ class ShardedSample:
             if getattr(self, "_chain_flag", None) is None:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
         else:
-            cursors = t.empty((C * 2 * (N + 1),), dtype=t.int32, device=dev)
+            cursors = self._work("cursors", (C * 2 * (N + 1),), t.int32)
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             if coll:
@@ -1027,6 +1027,24 @@ class ShardedSample:
             self._carry = (self._X, self._Z, self._X._version, self._Z._version, half,
                            carry[0], carry[1])
         return [np.mean(v) for v in self.values(counts)]
+
+    def _work(self, name, shape, dtype):
+        """A work tensor of `shape` kept on the sample across calls (one flat buffer per name,
+        grown when a call needs more): the chains' bags, positions and cursors.  Every call
+        ends with the counts read back (values()), so the next call finds them free.  Fresh
+        per-call bags (80 MB each at K = 20) beside the smaller cached blocks of shorter calls
+        made the caching allocator map new memory inside a call: the bench's K = 20 call ran
+        0.2-0.3 ms longer than the same call after another K = 20 call (profiles/r05s50_*)."""
+        ws = self.__dict__.setdefault("_ws", {})
+        numel = 1
+        for d in shape:
+            numel *= int(d)
+        buf = ws.get(name)
+        if (buf is None or buf.numel() < numel or buf.dtype != dtype
+                or buf.device != self.X.device):
+            ws[name] = None  # release the old buffer first
+            buf = ws[name] = self.t.empty((max(numel, 1),), dtype=dtype, device=self.X.device)
+        return buf[:numel].view(shape)
 
     def _all_to_all(self, out, inp, async_op=False):
         """Equal-split all-to-all of one flat tensor (RCCL all_to_all_single; gloo on CPU);
