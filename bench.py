@@ -1107,6 +1107,13 @@ def main():
         if not go:
             break
     S.UnN_many(range(args.warmup))
+    # the process's objects so far (torch's import, the sample, the pools) into the cyclic
+    # collector's permanent generation: its passes inside a timed call then scan only the
+    # call's own young objects (a 2e6-object heap cost a K = 20 call ~0.15 ms of host time,
+    # tools/headline_call_probe.py, profiles/r05s55_headline_call.log)
+    import gc
+    gc.collect()
+    gc.freeze()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
