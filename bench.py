@@ -1096,6 +1096,15 @@ def main():
     # one untimed run at the timed run's length first: the first K-step UnN_many of a process
     # ran ~7 % slower than the later ones at K = 100 (tools/bench_bisect.py)
     S.UnN_many(range(40_000, 40_000 + args.steps))
+    # the process's objects so far (torch's import, the sample, the pools) into the cyclic
+    # collector's permanent generation: its passes inside a timed call then scan only the
+    # call's own young objects (a 2e6-object heap cost a K = 20 call ~0.15 ms of host time,
+    # tools/headline_call_probe.py, profiles/r05s55_headline_call.log).  Before the settle
+    # steps: a collection right before the timed call idled the GPU long enough for its clock
+    # to drop (the count launch ran at 0.78 of peak instead of 0.95, profiles/r05s57_*)
+    import gc
+    gc.collect()
+    gc.freeze()
     t_s = time.perf_counter()
     while True:
         S.UnN_many(range(20_000, 20_005))
@@ -1107,13 +1116,6 @@ def main():
         if not go:
             break
     S.UnN_many(range(args.warmup))
-    # the process's objects so far (torch's import, the sample, the pools) into the cyclic
-    # collector's permanent generation: its passes inside a timed call then scan only the
-    # call's own young objects (a 2e6-object heap cost a K = 20 call ~0.15 ms of host time,
-    # tools/headline_call_probe.py, profiles/r05s55_headline_call.log)
-    import gc
-    gc.collect()
-    gc.freeze()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
