@@ -21,7 +21,7 @@ ops = HipOps()
 xr, zr = ops.rank_images_query(Z, X, Z, L.TW_F64, compact=True)
 xo = torch.tensor([0, n], dtype=torch.int64, device="cuda")
 out = torch.zeros((1, 1), dtype=torch.int64, device="cuda")
-plans = [(0, 0), (16, 600), (16, 1056), (16, 1600), (16, 2048), (8, 1056), (8, 2048)]
+plans = [(0, 0), (16, 600), (16, 256), (16, 384), (8, 256), (8, 512), (8, 1056), (16, 128)]
 res, ref = {p: [] for p in plans}, None
 for rep in range(5):
     for p in plans:

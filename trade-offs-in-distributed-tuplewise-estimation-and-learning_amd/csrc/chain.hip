@@ -566,12 +566,15 @@ static int64_t g_chain_zchunk = 0;
 
 // strict: R in {16, 8} x-images per lane, least padded slots (ties to 16); half: R = 8 {g, h}
 // pairs (the same 8 packed registers per lane).  z chunks: as many as give ~150 work items per
-// SIMD (kChainItems), each of >= 512 images — long items amortise a wave's x loads and
+// SIMD (kChainItems), each of >= 600 images — long items amortise a wave's x loads and
 // epilogue, enough of them keep the tail short.  Round 5 (tools/count_plan_ab.py, profiles/
 // r05s49_count_plan_ab.log, interleaved A/B): against round 4's fixed 1024-image chunks the
 // headline K = 20 launch 8.54 -> 8.31 ms, K = 32 13.68 -> 13.34, half ties 17.02 -> 16.54,
 // every per-rank shape of the strong problem 0.3-2.4 % faster, C2 within 1 %
 constexpr int64_t kChainItems = 256 * 4 * 150;
+// (C2's single 1e5 x 1e5 bag: 600-image chunks 276.9 us, 512 282.3 us, profiles/
+// r05s59_c2_plan.log; the large shapes are indifferent between 512 and 1024)
+constexpr int64_t kChainMinZ = 600;
 static ChainPlan plan_chain(int64_t max_nx, int64_t max_nz, int64_t n_bags, bool half) {
   ChainPlan p{half ? 8 : 16, 1, 1, max_nz, 0};
   if (!half) {
@@ -590,7 +593,8 @@ static ChainPlan plan_chain(int64_t max_nx, int64_t max_nz, int64_t n_bags, bool
   int64_t zc = g_chain_zchunk;
   if (zc <= 0)
     zc = std::max<int64_t>(
-        512, ceil_div(max_nz, std::max<int64_t>(1, ceil_div(kChainItems, std::max<int64_t>(1, base)))));
+        kChainMinZ,
+        ceil_div(max_nz, std::max<int64_t>(1, ceil_div(kChainItems, std::max<int64_t>(1, base)))));
   zc = std::min<int64_t>(zc, (int64_t)1 << 24);  // f32 lane counters stay exact
   p.z_chunk = ceil_div(std::min<int64_t>(zc, max_nz), 8) * 8;
   p.zchunks = (int)ceil_div(max_nz, p.z_chunk);
