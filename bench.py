@@ -872,7 +872,9 @@ def strong_c3(args, group, rank, world, barrier, torch, dist):
     reps = max(1, args.steps // T)
 
     def timed(fn):
-        fn(90_000)  # warm: same shapes, other keys
+        for w in range(3):  # warm: same shapes, other keys (a sample's first calls rank and
+            # allocate; est.UnNT is called in a loop, main.py:76-79 / 110-116)
+            fn(90_000 + 1000 * w)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
