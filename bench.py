@@ -873,7 +873,8 @@ def strong_c3(args, group, rank, world, barrier, torch, dist):
 
     def timed(fn):
         for w in range(3):  # warm: same shapes, other keys (a sample's first calls rank and
-            # allocate; est.UnNT is called in a loop, main.py:76-79 / 110-116)
+            # allocate; the reference calls est.UnNT in a loop, main.py:110-111 — on fresh
+            # samples there: the first-call cost is `first_call_ranking` beside the headline)
             fn(90_000 + 1000 * w)
         torch.cuda.synchronize()
         barrier()
