@@ -701,7 +701,9 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
   // (profiles/r04_chain_parts.log: 2e6 elements, 20 steps: EPR 8 / 1 step per round 257 us,
   // 8 / 2 296 us; 250k elements: 2 / 8 57 us, 2 / 1 79 us, 8 / 1 139 us)
   const int64_t elems = n_x + n_z;
-  const int epr = g_emit_epr ? g_emit_epr : elems >= 1500000 ? 8 : elems >= 600000 ? 4 : 2;
+  // (round 5, profiles/r05s46_emit_sweep_ranks.log: a G = 4 rank's 500k elements, 4 per
+  // thread and 4 steps per round: 30 against 36 us at K = 4, 92 against 100 at K = 20)
+  const int epr = g_emit_epr ? g_emit_epr : elems >= 1500000 ? 8 : elems >= 400000 ? 4 : 2;
   int spr = g_emit_s ? g_emit_s : epr == 8 ? 1 : 16 / epr;
   while (spr > 1 && spr * NB > kEmMaxB) spr >>= 1;
   if (NB > kEmMaxB) {
