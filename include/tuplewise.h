@@ -758,8 +758,8 @@ int tw_comm_set_prior_timeout(int64_t ms);
  * and the update launches (the shard mean of make_exps.py:126-141 / compute_stats.py:44-46,
  * split over ranks) by GPU-to-GPU stores into one peer buffer per rank, IPC-mapped into the
  * others.  tw_peer_buffer_bytes: the buffer size for n_total shards of d columns (-1: bad
- * sizes).  tw_peer_alloc: a zeroed device buffer, uncached where the driver allows
- * (*out_uncached = 1), else plain.  tw_peer_handle / tw_peer_open / tw_peer_close: the 64-byte
+ * sizes).  tw_peer_alloc: a zeroed UNCACHED device buffer (*out_uncached = 1); fails with
+ * TW_ERR_HIP when the driver cannot give uncached memory (no cached fallback: stale lines).  tw_peer_handle / tw_peer_open / tw_peer_close: the 64-byte
  * IPC handle of a buffer, mapped into another process (hipIpcMemLazyEnablePeerAccess).
  * d_peer_bases below: G device addresses in rank order (this rank's own buffer at `rank`). */
 int64_t tw_peer_buffer_bytes(int32_t n_total, int64_t d);

@@ -23,3 +23,16 @@ def shuttle_problem(seed: int = 20260):
     mon = list(zip(rng.randint(0, N_X, MONITOR_PAIRS).tolist(),
                    rng.randint(0, N_Z, MONITOR_PAIRS).tolist()))
     return X, Z, tX, tZ, w0, mon
+
+
+def large_inputs(spec: dict):
+    """Inputs of the large-n goldens (make_golden_large.py, tests/test_gpu_large_golden.py):
+    `RandomState(data_seed).normal(loc_x, 1, n)` then `.normal(0, 1, m)`, rounded to
+    `round` decimals when the case names it (tie-heavy scores).  Regenerated on the GPU box,
+    so golden_large.json holds only seeds, values and hashes."""
+    rng = np.random.RandomState(spec["data_seed"])
+    X = rng.normal(spec["loc_x"], 1, spec["n"])
+    Z = rng.normal(0.0, 1, spec["m"])
+    if spec.get("round") is not None:
+        X, Z = X.round(spec["round"]), Z.round(spec["round"])
+    return X, Z

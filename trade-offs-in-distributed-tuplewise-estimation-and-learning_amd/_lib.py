@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import pathlib
+import sys
 
 import numpy as np
 
@@ -225,6 +226,14 @@ _RESTYPES = {
 _lib = None
 
 
+class _NoTensor:  # stands in for torch.Tensor until lib() has imported torch
+    pass
+
+
+_TENSOR = _NoTensor  # torch.Tensor once lib() has run: call() converts such arguments
+_getrefcount = sys.getrefcount
+
+
 class TuplewiseError(RuntimeError):
     """A HIP runtime failure inside libtuplewise.so."""
 
@@ -237,7 +246,9 @@ def lib() -> ctypes.CDLL:
         # libtuplewise.so's NEEDED libamdhip64.so.7 must bind to that copy.  Loading our
         # library first would pull /opt/rocm's runtime in beside torch's (two HSA runtimes,
         # one of which then sees no device), so torch is imported before the dlopen.
-        import torch as _torch  # noqa: F401
+        import torch as _torch
+        global _TENSOR
+        _TENSOR = _torch.Tensor
         if not LIB_PATH.exists():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g;"
@@ -266,7 +277,18 @@ def check(rc: int) -> None:
 
 
 def call(name: str, *args) -> None:
-    check(getattr(lib(), name)(*args))
+    """Run one C-ABI entry point.  A torch tensor may be passed in place of its `ptr()`: it is
+    converted here and, being an element of `args`, stays referenced until the entry point has
+    returned (and, since every launch is stream-ordered after the caller's allocations, until
+    the caching allocator can no longer hand its block to a later temporary of the same
+    argument list — the round-5 aperture violation's class, learning.py:443-475)."""
+    fn = getattr(lib(), name)
+    T = _TENSOR
+    for a in args:
+        if isinstance(a, T):
+            args = tuple(ctypes.c_void_p(a.data_ptr()) if isinstance(a, T) else a for a in args)
+            break
+    check(fn(*args))
 
 
 # ----------------------------------------------------------------------------- device memory
@@ -301,7 +323,24 @@ def host_device_pointer(t):
 
 
 def ptr(t) -> ctypes.c_void_p:
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    """The device address of a tensor that someone else keeps alive.
+
+    A bare address does not hold its tensor: `ptr(to_device(a))` frees the block as soon as
+    this returns, so a later temporary of the same argument list can be handed the same block
+    (round 5: aliased bucket starts and an aperture violation in k_row_table_remote).  Such an
+    unreferenced temporary is refused here — by its reference count, which for an object only
+    the caller's evaluation stack holds is 3 inside this frame (stack, parameter, getrefcount's
+    argument), and for a view whose base nobody else holds the base's count is 2.  Pass the
+    tensor itself to `call()` instead, or bind it to a name first."""
+    if t is None:
+        return ctypes.c_void_p(0)
+    if _getrefcount(t) <= 3:
+        b = t._base
+        if b is None or _getrefcount(b) <= 3:  # 3 here: b, the view's own ref, the argument
+            raise TuplewiseError(
+                "tuplewise._lib.ptr: an unreferenced temporary tensor; its block would be freed "
+                "before the native call runs — pass the tensor to call() or name it first")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def to_device(arr: np.ndarray, dtype=None):

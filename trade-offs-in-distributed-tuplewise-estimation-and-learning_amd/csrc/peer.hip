@@ -165,12 +165,16 @@ extern "C" int64_t tw_peer_buffer_bytes(int32_t n_total, int64_t d) {
 extern "C" int tw_peer_alloc(int64_t bytes, void** d_out, int32_t* out_uncached) {
   TW_ARG_CHECK(bytes > 0 && d_out != nullptr, "tw_peer_alloc: bytes > 0 and an output");
   void* p = nullptr;
-  int unc = 1;
+  // Uncached or nothing: the hand-off relies on no device cache holding a slot or counter
+  // line (peer.h), and a cached fallback would let an owner read stale gradient rows that the
+  // hello handshake (one remote atomic) cannot detect.  Failing here makes every rank take
+  // the RCCL all-gather together (learning.py _PeerBuffers.create).
   if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();
-    unc = 0;
-    TW_HIP_CHECK(hipMalloc(&p, (size_t)bytes));
+    set_error("tw_peer_alloc: uncached device memory is unavailable; the peer exchange needs it");
+    return TW_ERR_HIP;
   }
+  const int unc = 1;
   if (hipMemset(p, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     (void)hipFree(p);
     set_error("tw_peer_alloc: zeroing the buffer failed");

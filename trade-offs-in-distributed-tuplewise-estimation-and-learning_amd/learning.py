@@ -442,13 +442,13 @@ class SGDEngine:
         rwords, rstart = layout(rc)
         send = self._records("send", int(sum(swords)))
         cursor = L.empty((G,), t.int64)
-        # device copies held in locals until the launches are enqueued: a temporary freed
-        # inside one call's argument list hands its block to the next temporary of the same
-        # list (the round-4 table call read its bucket starts from the prefix array — masked
-        # at G = 2, where both begin 0, 0; found at G = 3)
-        sstart_d = L.to_device(sstart)
+        # the device copies go to call() as tensors, held until the launch is enqueued: a
+        # bare ptr() of a temporary freed it inside the argument list and handed its block to
+        # the next temporary (round 4: the table call read its bucket starts from the prefix
+        # array — masked at G = 2, where both begin 0, 0; found at G = 3).  ptr() now refuses
+        # such a temporary (_lib.py).
         L.call("tw_row_pack_remote", L.ptr(rows), M, M_q, lo, hi, G, self.rank, L.ptr(part), d,
-               L.ptr(sstart_d), L.ptr(counts), L.ptr(cursor), L.ptr(send), s)
+               L.to_device(sstart), L.ptr(counts), L.ptr(cursor), L.ptr(send), s)
         mat = self.X if side == 0 else self.Z
         need = n_own + int(sum(rwords)) // d
         if need > mat.shape[0]:  # more remote rows than the receive area holds: grow it
@@ -463,9 +463,8 @@ class SGDEngine:
                                     input_split_sizes=swords, group=self.group)
         rprefix = np.concatenate([[0], np.cumsum(rc)]).astype(np.int64)
         bad = t.zeros((1,), dtype=t.int64, device=table.device)
-        rstart_d, rprefix_d = L.to_device(rstart), L.to_device(rprefix)
-        L.call("tw_row_table_remote", L.ptr(recv), G, L.ptr(rstart_d), L.ptr(rcounts),
-               L.ptr(rprefix_d), int(rprefix[-1]), d, n_own, L.ptr(table), table.numel(),
+        L.call("tw_row_table_remote", L.ptr(recv), G, L.to_device(rstart), L.ptr(rcounts),
+               L.to_device(rprefix), int(rprefix[-1]), d, n_own, L.ptr(table), table.numel(),
                recv.numel(), L.ptr(bad), s)
         b = int(bad.item())  # (the exchange already synchronised on its split sizes)
         if b:
@@ -1845,7 +1844,7 @@ class _DeferredEvals:
         # this evaluation covers every segment before it, without a device-wide wait here)
         if self.ctl is not None:
             if int(self.host[k, 4 + self.nw:].numpy().view(np.int64)[0]) != 0:
-                raise RuntimeError("tw_sgd_segment: a grid barrier timed out (blocks not "
+                raise RuntimeError("tw_sgd_segment_narrow: a grid barrier timed out (blocks not "
                                    "co-resident); the SGD state is invalid")
         elif self.check is not None:
             self.check()
