@@ -257,6 +257,21 @@ class OracleOpsChain(OracleOpsRank):
         Zo.numpy()[zpos.numpy().view(np.uint32)] = Z.numpy()
         return Xo, Zo
 
+    def words_checksum(self, A, B, acc, expect=None, verdict=None, good=1, bad=0):
+        """tw_words_checksum (csrc/guard.hip) restated: sum of splitmix64-finalised words
+        xored with position * golden, wrapping."""
+        w = np.concatenate([A.numpy().reshape(-1).view(np.uint64),
+                            B.numpy().reshape(-1).view(np.uint64)])
+        with np.errstate(over="ignore"):
+            z = w ^ (np.arange(w.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+            acc.numpy().view(np.uint64)[0] = z.sum(dtype=np.uint64)
+        if verdict is not None:
+            verdict[0] = good if int(acc[0]) == int(expect[0]) else bad
+        return acc
+
     def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z):
         out = []
         for A, base, cnt, keys in ((X_all, x_base, n, keys_x), (Z_all, z_base, m, keys_z)):
@@ -545,9 +560,14 @@ def _carry_worker(rank, G, port, q, mode):
             if mode == "inplace" and keys[0] == 8:
                 S.Z.mul_(1)  # an in-place change on every rank: the images are recomputed
             if mode == "one_rank" and keys[0] == 8 and rank == 0:
-                S.Z.mul_(1)  # on rank 0 alone: the ranks disagree, every rank raises
+                S.Z.mul_(1)  # on rank 0 alone: the ranks disagree, every rank recounts
+            if mode.startswith("hidden") and keys[0] == 8 and (rank == 0 or mode == "hidden"):
+                # two scores exchanged behind the version counter (.data has its own): the
+                # images still look carried, the checksum verdict makes every rank recount
+                S.X.data[[0, 1]] = S.X.data[[1, 0]].clone()
             out["carried"].append(S._carried(False) is not None)
             out["vals"] += [float(v) for v in S.UnN_many(keys)]
+        out["recounts"] = getattr(S, "stale_recounts", 0)
         Xg = [torch.empty_like(S.X) for _ in range(G)]
         Zg = [torch.empty_like(S.Z) for _ in range(G)]
         dist.all_gather(Xg, S.X)
@@ -560,13 +580,16 @@ def _carry_worker(rank, G, port, q, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("G,mode", [(2, "carry"), (3, "carry"), (2, "inplace"), (3, "one_rank")])
+@pytest.mark.parametrize("G,mode", [(2, "carry"), (3, "carry"), (2, "inplace"), (3, "one_rank"),
+                                    (2, "hidden"), (3, "hidden_one")])
 def test_carried_images_over_ranks(G, mode):
     """device.CARRY_IMAGES over ranks: the second and later UnN_many calls carry every rank's
     records through the inverse chains (all-gathered records, chain_gather) instead of ranking
     again; estimates and final arrays equal the one-process score path call after call.  An
     in-place change of the sample on every rank drops the carried images; on one rank alone the
-    ranks disagree and every rank raises in values()."""
+    ranks disagree and every rank recounts the call from a fresh ranking.  A write behind the
+    version counter (.data) on every rank or on one is caught by the arrays' checksum
+    (tw_words_checksum): every rank recounts, estimates stay exact."""
     import tuplewise  # noqa: F401
     from tuplewise.device import ShardedSample
     ctx = mp.get_context("spawn")
@@ -579,14 +602,22 @@ def test_carried_images_over_ranks(G, mode):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    if mode == "one_rank":
-        assert all("disagree" in got[r].get("raised", "") for r in range(G)), got
-        return
+    assert all("raised" not in got[r] for r in range(G)), got
     out = got[0]
-    assert out["carried"] == [False, True, mode == "carry"]
+    hidden = mode.startswith("hidden")
+    assert out["carried"] == [False, True, mode == "carry" or hidden]  # (rank 0's view)
+    assert all(got[r]["recounts"] == (1 if mode == "one_rank" or hidden else 0)
+               for r in range(G)), got
     X, Z = _global_data(G, 600, 450)
     S1 = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * 3,
                        ops=OracleOps(), algo="pairs")
-    want = [float(S1.UnN(k)) for k in [3, 4, 5, 6, 7, 8, 9, 10, 11]]
+    want = []
+    for k in [3, 4, 5, 6, 7, 8, 9, 10, 11]:
+        if k == 8 and hidden:  # the same exchange in the one-process reference
+            Xh = S1.X.clone()
+            for r in (range(G) if mode == "hidden" else [0]):
+                Xh[[r * 600, r * 600 + 1]] = Xh[[r * 600 + 1, r * 600]].clone()
+            S1.X = Xh
+        want.append(float(S1.UnN(k)))
     assert out["vals"] == want
     assert np.array_equal(out["X"], S1.X.numpy()) and np.array_equal(out["Z"], S1.Z.numpy())

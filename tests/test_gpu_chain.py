@@ -425,3 +425,42 @@ def test_carried_images_equal_fresh_ranking(gpu, tie_mode, algo):
     for (gv, gx, gz), (wv, wx, wz) in zip(got, want):
         assert gv == wv
         assert np.array_equal(gx, wx) and np.array_equal(gz, wz)
+
+
+@pytest.mark.parametrize("write", ["data_swap", "data_value", "dlpack"])
+def test_carried_images_writes_behind_version_counter(gpu, write):
+    """writes the version counter cannot see — through `S.X.data`, or a
+    DLPack alias of S.Z — still look carried to _carried(), but the arrays' checksum
+    (tw_words_checksum, csrc/guard.hip), verified in stream order, sends the call to a recount
+    from a fresh ranking: its estimates and final arrays equal a fresh sample's on the written
+    arrays, and the next call carries again."""
+    import torch
+    import torch.utils.dlpack as tdl
+    from tuplewise.device import ShardedSample
+    gen = torch.Generator(device="cuda").manual_seed(8)
+    n, N = 50_000, 16
+    X = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) + 0.3
+    Z = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+    S = ShardedSample(X.clone(), Z.clone(), N, algo="pairs")
+    S.UnN_many(range(3, 7))
+    v0x, v0z = S.X._version, S.Z._version
+    if write == "data_swap":
+        S.X.data[[0, 1, 2]] = S.X.data[[2, 0, 1]].clone()
+    elif write == "data_value":
+        S.X.data[:1000] += 2.5
+    else:
+        alias = tdl.from_dlpack(tdl.to_dlpack(S.Z))
+        alias[5000:9000] = -alias[5000:9000]
+    assert S.X._version == v0x and S.Z._version == v0z  # nothing the counters saw
+    assert S._carried(False) is not None
+    Xw, Zw = S.X.clone(), S.Z.clone()
+    got = [float(v) for v in S.UnN_many(range(10, 14))]
+    assert getattr(S, "stale_recounts", 0) == 1
+    F = ShardedSample(Xw, Zw, N, algo="pairs")
+    want = [float(v) for v in F.UnN_many(range(10, 14))]
+    assert got == want
+    assert torch.equal(S.X, F.X) and torch.equal(S.Z, F.Z)
+    assert S._carried(False) is not None  # carried again, and valid
+    assert [float(v) for v in S.UnN_many(range(20, 23))] == [
+        float(v) for v in F.UnN_many(range(20, 23))]
+    assert S.stale_recounts == 1

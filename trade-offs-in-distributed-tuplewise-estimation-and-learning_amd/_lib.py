@@ -197,6 +197,7 @@ _SIGNATURES = {
     "tw_copy_words": [_vp, _i64, _vp, _vp],
     "tw_stage_eval": [_vp, _i32, _vp, _i32, _vp, _vp, _vp],
     "tw_host_device_pointer": [_vp, _vp],
+    "tw_words_checksum": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],
     "tw_np_shuffle_draws32_range": [_vp, _vp, _i64, _i64, _i64, _vp],

@@ -21,6 +21,7 @@ that hold those positions, and all steps of a chunk are counted in one launch.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 
 import numpy as np
 
@@ -357,8 +358,29 @@ class HipOps:
                int(out_next.numel()) if out_next is not None else 0, L.stream_handle())
         return out
 
+    def words_checksum(self, A, B, acc, expect=None, verdict=None, good=1, bad=0):
+        """acc (one int64) = the position-keyed hash of [A | B]'s 8-byte words
+        (tw_words_checksum, csrc/guard.hip); with expect / verdict: verdict = good when acc ==
+        expect, else bad, in stream order.  verdict may be pinned host memory (written through
+        its device mapping, read by the host after the stream's next synchronisation)."""
+        vp = None
+        if verdict is not None:
+            vp = (ctypes.c_void_p(L.host_device_pointer(verdict)) if not verdict.is_cuda
+                  else L.ptr(verdict))
+            if vp.value is None:
+                raise L.TuplewiseError("words_checksum: the verdict word is not mapped memory")
+        L.call("tw_words_checksum", L.ptr(A), int(A.numel()), L.ptr(B), int(B.numel()),
+               L.ptr(acc), L.ptr(expect), vp, int(good), int(bad), L.stream_handle())
+        return acc
+
     def to_dev(self, arr):
         return L.to_device(arr)
+
+
+class _StaleImages(RuntimeError):
+    """The carried rank images no longer describe the arrays: a write torch's version counter
+    did not see (through `.data`, a DLPack alias, a foreign kernel).  UnN_many recounts the call
+    from a fresh ranking when it catches this (every rank together over ranks)."""
 
 
 class ShardedSample:
@@ -397,17 +419,37 @@ class ShardedSample:
         self._carry = None
 
     def _carried(self, half):
-        """The records {image, ...} of the current own elements carried from the last chain
-        call, or None: valid while X / Z are the tensors that call left (same objects, same
-        version counters) with the same tie mode."""
+        """(xr, zr, checksum): the records {image, ...} of the current own elements carried
+        from the last chain call and the hash of the arrays they describe, or None.  Valid while
+        X / Z are the tensors that call left (same objects, same version counters) with the same
+        tie mode; a write the version counters miss is caught by the checksum, verified in the
+        stream of the call that reuses them (_unn_many_chain)."""
         c = getattr(self, "_carry", None)
         if not CARRY_IMAGES or c is None:
             return None
-        X, Z, vx, vz, h, xr, zr = c
+        X, Z, vx, vz, h, xr, zr, cs = c
         if (X is self._X and Z is self._Z and X._version == vx and Z._version == vz
                 and h == half):
-            return xr, zr
+            return xr, zr, cs
         return None
+
+    def _checksum(self, expect=None, verdict=None, good=1, bad=0):
+        """A one-word device hash of the current X / Z (None where the ops lack the entry);
+        with expect / verdict, also the verdict word (see HipOps.words_checksum)."""
+        if not hasattr(self.ops, "words_checksum"):
+            return None
+        acc = self.t.empty((1,), dtype=self.t.int64, device=self.X.device)
+        return self.ops.words_checksum(self.X, self.Z, acc, expect, verdict, good, bad)
+
+    def _host_verdict(self):
+        """The pinned (device-mapped) host word the one-process verdict is written into."""
+        v = getattr(self, "_verdict", None)
+        if v is None:
+            t = self.t
+            v = self._verdict = (t.empty((1,), dtype=t.int64, pin_memory=True) if self.X.is_cuda
+                                 else t.empty((1,), dtype=t.int64))
+        v[0] = -1
+        return v
 
     def __init__(self, X, Z, N: int, group=None, tie_mode: str = "strict", ops=None,
                  algo: str = "auto", exchange: str = "fixed", collectives=None):
@@ -527,9 +569,12 @@ class ShardedSample:
         ranks' overflow flags summed in the SAME all-reduce (one extra element): a bucket that
         overflowed on any rank is then seen by every rank in values(), so all ranks raise
         together instead of the two involved ones only.  carried (the step
-        chains): whether this rank used carried images — summed in a second extra element, so a
-        rank whose sample changed alone (its images recomputed while the others carried theirs)
-        makes every rank raise in values()."""
+        chains): whether this rank used carried images (1; or a device verdict word: 1 when its
+        checksum held, G + 1 when the arrays were written behind the version counter) — summed
+        in a second extra element, so a rank whose sample changed alone (its images recomputed,
+        or found stale, while the others carried theirs) makes every rank redo the call: any
+        sum but 0 (nobody carried) or G (everybody carried valid images) raises _StaleImages
+        in values()."""
         t, G, N, r = self.t, self.G, self.N, self.rank
         T = counts.shape[0]
         extra = 1 if carried is None else 2
@@ -538,7 +583,9 @@ class ShardedSample:
         f = self._local_flag()
         if f is not None:
             flat[-1:] = f.reshape(1)
-        if carried:
+        if isinstance(carried, self.t.Tensor):  # the checksum verdict: 1 good, G + 1 stale
+            flat[-2:-1] = carried
+        elif carried:
             flat[-2:-1] = 1
         self.dist.all_reduce(flat, group=self.group)
         self._flag_all = flat[-1:]
@@ -567,9 +614,9 @@ class ShardedSample:
             raise RuntimeError("UnN_many: a step-chain bucket overflowed its capacity; the "
                                "counts and arrays are invalid")
         if carry_sum is not None and carry_sum not in (0, self.G):
-            raise RuntimeError("UnN_many: the ranks disagree on the carried rank images (a "
-                               "rank's sample was changed on that rank alone); the counts are "
-                               "invalid")
+            raise _StaleImages("UnN_many: the ranks disagree on the carried rank images (a "
+                               "rank's sample was changed on that rank alone, or written behind "
+                               "its version counter); the call is recounted")
 
     def _exchange_records(self, send, c):
         """All-to-all of the packed records (split sizes from the (4, G) host counts) and the
@@ -859,6 +906,19 @@ class ShardedSample:
         return [np.mean(v) for v in self.values(counts)]
 
     def _unn_many_chain(self, keys, bucket=False):
+        """_chain_call, recounted once from a fresh ranking when the carried images turn out
+        stale (_StaleImages: the arrays were written where torch's version counters do not
+        see, or over ranks some rank dropped its images): the call's inputs are still the
+        arrays it started from, so the recount gives the call's true estimates and arrays."""
+        X_in, Z_in = self._X, self._Z
+        try:
+            return self._chain_call(keys, bucket, True)
+        except _StaleImages:
+            self._X, self._Z, self._carry = X_in, Z_in, None
+            self.stale_recounts = getattr(self, "stale_recounts", 0) + 1
+            return self._chain_call(keys, bucket, False)
+
+    def _chain_call(self, keys, bucket, use_carry):
         """UnN_many as step chains (csrc/chain.hip; est.UnNT's loop, estimation-experiment/
         main.py:76-79).  One ranking per call: over ranks the Z structure of the all-gathered Z,
         images written for this rank's own elements only.  Then per chunk of <= CHAIN_MAX steps
@@ -876,8 +936,19 @@ class ShardedSample:
         half = self.pred == L.TW_PRED_HALF
         coll = self.coll  # the exchange branch (several ranks, or forced at world size 1)
         works = []  # the asynchronous all-gathers the final arrays wait for
-        rec = self._carried(half)
+        rec = self._carried(half) if use_carry else None
         carried = rec is not None
+        verdict = None
+        if carried:
+            # the hash of the arrays now against the one saved with the images, verified in
+            # stream order: over ranks the verdict rides in the counts' all-reduce, in one
+            # process it lands in a pinned host word read after the counts
+            xr, zr, cs = rec
+            rec = (xr, zr)
+            if cs is not None:
+                verdict = (self.t.empty((1,), dtype=self.t.int64, device=self.X.device) if coll
+                           else self._host_verdict())
+                self._checksum(cs, verdict, 1, self.G + 1 if coll else 0)
         if coll:
             # the ranking needs the whole Z now (unless the images are carried); the whole X
             # only for the final arrays (chain_gather), so its all-gather runs asynchronously
@@ -1018,15 +1089,20 @@ class ShardedSample:
             self.X, self.Z = final[0], final[1]
             if RX is not None:
                 carry = (final[2], final[3])
-            counts = self._reduce_counts(counts, carried=carried)
+            counts = self._reduce_counts(counts, carried=verdict if verdict is not None
+                                         else carried)
         else:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
             if CARRY_IMAGES:
                 carry = ops.chain_scatter(xr, xpos, zr, zpos)
         if carry is not None:  # after the assignments above (they drop the old ones)
             self._carry = (self._X, self._Z, self._X._version, self._Z._version, half,
-                           carry[0], carry[1])
-        return [np.mean(v) for v in self.values(counts)]
+                           carry[0], carry[1], self._checksum())
+        vals = self.values(counts)  # (over ranks: raises _StaleImages on a bad verdict sum)
+        if verdict is not None and not coll and int(verdict[0]) != 1:
+            raise _StaleImages("UnN_many: the sample was written behind its version counter; "
+                               "the carried rank images are stale")
+        return [np.mean(v) for v in vals]
 
     def _work(self, name, shape, dtype):
         """A work tensor of `shape` kept on the sample across calls (one flat buffer per name,
