@@ -882,6 +882,21 @@ int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
  * launch into h_out, pinned host memory of nres + nw + 1 8-byte words. */
 int tw_stage_eval(const void* d_res, int32_t nres, const void* d_w, int32_t nw,
                   const uint32_t* d_ctl, void* h_out, void* stream);
+/* The incomplete statistic on the step chains over ranks (cs.UnNBT, compute_stats.py:119-123,
+ * with device-RNG draws): tw_chain_unpack_exact writes every received record {image, local
+ * position} of a chunk's (source, step) buckets (tw_chain_emit's exchange layout, strict
+ * images) at its exact position of the step's bags [steps][n_x] / [steps][n_z];
+ * tw_count_pairs_chain_rng counts B device-drawn pairs (tw_count_pairs_rng's Philox/Lemire
+ * draws, step c keyed seed + c, shard streams stream_id + s) of every (step, shard) bag on
+ * those images, out [steps][n_shards] (zeroed here). */
+int tw_chain_unpack_exact(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
+                          int64_t n_x, int64_t n_z, void* d_x_bag, void* d_z_bag,
+                          int32_t* d_flag, void* stream);
+int tw_count_pairs_chain_rng(const float* d_x_bag, const int64_t* d_x_off, int64_t x_stride,
+                             const float* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
+                             int32_t n_shards, int32_t steps, int64_t max_nx, int64_t max_nz,
+                             int64_t B, uint64_t seed, uint64_t stream_id, uint64_t* d_out,
+                             void* stream);
 /* The carried rank images' validity check (ShardedSample.UnN_many, device.py CARRY_IMAGES;
  * the arrays only ever permute between calls, estimation-experiment/main.py:43-44): *d_acc =
  * sum over the na + nb 8-byte words of [d_a | d_b] of a position-keyed 64-bit hash.  With

@@ -257,6 +257,36 @@ class OracleOpsChain(OracleOpsRank):
         Zo.numpy()[zpos.numpy().view(np.uint32)] = Z.numpy()
         return Xo, Zo
 
+    def chain_unpack_exact(self, recv, world, steps, cap, n, m, x_bag, z_bag, flag):
+        """tw_chain_unpack_exact restated: every record at its exact position of its bag."""
+        buf = recv.numpy().view(np.uint64)
+        for b in range(world * steps):
+            c = b % steps
+            b0 = b * (cap + 1)
+            cnt = int(buf[b0] & np.uint64(0xFFFFFFFF))
+            if cnt > cap:
+                flag.numpy()[0] = 1
+            recs = buf[b0 + 1:b0 + 1 + min(cnt, cap)]
+            v = (recs & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            p = (recs >> np.uint64(32)).astype(np.int64)
+            isx = p < n
+            x_bag[c].numpy().view(np.uint32)[p[isx]] = v[isx]
+            z_bag[c].numpy().view(np.uint32)[p[~isx] - n] = v[~isx]
+
+    def count_chain_rng(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
+                        z_stride, max_nx, max_nz, B, seed, shard_base, out):
+        """tw_count_pairs_chain_rng restated: the oracle's device draws (count_rng's) of each
+        (step, shard) bag, compared on the images (x > z <=> g(x) - g(z) >= 1)."""
+        xo, zo = x_off_dev.numpy(), z_off_dev.numpy()
+        for c in range(steps):
+            xb = x_bag[c].numpy().view(np.float32)
+            zb = z_bag[c].numpy().view(np.float32)
+            for s in range(n_shards):
+                a, b = xb[xo[s]:xo[s + 1]], zb[zo[s]:zo[s + 1]]
+                i, j = O.rng_pairs(len(a), len(b), B, (seed + c) % 2 ** 64, shard_base + s)
+                out[c, s] = int((a[i] + b[j] >= 1).sum())
+        return out
+
     def words_checksum(self, A, B, acc, expect=None, verdict=None, good=1, bad=0):
         """tw_words_checksum (csrc/guard.hip) restated: sum of splitmix64-finalised words
         xored with position * golden, wrapping."""
@@ -412,6 +442,63 @@ def test_chain_steps_are_G_invariant(G, tie_mode, sub):
                         ops=OracleOpsChain(), tie_mode=tie_mode, algo="pairs")
     assert [float(v) for v in S1c.UnN_many(keys)] == vals  # the one-process chain
     assert np.array_equal(S1c.X.numpy(), Xg)
+
+
+def _rng_chain_worker(rank, G, port, n_loc, m_loc, N, B, seed, calls, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(G, n_loc, m_loc)
+    S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
+                      torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
+                      group=dist.group.WORLD, ops=OracleOpsChain(), algo="pairs")
+    assert S._chain_rng_ok()
+    vals, carried = [], []
+    for i, keys in enumerate(calls):  # later calls carry the images (device.CARRY_IMAGES)
+        carried.append(S._carried(False) is not None)
+        vals.append([float(v) for v in S.UnNB_many(B, seed + 100 * i, keys)])
+    Xg = [torch.empty_like(S.X) for _ in range(G)]
+    Zg = [torch.empty_like(S.Z) for _ in range(G)]
+    dist.all_gather(Xg, S.X)
+    dist.all_gather(Zg, S.Z)
+    if rank == 0:
+        q.put((vals, carried, torch.cat(Xg).numpy(), torch.cat(Zg).numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_incomplete_chain_steps_are_G_invariant(G):
+    """UnNB_many over ranks on the step chains (cs.UnNBT's loop,
+    compute_stats.py:119-123): one exchange per chunk, records unpacked at their EXACT
+    positions (tw_chain_unpack_exact, restated), B device-drawn pairs per (step, shard) bag
+    counted on the rank images (tw_count_pairs_chain_rng, restated).  Estimates equal the
+    one-process score path's UnNB(B, seed + t, key_t), key by key, including a second call that
+    carries the images; the ranks' final arrays equal the global permutation chain."""
+    import tuplewise  # noqa: F401
+    from tuplewise.device import ShardedSample
+    n_loc, m_loc, N, B, seed = 600, 450, 3, 700, 0xC3C3_0042
+    calls = [[5, 6, 9, 11], [2, 7]] if G != 8 else [[5, 6, 9], [2]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rng_chain_worker,
+                         args=(r, G, port, n_loc, m_loc, N, B, seed, calls, q))
+             for r in range(G)]
+    for p in procs:
+        p.start()
+    vals, carried, Xg, Zg = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert carried == [False, True]
+    X, Z = _global_data(G, n_loc, m_loc)
+    S1 = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), G * N,
+                       ops=OracleOps(), algo="pairs")
+    want = [[float(S1.UnNB(B, seed + 100 * i + t, k)) for t, k in enumerate(keys)]
+            for i, keys in enumerate(calls)]
+    assert vals == want
+    assert np.array_equal(Xg, S1.X.numpy()) and np.array_equal(Zg, S1.Z.numpy())
 
 
 def _overflow_worker(rank, G, port, q):

@@ -84,8 +84,13 @@ def _worker(port, q):
                         torch.randint(0, 480, (n,), device="cuda", generator=gen))}
         cases = [("f64", "strict", "fixed"), ("f64", "half", "fixed"), ("i64", "half", "fixed"),
                  ("f64", "strict", "exact")]
+        import tuplewise.device as D
         for dt, tie, exch in cases:
             X, Z = data[dt]
+            # UnNB_many over ranks: the step chains with exact-position bags (device.CHAIN_RNG,
+            # tw_chain_unpack_exact + tw_count_pairs_chain_rng); the "exact" case keeps the
+            # per-step exchange of _run_steps
+            D.CHAIN_RNG = exch != "exact"
             plain = ShardedSample(X.clone(), Z.clone(), 8, tie_mode=tie, algo="pairs")
             forced = ShardedSample(X.clone(), Z.clone(), 8, group=g, tie_mode=tie, algo="pairs",
                                    exchange=exch, collectives=True)
@@ -98,7 +103,23 @@ def _worker(port, q):
                 out["mismatch"].append((tag, "estimates"))
             if not (np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])):
                 out["mismatch"].append((tag, "final arrays"))
-        import tuplewise.device as D
+        D.CHAIN_RNG = True
+        # configs[2]'s incomplete leg at its size on the chains: n = 1e6 per class, N = 64,
+        # B = 1e6 pairs per shard, T = 4, two calls (the second carries the images)
+        Xc = torch.randn(1_000_000, dtype=torch.float64, device="cuda", generator=gen) + 0.5
+        Zc = torch.randn(1_000_000, dtype=torch.float64, device="cuda", generator=gen)
+        plain = ShardedSample(Xc.clone(), Zc.clone(), 64, algo="pairs")
+        forced = ShardedSample(Xc.clone(), Zc.clone(), 64, group=g, algo="pairs",
+                               collectives=True)
+        assert forced._chain_rng_ok()
+        for i, keys in enumerate(([31, 32, 33, 34], [35, 36, 37, 38])):
+            a = plain.UnNB_many(1_000_000, 0xC3C3 + 10 * i, keys)
+            b = forced.UnNB_many(1_000_000, 0xC3C3 + 10 * i, keys)
+            if a != b:
+                out["mismatch"].append((f"C3 incomplete chains call {i}", (a, b)))
+        if not (torch.equal(plain.X, forced.X) and torch.equal(plain.Z, forced.Z)):
+            out["mismatch"].append(("C3 incomplete chains", "final arrays"))
+        out["ran"].append("C3/incomplete/chains")
         X, Z = data["f64"]  # the chunks' sub-chunks (CHAIN_SUB > 0: emissions on a side stream)
         a = _estimates(ShardedSample(X.clone(), Z.clone(), 8, algo="pairs"), False)
         D.CHAIN_SUB = 5
@@ -154,5 +175,5 @@ def test_rccl_world_size_one_equals_one_process(gpu):
     pr.join(timeout=120)
     assert status == "ok", out
     assert pr.exitcode == 0
-    assert len(out["ran"]) == 13, out["ran"]
+    assert len(out["ran"]) == 14, out["ran"]
     assert out["mismatch"] == [], out["mismatch"]

@@ -197,6 +197,9 @@ _SIGNATURES = {
     "tw_copy_words": [_vp, _i64, _vp, _vp],
     "tw_stage_eval": [_vp, _i32, _vp, _i32, _vp, _vp, _vp],
     "tw_host_device_pointer": [_vp, _vp],
+    "tw_chain_unpack_exact": [_vp, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "tw_count_pairs_chain_rng": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i64,
+                                 _u64, _u64, _vp, _vp],
     "tw_words_checksum": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],

@@ -757,6 +757,48 @@ extern "C" int tw_chain_unpack(const uint64_t* d_recv, int32_t world, int32_t st
   return TW_OK;
 }
 
+// Receiver side at exact positions (the incomplete statistic over ranks, tw_chain_unpack_exact):
+// a device-RNG draw addresses a POSITION of the step's permuted arrays, so every record {image,
+// local position} lands at bag[c][position] — the step's permuted image arrays themselves, which
+// tw_count_pairs_chain_rng reads.  Strict images only (one 8-B record word).
+__global__ __launch_bounds__(kBlock) void k_chain_unpack_exact(
+    const uint64_t* __restrict__ recv, int world, int steps, int parts, int64_t cap, int64_t nx,
+    int64_t nz, uint32_t* __restrict__ xbag, uint32_t* __restrict__ zbag, int* __restrict__ flag) {
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int c = lb / (world * parts);
+  const int rem = lb - c * world * parts;
+  const int g = rem / parts, part = rem - g * parts;
+  const uint64_t* b = recv + ((int64_t)g * steps + c) * (cap + 1);
+  const int64_t cnt0 = (int64_t)(uint32_t)b[0];
+  if (cnt0 > cap && part == 0 && threadIdx.x == 0) *flag = 1;
+  const int64_t cnt = cnt0 < cap ? cnt0 : cap;
+  for (int64_t i = (int64_t)part * kBlock + threadIdx.x; i < cnt; i += (int64_t)parts * kBlock) {
+    const uint64_t r = __builtin_nontemporal_load(b + 1 + i);
+    const int64_t p = (int64_t)(r >> 32);
+    const uint32_t v = (uint32_t)r;
+    if (p < nx)
+      xbag[(int64_t)c * nx + p] = v;
+    else if (p < nx + nz)
+      zbag[(int64_t)c * nz + (p - nx)] = v;
+  }
+}
+
+extern "C" int tw_chain_unpack_exact(const uint64_t* d_recv, int32_t world, int32_t steps,
+                                     int64_t cap, int64_t n_x, int64_t n_z, void* d_x_bag,
+                                     void* d_z_bag, int32_t* d_flag, void* stream) {
+  TW_ARG_CHECK(world >= 1 && steps >= 0 && steps <= kChainMax && cap >= 1 && n_x >= 0 &&
+                   n_z >= 0 && (int64_t)world * steps < 65536 && n_x + n_z < (1ll << 32),
+               "tw_chain_unpack_exact: bad sizes");
+  if (steps == 0 || n_x + n_z == 0) return TW_OK;
+  TW_ARG_CHECK(d_recv && d_x_bag && d_z_bag && d_flag, "tw_chain_unpack_exact: buffers");
+  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(cap, (int64_t)kBlock * 4), 64));
+  hipLaunchKernelGGL(k_chain_unpack_exact, dim3((unsigned)(parts * world * steps)), dim3(kBlock),
+                     0, (hipStream_t)stream, d_recv, (int)world, (int)steps, parts, cap, n_x, n_z,
+                     (uint32_t*)d_x_bag, (uint32_t*)d_z_bag, d_flag);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
 extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
                                     int64_t x_stride, const void* d_z_bag,
                                     const int64_t* d_z_off, int64_t z_stride, int32_t n_shards,

@@ -386,6 +386,71 @@ __global__ __launch_bounds__(kImgThreads) void k_count_rng_img(
   }
 }
 
+// Device RNG on the step chains' bags (tw_count_pairs_chain_rng; cs.UnNBT over ranks,
+// compute_stats.py:119-123): the chunk's (step, shard) bags hold, at the exact positions of the
+// step's permuted arrays, integer rank images — x: g(x) = #{z : z < x}, z: -g(z) (csrc/pkcount.h)
+// — so x > z <=> g(x) + (-g(z)) >= 1 decides every pair, ties included, with no score gathers.
+// The draws are k_count_rng_img's (Philox block q -> pairs 2q and 2q+1 of shard `sid + s`, key
+// seed + c for step c, lemire4): the same pair indices, hence the same integers as the score
+// path's count of the same permuted arrays.  Grid: steps x shards x parts blocks, logical
+// order step-major (one step's bags meet in one XCD's L2).
+template <int QU>
+__global__ __launch_bounds__(kImgThreads) void k_count_rng_chain(
+    const float* __restrict__ xbag, const int64_t* __restrict__ x_off, int64_t x_stride,
+    const float* __restrict__ zbag, const int64_t* __restrict__ z_off, int64_t z_stride,
+    int n_shards, int64_t B, int parts, uint64_t seed, uint32_t sid,
+    unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float img[];
+  const int lb = xcd_block(blockIdx.x, gridDim.x);
+  const int v = lb / parts;
+  const int part = lb - v * parts;
+  const int c = v / n_shards, s = v - c * n_shards;
+  const int64_t xb = x_off[s], zb = z_off[s];
+  const int64_t nx = x_off[s + 1] - xb, nz = z_off[s + 1] - zb;
+  unsigned acc = 0;
+  if (nx > 0 && nz > 0) {
+    float* lx = img;
+    float* lz = img + al4(nx);
+    stage_images<float>(lx, xbag + (int64_t)c * x_stride + xb, nx);
+    stage_images<float>(lz, zbag + (int64_t)c * z_stride + zb, nz);
+    __syncthreads();
+    const uint64_t sd = seed + (uint64_t)c;
+    const uint32_t k0 = (uint32_t)sd, k1 = (uint32_t)(sd >> 32);
+    const uint32_t ss = (uint32_t)s + sid;
+    const int64_t nq = (B + 1) / 2;
+    const int64_t per = (nq + parts - 1) / parts;
+    const int64_t q0 = (int64_t)part * per, q1 = std::min<int64_t>(nq, q0 + per);
+    for (int64_t qb = q0; qb < q1; qb += (int64_t)QU * kImgThreads) {
+      u32x4 r[QU];
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int64_t q = qb + (int64_t)u * kImgThreads + threadIdx.x;
+        r[u] = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32), ss, 0u}, k0, k1);
+      }
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int64_t q = qb + (int64_t)u * kImgThreads + threadIdx.x;
+        const bool live = q < q1;
+        const bool two = live && 2 * q + 1 < B;
+        uint32_t i0, j0, i1, j1;
+        lemire4(r[u], (uint32_t)nx, (uint32_t)nz, q, ss, k0, k1, i0, j0, i1, j1);
+        acc += (live && lx[i0] + lz[j0] >= 1.0f ? 1u : 0u) +
+               (two && lx[i1] + lz[j1] >= 1.0f ? 1u : 0u);
+      }
+    }
+  }
+  unsigned long long tot = wave_sum_u64((unsigned long long)acc);
+  __shared__ unsigned long long part_sum[kImgThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) part_sum[wid] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < kImgThreads / kWave; ++w) b += part_sum[w];
+    if (b) atomicAdd(out + v, b);
+  }
+}
+
 static int g_img_parts = 0;  // tuning: blocks per shard (0 = plan)
 static int g_img_u = 1;      // tuning: index vectors per stream and batch (1, 2, 4)
 static int g_img_nt = 1;     // tuning: nontemporal index loads (default on: streamed once)
@@ -515,6 +580,43 @@ int launch_rng_images(const void* x, const int64_t* x_off, const void* z, const 
 }
 
 }  // namespace tw
+
+extern "C" int tw_count_pairs_chain_rng(const float* d_x_bag, const int64_t* d_x_off,
+                                        int64_t x_stride, const float* d_z_bag,
+                                        const int64_t* d_z_off, int64_t z_stride,
+                                        int32_t n_shards, int32_t steps, int64_t max_nx,
+                                        int64_t max_nz, int64_t B, uint64_t seed,
+                                        uint64_t stream_id, uint64_t* d_out, void* stream) {
+  using namespace tw;
+  TW_ARG_CHECK(n_shards >= 0 && steps >= 0 && B >= 0 && max_nx >= 0 && max_nz >= 0 &&
+                   x_stride >= 0 && z_stride >= 0,
+               "tw_count_pairs_chain_rng: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nbags = (int64_t)n_shards * steps;
+  if (nbags == 0) return TW_OK;
+  TW_ARG_CHECK(d_out != nullptr, "tw_count_pairs_chain_rng: out");
+  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)nbags, st));
+  if (B == 0 || max_nx == 0 || max_nz == 0) return TW_OK;
+  TW_ARG_CHECK(d_x_bag && d_z_bag && d_x_off && d_z_off, "tw_count_pairs_chain_rng: buffers");
+  ImgPlan p = plan_images(n_shards, max_nx, max_nz, TW_PRED_GT, (B + 1) / 2);
+  TW_ARG_CHECK(p.ok, "tw_count_pairs_chain_rng: a shard's images exceed the LDS (%lld + %lld)",
+               (long long)max_nx, (long long)max_nz);
+  // the plan spreads ONE step's shards over the CUs; the chunk's steps multiply the grid
+  TW_ARG_CHECK(nbags * p.parts < (1ll << 31), "tw_count_pairs_chain_rng: grid too large");
+  static bool attr = false;
+  if (!attr) {
+    TW_HIP_CHECK(hipFuncSetAttribute((const void*)k_count_rng_chain<2>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_count_rng_chain<2>, dim3((unsigned)(nbags * p.parts)), dim3(kImgThreads),
+                     p.lds, st, d_x_bag, d_x_off, x_stride, d_z_bag, d_z_off, z_stride,
+                     (int)n_shards, B, p.parts, seed, (uint32_t)stream_id,
+                     (unsigned long long*)d_out);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
 
 extern "C" int tw_count_rng_img_set_unroll(int32_t qu) {
   TW_ARG_CHECK(qu == 1 || qu == 2 || qu == 4, "tw_count_rng_img_set_unroll: 1, 2 or 4");

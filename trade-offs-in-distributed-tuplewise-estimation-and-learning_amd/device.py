@@ -55,6 +55,9 @@ CHAIN_SUB = 0
 # skips the ranking (and over ranks the Z all-gather it waits for).  Any assignment of X / Z or
 # an in-place change (the tensors' version counters) drops them.
 CARRY_IMAGES = True
+# UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
+# exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
+CHAIN_RNG = True
 # one-shot all-pairs counts (local_counts: est.Un / UnN without a repartition loop) on rank
 # images from this many pairs on; below, the double-compare kernel (no ranking to amortise)
 ONESHOT_RANK = True
@@ -240,6 +243,23 @@ class HipOps:
         L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
                int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
                L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
+
+    def chain_unpack_exact(self, recv, world, steps, cap, n, m, x_bag, z_bag, flag):
+        """The received records written at their exact positions of the step bags
+        (tw_chain_unpack_exact): the bags are the steps' permuted image arrays."""
+        L.call("tw_chain_unpack_exact", L.ptr(recv), int(world), int(steps), int(cap), int(n),
+               int(m), L.ptr(x_bag), L.ptr(z_bag), L.ptr(flag), L.stream_handle())
+
+    def count_chain_rng(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
+                        z_stride, max_nx, max_nz, B, seed, shard_base, out):
+        """B device-drawn pairs per (step, shard) bag of exact-position images
+        (tw_count_pairs_chain_rng): step c keyed seed + c, shard streams shard_base + s —
+        the draws of count_rng on the same permuted arrays; out (steps, n_shards)."""
+        L.call("tw_count_pairs_chain_rng", L.ptr(x_bag), L.ptr(x_off_dev), int(x_stride),
+               L.ptr(z_bag), L.ptr(z_off_dev), int(z_stride), int(n_shards), int(steps),
+               int(max_nx), int(max_nz), int(B), int(seed) & (2 ** 64 - 1), int(shard_base),
+               L.ptr(out), L.stream_handle())
+        return out
 
     def _unpack_cursors(self, words, dev):
         # one buffer per HipOps, grown as needed; unpacks on one stream reuse it in order
@@ -866,6 +886,16 @@ class ShardedSample:
                 and G * self.m_loc < (1 << 24) and G * (self.n_loc + self.m_loc) < (1 << 31)
                 and self.N < 8191 and G <= 512)
 
+    def _chain_rng_ok(self) -> bool:
+        """UnNB_many on the step chains (several ranks, or forced collectives): CHAIN_RNG, the
+        step-chain predicates with the strict predicate (one 4-B image per score at its exact
+        position), and a shard's images within a CU's LDS (tw_count_pairs_chain_rng)."""
+        al4 = (self.max_nx + 3) & ~3
+        return (CHAIN_RNG and self._chain_ok() and hasattr(self.ops, "count_chain_rng")
+                and (self.pred == L.TW_PRED_GT
+                     or (self.pred == L.TW_PRED_SUBGT and self.dtype == L.TW_F64))
+                and (al4 + self.max_nz) * 4 <= 160 * 1024 - 1024)
+
     def _unn_many_rank(self, keys):
         """UnN_many on rank images, one launch per step (the A/B baseline of the step chains):
         ONE ranking of X u Z per call (the multiset of scores is the same at every step), then
@@ -905,20 +935,20 @@ class ShardedSample:
             self.Z = self.ops.gather_records(Z0, zr)
         return [np.mean(v) for v in self.values(counts)]
 
-    def _unn_many_chain(self, keys, bucket=False):
+    def _unn_many_chain(self, keys, bucket=False, rng=None):
         """_chain_call, recounted once from a fresh ranking when the carried images turn out
         stale (_StaleImages: the arrays were written where torch's version counters do not
         see, or over ranks some rank dropped its images): the call's inputs are still the
         arrays it started from, so the recount gives the call's true estimates and arrays."""
         X_in, Z_in = self._X, self._Z
         try:
-            return self._chain_call(keys, bucket, True)
+            return self._chain_call(keys, bucket, True, rng)
         except _StaleImages:
             self._X, self._Z, self._carry = X_in, Z_in, None
             self.stale_recounts = getattr(self, "stale_recounts", 0) + 1
-            return self._chain_call(keys, bucket, False)
+            return self._chain_call(keys, bucket, False, rng)
 
-    def _chain_call(self, keys, bucket, use_carry):
+    def _chain_call(self, keys, bucket, use_carry, rng=None):
         """UnN_many as step chains (csrc/chain.hip; est.UnNT's loop, estimation-experiment/
         main.py:76-79).  One ranking per call: over ranks the Z structure of the all-gathered Z,
         images written for this rank's own elements only.  Then per chunk of <= CHAIN_MAX steps
@@ -929,7 +959,12 @@ class ShardedSample:
         positions (one process) or the inverse chains of the rank's own positions gathered from
         the all-gathered sample.  Same permutation chain, counts and final arrays as the
         one-launch-per-step paths, at any G.  bucket: the bags counted exactly in O(n + m) on
-        their integer images (algo="sorted") instead of all pairs — the same integers."""
+        their integer images (algo="sorted") instead of all pairs — the same integers.
+        rng = (B, seed): the incomplete statistic (UnNB_many over ranks, cs.UnNBT's loop,
+        compute_stats.py:119-123): the received records are written at their EXACT positions
+        (tw_chain_unpack_exact) — the device draws address positions — and B pairs per bag are
+        drawn and counted on the images (tw_count_pairs_chain_rng, step t keyed seed + t), the
+        integers of count_rng on the same permuted arrays."""
         t, ops, G, r = self.t, self.ops, self.G, self.rank
         n, m, N = self.n_loc, self.m_loc, self.N
         dev = self.X.device
@@ -1005,8 +1040,11 @@ class ShardedSample:
         kz = int((n + m) / N) - kx  # prop_swor_layout's shard sizes
         z_total = int(Z0.numel())  # the Z the images were ranked against: images <= z_total
 
-        def count(xb, zb, steps, out):  # the bags of `steps` steps -> out (steps, N)
-            if bucket:
+        def count(xb, zb, steps, out, t0):  # bags of steps t0.. -> out (steps, N)
+            if rng is not None:
+                ops.count_chain_rng(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
+                                    self.max_nx, self.max_nz, rng[0], rng[1] + t0, r * N, out)
+            elif bucket:
                 ops.count_chain_bucket(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
                                        self.max_nz, z_total, half, out)
             else:
@@ -1067,14 +1105,19 @@ class ShardedSample:
                 for a, cs, j, work in xchg:
                     if work is not None:
                         work.wait()
-                    ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
-                                     z_bag[a:a + cs], self._chain_flag, kx, kz, N)
-                    count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs])
+                    if rng is not None:
+                        ops.chain_unpack_exact(recvs[j], G, cs, cap, n, m, x_bag[a:a + cs],
+                                               z_bag[a:a + cs], self._chain_flag)
+                    else:
+                        ops.chain_unpack(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
+                                         z_bag[a:a + cs], self._chain_flag, kx, kz, N)
+                    count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs],
+                          i0 + a)
                 continue
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
-            count(x_bag, z_bag, c, counts[i0:i0 + c])
+            count(x_bag, z_bag, c, counts[i0:i0 + c], i0)
         carry = None
         if coll:
             if final is not None:
@@ -1098,7 +1141,8 @@ class ShardedSample:
         if carry is not None:  # after the assignments above (they drop the old ones)
             self._carry = (self._X, self._Z, self._X._version, self._Z._version, half,
                            carry[0], carry[1], self._checksum())
-        vals = self.values(counts)  # (over ranks: raises _StaleImages on a bad verdict sum)
+        # (over ranks: raises _StaleImages on a bad verdict sum)
+        vals = self.values(counts, pairs=None if rng is None else rng[0])
         if verdict is not None and not coll and int(verdict[0]) != 1:
             raise _StaleImages("UnN_many: the sample was written behind its version counter; "
                                "the carried rank images are stale")
@@ -1165,6 +1209,9 @@ class ShardedSample:
         seeds = [(seed + i) & (2 ** 64 - 1) for i in range(len(keys))]
         if not keys:
             return []
+        if self.coll and self._chain_rng_ok():
+            # over ranks: the step chains, one exchange per chunk (device.py _chain_call)
+            return self._unn_many_chain(keys, rng=(int(B), seeds[0]))
         if not self.X.is_cuda:
             return [self.UnNB(B, sd, k) for sd, k in zip(seeds, keys)]
         step = None
