@@ -785,6 +785,14 @@ int tw_peer_step(const double* d_grads_loc, int64_t words, int64_t offset_words,
                  void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total, int64_t d,
                  int32_t par, double* d_w, double* d_dw, double reg, double lr, double momentum,
                  uint64_t* d_step, uint32_t* d_abort, void* stream);
+/* Column-owned per-step form (round 6): tw_peer_step's arguments and the same w / dw bits on
+ * every rank; rank p sums and updates only columns [p d / G, (p+1) d / G) (each rank pushes
+ * each partial column to its owner only, owners publish their updated columns to every rank).
+ * words and offset_words are whole rows (multiples of d). */
+int tw_peer_step_cols(const double* d_grads_loc, int64_t words, int64_t offset_words,
+                      void* const* d_peer_bases, int32_t G, int32_t rank, int32_t n_total,
+                      int64_t d, int32_t par, double* d_w, double* d_dw, double reg, double lr,
+                      double momentum, uint64_t* d_step, uint32_t* d_abort, void* stream);
 /* The narrow persistent segment (tw_sgd_segment_narrow) over ranks: this rank's n_shards
  * blocks (global shards shard_base..) push every step's gradients into every rank's peer
  * buffer and wait for all n_total shards on their own; the last update is applied in the

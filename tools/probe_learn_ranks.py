@@ -2,7 +2,9 @@
 csrc/peer.hip): bench.py's sgd_steps_per_s at the C4 shape and at C5 B = 100 with G co-resident
 ranks, against one rank — the rehearsal VERDICT r04 item 3 asks for (on one GPU the ranks share
 the chip, so the G-rank step does the one-GPU step's work plus the exchange).
-    python tools/probe_learn_ranks.py G [c4|c5|both] [trace]
+    python tools/probe_learn_ranks.py G [c4|c5|both] [trace|allcols]
+allcols: the round-5 per-step exchange (every rank updates all d columns, tw_peer_step) instead
+of the column owners' (tw_peer_step_cols, learning.PEER_COLUMNS).
 trace: a further short run of each line under torch.profiler (kineto, in-process: no re-exec),
 rank 0's per-kernel mean device time printed beside the line."""
 import json
@@ -29,13 +31,15 @@ def kernel_means(fn):
     return out
 
 
-def worker(rank, G, port, what, q, trace=False):
+def worker(rank, G, port, what, q, trace=False, allcols=False):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     torch.cuda.set_device(0)
     import bench
+    import tuplewise.learning as lr
+    lr.PEER_COLUMNS = not allcols
     g = dist.group.WORLD
     out = {}
     if what in ("c4", "both"):
@@ -60,18 +64,20 @@ if __name__ == "__main__":
     G = int(sys.argv[1])
     what = sys.argv[2] if len(sys.argv) > 2 else "both"
     trace = len(sys.argv) > 3 and sys.argv[3] == "trace"
+    allcols = len(sys.argv) > 3 and sys.argv[3] == "allcols"
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, G, port, what, q, trace)) for r in range(G)]
+    ps = [ctx.Process(target=worker, args=(r, G, port, what, q, trace, allcols)) for r in range(G)]
     for p in ps:
         p.start()
     res = q.get(timeout=900)
     for p in ps:
         p.join(timeout=120)
-    print(json.dumps({"ranks": G, **{k: {kk: v[kk] for kk in ("steps_per_s", "ms_per_step",
+    print(json.dumps({"ranks": G, "exchange": "all columns" if allcols else "column owners",
+                      **{k: {kk: v[kk] for kk in ("steps_per_s", "ms_per_step",
                                                                "trajectory_equal_1rank", "kernels")
                                          if kk in v} | {"launches": v["config"]["launches"]}
                                      for k, v in res.items()}}), flush=True)

@@ -139,6 +139,8 @@ _SIGNATURES = {
     "tw_peer_check": [_vp, _i32, _u64, _vp],
     "tw_peer_step": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _f64, _f64,
                      _f64, _vp, _vp, _vp],
+    "tw_peer_step_cols": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i64, _i32, _vp, _vp, _f64,
+                          _f64, _f64, _vp, _vp, _vp],
     "tw_sgd_segment_narrow_peer": [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                                    _i64, _f64, _i32, _u64, _vp, _i32, _i32, _i64, _i64, _i64,
                                    _vp, _vp, _f64, _f64, _f64, _vp, _vp, _i32, _i32, _i32, _vp],

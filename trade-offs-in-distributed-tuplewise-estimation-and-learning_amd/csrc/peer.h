@@ -10,21 +10,25 @@
 //   64   u64 segment epoch: global steps done by this rank's persistent segments
 //   128  u64 per-step counters [2] (128, 192), by step parity (the publish / update launches)
 //   256  u64 hello words [16]: rank p's token, written by rank p at setup (tw_peer_hello)
+//   384  u64 per-step publication counters [2] (384, 448), by step parity (the column-owned
+//        step, tw_peer_step_cols: owners' updated columns of w / dw arrived)
 //   512  segment gradient slots [2][n_total][d] f64
 //   ...  per-step gradient slots [2][n_total][d] f64
+//   ...  per-step publication slots [2][2][d] f64: by parity, w then dw (tw_peer_step_cols)
 #pragma once
 #include "tw_common.h"
 
 namespace tw {
 
 constexpr size_t kPeerSegCtr = 0, kPeerEpoch = 64, kPeerStepCtr = 128, kPeerHello = 256,
-                 kPeerHdr = 512;
+                 kPeerPubCtr = 384, kPeerHdr = 512;
 
 __host__ __device__ inline size_t peer_slots_words(int64_t n_total, int64_t d) {
   return 2 * (size_t)n_total * (size_t)d;
 }
 __host__ __device__ inline size_t peer_buffer_bytes(int64_t n_total, int64_t d) {
-  return kPeerHdr + 2 * sizeof(double) * peer_slots_words(n_total, d);
+  return kPeerHdr + 2 * sizeof(double) * peer_slots_words(n_total, d) +
+         4 * sizeof(double) * (size_t)d;
 }
 
 constexpr int kPeerMax = 16;

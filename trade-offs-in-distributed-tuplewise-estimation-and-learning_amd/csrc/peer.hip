@@ -108,6 +108,126 @@ __global__ __launch_bounds__(kBlock) void k_peer_step(const double* __restrict__
   }
 }
 
+// Column-owned form (round 6): rank p OWNS columns [cb(p), cb(p+1)) of w,
+// cb(p) = p d / G.  One launch per step after the gradient launch:
+//  (A) this rank's (rows, d) partials, each column only to its owner's slot of parity `par`
+//      (1/G of the bytes of k_peer_step's push), then one arrival per block on every rank's
+//      gradient counter of that parity;
+//  (B) once P * G arrivals are in, the owner sums ITS columns over all n_shards rows in shard
+//      order from +0.0 (own rows from `src`, the others from its slot) and applies
+//      k_sgd_update's arithmetic to them (the same bits as the one-GPU update), publishes the
+//      updated w and dw columns into every rank's publication slot of parity `par`, then one
+//      arrival per block on every rank's publication counter;
+//  (C) once P * G publication arrivals are in, the other owners' columns of w and dw are read
+//      from this rank's publication slot.
+// Per step a rank pushes rows_loc d (G-1)/G + 2 d (G-1)/G words instead of rows_loc d (G-1),
+// and its update reads n_shards d / G slot words instead of n_shards d.  Counter and slot
+// reuse: as k_peer_step's, for each of the two counter pairs (block 0 zeroes both of this
+// rank's counters of the other parity; every arrival of step t+2 on them is ordered after this
+// rank's step t+1, which waited for step t+1's publication of every rank).
+struct PubSeg {
+  unsigned long long* ctr[kPeerMax];  // rank p's publication counter of this parity
+  double* slot[kPeerMax];             // rank p's publication slots [2][2][d]
+  unsigned long long* my_ctr;
+  const double* my_slot;
+};
+
+__device__ __forceinline__ int64_t col_begin(int p, int G, int64_t d) {
+  return (int64_t)p * d / G;
+}
+
+__global__ __launch_bounds__(kBlock) void k_peer_step_cols(
+    const double* __restrict__ src, int64_t rows, int64_t row0, PeerSeg ps, PubSeg pb, int rank,
+    int par, unsigned long long* reset_g, unsigned long long* reset_p, uint64_t target,
+    int n_shards, int64_t d, double* w, double* dw, double reg, double lr, double momentum,
+    uint64_t* __restrict__ d_step, uint32_t* abort_word) {
+  __shared__ double tile[kPUpdRows * kPUpdCols];
+  __shared__ int s_ok;
+  const int G = ps.G;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    __hip_atomic_store(reset_g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(reset_p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const size_t base = (size_t)par * ps.n_total + (size_t)row0 * d;
+  // (A) per column owner: its columns of this rank's rows, into the owner's slot
+  for (int p = 0; p < G; ++p) {
+    if (p == rank) continue;
+    const int64_t c0 = col_begin(p, G, d), nc = col_begin(p + 1, G, d) - c0;
+    const int64_t words = rows * nc;
+    double* dst = ps.slot[p] + base;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < words;
+         i += (int64_t)gridDim.x * kBlock) {
+      const int64_t r = i / nc, c = c0 + (i - r * nc);
+      st_sys(dst + r * d + c, src[r * d + c]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if ((int)threadIdx.x < G)
+    __hip_atomic_fetch_add(ps.ctr[threadIdx.x], 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!peer_wait(ps.my_ctr, target, abort_word, &s_ok)) return;
+  if (d_step && blockIdx.x == 0 && threadIdx.x == 0) *d_step += 1;
+  // (B) this rank's columns: the shard-order sum, the update, the publication
+  const int64_t m0 = col_begin(rank, G, d), m1 = col_begin(rank + 1, G, d);
+  const double* slot = ps.my_slot + (size_t)par * ps.n_total;
+  const int64_t lo = row0 * d, hi = (row0 + rows) * d;
+  for (int64_t j0 = m0 + (int64_t)blockIdx.x * kPUpdCols; j0 < m1;
+       j0 += (int64_t)gridDim.x * kPUpdCols) {
+    const int nc = (int)std::min<int64_t>(kPUpdCols, m1 - j0);
+    double sum = 0.0;
+    for (int s0 = 0; s0 < n_shards; s0 += kPUpdRows) {
+      const int ns = std::min(kPUpdRows, n_shards - s0);
+      __syncthreads();
+      for (int e = threadIdx.x; e < ns * kPUpdCols; e += kBlock) {
+        const int r = e / kPUpdCols, c = e - r * kPUpdCols;
+        const int64_t at = (int64_t)(s0 + r) * d + j0 + c;
+        tile[e] = c >= nc ? 0.0 : (at >= lo && at < hi) ? src[at - lo] : ld_sys(slot + at);
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < nc) {
+        int r = 0;
+        for (; r + 8 <= ns; r += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = tile[(r + u) * kPUpdCols + threadIdx.x];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sum += v[u];
+        }
+        for (; r < ns; ++r) sum += tile[r * kPUpdCols + threadIdx.x];
+      }
+    }
+    if ((int)threadIdx.x < nc) {
+      const int64_t j = j0 + threadIdx.x;
+      const double wj = w[j];
+      const double g = sum / (double)n_shards + reg * wj;
+      const double step = momentum >= 0.0 ? momentum * dw[j] + lr * g : lr * g;
+      dw[j] = step;
+      w[j] = wj - step;
+      for (int p = 0; p < G; ++p) {
+        if (p == rank) continue;
+        double* pub = pb.slot[p] + (size_t)par * 2 * d;
+        st_sys(pub + j, wj - step);
+        st_sys(pub + d + j, step);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if ((int)threadIdx.x < G)
+    __hip_atomic_fetch_add(pb.ctr[threadIdx.x], 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  // (C) the other owners' columns
+  if (!peer_wait(pb.my_ctr, target, abort_word, &s_ok)) return;
+  const double* pub = pb.my_slot + (size_t)par * 2 * d;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < d;
+       j += (int64_t)gridDim.x * kBlock) {
+    if (j >= m0 && j < m1) continue;
+    w[j] = ld_sys(pub + j);
+    dw[j] = ld_sys(pub + d + j);
+  }
+}
+
 // setup handshake: lane p swaps this rank's token into rank p's hello word for this rank —
 // a system-scope read-modify-write through the mapping, the kind of operation every step's
 // arrivals are (a peer whose remote atomics do not land fails the check, and the ranks fall
@@ -154,6 +274,49 @@ extern "C" int tw_peer_check(void* d_my_base, int32_t G, uint64_t token, int32_t
   int ok = 1;
   for (int p = 0; p < G; ++p) ok &= h[p] == token ? 1 : 0;
   *out_ok = ok;
+  return TW_OK;
+}
+
+// Column-owned per-step form (k_peer_step_cols): tw_peer_step's arguments and results (the
+// same w / dw bits on every rank), with rank p updating only columns [p d / G, (p+1) d / G).
+extern "C" int tw_peer_step_cols(const double* d_grads_loc, int64_t words, int64_t offset_words,
+                                 void* const* d_peer_bases, int32_t G, int32_t rank,
+                                 int32_t n_total, int64_t d, int32_t par, double* d_w,
+                                 double* d_dw, double reg, double lr, double momentum,
+                                 uint64_t* d_step, uint32_t* d_abort, void* stream) {
+  TW_ARG_CHECK(d_peer_bases != nullptr && G >= 1 && G <= kPeerMax && rank >= 0 && rank < G &&
+                   n_total >= 1 && d >= 1 && words >= 0 && offset_words >= 0 &&
+                   offset_words + words <= (int64_t)n_total * d && (par == 0 || par == 1) &&
+                   words % d == 0 && offset_words % d == 0,
+               "tw_peer_step_cols: bad sizes");
+  TW_ARG_CHECK(d_w && d_dw && d_abort, "tw_peer_step_cols: w, dw and the abort word required");
+  PeerSeg ps{};
+  PubSeg pb{};
+  const size_t step_slots = kPeerHdr + sizeof(double) * peer_slots_words(n_total, d);
+  const size_t pub_slots = step_slots + sizeof(double) * peer_slots_words(n_total, d);
+  for (int p = 0; p < G; ++p) {
+    char* b = (char*)d_peer_bases[p];
+    TW_ARG_CHECK(b != nullptr, "tw_peer_step_cols: rank %d's buffer missing", p);
+    ps.slot[p] = (double*)(b + step_slots);
+    ps.ctr[p] = (unsigned long long*)(b + kPeerStepCtr + 64 * par);
+    pb.ctr[p] = (unsigned long long*)(b + kPeerPubCtr + 64 * par);
+    pb.slot[p] = (double*)(b + pub_slots);
+  }
+  char* mine = (char*)d_peer_bases[rank];
+  ps.G = G;
+  ps.n_total = (int)((int64_t)n_total * d);
+  ps.my_ctr = (unsigned long long*)(mine + kPeerStepCtr + 64 * par);
+  ps.my_slot = (const double*)(mine + step_slots);
+  pb.my_ctr = (unsigned long long*)(mine + kPeerPubCtr + 64 * par);
+  pb.my_slot = (const double*)(mine + pub_slots);
+  auto* reset_g = (unsigned long long*)(mine + kPeerStepCtr + 64 * (1 - par));
+  auto* reset_p = (unsigned long long*)(mine + kPeerPubCtr + 64 * (1 - par));
+  const int P = step_blocks(d);  // the same on every rank: d is
+  hipLaunchKernelGGL(k_peer_step_cols, dim3(P), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_grads_loc, words / d, offset_words / d, ps, pb, (int)rank, (int)par,
+                     reset_g, reset_p, (uint64_t)P * (uint64_t)G, (int)n_total, d, d_w, d_dw,
+                     reg, lr, momentum, d_step, d_abort);
+  TW_LAUNCH_CHECK();
   return TW_OK;
 }
 

@@ -69,6 +69,10 @@ PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each
 # (csrc/peer.hip: the persistent narrow segment, or per step one publish-wait-update launch)
 # instead of a host-enqueued RCCL all-gather per step; False keeps the all-gather (A/B)
 PEER_EXCHANGE = True
+# the per-step peer exchange by column owners (tw_peer_step_cols: each partial column goes to
+# its owner only, the owner updates its columns and publishes them) rather than every rank
+# receiving every partial and updating all d columns (tw_peer_step); same bits
+PEER_COLUMNS = True
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
 SIZE_TRAIN_MONITOR = 450000
@@ -479,7 +483,8 @@ class SGDEngine:
             # one launch: this rank's partials into every rank's slot, wait for all, update
             par = self.peer.pstep & 1
             self.peer.pstep += 1
-            L.call("tw_peer_step", L.ptr(self.grads_loc), self.N_loc * self.d,
+            L.call("tw_peer_step_cols" if PEER_COLUMNS and self.G > 1 else "tw_peer_step",
+                   L.ptr(self.grads_loc), self.N_loc * self.d,
                    self.shard_base * self.d, self.peer.bases, self.G, self.rank, self.N, self.d,
                    par, L.ptr(self.w), L.ptr(self.dw), self.reg, self.lr, self.momentum,
                    L.ptr(self.step_ctr), L.ptr(self._ctl[1:]), L.stream_handle())
