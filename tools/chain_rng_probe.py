@@ -98,7 +98,7 @@ def per_step_call(G, r, T):
     return ev_time(call, 5)[0]
 
 
-def chain_call(G, r, T, carried):
+def chain_call(G, r, T, carried, parts=False):
     ops = HipOps()
     nl, Nl, xo, zo, x_off, z_off = rank_setup(G, r)
     kx = int(x_off[1] - x_off[0])
@@ -122,6 +122,24 @@ def chain_call(G, r, T, carried):
     Xg, Zg, RXg, RZg = (torch.empty_like(a) for a in (X, Z, XR, ZR))
     full = torch.zeros(T * N + 1, dtype=torch.int64, device="cuda")
     fs = torch.cuda.Stream()
+    t = {}
+
+    def mark(name, fn):  # parts: events around each launch (the side stream's work serial)
+        if not parts:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn()
+        e1.record()
+        t.setdefault(name, []).append((e0, e1))
+        return out
+
+    def final():
+        Xg.copy_(X)
+        ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs)
+        RXg.copy_(XR)
+        RZg.copy_(ZR)
+        ops.chain_gather(RXg, RZg, r * nl, nl, r * nl, nl, kxs, kzs)
 
     def call():
         main = torch.cuda.current_stream()
@@ -129,26 +147,33 @@ def chain_call(G, r, T, carried):
             xr, zr = xr_c, zr_c
         else:
             Zg.copy_(Z)
-            xr, zr = ops.rank_images_query(Zg, xq, zq, L.TW_F64)
-        fs.wait_stream(main)
-        with torch.cuda.stream(fs):
-            Xg.copy_(X)
-            ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs)
-            RXg.copy_(XR)
-            RZg.copy_(ZR)
-            ops.chain_gather(RXg, RZg, r * nl, nl, r * nl, nl, kxs, kzs)
+            xr, zr = mark("ranking", lambda: ops.rank_images_query(Zg, xq, zq, L.TW_F64))
+        if parts:
+            mark("final arrays (side stream in the product)", final)
+        else:
+            fs.wait_stream(main)
+            with torch.cuda.stream(fs):
+                final()
         for i0 in range(0, T, C):
             c = min(C, T - i0)
-            ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, r, G, kxs[i0:i0 + c],
-                           kzs[i0:i0 + c], kx, kz, Nl, send=send, cap=cap, flag=flag)
+            mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, r, G,
+                                                kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
+                                                send=send, cap=cap, flag=flag))
             sz = G * c * (cap + 1)
-            recv[:sz].copy_(send[:sz])
-            ops.chain_unpack_exact(recv, G, c, cap, nl, nl, x_bag, z_bag, flag)
-            ops.count_chain_rng(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz, B, 5 + i0, r * Nl,
-                                counts[i0:i0 + c])
-        main.wait_stream(fs)
-        full[:-1].view(T, N)[:, r * Nl:(r + 1) * Nl].copy_(counts)
-    return ev_time(call, 5)[0]
+            mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
+            mark("unpack exact", lambda: ops.chain_unpack_exact(recv, G, c, cap, nl, nl, x_bag,
+                                                                z_bag, flag))
+            mark("count", lambda: ops.count_chain_rng(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx,
+                                                      kz, B, 5 + i0, r * Nl,
+                                                      counts[i0:i0 + c]))
+        if not parts:
+            main.wait_stream(fs)
+        mark("counts reduce (local part)",
+             lambda: full[:-1].view(T, N)[:, r * Nl:(r + 1) * Nl].copy_(counts))
+    ms = ev_time(call, 5)[0]
+    if parts:
+        return {k: sum(a.elapsed_time(b) for a, b in v) / 8 for k, v in t.items()}
+    return ms
 
 
 for T in Ts:
@@ -160,7 +185,9 @@ for T in Ts:
         ps = max(per_step_call(G, r, T) for r in ranks)
         cf = max(chain_call(G, r, T, False) for r in ranks)
         cc = max(chain_call(G, r, T, True) for r in ranks)
+        pp = chain_call(G, G - 1, T, True, parts=True)
         print(f"  G={G}: ideal {ideal / G:.3f} ms; per-step exchange {ps:.3f} ms "
               f"(eff {ideal / G / ps:.3f}); chains first call {cf:.3f} ms (eff "
-              f"{ideal / G / cf:.3f}), carried {cc:.3f} ms (eff {ideal / G / cc:.3f})",
-              flush=True)
+              f"{ideal / G / cf:.3f}), carried {cc:.3f} ms (eff {ideal / G / cc:.3f}); "
+              "carried parts (ms/call, serialised) "
+              + ", ".join(f"{k} {v:.4f}" for k, v in pp.items()), flush=True)

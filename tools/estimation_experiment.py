@@ -3,7 +3,11 @@
 For each epsilon: n_tries draws of Un, UnN, UnNT with the Bernoulli generators of
 main.py:97-101 (n=5000, m=50, N=10, T=4, prop-SWOR), via estimation.replicate (bit-identical
 to the reference loop).  Prints wall time and the variance ratios the paper plots; with
---cpu also times the oracle's restatement of the same loop for a few tries.
+--cpu-tries also times the oracle's restatement of the same loop for a few tries.  Round 6: also
+the HOST FLOOR of the same loop — the NumPy work the drop-in must do on the host to stay
+bit-identical (the generators' binomial draws, and for UnN / UnNT the in-place
+np.random.shuffle of X and Z per repartition, main.py:46-47) with no estimator at all — which
+bounds what any device can save on this experiment.
 """
 import argparse
 import pathlib
@@ -49,3 +53,20 @@ for e in eps:
           f"UnNT {np.var(v3) / V:.3f}", flush=True)
 dt = time.perf_counter() - t0
 print(f"device: full experiment ({len(eps)} eps x {a.tries} tries x 3 estimators) {dt:.2f} s")
+
+# the host floor: the same RNG consumption with no estimator (generators; shuffles per UN call)
+np.random.seed(0)
+t0 = time.perf_counter()
+for e in eps:
+    gx = lambda: 2 * np.random.binomial(1, 1 - e, n)
+    gz = lambda: 2 * np.random.binomial(1, e, m) - 1
+    for shuffles in (0, 1, T):  # Un, UnN, UnNT
+        for _ in range(a.tries):
+            x, z = gx(), gz()
+            for _ in range(shuffles):
+                np.random.shuffle(x)
+                np.random.shuffle(z)
+fl = time.perf_counter() - t0
+print(f"host floor (generators + the reference's in-place shuffles, no estimator): {fl:.2f} s "
+      f"= {fl / dt:.2f} of the device run; device-side remainder {dt - fl:.2f} s "
+      f"({(dt - fl) / (len(eps) * a.tries * 3) * 1e6:.1f} us per estimator call)")

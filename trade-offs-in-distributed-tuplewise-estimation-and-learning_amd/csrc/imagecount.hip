@@ -598,10 +598,13 @@ extern "C" int tw_count_pairs_chain_rng(const float* d_x_bag, const int64_t* d_x
   TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)nbags, st));
   if (B == 0 || max_nx == 0 || max_nz == 0) return TW_OK;
   TW_ARG_CHECK(d_x_bag && d_z_bag && d_x_off && d_z_off, "tw_count_pairs_chain_rng: buffers");
-  ImgPlan p = plan_images(n_shards, max_nx, max_nz, TW_PRED_GT, (B + 1) / 2);
+  // the plan spreads the chunk's (step, shard) bags over the CUs: with 8 shards a rank (G = 8)
+  // and 4 steps, 8 blocks a bag rather than one step's 32 — every block stages its bag's
+  // 125 KB of images once, so a grid of steps x (256 / shards) blocks staged each bag 4x over
+  ImgPlan p = plan_images((int32_t)std::min<int64_t>(nbags, 1 << 30), max_nx, max_nz,
+                          TW_PRED_GT, (B + 1) / 2);
   TW_ARG_CHECK(p.ok, "tw_count_pairs_chain_rng: a shard's images exceed the LDS (%lld + %lld)",
                (long long)max_nx, (long long)max_nz);
-  // the plan spreads ONE step's shards over the CUs; the chunk's steps multiply the grid
   TW_ARG_CHECK(nbags * p.parts < (1ll << 31), "tw_count_pairs_chain_rng: grid too large");
   static bool attr = false;
   if (!attr) {
