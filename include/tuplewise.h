@@ -229,6 +229,13 @@ int tw_chain_gather(const void* d_x_all, const void* d_z_all, int64_t x_base, in
                     int64_t n_x_all, int64_t z_base, int64_t n_z, int64_t n_z_all,
                     const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
                     uint32_t* d_work, void* d_x_out, void* d_z_out, void* stream);
+/* tw_chain_gather of a second pair of arrays laid out like the first (the carried rank-image
+ * records beside the scores) from the same walk of the inverse chains. */
+int tw_chain_gather2(const void* d_x_all, const void* d_z_all, const void* d_x_all2,
+                     const void* d_z_all2, int64_t x_base, int64_t n_x, int64_t n_x_all,
+                     int64_t z_base, int64_t n_z, int64_t n_z_all, const uint64_t* keys_x,
+                     const uint64_t* keys_z, int32_t steps, uint32_t* d_work, void* d_x_out,
+                     void* d_z_out, void* d_x_out2, void* d_z_out2, void* stream);
 
 /* ---- f4: the same counts in O((n+m) log m): sort each z-chunk (<= 16384 keys) in LDS as
  * order-preserving u64 keys, then binary-search every x (csrc/rankcount.hip).  Bit-identical

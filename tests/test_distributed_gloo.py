@@ -302,14 +302,19 @@ class OracleOpsChain(OracleOpsRank):
             verdict[0] = good if int(acc[0]) == int(expect[0]) else bad
         return acc
 
-    def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z):
-        out = []
+    def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z, X2=None,
+                     Z2=None):
+        out, src = [], []
         for A, base, cnt, keys in ((X_all, x_base, n, keys_x), (Z_all, z_base, m, keys_z)):
             p = np.arange(base, base + cnt)
             for key in reversed(keys):
                 p = O.feistel_perm_inv(p, A.numel(), int(key))
             out.append(torch.from_numpy(A.numpy()[p].copy()))
-        return out[0], out[1]
+            src.append(p)
+        if X2 is not None:  # tw_chain_gather2: the second pair from the same walk
+            out += [torch.from_numpy(X2.numpy()[src[0]].copy()),
+                    torch.from_numpy(Z2.numpy()[src[1]].copy())]
+        return tuple(out)
 
 
 _OPS = {"plain": OracleOps, "fused": OracleOpsFused, "fixed": OracleOpsFixed,

@@ -129,10 +129,10 @@ def rank_call(G, r, K, parts=False, carried=False):
             Xg.copy_(X)
             if carried:
                 Zg.copy_(Z)
-            ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs)
             RXg.copy_(XR)
             RZg.copy_(ZR)
-            ops.chain_gather(RXg, RZg, r * nl, nl, r * nl, nl, kxs, kzs)
+            # one walk of the inverse chains for scores and records (tw_chain_gather2, r06)
+            ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs, RXg, RZg)
 
     def call():
         main = torch.cuda.current_stream()

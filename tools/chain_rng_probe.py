@@ -136,10 +136,9 @@ def chain_call(G, r, T, carried, parts=False):
 
     def final():
         Xg.copy_(X)
-        ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs)
         RXg.copy_(XR)
         RZg.copy_(ZR)
-        ops.chain_gather(RXg, RZg, r * nl, nl, r * nl, nl, kxs, kzs)
+        ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs, RXg, RZg)
 
     def call():
         main = torch.cuda.current_stream()

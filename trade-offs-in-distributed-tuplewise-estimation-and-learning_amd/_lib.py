@@ -62,6 +62,8 @@ _SIGNATURES = {
     "tw_chain_scatter": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
     "tw_chain_gather": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp,
                         _vp, _vp],
+    "tw_chain_gather2": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _i32,
+                         _vp, _vp, _vp, _vp, _vp, _vp],
     "tw_count_pairs_sorted_work_bytes": [_i32, _i64],
     "tw_count_sorted_set_chunk": [_i64],
     "tw_count_pairs_sorted": [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32, _vp, _vp, _vp],

@@ -527,7 +527,9 @@ __global__ __launch_bounds__(kBlock) void k_chain_inverse(
     int64_t xbase, int64_t nx, int64_t NX, int64_t zbase, int64_t nz, int64_t NZ,
     const uint32_t* __restrict__ pin, uint32_t* __restrict__ pout, ChainKeys keys, int steps,
     int gather, const uint64_t* __restrict__ xall, const uint64_t* __restrict__ zall,
-    uint64_t* __restrict__ xout, uint64_t* __restrict__ zout) {
+    uint64_t* __restrict__ xout, uint64_t* __restrict__ zout,
+    const uint64_t* __restrict__ xall2, const uint64_t* __restrict__ zall2,
+    uint64_t* __restrict__ xout2, uint64_t* __restrict__ zout2) {
   __shared__ Feistel fs[2 * kChainMax];
   if ((int)threadIdx.x < 2 * steps) {
     const int t = threadIdx.x;
@@ -545,11 +547,14 @@ __global__ __launch_bounds__(kBlock) void k_chain_inverse(
       p = feistel_once_inv32(F, p);
       while (p >= (uint32_t)Nt) p = feistel_once_inv32(F, p);
     }
-    if (gather) {
-      if (isx)
+    if (gather) {  // (a second pair of arrays, e.g. the carried records, from the same walk)
+      if (isx) {
         xout[i] = xall[p];
-      else
+        if (xall2) xout2[i] = xall2[p];
+      } else {
         zout[i - nx] = zall[p];
+        if (zall2) zout2[i - nx] = zall2[p];
+      }
     } else {
       pout[i] = p;
     }
@@ -1000,11 +1005,44 @@ extern "C" int tw_chain_scatter(const void* d_x, const uint32_t* d_x_pos, int64_
   return TW_OK;
 }
 
+static int chain_gather_impl(const void* d_x_all, const void* d_z_all, int64_t x_base,
+                             int64_t n_x, int64_t n_x_all, int64_t z_base, int64_t n_z,
+                             int64_t n_z_all, const uint64_t* keys_x, const uint64_t* keys_z,
+                             int32_t steps, uint32_t* d_work, void* d_x_out, void* d_z_out,
+                             const void* d_x_all2, const void* d_z_all2, void* d_x_out2,
+                             void* d_z_out2, void* stream);
+
 extern "C" int tw_chain_gather(const void* d_x_all, const void* d_z_all, int64_t x_base,
                                int64_t n_x, int64_t n_x_all, int64_t z_base, int64_t n_z,
                                int64_t n_z_all, const uint64_t* keys_x, const uint64_t* keys_z,
                                int32_t steps, uint32_t* d_work, void* d_x_out, void* d_z_out,
                                void* stream) {
+  return chain_gather_impl(d_x_all, d_z_all, x_base, n_x, n_x_all, z_base, n_z, n_z_all, keys_x,
+                           keys_z, steps, d_work, d_x_out, d_z_out, nullptr, nullptr, nullptr,
+                           nullptr, stream);
+}
+
+// tw_chain_gather of two pairs of arrays laid out alike (the scores and the carried records)
+// through ONE walk of the inverse chains
+extern "C" int tw_chain_gather2(const void* d_x_all, const void* d_z_all, const void* d_x_all2,
+                                const void* d_z_all2, int64_t x_base, int64_t n_x,
+                                int64_t n_x_all, int64_t z_base, int64_t n_z, int64_t n_z_all,
+                                const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
+                                uint32_t* d_work, void* d_x_out, void* d_z_out, void* d_x_out2,
+                                void* d_z_out2, void* stream) {
+  TW_ARG_CHECK(d_x_all2 && d_z_all2 && d_x_out2 && d_z_out2,
+               "tw_chain_gather2: the second pair of arrays");
+  return chain_gather_impl(d_x_all, d_z_all, x_base, n_x, n_x_all, z_base, n_z, n_z_all, keys_x,
+                           keys_z, steps, d_work, d_x_out, d_z_out, d_x_all2, d_z_all2, d_x_out2,
+                           d_z_out2, stream);
+}
+
+static int chain_gather_impl(const void* d_x_all, const void* d_z_all, int64_t x_base,
+                             int64_t n_x, int64_t n_x_all, int64_t z_base, int64_t n_z,
+                             int64_t n_z_all, const uint64_t* keys_x, const uint64_t* keys_z,
+                             int32_t steps, uint32_t* d_work, void* d_x_out, void* d_z_out,
+                             const void* d_x_all2, const void* d_z_all2, void* d_x_out2,
+                             void* d_z_out2, void* stream) {
   TW_ARG_CHECK(n_x >= 0 && n_z >= 0 && x_base >= 0 && z_base >= 0 && steps >= 0 &&
                    x_base + n_x <= n_x_all && z_base + n_z <= n_z_all &&
                    n_x_all < (1ll << 32) && n_z_all < (1ll << 32),
@@ -1026,7 +1064,8 @@ extern "C" int tw_chain_gather(const void* d_x_all, const void* d_z_all, int64_t
     hipLaunchKernelGGL(k_chain_inverse, dim3(grid), dim3(kBlock), 0, st, x_base, n_x, n_x_all,
                        z_base, n_z, n_z_all, have ? d_work : nullptr, d_work, k, hi - lo,
                        lo == 0 ? 1 : 0, (const uint64_t*)d_x_all, (const uint64_t*)d_z_all,
-                       (uint64_t*)d_x_out, (uint64_t*)d_z_out);
+                       (uint64_t*)d_x_out, (uint64_t*)d_z_out, (const uint64_t*)d_x_all2,
+                       (const uint64_t*)d_z_all2, (uint64_t*)d_x_out2, (uint64_t*)d_z_out2);
     TW_LAUNCH_CHECK();
     have = true;
     hi = lo;

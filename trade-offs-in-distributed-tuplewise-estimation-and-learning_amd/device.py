@@ -291,17 +291,30 @@ class HipOps:
                L.ptr(zpos), int(Z.numel()), L.ptr(Xo), L.ptr(Zo), L.stream_handle())
         return Xo, Zo
 
-    def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z):
+    def chain_gather(self, X_all, Z_all, x_base, n, z_base, m, keys_x, keys_z, X2=None,
+                     Z2=None):
+        """The rank's final arrays: the inverse chains of its own positions, gathered from the
+        all-gathered samples (tw_chain_gather); with X2 / Z2 (laid out like X_all / Z_all:
+        the carried records) also theirs, from the same walk (tw_chain_gather2)."""
         kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
         kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
         dev = X_all.device
         Xo = self.t.empty((n,), dtype=X_all.dtype, device=dev)
         Zo = self.t.empty((m,), dtype=Z_all.dtype, device=dev)
         work = self.t.empty((max(1, n + m),), dtype=self.t.int32, device=dev)
-        L.call("tw_chain_gather", L.ptr(X_all), L.ptr(Z_all), int(x_base), int(n),
-               int(X_all.numel()), int(z_base), int(m), int(Z_all.numel()), kxa.ctypes.data,
-               kza.ctypes.data, len(kxa), L.ptr(work), L.ptr(Xo), L.ptr(Zo), L.stream_handle())
-        return Xo, Zo
+        if X2 is None:
+            L.call("tw_chain_gather", L.ptr(X_all), L.ptr(Z_all), int(x_base), int(n),
+                   int(X_all.numel()), int(z_base), int(m), int(Z_all.numel()), kxa.ctypes.data,
+                   kza.ctypes.data, len(kxa), L.ptr(work), L.ptr(Xo), L.ptr(Zo),
+                   L.stream_handle())
+            return Xo, Zo
+        X2o = self.t.empty((n,), dtype=X2.dtype, device=dev)
+        Z2o = self.t.empty((m,), dtype=Z2.dtype, device=dev)
+        L.call("tw_chain_gather2", L.ptr(X_all), L.ptr(Z_all), L.ptr(X2), L.ptr(Z2), int(x_base),
+               int(n), int(X_all.numel()), int(z_base), int(m), int(Z_all.numel()),
+               kxa.ctypes.data, kza.ctypes.data, len(kxa), L.ptr(work), L.ptr(Xo), L.ptr(Zo),
+               L.ptr(X2o), L.ptr(Z2o), L.stream_handle())
+        return Xo, Zo, X2o, Z2o
 
     def count_rng(self, x, x_off_dev, z, z_off_dev, n_shards, B, seed, shard_base, dtype, pred,
                   max_nx=None, max_nz=None):
@@ -1031,9 +1044,7 @@ class ShardedSample:
                     if w is not None:
                         w.wait()
                 works = []
-                final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
-                if RX is not None:
-                    final = final + ops.chain_gather(RX, RZ, r * n, n, r * m, m, kxs, kzs)
+                final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs, RX, RZ)
                 for a in final:
                     a.record_stream(main)
         kx = int(n / N)
@@ -1126,9 +1137,7 @@ class ShardedSample:
                 for w in works:
                     if w is not None:
                         w.wait()
-                final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs)
-                if RX is not None:
-                    final = final + ops.chain_gather(RX, RZ, r * n, n, r * m, m, kxs, kzs)
+                final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs, RX, RZ)
             self.X, self.Z = final[0], final[1]
             if RX is not None:
                 carry = (final[2], final[3])
