@@ -19,13 +19,14 @@ def _port():
 _HIST = ("norm_w", "tr_AUC", "tc_AUC", "bc_AUC")
 
 
-def _learn_worker(rank, port, G, mode, q, layout="replicated"):
+def _learn_worker(rank, port, G, mode, q, layout="replicated", cols=None):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     torch.cuda.set_device(0)
     import tuplewise.learning as lr
+    lr.PEER_COLUMNS = cols  # True: the column owners' per-step exchange (tw_peer_step_cols)
     X, Z, w0, p = _problem()
     traj = []
     np.random.seed(99)
@@ -56,14 +57,17 @@ def _problem():
     return X, Z, w0, p
 
 
-@pytest.mark.parametrize("G,mode,layout",
-                         [(2, m, la) for m in ("replay", "device")
+@pytest.mark.parametrize("G,mode,layout,cols",
+                         [(2, m, la, None) for m in ("replay", "device")
                           for la in ("replicated", "partitioned")]
-                         + [(3, "replay", "replicated"), (3, "device", "partitioned")])
-def test_learning_two_ranks_equals_one(gpu, G, mode, layout):
+                         + [(3, "replay", "replicated", None), (3, "device", "partitioned", None),
+                            (2, "device", "replicated", True), (3, "replay", "partitioned", True)])
+def test_learning_two_ranks_equals_one(gpu, G, mode, layout, cols):
     """G ranks (gloo) on the box's GPU equal one rank bit for bit — with a trajectory (the
     per-step peer exchange) and without (the persistent peer segment, three evaluations).
-    G = 3: N = 8 shards split 2/3/3 (uneven splits, the reference's N = 100 over 8 GPUs)."""
+    G = 3: N = 8 shards split 2/3/3 (uneven splits, the reference's N = 100 over 8 GPUs).
+    cols=True: the per-step exchange by column owners (tw_peer_step_cols; d = 8 over 3 ranks
+    gives owners of 2, 3 and 3 columns)."""
     import torch.multiprocessing as mp
     import tuplewise.learning as lr
     X, Z, w0, p = _problem()
@@ -76,7 +80,7 @@ def test_learning_two_ranks_equals_one(gpu, G, mode, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_learn_worker, args=(r, port, G, mode, q, layout))
+    procs = [ctx.Process(target=_learn_worker, args=(r, port, G, mode, q, layout, cols))
              for r in range(G)]
     for pr in procs:
         pr.start()
@@ -106,6 +110,8 @@ def _est_worker(rank, port, G, q, exchange="fixed", chain=True):
                       group=dist.group.WORLD, exchange=exchange, algo="pairs")
     vals = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
     vals += [float(v) for v in S.UnN_many([5, 6, 7])]  # rank images: the step chains
+    # the incomplete statistic on the chains (exact-position bags, device draws on images)
+    vals += [float(v) for v in S.UnNB_many(700, 21, [15, 16, 17])]
     S.algo = "sorted"  # the chains' exact bucket count of every bag (per-step path unchained)
     vals += [float(v) for v in S.UnN_many([8, 9])]
     Xg = [torch.empty(S.X.shape, dtype=S.X.dtype) for _ in range(G)]
@@ -136,6 +142,7 @@ def test_sharded_sample_two_ranks_equals_one(gpu, G, exchange, chain):
                       algo="pairs")
     want = [float(S.UnN(k)) for k in (1, 2, 3)] + [float(S.UnNB(500, seed=4))]
     want += [float(v) for v in S.UnN_many([5, 6, 7])]
+    want += [float(S.UnNB(700, 21 + t, k)) for t, k in enumerate([15, 16, 17])]
     assert S._chain_ok() and S.algo == "pairs"
     S.algo = "sorted"
     want += [float(v) for v in S.UnN_many([8, 9])]

@@ -39,7 +39,7 @@ def worker(rank, G, port, what, q, trace=False, allcols=False):
     torch.cuda.set_device(0)
     import bench
     import tuplewise.learning as lr
-    lr.PEER_COLUMNS = not allcols
+    lr.PEER_COLUMNS = not allcols  # forced either way (the default picks by G)
     g = dist.group.WORLD
     out = {}
     if what in ("c4", "both"):

@@ -71,8 +71,12 @@ PIPE_STATS = None  # a list: the pipelined replay loop appends its wait for each
 PEER_EXCHANGE = True
 # the per-step peer exchange by column owners (tw_peer_step_cols: each partial column goes to
 # its owner only, the owner updates its columns and publishes them) rather than every rank
-# receiving every partial and updating all d columns (tw_peer_step); same bits
-PEER_COLUMNS = True
+# receiving every partial and updating all d columns (tw_peer_step); same bits.  None = from 8
+# ranks on: it moves (G-1)/G of the bytes less but adds a second cross-rank hand-off per step,
+# and co-resident rehearsals (ranks sharing one GPU's HBM, where bytes are cheap) measured it
+# slower at 2 and 4 ranks (C5 B = 100: 61.0 vs 57.2 us, 170 vs 161 us; profiles/r06_learn*)
+PEER_COLUMNS = None
+PEER_COLUMNS_MIN_RANKS = 8
 TYPE_TRAIN_MONITOR = "FIXED_PAIRS"  # or "SAME_AS_BATCH" (make_exps.py:31-33)
 SEED_TRAIN_MONITOR = 54
 SIZE_TRAIN_MONITOR = 450000
@@ -483,7 +487,9 @@ class SGDEngine:
             # one launch: this rank's partials into every rank's slot, wait for all, update
             par = self.peer.pstep & 1
             self.peer.pstep += 1
-            L.call("tw_peer_step_cols" if PEER_COLUMNS and self.G > 1 else "tw_peer_step",
+            cols = (self.G >= PEER_COLUMNS_MIN_RANKS if PEER_COLUMNS is None
+                    else bool(PEER_COLUMNS)) and self.G > 1
+            L.call("tw_peer_step_cols" if cols else "tw_peer_step",
                    L.ptr(self.grads_loc), self.N_loc * self.d,
                    self.shard_base * self.d, self.peer.bases, self.G, self.rank, self.N, self.d,
                    par, L.ptr(self.w), L.ptr(self.dw), self.reg, self.lr, self.momentum,
