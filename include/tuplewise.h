@@ -914,12 +914,14 @@ int tw_count_pairs_chain_rng(const float* d_x_bag, const int64_t* d_x_off, int64
                              void* stream);
 /* The carried rank images' validity check (ShardedSample.UnN_many, device.py CARRY_IMAGES;
  * the arrays only ever permute between calls, estimation-experiment/main.py:43-44): *d_acc =
- * sum over the na + nb 8-byte words of [d_a | d_b] of a position-keyed 64-bit hash.  With
+ * sum over the na + nb 8-byte words of [d_a | d_b] of a position-keyed 64-bit hash (d_acc:
+ * tw_words_checksum_acc_words() u64 words, the rest scratch for the blocks' partials).  With
  * d_expect (one device word) and d_verdict (one int64; device or mapped host memory) both set,
  * also *d_verdict = (*d_acc == *d_expect) ? good : bad, in stream order. */
 int tw_words_checksum(const void* d_a, int64_t na, const void* d_b, int64_t nb, void* d_acc,
                       const void* d_expect, void* d_verdict, int64_t good, int64_t bad,
                       void* stream);
+int64_t tw_words_checksum_acc_words(void);
 /* The device address of pinned, mapped host memory (hipHostGetDevicePointer); TW_ERR_ARG when
  * `host` is not such memory. */
 int tw_host_device_pointer(void* host, void** out_dev);

@@ -205,6 +205,7 @@ _SIGNATURES = {
     "tw_count_pairs_chain_rng": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i64,
                                  _u64, _u64, _vp, _vp],
     "tw_words_checksum": [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _vp],
+    "tw_words_checksum_acc_words": [],
     "tw_np_shuffle_pair": [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
     "tw_np_shuffle_draws32": [_vp, _vp, _i64, _vp],
     "tw_np_shuffle_draws32_range": [_vp, _vp, _i64, _i64, _i64, _vp],
@@ -229,6 +230,7 @@ _RESTYPES = {
     "tw_pair_hinge_sum_sorted_work_bytes": ctypes.c_int64,
     "tw_shuffle_swaps_work_bytes": ctypes.c_int64,
     "tw_eval_small_work": ctypes.c_int64,
+    "tw_words_checksum_acc_words": ctypes.c_int64,
 }
 
 _lib = None

@@ -22,10 +22,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64's finalis
 }
 
 // sum over words i of mix64(word_i ^ i * golden): a value change at any position, or two
-// positions exchanging unequal values, changes the sum (but for a 2^-64 collision)
+// positions exchanging unequal values, changes the sum (but for a 2^-64 collision).  One
+// partial per block (no atomics: 2000 same-address atomics serialised at one L2 channel cost the
+// first build ~0.2 ms per call, profiles/r06s11_chain_probe.log), summed by the verdict block.
+constexpr int kHashBlocks = 256;
+
 __global__ __launch_bounds__(256) void k_words_hash(const uint64_t* __restrict__ a, int64_t na,
                                                     const uint64_t* __restrict__ b, int64_t nb,
-                                                    unsigned long long* __restrict__ acc) {
+                                                    uint64_t* __restrict__ partial) {
   const int64_t n = na + nb;
   const int64_t stride = (int64_t)gridDim.x * 256;
   uint64_t s = 0;
@@ -35,14 +39,27 @@ __global__ __launch_bounds__(256) void k_words_hash(const uint64_t* __restrict__
     s += mix64(w ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull));
   }
   s = wave_sum_u64(s);
-  if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(acc, (unsigned long long)s);
+  __shared__ uint64_t ws[4];
+  if ((threadIdx.x & (kWave - 1)) == 0) ws[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-__global__ __launch_bounds__(64) void k_words_verdict(const uint64_t* __restrict__ acc,
-                                                      const uint64_t* __restrict__ expect,
-                                                      int64_t* __restrict__ verdict, int64_t good,
-                                                      int64_t bad) {
-  if (threadIdx.x == 0) verdict[0] = acc[0] == expect[0] ? good : bad;
+// acc[0] = the sum of the blocks' partials (acc[1 ..]); with expect: the verdict word
+__global__ __launch_bounds__(256) void k_words_verdict(uint64_t* __restrict__ acc, int nparts,
+                                                       const uint64_t* __restrict__ expect,
+                                                       int64_t* __restrict__ verdict,
+                                                       int64_t good, int64_t bad) {
+  uint64_t s = (int)threadIdx.x < nparts ? acc[1 + threadIdx.x] : 0ull;
+  s = wave_sum_u64(s);
+  __shared__ uint64_t ws[4];
+  if ((threadIdx.x & (kWave - 1)) == 0) ws[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t tot = ws[0] + ws[1] + ws[2] + ws[3];
+    acc[0] = tot;
+    if (verdict) verdict[0] = tot == expect[0] ? good : bad;
+  }
 }
 
 }  // namespace
@@ -59,19 +76,17 @@ extern "C" int tw_words_checksum(const void* d_a, int64_t na, const void* d_b, i
   TW_ARG_CHECK((d_expect == nullptr) == (d_verdict == nullptr),
                "tw_words_checksum: expect and verdict go together");
   hipStream_t st = (hipStream_t)stream;
-  TW_HIP_CHECK(tw_zero_async(d_acc, 0, sizeof(uint64_t), st));
   const int64_t n = na + nb;
-  if (n > 0) {
-    // 4 words per thread per pass at the chain sizes (2e6 words: ~2000 blocks, 8 per CU)
-    const unsigned g = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 1024)));
-    hipLaunchKernelGGL(k_words_hash, dim3(g), dim3(256), 0, st, (const uint64_t*)d_a, na,
-                       (const uint64_t*)d_b, nb, (unsigned long long*)d_acc);
-    TW_LAUNCH_CHECK();
-  }
-  if (d_expect != nullptr) {
-    hipLaunchKernelGGL(k_words_verdict, dim3(1), dim3(64), 0, st, (const uint64_t*)d_acc,
-                       (const uint64_t*)d_expect, (int64_t*)d_verdict, good, bad);
-    TW_LAUNCH_CHECK();
-  }
+  // one block per CU at most, ~8 words per thread at the chain sizes (2e6 words: 256 blocks)
+  const int g = (int)std::min<int64_t>(kHashBlocks, std::max<int64_t>(1, ceil_div(n, 2048)));
+  uint64_t* acc = (uint64_t*)d_acc;
+  hipLaunchKernelGGL(k_words_hash, dim3(g), dim3(256), 0, st, (const uint64_t*)d_a, na,
+                     (const uint64_t*)d_b, nb, acc + 1);
+  TW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_words_verdict, dim3(1), dim3(256), 0, st, acc, g,
+                     (const uint64_t*)d_expect, (int64_t*)d_verdict, good, bad);
+  TW_LAUNCH_CHECK();
   return TW_OK;
 }
+
+extern "C" int64_t tw_words_checksum_acc_words(void) { return 1 + kHashBlocks; }

@@ -391,6 +391,9 @@ class HipOps:
                int(out_next.numel()) if out_next is not None else 0, L.stream_handle())
         return out
 
+    def checksum_acc_words(self):
+        return int(L.lib().tw_words_checksum_acc_words())
+
     def words_checksum(self, A, B, acc, expect=None, verdict=None, good=1, bad=0):
         """acc (one int64) = the position-keyed hash of [A | B]'s 8-byte words
         (tw_words_checksum, csrc/guard.hip); with expect / verdict: verdict = good when acc ==
@@ -471,8 +474,10 @@ class ShardedSample:
         with expect / verdict, also the verdict word (see HipOps.words_checksum)."""
         if not hasattr(self.ops, "words_checksum"):
             return None
-        acc = self.t.empty((1,), dtype=self.t.int64, device=self.X.device)
-        return self.ops.words_checksum(self.X, self.Z, acc, expect, verdict, good, bad)
+        if getattr(self, "_acc_words", None) is None:
+            self._acc_words = int(getattr(self.ops, "checksum_acc_words", lambda: 1)())
+        acc = self.t.empty((self._acc_words,), dtype=self.t.int64, device=self.X.device)
+        return self.ops.words_checksum(self.X, self.Z, acc, expect, verdict, good, bad)[:1]
 
     def _host_verdict(self):
         """The pinned (device-mapped) host word the one-process verdict is written into."""
