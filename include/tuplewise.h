@@ -904,23 +904,6 @@ int tw_stage_eval(const void* d_res, int32_t nres, const void* d_w, int32_t nw,
  * tw_count_pairs_chain_rng counts B device-drawn pairs (tw_count_pairs_rng's Philox/Lemire
  * draws, step c keyed seed + c, shard streams stream_id + s) of every (step, shard) bag on
  * those images, out [steps][n_shards] (zeroed here). */
-/* The step chains' exchange with a RUN TABLE (round 6; strict images): tw_chain_emit_runs
- * writes every image into the run of its (destination rank, step, destination region) — one
- * (destination, step) block of per_step32 u32 words each: region counters, then the x and the z
- * runs (tw_chain_runs_layout: out[0..6] = H, capSx, capTx, capSz, capTz, zoff, per_step32) —
- * and after ONE equal-split all-to-all tw_count_pairs_chain_runs counts every (step, shard) bag
- * as its world x runs and world z runs in place (no unpack), out [steps][n_shards] zeroed here.
- * Every shard full: n_shards * shard <= n on both sides.  Overflowing runs raise *d_flag. */
-int tw_chain_runs_layout(int64_t n_x, int64_t n_z, int64_t x_shard, int64_t z_shard,
-                         int32_t n_shards, int32_t world, int64_t* out);
-int tw_chain_emit_runs(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec,
-                       int64_t n_z, uint32_t* d_x_pos, uint32_t* d_z_pos, int32_t first,
-                       int32_t rank, int32_t world, const uint64_t* keys_x,
-                       const uint64_t* keys_z, int32_t steps, int64_t x_shard, int64_t z_shard,
-                       int32_t n_shards, uint32_t* d_send, int32_t* d_flag, void* stream);
-int tw_count_pairs_chain_runs(const uint32_t* d_recv, int32_t world, int32_t steps, int64_t n_x,
-                              int64_t n_z, int64_t x_shard, int64_t z_shard, int32_t n_shards,
-                              uint64_t* d_out, void* stream);
 int tw_chain_unpack_exact(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
                           int64_t n_x, int64_t n_z, void* d_x_bag, void* d_z_bag,
                           int32_t* d_flag, void* stream);

@@ -257,68 +257,6 @@ class OracleOpsChain(OracleOpsRank):
         Zo.numpy()[zpos.numpy().view(np.uint32)] = Z.numpy()
         return Xo, Zo
 
-    def runs_layout(self, n, m, kx, kz, n_shards, world):
-        """tw_chain_runs_layout (a host function of the library: no device)."""
-        from tuplewise import _lib as L
-        out = np.zeros(7, dtype=np.int64)
-        L.call("tw_chain_runs_layout", int(n), int(m), int(kx), int(kz), int(n_shards),
-               int(world), out.ctypes.data)
-        return [int(v) for v in out]
-
-    def chain_emit_runs(self, xr, zr, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
-                        n_shards, send, flag):
-        """tw_chain_emit_runs restated: every image into the run of its (destination, step,
-        destination region), the runs' counters at the front of each (destination, step)
-        block (run order inside a run is free: the count needs the multiset)."""
-        n, m = xr.numel(), zr.numel()
-        H, capSx, capTx, capSz, capTz, zoff, ps = self.runs_layout(n, m, kx, kz, n_shards, world)
-        steps = len(keys_x)
-        buf = send.numpy().view(np.uint32)
-        for g in range(world):
-            for c in range(steps):
-                buf[(g * steps + c) * ps:(g * steps + c) * ps + H] = 0
-        for side, (rec, pos, keys, nl, k) in enumerate(((xr, xpos, keys_x, n, kx),
-                                                        (zr, zpos, keys_z, m, kz))):
-            val = (rec.numpy().view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-            p = (np.arange(rank * nl, (rank + 1) * nl) if first
-                 else pos.numpy().view(np.uint32).astype(np.int64))
-            for c, key in enumerate(keys):
-                p = O.feistel_perm(p, world * nl, int(key))
-                g, ql = p // nl, p % nl
-                rb = np.minimum(ql // k, n_shards) if k else np.full_like(ql, n_shards)
-                for gg in range(world):
-                    for b in range(n_shards + 1):
-                        sel = val[(g == gg) & (rb == b)]
-                        blk = (gg * steps + c) * ps
-                        cap = (capSx if b < n_shards else capTx) if side == 0 else (
-                            capSz if b < n_shards else capTz)
-                        off = (H + b * capSx) if side == 0 else (zoff + b * capSz)
-                        buf[blk + side * (n_shards + 1) + b] = len(sel)
-                        if len(sel) > cap:
-                            flag.numpy()[0] = 1
-                            sel = sel[:cap]
-                        buf[blk + off:blk + off + len(sel)] = sel
-            pos.numpy()[:] = p.astype(np.uint32).view(np.int32)
-
-    def count_chain_runs(self, recv, world, steps, n, m, kx, kz, n_shards, out):
-        """tw_count_pairs_chain_runs restated: bag (c, s) = the world x runs and world z runs
-        of region s in the world source blocks of step c."""
-        H, capSx, capTx, capSz, capTz, zoff, ps = self.runs_layout(n, m, kx, kz, n_shards, world)
-        buf = recv.numpy().view(np.uint32)
-        for c in range(steps):
-            for s_ in range(n_shards):
-                xs, zs = [], []
-                for g in range(world):
-                    blk = (g * steps + c) * ps
-                    nx_ = min(int(buf[blk + s_]), capSx)
-                    nz_ = min(int(buf[blk + n_shards + 1 + s_]), capSz)
-                    xs.append(buf[blk + H + s_ * capSx:blk + H + s_ * capSx + nx_])
-                    zs.append(buf[blk + zoff + s_ * capSz:blk + zoff + s_ * capSz + nz_])
-                a = np.concatenate(xs).view(np.float32)
-                b = np.concatenate(zs).view(np.float32)
-                out[c, s_] = int((a[:, None] + b[None, :] >= 1).sum())
-        return out
-
     def chain_unpack_exact(self, recv, world, steps, cap, n, m, x_bag, z_bag, flag):
         """tw_chain_unpack_exact restated: every record at its exact position of its bag."""
         buf = recv.numpy().view(np.uint64)

@@ -15,8 +15,7 @@ ranking; the all-gathers of both samples and of both record arrays, as device co
 inverse-chain gathers of scores and records on a side stream beside the counts), each against
 the one-GPU call of the same kind / G.  The sub-chunk schedules of the round-5 study are in
 profiles/r05s36_chain_probe.log.  Run on the GPU box:
-    python tools/chain_probe.py [K ...]   (TW_PROBE_RUNS=0: the round-5 records + unpack
-exchange instead of the round-6 run table, device.CHAIN_RUNS)"""
+    python tools/chain_probe.py [K ...]"""
 import pathlib
 import sys
 import time
@@ -29,9 +28,6 @@ import tuplewise  # noqa: F401
 from tuplewise import _lib as L
 from tuplewise import device as D
 from tuplewise.device import HipOps, ShardedSample, prop_swor_layout
-
-import os  # noqa: E402
-D.CHAIN_RUNS = os.environ.get("TW_PROBE_RUNS", "1") == "1"
 
 torch.cuda.set_device(0)
 gen = torch.Generator(device="cuda").manual_seed(1)
@@ -103,9 +99,6 @@ def rank_call(G, r, K, parts=False, carried=False):
     zpos = torch.empty(nl, dtype=torch.int32, device="cuda")
     counts = torch.empty((K, Nl), dtype=torch.int64, device="cuda")
     cur = torch.empty(C * 2 * (Nl + 1), dtype=torch.int32, device="cuda")
-    ps = ops.runs_layout(nl, nl, kx, kz, Nl, G)[6]
-    rsend = torch.empty(G * C * ps, dtype=torch.int32, device="cuda")
-    rrecv = torch.empty_like(rsend)
     keys = list(range(500, 500 + K))
     kxs = [(2 * k) & M64 for k in keys]
     kzs = [(2 * k + 1) & M64 for k in keys]
@@ -158,15 +151,6 @@ def rank_call(G, r, K, parts=False, carried=False):
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, 0, 1,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                     x_bag=x_bag, z_bag=z_bag, cursors=cur))
-            elif D.CHAIN_RUNS:  # the product's run table (round 6): no unpack
-                mark("emit", lambda: ops.chain_emit_runs(xr, zr, xpos, zpos, first, r, G,
-                                                         kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz,
-                                                         Nl, rsend, flag))
-                sz = G * c * ps
-                mark("exchange (device copy)", lambda: rrecv[:sz].copy_(rsend[:sz]))
-                mark("count", lambda: ops.count_chain_runs(rrecv, G, c, nl, nl, kx, kz, Nl,
-                                                           counts[i0:i0 + c]))
-                continue
             else:
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, r, G,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,

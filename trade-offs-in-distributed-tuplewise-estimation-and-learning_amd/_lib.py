@@ -201,10 +201,6 @@ _SIGNATURES = {
     "tw_copy_words": [_vp, _i64, _vp, _vp],
     "tw_stage_eval": [_vp, _i32, _vp, _i32, _vp, _vp, _vp],
     "tw_host_device_pointer": [_vp, _vp],
-    "tw_chain_runs_layout": [_i64, _i64, _i64, _i64, _i32, _i32, _vp],
-    "tw_chain_emit_runs": [_vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i64,
-                           _i64, _i32, _vp, _vp, _vp],
-    "tw_count_pairs_chain_runs": [_vp, _i32, _i32, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
     "tw_chain_unpack_exact": [_vp, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "tw_count_pairs_chain_rng": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i64,
                                  _u64, _u64, _vp, _vp],

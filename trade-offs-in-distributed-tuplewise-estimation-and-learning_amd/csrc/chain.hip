@@ -31,7 +31,6 @@
 // Half ties (tie_mode = "half"): an x image is the pair {g(x), h(x)}, h(x) = #{z : z <= x}
 // (tw_rank_images_query with half = 1), and ONE clamped packed add gives [x > z] and [x >= z]
 // for a z: clamp(h(x) - g(z)) == 1 <=> x >= z.  Half units = the sum of both lanes.
-#include <cmath>
 #include "feistel.h"
 #include "pkcount.h"
 #include "records.h"
@@ -78,40 +77,7 @@ struct ChainEmit {
   int64_t cap;
   int* flag;
   int bx;  // blocks of X tiles; the rest are Z tiles
-  // run-table exchange (round 6, tw_chain_emit_runs): strict images only (4 B), one run per
-  // (destination, step, side, destination region); layout of ChainRuns (per_step32 u32 words
-  // per (destination, step) block: [H counts | x runs | z runs])
-  int runs;
-  int64_t per_step32, H, capSx, capTx, capSz, capTz, zoff;
 };
-
-// The run-table layout of one (destination, step) block of a send / receive buffer, in u32
-// words: H counters (x regions 0..nsh, then z regions 0..nsh; padded to 16 words), the x runs
-// (nsh shard runs of capSx, then the tail run of capTx), the z runs likewise; every run starts
-// 16-B aligned.  A run holds the images one source sends one destination region at one step:
-// ~region / G of them (hypergeometric), capacity e + e/8 + 8 sqrt(e) + 32.  Host and device
-// agree through tw_chain_runs_layout.
-struct ChainRuns {
-  int64_t H, capSx, capTx, capSz, capTz, zoff, per_step32;
-};
-__host__ inline int64_t runs_cap(int64_t region, int world) {
-  if (region <= 0) return 0;
-  const double e = (double)region / world;
-  const int64_t c = (int64_t)(e + e / 8 + 8 * std::sqrt(e) + 32);
-  return (std::min<int64_t>(c, region) + 3) & ~(int64_t)3;
-}
-__host__ inline ChainRuns runs_layout(int64_t nx, int64_t nz, int64_t kx, int64_t kz, int nsh,
-                                      int world) {
-  ChainRuns r{};
-  r.H = ((2 * (int64_t)(nsh + 1)) + 15) & ~(int64_t)15;
-  r.capSx = runs_cap(kx, world);
-  r.capTx = runs_cap(nx - (int64_t)nsh * kx, world);
-  r.capSz = runs_cap(kz, world);
-  r.capTz = runs_cap(nz - (int64_t)nsh * kz, world);
-  r.zoff = r.H + (int64_t)nsh * r.capSx + r.capTx;
-  r.per_step32 = (r.zoff + (int64_t)nsh * r.capSz + r.capTz + 15) & ~(int64_t)15;
-  return r;
-}
 
 __device__ __forceinline__ int64_t em_region(int b, uint32_t k, int64_t n) {
   const int64_t o = (int64_t)b * k;
@@ -192,7 +158,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
     }
   }
   const int N = em.nsh;
-  const int NB = em.runs ? em.world * (N + 1) : em.xchg ? em.world : N + 1;
+  const int NB = em.xchg ? em.world : N + 1;
   const uint32_t kb = (uint32_t)(isx ? em.kx : em.kz);
   const FastDiv dk = isx ? em.dkx : em.dkz;
   const FastDiv dn = isx ? em.dnx : em.dnz;
@@ -219,11 +185,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
           if ((valid >> r) & 1u) {
             const uint32_t q = pos[r];
             int b;
-            if (em.runs) {  // (destination, its region of the local position)
-              const uint32_t g = fast_div32(q, dn);
-              const uint32_t ql = q - g * (uint32_t)n;
-              b = (int)g * (N + 1) + (kb == 0 ? N : (int)min(fast_div32(ql, dk), (uint32_t)N));
-            } else if (em.xchg) {
+            if (em.xchg) {
               const uint32_t g = fast_div32(q, dn);
               const uint32_t ql = q - g * (uint32_t)n;
               b = (int)g;
@@ -244,11 +206,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
       const int c = c0 + s;
       const unsigned h = hist[i];
       unsigned* cu;
-      if (em.runs) {
-        const int g = b / (N + 1), rb = b - g * (N + 1);
-        cu = (unsigned*)em.send + ((int64_t)g * em.steps + c) * em.per_step32 +
-             (isx ? 0 : N + 1) + rb;
-      } else if (em.xchg)
+      if (em.xchg)
         cu = (unsigned*)(em.send + ((int64_t)b * em.steps + c) * (em.cap + 1) * em.W);
       else
         cu = em.cur + ((int64_t)c * 2 + (isx ? 0 : 1)) * (N + 1) + b;
@@ -261,17 +219,7 @@ __global__ __launch_bounds__(kEmThreads) void k_chain_emit(ChainEmit em, ChainKe
     auto put = [&](int i, unsigned u, uint64_t v, uint32_t a) {
       const int s = i / NB, b = i - s * NB;
       const int c = c0 + s;
-      if (em.runs) {
-        const int g = b / (N + 1), rb = b - g * (N + 1);
-        const int64_t cap = rb < N ? (isx ? em.capSx : em.capSz) : (isx ? em.capTx : em.capTz);
-        if ((int64_t)u >= cap) {
-          *em.flag = 1;  // dropped, never written out of place; the host raises
-          return;
-        }
-        ((uint32_t*)em.send)[((int64_t)g * em.steps + c) * em.per_step32 +
-                             (isx ? em.H + (int64_t)rb * em.capSx
-                                  : em.zoff + (int64_t)rb * em.capSz) + u] = (uint32_t)v;
-      } else if (em.xchg) {
+      if (em.xchg) {
         if ((int64_t)u >= em.cap) {
           *em.flag = 1;  // dropped, never written out of place; the host raises
           return;
@@ -554,83 +502,6 @@ __global__ __launch_bounds__(kBlock) void k_count_chain(
   }
 }
 
-// the H counters of every (destination, step) block of a run-table send buffer
-__global__ __launch_bounds__(kBlock) void k_chain_zero_runs_heads(uint32_t* __restrict__ send,
-                                                                  int64_t blocks, int64_t stride,
-                                                                  int H) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < blocks * H;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int64_t b = i / H;
-    send[b * stride + (i - b * H)] = 0u;
-  }
-}
-
-// The chunk's counts straight from a run-table receive buffer (no unpack): bag (step c, shard s)
-// is the G x runs and G z runs of region s in the G source blocks of step c.  Work item: (bag,
-// x run gx, x tile tx of 64 R images inside it, z run gz, z chunk cz inside it) — tiles and
-// chunks never cross runs, so count_chain_item reads each as a contiguous range; the run lengths
-// come from the blocks' counters (items past a run's length exit).  Same pairs, same integers
-// as k_count_chain on the unpacked bags.
-template <int R>
-__global__ __launch_bounds__(kBlock) void k_count_chain_runs(
-    const uint32_t* __restrict__ recv, int64_t per_src32, int64_t per_step32, int64_t H,
-    int64_t capSx, int64_t capSz, int64_t zoff, int n_shards, int world, int n_bags,
-    int tiles_x, int zchunks, int64_t z_chunk, unsigned long long* __restrict__ out) {
-  const int per_bag = world * tiles_x * world * zchunks;
-  const int lb = xcd_block(blockIdx.x, gridDim.x);
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int item = lb * (kBlock / kWave) + wid;
-  const int v = item / per_bag;
-  bool active = v < n_bags;
-  const float* xr = nullptr;
-  const float* zr = nullptr;
-  int64_t x0 = 0, xe = 0, z0 = 0, z1 = 0;
-  if (active) {
-    const int c = v / n_shards, s = v - c * n_shards;
-    int rem = item - v * per_bag;
-    const int cz = rem % zchunks;
-    rem /= zchunks;
-    const int gz = rem % world;
-    rem /= world;
-    const int tx = rem % tiles_x;
-    const int gx = rem / tiles_x;
-    const uint32_t* bx = recv + (int64_t)gx * per_src32 + (int64_t)c * per_step32;
-    const uint32_t* bz = recv + (int64_t)gz * per_src32 + (int64_t)c * per_step32;
-    xe = (int64_t)min(bx[s], (uint32_t)capSx);
-    const int64_t nz = (int64_t)min(bz[n_shards + 1 + s], (uint32_t)capSz);
-    xr = (const float*)(bx + H + (int64_t)s * capSx);
-    zr = (const float*)(bz + zoff + (int64_t)s * capSz);
-    x0 = (int64_t)tx * (kWave * R);
-    z0 = (int64_t)cz * z_chunk;
-    z1 = z0 + z_chunk < nz ? z0 + z_chunk : nz;
-    active = x0 < xe && z0 < z1;
-  }
-  unsigned long long tot = 0;
-  if (active) tot = count_chain_item<R, false>(xr, x0, xe, zr, z0, z1, lane);
-  __shared__ unsigned long long part[kBlock / kWave];
-  __shared__ int part_v[kBlock / kWave];
-  if (lane == 0) {
-    part[wid] = tot;
-    part_v[wid] = active ? v : -1;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int cur = part_v[0];
-    unsigned long long sum = part[0];
-#pragma unroll
-    for (int w = 1; w < kBlock / kWave; ++w) {
-      if (part_v[w] != cur) {
-        if (cur >= 0 && sum) atomicAdd(out + cur, sum);
-        cur = part_v[w];
-        sum = 0;
-      }
-      sum += part[w];
-    }
-    if (cur >= 0 && sum) atomicAdd(out + cur, sum);
-  }
-}
-
 // ----------------------------------------------------------------------------- final order
 // One process: the scores at the chains' last positions, out[pos[e]] = in[e] (8-B values).
 __global__ __launch_bounds__(kBlock) void k_chain_scatter(const uint64_t* __restrict__ xin,
@@ -749,14 +620,6 @@ static ChainKeys chain_keys(const uint64_t* kx, const uint64_t* kz, int steps) {
 
 using namespace tw;
 
-static int chain_emit_impl(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec,
-                           int64_t n_z, int32_t half, uint32_t* d_x_pos, uint32_t* d_z_pos,
-                           int32_t first, int32_t rank, int32_t world, const uint64_t* keys_x,
-                           const uint64_t* keys_z, int32_t steps, int64_t x_shard,
-                           int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
-                           uint32_t* d_cursors, uint64_t* d_send, int64_t cap, int32_t* d_flag,
-                           int runs, void* stream);
-
 extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec,
                              int64_t n_z, int32_t half, uint32_t* d_x_pos, uint32_t* d_z_pos,
                              int32_t first, int32_t rank, int32_t world, const uint64_t* keys_x,
@@ -764,49 +627,6 @@ extern "C" int tw_chain_emit(const uint64_t* d_x_rec, int64_t n_x, const uint64_
                              int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
                              uint32_t* d_cursors, uint64_t* d_send, int64_t cap,
                              int32_t* d_flag, void* stream) {
-  return chain_emit_impl(d_x_rec, n_x, d_z_rec, n_z, half, d_x_pos, d_z_pos, first, rank, world,
-                         keys_x, keys_z, steps, x_shard, z_shard, n_shards, d_x_bag, d_z_bag,
-                         d_cursors, d_send, cap, d_flag, 0, stream);
-}
-
-// The run-table layout (ChainRuns) as out[0..6] = H, capSx, capTx, capSz, capTz, zoff,
-// per_step32 (u32 words) for every rank's local sizes n_x / n_z, shard sizes and world.
-extern "C" int tw_chain_runs_layout(int64_t n_x, int64_t n_z, int64_t x_shard, int64_t z_shard,
-                                    int32_t n_shards, int32_t world, int64_t* out) {
-  TW_ARG_CHECK(n_x >= 0 && n_z >= 0 && x_shard >= 0 && z_shard >= 0 && n_shards >= 0 &&
-                   world >= 1 && out != nullptr && (int64_t)n_shards * x_shard <= n_x &&
-                   (int64_t)n_shards * z_shard <= n_z,
-               "tw_chain_runs_layout: bad sizes (every shard full: n_shards * shard <= n)");
-  const ChainRuns r = runs_layout(n_x, n_z, x_shard, z_shard, n_shards, world);
-  const int64_t v[7] = {r.H, r.capSx, r.capTx, r.capSz, r.capTz, r.zoff, r.per_step32};
-  for (int i = 0; i < 7; ++i) out[i] = v[i];
-  return TW_OK;
-}
-
-// tw_chain_emit's exchange with a run-table send buffer (strict images): every image lands in
-// the run of its (destination, step, destination region); the receiver counts the runs in place
-// (tw_count_pairs_chain_runs), no unpack.  d_send: world * steps * per_step32 u32 words.
-extern "C" int tw_chain_emit_runs(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec,
-                                  int64_t n_z, uint32_t* d_x_pos, uint32_t* d_z_pos,
-                                  int32_t first, int32_t rank, int32_t world,
-                                  const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
-                                  int64_t x_shard, int64_t z_shard, int32_t n_shards,
-                                  uint32_t* d_send, int32_t* d_flag, void* stream) {
-  TW_ARG_CHECK(d_send != nullptr && d_flag != nullptr, "tw_chain_emit_runs: send and flag");
-  TW_ARG_CHECK((int64_t)n_shards * x_shard <= n_x && (int64_t)n_shards * z_shard <= n_z,
-               "tw_chain_emit_runs: every shard full (n_shards * shard <= n)");
-  return chain_emit_impl(d_x_rec, n_x, d_z_rec, n_z, 0, d_x_pos, d_z_pos, first, rank, world,
-                         keys_x, keys_z, steps, x_shard, z_shard, n_shards, nullptr, nullptr,
-                         nullptr, (uint64_t*)d_send, 1, d_flag, 1, stream);
-}
-
-static int chain_emit_impl(const uint64_t* d_x_rec, int64_t n_x, const uint64_t* d_z_rec,
-                           int64_t n_z, int32_t half, uint32_t* d_x_pos, uint32_t* d_z_pos,
-                           int32_t first, int32_t rank, int32_t world, const uint64_t* keys_x,
-                           const uint64_t* keys_z, int32_t steps, int64_t x_shard,
-                           int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
-                           uint32_t* d_cursors, uint64_t* d_send, int64_t cap, int32_t* d_flag,
-                           int runs, void* stream) {
   TW_ARG_CHECK(n_x >= 0 && n_z >= 0 && world >= 1 && rank >= 0 && rank < world &&
                    steps >= 0 && steps <= kChainMax && n_shards >= 0 && x_shard >= 0 &&
                    z_shard >= 0 && (half == 0 || half == 1) && (first == 0 || first == 1),
@@ -816,10 +636,8 @@ static int chain_emit_impl(const uint64_t* d_x_rec, int64_t n_x, const uint64_t*
   // the exchange mode is chosen by the send buffer, not by world > 1: a world-size-1 process
   // group can be forced through the collectives' path (ShardedSample(collectives=True))
   const bool xchg = d_send != nullptr;
-  TW_ARG_CHECK((runs ? (int64_t)world * (n_shards + 1) : xchg ? world : n_shards + 1) <=
-                   kEmMaxBig,
-               "tw_chain_emit: at most %d buckets (shards + 1, ranks, or ranks x (shards + 1))",
-               kEmMaxBig);
+  TW_ARG_CHECK((xchg ? world : n_shards + 1) <= kEmMaxBig,
+               "tw_chain_emit: at most %d buckets (shards + 1, or ranks)", kEmMaxBig);
   TW_ARG_CHECK(steps == 0 || (keys_x != nullptr && keys_z != nullptr),
                "tw_chain_emit: keys missing");
   if (steps == 0 || n_x + n_z == 0) return TW_OK;
@@ -861,23 +679,7 @@ static int chain_emit_impl(const uint64_t* d_x_rec, int64_t n_x, const uint64_t*
   em.send = d_send;
   em.cap = cap;
   em.flag = d_flag;
-  em.runs = runs;
-  if (runs) {
-    const ChainRuns rl = runs_layout(n_x, n_z, x_shard, z_shard, n_shards, world);
-    em.per_step32 = rl.per_step32;
-    em.H = rl.H;
-    em.capSx = rl.capSx;
-    em.capTx = rl.capTx;
-    em.capSz = rl.capSz;
-    em.capTz = rl.capTz;
-    em.zoff = rl.zoff;
-    const int64_t blocks = (int64_t)world * steps;
-    hipLaunchKernelGGL(k_chain_zero_runs_heads,
-                       dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(
-                           1024, ceil_div(blocks * rl.H, kBlock)))),
-                       dim3(kBlock), 0, st, (uint32_t*)d_send, blocks, rl.per_step32,
-                       (int)rl.H);
-  } else if (xchg) {
+  if (xchg) {
     const int64_t buckets = (int64_t)world * steps;
     hipLaunchKernelGGL(k_chain_zero_heads, dim3((unsigned)ceil_div(buckets, kBlock)),
                        dim3(kBlock), 0, st, d_send, buckets, (cap + 1) * em.W);
@@ -886,7 +688,7 @@ static int chain_emit_impl(const uint64_t* d_x_rec, int64_t n_x, const uint64_t*
                                sizeof(unsigned) * (size_t)steps * 2 * (n_shards + 1), st));
   }
   const ChainKeys k = chain_keys(keys_x, keys_z, steps);
-  const int NB = runs ? world * (n_shards + 1) : xchg ? world : n_shards + 1;
+  const int NB = xchg ? world : n_shards + 1;
   auto launch = [&](auto epr, auto spr, auto staged) {
     constexpr int EPR = decltype(epr)::value, S = decltype(spr)::value;
     constexpr bool ST = decltype(staged)::value;
@@ -998,44 +800,6 @@ extern "C" int tw_chain_unpack_exact(const uint64_t* d_recv, int32_t world, int3
   hipLaunchKernelGGL(k_chain_unpack_exact, dim3((unsigned)(parts * world * steps)), dim3(kBlock),
                      0, (hipStream_t)stream, d_recv, (int)world, (int)steps, parts, cap, n_x, n_z,
                      (uint32_t*)d_x_bag, (uint32_t*)d_z_bag, d_flag);
-  TW_LAUNCH_CHECK();
-  return TW_OK;
-}
-
-// The chunk's counts from a run-table receive buffer (tw_chain_emit_runs' layout from every
-// source; world source blocks of steps x per_step32 u32 words), strict images: out [steps][n]
-// (zeroed here).  Same integers as tw_count_pairs_chain on the unpacked bags.
-extern "C" int tw_count_pairs_chain_runs(const uint32_t* d_recv, int32_t world, int32_t steps,
-                                         int64_t n_x, int64_t n_z, int64_t x_shard,
-                                         int64_t z_shard, int32_t n_shards, uint64_t* d_out,
-                                         void* stream) {
-  TW_ARG_CHECK(world >= 1 && steps >= 0 && n_shards >= 0 && x_shard >= 0 && z_shard >= 0 &&
-                   (int64_t)n_shards * x_shard <= n_x && (int64_t)n_shards * z_shard <= n_z,
-               "tw_count_pairs_chain_runs: bad sizes");
-  TW_ARG_CHECK(z_shard < (1ll << 24), "tw_count_pairs_chain_runs: shards of < 2^24 z-images");
-  hipStream_t st = (hipStream_t)stream;
-  const int64_t bags = (int64_t)n_shards * steps;
-  if (bags == 0) return TW_OK;
-  TW_ARG_CHECK(d_recv != nullptr && d_out != nullptr, "tw_count_pairs_chain_runs: buffers");
-  TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)bags, st));
-  const ChainRuns rl = runs_layout(n_x, n_z, x_shard, z_shard, n_shards, world);
-  if (rl.capSx == 0 || rl.capSz == 0) return TW_OK;
-  constexpr int R = 8;
-  const int tiles_x = (int)ceil_div(rl.capSx, (int64_t)kWave * R);
-  // z chunks as plan_chain sizes them (~150 work items per SIMD, >= 600 images), per run
-  const int64_t base = (int64_t)world * tiles_x * world * bags;
-  int64_t zc = std::max<int64_t>(
-      kChainMinZ, ceil_div(rl.capSz, std::max<int64_t>(1, ceil_div(kChainItems, base))));
-  const int64_t z_chunk = ceil_div(std::min<int64_t>(zc, rl.capSz), 8) * 8;
-  const int zchunks = (int)ceil_div(rl.capSz, z_chunk);
-  const int64_t items = base * zchunks;
-  TW_ARG_CHECK(items < (1ll << 31) && (int64_t)world * tiles_x * world * zchunks < (1ll << 31),
-               "tw_count_pairs_chain_runs: grid too large");
-  const int64_t blocks = ceil_div(items, kBlock / kWave);
-  hipLaunchKernelGGL(k_count_chain_runs<R>, dim3((unsigned)blocks), dim3(kBlock), 0, st, d_recv,
-                     (int64_t)steps * rl.per_step32, rl.per_step32, rl.H, rl.capSx, rl.capSz,
-                     rl.zoff, (int)n_shards, (int)world, (int)bags, tiles_x, zchunks, z_chunk,
-                     (unsigned long long*)d_out);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

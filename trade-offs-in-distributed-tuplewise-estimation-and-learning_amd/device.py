@@ -55,10 +55,6 @@ CHAIN_SUB = 0
 # skips the ranking (and over ranks the Z all-gather it waits for).  Any assignment of X / Z or
 # an in-place change (the tensors' version counters) drops them.
 CARRY_IMAGES = True
-# over ranks, the complete strict count's exchange as a RUN TABLE (tw_chain_emit_runs /
-# tw_count_pairs_chain_runs: each image sent into the run of its (destination, step, shard), the
-# receiver counting the runs in place) instead of {image, position} records and an unpack
-CHAIN_RUNS = True
 # UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
 # exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
 CHAIN_RNG = True
@@ -247,31 +243,6 @@ class HipOps:
         L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
                int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
                L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
-
-    def runs_layout(self, n, m, kx, kz, n_shards, world):
-        """The run-table layout (tw_chain_runs_layout): H, capSx, capTx, capSz, capTz, zoff,
-        per_step32 in u32 words."""
-        out = np.zeros(7, dtype=np.int64)
-        L.call("tw_chain_runs_layout", int(n), int(m), int(kx), int(kz), int(n_shards),
-               int(world), out.ctypes.data)
-        return [int(v) for v in out]
-
-    def chain_emit_runs(self, xr, zr, xpos, zpos, first, rank, world, keys_x, keys_z, kx, kz,
-                        n_shards, send, flag):
-        """tw_chain_emit into a run-table send buffer (tw_chain_emit_runs)."""
-        kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
-        kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
-        L.call("tw_chain_emit_runs", L.ptr(xr), int(xr.numel()), L.ptr(zr), int(zr.numel()),
-               L.ptr(xpos), L.ptr(zpos), int(bool(first)), int(rank), int(world),
-               kxa.ctypes.data, kza.ctypes.data, len(kxa), int(kx), int(kz), int(n_shards),
-               L.ptr(send), L.ptr(flag), L.stream_handle())
-
-    def count_chain_runs(self, recv, world, steps, n, m, kx, kz, n_shards, out):
-        """The bags' counts from a run-table receive buffer in place (tw_count_pairs_chain_runs),
-        out (steps, n_shards)."""
-        L.call("tw_count_pairs_chain_runs", L.ptr(recv), int(world), int(steps), int(n), int(m),
-               int(kx), int(kz), int(n_shards), L.ptr(out), L.stream_handle())
-        return out
 
     def chain_unpack_exact(self, recv, world, steps, cap, n, m, x_bag, z_bag, flag):
         """The received records written at their exact positions of the step bags
@@ -1095,14 +1066,8 @@ class ShardedSample:
             else:
                 ops.count_chain(xb, self.x_off_dev, zb, self.z_off_dev, N, steps, n, m,
                                 self.max_nx, self.max_nz, half, out)
-        # the run-table exchange (CHAIN_RUNS): the complete strict count reads the received runs
-        # in place — no unpack launch, 4-B images instead of 8-B records on the wire
-        runs = (coll and CHAIN_RUNS and rng is None and not bucket and not half
-                and CHAIN_SUB == 0 and hasattr(ops, "chain_emit_runs")
-                and N * kx <= n and N * kz <= m)
-        if not runs:
-            x_bag = self._work("x_bag", (C, n), t.int64 if half else t.float32)
-            z_bag = self._work("z_bag", (C, m), t.float32)
+        x_bag = self._work("x_bag", (C, n), t.int64 if half else t.float32)
+        z_bag = self._work("z_bag", (C, m), t.float32)
         xpos = self._work("xpos", (n,), t.int32)
         zpos = self._work("zpos", (m,), t.int32)
         counts = t.empty((T, N), dtype=t.int64, device=dev)
@@ -1120,32 +1085,18 @@ class ShardedSample:
             # GB-scale allocations per call made the caching allocator flush and re-map)
             rk = (G, Sub, cap, W, nsub)
             ring = getattr(self, "_chain_ring", None)
-            if not runs and (ring is None or ring[0] != rk):
+            if ring is None or ring[0] != rk:
                 self._chain_ring = None  # release the old ring first
                 sends = [t.empty((G * Sub * (cap + 1) * W,), dtype=t.int64, device=dev)
                          for _ in range(nsub)]
                 self._chain_ring = ring = (rk, sends, [t.empty_like(b) for b in sends])
-            if not runs:
-                sends, recvs = ring[1], ring[2]
+            sends, recvs = ring[1], ring[2]
             if getattr(self, "_chain_flag", None) is None:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
-            if runs:
-                ps = ops.runs_layout(n, m, kx, kz, N, G)[6]
-                rsend = self._work("runs_send", (G * C * ps,), t.int32)
-                rrecv = self._work("runs_recv", (G * C * ps,), t.int32)
         else:
             cursors = self._work("cursors", (C * 2 * (N + 1),), t.int32)
         for i0 in range(0, T, C):
             c = min(C, T - i0)
-            if runs:
-                ops.chain_emit_runs(xr, zr, xpos, zpos, i0 == 0, r, G, kxs[i0:i0 + c],
-                                    kzs[i0:i0 + c], kx, kz, N, rsend, self._chain_flag)
-                sz = G * c * ps
-                work = self._all_to_all(rrecv[:sz], rsend[:sz], async_op=True)
-                if work is not None:
-                    work.wait()
-                ops.count_chain_runs(rrecv, G, c, n, m, kx, kz, N, counts[i0:i0 + c])
-                continue
             if coll:
                 # with sub-chunks, the emissions (and the all-to-alls issued behind them) on a
                 # side stream, so sub-chunk j+1's emission runs beside sub-chunk j's count; the
