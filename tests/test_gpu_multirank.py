@@ -61,13 +61,15 @@ def _problem():
                          [(2, m, la, None) for m in ("replay", "device")
                           for la in ("replicated", "partitioned")]
                          + [(3, "replay", "replicated", None), (3, "device", "partitioned", None),
-                            (2, "device", "replicated", True), (3, "replay", "partitioned", True)])
+                            (2, "device", "replicated", True), (3, "replay", "partitioned", True),
+                            (8, "device", "replicated", None)])
 def test_learning_two_ranks_equals_one(gpu, G, mode, layout, cols):
     """G ranks (gloo) on the box's GPU equal one rank bit for bit — with a trajectory (the
     per-step peer exchange) and without (the persistent peer segment, three evaluations).
     G = 3: N = 8 shards split 2/3/3 (uneven splits, the reference's N = 100 over 8 GPUs).
     cols=True: the per-step exchange by column owners (tw_peer_step_cols; d = 8 over 3 ranks
-    gives owners of 2, 3 and 3 columns)."""
+    gives owners of 2, 3 and 3 columns); G = 8 with the default (column owners from 8 ranks:
+    one shard and one column per rank) — the driver's 8-GPU learning lines' exchange."""
     import torch.multiprocessing as mp
     import tuplewise.learning as lr
     X, Z, w0, p = _problem()
