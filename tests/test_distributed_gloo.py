@@ -713,3 +713,28 @@ def test_carried_images_over_ranks(G, mode):
         want.append(float(S1.UnN(k)))
     assert out["vals"] == want
     assert np.array_equal(out["X"], S1.X.numpy()) and np.array_equal(out["Z"], S1.Z.numpy())
+
+
+def test_one_process_carried_images_checksum_verdict():
+    """The one-process branch of the carried images' guard (device.py _chain_call): the hash
+    verdict lands in a host word read after the counts; a write through `.data` between calls
+    (no version bump) makes the call recount from a fresh ranking — estimates and arrays equal
+    a fresh sample's on the written arrays; an untouched sample keeps carrying, no recount."""
+    import tuplewise  # noqa: F401
+    from tuplewise.device import ShardedSample
+    X, Z = _global_data(1, 1800, 1350)
+    for write in (False, True):
+        S = ShardedSample(torch.from_numpy(X.copy()), torch.from_numpy(Z.copy()), 9,
+                          ops=OracleOpsChain(), algo="pairs")
+        S.UnN_many([5, 6, 9])
+        assert S._carried(False) is not None
+        if write:
+            S.X.data[[0, 7]] = S.X.data[[7, 0]].clone()
+            S.Z.data[:40] += 0.25
+        Xw, Zw = S.X.clone(), S.Z.clone()
+        got = [float(v) for v in S.UnN_many([2, 7, 8])]
+        assert getattr(S, "stale_recounts", 0) == (1 if write else 0)
+        F = ShardedSample(Xw, Zw, 9, ops=OracleOps(), algo="pairs")
+        assert got == [float(F.UnN(k)) for k in (2, 7, 8)]
+        assert np.array_equal(S.X.numpy(), F.X.numpy()) and np.array_equal(S.Z.numpy(),
+                                                                            F.Z.numpy())
