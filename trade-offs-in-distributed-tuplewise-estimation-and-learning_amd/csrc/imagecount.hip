@@ -605,6 +605,23 @@ extern "C" int tw_count_pairs_chain_rng(const float* d_x_bag, const int64_t* d_x
                           TW_PRED_GT, (B + 1) / 2);
   TW_ARG_CHECK(p.ok, "tw_count_pairs_chain_rng: a shard's images exceed the LDS (%lld + %lld)",
                (long long)max_nx, (long long)max_nz);
+  // blocks per bag: one 1024-thread block per CU holds a bag's images, so the grid runs in
+  // waves of ~256 blocks; pick the split that minimises waves x (a block's draws + its staging,
+  // ~5k draws' worth) — 160 bags (G = 8, T = 20): 8 blocks a bag (5 full waves) rather than 2
+  // (a second wave of 64 blocks as long as the first)
+  {
+    const int64_t nq = (B + 1) / 2;
+    double best = -1.0;
+    for (int parts = 1; parts <= 64; ++parts) {
+      if (parts > 1 && nq / parts < 4096) break;
+      const double waves = (double)ceil_div(nbags * parts, 256);
+      const double cost = waves * ((double)ceil_div(nq, parts) + 2500.0);
+      if (best < 0 || cost < best) {
+        best = cost;
+        p.parts = parts;
+      }
+    }
+  }
   TW_ARG_CHECK(nbags * p.parts < (1ll << 31), "tw_count_pairs_chain_rng: grid too large");
   static bool attr = false;
   if (!attr) {
