@@ -1254,6 +1254,10 @@ def main():
     # cs.UnNBT's loop, device-RNG draws): pairs/s and the k_count_rng roofline
     ops.count_rng = kernel_ms.wrap(ops.count_rng)
     ops.count_rng_step = kernel_ms.wrap(ops.count_rng_step)  # count + next repartition
+    # over ranks (round 6) UnNB_many walks the step chains: one tw_count_pairs_chain_rng launch
+    # counts every step of a chunk (weight = its steps, so kernel_ms stays per step)
+    inc_chain = bool(S.coll and S._chain_rng_ok())
+    ops.count_chain_rng = kernel_ms.wrap(ops.count_chain_rng, weight=lambda *a, **k: a[5])
     B_inc = args.incomplete_B
     S.UnNB_many(B_inc, 5, range(30_000, 30_000 + args.warmup))
     torch.cuda.synchronize()
@@ -1268,9 +1272,10 @@ def main():
         tt = torch.tensor([dt_inc], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt_inc = float(tt.item())
-    kms_inc = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms.used()]))
+    kms_inc = kernel_ms.ms_per_unit()
     ops.count_rng = ops.count_rng.__wrapped__
     ops.count_rng_step = ops.count_rng_step.__wrapped__
+    ops.count_chain_rng = ops.count_chain_rng.__wrapped__
     inc_pairs_rank = shards * B_inc
     progress("incomplete replay")
     inc_replay = incomplete_replay(X, Z, shards, B_inc)
@@ -1474,13 +1479,16 @@ def main():
         "incomplete": {
             "note": "UnNBT loop (compute_stats.py:104-123): a device repartition + B device-"
                     "drawn pairs per shard (Philox4x32-10, two pairs per block, Lemire maps) "
-                    "counted per step on float32 score images in LDS; one launch per step "
-                    "(the next repartition rides in the count threads)",
+                    + ("counted on the step chains' exact-position rank-image bags, one "
+                       "exchange and one count launch per chunk (tw_count_pairs_chain_rng)"
+                       if inc_chain else
+                       "counted per step on float32 score images in LDS; one launch per step "
+                       "(the next repartition rides in the count threads)"),
             "B_per_shard": B_inc, "value": inc_pairs_rank * world * args.steps / dt_inc,
             "unit": "pairs/s", "ms_per_step": dt_inc / args.steps * 1e3,
             "estimate_last_step": float(est_inc),
             "roofline": {"bound": "valu",
-                         "kernel": "k_count_rng_img",
+                         "kernel": "k_count_rng_chain" if inc_chain else "k_count_rng_img",
                          "frac_vs_int32_op_peak": INC_LANE_OPS * inc_pairs_rank / (kms_inc * 1e-3)
                          / INT_LANE_OPS_MEASURED,
                          "int32_op_peak": INT_LANE_OPS_MEASURED / 1e12,
@@ -1491,7 +1499,9 @@ def main():
                          "kernel_ms": kms_inc,
                          "note": f"{INC_LANE_OPS} lane-ops per pair (SURVEY.md §8(d) contract "
                                  "constant: 2 Philox4x32-10 words + 2 range maps + 1 compare); "
-                                 "kernel_ms = the whole tw_count_pairs_rng_step call (one "
+                                 "kernel_ms = per step: over ranks the chunk's "
+                                 "tw_count_pairs_chain_rng launch / its steps; in one process "
+                                 "the whole tw_count_pairs_rng_step call (one "
                                  "kernel: float32 score images in LDS, Philox draws, compares, "
                                  "and the next repartition's gathers in the same threads); "
                                  "frac is against the f64 lane-op "
