@@ -55,10 +55,6 @@ CHAIN_SUB = 0
 # skips the ranking (and over ranks the Z all-gather it waits for).  Any assignment of X / Z or
 # an in-place change (the tensors' version counters) drops them.
 CARRY_IMAGES = True
-# one process: a call of at least CHAIN_OVERLAP_MIN steps runs as two or more chunks whose
-# emissions go on a side stream, so chunk j + 1's emission overlaps chunk j's count
-CHAIN_OVERLAP = True
-CHAIN_OVERLAP_MIN = 8
 # UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
 # exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
 CHAIN_RNG = True
@@ -1099,24 +1095,6 @@ class ShardedSample:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
         else:
             cursors = self._work("cursors", (C * 2 * (N + 1),), t.int32)
-        # one process, a call of CHAIN_OVERLAP_MIN or more steps: at least two chunks, chunk
-        # j + 1's emission on a side stream while chunk j is counted (double-buffered bags)
-        overlap = (not coll and CHAIN_OVERLAP and self.X.is_cuda and T >= CHAIN_OVERLAP_MIN)
-        if overlap:
-            if C == T:  # split the call's steps into two chunks
-                C = -(-T // 2)
-                x_bag = x_bag[:C]
-                z_bag = z_bag[:C]
-            bufs = [(x_bag, z_bag, cursors),
-                    (self._work("x_bag_b", (C, n), t.int64 if half else t.float32),
-                     self._work("z_bag_b", (C, m), t.float32),
-                     self._work("cursors_b", (C * 2 * (N + 1),), t.int32))]
-            ev_count = [None, None]
-            main = t.cuda.current_stream()
-            if getattr(self, "_emit_stream", None) is None:
-                self._emit_stream = t.cuda.Stream()
-            es = self._emit_stream
-            es.wait_stream(main)
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             if coll:
@@ -1152,29 +1130,10 @@ class ShardedSample:
                     count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs],
                           i0 + a)
                 continue
-            if overlap:
-                # chunk j's emission on the side stream into buffer pair j % 2, after the count
-                # of chunk j - 2 (the pair's last reader); the main stream counts it after it
-                b = (i0 // C) % 2
-                xb, zb, cu = bufs[b]
-                with t.cuda.stream(es):
-                    if ev_count[b] is not None:
-                        es.wait_event(ev_count[b])
-                    ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
-                                   kzs[i0:i0 + c], kx, kz, N, x_bag=xb, z_bag=zb, cursors=cu)
-                    ev = t.cuda.Event()
-                    ev.record(es)
-                main.wait_event(ev)
-                count(xb, zb, c, counts[i0:i0 + c], i0)
-                ev_count[b] = t.cuda.Event()
-                ev_count[b].record(main)
-                continue
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
             count(x_bag, z_bag, c, counts[i0:i0 + c], i0)
-        if overlap:
-            main.wait_stream(es)
         carry = None
         if coll:
             if final is not None:
