@@ -897,6 +897,22 @@ int tw_copy_words(const void* d_in, int64_t n, void* d_out, void* stream);
  * launch into h_out, pinned host memory of nres + nw + 1 8-byte words. */
 int tw_stage_eval(const void* d_res, int32_t nres, const void* d_w, int32_t nw,
                   const uint32_t* d_ctl, void* h_out, void* stream);
+/* The call's final arrays over ranks by ONE exchange (round 6): tw_chain_final_pack packs this
+ * rank's walked elements — scores d_x / d_z, rank-image records d_x_rec / d_z_rec, final global
+ * positions d_x_pos / d_z_pos (the chains' state after the call's last emission), n_x / n_z a
+ * rank — into world buckets of 1 + cap 24-B records {score, record, local position; z: n_x +
+ * position} (d_send: world * (cap + 1) * 3 u64; d_cursor: world u64, zero on entry, left
+ * zero); after an equal-split all-to-all tw_chain_final_scatter writes every received record
+ * at its position of d_x_out / d_x_rec_out / d_z_out / d_z_rec_out (n_x / n_z 8-B words).
+ * Replaces est.UnNT's final in-place arrays (main.py:46-47) gathered by inverse chains from
+ * all-gathered samples.  Overflows raise *d_flag. */
+int tw_chain_final_pack(const void* d_x, const uint64_t* d_x_rec, const uint32_t* d_x_pos,
+                        int64_t n_x, const void* d_z, const uint64_t* d_z_rec,
+                        const uint32_t* d_z_pos, int64_t n_z, int32_t world, int64_t cap,
+                        uint64_t* d_cursor, void* d_send, int32_t* d_flag, void* stream);
+int tw_chain_final_scatter(const void* d_recv, int32_t world, int64_t cap, int64_t n_x,
+                           int64_t n_z, void* d_x_out, void* d_x_rec_out, void* d_z_out,
+                           void* d_z_rec_out, int32_t* d_flag, void* stream);
 /* The incomplete statistic on the step chains over ranks (cs.UnNBT, compute_stats.py:119-123,
  * with device-RNG draws): tw_chain_unpack_exact writes every received record {image, local
  * position} of a chunk's (source, step) buckets (tw_chain_emit's exchange layout, strict

@@ -257,6 +257,44 @@ class OracleOpsChain(OracleOpsRank):
         Zo.numpy()[zpos.numpy().view(np.uint32)] = Z.numpy()
         return Xo, Zo
 
+    def chain_final_pack(self, X, xr, xpos, Z, zr, zpos, world, cap, cursor, send, flag):
+        """tw_chain_final_pack restated: {score, record, local position} records of the walked
+        elements into the buckets of the ranks holding their final positions (a header record
+        with the count first; order inside a bucket is free)."""
+        n, m = X.numel(), Z.numel()
+        buf = send.numpy().view(np.uint64).reshape(world, cap + 1, 3)
+        buf[:, 0, :] = 0
+        recs = []
+        for A, R, P, nl, off in ((X, xr, xpos, n, 0), (Z, zr, zpos, m, n)):
+            p = P.numpy().view(np.uint32).astype(np.int64)
+            recs.append((p // nl, A.numpy().view(np.uint64), R.numpy().view(np.uint64),
+                         (p % nl + off).astype(np.uint64)))
+        dst, val, rec, pos = (np.concatenate(c) for c in zip(*recs))
+        for g in range(world):
+            sel = np.flatnonzero(dst == g)
+            buf[g, 0, 0] = len(sel)
+            if len(sel) > cap:
+                flag.numpy()[0] = 1
+                sel = sel[:cap]
+            buf[g, 1:1 + len(sel), 0] = val[sel]
+            buf[g, 1:1 + len(sel), 1] = rec[sel]
+            buf[g, 1:1 + len(sel), 2] = pos[sel]
+
+    def chain_final_scatter(self, recv, world, cap, n, m, Xo, XRo, Zo, ZRo, flag):
+        """tw_chain_final_scatter restated."""
+        buf = recv.numpy().view(np.uint64).reshape(world, cap + 1, 3)
+        for g in range(world):
+            c = int(buf[g, 0, 0])
+            if c > cap:
+                flag.numpy()[0] = 1
+            r = buf[g, 1:1 + min(c, cap)]
+            p = r[:, 2].astype(np.int64)
+            isx = p < n
+            Xo.numpy().view(np.uint64)[p[isx]] = r[isx, 0]
+            XRo.numpy().view(np.uint64)[p[isx]] = r[isx, 1]
+            Zo.numpy().view(np.uint64)[p[~isx] - n] = r[~isx, 0]
+            ZRo.numpy().view(np.uint64)[p[~isx] - n] = r[~isx, 1]
+
     def chain_unpack_exact(self, recv, world, steps, cap, n, m, x_bag, z_bag, flag):
         """tw_chain_unpack_exact restated: every record at its exact position of its bag."""
         buf = recv.numpy().view(np.uint64)

@@ -120,19 +120,27 @@ def rank_call(G, r, K, parts=False, carried=False):
     fs = torch.cuda.Stream()
     xr_c, zr_c = XR[r * nl:(r + 1) * nl], ZR[r * nl:(r + 1) * nl]
 
-    def side_work():
-        # the product: the async all-gathers, then the inverse-chain gathers of the scores
-        # (and of the records when they are carried) on a side stream beside the counts
+    # round 6 (device.FINAL_EXCHANGE): the final arrays and carried records by one exchange of
+    # the walked elements, forked on the side stream once the last emission has run
+    tot = 2 * nl
+    fcap = max(1, tot // G + tot // (8 * G) + 1024)
+    fsend = torch.empty(G * (fcap + 1) * 3, dtype=torch.int64, device="cuda")
+    frecv = torch.empty_like(fsend)
+    fcur = torch.zeros(G, dtype=torch.int64, device="cuda")
+    Xf, Zf = torch.empty_like(xq), torch.empty_like(zq)
+    RXf, RZf = torch.empty(nl, dtype=torch.int64, device="cuda"), torch.empty(
+        nl, dtype=torch.int64, device="cuda")
+
+    def final_exchange(xr, zr):
+        ops.chain_final_pack(xq, xr, xpos, zq, zr, zpos, G, fcap, fcur, fsend, flag)
+        frecv.copy_(fsend)  # the all-to-all (device copy)
+        ops.chain_final_scatter(frecv, G, fcap, nl, nl, Xf, RXf, Zf, RZf, flag)
+
+    def side_work(xr, zr):
         main = torch.cuda.current_stream()
         fs.wait_stream(main)
         with torch.cuda.stream(fs):
-            Xg.copy_(X)
-            if carried:
-                Zg.copy_(Z)
-            RXg.copy_(XR)
-            RZg.copy_(ZR)
-            # one walk of the inverse chains for scores and records (tw_chain_gather2, r06)
-            ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs, RXg, RZg)
+            final_exchange(xr, zr)
 
     def call():
         main = torch.cuda.current_stream()
@@ -142,8 +150,10 @@ def rank_call(G, r, K, parts=False, carried=False):
             if G > 1:  # the Z all-gather the ranking waits for
                 mark("all-gather Z (device copy)", lambda: Zg.copy_(Z))
             xr, zr = mark("ranking", lambda: ops.rank_images_query(Z, xq, zq, L.TW_F64))
-        if G > 1:
-            side_work()
+        if G > 1 and carried:  # every rank's async Z all-gather (device copy)
+            fs.wait_stream(main)
+            with torch.cuda.stream(fs):
+                Zg.copy_(Z)
         for i0 in range(0, K, C):
             c = min(C, K - i0)
             first = i0 == 0
@@ -156,6 +166,12 @@ def rank_call(G, r, K, parts=False, carried=False):
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                     send=send, cap=cap, flag=flag))
                 sz = G * c * (cap + 1)
+                if i0 + c >= K:  # the final exchange beside the last chunk's count
+                    if parts:
+                        mark("final exchange (side stream in the product)",
+                             lambda: final_exchange(xr, zr))
+                    else:
+                        side_work(xr, zr)
                 mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
                 mark("unpack", lambda: ops.chain_unpack(recv, G, c, cap, False, nl, nl, x_bag,
                                                         z_bag, flag, kx, kz, Nl))

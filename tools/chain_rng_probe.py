@@ -134,11 +134,20 @@ def chain_call(G, r, T, carried, parts=False):
         t.setdefault(name, []).append((e0, e1))
         return out
 
-    def final():
-        Xg.copy_(X)
-        RXg.copy_(XR)
-        RZg.copy_(ZR)
-        ops.chain_gather(Xg, Zg, r * nl, nl, r * nl, nl, kxs, kzs, RXg, RZg)
+    # round 6 (device.FINAL_EXCHANGE): the final arrays and carried records by one exchange
+    # of the walked elements, forked on the side stream once the last emission has run
+    fcap = max(1, tot // G + tot // (8 * G) + 1024)
+    fsend = torch.empty(G * (fcap + 1) * 3, dtype=torch.int64, device="cuda")
+    frecv = torch.empty_like(fsend)
+    fcur = torch.zeros(G, dtype=torch.int64, device="cuda")
+    Xf, Zf = torch.empty_like(xq), torch.empty_like(zq)
+    RXf = torch.empty(nl, dtype=torch.int64, device="cuda")
+    RZf = torch.empty(nl, dtype=torch.int64, device="cuda")
+
+    def final(xr, zr):
+        ops.chain_final_pack(xq, xr, xpos, zq, zr, zpos, G, fcap, fcur, fsend, flag)
+        frecv.copy_(fsend)  # the all-to-all (device copy)
+        ops.chain_final_scatter(frecv, G, fcap, nl, nl, Xf, RXf, Zf, RZf, flag)
 
     def call():
         main = torch.cuda.current_stream()
@@ -147,18 +156,23 @@ def chain_call(G, r, T, carried, parts=False):
         else:
             Zg.copy_(Z)
             xr, zr = mark("ranking", lambda: ops.rank_images_query(Zg, xq, zq, L.TW_F64))
-        if parts:
-            mark("final arrays (side stream in the product)", final)
-        else:
+        if carried:  # every rank's async Z all-gather (device copy)
             fs.wait_stream(main)
             with torch.cuda.stream(fs):
-                final()
+                Zg.copy_(Z)
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, r, G,
                                                 kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                 send=send, cap=cap, flag=flag))
             sz = G * c * (cap + 1)
+            if i0 + c >= T:  # the final exchange beside the last chunk's unpack and count
+                if parts:
+                    mark("final exchange (side stream in the product)", lambda: final(xr, zr))
+                else:
+                    fs.wait_stream(main)
+                    with torch.cuda.stream(fs):
+                        final(xr, zr)
             mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
             mark("unpack exact", lambda: ops.chain_unpack_exact(recv, G, c, cap, nl, nl, x_bag,
                                                                 z_bag, flag))

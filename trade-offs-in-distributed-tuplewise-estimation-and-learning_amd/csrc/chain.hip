@@ -502,6 +502,120 @@ __global__ __launch_bounds__(kBlock) void k_count_chain(
   }
 }
 
+// ------------------------------------------- the call's final arrays over ranks: one exchange
+// (round 6) Every rank walked its own elements to their final global positions (the chains'
+// state after the call's last emission); each element's score and rank-image record travel
+// ONCE to the rank that holds its final position — 24-B records {score, record, local
+// position (z: n + position)} in G fixed-capacity buckets (k_exchange_pack_fixed's layout: a
+// header record with the count, then up to cap records) through one equal-split all-to-all —
+// and land at their positions: the rank's final arrays and the carried records of the next
+// call.  This replaces the all-gathers of both samples and of both record arrays (G x the
+// rank's bytes received per call) and the inverse-chain gathers from them.
+constexpr int kFinMaxG = 1024, kFinPer = 8, kFinChunk = kBlock * kFinPer;
+
+__global__ __launch_bounds__(kBlock) void k_chain_final_pack(
+    const uint64_t* __restrict__ xv, const uint64_t* __restrict__ xr,
+    const uint32_t* __restrict__ xpos, int64_t n, const uint64_t* __restrict__ zv,
+    const uint64_t* __restrict__ zr, const uint32_t* __restrict__ zpos, int64_t m, int G,
+    FastDiv dn, FastDiv dm, int64_t cap, unsigned long long* __restrict__ cursor,
+    uint64_t* __restrict__ send, int* __restrict__ flag) {
+  __shared__ unsigned lcnt[kFinMaxG];
+  __shared__ int64_t lbase[kFinMaxG];
+  const int64_t tot = n + m, bsz = cap + 1;
+  for (int64_t c0 = (int64_t)blockIdx.x * kFinChunk; c0 < tot;
+       c0 += (int64_t)gridDim.x * kFinChunk) {
+    for (int i = threadIdx.x; i < G; i += kBlock) lcnt[i] = 0;
+    __syncthreads();
+    int dst[kFinPer];
+    unsigned slot[kFinPer];
+    int64_t pos[kFinPer];
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+      const int64_t e = c0 + k * kBlock + threadIdx.x;
+      dst[k] = -1;
+      slot[k] = 0;
+      pos[k] = 0;
+      if (e < n) {
+        const uint64_t p = xpos[e];
+        const uint64_t g = fast_div(p, dn);
+        dst[k] = (int)g;
+        pos[k] = (int64_t)(p - g * (uint64_t)n);
+      } else if (e < tot) {
+        const uint64_t p = zpos[e - n];
+        const uint64_t g = fast_div(p, dm);
+        dst[k] = (int)g;
+        pos[k] = (int64_t)(p - g * (uint64_t)m) + n;
+      }
+      if (dst[k] >= G) {  // a position past the sample (never, for a valid chain state)
+        *flag = 1;
+        dst[k] = -1;
+      }
+      if (dst[k] >= 0) slot[k] = atomicAdd(&lcnt[dst[k]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G; i += kBlock)
+      if (lcnt[i]) lbase[i] = (int64_t)atomicAdd(cursor + i, (unsigned long long)lcnt[i]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+      if (dst[k] >= 0) {
+        const int64_t o = lbase[dst[k]] + slot[k];
+        if (o < cap) {
+          const int64_t e = c0 + k * kBlock + threadIdx.x;
+          uint64_t* r = send + 3 * ((int64_t)dst[k] * bsz + 1 + o);
+          r[0] = e < n ? xv[e] : zv[e - n];
+          r[1] = e < n ? xr[e] : zr[e - n];
+          r[2] = (uint64_t)pos[k];
+        } else {
+          *flag = 1;  // dropped, never written out of place; the host raises
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// the bucket headers from the cursors (then zeroed for the next call)
+__global__ void k_chain_final_seal(int G, int64_t cap, unsigned long long* __restrict__ cursor,
+                                   uint64_t* __restrict__ send, int* __restrict__ flag) {
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    const unsigned long long c = cursor[g];
+    uint64_t* h = send + 3 * ((int64_t)g * (cap + 1));
+    h[0] = c;
+    h[1] = 0;
+    h[2] = 0;
+    cursor[g] = 0;
+    if (c > (unsigned long long)cap) *flag = 1;
+  }
+}
+
+// receive side: every record of every bucket at its position of the final arrays
+__global__ __launch_bounds__(kBlock) void k_chain_final_scatter(
+    const uint64_t* __restrict__ recv, int G, int64_t cap, int64_t n, int64_t m,
+    uint64_t* __restrict__ xo, uint64_t* __restrict__ xro, uint64_t* __restrict__ zo,
+    uint64_t* __restrict__ zro, int* __restrict__ flag) {
+  const int64_t bsz = cap + 1, tot = (int64_t)G * cap;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t g = i / cap, r = i - g * cap;
+    const uint64_t c = recv[3 * (g * bsz)];
+    if (c > (uint64_t)cap && r == 0) *flag = 1;
+    if ((uint64_t)r < c && r < cap) {
+      const uint64_t* q = recv + 3 * (g * bsz + 1 + r);
+      const uint64_t p = q[2];
+      if (p < (uint64_t)n) {
+        xo[p] = q[0];
+        xro[p] = q[1];
+      } else if (p < (uint64_t)(n + m)) {
+        zo[p - n] = q[0];
+        zro[p - n] = q[1];
+      } else {
+        *flag = 1;
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- final order
 // One process: the scores at the chains' last positions, out[pos[e]] = in[e] (8-B values).
 __global__ __launch_bounds__(kBlock) void k_chain_scatter(const uint64_t* __restrict__ xin,
@@ -800,6 +914,54 @@ extern "C" int tw_chain_unpack_exact(const uint64_t* d_recv, int32_t world, int3
   hipLaunchKernelGGL(k_chain_unpack_exact, dim3((unsigned)(parts * world * steps)), dim3(kBlock),
                      0, (hipStream_t)stream, d_recv, (int)world, (int)steps, parts, cap, n_x, n_z,
                      (uint32_t*)d_x_bag, (uint32_t*)d_z_bag, d_flag);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+// The call's final arrays over ranks by one exchange (k_chain_final_pack / _seal / _scatter):
+// tw_chain_final_pack packs this rank's walked elements (scores d_x / d_z, records d_x_rec /
+// d_z_rec, final global positions d_x_pos / d_z_pos, each rank n_x / n_z of them) into world
+// buckets of 1 + cap 24-B records (d_send: world * (cap + 1) * 3 u64; d_cursor: world u64,
+// zero on entry and left zero); after an equal-split all-to-all, tw_chain_final_scatter writes
+// every received record into d_x_out / d_x_rec_out / d_z_out / d_z_rec_out at its position.
+extern "C" int tw_chain_final_pack(const void* d_x, const uint64_t* d_x_rec,
+                                   const uint32_t* d_x_pos, int64_t n_x, const void* d_z,
+                                   const uint64_t* d_z_rec, const uint32_t* d_z_pos, int64_t n_z,
+                                   int32_t world, int64_t cap, uint64_t* d_cursor, void* d_send,
+                                   int32_t* d_flag, void* stream) {
+  TW_ARG_CHECK(world >= 1 && world <= kFinMaxG && n_x >= 1 && n_z >= 1 && cap >= 1 &&
+                   (int64_t)world * n_x < (1ll << 32) && (int64_t)world * n_z < (1ll << 32),
+               "tw_chain_final_pack: bad sizes");
+  TW_ARG_CHECK(d_x && d_x_rec && d_x_pos && d_z && d_z_rec && d_z_pos && d_cursor && d_send &&
+                   d_flag,
+               "tw_chain_final_pack: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (int)std::min<int64_t>(2048, ceil_div(n_x + n_z, (int64_t)kFinChunk));
+  hipLaunchKernelGGL(k_chain_final_pack, dim3(blocks), dim3(kBlock), 0, st,
+                     (const uint64_t*)d_x, d_x_rec, d_x_pos, n_x, (const uint64_t*)d_z, d_z_rec,
+                     d_z_pos, n_z, (int)world, make_fastdiv((uint64_t)n_x),
+                     make_fastdiv((uint64_t)n_z), cap, (unsigned long long*)d_cursor,
+                     (uint64_t*)d_send, (int*)d_flag);
+  TW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_chain_final_seal, dim3(1), dim3(256), 0, st, (int)world, cap,
+                     (unsigned long long*)d_cursor, (uint64_t*)d_send, (int*)d_flag);
+  TW_LAUNCH_CHECK();
+  return TW_OK;
+}
+
+extern "C" int tw_chain_final_scatter(const void* d_recv, int32_t world, int64_t cap,
+                                      int64_t n_x, int64_t n_z, void* d_x_out,
+                                      void* d_x_rec_out, void* d_z_out, void* d_z_rec_out,
+                                      int32_t* d_flag, void* stream) {
+  TW_ARG_CHECK(world >= 1 && world <= kFinMaxG && cap >= 1 && n_x >= 0 && n_z >= 0 && d_recv &&
+                   d_x_out && d_x_rec_out && d_z_out && d_z_rec_out && d_flag,
+               "tw_chain_final_scatter: bad arguments");
+  const int blocks = (int)std::max<int64_t>(
+      1, std::min<int64_t>(2048, ceil_div((int64_t)world * cap, kBlock)));
+  hipLaunchKernelGGL(k_chain_final_scatter, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const uint64_t*)d_recv, (int)world, cap, n_x, n_z, (uint64_t*)d_x_out,
+                     (uint64_t*)d_x_rec_out, (uint64_t*)d_z_out, (uint64_t*)d_z_rec_out,
+                     (int*)d_flag);
   TW_LAUNCH_CHECK();
   return TW_OK;
 }

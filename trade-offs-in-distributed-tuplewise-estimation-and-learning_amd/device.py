@@ -55,6 +55,10 @@ CHAIN_SUB = 0
 # skips the ranking (and over ranks the Z all-gather it waits for).  Any assignment of X / Z or
 # an in-place change (the tensors' version counters) drops them.
 CARRY_IMAGES = True
+# over ranks, a chain call's final arrays and carried records by ONE exchange of the walked
+# elements to the owners of their final positions (tw_chain_final_pack / _scatter), instead of
+# all-gathers of both samples and both record arrays and inverse-chain gathers from them
+FINAL_EXCHANGE = True
 # UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
 # exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
 CHAIN_RNG = True
@@ -243,6 +247,17 @@ class HipOps:
         L.call("tw_chain_unpack", L.ptr(recv), int(world), int(steps), int(cap),
                int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
                L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
+
+    def chain_final_pack(self, X, xr, xpos, Z, zr, zpos, world, cap, cursor, send, flag):
+        """The walked elements into their final positions' buckets (tw_chain_final_pack)."""
+        L.call("tw_chain_final_pack", L.ptr(X), L.ptr(xr), L.ptr(xpos), int(X.numel()), L.ptr(Z),
+               L.ptr(zr), L.ptr(zpos), int(Z.numel()), int(world), int(cap), L.ptr(cursor),
+               L.ptr(send), L.ptr(flag), L.stream_handle())
+
+    def chain_final_scatter(self, recv, world, cap, n, m, Xo, XRo, Zo, ZRo, flag):
+        """The received final records at their positions (tw_chain_final_scatter)."""
+        L.call("tw_chain_final_scatter", L.ptr(recv), int(world), int(cap), int(n), int(m),
+               L.ptr(Xo), L.ptr(XRo), L.ptr(Zo), L.ptr(ZRo), L.ptr(flag), L.stream_handle())
 
     def chain_unpack_exact(self, recv, world, steps, cap, n, m, x_bag, z_bag, flag):
         """The received records written at their exact positions of the step bags
@@ -1002,17 +1017,26 @@ class ShardedSample:
                 verdict = (self.t.empty((1,), dtype=self.t.int64, device=self.X.device) if coll
                            else self._host_verdict())
                 self._checksum(cs, verdict, 1, self.G + 1 if coll else 0)
+        # over ranks the call's final arrays and carried records come by ONE exchange of the
+        # walked elements to the ranks holding their final positions (FINAL_EXCHANGE,
+        # tw_chain_final_pack / _scatter) instead of the all-gathers of X and of both record
+        # arrays and the inverse-chain gathers from them
+        fin_x = coll and FINAL_EXCHANGE and hasattr(ops, "chain_final_pack")
+        X0 = Z0 = None
         if coll:
-            # the ranking needs the whole Z now (unless the images are carried); the whole X
-            # only for the final arrays (chain_gather), so its all-gather runs asynchronously
-            # under the chunks' counts
-            if carried:
+            # the ranking needs the whole Z now (unless the images are carried); without the
+            # final exchange the whole X (and Z) only for the final arrays (chain_gather), so
+            # those all-gathers run asynchronously under the chunks' counts
+            # (every rank gathers Z, carried or not: a rank whose sample changed alone ranks
+            # afresh while the others carry, and the ranks' collectives must stay one sequence)
+            if not carried:
+                Z0 = self._all_gather(self.Z)
+            else:
                 Z0, w = self._all_gather(self.Z, async_op=True)
                 works.append(w)
-            else:
-                Z0 = self._all_gather(self.Z)
-            X0, w = self._all_gather(self.X, async_op=True)
-            works.append(w)
+            if not fin_x:
+                X0, w = self._all_gather(self.X, async_op=True)
+                works.append(w)
         else:
             X0, Z0 = self.X, self.Z
         if not carried:
@@ -1023,7 +1047,7 @@ class ShardedSample:
             return [self.UnN(k) for k in keys]
         xr, zr = rec
         RX = RZ = None
-        if coll and CARRY_IMAGES:
+        if coll and CARRY_IMAGES and not fin_x:
             # the records follow their elements: gathered by the same inverse chains as the
             # scores, from every rank's records (asynchronous, under the counts)
             RX, w = self._all_gather(xr, async_op=True)
@@ -1036,7 +1060,7 @@ class ShardedSample:
         kxs = [(2 * k) & M64 for k in keys]
         kzs = [(2 * k + 1) & M64 for k in keys]
         final = None
-        if coll and self.X.is_cuda:
+        if coll and self.X.is_cuda and not fin_x:
             # the final arrays depend on the keys and the all-gathered sample only: gathered on
             # a side stream beside the emission, exchanges and counts (not after them)
             main = t.cuda.current_stream()
@@ -1054,7 +1078,7 @@ class ShardedSample:
                     a.record_stream(main)
         kx = int(n / N)
         kz = int((n + m) / N) - kx  # prop_swor_layout's shard sizes
-        z_total = int(Z0.numel())  # the Z the images were ranked against: images <= z_total
+        z_total = G * m  # the Z the images were ranked against: images <= z_total
 
         def count(xb, zb, steps, out, t0):  # bags of steps t0.. -> out (steps, N)
             if rng is not None:
@@ -1118,6 +1142,12 @@ class ShardedSample:
                         sz = G * cs * (cap + 1) * W
                         xchg.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
                                                                 async_op=True)))
+                if fin_x and i0 + c >= T:
+                    # the walked elements' final positions are known once the call's last
+                    # emission ran: their exchange runs on a side stream beside the last
+                    # chunk's unpack and count (issued after the chunk's all-to-all on every
+                    # rank, so the collectives keep one order)
+                    final = self._final_exchange(xr, zr, xpos, zpos, es)
                 for a, cs, j, work in xchg:
                     if work is not None:
                         work.wait()
@@ -1137,7 +1167,13 @@ class ShardedSample:
         carry = None
         if coll:
             if final is not None:
-                t.cuda.current_stream().wait_stream(self._final_stream)
+                if self.X.is_cuda:
+                    t.cuda.current_stream().wait_stream(self._final_stream)
+                for w in works:  # (fin_x: the Z all-gather of a carried call, unused)
+                    if w is not None:
+                        w.wait()
+                if fin_x and CARRY_IMAGES:
+                    RX = xr  # (marks the carry: the records came with the final exchange)
             else:
                 for w in works:
                     if w is not None:
@@ -1161,6 +1197,44 @@ class ShardedSample:
             raise _StaleImages("UnN_many: the sample was written behind its version counter; "
                                "the carried rank images are stale")
         return [np.mean(v) for v in vals]
+
+    def _final_exchange(self, xr, zr, xpos, zpos, es=None):
+        """The call's final arrays over ranks (FINAL_EXCHANGE): on the final stream, after the
+        call's last emission (the chains' positions), this rank's walked elements — scores
+        self.X / self.Z, records xr / zr — packed into G fixed-capacity buckets of 24-B records
+        by their final positions (tw_chain_final_pack), ONE equal-split all-to-all, and every
+        received record written at its position (tw_chain_final_scatter): (X, Z, X records,
+        Z records) of the rank's final positions, recorded for the main stream."""
+        t, G, n, m = self.t, self.G, self.n_loc, self.m_loc
+        main = t.cuda.current_stream() if self.X.is_cuda else None
+        tot = n + m
+        cap = max(1, tot // G + tot // (8 * G) + 1024)
+        send = self._work("fin_send", (G * (cap + 1) * 3,), t.int64)
+        recv = self._work("fin_recv", (G * (cap + 1) * 3,), t.int64)
+        cur = getattr(self, "_fin_cursor", None)
+        if cur is None or cur.numel() != G:
+            cur = self._fin_cursor = t.zeros((G,), dtype=t.int64, device=self.X.device)
+        if main is None:
+            fs = None
+        else:
+            if getattr(self, "_final_stream", None) is None:
+                self._final_stream = t.cuda.Stream()
+            fs = self._final_stream
+            fs.wait_stream(main)
+            if es is not None:
+                fs.wait_stream(es)
+        with (t.cuda.stream(fs) if fs is not None else contextlib.nullcontext()):
+            self.ops.chain_final_pack(self.X, xr, xpos, self.Z, zr, zpos, G, cap, cur, send,
+                                      self._chain_flag)
+            self._all_to_all(recv, send)
+            out = (t.empty_like(self.X), t.empty_like(self.Z), t.empty_like(xr),
+                   t.empty_like(zr))
+            self.ops.chain_final_scatter(recv, G, cap, n, m, out[0], out[2], out[1], out[3],
+                                         self._chain_flag)
+            if fs is not None:
+                for a in out:
+                    a.record_stream(main)
+        return out
 
     def _work(self, name, shape, dtype):
         """A work tensor of `shape` kept on the sample across calls (one flat buffer per name,
