@@ -913,6 +913,14 @@ int tw_chain_final_pack(const void* d_x, const uint64_t* d_x_rec, const uint32_t
 int tw_chain_final_scatter(const void* d_recv, int32_t world, int64_t cap, int64_t n_x,
                            int64_t n_z, void* d_x_out, void* d_x_rec_out, void* d_z_out,
                            void* d_z_rec_out, int32_t* d_flag, void* stream);
+/* The final global positions of this rank's elements (x: x_base + e, z: z_base + e) after
+ * `steps` chained permutations of the n_x_all / n_z_all domains (keys as tw_chain_emit's): the
+ * chain state tw_chain_emit leaves after the same steps, computed without emitting, so that
+ * tw_chain_final_pack can run at a call's start beside its emissions and counts (main.py:46-47's
+ * final arrays, est.UnNT). */
+int tw_chain_walk(int64_t x_base, int64_t n_x, int64_t n_x_all, int64_t z_base, int64_t n_z,
+                  int64_t n_z_all, const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
+                  uint32_t* d_x_pos, uint32_t* d_z_pos, void* stream);
 /* The incomplete statistic on the step chains over ranks (cs.UnNBT, compute_stats.py:119-123,
  * with device-RNG draws): tw_chain_unpack_exact writes every received record {image, local
  * position} of a chunk's (source, step) buckets (tw_chain_emit's exchange layout, strict

@@ -257,6 +257,15 @@ class OracleOpsChain(OracleOpsRank):
         Zo.numpy()[zpos.numpy().view(np.uint32)] = Z.numpy()
         return Xo, Zo
 
+    def chain_walk(self, x_base, n, NX, z_base, m, NZ, keys_x, keys_z, xpos, zpos):
+        """tw_chain_walk restated: the rank's positions through every step, no emission."""
+        for base, cnt, N_, keys, out in ((x_base, n, NX, keys_x, xpos),
+                                         (z_base, m, NZ, keys_z, zpos)):
+            p = np.arange(base, base + cnt)
+            for key in keys:
+                p = O.feistel_perm(p, N_, int(key))
+            out.numpy()[:] = p.astype(np.uint32).view(np.int32)
+
     def chain_final_pack(self, X, xr, xpos, Z, zr, zpos, world, cap, cursor, send, flag):
         """tw_chain_final_pack restated: {score, record, local position} records of the walked
         elements into the buckets of the ranks holding their final positions (a header record
@@ -425,12 +434,17 @@ def test_multirank_repartition_is_G_invariant(G, fused):
     assert inc == float(S1.UnNB(B, seed=77))
 
 
-def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub=0):
+def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub=0,
+                 final="exchange"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     from tuplewise import device as D
     from tuplewise.device import ShardedSample
     D.CHAIN_SUB = sub
+    # the final arrays: one exchange after the last emission (default), one exchange forked at
+    # the call's start on walked positions (tw_chain_walk), or the inverse-chain gathers
+    D.FINAL_EXCHANGE = final != "gather"
+    D.FINAL_EARLY = final == "early"
     X, Z = _global_data(G, n_loc, m_loc)
     S = ShardedSample(torch.from_numpy(X[rank * n_loc:(rank + 1) * n_loc].copy()),
                       torch.from_numpy(Z[rank * m_loc:(rank + 1) * m_loc].copy()), N,
@@ -448,9 +462,11 @@ def _rank_worker(rank, G, port, n_loc, m_loc, N, keys, q, tie_mode="strict", sub
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("G,tie_mode,sub", [(2, "strict", 0), (4, "strict", 0), (8, "strict", 0),
-                                            (2, "half", 0), (4, "strict", 5)])
-def test_chain_steps_are_G_invariant(G, tie_mode, sub):
+@pytest.mark.parametrize("G,tie_mode,sub,final", [
+    (2, "strict", 0, "exchange"), (4, "strict", 0, "exchange"), (8, "strict", 0, "exchange"),
+    (2, "half", 0, "exchange"), (4, "strict", 5, "exchange"), (3, "half", 0, "early"),
+    (2, "strict", 5, "early"), (3, "strict", 0, "gather")])
+def test_chain_steps_are_G_invariant(G, tie_mode, sub, final):
     """UnN_many's step chains over G ranks (csrc/chain.hip, restated): every rank images its
     own elements against the all-gathered Z, walks their chains into per-(rank, step) buckets,
     one all-to-all per chunk (sub > 0: per sub-chunk of <= sub steps, async), counts its bags;
@@ -468,7 +484,7 @@ def test_chain_steps_are_G_invariant(G, tie_mode, sub):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_rank_worker,
-                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode, sub))
+                         args=(r, G, port, n_loc, m_loc, N, keys, q, tie_mode, sub, final))
              for r in range(G)]
     for p in procs:
         p.start()

@@ -154,6 +154,11 @@ def test_chain_exchange_simulated_ranks(gpu, G, half):
         ops.chain_emit(xr, zr, half, xpos, zpos, True, r, G, kxs, kzs, kx, kz, N, send=send,
                        cap=cap, flag=flag)
         assert int(flag.item()) == 0
+        # tw_chain_walk: the same chain state without emitting
+        wxp, wzp = torch.empty_like(xpos), torch.empty_like(zpos)
+        ops.chain_walk(r * n_loc, n_loc, G * n_loc, r * m_loc, m_loc, G * m_loc, kxs, kzs, wxp,
+                       wzp)
+        assert torch.equal(wxp, xpos) and torch.equal(wzp, zpos)
         sends.append(send.view(G, -1))
     x_off, z_off = _layout(n_loc, m_loc, N)
     xo, zo = torch.from_numpy(x_off).cuda(), torch.from_numpy(z_off).cuda()
@@ -227,6 +232,29 @@ def test_chain_gather_many_steps(gpu):
                                   r * n_loc, n_loc, r * m_loc, m_loc, kxs, kzs)
         assert np.array_equal(Xo.cpu().numpy(), xs[r * n_loc:(r + 1) * n_loc])
         assert np.array_equal(Zo.cpu().numpy(), zs[r * m_loc:(r + 1) * m_loc])
+
+
+def test_chain_walk_many_steps(gpu):
+    """tw_chain_walk over more than 32 steps (launch chunks) and over none: the oracle's
+    Feistel positions of the rank's elements."""
+    import torch
+    from tuplewise.device import HipOps
+    G, n_loc, m_loc = 3, 1000, 700
+    keys = list(range(300, 370))
+    kxs = [(2 * k) & M64 for k in keys]
+    kzs = [(2 * k + 1) & M64 for k in keys]
+    ops = HipOps()
+    for r in range(G):
+        for T in (0, 1, 32, 33, 70):
+            xp = torch.empty(n_loc, dtype=torch.int32, device="cuda")
+            zp = torch.empty(m_loc, dtype=torch.int32, device="cuda")
+            ops.chain_walk(r * n_loc, n_loc, G * n_loc, r * m_loc, m_loc, G * m_loc, kxs[:T],
+                           kzs[:T], xp, zp)
+            for got, base, nl, ks in ((xp, r * n_loc, n_loc, kxs), (zp, r * m_loc, m_loc, kzs)):
+                p = np.arange(base, base + nl)
+                for k in ks[:T]:
+                    p = O.feistel_perm(p, G * nl, int(k))
+                assert np.array_equal(got.cpu().numpy().view(np.uint32), p)
 
 
 @pytest.mark.parametrize("case", ["gauss", "ties_i64", "edge_ragged", "one_shard", "long"])

@@ -122,6 +122,8 @@ def rank_call(G, r, K, parts=False, carried=False):
 
     # round 6 (device.FINAL_EXCHANGE): the final arrays and carried records by one exchange of
     # the walked elements, forked on the side stream once the last emission has run
+    # (device.FINAL_EARLY, the fork at the call's start on tw_chain_walk positions, measured
+    # slower: profiles/r06s22_*)
     tot = 2 * nl
     fcap = max(1, tot // G + tot // (8 * G) + 1024)
     fsend = torch.empty(G * (fcap + 1) * 3, dtype=torch.int64, device="cuda")

@@ -675,6 +675,38 @@ __global__ __launch_bounds__(kBlock) void k_chain_inverse(
   }
 }
 
+// The forward walk alone: position base + e (pin null) or pin[e] through steps [0, steps) of a
+// chunk, cycle-walked exactly as chain_next does — the positions the emission of the same keys
+// leaves in its chain state, known before any emission has run (the final exchange forks at
+// the call's start, beside the emissions and counts).
+__global__ __launch_bounds__(kBlock) void k_chain_walk(int64_t xbase, int64_t nx, int64_t NX,
+                                                       int64_t zbase, int64_t nz, int64_t NZ,
+                                                       int have, uint32_t* __restrict__ xpos,
+                                                       uint32_t* __restrict__ zpos,
+                                                       ChainKeys keys, int steps) {
+  __shared__ Feistel fs[2 * kChainMax];
+  if ((int)threadIdx.x < 2 * steps) {
+    const int t = threadIdx.x;
+    fs[t] = t < steps ? make_feistel(NX > 1 ? NX : 1, keys.kx[t])
+                      : make_feistel(NZ > 1 ? NZ : 1, keys.kz[t - steps]);
+  }
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nx + nz;
+       i += (int64_t)gridDim.x * kBlock) {
+    const bool isx = i < nx;
+    const int64_t e = isx ? i : i - nx;
+    const uint32_t Nt = (uint32_t)(isx ? NX : NZ);
+    uint32_t* pa = isx ? xpos : zpos;
+    uint32_t p = have ? pa[e] : (uint32_t)((isx ? xbase : zbase) + e);
+    for (int c = 0; c < steps; ++c) {
+      const Feistel& F = fs[isx ? c : steps + c];
+      p = feistel_once32(F, p);
+      while (p >= Nt) p = feistel_once32(F, p);
+    }
+    pa[e] = p;
+  }
+}
+
 // ----------------------------------------------------------------------------- plan
 struct ChainPlan {
   int R, tiles_x, zchunks;
@@ -1197,6 +1229,36 @@ extern "C" int tw_chain_gather2(const void* d_x_all, const void* d_z_all, const 
   return chain_gather_impl(d_x_all, d_z_all, x_base, n_x, n_x_all, z_base, n_z, n_z_all, keys_x,
                            keys_z, steps, d_work, d_x_out, d_z_out, d_x_all2, d_z_all2, d_x_out2,
                            d_z_out2, stream);
+}
+
+// Final global positions of this rank's elements (x: x_base + e, z: z_base + e) after steps
+// chained permutations of the n_x_all / n_z_all domains (keys_x / keys_z): what tw_chain_emit's
+// chain state holds after the same steps, computed without emitting.
+extern "C" int tw_chain_walk(int64_t x_base, int64_t n_x, int64_t n_x_all, int64_t z_base,
+                             int64_t n_z, int64_t n_z_all, const uint64_t* keys_x,
+                             const uint64_t* keys_z, int32_t steps, uint32_t* d_x_pos,
+                             uint32_t* d_z_pos, void* stream) {
+  TW_ARG_CHECK(n_x >= 0 && n_z >= 0 && x_base >= 0 && z_base >= 0 && steps >= 0 &&
+                   x_base + n_x <= n_x_all && z_base + n_z <= n_z_all &&
+                   n_x_all < (1ll << 32) && n_z_all < (1ll << 32),
+               "tw_chain_walk: bad sizes");
+  TW_ARG_CHECK(steps == 0 || (keys_x != nullptr && keys_z != nullptr),
+               "tw_chain_walk: keys missing");
+  TW_ARG_CHECK((n_x == 0 || d_x_pos != nullptr) && (n_z == 0 || d_z_pos != nullptr),
+               "tw_chain_walk: null position arrays");
+  if (n_x + n_z == 0) return TW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)std::min<int64_t>(4096, ceil_div(n_x + n_z, kBlock));
+  int lo = 0;
+  do {  // chunks of <= 32 steps; a zero-step walk still writes the base positions
+    const int hi = std::min<int>(steps, lo + kChainMax);
+    const ChainKeys k = hi > lo ? chain_keys(keys_x + lo, keys_z + lo, hi - lo) : ChainKeys{};
+    hipLaunchKernelGGL(k_chain_walk, dim3(grid), dim3(kBlock), 0, st, x_base, n_x, n_x_all,
+                       z_base, n_z, n_z_all, lo > 0 ? 1 : 0, d_x_pos, d_z_pos, k, hi - lo);
+    TW_LAUNCH_CHECK();
+    lo = hi;
+  } while (lo < steps);
+  return TW_OK;
 }
 
 static int chain_gather_impl(const void* d_x_all, const void* d_z_all, int64_t x_base,

@@ -59,6 +59,11 @@ CARRY_IMAGES = True
 # elements to the owners of their final positions (tw_chain_final_pack / _scatter), instead of
 # all-gathers of both samples and both record arrays and inverse-chain gathers from them
 FINAL_EXCHANGE = True
+# ... forked at the call's start on positions walked without emitting (tw_chain_walk) instead
+# of after the last emission: off — on one GPU the walk and pack beside the emissions cost more
+# than they hide (profiles/r06s22_chain_probe.log), and over RCCL the exchange's all-to-all
+# issued first would queue ahead of the chunks' on the communicator
+FINAL_EARLY = False
 # UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
 # exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
 CHAIN_RNG = True
@@ -253,6 +258,15 @@ class HipOps:
         L.call("tw_chain_final_pack", L.ptr(X), L.ptr(xr), L.ptr(xpos), int(X.numel()), L.ptr(Z),
                L.ptr(zr), L.ptr(zpos), int(Z.numel()), int(world), int(cap), L.ptr(cursor),
                L.ptr(send), L.ptr(flag), L.stream_handle())
+
+    def chain_walk(self, x_base, n, NX, z_base, m, NZ, keys_x, keys_z, xpos, zpos):
+        """The final positions of the rank's elements after the keys' steps, without emitting
+        (tw_chain_walk): the chain state tw_chain_emit leaves after the same steps."""
+        kxa = np.ascontiguousarray(keys_x, dtype=np.uint64)
+        kza = np.ascontiguousarray(keys_z, dtype=np.uint64)
+        L.call("tw_chain_walk", int(x_base), int(n), int(NX), int(z_base), int(m), int(NZ),
+               kxa.ctypes.data, kza.ctypes.data, len(kxa), L.ptr(xpos), L.ptr(zpos),
+               L.stream_handle())
 
     def chain_final_scatter(self, recv, world, cap, n, m, Xo, XRo, Zo, ZRo, flag):
         """The received final records at their positions (tw_chain_final_scatter)."""
@@ -1076,6 +1090,12 @@ class ShardedSample:
                 final = ops.chain_gather(X0, Z0, r * n, n, r * m, m, kxs, kzs, RX, RZ)
                 for a in final:
                     a.record_stream(main)
+        early = fin_x and FINAL_EARLY and hasattr(ops, "chain_walk")
+        if early:
+            # the final positions walked without emitting (tw_chain_walk), so the final
+            # exchange forks now, beside the whole call's emissions and counts (its all-to-all
+            # is issued before the chunks' on every rank: one collective order)
+            final = self._final_exchange(xr, zr, walk=(kxs, kzs))
         kx = int(n / N)
         kz = int((n + m) / N) - kx  # prop_swor_layout's shard sizes
         z_total = G * m  # the Z the images were ranked against: images <= z_total
@@ -1142,7 +1162,7 @@ class ShardedSample:
                         sz = G * cs * (cap + 1) * W
                         xchg.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
                                                                 async_op=True)))
-                if fin_x and i0 + c >= T:
+                if fin_x and not early and i0 + c >= T:
                     # the walked elements' final positions are known once the call's last
                     # emission ran: their exchange runs on a side stream beside the last
                     # chunk's unpack and count (issued after the chunk's all-to-all on every
@@ -1198,19 +1218,23 @@ class ShardedSample:
                                "the carried rank images are stale")
         return [np.mean(v) for v in vals]
 
-    def _final_exchange(self, xr, zr, xpos, zpos, es=None):
-        """The call's final arrays over ranks (FINAL_EXCHANGE): on the final stream, after the
-        call's last emission (the chains' positions), this rank's walked elements — scores
-        self.X / self.Z, records xr / zr — packed into G fixed-capacity buckets of 24-B records
-        by their final positions (tw_chain_final_pack), ONE equal-split all-to-all, and every
-        received record written at its position (tw_chain_final_scatter): (X, Z, X records,
-        Z records) of the rank's final positions, recorded for the main stream."""
+    def _final_exchange(self, xr, zr, xpos=None, zpos=None, es=None, walk=None):
+        """The call's final arrays over ranks (FINAL_EXCHANGE): on the final stream, this
+        rank's walked elements — scores self.X / self.Z, records xr / zr — packed into G
+        fixed-capacity buckets of 24-B records by their final positions (tw_chain_final_pack),
+        ONE equal-split all-to-all, and every received record written at its position
+        (tw_chain_final_scatter): (X, Z, X records, Z records) of the rank's final positions,
+        recorded for the main stream.  The final positions: walk = (keys_x, keys_z), the
+        call's chains walked here without emitting (tw_chain_walk, at the call's start), or
+        xpos / zpos, the chain state after the call's last emission (on `es`)."""
         t, G, n, m = self.t, self.G, self.n_loc, self.m_loc
         main = t.cuda.current_stream() if self.X.is_cuda else None
         tot = n + m
         cap = max(1, tot // G + tot // (8 * G) + 1024)
         send = self._work("fin_send", (G * (cap + 1) * 3,), t.int64)
         recv = self._work("fin_recv", (G * (cap + 1) * 3,), t.int64)
+        if getattr(self, "_chain_flag", None) is None:
+            self._chain_flag = t.zeros((1,), dtype=t.int32, device=self.X.device)
         cur = getattr(self, "_fin_cursor", None)
         if cur is None or cur.numel() != G:
             cur = self._fin_cursor = t.zeros((G,), dtype=t.int64, device=self.X.device)
@@ -1224,6 +1248,11 @@ class ShardedSample:
             if es is not None:
                 fs.wait_stream(es)
         with (t.cuda.stream(fs) if fs is not None else contextlib.nullcontext()):
+            if walk is not None:
+                xpos = self._work("fin_xpos", (n,), t.int32)
+                zpos = self._work("fin_zpos", (m,), t.int32)
+                self.ops.chain_walk(self.rank * n, n, G * n, self.rank * m, m, G * m, walk[0],
+                                    walk[1], xpos, zpos)
             self.ops.chain_final_pack(self.X, xr, xpos, self.Z, zr, zpos, G, cap, cur, send,
                                       self._chain_flag)
             self._all_to_all(recv, send)
