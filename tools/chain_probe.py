@@ -15,7 +15,8 @@ ranking; the all-gathers of both samples and of both record arrays, as device co
 inverse-chain gathers of scores and records on a side stream beside the counts), each against
 the one-GPU call of the same kind / G.  The sub-chunk schedules of the round-5 study are in
 profiles/r05s36_chain_probe.log.  Run on the GPU box:
-    python tools/chain_probe.py [K ...]"""
+    python tools/chain_probe.py [K ...]      (TW_PROBE_G=8: only those G)"""
+import os
 import pathlib
 import sys
 import time
@@ -138,9 +139,12 @@ def rank_call(G, r, K, parts=False, carried=False):
         frecv.copy_(fsend)  # the all-to-all (device copy)
         ops.chain_final_scatter(frecv, G, fcap, nl, nl, Xf, RXf, Zf, RZf, flag)
 
-    def side_work(xr, zr):
-        main = torch.cuda.current_stream()
-        fs.wait_stream(main)
+    def side_work(xr, zr, ev=None):
+        # (ev: the last emission's event — the fork is enqueued after the count launch)
+        if ev is not None:
+            fs.wait_event(ev)
+        else:
+            fs.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(fs):
             final_exchange(xr, zr)
 
@@ -167,18 +171,20 @@ def rank_call(G, r, K, parts=False, carried=False):
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, r, G,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                     send=send, cap=cap, flag=flag))
+                ev = torch.cuda.Event()
+                ev.record()
                 sz = G * c * (cap + 1)
-                if i0 + c >= K:  # the final exchange beside the last chunk's count
-                    if parts:
-                        mark("final exchange (side stream in the product)",
-                             lambda: final_exchange(xr, zr))
-                    else:
-                        side_work(xr, zr)
                 mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
                 mark("unpack", lambda: ops.chain_unpack(recv, G, c, cap, False, nl, nl, x_bag,
                                                         z_bag, flag, kx, kz, Nl))
             mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz,
                                                   False, counts[i0:i0 + c]))
+            if G > 1 and i0 + c >= K:  # the final exchange beside the last chunk's count
+                if parts:
+                    mark("final exchange (side stream in the product)",
+                         lambda: final_exchange(xr, zr))
+                else:
+                    side_work(xr, zr, ev)
         if G == 1:
             mark("final scatter (scores, records)",
                  lambda: (ops.chain_scatter(X, xpos, Z, zpos),
@@ -202,7 +208,7 @@ for K in Ks:
     print(f"K={K}: one GPU, step chains {ch:.3f} ms/call with carried images ({ch / K:.4f} "
           f"ms/step; host {ch_host:.3f}), {chf:.3f} ranking every call; one launch per step "
           f"{st:.3f} ms/call ({st / K:.4f} ms/step)", flush=True)
-    for G in (1, 2, 4, 8):
+    for G in [int(g) for g in os.environ.get("TW_PROBE_G", "1,2,4,8").split(",")]:
         for carried, ideal, label in ((False, chf, "first call (ranking)"),
                                       (True, ch, "later calls (carried images)")):
             ms = [rank_call(G, r, K, carried=carried)[0] for r in sorted({0, G - 1})]

@@ -167,20 +167,22 @@ def chain_call(G, r, T, carried, parts=False):
             mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, i0 == 0, r, G,
                                                 kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                 send=send, cap=cap, flag=flag))
+            ev = torch.cuda.Event()  # (the fork below waits for the emission only)
+            ev.record()
             sz = G * c * (cap + 1)
-            if i0 + c >= T:  # the final exchange beside the last chunk's unpack and count
-                if parts:
-                    mark("final exchange (side stream in the product)", lambda: final(xr, zr))
-                else:
-                    fs.wait_stream(main)
-                    with torch.cuda.stream(fs):
-                        final(xr, zr)
             mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
             mark("unpack exact", lambda: ops.chain_unpack_exact(recv, G, c, cap, nl, nl, x_bag,
                                                                 z_bag, flag))
             mark("count", lambda: ops.count_chain_rng(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx,
                                                       kz, B, 5 + i0, r * Nl,
                                                       counts[i0:i0 + c]))
+            if i0 + c >= T:  # the final exchange beside the last chunk's count
+                if parts:
+                    mark("final exchange (side stream in the product)", lambda: final(xr, zr))
+                else:
+                    fs.wait_event(ev)
+                    with torch.cuda.stream(fs):
+                        final(xr, zr)
         if not parts:
             main.wait_stream(fs)
         mark("counts reduce (local part)",

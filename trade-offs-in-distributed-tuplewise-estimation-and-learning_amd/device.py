@@ -1162,12 +1162,12 @@ class ShardedSample:
                         sz = G * cs * (cap + 1) * W
                         xchg.append((a, cs, j, self._all_to_all(recvs[j][:sz], sends[j][:sz],
                                                                 async_op=True)))
-                if fin_x and not early and i0 + c >= T:
-                    # the walked elements' final positions are known once the call's last
-                    # emission ran: their exchange runs on a side stream beside the last
-                    # chunk's unpack and count (issued after the chunk's all-to-all on every
-                    # rank, so the collectives keep one order)
-                    final = self._final_exchange(xr, zr, xpos, zpos, es)
+                    emitted = None
+                    if fin_x and not early and i0 + c >= T and self.X.is_cuda:
+                        # the final exchange (enqueued after the last count) waits for this
+                        # event only: the chains' final positions, not the counts
+                        emitted = t.cuda.Event()
+                        emitted.record()
                 for a, cs, j, work in xchg:
                     if work is not None:
                         work.wait()
@@ -1179,6 +1179,13 @@ class ShardedSample:
                                          z_bag[a:a + cs], self._chain_flag, kx, kz, N)
                     count(x_bag[a:a + cs], z_bag[a:a + cs], cs, counts[i0 + a:i0 + a + cs],
                           i0 + a)
+                if fin_x and not early and i0 + c >= T:
+                    # the walked elements' final positions are known once the call's last
+                    # emission ran: their exchange runs on a side stream beside the last
+                    # chunk's count — enqueued AFTER that count, so the host's work for it
+                    # never delays the count's launch (the collectives keep one order: the
+                    # chunk's all-to-all was issued first on every rank)
+                    final = self._final_exchange(xr, zr, xpos, zpos, emitted)
                 continue
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
@@ -1226,7 +1233,8 @@ class ShardedSample:
         (tw_chain_final_scatter): (X, Z, X records, Z records) of the rank's final positions,
         recorded for the main stream.  The final positions: walk = (keys_x, keys_z), the
         call's chains walked here without emitting (tw_chain_walk, at the call's start), or
-        xpos / zpos, the chain state after the call's last emission (on `es`)."""
+        xpos / zpos, the chain state after the call's last emission (`es`: the stream it ran
+        on, or an event recorded after it)."""
         t, G, n, m = self.t, self.G, self.n_loc, self.m_loc
         main = t.cuda.current_stream() if self.X.is_cuda else None
         tot = n + m
@@ -1235,19 +1243,24 @@ class ShardedSample:
         recv = self._work("fin_recv", (G * (cap + 1) * 3,), t.int64)
         if getattr(self, "_chain_flag", None) is None:
             self._chain_flag = t.zeros((1,), dtype=t.int32, device=self.X.device)
-        cur = getattr(self, "_fin_cursor", None)
-        if cur is None or cur.numel() != G:
-            cur = self._fin_cursor = t.zeros((G,), dtype=t.int64, device=self.X.device)
         if main is None:
             fs = None
         else:
             if getattr(self, "_final_stream", None) is None:
                 self._final_stream = t.cuda.Stream()
             fs = self._final_stream
-            fs.wait_stream(main)
-            if es is not None:
-                fs.wait_stream(es)
+            if isinstance(es, t.cuda.Event):  # the last emission's completion (enqueued later)
+                fs.wait_event(es)
+            else:
+                fs.wait_stream(main)
+                if es is not None:
+                    fs.wait_stream(es)
         with (t.cuda.stream(fs) if fs is not None else contextlib.nullcontext()):
+            # the cursors (zero on entry, left zero by the pack): made on the final stream, so
+            # their zeroing is ordered before the pack whatever that stream waits for
+            cur = getattr(self, "_fin_cursor", None)
+            if cur is None or cur.numel() != G:
+                cur = self._fin_cursor = t.zeros((G,), dtype=t.int64, device=self.X.device)
             if walk is not None:
                 xpos = self._work("fin_xpos", (n,), t.int32)
                 zpos = self._work("fin_zpos", (m,), t.int32)
