@@ -1511,17 +1511,50 @@ def main():
         "incomplete_replay": inc_replay,
         "strong_C3": strong,
     }
+    # Every section after the headline runs guarded: an exception there is recorded in the line
+    # ({"error": ...}) and ends the remaining sections, on every rank alike (over ranks the
+    # ranks agree through one small all-reduce per section), so the headline is still printed
+    broken = []
+
+    def guarded(name, fn, collective=True, independent=False):
+        # collective=False: a section only rank 0 runs (no agreement round); independent: it
+        # runs even after a failed section (no collectives, nothing it needs from the others)
+        if broken and not independent:
+            return {"error": f"skipped: an earlier section failed ({broken[0]})"}
+        err = None
+        try:
+            if os.environ.get("TW_BENCH_FAIL_SECTION") == name:  # the guard's own test hook
+                raise RuntimeError(f"forced failure of section {name} (TW_BENCH_FAIL_SECTION)")
+            res = fn()
+        except Exception as e:  # noqa: BLE001 — recorded in the line, the run goes on
+            res, err = None, f"{type(e).__name__}: {e}"
+            sys.stderr.write(f"bench.py: section {name} failed: {err}\n")
+        if group is not None and collective:
+            flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device="cuda")
+            if dist.get_backend(group) != "nccl":
+                flag = flag.cpu()
+            dist.all_reduce(flag, group=group)
+            if int(flag.item()) and err is None:
+                err = "failed on another rank"
+        if err is not None:
+            broken.append(name)
+            return {"error": err}
+        return res
+
     if world > 1:
         # the weak-scaling form of the headline (per-GPU work of the one-GPU run)
         progress("weak C3")
-        out["weak_C3"] = weak_c3(args, group, rank, world, span, torch)
-    if not args.no_sgd:
+        out["weak_C3"] = guarded("weak_C3", lambda: weak_c3(args, group, rank, world, span,
+                                                            torch))
+
+    sec = {"metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)"}
+
+    def sgd_section():  # fills `sec` line by line (a failure keeps the lines before it)
         # reference CPU numbers (BASELINE.md, 1 core): 262-413 steps/s at C4, 3.3-9.4 at C5';
         # at G > 1 every line runs over the ranks (shards split, one all-gather of the shard
         # gradients per step; SGDEngine(group=)), C4/C5 checked against a one-rank run
         chk = 20 if world > 1 else 0
         g = group
-        sec = {"metric": "SGD steps/sec (pairwise hinge, linear scorer; no evaluation)"}
         progress("C4 device RNG")
         sec["C4_shuttle_shape"] = sgd_steps_per_s(9117, 702, 10, 100, 100, 25, 4000, 2, group=g,
                                                   span=span, check_prefix=chk)
@@ -1560,38 +1593,52 @@ def main():
                 C5_N, C5_N, 512, 256, 3)
             sec["C5_scaled_d512_complete_gradient_logistic"] = sgd_complete_steps_per_s(
                 C5_N, C5_N, 512, 256, 2, loss="logistic")
-        out["secondary"] = sec
+        return sec
+
+    if not args.no_sgd:
+        res = guarded("secondary", sgd_section)
+        out["secondary"] = sec if res is sec else {**sec, **res}
         if not args.no_tradeoff:
-            out["tradeoff_reshuffle_mod"] = tradeoff_curve(
-                args, group, span, rank == 0 and world == 1 and not args.no_cpu_baseline)
+            out["tradeoff_reshuffle_mod"] = guarded(
+                "tradeoff_reshuffle_mod", lambda: tradeoff_curve(
+                    args, group, span, rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and not args.no_cpu_baseline:
         # at every G (the GPU work of every rank is done; the others wait at the final barrier):
         # the reference's est.UnN restated on 1 core, and the same blocks spread over the host
         # cores of this run's CPU share: on a whole 8-GPU node every core of the affinity mask
         # (the node-wide figure); on the pool's smaller boxes 16 per GPU (os.cpu_count() and the
-        # affinity mask show the whole machine, which those boxes share out per GPU)
+        # affinity mask show the whole machine, which those boxes share out per GPU).  Host
+        # work only: run even after a failed GPU section, its own failure recorded
         progress("CPU baselines")
-        out["cpu_baseline"] = cpu_baseline(args.n, args.shards, args.cpu_shards)
-        aff = len(os.sched_getaffinity(0))
-        node = world >= 8
-        share = aff if node else min(16 * world, aff)
-        allc = cpu_baseline_all_cores(args.n, args.shards, share)
-        allc["label"] = ((f"{share} host cores = the whole affinity mask of the {world}-GPU node"
-                          if node else
-                          f"{share} host cores = 16 per GPU x {world} GPU(s), the pool's CPU "
-                          f"share") + f" (affinity mask {aff}, os.cpu_count() {os.cpu_count()})")
-        out["cpu_baseline"]["all_cores"] = allc
-        out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(args.n, args.shards, B_inc,
-                                                                    args.cpu_inc_shards)
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.n, args.shards, args.cpu_shards)
+            aff = len(os.sched_getaffinity(0))
+            node = world >= 8
+            share = aff if node else min(16 * world, aff)
+            allc = cpu_baseline_all_cores(args.n, args.shards, share)
+            allc["label"] = ((f"{share} host cores = the whole affinity mask of the {world}-GPU "
+                              "node" if node else
+                              f"{share} host cores = 16 per GPU x {world} GPU(s), the pool's "
+                              "CPU share") + f" (affinity mask {aff}, os.cpu_count() "
+                             f"{os.cpu_count()})")
+            out["cpu_baseline"]["all_cores"] = allc
+            out["incomplete"]["cpu_baseline"] = cpu_baseline_incomplete(
+                args.n, args.shards, B_inc, args.cpu_inc_shards)
+        except Exception as e:  # noqa: BLE001
+            sys.stderr.write(f"bench.py: CPU baselines failed: {type(e).__name__}: {e}\n")
+            out.setdefault("cpu_baseline", {})["error"] = f"{type(e).__name__}: {e}"
     if rank == 0 and world == 1:
         progress("drop-in C3")
-        d3 = drop_in_C3()
-        if "cpu_baseline" in out:  # the reference restated: T x one est.UnN of this run
-            unn_s = out["cpu_baseline"]["value"]
-            d3["cpu_port_ms_per_call"] = 4 * N_SHARDS * (n // N_SHARDS) ** 2 / unn_s * 1e3
-            d3["cpu_port_note"] = ("4 x the cpu_baseline est.UnN time (same blocks, NumPy "
-                                   "broadcast compare, 1 core); not rerun here (~23 s)")
-        out["drop_in_C3"] = d3
+
+        def drop_in():
+            d3 = drop_in_C3()
+            if "value" in out.get("cpu_baseline", {}):  # the reference restated: T x est.UnN
+                unn_s = out["cpu_baseline"]["value"]
+                d3["cpu_port_ms_per_call"] = 4 * N_SHARDS * (n // N_SHARDS) ** 2 / unn_s * 1e3
+                d3["cpu_port_note"] = ("4 x the cpu_baseline est.UnN time (same blocks, NumPy "
+                                       "broadcast compare, 1 core); not rerun here (~23 s)")
+            return d3
+        out["drop_in_C3"] = guarded("drop_in_C3", drop_in, collective=False, independent=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:
