@@ -1073,6 +1073,8 @@ def main():
     # and the chunk's emission
     chain_ms = EventPool(torch, 64)
     ops.count_chain = chain_ms.wrap(ops.count_chain, weight=lambda *a, **kw: a[5])
+    # (over ranks the chunk's unpack and count run as one native call: timed together)
+    ops.chain_unpack_count = chain_ms.wrap(ops.chain_unpack_count, weight=lambda *a, **kw: a[2])
     emit_ms = EventPool(torch, 64)
     ops.chain_emit = emit_ms.wrap(ops.chain_emit, weight=lambda *a, **kw: len(a[8]))
     chain_path = S._chain_ok()

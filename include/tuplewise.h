@@ -921,6 +921,16 @@ int tw_chain_final_scatter(const void* d_recv, int32_t world, int64_t cap, int64
 int tw_chain_walk(int64_t x_base, int64_t n_x, int64_t n_x_all, int64_t z_base, int64_t n_z,
                   int64_t n_z_all, const uint64_t* keys_x, const uint64_t* keys_z, int32_t steps,
                   uint32_t* d_x_pos, uint32_t* d_z_pos, void* stream);
+/* A chunk's receive side over ranks in ONE call (round 6): tw_chain_unpack (its arguments, in
+ * order) then tw_count_pairs_chain on the filled bags (shard offsets d_x_off / d_z_off, largest
+ * shards max_nx / max_nz, bag strides n_x / n_z, out [steps][n_shards]), the cursors and the
+ * counts zeroed by one launch — est.UnNT's per-step counts (main.py:72-79) of a chunk. */
+int tw_chain_unpack_count(const uint64_t* d_recv, int32_t world, int32_t steps, int64_t cap,
+                          int32_t half, int64_t n_x, int64_t n_z, int64_t x_shard,
+                          int64_t z_shard, int32_t n_shards, void* d_x_bag, void* d_z_bag,
+                          uint32_t* d_cursors, int32_t* d_flag, const int64_t* d_x_off,
+                          const int64_t* d_z_off, int64_t max_nx, int64_t max_nz,
+                          uint64_t* d_out, void* stream);
 /* The incomplete statistic on the step chains over ranks (cs.UnNBT, compute_stats.py:119-123,
  * with device-RNG draws): tw_chain_unpack_exact writes every received record {image, local
  * position} of a chunk's (source, step) buckets (tw_chain_emit's exchange layout, strict

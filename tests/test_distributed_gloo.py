@@ -235,6 +235,14 @@ class OracleOpsChain(OracleOpsRank):
             x_bag[c].numpy().view(np.uint64 if half else np.uint32)[p[isx]] = v[isx]
             z_bag[c].numpy().view(np.uint32)[p[~isx] - n] = v[~isx]
 
+    def chain_unpack_count(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx,
+                           kz, n_shards, x_off_dev, z_off_dev, max_nx, max_nz, out):
+        """tw_chain_unpack_count restated: the unpack, then the count of the filled bags."""
+        self.chain_unpack(recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx, kz,
+                          n_shards)
+        return self.count_chain(x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, n, m,
+                                max_nx, max_nz, half, out)
+
     def count_chain(self, x_bag, x_off_dev, z_bag, z_off_dev, n_shards, steps, x_stride,
                     z_stride, max_nx, max_nz, half, out):
         xo, zo = x_off_dev.numpy(), z_off_dev.numpy()

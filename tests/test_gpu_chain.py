@@ -176,6 +176,12 @@ def test_chain_exchange_simulated_ranks(gpu, G, half):
         ops.count_chain(x_bag, xo, z_bag, zo, N, T, n_loc, m_loc, kx, kz, half, out)
         counts.append(out.cpu().numpy())
         assert int(flag.item()) == 0
+        # tw_chain_unpack_count: the same receive side in one call (fresh bags, garbage out)
+        xb2, zb2 = torch.empty_like(x_bag), torch.empty_like(z_bag)
+        out2 = torch.full((T, N), 12345, dtype=torch.int64, device="cuda")
+        ops.chain_unpack_count(recv, G, T, cap, half, n_loc, m_loc, xb2, zb2, flag, kx, kz, N,
+                               xo, zo, kx, kz, out2)
+        assert int(flag.item()) == 0 and np.array_equal(out2.cpu().numpy(), counts[-1])
         # each shard's region of the receiver's bags (and the tail past the last shard) holds
         # the oracle's permuted images of those positions, as a multiset (runs appended by
         # tw_chain_unpack in no particular order)

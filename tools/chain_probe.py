@@ -167,6 +167,8 @@ def rank_call(G, r, K, parts=False, carried=False):
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, 0, 1,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
                                                     x_bag=x_bag, z_bag=z_bag, cursors=cur))
+                mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx,
+                                                      kz, False, counts[i0:i0 + c]))
             else:
                 mark("emit", lambda: ops.chain_emit(xr, zr, False, xpos, zpos, first, r, G,
                                                     kxs[i0:i0 + c], kzs[i0:i0 + c], kx, kz, Nl,
@@ -175,10 +177,10 @@ def rank_call(G, r, K, parts=False, carried=False):
                 ev.record()
                 sz = G * c * (cap + 1)
                 mark("exchange (device copy)", lambda: recv[:sz].copy_(send[:sz]))
-                mark("unpack", lambda: ops.chain_unpack(recv, G, c, cap, False, nl, nl, x_bag,
-                                                        z_bag, flag, kx, kz, Nl))
-            mark("count", lambda: ops.count_chain(x_bag, xo, z_bag, zo, Nl, c, nl, nl, kx, kz,
-                                                  False, counts[i0:i0 + c]))
+                # (round 6: the product's receive side in one native call)
+                mark("unpack + count", lambda: ops.chain_unpack_count(
+                    recv, G, c, cap, False, nl, nl, x_bag, z_bag, flag, kx, kz, Nl, xo, zo, kx,
+                    kz, counts[i0:i0 + c]))
             if G > 1 and i0 + c >= K:  # the final exchange beside the last chunk's count
                 if parts:
                     mark("final exchange (side stream in the product)",

@@ -205,6 +205,8 @@ _SIGNATURES = {
                             _vp],
     "tw_chain_final_scatter": [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "tw_chain_walk": [_i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "tw_chain_unpack_count": [_vp, _i32, _i32, _i64, _i32, _i64, _i64, _i64, _i64, _i32, _vp,
+                              _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp],
     "tw_chain_unpack_exact": [_vp, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "tw_count_pairs_chain_rng": [_vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i64, _i64, _i64,
                                  _u64, _u64, _vp, _vp],

@@ -998,6 +998,14 @@ extern "C" int tw_chain_final_scatter(const void* d_recv, int32_t world, int64_t
   return TW_OK;
 }
 
+namespace tw {
+// the count launch of tw_count_pairs_chain on an output already zeroed
+static int count_chain_launch(const void* d_x_bag, const int64_t* d_x_off, int64_t x_stride,
+                              const void* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
+                              int32_t n_shards, int32_t steps, int64_t max_nx, int64_t max_nz,
+                              int32_t half, uint64_t* d_out, hipStream_t st);
+}  // namespace tw
+
 extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
                                     int64_t x_stride, const void* d_z_bag,
                                     const int64_t* d_z_off, int64_t z_stride, int32_t n_shards,
@@ -1011,6 +1019,68 @@ extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
   const int64_t bags = (int64_t)n_shards * steps;
   if (bags == 0) return TW_OK;
   TW_HIP_CHECK(tw_zero_async(d_out, 0, sizeof(uint64_t) * (size_t)bags, st));
+  return count_chain_launch(d_x_bag, d_x_off, x_stride, d_z_bag, d_z_off, z_stride, n_shards,
+                            steps, max_nx, max_nz, half, d_out, st);
+}
+
+// Over ranks, a chunk's receive side in ONE call: the unpack's cursors and the counts zeroed by
+// one launch, tw_chain_unpack's kernel, tw_count_pairs_chain's count — three launches
+// back to back from the host instead of four from two calls (at G = 8 the chunk's device work
+// is short and the host's launch gaps showed, profiles/r06s23_rank_call_timeline_G8_K4.log).
+// Arguments: tw_chain_unpack's, then the count's shard offsets, largest shards and out
+// [steps][n_shards] (bag strides n_x / n_z).
+static __global__ __launch_bounds__(256) void k_zero_two(uint32_t* __restrict__ a, int64_t na,
+                                                  uint64_t* __restrict__ b, int64_t nb) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < na + nb;
+       i += (int64_t)gridDim.x * 256) {
+    if (i < na)
+      a[i] = 0u;
+    else
+      b[i - na] = 0ull;
+  }
+}
+
+extern "C" int tw_chain_unpack_count(const uint64_t* d_recv, int32_t world, int32_t steps,
+                                     int64_t cap, int32_t half, int64_t n_x, int64_t n_z,
+                                     int64_t x_shard, int64_t z_shard, int32_t n_shards,
+                                     void* d_x_bag, void* d_z_bag, uint32_t* d_cursors,
+                                     int32_t* d_flag, const int64_t* d_x_off,
+                                     const int64_t* d_z_off, int64_t max_nx, int64_t max_nz,
+                                     uint64_t* d_out, void* stream) {
+  TW_ARG_CHECK(world >= 1 && steps >= 0 && steps <= kChainMax && cap >= 1 && n_x >= 0 &&
+                   n_z >= 0 && (half == 0 || half == 1) && (int64_t)world * steps < 65536 &&
+                   x_shard >= 0 && z_shard >= 0 && n_shards >= 0 && n_shards < kEmMaxBig &&
+                   max_nx >= 0 && max_nz >= 0,
+               "tw_chain_unpack_count: bad sizes");
+  TW_ARG_CHECK(max_nz < (1ll << 24), "tw_chain_unpack_count: shards of < 2^24 z-images");
+  const int64_t bags = (int64_t)n_shards * steps;
+  if (bags == 0) return TW_OK;
+  TW_ARG_CHECK(d_cursors != nullptr && d_flag != nullptr && d_out != nullptr,
+               "tw_chain_unpack_count: cursors, flag and out");
+  hipStream_t st = (hipStream_t)stream;
+  const int NB = 2 * (n_shards + 1);
+  const int64_t nc = (int64_t)NB * steps;
+  hipLaunchKernelGGL(k_zero_two, dim3((unsigned)std::min<int64_t>(64, ceil_div(nc + bags, 256))),
+                     dim3(256), 0, st, d_cursors, nc, d_out, bags);
+  TW_LAUNCH_CHECK();
+  if (n_x + n_z == 0) return TW_OK;
+  const int parts = (int)std::max<int64_t>(
+      1, std::min<int64_t>(ceil_div(cap, (int64_t)kBlock * kUnpackPer), 64));
+  hipLaunchKernelGGL(k_chain_unpack, dim3((unsigned)(parts * world * steps)), dim3(kBlock),
+                     sizeof(unsigned) * 2 * (size_t)NB, st, d_recv, (int)world, (int)steps, parts,
+                     cap, half ? 2 : 1, (int)half, n_x, n_z, x_shard, z_shard, (int)n_shards,
+                     d_x_bag, (uint32_t*)d_z_bag, (unsigned*)d_cursors, d_flag);
+  TW_LAUNCH_CHECK();
+  return count_chain_launch(d_x_bag, d_x_off, n_x, d_z_bag, d_z_off, n_z, n_shards, steps,
+                            max_nx, max_nz, half, d_out, st);
+}
+
+namespace tw {
+static int count_chain_launch(const void* d_x_bag, const int64_t* d_x_off, int64_t x_stride,
+                              const void* d_z_bag, const int64_t* d_z_off, int64_t z_stride,
+                              int32_t n_shards, int32_t steps, int64_t max_nx, int64_t max_nz,
+                              int32_t half, uint64_t* d_out, hipStream_t st) {
+  const int64_t bags = (int64_t)n_shards * steps;
   if (max_nx == 0 || max_nz == 0) return TW_OK;
   const ChainPlan p = plan_chain(max_nx, max_nz, bags, half != 0);
   TW_ARG_CHECK(p.blocks * (kBlock / kWave) < (1ll << 31) && bags < (1ll << 31),
@@ -1033,6 +1103,7 @@ extern "C" int tw_count_pairs_chain(const void* d_x_bag, const int64_t* d_x_off,
   TW_LAUNCH_CHECK();
   return TW_OK;
 }
+}  // namespace tw
 
 // ----------------------------------------------------------------------------- exact count
 // The exact O(n + m) count of the bags (algo="sorted", row f4) on the rank images themselves:

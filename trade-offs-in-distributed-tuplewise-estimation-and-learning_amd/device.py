@@ -253,6 +253,17 @@ class HipOps:
                int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
                L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.stream_handle())
 
+    def chain_unpack_count(self, recv, world, steps, cap, half, n, m, x_bag, z_bag, flag, kx,
+                           kz, n_shards, x_off_dev, z_off_dev, max_nx, max_nz, out):
+        """chain_unpack then count_chain in ONE native call (tw_chain_unpack_count): the
+        cursors and counts zeroed by one launch, the three launches back to back."""
+        cur = self._unpack_cursors(int(steps) * 2 * (int(n_shards) + 1), x_bag.device)
+        L.call("tw_chain_unpack_count", L.ptr(recv), int(world), int(steps), int(cap),
+               int(bool(half)), int(n), int(m), int(kx), int(kz), int(n_shards), L.ptr(x_bag),
+               L.ptr(z_bag), L.ptr(cur), L.ptr(flag), L.ptr(x_off_dev), L.ptr(z_off_dev),
+               int(max_nx), int(max_nz), L.ptr(out), L.stream_handle())
+        return out
+
     def chain_final_pack(self, X, xr, xpos, Z, zr, zpos, world, cap, cursor, send, flag):
         """The walked elements into their final positions' buckets (tw_chain_final_pack)."""
         L.call("tw_chain_final_pack", L.ptr(X), L.ptr(xr), L.ptr(xpos), int(X.numel()), L.ptr(Z),
@@ -1171,6 +1182,13 @@ class ShardedSample:
                 for a, cs, j, work in xchg:
                     if work is not None:
                         work.wait()
+                    if rng is None and not bucket and hasattr(ops, "chain_unpack_count"):
+                        # the receive side in one native call (unpack + count)
+                        ops.chain_unpack_count(recvs[j], G, cs, cap, half, n, m, x_bag[a:a + cs],
+                                               z_bag[a:a + cs], self._chain_flag, kx, kz, N,
+                                               self.x_off_dev, self.z_off_dev, self.max_nx,
+                                               self.max_nz, counts[i0 + a:i0 + a + cs])
+                        continue
                     if rng is not None:
                         ops.chain_unpack_exact(recvs[j], G, cs, cap, n, m, x_bag[a:a + cs],
                                                z_bag[a:a + cs], self._chain_flag)
