@@ -64,6 +64,9 @@ FINAL_EXCHANGE = True
 # than they hide (profiles/r06s22_chain_probe.log), and over RCCL the exchange's all-to-all
 # issued first would queue ahead of the chunks' on the communicator
 FINAL_EARLY = False
+# one process: the call's final scatters (scores and carried records, memory-bound) on a side
+# stream beside the last chunk's count (VALU-bound) instead of after it
+FINAL_BESIDE_COUNT = True
 # UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
 # exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
 CHAIN_RNG = True
@@ -1150,6 +1153,7 @@ class ShardedSample:
                 self._chain_flag = t.zeros((1,), dtype=t.int32, device=dev)
         else:
             cursors = self._work("cursors", (C * 2 * (N + 1),), t.int32)
+        scattered = None  # one process: the final scatters forked beside the last count
         for i0 in range(0, T, C):
             c = min(C, T - i0)
             if coll:
@@ -1208,7 +1212,15 @@ class ShardedSample:
             ops.chain_emit(xr, zr, half, xpos, zpos, i0 == 0, 0, 1, kxs[i0:i0 + c],
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
+            fork = None
+            if FINAL_BESIDE_COUNT and i0 + c >= T and self.X.is_cuda:
+                fork = t.cuda.Event()  # the chains' final positions are written
+                fork.record()
             count(x_bag, z_bag, c, counts[i0:i0 + c], i0)
+            if fork is not None:
+                # the final scatters (memory-bound) beside the last count (VALU-bound), on a
+                # side stream enqueued after the count's launch
+                scattered = self._final_scatter(X0, Z0, xr, zr, xpos, zpos, fork)
         carry = None
         if coll:
             if final is not None:
@@ -1229,6 +1241,11 @@ class ShardedSample:
                 carry = (final[2], final[3])
             counts = self._reduce_counts(counts, carried=verdict if verdict is not None
                                          else carried)
+        elif scattered is not None:
+            t.cuda.current_stream().wait_stream(self._final_stream)
+            self.X, self.Z = scattered[0], scattered[1]
+            if CARRY_IMAGES:
+                carry = scattered[2], scattered[3]
         else:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
             if CARRY_IMAGES:
@@ -1242,6 +1259,25 @@ class ShardedSample:
             raise _StaleImages("UnN_many: the sample was written behind its version counter; "
                                "the carried rank images are stale")
         return [np.mean(v) for v in vals]
+
+    def _final_scatter(self, X0, Z0, xr, zr, xpos, zpos, fork):
+        """One process: the final arrays and (CARRY_IMAGES) the carried records scattered by
+        the chains' last positions (tw_chain_scatter) on the final stream, after `fork` (an
+        event behind the last emission): (X, Z[, X records, Z records]), recorded for the main
+        stream, which waits for the final stream before using them."""
+        t = self.t
+        main = t.cuda.current_stream()
+        if getattr(self, "_final_stream", None) is None:
+            self._final_stream = t.cuda.Stream()
+        fs = self._final_stream
+        fs.wait_event(fork)
+        with t.cuda.stream(fs):
+            out = self.ops.chain_scatter(X0, xpos, Z0, zpos)
+            if CARRY_IMAGES:
+                out = out + self.ops.chain_scatter(xr, xpos, zr, zpos)
+            for a in out:
+                a.record_stream(main)
+        return out
 
     def _final_exchange(self, xr, zr, xpos=None, zpos=None, es=None, walk=None):
         """The call's final arrays over ranks (FINAL_EXCHANGE): on the final stream, this
