@@ -65,8 +65,12 @@ FINAL_EXCHANGE = True
 # issued first would queue ahead of the chunks' on the communicator
 FINAL_EARLY = False
 # one process: the call's final scatters (scores and carried records, memory-bound) on a side
-# stream beside the last chunk's count (VALU-bound) instead of after it
+# stream beside the last chunk's count (VALU-bound) instead of after it — when that count is
+# short (<= FINAL_BESIDE_MAX_STEPS steps): its blocks, starved beside a long count, hold wave
+# slots the count needs (K = 4 1.994 -> 1.957 ms per call, K = 20 8.878 -> 8.946,
+# profiles/r06s33_ab_final_scatter.log)
 FINAL_BESIDE_COUNT = True
+FINAL_BESIDE_MAX_STEPS = 8
 # UnNB_many over ranks on the step chains (one exchange per chunk of CHAIN_MAX steps, bags at
 # exact positions, tw_count_pairs_chain_rng) instead of one repartition exchange per step
 CHAIN_RNG = True
@@ -517,10 +521,16 @@ class ShardedSample:
         with expect / verdict, also the verdict word (see HipOps.words_checksum)."""
         if not hasattr(self.ops, "words_checksum"):
             return None
+        return self._hash_pair(self.X, self.Z, expect, verdict, good, bad)
+
+    def _hash_pair(self, X, Z, expect=None, verdict=None, good=1, bad=0):
+        """_checksum of the arrays X / Z (None where the ops lack the entry)."""
+        if not hasattr(self.ops, "words_checksum"):
+            return None
         if getattr(self, "_acc_words", None) is None:
             self._acc_words = int(getattr(self.ops, "checksum_acc_words", lambda: 1)())
-        acc = self.t.empty((self._acc_words,), dtype=self.t.int64, device=self.X.device)
-        return self.ops.words_checksum(self.X, self.Z, acc, expect, verdict, good, bad)[:1]
+        acc = self.t.empty((self._acc_words,), dtype=self.t.int64, device=X.device)
+        return self.ops.words_checksum(X, Z, acc, expect, verdict, good, bad)[:1]
 
     def _host_verdict(self):
         """The pinned (device-mapped) host word the one-process verdict is written into."""
@@ -1044,7 +1054,19 @@ class ShardedSample:
             if cs is not None:
                 verdict = (self.t.empty((1,), dtype=self.t.int64, device=self.X.device) if coll
                            else self._host_verdict())
-                self._checksum(cs, verdict, 1, self.G + 1 if coll else 0)
+                if self.X.is_cuda:
+                    # on a side stream beside the emission (both only read): joined before the
+                    # counts' reduction / the host's read of the verdict
+                    if getattr(self, "_guard_stream", None) is None:
+                        self._guard_stream = self.t.cuda.Stream()
+                    gs = self._guard_stream
+                    gs.wait_stream(self.t.cuda.current_stream())
+                    with self.t.cuda.stream(gs):
+                        self._checksum(cs, verdict, 1, self.G + 1 if coll else 0)
+                    if coll:
+                        verdict.record_stream(gs)  # (made on the main stream, written on gs)
+                else:
+                    self._checksum(cs, verdict, 1, self.G + 1 if coll else 0)
         # over ranks the call's final arrays and carried records come by ONE exchange of the
         # walked elements to the ranks holding their final positions (FINAL_EXCHANGE,
         # tw_chain_final_pack / _scatter) instead of the all-gathers of X and of both record
@@ -1213,7 +1235,8 @@ class ShardedSample:
                            kzs[i0:i0 + c], kx, kz, N, x_bag=x_bag, z_bag=z_bag,
                            cursors=cursors)
             fork = None
-            if FINAL_BESIDE_COUNT and i0 + c >= T and self.X.is_cuda:
+            if (FINAL_BESIDE_COUNT and i0 + c >= T and c <= FINAL_BESIDE_MAX_STEPS
+                    and self.X.is_cuda):
                 fork = t.cuda.Event()  # the chains' final positions are written
                 fork.record()
             count(x_bag, z_bag, c, counts[i0:i0 + c], i0)
@@ -1239,20 +1262,26 @@ class ShardedSample:
             self.X, self.Z = final[0], final[1]
             if RX is not None:
                 carry = (final[2], final[3])
+            self._join_guard()
             counts = self._reduce_counts(counts, carried=verdict if verdict is not None
                                          else carried)
         elif scattered is not None:
             t.cuda.current_stream().wait_stream(self._final_stream)
-            self.X, self.Z = scattered[0], scattered[1]
+            self.X, self.Z = scattered[0][0], scattered[0][1]
             if CARRY_IMAGES:
-                carry = scattered[2], scattered[3]
+                carry = scattered[0][2], scattered[0][3]
         else:
             self.X, self.Z = ops.chain_scatter(X0, xpos, Z0, zpos)
             if CARRY_IMAGES:
                 carry = ops.chain_scatter(xr, xpos, zr, zpos)
+        if not coll:
+            self._join_guard()
         if carry is not None:  # after the assignments above (they drop the old ones)
+            # (the hash of the new arrays: made on the final stream beside the count when the
+            # scatters ran there)
+            h = scattered[1] if scattered is not None else self._checksum()
             self._carry = (self._X, self._Z, self._X._version, self._Z._version, half,
-                           carry[0], carry[1], self._checksum())
+                           carry[0], carry[1], h)
         # (over ranks: raises _StaleImages on a bad verdict sum)
         vals = self.values(counts, pairs=None if rng is None else rng[0])
         if verdict is not None and not coll and int(verdict[0]) != 1:
@@ -1271,13 +1300,21 @@ class ShardedSample:
             self._final_stream = t.cuda.Stream()
         fs = self._final_stream
         fs.wait_event(fork)
+        h = None
         with t.cuda.stream(fs):
             out = self.ops.chain_scatter(X0, xpos, Z0, zpos)
             if CARRY_IMAGES:
                 out = out + self.ops.chain_scatter(xr, xpos, zr, zpos)
-            for a in out:
+                h = self._hash_pair(out[0], out[1])  # the carried images' guard hash
+            for a in out + ((h,) if h is not None else ()):
                 a.record_stream(main)
-        return out
+        return out, h
+
+    def _join_guard(self):
+        """The main stream after the guard stream's verdict hash (a no-op without one)."""
+        gs = getattr(self, "_guard_stream", None)
+        if gs is not None:
+            self.t.cuda.current_stream().wait_stream(gs)
 
     def _final_exchange(self, xr, zr, xpos=None, zpos=None, es=None, walk=None):
         """The call's final arrays over ranks (FINAL_EXCHANGE): on the final stream, this
