@@ -293,6 +293,55 @@ def test_replicate_equals_reference_loop(gpu, which):
     assert got == want and probe_got == probe_want
 
 
+@pytest.mark.parametrize("case", ["sizes_change", "empty_blocks", "half_ties", "floats"])
+def test_replicate_fixed_layout_equals_general(gpu, case):
+    """replicate's fixed-layout path (Un / prop-SWOR: snapshot rows, broadcast offsets, row
+    means) == the general per-block path and, where the oracle covers it, the reference loop:
+    tries whose sizes change (the layout is rebuilt after a flush), plans with empty blocks
+    (the general path's nan), tie_mode="half", float scores with ties."""
+    import tuplewise.estimation as est
+    sizes = {"sizes_change": [(300, 40), (301, 40), (300, 41)], "empty_blocks": [(95, 3)],
+             "half_ties": [(400, 60)], "floats": [(350, 45)]}[case]
+    it = {"i": 0}
+
+    def gen_X():
+        n = sizes[it["i"] % len(sizes)][0]
+        if case == "floats":
+            return np.round(np.random.normal(0.2, 1, n), 1)
+        return 2 * np.random.binomial(1, 0.9, n)
+
+    def gen_Z():
+        m = sizes[it["i"] % len(sizes)][1]
+        it["i"] += 1
+        if case == "floats":
+            return np.round(np.random.normal(0, 1, m), 1)
+        return 2 * np.random.binomial(1, 0.1, m) - 1
+    tie = "half" if case == "half_ties" else "strict"
+    spec = (est._UN_HALF if tie == "half" else est._UN_STRICT)._tw_block
+    for which, args, reps, N, st in (("Un", (), 1, None, None),
+                                     ("UnN", (10, "prop-SWOR"), 1, 10, "prop-SWOR"),
+                                     ("UnNT", (10, 3, "prop-SWOR"), 3, 10, "prop-SWOR")):
+        fn = getattr(est, which)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            np.random.seed(4)
+            it["i"] = 0
+            got = est.replicate(fn, gen_X, gen_Z, 25, *args, tie_mode=tie, flush_elems=3000)
+            probe_got = np.random.randint(2 ** 30)
+            np.random.seed(4)
+            it["i"] = 0
+            want = est._replicate_general(fn, gen_X, gen_Z, 25, spec, reps, N, st, 3000)
+            probe_want = np.random.randint(2 ** 30)
+            assert probe_got == probe_want, which
+            assert np.array_equal(np.array(got), np.array(want), equal_nan=True), which
+            if tie == "strict":
+                fo = {"Un": O.est_Un, "UnN": O.est_UnN, "UnNT": O.est_UnNT}[which]
+                np.random.seed(4)
+                it["i"] = 0
+                ref = [fo(gen_X(), gen_Z(), *args) for _ in range(25)]
+                assert np.array_equal(np.array(got), np.array(ref), equal_nan=True), which
+
+
 def test_pipelined_unn_many_equals_sequential(gpu):
     """ShardedSample.UnN_many (repartition i+1 on a side stream during the counts of step i,
     counts combined at the end) == one UnN call per key, value for value, and leaves the

@@ -7,7 +7,9 @@ to the reference loop).  Prints wall time and the variance ratios the paper plot
 the HOST FLOOR of the same loop — the NumPy work the drop-in must do on the host to stay
 bit-identical (the generators' binomial draws, and for UnN / UnNT the in-place
 np.random.shuffle of X and Z per repartition, main.py:46-47) with no estimator at all — which
-bounds what any device can save on this experiment.
+bounds what any device can save on this experiment.  Round 6, late: the floor again with the
+drop-in's own native shuffles, and estimation.replicate's fixed-layout path (Un / prop-SWOR:
+snapshot rows, broadcast offsets, row means instead of per-block Python).
 """
 import argparse
 import pathlib
@@ -68,5 +70,21 @@ for e in eps:
                 np.random.shuffle(z)
 fl = time.perf_counter() - t0
 print(f"host floor (generators + the reference's in-place shuffles, no estimator): {fl:.2f} s "
-      f"= {fl / dt:.2f} of the device run; device-side remainder {dt - fl:.2f} s "
-      f"({(dt - fl) / (len(eps) * a.tries * 3) * 1e6:.1f} us per estimator call)")
+      f"= {fl / dt:.2f} of the device run")
+# the same with the drop-in's own in-place shuffles (numpy_rng.shuffle_pair: NumPy's legacy
+# draws and swaps in native code, bit-identical): the floor the drop-in itself runs against
+from tuplewise._blocks import shuffle_pair  # noqa: E402
+np.random.seed(0)
+t0 = time.perf_counter()
+for e in eps:
+    gx = lambda: 2 * np.random.binomial(1, 1 - e, n)
+    gz = lambda: 2 * np.random.binomial(1, e, m) - 1
+    for shuffles in (0, 1, T):
+        for _ in range(a.tries):
+            x, z = gx(), gz()
+            for _ in range(shuffles):
+                shuffle_pair(x, z)
+fn = time.perf_counter() - t0
+print(f"host floor with the drop-in's native shuffles: {fn:.2f} s = {fn / dt:.2f} of the device "
+      f"run; the rest {dt - fn:.2f} s ({(dt - fn) / (len(eps) * a.tries * 3) * 1e6:.1f} us per "
+      f"estimator call: snapshots, one batched count per ~16M scores, block values)")

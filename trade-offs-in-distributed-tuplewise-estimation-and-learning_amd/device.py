@@ -794,12 +794,26 @@ class ShardedSample:
         shard (default: all pairs of each shard; B for the incomplete statistic)."""
         c = np.asarray(counts.cpu().numpy()).view(np.uint64)
         self.check_exchange()
-        keep = np.tile(self.keep, self.G)
-        scale = 2 if self.tie_mode == "half" else 1
-        per = np.tile(self.pairs, self.G) if pairs is None else [pairs] * (self.G * self.N)
-        # uint64 -> float64 and Python int -> float are both correctly rounded, like E.ratio
-        den = np.array([float(scale * int(p)) for p in per])
+        # the denominators and kept shards of this layout, built once per (pairs, tie mode):
+        # this runs after the call's device work, on its critical path
+        ck = (pairs, self.tie_mode, self.G, self.N)
+        cache = self.__dict__.setdefault("_den_cache", {})
+        ent = cache.get(ck)
+        if ent is None:
+            keep = np.tile(self.keep, self.G)
+            scale = 2 if self.tie_mode == "half" else 1
+            per = np.tile(self.pairs, self.G) if pairs is None else [pairs] * (self.G * self.N)
+            # uint64 -> float64 and Python int -> float are both correctly rounded, like E.ratio
+            den = np.array([float(scale * int(p)) for p in per])
+            ent = cache[ck] = (keep, den)
+        keep, den = ent
         return (c.astype(np.float64) / den)[..., keep]
+
+    @staticmethod
+    def _row_means(vals) -> list:
+        """np.mean of each row (the per-step estimates): one reduction over the last,
+        contiguous axis — the same pairwise sums as np.mean of each row alone."""
+        return list(np.ascontiguousarray(vals).mean(axis=-1))
 
     def UnN(self, key=None) -> np.float64:
         """Block-wise complete U-statistic over all G*N shards (est.UnN with prop-SWOR,
@@ -914,7 +928,7 @@ class ShardedSample:
                                             keys)
             if r is not None:
                 counts, self.X, self.Z = r
-                return [np.mean(v) for v in self.values(counts)]
+                return self._row_means(self.values(counts))
         fusable = self.algo == "pairs"
         if fusable and self._rank_path_ok():
             r = self._unn_many_rank(keys)
@@ -933,7 +947,7 @@ class ShardedSample:
                                            self.max_nx, self.max_nz, self.dtype, self.pred, out,
                                            Xn, kx, Zn, kz, out_n)
         counts = self._run_steps(keys, lambda i: self.local_counts(), fusable, step)
-        return [np.mean(v) for v in self.values(counts)]
+        return self._row_means(self.values(counts))
 
     def _rank_path_ok(self) -> bool:
         """The all-pairs steps on rank images (csrc/rankimage.hip) apply to the strict
@@ -1004,7 +1018,7 @@ class ShardedSample:
             xr, zr = self.X, self.Z
             self.X = self.ops.gather_records(X0, xr)
             self.Z = self.ops.gather_records(Z0, zr)
-        return [np.mean(v) for v in self.values(counts)]
+        return self._row_means(self.values(counts))
 
     def _unn_many_chain(self, keys, bucket=False, rng=None):
         """_chain_call, recounted once from a fresh ranking when the carried images turn out
@@ -1287,7 +1301,7 @@ class ShardedSample:
         if verdict is not None and not coll and int(verdict[0]) != 1:
             raise _StaleImages("UnN_many: the sample was written behind its version counter; "
                                "the carried rank images are stale")
-        return [np.mean(v) for v in vals]
+        return self._row_means(vals)
 
     def _final_scatter(self, X0, Z0, xr, zr, xpos, zpos, fork):
         """One process: the final arrays and (CARRY_IMAGES) the carried records scattered by
@@ -1442,4 +1456,4 @@ class ShardedSample:
                                         B, seeds[i], self.rank * self.N, self.dtype, self.pred,
                                         self.max_nx, self.max_nz, out, Xn, kx, Zn, kz, out_n)
         counts = self._run_steps(keys, lambda i: self._count_rng(B, seeds[i]), False, step)
-        return [np.mean(v) for v in self.values(counts, pairs=B)]
+        return self._row_means(self.values(counts, pairs=B))

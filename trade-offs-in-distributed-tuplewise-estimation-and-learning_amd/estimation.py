@@ -109,7 +109,8 @@ def replicate(estimator, gen_X, gen_Z, n_tries, *args, flush_elems=1 << 24, **kw
         raise TypeError(f"unexpected keyword arguments {sorted(kwargs)}")
     spec = (_UN_HALF if tie_mode == "half" else _UN_STRICT)._tw_block
     if estimator is Un:
-        reps, mk = 1, None
+        reps = 1
+        N = sampling_type = None
     elif estimator is UnN:
         N, sampling_type = args
         reps = 1
@@ -118,7 +119,19 @@ def replicate(estimator, gen_X, gen_Z, n_tries, *args, flush_elems=1 << 24, **kw
         reps = T
     else:
         raise ValueError("replicate supports estimation.Un, UnN and UnNT")
+    if estimator is Un or (sampling_type.startswith("prop") and sampling_type != "prop-SWR"):
+        # the fixed-layout plans (Un's one block; prop-SWOR's N blocks of fixed sizes, no RNG
+        # draw in the plan): tries batched into preallocated snapshot rows, no per-block Python
+        return _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N,
+                                sampling_type, flush_elems)
+    return _replicate_general(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_type,
+                              flush_elems)
 
+
+def _replicate_general(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_type,
+                       flush_elems):
+    """replicate() for any plan: per try and repetition, plan_un's shuffles and draws, a
+    snapshot and its blocks; the pending tries' blocks counted in one launch per flush."""
     results = []
     pending = []  # (try index, [(plan, job) per repetition])
     jobs = []
@@ -158,4 +171,108 @@ def replicate(estimator, gen_X, gen_Z, n_tries, *args, flush_elems=1 << 24, **kw
             flush()
     if jobs:
         flush()
+    return results
+
+
+def _fixed_layout(n, m, N, spec, sampling_type):
+    """The block ranges of a plan that depends on the sizes only (Un: one whole block;
+    prop-SWOR: plan_un's N blocks, which draw nothing), as (x starts, x end, z starts, z end,
+    pairs per block) — or None where the plan has an empty block (the general path's nan) or
+    a block that is not a consecutive slice."""
+    if N is None:
+        xs, zs = [(0, n)], [(0, m)]
+    else:
+        plan = Bk.plan_un(np.empty(n), np.empty(m), N, spec, sampling_type, "est",
+                          shuffle=lambda a, b: None)
+        if not plan or any(p[0] != "val" for p in plan):
+            return None
+        xs = [p[1].x for p in plan]
+        zs = [p[1].z for p in plan]
+        if not all(isinstance(a, tuple) for a in xs + zs):
+            return None
+    for sel in (xs, zs):
+        if sel[0][0] != 0 or any(a[1] != b[0] for a, b in zip(sel, sel[1:])):
+            return None
+    pairs = np.array([(a[1] - a[0]) * (b[1] - b[0]) for a, b in zip(xs, zs)], dtype=np.int64)
+    if not np.all(pairs > 0):
+        return None
+    return (np.array([a[0] for a in xs], dtype=np.int64), xs[-1][1],
+            np.array([b[0] for b in zs], dtype=np.int64), zs[-1][1], pairs)
+
+
+def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_type,
+                     flush_elems):
+    """replicate() for fixed-layout plans: every try's snapshot (after its in-place shuffles,
+    per repetition) is copied into one row of a preallocated host buffer holding only the
+    elements the blocks read; a flush counts all rows' blocks in one launch with offsets built
+    by broadcasting, and the block values, each try's np.mean over its blocks and UnNT's mean
+    over its repetitions are row reductions (np.mean's pairwise sums along the contiguous last
+    axis, the same bits as np.mean of each row).  The same draws, shuffles and values as the
+    general path; a try whose shapes or dtypes differ from the last one's flushes first and
+    gets its own layout."""
+    from . import _engine as E
+    from . import _lib as L
+    results = []
+    st = {"key": None}
+
+    def new_layout(X, Z):
+        lay = _fixed_layout(X.shape[0], Z.shape[0], N, spec, sampling_type)
+        st["key"] = (X.shape, Z.shape, X.dtype, Z.dtype)
+        st["lay"] = lay
+        if lay is None:
+            return
+        xs, lx, zs, lz, _ = lay
+        rows = max(reps, (max(1, flush_elems // max(1, lx + lz)) // reps) * reps)
+        st["bx"] = np.empty((rows, lx), dtype=X.dtype)
+        st["bz"] = np.empty((rows, lz), dtype=Z.dtype)
+        st["rows"] = 0
+
+    def flush():
+        J = st.get("rows", 0)
+        if not J:
+            return
+        xs, lx, zs, lz, pairs = st["lay"]
+        x, z, code, mode = spec.operands(st["bx"][:J].reshape(-1), st["bz"][:J].reshape(-1))
+        nb = len(xs)
+        xo = np.concatenate([(np.arange(J, dtype=np.int64)[:, None] * lx + xs).ravel(),
+                             [J * lx]]).astype(np.int64)
+        zo = np.concatenate([(np.arange(J, dtype=np.int64)[:, None] * lz + zs).ravel(),
+                             [J * lz]]).astype(np.int64)
+        xa, za, xod, zod = L.to_device_many([x, z, xo, zo])
+        sh = E.Shards(xa, xo, za, zo, code)
+        sh._x_off_dev, sh._z_off_dev = xod, zod
+        counts = np.asarray(E.count_complete(sh, mode)).view(np.uint64)
+        den = (2 * pairs if mode == "half" else pairs).astype(np.float64)
+        # E.ratio per block: float64(count) / float64(pairs), correctly rounded either way
+        vals = counts.astype(np.float64).reshape(J, nb) / den
+        per = vals[:, 0] if N is None else vals.mean(axis=-1)  # finish_un: np.mean per plan
+        per = per.reshape(J // reps, reps)
+        results.extend(per[:, 0] if reps == 1 else per.mean(axis=-1))
+        st["rows"] = 0
+
+    for _ in range(n_tries):
+        X = np.asarray(gen_X())
+        Z = np.asarray(gen_Z())
+        if (X.shape, Z.shape, X.dtype, Z.dtype) != st["key"] or X.ndim != 1 or Z.ndim != 1:
+            flush()
+            if X.ndim != 1 or Z.ndim != 1:
+                st["key"], st["lay"] = None, None
+            else:
+                new_layout(X, Z)
+        if st.get("lay") is None:  # this try by the general path (its own launch)
+            results.extend(_replicate_general(estimator, iter([X]).__next__,
+                                              iter([Z]).__next__, 1, spec, reps, N,
+                                              sampling_type, 0))
+            continue
+        xs, lx, zs, lz, _ = st["lay"]
+        for _ in range(reps):
+            if N is not None:
+                Bk.shuffle_pair(X, Z)  # plan_un's in-place shuffles, bit for bit
+            r = st["rows"]
+            st["bx"][r] = X[:lx]
+            st["bz"][r] = Z[:lz]
+            st["rows"] = r + 1
+        if st["rows"] == st["bx"].shape[0]:
+            flush()
+    flush()
     return results
