@@ -491,9 +491,67 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
     if (isinstance(X, np.ndarray) and isinstance(Z, np.ndarray)
             and _device_shuffle_ok(X, Z, spec)):
         return _run_un_repeated_device(X, Z, N, spec, sampling_type, variant, 1)
+    if (isinstance(X, np.ndarray) and isinstance(Z, np.ndarray) and X.ndim == 1
+            and Z.ndim == 1 and sampling_type.startswith("prop") and sampling_type != "prop-SWR"
+            and fixed_layout(X.shape[0], Z.shape[0], N, spec, sampling_type) is not None):
+        return run_un_repeated(X, Z, N, spec, sampling_type, variant, 1)  # the fixed layout
     plan = plan_un(X, Z, N, spec, sampling_type, variant)
     blocks = [p[1] for p in plan if p[0] == "val"]
     return finish_un(plan, spec.evaluate(X, Z, blocks) if blocks else [])
+
+
+_LAYOUTS = {}  # (n, m, N, sampling_type, spec) -> fixed_layout
+
+
+def fixed_layout(n, m, N, spec, sampling_type):
+    """The block ranges of a plan that depends on the sizes only — Un's one whole block
+    (N None) or prop-SWOR / prop-SWR-free plan_un's N blocks, which draw nothing — as
+    (x starts, x end, z starts, z end, pairs per block); None where the spec is not a
+    CompleteCount, the plan has an empty block or skips one (the general path's nan / the
+    reference's assert), or a block is not a consecutive slice from 0.  Cached per shape."""
+    key = (n, m, N, sampling_type, spec)
+    if key in _LAYOUTS:
+        return _LAYOUTS[key]
+    lay = None
+    if type(spec) is CompleteCount:
+        if N is None:
+            xs, zs = [(0, n)], [(0, m)]
+        else:
+            plan = plan_un(np.empty(n), np.empty(m), N, spec, sampling_type, "est",
+                           shuffle=lambda a, b: None)
+            ok = bool(plan) and all(p[0] == "val" for p in plan)
+            xs = [p[1].x for p in plan] if ok else []
+            zs = [p[1].z for p in plan] if ok else []
+        if xs and all(isinstance(a, tuple) for a in xs + zs) and all(
+                sel[0][0] == 0 and all(a[1] == b[0] for a, b in zip(sel, sel[1:]))
+                for sel in (xs, zs)):
+            pairs = np.array([(a[1] - a[0]) * (b[1] - b[0]) for a, b in zip(xs, zs)],
+                             dtype=np.int64)
+            if np.all(pairs > 0):
+                lay = (np.array([a[0] for a in xs], dtype=np.int64), xs[-1][1],
+                       np.array([b[0] for b in zs], dtype=np.int64), zs[-1][1], pairs)
+    if len(_LAYOUTS) > 256:
+        _LAYOUTS.clear()
+    _LAYOUTS[key] = lay
+    return lay
+
+
+def fixed_values(spec, bx, bz, lay) -> np.ndarray:
+    """Block values (J, blocks) of J snapshot rows bx (J, x end) / bz (J, z end) under one
+    fixed layout: one upload, one count launch over all rows' blocks (offsets by
+    broadcasting), E.ratio's float64(count) / float64(pairs) as one array division."""
+    xs, lx, zs, lz, pairs = lay
+    J = bx.shape[0]
+    x, z, code, mode = spec.operands(bx.reshape(-1), bz.reshape(-1))
+    rows = np.arange(J, dtype=np.int64)[:, None]
+    xo = np.append((rows * lx + xs).ravel(), J * lx).astype(np.int64)
+    zo = np.append((rows * lz + zs).ravel(), J * lz).astype(np.int64)
+    xa, za, xod, zod = L.to_device_many([x, z, xo, zo])
+    sh = E.Shards(xa, xo, za, zo, code)
+    sh._x_off_dev, sh._z_off_dev = xod, zod
+    counts = np.asarray(E.count_complete(sh, mode)).view(np.uint64)
+    den = (2 * pairs if mode == "half" else pairs).astype(np.float64)
+    return counts.astype(np.float64).reshape(J, len(xs)) / den
 
 
 def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
@@ -507,6 +565,19 @@ def run_un_repeated(X, Z, N, spec, sampling_type, variant: str, T: int):
         return None
     if _device_shuffle_ok(X, Z, spec, N, T):
         return _run_un_repeated_device(X, Z, N, spec, sampling_type, variant, T)
+    if (X.ndim == 1 and Z.ndim == 1 and sampling_type.startswith("prop")
+            and sampling_type != "prop-SWR" and T >= 1):
+        lay = fixed_layout(X.shape[0], Z.shape[0], N, spec, sampling_type)
+        if lay is not None:
+            # the T snapshots as rows, all blocks in one launch, the plan means and the
+            # repetitions' mean as row reductions (the same bits as finish_un / np.mean)
+            bx = np.empty((T, lay[1]), dtype=X.dtype)
+            bz = np.empty((T, lay[3]), dtype=Z.dtype)
+            for t in range(T):
+                shuffle_pair(X, Z)  # plan_un's in-place shuffles, bit for bit
+                bx[t] = X[:lay[1]]
+                bz[t] = Z[:lay[3]]
+            return np.mean(fixed_values(spec, bx, bz, lay).mean(axis=-1))
     plans, jobs = [], []
     for t in range(T):
         plan = plan_un(X, Z, N, spec, sampling_type, variant)

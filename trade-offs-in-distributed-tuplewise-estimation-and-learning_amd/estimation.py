@@ -174,32 +174,6 @@ def _replicate_general(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling
     return results
 
 
-def _fixed_layout(n, m, N, spec, sampling_type):
-    """The block ranges of a plan that depends on the sizes only (Un: one whole block;
-    prop-SWOR: plan_un's N blocks, which draw nothing), as (x starts, x end, z starts, z end,
-    pairs per block) — or None where the plan has an empty block (the general path's nan) or
-    a block that is not a consecutive slice."""
-    if N is None:
-        xs, zs = [(0, n)], [(0, m)]
-    else:
-        plan = Bk.plan_un(np.empty(n), np.empty(m), N, spec, sampling_type, "est",
-                          shuffle=lambda a, b: None)
-        if not plan or any(p[0] != "val" for p in plan):
-            return None
-        xs = [p[1].x for p in plan]
-        zs = [p[1].z for p in plan]
-        if not all(isinstance(a, tuple) for a in xs + zs):
-            return None
-    for sel in (xs, zs):
-        if sel[0][0] != 0 or any(a[1] != b[0] for a, b in zip(sel, sel[1:])):
-            return None
-    pairs = np.array([(a[1] - a[0]) * (b[1] - b[0]) for a, b in zip(xs, zs)], dtype=np.int64)
-    if not np.all(pairs > 0):
-        return None
-    return (np.array([a[0] for a in xs], dtype=np.int64), xs[-1][1],
-            np.array([b[0] for b in zs], dtype=np.int64), zs[-1][1], pairs)
-
-
 def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_type,
                      flush_elems):
     """replicate() for fixed-layout plans: every try's snapshot (after its in-place shuffles,
@@ -210,18 +184,16 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
     axis, the same bits as np.mean of each row).  The same draws, shuffles and values as the
     general path; a try whose shapes or dtypes differ from the last one's flushes first and
     gets its own layout."""
-    from . import _engine as E
-    from . import _lib as L
     results = []
     st = {"key": None}
 
     def new_layout(X, Z):
-        lay = _fixed_layout(X.shape[0], Z.shape[0], N, spec, sampling_type)
+        lay = Bk.fixed_layout(X.shape[0], Z.shape[0], N, spec, sampling_type)
         st["key"] = (X.shape, Z.shape, X.dtype, Z.dtype)
         st["lay"] = lay
         if lay is None:
             return
-        xs, lx, zs, lz, _ = lay
+        lx, lz = lay[1], lay[3]
         rows = max(reps, (max(1, flush_elems // max(1, lx + lz)) // reps) * reps)
         st["bx"] = np.empty((rows, lx), dtype=X.dtype)
         st["bz"] = np.empty((rows, lz), dtype=Z.dtype)
@@ -231,20 +203,7 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
         J = st.get("rows", 0)
         if not J:
             return
-        xs, lx, zs, lz, pairs = st["lay"]
-        x, z, code, mode = spec.operands(st["bx"][:J].reshape(-1), st["bz"][:J].reshape(-1))
-        nb = len(xs)
-        xo = np.concatenate([(np.arange(J, dtype=np.int64)[:, None] * lx + xs).ravel(),
-                             [J * lx]]).astype(np.int64)
-        zo = np.concatenate([(np.arange(J, dtype=np.int64)[:, None] * lz + zs).ravel(),
-                             [J * lz]]).astype(np.int64)
-        xa, za, xod, zod = L.to_device_many([x, z, xo, zo])
-        sh = E.Shards(xa, xo, za, zo, code)
-        sh._x_off_dev, sh._z_off_dev = xod, zod
-        counts = np.asarray(E.count_complete(sh, mode)).view(np.uint64)
-        den = (2 * pairs if mode == "half" else pairs).astype(np.float64)
-        # E.ratio per block: float64(count) / float64(pairs), correctly rounded either way
-        vals = counts.astype(np.float64).reshape(J, nb) / den
+        vals = Bk.fixed_values(spec, st["bx"][:J], st["bz"][:J], st["lay"])
         per = vals[:, 0] if N is None else vals.mean(axis=-1)  # finish_un: np.mean per plan
         per = per.reshape(J // reps, reps)
         results.extend(per[:, 0] if reps == 1 else per.mean(axis=-1))
@@ -264,7 +223,7 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
                                               iter([Z]).__next__, 1, spec, reps, N,
                                               sampling_type, 0))
             continue
-        xs, lx, zs, lz, _ = st["lay"]
+        lx, lz = st["lay"][1], st["lay"][3]
         for _ in range(reps):
             if N is not None:
                 Bk.shuffle_pair(X, Z)  # plan_un's in-place shuffles, bit for bit
