@@ -500,7 +500,7 @@ def run_un(X, Z, N, f_block, sampling_type, variant: str):
     return finish_un(plan, spec.evaluate(X, Z, blocks) if blocks else [])
 
 
-_LAYOUTS = {}  # (n, m, N, sampling_type, spec) -> fixed_layout
+_LAYOUTS = {}  # (n, m, N, sampling_type) -> fixed_layout (CompleteCount plans draw nothing)
 
 
 def fixed_layout(n, m, N, spec, sampling_type):
@@ -509,27 +509,28 @@ def fixed_layout(n, m, N, spec, sampling_type):
     (x starts, x end, z starts, z end, pairs per block); None where the spec is not a
     CompleteCount, the plan has an empty block or skips one (the general path's nan / the
     reference's assert), or a block is not a consecutive slice from 0.  Cached per shape."""
-    key = (n, m, N, sampling_type, spec)
+    if type(spec) is not CompleteCount:
+        return None
+    key = (n, m, N, sampling_type)
     if key in _LAYOUTS:
         return _LAYOUTS[key]
-    lay = None
-    if type(spec) is CompleteCount:
-        if N is None:
-            xs, zs = [(0, n)], [(0, m)]
-        else:
-            plan = plan_un(np.empty(n), np.empty(m), N, spec, sampling_type, "est",
-                           shuffle=lambda a, b: None)
-            ok = bool(plan) and all(p[0] == "val" for p in plan)
-            xs = [p[1].x for p in plan] if ok else []
-            zs = [p[1].z for p in plan] if ok else []
-        if xs and all(isinstance(a, tuple) for a in xs + zs) and all(
-                sel[0][0] == 0 and all(a[1] == b[0] for a, b in zip(sel, sel[1:]))
-                for sel in (xs, zs)):
-            pairs = np.array([(a[1] - a[0]) * (b[1] - b[0]) for a, b in zip(xs, zs)],
-                             dtype=np.int64)
-            if np.all(pairs > 0):
-                lay = (np.array([a[0] for a in xs], dtype=np.int64), xs[-1][1],
-                       np.array([b[0] for b in zs], dtype=np.int64), zs[-1][1], pairs)
+    lay = None  # (the plan of a CompleteCount depends on the sizes only)
+    if N is None:
+        xs, zs = [(0, n)], [(0, m)]
+    else:
+        plan = plan_un(np.empty(n, np.uint8), np.empty(m, np.uint8), N, spec, sampling_type,
+                       "est", shuffle=lambda a, b: None)
+        ok = bool(plan) and all(p[0] == "val" for p in plan)
+        xs = [p[1].x for p in plan] if ok else []
+        zs = [p[1].z for p in plan] if ok else []
+    if xs and all(isinstance(a, tuple) for a in xs + zs) and all(
+            sel[0][0] == 0 and all(a[1] == b[0] for a, b in zip(sel, sel[1:]))
+            for sel in (xs, zs)):
+        pairs = np.array([(a[1] - a[0]) * (b[1] - b[0]) for a, b in zip(xs, zs)],
+                         dtype=np.int64)
+        if np.all(pairs > 0):
+            lay = (np.array([a[0] for a in xs], dtype=np.int64), xs[-1][1],
+                   np.array([b[0] for b in zs], dtype=np.int64), zs[-1][1], pairs)
     if len(_LAYOUTS) > 256:
         _LAYOUTS.clear()
     _LAYOUTS[key] = lay
