@@ -13,6 +13,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _blocks as Bk
+from . import _lib as L
 
 
 def p(e):
@@ -181,13 +182,38 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
     elements the blocks read; a flush counts all rows' blocks in one launch with offsets built
     by broadcasting, and the block values, each try's np.mean over its blocks and UnNT's mean
     over its repetitions are row reductions (np.mean's pairwise sums along the contiguous last
-    axis, the same bits as np.mean of each row).  The same draws, shuffles and values as the
-    general path; a try whose shapes or dtypes differ from the last one's flushes first and
-    gets its own layout."""
+    axis, the same bits as np.mean of each row).  A flush runs on a worker thread (its upload,
+    count and read-back release the GIL) while this thread draws and shuffles the next tries
+    into the other of two buffer pairs; results are collected in try order.  The same draws,
+    shuffles and values as the general path; a try whose shapes or dtypes differ from the last
+    one's flushes first and gets its own layout."""
+    from collections import deque
+    from concurrent.futures import ThreadPoolExecutor
+    t = L.torch()
+    dev = t.cuda.current_device() if t.cuda.is_available() else None
     results = []
     st = {"key": None}
+    pending = deque()  # (future, buffer pair) in flush order
+    free = []  # buffer pairs of the current layout not in flight
+
+    def work(bx, bz, lay):
+        if dev is not None:
+            t.cuda.set_device(dev)
+        vals = Bk.fixed_values(spec, bx, bz, lay)
+        per = vals[:, 0] if N is None else vals.mean(axis=-1)  # finish_un: np.mean per plan
+        per = per.reshape(bx.shape[0] // reps, reps)
+        return list(per[:, 0] if reps == 1 else per.mean(axis=-1))
+
+    def collect(keep=0):  # results of the oldest flushes, in order, until `keep` remain
+        while len(pending) > keep:
+            fut, pair = pending.popleft()
+            results.extend(fut.result())
+            if pair is not None and pair[0].shape == st.get("shape"):
+                free.append(pair)
 
     def new_layout(X, Z):
+        collect()
+        free.clear()
         lay = Bk.fixed_layout(X.shape[0], Z.shape[0], N, spec, sampling_type)
         st["key"] = (X.shape, Z.shape, X.dtype, Z.dtype)
         st["lay"] = lay
@@ -195,43 +221,53 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
             return
         lx, lz = lay[1], lay[3]
         rows = max(reps, (max(1, flush_elems // max(1, lx + lz)) // reps) * reps)
-        st["bx"] = np.empty((rows, lx), dtype=X.dtype)
-        st["bz"] = np.empty((rows, lz), dtype=Z.dtype)
+        st["shape"] = (rows, lx)
+        st["bufs"] = (np.empty((rows, lx), dtype=X.dtype), np.empty((rows, lz), dtype=Z.dtype))
         st["rows"] = 0
 
-    def flush():
+    def flush(pool):
         J = st.get("rows", 0)
         if not J:
             return
-        vals = Bk.fixed_values(spec, st["bx"][:J], st["bz"][:J], st["lay"])
-        per = vals[:, 0] if N is None else vals.mean(axis=-1)  # finish_un: np.mean per plan
-        per = per.reshape(J // reps, reps)
-        results.extend(per[:, 0] if reps == 1 else per.mean(axis=-1))
+        bx, bz = st["bufs"]
+        pending.append((pool.submit(work, bx[:J], bz[:J], st["lay"]), (bx, bz)))
         st["rows"] = 0
+        collect(keep=1)  # at most one flush in flight beside the drawing
+        if free:
+            st["bufs"] = free.pop()
+        else:
+            lx, lz = st["lay"][1], st["lay"][3]
+            st["bufs"] = (np.empty((st["shape"][0], lx), dtype=bx.dtype),
+                          np.empty((st["shape"][0], lz), dtype=bz.dtype))
 
-    for _ in range(n_tries):
-        X = np.asarray(gen_X())
-        Z = np.asarray(gen_Z())
-        if (X.shape, Z.shape, X.dtype, Z.dtype) != st["key"] or X.ndim != 1 or Z.ndim != 1:
-            flush()
-            if X.ndim != 1 or Z.ndim != 1:
-                st["key"], st["lay"] = None, None
-            else:
-                new_layout(X, Z)
-        if st.get("lay") is None:  # this try by the general path (its own launch)
-            results.extend(_replicate_general(estimator, iter([X]).__next__,
-                                              iter([Z]).__next__, 1, spec, reps, N,
-                                              sampling_type, 0))
-            continue
-        lx, lz = st["lay"][1], st["lay"][3]
-        for _ in range(reps):
-            if N is not None:
-                Bk.shuffle_pair(X, Z)  # plan_un's in-place shuffles, bit for bit
-            r = st["rows"]
-            st["bx"][r] = X[:lx]
-            st["bz"][r] = Z[:lz]
-            st["rows"] = r + 1
-        if st["rows"] == st["bx"].shape[0]:
-            flush()
-    flush()
+    with ThreadPoolExecutor(max_workers=1) as pool:
+        for _ in range(n_tries):
+            X = np.asarray(gen_X())
+            Z = np.asarray(gen_Z())
+            if (X.shape, Z.shape, X.dtype, Z.dtype) != st["key"] or X.ndim != 1 or Z.ndim != 1:
+                flush(pool)
+                if X.ndim != 1 or Z.ndim != 1:
+                    collect()
+                    st["key"], st["lay"] = None, None
+                else:
+                    new_layout(X, Z)
+            if st.get("lay") is None:  # this try by the general path (its own launch)
+                collect()
+                results.extend(_replicate_general(estimator, iter([X]).__next__,
+                                                  iter([Z]).__next__, 1, spec, reps, N,
+                                                  sampling_type, 0))
+                continue
+            lx, lz = st["lay"][1], st["lay"][3]
+            bx, bz = st["bufs"]
+            for _ in range(reps):
+                if N is not None:
+                    Bk.shuffle_pair(X, Z)  # plan_un's in-place shuffles, bit for bit
+                r = st["rows"]
+                bx[r] = X[:lx]
+                bz[r] = Z[:lz]
+                st["rows"] = r + 1
+            if st["rows"] == bx.shape[0]:
+                flush(pool)
+        flush(pool)
+        collect()
     return results
