@@ -547,7 +547,16 @@ def fixed_values(spec, bx, bz, lay) -> np.ndarray:
     rows = np.arange(J, dtype=np.int64)[:, None]
     xo = np.append((rows * lx + xs).ravel(), J * lx).astype(np.int64)
     zo = np.append((rows * lz + zs).ravel(), J * lz).astype(np.int64)
-    xa, za, xod, zod = L.to_device_many([x, z, xo, zo])
+    t = L.torch()
+    xt, zt = t.from_numpy(x), t.from_numpy(z)
+    if x.size > (1 << 16) and xt.is_pinned() and zt.is_pinned():
+        # rows staged in page-locked buffers by the caller (replicate): uploaded as they lie,
+        # no packing copy on the host; the small offsets in one staged copy
+        xa = xt.to(L.device(), non_blocking=True)
+        za = zt.to(L.device(), non_blocking=True)
+        xod, zod = L.to_device_many([xo, zo])
+    else:
+        xa, za, xod, zod = L.to_device_many([x, z, xo, zo])
     sh = E.Shards(xa, xo, za, zo, code)
     sh._x_off_dev, sh._z_off_dev = xod, zod
     counts = np.asarray(E.count_complete(sh, mode)).view(np.uint64)

@@ -196,6 +196,14 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
     pending = deque()  # (future, buffer pair) in flush order
     free = []  # buffer pairs of the current layout not in flight
 
+    def alloc(rows, cols, dtype):
+        # page-locked rows on a GPU process (torch's caching host allocator keeps them for
+        # the next call): the flush uploads them by DMA without a packing copy
+        if dev is None:
+            return np.empty((rows, cols), dtype=dtype)
+        td = t.from_numpy(np.empty(0, dtype=dtype)).dtype
+        return t.empty((rows, cols), dtype=td, pin_memory=True).numpy()
+
     def work(bx, bz, lay):
         if dev is not None:
             t.cuda.set_device(dev)
@@ -222,7 +230,7 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
         lx, lz = lay[1], lay[3]
         rows = max(reps, (max(1, flush_elems // max(1, lx + lz)) // reps) * reps)
         st["shape"] = (rows, lx)
-        st["bufs"] = (np.empty((rows, lx), dtype=X.dtype), np.empty((rows, lz), dtype=Z.dtype))
+        st["bufs"] = (alloc(rows, lx, X.dtype), alloc(rows, lz, Z.dtype))
         st["rows"] = 0
 
     def flush(pool):
@@ -237,8 +245,8 @@ def _replicate_fixed(estimator, gen_X, gen_Z, n_tries, spec, reps, N, sampling_t
             st["bufs"] = free.pop()
         else:
             lx, lz = st["lay"][1], st["lay"][3]
-            st["bufs"] = (np.empty((st["shape"][0], lx), dtype=bx.dtype),
-                          np.empty((st["shape"][0], lz), dtype=bz.dtype))
+            rows = st["shape"][0]
+            st["bufs"] = (alloc(rows, lx, bx.dtype), alloc(rows, lz, bz.dtype))
 
     with ThreadPoolExecutor(max_workers=1) as pool:
         for _ in range(n_tries):
